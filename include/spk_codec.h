@@ -1,0 +1,208 @@
+/*
+ * spk_codec.h — C ABI of the MI355X struct_pack batch codec.
+ *
+ * This is the drop-in boundary between a host-side struct_pack front end
+ * (our C++20 header include/ylt/struct_pack.hpp, or the Python mirror
+ * yalantinglibs_amd/struct_pack.py) and the hand-written gfx950 HIP kernels
+ * in yalantinglibs_amd/csrc/spk_codec.hip. Plain C: no HIP/torch types, all
+ * buffers are raw pointers + sizes, streams are opaque `void*` (hipStream_t).
+ *
+ * The reference has no C ABI: struct_pack is a header-only template library.
+ * Each entry point below replaces one template entry point of
+ * /root/reference/include/ylt/struct_pack.hpp for a *batch* of records that
+ * lives in device memory (cited per function). The wire bytes are the
+ * reference's, byte for byte.
+ *
+ * Record model ("device record" = what a layout descriptor describes)
+ * -------------------------------------------------------------------
+ * A record type T is flattened by host reflection into `rec_stride`-byte
+ * device records plus one heap per variable-length member:
+ *   SPK_OP_COPY  {rec_off, size}            `size` raw bytes of the record
+ *                                           (fundamentals, enums, std::array,
+ *                                           trivially-serializable sub-structs
+ *                                           incl. their padding) — written
+ *                                           verbatim, in declaration order.
+ *   SPK_OP_SPAN  {rec_off, size, aux}       a std::string / std::vector<U> with
+ *                                           U trivially serializable: the record
+ *                                           holds a u32 element count at
+ *                                           rec_off and a u64 element offset into
+ *                                           this span's heap at aux; `size` =
+ *                                           sizeof(U). Wire: [count:w][bytes].
+ * A trivially-serializable T (SPK_LAYOUT_TRIVIAL) is a single COPY of the
+ * whole record (reference packer.hpp:418-421, unpacker.hpp:1300-1312).
+ *
+ * Batch modes
+ *   SPK_MODE_VECTOR   one message  == serialize(std::vector<T>{recs...})
+ *   SPK_MODE_MESSAGES n messages   == serialize(rec_i) back to back
+ *                                     (coro_rpc payload batch), with a u64
+ *                                     offsets array of n+1 entries.
+ *
+ * Error model: functions return SPK_OK or a negative SPK_E_* (bad argument,
+ * unsupported layout, HIP failure). Data-dependent wire errors are reported
+ * stream-ordered in device memory with the reference's errc values
+ * (error_code.hpp:21-27): 0 ok, 1 no_buffer_space, 2 invalid_buffer,
+ * 3 hash_conflict, 4 invalid_width_of_container_length.
+ *
+ * Threading: every call is reentrant; the library keeps no mutable global
+ * state; descriptors are immutable and may be cached per type. All device
+ * work is enqueued on `stream` with no host synchronisation and no
+ * allocation (caller-owned workspace), so calls are hipGraph-capturable.
+ */
+#ifndef SPK_CODEC_H
+#define SPK_CODEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPK_ABI_VERSION 1u
+#define SPK_MAX_OPS 64u
+#define SPK_MAX_SPANS 8u
+#define SPK_MAX_LITERAL 240u
+
+/* return codes (host-side; negative) */
+#define SPK_OK 0
+#define SPK_E_ARG -1         /* null pointer / bad size / bad mode          */
+#define SPK_E_LAYOUT -2      /* descriptor malformed or unsupported         */
+#define SPK_E_WORKSPACE -3   /* workspace too small                         */
+#define SPK_E_CAPACITY -4    /* output buffer provably too small            */
+#define SPK_E_HIP -5         /* a HIP runtime call failed                   */
+
+/* reference errc (include/ylt/struct_pack/error_code.hpp:21-27) */
+#define SPK_ERRC_OK 0
+#define SPK_ERRC_NO_BUFFER_SPACE 1
+#define SPK_ERRC_INVALID_BUFFER 2
+#define SPK_ERRC_HASH_CONFLICT 3
+#define SPK_ERRC_INVALID_WIDTH 4
+/* device-side capacity overflow during decode (not a reference errc) */
+#define SPK_ERRC_CAPACITY 100
+
+#define SPK_OP_COPY 1u
+#define SPK_OP_SPAN 2u
+
+#define SPK_MODE_VECTOR 0
+#define SPK_MODE_MESSAGES 1
+
+/* spk_msgfmt.flags — resolved per message type by the host front end from
+ * the type and its sp_config exactly like type_calculate.hpp:744-891 */
+#define SPK_MF_HASH_HEAD 0x1u     /* !check_if_disable_hash_head            */
+#define SPK_MF_TYPE_LITERAL 0x2u  /* check_if_add_type_literal (debug/ENABLE_TYPE_INFO) */
+#define SPK_MF_HAS_CONTAINER 0x4u /* check_if_has_container<T>              */
+
+/* spk_layout.flags */
+#define SPK_LAYOUT_TRIVIAL 0x1u   /* is_trivial_serializable<T>: 1 COPY op  */
+
+typedef struct spk_op {
+  uint32_t kind;    /* SPK_OP_COPY | SPK_OP_SPAN                             */
+  uint32_t rec_off; /* COPY: source byte offset; SPAN: u32 count offset      */
+  uint32_t size;    /* COPY: byte length;       SPAN: element size (bytes)   */
+  uint32_t aux;     /* SPAN: u64 heap element-offset field offset; COPY: 0   */
+} spk_op;
+
+/* Wire format of one message type (get_type_code / get_type_literal). */
+typedef struct spk_msgfmt {
+  uint32_t code;           /* get_type_code<M>() : MD5_32(literal) & ~1      */
+  uint32_t flags;          /* SPK_MF_*                                       */
+  uint32_t literal_len;    /* strlen of get_type_literal<M>() (no NUL)       */
+  uint32_t reserved;
+  uint8_t literal[SPK_MAX_LITERAL]; /* always filled: decode checks it when
+                                       a buffer carries type info            */
+} spk_msgfmt;
+
+typedef struct spk_layout {
+  uint32_t abi;        /* SPK_ABI_VERSION                                   */
+  uint32_t flags;      /* SPK_LAYOUT_*                                      */
+  uint32_t rec_stride; /* bytes per device record (multiple of 4)           */
+  uint32_t n_ops;
+  spk_op ops[SPK_MAX_OPS];
+  spk_msgfmt fmt_vector; /* message type std::vector<T> (SPK_MODE_VECTOR)   */
+  spk_msgfmt fmt_one;    /* message type T             (SPK_MODE_MESSAGES)  */
+} spk_layout;
+
+/* Size pass result (device memory, written by spk_plan).
+ * Mirrors serialize_buffer_size {len_, metainfo_} (calculate_size.hpp:391-405). */
+typedef struct spk_plan_t {
+  uint64_t total_bytes; /* SPK_MODE_VECTOR: message length; MESSAGES: sum  */
+  uint64_t max_count;   /* max element count over every container          */
+  uint64_t var_bytes;   /* sum of span payload bytes                       */
+  uint32_t width;       /* container-length width in bytes (1/2/4/8)       */
+  uint32_t header_bytes;/* bytes before the first record (VECTOR mode)     */
+  uint32_t metainfo;    /* metainfo byte value (valid if has_meta)         */
+  uint32_t has_meta;
+} spk_plan_t;
+
+/* Decode result (device memory, written by spk_decode). */
+typedef struct spk_dresult_t {
+  int32_t errc;         /* reference errc, or SPK_ERRC_CAPACITY            */
+  uint32_t width;
+  uint64_t count;       /* records decoded (VECTOR) / messages ok (MESSAGES)*/
+  uint64_t consumed;    /* consume_len (struct_pack.hpp:343-357)           */
+  uint64_t heap_used[SPK_MAX_SPANS]; /* elements written per span heap     */
+} spk_dresult_t;
+
+/* ------------------------------------------------------------------------ */
+uint32_t spk_abi_version(void);
+const char *spk_errc_message(int32_t errc); /* error_code.hpp:28-43 */
+
+/* Validate a descriptor (host only, no device work). SPK_OK or SPK_E_LAYOUT. */
+int spk_layout_check(const spk_layout *L);
+
+/* Device workspace needed for `n` records (encode) or a `wire_len`-byte
+ * input (decode) in `mode`. */
+size_t spk_workspace_bytes(const spk_layout *L, int mode, uint64_t n,
+                           uint64_t wire_len);
+
+/* Size pass: get_needed_size / get_serialize_runtime_info
+ * (ref struct_pack.hpp:131-135, calculate_size.hpp:407-474).
+ * Reads only the span counts of variable records; O(1) for trivial T.
+ * Writes *d_plan (device). */
+int spk_plan(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
+             spk_plan_t *d_plan, void *d_ws, size_t ws_bytes, void *stream);
+
+/* Write pass: serialize_to(char*, serialize_buffer_size, vector<T>) for
+ * SPK_MODE_VECTOR (ref struct_pack.hpp:161-167, packer.hpp:535-585), or n
+ * independent serialize_to calls for SPK_MODE_MESSAGES (then
+ * d_msg_offsets[0..n] receives the message boundaries; nullable).
+ * `d_heaps` is a HOST array of n_span DEVICE pointers. `d_plan` must come
+ * from spk_plan on the same records (stream-ordered). Writes at most
+ * out_cap bytes; if the plan exceeds out_cap nothing is written and
+ * d_plan->total_bytes tells the caller the size needed. */
+int spk_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
+               const void *const *d_heaps, const spk_plan_t *d_plan,
+               void *d_out, uint64_t out_cap, uint64_t *d_msg_offsets,
+               void *d_ws, size_t ws_bytes, void *stream);
+
+/* Decode: deserialize_to(vector<T>&, const char*, size_t, size_t&)
+ * (ref struct_pack.hpp:343-357, unpacker.hpp:101-162,548-619,780-1349) for
+ * SPK_MODE_VECTOR; for SPK_MODE_MESSAGES, message i is
+ * d_wire[d_msg_offsets[i] .. d_msg_offsets[i+1]) and is decoded into record
+ * i with its errc in d_errc[i] (nullable) and d_res->count = #ok.
+ * Records go to d_recs (capacity rec_cap records); span elements go to
+ * d_heaps[k] (capacity heap_caps[k] elements; HOST arrays of device
+ * pointers / sizes) at canonical offsets (record order, packed). */
+int spk_decode(const spk_layout *L, int mode, const void *d_wire,
+               uint64_t wire_len, const uint64_t *d_msg_offsets, uint64_t n_msgs,
+               void *d_recs, uint64_t rec_cap, void *const *d_heaps,
+               const uint64_t *heap_caps, spk_dresult_t *d_res,
+               int32_t *d_errc, void *d_ws, size_t ws_bytes, void *stream);
+
+/* ---- synthetic inputs (bench / tests): the seeded generator of
+ * oracle/ref/types.hpp, restated on the device so the GPU box regenerates
+ * exactly the inputs the golden digests were taken from. ---------------- */
+#define SPK_SYNTH_REC64 1
+#define SPK_SYNTH_RECS 2
+#define SPK_SYNTH_OUTER 3
+int spk_synth(int kind, uint64_t seed, uint64_t first, uint64_t n,
+              uint32_t param, void *d_recs, void *d_heap,
+              const uint64_t *d_heap_offsets, void *stream);
+/* per-record span counts for variable kinds (to size/prefix the heap) */
+int spk_synth_counts(int kind, uint64_t seed, uint64_t first, uint64_t n,
+                     uint32_t param, uint64_t *d_counts, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPK_CODEC_H */

@@ -1,0 +1,288 @@
+// Golden-vector generator built against the REFERENCE struct_pack headers
+// (/root/reference/include, read-only). TEST INFRASTRUCTURE ONLY: the binary
+// lives in oracle/_ref/ and is driven by tests/golden/make_golden.py, which
+// commits small fixtures + SHA-256 digests under tests/golden/.
+//
+// Subcommands
+//   kat                                  type literals / type codes (JSON)
+//   emit <case> <n> <seed> <param> <conf> <wire_out> [<lens_out>]
+//        mode "A" cases serialize one std::vector<T> message,
+//        mode "B" cases serialize n independent T messages back to back and
+//        write the per-message byte lengths (u64 LE) to <lens_out>.
+//   errs <case> <n> <seed> <param> <conf> <mutations> <wire_in>
+//        decode every mutation of <wire_in> with the reference deserialize_to
+//        and print errc / consume_len / canonical re-encoding digest (JSON).
+#include <ylt/struct_pack.hpp>
+
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "types.hpp"
+
+using namespace spk_gold;
+using struct_pack::sp_config;
+
+static void hexlit(std::ostream &os, const char *p, size_t n) {
+  os << "\"";
+  static const char *hx = "0123456789abcdef";
+  for (size_t i = 0; i < n; ++i) {
+    unsigned char c = (unsigned char)p[i];
+    os << hx[c >> 4] << hx[c & 15];
+  }
+  os << "\"";
+}
+
+template <typename... T>
+static void kat_one(std::ostream &os, const char *name, bool &first) {
+  constexpr auto lit = struct_pack::get_type_literal<T...>();
+  uint32_t code = struct_pack::get_type_code<T...>();
+  if (!first) os << ",\n";
+  first = false;
+  os << "  \"" << name << "\": {\"code\": " << code << ", \"literal\": ";
+  hexlit(os, lit.data(), lit.size());
+  os << "}";
+}
+
+static int cmd_kat() {
+  std::ostringstream os;
+  bool first = true;
+  os << "{\n";
+  kat_one<Rec64>(os, "Rec64", first);
+  kat_one<std::vector<Rec64>>(os, "vector<Rec64>", first);
+  kat_one<RecS>(os, "RecS", first);
+  kat_one<std::vector<RecS>>(os, "vector<RecS>", first);
+  kat_one<Inner>(os, "Inner", first);
+  kat_one<Outer>(os, "Outer", first);
+  kat_one<std::vector<Outer>>(os, "vector<Outer>", first);
+  kat_one<Pad>(os, "Pad", first);
+  kat_one<std::vector<Pad>>(os, "vector<Pad>", first);
+  kat_one<Mixed>(os, "Mixed", first);
+  kat_one<std::vector<Mixed>>(os, "vector<Mixed>", first);
+  kat_one<rect<int>>(os, "rect<int>", first);
+  kat_one<std::vector<rect<int>>>(os, "vector<rect<int>>", first);
+  kat_one<rpcb::point>(os, "rpc::point", first);
+  kat_one<rpcb::rect>(os, "rpc::rect", first);
+  kat_one<std::vector<rpcb::rect>>(os, "vector<rpc::rect>", first);
+  kat_one<rpcb::person>(os, "person", first);
+  kat_one<std::vector<rpcb::person>>(os, "vector<person>", first);
+  kat_one<std::vector<int32_t>>(os, "vector<int32_t>", first);
+  kat_one<std::string>(os, "string", first);
+  kat_one<int32_t>(os, "int32_t", first);
+  kat_one<int32_t, int32_t, int16_t>(os, "<int32_t,int32_t,int16_t>", first);
+  kat_one<rpcb::req_header>(os, "req_header", first);
+  kat_one<rpcb::resp_header>(os, "resp_header", first);
+  kat_one<std::monostate>(os, "monostate", first);
+  kat_one<std::array<int16_t, 3>>(os, "array<int16_t,3>", first);
+  kat_one<std::vector<std::string>>(os, "vector<string>", first);
+  kat_one<uint8_t, uint16_t, uint32_t, uint64_t, int8_t, int16_t, int64_t,
+          bool, char, float, double>(os, "fundamentals", first);
+  os << "\n}\n";
+  std::cout << os.str();
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+struct Args {
+  std::string kase;
+  uint64_t n, seed;
+  uint32_t param;
+  std::string conf;
+};
+
+template <uint64_t conf, typename T>
+static void ser_append(std::string &out, const T &v) {
+  struct_pack::serialize_to<conf>(out, v);
+}
+
+template <typename T, typename Gen>
+static void emit_typed(const Args &a, Gen gen, std::string &wire,
+                       std::vector<uint64_t> &lens, bool modeB) {
+  if (!modeB) {
+    std::vector<T> v(a.n);  // value-initialised: zero padding
+    for (uint64_t i = 0; i < a.n; ++i) gen(v[i], i);
+    if (a.conf == "typeinfo")
+      ser_append<sp_config::ENABLE_TYPE_INFO>(wire, v);
+    else if (a.conf == "nometa")
+      ser_append<sp_config::DISABLE_ALL_META_INFO>(wire, v);
+    else
+      ser_append<sp_config::DEFAULT>(wire, v);
+    lens.push_back(wire.size());
+  }
+  else {
+    for (uint64_t i = 0; i < a.n; ++i) {
+      T v{};
+      gen(v, i);
+      size_t before = wire.size();
+      if (a.conf == "typeinfo")
+        ser_append<sp_config::ENABLE_TYPE_INFO>(wire, v);
+      else if (a.conf == "nometa")
+        ser_append<sp_config::DISABLE_ALL_META_INFO>(wire, v);
+      else
+        ser_append<sp_config::DEFAULT>(wire, v);
+      lens.push_back(wire.size() - before);
+    }
+  }
+}
+
+// dispatch on the case name; calls f.template operator()<T>(gen)
+template <typename F>
+static bool with_case(const Args &a, F &&f) {
+  const std::string &k = a.kase;
+  uint64_t s = a.seed;
+  uint32_t p = a.param;
+  if (k == "rec64")
+    return f.template operator()<Rec64>([=](Rec64 &o, uint64_t i) { o = make_rec64(s, i); });
+  if (k == "recs")
+    return f.template operator()<RecS>([=](RecS &o, uint64_t i) { o = make_recs(s, i, p); });
+  if (k == "outer")
+    return f.template operator()<Outer>([=](Outer &o, uint64_t i) { o = make_outer(s, i, p); });
+  if (k == "pad")
+    return f.template operator()<Pad>([=](Pad &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "mixed")
+    return f.template operator()<Mixed>([=](Mixed &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "rect")  // C1: benchmark rect<int> default values
+    return f.template operator()<rect<int>>([=](rect<int> &o, uint64_t) { o = rect<int>{}; });
+  if (k == "rpcrect")
+    return f.template operator()<rpcb::rect>([=](rpcb::rect &o, uint64_t i) { o = make_rpc_rect(s, i); });
+  if (k == "person")
+    return f.template operator()<rpcb::person>([=](rpcb::person &o, uint64_t i) { o = make_person(s, i, p); });
+  if (k == "ints")  // messages of std::vector<int32_t>
+    return f.template operator()<std::vector<int32_t>>(
+        [=](std::vector<int32_t> &o, uint64_t i) { o = make_ints(s, i, p); });
+  return false;
+}
+
+static bool write_file(const std::string &path, const void *p, size_t n) {
+  FILE *f = fopen(path.c_str(), "wb");
+  if (!f) return false;
+  size_t w = n ? fwrite(p, 1, n, f) : 0;
+  fclose(f);
+  return w == n;
+}
+
+static int cmd_emit(const Args &a, bool modeB, const std::string &wire_out,
+                    const std::string &lens_out) {
+  std::string wire;
+  std::vector<uint64_t> lens;
+  bool ok = with_case(a, [&]<typename T>(auto gen) {
+    emit_typed<T>(a, gen, wire, lens, modeB);
+    return true;
+  });
+  if (!ok) {
+    std::cerr << "unknown case " << a.kase << "\n";
+    return 2;
+  }
+  if (!write_file(wire_out, wire.data(), wire.size())) return 3;
+  if (!lens_out.empty() &&
+      !write_file(lens_out, lens.data(), lens.size() * sizeof(uint64_t)))
+    return 3;
+  std::cout << wire.size() << "\n";
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Negative / mutation tests: mutation list file has lines
+//   trunc <len>            keep the first <len> bytes
+//   set <pos> <byte>       overwrite one byte
+// Output: one JSON object per line {errc, consume, reenc_hex|null}
+template <uint64_t conf, typename T>
+static void decode_report(const std::string &buf, std::ostream &os) {
+  T obj{};
+  size_t consume = 0;
+  auto ec = struct_pack::deserialize_to<conf>(obj, buf.data(), buf.size(),
+                                              consume);
+  os << "{\"errc\": " << (int)ec.ec << ", \"consume\": " << consume
+     << ", \"reenc\": ";
+  if (!ec) {
+    std::string re;
+    struct_pack::serialize_to<conf>(re, obj);
+    hexlit(os, re.data(), re.size());
+  }
+  else {
+    os << "null";
+  }
+  os << "}\n";
+}
+
+static int cmd_errs(const Args &a, bool modeB, const std::string &muts,
+                    const std::string &wire_in) {
+  std::ifstream wf(wire_in, std::ios::binary);
+  std::string wire((std::istreambuf_iterator<char>(wf)),
+                   std::istreambuf_iterator<char>());
+  std::ifstream mf(muts);
+  std::string line;
+  std::ostringstream os;
+  while (std::getline(mf, line)) {
+    if (line.empty()) continue;
+    std::istringstream ls(line);
+    std::string op;
+    ls >> op;
+    std::string buf = wire;
+    while (!op.empty()) {
+      if (op == "trunc") {
+        size_t n;
+        ls >> n;
+        buf.resize(std::min(n, buf.size()));
+      }
+      else if (op == "set") {
+        size_t pos;
+        unsigned v;
+        ls >> pos >> v;
+        if (pos < buf.size()) buf[pos] = (char)v;
+      }
+      op.clear();
+      ls >> op;
+    }
+    with_case(a, [&]<typename T>(auto) {
+      using M = std::conditional_t<true, T, void>;
+      if (!modeB) {
+        if (a.conf == "typeinfo")
+          decode_report<sp_config::ENABLE_TYPE_INFO, std::vector<M>>(buf, os);
+        else if (a.conf == "nometa")
+          decode_report<sp_config::DISABLE_ALL_META_INFO, std::vector<M>>(buf, os);
+        else
+          decode_report<sp_config::DEFAULT, std::vector<M>>(buf, os);
+      }
+      else {
+        if (a.conf == "typeinfo")
+          decode_report<sp_config::ENABLE_TYPE_INFO, M>(buf, os);
+        else if (a.conf == "nometa")
+          decode_report<sp_config::DISABLE_ALL_META_INFO, M>(buf, os);
+        else
+          decode_report<sp_config::DEFAULT, M>(buf, os);
+      }
+      return true;
+    });
+  }
+  std::cout << os.str();
+  return 0;
+}
+
+int main(int argc, char **argv) {
+  if (argc < 2) {
+    std::cerr << "usage: golden_gen kat | emit ... | errs ...\n";
+    return 2;
+  }
+  std::string cmd = argv[1];
+  if (cmd == "kat") return cmd_kat();
+  if ((cmd == "emit" || cmd == "errs") && argc >= 8) {
+    Args a;
+    std::string kase = argv[2];
+    bool modeB = kase.size() > 2 && kase.substr(kase.size() - 2) == "_B";
+    a.kase = kase.substr(0, kase.size() - 2);  // strip _A / _B
+    a.n = strtoull(argv[3], nullptr, 0);
+    a.seed = strtoull(argv[4], nullptr, 0);
+    a.param = (uint32_t)strtoul(argv[5], nullptr, 0);
+    a.conf = argv[6];
+    if (cmd == "emit")
+      return cmd_emit(a, modeB, argv[7], argc > 8 ? argv[8] : "");
+    if (argc >= 9) return cmd_errs(a, modeB, argv[7], argv[8]);
+  }
+  std::cerr << "bad arguments\n";
+  return 2;
+}

@@ -1,0 +1,225 @@
+// Record types and the seeded input generator shared by the golden generator
+// (golden_gen.cpp) and the reference CPU baseline (ref_bench.cpp).
+//
+// TEST INFRASTRUCTURE ONLY. These translation units are compiled against the
+// read-only reference headers under /root/reference/include (see
+// oracle/Makefile); their binaries land in oracle/_ref/ and are never linked
+// into the product library.
+//
+// The generator formula is restated bit-for-bit in
+//   * yalantinglibs_amd/csrc/spk_synth.hip (device generator used at full size)
+//   * yalantinglibs_amd/synth.py (numpy, small sizes)
+// so that the GPU box can regenerate the exact same inputs from a seed.
+#pragma once
+#include <array>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace spk_gold {
+
+inline uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+// counter-based: word k (0..63) of record i
+inline uint64_t rnd(uint64_t seed, uint64_t i, uint64_t k) {
+  return mix64(seed + (i * 64 + k + 1) * 0x9E3779B97F4A7C15ULL);
+}
+inline float rf(uint64_t r) { return (float)(int32_t)(uint32_t)r / 65536.0f; }
+inline double rd(uint64_t r) { return (double)(int32_t)(uint32_t)r / 65536.0; }
+
+}  // namespace spk_gold
+
+// ---- C2: 64-byte fixed-width POD ---------------------------------------
+struct Rec64 {
+  int32_t i0, i1, i2, i3;
+  float f0, f1, f2, f3;
+  double d0, d1, d2, d3;
+};
+static_assert(sizeof(Rec64) == 64);
+
+// ---- C3: one std::string field -----------------------------------------
+struct RecS {
+  int32_t id;
+  std::string name;
+  double v;
+};
+
+// ---- C4: nested vector of trivially-copyable inner records -------------
+struct Inner {
+  int32_t x;
+  float y;
+};
+struct Outer {
+  int64_t key;
+  std::vector<Inner> items;
+};
+
+// ---- padding / mixed-member coverage -----------------------------------
+struct Pad {  // trivially serializable, 12 bytes with 3+0+2 padding bytes
+  int8_t a;
+  int32_t b;
+  int16_t c;
+};
+struct Mixed {  // non-trivial: raw Pad (with padding), raw array, two spans
+  Pad p;
+  int64_t k;
+  std::array<int16_t, 3> arr;
+  std::string s;
+  std::vector<int32_t> v;
+};
+
+// ---- C1: src/struct_pack/benchmark/data_def.hpp rect<int> --------------
+template <typename T>
+struct rect {
+  T x = 1;
+  T y = 0;
+  T width = 11;
+  T height = 1;
+};
+inline constexpr struct_pack::sp_config set_sp_config(rect<int> *) {
+  return struct_pack::DISABLE_ALL_META_INFO;
+}
+inline constexpr struct_pack::sp_config set_sp_config(
+    std::vector<rect<int>> *) {
+  return struct_pack::DISABLE_ALL_META_INFO;
+}
+
+// ---- C5: coro_rpc benchmark payload shapes ------------------------------
+namespace rpcb {
+struct point {
+  double x, y;
+};
+struct rect {
+  point p1, p2;
+};
+struct person {  // src/struct_pack/benchmark/data_def.hpp person
+  int32_t id;
+  std::string name;
+  int age;
+  double salary;
+};
+// coro_rpc req_header (include/ylt/coro_rpc/impl/protocol/coro_rpc_protocol.hpp:60-68)
+struct req_header {
+  uint8_t magic;
+  uint8_t version;
+  uint8_t serialize_type;
+  uint8_t msg_type;
+  uint32_t seq_num;
+  uint32_t function_id;
+  uint32_t length;
+  uint32_t attach_length;
+};
+struct resp_header {
+  uint8_t magic;
+  uint8_t version;
+  uint8_t err_code;
+  uint8_t msg_type;
+  uint32_t seq_num;
+  uint32_t length;
+  uint32_t attach_length;
+};
+}  // namespace rpcb
+
+namespace spk_gold {
+
+inline Rec64 make_rec64(uint64_t seed, uint64_t i) {
+  Rec64 r;
+  r.i0 = (int32_t)(uint32_t)rnd(seed, i, 0);
+  r.i1 = (int32_t)(uint32_t)rnd(seed, i, 1);
+  r.i2 = (int32_t)(uint32_t)rnd(seed, i, 2);
+  r.i3 = (int32_t)(uint32_t)rnd(seed, i, 3);
+  r.f0 = rf(rnd(seed, i, 4));
+  r.f1 = rf(rnd(seed, i, 5));
+  r.f2 = rf(rnd(seed, i, 6));
+  r.f3 = rf(rnd(seed, i, 7));
+  r.d0 = rd(rnd(seed, i, 8));
+  r.d1 = rd(rnd(seed, i, 9));
+  r.d2 = rd(rnd(seed, i, 10));
+  r.d3 = rd(rnd(seed, i, 11));
+  return r;
+}
+
+// string of record i: length rnd(i,1) % (maxlen+1); char j from word 2+j/8
+inline std::string make_chars(uint64_t seed, uint64_t i, uint32_t maxlen) {
+  uint32_t len = (uint32_t)(rnd(seed, i, 1) % (uint64_t)(maxlen + 1));
+  std::string s(len, '\0');
+  for (uint32_t j = 0; j < len; ++j) {
+    uint64_t w = rnd(seed, i, 2 + (j >> 3) % 56);  // words 2..57, recycled
+    s[j] = (char)('a' + ((w >> ((j & 7) * 8)) & 0xFF) % 26);
+  }
+  return s;
+}
+
+inline RecS make_recs(uint64_t seed, uint64_t i, uint32_t maxlen) {
+  RecS r;
+  r.id = (int32_t)(uint32_t)rnd(seed, i, 0);
+  r.name = make_chars(seed, i, maxlen);
+  r.v = rd(rnd(seed, i, 60));
+  return r;
+}
+
+inline Outer make_outer(uint64_t seed, uint64_t i, uint32_t maxn) {
+  Outer o;
+  o.key = (int64_t)rnd(seed, i, 0);
+  uint32_t n = (uint32_t)(rnd(seed, i, 1) % (uint64_t)(maxn + 1));
+  o.items.resize(n);
+  for (uint32_t j = 0; j < n; ++j) {
+    uint64_t w = rnd(seed, i, 2 + j % 62);
+    uint64_t w2 = mix64(w ^ (uint64_t)j);
+    o.items[j].x = (int32_t)(uint32_t)w2;
+    o.items[j].y = rf(w2 >> 32);
+  }
+  return o;
+}
+
+// Generators fill objects IN PLACE (T& out): padding bytes of trivially
+// serializable structs travel verbatim on the wire, so they must stay the
+// zeros of value-initialisation (a by-value copy may leave them garbage).
+inline void fill(Pad &p, uint64_t seed, uint64_t i, uint32_t) {
+  std::memset((void *)&p, 0, sizeof(p));
+  uint64_t w = rnd(seed, i, 0);
+  p.a = (int8_t)(w & 0xFF);
+  p.b = (int32_t)(uint32_t)(w >> 8);
+  p.c = (int16_t)(w >> 40);
+}
+
+inline void fill(Mixed &m, uint64_t seed, uint64_t i, uint32_t maxlen) {
+  fill(m.p, seed, i, 0);
+  m.k = (int64_t)rnd(seed, i, 58);
+  uint64_t a = rnd(seed, i, 59);
+  m.arr = {(int16_t)a, (int16_t)(a >> 16), (int16_t)(a >> 32)};
+  m.s = make_chars(seed, i, maxlen);
+  uint32_t n = (uint32_t)(rnd(seed, i, 61) % (uint64_t)(maxlen + 1));
+  m.v.resize(n);
+  for (uint32_t j = 0; j < n; ++j)
+    m.v[j] = (int32_t)(uint32_t)mix64(rnd(seed, i, 62) + j);
+}
+
+inline rpcb::rect make_rpc_rect(uint64_t seed, uint64_t i) {
+  return rpcb::rect{{rd(rnd(seed, i, 0)), rd(rnd(seed, i, 1))},
+                    {rd(rnd(seed, i, 2)), rd(rnd(seed, i, 3))}};
+}
+
+inline rpcb::person make_person(uint64_t seed, uint64_t i, uint32_t maxlen) {
+  rpcb::person p;
+  p.id = (int32_t)(uint32_t)rnd(seed, i, 0);
+  p.name = make_chars(seed, i, maxlen);
+  p.age = (int32_t)(rnd(seed, i, 60) % 100);
+  p.salary = rd(rnd(seed, i, 61));
+  return p;
+}
+
+inline std::vector<int32_t> make_ints(uint64_t seed, uint64_t i,
+                                      uint32_t maxn) {
+  uint32_t n = (uint32_t)(rnd(seed, i, 1) % (uint64_t)(maxn + 1));
+  std::vector<int32_t> v(n);
+  for (uint32_t j = 0; j < n; ++j)
+    v[j] = (int32_t)(uint32_t)mix64(rnd(seed, i, 2) + j);
+  return v;
+}
+
+}  // namespace spk_gold

@@ -1,0 +1,404 @@
+/*
+ * spk_oracle.c — plain-C restatement of struct_pack's encode/decode for the
+ * record model of include/spk_codec.h. TEST INFRASTRUCTURE ONLY (see
+ * spk_oracle.h); pinned against the reference's own bytes in tests/golden/.
+ *
+ * Every function cites the reference code (paths relative to
+ * /root/reference/include/ylt/) whose behaviour it restates.
+ */
+#include "spk_oracle.h"
+
+#include <string.h>
+
+/* ---- little-endian primitives: struct_pack/endian_wrapper.hpp:136-271 -- */
+static void put_le(uint8_t *p, uint64_t v, unsigned w) {
+  for (unsigned i = 0; i < w; ++i) p[i] = (uint8_t)(v >> (8 * i));
+}
+static uint64_t get_le(const uint8_t *p, unsigned w) {
+  uint64_t v = 0;
+  for (unsigned i = 0; i < w; ++i) v |= (uint64_t)p[i] << (8 * i);
+  return v;
+}
+
+/* ---- layout helpers ---------------------------------------------------- */
+static unsigned n_spans(const spk_layout *L) {
+  unsigned k = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i) k += L->ops[i].kind == SPK_OP_SPAN;
+  return k;
+}
+static uint64_t rec_count(const uint8_t *rec, const spk_op *op) {
+  uint32_t c;
+  memcpy(&c, rec + op->rec_off, 4);
+  return c;
+}
+static uint64_t rec_heapoff(const uint8_t *rec, const spk_op *op) {
+  uint64_t o;
+  memcpy(&o, rec + op->aux, 8);
+  return o;
+}
+
+/* width selection: calculate_size.hpp:426-447 */
+static unsigned width_of(uint64_t max_count) {
+  if (max_count < (1ull << 8)) return 1;
+  if (max_count < (1ull << 16)) return 2;
+  if (max_count < (1ull << 32)) return 4;
+  return 8;
+}
+static unsigned width_bits(unsigned w) {
+  return w == 1 ? 0u : w == 2 ? 0x08u : w == 4 ? 0x10u : 0x18u;
+}
+
+/* Header shape: check_has_metainfo (type_calculate.hpp:884-891),
+ * get_serialize_runtime_info (calculate_size.hpp:407-474) and
+ * serialize_metainfo (packer.hpp:100-139). Compatible fields unsupported. */
+typedef struct hdr_t {
+  unsigned head, lit, has_meta, len;
+  uint8_t meta;
+} hdr_t;
+
+static hdr_t header_shape(const spk_msgfmt *f, unsigned w) {
+  hdr_t h;
+  unsigned has_container = (f->flags & SPK_MF_HAS_CONTAINER) != 0;
+  h.head = (f->flags & SPK_MF_HASH_HEAD) != 0;
+  h.lit = h.head && (f->flags & SPK_MF_TYPE_LITERAL);
+  unsigned meta_fixed = h.lit || (!h.head && has_container);
+  if (!has_container) w = 1;
+  h.has_meta = meta_fixed || w > 1;
+  h.meta = (uint8_t)(width_bits(w) | (h.lit ? 0x04u : 0u));
+  h.len = (h.head ? 4u : 0u) + (h.has_meta ? 1u : 0u) +
+          (h.lit ? f->literal_len + 1u : 0u);
+  return h;
+}
+
+static uint8_t *write_header(uint8_t *p, const spk_msgfmt *f, const hdr_t *h) {
+  if (h->head) { /* packer.hpp:103-107: LSB = more metainfo follows */
+    put_le(p, (f->code & ~1u) | (h->has_meta ? 1u : 0u), 4);
+    p += 4;
+  }
+  if (h->has_meta) *p++ = h->meta; /* packer.hpp:108-110 */
+  if (h->lit) {                    /* packer.hpp:132-137: literal + NUL */
+    memcpy(p, f->literal, f->literal_len);
+    p += f->literal_len;
+    *p++ = 0;
+  }
+  return p;
+}
+
+/* per-record wire bytes: calculate_one_size (calculate_size.hpp:39-183) */
+static uint64_t rec_wire_size(const spk_layout *L, const uint8_t *rec,
+                              unsigned w) {
+  if (L->flags & SPK_LAYOUT_TRIVIAL) return L->rec_stride;
+  uint64_t s = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i) {
+    const spk_op *op = &L->ops[i];
+    if (op->kind == SPK_OP_COPY)
+      s += op->size;
+    else
+      s += w + rec_count(rec, op) * op->size;
+  }
+  return s;
+}
+
+static uint64_t rec_max_count(const spk_layout *L, const uint8_t *rec) {
+  uint64_t m = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i)
+    if (L->ops[i].kind == SPK_OP_SPAN) {
+      uint64_t c = rec_count(rec, &L->ops[i]);
+      if (c > m) m = c;
+    }
+  return m;
+}
+
+/* serialize_one (packer.hpp:237-527) for one flattened record */
+static uint8_t *write_record(const spk_layout *L, const uint8_t *rec,
+                             const void *const *heaps, unsigned w, uint8_t *p) {
+  if (L->flags & SPK_LAYOUT_TRIVIAL) { /* packer.hpp:418-421 (incl. padding) */
+    memcpy(p, rec, L->rec_stride);
+    return p + L->rec_stride;
+  }
+  unsigned sk = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i) {
+    const spk_op *op = &L->ops[i];
+    if (op->kind == SPK_OP_COPY) { /* write_wrapper<sizeof(T)> :264-267 */
+      memcpy(p, rec + op->rec_off, op->size);
+      p += op->size;
+    }
+    else { /* container: low_bytes_write_wrapper<w> + memcpy (:304-363) */
+      uint64_t c = rec_count(rec, op);
+      put_le(p, c, w);
+      p += w;
+      uint64_t nb = c * op->size;
+      if (nb) {
+        const uint8_t *src =
+            (const uint8_t *)heaps[sk] + rec_heapoff(rec, op) * op->size;
+        memcpy(p, src, nb);
+        p += nb;
+      }
+      ++sk;
+    }
+  }
+  return p;
+}
+
+int spko_plan(const spk_layout *L, int mode, uint64_t n, const void *recs,
+              spk_plan_t *plan) {
+  if (!L || !plan || (n && !recs)) return SPK_E_ARG;
+  const uint8_t *r = (const uint8_t *)recs;
+  memset(plan, 0, sizeof(*plan));
+  if (mode == SPK_MODE_VECTOR) {
+    /* calculate_one_size container branch: size_cnt += 1, max_size = n */
+    uint64_t maxc = n, var = 0, nsp = n_spans(L);
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint8_t *rec = r + i * L->rec_stride;
+      uint64_t m = rec_max_count(L, rec);
+      if (m > maxc) maxc = m;
+      var += rec_wire_size(L, rec, 0);
+    }
+    unsigned w = width_of(maxc);
+    hdr_t h = header_shape(&L->fmt_vector, w);
+    plan->max_count = maxc;
+    plan->var_bytes = var;
+    plan->width = w;
+    plan->header_bytes = h.len + w;
+    plan->metainfo = h.meta;
+    plan->has_meta = h.has_meta;
+    plan->total_bytes = h.len + w + var + nsp * n * w;
+  }
+  else if (mode == SPK_MODE_MESSAGES) {
+    uint64_t tot = 0, maxc = 0, var = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint8_t *rec = r + i * L->rec_stride;
+      uint64_t m = rec_max_count(L, rec);
+      unsigned w = width_of(m);
+      hdr_t h = header_shape(&L->fmt_one, w);
+      if (m > maxc) maxc = m;
+      var += rec_wire_size(L, rec, 0);
+      tot += h.len + rec_wire_size(L, rec, w);
+    }
+    plan->max_count = maxc;
+    plan->var_bytes = var;
+    plan->width = width_of(maxc);
+    plan->total_bytes = tot;
+  }
+  else
+    return SPK_E_ARG;
+  return SPK_OK;
+}
+
+int spko_encode(const spk_layout *L, int mode, uint64_t n, const void *recs,
+                const void *const *heaps, void *out, uint64_t out_cap,
+                uint64_t *msg_offsets, uint64_t *written) {
+  spk_plan_t plan;
+  int rc = spko_plan(L, mode, n, recs, &plan);
+  if (rc) return rc;
+  if (written) *written = plan.total_bytes;
+  if (plan.total_bytes > out_cap) return SPK_E_CAPACITY;
+  const uint8_t *r = (const uint8_t *)recs;
+  uint8_t *p = (uint8_t *)out;
+  if (mode == SPK_MODE_VECTOR) {
+    unsigned w = plan.width;
+    hdr_t h = header_shape(&L->fmt_vector, w);
+    p = write_header(p, &L->fmt_vector, &h);
+    put_le(p, n, w); /* outer vector length prefix */
+    p += w;
+    for (uint64_t i = 0; i < n; ++i)
+      p = write_record(L, r + i * L->rec_stride, heaps, w, p);
+  }
+  else {
+    uint8_t *base = p;
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint8_t *rec = r + i * L->rec_stride;
+      unsigned w = width_of(rec_max_count(L, rec));
+      hdr_t h = header_shape(&L->fmt_one, w);
+      if (msg_offsets) msg_offsets[i] = (uint64_t)(p - base);
+      p = write_header(p, &L->fmt_one, &h);
+      p = write_record(L, rec, heaps, w, p);
+    }
+    if (msg_offsets) msg_offsets[n] = (uint64_t)(p - base);
+  }
+  return SPK_OK;
+}
+
+/* ---- decode ------------------------------------------------------------ */
+typedef struct rd_t {
+  const uint8_t *now, *end;
+} rd_t; /* memory_reader (unpacker.hpp:46-76) */
+
+static int rd_take(rd_t *r, uint64_t n, const uint8_t **p) {
+  if ((uint64_t)(r->end - r->now) < n) return 0;
+  *p = r->now;
+  r->now += n;
+  return 1;
+}
+
+/* deserialize_metainfo (unpacker.hpp:548-619) */
+static int32_t parse_header(const spk_msgfmt *f, rd_t *r, unsigned *w,
+                            uint64_t *data_len) {
+  const uint8_t *p;
+  unsigned has_container = (f->flags & SPK_MF_HAS_CONTAINER) != 0;
+  *data_len = 0;
+  *w = 1;
+  if (!(f->flags & SPK_MF_HASH_HEAD)) { /* :551-569 */
+    if (has_container) {
+      if (!rd_take(r, 1, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
+      *w = 1u << ((p[0] >> 3) & 3);
+    }
+    return SPK_ERRC_OK;
+  }
+  if (!rd_take(r, 4, &p)) return SPK_ERRC_NO_BUFFER_SPACE; /* :579-581 */
+  uint32_t cur = (uint32_t)get_le(p, 4);
+  if ((cur >> 1) != (f->code >> 1)) return SPK_ERRC_INVALID_BUFFER; /* :583 */
+  if (!(cur & 1)) return SPK_ERRC_OK; /* :586-590 no metainfo: width 1 */
+  if (!rd_take(r, 1, &p)) return SPK_ERRC_NO_BUFFER_SPACE; /* :596-600 */
+  uint8_t meta = p[0];
+  unsigned csz = meta & 3; /* compatible length field, :601-608, :494-512 */
+  if (csz) {
+    unsigned nb = csz == 1 ? 2 : csz == 2 ? 4 : 8;
+    if (!rd_take(r, nb, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
+    *data_len = get_le(p, nb);
+  }
+  if (meta & 4) { /* deserialize_type_literal :523-546 */
+    if (!rd_take(r, (uint64_t)f->literal_len + 1, &p))
+      return SPK_ERRC_NO_BUFFER_SPACE;
+    if (memcmp(p, f->literal, f->literal_len) || p[f->literal_len] != 0)
+      return SPK_ERRC_HASH_CONFLICT;
+  }
+  *w = 1u << ((meta >> 3) & 3);
+  return SPK_ERRC_OK;
+}
+
+typedef struct dctx_t {
+  const spk_layout *L;
+  void *const *heaps;
+  const uint64_t *heap_caps;
+  uint64_t used[SPK_MAX_SPANS];
+  int overflow;
+} dctx_t;
+
+/* deserialize_one for one flattened record (unpacker.hpp:780-1349):
+ * every payload failure is no_buffer_space (memory_reader::read/check). */
+static int32_t read_record(dctx_t *c, rd_t *r, unsigned w, uint8_t *rec) {
+  const spk_layout *L = c->L;
+  const uint8_t *p;
+  if (L->flags & SPK_LAYOUT_TRIVIAL) {
+    if (!rd_take(r, L->rec_stride, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
+    if (rec) memcpy(rec, p, L->rec_stride);
+    return SPK_ERRC_OK;
+  }
+  unsigned sk = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i) {
+    const spk_op *op = &L->ops[i];
+    if (op->kind == SPK_OP_COPY) {
+      if (!rd_take(r, op->size, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
+      if (rec) memcpy(rec + op->rec_off, p, op->size);
+      continue;
+    }
+    if (!rd_take(r, w, &p)) return SPK_ERRC_NO_BUFFER_SPACE; /* :905-979 */
+    uint64_t cnt = get_le(p, w);
+    if (cnt) { /* size==0 returns early (:980-982) */
+      if (op->size > 1 && cnt > UINT64_MAX / op->size) /* :1128-1132 */
+        return SPK_ERRC_NO_BUFFER_SPACE;
+      if (!rd_take(r, cnt * op->size, &p)) /* check(mem_sz) :1147-1149 */
+        return SPK_ERRC_NO_BUFFER_SPACE;
+    }
+    if (rec) {
+      uint64_t off = c->used[sk];
+      if (cnt > 0xFFFFFFFFull || off + cnt > c->heap_caps[sk]) {
+        c->overflow = 1;
+      }
+      else {
+        uint32_t c32 = (uint32_t)cnt;
+        memcpy(rec + op->rec_off, &c32, 4);
+        memcpy(rec + op->aux, &off, 8);
+        if (cnt)
+          memcpy((uint8_t *)c->heaps[sk] + off * op->size, p, cnt * op->size);
+        c->used[sk] = off + cnt;
+      }
+    }
+    ++sk;
+  }
+  return SPK_ERRC_OK;
+}
+
+int spko_decode(const spk_layout *L, int mode, const void *wire,
+                uint64_t wire_len, const uint64_t *msg_offsets, uint64_t n_msgs,
+                void *recs, uint64_t rec_cap, void *const *heaps,
+                const uint64_t *heap_caps, spk_dresult_t *res, int32_t *errc) {
+  if (!L || !res || (wire_len && !wire)) return SPK_E_ARG;
+  dctx_t c;
+  memset(&c, 0, sizeof(c));
+  c.L = L;
+  c.heaps = heaps;
+  c.heap_caps = heap_caps;
+  memset(res, 0, sizeof(*res));
+  const uint8_t *base = (const uint8_t *)wire;
+  uint8_t *out = (uint8_t *)recs;
+  if (mode == SPK_MODE_VECTOR) {
+    rd_t r = {base, base + wire_len};
+    unsigned w;
+    uint64_t data_len;
+    int32_t e = parse_header(&L->fmt_vector, &r, &w, &data_len);
+    res->width = w;
+    if (e) {
+      res->errc = e;
+      return SPK_OK;
+    }
+    const uint8_t *p;
+    if (!rd_take(&r, w, &p)) {
+      res->errc = SPK_ERRC_NO_BUFFER_SPACE;
+      return SPK_OK;
+    }
+    uint64_t n = get_le(p, w);
+    if (L->flags & SPK_LAYOUT_TRIVIAL) { /* unpacker.hpp:1127-1156 */
+      if (n > UINT64_MAX / L->rec_stride ||
+          (uint64_t)(r.end - r.now) < n * L->rec_stride) {
+        res->errc = SPK_ERRC_NO_BUFFER_SPACE;
+        return SPK_OK;
+      }
+    }
+    for (uint64_t i = 0; i < n; ++i) { /* emplace_back loop :1208-1226 */
+      uint8_t *rec = (i < rec_cap && out) ? out + i * L->rec_stride : NULL;
+      if (i >= rec_cap) c.overflow = 1;
+      e = read_record(&c, &r, w, rec);
+      if (e) {
+        res->errc = e;
+        return SPK_OK;
+      }
+    }
+    res->count = n;
+    uint64_t pos = (uint64_t)(r.now - base);
+    res->consumed = pos > data_len ? pos : data_len;
+    for (unsigned k = 0; k < SPK_MAX_SPANS; ++k) res->heap_used[k] = c.used[k];
+    if (c.overflow) res->errc = SPK_ERRC_CAPACITY;
+    return SPK_OK;
+  }
+  if (mode != SPK_MODE_MESSAGES || (n_msgs && !msg_offsets)) return SPK_E_ARG;
+  uint64_t ok = 0, consumed = 0;
+  for (uint64_t i = 0; i < n_msgs; ++i) {
+    uint64_t a = msg_offsets[i], b = msg_offsets[i + 1];
+    if (b < a || b > wire_len) return SPK_E_ARG;
+    rd_t r = {base + a, base + b};
+    unsigned w;
+    uint64_t data_len;
+    int32_t e = parse_header(&L->fmt_one, &r, &w, &data_len);
+    if (!e) {
+      if (i >= rec_cap) c.overflow = 1;
+      uint64_t save[SPK_MAX_SPANS];
+      memcpy(save, c.used, sizeof(save));
+      e = read_record(&c, &r, w,
+                      (i < rec_cap && out) ? out + i * L->rec_stride : NULL);
+      if (e) memcpy(c.used, save, sizeof(save)); /* failed: no heap use */
+    }
+    if (errc) errc[i] = e;
+    if (!e) {
+      ++ok;
+      uint64_t pos = (uint64_t)(r.now - (base + a));
+      consumed += pos > data_len ? pos : data_len;
+    }
+  }
+  res->count = ok;
+  res->consumed = consumed;
+  for (unsigned k = 0; k < SPK_MAX_SPANS; ++k) res->heap_used[k] = c.used[k];
+  res->errc = c.overflow ? SPK_ERRC_CAPACITY : SPK_ERRC_OK;
+  return SPK_OK;
+}

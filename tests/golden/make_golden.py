@@ -1,0 +1,217 @@
+#!/usr/bin/env python3
+"""Regenerate tests/golden/ from the REFERENCE struct_pack.
+
+Runs oracle/_ref/golden_gen (compiled by `make -C oracle ref` from the
+unmodified headers under /root/reference/include) and records:
+  kat.json        type literals / type codes of every record type
+  manifest.json   one entry per fixture: case, mode, n, seed, param, conf,
+                  wire length, sha256 of the wire (and of the mode-B message
+                  lengths); small fixtures also keep the wire as <name>.bin
+  errs.json       mutation tests: base wire + edits → reference errc,
+                  consume_len and canonical re-encoding of the decoded value
+The inputs are NOT stored: they are regenerated from (case, n, seed, param)
+by yalantinglibs_amd/synth.py (CPU) or spk_synth (GPU).
+
+Usage: python tests/golden/make_golden.py [--big]
+"""
+import argparse
+import hashlib
+import json
+import os
+import random
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+GEN = os.path.join(ROOT, "oracle", "_ref", "golden_gen")
+
+SEED = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004,
+        "pad": 0x5EED0005, "mixed": 0x5EED0006, "rect": 0, "rpcrect": 0x5EED0007,
+        "person": 0x5EED0008, "ints": 0x5EED0009}
+
+# (case_mode, n, param, conf, keep_bin)
+SMALL = [
+    ("rect_A", 1000, 0, "default"), ("rect_A", 20, 0, "default"),
+    ("rect_A", 0, 0, "default"), ("rect_B", 10, 0, "default"),
+    ("rec64_A", 0, 0, "default"), ("rec64_A", 1, 0, "default"),
+    ("rec64_A", 255, 0, "default"), ("rec64_A", 256, 0, "default"),
+    ("rec64_A", 1000, 0, "default"), ("rec64_A", 1000, 0, "typeinfo"),
+    ("rec64_A", 1000, 0, "nometa"), ("rec64_A", 200, 0, "nometa"),
+    ("rec64_B", 300, 0, "default"), ("rec64_B", 50, 0, "typeinfo"),
+    ("rec64_B", 50, 0, "nometa"),
+    ("recs_A", 0, 48, "default"), ("recs_A", 1, 48, "default"),
+    ("recs_A", 100, 48, "default"), ("recs_A", 300, 48, "default"),
+    ("recs_A", 3000, 48, "default"), ("recs_A", 40, 300, "default"),
+    ("recs_A", 300, 48, "typeinfo"), ("recs_A", 300, 48, "nometa"),
+    ("recs_A", 100, 48, "nometa"),
+    ("recs_B", 500, 300, "default"), ("recs_B", 200, 48, "typeinfo"),
+    ("recs_B", 100, 48, "nometa"),
+    ("outer_A", 0, 16, "default"), ("outer_A", 1, 16, "default"),
+    ("outer_A", 100, 16, "default"), ("outer_A", 1000, 16, "default"),
+    ("outer_A", 30, 400, "default"), ("outer_B", 300, 16, "default"),
+    ("outer_B", 40, 400, "default"),
+    ("pad_A", 1000, 0, "default"), ("pad_B", 100, 0, "default"),
+    ("mixed_A", 200, 40, "default"), ("mixed_A", 50, 400, "default"),
+    ("mixed_B", 200, 300, "default"), ("mixed_A", 60, 40, "typeinfo"),
+    ("rpcrect_A", 100, 0, "default"), ("rpcrect_B", 100, 0, "default"),
+    ("person_A", 100, 64, "default"), ("person_B", 100, 300, "default"),
+    ("ints_B", 100, 300, "default"), ("ints_B", 20, 3000, "default"),
+]
+MEDIUM = [  # digest only (wire > ~1 MB)
+    ("rec64_A", 65535, 0, "default"), ("rec64_A", 65536, 0, "default"),
+    ("rec64_A", 70000, 0, "default"), ("recs_A", 70000, 48, "default"),
+    ("outer_A", 70000, 16, "default"), ("mixed_A", 20000, 40, "default"),
+    ("recs_B", 70000, 48, "default"), ("outer_B", 70000, 16, "default"),
+    ("ints_B", 3, 70000, "default"), ("ints_B", 20, 70000, "default"),
+]
+BIG = [  # BASELINE.json full-size configs (digest only)
+    ("rec64_A", 100_000_000, 0, "default"),
+    ("recs_A", 10_000_000, 48, "default"),
+    ("outer_A", 10_000_000, 16, "default"),
+    ("rec64_B", 1_000_000, 0, "default"),
+    ("recs_B", 1_000_000, 48, "default"),
+]
+
+
+def name_of(cm, n, param, conf):
+    return f"{cm}_n{n}_p{param}_{conf}"
+
+
+def sha256_file(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        while True:
+            b = f.read(1 << 24)
+            if not b:
+                break
+            h.update(b)
+    return h.hexdigest()
+
+
+def emit(cm, n, param, conf, keep_bin, tmp):
+    case = cm[:-2]
+    seed = SEED[case]
+    wire = os.path.join(tmp, "wire.bin")
+    lens = os.path.join(tmp, "lens.bin")
+    subprocess.run([GEN, "emit", cm, str(n), str(seed), str(param), conf, wire, lens],
+                   check=True, stdout=subprocess.DEVNULL)
+    ent = {"name": name_of(cm, n, param, conf), "case": case, "mode": cm[-1],
+           "n": n, "seed": seed, "param": param, "conf": conf,
+           "wire_len": os.path.getsize(wire), "sha256": sha256_file(wire)}
+    if cm.endswith("_B"):
+        ent["lens_sha256"] = sha256_file(lens)
+    if keep_bin:
+        with open(wire, "rb") as f:
+            data = f.read()
+        with open(os.path.join(HERE, ent["name"] + ".bin"), "wb") as f:
+            f.write(data)
+        if cm.endswith("_B"):
+            with open(lens, "rb") as f:
+                ld = f.read()
+            with open(os.path.join(HERE, ent["name"] + ".lens"), "wb") as f:
+                f.write(ld)
+        ent["file"] = ent["name"] + ".bin"
+    os.remove(wire)
+    if os.path.exists(lens):
+        os.remove(lens)
+    return ent
+
+
+# ---- mutation tests -------------------------------------------------------
+ERR_BASES = [
+    ("recs_A", 5, 10, "default"), ("recs_A", 300, 48, "default"),
+    ("rec64_A", 3, 0, "default"), ("recs_A", 3, 20, "typeinfo"),
+    ("rect_A", 3, 0, "default"), ("outer_A", 4, 8, "default"),
+    ("rec64_A", 300, 0, "default"), ("recs_B", 1, 300, "default"),
+    ("rec64_B", 1, 0, "default"), ("mixed_A", 3, 300, "default"),
+]
+
+
+def mutations(wire_len, rng):
+    muts = [f"trunc {i}" for i in range(0, min(wire_len, 48))]
+    muts += [f"trunc {wire_len - d}" for d in (1, 2, 3, 7, 8, 9) if wire_len - d >= 48]
+    for pos in range(min(wire_len, 12)):
+        for v in (0x00, 0xFF, 0x01, 0x08, 0x10, 0x18, 0x04, 0x0C, 0x03):
+            muts.append(f"set {pos} {v}")
+    for _ in range(64):
+        pos = rng.randrange(wire_len) if wire_len else 0
+        muts.append(f"set {pos} {rng.randrange(256)}")
+    for _ in range(16):
+        pos = rng.randrange(wire_len) if wire_len else 0
+        muts.append(f"set {pos} {rng.randrange(256)} trunc {rng.randrange(wire_len + 1)}")
+    return muts
+
+
+def make_errs(tmp):
+    rng = random.Random(1234)
+    out = []
+    for cm, n, param, conf in ERR_BASES:
+        case = cm[:-2]
+        seed = SEED[case]
+        wire = os.path.join(tmp, "ewire.bin")
+        subprocess.run([GEN, "emit", cm, str(n), str(seed), str(param), conf, wire,
+                        os.path.join(tmp, "elens.bin")], check=True,
+                       stdout=subprocess.DEVNULL)
+        with open(wire, "rb") as f:
+            base = f.read()
+        muts = mutations(len(base), rng)
+        mfile = os.path.join(tmp, "muts.txt")
+        with open(mfile, "w") as f:
+            f.write("\n".join(muts) + "\n")
+        res = subprocess.run([GEN, "errs", cm, str(n), str(seed), str(param), conf,
+                              mfile, wire], check=True, capture_output=True, text=True)
+        rows = [json.loads(line) for line in res.stdout.splitlines() if line.strip()]
+        for r in rows:  # keep a digest of the canonical re-encoding, not the bytes
+            re_hex = r.pop("reenc")
+            r["reenc_sha256"] = (hashlib.sha256(bytes.fromhex(re_hex)).hexdigest()
+                                 if re_hex is not None else None)
+        assert len(rows) == len(muts), (cm, len(rows), len(muts))
+        out.append({"case": case, "mode": cm[-1], "n": n, "seed": seed, "param": param,
+                    "conf": conf, "base": base.hex(),
+                    "tests": [{"mut": m, **r} for m, r in zip(muts, rows)]})
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--big", action="store_true", help="also the full-size configs")
+    args = ap.parse_args()
+    if not os.path.exists(GEN):
+        sys.exit(f"{GEN} missing: run `make -C oracle ref` (needs /root/reference)")
+    kat = json.loads(subprocess.run([GEN, "kat"], check=True, capture_output=True,
+                                    text=True).stdout)
+    with open(os.path.join(HERE, "kat.json"), "w") as f:
+        json.dump(kat, f, indent=1, sort_keys=True)
+    man_path = os.path.join(HERE, "manifest.json")
+    old = {}
+    if os.path.exists(man_path):
+        with open(man_path) as f:
+            old = {e["name"]: e for e in json.load(f)}
+    ents = []
+    with tempfile.TemporaryDirectory() as tmp:
+        for cm, n, p, c in SMALL:
+            ents.append(emit(cm, n, p, c, True, tmp))
+        for cm, n, p, c in MEDIUM:
+            ents.append(emit(cm, n, p, c, False, tmp))
+        for cm, n, p, c in BIG:
+            nm = name_of(cm, n, p, c)
+            if args.big:
+                print("big:", nm, flush=True)
+                ents.append(emit(cm, n, p, c, False, tmp))
+            elif nm in old:
+                ents.append(old[nm])
+        for e in ents:
+            e.setdefault("size_class", "big" if any(
+                name_of(*b) == e["name"] for b in BIG) else "small")
+        with open(man_path, "w") as f:
+            json.dump(ents, f, indent=1)
+        errs = make_errs(tmp)
+    with open(os.path.join(HERE, "errs.json"), "w") as f:
+        json.dump(errs, f, indent=0)
+    print(f"{len(ents)} fixtures, {sum(len(e['tests']) for e in errs)} mutation tests")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,122 @@
+"""Shared test helpers: golden fixtures and the CPU oracle (checker only)."""
+from __future__ import annotations
+
+import ctypes as ct
+import hashlib
+import json
+import os
+
+import numpy as np
+
+from yalantinglibs_amd import _capi as C
+from yalantinglibs_amd import layout as LY
+from yalantinglibs_amd import schema as S
+from yalantinglibs_amd import synth
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+
+CONF = {"default": S.DEFAULT, "typeinfo": S.ENABLE_TYPE_INFO,
+        "nometa": S.DISABLE_ALL_META_INFO}
+
+
+def manifest():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return json.load(f)
+
+
+def kat():
+    with open(os.path.join(GOLDEN, "kat.json")) as f:
+        return json.load(f)
+
+
+def errs():
+    with open(os.path.join(GOLDEN, "errs.json")) as f:
+        return json.load(f)
+
+
+def read_fixture(ent):
+    with open(os.path.join(GOLDEN, ent["file"]), "rb") as f:
+        wire = f.read()
+    lens = None
+    if ent["mode"] == "B":
+        with open(os.path.join(GOLDEN, ent["name"] + ".lens"), "rb") as f:
+            lens = np.frombuffer(f.read(), dtype=np.uint64)
+    return wire, lens
+
+
+def sha256(b) -> str:
+    return hashlib.sha256(bytes(b)).hexdigest()
+
+
+def layout_for(ent):
+    return LY.case_layout(ent["case"], CONF[ent["conf"]])
+
+
+def mode_of(ent):
+    return C.SPK_MODE_VECTOR if ent["mode"] == "A" else C.SPK_MODE_MESSAGES
+
+
+def batch_for(ent):
+    return synth.make_batch(ent["case"], ent["n"], ent["seed"], ent["param"])
+
+
+def _ptr(a):
+    return ct.c_void_p(a.ctypes.data) if a is not None and a.size else ct.c_void_p(0)
+
+
+# ---- oracle wrappers (CPU checker) -----------------------------------------
+def oracle_encode(L, mode, recs, heaps):
+    o = C.load_oracle()
+    n = len(recs)
+    plan = C.spk_plan_t()
+    rc = o.spko_plan(L.ptr, mode, n, _ptr(recs), ct.byref(plan))
+    assert rc == 0, rc
+    out = np.zeros(max(plan.total_bytes, 1), np.uint8)
+    offs = np.zeros(n + 1, np.uint64)
+    hp = (ct.c_void_p * max(len(heaps), 1))(*[h.ctypes.data for h in heaps])
+    written = ct.c_uint64(0)
+    rc = o.spko_encode(L.ptr, mode, n, _ptr(recs), hp, _ptr(out), out.size,
+                       _ptr(offs), ct.byref(written))
+    assert rc == 0, rc
+    return out[:plan.total_bytes].tobytes(), offs, plan
+
+
+def oracle_decode(L, mode, wire: bytes, offsets=None, n_msgs=0, rec_cap=None,
+                  heap_caps=None):
+    o = C.load_oracle()
+    w = np.frombuffer(wire, np.uint8) if len(wire) else np.zeros(1, np.uint8)
+    if rec_cap is None:
+        rec_cap = max(len(wire), 1) if mode == C.SPK_MODE_VECTOR else max(n_msgs, 1)
+    recs = np.zeros(rec_cap, L.dev.dtype)
+    heaps, caps = [], []
+    for sp in L.dev.spans:
+        cap = heap_caps or (len(wire) // max(sp.elem.size, 1) + 1)
+        heaps.append(np.zeros(cap * sp.elem.size, np.uint8))
+        caps.append(cap)
+    hp = (ct.c_void_p * max(len(heaps), 1))(*[h.ctypes.data for h in heaps])
+    hc = (ct.c_uint64 * max(len(caps), 1))(*caps)
+    res = C.spk_dresult_t()
+    errc = np.zeros(max(n_msgs, 1), np.int32)
+    offs = offsets if offsets is not None else np.zeros(1, np.uint64)
+    rc = o.spko_decode(L.ptr, mode, _ptr(w), len(wire), _ptr(offs), n_msgs,
+                       _ptr(recs), rec_cap, hp, hc, ct.byref(res), _ptr(errc))
+    assert rc == 0, rc
+    return res, recs, heaps, errc
+
+
+def lens_to_offsets(lens):
+    offs = np.zeros(len(lens) + 1, np.uint64)
+    offs[1:] = np.cumsum(lens.astype(np.uint64))
+    return offs
+
+
+def records_equal(L, a, b, heaps_a, heaps_b):
+    """Compare decoded records/heaps with the synth inputs (canonical heap)."""
+    if L.dev.trivial:
+        return a.tobytes() == b.tobytes()
+    ok = a.tobytes() == b.tobytes()
+    for k, sp in enumerate(L.dev.spans):
+        used = int(a[sp.path + ".n"].astype(np.uint64).sum()) * sp.elem.size
+        ok = ok and heaps_a[k][:used].tobytes() == heaps_b[k][:used].tobytes()
+    return ok

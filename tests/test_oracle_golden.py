@@ -1,0 +1,144 @@
+"""CPU: pin the oracle and the host type model against the REFERENCE's bytes.
+
+Fixtures in tests/golden/ were produced by oracle/_ref/golden_gen, compiled
+from the unmodified reference headers (tests/golden/make_golden.py). This
+suite establishes that our CPU restatement (oracle/spk_oracle.c) and type
+model (yalantinglibs_amd/schema.py) reproduce them, so that the GPU parity
+tests may use the oracle as the checker at sizes/inputs the fixtures do not
+cover.
+"""
+import numpy as np
+import pytest
+
+import spk_helpers as H
+from yalantinglibs_amd import _capi as C
+from yalantinglibs_amd import schema as S
+from yalantinglibs_amd import synth
+
+KAT_TYPES = {
+    "Rec64": synth.Rec64, "vector<Rec64>": S.Vector(synth.Rec64),
+    "RecS": synth.RecS, "vector<RecS>": S.Vector(synth.RecS),
+    "Inner": synth.Inner, "Outer": synth.Outer, "vector<Outer>": S.Vector(synth.Outer),
+    "Pad": synth.Pad, "vector<Pad>": S.Vector(synth.Pad),
+    "Mixed": synth.Mixed, "vector<Mixed>": S.Vector(synth.Mixed),
+    "rect<int>": synth.RectInt, "vector<rect<int>>": S.Vector(synth.RectInt),
+    "rpc::point": synth.Point, "rpc::rect": synth.RpcRect,
+    "vector<rpc::rect>": S.Vector(synth.RpcRect),
+    "person": synth.Person, "vector<person>": S.Vector(synth.Person),
+    "vector<int32_t>": S.Vector(S.int32), "string": S.String(), "int32_t": S.int32,
+    "req_header": synth.ReqHeader, "resp_header": synth.RespHeader,
+    "monostate": S.Monostate(), "array<int16_t,3>": S.Array(S.int16, 3),
+    "vector<string>": S.Vector(S.String()),
+}
+
+
+@pytest.mark.parametrize("name", sorted(KAT_TYPES))
+def test_type_literal_and_code(name):
+    k = H.kat()[name]
+    t = KAT_TYPES[name]
+    assert t.root_literal().hex() == k["literal"]
+    assert t.code() == k["code"]
+
+
+def test_tuple_and_fundamentals_codes():
+    k = H.kat()
+    assert S.get_type_code(S.int32, S.int32, S.int16) == k["<int32_t,int32_t,int16_t>"]["code"]
+    fs = [S.uint8, S.uint16, S.uint32, S.uint64, S.int8, S.int16, S.int64,
+          S.boolean, S.char, S.float32, S.float64]
+    assert S.get_type_literal(*fs).hex() == k["fundamentals"]["literal"]
+
+
+def test_size_literal():
+    # get_size_literal (type_calculate.hpp:26-97)
+    assert S.size_literal(0) == bytes([129])
+    assert S.size_literal(126) == bytes([255])
+    assert S.size_literal(127) == bytes([1, 130])
+    assert S.size_literal(127 * 127) == bytes([1, 1, 130])
+
+
+SMALL = [e for e in H.manifest() if "file" in e]
+MEDIUM = [e for e in H.manifest() if "file" not in e and e["size_class"] == "small"]
+
+
+@pytest.mark.parametrize("ent", SMALL, ids=[e["name"] for e in SMALL])
+def test_oracle_encode_matches_reference(ent):
+    L = H.layout_for(ent)
+    wire, lens = H.read_fixture(ent)
+    _, recs, heaps = H.batch_for(ent)
+    got, offs, plan = H.oracle_encode(L, H.mode_of(ent), recs, heaps)
+    assert len(got) == ent["wire_len"] == len(wire)
+    assert got == wire
+    if lens is not None:
+        assert np.array_equal(np.diff(offs), lens)
+
+
+@pytest.mark.parametrize("ent", SMALL, ids=[e["name"] for e in SMALL])
+def test_oracle_decode_roundtrip_reference(ent):
+    L = H.layout_for(ent)
+    wire, lens = H.read_fixture(ent)
+    _, recs, heaps = H.batch_for(ent)
+    if ent["mode"] == "A":
+        res, out, oh, _ = H.oracle_decode(L, C.SPK_MODE_VECTOR, wire)
+        assert res.errc == 0
+        assert res.count == ent["n"]
+        assert res.consumed == len(wire)
+    else:
+        offs = H.lens_to_offsets(lens)
+        res, out, oh, errc = H.oracle_decode(L, C.SPK_MODE_MESSAGES, wire, offs, ent["n"])
+        assert res.errc == 0 and res.count == ent["n"]
+        assert (errc[:ent["n"]] == 0).all()
+    assert H.records_equal(L, out[:ent["n"]], recs, oh, heaps)
+
+
+@pytest.mark.parametrize("ent", MEDIUM, ids=[e["name"] for e in MEDIUM])
+def test_oracle_encode_digest_medium(ent):
+    L = H.layout_for(ent)
+    _, recs, heaps = H.batch_for(ent)
+    got, offs, _ = H.oracle_encode(L, H.mode_of(ent), recs, heaps)
+    assert len(got) == ent["wire_len"]
+    assert H.sha256(got) == ent["sha256"]
+    if ent["mode"] == "B":
+        assert H.sha256(np.diff(offs).astype(np.uint64).tobytes()) == ent["lens_sha256"]
+
+
+ERRS = H.errs()
+
+
+@pytest.mark.parametrize("base", ERRS, ids=[f"{b['case']}_{b['mode']}_{b['n']}_{b['conf']}"
+                                            for b in ERRS])
+def test_oracle_error_parity(base):
+    """errc / consume_len / decoded value of mutated buffers == reference."""
+    ent = dict(base)
+    L = H.layout_for(ent)
+    wire0 = bytes.fromhex(base["base"])
+    mode = H.mode_of(ent)
+    bad = []
+    for t in base["tests"]:
+        buf = bytearray(wire0)
+        toks = t["mut"].split()
+        i = 0
+        while i < len(toks):
+            if toks[i] == "trunc":
+                del buf[int(toks[i + 1]):]
+                i += 2
+            else:
+                p, v = int(toks[i + 1]), int(toks[i + 2])
+                if p < len(buf):
+                    buf[p] = v
+                i += 3
+        buf = bytes(buf)
+        if mode == C.SPK_MODE_VECTOR:
+            res, out, oh, _ = H.oracle_decode(L, mode, buf)
+            e, consumed, cnt = res.errc, res.consumed, res.count
+        else:
+            offs = np.array([0, len(buf)], np.uint64)
+            res, out, oh, errc = H.oracle_decode(L, mode, buf, offs, 1)
+            e, consumed, cnt = int(errc[0]), res.consumed, 1
+        if e != t["errc"] or (e == 0 and consumed != t["consume"]):
+            bad.append((t["mut"], e, t["errc"], consumed, t["consume"]))
+            continue
+        if e == 0:
+            re, _, _ = H.oracle_encode(L, mode, out[:cnt], oh)
+            if H.sha256(re) != t["reenc_sha256"]:
+                bad.append((t["mut"], "reenc"))
+    assert not bad, bad[:10]

@@ -1,0 +1,379 @@
+"""Host-side type model for struct_pack records (Python mirror of the C++20
+reflection in include/ylt/struct_pack/spk_reflect.hpp).
+
+Computes, exactly as the reference does at compile time:
+  * the type literal  — get_type_literal (ref include/ylt/struct_pack/
+    type_calculate.hpp:194-373) with type_id codes of type_id.hpp:25-81 and
+    get_size_literal (type_calculate.hpp:26-97);
+  * the type code     — MD5Hash32Constexpr(literal) & 0xFFFFFFFE
+    (type_calculate.hpp:507-516, md5_constexpr.hpp:315-331);
+  * is_trivial_serializable (ref reflection.hpp:851-922), alignment literals
+    (alignment.hpp:90-122) and check_if_has_container
+    (type_calculate.hpp:793-857);
+  * the sp_config resolution that decides hash head / type literal
+    (type_calculate.hpp:158-172, 744-891);
+and flattens a record type into the spk_layout descriptor of
+include/spk_codec.h (COPY / SPAN ops over a "device record").
+"""
+from __future__ import annotations
+
+import hashlib
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+# ---- sp_config (ref reflection.hpp:53-60) ---------------------------------
+DEFAULT = 0
+DISABLE_TYPE_INFO = 0b1
+ENABLE_TYPE_INFO = 0b10
+DISABLE_ALL_META_INFO = 0b11
+
+# ---- type_id (ref type_id.hpp:25-81) --------------------------------------
+TID_INT32, TID_UINT32, TID_INT64, TID_UINT64 = 1, 2, 3, 4
+TID_INT8, TID_UINT8, TID_INT16, TID_UINT16 = 5, 6, 7, 8
+TID_BOOL, TID_CHAR8 = 11, 12
+TID_FLOAT32, TID_FLOAT64 = 17, 18
+TID_STRING, TID_ARRAY, TID_MAP, TID_SET, TID_CONTAINER = 128, 129, 130, 131, 132
+TID_OPTIONAL, TID_VARIANT = 133, 134
+TID_MONOSTATE = 250
+TID_STRUCT = 253
+TID_END = 255
+
+
+def size_literal(n: int) -> bytes:
+    """get_size_literal<n>() (ref type_calculate.hpp:26-97): base-127
+    little-endian digits +1, the most significant digit +129."""
+    out = []
+    while n >= 127:
+        out.append(n % 127 + 1)
+        n //= 127
+    out.append(n + 129)
+    return bytes(out)
+
+
+def md5_hash32(data: bytes) -> int:
+    """MD5Hash32Constexpr (ref md5_constexpr.hpp:315-331): SwapEndian(a) of
+    the MD5 state == the first four digest bytes read big-endian."""
+    return int.from_bytes(hashlib.md5(data).digest()[:4], "big")
+
+
+class SpType:
+    name: str = "?"
+
+    def literal(self) -> bytes:  # get_type_literal<T>
+        raise NotImplementedError
+
+    @property
+    def trivial(self) -> bool:  # is_trivial_serializable<T>
+        return False
+
+    @property
+    def has_container(self) -> bool:  # check_if_has_container<T>
+        return False
+
+    # C layout (only meaningful for trivially serializable types)
+    size: int = 0
+    align: int = 1
+    config: int = DEFAULT  # per-type sp_config (set_sp_config ADL)
+
+    def root_literal(self) -> bytes:  # get_types_literal<T, get_types<T>...>
+        return self.literal()
+
+    def code(self) -> int:  # get_type_code<T>()
+        return md5_hash32(self.root_literal()) & 0xFFFFFFFE
+
+    def __repr__(self):
+        return self.name
+
+
+class Fund(SpType):
+    """Fundamental / enum member (get_integral_type, type_id.hpp:130-280)."""
+
+    def __init__(self, name: str, tid: int, size: int, npdt: str):
+        self.name, self.tid, self.size, self.npdt = name, tid, size, npdt
+        self.align = size
+        self.config = DEFAULT
+
+    def literal(self):
+        return bytes([self.tid])
+
+    @property
+    def trivial(self):
+        return True
+
+
+int8 = Fund("int8_t", TID_INT8, 1, "<i1")
+uint8 = Fund("uint8_t", TID_UINT8, 1, "<u1")
+int16 = Fund("int16_t", TID_INT16, 2, "<i2")
+uint16 = Fund("uint16_t", TID_UINT16, 2, "<u2")
+int32 = Fund("int32_t", TID_INT32, 4, "<i4")
+uint32 = Fund("uint32_t", TID_UINT32, 4, "<u4")
+int64 = Fund("int64_t", TID_INT64, 8, "<i8")
+uint64 = Fund("uint64_t", TID_UINT64, 8, "<u8")
+boolean = Fund("bool", TID_BOOL, 1, "<u1")
+char = Fund("char", TID_CHAR8, 1, "<u1")
+float32 = Fund("float", TID_FLOAT32, 4, "<f4")
+float64 = Fund("double", TID_FLOAT64, 8, "<f8")
+
+
+class Monostate(SpType):
+    name = "std::monostate"
+    size = 1
+    align = 1
+
+    def literal(self):
+        return bytes([TID_MONOSTATE])
+
+    @property
+    def trivial(self):
+        return True
+
+
+class Vector(SpType):
+    """std::vector<T> (container_t) — also std::span<T> (same bytes)."""
+
+    def __init__(self, elem: SpType, config: int = DEFAULT):
+        self.elem = elem
+        self.config = config
+        self.name = f"std::vector<{elem.name}>"
+
+    def literal(self):
+        return bytes([TID_CONTAINER]) + self.elem.literal()
+
+    @property
+    def has_container(self):
+        return True
+
+
+class String(SpType):
+    """std::string / std::string_view (string_t of char)."""
+
+    name = "std::string"
+
+    def __init__(self, config: int = DEFAULT):
+        self.config = config
+        self.elem = char
+
+    def literal(self):
+        return bytes([TID_STRING, TID_CHAR8])
+
+    @property
+    def has_container(self):
+        return True
+
+
+class Array(SpType):
+    """std::array<T, n> / T[n] (array_t): no length prefix on the wire."""
+
+    def __init__(self, elem: SpType, n: int):
+        assert n > 0
+        self.elem, self.n = elem, n
+        self.name = f"std::array<{elem.name},{n}>"
+        self.size = elem.size * n
+        self.align = elem.align
+        self.config = DEFAULT
+
+    def literal(self):
+        return bytes([TID_ARRAY]) + self.elem.literal() + size_literal(self.n)
+
+    @property
+    def trivial(self):
+        return self.elem.trivial
+
+    @property
+    def has_container(self):
+        return self.elem.has_container
+
+
+class Struct(SpType):
+    """An aggregate: members in declaration order (visit_members)."""
+
+    def __init__(self, name: str, fields: Sequence[Tuple[str, SpType]],
+                 config: int = DEFAULT, alignas: int = 0):
+        self.name = name
+        self.fields = list(fields)
+        self.config = config
+        self._alignas = alignas
+        # C layout
+        off = 0
+        al = 1
+        self.offsets = []
+        for _, t in self.fields:
+            a = t.align
+            off = (off + a - 1) // a * a
+            self.offsets.append(off)
+            off += t.size
+            al = max(al, a)
+        if alignas:
+            al = max(al, alignas)
+        self.align = al
+        self.size = (off + al - 1) // al * al if self.fields else 1
+
+    @property
+    def trivial(self):
+        return all(t.trivial for _, t in self.fields)
+
+    @property
+    def has_container(self):
+        return any(t.has_container for _, t in self.fields)
+
+    def literal(self):
+        body = b"".join(t.literal() for _, t in self.fields)
+        if self.trivial:
+            # pack_alignment_v (max member alignment_v) and alignment_v
+            # (alignof) literals: type_calculate.hpp:232-239, alignment.hpp
+            pack = max((t.align for _, t in self.fields), default=1)
+            return (bytes([TID_STRUCT]) + body + size_literal(pack) +
+                    size_literal(self.align) + bytes([TID_END]))
+        return bytes([TID_STRUCT]) + body + bytes([TID_END])
+
+
+class Tuple(SpType):
+    """serialize(a, b, ...) packs std::tuple<A, B, ...> (never trivial)."""
+
+    def __init__(self, *elems: SpType):
+        self.elems = elems
+        self.name = "std::tuple<" + ",".join(e.name for e in elems) + ">"
+        self.config = DEFAULT
+
+    def literal(self):
+        return (bytes([TID_STRUCT]) + b"".join(e.literal() for e in self.elems)
+                + bytes([TID_END]))
+
+    @property
+    def has_container(self):
+        return any(e.has_container for e in self.elems)
+
+
+def get_type_code(*types: SpType) -> int:
+    """struct_pack::get_type_code<Args...>() (ref struct_pack.hpp:75-92)."""
+    t = types[0] if len(types) == 1 else Tuple(*types)
+    return t.code()
+
+
+def get_type_literal(*types: SpType) -> bytes:
+    t = types[0] if len(types) == 1 else Tuple(*types)
+    return t.root_literal()
+
+
+# ---- config resolution (ref type_calculate.hpp:744-891) ------------------
+def resolve_flags(msg: SpType, conf: int = DEFAULT, debug: bool = False) -> int:
+    """SPK_MF_* flags for message type `msg` serialized with call-site
+    sp_config `conf`. `debug` models a build without NDEBUG
+    (serialize_static_config::has_type_literal, type_calculate.hpp:744-752)."""
+    from . import _capi as C
+    c = conf & 0b11
+    if c == DEFAULT:
+        c = msg.config & 0b11
+    disable_head = c == DISABLE_ALL_META_INFO
+    if c == DEFAULT:
+        type_lit = debug
+    else:
+        type_lit = c == ENABLE_TYPE_INFO
+    flags = 0
+    if not disable_head:
+        flags |= C.SPK_MF_HASH_HEAD
+        if type_lit:
+            flags |= C.SPK_MF_TYPE_LITERAL
+    if msg.has_container:
+        flags |= C.SPK_MF_HAS_CONTAINER
+    return flags
+
+
+# ---- flattening into the device-record descriptor ------------------------
+@dataclass
+class SpanField:
+    path: str
+    elem: SpType
+    count_off: int
+    off_off: int
+
+
+@dataclass
+class DeviceLayout:
+    """The flattened record: COPY / SPAN ops plus a numpy dtype of the
+    device record (what spk_codec kernels read and write)."""
+    rtype: SpType
+    stride: int
+    ops: List[Tuple[int, int, int, int]]  # (kind, rec_off, size, aux)
+    spans: List[SpanField]
+    np_fields: List[Tuple[str, str, int]]  # (name, dtype, offset)
+    trivial: bool
+
+    @property
+    def dtype(self) -> np.dtype:
+        if self.trivial:
+            return np.dtype((np.void, self.stride))
+        names = [n for n, _, _ in self.np_fields]
+        fmts = [f for _, f, _ in self.np_fields]
+        offs = [o for _, _, o in self.np_fields]
+        return np.dtype({"names": names, "formats": fmts, "offsets": offs,
+                         "itemsize": self.stride})
+
+
+def _np_format(t: SpType) -> str:
+    if isinstance(t, Fund):
+        return t.npdt
+    return f"V{t.size}"
+
+
+def flatten(rtype: SpType) -> DeviceLayout:
+    """Flatten a record type (ref packer.hpp:411-448 decides per member:
+    trivially serializable → raw sizeof bytes incl. padding; container of
+    trivially serializable → [count][raw elements])."""
+    from . import _capi as C
+    if rtype.trivial:
+        return DeviceLayout(rtype, rtype.size, [(C.SPK_OP_COPY, 0, rtype.size, 0)],
+                            [], [("raw", f"V{rtype.size}", 0)], True)
+    ops: List[Tuple[int, int, int, int]] = []
+    spans: List[SpanField] = []
+    npf: List[Tuple[str, str, int]] = []
+    cur = [0, 1]  # offset, max align
+
+    def place(size: int, align: int) -> int:
+        off = (cur[0] + align - 1) // align * align
+        cur[0] = off + size
+        cur[1] = max(cur[1], align)
+        return off
+
+    def visit(t: SpType, path: str):
+        if t.trivial:
+            off = place(t.size, t.align)
+            ops.append((C.SPK_OP_COPY, off, t.size, 0))
+            npf.append((path, _np_format(t), off))
+        elif isinstance(t, (String, Vector)):
+            if not t.elem.trivial:
+                raise NotImplementedError(
+                    f"{path}: container of non-trivially-serializable "
+                    f"{t.elem.name} is outside the flat record model")
+            coff = place(4, 4)
+            ooff = place(8, 8)
+            ops.append((C.SPK_OP_SPAN, coff, t.elem.size, ooff))
+            spans.append(SpanField(path, t.elem, coff, ooff))
+            npf.append((path + ".n", "<u4", coff))
+            npf.append((path + ".off", "<u8", ooff))
+        elif isinstance(t, Struct):
+            for fname, ft in t.fields:
+                visit(ft, f"{path}.{fname}" if path else fname)
+        elif isinstance(t, Array):
+            for i in range(t.n):
+                visit(t.elem, f"{path}[{i}]")
+        else:
+            raise NotImplementedError(f"{path}: {t.name} not in flat model")
+
+    visit(rtype, "" if isinstance(rtype, Struct) else "value")
+    if len(spans) > C.SPK_MAX_SPANS:
+        raise NotImplementedError("too many variable-length members")
+    # merge COPY runs contiguous in the record (always contiguous on the wire)
+    merged: List[Tuple[int, int, int, int]] = []
+    for op in ops:
+        if (merged and op[0] == C.SPK_OP_COPY and merged[-1][0] == C.SPK_OP_COPY
+                and merged[-1][1] + merged[-1][2] == op[1]):
+            k, o, s, a = merged[-1]
+            merged[-1] = (k, o, s + op[2], a)
+        else:
+            merged.append(op)
+    align = max(cur[1], 4)
+    stride = (cur[0] + align - 1) // align * align
+    return DeviceLayout(rtype, stride, merged, spans, npf, False)

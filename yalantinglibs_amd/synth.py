@@ -1,0 +1,193 @@
+"""Seeded synthetic record batches (numpy, host side).
+
+Restates the generator of oracle/ref/types.hpp (used by the golden
+generator compiled against the reference) so tests can rebuild the exact
+inputs behind each fixture; the device restatement is spk_synth in
+yalantinglibs_amd/csrc/spk_codec.hip (used at full size on the GPU box).
+Outputs are in device-record form (schema.flatten): a structured array of
+records plus one heap per span member.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import schema as S
+
+GOLD = np.uint64(0x9E3779B97F4A7C15)
+M1 = np.uint64(0xBF58476D1CE4E5B9)
+M2 = np.uint64(0x94D049BB133111EB)
+
+
+def mix64(z):
+    z = np.asarray(z, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * M1
+        z = (z ^ (z >> np.uint64(27))) * M2
+    return z ^ (z >> np.uint64(31))
+
+
+def rnd(seed: int, i, k):
+    i = np.asarray(i, dtype=np.uint64)
+    k = np.asarray(k, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        x = np.uint64(seed) + (i * np.uint64(64) + k + np.uint64(1)) * GOLD
+    return mix64(x)
+
+
+def rf(r):
+    return (np.asarray(r, np.uint64).astype(np.uint32).view(np.int32)
+            .astype(np.float32) / np.float32(65536.0))
+
+
+def rd(r):
+    return (np.asarray(r, np.uint64).astype(np.uint32).view(np.int32)
+            .astype(np.float64) / 65536.0)
+
+
+def i32(r):
+    return np.asarray(r, np.uint64).astype(np.uint32).view(np.int32)
+
+
+# ---- record types of the BASELINE configs (oracle/ref/types.hpp) --------
+Rec64 = S.Struct("Rec64", [("i0", S.int32), ("i1", S.int32), ("i2", S.int32),
+                           ("i3", S.int32), ("f0", S.float32), ("f1", S.float32),
+                           ("f2", S.float32), ("f3", S.float32),
+                           ("d0", S.float64), ("d1", S.float64),
+                           ("d2", S.float64), ("d3", S.float64)])
+RecS = S.Struct("RecS", [("id", S.int32), ("name", S.String()), ("v", S.float64)])
+Inner = S.Struct("Inner", [("x", S.int32), ("y", S.float32)])
+Outer = S.Struct("Outer", [("key", S.int64), ("items", S.Vector(Inner))])
+Pad = S.Struct("Pad", [("a", S.int8), ("b", S.int32), ("c", S.int16)])
+Mixed = S.Struct("Mixed", [("p", Pad), ("k", S.int64), ("arr", S.Array(S.int16, 3)),
+                           ("s", S.String()), ("v", S.Vector(S.int32))])
+RectInt = S.Struct("rect<int>", [("x", S.int32), ("y", S.int32), ("width", S.int32),
+                                 ("height", S.int32)],
+                   config=S.DISABLE_ALL_META_INFO)
+Point = S.Struct("point", [("x", S.float64), ("y", S.float64)])
+RpcRect = S.Struct("rect", [("p1", Point), ("p2", Point)])
+Person = S.Struct("person", [("id", S.int32), ("name", S.String()), ("age", S.int32),
+                             ("salary", S.float64)])
+Ints = S.Vector(S.int32)
+ReqHeader = S.Struct("req_header", [("magic", S.uint8), ("version", S.uint8),
+                                    ("serialize_type", S.uint8), ("msg_type", S.uint8),
+                                    ("seq_num", S.uint32), ("function_id", S.uint32),
+                                    ("length", S.uint32), ("attach_length", S.uint32)])
+RespHeader = S.Struct("resp_header", [("magic", S.uint8), ("version", S.uint8),
+                                      ("err_code", S.uint8), ("msg_type", S.uint8),
+                                      ("seq_num", S.uint32), ("length", S.uint32),
+                                      ("attach_length", S.uint32)])
+
+CASE_TYPES = {"rec64": Rec64, "recs": RecS, "outer": Outer, "pad": Pad,
+              "mixed": Mixed, "rect": RectInt, "rpcrect": RpcRect,
+              "person": Person, "ints": Ints}
+# vector<rect<int>> has its own ADL set_sp_config (benchmark data_def.hpp:69-72)
+VECTOR_CONFIG = {"rect": S.DISABLE_ALL_META_INFO}
+
+
+def _chars(seed, idx, lens):
+    """make_chars: char j of record i from word 2 + (j>>3)%56."""
+    total = int(lens.sum())
+    rec = np.repeat(idx, lens)
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]]) if len(lens) else np.zeros(0, np.int64)
+    j = np.arange(total, dtype=np.uint64) - np.repeat(starts, lens).astype(np.uint64)
+    w = rnd(seed, rec, np.uint64(2) + (j >> np.uint64(3)) % np.uint64(56))
+    b = (w >> ((j & np.uint64(7)) * np.uint64(8))) & np.uint64(0xFF)
+    return (np.uint64(ord("a")) + b % np.uint64(26)).astype(np.uint8)
+
+
+def make_batch(case: str, n: int, seed: int, param: int = 48):
+    """Return (layout, records ndarray, [heaps]) for n records of `case`."""
+    t = CASE_TYPES[case]
+    L = S.flatten(t)
+    recs = np.zeros(n, dtype=L.dtype)
+    idx = np.arange(n, dtype=np.uint64)
+    heaps = []
+    if case == "rec64":
+        raw = np.zeros((n, 64), np.uint8)
+        v = raw.view(np.int32).reshape(n, 16)
+        for k in range(4):
+            v[:, k] = i32(rnd(seed, idx, k))
+        raw.view(np.float32).reshape(n, 16)[:, 4:8] = np.stack(
+            [rf(rnd(seed, idx, 4 + k)) for k in range(4)], 1)
+        raw.view(np.float64).reshape(n, 8)[:, 4:8] = np.stack(
+            [rd(rnd(seed, idx, 8 + k)) for k in range(4)], 1)
+        recs = raw.view(L.dtype).reshape(n)
+    elif case == "recs":
+        lens = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+        recs["id"] = i32(rnd(seed, idx, 0))
+        recs["name.n"] = lens
+        recs["name.off"] = np.concatenate([[0], np.cumsum(lens)[:-1]]) if n else []
+        recs["v"] = rd(rnd(seed, idx, 60))
+        heaps.append(_chars(seed, idx, lens))
+    elif case == "outer":
+        cnt = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+        recs["key"] = rnd(seed, idx, 0).view(np.int64)
+        recs["items.n"] = cnt
+        recs["items.off"] = np.concatenate([[0], np.cumsum(cnt)[:-1]]) if n else []
+        rec = np.repeat(idx, cnt)
+        starts = np.concatenate([[0], np.cumsum(cnt)[:-1]]) if n else np.zeros(0, np.int64)
+        j = (np.arange(int(cnt.sum()), dtype=np.int64) - np.repeat(starts, cnt)).astype(np.uint64)
+        w = rnd(seed, rec, np.uint64(2) + j % np.uint64(62))
+        w2 = mix64(w ^ j)
+        inner = np.zeros((len(j), 8), np.uint8)
+        inner.view(np.int32).reshape(-1, 2)[:, 0] = i32(w2)
+        inner.view(np.float32).reshape(-1, 2)[:, 1] = rf(w2 >> np.uint64(32))
+        heaps.append(inner.reshape(-1))
+    elif case == "pad":
+        w = rnd(seed, idx, 0)
+        raw = np.zeros((n, 12), np.uint8)
+        raw[:, 0] = (w & np.uint64(0xFF)).astype(np.uint8)
+        raw[:, 4:8] = (w >> np.uint64(8)).astype(np.uint32)[:, None].view(np.uint8).reshape(n, 4)
+        raw[:, 8:10] = (w >> np.uint64(40)).astype(np.uint16)[:, None].view(np.uint8).reshape(n, 2)
+        recs = raw.view(L.dtype).reshape(n)
+    elif case == "mixed":
+        w = rnd(seed, idx, 0)
+        praw = np.zeros((n, 12), np.uint8)
+        praw[:, 0] = (w & np.uint64(0xFF)).astype(np.uint8)
+        praw[:, 4:8] = (w >> np.uint64(8)).astype(np.uint32)[:, None].view(np.uint8).reshape(n, 4)
+        praw[:, 8:10] = (w >> np.uint64(40)).astype(np.uint16)[:, None].view(np.uint8).reshape(n, 2)
+        recs["p"] = praw.view("V12").reshape(n)
+        recs["k"] = rnd(seed, idx, 58).view(np.int64)
+        a = rnd(seed, idx, 59)
+        arr = np.stack([(a >> np.uint64(s)).astype(np.uint16) for s in (0, 16, 32)], 1)
+        recs["arr"] = arr.view("V6").reshape(n)
+        lens = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+        recs["s.n"] = lens
+        recs["s.off"] = np.concatenate([[0], np.cumsum(lens)[:-1]]) if n else []
+        heaps.append(_chars(seed, idx, lens))
+        cnt = (rnd(seed, idx, 61) % np.uint64(param + 1)).astype(np.int64)
+        recs["v.n"] = cnt
+        recs["v.off"] = np.concatenate([[0], np.cumsum(cnt)[:-1]]) if n else []
+        rec = np.repeat(idx, cnt)
+        starts = np.concatenate([[0], np.cumsum(cnt)[:-1]]) if n else np.zeros(0, np.int64)
+        j = (np.arange(int(cnt.sum()), dtype=np.int64) - np.repeat(starts, cnt)).astype(np.uint64)
+        with np.errstate(over="ignore"):
+            vals = mix64(rnd(seed, rec, 62) + j)
+        heaps.append(i32(vals).view(np.uint8))
+    elif case == "rect":
+        raw = np.tile(np.array([1, 0, 11, 1], np.int32), (n, 1))
+        recs = raw.view(np.uint8).reshape(n, 16).view(L.dtype).reshape(n)
+    elif case == "rpcrect":
+        raw = np.stack([rd(rnd(seed, idx, k)) for k in range(4)], 1) if n else np.zeros((0, 4))
+        recs = raw.astype(np.float64).view(np.uint8).reshape(n, 32).view(L.dtype).reshape(n)
+    elif case == "person":
+        lens = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+        recs["id"] = i32(rnd(seed, idx, 0))
+        recs["name.n"] = lens
+        recs["name.off"] = np.concatenate([[0], np.cumsum(lens)[:-1]]) if n else []
+        recs["age"] = (rnd(seed, idx, 60) % np.uint64(100)).astype(np.int32)
+        recs["salary"] = rd(rnd(seed, idx, 61))
+        heaps.append(_chars(seed, idx, lens))
+    elif case == "ints":
+        cnt = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+        recs["value.n"] = cnt
+        recs["value.off"] = np.concatenate([[0], np.cumsum(cnt)[:-1]]) if n else []
+        rec = np.repeat(idx, cnt)
+        starts = np.concatenate([[0], np.cumsum(cnt)[:-1]]) if n else np.zeros(0, np.int64)
+        j = (np.arange(int(cnt.sum()), dtype=np.int64) - np.repeat(starts, cnt)).astype(np.uint64)
+        with np.errstate(over="ignore"):
+            vals = mix64(rnd(seed, rec, 2) + j)
+        heaps.append(i32(vals).view(np.uint8))
+    else:
+        raise KeyError(case)
+    return L, recs, heaps
