@@ -1,0 +1,260 @@
+#!/usr/bin/env python3
+"""bench.py — struct_pack encode+decode throughput on MI355X (device-resident).
+
+A "step" = one serialize + one deserialize of this rank's whole record batch
+through the C ABI (spk_plan + spk_encode + spk_decode), inputs already in HBM.
+Default workload (BASELINE.json configs[1], "C2"): 100M 64-byte Rec64 records
+per GPU as one struct_pack message, serialize(std::vector<Rec64>) and
+deserialize_to back. Multi-GPU: each rank owns an independent 100M-record
+shard (record-range partition, no data-path collective) => weak scaling.
+
+value = algorithmic bytes of all ranks / max-over-ranks wall time, in GiB/s:
+  per record: encode reads the record and writes its wire bytes, decode reads
+  the wire bytes and writes the record: 4 x 64 B for C2.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2b|c3|c4]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (case, records per GPU, param, mode, description)
+    "c2": ("rec64", 100_000_000, 0, "A",
+           "C2: 100M x 64-byte Rec64{int32 x4, float x4, double x4} per GPU, "
+           "serialize(vector<Rec64>) + deserialize_to"),
+    "c2b": ("rec64", 100_000_000, 0, "B",
+            "C2 mode B: 100M independent 68-byte Rec64 messages per GPU (coro_rpc payload shape)"),
+    "c3": ("recs", 10_000_000, 48, "A",
+           "C3: 10M RecS{int32, std::string len U[0,48], double} per GPU, one vector message"),
+    "c4": ("outer", 10_000_000, 16, "A",
+           "C4: 10M Outer{int64, vector<Inner{int32,float}> n U[0,16]} per GPU, one vector message"),
+}
+SEEDS = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--records", type=int, default=0, help="override records per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--host-path", action="store_true",
+                    help="also time H2D + encode + decode + D2H from pinned host buffers")
+    ap.add_argument("--pmc-json", default="", help="rocprofv3 PMC summary for roofline.traffic")
+    return ap.parse_args()
+
+
+def cpu_baseline(case, param):
+    """Reference header-only struct_pack on the host cores (rank 0 only)."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
+    if not os.path.exists(exe):
+        return None
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    n = {"rec64": 20_000_000, "recs": 4_000_000, "outer": 4_000_000}[case]
+    out = {}
+    for t in sorted({1, threads}):
+        r = subprocess.run([exe, case, str(n), str(SEEDS[case]), str(param), str(t), "10"],
+                           capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            return None
+        out[t] = json.loads(r.stdout.strip().splitlines()[-1])
+    return out, n, threads
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from yalantinglibs_amd import _capi as C
+    from yalantinglibs_amd import layout as LY
+    from yalantinglibs_amd import struct_pack as SP
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+
+    case, n, param, modech, desc = CONFIGS[args.config]
+    if args.records:
+        n = args.records
+    mode = SP.MODE_VECTOR if modech == "A" else SP.MODE_MESSAGES
+    cd = SP.Codec(LY.case_layout(case), device=dev)
+    # this rank's shard: global records [rank*n, (rank+1)*n)
+    batch = SP.synth_batch(cd, case, n, SEEDS[case], param, first=rank * n)
+    plan = cd.get_needed_size(batch, mode)
+    wire = torch.empty(plan.total_bytes + 64, dtype=torch.uint8, device=dev)
+    offs = torch.empty(n + 1, dtype=torch.int64, device=dev) if mode == SP.MODE_MESSAGES else None
+    elems = [int(h.numel()) // sp.elem.size for h, sp in zip(batch.heaps, cd.L.dev.spans)]
+    dec = cd.alloc_batch(n, elems)
+    stream = torch.cuda.current_stream(dev)
+
+    rec_bytes = batch.recs.numel() + sum(int(h.numel()) for h in batch.heaps)
+    if batch.heaps and any(e == 0 for e in elems):
+        rec_bytes = batch.recs.numel()
+    wire_bytes = plan.total_bytes
+    algo_bytes = 2 * rec_bytes + 2 * wire_bytes  # enc in/out + dec in/out
+
+    ev = []
+
+    def step(record=False):
+        e0 = torch.cuda.Event(enable_timing=True) if record else None
+        if record:
+            e0.record(stream)
+        cd.plan(batch, mode, stream)
+        e1 = torch.cuda.Event(enable_timing=True) if record else None
+        if record:
+            e1.record(stream)
+        cd.serialize_to(wire, batch, mode, offs, stream=stream, planned=True)
+        e2 = torch.cuda.Event(enable_timing=True) if record else None
+        if record:
+            e2.record(stream)
+        cd.deserialize_to(dec, wire[:plan.total_bytes], mode, offs,
+                          n if mode == SP.MODE_MESSAGES else 0, stream=stream)
+        if record:
+            e3 = torch.cuda.Event(enable_timing=True)
+            e3.record(stream)
+            ev.append((e0, e1, e2, e3))
+
+    # correctness gate before timing: round trip must be exact
+    step()
+    torch.cuda.synchronize(dev)
+    res = cd.result()
+    ok = res.errc == 0 and res.count == n and torch.equal(dec.recs, batch.recs)
+    if not ok:
+        print(json.dumps({"error": "round trip mismatch", "errc": res.errc}), flush=True)
+        sys.exit(3)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(record=True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    plan_ms = sum(a.elapsed_time(b) for a, b, _, _ in ev) / len(ev)
+    enc_ms = sum(b.elapsed_time(c) for _, b, c, _ in ev) / len(ev)
+    dec_ms = sum(c.elapsed_time(d) for _, _, c, d in ev) / len(ev)
+    ms_step = dt * 1e3 / args.steps
+    total_bytes = algo_bytes * world * args.steps
+    value = total_bytes / dt / 2**30
+    mrec = n * world * args.steps / dt / 1e6
+
+    # dominant kernel: the encode write pass (C2: shift_copy_kernel), which
+    # moves record bytes in and wire bytes out; per launch algorithmic bytes
+    enc_bytes = rec_bytes + wire_bytes
+    roof_ach = enc_bytes / (enc_ms * 1e-3) / 1e9
+    traffic = None
+    if args.pmc_json and os.path.exists(args.pmc_json):
+        with open(args.pmc_json) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    host = None
+    if args.host_path and rank == 0:
+        host = host_path(cd, batch, mode, plan, wire, dec, offs, n, stream, dev)
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cb = cpu_baseline(case, param)
+        if cb:
+            runs, cn, threads = cb
+            best = runs[threads]
+            per_rec = algo_bytes / n
+            tsec = best["encode_s"] + best["decode_s"]
+            single = runs[1]
+            cpu = {"value": round(per_rec * cn / tsec / 2**30, 3), "unit": "GiB/s",
+                   "cores": threads, "kind": "reference",
+                   "sample": f"{cn} {case} records, reference struct_pack serialize_to + "
+                             f"deserialize_to (-O3 -DNDEBUG -DSTRUCT_PACK_OPTIMIZE), "
+                             f"{threads} threads x contiguous slices, best of 10",
+                   "single_thread_gib_s": round(per_rec * cn / (single["encode_s"] +
+                                                                single["decode_s"]) / 2**30, 3),
+                   "mrec_per_s": round(cn / tsec / 1e6, 2)}
+
+    if rank == 0:
+        line = {
+            "metric": "struct_pack encode+decode throughput, device-resident (GiB/s)",
+            "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u8", "data": f"synthetic (spk_synth seeded {case}, seed {SEEDS[case]:#x})",
+            "config": {"workload": desc, "records_per_gpu": n,
+                       "mode": "vector" if modech == "A" else "messages",
+                       "wire_bytes_per_gpu": wire_bytes, "record_bytes_per_gpu": rec_bytes,
+                       "algorithmic_bytes_per_step_per_gpu": algo_bytes,
+                       "parallelism": f"record-range shards x{world}, no data-path collective"},
+            "mrec_per_s": round(mrec, 2),
+            "phase_ms": {"plan": round(plan_ms, 4), "encode": round(enc_ms, 4),
+                         "decode": round(dec_ms, 4)},
+            "roofline": {"bound": "hbm", "kernel": "encode write pass",
+                         "achieved": round(roof_ach, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(roof_ach / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "step_achieved": round(algo_bytes / (ms_step * 1e-3) / 1e9, 1),
+                         "step_frac": round(algo_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            "cpu_baseline": cpu,
+        }
+        if host:
+            line["host_path"] = host
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def host_path(cd, batch, mode, plan, wire, dec, offs, n, stream, dev):
+    """PCIe-inclusive rate: pinned host records -> H2D -> encode -> D2H wire;
+    pinned host wire -> H2D -> decode -> D2H records."""
+    import torch
+    from yalantinglibs_amd import struct_pack as SP
+    h_recs = torch.empty_like(batch.recs, device="cpu").pin_memory()
+    h_recs.copy_(batch.recs)
+    h_wire = torch.empty(plan.total_bytes, dtype=torch.uint8).pin_memory()
+    h_dec = torch.empty_like(dec.recs, device="cpu").pin_memory()
+    torch.cuda.synchronize(dev)
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        batch.recs.copy_(h_recs, non_blocking=True)
+        cd.plan(batch, mode, stream)
+        cd.serialize_to(wire, batch, mode, offs, stream=stream, planned=True)
+        h_wire.copy_(wire[:plan.total_bytes], non_blocking=True)
+        wire[:plan.total_bytes].copy_(h_wire, non_blocking=True)
+        cd.deserialize_to(dec, wire[:plan.total_bytes], mode, offs,
+                          n if mode == SP.MODE_MESSAGES else 0, stream=stream)
+        h_dec.copy_(dec.recs, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / reps
+    algo = 2 * batch.recs.numel() + 2 * plan.total_bytes
+    return {"ms_per_step": round(dt * 1e3, 3), "gib_s": round(algo / dt / 2**30, 3),
+            "note": "includes H2D of records and wire, D2H of wire and decoded records"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,80 @@
+"""CPU: the C-ABI library loads, exports every symbol include/spk_codec.h
+declares, and validates descriptors (no device work without a GPU)."""
+import ctypes as ct
+import os
+import re
+
+import pytest
+
+from yalantinglibs_amd import _capi as C
+from yalantinglibs_amd import layout as LY
+from yalantinglibs_amd import schema as S
+from yalantinglibs_amd import synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    with open(os.path.join(ROOT, "include", "spk_codec.h")) as f:
+        src = f.read()
+    return sorted(set(re.findall(r"\b(spk_[a-z_]+)\s*\(", src)))
+
+
+def test_header_symbols_exported():
+    lib = C.load_codec()
+    syms = header_symbols()
+    assert set(syms) == set(C.CODEC_SYMBOLS)
+    for s in syms:
+        assert hasattr(lib, s), s
+
+
+def test_abi_and_messages():
+    lib = C.load_codec()
+    assert lib.spk_abi_version() == C.SPK_ABI_VERSION
+    assert lib.spk_errc_message(1) == b"no buffer space"
+    assert lib.spk_errc_message(2) == b"invalid argument"
+    assert lib.spk_errc_message(3) == b"hash conflict"
+
+
+def test_struct_sizes_match_header():
+    assert ct.sizeof(C.spk_op) == 16
+    assert ct.sizeof(C.spk_msgfmt) == 16 + C.SPK_MAX_LITERAL
+    assert ct.sizeof(C.spk_plan_t) == 40
+    assert ct.sizeof(C.spk_dresult_t) == 24 + 8 * C.SPK_MAX_SPANS
+
+
+@pytest.mark.parametrize("case", sorted(synth.CASE_TYPES))
+def test_layout_check_accepts_configs(case):
+    lib = C.load_codec()
+    L = LY.case_layout(case)
+    assert lib.spk_layout_check(L.ptr) == 0
+    assert lib.spk_workspace_bytes(L.ptr, C.SPK_MODE_VECTOR, 1000, 1 << 20) > 0
+
+
+def test_layout_check_rejects_malformed():
+    lib = C.load_codec()
+    L = LY.case_layout("recs")
+    L.c.abi = 99
+    assert lib.spk_layout_check(L.ptr) == C.SPK_E_LAYOUT
+    L = LY.case_layout("recs")
+    L.c.ops[1].rec_off = 3  # misaligned count
+    assert lib.spk_layout_check(L.ptr) == C.SPK_E_LAYOUT
+    L = LY.case_layout("rec64")
+    L.c.ops[0].size = 60  # trivial layout must copy the whole record
+    assert lib.spk_layout_check(L.ptr) == C.SPK_E_LAYOUT
+
+
+def test_encode_rejects_bad_args_without_device_work():
+    lib = C.load_codec()
+    L = LY.case_layout("rec64")
+    rc = lib.spk_encode(L.ptr, 7, 10, None, None, None, None, 0, None, None, 0, None)
+    assert rc == C.SPK_E_ARG
+    rc = lib.spk_plan(L.ptr, C.SPK_MODE_VECTOR, 10, None, None, None, 0, None)
+    assert rc == C.SPK_E_ARG
+
+
+def test_oracle_is_separate_library():
+    # the product library never links the CPU restatement
+    with open(C.CODEC_PATH, "rb") as f:
+        blob = f.read()
+    assert b"spko_" not in blob

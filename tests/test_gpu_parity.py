@@ -1,0 +1,258 @@
+"""GPU parity: the HIP codec (through the C ABI) vs the reference's bytes.
+
+Checkers, in order of strength:
+  1. byte fixtures written by the reference itself (tests/golden/*.bin);
+  2. SHA-256 digests of reference outputs for larger / full-size inputs,
+     regenerated here from the same seed by spk_synth (device) or synth.py;
+  3. reference errc / consume_len for ~2.4k mutated buffers (errs.json);
+  4. the CPU oracle (pinned to 1-3 by test_oracle_golden.py) for random
+     shapes the fixtures do not cover;
+  5. size-independent properties at full size (round trip; for trivially
+     serializable records the body is the input bytes verbatim).
+Everything is bit-exact: this is byte/integer work.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+import spk_helpers as H
+from yalantinglibs_amd import _capi as C
+from yalantinglibs_amd import schema as S
+from yalantinglibs_amd import struct_pack as SP
+from yalantinglibs_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    C.load_codec()  # fail loudly if the HIP codec is missing
+
+
+_codecs = {}
+
+
+def codec_for(case, conf="default", debug=False):
+    key = (case, conf, debug)
+    if key not in _codecs:
+        from yalantinglibs_amd import layout as LY
+        _codecs[key] = SP.Codec(LY.case_layout(case, H.CONF[conf], debug))
+    return _codecs[key]
+
+
+def to_dev(codec, recs, heaps):
+    n = len(recs)
+    r = torch.from_numpy(np.ascontiguousarray(recs).view(np.uint8).reshape(n, codec.L.stride)
+                         .copy()).cuda() if n else torch.zeros((0, codec.L.stride),
+                                                               dtype=torch.uint8, device="cuda")
+    hs = [torch.from_numpy(np.ascontiguousarray(h).view(np.uint8).copy()).cuda() for h in heaps]
+    return SP.RecordBatch(codec.L, r, hs)
+
+
+def wire_dev(b: bytes):
+    a = np.frombuffer(b, np.uint8).copy() if len(b) else np.zeros(0, np.uint8)
+    return torch.from_numpy(a).cuda()
+
+
+SMALL = [e for e in H.manifest() if "file" in e]
+MEDIUM = [e for e in H.manifest() if "file" not in e and e["size_class"] == "small"]
+
+
+@pytest.mark.parametrize("ent", SMALL, ids=[e["name"] for e in SMALL])
+def test_encode_matches_reference_fixture(ent):
+    cd = codec_for(ent["case"], ent["conf"])
+    wire, lens = H.read_fixture(ent)
+    _, recs, heaps = H.batch_for(ent)
+    b = to_dev(cd, recs, heaps)
+    mode = H.mode_of(ent)
+    out, offs = cd.serialize(b, mode)
+    got = out.cpu().numpy().tobytes()
+    assert len(got) == len(wire)
+    assert got == wire
+    if lens is not None:
+        o = offs.cpu().numpy().astype(np.uint64)
+        assert o[0] == 0 and np.array_equal(np.diff(o), lens)
+
+
+@pytest.mark.parametrize("ent", SMALL, ids=[e["name"] for e in SMALL])
+def test_decode_reference_fixture(ent):
+    cd = codec_for(ent["case"], ent["conf"])
+    wire, lens = H.read_fixture(ent)
+    _, recs, heaps = H.batch_for(ent)
+    mode = H.mode_of(ent)
+    if mode == C.SPK_MODE_VECTOR:
+        res, out, _ = cd.deserialize(wire_dev(wire), mode)
+        assert res.errc == 0 and res.count == ent["n"]
+        assert res.consumed == len(wire)
+    else:
+        offs = torch.from_numpy(H.lens_to_offsets(lens).astype(np.int64)).cuda()
+        res, out, ec = cd.deserialize(wire_dev(wire), mode, offs, ent["n"])
+        assert res.errc == 0 and res.count == ent["n"]
+        assert (ec.cpu().numpy()[:ent["n"]] == 0).all()
+        assert res.consumed == len(wire)
+    got = out.recs.cpu().numpy()
+    exp = np.ascontiguousarray(recs).view(np.uint8).reshape(ent["n"], cd.L.stride)
+    assert got.tobytes() == exp.tobytes()
+    for k, sp in enumerate(cd.L.dev.spans):
+        used = res.heap_used[k] * sp.elem.size
+        assert used == len(heaps[k])
+        assert out.heaps[k][:used].cpu().numpy().tobytes() == heaps[k].tobytes()
+
+
+@pytest.mark.parametrize("ent", MEDIUM, ids=[e["name"] for e in MEDIUM])
+def test_encode_digest_medium(ent):
+    cd = codec_for(ent["case"], ent["conf"])
+    _, recs, heaps = H.batch_for(ent)
+    out, offs = cd.serialize(to_dev(cd, recs, heaps), H.mode_of(ent))
+    got = out.cpu().numpy().tobytes()
+    assert len(got) == ent["wire_len"]
+    assert H.sha256(got) == ent["sha256"]
+    if ent["mode"] == "A":  # and back
+        res, back, _ = cd.deserialize(out, C.SPK_MODE_VECTOR)
+        assert res.errc == 0 and res.count == ent["n"]
+        assert back.recs.cpu().numpy().tobytes() == np.ascontiguousarray(recs).view(np.uint8).tobytes()
+    else:
+        o = offs.cpu().numpy().astype(np.uint64)
+        assert H.sha256(np.diff(o).astype(np.uint64).tobytes()) == ent["lens_sha256"]
+
+
+ERRS = H.errs()
+
+
+@pytest.mark.parametrize("base", ERRS, ids=[f"{b['case']}_{b['mode']}_{b['n']}_{b['conf']}"
+                                            for b in ERRS])
+def test_error_parity(base):
+    """errc, consume_len and decoded value of mutated buffers == reference."""
+    ent = dict(base)
+    cd = codec_for(ent["case"], ent["conf"])
+    wire0 = bytes.fromhex(base["base"])
+    mode = H.mode_of(ent)
+    bad = []
+    for t in base["tests"]:
+        buf = bytearray(wire0)
+        toks = t["mut"].split()
+        i = 0
+        while i < len(toks):
+            if toks[i] == "trunc":
+                del buf[int(toks[i + 1]):]
+                i += 2
+            else:
+                p, v = int(toks[i + 1]), int(toks[i + 2])
+                if p < len(buf):
+                    buf[p] = v
+                i += 3
+        buf = bytes(buf)
+        if mode == C.SPK_MODE_VECTOR:
+            res, out, _ = cd.deserialize(wire_dev(buf), mode)
+            e, consumed = res.errc, res.consumed
+        else:
+            offs = torch.tensor([0, len(buf)], dtype=torch.int64, device="cuda")
+            res, out, ec = cd.deserialize(wire_dev(buf), mode, offs, 1)
+            e, consumed = int(ec[0].item()), res.consumed
+        if e != t["errc"] or (e == 0 and consumed != t["consume"]):
+            bad.append((t["mut"], e, t["errc"], consumed, t["consume"]))
+            continue
+        if e == 0:
+            b2 = SP.RecordBatch(cd.L, out.recs, [h for h in out.heaps])
+            re, _ = cd.serialize(b2, mode)
+            if H.sha256(re.cpu().numpy().tobytes()) != t["reenc_sha256"]:
+                bad.append((t["mut"], "reenc"))
+    assert not bad, bad[:10]
+
+
+RANDOM = [("recs", 1, 300), ("recs", 257, 5), ("recs", 5000, 48), ("recs", 20000, 200),
+          ("outer", 3000, 16), ("outer", 500, 300), ("mixed", 700, 70), ("person", 999, 30),
+          ("pad", 12345, 0), ("rec64", 4099, 0), ("rpcrect", 77, 0), ("ints", 400, 100)]
+
+
+@pytest.mark.parametrize("case,n,param", RANDOM)
+@pytest.mark.parametrize("modech", ["A", "B"])
+def test_random_vs_oracle(case, n, param, modech):
+    cd = codec_for(case)
+    L, recs, heaps = synth.make_batch(case, n, 0xC0FFEE + n, param)
+    mode = C.SPK_MODE_VECTOR if modech == "A" else C.SPK_MODE_MESSAGES
+    exp, eoffs, _ = H.oracle_encode(cd.L, mode, recs, heaps)
+    out, offs = cd.serialize(to_dev(cd, recs, heaps), mode)
+    assert out.cpu().numpy().tobytes() == exp
+    if mode == C.SPK_MODE_VECTOR:
+        res, back, _ = cd.deserialize(out, mode)
+    else:
+        assert np.array_equal(offs.cpu().numpy().astype(np.uint64), eoffs)
+        res, back, _ = cd.deserialize(out, mode, offs, n)
+    assert res.errc == 0 and res.count == n
+    assert back.recs.cpu().numpy().tobytes() == np.ascontiguousarray(recs).view(np.uint8).tobytes()
+    for k in range(len(heaps)):
+        nb = len(heaps[k])
+        assert back.heaps[k][:nb].cpu().numpy().tobytes() == heaps[k].tobytes()
+
+
+def test_large_records_fallback():
+    """Records straddling chunk boundaries by >255 B take the sequential walker."""
+    cd = codec_for("recs")
+    L, recs, heaps = synth.make_batch("recs", 300, 77, 20000)
+    exp, _, _ = H.oracle_encode(cd.L, C.SPK_MODE_VECTOR, recs, heaps)
+    res, back, _ = cd.deserialize(wire_dev(exp), C.SPK_MODE_VECTOR)
+    assert res.errc == 0 and res.count == 300 and res.consumed == len(exp)
+    assert back.recs.cpu().numpy().tobytes() == np.ascontiguousarray(recs).view(np.uint8).tobytes()
+    assert back.heaps[0][:len(heaps[0])].cpu().numpy().tobytes() == heaps[0].tobytes()
+
+
+@pytest.mark.parametrize("kind,case,param", [("rec64", "rec64", 0), ("recs", "recs", 48),
+                                              ("outer", "outer", 16)])
+def test_device_synth_matches_host_generator(kind, case, param):
+    cd = codec_for(case)
+    n = 3001
+    seed = 0x5EED0003
+    b = SP.synth_batch(cd, kind, n, seed, param)
+    _, recs, heaps = synth.make_batch(case, n, seed, param)
+    assert b.recs.cpu().numpy().tobytes() == np.ascontiguousarray(recs).view(np.uint8).tobytes()
+    for k in range(len(heaps)):
+        assert b.heaps[k][:len(heaps[k])].cpu().numpy().tobytes() == heaps[k].tobytes()
+
+
+BIG = [e for e in H.manifest() if e["size_class"] == "big"]
+
+
+def _sha_dev(t: torch.Tensor) -> str:
+    h = hashlib.sha256()
+    step = 1 << 28
+    for i in range(0, t.numel(), step):
+        h.update(t[i:i + step].cpu().numpy().tobytes())
+    return h.hexdigest()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("ent", BIG, ids=[e["name"] for e in BIG])
+def test_full_size_configs(ent):
+    """BASELINE configs at full size: digest of the reference's bytes for the
+    same seeded input, plus the decode round trip."""
+    cd = codec_for(ent["case"])
+    b = SP.synth_batch(cd, ent["case"], ent["n"], ent["seed"], ent["param"])
+    mode = H.mode_of(ent)
+    out, offs = cd.serialize(b, mode)
+    assert out.numel() == ent["wire_len"]
+    if ent["case"] == "rec64" and mode == C.SPK_MODE_VECTOR:
+        # size-independent: trivially serializable body == input bytes
+        hdr = out.numel() - b.recs.numel()
+        assert torch.equal(out[hdr:], b.recs.reshape(-1))
+    assert _sha_dev(out) == ent["sha256"]
+    elems = [int(h.numel()) // sp.elem.size for h, sp in zip(b.heaps, cd.L.dev.spans)]
+    if mode == C.SPK_MODE_VECTOR:
+        dec = cd.alloc_batch(ent["n"], elems)
+        cd.deserialize_to(dec, out, mode)
+        res = cd.result()
+        assert res.errc == 0 and res.count == ent["n"] and res.consumed == out.numel()
+    else:
+        dec = cd.alloc_batch(ent["n"], elems)
+        cd.deserialize_to(dec, out, mode, offs, ent["n"])
+        res = cd.result()
+        assert res.errc == 0 and res.count == ent["n"]
+    assert torch.equal(dec.recs, b.recs)
+    for k in range(len(b.heaps)):
+        assert torch.equal(dec.heaps[k], b.heaps[k])
+    del out, dec, b
+    torch.cuda.empty_cache()

@@ -1,0 +1,146 @@
+// spk_api.hip — the extern "C" boundary of include/spk_codec.h.
+//
+// Host-side argument validation and dispatch only: trivially-serializable
+// layouts go to spk_fixed.hip, layouts with variable-length members to
+// spk_var.hip. No allocation, no synchronisation: everything is enqueued on
+// the caller's stream. There is no CPU path behind these symbols.
+#include "spk_internal.hpp"
+
+using namespace spk;
+
+static int hip_rc(hipError_t e) { return e == hipSuccess ? SPK_OK : SPK_E_HIP; }
+
+static bool is_trivial(const spk_layout *L) { return (L->flags & SPK_LAYOUT_TRIVIAL) != 0; }
+
+extern "C" {
+
+uint32_t spk_abi_version(void) { return SPK_ABI_VERSION; }
+
+// error_code.hpp:28-43 (make_error_message)
+const char *spk_errc_message(int32_t e) {
+  switch (e) {
+    case SPK_ERRC_OK: return "ok";
+    case SPK_ERRC_NO_BUFFER_SPACE: return "no buffer space";
+    case SPK_ERRC_INVALID_BUFFER: return "invalid argument";
+    case SPK_ERRC_HASH_CONFLICT: return "hash conflict";
+    case SPK_ERRC_INVALID_WIDTH: return "invalid width of container length";
+    case SPK_ERRC_CAPACITY: return "device output capacity exceeded";
+    default: return "(unrecognized error)";
+  }
+}
+
+int spk_layout_check(const spk_layout *L) {
+  if (!L || L->abi != SPK_ABI_VERSION) return SPK_E_LAYOUT;
+  if (L->n_ops == 0 || L->n_ops > SPK_MAX_OPS || L->rec_stride == 0) return SPK_E_LAYOUT;
+  if (L->fmt_vector.literal_len > SPK_MAX_LITERAL || L->fmt_one.literal_len > SPK_MAX_LITERAL)
+    return SPK_E_LAYOUT;
+  if (!(L->fmt_vector.flags & SPK_MF_HAS_CONTAINER)) return SPK_E_LAYOUT;  // vector<T>
+  if (is_trivial(L)) {
+    const spk_op &o = L->ops[0];
+    if (L->n_ops != 1 || o.kind != SPK_OP_COPY || o.rec_off != 0 || o.size != L->rec_stride)
+      return SPK_E_LAYOUT;
+    if (L->fmt_one.flags & SPK_MF_HAS_CONTAINER) return SPK_E_LAYOUT;
+    return SPK_OK;
+  }
+  uint32_t spans = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i) {
+    const spk_op &o = L->ops[i];
+    if (o.kind == SPK_OP_COPY) {
+      if (o.size == 0 || (uint64_t)o.rec_off + o.size > L->rec_stride) return SPK_E_LAYOUT;
+    } else if (o.kind == SPK_OP_SPAN) {
+      if (o.size == 0 || o.rec_off % 4 || o.aux % 8 || o.rec_off + 4 > L->rec_stride ||
+          o.aux + 8 > L->rec_stride)
+        return SPK_E_LAYOUT;
+      ++spans;
+    } else {
+      return SPK_E_LAYOUT;
+    }
+  }
+  if (spans == 0 || spans > SPK_MAX_SPANS || L->rec_stride % 8) return SPK_E_LAYOUT;
+  if (!(L->fmt_one.flags & SPK_MF_HAS_CONTAINER)) return SPK_E_LAYOUT;
+  return SPK_OK;
+}
+
+size_t spk_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len) {
+  if (spk_layout_check(L) != SPK_OK) return 0;
+  if (is_trivial(L)) return kWsScratch + (n + 1) * 8 + 256;
+  return var_workspace_bytes(L, mode, n, wire_len);
+}
+
+int spk_plan(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
+             spk_plan_t *d_plan, void *d_ws, size_t ws_bytes, void *stream) {
+  int rc = spk_layout_check(L);
+  if (rc) return rc;
+  if ((mode != SPK_MODE_VECTOR && mode != SPK_MODE_MESSAGES) || !d_plan || !d_ws)
+    return SPK_E_ARG;
+  if (n && !d_recs) return SPK_E_ARG;
+  if (ws_bytes < spk_workspace_bytes(L, mode, n, 0)) return SPK_E_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  if (is_trivial(L)) return hip_rc(launch_fixed_plan(L, mode, n, d_plan, d_ws, s));
+  if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
+  return hip_rc(launch_var_plan(L, mode, n, d_recs, d_plan, d_ws, ws_bytes, s));
+}
+
+int spk_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
+               const void *const *d_heaps, const spk_plan_t *d_plan, void *d_out,
+               uint64_t out_cap, uint64_t *d_msg_offsets, void *d_ws, size_t ws_bytes,
+               void *stream) {
+  int rc = spk_layout_check(L);
+  if (rc) return rc;
+  if ((mode != SPK_MODE_VECTOR && mode != SPK_MODE_MESSAGES) || !d_plan || !d_ws || !d_out)
+    return SPK_E_ARG;
+  if (n && !d_recs) return SPK_E_ARG;
+  if (ws_bytes < spk_workspace_bytes(L, mode, n, 0)) return SPK_E_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  if (is_trivial(L)) {
+    uint8_t hb[4 + 1 + SPK_MAX_LITERAL + 1];
+    if (mode == SPK_MODE_VECTOR) {
+      const uint32_t w = width_of(n);
+      const uint64_t total = write_hdr(hb, L->fmt_vector, w) + w + n * (uint64_t)L->rec_stride;
+      if (total > out_cap) return SPK_E_CAPACITY;
+      return hip_rc(launch_fixed_encode_vector(L, n, d_recs, d_out, d_ws, s));
+    }
+    const uint64_t total = n * (uint64_t)(write_hdr(hb, L->fmt_one, 1) + L->rec_stride);
+    if (total > out_cap) return SPK_E_CAPACITY;
+    return hip_rc(launch_fixed_encode_messages(L, n, d_recs, d_out, d_msg_offsets, s));
+  }
+  if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
+  uint32_t spans = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i) spans += L->ops[i].kind == SPK_OP_SPAN;
+  if (!d_heaps) return SPK_E_ARG;
+  for (uint32_t k = 0; k < spans; ++k)
+    if (!d_heaps[k] && n) return SPK_E_ARG;
+  return hip_rc(launch_var_encode(L, mode, n, d_recs, d_heaps, d_plan, d_out, out_cap,
+                                  d_msg_offsets, d_ws, ws_bytes, s));
+}
+
+int spk_decode(const spk_layout *L, int mode, const void *d_wire, uint64_t wire_len,
+               const uint64_t *d_msg_offsets, uint64_t n_msgs, void *d_recs,
+               uint64_t rec_cap, void *const *d_heaps, const uint64_t *heap_caps,
+               spk_dresult_t *d_res, int32_t *d_errc, void *d_ws, size_t ws_bytes,
+               void *stream) {
+  int rc = spk_layout_check(L);
+  if (rc) return rc;
+  if ((mode != SPK_MODE_VECTOR && mode != SPK_MODE_MESSAGES) || !d_res || !d_ws)
+    return SPK_E_ARG;
+  if (wire_len && !d_wire) return SPK_E_ARG;
+  if (rec_cap && !d_recs) return SPK_E_ARG;
+  const uint64_t nrec = mode == SPK_MODE_VECTOR ? rec_cap : n_msgs;
+  if (ws_bytes < spk_workspace_bytes(L, mode, nrec, wire_len)) return SPK_E_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  if (is_trivial(L)) {
+    if (mode == SPK_MODE_VECTOR)
+      return hip_rc(launch_fixed_decode_vector(L, d_wire, wire_len, d_recs, rec_cap, d_res,
+                                               d_ws, s));
+    return hip_rc(launch_fixed_decode_messages(L, d_wire, wire_len, d_msg_offsets, n_msgs,
+                                               d_recs, rec_cap, d_res, d_errc, d_ws, s));
+  }
+  if (d_recs && (uintptr_t)d_recs % 8) return SPK_E_ARG;
+  if (!d_heaps || !heap_caps) return SPK_E_ARG;
+  if (mode == SPK_MODE_MESSAGES && n_msgs && !d_msg_offsets) return SPK_E_ARG;
+  return hip_rc(launch_var_decode(L, mode, d_wire, wire_len, d_msg_offsets, n_msgs, d_recs,
+                                  rec_cap, d_heaps, heap_caps, d_res, d_errc, d_ws, ws_bytes,
+                                  s));
+}
+
+}  // extern "C"

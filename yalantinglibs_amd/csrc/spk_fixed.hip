@@ -1,0 +1,529 @@
+// spk_fixed.hip — gfx950 kernels for trivially-serializable records
+// (is_trivial_serializable<T>: one raw sizeof(T) copy per record, incl.
+// padding — ref packer.hpp:411-421, unpacker.hpp:1127-1156,1293-1312).
+//
+// SPK_MODE_VECTOR: the message is [header][count:w][n*stride raw bytes], so
+// encode and decode are byte-shifted stream copies between a 16-B aligned
+// buffer and one displaced by the header length h. `shift_copy` moves whole
+// aligned 16-B chunks: each lane loads one chunk per unroll step
+// (global_load_dwordx4, 1 KiB per wave-instruction, fully coalesced), takes
+// its right neighbour's chunk with ds_bpermute (lane 63 takes the next
+// step's lane 0 via v_readlane) and funnels the two with v_alignbyte into the
+// displaced output chunk — every HBM byte is read once and written once.
+// The shift is data-dependent on decode (width/meta/type-literal of the
+// incoming header), so the kernel switches on it (wave-uniform) among 16
+// template instances instead of re-launching.
+//
+// SPK_MODE_MESSAGES: n independent [header][record] messages (coro_rpc
+// payloads): a dword gather when header and stride are multiples of 4,
+// byte gather otherwise.
+#include "spk_internal.hpp"
+
+namespace spk {
+
+// ---------------------------------------------------------------------------
+// copy job: dst[dst_off + i] = src[src_off + i], i < nbytes; optionally
+// prefixed by hdr_len header bytes taken from `hdr` written at dst[dst_off -
+// hdr_len ...]. Lives in device memory so that decode can derive it from the
+// incoming header without a host round trip.
+struct CopyJob {
+  uint64_t dst_off;
+  uint64_t src_off;
+  uint64_t nbytes;
+  uint64_t hdr_len;  // header bytes written before dst_off (encode)
+};
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t r) {
+  // bytes [r, r+4) of the 8-byte little-endian pair (lo, hi)
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * r));
+}
+
+template <int R>
+__device__ __forceinline__ v4u funnel16(const v4u &a, const v4u &b) {
+  if constexpr (R == 0) {
+    return a;
+  } else {
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    constexpr int q = R >> 2, r = R & 3;
+    v4u o;
+    if constexpr (r == 0) {
+      o.x = w[q + 0];
+      o.y = w[q + 1];
+      o.z = w[q + 2];
+      o.w = w[q + 3];
+    } else {
+      o.x = funnel(w[q + 0], w[q + 1], r);
+      o.y = funnel(w[q + 1], w[q + 2], r);
+      o.z = funnel(w[q + 2], w[q + 3], r);
+      o.w = funnel(w[q + 3], w[q + 4], r);
+    }
+    return o;
+  }
+}
+
+__device__ __forceinline__ v4u shfl_next(const v4u &v, uint32_t lane) {
+  const int addr = (int)(((lane + 1) & 63) << 2);
+  v4u o;
+  o.x = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v.x);
+  o.y = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v.y);
+  o.z = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v.z);
+  o.w = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v.w);
+  return o;
+}
+__device__ __forceinline__ v4u lane0_of(const v4u &v) {
+  v4u o;
+  o.x = (uint32_t)__builtin_amdgcn_readlane((int)v.x, 0);
+  o.y = (uint32_t)__builtin_amdgcn_readlane((int)v.y, 0);
+  o.z = (uint32_t)__builtin_amdgcn_readlane((int)v.z, 0);
+  o.w = (uint32_t)__builtin_amdgcn_readlane((int)v.w, 0);
+  return o;
+}
+
+constexpr int kCopyThreads = 256;
+constexpr int kCopyUnroll = 4;
+constexpr uint64_t kTile = 64ull * kCopyUnroll;  // chunks per wave-tile
+
+// dst chunk k (k in [k0, k1)) = src bytes [16*(k+q) + R, +16)
+template <int R>
+__device__ void shift_body(v4u *__restrict__ dst, const v4u *__restrict__ src,
+                           uint64_t k0, uint64_t k1, int64_t q) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wid = (uint64_t)blockIdx.x * (kCopyThreads / 64) + (threadIdx.x >> 6);
+  const uint64_t nw = (uint64_t)gridDim.x * (kCopyThreads / 64);
+  for (uint64_t t0 = k0 + wid * kTile; t0 < k1; t0 += nw * kTile) {
+    if (t0 + kTile <= k1) {
+      v4u cur[kCopyUnroll];
+#pragma unroll
+      for (int j = 0; j < kCopyUnroll; ++j)
+        cur[j] = __builtin_nontemporal_load(&src[(int64_t)(t0 + j * 64 + lane) + q]);
+      if constexpr (R == 0) {
+#pragma unroll
+        for (int j = 0; j < kCopyUnroll; ++j)
+          __builtin_nontemporal_store(cur[j], &dst[t0 + j * 64 + lane]);
+      } else {
+        // first chunk after the tile (same address in every lane: 1 request)
+        const v4u extra = src[(int64_t)(t0 + kTile) + q];
+#pragma unroll
+        for (int j = 0; j < kCopyUnroll; ++j) {
+          // lane 0 of the next step, read with v_readlane while all lanes
+          // are active (never inside the lane==63 branch)
+          const v4u l0 = (j + 1 < kCopyUnroll) ? lane0_of(cur[j + 1]) : extra;
+          const v4u nb = shfl_next(cur[j], lane);
+          const v4u nx = lane == 63 ? l0 : nb;
+          __builtin_nontemporal_store(funnel16<R>(cur[j], nx), &dst[t0 + j * 64 + lane]);
+        }
+      }
+    } else {
+      for (uint64_t k = t0 + lane; k < k1 && k < t0 + kTile; k += 64) {
+        const v4u a = src[(int64_t)k + q];
+        const v4u b = R ? src[(int64_t)k + q + 1] : a;
+        dst[k] = funnel16<R>(a, b);
+      }
+    }
+  }
+}
+
+// One launch covers: header bytes, the byte-wise head/tail of the range, and
+// the aligned interior. `job` may be written by a preceding kernel.
+__global__ __launch_bounds__(kCopyThreads) void shift_copy_kernel(
+    uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+    const CopyJob *__restrict__ job, const uint8_t *__restrict__ hdr) {
+  const uint64_t dst_off = job->dst_off, src_off = job->src_off, nb = job->nbytes;
+  const uint64_t hdr_len = job->hdr_len;
+  uint8_t *d = dst + dst_off;
+  const uint8_t *s = src + src_off;
+  const uint64_t dmis = (uint64_t)d & 15;
+  // interior: aligned dst chunks fully inside [d, d+nb)
+  uint64_t head = dmis ? 16 - dmis : 0;
+  if (head > nb) head = nb;
+  const uint64_t body = (nb - head) & ~15ull;
+  const uint64_t tail_start = head + body;
+  if (blockIdx.x == 0) {
+    for (uint64_t i = threadIdx.x; i < hdr_len; i += blockDim.x)
+      dst[dst_off - hdr_len + i] = hdr[i];
+    for (uint64_t i = threadIdx.x; i < head; i += blockDim.x) d[i] = s[i];
+    for (uint64_t i = tail_start + threadIdx.x; i < nb; i += blockDim.x) d[i] = s[i];
+  }
+  if (body == 0) return;
+  v4u *dc = reinterpret_cast<v4u *>(d + head);
+  const uint8_t *sp = s + head;  // source of dc[0]
+  const uint64_t smis = (uint64_t)sp & 15;
+  const v4u *sc = reinterpret_cast<const v4u *>(sp - smis);
+  const uint64_t nk = body >> 4;
+  switch (smis) {  // wave-uniform
+#define SPK_CASE(r) \
+  case r:           \
+    shift_body<r>(dc, sc, 0, nk, 0); \
+    break;
+    SPK_CASE(0) SPK_CASE(1) SPK_CASE(2) SPK_CASE(3) SPK_CASE(4) SPK_CASE(5)
+    SPK_CASE(6) SPK_CASE(7) SPK_CASE(8) SPK_CASE(9) SPK_CASE(10) SPK_CASE(11)
+    SPK_CASE(12) SPK_CASE(13) SPK_CASE(14) SPK_CASE(15)
+#undef SPK_CASE
+  }
+}
+
+static unsigned copy_grid(uint64_t max_bytes) {
+  uint64_t tiles = (max_bytes / 16 + kTile - 1) / kTile;
+  uint64_t blocks = (tiles + (kCopyThreads / 64) - 1) / (kCopyThreads / 64);
+  // enough waves to fill 256 CUs x 8 waves, grid-stride beyond that
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  return (unsigned)blocks;
+}
+
+// ---------------------------------------------------------------------------
+// Plan for trivial records: O(1), written by a 1-thread kernel so the whole
+// encode stays stream-ordered and graph-capturable.
+struct FixedPlanArgs {
+  spk_msgfmt fmt;  // message format (vector or one)
+  uint64_t n;
+  uint32_t stride;
+  int mode;
+};
+
+__global__ void fixed_plan_kernel(FixedPlanArgs a, spk_plan_t *plan, uint8_t *ws) {
+  if (threadIdx.x != 0) return;
+  spk_plan_t p;
+  if (a.mode == SPK_MODE_VECTOR) {
+    const uint32_t w = width_of(a.n);  // max_size = n (calculate_size.hpp:79)
+    const HdrShape h = hdr_shape(a.fmt.flags, a.fmt.literal_len, w);
+    uint8_t *hb = ws + kWsHdrVec;
+    uint32_t len = write_hdr(hb, a.fmt, w);
+    for (uint32_t i = 0; i < w; ++i) hb[len + i] = (uint8_t)(a.n >> (8 * i));
+    CopyJob *job = reinterpret_cast<CopyJob *>(ws + kWsCtl);
+    job->hdr_len = len + w;
+    job->dst_off = len + w;
+    job->src_off = 0;
+    job->nbytes = a.n * a.stride;
+    p.total_bytes = len + w + a.n * a.stride;
+    p.max_count = a.n;
+    p.var_bytes = a.n * a.stride;
+    p.width = w;
+    p.header_bytes = len + w;
+    p.metainfo = h.meta;
+    p.has_meta = h.has_meta;
+  } else {
+    const HdrShape h = hdr_shape(a.fmt.flags, a.fmt.literal_len, 1);
+    write_hdr(ws + kWsHdrMsg, a.fmt, 1);
+    p.total_bytes = a.n * (h.len + a.stride);
+    p.max_count = 0;
+    p.var_bytes = a.n * a.stride;
+    p.width = 1;
+    p.header_bytes = h.len;
+    p.metainfo = h.meta;
+    p.has_meta = h.has_meta;
+  }
+  *plan = p;
+}
+
+hipError_t launch_fixed_plan(const spk_layout *L, int mode, uint64_t n,
+                             spk_plan_t *d_plan, void *d_ws, hipStream_t s) {
+  FixedPlanArgs a;
+  a.fmt = mode == SPK_MODE_VECTOR ? L->fmt_vector : L->fmt_one;
+  a.n = n;
+  a.stride = L->rec_stride;
+  a.mode = mode;
+  hipLaunchKernelGGL(fixed_plan_kernel, dim3(1), dim3(64), 0, s, a, d_plan,
+                     (uint8_t *)d_ws);
+  return hipGetLastError();
+}
+
+hipError_t launch_fixed_encode_vector(const spk_layout *L, uint64_t n,
+                                      const void *d_recs, void *d_out,
+                                      const void *d_ws, hipStream_t s) {
+  const uint8_t *ws = (const uint8_t *)d_ws;
+  const uint64_t max_bytes = n * (uint64_t)L->rec_stride;
+  hipLaunchKernelGGL(shift_copy_kernel, dim3(copy_grid(max_bytes)), dim3(kCopyThreads),
+                     0, s, (uint8_t *)d_out, (const uint8_t *)d_recs,
+                     reinterpret_cast<const CopyJob *>(ws + kWsCtl), ws + kWsHdrVec);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// SPK_MODE_VECTOR decode: parse + validate the header on one wave (the
+// reference's deserialize_metainfo, unpacker.hpp:548-619, then the
+// trivially-copyable container branch :904-982,1127-1156), publish a CopyJob,
+// then the same shift_copy moves the payload. The result is written before
+// the copy; the copy length is 0 unless the header and length check passed.
+struct FixedDecArgs {
+  spk_msgfmt fmt;
+  uint64_t wire_len;
+  uint64_t rec_cap;
+  uint32_t stride;
+};
+
+__global__ void fixed_decode_hdr_kernel(FixedDecArgs a, const uint8_t *wire,
+                                        CopyJob *job, spk_dresult_t *res) {
+  if (threadIdx.x != 0) return;
+  uint64_t pos, data_len;
+  uint32_t w;
+  int32_t e = parse_hdr(a.fmt, wire, a.wire_len, &pos, &w, &data_len);
+  uint64_t n = 0;
+  if (!e) {
+    if (a.wire_len < pos + w) {
+      e = SPK_ERRC_NO_BUFFER_SPACE;
+    } else {
+      n = ld_le(wire + pos, w);
+      pos += w;
+      // overflow guard + check(mem_sz) (unpacker.hpp:1128-1149)
+      if (n > ~0ull / a.stride || a.wire_len - pos < n * a.stride)
+        e = SPK_ERRC_NO_BUFFER_SPACE;
+    }
+  }
+  spk_dresult_t r = {};
+  r.errc = e;
+  r.width = w;
+  job->hdr_len = 0;
+  job->dst_off = 0;
+  job->src_off = pos;
+  job->nbytes = 0;
+  if (!e) {
+    r.count = n;
+    const uint64_t end = pos + n * a.stride;
+    r.consumed = end > data_len ? end : data_len;
+    if (n > a.rec_cap)
+      r.errc = SPK_ERRC_CAPACITY;
+    else
+      job->nbytes = n * a.stride;
+  }
+  *res = r;
+}
+
+hipError_t launch_fixed_decode_vector(const spk_layout *L, const void *d_wire,
+                                         uint64_t wire_len, void *d_recs,
+                                         uint64_t rec_cap, spk_dresult_t *d_res,
+                                         void *d_ws, hipStream_t s) {
+  FixedDecArgs a;
+  a.fmt = L->fmt_vector;
+  a.wire_len = wire_len;
+  a.rec_cap = rec_cap;
+  a.stride = L->rec_stride;
+  CopyJob *job = reinterpret_cast<CopyJob *>((uint8_t *)d_ws + kWsCtl);
+  hipLaunchKernelGGL(fixed_decode_hdr_kernel, dim3(1), dim3(64), 0, s, a,
+                     (const uint8_t *)d_wire, job, d_res);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  uint64_t max_bytes = rec_cap * (uint64_t)L->rec_stride;
+  if (max_bytes > wire_len) max_bytes = wire_len;
+  hipLaunchKernelGGL(shift_copy_kernel, dim3(copy_grid(max_bytes)), dim3(kCopyThreads),
+                     0, s, (uint8_t *)d_recs, (const uint8_t *)d_wire,
+                     (const CopyJob *)job, (const uint8_t *)nullptr);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// SPK_MODE_MESSAGES, trivial records: message i = [hdr (H bytes)][record].
+struct MsgEncArgs {
+  uint64_t n;
+  uint32_t stride;  // bytes
+  uint32_t hlen;    // header bytes
+  uint8_t hdr[256];
+};
+
+// dword gather: out dword d -> message i = d / Mw, word r = d % Mw
+__global__ __launch_bounds__(256) void fixed_msg_encode_w4(
+    MsgEncArgs a, const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+    uint64_t *__restrict__ offs) {
+  const uint32_t Hw = a.hlen >> 2, Sw = a.stride >> 2, Mw = Hw + Sw;
+  const uint64_t total_w = a.n * Mw;
+  const uint64_t nchunks = (total_w + 3) >> 2;
+  const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks;
+       c += gstride) {
+    const uint64_t d0 = c << 2;
+    uint64_t i = d0 / Mw;
+    uint32_t r = (uint32_t)(d0 - i * Mw);
+    uint32_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (r < Hw) {
+        uint32_t h;
+        __builtin_memcpy(&h, a.hdr + 4 * r, 4);
+        v[j] = h;
+      } else {
+        v[j] = (d0 + j < total_w) ? in[i * Sw + (r - Hw)] : 0u;
+      }
+      if (++r == Mw) {
+        r = 0;
+        ++i;
+      }
+    }
+    if (d0 + 4 <= total_w) {
+      *reinterpret_cast<uint4 *>(out + d0) = make_uint4(v[0], v[1], v[2], v[3]);
+    } else {
+      for (int j = 0; j < 4; ++j)
+        if (d0 + j < total_w) out[d0 + j] = v[j];
+    }
+  }
+  if (offs) {
+    const uint64_t M = (uint64_t)Mw * 4;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= a.n;
+         i += gstride)
+      offs[i] = i * M;
+  }
+}
+
+// byte gather (header or stride not dword multiples)
+__global__ __launch_bounds__(256) void fixed_msg_encode_b1(
+    MsgEncArgs a, const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
+    uint64_t *__restrict__ offs) {
+  const uint64_t M = (uint64_t)a.hlen + a.stride;
+  const uint64_t total = a.n * M;
+  const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < total;
+       b += gstride) {
+    const uint64_t i = b / M;
+    const uint32_t r = (uint32_t)(b - i * M);
+    out[b] = r < a.hlen ? a.hdr[r] : in[i * a.stride + (r - a.hlen)];
+  }
+  if (offs)
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= a.n;
+         i += gstride)
+      offs[i] = i * M;
+}
+
+static unsigned elem_grid(uint64_t items, unsigned threads = 256) {
+  uint64_t b = (items + threads - 1) / threads;
+  if (b > 4096) b = 4096;
+  if (b < 1) b = 1;
+  return (unsigned)b;
+}
+
+hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
+                                        const void *d_recs, void *d_out,
+                                        uint64_t *d_offsets, hipStream_t s) {
+  MsgEncArgs a = {};
+  a.n = n;
+  a.stride = L->rec_stride;
+  a.hlen = write_hdr(a.hdr, L->fmt_one, 1);
+  const bool w4 = (a.hlen % 4 == 0) && (a.stride % 4 == 0) &&
+                  ((uintptr_t)d_recs % 4 == 0) && ((uintptr_t)d_out % 16 == 0);
+  if (w4) {
+    const uint64_t chunks = (n * ((a.hlen + a.stride) / 4) + 3) / 4;
+    hipLaunchKernelGGL(fixed_msg_encode_w4, dim3(elem_grid(chunks > n ? chunks : n + 1)),
+                       dim3(256), 0, s, a, (const uint32_t *)d_recs, (uint32_t *)d_out,
+                       d_offsets);
+  } else {
+    hipLaunchKernelGGL(fixed_msg_encode_b1, dim3(elem_grid(n * (a.hlen + a.stride) + 1)),
+                       dim3(256), 0, s, a, (const uint8_t *)d_recs, (uint8_t *)d_out,
+                       d_offsets);
+  }
+  return hipGetLastError();
+}
+
+// Decode: one thread per message parses the header (parse_hdr), then the
+// record bytes are moved by a dword/byte gather over output records.
+struct MsgDecArgs {
+  spk_msgfmt fmt;
+  uint64_t n;
+  uint64_t wire_len;
+  uint64_t rec_cap;
+  uint32_t stride;
+  uint32_t fixed_M;  // implicit message stride when offsets == nullptr
+};
+
+__global__ __launch_bounds__(256) void fixed_msg_parse(
+    MsgDecArgs a, const uint8_t *__restrict__ wire, const uint64_t *__restrict__ offs,
+    uint64_t *__restrict__ payload, int32_t *__restrict__ errc,
+    spk_dresult_t *__restrict__ res) {
+  const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+  unsigned long long ok = 0, consumed = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n;
+       i += gstride) {
+    uint64_t b = offs ? offs[i] : i * a.fixed_M;
+    uint64_t e = offs ? offs[i + 1] : (i + 1) * a.fixed_M;
+    int32_t ec = SPK_ERRC_OK;
+    uint64_t pos = 0, dl = 0;
+    uint32_t w = 1;
+    if (e < b || e > a.wire_len) {
+      ec = SPK_ERRC_NO_BUFFER_SPACE;
+    } else {
+      ec = parse_hdr(a.fmt, wire + b, e - b, &pos, &w, &dl);
+      if (!ec && e - b - pos < a.stride) ec = SPK_ERRC_NO_BUFFER_SPACE;
+    }
+    if (!ec && i >= a.rec_cap) ec = SPK_ERRC_CAPACITY;
+    if (errc) errc[i] = ec;
+    payload[i] = ec ? ~0ull : b + pos;
+    if (!ec) {
+      ++ok;
+      const uint64_t used = pos + a.stride;
+      consumed += used > dl ? used : dl;
+    }
+  }
+  // wave reduce then one atomic per wave
+  for (int o = 32; o > 0; o >>= 1) {
+    ok += __shfl_down(ok, o);
+    consumed += __shfl_down(consumed, o);
+  }
+  if ((threadIdx.x & 63) == 0 && (ok || consumed)) {
+    atomicAdd((unsigned long long *)&res->count, ok);
+    atomicAdd((unsigned long long *)&res->consumed, consumed);
+  }
+}
+
+__global__ __launch_bounds__(256) void fixed_msg_gather(
+    uint64_t n, uint32_t stride, const uint8_t *__restrict__ wire,
+    const uint64_t *__restrict__ payload, uint8_t *__restrict__ out) {
+  const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
+  if ((stride & 3) == 0) {
+    const uint32_t Sw = stride >> 2;
+    const uint64_t total = n * Sw;
+    for (uint64_t d = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; d < total;
+         d += gstride) {
+      const uint64_t i = d / Sw;
+      const uint32_t j = (uint32_t)(d - i * Sw);
+      const uint64_t p = payload[i];
+      if (p == ~0ull) continue;
+      const uint8_t *src = wire + p + 4 * j;
+      uint32_t v;
+      if (((uintptr_t)src & 3) == 0) {
+        v = *reinterpret_cast<const uint32_t *>(src);
+      } else {
+        v = (uint32_t)src[0] | ((uint32_t)src[1] << 8) | ((uint32_t)src[2] << 16) |
+            ((uint32_t)src[3] << 24);
+      }
+      reinterpret_cast<uint32_t *>(out)[d] = v;
+    }
+  } else {
+    const uint64_t total = n * stride;
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < total;
+         b += gstride) {
+      const uint64_t i = b / stride;
+      const uint64_t p = payload[i];
+      if (p == ~0ull) continue;
+      out[b] = wire[p + (b - i * stride)];
+    }
+  }
+}
+
+hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
+                                           uint64_t wire_len, const uint64_t *d_offsets,
+                                           uint64_t n, void *d_recs, uint64_t rec_cap,
+                                           spk_dresult_t *d_res, int32_t *d_errc,
+                                           void *d_ws, hipStream_t s) {
+  MsgDecArgs a;
+  a.fmt = L->fmt_one;
+  a.n = n;
+  a.wire_len = wire_len;
+  a.rec_cap = rec_cap;
+  a.stride = L->rec_stride;
+  uint8_t hb[4 + 1 + SPK_MAX_LITERAL + 1];
+  a.fixed_M = write_hdr(hb, L->fmt_one, 1) + L->rec_stride;
+  uint64_t *payload = reinterpret_cast<uint64_t *>((uint8_t *)d_ws + kWsScratch);
+  hipError_t e = hipMemsetAsync(d_res, 0, sizeof(spk_dresult_t), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(fixed_msg_parse, dim3(elem_grid(n)), dim3(256), 0, s, a,
+                     (const uint8_t *)d_wire, d_offsets, payload, d_errc, d_res);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const uint64_t nrec = n < rec_cap ? n : rec_cap;
+  const uint64_t items = (L->rec_stride % 4 == 0) ? nrec * (L->rec_stride / 4)
+                                                  : nrec * L->rec_stride;
+  hipLaunchKernelGGL(fixed_msg_gather, dim3(elem_grid(items)), dim3(256), 0, s, nrec,
+                     (uint32_t)L->rec_stride, (const uint8_t *)d_wire,
+                     (const uint64_t *)payload, (uint8_t *)d_recs);
+  return hipGetLastError();
+}
+
+}  // namespace spk

@@ -1,0 +1,202 @@
+// spk_internal.hpp — shared device/host definitions of the gfx950 struct_pack
+// batch codec (not part of the public ABI; see include/spk_codec.h).
+//
+// Wire-format rules restated here follow the reference (paths relative to
+// /root/reference/include/ylt/struct_pack/):
+//   width selection     calculate_size.hpp:426-447
+//   header / metainfo   packer.hpp:90-139, type_calculate.hpp:884-891
+//   header validation   unpacker.hpp:548-619
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/spk_codec.h"
+
+namespace spk {
+
+constexpr int kWave = 64;
+
+// Kernel-argument copy of the descriptor, without the literal tables (the
+// type literal lives in the device header buffer produced by the plan).
+struct KLayout {
+  uint32_t stride;
+  uint32_t n_ops;
+  uint32_t trivial;
+  uint32_t n_spans;
+  uint32_t fixed_bytes;  // sum of COPY sizes (== stride when trivial)
+  uint32_t pad_;
+  spk_op ops[SPK_MAX_OPS];
+};
+
+// Everything the write pass needs about one message format, resolved for a
+// given width. Computed on the host when the width is known there (trivial
+// records) and on the device otherwise (plan kernel).
+struct MsgHdr {
+  uint32_t len;   // header bytes (head + meta + literal + NUL)
+  uint32_t code;  // type code (LSB clear)
+  uint32_t flags; // SPK_MF_*
+  uint32_t lit_len;
+};
+
+__host__ __device__ inline uint32_t width_of(uint64_t max_count) {
+  return max_count < (1ull << 8)    ? 1u
+         : max_count < (1ull << 16) ? 2u
+         : max_count < (1ull << 32) ? 4u
+                                    : 8u;
+}
+__host__ __device__ inline uint32_t width_bits(uint32_t w) {
+  return w == 1 ? 0u : w == 2 ? 0x08u : w == 4 ? 0x10u : 0x18u;
+}
+
+// Header shape for message format (flags, literal_len) at width w.
+struct HdrShape {
+  uint32_t head, lit, has_meta, len, meta;
+};
+__host__ __device__ inline HdrShape hdr_shape(uint32_t flags, uint32_t lit_len,
+                                              uint32_t w) {
+  HdrShape h;
+  const uint32_t has_container = (flags & SPK_MF_HAS_CONTAINER) != 0;
+  h.head = (flags & SPK_MF_HASH_HEAD) != 0;
+  h.lit = h.head && (flags & SPK_MF_TYPE_LITERAL);
+  const uint32_t meta_fixed = h.lit || (!h.head && has_container);
+  if (!has_container) w = 1;
+  h.has_meta = meta_fixed || w > 1;
+  h.meta = width_bits(w) | (h.lit ? 0x04u : 0u);
+  h.len = (h.head ? 4u : 0u) + (h.has_meta ? 1u : 0u) + (h.lit ? lit_len + 1u : 0u);
+  return h;
+}
+
+// Writes the header bytes (at most 4+1+SPK_MAX_LITERAL+1) into dst.
+__host__ __device__ inline uint32_t write_hdr(uint8_t *dst, const spk_msgfmt &f,
+                                              uint32_t w) {
+  HdrShape h = hdr_shape(f.flags, f.literal_len, w);
+  uint32_t p = 0;
+  if (h.head) {
+    uint32_t head = (f.code & ~1u) | (h.has_meta ? 1u : 0u);
+    dst[p++] = (uint8_t)head;
+    dst[p++] = (uint8_t)(head >> 8);
+    dst[p++] = (uint8_t)(head >> 16);
+    dst[p++] = (uint8_t)(head >> 24);
+  }
+  if (h.has_meta) dst[p++] = (uint8_t)h.meta;
+  if (h.lit) {
+    for (uint32_t i = 0; i < f.literal_len; ++i) dst[p++] = f.literal[i];
+    dst[p++] = 0;
+  }
+  return p;
+}
+
+// Workspace layout (device): fixed region first, then per-launch scratch.
+//   [0, 512)        : header bytes of the VECTOR message (+ count prefix)
+//   [512, 1536)     : header bytes of the MESSAGES format, one 256-B slot
+//                     per width 1/2/4/8 (slot = log2(w))
+//   [2048, 2304)    : control words (CopyJob / decode state)
+//   [4096, ...)     : per-block partials, scan buffers, boundary tables
+constexpr size_t kWsHdrVec = 0;
+constexpr size_t kWsHdrMsg = 512;
+constexpr size_t kWsHdrSlot = 256;
+constexpr size_t kWsCtl = 2048;
+constexpr size_t kWsScratch = 4096;
+
+// control words (uint64) at kWsCtl
+struct Ctl {
+  unsigned long long max_count;   // atomicMax target
+  unsigned long long err_pos;     // first failing position (decode)
+  unsigned long long flags;       // misc
+  unsigned long long n_records;   // decode: records found
+  int32_t errc;                   // decode errc (atomicMin of nonzero)
+  uint32_t pad;
+};
+
+__device__ __forceinline__ uint64_t ld_le(const uint8_t *p, uint32_t w) {
+  uint64_t v = 0;
+  for (uint32_t i = 0; i < w; ++i) v |= (uint64_t)p[i] << (8 * i);
+  return v;
+}
+
+// Parse a message header at p[0..len). Returns errc; sets *pos to the first
+// payload byte, *w to the width, *data_len to the compatible length field.
+__device__ inline int32_t parse_hdr(const spk_msgfmt &f, const uint8_t *p, uint64_t len,
+                             uint64_t *pos, uint32_t *w, uint64_t *data_len) {
+  *w = 1;
+  *data_len = 0;
+  *pos = 0;
+  const bool has_container = (f.flags & SPK_MF_HAS_CONTAINER) != 0;
+  if (!(f.flags & SPK_MF_HASH_HEAD)) {
+    if (has_container) {
+      if (len < 1) return SPK_ERRC_NO_BUFFER_SPACE;
+      *w = 1u << ((p[0] >> 3) & 3);
+      *pos = 1;
+    }
+    return SPK_ERRC_OK;
+  }
+  if (len < 4) return SPK_ERRC_NO_BUFFER_SPACE;
+  const uint32_t cur = (uint32_t)ld_le(p, 4);
+  if ((cur >> 1) != (f.code >> 1)) return SPK_ERRC_INVALID_BUFFER;
+  uint64_t at = 4;
+  if (!(cur & 1)) {
+    *pos = at;
+    return SPK_ERRC_OK;
+  }
+  if (len < at + 1) return SPK_ERRC_NO_BUFFER_SPACE;
+  const uint8_t meta = p[at++];
+  const uint32_t csz = meta & 3;
+  if (csz) {
+    const uint32_t nb = csz == 1 ? 2 : csz == 2 ? 4 : 8;
+    if (len < at + nb) return SPK_ERRC_NO_BUFFER_SPACE;
+    *data_len = ld_le(p + at, nb);
+    at += nb;
+  }
+  if (meta & 4) {
+    if (len < at + f.literal_len + 1) return SPK_ERRC_NO_BUFFER_SPACE;
+    for (uint32_t i = 0; i < f.literal_len; ++i)
+      if (p[at + i] != f.literal[i]) return SPK_ERRC_HASH_CONFLICT;
+    if (p[at + f.literal_len] != 0) return SPK_ERRC_HASH_CONFLICT;
+    at += f.literal_len + 1;
+  }
+  *w = 1u << ((meta >> 3) & 3);
+  *pos = at;
+  return SPK_ERRC_OK;
+}
+
+}  // namespace spk
+
+// ---- launch wrappers implemented in the kernel TUs -----------------------
+namespace spk {
+// spk_fixed.hip
+hipError_t launch_fixed_plan(const spk_layout *L, int mode, uint64_t n,
+                             spk_plan_t *d_plan, void *d_ws, hipStream_t s);
+hipError_t launch_fixed_encode_vector(const spk_layout *L, uint64_t n,
+                                      const void *d_recs, void *d_out,
+                                      const void *d_ws, hipStream_t s);
+hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
+                                        const void *d_recs, void *d_out,
+                                        uint64_t *d_offsets, hipStream_t s);
+hipError_t launch_fixed_decode_vector(const spk_layout *L, const void *d_wire,
+                                      uint64_t wire_len, void *d_recs,
+                                      uint64_t rec_cap, spk_dresult_t *d_res,
+                                      void *d_ws, hipStream_t s);
+hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
+                                        uint64_t wire_len,
+                                        const uint64_t *d_offsets, uint64_t n,
+                                        void *d_recs, uint64_t rec_cap,
+                                        spk_dresult_t *d_res, int32_t *d_errc,
+                                        void *d_ws, hipStream_t s);
+// spk_var.hip
+size_t var_workspace_bytes(const spk_layout *L, int mode, uint64_t n,
+                           uint64_t wire_len);
+hipError_t launch_var_plan(const spk_layout *L, int mode, uint64_t n,
+                           const void *d_recs, spk_plan_t *d_plan, void *d_ws,
+                           size_t ws_bytes, hipStream_t s);
+hipError_t launch_var_encode(const spk_layout *L, int mode, uint64_t n,
+                             const void *d_recs, const void *const *d_heaps,
+                             const spk_plan_t *d_plan, void *d_out,
+                             uint64_t out_cap, uint64_t *d_offsets, void *d_ws,
+                             size_t ws_bytes, hipStream_t s);
+hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
+                             uint64_t wire_len, const uint64_t *d_offsets,
+                             uint64_t n_msgs, void *d_recs, uint64_t rec_cap,
+                             void *const *d_heaps, const uint64_t *heap_caps,
+                             spk_dresult_t *d_res, int32_t *d_errc, void *d_ws,
+                             size_t ws_bytes, hipStream_t s);
+}  // namespace spk

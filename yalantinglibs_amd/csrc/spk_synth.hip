@@ -1,0 +1,143 @@
+// spk_synth.hip — device restatement of the seeded record generator of
+// oracle/ref/types.hpp (used by the golden generator built against the
+// reference), so the GPU box regenerates bit-identical inputs for the
+// full-size BASELINE configs and compares digests. Bench/test support only;
+// it is exported through the same C ABI for convenience.
+#include "spk_internal.hpp"
+
+namespace {
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t rnd(uint64_t seed, uint64_t i, uint64_t k) {
+  return mix64(seed + (i * 64 + k + 1) * 0x9E3779B97F4A7C15ULL);
+}
+__device__ __forceinline__ float rf(uint64_t r) {
+  return (float)(int32_t)(uint32_t)r / 65536.0f;
+}
+__device__ __forceinline__ double rd(uint64_t r) {
+  return (double)(int32_t)(uint32_t)r / 65536.0;
+}
+
+struct Rec64 {
+  int32_t i[4];
+  float f[4];
+  double d[4];
+};
+struct RecSDev {  // schema.flatten(RecS): id, name.n, name.off, v
+  int32_t id;
+  uint32_t n;
+  uint64_t off;
+  double v;
+};
+struct OuterDev {  // schema.flatten(Outer): key, items.n, items.off
+  int64_t key;
+  uint32_t n;
+  uint32_t pad;
+  uint64_t off;
+};
+
+__global__ void synth_rec64(uint64_t seed, uint64_t first, uint64_t n, Rec64 *out) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gs) {
+    const uint64_t i = first + t;
+    Rec64 r;
+    for (int k = 0; k < 4; ++k) r.i[k] = (int32_t)(uint32_t)rnd(seed, i, k);
+    for (int k = 0; k < 4; ++k) r.f[k] = rf(rnd(seed, i, 4 + k));
+    for (int k = 0; k < 4; ++k) r.d[k] = rd(rnd(seed, i, 8 + k));
+    out[t] = r;
+  }
+}
+
+__global__ void synth_counts(int kind, uint64_t seed, uint64_t first, uint64_t n,
+                             uint32_t param, uint64_t *cnt) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gs)
+    cnt[t] = rnd(seed, first + t, 1) % (uint64_t)(param + 1);
+}
+
+__global__ void synth_recs(uint64_t seed, uint64_t first, uint64_t n, uint32_t param,
+                           RecSDev *out, uint8_t *heap, const uint64_t *hoff) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gs) {
+    const uint64_t i = first + t;
+    RecSDev r;
+    r.id = (int32_t)(uint32_t)rnd(seed, i, 0);
+    r.n = (uint32_t)(rnd(seed, i, 1) % (uint64_t)(param + 1));
+    r.off = hoff[t];
+    r.v = rd(rnd(seed, i, 60));
+    out[t] = r;
+    uint8_t *dst = heap + r.off;
+    for (uint32_t j = 0; j < r.n; ++j) {
+      const uint64_t w = rnd(seed, i, 2 + (j >> 3) % 56);
+      dst[j] = (uint8_t)('a' + ((w >> ((j & 7) * 8)) & 0xFF) % 26);
+    }
+  }
+}
+
+__global__ void synth_outer(uint64_t seed, uint64_t first, uint64_t n, uint32_t param,
+                            OuterDev *out, uint8_t *heap, const uint64_t *hoff) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gs) {
+    const uint64_t i = first + t;
+    OuterDev o;
+    o.key = (int64_t)rnd(seed, i, 0);
+    o.n = (uint32_t)(rnd(seed, i, 1) % (uint64_t)(param + 1));
+    o.pad = 0;
+    o.off = hoff[t];
+    out[t] = o;
+    int32_t *dst = reinterpret_cast<int32_t *>(heap + o.off * 8);
+    for (uint32_t j = 0; j < o.n; ++j) {
+      const uint64_t w = rnd(seed, i, 2 + j % 62);
+      const uint64_t w2 = mix64(w ^ (uint64_t)j);
+      dst[2 * j] = (int32_t)(uint32_t)w2;
+      const float y = rf(w2 >> 32);
+      dst[2 * j + 1] = __float_as_int(y);
+    }
+  }
+}
+
+unsigned grid_of(uint64_t n) {
+  uint64_t b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  return (unsigned)(b ? b : 1);
+}
+
+}  // namespace
+
+extern "C" int spk_synth_counts(int kind, uint64_t seed, uint64_t first, uint64_t n,
+                                uint32_t param, uint64_t *d_counts, void *stream) {
+  if (!d_counts || (kind != SPK_SYNTH_RECS && kind != SPK_SYNTH_OUTER)) return SPK_E_ARG;
+  hipLaunchKernelGGL(synth_counts, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, kind,
+                     seed, first, n, param, d_counts);
+  return hipGetLastError() == hipSuccess ? SPK_OK : SPK_E_HIP;
+}
+
+extern "C" int spk_synth(int kind, uint64_t seed, uint64_t first, uint64_t n, uint32_t param,
+                         void *d_recs, void *d_heap, const uint64_t *d_heap_offsets,
+                         void *stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!d_recs && n) return SPK_E_ARG;
+  switch (kind) {
+    case SPK_SYNTH_REC64:
+      hipLaunchKernelGGL(synth_rec64, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n,
+                         (Rec64 *)d_recs);
+      break;
+    case SPK_SYNTH_RECS:
+      if (!d_heap_offsets) return SPK_E_ARG;
+      hipLaunchKernelGGL(synth_recs, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n, param,
+                         (RecSDev *)d_recs, (uint8_t *)d_heap, d_heap_offsets);
+      break;
+    case SPK_SYNTH_OUTER:
+      if (!d_heap_offsets) return SPK_E_ARG;
+      hipLaunchKernelGGL(synth_outer, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n, param,
+                         (OuterDev *)d_recs, (uint8_t *)d_heap, d_heap_offsets);
+      break;
+    default:
+      return SPK_E_ARG;
+  }
+  return hipGetLastError() == hipSuccess ? SPK_OK : SPK_E_HIP;
+}

@@ -1,0 +1,214 @@
+"""struct_pack entry points over the MI355X codec (Python host mirror).
+
+Mirrors the reference's API (include/ylt/struct_pack.hpp) for batches of
+records resident in device memory:
+
+  get_type_code(T)                      struct_pack.hpp:75-92
+  get_needed_size(batch, mode)          struct_pack.hpp:131-135
+  serialize_to(out, batch, mode)        struct_pack.hpp:161-167
+  serialize(batch, mode)                struct_pack.hpp:198-207
+  deserialize_to(batch_out, wire, ...)  struct_pack.hpp:343-357
+  deserialize(T, wire, ...)             struct_pack.hpp:393-413
+
+A batch is `RecordBatch(layout, recs, heaps)`: `recs` is a (n, stride)
+uint8 CUDA tensor of device records (schema.flatten), `heaps` one uint8
+CUDA tensor per variable-length member. Errors follow the reference's errc
+values (error_code.hpp:21-27) via `errc` below; there is no CPU fallback —
+every call goes through libspk_codec.so and fails loudly without it.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+
+from . import _capi as C
+from . import schema as S
+from .layout import Layout, make_layout
+
+MODE_VECTOR = C.SPK_MODE_VECTOR
+MODE_MESSAGES = C.SPK_MODE_MESSAGES
+
+
+class errc:  # struct_pack::errc
+    ok = C.ERRC_OK
+    no_buffer_space = C.ERRC_NO_BUFFER_SPACE
+    invalid_buffer = C.ERRC_INVALID_BUFFER
+    hash_conflict = C.ERRC_HASH_CONFLICT
+    invalid_width_of_container_length = C.ERRC_INVALID_WIDTH
+    capacity = C.ERRC_CAPACITY  # device-side output capacity (not in the reference)
+
+
+def get_type_code(*types: S.SpType) -> int:
+    return S.get_type_code(*types)
+
+
+def _stream(stream=None) -> ct.c_void_p:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ct.c_void_p(s.cuda_stream)
+
+
+def _p(t: Optional[torch.Tensor]) -> ct.c_void_p:
+    return ct.c_void_p(t.data_ptr() if t is not None and t.numel() else 0)
+
+
+@dataclass
+class RecordBatch:
+    layout: Layout
+    recs: torch.Tensor                      # (n, stride) uint8, device
+    heaps: List[torch.Tensor] = field(default_factory=list)
+
+    @property
+    def n(self) -> int:
+        return int(self.recs.shape[0])
+
+
+class Codec:
+    """Per-type codec: descriptor + cached workspace / plan buffers."""
+
+    def __init__(self, layout: Layout, device="cuda"):
+        self.L = layout
+        self.lib = C.load_codec()
+        self.device = torch.device(device)
+        rc = self.lib.spk_layout_check(self.L.ptr)
+        if rc != 0:
+            raise ValueError(f"layout rejected by spk_layout_check ({rc})")
+        self._ws = torch.empty(0, dtype=torch.uint8, device=self.device)
+        self.plan_buf = torch.zeros(C.PLAN_BYTES, dtype=torch.uint8, device=self.device)
+        self.res_buf = torch.zeros(C.DRES_BYTES, dtype=torch.uint8, device=self.device)
+
+    @classmethod
+    def for_type(cls, t: S.SpType, conf: int = S.DEFAULT, debug: bool = False,
+                 vector_config=None, device="cuda"):
+        return cls(make_layout(t, conf, debug, vector_config), device)
+
+    # ---- workspace -------------------------------------------------------
+    def workspace(self, mode: int, n: int, wire_len: int = 0) -> torch.Tensor:
+        need = int(self.lib.spk_workspace_bytes(self.L.ptr, mode, n, wire_len))
+        if need == 0:
+            raise ValueError("spk_workspace_bytes rejected the layout")
+        if self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def _heap_ptrs(self, heaps):
+        # empty heaps (all counts zero) still need a valid device pointer
+        if not hasattr(self, "_dummy"):
+            self._dummy = torch.zeros(16, dtype=torch.uint8, device=self.device)
+        k = max(self.L.n_spans, 1)
+        ptrs = [h.data_ptr() if h.numel() else self._dummy.data_ptr() for h in heaps]
+        return (ct.c_void_p * k)(*(ptrs or [0]))
+
+    @staticmethod
+    def _check(rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed with {rc}")
+
+    # ---- encode ----------------------------------------------------------
+    def plan(self, batch: RecordBatch, mode: int, stream=None) -> torch.Tensor:
+        """Size pass (stream-ordered): writes spk_plan_t into self.plan_buf."""
+        ws = self.workspace(mode, batch.n)
+        self._check(self.lib.spk_plan(self.L.ptr, mode, batch.n, _p(batch.recs),
+                                      _p(self.plan_buf), _p(ws), ws.numel(),
+                                      _stream(stream)), "spk_plan")
+        return self.plan_buf
+
+    def get_needed_size(self, batch: RecordBatch, mode: int = MODE_VECTOR) -> C.spk_plan_t:
+        """Host copy of the size pass (synchronises)."""
+        self.plan(batch, mode)
+        return C.spk_plan_t.from_buffer_copy(bytes(self.plan_buf.cpu().numpy()))
+
+    def serialize_to(self, out: torch.Tensor, batch: RecordBatch, mode: int = MODE_VECTOR,
+                     offsets: Optional[torch.Tensor] = None, stream=None,
+                     planned: bool = False):
+        """Plan + write into a caller-owned device buffer (no host sync)."""
+        if not planned:
+            self.plan(batch, mode, stream)
+        ws = self.workspace(mode, batch.n)
+        self._check(self.lib.spk_encode(self.L.ptr, mode, batch.n, _p(batch.recs),
+                                        self._heap_ptrs(batch.heaps), _p(self.plan_buf),
+                                        _p(out), out.numel(), _p(offsets), _p(ws),
+                                        ws.numel(), _stream(stream)), "spk_encode")
+
+    def serialize(self, batch: RecordBatch, mode: int = MODE_VECTOR):
+        """Returns (wire uint8 tensor, message offsets or None)."""
+        plan = self.get_needed_size(batch, mode)
+        out = torch.empty(max(plan.total_bytes, 1), dtype=torch.uint8, device=self.device)
+        offs = (torch.empty(batch.n + 1, dtype=torch.int64, device=self.device)
+                if mode == MODE_MESSAGES else None)
+        self.serialize_to(out, batch, mode, offs, planned=True)
+        return out[:plan.total_bytes], offs
+
+    # ---- decode ----------------------------------------------------------
+    def deserialize_to(self, out: RecordBatch, wire: torch.Tensor, mode: int = MODE_VECTOR,
+                       offsets: Optional[torch.Tensor] = None, n_msgs: int = 0,
+                       errc_out: Optional[torch.Tensor] = None, heap_caps=None,
+                       stream=None) -> torch.Tensor:
+        """Decode into caller-owned buffers; returns the device result
+        (spk_dresult_t bytes). Stream-ordered, no host sync."""
+        cap = out.n
+        ws = self.workspace(mode, cap if mode == MODE_VECTOR else n_msgs, wire.numel())
+        caps = heap_caps or [h.numel() // sp.elem.size
+                             for h, sp in zip(out.heaps, self.L.dev.spans)]
+        hc = (ct.c_uint64 * max(len(caps), 1))(*(caps or [0]))
+        self._check(self.lib.spk_decode(self.L.ptr, mode, _p(wire), wire.numel(), _p(offsets),
+                                        n_msgs, _p(out.recs), cap, self._heap_ptrs(out.heaps),
+                                        hc, _p(self.res_buf), _p(errc_out), _p(ws),
+                                        ws.numel(), _stream(stream)), "spk_decode")
+        return self.res_buf
+
+    def result(self) -> C.spk_dresult_t:
+        return C.spk_dresult_t.from_buffer_copy(bytes(self.res_buf.cpu().numpy()))
+
+    def alloc_batch(self, n: int, heap_elems: Optional[List[int]] = None) -> RecordBatch:
+        recs = torch.zeros((max(n, 0), self.L.stride), dtype=torch.uint8, device=self.device)
+        heaps = []
+        for k, sp in enumerate(self.L.dev.spans):
+            cnt = heap_elems[k] if heap_elems else 0
+            heaps.append(torch.zeros(max(cnt, 1) * sp.elem.size, dtype=torch.uint8,
+                                     device=self.device))
+        return RecordBatch(self.L, recs, heaps)
+
+    def deserialize(self, wire: torch.Tensor, mode: int = MODE_VECTOR,
+                    offsets: Optional[torch.Tensor] = None, n_msgs: int = 0):
+        """Allocating decode: capacities bounded by the wire length.
+        Returns (result, RecordBatch, errc tensor or None)."""
+        wl = wire.numel()
+        min_rec = max(1, sum(op[2] for op in self.L.dev.ops if op[0] == C.SPK_OP_COPY) +
+                      len(self.L.dev.spans))
+        cap = (wl // min_rec + 1) if mode == MODE_VECTOR else n_msgs
+        elems = [wl // sp.elem.size + 1 for sp in self.L.dev.spans]
+        out = self.alloc_batch(cap, elems)
+        ec = (torch.zeros(max(n_msgs, 1), dtype=torch.int32, device=self.device)
+              if mode == MODE_MESSAGES else None)
+        self.deserialize_to(out, wire, mode, offsets, n_msgs, ec)
+        res = self.result()
+        n = res.count if mode == MODE_VECTOR else n_msgs
+        out = RecordBatch(self.L, out.recs[:n], out.heaps)
+        return res, out, ec
+
+
+def synth_batch(codec: Codec, kind: str, n: int, seed: int, param: int = 48,
+                first: int = 0, stream=None) -> RecordBatch:
+    """Device-generated synthetic batch (spk_synth) for rec64 / recs / outer."""
+    lib = codec.lib
+    dev = codec.device
+    kinds = {"rec64": C.SPK_SYNTH_REC64, "recs": C.SPK_SYNTH_RECS, "outer": C.SPK_SYNTH_OUTER}
+    k = kinds[kind]
+    recs = torch.empty((n, codec.L.stride), dtype=torch.uint8, device=dev)
+    st = _stream(stream)
+    if k == C.SPK_SYNTH_REC64:
+        Codec._check(lib.spk_synth(k, seed, first, n, param, _p(recs), None, None, st),
+                     "spk_synth")
+        return RecordBatch(codec.L, recs, [])
+    cnt = torch.empty(n, dtype=torch.int64, device=dev)
+    Codec._check(lib.spk_synth_counts(k, seed, first, n, param, _p(cnt), st), "spk_synth_counts")
+    offs = torch.cumsum(cnt, 0) - cnt
+    total = int(cnt.sum().item()) if n else 0
+    esz = codec.L.dev.spans[0].elem.size
+    heap = torch.zeros(max(total, 1) * esz, dtype=torch.uint8, device=dev)
+    Codec._check(lib.spk_synth(k, seed, first, n, param, _p(recs), _p(heap), _p(offs), st),
+                 "spk_synth")
+    return RecordBatch(codec.L, recs, [heap])
