@@ -4,15 +4,16 @@
 //
 // SPK_MODE_VECTOR: the message is [header][count:w][n*stride raw bytes], so
 // encode and decode are byte-shifted stream copies between a 16-B aligned
-// buffer and one displaced by the header length h. `shift_copy` moves whole
-// aligned 16-B chunks: each lane loads one chunk per unroll step
-// (global_load_dwordx4, 1 KiB per wave-instruction, fully coalesced), takes
-// its right neighbour's chunk with ds_bpermute (lane 63 takes the next
-// step's lane 0 via v_readlane) and funnels the two with v_alignbyte into the
-// displaced output chunk — every HBM byte is read once and written once.
+// buffer and one displaced by the header length h (9 bytes for C2). The
+// copy writes whole aligned 16-B chunks (global_store_dwordx4, 1 KiB per
+// wave-instruction) and reads each one with a single byte-aligned
+// global_load_dwordx4 (gfx950 runs in unaligned-access mode): every HBM byte
+// is read once and written once, no cross-lane shuffles. Measured on MI355X
+// (scripts/probes/copy_probe.hip): this form sustains the same 5.9-6.0 TB/s
+// as an aligned 16-B copy, 8 chunks in flight per lane, 16 Ki blocks.
 // The shift is data-dependent on decode (width/meta/type-literal of the
-// incoming header), so the kernel switches on it (wave-uniform) among 16
-// template instances instead of re-launching.
+// incoming header): the kernel reads it from a device-side CopyJob written by
+// the header kernel, so no host round trip is needed.
 //
 // SPK_MODE_MESSAGES: n independent [header][record] messages (coro_rpc
 // payloads): a dword gather when header and stride are multiples of 4,
@@ -35,92 +36,29 @@ struct CopyJob {
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ uint32_t funnel(uint32_t lo, uint32_t hi, uint32_t r) {
-  // bytes [r, r+4) of the 8-byte little-endian pair (lo, hi)
-  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * r));
-}
-
-template <int R>
-__device__ __forceinline__ v4u funnel16(const v4u &a, const v4u &b) {
-  if constexpr (R == 0) {
-    return a;
-  } else {
-    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    constexpr int q = R >> 2, r = R & 3;
-    v4u o;
-    if constexpr (r == 0) {
-      o.x = w[q + 0];
-      o.y = w[q + 1];
-      o.z = w[q + 2];
-      o.w = w[q + 3];
-    } else {
-      o.x = funnel(w[q + 0], w[q + 1], r);
-      o.y = funnel(w[q + 1], w[q + 2], r);
-      o.z = funnel(w[q + 2], w[q + 3], r);
-      o.w = funnel(w[q + 3], w[q + 4], r);
-    }
-    return o;
-  }
-}
-
-__device__ __forceinline__ v4u shfl_next(const v4u &v, uint32_t lane) {
-  const int addr = (int)(((lane + 1) & 63) << 2);
-  v4u o;
-  o.x = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v.x);
-  o.y = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v.y);
-  o.z = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v.z);
-  o.w = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)v.w);
-  return o;
-}
-__device__ __forceinline__ v4u lane0_of(const v4u &v) {
-  v4u o;
-  o.x = (uint32_t)__builtin_amdgcn_readlane((int)v.x, 0);
-  o.y = (uint32_t)__builtin_amdgcn_readlane((int)v.y, 0);
-  o.z = (uint32_t)__builtin_amdgcn_readlane((int)v.z, 0);
-  o.w = (uint32_t)__builtin_amdgcn_readlane((int)v.w, 0);
-  return o;
-}
+typedef v4u v4u_unaligned __attribute__((aligned(1)));
 
 constexpr int kCopyThreads = 256;
-constexpr int kCopyUnroll = 4;
+constexpr int kCopyUnroll = 8;
 constexpr uint64_t kTile = 64ull * kCopyUnroll;  // chunks per wave-tile
 
-// dst chunk k (k in [k0, k1)) = src bytes [16*(k+q) + R, +16)
-template <int R>
-__device__ void shift_body(v4u *__restrict__ dst, const v4u *__restrict__ src,
-                           uint64_t k0, uint64_t k1, int64_t q) {
+// dst chunk k (k in [0, nk)) = 16 source bytes at sp + 16k (any alignment)
+__device__ __forceinline__ void shift_body(v4u *__restrict__ dst,
+                                           const uint8_t *__restrict__ sp, uint64_t nk) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wid = (uint64_t)blockIdx.x * (kCopyThreads / 64) + (threadIdx.x >> 6);
   const uint64_t nw = (uint64_t)gridDim.x * (kCopyThreads / 64);
-  for (uint64_t t0 = k0 + wid * kTile; t0 < k1; t0 += nw * kTile) {
-    if (t0 + kTile <= k1) {
-      v4u cur[kCopyUnroll];
+  for (uint64_t t0 = wid * kTile; t0 < nk; t0 += nw * kTile) {
+    if (t0 + kTile <= nk) {
+      v4u c[kCopyUnroll];
 #pragma unroll
       for (int j = 0; j < kCopyUnroll; ++j)
-        cur[j] = __builtin_nontemporal_load(&src[(int64_t)(t0 + j * 64 + lane) + q]);
-      if constexpr (R == 0) {
+        c[j] = *reinterpret_cast<const v4u_unaligned *>(sp + 16 * (t0 + j * 64 + lane));
 #pragma unroll
-        for (int j = 0; j < kCopyUnroll; ++j)
-          __builtin_nontemporal_store(cur[j], &dst[t0 + j * 64 + lane]);
-      } else {
-        // first chunk after the tile (same address in every lane: 1 request)
-        const v4u extra = src[(int64_t)(t0 + kTile) + q];
-#pragma unroll
-        for (int j = 0; j < kCopyUnroll; ++j) {
-          // lane 0 of the next step, read with v_readlane while all lanes
-          // are active (never inside the lane==63 branch)
-          const v4u l0 = (j + 1 < kCopyUnroll) ? lane0_of(cur[j + 1]) : extra;
-          const v4u nb = shfl_next(cur[j], lane);
-          const v4u nx = lane == 63 ? l0 : nb;
-          __builtin_nontemporal_store(funnel16<R>(cur[j], nx), &dst[t0 + j * 64 + lane]);
-        }
-      }
+      for (int j = 0; j < kCopyUnroll; ++j) dst[t0 + j * 64 + lane] = c[j];
     } else {
-      for (uint64_t k = t0 + lane; k < k1 && k < t0 + kTile; k += 64) {
-        const v4u a = src[(int64_t)k + q];
-        const v4u b = R ? src[(int64_t)k + q + 1] : a;
-        dst[k] = funnel16<R>(a, b);
-      }
+      for (uint64_t k = t0 + lane; k < nk; k += 64)
+        dst[k] = *reinterpret_cast<const v4u_unaligned *>(sp + 16 * k);
     }
   }
 }
@@ -147,28 +85,14 @@ __global__ __launch_bounds__(kCopyThreads) void shift_copy_kernel(
     for (uint64_t i = tail_start + threadIdx.x; i < nb; i += blockDim.x) d[i] = s[i];
   }
   if (body == 0) return;
-  v4u *dc = reinterpret_cast<v4u *>(d + head);
-  const uint8_t *sp = s + head;  // source of dc[0]
-  const uint64_t smis = (uint64_t)sp & 15;
-  const v4u *sc = reinterpret_cast<const v4u *>(sp - smis);
-  const uint64_t nk = body >> 4;
-  switch (smis) {  // wave-uniform
-#define SPK_CASE(r) \
-  case r:           \
-    shift_body<r>(dc, sc, 0, nk, 0); \
-    break;
-    SPK_CASE(0) SPK_CASE(1) SPK_CASE(2) SPK_CASE(3) SPK_CASE(4) SPK_CASE(5)
-    SPK_CASE(6) SPK_CASE(7) SPK_CASE(8) SPK_CASE(9) SPK_CASE(10) SPK_CASE(11)
-    SPK_CASE(12) SPK_CASE(13) SPK_CASE(14) SPK_CASE(15)
-#undef SPK_CASE
-  }
+  shift_body(reinterpret_cast<v4u *>(d + head), s + head, body >> 4);
 }
 
 static unsigned copy_grid(uint64_t max_bytes) {
   uint64_t tiles = (max_bytes / 16 + kTile - 1) / kTile;
   uint64_t blocks = (tiles + (kCopyThreads / 64) - 1) / (kCopyThreads / 64);
-  // enough waves to fill 256 CUs x 8 waves, grid-stride beyond that
-  if (blocks > 2048) blocks = 2048;
+  // 16 Ki blocks (64 Ki waves) then grid-stride: the probe's best point
+  if (blocks > 16384) blocks = 16384;
   if (blocks < 1) blocks = 1;
   return (unsigned)blocks;
 }

@@ -574,26 +574,46 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
 // ===========================================================================
 // DECODE, SPK_MODE_VECTOR — chunked transition functions
 // ===========================================================================
+// The payload is cut into kChunk-byte chunks. For every byte position p of a
+// chunk a block computes, fully in parallel, "if a record started at p, where
+// would the next one start" (one parse per position, in LDS), then pointer-
+// jumps those links in place (one packed 32-bit (next, count) word per
+// position, so asynchronous updates keep the invariant) until every position
+// knows the first record start at/after the chunk end and how many complete
+// records lie on the way. The first kK entries form the chunk's transition
+// table; tables are composed hierarchically (fan-in kGroup) to give each
+// chunk its true entry and first record index. A second pass re-derives the
+// links with 256-byte sub-chunk boundaries so 32 lanes can place the records
+// of a chunk in parallel.
 constexpr uint32_t kChunk = 8192;           // payload bytes per chunk
-constexpr uint32_t kCand = 256;             // candidate entry offsets per chunk
+constexpr uint32_t kChunkShift = 13;
+constexpr uint32_t kK = 1024;               // table entries (entry offsets) per chunk
+constexpr uint32_t kSubShift = 8;           // 256-byte sub-chunks in the start pass
+constexpr uint32_t kNSub = kChunk >> kSubShift;
 constexpr uint32_t kGroup = 64;             // composition fan-in
 constexpr uint32_t kStage = kChunk + 1024;  // bytes staged in LDS per chunk
+constexpr uint32_t kVThreads = 256;
 
-// transition-table entry (u64): exit entry offset into the next chunk (low
-// 16 bits), flags (bits 16-17), complete-record count (high 32 bits)
 constexpr uint32_t kFlagIncomplete = 1u;  // a record runs past the wire end
-constexpr uint32_t kFlagTooBig = 2u;      // exit offset >= kCand
+constexpr uint32_t kFlagTooBig = 2u;      // exit offset >= kK
 constexpr uint32_t kNoStart = 4u;         // (entries only) no record starts here
+
+// level >= 1 tables (u64): exit (16) | flags (3) << 16 | count << 32
 __host__ __device__ __forceinline__ uint64_t tpack(uint32_t exit, uint32_t flags,
                                                    uint64_t count) {
   return (uint64_t)(exit & 0xFFFF) | ((uint64_t)(flags & 7) << 16) | (count << 32);
 }
-__host__ __device__ __forceinline__ uint32_t t_exit(uint64_t t) { return (uint32_t)t & 0xFFFF; }
-__host__ __device__ __forceinline__ uint32_t t_flags(uint64_t t) {
-  return (uint32_t)(t >> 16) & 7;
+// level 0 tables (u32): exit (11) | flags (2) << 11 | count << 16
+__host__ __device__ __forceinline__ uint32_t t0pack(uint32_t exit, uint32_t flags,
+                                                    uint32_t count) {
+  return (exit & 0x7FF) | ((flags & 3) << 11) | (count << 16);
 }
+__host__ __device__ __forceinline__ uint32_t t_exit(uint64_t t) { return (uint32_t)t & 0xFFFF; }
+__host__ __device__ __forceinline__ uint32_t t_flags(uint64_t t) { return (uint32_t)(t >> 16) & 7; }
 __host__ __device__ __forceinline__ uint64_t t_count(uint64_t t) { return t >> 32; }
-// chunk entries use the same packing without the count: entry | flags<<16
+__host__ __device__ __forceinline__ uint32_t t_exit(uint32_t t) { return t & 0x7FF; }
+__host__ __device__ __forceinline__ uint32_t t_flags(uint32_t t) { return (t >> 11) & 3; }
+__host__ __device__ __forceinline__ uint64_t t_count(uint32_t t) { return t >> 16; }
 
 struct VCtl {
   uint64_t p0;       // payload start (after header + count)
@@ -607,16 +627,48 @@ struct VCtl {
   uint32_t pad;
 };
 
-// LDS-staged byte reader: bytes [base, base+kStage) come from LDS
-struct StagedReader {
-  const uint8_t *lds;
+// Compact walk program of a record: fixed bytes, then per span
+// [count:w][count*esz bytes][fixed bytes]. Built once on the host from the
+// descriptor so the walker's loop constants sit in SGPRs.
+struct WalkProg {
+  uint32_t ns;
+  uint32_t skip[SPK_MAX_SPANS + 1];
+  uint32_t esz[SPK_MAX_SPANS];
+};
+
+static WalkProg make_walkprog(const spk_layout *L) {
+  WalkProg p = {};
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i) {
+    if (L->ops[i].kind == SPK_OP_COPY) {
+      p.skip[k] += L->ops[i].size;
+    } else {
+      p.esz[k] = L->ops[i].size;
+      ++k;
+    }
+  }
+  p.ns = k;
+  return p;
+}
+
+// LDS pointers carry address space 3 so reads lower to ds_read_u8, not
+// flat_load_ubyte (a generic pointer would go through the flat path).
+typedef __attribute__((address_space(3))) const uint8_t lds_cu8;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+struct StagedReader {  // bytes [base, base+kStage) from LDS, others from HBM
+  lds_cu8 *lds;
   const uint8_t *wire;
   uint64_t base;
   __device__ __forceinline__ uint8_t operator()(uint64_t x) const {
     const uint64_t r = x - base;
-    return r < kStage ? lds[r] : wire[x];
+    if (r < kStage) return lds[r];
+    return wire[x];
   }
 };
+__device__ __forceinline__ lds_cu8 *as_lds(const uint8_t *p) {
+  return (lds_cu8 *)(p);
+}
 struct GlobalReader {
   const uint8_t *wire;
   __device__ __forceinline__ uint8_t operator()(uint64_t x) const { return wire[x]; }
@@ -624,44 +676,114 @@ struct GlobalReader {
 
 template <class Rd>
 __device__ __forceinline__ uint64_t rd_le(const Rd &rd, uint64_t x, uint32_t w) {
-  uint64_t v = 0;
-  for (uint32_t i = 0; i < w; ++i) v |= (uint64_t)rd(x + i) << (8 * i);
+  uint64_t v = rd(x);
+  if (w > 1) v |= (uint64_t)rd(x + 1) << 8;
+  if (w > 2) {
+    v |= (uint64_t)rd(x + 2) << 16;
+    v |= (uint64_t)rd(x + 3) << 24;
+  }
+  if (w > 4)
+    for (uint32_t i = 4; i < 8; ++i) v |= (uint64_t)rd(x + i) << (8 * i);
   return v;
 }
 
-// record length at pos (0 if incomplete); also accumulates span counts
-template <class Rd>
-__device__ __forceinline__ uint64_t walk_len(const KLayout &L, const Rd &rd, uint64_t len,
-                                             uint64_t pos, uint32_t w, uint64_t *acc) {
-  const uint64_t p0 = pos;
-  uint32_t sk = 0;
-  for (uint32_t o = 0; o < L.n_ops; ++o) {
-    const spk_op op = L.ops[o];
-    if (op.kind == SPK_OP_COPY) {
-      pos += op.size;
-      if (pos > len) return 0;
-    } else {
-      if (pos + w > len) return 0;
-      const uint64_t c = rd_le(rd, pos, w);
-      pos += w;
-      if (c) {
-        if (op.size > 1 && c > ~0ull / op.size) return 0;
-        const uint64_t nb = c * op.size;
-        if (nb > len - pos) return 0;
-        pos += nb;
-      }
-      if (acc) acc[sk] += c;
-      ++sk;
+// Wire length of the record at `pos` (0 = incomplete: the reference fails it
+// with no_buffer_space). NS > 0: compile-time span count.
+template <int NS, class Rd>
+__device__ __forceinline__ uint64_t wlen(const WalkProg &P, const Rd &rd, uint64_t len,
+                                         uint64_t pos, uint32_t w, uint64_t *acc) {
+  uint64_t p = pos + P.skip[0];
+  const uint32_t ns = NS > 0 ? (uint32_t)NS : P.ns;
+#pragma unroll
+  for (uint32_t k = 0; k < (NS > 0 ? (uint32_t)NS : SPK_MAX_SPANS); ++k) {
+    if (NS == 0 && k >= ns) break;
+    if (p + w > len) return 0;
+    const uint64_t c = rd_le(rd, p, w);
+    p += w;
+    if (c) {
+      if (P.esz[k] > 1 && c > ~0ull / P.esz[k]) return 0;
+      const uint64_t nb = c * P.esz[k];
+      if (nb > len - p) return 0;
+      p += nb;
     }
+    if (acc) acc[k] += c;
+    p += P.skip[k + 1];
   }
-  return pos - p0;
+  if (p > len) return 0;
+  return p - pos;
 }
 
-__device__ void stage_chunk(uint8_t *stage, const uint8_t *wire, uint64_t cs,
-                            uint64_t wire_len) {
-  // 16-B vector loads when aligned, bytes at the ends
-  for (uint32_t x = threadIdx.x; x < kStage; x += blockDim.x)
-    stage[x] = (cs + x < wire_len) ? wire[cs + x] : 0;
+__device__ __forceinline__ void stage_chunk(uint8_t *stage, const uint8_t *wire, uint64_t cs,
+                                            uint64_t wire_len) {
+  typedef uint32_t u32_unaligned __attribute__((aligned(1)));
+  uint32_t *st32 = reinterpret_cast<uint32_t *>(stage);
+  for (uint32_t x = threadIdx.x; x < kStage / 4; x += blockDim.x) {
+    const uint64_t a = cs + 4ull * x;
+    uint32_t v;
+    if (a + 4 <= wire_len) {
+      v = *reinterpret_cast<const u32_unaligned *>(wire + a);
+    } else {
+      v = 0;
+      for (uint32_t i = 0; i < 4; ++i)
+        if (a + i < wire_len) v |= (uint32_t)wire[a + i] << (8 * i);
+    }
+    st32[x] = v;
+  }
+}
+
+// Packed per-position state (u32): count << 16 | link, link = next position
+// (< kChunk) or terminal (bit 15) with q = first start at/after the boundary
+// (bits 0-13, clamped to 16383) and bit 14 = incomplete record.
+constexpr uint32_t kTerm = 0x8000u, kInc = 0x4000u, kQMask = 0x3FFFu;
+
+constexpr uint32_t kPPT = kChunk / kVThreads;  // positions per thread (32)
+
+// Each thread owns positions p = tid + 256*j (j < 32) and keeps their
+// states in registers, so every jump round issues 32 independent LDS loads
+// back to back instead of a dependent load chain per position.
+template <int NS>
+__device__ void build_links(uint32_t *S, const WalkProg &P, const uint8_t *stage,
+                            const uint8_t *wire, uint64_t cs, uint64_t wire_len, uint32_t w,
+                            uint32_t sh) {
+  const StagedReader rd{as_lds(stage), wire, cs};
+#pragma unroll 4
+  for (uint32_t j = 0; j < kPPT; ++j) {
+    const uint32_t p = threadIdx.x + j * kVThreads;
+    uint32_t v;
+    if (cs + p >= wire_len) {
+      v = kTerm | p;  // wire end: no record here
+    } else {
+      const uint64_t L = wlen<NS>(P, rd, wire_len, cs + p, w, (uint64_t *)nullptr);
+      if (!L) {
+        v = kTerm | kInc | p;
+      } else {
+        const uint64_t q = p + L;
+        const uint64_t bnd = (uint64_t)((p >> sh) + 1) << sh;
+        v = (1u << 16) | (q >= bnd ? (kTerm | (uint32_t)(q < kQMask ? q : kQMask))
+                                   : (uint32_t)q);
+      }
+    }
+    S[p] = v;
+  }
+  __syncthreads();
+  uint32_t st[kPPT];
+#pragma unroll
+  for (uint32_t j = 0; j < kPPT; ++j) st[j] = S[threadIdx.x + j * kVThreads];
+  for (;;) {
+    uint32_t u[kPPT];
+#pragma unroll
+    for (uint32_t j = 0; j < kPPT; ++j) u[j] = (st[j] & kTerm) ? 0u : S[st[j] & 0x7FFF];
+    bool more = false;
+#pragma unroll
+    for (uint32_t j = 0; j < kPPT; ++j) {
+      if (!(st[j] & kTerm)) {
+        st[j] = (u[j] & 0xFFFF) | (((st[j] >> 16) + (u[j] >> 16)) << 16);
+        S[threadIdx.x + j * kVThreads] = st[j];
+        more |= !(u[j] & kTerm);
+      }
+    }
+    if (!__syncthreads_or(more)) break;
+  }
 }
 
 __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
@@ -692,7 +814,7 @@ __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
   c->w = w;
   c->errc = e;
   c->data_len = dl;
-  c->end_pos = pos;
+  c->end_pos = 0;  // set by the lane that places record n-1
   c->need_fallback = 0;
   const uint64_t payload = (!e && a.wire_len > pos) ? a.wire_len - pos : 0;
   c->nchunks = (c->n == 0) ? 0 : (payload + kChunk - 1) / kChunk;
@@ -703,98 +825,66 @@ __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
   *res = r;
 }
 
-// candidate walks: block = one chunk, thread = one entry offset
-__global__ __launch_bounds__(kCand) void vec_chunk_tables(
-    DecArgs a, const uint8_t *__restrict__ wire, const uint8_t *__restrict__ ws,
-    uint64_t *__restrict__ table) {
-  __shared__ uint32_t visit[kChunk];
+// per chunk: transition table for entry offsets [0, kK)
+template <int NS>
+__global__ __launch_bounds__(kVThreads) void vec_tables(DecArgs a, WalkProg P,
+                                                        const uint8_t *__restrict__ wire,
+                                                        const uint8_t *__restrict__ ws,
+                                                        uint32_t *__restrict__ table) {
+  __shared__ uint32_t S[kChunk];
   __shared__ __align__(16) uint8_t stage[kStage];
-  __shared__ uint32_t link_t[kCand], link_step[kCand];
-  __shared__ uint64_t res_t[kCand];
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   const uint64_t nchunks = c->nchunks;
   const uint32_t w = c->w;
-  const uint32_t e = threadIdx.x;
   for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-    const uint64_t cs = c->p0 + ch * kChunk;  // absolute chunk start
-    for (uint32_t x = threadIdx.x; x < kChunk; x += blockDim.x) visit[x] = 0xFFFFFFFFu;
+    const uint64_t cs = c->p0 + ch * kChunk;
     stage_chunk(stage, wire, cs, a.wire_len);
     __syncthreads();
-    const StagedReader rd{stage, wire, cs};
-    uint64_t pos = cs + e;
-    uint32_t steps = 0, flags = 0, linked = 0;
-    while (pos < cs + kChunk && pos < a.wire_len) {
-      const uint32_t rel = (uint32_t)(pos - cs);
-      const uint32_t mine = (e << 16) | (steps & 0xFFFF);
-      const uint32_t old = atomicCAS(&visit[rel], 0xFFFFFFFFu, mine);
-      if (old != 0xFFFFFFFFu) {  // another walk got here first: link to it
-        link_t[e] = old >> 16;
-        link_step[e] = old & 0xFFFF;
-        linked = 1;
-        break;
-      }
-      const uint64_t rl = walk_len(a.L, rd, a.wire_len, pos, w, (uint64_t *)nullptr);
-      if (!rl) {
-        flags = kFlagIncomplete;
-        break;
-      }
-      pos += rl;
-      ++steps;
+    build_links<NS>(S, P, stage, wire, cs, a.wire_len, w, kChunkShift);
+    for (uint32_t e = threadIdx.x; e < kK; e += blockDim.x) {
+      const uint32_t v = S[e];
+      const uint32_t q = v & kQMask, cnt = v >> 16;
+      uint32_t t;
+      if (v & kInc)
+        t = t0pack(0, kFlagIncomplete, cnt);
+      else if (q < kChunk)  // clean wire end inside the (last) chunk
+        t = t0pack(0, 0, cnt);
+      else if (q - kChunk >= kK || q == kQMask)
+        t = t0pack(0, kFlagTooBig, cnt);
+      else
+        t = t0pack(q - kChunk, 0, cnt);
+      table[ch * kK + e] = t;
     }
-    uint32_t exit = 0, fl = flags;
-    if (!linked && !flags && pos >= cs + kChunk) {
-      const uint64_t ex = pos - (cs + kChunk);
-      if (ex >= kCand) fl = kFlagTooBig; else exit = (uint32_t)ex;
-    }
-    res_t[e] = tpack(exit, fl, steps);
-    if (!linked) link_t[e] = 0xFFFF;
-    __syncthreads();
-    // resolve links: the target visited the meeting point earlier in time,
-    // so chains are acyclic; two-phase updates, iterate until stable
-    for (;;) {
-      bool upd = false;
-      uint64_t nr = 0;
-      const uint32_t t = link_t[e];
-      if (t != 0xFFFF && link_t[t] == 0xFFFF) {
-        const uint64_t r = res_t[t];
-        nr = tpack(t_exit(r), t_flags(r), steps + (t_count(r) - link_step[e]));
-        upd = true;
-      }
-      __syncthreads();
-      if (upd) {
-        res_t[e] = nr;
-        link_t[e] = 0xFFFF;
-      }
-      if (!__syncthreads_or(link_t[e] != 0xFFFF)) break;
-    }
-    table[ch * kCand + e] = res_t[e];
     __syncthreads();
   }
 }
 
 // up-sweep: out[g][e] = T[g*G+G-1] o ... o T[g*G] (e)
-__global__ __launch_bounds__(kCand) void vec_compose_up(const uint64_t *__restrict__ in,
-                                                        uint64_t n_in,
-                                                        uint64_t *__restrict__ out) {
+template <typename TIn>
+__global__ __launch_bounds__(256) void vec_compose_up(const TIn *__restrict__ in,
+                                                      uint64_t n_in,
+                                                      uint64_t *__restrict__ out) {
   const uint64_t g = blockIdx.x;
-  const uint32_t e0 = threadIdx.x;
-  uint32_t e = e0, fl = 0;
-  uint64_t cnt = 0;
-  for (uint64_t j = g * kGroup; j < n_in && j < (g + 1) * kGroup; ++j) {
-    const uint64_t t = in[j * kCand + e];
-    cnt += t_count(t);
-    if (t_flags(t)) {
-      fl = t_flags(t);
-      break;
+  for (uint32_t e0 = threadIdx.x; e0 < kK; e0 += blockDim.x) {
+    uint32_t e = e0, fl = 0;
+    uint64_t cnt = 0;
+    for (uint64_t j = g * kGroup; j < n_in && j < (g + 1) * kGroup; ++j) {
+      const TIn t = in[j * kK + e];
+      cnt += t_count(t);
+      if (t_flags(t)) {
+        fl = t_flags(t);
+        break;
+      }
+      e = t_exit(t);
     }
-    e = t_exit(t);
+    out[g * kK + e0] = tpack(e, fl, cnt);
   }
-  out[g * kCand + e0] = tpack(e, fl, cnt);
 }
 
 // down-sweep: entry/base of each group -> entry/base of each member.
 // Entries are (offset | flags << 16); a flagged entry propagates unchanged.
-__global__ void vec_compose_down(const uint64_t *__restrict__ tab, uint64_t n_in,
+template <typename TIn>
+__global__ void vec_compose_down(const TIn *__restrict__ tab, uint64_t n_in,
                                  uint64_t n_groups, const uint32_t *__restrict__ g_entry,
                                  const uint64_t *__restrict__ g_base,
                                  uint32_t *__restrict__ m_entry,
@@ -807,14 +897,14 @@ __global__ void vec_compose_down(const uint64_t *__restrict__ tab, uint64_t n_in
     m_entry[j] = ent;
     m_base[j] = base;
     if (ent >> 16) continue;
-    const uint64_t t = tab[j * kCand + ent];
+    const TIn t = tab[j * kK + ent];
     base += t_count(t);
     ent = t_flags(t) ? (t_flags(t) << 16) : t_exit(t);
   }
 }
 
-// TooBig before record n: records straddle chunk boundaries by >= kCand
-// bytes; request the sequential fallback.
+// TooBig before record n: records straddle chunk boundaries by >= kK bytes;
+// request the sequential fallback.
 __global__ void vec_check_entries(uint8_t *__restrict__ ws,
                                   const uint32_t *__restrict__ m_entry,
                                   const uint64_t *__restrict__ m_base) {
@@ -826,7 +916,7 @@ __global__ void vec_check_entries(uint8_t *__restrict__ ws,
 
 // Sequential fallback: one lane walks every record (global reads) and writes
 // each chunk's entry/base directly. Correct for any record size; slow.
-__global__ void vec_seq_walk(DecArgs a, const uint8_t *__restrict__ wire,
+__global__ void vec_seq_walk(DecArgs a, WalkProg P, const uint8_t *__restrict__ wire,
                              uint8_t *__restrict__ ws, uint32_t *__restrict__ m_entry,
                              uint64_t *__restrict__ m_base) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -846,7 +936,7 @@ __global__ void vec_seq_walk(DecArgs a, const uint8_t *__restrict__ wire,
       m_base[ch] = rec;
       ++ch;
     }
-    const uint64_t rl = walk_len(a.L, rd, a.wire_len, pos, c->w, (uint64_t *)nullptr);
+    const uint64_t rl = wlen<0>(P, rd, a.wire_len, pos, c->w, (uint64_t *)nullptr);
     if (!rl) {
       flag = kFlagIncomplete;
       break;
@@ -860,18 +950,19 @@ __global__ void vec_seq_walk(DecArgs a, const uint8_t *__restrict__ wire,
   }
 }
 
-// pass 0, block per chunk: stage, walk from the true entry (thread 0, in
-// LDS), write record starts to `starts`, per-chunk span totals to `csum`,
-// detect a short payload, and the end of record n-1.
-__global__ __launch_bounds__(64) void vec_chunk_walk(DecArgs a,
-                                                     const uint8_t *__restrict__ wire,
-                                                     uint8_t *__restrict__ ws,
-                                                     const uint32_t *__restrict__ m_entry,
-                                                     const uint64_t *__restrict__ m_base,
-                                                     uint64_t *__restrict__ starts,
-                                                     uint64_t *__restrict__ csum,
-                                                     spk_dresult_t *res) {
+// Start pass, block per chunk with a known entry: sub-chunk links, thread 0
+// chains the 32 sub-chunk entries, then one lane per sub-chunk places its
+// records (starts[]), sums span counts, and detects a short payload / the
+// end of record n-1.
+template <int NS>
+__global__ __launch_bounds__(kVThreads) void vec_starts(
+    DecArgs a, WalkProg P, const uint8_t *__restrict__ wire, uint8_t *__restrict__ ws,
+    const uint32_t *__restrict__ m_entry, const uint64_t *__restrict__ m_base,
+    uint64_t *__restrict__ starts, uint64_t *__restrict__ csum, spk_dresult_t *res) {
+  __shared__ uint32_t S[kChunk];
   __shared__ __align__(16) uint8_t stage[kStage];
+  __shared__ uint32_t sub_ent[kNSub], sub_base[kNSub];
+  __shared__ uint64_t red[kVThreads / 64];
   VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
   if (c->errc) return;
   const uint64_t nchunks = c->nchunks, n = c->n;
@@ -883,27 +974,52 @@ __global__ __launch_bounds__(64) void vec_chunk_walk(DecArgs a,
     const uint64_t cs = c->p0 + ch * kChunk;
     stage_chunk(stage, wire, cs, a.wire_len);
     __syncthreads();
+    build_links<NS>(S, P, stage, wire, cs, a.wire_len, w, kSubShift);
+    if (threadIdx.x < kNSub) sub_ent[threadIdx.x] = 0xFFFFFFFFu;
+    __syncthreads();
     if (threadIdx.x == 0) {
-      const StagedReader rd{stage, wire, cs};
-      uint64_t acc[SPK_MAX_SPANS] = {};
-      uint64_t pos = cs + ent, k = base;
-      bool broke = false;
-      while (pos < cs + kChunk && k < n) {
-        const uint64_t rl = walk_len(a.L, rd, a.wire_len, pos, w, acc);
-        if (!rl) {
-          broke = true;
-          break;
-        }
+      uint32_t e = ent, k = 0;
+      while (e < kChunk) {
+        const uint32_t j = e >> kSubShift;
+        sub_ent[j] = e;
+        sub_base[j] = k;
+        const uint32_t v = S[e];
+        k += v >> 16;
+        const uint32_t q = v & kQMask;
+        if ((v & kInc) || q < ((j + 1) << kSubShift)) break;  // incomplete / wire end
+        e = q;
+      }
+    }
+    __syncthreads();
+    uint64_t acc[SPK_MAX_SPANS] = {};
+    if (threadIdx.x < kNSub && sub_ent[threadIdx.x] != 0xFFFFFFFFu) {
+      const StagedReader rd{as_lds(stage), wire, cs};
+      const uint32_t j = threadIdx.x;
+      uint64_t pos = cs + sub_ent[j], k = base + sub_base[j];
+      const uint64_t bnd = cs + ((uint64_t)(j + 1) << kSubShift);
+      while (pos < bnd && k < n) {
+        const uint64_t L = wlen<NS>(P, rd, a.wire_len, pos, w, acc);
+        if (!L) break;
         if (k < a.rec_cap) starts[k] = pos;
-        pos += rl;
+        pos += L;
         ++k;
       }
       if (k == n) atomicMax(&c->end_pos, (unsigned long long)pos);
-      // the walk stopped inside this chunk before record n: the payload is
-      // short (the reference fails reading record k with no_buffer_space)
-      if (k < n && (broke || pos >= a.wire_len))
-        atomicCAS(&res->errc, 0, SPK_ERRC_NO_BUFFER_SPACE);
-      for (uint32_t s2 = 0; s2 < a.L.n_spans; ++s2) csum[ch * SPK_MAX_SPANS + s2] = acc[s2];
+      // stopped before record n without crossing the sub-chunk boundary:
+      // an incomplete record or the wire end (reference: no_buffer_space)
+      if (k < n && pos < bnd) atomicCAS(&res->errc, 0, SPK_ERRC_NO_BUFFER_SPACE);
+    }
+    for (uint32_t s2 = 0; s2 < P.ns; ++s2) {
+      uint64_t v = acc[s2];
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o);
+      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (uint32_t i = 0; i < kVThreads / 64; ++i) t += red[i];
+        csum[ch * SPK_MAX_SPANS + s2] = t;
+      }
+      __syncthreads();
     }
     __syncthreads();
   }
@@ -914,6 +1030,8 @@ __global__ void vec_finish(DecArgs a, uint8_t *__restrict__ ws, spk_dresult_t *r
   VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
   if (c->errc) return;
   spk_dresult_t r = *res;
+  // record n-1 was never placed: the payload holds fewer than n records
+  if (c->n && c->end_pos == 0 && r.errc == 0) r.errc = SPK_ERRC_NO_BUFFER_SPACE;
   if (r.errc == SPK_ERRC_NO_BUFFER_SPACE) {
     r.count = 0;
     r.consumed = 0;
@@ -922,12 +1040,12 @@ __global__ void vec_finish(DecArgs a, uint8_t *__restrict__ ws, spk_dresult_t *r
     r.count = c->n;
     const uint64_t end = c->n ? (uint64_t)c->end_pos : c->p0;
     r.consumed = end > c->data_len ? end : c->data_len;
-    if (c->n > a.rec_cap) r.errc = SPK_ERRC_CAPACITY;
+    if (c->n > a.rec_cap && r.errc == 0) r.errc = SPK_ERRC_CAPACITY;
   }
   *res = r;
 }
 
-// pass 1, block per chunk: decode records [base, base + nrec) from `starts`
+// decode pass, block per chunk: records [base, next_base) from starts[]
 __global__ __launch_bounds__(kThreads) void vec_chunk_decode(
     DecArgs a, const uint8_t *__restrict__ wire, const uint8_t *__restrict__ ws,
     const uint32_t *__restrict__ m_entry, const uint64_t *__restrict__ m_base,
@@ -943,8 +1061,15 @@ __global__ __launch_bounds__(kThreads) void vec_chunk_decode(
     const uint32_t ent = m_entry[ch];
     const uint64_t base = m_base[ch];
     if ((ent >> 16) || base >= n) continue;
-    const uint64_t next = (ch + 1 < nchunks && !(m_entry[ch + 1] >> 16)) ? m_base[ch + 1] : n;
-    const uint64_t hi = next < n ? next : n;
+    // records of this chunk end where the next chunk with a start begins
+    uint64_t hi = n;
+    for (uint64_t c2 = ch + 1; c2 < nchunks; ++c2) {
+      if (!(m_entry[c2] >> 16)) {
+        hi = m_base[c2] < n ? m_base[c2] : n;
+        break;
+      }
+      if ((m_entry[c2] >> 16) & (kFlagIncomplete | kFlagTooBig)) break;
+    }
     if (threadIdx.x < SPK_MAX_SPANS) run[threadIdx.x] = csum[ch * SPK_MAX_SPANS + threadIdx.x];
     __syncthreads();
     for (uint64_t r0 = base; r0 < hi; r0 += kThreads) {
@@ -987,7 +1112,7 @@ static VecWs vec_ws_layout(uint64_t wire_len, uint64_t max_records) {
     off += (bytes + 255) & ~size_t(255);
     return o;
   };
-  v.table = take(nch * kCand * 8);
+  v.table = take(nch * kK * 4);
   uint64_t cnt = nch;
   v.nlev[0] = nch;
   v.levels = 0;
@@ -995,7 +1120,7 @@ static VecWs vec_ws_layout(uint64_t wire_len, uint64_t max_records) {
     cnt = (cnt + kGroup - 1) / kGroup;
     ++v.levels;
     v.nlev[v.levels] = cnt;
-    v.lv[v.levels] = take(cnt * kCand * 8);
+    v.lv[v.levels] = take(cnt * kK * 8);
   }
   for (int l = 0; l <= v.levels; ++l) {
     v.ent[l] = take(v.nlev[l] * 4 + 8);
@@ -1005,6 +1130,20 @@ static VecWs vec_ws_layout(uint64_t wire_len, uint64_t max_records) {
   v.starts = take(max_records * 8 + 8);
   v.end = off;
   return v;
+}
+
+template <int NS>
+static void launch_vec_tables(unsigned grid, hipStream_t s, const DecArgs &a, const WalkProg &P,
+                              const uint8_t *wire, const uint8_t *ws, uint32_t *table) {
+  hipLaunchKernelGGL(vec_tables<NS>, dim3(grid), dim3(kVThreads), 0, s, a, P, wire, ws, table);
+}
+template <int NS>
+static void launch_vec_starts(unsigned grid, hipStream_t s, const DecArgs &a, const WalkProg &P,
+                              const uint8_t *wire, uint8_t *ws, const uint32_t *m_entry,
+                              const uint64_t *m_base, uint64_t *starts, uint64_t *csum,
+                              spk_dresult_t *res) {
+  hipLaunchKernelGGL(vec_starts<NS>, dim3(grid), dim3(kVThreads), 0, s, a, P, wire, ws, m_entry,
+                     m_base, starts, csum, res);
 }
 
 size_t var_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len) {
@@ -1112,41 +1251,58 @@ hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
   }
   // ---- VECTOR ----
   const VecWs v = vec_ws_layout(wire_len, rec_cap);
-  uint64_t *table = reinterpret_cast<uint64_t *>(ws + v.table);
+  const WalkProg P = make_walkprog(L);
+  const int NS = P.ns == 1 ? 1 : P.ns == 2 ? 2 : 0;
+  uint32_t *table = reinterpret_cast<uint32_t *>(ws + v.table);
   hipLaunchKernelGGL(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res);
   const uint64_t max_chunks = v.nlev[0];
-  const unsigned tb = (unsigned)(max_chunks < 8192 ? max_chunks : 8192);
-  hipLaunchKernelGGL(vec_chunk_tables, dim3(tb), dim3(kCand), 0, s, a, wire,
-                     (const uint8_t *)ws, table);
-  const uint64_t *lvl_tab[8];
-  lvl_tab[0] = table;
+  const unsigned tb = (unsigned)(max_chunks < 16384 ? max_chunks : 16384);
+  if (NS == 1)
+    launch_vec_tables<1>(tb, s, a, P, wire, ws, table);
+  else if (NS == 2)
+    launch_vec_tables<2>(tb, s, a, P, wire, ws, table);
+  else
+    launch_vec_tables<0>(tb, s, a, P, wire, ws, table);
+  const uint64_t *lvl_tab[8] = {};
   for (int l = 1; l <= v.levels; ++l) {
     uint64_t *out = reinterpret_cast<uint64_t *>(ws + v.lv[l]);
-    hipLaunchKernelGGL(vec_compose_up, dim3((unsigned)v.nlev[l]), dim3(kCand), 0, s,
-                       lvl_tab[l - 1], v.nlev[l - 1], out);
+    if (l == 1)
+      hipLaunchKernelGGL(vec_compose_up<uint32_t>, dim3((unsigned)v.nlev[l]), dim3(256), 0, s,
+                         (const uint32_t *)table, v.nlev[0], out);
+    else
+      hipLaunchKernelGGL(vec_compose_up<uint64_t>, dim3((unsigned)v.nlev[l]), dim3(256), 0, s,
+                         lvl_tab[l - 1], v.nlev[l - 1], out);
     lvl_tab[l] = out;
   }
   if ((e = hipMemsetAsync(ws + v.ent[v.levels], 0, 8, s)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(ws + v.base[v.levels], 0, 16, s)) != hipSuccess) return e;
   for (int l = v.levels; l >= 1; --l) {
     const uint64_t ng = v.nlev[l];
-    hipLaunchKernelGGL(vec_compose_down, dim3(grid_for(ng, 64)), dim3(64), 0, s,
-                       lvl_tab[l - 1], v.nlev[l - 1], ng,
-                       (const uint32_t *)(ws + v.ent[l]), (const uint64_t *)(ws + v.base[l]),
-                       reinterpret_cast<uint32_t *>(ws + v.ent[l - 1]),
-                       reinterpret_cast<uint64_t *>(ws + v.base[l - 1]));
+    const uint32_t *ge = (const uint32_t *)(ws + v.ent[l]);
+    const uint64_t *gb = (const uint64_t *)(ws + v.base[l]);
+    uint32_t *me = reinterpret_cast<uint32_t *>(ws + v.ent[l - 1]);
+    uint64_t *mb = reinterpret_cast<uint64_t *>(ws + v.base[l - 1]);
+    if (l == 1)
+      hipLaunchKernelGGL(vec_compose_down<uint32_t>, dim3(grid_for(ng, 64)), dim3(64), 0, s,
+                         (const uint32_t *)table, v.nlev[0], ng, ge, gb, me, mb);
+    else
+      hipLaunchKernelGGL(vec_compose_down<uint64_t>, dim3(grid_for(ng, 64)), dim3(64), 0, s,
+                         lvl_tab[l - 1], v.nlev[l - 1], ng, ge, gb, me, mb);
   }
   uint32_t *m_entry = reinterpret_cast<uint32_t *>(ws + v.ent[0]);
   uint64_t *m_base = reinterpret_cast<uint64_t *>(ws + v.base[0]);
   hipLaunchKernelGGL(vec_check_entries, dim3(grid_for(max_chunks, 256)), dim3(256), 0, s, ws,
                      (const uint32_t *)m_entry, (const uint64_t *)m_base);
-  hipLaunchKernelGGL(vec_seq_walk, dim3(1), dim3(64), 0, s, a, wire, ws, m_entry, m_base);
+  hipLaunchKernelGGL(vec_seq_walk, dim3(1), dim3(64), 0, s, a, P, wire, ws, m_entry, m_base);
   uint64_t *csum = reinterpret_cast<uint64_t *>(ws + v.csum);
   uint64_t *starts = reinterpret_cast<uint64_t *>(ws + v.starts);
   if ((e = hipMemsetAsync(csum, 0, max_chunks * SPK_MAX_SPANS * 8, s)) != hipSuccess) return e;
-  const unsigned wb = (unsigned)(max_chunks < 65536 ? max_chunks : 65536);
-  hipLaunchKernelGGL(vec_chunk_walk, dim3(wb), dim3(64), 0, s, a, wire, ws,
-                     (const uint32_t *)m_entry, (const uint64_t *)m_base, starts, csum, d_res);
+  if (NS == 1)
+    launch_vec_starts<1>(tb, s, a, P, wire, ws, m_entry, m_base, starts, csum, d_res);
+  else if (NS == 2)
+    launch_vec_starts<2>(tb, s, a, P, wire, ws, m_entry, m_base, starts, csum, d_res);
+  else
+    launch_vec_starts<0>(tb, s, a, P, wire, ws, m_entry, m_base, starts, csum, d_res);
   hipLaunchKernelGGL(var_scan_blocks, dim3(1), dim3(1024), 0, s, max_chunks, a.L.n_spans,
                      csum, a, d_res);
   hipLaunchKernelGGL(vec_finish, dim3(1), dim3(64), 0, s, a, ws, d_res);
