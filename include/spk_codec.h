@@ -189,6 +189,25 @@ int spk_decode(const spk_layout *L, int mode, const void *d_wire,
                const uint64_t *heap_caps, spk_dresult_t *d_res,
                int32_t *d_errc, void *d_ws, size_t ws_bytes, void *stream);
 
+/* ---- sharded single-message encode (multi-GPU, SPK_MODE_VECTOR) --------
+ * One std::vector<T> message whose records are spread over several GPUs:
+ * every shard encodes only its records' bytes ("body") with the GLOBAL
+ * container-length width (max over all shards' counts and the global record
+ * count: calculate_size.hpp:426-447), and the shard holding record 0 also
+ * writes the header + global count (spk_vector_header). Concatenating the
+ * shard bodies after the header in shard order gives exactly the bytes of
+ * serialize(vector<T>) over all records.
+ * spk_plan(SPK_MODE_VECTOR) on the shard gives max_count (local) and
+ * var_bytes; body size = var_bytes + n * n_spans * width. */
+int spk_encode_body(const spk_layout *L, uint64_t n, const void *d_recs,
+                    const void *const *d_heaps, uint32_t width, void *d_out,
+                    uint64_t out_cap, void *d_ws, size_t ws_bytes, void *stream);
+/* Host-side: header + count prefix of a VECTOR message of total_n records at
+ * `width` into h_out (HOST memory, capacity cap). Returns its length, or a
+ * negative SPK_E_*. (packer.hpp:100-139) */
+int spk_vector_header(const spk_layout *L, uint64_t total_n, uint32_t width,
+                      uint8_t *h_out, uint32_t cap);
+
 /* ---- synthetic inputs (bench / tests): the seeded generator of
  * oracle/ref/types.hpp, restated on the device so the GPU box regenerates
  * exactly the inputs the golden digests were taken from. ---------------- */

@@ -219,6 +219,22 @@ int spko_encode(const spk_layout *L, int mode, uint64_t n, const void *recs,
   return SPK_OK;
 }
 
+int spko_encode_body(const spk_layout *L, uint64_t n, const void *recs,
+                     const void *const *heaps, unsigned width, void *out,
+                     uint64_t out_cap, uint64_t *written) {
+  if (!L || (n && !recs) || (width != 1 && width != 2 && width != 4 && width != 8))
+    return SPK_E_ARG;
+  const uint8_t *r = (const uint8_t *)recs;
+  uint64_t tot = 0;
+  for (uint64_t i = 0; i < n; ++i) tot += rec_wire_size(L, r + i * L->rec_stride, width);
+  if (written) *written = tot;
+  if (tot > out_cap) return SPK_E_CAPACITY;
+  uint8_t *p = (uint8_t *)out;
+  for (uint64_t i = 0; i < n; ++i)
+    p = write_record(L, r + i * L->rec_stride, heaps, width, p);
+  return SPK_OK;
+}
+
 /* ---- decode ------------------------------------------------------------ */
 typedef struct rd_t {
   const uint8_t *now, *end;

@@ -26,6 +26,11 @@ int spko_plan(const spk_layout *L, int mode, uint64_t n, const void *recs,
 int spko_encode(const spk_layout *L, int mode, uint64_t n, const void *recs,
                 const void *const *heaps, void *out, uint64_t out_cap,
                 uint64_t *msg_offsets, uint64_t *written);
+/* body bytes of records [0,n) at an imposed width (no header/count):
+ * the per-shard piece of a multi-GPU single message. */
+int spko_encode_body(const spk_layout *L, uint64_t n, const void *recs,
+                     const void *const *heaps, unsigned width, void *out,
+                     uint64_t out_cap, uint64_t *written);
 int spko_decode(const spk_layout *L, int mode, const void *wire,
                 uint64_t wire_len, const uint64_t *msg_offsets, uint64_t n_msgs,
                 void *recs, uint64_t rec_cap, void *const *heaps,

@@ -256,3 +256,38 @@ def test_full_size_configs(ent):
         assert torch.equal(dec.heaps[k], b.heaps[k])
     del out, dec, b
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("case,n,param", [("rec64", 3000, 0), ("recs", 5000, 48),
+                                          ("recs", 600, 300), ("outer", 2000, 16),
+                                          ("mixed", 300, 300)])
+def test_sharded_bodies_concatenate_to_reference(case, n, param):
+    """Multi-GPU single message on one device: shard bodies encoded with the
+    agreed global width + rank-0 header == serialize(vector<T>) of all."""
+    import ctypes as ct
+    from yalantinglibs_amd import parallel as PAR
+    cd = codec_for(case)
+    _, recs, heaps = synth.make_batch(case, n, 4242, param)
+    exp, _, _ = H.oracle_encode(cd.L, C.SPK_MODE_VECTOR, recs, heaps)
+    full = to_dev(cd, recs, heaps)
+    cuts = [0, n // 3, n // 2, n]
+    plans, bodies = [], []
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        sub = SP.RecordBatch(cd.L, full.recs[lo:hi], full.heaps)  # heap offsets stay global
+        plans.append(cd.get_needed_size(sub, C.SPK_MODE_VECTOR))
+    gmax = max([n] + [p.max_count for p in plans])
+    w = PAR.width_of(gmax)
+    buf = (ct.c_uint8 * 512)()
+    hl = cd.lib.spk_vector_header(cd.L.ptr, n, w, buf, 512)
+    parts = [bytes(buf[:hl])]
+    for (lo, hi), p in zip(zip(cuts[:-1], cuts[1:]), plans):
+        sub = SP.RecordBatch(cd.L, full.recs[lo:hi], full.heaps)
+        size = p.var_bytes + (hi - lo) * cd.L.n_spans * w
+        out = torch.empty(max(size, 1), dtype=torch.uint8, device="cuda")
+        ws = cd.workspace(C.SPK_MODE_VECTOR, hi - lo)
+        rc = cd.lib.spk_encode_body(cd.L.ptr, hi - lo, SP._p(sub.recs), cd._heap_ptrs(sub.heaps),
+                                    w, SP._p(out), out.numel(), SP._p(ws), ws.numel(),
+                                    SP._stream())
+        assert rc == 0
+        parts.append(out[:size].cpu().numpy().tobytes())
+    assert b"".join(parts) == exp

@@ -1,0 +1,100 @@
+"""Multi-GPU sharding logic on CPU (gloo, world_size 2): the ranks agree on
+the global width / offsets and the concatenated shard bodies + header equal
+the reference bytes of serialize(vector<T>) over all records. The oracle
+stands in for the per-shard body encode (checker only); the same collective
+code drives spk_encode_body on GPUs (test_gpu_parity::test_sharded_*)."""
+import ctypes as ct
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import spk_helpers as H
+from yalantinglibs_amd import _capi as C
+from yalantinglibs_amd import layout as LY
+from yalantinglibs_amd import parallel as PAR
+from yalantinglibs_amd import synth
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_header(L, n, w):
+    lib = C.load_codec()
+    buf = (ct.c_uint8 * 512)()
+    k = lib.spk_vector_header(L.ptr, n, w, buf, 512)
+    assert k > 0
+    return bytes(buf[:k])
+
+
+def _worker(rank, world, port, case, n, param, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        L = LY.case_layout(case)
+        _, recs, heaps = synth.make_batch(case, n, H.SEED if hasattr(H, "SEED") else 7, param)
+        lo, hi = n * rank // world, n * (rank + 1) // world
+        # this rank's shard, re-based heaps (a real rank owns its own heap)
+        sub = recs[lo:hi].copy()
+        sh = []
+        for k, sp in enumerate(L.dev.spans):
+            cnt = sub[sp.path + ".n"].astype(np.int64)
+            off = sub[sp.path + ".off"].astype(np.int64)
+            parts = [heaps[k][o * sp.elem.size:(o + c) * sp.elem.size] for o, c in zip(off, cnt)]
+            h = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+            sub[sp.path + ".off"] = np.concatenate([[0], np.cumsum(cnt)[:-1]]) if len(cnt) else []
+            sh.append(np.ascontiguousarray(h, dtype=np.uint8))
+        o = C.load_oracle()
+        plan = C.spk_plan_t()
+        assert o.spko_plan(L.ptr, C.SPK_MODE_VECTOR, len(sub), H._ptr(sub), ct.byref(plan)) == 0
+        sp = PAR.agree_shard_plan(len(sub), plan.max_count, plan.var_bytes, L.n_spans,
+                                  lambda gn, w: _oracle_header(L, gn, w))
+        hp = (ct.c_void_p * max(len(sh), 1))(*[h.ctypes.data if h.size else 0 for h in sh])
+        body = np.zeros(max(sp.body_bytes[rank], 1), np.uint8)
+        wr = ct.c_uint64()
+        assert o.spko_encode_body(L.ptr, len(sub), H._ptr(sub), hp, sp.width, H._ptr(body),
+                                  body.size, ct.byref(wr)) == 0
+        assert wr.value == sp.body_bytes[rank]
+        bodies = [None] * world
+        dist.all_gather_object(bodies, body[:wr.value].tobytes())
+        if rank == 0:
+            msg = sp.header + b"".join(bodies)
+            full, _, _ = H.oracle_encode(L, C.SPK_MODE_VECTOR, recs, heaps)
+            q.put((msg == full, len(msg), sp.total_bytes, sp.width))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,n,param", [("rec64", 1000, 0), ("recs", 3000, 48),
+                                          ("recs", 300, 400), ("outer", 700, 16),
+                                          ("mixed", 200, 300)])
+def test_sharded_vector_message_gloo(case, n, param):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, n, param, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    ok, ln, total, w = q.get(timeout=10)
+    assert ok and ln == total
+
+
+def test_width_agreement_uses_global_count():
+    # 200 records per shard: each shard alone would use width 1, the message
+    # of 400 records needs width 2 (calculate_size.hpp:79,426-447)
+    assert PAR.width_of(200) == 1 and PAR.width_of(400) == 2

@@ -87,7 +87,8 @@ ORACLE_PATH = os.path.join(_ROOT, "oracle", "libspk_oracle.so")
 # exported symbols of include/spk_codec.h (checked by tests/test_capi.py)
 CODEC_SYMBOLS = ["spk_abi_version", "spk_errc_message", "spk_layout_check",
                  "spk_workspace_bytes", "spk_plan", "spk_encode", "spk_decode",
-                 "spk_synth", "spk_synth_counts"]
+                 "spk_synth", "spk_synth_counts", "spk_encode_body",
+                 "spk_vector_header"]
 
 _codec = None
 _oracle = None
@@ -111,6 +112,10 @@ def _bind_codec(lib):
                                ct.POINTER(P), ct.POINTER(U64), P, P, P,
                                ct.c_size_t, P]
     lib.spk_synth.argtypes = [ct.c_int, U64, U64, U64, ct.c_uint32, P, P, P, P]
+    lib.spk_encode_body.argtypes = [PL, U64, P, ct.POINTER(P), ct.c_uint32, P, U64, P,
+                                    ct.c_size_t, P]
+    lib.spk_vector_header.argtypes = [PL, U64, ct.c_uint32, ct.POINTER(ct.c_uint8),
+                                      ct.c_uint32]
     lib.spk_synth_counts.argtypes = [ct.c_int, U64, U64, U64, ct.c_uint32, P, P]
     return lib
 
@@ -139,6 +144,8 @@ def load_oracle():
         lib.spko_plan.argtypes = [PL, ct.c_int, U64, P, ct.POINTER(spk_plan_t)]
         lib.spko_encode.argtypes = [PL, ct.c_int, U64, P, ct.POINTER(P), P, U64,
                                     P, ct.POINTER(U64)]
+        lib.spko_encode_body.argtypes = [PL, U64, P, ct.POINTER(P), ct.c_uint, P, U64,
+                                         ct.POINTER(U64)]
         lib.spko_decode.argtypes = [PL, ct.c_int, P, U64, P, U64, P, U64,
                                     ct.POINTER(P), ct.POINTER(U64),
                                     ct.POINTER(spk_dresult_t), P]

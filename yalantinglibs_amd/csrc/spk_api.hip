@@ -143,4 +143,38 @@ int spk_decode(const spk_layout *L, int mode, const void *d_wire, uint64_t wire_
                                   s));
 }
 
+int spk_encode_body(const spk_layout *L, uint64_t n, const void *d_recs,
+                    const void *const *d_heaps, uint32_t width, void *d_out,
+                    uint64_t out_cap, void *d_ws, size_t ws_bytes, void *stream) {
+  int rc = spk_layout_check(L);
+  if (rc) return rc;
+  if (width != 1 && width != 2 && width != 4 && width != 8) return SPK_E_ARG;
+  if ((n && !d_recs) || !d_out || !d_ws) return SPK_E_ARG;
+  if (ws_bytes < spk_workspace_bytes(L, SPK_MODE_VECTOR, n, 0)) return SPK_E_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  if (is_trivial(L)) {  // body == the records verbatim (packer.hpp:418-421)
+    const uint64_t nb = n * (uint64_t)L->rec_stride;
+    if (nb > out_cap) return SPK_E_CAPACITY;
+    return hip_rc(hipMemcpyAsync(d_out, d_recs, nb, hipMemcpyDeviceToDevice, s));
+  }
+  if ((uintptr_t)d_recs % 8 || !d_heaps) return SPK_E_ARG;
+  return hip_rc(launch_var_encode_body(L, n, d_recs, d_heaps, width, d_out, out_cap, d_ws,
+                                       ws_bytes, s));
+}
+
+int spk_vector_header(const spk_layout *L, uint64_t total_n, uint32_t width, uint8_t *h_out,
+                      uint32_t cap) {
+  int rc = spk_layout_check(L);
+  if (rc) return rc;
+  if ((width != 1 && width != 2 && width != 4 && width != 8) || !h_out) return SPK_E_ARG;
+  if (width < width_of(total_n)) return SPK_E_ARG;  // the count itself must fit
+  uint8_t hb[4 + 1 + SPK_MAX_LITERAL + 1 + 8];
+  uint32_t len = write_hdr(hb, L->fmt_vector, width);
+  for (uint32_t i = 0; i < width; ++i) hb[len + i] = (uint8_t)(total_n >> (8 * i));
+  len += width;
+  if (len > cap) return SPK_E_CAPACITY;
+  for (uint32_t i = 0; i < len; ++i) h_out[i] = hb[i];
+  return (int)len;
+}
+
 }  // extern "C"

@@ -193,6 +193,10 @@ hipError_t launch_var_encode(const spk_layout *L, int mode, uint64_t n,
                              const spk_plan_t *d_plan, void *d_out,
                              uint64_t out_cap, uint64_t *d_offsets, void *d_ws,
                              size_t ws_bytes, hipStream_t s);
+hipError_t launch_var_encode_body(const spk_layout *L, uint64_t n, const void *d_recs,
+                                  const void *const *d_heaps, uint32_t width, void *d_out,
+                                  uint64_t out_cap, void *d_ws, size_t ws_bytes,
+                                  hipStream_t s);
 hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
                              uint64_t wire_len, const uint64_t *d_offsets,
                              uint64_t n_msgs, void *d_recs, uint64_t rec_cap,

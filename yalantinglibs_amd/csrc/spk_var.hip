@@ -1216,6 +1216,32 @@ hipError_t launch_var_encode(const spk_layout *L, int mode, uint64_t n,
   return hipGetLastError();
 }
 
+// plan override for a sharded body: imposed width, no header
+__global__ void body_plan_kernel(spk_plan_t *plan, uint64_t n, uint32_t n_spans,
+                                 uint32_t width) {
+  if (threadIdx.x != 0) return;
+  spk_plan_t p = *plan;
+  p.width = width;
+  p.header_bytes = 0;
+  p.total_bytes = p.var_bytes + n * (uint64_t)n_spans * width;
+  *plan = p;
+}
+
+hipError_t launch_var_encode_body(const spk_layout *L, uint64_t n, const void *d_recs,
+                                  const void *const *d_heaps, uint32_t width, void *d_out,
+                                  uint64_t out_cap, void *d_ws, size_t ws_bytes,
+                                  hipStream_t s) {
+  // the plan lives in the workspace control area for this call
+  spk_plan_t *plan = reinterpret_cast<spk_plan_t *>((uint8_t *)d_ws + kWsCtl + 1024);
+  hipError_t e = launch_var_plan(L, SPK_MODE_VECTOR, n, d_recs, plan, d_ws, ws_bytes, s);
+  if (e != hipSuccess) return e;
+  uint32_t ns = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i) ns += L->ops[i].kind == SPK_OP_SPAN;
+  hipLaunchKernelGGL(body_plan_kernel, dim3(1), dim3(64), 0, s, plan, n, ns, width);
+  return launch_var_encode(L, SPK_MODE_VECTOR, n, d_recs, d_heaps, plan, d_out, out_cap,
+                           nullptr, d_ws, ws_bytes, s);
+}
+
 hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
                              uint64_t wire_len, const uint64_t *d_offsets,
                              uint64_t n_msgs, void *d_recs, uint64_t rec_cap,

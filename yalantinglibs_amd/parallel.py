@@ -1,0 +1,149 @@
+"""Multi-GPU struct_pack: record-range shards, one process per GPU.
+
+Two shapes:
+
+* Independent shards (the bench's weak-scaling path): every rank encodes /
+  decodes its own records as its own messages. No data-path collective.
+
+* One message over all shards (`ShardedVectorEncoder`): the bytes of
+  serialize(std::vector<T>) over the concatenation of every rank's records.
+  The container-length width is a whole-message property (max element count
+  over every container, incl. the global record count:
+  calculate_size.hpp:426-447), so the ranks agree on it with one 8-byte
+  all-reduce(MAX); an all-gather of each rank's body size gives its byte
+  offset; every rank encodes its body with the global width (spk_encode_body)
+  and rank 0 prepends the header (spk_vector_header). Concatenation is a
+  grouped RCCL send/recv of the bodies into rank 0's output buffer (over
+  xGMI), or — for the coro_rpc destination — each rank's D2H into its offset
+  of one pinned host buffer.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import _capi as C
+from .struct_pack import Codec, RecordBatch, _p, _stream
+
+
+@dataclass
+class ShardPlan:
+    global_n: int
+    width: int
+    header: bytes            # rank 0's header + count prefix
+    body_bytes: List[int]    # per rank
+    offsets: List[int]       # byte offset of each rank's body in the message
+    total_bytes: int
+
+
+def width_of(max_count: int) -> int:
+    """calculate_size.hpp:426-447."""
+    return 1 if max_count < 1 << 8 else 2 if max_count < 1 << 16 else 4 if max_count < 1 << 32 else 8
+
+
+def agree_shard_plan(local_n: int, local_max_count: int, local_var_bytes: int,
+                     n_spans: int, header_fn, group=None, device=None) -> ShardPlan:
+    """Collective part of the sharded encode (works on gloo or nccl):
+    all-reduce(SUM) of record counts, all-reduce(MAX) of the largest element
+    count, all-gather of body sizes."""
+    world = dist.get_world_size(group)
+    dev = device if device is not None else torch.device("cpu")
+    t = torch.tensor([local_n, local_max_count], dtype=torch.int64, device=dev)
+    s = t.clone()
+    dist.all_reduce(s[:1], op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(s[1:], op=dist.ReduceOp.MAX, group=group)
+    global_n, gmax = int(s[0].item()), int(s[1].item())
+    w = width_of(max(global_n, gmax))
+    body = local_var_bytes + local_n * n_spans * w
+    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([body], dtype=torch.int64, device=dev), group=group)
+    body_bytes = [int(x.item()) for x in sizes]
+    header = header_fn(global_n, w)
+    offsets, off = [], len(header)
+    for b in body_bytes:
+        offsets.append(off)
+        off += b
+    return ShardPlan(global_n, w, header, body_bytes, offsets, off)
+
+
+class ShardedVectorEncoder:
+    """serialize(std::vector<T>) of records spread over the ranks of a
+    process group (one GPU per rank)."""
+
+    def __init__(self, codec: Codec, group=None):
+        self.cd = codec
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+
+    def header(self, global_n: int, width: int) -> bytes:
+        buf = (ct.c_uint8 * 512)()
+        n = self.cd.lib.spk_vector_header(self.cd.L.ptr, global_n, width, buf, 512)
+        if n < 0:
+            raise RuntimeError(f"spk_vector_header failed ({n})")
+        return bytes(buf[:n])
+
+    def plan(self, batch: RecordBatch) -> ShardPlan:
+        p = self.cd.get_needed_size(batch, C.SPK_MODE_VECTOR)
+        return agree_shard_plan(batch.n, p.max_count, p.var_bytes, self.cd.L.n_spans,
+                                self.header, self.group, self.cd.device)
+
+    def encode_body(self, batch: RecordBatch, width: int, out: torch.Tensor, stream=None):
+        ws = self.cd.workspace(C.SPK_MODE_VECTOR, batch.n)
+        rc = self.cd.lib.spk_encode_body(self.cd.L.ptr, batch.n, _p(batch.recs),
+                                         self.cd._heap_ptrs(batch.heaps), width, _p(out),
+                                         out.numel(), _p(ws), ws.numel(), _stream(stream))
+        if rc != 0:
+            raise RuntimeError(f"spk_encode_body failed ({rc})")
+
+    def encode(self, batch: RecordBatch, root: int = 0) -> Optional[torch.Tensor]:
+        """Returns the whole message on `root` (None elsewhere). The bodies
+        move to root with grouped RCCL point-to-point transfers straight into
+        their slices of the output buffer."""
+        sp = self.plan(batch)
+        mine = sp.body_bytes[self.rank]
+        body = torch.empty(max(mine, 1), dtype=torch.uint8, device=self.cd.device)
+        self.encode_body(batch, sp.width, body)
+        if self.rank == root:
+            out = torch.empty(sp.total_bytes, dtype=torch.uint8, device=self.cd.device)
+            hdr = torch.frombuffer(bytearray(sp.header), dtype=torch.uint8)
+            out[:len(sp.header)].copy_(hdr)
+            o = sp.offsets[self.rank]
+            out[o:o + mine].copy_(body[:mine])
+            ops = []
+            for r in range(self.world):
+                if r != root and sp.body_bytes[r]:
+                    o = sp.offsets[r]
+                    ops.append(dist.P2POp(dist.irecv, out[o:o + sp.body_bytes[r]], r,
+                                          self.group))
+            if ops:
+                for req in dist.batch_isend_irecv(ops):
+                    req.wait()
+            return out
+        if mine:
+            for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, body[:mine], root,
+                                                          self.group)]):
+                req.wait()
+        return None
+
+    def encode_to_host(self, batch: RecordBatch, host_out: torch.Tensor) -> ShardPlan:
+        """coro_rpc destination: every rank copies its body D2H straight into
+        its offset of one (shared, pinned) host buffer; rank 0 also writes
+        the header. `host_out` must be visible to all ranks (e.g. a shared
+        memory tensor) and at least plan.total_bytes long."""
+        sp = self.plan(batch)
+        mine = sp.body_bytes[self.rank]
+        body = torch.empty(max(mine, 1), dtype=torch.uint8, device=self.cd.device)
+        self.encode_body(batch, sp.width, body)
+        o = sp.offsets[self.rank]
+        host_out[o:o + mine].copy_(body[:mine])
+        if self.rank == 0:
+            host_out[:len(sp.header)].copy_(torch.frombuffer(bytearray(sp.header),
+                                                             dtype=torch.uint8))
+        torch.cuda.synchronize(self.cd.device)
+        dist.barrier(self.group)
+        return sp
