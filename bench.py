@@ -36,6 +36,7 @@ CONFIGS = {
     "c4": ("outer", 10_000_000, 16, "A",
            "C4: 10M Outer{int64, vector<Inner{int32,float}> n U[0,16]} per GPU, one vector message"),
 }
+DOMINANT = {"c2": "spk::shift_copy_kernel"}  # dominant kernel per config (rocprof name)
 SEEDS = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -175,10 +176,16 @@ def main():
     # moves record bytes in and wire bytes out; per launch algorithmic bytes
     enc_bytes = rec_bytes + wire_bytes
     roof_ach = enc_bytes / (enc_ms * 1e-3) / 1e9
+    # HBM bytes per launch of the same kernel from a separate rocprofv3 PMC run
+    # of this command (scripts/gpu_pmc.sh -> profiles/r01/pmc_<config>.json;
+    # FETCH_SIZE doubled per the gfx950 correction, WRITE_SIZE exact)
     traffic = None
-    if args.pmc_json and os.path.exists(args.pmc_json):
-        with open(args.pmc_json) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+    pmc = args.pmc_json or os.path.join(ROOT, "profiles", "r01", f"pmc_{args.config}.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            for k, v in json.load(f).items():
+                if k.startswith(DOMINANT.get(args.config, "~")):
+                    traffic = v.get("hbm_bytes_per_launch")
 
     host = None
     if args.host_path and rank == 0:

@@ -1,0 +1,217 @@
+// spk_layout.hpp — host C++20 reflection -> spk_layout descriptor, and the
+// host-object <-> device-record marshalling used when a batch starts or ends
+// in host memory (coro_rpc socket buffers).
+//
+// Device record of a record type T:
+//   * T trivially serializable (reference reflection.hpp:851-922): the device
+//     record IS T, byte for byte (padding included) — one COPY op.
+//   * otherwise members are flattened in declaration order (reference
+//     packer.hpp:432-447): trivially serializable members become COPY ops at
+//     a C-like offset of the device record; std::string / std::vector<U>
+//     (U trivially serializable) become a SPAN op {u32 count; u64 element
+//     offset into that member's heap}. Nested non-trivial aggregates are
+//     flattened inline.
+// This is the same flattening as yalantinglibs_amd/schema.py:flatten, so
+// Python and C++ front ends produce identical descriptors.
+#pragma once
+#include <cstring>
+#include <stdexcept>
+#include <vector>
+
+#include "../../spk_codec.h"
+#include "spk_type_code.hpp"
+
+namespace struct_pack {
+namespace spk_detail {
+
+struct layout_builder {
+  spk_layout L{};
+  uint32_t off = 0, align = 1, spans = 0;
+  uint32_t place(uint32_t size, uint32_t al) {
+    off = (off + al - 1) / al * al;
+    const uint32_t o = off;
+    off += size;
+    if (al > align) align = al;
+    return o;
+  }
+  void copy(uint32_t size, uint32_t al) {
+    const uint32_t o = place(size, al);
+    if (L.n_ops && L.ops[L.n_ops - 1].kind == SPK_OP_COPY &&
+        L.ops[L.n_ops - 1].rec_off + L.ops[L.n_ops - 1].size == o) {
+      L.ops[L.n_ops - 1].size += size;  // merge runs contiguous in the record
+      return;
+    }
+    if (L.n_ops >= SPK_MAX_OPS) throw std::length_error("struct_pack: too many members");
+    L.ops[L.n_ops++] = spk_op{SPK_OP_COPY, o, size, 0};
+  }
+  void span(uint32_t esz) {
+    const uint32_t c = place(4, 4), a = place(8, 8);
+    if (L.n_ops >= SPK_MAX_OPS || spans >= SPK_MAX_SPANS)
+      throw std::length_error("struct_pack: too many variable-length members");
+    L.ops[L.n_ops++] = spk_op{SPK_OP_SPAN, c, esz, a};
+    ++spans;
+  }
+};
+
+template <typename T>
+void flatten_into(layout_builder &b) {
+  if constexpr (is_trivially_serializable<T>()) {
+    b.copy(sizeof(T), alignof(T));
+  } else if constexpr (is_string_v<T>) {
+    b.span(1);
+  } else if constexpr (is_container_v<T>) {
+    using E = remove_cvref_t<typename T::value_type>;
+    static_assert(is_trivially_serializable<E>(),
+                  "MI355X codec: containers of non-trivially-serializable elements are "
+                  "outside the flat record model");
+    b.span(sizeof(E));
+  } else if constexpr (is_std_array<T>::value) {
+    for (std::size_t i = 0; i < std::tuple_size_v<T>; ++i)
+      flatten_into<typename T::value_type>(b);
+  } else {
+    using M = members_tuple_t<T>;
+    [&]<std::size_t... I>(std::index_sequence<I...>) {
+      (flatten_into<std::tuple_element_t<I, M>>(b), ...);
+    }(std::make_index_sequence<std::tuple_size_v<M>>{});
+  }
+}
+
+inline void fill_fmt(spk_msgfmt &f, uint32_t code, uint32_t flags, const lit_t &lit) {
+  f.code = code;
+  f.flags = flags;
+  f.literal_len = static_cast<uint32_t>(lit.n);
+  for (std::size_t i = 0; i < lit.n && i < SPK_MAX_LITERAL; ++i) f.literal[i] = lit.d[i];
+}
+
+// sp_config resolution (type_calculate.hpp:744-891): call-site conf first,
+// then the message type's own config; DEFAULT -> type literal iff !NDEBUG.
+template <typename Msg, uint64_t conf>
+constexpr uint32_t msg_flags() {
+  uint64_t c = conf & 0b11;
+  if (c == sp_config::DEFAULT) c = type_config<Msg>() & 0b11;
+  const bool no_head = c == sp_config::DISABLE_ALL_META_INFO;
+#ifdef NDEBUG
+  constexpr bool debug_literal = false;
+#else
+  constexpr bool debug_literal = true;
+#endif
+  const bool lit = c == sp_config::DEFAULT ? debug_literal : c == sp_config::ENABLE_TYPE_INFO;
+  uint32_t f = 0;
+  if (!no_head) {
+    f |= SPK_MF_HASH_HEAD;
+    if (lit) f |= SPK_MF_TYPE_LITERAL;
+  }
+  if (has_container<Msg>()) f |= SPK_MF_HAS_CONTAINER;
+  return f;
+}
+
+}  // namespace spk_detail
+
+// Descriptor of record type T for the batch codec (cacheable, immutable).
+template <typename T, uint64_t conf = sp_config::DEFAULT>
+spk_layout make_spk_layout() {
+  using namespace spk_detail;
+  layout_builder b;
+  b.L.abi = SPK_ABI_VERSION;
+  flatten_into<T>(b);
+  if constexpr (is_trivially_serializable<T>()) {
+    b.L.flags = SPK_LAYOUT_TRIVIAL;
+    b.L.rec_stride = sizeof(T);
+  } else {
+    const uint32_t al = b.align < 4 ? 4 : b.align;
+    b.L.rec_stride = (b.off + al - 1) / al * al;
+  }
+  fill_fmt(b.L.fmt_vector, get_type_code<std::vector<T>>(),
+           msg_flags<std::vector<T>, conf>(), get_type_literal<std::vector<T>>());
+  fill_fmt(b.L.fmt_one, get_type_code<T>(), msg_flags<T, conf>(), get_type_literal<T>());
+  return b.L;
+}
+
+namespace spk_detail {
+
+// ---- host object <-> device record ----------------------------------------
+struct marshal_state {
+  const spk_layout *L;
+  uint8_t *rec;                                   // current device record
+  uint32_t op = 0, within = 0;                    // walking the op list
+  std::vector<std::vector<uint8_t>> *heaps;       // one per span
+  uint32_t span = 0;
+};
+
+inline void put_copy(marshal_state &s, const void *src, uint32_t size) {
+  // COPY ops may merge several members: advance through the current op
+  const spk_op &op = s.L->ops[s.op];
+  std::memcpy(s.rec + op.rec_off + s.within, src, size);
+  s.within += size;
+  if (s.within == op.size) {
+    ++s.op;
+    s.within = 0;
+  }
+}
+
+template <typename T>
+void to_device(const T &v, marshal_state &s) {
+  if constexpr (is_trivially_serializable<T>()) {
+    put_copy(s, &v, sizeof(T));
+  } else if constexpr (is_string_v<T> || is_container_v<T>) {
+    const spk_op &op = s.L->ops[s.op++];
+    auto &heap = (*s.heaps)[s.span++];
+    const uint32_t cnt = static_cast<uint32_t>(v.size());
+    const uint64_t eoff = heap.size() / op.size;
+    std::memcpy(s.rec + op.rec_off, &cnt, 4);
+    std::memcpy(s.rec + op.aux, &eoff, 8);
+    const auto *p = reinterpret_cast<const uint8_t *>(v.data());
+    heap.insert(heap.end(), p, p + static_cast<std::size_t>(cnt) * op.size);
+  } else if constexpr (is_std_array<T>::value) {
+    for (const auto &e : v) to_device(e, s);
+  } else {
+    std::apply([&](const auto &...m) { (to_device(m, s), ...); }, tie_members(v));
+  }
+}
+
+struct unmarshal_state {
+  const spk_layout *L;
+  const uint8_t *rec;
+  uint32_t op = 0, within = 0;
+  const uint8_t *const *heaps;
+  uint32_t span = 0;
+};
+
+inline void get_copy(unmarshal_state &s, void *dst, uint32_t size) {
+  const spk_op &op = s.L->ops[s.op];
+  std::memcpy(dst, s.rec + op.rec_off + s.within, size);
+  s.within += size;
+  if (s.within == op.size) {
+    ++s.op;
+    s.within = 0;
+  }
+}
+
+template <typename T>
+void from_device(T &v, unmarshal_state &s) {
+  if constexpr (is_trivially_serializable<T>()) {
+    get_copy(s, &v, sizeof(T));
+  } else if constexpr (is_string_v<T> || is_container_v<T>) {
+    const spk_op &op = s.L->ops[s.op++];
+    const uint8_t *heap = s.heaps[s.span++];
+    uint32_t cnt;
+    uint64_t eoff;
+    std::memcpy(&cnt, s.rec + op.rec_off, 4);
+    std::memcpy(&eoff, s.rec + op.aux, 8);
+    const uint8_t *src = heap + eoff * op.size;
+    if constexpr (std::is_same_v<T, std::string_view> || is_std_span<T>::value) {
+      // views alias the decoded heap (the reference's views alias the input)
+      v = T(reinterpret_cast<typename T::const_pointer>(src), cnt);
+    } else {
+      v.resize(cnt);
+      if (cnt) std::memcpy(v.data(), src, static_cast<std::size_t>(cnt) * op.size);
+    }
+  } else if constexpr (is_std_array<T>::value) {
+    for (auto &e : v) from_device(e, s);
+  } else {
+    std::apply([&](auto &...m) { (from_device(m, s), ...); }, tie_members(v));
+  }
+}
+
+}  // namespace spk_detail
+}  // namespace struct_pack

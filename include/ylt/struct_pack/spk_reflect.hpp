@@ -1,0 +1,159 @@
+// spk_reflect.hpp — compile-time reflection for the MI355X struct_pack front
+// end (our own implementation; behaviour follows the reference's
+// ylt::reflection member_count.hpp:158-209 / member_ptr.hpp:95-137 for
+// aggregates): member count by brace-initialisation probing, member access
+// by structured bindings.
+//
+// Supported members: fundamentals, enums, std::string / std::string_view,
+// std::vector<T> / std::span<T>, std::array<T, N>, and nested aggregates.
+// (C arrays inside aggregates defeat brace-init counting — use std::array.)
+#pragma once
+#include <array>
+#include <cstddef>
+#include <cstdint>
+#include <span>
+#include <string>
+#include <string_view>
+#include <tuple>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+namespace struct_pack {
+
+// sp_config (ref include/ylt/struct_pack/reflection.hpp:53-60)
+enum sp_config : uint64_t {
+  DEFAULT = 0,
+  DISABLE_TYPE_INFO = 0b1,
+  ENABLE_TYPE_INFO = 0b10,
+  DISABLE_ALL_META_INFO = 0b11,
+  ENCODING_WITH_VARINT = 0b100,
+  USE_FAST_VARINT = 0b1000
+};
+
+namespace spk_detail {
+
+template <typename T>
+using remove_cvref_t = std::remove_cv_t<std::remove_reference_t<T>>;
+
+template <typename T> struct is_std_vector : std::false_type {};
+template <typename T, typename A> struct is_std_vector<std::vector<T, A>> : std::true_type {};
+template <typename T> struct is_std_span : std::false_type {};
+template <typename T, std::size_t E> struct is_std_span<std::span<T, E>> : std::bool_constant<E == std::dynamic_extent> {};
+template <typename T> struct is_std_array : std::false_type {};
+template <typename T, std::size_t N> struct is_std_array<std::array<T, N>> : std::true_type {};
+
+template <typename T>
+constexpr bool is_string_v = std::is_same_v<T, std::string> || std::is_same_v<T, std::string_view>;
+template <typename T>
+constexpr bool is_container_v = is_std_vector<T>::value || is_std_span<T>::value;
+template <typename T>
+constexpr bool is_fundamental_v = std::is_arithmetic_v<T> || std::is_enum_v<T>;
+template <typename T>
+constexpr bool is_record_v = std::is_aggregate_v<T> && std::is_class_v<T> &&
+                             !is_std_array<T>::value && !is_string_v<T> && !is_container_v<T>;
+
+// ---- aggregate member count (brace-init probing) ----------------------------
+struct any_init {
+  template <typename T>
+  constexpr operator T() const noexcept;  // unevaluated only
+};
+
+template <typename T, std::size_t... I>
+constexpr bool brace_constructible(std::index_sequence<I...>) {
+  return requires { T{((void)I, any_init{})...}; };
+}
+
+template <typename T, std::size_t N = 0>
+constexpr std::size_t members_count_impl() {
+  if constexpr (N > 40) {
+    return N;  // give up (static_assert below)
+  } else if constexpr (brace_constructible<T>(std::make_index_sequence<N + 1>{})) {
+    return members_count_impl<T, N + 1>();
+  } else {
+    return N;
+  }
+}
+
+template <typename T>
+constexpr std::size_t members_count_v = members_count_impl<T>();
+
+// ---- tie members by structured bindings --------------------------------------
+#define SPK_TIE_CASE(N, ...)                   \
+  else if constexpr (n == N) {                 \
+    auto &&[__VA_ARGS__] = obj;                \
+    return std::forward_as_tuple(__VA_ARGS__); \
+  }
+
+template <typename T>
+constexpr auto tie_members(T &&obj) {
+  using U = remove_cvref_t<T>;
+  constexpr std::size_t n = members_count_v<U>;
+  static_assert(n <= 24, "struct_pack MI355X front end: at most 24 members per aggregate");
+  if constexpr (n == 0) {
+    return std::tuple<>{};
+  }
+  SPK_TIE_CASE(1, a0)
+  SPK_TIE_CASE(2, a0, a1)
+  SPK_TIE_CASE(3, a0, a1, a2)
+  SPK_TIE_CASE(4, a0, a1, a2, a3)
+  SPK_TIE_CASE(5, a0, a1, a2, a3, a4)
+  SPK_TIE_CASE(6, a0, a1, a2, a3, a4, a5)
+  SPK_TIE_CASE(7, a0, a1, a2, a3, a4, a5, a6)
+  SPK_TIE_CASE(8, a0, a1, a2, a3, a4, a5, a6, a7)
+  SPK_TIE_CASE(9, a0, a1, a2, a3, a4, a5, a6, a7, a8)
+  SPK_TIE_CASE(10, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9)
+  SPK_TIE_CASE(11, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10)
+  SPK_TIE_CASE(12, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11)
+  SPK_TIE_CASE(13, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, a12)
+  SPK_TIE_CASE(14, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, a12, a13)
+  SPK_TIE_CASE(15, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, a12, a13, a14)
+  SPK_TIE_CASE(16, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, a12, a13, a14, a15)
+  SPK_TIE_CASE(17, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, a12, a13, a14, a15, a16)
+  SPK_TIE_CASE(18, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, a12, a13, a14, a15, a16,
+               a17)
+  SPK_TIE_CASE(19, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, a12, a13, a14, a15, a16,
+               a17, a18)
+  SPK_TIE_CASE(20, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, a12, a13, a14, a15, a16,
+               a17, a18, a19)
+  SPK_TIE_CASE(21, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, a12, a13, a14, a15, a16,
+               a17, a18, a19, a20)
+  SPK_TIE_CASE(22, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, a12, a13, a14, a15, a16,
+               a17, a18, a19, a20, a21)
+  SPK_TIE_CASE(23, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, a12, a13, a14, a15, a16,
+               a17, a18, a19, a20, a21, a22)
+  SPK_TIE_CASE(24, a0, a1, a2, a3, a4, a5, a6, a7, a8, a9, a10, a11, a12, a13, a14, a15, a16,
+               a17, a18, a19, a20, a21, a22, a23)
+}
+#undef SPK_TIE_CASE
+
+// member types as a tuple of values (for compile-time walks)
+template <typename T>
+using members_tuple_t =
+    decltype(std::apply([](auto &...m) { return std::tuple<remove_cvref_t<decltype(m)>...>{}; },
+                        tie_members(std::declval<T &>())));
+
+template <typename T, typename F>
+constexpr void visit_members(T &obj, F &&f) {
+  std::apply([&](auto &...m) { (f(m), ...); }, tie_members(obj));
+}
+
+// ---- per-type sp_config: ADL set_sp_config(T*) or T::struct_pack_config
+// (ref type_calculate.hpp:158-172) -----------------------------------------
+template <typename T>
+concept adl_config = requires { set_sp_config(static_cast<T *>(nullptr)); };
+template <typename T>
+concept member_config = requires { T::struct_pack_config; };
+
+template <typename T>
+constexpr uint64_t type_config() {
+  if constexpr (adl_config<T>)
+    return static_cast<uint64_t>(set_sp_config(static_cast<T *>(nullptr)));
+  else if constexpr (member_config<T>)
+    return static_cast<uint64_t>(T::struct_pack_config);
+  else
+    return sp_config::DEFAULT;
+}
+
+}  // namespace spk_detail
+}  // namespace struct_pack

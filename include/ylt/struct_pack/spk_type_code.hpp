@@ -1,0 +1,249 @@
+// spk_type_code.hpp — compile-time type literal and 32-bit type code of the
+// MI355X struct_pack front end (our own implementation of the reference's
+// wire contract):
+//   type_id bytes           ref include/ylt/struct_pack/type_id.hpp:25-81
+//   get_type_literal         ref type_calculate.hpp:194-373
+//   get_size_literal         ref type_calculate.hpp:26-97
+//   code = MD5_32 & ~1       ref type_calculate.hpp:507-516, md5_constexpr.hpp
+//   is_trivial_serializable  ref reflection.hpp:851-922
+//   check_if_has_container   ref type_calculate.hpp:793-857
+// The MD5 below is a straightforward constexpr RFC 1321 implementation.
+#pragma once
+#include <array>
+#include <cstdint>
+
+#include "spk_reflect.hpp"
+
+namespace struct_pack {
+namespace spk_detail {
+
+// ---- fixed-capacity constexpr byte string ----------------------------------
+struct lit_t {
+  std::array<uint8_t, 256> d{};
+  std::size_t n = 0;
+  constexpr void push(uint8_t b) { d[n++] = b; }
+  constexpr void append(const lit_t &o) {
+    for (std::size_t i = 0; i < o.n; ++i) d[n++] = o.d[i];
+  }
+};
+
+enum : uint8_t {
+  TID_INT32 = 1, TID_UINT32 = 2, TID_INT64 = 3, TID_UINT64 = 4, TID_INT8 = 5,
+  TID_UINT8 = 6, TID_INT16 = 7, TID_UINT16 = 8, TID_BOOL = 11, TID_CHAR8 = 12,
+  TID_CHAR16 = 13, TID_CHAR32 = 14, TID_FLOAT32 = 17, TID_FLOAT64 = 18,
+  TID_STRING = 128, TID_ARRAY = 129, TID_CONTAINER = 132, TID_STRUCT = 253,
+  TID_END = 255
+};
+
+template <typename T>
+constexpr uint8_t fundamental_id() {
+  if constexpr (std::is_enum_v<T>) {
+    return fundamental_id<std::underlying_type_t<T>>();
+  } else if constexpr (std::is_same_v<T, bool>) {
+    return TID_BOOL;
+  } else if constexpr (std::is_same_v<T, char> || std::is_same_v<T, char8_t>) {
+    return TID_CHAR8;  // char is saved as unsigned (type_id.hpp:160-166)
+  } else if constexpr (std::is_same_v<T, char16_t>) {
+    return TID_CHAR16;
+  } else if constexpr (std::is_same_v<T, char32_t>) {
+    return TID_CHAR32;
+  } else if constexpr (std::is_floating_point_v<T>) {
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "long double unsupported");
+    return sizeof(T) == 4 ? TID_FLOAT32 : TID_FLOAT64;
+  } else {
+    static_assert(std::is_integral_v<T>);
+    if constexpr (std::is_signed_v<T>)
+      return sizeof(T) == 1 ? TID_INT8 : sizeof(T) == 2 ? TID_INT16
+                                       : sizeof(T) == 4 ? TID_INT32 : TID_INT64;
+    else
+      return sizeof(T) == 1 ? TID_UINT8 : sizeof(T) == 2 ? TID_UINT16
+                                        : sizeof(T) == 4 ? TID_UINT32 : TID_UINT64;
+  }
+}
+
+constexpr lit_t size_literal(std::size_t n) {
+  lit_t l;
+  while (n >= 127) {
+    l.push(static_cast<uint8_t>(n % 127 + 1));
+    n /= 127;
+  }
+  l.push(static_cast<uint8_t>(n + 129));
+  return l;
+}
+
+template <typename T>
+constexpr bool is_trivially_serializable();
+
+template <typename Tup, std::size_t... I>
+constexpr bool all_trivial(std::index_sequence<I...>) {
+  return (is_trivially_serializable<std::tuple_element_t<I, Tup>>() && ...);
+}
+
+template <typename T>
+constexpr bool is_trivially_serializable() {
+  if constexpr (is_fundamental_v<T>) {
+    return true;
+  } else if constexpr (is_std_array<T>::value) {
+    return is_trivially_serializable<typename T::value_type>();
+  } else if constexpr (is_string_v<T> || is_container_v<T>) {
+    return false;
+  } else {
+    static_assert(is_record_v<T>, "unsupported member type");
+    using M = members_tuple_t<T>;
+    return all_trivial<M>(std::make_index_sequence<std::tuple_size_v<M>>{});
+  }
+}
+
+template <typename T>
+constexpr bool has_container();
+template <typename Tup, std::size_t... I>
+constexpr bool any_container(std::index_sequence<I...>) {
+  return (has_container<std::tuple_element_t<I, Tup>>() || ...);
+}
+template <typename T>
+constexpr bool has_container() {
+  if constexpr (is_string_v<T> || is_container_v<T>)
+    return true;
+  else if constexpr (is_std_array<T>::value)
+    return has_container<typename T::value_type>();
+  else if constexpr (is_record_v<T>) {
+    using M = members_tuple_t<T>;
+    return any_container<M>(std::make_index_sequence<std::tuple_size_v<M>>{});
+  } else
+    return false;
+}
+
+// alignment_v (alignment.hpp:90-122) without alignas/pragma-pack overrides
+template <typename T>
+constexpr std::size_t alignment_of() {
+  if constexpr (is_record_v<T> && !is_trivially_serializable<T>()) {
+    using M = members_tuple_t<T>;
+    return []<std::size_t... I>(std::index_sequence<I...>) {
+      std::size_t a = 0;
+      ((a = alignment_of<std::tuple_element_t<I, M>>() > a
+                ? alignment_of<std::tuple_element_t<I, M>>() : a), ...);
+      return a;
+    }(std::make_index_sequence<std::tuple_size_v<M>>{});
+  } else {
+    return alignof(T);
+  }
+}
+
+template <typename T>
+constexpr lit_t type_literal();
+
+template <typename Tup, std::size_t... I>
+constexpr void append_members(lit_t &l, std::index_sequence<I...>) {
+  (l.append(type_literal<std::tuple_element_t<I, Tup>>()), ...);
+}
+
+template <typename T>
+constexpr lit_t type_literal() {
+  lit_t l;
+  if constexpr (is_fundamental_v<T>) {
+    l.push(fundamental_id<T>());
+  } else if constexpr (is_string_v<T>) {
+    l.push(TID_STRING);
+    l.push(TID_CHAR8);
+  } else if constexpr (is_container_v<T>) {
+    l.push(TID_CONTAINER);
+    l.append(type_literal<remove_cvref_t<typename T::value_type>>());
+  } else if constexpr (is_std_array<T>::value) {
+    l.push(TID_ARRAY);
+    l.append(type_literal<typename T::value_type>());
+    l.append(size_literal(std::tuple_size_v<T>));
+  } else {
+    static_assert(is_record_v<T>, "unsupported type");
+    using M = members_tuple_t<T>;
+    l.push(TID_STRUCT);
+    append_members<M>(l, std::make_index_sequence<std::tuple_size_v<M>>{});
+    if constexpr (is_trivially_serializable<T>()) {
+      std::size_t pack = 1;
+      [&]<std::size_t... I>(std::index_sequence<I...>) {
+        ((pack = alignment_of<std::tuple_element_t<I, M>>() > pack
+                     ? alignment_of<std::tuple_element_t<I, M>>() : pack), ...);
+      }(std::make_index_sequence<std::tuple_size_v<M>>{});
+      l.append(size_literal(pack));
+      l.append(size_literal(alignof(T)));
+    }
+    l.push(TID_END);
+  }
+  return l;
+}
+
+// ---- constexpr MD5 (RFC 1321) ------------------------------------------------
+constexpr uint32_t md5_rotl(uint32_t x, int c) { return (x << c) | (x >> (32 - c)); }
+
+constexpr std::array<uint8_t, 16> md5(const uint8_t *msg, std::size_t len) {
+  constexpr uint32_t K[64] = {
+      0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613,
+      0xfd469501, 0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193,
+      0xa679438e, 0x49b40821, 0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d,
+      0x02441453, 0xd8a1e681, 0xe7d3fbc8, 0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed,
+      0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a, 0xfffa3942, 0x8771f681, 0x6d9d6122,
+      0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70, 0x289b7ec6, 0xeaa127fa,
+      0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665, 0xf4292244,
+      0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
+      0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb,
+      0xeb86d391};
+  constexpr int R[64] = {7, 12, 17, 22, 7, 12, 17, 22, 7, 12, 17, 22, 7, 12, 17, 22,
+                         5, 9,  14, 20, 5, 9,  14, 20, 5, 9,  14, 20, 5, 9,  14, 20,
+                         4, 11, 16, 23, 4, 11, 16, 23, 4, 11, 16, 23, 4, 11, 16, 23,
+                         6, 10, 15, 21, 6, 10, 15, 21, 6, 10, 15, 21, 6, 10, 15, 21};
+  uint32_t a0 = 0x67452301, b0 = 0xefcdab89, c0 = 0x98badcfe, d0 = 0x10325476;
+  const std::size_t total = ((len + 8) / 64 + 1) * 64;
+  for (std::size_t blk = 0; blk < total; blk += 64) {
+    uint32_t M[16] = {};
+    for (int i = 0; i < 64; ++i) {
+      const std::size_t idx = blk + i;
+      uint8_t b = 0;
+      if (idx < len)
+        b = msg[idx];
+      else if (idx == len)
+        b = 0x80;
+      else if (idx >= total - 8)
+        b = static_cast<uint8_t>((static_cast<uint64_t>(len) * 8) >> (8 * (idx - (total - 8))));
+      M[i / 4] |= static_cast<uint32_t>(b) << (8 * (i % 4));
+    }
+    uint32_t A = a0, B = b0, C = c0, D = d0;
+    for (int i = 0; i < 64; ++i) {
+      uint32_t F;
+      int g;
+      if (i < 16) { F = (B & C) | (~B & D); g = i; }
+      else if (i < 32) { F = (D & B) | (~D & C); g = (5 * i + 1) % 16; }
+      else if (i < 48) { F = B ^ C ^ D; g = (3 * i + 5) % 16; }
+      else { F = C ^ (B | ~D); g = (7 * i) % 16; }
+      F = F + A + K[i] + M[g];
+      A = D;
+      D = C;
+      C = B;
+      B = B + md5_rotl(F, R[i]);
+    }
+    a0 += A; b0 += B; c0 += C; d0 += D;
+  }
+  std::array<uint8_t, 16> out{};
+  const uint32_t h[4] = {a0, b0, c0, d0};
+  for (int i = 0; i < 16; ++i) out[i] = static_cast<uint8_t>(h[i / 4] >> (8 * (i % 4)));
+  return out;
+}
+
+// MD5Hash32Constexpr: the first four digest bytes read big-endian
+constexpr uint32_t md5_hash32(const lit_t &l) {
+  const auto d = md5(l.d.data(), l.n);
+  return (static_cast<uint32_t>(d[0]) << 24) | (static_cast<uint32_t>(d[1]) << 16) |
+         (static_cast<uint32_t>(d[2]) << 8) | static_cast<uint32_t>(d[3]);
+}
+
+}  // namespace spk_detail
+
+// Public: get_type_literal / get_type_code of one type (struct_pack.hpp:75-110)
+template <typename T>
+constexpr auto get_type_literal() {
+  return spk_detail::type_literal<spk_detail::remove_cvref_t<T>>();
+}
+template <typename T>
+constexpr uint32_t get_type_code() {
+  return spk_detail::md5_hash32(get_type_literal<T>()) & 0xFFFFFFFEu;
+}
+
+}  // namespace struct_pack

@@ -1,0 +1,32 @@
+"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes per kernel.
+
+Units: rocprofv3 reports FETCH_SIZE / WRITE_SIZE in KiB per dispatch. On
+gfx950 FETCH_SIZE reads exactly half the bytes of a wide coalesced streaming
+read (MI355X_MICROARCH.md §HBM), so the corrected read bytes are 2x; WRITE_SIZE
+is exact for 16-B-per-lane streaming stores."""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
+out = {}
+for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+    files = glob.glob(f"gpurun_out/pmc_{cfg}_{ctr}/**/*counter_collection.csv", recursive=True)
+    acc = defaultdict(list)
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") == ctr:
+                acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    for k, v in acc.items():
+        out.setdefault(k, {})[ctr + "_KiB_avg"] = sum(v) / len(v)
+        out[k]["dispatches"] = len(v)
+res = {}
+for k, v in out.items():
+    if "FETCH_SIZE_KiB_avg" in v and "WRITE_SIZE_KiB_avg" in v:
+        rd = v["FETCH_SIZE_KiB_avg"] * 1024
+        wr = v["WRITE_SIZE_KiB_avg"] * 1024
+        res[k[:90]] = {"fetch_bytes_raw": rd, "fetch_bytes_x2": 2 * rd, "write_bytes": wr,
+                       "hbm_bytes_per_launch": 2 * rd + wr, "dispatches": v["dispatches"]}
+print(json.dumps(res, indent=1))

@@ -1,0 +1,125 @@
+// GPU: the C++20 front end end-to-end through the HIP codec, checked against
+// the REFERENCE's own bytes (tests/golden/*.bin written by golden_gen built
+// from /root/reference). Reads like the reference's doctest suites
+// (src/struct_pack/tests/test_serialize.cpp): serialize -> compare bytes,
+// deserialize -> compare objects, truncated / corrupted buffers -> errc.
+#include <cstdio>
+#include <fstream>
+#include <iterator>
+#include <string>
+#include <vector>
+
+#include "ylt/struct_pack.hpp"
+#include "../../oracle/ref/types.hpp"
+
+using namespace struct_pack;
+static int g_fail = 0, g_checks = 0;
+#define CHECK(c)                                                        \
+  do {                                                                  \
+    ++g_checks;                                                         \
+    if (!(c)) {                                                         \
+      ++g_fail;                                                         \
+      std::fprintf(stderr, "%s:%d: CHECK(%s) failed\n", __FILE__, __LINE__, #c); \
+    }                                                                   \
+  } while (0)
+
+static std::string golden(const std::string &name) {
+  std::ifstream f(std::string(SPK_GOLDEN_DIR) + "/" + name, std::ios::binary);
+  return std::string((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+}
+static std::vector<uint64_t> golden_lens(const std::string &name) {
+  std::string b = golden(name);
+  std::vector<uint64_t> v(b.size() / 8);
+  std::memcpy(v.data(), b.data(), b.size());
+  return v;
+}
+
+bool operator==(const Rec64 &a, const Rec64 &b) { return std::memcmp(&a, &b, sizeof a) == 0; }
+bool operator==(const RecS &a, const RecS &b) { return a.id == b.id && a.name == b.name && a.v == b.v; }
+bool operator==(const Inner &a, const Inner &b) { return a.x == b.x && a.y == b.y; }
+bool operator==(const Outer &a, const Outer &b) { return a.key == b.key && a.items == b.items; }
+namespace rpcb {
+bool operator==(const person &a, const person &b) {
+  return a.id == b.id && a.name == b.name && a.age == b.age && a.salary == b.salary;
+}
+}  // namespace rpcb
+
+template <typename T, typename Gen>
+static void roundtrip_vector(const char *fixture, std::size_t n, Gen gen) {
+  std::vector<T> v(n);
+  for (std::size_t i = 0; i < n; ++i) gen(v[i], i);
+  const std::string want = golden(fixture);
+  CHECK(!want.empty());
+  auto sz = get_needed_size(v);
+  CHECK(sz.size() == want.size());
+  auto bytes = serialize<sp_config::DEFAULT, std::string>(v);
+  CHECK(bytes == want);
+  std::vector<T> back;
+  std::size_t consumed = 0;
+  auto ec = deserialize_to(back, want.data(), want.size(), consumed);
+  CHECK(!ec);
+  CHECK(consumed == want.size());
+  CHECK(back == v);
+  // truncation: the reference reports no_buffer_space (test_serialize.cpp:816-845)
+  if (want.size() > 5) {
+    std::vector<T> t;
+    auto e2 = deserialize_to(t, want.data(), want.size() - 1);
+    CHECK(e2.ec == errc::no_buffer_space);
+  }
+  // hash mismatch -> invalid_buffer (test_serialize.cpp:529-547)
+  std::string bad = want;
+  bad[1] ^= 0x40;
+  std::vector<T> t2;
+  CHECK(deserialize_to(t2, bad.data(), bad.size()).ec == errc::invalid_buffer);
+  auto r = deserialize<std::vector<T>>(want.data(), want.size());
+  CHECK(r.has_value() && r.value() == v);
+}
+
+template <typename T, typename Gen>
+static void roundtrip_messages(const char *fixture, const char *lens, std::size_t n, Gen gen) {
+  std::vector<T> v(n);
+  for (std::size_t i = 0; i < n; ++i) gen(v[i], i);
+  const std::string want = golden(fixture);
+  std::vector<uint64_t> offs;
+  auto bytes = serialize_messages(v, offs);
+  CHECK(std::string(bytes.begin(), bytes.end()) == want);
+  auto l = golden_lens(lens);
+  CHECK(offs.size() == n + 1);
+  for (std::size_t i = 0; i < n && i < l.size(); ++i) CHECK(offs[i + 1] - offs[i] == l[i]);
+  std::vector<T> back;
+  auto errs = deserialize_messages(back, want.data(), want.size(), offs);
+  bool all_ok = true;
+  for (auto &e : errs) all_ok &= !e;
+  CHECK(all_ok);
+  CHECK(back == v);
+}
+
+int main() {
+  using namespace spk_gold;
+  const uint64_t S2 = 0x5EED0002, S3 = 0x5EED0003, S4 = 0x5EED0004, S8 = 0x5EED0008;
+  roundtrip_vector<Rec64>("rec64_A_n1000_p0_default.bin", 1000,
+                          [&](Rec64 &o, uint64_t i) { o = make_rec64(S2, i); });
+  roundtrip_vector<Rec64>("rec64_A_n255_p0_default.bin", 255,
+                          [&](Rec64 &o, uint64_t i) { o = make_rec64(S2, i); });
+  roundtrip_vector<RecS>("recs_A_n300_p48_default.bin", 300,
+                         [&](RecS &o, uint64_t i) { o = make_recs(S3, i, 48); });
+  roundtrip_vector<RecS>("recs_A_n40_p300_default.bin", 40,
+                         [&](RecS &o, uint64_t i) { o = make_recs(S3, i, 300); });
+  roundtrip_vector<Outer>("outer_A_n1000_p16_default.bin", 1000,
+                          [&](Outer &o, uint64_t i) { o = make_outer(S4, i, 16); });
+  roundtrip_vector<rpcb::person>("person_A_n100_p64_default.bin", 100,
+                                 [&](rpcb::person &o, uint64_t i) { o = make_person(S8, i, 64); });
+  // C1: benchmark rect<int> with ADL DISABLE_ALL_META_INFO (16,003 B)
+  {
+    std::vector<rect<int>> v(1000);
+    auto bytes = serialize<sp_config::DEFAULT, std::string>(v);
+    CHECK(bytes == golden("rect_A_n1000_p0_default.bin"));
+    CHECK(bytes.size() == 16003);
+  }
+  roundtrip_messages<RecS>("recs_B_n500_p300_default.bin", "recs_B_n500_p300_default.lens", 500,
+                           [&](RecS &o, uint64_t i) { o = make_recs(S3, i, 300); });
+  roundtrip_messages<Rec64>("rec64_B_n300_p0_default.bin", "rec64_B_n300_p0_default.lens", 300,
+                            [&](Rec64 &o, uint64_t i) { o = make_rec64(S2, i); });
+  std::printf("{\"checks\": %d, \"failures\": %d}\n", g_checks, g_fail);
+  return g_fail ? 1 : 0;
+}

@@ -1,0 +1,91 @@
+// CPU: the C++20 front end's compile-time type codes / literals and the
+// descriptors it emits (no HIP needed). Prints JSON compared by
+// tests/test_cpp_frontend.py against tests/golden/kat.json (reference KATs)
+// and yalantinglibs_amd/layout.py (Python mirror).
+#include <cstdio>
+#include <string>
+
+#include "ylt/struct_pack/spk_layout.hpp"
+#include "../../oracle/ref/types.hpp"
+
+using namespace struct_pack;
+
+// compile-time checks against the reference's KATs
+static_assert(get_type_code<Rec64>() == 0xd3e789e0u);
+static_assert(get_type_code<std::vector<Rec64>>() == 0xfe16d1dau);
+static_assert(get_type_code<RecS>() == 0xb7ce112eu);
+static_assert(get_type_code<std::vector<RecS>>() == 0xd2c6fa72u);
+static_assert(get_type_code<std::vector<Outer>>() == 0xfea939d6u);
+static_assert(get_type_code<rect<int>>() == 0x5d2be0aau);
+static_assert(get_type_code<std::vector<rect<int>>>() == 0xe8fa8a7cu);
+static_assert(spk_detail::is_trivially_serializable<Rec64>());
+static_assert(!spk_detail::is_trivially_serializable<RecS>());
+static_assert(spk_detail::members_count_v<Mixed> == 5);
+
+template <typename T>
+static void lit_json(const char *name, bool &first) {
+  constexpr auto l = get_type_literal<T>();
+  printf("%s\"%s\": {\"code\": %u, \"literal\": \"", first ? "" : ",\n", name,
+         get_type_code<T>());
+  for (std::size_t i = 0; i < l.n; ++i) printf("%02x", l.d[i]);
+  printf("\"}");
+  first = false;
+}
+
+template <typename T, uint64_t conf = sp_config::DEFAULT>
+static void layout_json(const char *name, bool &first) {
+  spk_layout L = make_spk_layout<T, conf>();
+  printf("%s\"%s\": {\"flags\": %u, \"stride\": %u, \"ops\": [", first ? "" : ",\n", name,
+         L.flags, L.rec_stride);
+  for (uint32_t i = 0; i < L.n_ops; ++i)
+    printf("%s[%u, %u, %u, %u]", i ? ", " : "", L.ops[i].kind, L.ops[i].rec_off, L.ops[i].size,
+           L.ops[i].aux);
+  printf("], \"vec\": [%u, %u, %u], \"one\": [%u, %u, %u]}", L.fmt_vector.code,
+         L.fmt_vector.flags, L.fmt_vector.literal_len, L.fmt_one.code, L.fmt_one.flags,
+         L.fmt_one.literal_len);
+  first = false;
+}
+
+int main() {
+  bool first = true;
+  printf("{\"kat\": {\n");
+  lit_json<Rec64>("Rec64", first);
+  lit_json<std::vector<Rec64>>("vector<Rec64>", first);
+  lit_json<RecS>("RecS", first);
+  lit_json<std::vector<RecS>>("vector<RecS>", first);
+  lit_json<Inner>("Inner", first);
+  lit_json<Outer>("Outer", first);
+  lit_json<std::vector<Outer>>("vector<Outer>", first);
+  lit_json<Pad>("Pad", first);
+  lit_json<std::vector<Pad>>("vector<Pad>", first);
+  lit_json<Mixed>("Mixed", first);
+  lit_json<std::vector<Mixed>>("vector<Mixed>", first);
+  lit_json<rect<int>>("rect<int>", first);
+  lit_json<std::vector<rect<int>>>("vector<rect<int>>", first);
+  lit_json<rpcb::point>("rpc::point", first);
+  lit_json<rpcb::rect>("rpc::rect", first);
+  lit_json<std::vector<rpcb::rect>>("vector<rpc::rect>", first);
+  lit_json<rpcb::person>("person", first);
+  lit_json<std::vector<rpcb::person>>("vector<person>", first);
+  lit_json<std::vector<int32_t>>("vector<int32_t>", first);
+  lit_json<std::string>("string", first);
+  lit_json<int32_t>("int32_t", first);
+  lit_json<rpcb::req_header>("req_header", first);
+  lit_json<rpcb::resp_header>("resp_header", first);
+  lit_json<std::array<int16_t, 3>>("array<int16_t,3>", first);
+  printf("},\n\"layout\": {\n");
+  first = true;
+  layout_json<Rec64>("rec64", first);
+  layout_json<RecS>("recs", first);
+  layout_json<Outer>("outer", first);
+  layout_json<Pad>("pad", first);
+  layout_json<Mixed>("mixed", first);
+  layout_json<rect<int>>("rect", first);
+  layout_json<rpcb::rect>("rpcrect", first);
+  layout_json<rpcb::person>("person", first);
+  layout_json<std::vector<int32_t>>("ints", first);
+  layout_json<RecS, sp_config::ENABLE_TYPE_INFO>("recs_typeinfo", first);
+  layout_json<Rec64, sp_config::DISABLE_ALL_META_INFO>("rec64_nometa", first);
+  printf("}}\n");
+  return 0;
+}

@@ -1,0 +1,53 @@
+"""CPU: the C++20 front end (include/ylt/struct_pack.hpp and friends).
+
+Compiles tests/cpp/test_type_code.cpp host-only (it static_asserts the
+reference's type-code KATs at compile time) and checks its JSON against the
+reference's KATs (tests/golden/kat.json) and the Python mirror's
+descriptors (yalantinglibs_amd/layout.py): both front ends must hand the
+C ABI identical descriptors."""
+import json
+import os
+import subprocess
+
+import pytest
+
+import spk_helpers as H
+from yalantinglibs_amd import layout as LY
+from yalantinglibs_amd import schema as S
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLANG = "/opt/rocm/llvm/bin/clang++"
+
+
+@pytest.fixture(scope="module")
+def cpp_json(tmp_path_factory):
+    if not os.path.exists(CLANG):
+        pytest.skip("clang++ not available")
+    exe = str(tmp_path_factory.mktemp("cpp") / "ttc")
+    subprocess.run([CLANG, "-std=c++20", "-O1", "-DNDEBUG", "-I", os.path.join(ROOT, "include"),
+                    "-o", exe, os.path.join(ROOT, "tests", "cpp", "test_type_code.cpp")],
+                   check=True)
+    return json.loads(subprocess.run([exe], check=True, capture_output=True, text=True).stdout)
+
+
+def test_cpp_type_codes_match_reference_kats(cpp_json):
+    kat = H.kat()
+    for name, v in cpp_json["kat"].items():
+        assert v["code"] == kat[name]["code"], name
+        assert v["literal"] == kat[name]["literal"], name
+
+
+@pytest.mark.parametrize("case,conf", [("rec64", 0), ("recs", 0), ("outer", 0), ("pad", 0),
+                                       ("mixed", 0), ("rect", 0), ("rpcrect", 0),
+                                       ("person", 0), ("ints", 0),
+                                       ("recs", S.ENABLE_TYPE_INFO),
+                                       ("rec64", S.DISABLE_ALL_META_INFO)])
+def test_cpp_and_python_descriptors_agree(cpp_json, case, conf):
+    key = case + {0: "", S.ENABLE_TYPE_INFO: "_typeinfo", S.DISABLE_ALL_META_INFO: "_nometa"}[conf]
+    c = cpp_json["layout"][key]
+    L = LY.case_layout(case, conf).c
+    assert c["flags"] == L.flags and c["stride"] == L.rec_stride
+    assert c["ops"] == [[L.ops[i].kind, L.ops[i].rec_off, L.ops[i].size, L.ops[i].aux]
+                        for i in range(L.n_ops)]
+    assert c["vec"] == [L.fmt_vector.code, L.fmt_vector.flags, L.fmt_vector.literal_len]
+    assert c["one"] == [L.fmt_one.code, L.fmt_one.flags, L.fmt_one.literal_len]
