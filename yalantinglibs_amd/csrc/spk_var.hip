@@ -572,59 +572,47 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
 }
 
 // ===========================================================================
-// DECODE, SPK_MODE_VECTOR — chunked transition functions
+// DECODE, SPK_MODE_VECTOR — speculative chunk walks
 // ===========================================================================
-// The payload is cut into kChunk-byte chunks. For every byte position p of a
-// chunk a block computes, fully in parallel, "if a record started at p, where
-// would the next one start" (one parse per position, in LDS), then pointer-
-// jumps those links in place (one packed 32-bit (next, count) word per
-// position, so asynchronous updates keep the invariant) until every position
-// knows the first record start at/after the chunk end and how many complete
-// records lie on the way. The first kK entries form the chunk's transition
-// table; tables are composed hierarchically (fan-in kGroup) to give each
-// chunk its true entry and first record index. A second pass re-derives the
-// links with 256-byte sub-chunk boundaries so 32 lanes can place the records
-// of a chunk in parallel.
-constexpr uint32_t kChunk = 8192;           // payload bytes per chunk
-constexpr uint32_t kChunkShift = 13;
-constexpr uint32_t kK = 1024;               // table entries (entry offsets) per chunk
-constexpr uint32_t kSubShift = 8;           // 256-byte sub-chunks in the start pass
-constexpr uint32_t kNSub = kChunk >> kSubShift;
-constexpr uint32_t kGroup = 64;             // composition fan-in
-constexpr uint32_t kStage = kChunk + 1024;  // bytes staged in LDS per chunk
-constexpr uint32_t kVThreads = 256;
+// Record k's start depends on every earlier length field, so the payload is
+// cut into kSpec-byte chunks and each chunk is parsed speculatively by one
+// lane, in parallel: the walk starts at the chunk's first byte (the next
+// candidate byte when the first records it would parse are implausibly long)
+// and records the positions it visits in the chunk (P list) and in the next
+// kExt records past it (E list). Chunk 0 starts at the true payload start,
+// so its walk is exact. Chunk c's walk is on the true path from the first
+// position it shares with chunk c-1's extension (E_{c-1} is the true path
+// when chunk c-1 is verified), which a second parallel pass finds by merging
+// the two sorted lists. Chunks without such a meeting point (records larger
+// than the extension window, pathological data) are re-walked in order by a
+// single fixup lane from the true position, until the path meets a
+// speculative walk again. Then per-chunk record counts are scanned into
+// record indices, one lane per chunk re-walks its true records to place
+// their starts, a device-wide scan turns span counts into heap offsets, and
+// one thread per record decodes it.
+constexpr uint32_t kSpec = 2048;       // payload bytes per speculation chunk
+constexpr uint32_t kExt = 16;          // records a spec walk continues past its chunk
+constexpr uint32_t kMaxTries = 256;    // candidate start bytes per chunk
+constexpr uint32_t kNone32 = 0xFFFFFFFFu;
 
-constexpr uint32_t kFlagIncomplete = 1u;  // a record runs past the wire end
-constexpr uint32_t kFlagTooBig = 2u;      // exit offset >= kK
-constexpr uint32_t kNoStart = 4u;         // (entries only) no record starts here
-
-// level >= 1 tables (u64): exit (16) | flags (3) << 16 | count << 32
-__host__ __device__ __forceinline__ uint64_t tpack(uint32_t exit, uint32_t flags,
-                                                   uint64_t count) {
-  return (uint64_t)(exit & 0xFFFF) | ((uint64_t)(flags & 7) << 16) | (count << 32);
-}
-// level 0 tables (u32): exit (11) | flags (2) << 11 | count << 16
-__host__ __device__ __forceinline__ uint32_t t0pack(uint32_t exit, uint32_t flags,
-                                                    uint32_t count) {
-  return (exit & 0x7FF) | ((flags & 3) << 11) | (count << 16);
-}
-__host__ __device__ __forceinline__ uint32_t t_exit(uint64_t t) { return (uint32_t)t & 0xFFFF; }
-__host__ __device__ __forceinline__ uint32_t t_flags(uint64_t t) { return (uint32_t)(t >> 16) & 7; }
-__host__ __device__ __forceinline__ uint64_t t_count(uint64_t t) { return t >> 32; }
-__host__ __device__ __forceinline__ uint32_t t_exit(uint32_t t) { return t & 0x7FF; }
-__host__ __device__ __forceinline__ uint32_t t_flags(uint32_t t) { return (t >> 11) & 3; }
-__host__ __device__ __forceinline__ uint64_t t_count(uint32_t t) { return t >> 16; }
+// per-chunk verification flags
+constexpr uint32_t kOk = 1u;           // true records of the chunk are known
+constexpr uint32_t kTerm = 2u;         // the true path terminates inside this chunk
+constexpr uint32_t kWalkTerm = 4u;     // the spec walk itself ended (INC / wire end)
 
 struct VCtl {
   uint64_t p0;       // payload start (after header + count)
   uint64_t n;        // record count from the header
-  uint64_t nchunks;  // chunks covering [p0, wire_len) (0 if n == 0)
+  uint64_t nchunks;  // chunks covering [p0, wire_len)
   uint64_t data_len;
   unsigned long long end_pos;  // absolute end of record n-1
+  unsigned long long total;    // complete records on the true path
   uint32_t w;
-  int32_t errc;  // header errc
-  uint32_t need_fallback;
-  uint32_t pad;
+  int32_t errc;      // header errc
+  uint32_t lp;       // P-list capacity per chunk
+  uint32_t n_unver;  // entries in the unverified list
+  uint32_t term_chunk;  // first chunk where the true path terminates (kNone32)
+  uint32_t overflow;    // a P list overflowed (records < 1 B impossible; guard)
 };
 
 // Compact walk program of a record: fixed bytes, then per span
@@ -651,54 +639,31 @@ static WalkProg make_walkprog(const spk_layout *L) {
   return p;
 }
 
-// LDS pointers carry address space 3 so reads lower to ds_read_u8, not
-// flat_load_ubyte (a generic pointer would go through the flat path).
-typedef __attribute__((address_space(3))) const uint8_t lds_cu8;
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef uint32_t u32_unaligned __attribute__((aligned(1)));
+typedef uint64_t u64_unaligned __attribute__((aligned(1)));
 
-struct StagedReader {  // bytes [base, base+kStage) from LDS, others from HBM
-  lds_cu8 *lds;
-  const uint8_t *wire;
-  uint64_t base;
-  __device__ __forceinline__ uint8_t operator()(uint64_t x) const {
-    const uint64_t r = x - base;
-    if (r < kStage) return lds[r];
-    return wire[x];
+// little-endian w-byte count at wire[x] (x + w <= len checked by the caller)
+__device__ __forceinline__ uint64_t wire_le(const uint8_t *wire, uint64_t x, uint32_t w) {
+  switch (w) {
+    case 1: return wire[x];
+    case 2: return (uint64_t)wire[x] | ((uint64_t)wire[x + 1] << 8);
+    case 4: return *reinterpret_cast<const u32_unaligned *>(wire + x);
+    default: return *reinterpret_cast<const u64_unaligned *>(wire + x);
   }
-};
-__device__ __forceinline__ lds_cu8 *as_lds(const uint8_t *p) {
-  return (lds_cu8 *)(p);
-}
-struct GlobalReader {
-  const uint8_t *wire;
-  __device__ __forceinline__ uint8_t operator()(uint64_t x) const { return wire[x]; }
-};
-
-template <class Rd>
-__device__ __forceinline__ uint64_t rd_le(const Rd &rd, uint64_t x, uint32_t w) {
-  uint64_t v = rd(x);
-  if (w > 1) v |= (uint64_t)rd(x + 1) << 8;
-  if (w > 2) {
-    v |= (uint64_t)rd(x + 2) << 16;
-    v |= (uint64_t)rd(x + 3) << 24;
-  }
-  if (w > 4)
-    for (uint32_t i = 4; i < 8; ++i) v |= (uint64_t)rd(x + i) << (8 * i);
-  return v;
 }
 
 // Wire length of the record at `pos` (0 = incomplete: the reference fails it
 // with no_buffer_space). NS > 0: compile-time span count.
-template <int NS, class Rd>
-__device__ __forceinline__ uint64_t wlen(const WalkProg &P, const Rd &rd, uint64_t len,
-                                         uint64_t pos, uint32_t w, uint64_t *acc) {
+template <int NS>
+__device__ __forceinline__ uint64_t wlen(const WalkProg &P, const uint8_t *wire, uint64_t len,
+                                         uint64_t pos, uint32_t w, uint32_t *cnt) {
   uint64_t p = pos + P.skip[0];
   const uint32_t ns = NS > 0 ? (uint32_t)NS : P.ns;
 #pragma unroll
   for (uint32_t k = 0; k < (NS > 0 ? (uint32_t)NS : SPK_MAX_SPANS); ++k) {
     if (NS == 0 && k >= ns) break;
     if (p + w > len) return 0;
-    const uint64_t c = rd_le(rd, p, w);
+    const uint64_t c = wire_le(wire, p, w);
     p += w;
     if (c) {
       if (P.esz[k] > 1 && c > ~0ull / P.esz[k]) return 0;
@@ -706,88 +671,15 @@ __device__ __forceinline__ uint64_t wlen(const WalkProg &P, const Rd &rd, uint64
       if (nb > len - p) return 0;
       p += nb;
     }
-    if (acc) acc[k] += c;
+    if (cnt) cnt[k] = (uint32_t)c;  // device records hold u32 counts
     p += P.skip[k + 1];
   }
   if (p > len) return 0;
   return p - pos;
 }
 
-__device__ __forceinline__ void stage_chunk(uint8_t *stage, const uint8_t *wire, uint64_t cs,
-                                            uint64_t wire_len) {
-  typedef uint32_t u32_unaligned __attribute__((aligned(1)));
-  uint32_t *st32 = reinterpret_cast<uint32_t *>(stage);
-  for (uint32_t x = threadIdx.x; x < kStage / 4; x += blockDim.x) {
-    const uint64_t a = cs + 4ull * x;
-    uint32_t v;
-    if (a + 4 <= wire_len) {
-      v = *reinterpret_cast<const u32_unaligned *>(wire + a);
-    } else {
-      v = 0;
-      for (uint32_t i = 0; i < 4; ++i)
-        if (a + i < wire_len) v |= (uint32_t)wire[a + i] << (8 * i);
-    }
-    st32[x] = v;
-  }
-}
-
-// Packed per-position state (u32): count << 16 | link, link = next position
-// (< kChunk) or terminal (bit 15) with q = first start at/after the boundary
-// (bits 0-13, clamped to 16383) and bit 14 = incomplete record.
-constexpr uint32_t kTerm = 0x8000u, kInc = 0x4000u, kQMask = 0x3FFFu;
-
-constexpr uint32_t kPPT = kChunk / kVThreads;  // positions per thread (32)
-
-// Each thread owns positions p = tid + 256*j (j < 32) and keeps their
-// states in registers, so every jump round issues 32 independent LDS loads
-// back to back instead of a dependent load chain per position.
-template <int NS>
-__device__ void build_links(uint32_t *S, const WalkProg &P, const uint8_t *stage,
-                            const uint8_t *wire, uint64_t cs, uint64_t wire_len, uint32_t w,
-                            uint32_t sh) {
-  const StagedReader rd{as_lds(stage), wire, cs};
-#pragma unroll 4
-  for (uint32_t j = 0; j < kPPT; ++j) {
-    const uint32_t p = threadIdx.x + j * kVThreads;
-    uint32_t v;
-    if (cs + p >= wire_len) {
-      v = kTerm | p;  // wire end: no record here
-    } else {
-      const uint64_t L = wlen<NS>(P, rd, wire_len, cs + p, w, (uint64_t *)nullptr);
-      if (!L) {
-        v = kTerm | kInc | p;
-      } else {
-        const uint64_t q = p + L;
-        const uint64_t bnd = (uint64_t)((p >> sh) + 1) << sh;
-        v = (1u << 16) | (q >= bnd ? (kTerm | (uint32_t)(q < kQMask ? q : kQMask))
-                                   : (uint32_t)q);
-      }
-    }
-    S[p] = v;
-  }
-  __syncthreads();
-  uint32_t st[kPPT];
-#pragma unroll
-  for (uint32_t j = 0; j < kPPT; ++j) st[j] = S[threadIdx.x + j * kVThreads];
-  for (;;) {
-    uint32_t u[kPPT];
-#pragma unroll
-    for (uint32_t j = 0; j < kPPT; ++j) u[j] = (st[j] & kTerm) ? 0u : S[st[j] & 0x7FFF];
-    bool more = false;
-#pragma unroll
-    for (uint32_t j = 0; j < kPPT; ++j) {
-      if (!(st[j] & kTerm)) {
-        st[j] = (u[j] & 0xFFFF) | (((st[j] >> 16) + (u[j] >> 16)) << 16);
-        S[threadIdx.x + j * kVThreads] = st[j];
-        more |= !(u[j] & kTerm);
-      }
-    }
-    if (!__syncthreads_or(more)) break;
-  }
-}
-
 __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
-                               uint8_t *__restrict__ ws, spk_dresult_t *res) {
+                               uint8_t *__restrict__ ws, spk_dresult_t *res, uint32_t lp) {
   if (threadIdx.x != 0) return;
   VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
   uint64_t pos, dl;
@@ -814,10 +706,14 @@ __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
   c->w = w;
   c->errc = e;
   c->data_len = dl;
-  c->end_pos = 0;  // set by the lane that places record n-1
-  c->need_fallback = 0;
+  c->end_pos = 0;
+  c->total = 0;
+  c->lp = lp;
+  c->n_unver = 0;
+  c->term_chunk = kNone32;
+  c->overflow = 0;
   const uint64_t payload = (!e && a.wire_len > pos) ? a.wire_len - pos : 0;
-  c->nchunks = (c->n == 0) ? 0 : (payload + kChunk - 1) / kChunk;
+  c->nchunks = (c->n == 0) ? 0 : (payload + kSpec - 1) / kSpec;
   spk_dresult_t r = {};
   r.errc = e;
   r.width = w;
@@ -825,213 +721,343 @@ __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
   *res = r;
 }
 
-// per chunk: transition table for entry offsets [0, kK)
+struct VecBufs {
+  uint16_t *P;      // [nchunks][lp]   positions in the chunk (rel. chunk start)
+  uint32_t *Pn;     // [nchunks]
+  uint32_t *E;      // [nchunks][kExt] positions past the chunk (rel. chunk start)
+  uint32_t *En;     // [nchunks]
+  uint32_t *flags;  // [nchunks]
+  uint64_t *T;      // [nchunks] first true record start >= chunk start (abs), ~0 none
+  uint32_t *cnt;    // [nchunks] complete true records starting in the chunk
+  uint64_t *base;   // [nchunks] index of the chunk's first true record
+  uint32_t *unver;  // [nchunks] chunks still dirty after the parallel rounds
+  uint64_t *exitp;  // [nchunks] true exit of the chunk (first start past it)
+  uint64_t *used;   // [nchunks] entry the chunk was last verified with
+  uint32_t *dirty;  // [2][nchunks] re-verification flags (double buffered)
+  uint64_t *starts; // [rec_cap]
+  uint32_t *rcnt;   // [n_spans][rec_cap] span counts per record
+  uint64_t *hoff;   // [n_spans][rec_cap] heap element offsets per record
+  uint64_t *scan;   // block sums for the device-wide scans
+};
+
+// one lane per chunk: speculative walk
 template <int NS>
-__global__ __launch_bounds__(kVThreads) void vec_tables(DecArgs a, WalkProg P,
-                                                        const uint8_t *__restrict__ wire,
-                                                        const uint8_t *__restrict__ ws,
-                                                        uint32_t *__restrict__ table) {
-  __shared__ uint32_t S[kChunk];
-  __shared__ __align__(16) uint8_t stage[kStage];
-  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
-  const uint64_t nchunks = c->nchunks;
-  const uint32_t w = c->w;
-  for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-    const uint64_t cs = c->p0 + ch * kChunk;
-    stage_chunk(stage, wire, cs, a.wire_len);
-    __syncthreads();
-    build_links<NS>(S, P, stage, wire, cs, a.wire_len, w, kChunkShift);
-    for (uint32_t e = threadIdx.x; e < kK; e += blockDim.x) {
-      const uint32_t v = S[e];
-      const uint32_t q = v & kQMask, cnt = v >> 16;
-      uint32_t t;
-      if (v & kInc)
-        t = t0pack(0, kFlagIncomplete, cnt);
-      else if (q < kChunk)  // clean wire end inside the (last) chunk
-        t = t0pack(0, 0, cnt);
-      else if (q - kChunk >= kK || q == kQMask)
-        t = t0pack(0, kFlagTooBig, cnt);
-      else
-        t = t0pack(q - kChunk, 0, cnt);
-      table[ch * kK + e] = t;
-    }
-    __syncthreads();
-  }
-}
-
-// up-sweep: out[g][e] = T[g*G+G-1] o ... o T[g*G] (e)
-template <typename TIn>
-__global__ __launch_bounds__(256) void vec_compose_up(const TIn *__restrict__ in,
-                                                      uint64_t n_in,
-                                                      uint64_t *__restrict__ out) {
-  const uint64_t g = blockIdx.x;
-  for (uint32_t e0 = threadIdx.x; e0 < kK; e0 += blockDim.x) {
-    uint32_t e = e0, fl = 0;
-    uint64_t cnt = 0;
-    for (uint64_t j = g * kGroup; j < n_in && j < (g + 1) * kGroup; ++j) {
-      const TIn t = in[j * kK + e];
-      cnt += t_count(t);
-      if (t_flags(t)) {
-        fl = t_flags(t);
-        break;
-      }
-      e = t_exit(t);
-    }
-    out[g * kK + e0] = tpack(e, fl, cnt);
-  }
-}
-
-// down-sweep: entry/base of each group -> entry/base of each member.
-// Entries are (offset | flags << 16); a flagged entry propagates unchanged.
-template <typename TIn>
-__global__ void vec_compose_down(const TIn *__restrict__ tab, uint64_t n_in,
-                                 uint64_t n_groups, const uint32_t *__restrict__ g_entry,
-                                 const uint64_t *__restrict__ g_base,
-                                 uint32_t *__restrict__ m_entry,
-                                 uint64_t *__restrict__ m_base) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n_groups) return;
-  uint32_t ent = g_entry[g];
-  uint64_t base = g_base[g];
-  for (uint64_t j = g * kGroup; j < n_in && j < (g + 1) * kGroup; ++j) {
-    m_entry[j] = ent;
-    m_base[j] = base;
-    if (ent >> 16) continue;
-    const TIn t = tab[j * kK + ent];
-    base += t_count(t);
-    ent = t_flags(t) ? (t_flags(t) << 16) : t_exit(t);
-  }
-}
-
-// TooBig before record n: records straddle chunk boundaries by >= kK bytes;
-// request the sequential fallback.
-__global__ void vec_check_entries(uint8_t *__restrict__ ws,
-                                  const uint32_t *__restrict__ m_entry,
-                                  const uint64_t *__restrict__ m_base) {
+__global__ __launch_bounds__(256) void vec_spec(DecArgs a, WalkProg P,
+                                                const uint8_t *__restrict__ wire,
+                                                uint8_t *__restrict__ ws, VecBufs B) {
   VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
   const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= c->nchunks || c->errc) return;
-  if (m_base[ch] < c->n && ((m_entry[ch] >> 16) & kFlagTooBig)) c->need_fallback = 1;
+  if (ch >= c->nchunks) return;
+  const uint32_t w = c->w, lp = c->lp;
+  const uint64_t len = a.wire_len;
+  const uint64_t cs = c->p0 + ch * kSpec;
+  const uint64_t ce = cs + kSpec < len ? cs + kSpec : len;
+  uint16_t *Pl = B.P + ch * lp;
+  uint32_t *El = B.E + ch * kExt;
+  uint32_t np = 0, ne = 0, fl = 0;
+  const uint32_t tries = ch == 0 ? 1 : kMaxTries;
+  for (uint32_t t = 0; t < tries; ++t) {
+    uint64_t x = cs + t;
+    if (x >= ce) break;
+    np = ne = fl = 0;
+    bool ok = true;
+    for (;;) {
+      if (x >= ce && ne == kExt) break;
+      const uint64_t L = x < len ? wlen<NS>(P, wire, len, x, w, (uint32_t *)nullptr) : 0;
+      // inside the chunk, a speculative walk (chunk > 0) that meets an
+      // implausible record -- longer than the chunk, or incomplete before
+      // the wire end -- started off the record grid: restart one byte on
+      if (ch != 0 && x < ce && ((L == 0 && x < len) || L > kSpec)) {
+        ok = false;
+        break;
+      }
+      if (x < ce) {
+        if (np < lp) Pl[np] = (uint16_t)(x - cs);
+        ++np;
+      } else {
+        El[ne++] = (x - cs) < 0xFFFFFFFFull ? (uint32_t)(x - cs) : 0xFFFFFFFEu;
+      }
+      if (!L) {  // incomplete record or the wire end: the walk terminates here
+        fl = kWalkTerm;
+        break;
+      }
+      x += L;
+    }
+    if (ok) break;
+    np = ne = 0;
+  }
+  if (np > lp) {
+    atomicOr(&c->overflow, 1u);
+    np = lp;
+  }
+  B.Pn[ch] = np;
+  B.En[ch] = ne;
+  B.flags[ch] = fl;
 }
 
-// Sequential fallback: one lane walks every record (global reads) and writes
-// each chunk's entry/base directly. Correct for any record size; slow.
-__global__ void vec_seq_walk(DecArgs a, WalkProg P, const uint8_t *__restrict__ wire,
-                             uint8_t *__restrict__ ws, uint32_t *__restrict__ m_entry,
-                             uint64_t *__restrict__ m_base) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
-  if (!c->need_fallback) return;
-  const GlobalReader rd{wire};
-  uint64_t pos = c->p0, rec = 0, ch = 0;
-  uint32_t flag = 0;
-  while (rec < c->n) {
-    while (ch < c->nchunks && c->p0 + (ch + 1) * kChunk <= pos) {  // chunks passed over
-      m_entry[ch] = kNoStart << 16;
-      m_base[ch] = rec;
-      ++ch;
-    }
-    if (ch < c->nchunks && c->p0 + ch * kChunk <= pos) {  // first start in chunk ch
-      m_entry[ch] = (uint32_t)(pos - (c->p0 + ch * kChunk));
-      m_base[ch] = rec;
-      ++ch;
-    }
-    const uint64_t rl = wlen<0>(P, rd, a.wire_len, pos, c->w, (uint64_t *)nullptr);
-    if (!rl) {
-      flag = kFlagIncomplete;
+constexpr uint64_t kTermPos = ~0ull;  // "the true path ended before this chunk"
+constexpr int kRounds = 6;            // parallel re-verification rounds
+
+// Walk the true path of chunk `ch` from `entry` until it meets the chunk's
+// speculative walk (two-pointer merge against the sorted P list) or leaves
+// the chunk. Returns the chunk's exit (first true start past it, or
+// kTermPos when the path ends inside) and its complete-record count.
+template <int NS>
+__device__ void walk_chunk(const DecArgs &a, const WalkProg &P, const uint8_t *wire,
+                           const VCtl *c, const VecBufs &B, uint64_t ch, uint64_t entry,
+                           uint64_t *exit, uint32_t *count, uint32_t *flags, uint64_t *T) {
+  const uint64_t len = a.wire_len;
+  const uint64_t cs = c->p0 + ch * kSpec;
+  const uint64_t ce = cs + kSpec < len ? cs + kSpec : len;
+  const uint16_t *Pl = B.P + ch * c->lp;
+  const uint32_t np = B.Pn[ch], en = B.En[ch];
+  const bool walk_term = B.flags[ch] & kWalkTerm;
+  *T = entry < ce ? entry : ~0ull;
+  uint32_t fl = B.flags[ch] & kWalkTerm;
+  if (entry == kTermPos) {
+    *exit = kTermPos;
+    *count = 0;
+    *flags = fl | kOk;
+    *T = ~0ull;
+    return;
+  }
+  uint32_t j = 0, k = 0;
+  uint64_t pos = entry;
+  bool merged = false, term = false;
+  while (pos < ce) {
+    while (j < np && cs + Pl[j] < pos) ++j;
+    if (j < np && cs + Pl[j] == pos) {
+      merged = true;
       break;
     }
-    pos += rl;
-    ++rec;
+    const uint64_t L = pos < len ? wlen<NS>(P, wire, len, pos, c->w, (uint32_t *)nullptr) : 0;
+    if (!L) {
+      term = true;
+      break;
+    }
+    ++k;
+    pos += L;
   }
-  for (; ch < c->nchunks; ++ch) {
-    m_entry[ch] = (flag ? kFlagIncomplete : kNoStart) << 16;
-    m_base[ch] = rec;
+  if (merged) {
+    k += np - j;
+    if (walk_term && en == 0) {  // the merged walk ends inside this chunk
+      k -= 1;
+      term = true;
+    }
+  }
+  if (term) {
+    *exit = kTermPos;
+    fl |= kTerm;
+  } else if (merged) {
+    *exit = cs + B.E[ch * kExt];  // E lists are relative to the chunk start
+  } else {
+    *exit = pos;
+  }
+  *count = k;
+  *flags = fl | kOk;
+}
+
+// flag chunk x for the next round; after the last round, also list it
+// (once) for the sequential fixup
+__device__ __forceinline__ void mark_dirty(VCtl *c, const VecBufs &B, uint32_t *dirty_out,
+                                           uint64_t x, int last) {
+  if (atomicExch(&dirty_out[x], 1u) == 0u && last) {
+    const uint32_t slot = atomicAdd(&c->n_unver, 1u);
+    B.unver[slot] = (uint32_t)x;
   }
 }
 
-// Start pass, block per chunk with a known entry: sub-chunk links, thread 0
-// chains the 32 sub-chunk entries, then one lane per sub-chunk places its
-// records (starts[]), sums span counts, and detects a short payload / the
-// end of record n-1.
+// Round r of the verification: round 0 processes every chunk with the
+// optimistic entry E_{c-1}[0]; later rounds only chunks whose entry changed
+// (dirty_in), once their predecessor is final. A chunk whose exit differs
+// from the entry its successor last used marks the successor dirty.
 template <int NS>
-__global__ __launch_bounds__(kVThreads) void vec_starts(
-    DecArgs a, WalkProg P, const uint8_t *__restrict__ wire, uint8_t *__restrict__ ws,
-    const uint32_t *__restrict__ m_entry, const uint64_t *__restrict__ m_base,
-    uint64_t *__restrict__ starts, uint64_t *__restrict__ csum, spk_dresult_t *res) {
-  __shared__ uint32_t S[kChunk];
-  __shared__ __align__(16) uint8_t stage[kStage];
-  __shared__ uint32_t sub_ent[kNSub], sub_base[kNSub];
-  __shared__ uint64_t red[kVThreads / 64];
+__global__ __launch_bounds__(256) void vec_verify_round(DecArgs a, WalkProg P,
+                                                        const uint8_t *__restrict__ wire,
+                                                        uint8_t *__restrict__ ws, VecBufs B,
+                                                        int round, const uint32_t *dirty_in,
+                                                        uint32_t *dirty_out, int last) {
+  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
+  const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nch = c->nchunks;
+  if (ch >= nch) return;
+  uint64_t entry;
+  if (round == 0) {
+    if (ch == 0)
+      entry = c->p0;
+    else
+      entry = B.En[ch - 1] ? c->p0 + (ch - 1) * kSpec + B.E[(ch - 1) * kExt] : kTermPos;
+  } else {
+    if (!dirty_in[ch]) return;
+    if (ch > 0 && dirty_in[ch - 1]) {  // predecessor not final yet
+      mark_dirty(c, B, dirty_out, ch, last);
+      return;
+    }
+    entry = B.exitp[ch - 1];
+  }
+  uint64_t exit, T;
+  uint32_t count, flags;
+  walk_chunk<NS>(a, P, wire, c, B, ch, entry, &exit, &count, &flags, &T);
+  B.used[ch] = entry;
+  B.exitp[ch] = exit;
+  B.T[ch] = T;
+  B.cnt[ch] = count;
+  B.flags[ch] = flags;
+  if (ch + 1 < nch) {
+    uint64_t next_used;
+    if (round == 0)
+      next_used = B.En[ch] ? c->p0 + ch * kSpec + B.E[ch * kExt] : kTermPos;
+    else
+      next_used = B.used[ch + 1];
+    if (exit != next_used) {
+      mark_dirty(c, B, dirty_out, ch + 1, last);
+    }
+  }
+}
+
+// last resort, single lane: chunks still dirty after kRounds, in order
+template <int NS>
+__global__ void vec_fixup(DecArgs a, WalkProg P, const uint8_t *__restrict__ wire,
+                          uint8_t *__restrict__ ws, VecBufs B) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
+  const uint32_t nu = c->n_unver;
+  if (!nu) return;
+  uint32_t first = kNone32;
+  for (uint32_t i = 0; i < nu; ++i) first = B.unver[i] < first ? B.unver[i] : first;
+  const uint64_t nch = c->nchunks;
+  // from the earliest still-dirty chunk on, propagate sequentially until the
+  // entry a chunk receives equals the one it was verified with, and no later
+  // dirty chunk remains
+  uint64_t last_dirty = 0;
+  for (uint32_t i = 0; i < nu; ++i) last_dirty = B.unver[i] > last_dirty ? B.unver[i] : last_dirty;
+  for (uint64_t ch = first; ch < nch; ++ch) {
+    const uint64_t entry = B.exitp[ch - 1];
+    if (entry == B.used[ch] && ch > last_dirty) break;
+    uint64_t exit, T;
+    uint32_t count, flags;
+    walk_chunk<NS>(a, P, wire, c, B, ch, entry, &exit, &count, &flags, &T);
+    B.used[ch] = entry;
+    B.exitp[ch] = exit;
+    B.T[ch] = T;
+    B.cnt[ch] = count;
+    B.flags[ch] = flags;
+  }
+}
+
+// first chunk where the true path terminates; zero the counts after it
+__global__ void vec_term_min(uint8_t *__restrict__ ws, const VecBufs B) {
+  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
+  const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch < c->nchunks && (B.flags[ch] & kTerm)) atomicMin(&c->term_chunk, (uint32_t)ch);
+}
+__global__ void vec_term_zero(uint8_t *__restrict__ ws, VecBufs B) {
+  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
+  const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch < c->nchunks && c->term_chunk != kNone32 && ch > c->term_chunk) B.cnt[ch] = 0;
+}
+
+// ---- device-wide exclusive scan u32 -> u64 (3 phases) ----------------------
+constexpr uint32_t kScanIPT = 16;
+constexpr uint64_t kScanBlock = 256ull * kScanIPT;
+
+__global__ __launch_bounds__(256) void scan_reduce(const uint32_t *__restrict__ in, uint64_t n,
+                                                   uint64_t *__restrict__ bsum) {
+  __shared__ uint64_t sh[4];
+  const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock;
+  uint64_t s = 0;
+  for (uint32_t j = 0; j < kScanIPT; ++j) {
+    const uint64_t i = b0 + (uint64_t)j * 256 + threadIdx.x;
+    if (i < n) s += in[i];
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) bsum[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+// exclusive scan of bsum in place; *total = sum (one block)
+__global__ __launch_bounds__(1024) void scan_blocks(uint64_t *__restrict__ bsum, uint64_t nb,
+                                                    uint64_t *__restrict__ total) {
+  __shared__ uint64_t sh[16];
+  uint64_t carry = 0;
+  for (uint64_t b0 = 0; b0 < nb; b0 += blockDim.x) {
+    const uint64_t b = b0 + threadIdx.x;
+    const uint64_t v = b < nb ? bsum[b] : 0;
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan(v, &tot, sh);
+    if (b < nb) bsum[b] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0 && total) *total = carry;
+}
+
+__global__ __launch_bounds__(256) void scan_apply(const uint32_t *__restrict__ in, uint64_t n,
+                                                  const uint64_t *__restrict__ bsum,
+                                                  uint64_t *__restrict__ out) {
+  __shared__ uint64_t sh[4];
+  // thread t handles kScanIPT consecutive elements
+  const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock;
+  const uint64_t i0 = b0 + (uint64_t)threadIdx.x * kScanIPT;
+  uint32_t v[kScanIPT];
+  uint64_t s = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kScanIPT; ++j) {
+    v[j] = i0 + j < n ? in[i0 + j] : 0;
+    s += v[j];
+  }
+  uint64_t tot;
+  uint64_t run = bsum[blockIdx.x] + block_excl_scan(s, &tot, sh);
+#pragma unroll
+  for (uint32_t j = 0; j < kScanIPT; ++j) {
+    if (i0 + j < n) out[i0 + j] = run;
+    run += v[j];
+  }
+}
+
+// total records on the true path and the short-payload check
+__global__ void vec_count_check(uint8_t *__restrict__ ws, const uint64_t *__restrict__ total,
+                                spk_dresult_t *res) {
+  if (threadIdx.x != 0) return;
   VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
   if (c->errc) return;
-  const uint64_t nchunks = c->nchunks, n = c->n;
+  c->total = *total;
+  if (c->n && *total < c->n) res->errc = SPK_ERRC_NO_BUFFER_SPACE;
+}
+
+// one lane per chunk: place the chunk's true records (index base..)
+template <int NS>
+__global__ __launch_bounds__(256) void vec_place(DecArgs a, WalkProg P,
+                                                 const uint8_t *__restrict__ wire,
+                                                 uint8_t *__restrict__ ws, VecBufs B,
+                                                 const spk_dresult_t *res) {
+  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
+  const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= c->nchunks || c->errc || res->errc) return;
+  const uint64_t n = c->n, base = B.base[ch];
+  uint32_t k = B.cnt[ch];
+  if (!k || base >= n) return;
   const uint32_t w = c->w;
-  for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-    const uint32_t ent = m_entry[ch];
-    const uint64_t base = m_base[ch];
-    if ((ent >> 16) || base >= n) continue;  // block-uniform
-    const uint64_t cs = c->p0 + ch * kChunk;
-    stage_chunk(stage, wire, cs, a.wire_len);
-    __syncthreads();
-    build_links<NS>(S, P, stage, wire, cs, a.wire_len, w, kSubShift);
-    if (threadIdx.x < kNSub) sub_ent[threadIdx.x] = 0xFFFFFFFFu;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t e = ent, k = 0;
-      while (e < kChunk) {
-        const uint32_t j = e >> kSubShift;
-        sub_ent[j] = e;
-        sub_base[j] = k;
-        const uint32_t v = S[e];
-        k += v >> 16;
-        const uint32_t q = v & kQMask;
-        if ((v & kInc) || q < ((j + 1) << kSubShift)) break;  // incomplete / wire end
-        e = q;
-      }
+  uint64_t pos = B.T[ch];
+  uint32_t cnt[SPK_MAX_SPANS];
+  for (uint32_t j = 0; j < k && base + j < n; ++j) {
+    const uint64_t L = wlen<NS>(P, wire, a.wire_len, pos, w, cnt);
+    const uint64_t i = base + j;
+    if (i < a.rec_cap) {
+      B.starts[i] = pos;
+      for (uint32_t s = 0; s < P.ns; ++s) B.rcnt[(uint64_t)s * a.rec_cap + i] = cnt[s];
     }
-    __syncthreads();
-    uint64_t acc[SPK_MAX_SPANS] = {};
-    if (threadIdx.x < kNSub && sub_ent[threadIdx.x] != 0xFFFFFFFFu) {
-      const StagedReader rd{as_lds(stage), wire, cs};
-      const uint32_t j = threadIdx.x;
-      uint64_t pos = cs + sub_ent[j], k = base + sub_base[j];
-      const uint64_t bnd = cs + ((uint64_t)(j + 1) << kSubShift);
-      while (pos < bnd && k < n) {
-        const uint64_t L = wlen<NS>(P, rd, a.wire_len, pos, w, acc);
-        if (!L) break;
-        if (k < a.rec_cap) starts[k] = pos;
-        pos += L;
-        ++k;
-      }
-      if (k == n) atomicMax(&c->end_pos, (unsigned long long)pos);
-      // stopped before record n without crossing the sub-chunk boundary:
-      // an incomplete record or the wire end (reference: no_buffer_space)
-      if (k < n && pos < bnd) atomicCAS(&res->errc, 0, SPK_ERRC_NO_BUFFER_SPACE);
-    }
-    for (uint32_t s2 = 0; s2 < P.ns; ++s2) {
-      uint64_t v = acc[s2];
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o);
-      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        uint64_t t = 0;
-        for (uint32_t i = 0; i < kVThreads / 64; ++i) t += red[i];
-        csum[ch * SPK_MAX_SPANS + s2] = t;
-      }
-      __syncthreads();
-    }
-    __syncthreads();
+    pos += L;
+    if (i + 1 == n) c->end_pos = pos;
   }
 }
 
-__global__ void vec_finish(DecArgs a, uint8_t *__restrict__ ws, spk_dresult_t *res) {
+__global__ void vec_finish(DecArgs a, uint8_t *__restrict__ ws, spk_dresult_t *res,
+                           const uint64_t *__restrict__ heap_tot) {
   if (threadIdx.x != 0) return;
   VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
   if (c->errc) return;
   spk_dresult_t r = *res;
-  // record n-1 was never placed: the payload holds fewer than n records
-  if (c->n && c->end_pos == 0 && r.errc == 0) r.errc = SPK_ERRC_NO_BUFFER_SPACE;
   if (r.errc == SPK_ERRC_NO_BUFFER_SPACE) {
     r.count = 0;
     r.consumed = 0;
@@ -1041,51 +1067,28 @@ __global__ void vec_finish(DecArgs a, uint8_t *__restrict__ ws, spk_dresult_t *r
     const uint64_t end = c->n ? (uint64_t)c->end_pos : c->p0;
     r.consumed = end > c->data_len ? end : c->data_len;
     if (c->n > a.rec_cap && r.errc == 0) r.errc = SPK_ERRC_CAPACITY;
+    for (uint32_t k = 0; k < a.L.n_spans; ++k) {
+      r.heap_used[k] = c->n ? heap_tot[k] : 0;
+      if (r.heap_used[k] > a.heap_cap[k] && r.errc == 0) r.errc = SPK_ERRC_CAPACITY;
+    }
   }
   *res = r;
 }
 
-// decode pass, block per chunk: records [base, next_base) from starts[]
-__global__ __launch_bounds__(kThreads) void vec_chunk_decode(
-    DecArgs a, const uint8_t *__restrict__ wire, const uint8_t *__restrict__ ws,
-    const uint32_t *__restrict__ m_entry, const uint64_t *__restrict__ m_base,
-    const uint64_t *__restrict__ starts, const uint64_t *__restrict__ csum,
-    uint8_t *__restrict__ recs, const spk_dresult_t *res) {
-  __shared__ uint64_t sh[kThreads / 64];
-  __shared__ uint64_t run[SPK_MAX_SPANS];
+// thread per record: decode from its start with precomputed heap offsets
+__global__ __launch_bounds__(256) void vec_decode(DecArgs a, const uint8_t *__restrict__ wire,
+                                                  const uint8_t *__restrict__ ws, VecBufs B,
+                                                  uint8_t *__restrict__ recs,
+                                                  const spk_dresult_t *res) {
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   if (c->errc || res->errc) return;
-  const uint64_t nchunks = c->nchunks, n = c->n;
+  const uint64_t n = c->n;
   const uint32_t w = c->w;
-  for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-    const uint32_t ent = m_entry[ch];
-    const uint64_t base = m_base[ch];
-    if ((ent >> 16) || base >= n) continue;
-    // records of this chunk end where the next chunk with a start begins
-    uint64_t hi = n;
-    for (uint64_t c2 = ch + 1; c2 < nchunks; ++c2) {
-      if (!(m_entry[c2] >> 16)) {
-        hi = m_base[c2] < n ? m_base[c2] : n;
-        break;
-      }
-      if ((m_entry[c2] >> 16) & (kFlagIncomplete | kFlagTooBig)) break;
-    }
-    if (threadIdx.x < SPK_MAX_SPANS) run[threadIdx.x] = csum[ch * SPK_MAX_SPANS + threadIdx.x];
-    __syncthreads();
-    for (uint64_t r0 = base; r0 < hi; r0 += kThreads) {
-      const uint64_t i = r0 + threadIdx.x;
-      uint64_t cnt[SPK_MAX_SPANS] = {};
-      if (i < hi) rec_counts(a.L, wire, starts[i], w, cnt);
-      uint64_t hoff[SPK_MAX_SPANS] = {};
-      for (uint32_t k = 0; k < a.L.n_spans; ++k) {
-        uint64_t tot;
-        hoff[k] = run[k] + block_excl_scan(cnt[k], &tot, sh);
-        __syncthreads();
-        if (threadIdx.x == 0) run[k] += tot;
-      }
-      if (i < hi) decode_record(a.L, wire, starts[i], w, recs + i * a.L.stride, a.heaps, hoff);
-      __syncthreads();
-    }
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
+    uint64_t hoff[SPK_MAX_SPANS];
+    for (uint32_t k = 0; k < a.L.n_spans; ++k) hoff[k] = B.hoff[(uint64_t)k * a.rec_cap + i];
+    decode_record(a.L, wire, B.starts[i], w, recs + i * a.L.stride, a.heaps, hoff);
   }
 }
 
@@ -1097,64 +1100,131 @@ static unsigned grid_for(uint64_t items, uint64_t per_block) {
   return (unsigned)(b ? b : 1);
 }
 
-struct VecWs {  // byte offsets inside the workspace for vector decode
-  size_t table, lv[8], ent[8], base[8], csum, starts, end;
-  uint64_t nlev[8];
-  int levels;
+struct VecWs {
+  size_t P, Pn, E, En, flags, T, cnt, base, unver, exitp, used, dirty, starts, rcnt, hoff, scan,
+      tot, end;
+  uint64_t nch;
+  uint32_t lp;
 };
 
-static VecWs vec_ws_layout(uint64_t wire_len, uint64_t max_records) {
+static VecWs vec_ws_layout(const spk_layout *L, uint64_t wire_len, uint64_t rec_cap) {
   VecWs v = {};
-  const uint64_t nch = wire_len / kChunk + 2;
+  v.nch = wire_len / kSpec + 2;
+  uint32_t min_rec = 0, ns = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i) {
+    if (L->ops[i].kind == SPK_OP_COPY) min_rec += L->ops[i].size; else { ++min_rec; ++ns; }
+  }
+  if (!min_rec) min_rec = 1;
+  v.lp = kSpec / min_rec + 2;
   size_t off = kWsScratch;
   auto take = [&](size_t bytes) {
     size_t o = off;
     off += (bytes + 255) & ~size_t(255);
     return o;
   };
-  v.table = take(nch * kK * 4);
-  uint64_t cnt = nch;
-  v.nlev[0] = nch;
-  v.levels = 0;
-  while (cnt > 1 && v.levels < 7) {
-    cnt = (cnt + kGroup - 1) / kGroup;
-    ++v.levels;
-    v.nlev[v.levels] = cnt;
-    v.lv[v.levels] = take(cnt * kK * 8);
-  }
-  for (int l = 0; l <= v.levels; ++l) {
-    v.ent[l] = take(v.nlev[l] * 4 + 8);
-    v.base[l] = take(v.nlev[l] * 8 + 8);
-  }
-  v.csum = take(nch * SPK_MAX_SPANS * 8);
-  v.starts = take(max_records * 8 + 8);
+  v.P = take(v.nch * v.lp * 2);
+  v.Pn = take(v.nch * 4);
+  v.E = take(v.nch * kExt * 4);
+  v.En = take(v.nch * 4);
+  v.flags = take(v.nch * 4);
+  v.T = take(v.nch * 8);
+  v.cnt = take(v.nch * 4);
+  v.base = take(v.nch * 8);
+  v.unver = take(v.nch * 4);
+  v.exitp = take(v.nch * 8);
+  v.used = take(v.nch * 8);
+  v.dirty = take(2 * v.nch * 4);
+  v.starts = take((rec_cap + 1) * 8);
+  v.rcnt = take((uint64_t)(ns ? ns : 1) * (rec_cap + 1) * 4);
+  v.hoff = take((uint64_t)(ns ? ns : 1) * (rec_cap + 1) * 8);
+  const uint64_t nsb = (rec_cap > v.nch ? rec_cap : v.nch) / kScanBlock + 2;
+  v.scan = take(nsb * 8);
+  v.tot = take(16 * 8);
   v.end = off;
   return v;
 }
 
-template <int NS>
-static void launch_vec_tables(unsigned grid, hipStream_t s, const DecArgs &a, const WalkProg &P,
-                              const uint8_t *wire, const uint8_t *ws, uint32_t *table) {
-  hipLaunchKernelGGL(vec_tables<NS>, dim3(grid), dim3(kVThreads), 0, s, a, P, wire, ws, table);
+static VecBufs vec_bufs(uint8_t *ws, const VecWs &v) {
+  VecBufs B;
+  B.P = reinterpret_cast<uint16_t *>(ws + v.P);
+  B.Pn = reinterpret_cast<uint32_t *>(ws + v.Pn);
+  B.E = reinterpret_cast<uint32_t *>(ws + v.E);
+  B.En = reinterpret_cast<uint32_t *>(ws + v.En);
+  B.flags = reinterpret_cast<uint32_t *>(ws + v.flags);
+  B.T = reinterpret_cast<uint64_t *>(ws + v.T);
+  B.cnt = reinterpret_cast<uint32_t *>(ws + v.cnt);
+  B.base = reinterpret_cast<uint64_t *>(ws + v.base);
+  B.unver = reinterpret_cast<uint32_t *>(ws + v.unver);
+  B.exitp = reinterpret_cast<uint64_t *>(ws + v.exitp);
+  B.used = reinterpret_cast<uint64_t *>(ws + v.used);
+  B.dirty = reinterpret_cast<uint32_t *>(ws + v.dirty);
+  B.starts = reinterpret_cast<uint64_t *>(ws + v.starts);
+  B.rcnt = reinterpret_cast<uint32_t *>(ws + v.rcnt);
+  B.hoff = reinterpret_cast<uint64_t *>(ws + v.hoff);
+  B.scan = reinterpret_cast<uint64_t *>(ws + v.scan);
+  return B;
 }
+
+// exclusive scan in[0..n) -> out, total -> *tot (device)
+static void scan_u32(const uint32_t *in, uint64_t n, uint64_t *out, uint64_t *bsum,
+                     uint64_t *tot, hipStream_t s) {
+  const unsigned nb = grid_for(n ? n : 1, kScanBlock);
+  hipLaunchKernelGGL(scan_reduce, dim3(nb), dim3(256), 0, s, in, n, bsum);
+  hipLaunchKernelGGL(scan_blocks, dim3(1), dim3(1024), 0, s, bsum, (uint64_t)nb, tot);
+  hipLaunchKernelGGL(scan_apply, dim3(nb), dim3(256), 0, s, in, n, (const uint64_t *)bsum, out);
+}
+
 template <int NS>
-static void launch_vec_starts(unsigned grid, hipStream_t s, const DecArgs &a, const WalkProg &P,
-                              const uint8_t *wire, uint8_t *ws, const uint32_t *m_entry,
-                              const uint64_t *m_base, uint64_t *starts, uint64_t *csum,
-                              spk_dresult_t *res) {
-  hipLaunchKernelGGL(vec_starts<NS>, dim3(grid), dim3(kVThreads), 0, s, a, P, wire, ws, m_entry,
-                     m_base, starts, csum, res);
+static hipError_t launch_vec_decode_ns(const DecArgs &a, const WalkProg &P, const uint8_t *wire,
+                                       uint8_t *ws, const VecWs &v, spk_dresult_t *d_res,
+                                       uint8_t *d_recs, hipStream_t s) {
+  VecBufs B = vec_bufs(ws, v);
+  hipError_t e;
+  // counts past the device-side chunk / record totals must read as zero
+  if ((e = hipMemsetAsync(B.cnt, 0, v.nch * 4, s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(B.rcnt, 0, (uint64_t)(P.ns ? P.ns : 1) * (a.rec_cap + 1) * 4, s)) !=
+      hipSuccess)
+    return e;
+  hipLaunchKernelGGL(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, v.lp);
+  const unsigned cg = grid_for(v.nch, 256);
+  hipLaunchKernelGGL(vec_spec<NS>, dim3(cg), dim3(256), 0, s, a, P, wire, ws, B);
+  uint32_t *dA = B.dirty, *dB = B.dirty + v.nch;
+  for (int r = 0; r < kRounds; ++r) {
+    uint32_t *din = (r & 1) ? dB : dA, *dout = (r & 1) ? dA : dB;
+    if ((e = hipMemsetAsync(dout, 0, v.nch * 4, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(vec_verify_round<NS>, dim3(cg), dim3(256), 0, s, a, P, wire, ws, B, r,
+                       (const uint32_t *)din, dout, r == kRounds - 1 ? 1 : 0);
+  }
+  hipLaunchKernelGGL(vec_fixup<NS>, dim3(1), dim3(64), 0, s, a, P, wire, ws, B);
+  hipLaunchKernelGGL(vec_term_min, dim3(cg), dim3(256), 0, s, ws, B);
+  hipLaunchKernelGGL(vec_term_zero, dim3(cg), dim3(256), 0, s, ws, B);
+  uint64_t *tot = reinterpret_cast<uint64_t *>(ws + v.tot);
+  // chunk record counts -> bases. nchunks is device-side; scan the capacity
+  // (entries past nchunks are never read)
+  scan_u32(B.cnt, v.nch, B.base, B.scan, tot, s);
+  hipLaunchKernelGGL(vec_count_check, dim3(1), dim3(64), 0, s, ws, (const uint64_t *)tot, d_res);
+  hipLaunchKernelGGL(vec_place<NS>, dim3(cg), dim3(256), 0, s, a, P, wire, ws, B,
+                     (const spk_dresult_t *)d_res);
+  for (uint32_t k = 0; k < P.ns; ++k)
+    scan_u32(B.rcnt + (uint64_t)k * a.rec_cap, a.rec_cap, B.hoff + (uint64_t)k * a.rec_cap,
+             B.scan, tot + 1 + k, s);
+  hipLaunchKernelGGL(vec_finish, dim3(1), dim3(64), 0, s, a, ws, d_res,
+                     (const uint64_t *)(tot + 1));
+  uint64_t rb = (a.rec_cap + 255) / 256;
+  if (rb > 65536) rb = 65536;
+  hipLaunchKernelGGL(vec_decode, dim3((unsigned)(rb ? rb : 1)), dim3(256), 0, s, a, wire,
+                     (const uint8_t *)ws, B, d_recs, (const spk_dresult_t *)d_res);
+  return hipGetLastError();
 }
 
 size_t var_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len) {
   size_t enc = kWsScratch + (grid_for(n, kRPB) + 1) * sizeof(Partial) + 256;
   size_t dec_msg = kWsScratch + n * sizeof(MsgState) +
                    (grid_for(n, kThreads) + 1) * SPK_MAX_SPANS * 8 + 256;
-  size_t dec_vec = vec_ws_layout(wire_len, n).end + 256;
+  size_t dec_vec = vec_ws_layout(L, wire_len, n).end + 256;
   size_t m = enc;
   if (mode == SPK_MODE_MESSAGES) m = m > dec_msg ? m : dec_msg;
   if (mode == SPK_MODE_VECTOR) m = m > dec_vec ? m : dec_vec;
-  (void)L;
   return m;
 }
 
@@ -1276,69 +1346,13 @@ hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
     return hipGetLastError();
   }
   // ---- VECTOR ----
-  const VecWs v = vec_ws_layout(wire_len, rec_cap);
+  const VecWs v = vec_ws_layout(L, wire_len, rec_cap);
   const WalkProg P = make_walkprog(L);
-  const int NS = P.ns == 1 ? 1 : P.ns == 2 ? 2 : 0;
-  uint32_t *table = reinterpret_cast<uint32_t *>(ws + v.table);
-  hipLaunchKernelGGL(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res);
-  const uint64_t max_chunks = v.nlev[0];
-  const unsigned tb = (unsigned)(max_chunks < 16384 ? max_chunks : 16384);
-  if (NS == 1)
-    launch_vec_tables<1>(tb, s, a, P, wire, ws, table);
-  else if (NS == 2)
-    launch_vec_tables<2>(tb, s, a, P, wire, ws, table);
-  else
-    launch_vec_tables<0>(tb, s, a, P, wire, ws, table);
-  const uint64_t *lvl_tab[8] = {};
-  for (int l = 1; l <= v.levels; ++l) {
-    uint64_t *out = reinterpret_cast<uint64_t *>(ws + v.lv[l]);
-    if (l == 1)
-      hipLaunchKernelGGL(vec_compose_up<uint32_t>, dim3((unsigned)v.nlev[l]), dim3(256), 0, s,
-                         (const uint32_t *)table, v.nlev[0], out);
-    else
-      hipLaunchKernelGGL(vec_compose_up<uint64_t>, dim3((unsigned)v.nlev[l]), dim3(256), 0, s,
-                         lvl_tab[l - 1], v.nlev[l - 1], out);
-    lvl_tab[l] = out;
-  }
-  if ((e = hipMemsetAsync(ws + v.ent[v.levels], 0, 8, s)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(ws + v.base[v.levels], 0, 16, s)) != hipSuccess) return e;
-  for (int l = v.levels; l >= 1; --l) {
-    const uint64_t ng = v.nlev[l];
-    const uint32_t *ge = (const uint32_t *)(ws + v.ent[l]);
-    const uint64_t *gb = (const uint64_t *)(ws + v.base[l]);
-    uint32_t *me = reinterpret_cast<uint32_t *>(ws + v.ent[l - 1]);
-    uint64_t *mb = reinterpret_cast<uint64_t *>(ws + v.base[l - 1]);
-    if (l == 1)
-      hipLaunchKernelGGL(vec_compose_down<uint32_t>, dim3(grid_for(ng, 64)), dim3(64), 0, s,
-                         (const uint32_t *)table, v.nlev[0], ng, ge, gb, me, mb);
-    else
-      hipLaunchKernelGGL(vec_compose_down<uint64_t>, dim3(grid_for(ng, 64)), dim3(64), 0, s,
-                         lvl_tab[l - 1], v.nlev[l - 1], ng, ge, gb, me, mb);
-  }
-  uint32_t *m_entry = reinterpret_cast<uint32_t *>(ws + v.ent[0]);
-  uint64_t *m_base = reinterpret_cast<uint64_t *>(ws + v.base[0]);
-  hipLaunchKernelGGL(vec_check_entries, dim3(grid_for(max_chunks, 256)), dim3(256), 0, s, ws,
-                     (const uint32_t *)m_entry, (const uint64_t *)m_base);
-  hipLaunchKernelGGL(vec_seq_walk, dim3(1), dim3(64), 0, s, a, P, wire, ws, m_entry, m_base);
-  uint64_t *csum = reinterpret_cast<uint64_t *>(ws + v.csum);
-  uint64_t *starts = reinterpret_cast<uint64_t *>(ws + v.starts);
-  if ((e = hipMemsetAsync(csum, 0, max_chunks * SPK_MAX_SPANS * 8, s)) != hipSuccess) return e;
-  if (NS == 1)
-    launch_vec_starts<1>(tb, s, a, P, wire, ws, m_entry, m_base, starts, csum, d_res);
-  else if (NS == 2)
-    launch_vec_starts<2>(tb, s, a, P, wire, ws, m_entry, m_base, starts, csum, d_res);
-  else
-    launch_vec_starts<0>(tb, s, a, P, wire, ws, m_entry, m_base, starts, csum, d_res);
-  hipLaunchKernelGGL(var_scan_blocks, dim3(1), dim3(1024), 0, s, max_chunks, a.L.n_spans,
-                     csum, a, d_res);
-  hipLaunchKernelGGL(vec_finish, dim3(1), dim3(64), 0, s, a, ws, d_res);
-  const unsigned db = (unsigned)(max_chunks < 16384 ? max_chunks : 16384);
-  hipLaunchKernelGGL(vec_chunk_decode, dim3(db), dim3(kThreads), 0, s, a, wire,
-                     (const uint8_t *)ws, (const uint32_t *)m_entry,
-                     (const uint64_t *)m_base, (const uint64_t *)starts,
-                     (const uint64_t *)csum, (uint8_t *)d_recs, (const spk_dresult_t *)d_res);
+  (void)e;
   (void)ws_bytes;
-  return hipGetLastError();
+  if (P.ns == 1) return launch_vec_decode_ns<1>(a, P, wire, ws, v, d_res, (uint8_t *)d_recs, s);
+  if (P.ns == 2) return launch_vec_decode_ns<2>(a, P, wire, ws, v, d_res, (uint8_t *)d_recs, s);
+  return launch_vec_decode_ns<0>(a, P, wire, ws, v, d_res, (uint8_t *)d_recs, s);
 }
 
 }  // namespace spk
