@@ -4,7 +4,7 @@
  * This is the drop-in boundary between a host-side struct_pack front end
  * (our C++20 header include/ylt/struct_pack.hpp, or the Python mirror
  * yalantinglibs_amd/struct_pack.py) and the hand-written gfx950 HIP kernels
- * in yalantinglibs_amd/csrc/spk_codec.hip. Plain C: no HIP/torch types, all
+ * in yalantinglibs_amd/csrc/ (spk_api.hip, spk_fixed.hip, spk_var.hip). Plain C: no HIP/torch types, all
  * buffers are raw pointers + sizes, streams are opaque `void*` (hipStream_t).
  *
  * The reference has no C ABI: struct_pack is a header-only template library.

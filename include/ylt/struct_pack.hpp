@@ -325,7 +325,15 @@ void serialize_to(Buffer &buffer, const std::vector<T> &v) {
   device::check(hipStreamSynchronize(c.stream()), "sync");
 }
 
-template <uint64_t conf = sp_config::DEFAULT, typename Buffer = std::vector<char>, typename T>
+// serialize<Buffer>(v) and serialize<conf, Buffer>(v), as the reference's two
+// overloads (struct_pack.hpp:191-207, 228-244)
+template <typename Buffer = std::vector<char>, typename T>
+Buffer serialize(const std::vector<T> &v) {
+  Buffer b;
+  serialize_to<sp_config::DEFAULT>(b, v);
+  return b;
+}
+template <uint64_t conf, typename Buffer = std::vector<char>, typename T>
 Buffer serialize(const std::vector<T> &v) {
   Buffer b;
   serialize_to<conf>(b, v);

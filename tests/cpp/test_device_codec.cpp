@@ -115,6 +115,10 @@ int main() {
     auto bytes = serialize<sp_config::DEFAULT, std::string>(v);
     CHECK(bytes == golden("rect_A_n1000_p0_default.bin"));
     CHECK(bytes.size() == 16003);
+    // the reference's other overloads: serialize<Buffer>(v), serialize(v)
+    CHECK(serialize<std::string>(v) == bytes);
+    const std::vector<char> vc = serialize(v);
+    CHECK(std::string(vc.begin(), vc.end()) == bytes);
   }
   roundtrip_messages<RecS>("recs_B_n500_p300_default.bin", "recs_B_n500_p300_default.lens", 500,
                            [&](RecS &o, uint64_t i) { o = make_recs(S3, i, 300); });

@@ -590,9 +590,11 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
 // record indices, one lane per chunk re-walks its true records to place
 // their starts, a device-wide scan turns span counts into heap offsets, and
 // one thread per record decodes it.
-constexpr uint32_t kSpec = 2048;       // payload bytes per speculation chunk
-constexpr uint32_t kExt = 16;          // records a spec walk continues past its chunk
-constexpr uint32_t kMaxTries = 256;    // candidate start bytes per chunk
+constexpr uint32_t kSpec = 256;        // payload bytes per speculation chunk
+constexpr uint32_t kWinExtra = 512;    // extension bytes staged past a wave's chunks
+constexpr uint32_t kPlaus = 4096;      // longest record a speculative walk accepts
+constexpr int kRounds = 8;             // parallel re-verification rounds
+constexpr uint32_t kExt = 4;           // records a spec walk continues past its chunk
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
 
 // per-chunk verification flags
@@ -610,9 +612,10 @@ struct VCtl {
   uint32_t w;
   int32_t errc;      // header errc
   uint32_t lp;       // P-list capacity per chunk
-  uint32_t n_unver;  // entries in the unverified list
+  uint32_t n_unver;  // chunks left for the sequential fixup (diagnostic)
   uint32_t term_chunk;  // first chunk where the true path terminates (kNone32)
   uint32_t overflow;    // a P list overflowed (records < 1 B impossible; guard)
+  uint32_t wl_n[kRounds + 1];  // re-verification worklist length per round
 };
 
 // Compact walk program of a record: fixed bytes, then per span
@@ -622,6 +625,8 @@ struct WalkProg {
   uint32_t ns;
   uint32_t skip[SPK_MAX_SPANS + 1];
   uint32_t esz[SPK_MAX_SPANS];
+  uint32_t c0max;                  // largest first count of a plausible record
+  uint64_t cmax[SPK_MAX_SPANS];    // largest count whose byte size fits 64 bits
 };
 
 static WalkProg make_walkprog(const spk_layout *L) {
@@ -636,6 +641,8 @@ static WalkProg make_walkprog(const spk_layout *L) {
     }
   }
   p.ns = k;
+  for (uint32_t j = 0; j < k; ++j) p.cmax[j] = ~0ull / (p.esz[j] ? p.esz[j] : 1);
+  p.c0max = k ? (kPlaus > p.skip[0] ? (kPlaus - p.skip[0]) / (p.esz[0] ? p.esz[0] : 1) : 0) : 0;
   return p;
 }
 
@@ -666,7 +673,7 @@ __device__ __forceinline__ uint64_t wlen(const WalkProg &P, const uint8_t *wire,
     const uint64_t c = wire_le(wire, p, w);
     p += w;
     if (c) {
-      if (P.esz[k] > 1 && c > ~0ull / P.esz[k]) return 0;
+      if (c > P.cmax[k]) return 0;
       const uint64_t nb = c * P.esz[k];
       if (nb > len - p) return 0;
       p += nb;
@@ -710,6 +717,7 @@ __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
   c->total = 0;
   c->lp = lp;
   c->n_unver = 0;
+  for (int r = 0; r <= kRounds; ++r) c->wl_n[r] = 0;
   c->term_chunk = kNone32;
   c->overflow = 0;
   const uint64_t payload = (!e && a.wire_len > pos) ? a.wire_len - pos : 0;
@@ -730,62 +738,188 @@ struct VecBufs {
   uint64_t *T;      // [nchunks] first true record start >= chunk start (abs), ~0 none
   uint32_t *cnt;    // [nchunks] complete true records starting in the chunk
   uint64_t *base;   // [nchunks] index of the chunk's first true record
-  uint32_t *unver;  // [nchunks] chunks still dirty after the parallel rounds
+  uint32_t *wl;     // [2][nchunks] re-verification worklists (alternating)
   uint64_t *exitp;  // [nchunks] true exit of the chunk (first start past it)
   uint64_t *used;   // [nchunks] entry the chunk was last verified with
-  uint32_t *dirty;  // [2][nchunks] re-verification flags (double buffered)
+  uint32_t *dirty;  // [2][nchunks] round a chunk is listed for (alternating)
+  uint32_t *mj;     // [nchunks] P index where the true path meets the spec walk
+                    //           | records walked before it << 16
   uint64_t *starts; // [rec_cap]
   uint32_t *rcnt;   // [n_spans][rec_cap] span counts per record
   uint64_t *hoff;   // [n_spans][rec_cap] heap element offsets per record
   uint64_t *scan;   // block sums for the device-wide scans
 };
 
-// one lane per chunk: speculative walk
+typedef uint32_t v4u_t __attribute__((ext_vector_type(4)));
+typedef v4u_t v4u_una __attribute__((aligned(1)));
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// Count-field reader over a chunk's LDS window: bytes [cs, wend) of the wire
+// are staged in LDS; reads past the window go to global memory.
+struct WinReader {
+  const lds_u32 *d;
+  const uint8_t *wire;
+  uint64_t cs, wend;
+  uint32_t w;
+  __device__ __forceinline__ uint64_t operator()(uint64_t x) const {
+    if (x + w <= wend) {
+      const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = o >> 2;
+      const uint32_t d0 = d[i], d1 = d[i + 1];
+      const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
+      if (w == 1) return lo & 0xFFu;
+      if (w == 2) return lo & 0xFFFFu;
+      if (w == 4) return lo;
+      return lo | ((uint64_t)__builtin_amdgcn_alignbyte(d[i + 2], d1, sh) << 32);
+    }
+    return wire_le(wire, x, w);
+  }
+};
+
+// wlen() with the count fields read through `rd`
+template <int NS, typename Rd>
+__device__ __forceinline__ uint64_t wlen_rd(const WalkProg &P, const Rd &rd, uint64_t len,
+                                            uint64_t pos, uint32_t w) {
+  uint64_t p = pos + P.skip[0];
+  const uint32_t ns = NS > 0 ? (uint32_t)NS : P.ns;
+#pragma unroll
+  for (uint32_t k = 0; k < (NS > 0 ? (uint32_t)NS : SPK_MAX_SPANS); ++k) {
+    if (NS == 0 && k >= ns) break;
+    if (p + w > len) return 0;
+    const uint64_t c = rd(p);
+    p += w;
+    if (c) {
+      if (c > P.cmax[k]) return 0;
+      const uint64_t nb = c * P.esz[k];
+      if (nb > len - p) return 0;
+      p += nb;
+    }
+    p += P.skip[k + 1];
+  }
+  if (p > len) return 0;
+  return p - pos;
+}
+
+constexpr uint32_t kRegion = 64 * kSpec;                    // chunk bytes per wave
+constexpr uint32_t kRegionVec = (kRegion + kWinExtra) / 16;  // 16-B LDS slots per wave
+constexpr uint32_t kSpecWaves = 2;                           // waves per block
+
+// One lane per chunk; a wave stages its 64 consecutive chunks (plus the head
+// of the extension) in LDS with coalesced 16-B loads, then every lane walks
+// its own chunk there. A candidate start byte is plausible when no record of
+// its walk -- in the chunk or in the extension -- is implausible (longer than
+// kPlaus, or incomplete before the wire end); the lane takes the first
+// plausible candidate and records its walk: positions in the chunk (P) and
+// kExt positions past it (E). Chunk 0 starts at the payload start (exact).
 template <int NS>
-__global__ __launch_bounds__(256) void vec_spec(DecArgs a, WalkProg P,
-                                                const uint8_t *__restrict__ wire,
-                                                uint8_t *__restrict__ ws, VecBufs B) {
+__global__ __launch_bounds__(64 * kSpecWaves) void vec_spec(DecArgs a, WalkProg P,
+                                                            const uint8_t *__restrict__ wire,
+                                                            uint8_t *__restrict__ ws, VecBufs B) {
+  __shared__ v4u_t reg_s[kSpecWaves][kRegionVec + 1];
   VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
-  const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= c->nchunks) return;
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t ch0 = ((uint64_t)blockIdx.x * kSpecWaves + wv) * 64;
+  const uint64_t nch = c->nchunks;
+  if (ch0 >= nch) return;  // wave-uniform; only wave-level sync below
   const uint32_t w = c->w, lp = c->lp;
   const uint64_t len = a.wire_len;
+  const uint64_t rs = c->p0 + ch0 * kSpec;
+  const uint64_t wend = rs + kRegionVec * 16 < len ? rs + kRegionVec * 16 : len;
+  v4u_t *reg = reg_s[wv];
+  for (uint32_t v = lane; v < kRegionVec; v += 64) {
+    const uint64_t g = rs + 16ull * v;
+    v4u_t val = {0u, 0u, 0u, 0u};
+    if (g + 16 <= len) {
+      val = *reinterpret_cast<const v4u_una *>(wire + g);
+    } else if (g < len) {
+      uint32_t t[4] = {0u, 0u, 0u, 0u};
+      for (uint64_t q = g; q < len; ++q) t[(q - g) >> 2] |= (uint32_t)wire[q] << (8 * ((q - g) & 3));
+      val = v4u_t{t[0], t[1], t[2], t[3]};
+    }
+    reg[v] = val;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint64_t ch = ch0 + lane;
+  if (ch >= nch) return;
+  WinReader rd;
+  rd.d = (const lds_u32 *)(reg);
+  rd.wire = wire;
+  rd.cs = rs;
+  rd.wend = wend;
+  rd.w = w;
   const uint64_t cs = c->p0 + ch * kSpec;
   const uint64_t ce = cs + kSpec < len ? cs + kSpec : len;
   uint16_t *Pl = B.P + ch * lp;
   uint32_t *El = B.E + ch * kExt;
   uint32_t np = 0, ne = 0, fl = 0;
-  const uint32_t tries = ch == 0 ? 1 : kMaxTries;
-  for (uint32_t t = 0; t < tries; ++t) {
-    uint64_t x = cs + t;
-    if (x >= ce) break;
-    np = ne = fl = 0;
-    bool ok = true;
-    for (;;) {
-      if (x >= ce && ne == kExt) break;
-      const uint64_t L = x < len ? wlen<NS>(P, wire, len, x, w, (uint32_t *)nullptr) : 0;
-      // inside the chunk, a speculative walk (chunk > 0) that meets an
-      // implausible record -- longer than the chunk, or incomplete before
-      // the wire end -- started off the record grid: restart one byte on
-      if (ch != 0 && x < ce && ((L == 0 && x < len) || L > kSpec)) {
-        ok = false;
-        break;
-      }
-      if (x < ce) {
-        if (np < lp) Pl[np] = (uint16_t)(x - cs);
-        ++np;
+  // One record step per iteration for every lane (a nested try/walk loop
+  // would make the wave wait for each lane's walk in turn). While searching,
+  // 8 candidate start bytes are screened per iteration on their first count.
+  uint64_t t = 0, x = cs;
+  bool searching = ch != 0, done = false;
+  const uint32_t s0 = P.skip[0];
+  while (!done) {
+    if (searching) {
+      const uint64_t b0 = cs + t + s0;  // first count field of candidate cs+t
+      uint32_t m = 0;
+      if (b0 + 20 <= wend) {
+        const uint32_t o0 = (uint32_t)(b0 - rs), i = o0 >> 2, sh = o0 & 3;
+        const lds_u32 *d = rd.d;
+        const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2], d3 = d[i + 3], d4 = d[i + 4];
+        const uint32_t wd[4] = {__builtin_amdgcn_alignbyte(d1, d0, sh),
+                                __builtin_amdgcn_alignbyte(d2, d1, sh),
+                                __builtin_amdgcn_alignbyte(d3, d2, sh),
+                                __builtin_amdgcn_alignbyte(d4, d3, sh)};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t lo = __builtin_amdgcn_alignbyte(wd[(k >> 2) + 1], wd[k >> 2], k & 3);
+          uint64_t cv = w == 1 ? (lo & 0xFFu) : w == 2 ? (lo & 0xFFFFu) : lo;
+          if (w == 8)
+            cv |= (uint64_t)__builtin_amdgcn_alignbyte(wd[(k >> 2) + 2], wd[(k >> 2) + 1], k & 3)
+                  << 32;
+          m |= (cv <= P.c0max ? 1u : 0u) << k;
+        }
       } else {
-        El[ne++] = (x - cs) < 0xFFFFFFFFull ? (uint32_t)(x - cs) : 0xFFFFFFFEu;
+        for (int k = 0; k < 8; ++k) {
+          const uint64_t q = b0 + k;
+          const uint64_t cv = q + w <= len ? rd(q) : ~0ull;
+          m |= (cv <= P.c0max ? 1u : 0u) << k;
+        }
       }
-      if (!L) {  // incomplete record or the wire end: the walk terminates here
-        fl = kWalkTerm;
-        break;
+      const uint64_t rem = ce - (cs + t);  // candidates must start in the chunk
+      if (rem < 8) m &= (1u << rem) - 1u;
+      if (!m) {
+        t += 8;
+        if (cs + t >= ce) done = true;
+        continue;
       }
-      x += L;
+      t += (uint32_t)__builtin_ctz(m);
+      x = cs + t;
+      np = ne = 0;
+      searching = false;
     }
-    if (ok) break;
-    np = ne = 0;
+    const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w) : 0;
+    if (ch != 0 && ((L == 0 && x < len) || L > kPlaus)) {  // off the record grid
+      t += 1;
+      searching = true;
+      if (cs + t >= ce) done = true;
+      continue;
+    }
+    if (x < ce) {
+      if (np < lp) Pl[np] = (uint16_t)(x - cs);
+      ++np;
+    } else {
+      El[ne++] = (x - cs) < 0xFFFFFFFFull ? (uint32_t)(x - cs) : 0xFFFFFFFEu;
+    }
+    if (!L) {  // incomplete record or the wire end: the walk terminates here
+      fl = kWalkTerm;
+      break;
+    }
+    x += L;
+    if (x >= ce && ne == kExt) done = true;
   }
+  if (searching) np = ne = fl = 0;  // no plausible start in the chunk
   if (np > lp) {
     atomicOr(&c->overflow, 1u);
     np = lp;
@@ -793,10 +927,11 @@ __global__ __launch_bounds__(256) void vec_spec(DecArgs a, WalkProg P,
   B.Pn[ch] = np;
   B.En[ch] = ne;
   B.flags[ch] = fl;
+  B.dirty[ch] = kNone32;
+  B.dirty[nch + ch] = kNone32;
 }
 
 constexpr uint64_t kTermPos = ~0ull;  // "the true path ended before this chunk"
-constexpr int kRounds = 6;            // parallel re-verification rounds
 
 // Walk the true path of chunk `ch` from `entry` until it meets the chunk's
 // speculative walk (two-pointer merge against the sorted P list) or leaves
@@ -805,7 +940,8 @@ constexpr int kRounds = 6;            // parallel re-verification rounds
 template <int NS>
 __device__ void walk_chunk(const DecArgs &a, const WalkProg &P, const uint8_t *wire,
                            const VCtl *c, const VecBufs &B, uint64_t ch, uint64_t entry,
-                           uint64_t *exit, uint32_t *count, uint32_t *flags, uint64_t *T) {
+                           uint64_t *exit, uint32_t *count, uint32_t *flags, uint64_t *T,
+                           uint32_t *mj) {
   const uint64_t len = a.wire_len;
   const uint64_t cs = c->p0 + ch * kSpec;
   const uint64_t ce = cs + kSpec < len ? cs + kSpec : len;
@@ -819,6 +955,7 @@ __device__ void walk_chunk(const DecArgs &a, const WalkProg &P, const uint8_t *w
     *count = 0;
     *flags = fl | kOk;
     *T = ~0ull;
+    *mj = 0;
     return;
   }
   uint32_t j = 0, k = 0;
@@ -838,6 +975,7 @@ __device__ void walk_chunk(const DecArgs &a, const WalkProg &P, const uint8_t *w
     ++k;
     pos += L;
   }
+  const uint32_t k0 = k;  // records walked before the meeting point
   if (merged) {
     k += np - j;
     if (walk_term && en == 0) {  // the merged walk ends inside this chunk
@@ -855,93 +993,132 @@ __device__ void walk_chunk(const DecArgs &a, const WalkProg &P, const uint8_t *w
   }
   *count = k;
   *flags = fl | kOk;
+  *mj = (merged ? j : np) | (k0 << 16);
 }
 
-// flag chunk x for the next round; after the last round, also list it
-// (once) for the sequential fixup
-__device__ __forceinline__ void mark_dirty(VCtl *c, const VecBufs &B, uint32_t *dirty_out,
-                                           uint64_t x, int last) {
-  if (atomicExch(&dirty_out[x], 1u) == 0u && last) {
-    const uint32_t slot = atomicAdd(&c->n_unver, 1u);
-    B.unver[slot] = (uint32_t)x;
-  }
-}
-
-// Round r of the verification: round 0 processes every chunk with the
-// optimistic entry E_{c-1}[0]; later rounds only chunks whose entry changed
-// (dirty_in), once their predecessor is final. A chunk whose exit differs
-// from the entry its successor last used marks the successor dirty.
-template <int NS>
-__global__ __launch_bounds__(256) void vec_verify_round(DecArgs a, WalkProg P,
-                                                        const uint8_t *__restrict__ wire,
-                                                        uint8_t *__restrict__ ws, VecBufs B,
-                                                        int round, const uint32_t *dirty_in,
-                                                        uint32_t *dirty_out, int last) {
-  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
-  const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// list chunk x for round r (once)
+__device__ __forceinline__ void mark_dirty(VCtl *c, const VecBufs &B, uint64_t x, uint32_t r) {
   const uint64_t nch = c->nchunks;
-  if (ch >= nch) return;
-  uint64_t entry;
-  if (round == 0) {
-    if (ch == 0)
-      entry = c->p0;
-    else
-      entry = B.En[ch - 1] ? c->p0 + (ch - 1) * kSpec + B.E[(ch - 1) * kExt] : kTermPos;
-  } else {
-    if (!dirty_in[ch]) return;
-    if (ch > 0 && dirty_in[ch - 1]) {  // predecessor not final yet
-      mark_dirty(c, B, dirty_out, ch, last);
-      return;
-    }
-    entry = B.exitp[ch - 1];
+  uint32_t *stamp = B.dirty + (r & 1) * nch;
+  if (atomicExch(&stamp[x], r) != r) {
+    const uint32_t slot = atomicAdd(&c->wl_n[r], 1u);
+    B.wl[(r & 1) * nch + slot] = (uint32_t)x;
   }
+}
+
+template <int NS>
+__device__ __forceinline__ void verify_chunk(const DecArgs &a, const WalkProg &P,
+                                             const uint8_t *wire, VCtl *c, const VecBufs &B,
+                                             uint64_t ch, uint64_t entry, uint64_t next_used,
+                                             uint32_t r) {
   uint64_t exit, T;
-  uint32_t count, flags;
-  walk_chunk<NS>(a, P, wire, c, B, ch, entry, &exit, &count, &flags, &T);
+  uint32_t count, flags, mj;
+  walk_chunk<NS>(a, P, wire, c, B, ch, entry, &exit, &count, &flags, &T, &mj);
+  B.mj[ch] = mj;
   B.used[ch] = entry;
   B.exitp[ch] = exit;
   B.T[ch] = T;
   B.cnt[ch] = count;
   B.flags[ch] = flags;
-  if (ch + 1 < nch) {
-    uint64_t next_used;
-    if (round == 0)
-      next_used = B.En[ch] ? c->p0 + ch * kSpec + B.E[ch * kExt] : kTermPos;
-    else
-      next_used = B.used[ch + 1];
-    if (exit != next_used) {
-      mark_dirty(c, B, dirty_out, ch + 1, last);
+  if (r < (uint32_t)kRounds && ch + 1 < c->nchunks && exit != next_used)
+    mark_dirty(c, B, ch + 1, r + 1);
+}
+
+// Round 0 of the verification, one lane per chunk: walk the chunk's true
+// path from the optimistic entry E_{c-1}[0] until it meets the chunk's spec
+// walk; a chunk whose exit differs from the entry its successor assumed
+// lists the successor for round 1.
+template <int NS>
+__global__ __launch_bounds__(256) void vec_verify0(DecArgs a, WalkProg P,
+                                                   const uint8_t *__restrict__ wire,
+                                                   uint8_t *__restrict__ ws, VecBufs B) {
+  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
+  const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nch = c->nchunks;
+  if (ch >= nch) return;
+  const uint64_t entry =
+      ch == 0 ? c->p0
+              : (B.En[ch - 1] ? c->p0 + (ch - 1) * kSpec + B.E[(ch - 1) * kExt] : kTermPos);
+  const uint64_t next_used = B.En[ch] ? c->p0 + ch * kSpec + B.E[ch * kExt] : kTermPos;
+  verify_chunk<NS>(a, P, wire, c, B, ch, entry, next_used, 0);
+}
+
+// Round r >= 1 over round r's worklist: a listed chunk whose predecessor is
+// listed too waits for the next round; otherwise it is re-walked from its
+// predecessor's (now final) exit.
+template <int NS>
+__global__ __launch_bounds__(256) void vec_verify_round(DecArgs a, WalkProg P,
+                                                        const uint8_t *__restrict__ wire,
+                                                        uint8_t *__restrict__ ws, VecBufs B,
+                                                        uint32_t r) {
+  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
+  const uint64_t nch = c->nchunks;
+  const uint32_t n_in = c->wl_n[r];
+  const uint32_t *list = B.wl + (r & 1) * nch;
+  const uint32_t *stamp = B.dirty + (r & 1) * nch;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_in; i += gridDim.x * blockDim.x) {
+    const uint64_t ch = list[i];
+    if (stamp[ch - 1] == r) {  // predecessor not final yet (chunk 0 is never listed)
+      mark_dirty(c, B, ch, r + 1);
+      continue;
     }
+    const uint64_t next_used = ch + 1 < nch ? B.used[ch + 1] : 0;
+    verify_chunk<NS>(a, P, wire, c, B, ch, B.exitp[ch - 1], next_used, r);
   }
 }
 
-// last resort, single lane: chunks still dirty after kRounds, in order
+// Last resort, one block: chunks still listed after kRounds rounds, in
+// ascending order (bitonic sort in LDS), each re-walked with its cascade
+// until a chunk's state matches its predecessor's exit.
+constexpr uint32_t kFixSort = 4096;
 template <int NS>
-__global__ void vec_fixup(DecArgs a, WalkProg P, const uint8_t *__restrict__ wire,
-                          uint8_t *__restrict__ ws, VecBufs B) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__global__ __launch_bounds__(1024) void vec_fixup(DecArgs a, WalkProg P,
+                                                  const uint8_t *__restrict__ wire,
+                                                  uint8_t *__restrict__ ws, VecBufs B) {
+  __shared__ uint32_t sh[kFixSort];
   VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
-  const uint32_t nu = c->n_unver;
-  if (!nu) return;
-  uint32_t first = kNone32;
-  for (uint32_t i = 0; i < nu; ++i) first = B.unver[i] < first ? B.unver[i] : first;
+  const uint32_t n = c->wl_n[kRounds];
+  if (threadIdx.x == 0) c->n_unver = n;
+  if (!n) return;
   const uint64_t nch = c->nchunks;
-  // from the earliest still-dirty chunk on, propagate sequentially until the
-  // entry a chunk receives equals the one it was verified with, and no later
-  // dirty chunk remains
-  uint64_t last_dirty = 0;
-  for (uint32_t i = 0; i < nu; ++i) last_dirty = B.unver[i] > last_dirty ? B.unver[i] : last_dirty;
-  for (uint64_t ch = first; ch < nch; ++ch) {
-    const uint64_t entry = B.exitp[ch - 1];
-    if (entry == B.used[ch] && ch > last_dirty) break;
-    uint64_t exit, T;
-    uint32_t count, flags;
-    walk_chunk<NS>(a, P, wire, c, B, ch, entry, &exit, &count, &flags, &T);
-    B.used[ch] = entry;
-    B.exitp[ch] = exit;
-    B.T[ch] = T;
-    B.cnt[ch] = count;
-    B.flags[ch] = flags;
+  const uint32_t *list = B.wl + (kRounds & 1) * nch;
+  if (n <= kFixSort) {
+    for (uint32_t i = threadIdx.x; i < kFixSort; i += blockDim.x) sh[i] = i < n ? list[i] : kNone32;
+    __syncthreads();
+    for (uint32_t k = 2; k <= kFixSort; k <<= 1) {
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        for (uint32_t i = threadIdx.x; i < kFixSort; i += blockDim.x) {
+          const uint32_t l = i ^ j;
+          if (l > i) {
+            const uint32_t x = sh[i], y = sh[l];
+            if (((i & k) == 0) == (x > y)) {
+              sh[i] = y;
+              sh[l] = x;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+  }
+  if (threadIdx.x != 0) return;
+  if (n <= kFixSort) {
+    uint64_t done_to = 0;  // chunks < done_to are final
+    for (uint32_t i = 0; i < n; ++i) {
+      uint64_t ch = sh[i];
+      if (ch < done_to) continue;
+      for (; ch < nch; ++ch) {
+        const uint64_t entry = B.exitp[ch - 1];
+        if (entry == B.used[ch]) break;
+        verify_chunk<NS>(a, P, wire, c, B, ch, entry, 0, kRounds);
+      }
+      done_to = ch + 1;
+    }
+  } else {
+    for (uint64_t ch = 1; ch < nch; ++ch) {  // long list: scan every chunk
+      const uint64_t entry = B.exitp[ch - 1];
+      if (entry != B.used[ch]) verify_chunk<NS>(a, P, wire, c, B, ch, entry, 0, kRounds);
+    }
   }
 }
 
@@ -1025,7 +1202,9 @@ __global__ void vec_count_check(uint8_t *__restrict__ ws, const uint64_t *__rest
   if (c->n && *total < c->n) res->errc = SPK_ERRC_NO_BUFFER_SPACE;
 }
 
-// one lane per chunk: place the chunk's true records (index base..)
+// one lane per chunk: place the chunk's true records (index base..): the
+// records before the meeting point are walked from T, the rest are the
+// chunk's P entries from the meeting index on (independent loads)
 template <int NS>
 __global__ __launch_bounds__(256) void vec_place(DecArgs a, WalkProg P,
                                                  const uint8_t *__restrict__ wire,
@@ -1035,14 +1214,18 @@ __global__ __launch_bounds__(256) void vec_place(DecArgs a, WalkProg P,
   const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (ch >= c->nchunks || c->errc || res->errc) return;
   const uint64_t n = c->n, base = B.base[ch];
-  uint32_t k = B.cnt[ch];
+  const uint32_t k = B.cnt[ch];
   if (!k || base >= n) return;
-  const uint32_t w = c->w;
+  const uint32_t w = c->w, mj = B.mj[ch];
+  const uint32_t k0 = mj >> 16, j0 = mj & 0xFFFFu;
+  const uint64_t cs = c->p0 + ch * kSpec;
+  const uint16_t *Pl = B.P + ch * c->lp;
   uint64_t pos = B.T[ch];
   uint32_t cnt[SPK_MAX_SPANS];
-  for (uint32_t j = 0; j < k && base + j < n; ++j) {
+  for (uint32_t r = 0; r < k && base + r < n; ++r) {
+    if (r >= k0) pos = cs + Pl[j0 + (r - k0)];
     const uint64_t L = wlen<NS>(P, wire, a.wire_len, pos, w, cnt);
-    const uint64_t i = base + j;
+    const uint64_t i = base + r;
     if (i < a.rec_cap) {
       B.starts[i] = pos;
       for (uint32_t s = 0; s < P.ns; ++s) B.rcnt[(uint64_t)s * a.rec_cap + i] = cnt[s];
@@ -1101,7 +1284,7 @@ static unsigned grid_for(uint64_t items, uint64_t per_block) {
 }
 
 struct VecWs {
-  size_t P, Pn, E, En, flags, T, cnt, base, unver, exitp, used, dirty, starts, rcnt, hoff, scan,
+  size_t P, Pn, E, En, flags, T, cnt, base, wl, exitp, used, dirty, mj, starts, rcnt, hoff, scan,
       tot, end;
   uint64_t nch;
   uint32_t lp;
@@ -1130,10 +1313,11 @@ static VecWs vec_ws_layout(const spk_layout *L, uint64_t wire_len, uint64_t rec_
   v.T = take(v.nch * 8);
   v.cnt = take(v.nch * 4);
   v.base = take(v.nch * 8);
-  v.unver = take(v.nch * 4);
+  v.wl = take(2 * v.nch * 4);
   v.exitp = take(v.nch * 8);
   v.used = take(v.nch * 8);
   v.dirty = take(2 * v.nch * 4);
+  v.mj = take(v.nch * 4);
   v.starts = take((rec_cap + 1) * 8);
   v.rcnt = take((uint64_t)(ns ? ns : 1) * (rec_cap + 1) * 4);
   v.hoff = take((uint64_t)(ns ? ns : 1) * (rec_cap + 1) * 8);
@@ -1154,10 +1338,11 @@ static VecBufs vec_bufs(uint8_t *ws, const VecWs &v) {
   B.T = reinterpret_cast<uint64_t *>(ws + v.T);
   B.cnt = reinterpret_cast<uint32_t *>(ws + v.cnt);
   B.base = reinterpret_cast<uint64_t *>(ws + v.base);
-  B.unver = reinterpret_cast<uint32_t *>(ws + v.unver);
+  B.wl = reinterpret_cast<uint32_t *>(ws + v.wl);
   B.exitp = reinterpret_cast<uint64_t *>(ws + v.exitp);
   B.used = reinterpret_cast<uint64_t *>(ws + v.used);
   B.dirty = reinterpret_cast<uint32_t *>(ws + v.dirty);
+  B.mj = reinterpret_cast<uint32_t *>(ws + v.mj);
   B.starts = reinterpret_cast<uint64_t *>(ws + v.starts);
   B.rcnt = reinterpret_cast<uint32_t *>(ws + v.rcnt);
   B.hoff = reinterpret_cast<uint64_t *>(ws + v.hoff);
@@ -1187,15 +1372,12 @@ static hipError_t launch_vec_decode_ns(const DecArgs &a, const WalkProg &P, cons
     return e;
   hipLaunchKernelGGL(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, v.lp);
   const unsigned cg = grid_for(v.nch, 256);
-  hipLaunchKernelGGL(vec_spec<NS>, dim3(cg), dim3(256), 0, s, a, P, wire, ws, B);
-  uint32_t *dA = B.dirty, *dB = B.dirty + v.nch;
-  for (int r = 0; r < kRounds; ++r) {
-    uint32_t *din = (r & 1) ? dB : dA, *dout = (r & 1) ? dA : dB;
-    if ((e = hipMemsetAsync(dout, 0, v.nch * 4, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(vec_verify_round<NS>, dim3(cg), dim3(256), 0, s, a, P, wire, ws, B, r,
-                       (const uint32_t *)din, dout, r == kRounds - 1 ? 1 : 0);
-  }
-  hipLaunchKernelGGL(vec_fixup<NS>, dim3(1), dim3(64), 0, s, a, P, wire, ws, B);
+  hipLaunchKernelGGL(vec_spec<NS>, dim3(grid_for(v.nch, 64 * kSpecWaves)), dim3(64 * kSpecWaves), 0,
+                     s, a, P, wire, ws, B);
+  hipLaunchKernelGGL(vec_verify0<NS>, dim3(cg), dim3(256), 0, s, a, P, wire, ws, B);
+  for (uint32_t r = 1; r < (uint32_t)kRounds; ++r)
+    hipLaunchKernelGGL(vec_verify_round<NS>, dim3(64), dim3(256), 0, s, a, P, wire, ws, B, r);
+  hipLaunchKernelGGL(vec_fixup<NS>, dim3(1), dim3(1024), 0, s, a, P, wire, ws, B);
   hipLaunchKernelGGL(vec_term_min, dim3(cg), dim3(256), 0, s, ws, B);
   hipLaunchKernelGGL(vec_term_zero, dim3(cg), dim3(256), 0, s, ws, B);
   uint64_t *tot = reinterpret_cast<uint64_t *>(ws + v.tot);
