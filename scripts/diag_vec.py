@@ -49,3 +49,11 @@ print(f"chunks whose spec entry was wrong (re-walked): {int(wrongE.sum())}")
 bad = np.nonzero(miss)[0][:5] + 1
 for c in bad:
     print("chunk", c, "cs", cs[c], "used", int(used[c]), "E_prev", (cs[c-1] + E[c-1, :En[c-1]]).tolist(), "P", (cs[c] + P[c, :Pn[c]]).tolist())
+# chunks left for the sequential fixup (final worklist, parity kRounds & 1 = 0)
+olist = ounv
+fin = ws[olist:olist + int(wl[-1]) * 4].view(np.uint32)
+exitp = ws[oex:oex + nch * 8].view(np.uint64)
+print("fixup list:", fin.tolist())
+for c in sorted(fin.tolist())[:6]:
+    print("  chunk", c, "cs", cs[c], "used", int(used[c]), "exit_prev", int(exitp[c-1]), "exit", int(exitp[c]),
+          "En_prev", int(En[c-1]), "E_prev", (cs[c-1] + E[c-1, :En[c-1]]).tolist(), "P", (cs[c] + P[c, :Pn[c]]).tolist(), "flags", int(fl[c]))

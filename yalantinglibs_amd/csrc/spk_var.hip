@@ -41,7 +41,6 @@ namespace spk {
 constexpr int kThreads = 256;
 constexpr int kIPT = 4;                     // records per thread (encode)
 constexpr uint64_t kRPB = kThreads * kIPT;  // records per block (encode)
-constexpr uint32_t kWin = 40 * 1024;        // LDS assembly window (bytes)
 
 struct VarArgs {
   KLayout L;
@@ -71,6 +70,38 @@ __device__ __forceinline__ uint32_t rec_u32(const uint8_t *rec, uint32_t off) {
 }
 __device__ __forceinline__ uint64_t rec_u64(const uint8_t *rec, uint32_t off) {
   return *reinterpret_cast<const uint64_t *>(rec + off);
+}
+
+typedef uint16_t u16_unaligned __attribute__((aligned(1)));
+typedef uint32_t u32_unaligned __attribute__((aligned(1)));
+typedef uint64_t u64_unaligned __attribute__((aligned(1)));
+typedef uint32_t v4u_t __attribute__((ext_vector_type(4)));
+typedef v4u_t v4u_una __attribute__((aligned(1)));
+
+// unaligned byte copy in 16/8/4/1-byte pieces (gfx950 runs in unaligned mode)
+__device__ __forceinline__ void copy_bytes(uint8_t *d, const uint8_t *s, uint64_t n) {
+  uint64_t i = 0;
+  for (; i + 16 <= n; i += 16)
+    *reinterpret_cast<v4u_una *>(d + i) = *reinterpret_cast<const v4u_una *>(s + i);
+  if (n - i >= 8) {
+    *reinterpret_cast<u64_unaligned *>(d + i) = *reinterpret_cast<const u64_unaligned *>(s + i);
+    i += 8;
+  }
+  if (n - i >= 4) {
+    *reinterpret_cast<u32_unaligned *>(d + i) = *reinterpret_cast<const u32_unaligned *>(s + i);
+    i += 4;
+  }
+  for (; i < n; ++i) d[i] = s[i];
+}
+
+// little-endian w-byte store (unaligned)
+__device__ __forceinline__ void store_le(uint8_t *d, uint64_t v, uint32_t w) {
+  switch (w) {
+    case 1: *d = (uint8_t)v; break;
+    case 2: *reinterpret_cast<u16_unaligned *>(d) = (uint16_t)v; break;
+    case 4: *reinterpret_cast<u32_unaligned *>(d) = (uint32_t)v; break;
+    default: *reinterpret_cast<u64_unaligned *>(d) = v; break;
+  }
 }
 
 // w-independent bytes of one record (fixed + span payloads) and its max count
@@ -235,142 +266,78 @@ __global__ void write_msg_hdrs(MsgHdrTable t, uint8_t *ws) {
   if (threadIdx.x < 4) ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + threadIdx.x] = t.len[threadIdx.x];
 }
 
-// LDS window writer ----------------------------------------------------------
-struct Win {
-  uint8_t *lds;
-  uint64_t lo, hi;  // global byte range currently held [lo, hi)
-};
-
-__device__ __forceinline__ void win_put_bytes_global(const Win &W, uint64_t pos,
-                                                     const uint8_t *src, uint64_t len) {
-  uint64_t a = pos > W.lo ? pos : W.lo;
-  uint64_t b = pos + len < W.hi ? pos + len : W.hi;
-  for (uint64_t x = a; x < b; ++x) W.lds[x - W.lo] = src[x - pos];
-}
-__device__ __forceinline__ void win_put_le(const Win &W, uint64_t pos, uint64_t v,
-                                           uint32_t w) {
-  for (uint32_t i = 0; i < w; ++i) {
-    const uint64_t x = pos + i;
-    if (x >= W.lo && x < W.hi) W.lds[x - W.lo] = (uint8_t)(v >> (8 * i));
-  }
-}
-
-// emit one record at global position pos (width w) into the window
-__device__ void emit_record(const VarArgs &a, const uint8_t *rec, uint32_t w,
-                            uint64_t pos, const Win &W) {
+// one record at output position pos (width w), written straight to HBM
+__device__ __forceinline__ void put_record(const VarArgs &a, const uint8_t *rec, uint32_t w,
+                                           uint64_t pos, uint8_t *out) {
   uint32_t sk = 0;
   for (uint32_t o = 0; o < a.L.n_ops; ++o) {
     const spk_op op = a.L.ops[o];
     if (op.kind == SPK_OP_COPY) {
-      win_put_bytes_global(W, pos, rec + op.rec_off, op.size);
+      copy_bytes(out + pos, rec + op.rec_off, op.size);
       pos += op.size;
     } else {
       const uint64_t c = rec_u32(rec, op.rec_off);
-      win_put_le(W, pos, c, w);
+      store_le(out + pos, c, w);
       pos += w;
       const uint64_t nb = c * op.size;
-      if (nb) {
-        const uint8_t *src = a.heaps[sk] + rec_u64(rec, op.aux) * op.size;
-        win_put_bytes_global(W, pos, src, nb);
-      }
+      if (nb) copy_bytes(out + pos, a.heaps[sk] + rec_u64(rec, op.aux) * op.size, nb);
       pos += nb;
       ++sk;
     }
   }
 }
 
+// Write pass: one record per lane, consecutive lanes on consecutive records
+// (so a wave's stores cover one contiguous stretch of the output), byte
+// offsets from a block scan per round on top of the block's planned base.
 __global__ __launch_bounds__(kThreads) void var_encode_write(
     VarArgs a, const uint8_t *__restrict__ recs, uint8_t *__restrict__ out,
     uint64_t out_cap, const uint8_t *__restrict__ ws,
     const spk_plan_t *__restrict__ plan, uint64_t *__restrict__ offs) {
-  extern __shared__ __align__(16) uint8_t lds[];
   __shared__ uint64_t sh[kThreads / 64];
-  __shared__ uint64_t s_g0, s_tot;
   const uint64_t total = plan->total_bytes;
   if (total > out_cap) return;  // caller reads plan->total_bytes
   const uint32_t w_vec = plan->width;
   const uint32_t hdr_vec = plan->header_bytes;
   const Partial *part = reinterpret_cast<const Partial *>(ws + kWsScratch);
   const uint64_t r0 = (uint64_t)blockIdx.x * kRPB;
-  // this thread's records are contiguous: r0 + t*kIPT + j (output contiguity)
-  const uint64_t t0 = r0 + (uint64_t)threadIdx.x * kIPT;
-  uint64_t sz[kIPT];
-  uint32_t wr[kIPT];
-  uint64_t tsum = 0;
-  for (int j = 0; j < kIPT; ++j) {
-    const uint64_t i = t0 + j;
-    sz[j] = 0;
-    wr[j] = 1;
-    if (i < a.n) {
-      uint64_t var, maxc;
-      rec_sizes(a.L, recs + i * a.L.stride, var, maxc);
-      if (a.mode == SPK_MODE_VECTOR) {
-        wr[j] = w_vec;
-        sz[j] = var + (uint64_t)a.L.n_spans * w_vec;
-      } else {
-        wr[j] = width_of(maxc);
-        sz[j] = ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + wlog(wr[j])] + var +
-                (uint64_t)a.L.n_spans * wr[j];
-      }
-    }
-    tsum += sz[j];
-  }
-  uint64_t btot;
-  const uint64_t toff = block_excl_scan(tsum, &btot, sh);
-  if (threadIdx.x == 0) {
-    s_g0 = a.mode == SPK_MODE_VECTOR
-               ? hdr_vec + part[blockIdx.x].sum + r0 * (uint64_t)a.L.n_spans * w_vec
-               : part[blockIdx.x].sum;
-    s_tot = btot;
-  }
-  __syncthreads();
-  const uint64_t g0 = s_g0, g1 = s_g0 + s_tot;
+  uint64_t g = a.mode == SPK_MODE_VECTOR
+                   ? hdr_vec + part[blockIdx.x].sum + r0 * (uint64_t)a.L.n_spans * w_vec
+                   : part[blockIdx.x].sum;
   if (a.mode == SPK_MODE_VECTOR && blockIdx.x == 0)
     for (uint32_t i = threadIdx.x; i < hdr_vec; i += blockDim.x) out[i] = ws[kWsHdrVec + i];
-  if (a.mode == SPK_MODE_MESSAGES && offs) {
-    uint64_t p = g0 + toff;
-    for (int j = 0; j < kIPT; ++j) {
-      if (t0 + j < a.n) offs[t0 + j] = p;
-      p += sz[j];
-    }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) offs[a.n] = total;
-  }
-  if (g1 == g0) return;
-  const uint64_t abase = g0 & ~15ull;
-  for (uint64_t wlo = abase; wlo < g1; wlo += kWin) {
-    Win W{lds, wlo, wlo + kWin < g1 ? wlo + kWin : g1};
-    uint64_t p = g0 + toff;
-    if (p < W.hi && p + tsum > W.lo) {
-      for (int j = 0; j < kIPT; ++j) {
-        const uint64_t i = t0 + j;
-        if (i >= a.n) break;
-        if (p < W.hi && p + sz[j] > W.lo) {
-          uint64_t q = p;
-          if (a.mode == SPK_MODE_MESSAGES) {
-            const uint32_t s = wlog(wr[j]);
-            const uint32_t hl = ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + s];
-            win_put_bytes_global(W, q, ws + kWsHdrMsg + s * kWsHdrSlot, hl);
-            q += hl;
-          }
-          emit_record(a, recs + i * a.L.stride, wr[j], q, W);
-        }
-        p += sz[j];
-      }
-    }
-    __syncthreads();
-    // flush [max(W.lo,g0), W.hi): aligned 16-B chunks, bytes at the edges
-    for (uint64_t c = W.lo + (uint64_t)threadIdx.x * 16; c < W.hi; c += kThreads * 16) {
-      const uint64_t lo = c > g0 ? c : g0;
-      const uint64_t hi = c + 16 < W.hi ? c + 16 : W.hi;
-      if (lo == c && hi == c + 16) {
-        *reinterpret_cast<uint4 *>(out + c) =
-            *reinterpret_cast<const uint4 *>(lds + (c - W.lo));
+  for (int j = 0; j < kIPT; ++j) {
+    if (r0 + (uint64_t)j * kThreads >= a.n) break;  // block-uniform
+    const uint64_t i = r0 + (uint64_t)j * kThreads + threadIdx.x;
+    const uint8_t *rec = recs + i * a.L.stride;
+    uint64_t sz = 0;
+    uint32_t w = w_vec;
+    if (i < a.n) {
+      uint64_t var, maxc;
+      rec_sizes(a.L, rec, var, maxc);
+      if (a.mode == SPK_MODE_VECTOR) {
+        sz = var + (uint64_t)a.L.n_spans * w_vec;
       } else {
-        for (uint64_t x = lo; x < hi; ++x) out[x] = lds[x - W.lo];
+        w = width_of(maxc);
+        sz = ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + wlog(w)] + var + (uint64_t)a.L.n_spans * w;
       }
     }
-    __syncthreads();
+    uint64_t btot;
+    const uint64_t p = g + block_excl_scan(sz, &btot, sh);
+    g += btot;
+    if (i >= a.n) continue;
+    uint64_t q = p;
+    if (a.mode == SPK_MODE_MESSAGES) {
+      if (offs) offs[i] = p;
+      const uint32_t sl = wlog(w);
+      const uint32_t hl = ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + sl];
+      copy_bytes(out + q, ws + kWsHdrMsg + sl * kWsHdrSlot, hl);
+      q += hl;
+    }
+    put_record(a, rec, w, q, out);
   }
+  if (a.mode == SPK_MODE_MESSAGES && offs && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+    offs[a.n] = total;
 }
 
 // ===========================================================================
@@ -411,7 +378,7 @@ __device__ void decode_record(const KLayout &L, const uint8_t *wire, uint64_t po
   for (uint32_t o = 0; o < L.n_ops; ++o) {
     const spk_op op = L.ops[o];
     if (op.kind == SPK_OP_COPY) {
-      for (uint32_t b = 0; b < op.size; ++b) rec[op.rec_off + b] = wire[pos + b];
+      copy_bytes(rec + op.rec_off, wire + pos, op.size);
       pos += op.size;
     } else {
       const uint64_t c = ld_le(wire + pos, w);
@@ -419,8 +386,7 @@ __device__ void decode_record(const KLayout &L, const uint8_t *wire, uint64_t po
       *reinterpret_cast<uint32_t *>(rec + op.rec_off) = (uint32_t)c;
       *reinterpret_cast<uint64_t *>(rec + op.aux) = heap_off[sk];
       const uint64_t nb = c * op.size;
-      uint8_t *dst = heaps[sk] + heap_off[sk] * op.size;
-      for (uint64_t b = 0; b < nb; ++b) dst[b] = wire[pos + b];
+      copy_bytes(heaps[sk] + heap_off[sk] * op.size, wire + pos, nb);
       pos += nb;
       ++sk;
     }
@@ -616,6 +582,8 @@ struct VCtl {
   uint32_t term_chunk;  // first chunk where the true path terminates (kNone32)
   uint32_t overflow;    // a P list overflowed (records < 1 B impossible; guard)
   uint32_t wl_n[kRounds + 1];  // re-verification worklist length per round
+  uint32_t pad_;
+  uint64_t cap;                // chunk capacity: stride of the per-span chunk arrays
 };
 
 // Compact walk program of a record: fixed bytes, then per span
@@ -646,8 +614,6 @@ static WalkProg make_walkprog(const spk_layout *L) {
   return p;
 }
 
-typedef uint32_t u32_unaligned __attribute__((aligned(1)));
-typedef uint64_t u64_unaligned __attribute__((aligned(1)));
 
 // little-endian w-byte count at wire[x] (x + w <= len checked by the caller)
 __device__ __forceinline__ uint64_t wire_le(const uint8_t *wire, uint64_t x, uint32_t w) {
@@ -663,7 +629,7 @@ __device__ __forceinline__ uint64_t wire_le(const uint8_t *wire, uint64_t x, uin
 // with no_buffer_space). NS > 0: compile-time span count.
 template <int NS>
 __device__ __forceinline__ uint64_t wlen(const WalkProg &P, const uint8_t *wire, uint64_t len,
-                                         uint64_t pos, uint32_t w, uint32_t *cnt) {
+                                         uint64_t pos, uint32_t w) {
   uint64_t p = pos + P.skip[0];
   const uint32_t ns = NS > 0 ? (uint32_t)NS : P.ns;
 #pragma unroll
@@ -678,15 +644,47 @@ __device__ __forceinline__ uint64_t wlen(const WalkProg &P, const uint8_t *wire,
       if (nb > len - p) return 0;
       p += nb;
     }
-    if (cnt) cnt[k] = (uint32_t)c;  // device records hold u32 counts
     p += P.skip[k + 1];
   }
   if (p > len) return 0;
   return p - pos;
 }
 
+// wlen() with the count fields read through `rd`
+template <int NS, typename Rd>
+__device__ __forceinline__ uint64_t wlen_rd(const WalkProg &P, const Rd &rd, uint64_t len,
+                                            uint64_t pos, uint32_t w, uint64_t *cnt = nullptr) {
+  uint64_t p = pos + P.skip[0];
+  const uint32_t ns = NS > 0 ? (uint32_t)NS : P.ns;
+#pragma unroll
+  for (uint32_t k = 0; k < (NS > 0 ? (uint32_t)NS : SPK_MAX_SPANS); ++k) {
+    if (NS == 0 && k >= ns) break;
+    if (p + w > len) return 0;
+    const uint64_t c = rd(p);
+    p += w;
+    if (c) {
+      if (c > P.cmax[k]) return 0;
+      const uint64_t nb = c * P.esz[k];
+      if (nb > len - p) return 0;
+      p += nb;
+    }
+    if (cnt) cnt[k] = c;
+    p += P.skip[k + 1];
+  }
+  if (p > len) return 0;
+  return p - pos;
+}
+
+// count-field reader straight from the wire (global memory)
+struct GReader {
+  const uint8_t *wire;
+  uint32_t w;
+  __device__ __forceinline__ uint64_t operator()(uint64_t x) const { return wire_le(wire, x, w); }
+};
+
 __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
-                               uint8_t *__restrict__ ws, spk_dresult_t *res, uint32_t lp) {
+                               uint8_t *__restrict__ ws, spk_dresult_t *res, uint32_t lp,
+                               uint64_t cap) {
   if (threadIdx.x != 0) return;
   VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
   uint64_t pos, dl;
@@ -716,6 +714,7 @@ __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
   c->end_pos = 0;
   c->total = 0;
   c->lp = lp;
+  c->cap = cap;
   c->n_unver = 0;
   for (int r = 0; r <= kRounds; ++r) c->wl_n[r] = 0;
   c->term_chunk = kNone32;
@@ -744,14 +743,12 @@ struct VecBufs {
   uint32_t *dirty;  // [2][nchunks] round a chunk is listed for (alternating)
   uint32_t *mj;     // [nchunks] P index where the true path meets the spec walk
                     //           | records walked before it << 16
-  uint64_t *starts; // [rec_cap]
-  uint32_t *rcnt;   // [n_spans][rec_cap] span counts per record
-  uint64_t *hoff;   // [n_spans][rec_cap] heap element offsets per record
+  uint64_t *psum;   // [n_spans][nchunks] span-count sums over the spec walk's records
+  uint64_t *hs;     // [n_spans][nchunks] span-count sums over the chunk's true records
+  uint64_t *hb;     // [n_spans][nchunks] heap element offset of the chunk's first record
   uint64_t *scan;   // block sums for the device-wide scans
 };
 
-typedef uint32_t v4u_t __attribute__((ext_vector_type(4)));
-typedef v4u_t v4u_una __attribute__((aligned(1)));
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 // Count-field reader over a chunk's LDS window: bytes [cs, wend) of the wire
@@ -774,30 +771,6 @@ struct WinReader {
     return wire_le(wire, x, w);
   }
 };
-
-// wlen() with the count fields read through `rd`
-template <int NS, typename Rd>
-__device__ __forceinline__ uint64_t wlen_rd(const WalkProg &P, const Rd &rd, uint64_t len,
-                                            uint64_t pos, uint32_t w) {
-  uint64_t p = pos + P.skip[0];
-  const uint32_t ns = NS > 0 ? (uint32_t)NS : P.ns;
-#pragma unroll
-  for (uint32_t k = 0; k < (NS > 0 ? (uint32_t)NS : SPK_MAX_SPANS); ++k) {
-    if (NS == 0 && k >= ns) break;
-    if (p + w > len) return 0;
-    const uint64_t c = rd(p);
-    p += w;
-    if (c) {
-      if (c > P.cmax[k]) return 0;
-      const uint64_t nb = c * P.esz[k];
-      if (nb > len - p) return 0;
-      p += nb;
-    }
-    p += P.skip[k + 1];
-  }
-  if (p > len) return 0;
-  return p - pos;
-}
 
 constexpr uint32_t kRegion = 64 * kSpec;                    // chunk bytes per wave
 constexpr uint32_t kRegionVec = (kRegion + kWinExtra) / 16;  // 16-B LDS slots per wave
@@ -858,6 +831,9 @@ __global__ __launch_bounds__(64 * kSpecWaves) void vec_spec(DecArgs a, WalkProg 
   // 8 candidate start bytes are screened per iteration on their first count.
   uint64_t t = 0, x = cs;
   bool searching = ch != 0, done = false;
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  uint64_t ps[NS > 0 ? NS : SPK_MAX_SPANS];
+  for (uint32_t k = 0; k < nsp; ++k) ps[k] = 0;
   const uint32_t s0 = P.skip[0];
   while (!done) {
     if (searching) {
@@ -897,9 +873,11 @@ __global__ __launch_bounds__(64 * kSpecWaves) void vec_spec(DecArgs a, WalkProg 
       t += (uint32_t)__builtin_ctz(m);
       x = cs + t;
       np = ne = 0;
+      for (uint32_t k = 0; k < nsp; ++k) ps[k] = 0;
       searching = false;
     }
-    const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w) : 0;
+    uint64_t rc[NS > 0 ? NS : SPK_MAX_SPANS];
+    const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w, rc) : 0;
     if (ch != 0 && ((L == 0 && x < len) || L > kPlaus)) {  // off the record grid
       t += 1;
       searching = true;
@@ -909,6 +887,8 @@ __global__ __launch_bounds__(64 * kSpecWaves) void vec_spec(DecArgs a, WalkProg 
     if (x < ce) {
       if (np < lp) Pl[np] = (uint16_t)(x - cs);
       ++np;
+      if (L)
+        for (uint32_t k = 0; k < nsp; ++k) ps[k] += rc[k];
     } else {
       El[ne++] = (x - cs) < 0xFFFFFFFFull ? (uint32_t)(x - cs) : 0xFFFFFFFEu;
     }
@@ -929,6 +909,7 @@ __global__ __launch_bounds__(64 * kSpecWaves) void vec_spec(DecArgs a, WalkProg 
   B.flags[ch] = fl;
   B.dirty[ch] = kNone32;
   B.dirty[nch + ch] = kNone32;
+  for (uint32_t k = 0; k < nsp; ++k) B.psum[k * c->cap + ch] = searching ? 0 : ps[k];
 }
 
 constexpr uint64_t kTermPos = ~0ull;  // "the true path ended before this chunk"
@@ -941,7 +922,9 @@ template <int NS>
 __device__ void walk_chunk(const DecArgs &a, const WalkProg &P, const uint8_t *wire,
                            const VCtl *c, const VecBufs &B, uint64_t ch, uint64_t entry,
                            uint64_t *exit, uint32_t *count, uint32_t *flags, uint64_t *T,
-                           uint32_t *mj) {
+                           uint32_t *mj, uint64_t *hs) {
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  for (uint32_t q = 0; q < nsp; ++q) hs[q] = 0;
   const uint64_t len = a.wire_len;
   const uint64_t cs = c->p0 + ch * kSpec;
   const uint64_t ce = cs + kSpec < len ? cs + kSpec : len;
@@ -967,12 +950,14 @@ __device__ void walk_chunk(const DecArgs &a, const WalkProg &P, const uint8_t *w
       merged = true;
       break;
     }
-    const uint64_t L = pos < len ? wlen<NS>(P, wire, len, pos, c->w, (uint32_t *)nullptr) : 0;
+    uint64_t rc[SPK_MAX_SPANS];
+    const uint64_t L = pos < len ? wlen_rd<NS>(P, GReader{wire, c->w}, len, pos, c->w, rc) : 0;
     if (!L) {
       term = true;
       break;
     }
     ++k;
+    for (uint32_t q = 0; q < nsp; ++q) hs[q] += rc[q];
     pos += L;
   }
   const uint32_t k0 = k;  // records walked before the meeting point
@@ -981,6 +966,15 @@ __device__ void walk_chunk(const DecArgs &a, const WalkProg &P, const uint8_t *w
     if (walk_term && en == 0) {  // the merged walk ends inside this chunk
       k -= 1;
       term = true;
+    }
+    if (j == 0) {  // the whole spec walk is true: its count sums hold
+      for (uint32_t q = 0; q < nsp; ++q) hs[q] += B.psum[q * c->cap + ch];
+    } else {
+      for (uint32_t i = j; i < np; ++i) {
+        uint64_t rc[SPK_MAX_SPANS];
+        if (wlen_rd<NS>(P, GReader{wire, c->w}, len, cs + Pl[i], c->w, rc))
+          for (uint32_t q = 0; q < nsp; ++q) hs[q] += rc[q];
+      }
     }
   }
   if (term) {
@@ -1011,9 +1005,11 @@ __device__ __forceinline__ void verify_chunk(const DecArgs &a, const WalkProg &P
                                              const uint8_t *wire, VCtl *c, const VecBufs &B,
                                              uint64_t ch, uint64_t entry, uint64_t next_used,
                                              uint32_t r) {
-  uint64_t exit, T;
+  uint64_t exit, T, hs[SPK_MAX_SPANS];
   uint32_t count, flags, mj;
-  walk_chunk<NS>(a, P, wire, c, B, ch, entry, &exit, &count, &flags, &T, &mj);
+  walk_chunk<NS>(a, P, wire, c, B, ch, entry, &exit, &count, &flags, &T, &mj, hs);
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  for (uint32_t q = 0; q < nsp; ++q) B.hs[q * c->cap + ch] = hs[q];
   B.mj[ch] = mj;
   B.used[ch] = entry;
   B.exitp[ch] = exit;
@@ -1128,17 +1124,21 @@ __global__ void vec_term_min(uint8_t *__restrict__ ws, const VecBufs B) {
   const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (ch < c->nchunks && (B.flags[ch] & kTerm)) atomicMin(&c->term_chunk, (uint32_t)ch);
 }
-__global__ void vec_term_zero(uint8_t *__restrict__ ws, VecBufs B) {
+__global__ void vec_term_zero(uint8_t *__restrict__ ws, VecBufs B, uint32_t ns) {
   VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
   const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch < c->nchunks && c->term_chunk != kNone32 && ch > c->term_chunk) B.cnt[ch] = 0;
+  if (ch < c->nchunks && c->term_chunk != kNone32 && ch > c->term_chunk) {
+    B.cnt[ch] = 0;
+    for (uint32_t q = 0; q < ns; ++q) B.hs[q * c->cap + ch] = 0;
+  }
 }
 
 // ---- device-wide exclusive scan u32 -> u64 (3 phases) ----------------------
 constexpr uint32_t kScanIPT = 16;
 constexpr uint64_t kScanBlock = 256ull * kScanIPT;
 
-__global__ __launch_bounds__(256) void scan_reduce(const uint32_t *__restrict__ in, uint64_t n,
+template <typename In>
+__global__ __launch_bounds__(256) void scan_reduce(const In *__restrict__ in, uint64_t n,
                                                    uint64_t *__restrict__ bsum) {
   __shared__ uint64_t sh[4];
   const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock;
@@ -1169,14 +1169,15 @@ __global__ __launch_bounds__(1024) void scan_blocks(uint64_t *__restrict__ bsum,
   if (threadIdx.x == 0 && total) *total = carry;
 }
 
-__global__ __launch_bounds__(256) void scan_apply(const uint32_t *__restrict__ in, uint64_t n,
+template <typename In>
+__global__ __launch_bounds__(256) void scan_apply(const In *__restrict__ in, uint64_t n,
                                                   const uint64_t *__restrict__ bsum,
                                                   uint64_t *__restrict__ out) {
   __shared__ uint64_t sh[4];
   // thread t handles kScanIPT consecutive elements
   const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock;
   const uint64_t i0 = b0 + (uint64_t)threadIdx.x * kScanIPT;
-  uint32_t v[kScanIPT];
+  In v[kScanIPT];
   uint64_t s = 0;
 #pragma unroll
   for (uint32_t j = 0; j < kScanIPT; ++j) {
@@ -1202,37 +1203,34 @@ __global__ void vec_count_check(uint8_t *__restrict__ ws, const uint64_t *__rest
   if (c->n && *total < c->n) res->errc = SPK_ERRC_NO_BUFFER_SPACE;
 }
 
-// one lane per chunk: place the chunk's true records (index base..): the
-// records before the meeting point are walked from T, the rest are the
-// chunk's P entries from the meeting index on (independent loads)
+// The chunk holding record n-1 (one lane): the message end (consume_len)
+// and the heap elements used by records 0..n-1, for the capacity checks.
 template <int NS>
-__global__ __launch_bounds__(256) void vec_place(DecArgs a, WalkProg P,
+__global__ __launch_bounds__(256) void vec_total(DecArgs a, WalkProg P,
                                                  const uint8_t *__restrict__ wire,
                                                  uint8_t *__restrict__ ws, VecBufs B,
-                                                 const spk_dresult_t *res) {
+                                                 uint64_t *heap_tot) {
   VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
   const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= c->nchunks || c->errc || res->errc) return;
+  if (ch >= c->nchunks || c->errc) return;
   const uint64_t n = c->n, base = B.base[ch];
   const uint32_t k = B.cnt[ch];
-  if (!k || base >= n) return;
-  const uint32_t w = c->w, mj = B.mj[ch];
-  const uint32_t k0 = mj >> 16, j0 = mj & 0xFFFFu;
+  if (!n || !k || n - 1 < base || n - 1 >= base + k) return;
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  uint64_t h[SPK_MAX_SPANS];
+  for (uint32_t q = 0; q < nsp; ++q) h[q] = B.hb[q * c->cap + ch];
+  const uint32_t mj = B.mj[ch], k0 = mj >> 16, j0 = mj & 0xFFFFu;
   const uint64_t cs = c->p0 + ch * kSpec;
   const uint16_t *Pl = B.P + ch * c->lp;
   uint64_t pos = B.T[ch];
-  uint32_t cnt[SPK_MAX_SPANS];
-  for (uint32_t r = 0; r < k && base + r < n; ++r) {
+  for (uint32_t r = 0; r <= n - 1 - base; ++r) {
     if (r >= k0) pos = cs + Pl[j0 + (r - k0)];
-    const uint64_t L = wlen<NS>(P, wire, a.wire_len, pos, w, cnt);
-    const uint64_t i = base + r;
-    if (i < a.rec_cap) {
-      B.starts[i] = pos;
-      for (uint32_t s = 0; s < P.ns; ++s) B.rcnt[(uint64_t)s * a.rec_cap + i] = cnt[s];
-    }
-    pos += L;
-    if (i + 1 == n) c->end_pos = pos;
+    uint64_t rc[SPK_MAX_SPANS];
+    pos += wlen_rd<NS>(P, GReader{wire, c->w}, a.wire_len, pos, c->w, rc);
+    for (uint32_t q = 0; q < nsp; ++q) h[q] += rc[q];
   }
+  c->end_pos = pos;
+  for (uint32_t q = 0; q < nsp; ++q) heap_tot[q] = h[q];
 }
 
 __global__ void vec_finish(DecArgs a, uint8_t *__restrict__ ws, spk_dresult_t *res,
@@ -1258,20 +1256,104 @@ __global__ void vec_finish(DecArgs a, uint8_t *__restrict__ ws, spk_dresult_t *r
   *res = r;
 }
 
-// thread per record: decode from its start with precomputed heap offsets
-__global__ __launch_bounds__(256) void vec_decode(DecArgs a, const uint8_t *__restrict__ wire,
-                                                  const uint8_t *__restrict__ ws, VecBufs B,
-                                                  uint8_t *__restrict__ recs,
-                                                  const spk_dresult_t *res) {
+// decode_record with piecewise copies; off[k] = heap element offset of span k
+__device__ __forceinline__ void emit_record(const KLayout &L, const uint8_t *wire, uint64_t pos,
+                                            uint32_t w, uint8_t *rec, uint8_t *const *heaps,
+                                            const uint64_t *off) {
+  uint32_t sk = 0;
+  for (uint32_t o = 0; o < L.n_ops; ++o) {
+    const spk_op op = L.ops[o];
+    if (op.kind == SPK_OP_COPY) {
+      copy_bytes(rec + op.rec_off, wire + pos, op.size);
+      pos += op.size;
+    } else {
+      const uint64_t cnt = wire_le(wire, pos, w);
+      pos += w;
+      *reinterpret_cast<uint32_t *>(rec + op.rec_off) = (uint32_t)cnt;
+      *reinterpret_cast<uint64_t *>(rec + op.aux) = off[sk];
+      const uint64_t nb = cnt * op.size;
+      copy_bytes(heaps[sk] + off[sk] * op.size, wire + pos, nb);
+      pos += nb;
+      ++sk;
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t wave_excl_scan_u64(uint64_t v, uint32_t lane, uint64_t *tot) {
+  uint64_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d);
+    if (lane >= (uint32_t)d) x += y;
+  }
+  *tot = __shfl(x, 63);
+  return x - v;
+}
+
+// One wave per group of G chunks: the group's true record starts go to an
+// LDS table (P entries from the meeting index on, plus any records walked
+// before it), then lanes take 64 consecutive records at a time, scan their
+// span counts across the wave for heap offsets (group base from the chunk
+// scan) and write the device records and heap bytes.
+constexpr uint32_t kEmitRecs = 4096;  // record slots per wave
+constexpr uint32_t kEmitWaves = 4;
+template <int NS>
+__global__ __launch_bounds__(64 * kEmitWaves) void vec_emit(DecArgs a, WalkProg P,
+                                                            const uint8_t *__restrict__ wire,
+                                                            const uint8_t *__restrict__ ws,
+                                                            VecBufs B, uint8_t *__restrict__ recs,
+                                                            const spk_dresult_t *res, uint32_t G) {
+  __shared__ uint16_t tab_s[kEmitWaves][kEmitRecs];
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   if (c->errc || res->errc) return;
-  const uint64_t n = c->n;
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t nch = c->nchunks;
+  const uint64_t g0 = ((uint64_t)blockIdx.x * kEmitWaves + wv) * G;
+  if (g0 >= nch) return;  // wave-uniform
+  const uint64_t n = c->n, R0 = B.base[g0];
+  if (R0 >= n) return;
+  const uint64_t gend = g0 + G < nch ? g0 + G : nch;
+  uint64_t R1 = B.base[gend - 1] + B.cnt[gend - 1];
+  if (R1 > n) R1 = n;
   const uint32_t w = c->w;
-  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gs) {
-    uint64_t hoff[SPK_MAX_SPANS];
-    for (uint32_t k = 0; k < a.L.n_spans; ++k) hoff[k] = B.hoff[(uint64_t)k * a.rec_cap + i];
-    decode_record(a.L, wire, B.starts[i], w, recs + i * a.L.stride, a.heaps, hoff);
+  const uint64_t gs = c->p0 + g0 * kSpec;
+  uint16_t *tab = tab_s[wv];
+  if (lane < gend - g0) {
+    const uint64_t ch = g0 + lane, base = B.base[ch];
+    const uint32_t k = B.cnt[ch];
+    const uint64_t lim = R1 > base ? (R1 - base < k ? R1 - base : k) : 0;
+    const uint32_t mj = B.mj[ch], k0 = mj >> 16, j0 = mj & 0xFFFFu;
+    const uint16_t *Pl = B.P + ch * c->lp;
+    const uint16_t rel = (uint16_t)(ch - g0) * (uint16_t)kSpec;
+    uint16_t *dst = tab + (base - R0);
+    uint64_t pos = B.T[ch];
+    uint32_t r = 0;
+    for (; r < k0 && r < lim; ++r) {  // records before the meeting point
+      dst[r] = (uint16_t)(pos - gs);
+      pos += wlen<NS>(P, wire, a.wire_len, pos, w);
+    }
+    for (; r < lim; ++r) dst[r] = (uint16_t)(rel + Pl[j0 + (r - k0)]);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : a.L.n_spans;
+  uint64_t carry[NS > 0 ? NS : SPK_MAX_SPANS];
+  for (uint32_t q = 0; q < nsp; ++q) carry[q] = B.hb[q * c->cap + g0];
+  const uint64_t nrec = R1 - R0;
+  for (uint64_t i0 = 0; i0 < nrec; i0 += 64) {
+    const uint64_t i = i0 + lane;
+    const bool act = i < nrec;
+    const uint64_t pos = gs + (act ? tab[i] : 0);
+    uint64_t rc[SPK_MAX_SPANS] = {};
+    if (act) wlen_rd<NS>(P, GReader{wire, w}, a.wire_len, pos, w, rc);
+    uint64_t off[SPK_MAX_SPANS];
+    for (uint32_t q = 0; q < nsp; ++q) {
+      uint64_t tot;
+      off[q] = carry[q] + wave_excl_scan_u64(act ? rc[q] : 0, lane, &tot);
+      carry[q] += tot;
+    }
+    if (act) emit_record(a.L, wire, pos, w, recs + (R0 + i) * a.L.stride, a.heaps, off);
   }
 }
 
@@ -1284,8 +1366,8 @@ static unsigned grid_for(uint64_t items, uint64_t per_block) {
 }
 
 struct VecWs {
-  size_t P, Pn, E, En, flags, T, cnt, base, wl, exitp, used, dirty, mj, starts, rcnt, hoff, scan,
-      tot, end;
+  size_t P, Pn, E, En, flags, T, cnt, base, wl, exitp, used, dirty, mj, psum, hs, hb, scan, tot,
+      end;
   uint64_t nch;
   uint32_t lp;
 };
@@ -1318,10 +1400,11 @@ static VecWs vec_ws_layout(const spk_layout *L, uint64_t wire_len, uint64_t rec_
   v.used = take(v.nch * 8);
   v.dirty = take(2 * v.nch * 4);
   v.mj = take(v.nch * 4);
-  v.starts = take((rec_cap + 1) * 8);
-  v.rcnt = take((uint64_t)(ns ? ns : 1) * (rec_cap + 1) * 4);
-  v.hoff = take((uint64_t)(ns ? ns : 1) * (rec_cap + 1) * 8);
-  const uint64_t nsb = (rec_cap > v.nch ? rec_cap : v.nch) / kScanBlock + 2;
+  v.psum = take((uint64_t)(ns ? ns : 1) * v.nch * 8);
+  v.hs = take((uint64_t)(ns ? ns : 1) * v.nch * 8);
+  v.hb = take((uint64_t)(ns ? ns : 1) * v.nch * 8);
+  (void)rec_cap;
+  const uint64_t nsb = v.nch / kScanBlock + 2;
   v.scan = take(nsb * 8);
   v.tot = take(16 * 8);
   v.end = off;
@@ -1343,20 +1426,22 @@ static VecBufs vec_bufs(uint8_t *ws, const VecWs &v) {
   B.used = reinterpret_cast<uint64_t *>(ws + v.used);
   B.dirty = reinterpret_cast<uint32_t *>(ws + v.dirty);
   B.mj = reinterpret_cast<uint32_t *>(ws + v.mj);
-  B.starts = reinterpret_cast<uint64_t *>(ws + v.starts);
-  B.rcnt = reinterpret_cast<uint32_t *>(ws + v.rcnt);
-  B.hoff = reinterpret_cast<uint64_t *>(ws + v.hoff);
+  B.psum = reinterpret_cast<uint64_t *>(ws + v.psum);
+  B.hs = reinterpret_cast<uint64_t *>(ws + v.hs);
+  B.hb = reinterpret_cast<uint64_t *>(ws + v.hb);
   B.scan = reinterpret_cast<uint64_t *>(ws + v.scan);
   return B;
 }
 
 // exclusive scan in[0..n) -> out, total -> *tot (device)
-static void scan_u32(const uint32_t *in, uint64_t n, uint64_t *out, uint64_t *bsum,
-                     uint64_t *tot, hipStream_t s) {
+template <typename In>
+static void scan_dev(const In *in, uint64_t n, uint64_t *out, uint64_t *bsum, uint64_t *tot,
+                     hipStream_t s) {
   const unsigned nb = grid_for(n ? n : 1, kScanBlock);
-  hipLaunchKernelGGL(scan_reduce, dim3(nb), dim3(256), 0, s, in, n, bsum);
+  hipLaunchKernelGGL(scan_reduce<In>, dim3(nb), dim3(256), 0, s, in, n, bsum);
   hipLaunchKernelGGL(scan_blocks, dim3(1), dim3(1024), 0, s, bsum, (uint64_t)nb, tot);
-  hipLaunchKernelGGL(scan_apply, dim3(nb), dim3(256), 0, s, in, n, (const uint64_t *)bsum, out);
+  hipLaunchKernelGGL(scan_apply<In>, dim3(nb), dim3(256), 0, s, in, n, (const uint64_t *)bsum,
+                     out);
 }
 
 template <int NS>
@@ -1365,12 +1450,13 @@ static hipError_t launch_vec_decode_ns(const DecArgs &a, const WalkProg &P, cons
                                        uint8_t *d_recs, hipStream_t s) {
   VecBufs B = vec_bufs(ws, v);
   hipError_t e;
-  // counts past the device-side chunk / record totals must read as zero
+  const uint32_t ns = P.ns;
+  // chunk counts past the device-side chunk total must read as zero
   if ((e = hipMemsetAsync(B.cnt, 0, v.nch * 4, s)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(B.rcnt, 0, (uint64_t)(P.ns ? P.ns : 1) * (a.rec_cap + 1) * 4, s)) !=
-      hipSuccess)
-    return e;
-  hipLaunchKernelGGL(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, v.lp);
+  if ((e = hipMemsetAsync(B.hs, 0, (uint64_t)(ns ? ns : 1) * v.nch * 8, s)) != hipSuccess) return e;
+  uint64_t *tot = reinterpret_cast<uint64_t *>(ws + v.tot);
+  if ((e = hipMemsetAsync(tot, 0, 16 * 8, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, v.lp, v.nch);
   const unsigned cg = grid_for(v.nch, 256);
   hipLaunchKernelGGL(vec_spec<NS>, dim3(grid_for(v.nch, 64 * kSpecWaves)), dim3(64 * kSpecWaves), 0,
                      s, a, P, wire, ws, B);
@@ -1379,23 +1465,23 @@ static hipError_t launch_vec_decode_ns(const DecArgs &a, const WalkProg &P, cons
     hipLaunchKernelGGL(vec_verify_round<NS>, dim3(64), dim3(256), 0, s, a, P, wire, ws, B, r);
   hipLaunchKernelGGL(vec_fixup<NS>, dim3(1), dim3(1024), 0, s, a, P, wire, ws, B);
   hipLaunchKernelGGL(vec_term_min, dim3(cg), dim3(256), 0, s, ws, B);
-  hipLaunchKernelGGL(vec_term_zero, dim3(cg), dim3(256), 0, s, ws, B);
-  uint64_t *tot = reinterpret_cast<uint64_t *>(ws + v.tot);
-  // chunk record counts -> bases. nchunks is device-side; scan the capacity
-  // (entries past nchunks are never read)
-  scan_u32(B.cnt, v.nch, B.base, B.scan, tot, s);
+  hipLaunchKernelGGL(vec_term_zero, dim3(cg), dim3(256), 0, s, ws, B, ns);
+  // chunk record counts -> record bases; chunk span-count sums -> heap bases
+  // (nchunks is device-side: the capacity is scanned, entries past it are 0)
+  scan_dev<uint32_t>(B.cnt, v.nch, B.base, B.scan, tot, s);
   hipLaunchKernelGGL(vec_count_check, dim3(1), dim3(64), 0, s, ws, (const uint64_t *)tot, d_res);
-  hipLaunchKernelGGL(vec_place<NS>, dim3(cg), dim3(256), 0, s, a, P, wire, ws, B,
-                     (const spk_dresult_t *)d_res);
-  for (uint32_t k = 0; k < P.ns; ++k)
-    scan_u32(B.rcnt + (uint64_t)k * a.rec_cap, a.rec_cap, B.hoff + (uint64_t)k * a.rec_cap,
-             B.scan, tot + 1 + k, s);
+  for (uint32_t k = 0; k < ns; ++k)
+    scan_dev<uint64_t>(B.hs + (uint64_t)k * v.nch, v.nch, B.hb + (uint64_t)k * v.nch, B.scan,
+                       (uint64_t *)nullptr, s);
+  hipLaunchKernelGGL(vec_total<NS>, dim3(cg), dim3(256), 0, s, a, P, wire, ws, B, tot + 1);
   hipLaunchKernelGGL(vec_finish, dim3(1), dim3(64), 0, s, a, ws, d_res,
                      (const uint64_t *)(tot + 1));
-  uint64_t rb = (a.rec_cap + 255) / 256;
-  if (rb > 65536) rb = 65536;
-  hipLaunchKernelGGL(vec_decode, dim3((unsigned)(rb ? rb : 1)), dim3(256), 0, s, a, wire,
-                     (const uint8_t *)ws, B, d_recs, (const spk_dresult_t *)d_res);
+  uint32_t G = kEmitRecs / v.lp;
+  if (G > 64) G = 64;
+  if (G < 1) G = 1;
+  const uint64_t groups = (v.nch + G - 1) / G;
+  hipLaunchKernelGGL(vec_emit<NS>, dim3(grid_for(groups, kEmitWaves)), dim3(64 * kEmitWaves), 0, s,
+                     a, P, wire, (const uint8_t *)ws, B, d_recs, (const spk_dresult_t *)d_res, G);
   return hipGetLastError();
 }
 
@@ -1461,7 +1547,7 @@ hipError_t launch_var_encode(const spk_layout *L, int mode, uint64_t n,
   if (n == 0) {
     // header (+ zero count) only; reuse the write kernel with one block
   }
-  hipLaunchKernelGGL(var_encode_write, dim3(grid_for(n ? n : 1, kRPB)), dim3(kThreads), kWin,
+  hipLaunchKernelGGL(var_encode_write, dim3(grid_for(n ? n : 1, kRPB)), dim3(kThreads), 0,
                      s, a, (const uint8_t *)d_recs, (uint8_t *)d_out, out_cap,
                      (const uint8_t *)ws, d_plan, d_offsets);
   (void)ws_bytes;
