@@ -559,7 +559,7 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
 constexpr uint32_t kSpec = 256;        // payload bytes per speculation chunk
 constexpr uint32_t kWinExtra = 512;    // extension bytes staged past a wave's chunks
 constexpr uint32_t kPlaus = 4096;      // longest record a speculative walk accepts
-constexpr int kRounds = 8;             // parallel re-verification rounds
+constexpr int kRounds = 6;             // parallel re-verification rounds
 constexpr uint32_t kExt = 4;           // records a spec walk continues past its chunk
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
 
@@ -776,142 +776,6 @@ constexpr uint32_t kRegion = 64 * kSpec;                    // chunk bytes per w
 constexpr uint32_t kRegionVec = (kRegion + kWinExtra) / 16;  // 16-B LDS slots per wave
 constexpr uint32_t kSpecWaves = 2;                           // waves per block
 
-// One lane per chunk; a wave stages its 64 consecutive chunks (plus the head
-// of the extension) in LDS with coalesced 16-B loads, then every lane walks
-// its own chunk there. A candidate start byte is plausible when no record of
-// its walk -- in the chunk or in the extension -- is implausible (longer than
-// kPlaus, or incomplete before the wire end); the lane takes the first
-// plausible candidate and records its walk: positions in the chunk (P) and
-// kExt positions past it (E). Chunk 0 starts at the payload start (exact).
-template <int NS>
-__global__ __launch_bounds__(64 * kSpecWaves) void vec_spec(DecArgs a, WalkProg P,
-                                                            const uint8_t *__restrict__ wire,
-                                                            uint8_t *__restrict__ ws, VecBufs B) {
-  __shared__ v4u_t reg_s[kSpecWaves][kRegionVec + 1];
-  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t ch0 = ((uint64_t)blockIdx.x * kSpecWaves + wv) * 64;
-  const uint64_t nch = c->nchunks;
-  if (ch0 >= nch) return;  // wave-uniform; only wave-level sync below
-  const uint32_t w = c->w, lp = c->lp;
-  const uint64_t len = a.wire_len;
-  const uint64_t rs = c->p0 + ch0 * kSpec;
-  const uint64_t wend = rs + kRegionVec * 16 < len ? rs + kRegionVec * 16 : len;
-  v4u_t *reg = reg_s[wv];
-  for (uint32_t v = lane; v < kRegionVec; v += 64) {
-    const uint64_t g = rs + 16ull * v;
-    v4u_t val = {0u, 0u, 0u, 0u};
-    if (g + 16 <= len) {
-      val = *reinterpret_cast<const v4u_una *>(wire + g);
-    } else if (g < len) {
-      uint32_t t[4] = {0u, 0u, 0u, 0u};
-      for (uint64_t q = g; q < len; ++q) t[(q - g) >> 2] |= (uint32_t)wire[q] << (8 * ((q - g) & 3));
-      val = v4u_t{t[0], t[1], t[2], t[3]};
-    }
-    reg[v] = val;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const uint64_t ch = ch0 + lane;
-  if (ch >= nch) return;
-  WinReader rd;
-  rd.d = (const lds_u32 *)(reg);
-  rd.wire = wire;
-  rd.cs = rs;
-  rd.wend = wend;
-  rd.w = w;
-  const uint64_t cs = c->p0 + ch * kSpec;
-  const uint64_t ce = cs + kSpec < len ? cs + kSpec : len;
-  uint16_t *Pl = B.P + ch * lp;
-  uint32_t *El = B.E + ch * kExt;
-  uint32_t np = 0, ne = 0, fl = 0;
-  // One record step per iteration for every lane (a nested try/walk loop
-  // would make the wave wait for each lane's walk in turn). While searching,
-  // 8 candidate start bytes are screened per iteration on their first count.
-  uint64_t t = 0, x = cs;
-  bool searching = ch != 0, done = false;
-  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
-  uint64_t ps[NS > 0 ? NS : SPK_MAX_SPANS];
-  for (uint32_t k = 0; k < nsp; ++k) ps[k] = 0;
-  const uint32_t s0 = P.skip[0];
-  while (!done) {
-    if (searching) {
-      const uint64_t b0 = cs + t + s0;  // first count field of candidate cs+t
-      uint32_t m = 0;
-      if (b0 + 20 <= wend) {
-        const uint32_t o0 = (uint32_t)(b0 - rs), i = o0 >> 2, sh = o0 & 3;
-        const lds_u32 *d = rd.d;
-        const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2], d3 = d[i + 3], d4 = d[i + 4];
-        const uint32_t wd[4] = {__builtin_amdgcn_alignbyte(d1, d0, sh),
-                                __builtin_amdgcn_alignbyte(d2, d1, sh),
-                                __builtin_amdgcn_alignbyte(d3, d2, sh),
-                                __builtin_amdgcn_alignbyte(d4, d3, sh)};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint32_t lo = __builtin_amdgcn_alignbyte(wd[(k >> 2) + 1], wd[k >> 2], k & 3);
-          uint64_t cv = w == 1 ? (lo & 0xFFu) : w == 2 ? (lo & 0xFFFFu) : lo;
-          if (w == 8)
-            cv |= (uint64_t)__builtin_amdgcn_alignbyte(wd[(k >> 2) + 2], wd[(k >> 2) + 1], k & 3)
-                  << 32;
-          m |= (cv <= P.c0max ? 1u : 0u) << k;
-        }
-      } else {
-        for (int k = 0; k < 8; ++k) {
-          const uint64_t q = b0 + k;
-          const uint64_t cv = q + w <= len ? rd(q) : ~0ull;
-          m |= (cv <= P.c0max ? 1u : 0u) << k;
-        }
-      }
-      const uint64_t rem = ce - (cs + t);  // candidates must start in the chunk
-      if (rem < 8) m &= (1u << rem) - 1u;
-      if (!m) {
-        t += 8;
-        if (cs + t >= ce) done = true;
-        continue;
-      }
-      t += (uint32_t)__builtin_ctz(m);
-      x = cs + t;
-      np = ne = 0;
-      for (uint32_t k = 0; k < nsp; ++k) ps[k] = 0;
-      searching = false;
-    }
-    uint64_t rc[NS > 0 ? NS : SPK_MAX_SPANS];
-    const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w, rc) : 0;
-    if (ch != 0 && ((L == 0 && x < len) || L > kPlaus)) {  // off the record grid
-      t += 1;
-      searching = true;
-      if (cs + t >= ce) done = true;
-      continue;
-    }
-    if (x < ce) {
-      if (np < lp) Pl[np] = (uint16_t)(x - cs);
-      ++np;
-      if (L)
-        for (uint32_t k = 0; k < nsp; ++k) ps[k] += rc[k];
-    } else {
-      El[ne++] = (x - cs) < 0xFFFFFFFFull ? (uint32_t)(x - cs) : 0xFFFFFFFEu;
-    }
-    if (!L) {  // incomplete record or the wire end: the walk terminates here
-      fl = kWalkTerm;
-      break;
-    }
-    x += L;
-    if (x >= ce && ne == kExt) done = true;
-  }
-  if (searching) np = ne = fl = 0;  // no plausible start in the chunk
-  if (np > lp) {
-    atomicOr(&c->overflow, 1u);
-    np = lp;
-  }
-  B.Pn[ch] = np;
-  B.En[ch] = ne;
-  B.flags[ch] = fl;
-  B.dirty[ch] = kNone32;
-  B.dirty[nch + ch] = kNone32;
-  for (uint32_t k = 0; k < nsp; ++k) B.psum[k * c->cap + ch] = searching ? 0 : ps[k];
-}
-
 constexpr uint64_t kTermPos = ~0ull;  // "the true path ended before this chunk"
 
 // Walk the true path of chunk `ch` from `entry` until it meets the chunk's
@@ -1020,23 +884,171 @@ __device__ __forceinline__ void verify_chunk(const DecArgs &a, const WalkProg &P
     mark_dirty(c, B, ch + 1, r + 1);
 }
 
-// Round 0 of the verification, one lane per chunk: walk the chunk's true
-// path from the optimistic entry E_{c-1}[0] until it meets the chunk's spec
-// walk; a chunk whose exit differs from the entry its successor assumed
-// lists the successor for round 1.
+// One lane per chunk; a wave stages its 64 consecutive chunks (plus the head
+// of the extension) in LDS with coalesced 16-B loads, then every lane walks
+// its own chunk there. Lane 0 re-walks the last chunk of the previous wave
+// (63 new chunks per wave) so that every other lane gets its predecessor's
+// first extension position by a lane shuffle: round 0 of the verification
+// runs here, with the common case -- that position is the chunk's first
+// spec position -- settled in registers. A candidate start byte is plausible when no record of
+// its walk -- in the chunk or in the extension -- is implausible (longer than
+// kPlaus, or incomplete before the wire end); the lane takes the first
+// plausible candidate and records its walk: positions in the chunk (P) and
+// kExt positions past it (E). Chunk 0 starts at the payload start (exact).
+constexpr uint32_t kSpecStep = 63;  // new chunks per wave
 template <int NS>
-__global__ __launch_bounds__(256) void vec_verify0(DecArgs a, WalkProg P,
-                                                   const uint8_t *__restrict__ wire,
-                                                   uint8_t *__restrict__ ws, VecBufs B) {
+__global__ __launch_bounds__(64 * kSpecWaves) void vec_spec(DecArgs a, WalkProg P,
+                                                            const uint8_t *__restrict__ wire,
+                                                            uint8_t *__restrict__ ws, VecBufs B) {
+  __shared__ v4u_t reg_s[kSpecWaves][kRegionVec + 1];
   VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
-  const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t ch0 = ((uint64_t)blockIdx.x * kSpecWaves + wv) * kSpecStep;
   const uint64_t nch = c->nchunks;
-  if (ch >= nch) return;
-  const uint64_t entry =
-      ch == 0 ? c->p0
-              : (B.En[ch - 1] ? c->p0 + (ch - 1) * kSpec + B.E[(ch - 1) * kExt] : kTermPos);
-  const uint64_t next_used = B.En[ch] ? c->p0 + ch * kSpec + B.E[ch * kExt] : kTermPos;
-  verify_chunk<NS>(a, P, wire, c, B, ch, entry, next_used, 0);
+  if (ch0 >= nch) return;  // wave-uniform; only wave-level sync below
+  const uint32_t w = c->w, lp = c->lp;
+  const uint64_t len = a.wire_len;
+  const uint64_t chf = ch0 ? ch0 - 1 : 0;  // first chunk in the region
+  const uint64_t rs = c->p0 + chf * kSpec;
+  const uint64_t wend = rs + kRegionVec * 16 < len ? rs + kRegionVec * 16 : len;
+  v4u_t *reg = reg_s[wv];
+  for (uint32_t v = lane; v < kRegionVec; v += 64) {
+    const uint64_t g = rs + 16ull * v;
+    v4u_t val = {0u, 0u, 0u, 0u};
+    if (g + 16 <= len) {
+      val = *reinterpret_cast<const v4u_una *>(wire + g);
+    } else if (g < len) {
+      uint32_t t[4] = {0u, 0u, 0u, 0u};
+      for (uint64_t q = g; q < len; ++q) t[(q - g) >> 2] |= (uint32_t)wire[q] << (8 * ((q - g) & 3));
+      val = v4u_t{t[0], t[1], t[2], t[3]};
+    }
+    reg[v] = val;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // lane l walks chunk ch0 - 1 + l (lane 0 of wave 0 has none)
+  const bool live = (ch0 > 0 || lane > 0) && ch0 + lane - 1 < nch;
+  const uint64_t ch = live ? ch0 + lane - 1 : chf;
+  WinReader rd;
+  rd.d = (const lds_u32 *)(reg);
+  rd.wire = wire;
+  rd.cs = rs;
+  rd.wend = wend;
+  rd.w = w;
+  const uint64_t cs = c->p0 + ch * kSpec;
+  const uint64_t ce = cs + kSpec < len ? cs + kSpec : len;
+  uint16_t *Pl = B.P + ch * lp;
+  uint32_t *El = B.E + ch * kExt;
+  uint32_t np = 0, ne = 0, fl = 0, p0rel = 0, e0rel = 0;
+  // One record step per iteration for every lane (a nested try/walk loop
+  // would make the wave wait for each lane's walk in turn). While searching,
+  // 8 candidate start bytes are screened per iteration on their first count.
+  uint64_t t = 0, x = cs;
+  bool searching = ch != 0, done = !live;
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  uint64_t ps[NS > 0 ? NS : SPK_MAX_SPANS];
+  for (uint32_t k = 0; k < nsp; ++k) ps[k] = 0;
+  const uint32_t s0 = P.skip[0];
+  while (!done) {
+    if (searching) {
+      const uint64_t b0 = cs + t + s0;  // first count field of candidate cs+t
+      uint32_t m = 0;
+      if (b0 + 20 <= wend) {
+        const uint32_t o0 = (uint32_t)(b0 - rs), i = o0 >> 2, sh = o0 & 3;
+        const lds_u32 *d = rd.d;
+        const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2], d3 = d[i + 3], d4 = d[i + 4];
+        const uint32_t wd[4] = {__builtin_amdgcn_alignbyte(d1, d0, sh),
+                                __builtin_amdgcn_alignbyte(d2, d1, sh),
+                                __builtin_amdgcn_alignbyte(d3, d2, sh),
+                                __builtin_amdgcn_alignbyte(d4, d3, sh)};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t lo = __builtin_amdgcn_alignbyte(wd[(k >> 2) + 1], wd[k >> 2], k & 3);
+          uint64_t cv = w == 1 ? (lo & 0xFFu) : w == 2 ? (lo & 0xFFFFu) : lo;
+          if (w == 8)
+            cv |= (uint64_t)__builtin_amdgcn_alignbyte(wd[(k >> 2) + 2], wd[(k >> 2) + 1], k & 3)
+                  << 32;
+          m |= (cv <= P.c0max ? 1u : 0u) << k;
+        }
+      } else {
+        for (int k = 0; k < 8; ++k) {
+          const uint64_t q = b0 + k;
+          const uint64_t cv = q + w <= len ? rd(q) : ~0ull;
+          m |= (cv <= P.c0max ? 1u : 0u) << k;
+        }
+      }
+      const uint64_t rem = ce - (cs + t);  // candidates must start in the chunk
+      if (rem < 8) m &= (1u << rem) - 1u;
+      if (!m) {
+        t += 8;
+        if (cs + t >= ce) done = true;
+        continue;
+      }
+      t += (uint32_t)__builtin_ctz(m);
+      x = cs + t;
+      np = ne = 0;
+      for (uint32_t k = 0; k < nsp; ++k) ps[k] = 0;
+      searching = false;
+    }
+    uint64_t rc[NS > 0 ? NS : SPK_MAX_SPANS];
+    const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w, rc) : 0;
+    if (ch != 0 && ((L == 0 && x < len) || L > kPlaus)) {  // off the record grid
+      t += 1;
+      searching = true;
+      if (cs + t >= ce) done = true;
+      continue;
+    }
+    if (x < ce) {
+      if (!np) p0rel = (uint32_t)(x - cs);
+      if (np < lp && lane) Pl[np] = (uint16_t)(x - cs);
+      ++np;
+      if (L)
+        for (uint32_t k = 0; k < nsp; ++k) ps[k] += rc[k];
+    } else {
+      const uint32_t er = (x - cs) < 0xFFFFFFFFull ? (uint32_t)(x - cs) : 0xFFFFFFFEu;
+      if (!ne) e0rel = er;
+      if (lane) El[ne] = er;
+      ++ne;
+    }
+    if (!L) {  // incomplete record or the wire end: the walk terminates here
+      fl = kWalkTerm;
+      break;
+    }
+    x += L;
+    if (x >= ce && ne == kExt) done = true;
+  }
+  if (searching) np = ne = fl = 0;  // no plausible start in the chunk
+  if (np > lp) {
+    atomicOr(&c->overflow, 1u);
+    np = lp;
+  }
+  // ---- round 0 of the verification ----
+  const uint64_t e0 = ne ? cs + e0rel : kTermPos;  // this chunk's first position past it
+  const uint64_t prev_e0 = __shfl_up(e0, 1);
+  if (!live || lane == 0) return;  // lane 0 only fed lane 1
+  B.Pn[ch] = np;
+  B.En[ch] = ne;
+  B.flags[ch] = fl;
+  // a later round may re-walk this chunk and meet the walk at its start
+  for (uint32_t k = 0; k < nsp; ++k) B.psum[k * c->cap + ch] = searching ? 0 : ps[k];
+  const uint64_t entry = ch == 0 ? c->p0 : prev_e0;
+  if (np && entry == cs + p0rel) {
+    // the true path enters at the spec walk's first position: all of it holds
+    const bool term = fl == kWalkTerm && ne == 0;  // the walk ends inside the chunk
+    B.mj[ch] = 0;
+    B.used[ch] = entry;
+    B.exitp[ch] = term ? kTermPos : e0;
+    B.T[ch] = entry;
+    B.cnt[ch] = term ? np - 1 : np;
+    B.flags[ch] = fl | kOk | (term ? kTerm : 0u);
+    for (uint32_t k = 0; k < nsp; ++k) B.hs[k * c->cap + ch] = ps[k];
+    return;
+  }
+  // otherwise the chunk is re-walked in round 1 (after its predecessor is
+  // final): one slow lane here would stall its whole wave
+  B.used[ch] = kTermPos - 1;  // no true entry equals this: "never verified"
+  mark_dirty(c, B, ch, 1);
 }
 
 // Round r >= 1 over round r's worklist: a listed chunk whose predecessor is
@@ -1078,12 +1090,14 @@ __global__ __launch_bounds__(1024) void vec_fixup(DecArgs a, WalkProg P,
   if (!n) return;
   const uint64_t nch = c->nchunks;
   const uint32_t *list = B.wl + (kRounds & 1) * nch;
+  uint32_t m = 2;  // sort size: next power of two >= n
+  while (m < n) m <<= 1;
   if (n <= kFixSort) {
-    for (uint32_t i = threadIdx.x; i < kFixSort; i += blockDim.x) sh[i] = i < n ? list[i] : kNone32;
+    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) sh[i] = i < n ? list[i] : kNone32;
     __syncthreads();
-    for (uint32_t k = 2; k <= kFixSort; k <<= 1) {
+    for (uint32_t k = 2; k <= m; k <<= 1) {
       for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-        for (uint32_t i = threadIdx.x; i < kFixSort; i += blockDim.x) {
+        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
           const uint32_t l = i ^ j;
           if (l > i) {
             const uint32_t x = sh[i], y = sh[l];
@@ -1458,11 +1472,12 @@ static hipError_t launch_vec_decode_ns(const DecArgs &a, const WalkProg &P, cons
   if ((e = hipMemsetAsync(tot, 0, 16 * 8, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, v.lp, v.nch);
   const unsigned cg = grid_for(v.nch, 256);
-  hipLaunchKernelGGL(vec_spec<NS>, dim3(grid_for(v.nch, 64 * kSpecWaves)), dim3(64 * kSpecWaves), 0,
-                     s, a, P, wire, ws, B);
-  hipLaunchKernelGGL(vec_verify0<NS>, dim3(cg), dim3(256), 0, s, a, P, wire, ws, B);
+  // re-verification stamps start as "never listed"
+  if ((e = hipMemsetAsync(B.dirty, 0xFF, 2 * v.nch * 4, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(vec_spec<NS>, dim3(grid_for(v.nch, (uint64_t)kSpecStep * kSpecWaves)),
+                     dim3(64 * kSpecWaves), 0, s, a, P, wire, ws, B);
   for (uint32_t r = 1; r < (uint32_t)kRounds; ++r)
-    hipLaunchKernelGGL(vec_verify_round<NS>, dim3(64), dim3(256), 0, s, a, P, wire, ws, B, r);
+    hipLaunchKernelGGL(vec_verify_round<NS>, dim3(256), dim3(256), 0, s, a, P, wire, ws, B, r);
   hipLaunchKernelGGL(vec_fixup<NS>, dim3(1), dim3(1024), 0, s, a, P, wire, ws, B);
   hipLaunchKernelGGL(vec_term_min, dim3(cg), dim3(256), 0, s, ws, B);
   hipLaunchKernelGGL(vec_term_zero, dim3(cg), dim3(256), 0, s, ws, B, ns);
