@@ -39,8 +39,10 @@
 namespace spk {
 
 constexpr int kThreads = 256;
-constexpr int kIPT = 4;                     // records per thread (encode)
-constexpr uint64_t kRPB = kThreads * kIPT;  // records per block (encode)
+constexpr int kIPT = 1;                     // records per thread (encode write)
+constexpr uint64_t kRPB = kThreads * kIPT;  // records per block (encode write)
+constexpr int kPlanSub = 4;                 // write blocks per plan block
+constexpr uint64_t kPlanRPB = kRPB * kPlanSub;  // records per plan block
 
 struct VarArgs {
   KLayout L;
@@ -169,33 +171,40 @@ __device__ uint64_t block_max(uint64_t v, uint64_t *sh) {
 struct Partial {
   uint64_t sum;   // VECTOR: sum of w-independent bytes; MESSAGES: message bytes
   uint64_t maxc;  // max element count
+  uint64_t sub[kPlanSub];  // the same sum per write block (kRPB records)
 };
 
 __global__ __launch_bounds__(kThreads) void var_plan_reduce(
     VarArgs a, const uint8_t *__restrict__ recs, uint8_t *__restrict__ ws,
     const uint8_t *__restrict__ hdrlen_tbl) {
   __shared__ uint64_t sh[kThreads / 64];
-  const uint64_t r0 = (uint64_t)blockIdx.x * kRPB;
-  uint64_t sum = 0, mx = 0;
-  for (int j = 0; j < kIPT; ++j) {
+  const uint64_t r0 = (uint64_t)blockIdx.x * kPlanRPB;
+  uint64_t mx = 0, tot = 0, sub[kPlanSub];
+  for (int j = 0; j < kPlanSub; ++j) {
     const uint64_t i = r0 + (uint64_t)j * kThreads + threadIdx.x;  // coalesced
-    if (i >= a.n) break;
-    uint64_t var, maxc;
-    rec_sizes(a.L, recs + i * a.L.stride, var, maxc);
-    if (a.mode == SPK_MODE_VECTOR) {
-      sum += var;
-    } else {
-      const uint32_t w = width_of(maxc);
-      sum += hdrlen_tbl[wlog(w)] + var + (uint64_t)a.L.n_spans * w;
+    uint64_t sum = 0;
+    if (i < a.n) {
+      uint64_t var, maxc;
+      rec_sizes(a.L, recs + i * a.L.stride, var, maxc);
+      if (a.mode == SPK_MODE_VECTOR) {
+        sum = var;
+      } else {
+        const uint32_t w = width_of(maxc);
+        sum = hdrlen_tbl[wlog(w)] + var + (uint64_t)a.L.n_spans * w;
+      }
+      mx = maxc > mx ? maxc : mx;
     }
-    mx = maxc > mx ? maxc : mx;
+    block_excl_scan(sum, &sub[j], sh);
+    tot += sub[j];
   }
-  uint64_t tot;
-  block_excl_scan(sum, &tot, sh);
   const uint64_t m = block_max(mx, sh);
   if (threadIdx.x == 0) {
     Partial *p = reinterpret_cast<Partial *>(ws + kWsScratch);
-    p[blockIdx.x] = Partial{tot, m};
+    Partial q;
+    q.sum = tot;
+    q.maxc = m;
+    for (int j = 0; j < kPlanSub; ++j) q.sub[j] = sub[j];
+    p[blockIdx.x] = q;
   }
 }
 
@@ -217,12 +226,13 @@ __global__ __launch_bounds__(1024) void var_plan_finalize(FinArgs a,
   uint64_t carry = 0, mx = 0;
   for (uint64_t b0 = 0; b0 < a.nblocks; b0 += blockDim.x) {
     const uint64_t b = b0 + threadIdx.x;
-    const Partial v = b < a.nblocks ? p[b] : Partial{0, 0};
+    const uint64_t v = b < a.nblocks ? p[b].sum : 0;
+    const uint64_t m = b < a.nblocks ? p[b].maxc : 0;
     uint64_t tot;
-    const uint64_t ex = block_excl_scan(v.sum, &tot, sh);
+    const uint64_t ex = block_excl_scan(v, &tot, sh);
     if (b < a.nblocks) p[b].sum = carry + ex;
     carry += tot;
-    mx = v.maxc > mx ? v.maxc : mx;
+    mx = m > mx ? m : mx;
   }
   mx = block_max(mx, sh);
   if (threadIdx.x != 0) return;
@@ -266,34 +276,89 @@ __global__ void write_msg_hdrs(MsgHdrTable t, uint8_t *ws) {
   if (threadIdx.x < 4) ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + threadIdx.x] = t.len[threadIdx.x];
 }
 
-// one record at output position pos (width w), written straight to HBM
-__device__ __forceinline__ void put_record(const VarArgs &a, const uint8_t *rec, uint32_t w,
-                                           uint64_t pos, uint8_t *out) {
+// ---- LDS-staged output ------------------------------------------------------
+// Partial, unaligned stores straight to HBM cost 2-4x their bytes in write
+// traffic (measured with WRITE_SIZE), so a block assembles its contiguous
+// output range in an LDS window with byte stores fed by wide unaligned
+// global loads, then flushes it with aligned 16-B stores.
+struct Win {
+  uint8_t *lds;
+  uint64_t lo, hi;  // output byte range currently held [lo, hi)
+};
+
+__device__ __forceinline__ void lds_put_u32(uint8_t *d, uint32_t v, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) d[i] = (uint8_t)(v >> (8 * i));
+}
+
+// bytes [pos, pos+n) of the output come from src[0, n): store the part that
+// falls in the window
+__device__ __forceinline__ void win_put(const Win &W, uint64_t pos, const uint8_t *src,
+                                        uint64_t n) {
+  const uint64_t a = pos > W.lo ? pos : W.lo;
+  const uint64_t b = pos + n < W.hi ? pos + n : W.hi;
+  if (a >= b) return;
+  uint64_t i = a - pos;
+  const uint64_t e = b - pos;
+  uint8_t *d = W.lds + (pos - W.lo);
+  for (; i + 16 <= e; i += 16) {
+    const v4u_t v = *reinterpret_cast<const v4u_una *>(src + i);
+    lds_put_u32(d + i, v.x, 4);
+    lds_put_u32(d + i + 4, v.y, 4);
+    lds_put_u32(d + i + 8, v.z, 4);
+    lds_put_u32(d + i + 12, v.w, 4);
+  }
+  if (e - i >= 8) {
+    const uint64_t v = *reinterpret_cast<const u64_unaligned *>(src + i);
+    lds_put_u32(d + i, (uint32_t)v, 4);
+    lds_put_u32(d + i + 4, (uint32_t)(v >> 32), 4);
+    i += 8;
+  }
+  if (e - i >= 4) {
+    lds_put_u32(d + i, *reinterpret_cast<const u32_unaligned *>(src + i), 4);
+    i += 4;
+  }
+  for (; i < e; ++i) d[i] = src[i];
+}
+
+// little-endian w-byte value at output position pos
+__device__ __forceinline__ void win_put_le(const Win &W, uint64_t pos, uint64_t v, uint32_t w) {
+  for (uint32_t i = 0; i < w; ++i) {
+    const uint64_t x = pos + i;
+    if (x >= W.lo && x < W.hi) W.lds[x - W.lo] = (uint8_t)(v >> (8 * i));
+  }
+}
+
+// one record at output position pos (width w) into the window
+__device__ __forceinline__ void win_record(const VarArgs &a, const uint8_t *rec, uint32_t w,
+                                           uint64_t pos, const Win &W) {
   uint32_t sk = 0;
   for (uint32_t o = 0; o < a.L.n_ops; ++o) {
     const spk_op op = a.L.ops[o];
     if (op.kind == SPK_OP_COPY) {
-      copy_bytes(out + pos, rec + op.rec_off, op.size);
+      win_put(W, pos, rec + op.rec_off, op.size);
       pos += op.size;
     } else {
       const uint64_t c = rec_u32(rec, op.rec_off);
-      store_le(out + pos, c, w);
+      win_put_le(W, pos, c, w);
       pos += w;
       const uint64_t nb = c * op.size;
-      if (nb) copy_bytes(out + pos, a.heaps[sk] + rec_u64(rec, op.aux) * op.size, nb);
+      if (nb) win_put(W, pos, a.heaps[sk] + rec_u64(rec, op.aux) * op.size, nb);
       pos += nb;
       ++sk;
     }
   }
 }
 
-// Write pass: one record per lane, consecutive lanes on consecutive records
-// (so a wave's stores cover one contiguous stretch of the output), byte
-// offsets from a block scan per round on top of the block's planned base.
+constexpr uint32_t kEncWin = 20 * 1024;  // LDS assembly window per block
+
+// Write pass: records r0 + j*kThreads + tid (consecutive lanes on consecutive
+// records), byte offsets from a block scan per round on top of the block's
+// planned base; the block's output range is assembled window by window.
 __global__ __launch_bounds__(kThreads) void var_encode_write(
     VarArgs a, const uint8_t *__restrict__ recs, uint8_t *__restrict__ out,
     uint64_t out_cap, const uint8_t *__restrict__ ws,
     const spk_plan_t *__restrict__ plan, uint64_t *__restrict__ offs) {
+  __shared__ __align__(16) uint8_t lds[kEncWin];
   __shared__ uint64_t sh[kThreads / 64];
   const uint64_t total = plan->total_bytes;
   if (total > out_cap) return;  // caller reads plan->total_bytes
@@ -301,20 +366,24 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
   const uint32_t hdr_vec = plan->header_bytes;
   const Partial *part = reinterpret_cast<const Partial *>(ws + kWsScratch);
   const uint64_t r0 = (uint64_t)blockIdx.x * kRPB;
-  uint64_t g = a.mode == SPK_MODE_VECTOR
-                   ? hdr_vec + part[blockIdx.x].sum + r0 * (uint64_t)a.L.n_spans * w_vec
-                   : part[blockIdx.x].sum;
+  const Partial &pb = part[blockIdx.x / kPlanSub];
+  uint64_t gb = pb.sum;
+  for (uint32_t j = 0; j < blockIdx.x % kPlanSub; ++j) gb += pb.sub[j];
+  const uint64_t g0 = a.mode == SPK_MODE_VECTOR
+                          ? hdr_vec + gb + r0 * (uint64_t)a.L.n_spans * w_vec
+                          : gb;
   if (a.mode == SPK_MODE_VECTOR && blockIdx.x == 0)
     for (uint32_t i = threadIdx.x; i < hdr_vec; i += blockDim.x) out[i] = ws[kWsHdrVec + i];
+  uint64_t pj[kIPT], szj[kIPT];
+  uint32_t wj[kIPT];
+  uint64_t g = g0;
   for (int j = 0; j < kIPT; ++j) {
-    if (r0 + (uint64_t)j * kThreads >= a.n) break;  // block-uniform
     const uint64_t i = r0 + (uint64_t)j * kThreads + threadIdx.x;
-    const uint8_t *rec = recs + i * a.L.stride;
     uint64_t sz = 0;
     uint32_t w = w_vec;
     if (i < a.n) {
       uint64_t var, maxc;
-      rec_sizes(a.L, rec, var, maxc);
+      rec_sizes(a.L, recs + i * a.L.stride, var, maxc);
       if (a.mode == SPK_MODE_VECTOR) {
         sz = var + (uint64_t)a.L.n_spans * w_vec;
       } else {
@@ -323,21 +392,43 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
       }
     }
     uint64_t btot;
-    const uint64_t p = g + block_excl_scan(sz, &btot, sh);
+    pj[j] = g + block_excl_scan(sz, &btot, sh);
+    szj[j] = sz;
+    wj[j] = w;
     g += btot;
-    if (i >= a.n) continue;
-    uint64_t q = p;
-    if (a.mode == SPK_MODE_MESSAGES) {
-      if (offs) offs[i] = p;
-      const uint32_t sl = wlog(w);
-      const uint32_t hl = ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + sl];
-      copy_bytes(out + q, ws + kWsHdrMsg + sl * kWsHdrSlot, hl);
-      q += hl;
-    }
-    put_record(a, rec, w, q, out);
+    if (a.mode == SPK_MODE_MESSAGES && offs && i < a.n) offs[i] = pj[j];
   }
   if (a.mode == SPK_MODE_MESSAGES && offs && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
     offs[a.n] = total;
+  const uint64_t g1 = g;
+  if (g1 == g0) return;
+  for (uint64_t wlo = g0 & ~15ull; wlo < g1; wlo += kEncWin) {
+    const Win W{lds, wlo, wlo + kEncWin < g1 ? wlo + kEncWin : g1};
+    for (int j = 0; j < kIPT; ++j) {
+      const uint64_t i = r0 + (uint64_t)j * kThreads + threadIdx.x;
+      if (i >= a.n || pj[j] >= W.hi || pj[j] + szj[j] <= W.lo) continue;
+      uint64_t q = pj[j];
+      if (a.mode == SPK_MODE_MESSAGES) {
+        const uint32_t sl = wlog(wj[j]);
+        const uint32_t hl = ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + sl];
+        win_put(W, q, ws + kWsHdrMsg + sl * kWsHdrSlot, hl);
+        q += hl;
+      }
+      win_record(a, recs + i * a.L.stride, wj[j], q, W);
+    }
+    __syncthreads();
+    // flush [max(W.lo, g0), W.hi): aligned 16-B chunks, bytes at the edges
+    for (uint64_t c = W.lo + (uint64_t)threadIdx.x * 16; c < W.hi; c += kThreads * 16) {
+      const uint64_t lo = c > g0 ? c : g0;
+      const uint64_t hi = c + 16 < W.hi ? c + 16 : W.hi;
+      if (lo == c && hi == c + 16) {
+        *reinterpret_cast<v4u_t *>(out + c) = *reinterpret_cast<const v4u_t *>(lds + (c - W.lo));
+      } else {
+        for (uint64_t x = lo; x < hi; ++x) out[x] = lds[x - W.lo];
+      }
+    }
+    __syncthreads();
+  }
 }
 
 // ===========================================================================
@@ -1501,7 +1592,7 @@ static hipError_t launch_vec_decode_ns(const DecArgs &a, const WalkProg &P, cons
 }
 
 size_t var_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len) {
-  size_t enc = kWsScratch + (grid_for(n, kRPB) + 1) * sizeof(Partial) + 256;
+  size_t enc = kWsScratch + (grid_for(n, kPlanRPB) + 1) * sizeof(Partial) + 256;
   size_t dec_msg = kWsScratch + n * sizeof(MsgState) +
                    (grid_for(n, kThreads) + 1) * SPK_MAX_SPANS * 8 + 256;
   size_t dec_vec = vec_ws_layout(L, wire_len, n).end + 256;
@@ -1536,7 +1627,7 @@ hipError_t launch_var_plan(const spk_layout *L, int mode, uint64_t n, const void
   uint8_t *ws = (uint8_t *)d_ws;
   const MsgHdrTable t = msg_hdr_table(L);
   hipLaunchKernelGGL(write_msg_hdrs, dim3(1), dim3(256), 0, s, t, ws);
-  const uint64_t nb = grid_for(n, kRPB);
+  const uint64_t nb = grid_for(n, kPlanRPB);
   const uint8_t *tbl = ws + kWsHdrMsg + 4 * kWsHdrSlot - 8;
   if (n)
     hipLaunchKernelGGL(var_plan_reduce, dim3(nb), dim3(kThreads), 0, s, a,
