@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--records", type=int, default=0, help="override records per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--settle", type=float, default=1.0,
+                    help="seconds of untimed steps before the warmup (GPU clock ramp)")
     ap.add_argument("--host-path", action="store_true",
                     help="also time H2D + encode + decode + D2H from pinned host buffers")
     ap.add_argument("--pmc-json", default="", help="rocprofv3 PMC summary for roofline.traffic")
@@ -141,6 +143,14 @@ def main():
         print(json.dumps({"error": "round trip mismatch", "errc": res.errc}), flush=True)
         sys.exit(3)
 
+    # untimed settle: the GPU needs ~0.5-1 s of sustained load before its
+    # clocks reach the steady state (a copy runs ~13 % slower in the first
+    # few hundred ms: scripts/probes/copy_probe.hip before/after a bench in
+    # one call), so keep stepping for --settle seconds before the warmup
+    t_settle = time.perf_counter()
+    while time.perf_counter() - t_settle < args.settle:
+        step()
+        torch.cuda.synchronize(dev)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)

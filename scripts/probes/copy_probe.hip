@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void k(v4u* __restrict__ dst, const uint8_t* _
     if constexpr (VAR == 1) {
       v4u c[U];
 #pragma unroll
-      for (int j = 0; j < U; ++j) c[j] = *(const v4u_u*)(srcb + 16 * (t0 + j * 64 + lane) + R);
+      for (int j = 0; j < U; ++j) c[j] = NTL ? __builtin_nontemporal_load((const v4u_u*)(srcb + 16 * (t0 + j * 64 + lane) + R)) : *(const v4u_u*)(srcb + 16 * (t0 + j * 64 + lane) + R);
 #pragma unroll
       for (int j = 0; j < U; ++j) st(c[j], &dst[t0 + j * 64 + lane], NTS);
     } else {
@@ -83,17 +83,16 @@ int main() {
   hipMemset(s, 1, bytes + 4096); hipMemset(d, 0, bytes + 4096);
   const uint64_t nk = bytes / 16 - 1024;
   const uint64_t full8 = nk / (64 * 8) / 4, full16 = nk / (64 * 16) / 4;
-  for (int blocks : {8192, 16384, 32768, 65536}) {
-    run<2, 8, 0, 0, 0>("pure copy U8", (v4u*)d, s, nk, blocks);
-    run<2, 16, 0, 0, 0>("pure copy U16", (v4u*)d, s, nk, blocks);
-    run<0, 8, 0, 0, 7>("funnel R7 U8", (v4u*)d, s, nk, blocks);
-    run<0, 16, 0, 0, 7>("funnel R7 U16", (v4u*)d, s, nk, blocks);
-    run<0, 8, 0, 0, 9>("funnel R9 U8", (v4u*)d, s, nk, blocks);
-    run<1, 8, 0, 0, 7>("unaligned R7 U8", (v4u*)d, s, nk, blocks);
+  for (int blocks : {32768}) {
+    run<1, 16, 0, 0, 7>("unaligned R7 U16 dst+0", (v4u*)d, s, nk, blocks);
+    run<1, 16, 0, 0, 7>("unaligned R7 U16 dst+16", (v4u*)(d + 16), s, nk, blocks);
+    run<1, 16, 0, 0, 7>("unaligned R7 U16 dst+64", (v4u*)(d + 64), s, nk, blocks);
+    run<1, 16, 0, 0, 7>("unaligned R7 U16 dst+128", (v4u*)(d + 128), s, nk, blocks);
+    run<1, 16, 0, 0, 9>("unaligned R9 U16 dst+0", (v4u*)d, s, nk, blocks);
+    run<1, 16, 0, 0, 7>("unaligned R7 U16 dst+0", (v4u*)d, s, nk, blocks);
+    run<1, 16, 0, 0, 7>("unaligned R7 U16 dst+16", (v4u*)(d + 16), s, nk, blocks);
+    run<2, 16, 0, 0, 0>("pure copy U16 dst+16", (v4u*)(d + 16), s, nk, blocks);
+    run<2, 16, 0, 0, 0>("pure copy U16 dst+0", (v4u*)(d), s, nk, blocks);
   }
-  run<2, 8, 0, 0, 0>("pure copy U8 full grid", (v4u*)d, s, nk, (int)full8);
-  run<0, 8, 0, 0, 7>("funnel R7 U8 full grid", (v4u*)d, s, nk, (int)full8);
-  run<2, 16, 0, 0, 0>("pure copy U16 full grid", (v4u*)d, s, nk, (int)full16);
-  run<0, 16, 0, 0, 7>("funnel R7 U16 full grid", (v4u*)d, s, nk, (int)full16);
   return 0;
 }

@@ -9,8 +9,9 @@
 // wave-instruction) and reads each one with a single byte-aligned
 // global_load_dwordx4 (gfx950 runs in unaligned-access mode): every HBM byte
 // is read once and written once, no cross-lane shuffles. Measured on MI355X
-// (scripts/probes/copy_probe.hip): this form sustains the same 5.9-6.0 TB/s
-// as an aligned 16-B copy, 8 chunks in flight per lane, 16 Ki blocks.
+// (scripts/probes/copy_probe.hip): this form runs at least as fast as an
+// aligned 16-B copy; 16 chunks in flight per lane (256 B) beat 8 by 5-13 %
+// (6.1-6.2 TB/s on a good box), 32 Ki blocks.
 // The shift is data-dependent on decode (width/meta/type-literal of the
 // incoming header): the kernel reads it from a device-side CopyJob written by
 // the header kernel, so no host round trip is needed.
@@ -39,7 +40,7 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef v4u v4u_unaligned __attribute__((aligned(1)));
 
 constexpr int kCopyThreads = 256;
-constexpr int kCopyUnroll = 8;
+constexpr int kCopyUnroll = 16;
 constexpr uint64_t kTile = 64ull * kCopyUnroll;  // chunks per wave-tile
 
 // dst chunk k (k in [0, nk)) = 16 source bytes at sp + 16k (any alignment)
@@ -54,6 +55,11 @@ __device__ __forceinline__ void shift_body(v4u *__restrict__ dst,
 #pragma unroll
       for (int j = 0; j < kCopyUnroll; ++j)
         c[j] = *reinterpret_cast<const v4u_unaligned *>(sp + 16 * (t0 + j * 64 + lane));
+      // Keep all kCopyUnroll loads in flight before the first store: after
+      // inlining, the compiler no longer proves dst and sp disjoint and
+      // would otherwise interleave load/store pairs (2 loads in flight,
+      // ~12 % slower: scripts/probes/c2_probe.cpp vs copy_probe.hip).
+      asm volatile("" ::: "memory");
 #pragma unroll
       for (int j = 0; j < kCopyUnroll; ++j) dst[t0 + j * 64 + lane] = c[j];
     } else {
@@ -91,8 +97,9 @@ __global__ __launch_bounds__(kCopyThreads) void shift_copy_kernel(
 static unsigned copy_grid(uint64_t max_bytes) {
   uint64_t tiles = (max_bytes / 16 + kTile - 1) / kTile;
   uint64_t blocks = (tiles + (kCopyThreads / 64) - 1) / (kCopyThreads / 64);
-  // 16 Ki blocks (64 Ki waves) then grid-stride: the probe's best point
-  if (blocks > 16384) blocks = 16384;
+  // 32 Ki blocks (128 Ki waves) then grid-stride: the probe's best point
+  // (scripts/probes/copy_probe.hip: 16 chunks in flight per lane, 6.1-6.2 TB/s)
+  if (blocks > 32768) blocks = 32768;
   if (blocks < 1) blocks = 1;
   return (unsigned)blocks;
 }
