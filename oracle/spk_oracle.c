@@ -389,20 +389,34 @@ int spko_decode(const spk_layout *L, int mode, const void *wire,
     return SPK_OK;
   }
   if (mode != SPK_MODE_MESSAGES || (n_msgs && !msg_offsets)) return SPK_E_ARG;
+  /* Batch contract (ours, not the reference's: it has no batches): message i
+   * is wire[offsets[i], offsets[i+1]); a range that is reversed or ends past
+   * the wire reads as truncated (no_buffer_space); a well-formed message with
+   * no output slot (i >= rec_cap) gets SPK_ERRC_CAPACITY, is not counted and
+   * uses no heap. */
   uint64_t ok = 0, consumed = 0;
   for (uint64_t i = 0; i < n_msgs; ++i) {
     uint64_t a = msg_offsets[i], b = msg_offsets[i + 1];
-    if (b < a || b > wire_len) return SPK_E_ARG;
-    rd_t r = {base + a, base + b};
-    unsigned w;
-    uint64_t data_len;
-    int32_t e = parse_header(&L->fmt_one, &r, &w, &data_len);
+    int32_t e = SPK_ERRC_OK;
+    rd_t r = {base, base};
+    unsigned w = 1;
+    uint64_t data_len = 0;
+    if (b < a || b > wire_len) {
+      e = SPK_ERRC_NO_BUFFER_SPACE;
+    } else {
+      r.now = base + a;
+      r.end = base + b;
+      e = parse_header(&L->fmt_one, &r, &w, &data_len);
+    }
     if (!e) {
-      if (i >= rec_cap) c.overflow = 1;
       uint64_t save[SPK_MAX_SPANS];
       memcpy(save, c.used, sizeof(save));
       e = read_record(&c, &r, w,
                       (i < rec_cap && out) ? out + i * L->rec_stride : NULL);
+      if (!e && i >= rec_cap) {
+        e = SPK_ERRC_CAPACITY;
+        c.overflow = 1;
+      }
       if (e) memcpy(c.used, save, sizeof(save)); /* failed: no heap use */
     }
     if (errc) errc[i] = e;

@@ -190,6 +190,66 @@ def test_random_vs_oracle(case, n, param, modech):
         assert back.heaps[k][:nb].cpu().numpy().tobytes() == heaps[k].tobytes()
 
 
+def _irregular_messages(cd, case, n, seed, param):
+    """A coro_rpc-style batch whose messages are not all canonical: trailing
+    bytes, an explicit (zero) metainfo byte, truncations, broken heads,
+    reversed / out-of-range offsets and one oversized message (forces the
+    kernels' non-staged path for its block)."""
+    _, recs, heaps = synth.make_batch(case, n, seed, param)
+    wire, offs, _ = H.oracle_encode(cd.L, C.SPK_MODE_MESSAGES, recs, heaps)
+    rng = np.random.default_rng(seed)
+    msgs = [bytearray(wire[offs[i]:offs[i + 1]]) for i in range(n)]
+    for i in range(n):
+        r = rng.integers(0, 12)
+        m = msgs[i]
+        if r == 0:
+            m += bytes(rng.integers(0, 256, rng.integers(1, 40), dtype=np.uint8))
+        elif r == 1 and len(m) >= 4 and not (m[0] & 1):
+            m[0] |= 1  # head LSB set: a metainfo byte follows (width 1, no literal)
+            m[4:4] = b"\x00"
+        elif r == 2 and len(m):
+            del m[rng.integers(0, len(m)):]
+        elif r == 3 and len(m) >= 4:
+            m[rng.integers(0, 4)] ^= 0x40
+    msgs[n // 2] += bytes(40000)  # one message larger than a staging buffer
+    lens = np.array([len(m) for m in msgs], np.uint64)
+    o = H.lens_to_offsets(lens)
+    o[3], o[4] = o[4], o[3]       # message 3 reversed (e < b), message 2 overlaps
+    o[7] = o[-1] + 5              # messages 6 ends / 7 starts past the wire
+    return b"".join(bytes(m) for m in msgs), o
+
+
+@pytest.mark.parametrize("case,n,param", [("rec64", 1000, 0), ("pad", 777, 0),
+                                          ("rpcrect", 300, 0), ("person", 500, 40),
+                                          ("ints", 200, 60)])
+@pytest.mark.parametrize("cap_frac", [1.0, 0.6])
+def test_messages_irregular_vs_oracle(case, n, param, cap_frac):
+    """Mode B decode of non-canonical message batches: per-message errc,
+    count, consume_len and every decoded record == the CPU oracle."""
+    cd = codec_for(case)
+    wire, o = _irregular_messages(cd, case, n, 0xBADC0DE + n, param)
+    cap = int(n * cap_frac)
+    eres, erecs, eheaps, eerr = H.oracle_decode(cd.L, C.SPK_MODE_MESSAGES, wire, o, n,
+                                                rec_cap=cap)
+    elems = [len(wire) // sp.elem.size + 1 for sp in cd.L.dev.spans]
+    out = cd.alloc_batch(cap, elems)
+    ec = torch.zeros(n, dtype=torch.int32, device="cuda")
+    offs = torch.from_numpy(o.astype(np.int64)).cuda()
+    cd.deserialize_to(out, wire_dev(wire), C.SPK_MODE_MESSAGES, offs, n, ec)
+    res = cd.result()
+    got_err = ec.cpu().numpy()
+    assert np.array_equal(got_err, eerr[:n]), np.nonzero(got_err != eerr[:n])[0][:10]
+    assert res.count == eres.count and res.consumed == eres.consumed
+    ok = np.nonzero(got_err[:cap] == 0)[0]
+    got = out.recs.cpu().numpy()
+    exp = np.ascontiguousarray(erecs[:cap]).view(np.uint8).reshape(cap, cd.L.stride)
+    assert got[ok].tobytes() == exp[ok].tobytes()
+    for k in range(len(cd.L.dev.spans)):
+        used = int(eres.heap_used[k]) * cd.L.dev.spans[k].elem.size
+        assert res.heap_used[k] == eres.heap_used[k]
+        assert out.heaps[k][:used].cpu().numpy().tobytes() == eheaps[k][:used].tobytes()
+
+
 def test_large_records_fallback():
     """Records straddling chunk boundaries by >255 B take the sequential walker."""
     cd = codec_for("recs")

@@ -17,8 +17,10 @@
 // the header kernel, so no host round trip is needed.
 //
 // SPK_MODE_MESSAGES: n independent [header][record] messages (coro_rpc
-// payloads): a dword gather when header and stride are multiples of 4,
-// byte gather otherwise.
+// payloads): blocks of R messages staged through LDS so that both the
+// record stream and the wire stream move as aligned 16-B chunks
+// (fixed_msg_encode_lds / fixed_msg_decode_lds); a plain dword/byte gather
+// remains for records too large to stage.
 #include "spk_internal.hpp"
 
 namespace spk {
@@ -322,9 +324,266 @@ static unsigned elem_grid(uint64_t items, unsigned threads = 256) {
   return (unsigned)b;
 }
 
+// ---------------------------------------------------------------------------
+// LDS-staged message batches. A block owns R consecutive messages (R a
+// multiple of 16, so every block's record range and — when the header is a
+// dword multiple — its wire range start on 64-B boundaries):
+//   encode: the block's R*S record bytes are staged in LDS with 16-B loads,
+//           then each lane assembles one aligned 16-B wire chunk from the
+//           header (LDS) and the staged records and stores it: reads and
+//           writes are both contiguous streams, one HBM pass each;
+//   decode: the block's wire span is staged the same way, every lane parses
+//           its message header from LDS (parse_hdr), and the records are
+//           written as aligned 16-B chunks assembled with v_alignbyte from
+//           the staged bytes (payloads start at any byte offset).
+// Spans that do not fit the staging buffer (malformed offsets) fall back to
+// global loads inside the same kernel, so results never depend on the path.
+constexpr int kMsgThreads = 256;
+constexpr uint32_t kMsgStageMax = 32768;  // staging bytes per block
+
+struct MsgLdsArgs {
+  spk_msgfmt fmt;   // decode only
+  uint64_t n;
+  uint64_t wire_len;
+  uint64_t rec_cap;
+  uint32_t stride;  // S (multiple of 4)
+  uint32_t hlen;    // H (encode header bytes)
+  uint32_t R;       // messages per block
+  uint32_t cap;     // staging bytes (decode)
+  uint32_t fixed_M; // implicit message stride when offsets == nullptr
+  uint32_t pad_;
+  uint8_t hdr[256];
+};
+
+__device__ __forceinline__ uint32_t lds_u32_at(const uint8_t *lds, uint32_t pos) {
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(lds + (pos & ~3u));
+  return __builtin_amdgcn_alignbyte(w[1], w[0], pos & 3u);  // shift in bytes
+}
+
+__device__ __forceinline__ uint32_t g_u32_at(const uint8_t *p) {
+  return *reinterpret_cast<const uint32_t __attribute__((aligned(1))) *>(p);
+}
+
+template <bool DW>
+__global__ __launch_bounds__(kMsgThreads) void fixed_msg_encode_lds(
+    MsgLdsArgs a, const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
+    uint64_t *__restrict__ offs) {
+  extern __shared__ v4u smem_v4[];
+  uint8_t *hdr = reinterpret_cast<uint8_t *>(smem_v4);
+  uint8_t *inl = hdr + 256;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t S = a.stride, H = a.hlen, M = H + S;
+  const uint64_t first = (uint64_t)blockIdx.x * a.R;
+  if (offs && blockIdx.x == gridDim.x - 1 && tid == 0) offs[a.n] = a.n * M;
+  if (first >= a.n) return;
+  const uint32_t nR = (uint32_t)((a.n - first) < a.R ? (a.n - first) : a.R);
+  if (tid < H) hdr[tid] = a.hdr[tid];
+  const uint8_t *src = in + first * S;
+  const uint32_t bin = nR * S;  // multiple of 4
+  for (uint32_t c = tid; c < bin / 16; c += kMsgThreads)
+    reinterpret_cast<v4u *>(inl)[c] = *reinterpret_cast<const v4u_unaligned *>(src + 16 * c);
+  for (uint32_t d = (bin / 16) * 4 + tid; d < bin / 4; d += kMsgThreads)
+    reinterpret_cast<uint32_t *>(inl)[d] = reinterpret_cast<const uint32_t *>(src)[d];
+  if (offs)
+    for (uint32_t k = tid; k < nR; k += kMsgThreads) offs[first + k] = (first + k) * M;
+  __syncthreads();
+  uint8_t *dst = out + first * M;
+  const uint32_t bout = nR * M;
+  if constexpr (DW) {
+    const uint32_t Mw = M / 4, Hw = H / 4, Sw = S / 4, nq = bout / 4;
+    const uint32_t *hw = reinterpret_cast<const uint32_t *>(hdr);
+    const uint32_t *iw = reinterpret_cast<const uint32_t *>(inl);
+    for (uint32_t t = tid; 4 * t < nq; t += kMsgThreads) {
+      const uint32_t q0 = 4 * t;
+      uint32_t i = q0 / Mw, r = q0 - i * Mw;
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[k] = r < Hw ? hw[r] : iw[i * Sw + (r - Hw)];
+        if (++r == Mw) {
+          r = 0;
+          ++i;
+        }
+      }
+      if (q0 + 4 <= nq) {
+        v4u o = {v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<v4u *>(dst + 16 * t) = o;
+      } else {
+        for (uint32_t k = 0; q0 + k < nq; ++k)
+          reinterpret_cast<uint32_t *>(dst)[q0 + k] = v[k];
+      }
+    }
+  } else {
+    for (uint32_t j = tid; j < bout; j += kMsgThreads) {
+      const uint32_t i = j / M, r = j - i * M;
+      dst[j] = r < H ? hdr[r] : inl[i * S + (r - H)];
+    }
+  }
+}
+
+__global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
+    MsgLdsArgs a, const uint8_t *__restrict__ wire, const uint64_t *__restrict__ offs,
+    int32_t *__restrict__ errc, spk_dresult_t *__restrict__ res, uint8_t *__restrict__ out) {
+  extern __shared__ v4u smem_v4[];
+  uint8_t *stage = reinterpret_cast<uint8_t *>(smem_v4);
+  __shared__ uint64_t s_lo[kMsgThreads / 64], s_hi[kMsgThreads / 64];
+  __shared__ uint64_t s_pay[kMsgThreads];  // payload position (staged: LDS offset)
+  const uint32_t tid = threadIdx.x;
+  const uint32_t S = a.stride;
+  const uint64_t ngroups = (a.n + a.R - 1) / a.R;
+  // ok / consumed accumulate over the block's groups: one atomic per wave at
+  // the end (same-address atomics per group would serialise in L2)
+  unsigned long long ok = 0, consumed = 0;
+  bool cap_hit = false;
+  for (uint64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const uint64_t first = g * a.R;
+    const uint32_t nR = (uint32_t)((a.n - first) < a.R ? (a.n - first) : a.R);
+    uint64_t b = 0, e = 0;
+    bool inr = false;
+    if (tid < nR) {
+      const uint64_t i = first + tid;
+      b = offs ? offs[i] : i * a.fixed_M;
+      e = offs ? offs[i + 1] : (i + 1) * a.fixed_M;
+      inr = e >= b && e <= a.wire_len;
+    }
+    // block min of starts / max of ends over in-range messages
+    uint64_t mn = inr ? b : ~0ull, mx = inr ? e : 0;
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint64_t on = __shfl_xor(mn, o), ox = __shfl_xor(mx, o);
+      mn = on < mn ? on : mn;
+      mx = ox > mx ? ox : mx;
+    }
+    if ((tid & 63) == 0) {
+      s_lo[tid >> 6] = mn;
+      s_hi[tid >> 6] = mx;
+    }
+    __syncthreads();
+    uint64_t blo = s_lo[0], hi = s_hi[0];
+    for (int k = 1; k < kMsgThreads / 64; ++k) {
+      blo = s_lo[k] < blo ? s_lo[k] : blo;
+      hi = s_hi[k] > hi ? s_hi[k] : hi;
+    }
+    const uint64_t lo = blo & ~15ull;
+    const bool staged = blo != ~0ull && hi - lo <= a.cap;
+    if (staged) {
+      const uint32_t nb = (uint32_t)(hi - lo);
+      const uint64_t full = (a.wire_len - lo) / 16;  // 16-B chunks inside the wire
+      for (uint32_t c = tid; 16 * c < nb; c += kMsgThreads) {
+        if (c < full) {
+          reinterpret_cast<v4u *>(stage)[c] =
+              *reinterpret_cast<const v4u_unaligned *>(wire + lo + 16 * (uint64_t)c);
+        } else {
+          for (uint32_t k = 0; k < 16 && 16 * c + k < nb; ++k)
+            stage[16 * c + k] = wire[lo + 16 * (uint64_t)c + k];
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < nR) {
+      const uint64_t i = first + tid;
+      int32_t ec = SPK_ERRC_OK;
+      uint64_t pos = 0, dl = 0;
+      uint32_t w = 1;
+      if (!inr) {
+        ec = SPK_ERRC_NO_BUFFER_SPACE;
+      } else {
+        const uint8_t *p = staged ? stage + (b - lo) : wire + b;
+        ec = parse_hdr(a.fmt, p, e - b, &pos, &w, &dl);
+        if (!ec && e - b - pos < S) ec = SPK_ERRC_NO_BUFFER_SPACE;
+      }
+      if (!ec && i >= a.rec_cap) {
+        ec = SPK_ERRC_CAPACITY;
+        cap_hit = true;
+      }
+      if (errc) errc[i] = ec;
+      s_pay[tid] = ec ? ~0ull : (staged ? b - lo : b) + pos;
+      if (!ec) {
+        ++ok;
+        const uint64_t used = pos + S;
+        consumed += used > dl ? used : dl;
+      }
+    }
+    __syncthreads();
+    if (first < a.rec_cap) {
+      const uint32_t nW = (uint32_t)((a.rec_cap - first) < nR ? (a.rec_cap - first) : nR);
+      const uint32_t Sw = S / 4, nd = nW * Sw;
+      uint8_t *dst = out + first * S;
+      for (uint32_t t = tid; 4 * t < nd; t += kMsgThreads) {
+        const uint32_t d0 = 4 * t;
+        uint32_t i = d0 / Sw, j = d0 - i * Sw;
+        uint32_t v[4];
+        uint32_t valid = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (d0 + k < nd) {
+            const uint64_t p = s_pay[i];
+            if (p != ~0ull) {
+              v[k] = staged ? lds_u32_at(stage, (uint32_t)p + 4 * j)
+                            : g_u32_at(wire + p + 4 * j);
+              valid |= 1u << k;
+            }
+          }
+          if (++j == Sw) {
+            j = 0;
+            ++i;
+          }
+        }
+        if (valid == 0xF) {
+          v4u o = {v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<v4u *>(dst + 16 * t) = o;
+        } else {
+          for (int k = 0; k < 4; ++k)
+            if (valid & (1u << k)) reinterpret_cast<uint32_t *>(dst)[d0 + k] = v[k];
+        }
+      }
+    }
+    __syncthreads();  // stage / s_pay are reused by the next group
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    ok += __shfl_down(ok, o);
+    consumed += __shfl_down(consumed, o);
+  }
+  if ((tid & 63) == 0 && (ok || consumed)) {
+    atomicAdd((unsigned long long *)&res->count, ok);
+    atomicAdd((unsigned long long *)&res->consumed, consumed);
+  }
+  if (__any(cap_hit) && (tid & 63) == 0) atomicExch(&res->errc, SPK_ERRC_CAPACITY);
+}
+
+// messages per block for the LDS-staged kernels: a multiple of 16 whose
+// staging (R messages of M bytes, + alignment slack) fits kMsgStageMax; 0 if
+// a single group of 16 does not fit (very large records: global path)
+static uint32_t msg_block_R(uint32_t M) {
+  uint32_t R = (kMsgStageMax - 64) / M;
+  if (R > (uint32_t)kMsgThreads) R = kMsgThreads;
+  return R & ~15u;
+}
+
 hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
                                         const void *d_recs, void *d_out,
                                         uint64_t *d_offsets, hipStream_t s) {
+  {
+    MsgLdsArgs b = {};
+    b.n = n;
+    b.stride = L->rec_stride;
+    b.hlen = write_hdr(b.hdr, L->fmt_one, 1);
+    const uint32_t M = b.hlen + b.stride;
+    b.R = msg_block_R(M);
+    const bool dw = (b.hlen % 4 == 0) && ((uintptr_t)d_out % 16 == 0);
+    if (b.R && b.hlen <= 256 && (uintptr_t)d_recs % 4 == 0) {
+      const uint64_t blocks = n ? (n + b.R - 1) / b.R : 1;
+      const size_t lds = 256 + (size_t)b.R * b.stride + 16;
+      if (dw)
+        hipLaunchKernelGGL(fixed_msg_encode_lds<true>, dim3((unsigned)blocks),
+                           dim3(kMsgThreads), lds, s, b, (const uint8_t *)d_recs,
+                           (uint8_t *)d_out, d_offsets);
+      else
+        hipLaunchKernelGGL(fixed_msg_encode_lds<false>, dim3((unsigned)blocks),
+                           dim3(kMsgThreads), lds, s, b, (const uint8_t *)d_recs,
+                           (uint8_t *)d_out, d_offsets);
+      return hipGetLastError();
+    }
+  }
   MsgEncArgs a = {};
   a.n = n;
   a.stride = L->rec_stride;
@@ -374,7 +633,10 @@ __global__ __launch_bounds__(256) void fixed_msg_parse(
       ec = parse_hdr(a.fmt, wire + b, e - b, &pos, &w, &dl);
       if (!ec && e - b - pos < a.stride) ec = SPK_ERRC_NO_BUFFER_SPACE;
     }
-    if (!ec && i >= a.rec_cap) ec = SPK_ERRC_CAPACITY;
+    if (!ec && i >= a.rec_cap) {
+      ec = SPK_ERRC_CAPACITY;
+      atomicExch(&res->errc, SPK_ERRC_CAPACITY);
+    }
     if (errc) errc[i] = ec;
     payload[i] = ec ? ~0ull : b + pos;
     if (!ec) {
@@ -445,6 +707,25 @@ hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
   uint64_t *payload = reinterpret_cast<uint64_t *>((uint8_t *)d_ws + kWsScratch);
   hipError_t e = hipMemsetAsync(d_res, 0, sizeof(spk_dresult_t), s);
   if (e != hipSuccess) return e;
+  {
+    MsgLdsArgs b = {};
+    b.fmt = L->fmt_one;
+    b.n = n;
+    b.wire_len = wire_len;
+    b.rec_cap = rec_cap;
+    b.stride = L->rec_stride;
+    b.fixed_M = a.fixed_M;
+    b.R = msg_block_R(a.fixed_M);
+    if (b.R && (uintptr_t)d_recs % 16 == 0 && n > 0) {
+      b.cap = b.R * a.fixed_M + 32;
+      uint64_t blocks = (n + b.R - 1) / b.R;
+      if (blocks > 4096) blocks = 4096;  // groups are strided over the grid
+      hipLaunchKernelGGL(fixed_msg_decode_lds, dim3((unsigned)blocks), dim3(kMsgThreads),
+                         (size_t)b.cap + 16, s, b, (const uint8_t *)d_wire, d_offsets, d_errc,
+                         d_res, (uint8_t *)d_recs);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL(fixed_msg_parse, dim3(elem_grid(n)), dim3(256), 0, s, a,
                      (const uint8_t *)d_wire, d_offsets, payload, d_errc, d_res);
   if ((e = hipGetLastError()) != hipSuccess) return e;

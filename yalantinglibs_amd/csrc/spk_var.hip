@@ -611,7 +611,10 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
   const MsgState *st = reinterpret_cast<const MsgState *>(ws + kWsScratch);
   const uint64_t *bsum = reinterpret_cast<const uint64_t *>(ws + kWsScratch +
                                                             sizeof(MsgState) * a.n_msgs);
-  if (res->errc == SPK_ERRC_CAPACITY) return;  // heaps too small: write nothing
+  // heaps too small: write nothing (messages past rec_cap carry their own
+  // CAPACITY errc and are skipped below; the others are still written)
+  for (uint32_t k = 0; k < a.L.n_spans; ++k)
+    if (res->heap_used[k] > a.heap_cap[k]) return;
   const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
   MsgState s{~0ull, 1, 1};
   uint64_t cnt[SPK_MAX_SPANS] = {};
