@@ -189,6 +189,46 @@ int spk_decode(const spk_layout *L, int mode, const void *d_wire,
                const uint64_t *heap_caps, spk_dresult_t *d_res,
                int32_t *d_errc, void *d_ws, size_t ws_bytes, void *stream);
 
+/* ---- framed message batches (coro_rpc payloads, SPK_MODE_MESSAGES) -----
+ * coro_rpc sends every request as [req_header (20 B)][serialize(args)] and
+ * every response as [resp_header (16 B)][serialize(ret)]: the client reserves
+ * the header with serialize_to_with_offset (ref struct_pack.hpp:176-189,
+ * coro_rpc_client.hpp:1285-1335) and fills it with the DISABLE_ALL_META_INFO
+ * encoding of the header struct, i.e. its raw bytes; the server does the same
+ * with resp_header (coro_rpc_protocol.hpp:191-240). A spk_frame describes
+ * that prefix: a template plus two u32 LE fields patched per message — the
+ * sequence number (seq_base + message index) and the payload length. */
+#define SPK_MAX_FRAME 64u
+#define SPK_FRAME_NONE 0xFFFFFFFFu
+typedef struct spk_frame {
+  uint32_t prefix_len;  /* bytes before every message (0..SPK_MAX_FRAME)     */
+  uint32_t seq_off;     /* u32 LE = seq_base + i at this offset, or NONE     */
+  uint32_t len_off;     /* u32 LE = struct_pack message length, or NONE      */
+  uint32_t seq_base;
+  uint8_t tmpl[SPK_MAX_FRAME]; /* the other prefix bytes (magic, version,
+                                  function_id, attach_length ...)           */
+} spk_frame;
+
+/* spk_encode for SPK_MODE_MESSAGES with a frame prefix before every message:
+ * message i = [prefix][serialize(rec_i)], d_msg_offsets[i] = its frame start;
+ * total = d_plan->total_bytes + n * prefix_len. */
+int spk_encode_framed(const spk_layout *L, uint64_t n, const void *d_recs,
+                      const void *const *d_heaps, const spk_plan_t *d_plan,
+                      const spk_frame *F, void *d_out, uint64_t out_cap,
+                      uint64_t *d_msg_offsets, void *d_ws, size_t ws_bytes,
+                      void *stream);
+/* spk_decode for SPK_MODE_MESSAGES where frame i is
+ * d_wire[d_msg_offsets[i] .. d_msg_offsets[i+1]) and its struct_pack message
+ * starts prefix_len bytes in (the header fields were already checked by the
+ * transport, coro_rpc_protocol.hpp:98-117). A frame shorter than the prefix
+ * reads as no_buffer_space; `consumed` counts message bytes only. */
+int spk_decode_framed(const spk_layout *L, const void *d_wire, uint64_t wire_len,
+                      const uint64_t *d_msg_offsets, uint64_t n_msgs,
+                      uint32_t prefix_len, void *d_recs, uint64_t rec_cap,
+                      void *const *d_heaps, const uint64_t *heap_caps,
+                      spk_dresult_t *d_res, int32_t *d_errc, void *d_ws,
+                      size_t ws_bytes, void *stream);
+
 /* ---- sharded single-message encode (multi-GPU, SPK_MODE_VECTOR) --------
  * One std::vector<T> message whose records are spread over several GPUs:
  * every shard encodes only its records' bytes ("body") with the GLOBAL

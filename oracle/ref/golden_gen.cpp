@@ -9,6 +9,13 @@
 //        mode "A" cases serialize one std::vector<T> message,
 //        mode "B" cases serialize n independent T messages back to back and
 //        write the per-message byte lengths (u64 LE) to <lens_out>.
+//   frames <case> <n> <seed> <param> <req|resp> <function_id> <seq_base>
+//          <wire_out> <lens_out>
+//        coro_rpc framing of n messages, built the way coro_rpc does it:
+//        serialize_to_with_offset(buf, REQ_HEAD_LEN, arg) then the header
+//        struct serialized with DISABLE_ALL_META_INFO into the reserved bytes
+//        (coro_rpc_client.hpp:1285-1335); responses = resp_header bytes +
+//        serialize(ret) (coro_rpc_protocol.hpp:191-240)
 //   errs <case> <n> <seed> <param> <conf> <mutations> <wire_in>
 //        decode every mutation of <wire_in> with the reference deserialize_to
 //        and print errc / consume_len / canonical re-encoding digest (JSON).
@@ -186,6 +193,49 @@ static int cmd_emit(const Args &a, bool modeB, const std::string &wire_out,
 }
 
 // ---------------------------------------------------------------------------
+static int cmd_frames(const Args &a, bool req, uint32_t fid, uint32_t seq_base,
+                      const std::string &wire_out, const std::string &lens_out) {
+  std::string wire;
+  std::vector<uint64_t> lens;
+  bool ok = with_case(a, [&]<typename T>(auto gen) {
+    for (uint64_t i = 0; i < a.n; ++i) {
+      T v{};
+      gen(v, i);
+      std::string buf;
+      if (req) {
+        constexpr size_t off = sizeof(rpcb::req_header);  // REQ_HEAD_LEN = 20
+        struct_pack::serialize_to_with_offset(buf, off, v);
+        rpcb::req_header h{};
+        h.magic = 21;  // coro_rpc_protocol::magic_number
+        h.function_id = fid;
+        h.seq_num = seq_base + (uint32_t)i;
+        h.length = (uint32_t)(buf.size() - off);
+        auto hl = struct_pack::get_needed_size<sp_config::DISABLE_ALL_META_INFO>(h);
+        struct_pack::serialize_to<sp_config::DISABLE_ALL_META_INFO>(buf.data(), hl, h);
+      }
+      else {
+        std::string body;
+        struct_pack::serialize_to(body, v);
+        rpcb::resp_header h{};
+        h.magic = 21;
+        h.seq_num = seq_base + (uint32_t)i;
+        h.length = (uint32_t)body.size();
+        struct_pack::serialize_to<sp_config::DISABLE_ALL_META_INFO>(buf, h);
+        buf += body;
+      }
+      wire += buf;
+      lens.push_back(buf.size());
+    }
+    return true;
+  });
+  if (!ok) return 2;
+  if (!write_file(wire_out, wire.data(), wire.size())) return 3;
+  if (!write_file(lens_out, lens.data(), lens.size() * sizeof(uint64_t))) return 3;
+  std::cout << wire.size() << "\n";
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
 // Negative / mutation tests: mutation list file has lines
 //   trunc <len>            keep the first <len> bytes
 //   set <pos> <byte>       overwrite one byte
@@ -270,6 +320,18 @@ int main(int argc, char **argv) {
   }
   std::string cmd = argv[1];
   if (cmd == "kat") return cmd_kat();
+  if (cmd == "frames" && argc >= 11) {
+    Args a;
+    std::string kase = argv[2];
+    a.kase = kase.substr(0, kase.size() - 2);
+    a.n = strtoull(argv[3], nullptr, 0);
+    a.seed = strtoull(argv[4], nullptr, 0);
+    a.param = (uint32_t)strtoul(argv[5], nullptr, 0);
+    a.conf = "default";
+    return cmd_frames(a, std::string(argv[6]) == "req",
+                      (uint32_t)strtoul(argv[7], nullptr, 0),
+                      (uint32_t)strtoul(argv[8], nullptr, 0), argv[9], argv[10]);
+  }
   if ((cmd == "emit" || cmd == "errs") && argc >= 8) {
     Args a;
     std::string kase = argv[2];

@@ -75,6 +75,37 @@ BIG = [  # BASELINE.json full-size configs (digest only)
 ]
 
 
+# coro_rpc framed batches: (case_B, n, param, req|resp, function name, seq_base)
+FRAMES = [
+    ("rpcrect_B", 100, 0, "req", "echo_rect", 1), ("rpcrect_B", 100, 0, "resp", "", 1),
+    ("person_B", 120, 48, "req", "echo_person", 7), ("person_B", 120, 48, "resp", "", 7),
+    ("ints_B", 20, 1000, "req", "array_1K_int", 0xFFFFFFF0),
+    ("ints_B", 20, 1000, "resp", "", 0xFFFFFFF0), ("rec64_B", 40, 0, "req", "echo_rec64", 0),
+]
+
+
+def func_id(name):
+    """router.hpp:121-127: MD5Hash32Constexpr(function name)"""
+    return int.from_bytes(hashlib.md5(name.encode()).digest()[:4], "big") if name else 0
+
+
+def make_frames(tmp):
+    out = []
+    for cm, n, param, kind, fname, seq in FRAMES:
+        case = cm[:-2]
+        name = f"frames_{case}_{kind}_n{n}_p{param}"
+        wire = os.path.join(HERE, name + ".bin")
+        lens = os.path.join(HERE, name + ".lens")
+        fid = func_id(fname)
+        subprocess.run([GEN, "frames", cm, str(n), str(SEED[case]), str(param), kind, str(fid),
+                        str(seq), wire, lens], check=True, stdout=subprocess.DEVNULL)
+        out.append({"name": name, "case": case, "n": n, "seed": SEED[case], "param": param,
+                    "kind": kind, "function": fname, "function_id": fid, "seq_base": seq,
+                    "file": name + ".bin", "lens": name + ".lens",
+                    "wire_len": os.path.getsize(wire), "sha256": sha256_file(wire)})
+    return out
+
+
 def name_of(cm, n, param, conf):
     return f"{cm}_n{n}_p{param}_{conf}"
 
@@ -208,6 +239,9 @@ def main():
         with open(man_path, "w") as f:
             json.dump(ents, f, indent=1)
         errs = make_errs(tmp)
+        frames = make_frames(tmp)
+    with open(os.path.join(HERE, "frames.json"), "w") as f:
+        json.dump(frames, f, indent=1)
     with open(os.path.join(HERE, "errs.json"), "w") as f:
         json.dump(errs, f, indent=0)
     print(f"{len(ents)} fixtures, {sum(len(e['tests']) for e in errs)} mutation tests")

@@ -15,6 +15,8 @@ SPK_ABI_VERSION = 1
 SPK_MAX_OPS = 64
 SPK_MAX_SPANS = 8
 SPK_MAX_LITERAL = 240
+SPK_MAX_FRAME = 64
+SPK_FRAME_NONE = 0xFFFFFFFF
 
 SPK_OK = 0
 SPK_E_ARG = -1
@@ -76,6 +78,12 @@ class spk_dresult_t(ct.Structure):
                 ("heap_used", ct.c_uint64 * SPK_MAX_SPANS)]
 
 
+class spk_frame(ct.Structure):
+    _fields_ = [("prefix_len", ct.c_uint32), ("seq_off", ct.c_uint32),
+                ("len_off", ct.c_uint32), ("seq_base", ct.c_uint32),
+                ("tmpl", ct.c_uint8 * SPK_MAX_FRAME)]
+
+
 PLAN_BYTES = ct.sizeof(spk_plan_t)
 DRES_BYTES = ct.sizeof(spk_dresult_t)
 
@@ -88,7 +96,7 @@ ORACLE_PATH = os.path.join(_ROOT, "oracle", "libspk_oracle.so")
 CODEC_SYMBOLS = ["spk_abi_version", "spk_errc_message", "spk_layout_check",
                  "spk_workspace_bytes", "spk_plan", "spk_encode", "spk_decode",
                  "spk_synth", "spk_synth_counts", "spk_encode_body",
-                 "spk_vector_header"]
+                 "spk_vector_header", "spk_encode_framed", "spk_decode_framed"]
 
 _codec = None
 _oracle = None
@@ -116,6 +124,11 @@ def _bind_codec(lib):
                                     ct.c_size_t, P]
     lib.spk_vector_header.argtypes = [PL, U64, ct.c_uint32, ct.POINTER(ct.c_uint8),
                                       ct.c_uint32]
+    lib.spk_encode_framed.argtypes = [PL, U64, P, ct.POINTER(P), P, ct.POINTER(spk_frame),
+                                      P, U64, P, P, ct.c_size_t, P]
+    lib.spk_decode_framed.argtypes = [PL, P, U64, P, U64, ct.c_uint32, P, U64,
+                                      ct.POINTER(P), ct.POINTER(U64), P, P, P,
+                                      ct.c_size_t, P]
     lib.spk_synth_counts.argtypes = [ct.c_int, U64, U64, U64, ct.c_uint32, P, P]
     return lib
 

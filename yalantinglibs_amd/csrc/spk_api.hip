@@ -81,10 +81,18 @@ int spk_plan(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
   return hip_rc(launch_var_plan(L, mode, n, d_recs, d_plan, d_ws, ws_bytes, s));
 }
 
-int spk_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
-               const void *const *d_heaps, const spk_plan_t *d_plan, void *d_out,
-               uint64_t out_cap, uint64_t *d_msg_offsets, void *d_ws, size_t ws_bytes,
-               void *stream) {
+static int frame_check(const spk_frame *F) {
+  if (!F) return SPK_OK;
+  if (F->prefix_len > SPK_MAX_FRAME) return SPK_E_ARG;
+  if (F->seq_off != SPK_FRAME_NONE && (uint64_t)F->seq_off + 4 > F->prefix_len) return SPK_E_ARG;
+  if (F->len_off != SPK_FRAME_NONE && (uint64_t)F->len_off + 4 > F->prefix_len) return SPK_E_ARG;
+  return SPK_OK;
+}
+
+static int encode_impl(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
+                       const void *const *d_heaps, const spk_plan_t *d_plan, void *d_out,
+                       uint64_t out_cap, uint64_t *d_msg_offsets, const spk_frame *F,
+                       void *d_ws, size_t ws_bytes, void *stream) {
   int rc = spk_layout_check(L);
   if (rc) return rc;
   if ((mode != SPK_MODE_VECTOR && mode != SPK_MODE_MESSAGES) || !d_plan || !d_ws || !d_out)
@@ -100,9 +108,10 @@ int spk_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
       if (total > out_cap) return SPK_E_CAPACITY;
       return hip_rc(launch_fixed_encode_vector(L, n, d_recs, d_out, d_ws, s));
     }
-    const uint64_t total = n * (uint64_t)(write_hdr(hb, L->fmt_one, 1) + L->rec_stride);
+    const uint32_t P = F ? F->prefix_len : 0;
+    const uint64_t total = n * (uint64_t)(P + write_hdr(hb, L->fmt_one, 1) + L->rec_stride);
     if (total > out_cap) return SPK_E_CAPACITY;
-    return hip_rc(launch_fixed_encode_messages(L, n, d_recs, d_out, d_msg_offsets, s));
+    return hip_rc(launch_fixed_encode_messages(L, n, d_recs, d_out, d_msg_offsets, F, s));
   }
   if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
   uint32_t spans = 0;
@@ -111,14 +120,33 @@ int spk_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
   for (uint32_t k = 0; k < spans; ++k)
     if (!d_heaps[k] && n) return SPK_E_ARG;
   return hip_rc(launch_var_encode(L, mode, n, d_recs, d_heaps, d_plan, d_out, out_cap,
-                                  d_msg_offsets, d_ws, ws_bytes, s));
+                                  d_msg_offsets, F, d_ws, ws_bytes, s));
 }
 
-int spk_decode(const spk_layout *L, int mode, const void *d_wire, uint64_t wire_len,
-               const uint64_t *d_msg_offsets, uint64_t n_msgs, void *d_recs,
-               uint64_t rec_cap, void *const *d_heaps, const uint64_t *heap_caps,
-               spk_dresult_t *d_res, int32_t *d_errc, void *d_ws, size_t ws_bytes,
+int spk_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
+               const void *const *d_heaps, const spk_plan_t *d_plan, void *d_out,
+               uint64_t out_cap, uint64_t *d_msg_offsets, void *d_ws, size_t ws_bytes,
                void *stream) {
+  return encode_impl(L, mode, n, d_recs, d_heaps, d_plan, d_out, out_cap, d_msg_offsets,
+                     nullptr, d_ws, ws_bytes, stream);
+}
+
+int spk_encode_framed(const spk_layout *L, uint64_t n, const void *d_recs,
+                      const void *const *d_heaps, const spk_plan_t *d_plan,
+                      const spk_frame *F, void *d_out, uint64_t out_cap,
+                      uint64_t *d_msg_offsets, void *d_ws, size_t ws_bytes, void *stream) {
+  if (!F) return SPK_E_ARG;
+  int rc = frame_check(F);
+  if (rc) return rc;
+  return encode_impl(L, SPK_MODE_MESSAGES, n, d_recs, d_heaps, d_plan, d_out, out_cap,
+                     d_msg_offsets, F, d_ws, ws_bytes, stream);
+}
+
+static int decode_impl(const spk_layout *L, int mode, const void *d_wire, uint64_t wire_len,
+                       const uint64_t *d_msg_offsets, uint64_t n_msgs, uint32_t prefix,
+                       void *d_recs, uint64_t rec_cap, void *const *d_heaps,
+                       const uint64_t *heap_caps, spk_dresult_t *d_res, int32_t *d_errc,
+                       void *d_ws, size_t ws_bytes, void *stream) {
   int rc = spk_layout_check(L);
   if (rc) return rc;
   if ((mode != SPK_MODE_VECTOR && mode != SPK_MODE_MESSAGES) || !d_res || !d_ws)
@@ -133,14 +161,35 @@ int spk_decode(const spk_layout *L, int mode, const void *d_wire, uint64_t wire_
       return hip_rc(launch_fixed_decode_vector(L, d_wire, wire_len, d_recs, rec_cap, d_res,
                                                d_ws, s));
     return hip_rc(launch_fixed_decode_messages(L, d_wire, wire_len, d_msg_offsets, n_msgs,
-                                               d_recs, rec_cap, d_res, d_errc, d_ws, s));
+                                               prefix, d_recs, rec_cap, d_res, d_errc, d_ws,
+                                               s));
   }
   if (d_recs && (uintptr_t)d_recs % 8) return SPK_E_ARG;
   if (!d_heaps || !heap_caps) return SPK_E_ARG;
   if (mode == SPK_MODE_MESSAGES && n_msgs && !d_msg_offsets) return SPK_E_ARG;
-  return hip_rc(launch_var_decode(L, mode, d_wire, wire_len, d_msg_offsets, n_msgs, d_recs,
-                                  rec_cap, d_heaps, heap_caps, d_res, d_errc, d_ws, ws_bytes,
-                                  s));
+  return hip_rc(launch_var_decode(L, mode, d_wire, wire_len, d_msg_offsets, n_msgs, prefix,
+                                  d_recs, rec_cap, d_heaps, heap_caps, d_res, d_errc, d_ws,
+                                  ws_bytes, s));
+}
+
+int spk_decode(const spk_layout *L, int mode, const void *d_wire, uint64_t wire_len,
+               const uint64_t *d_msg_offsets, uint64_t n_msgs, void *d_recs,
+               uint64_t rec_cap, void *const *d_heaps, const uint64_t *heap_caps,
+               spk_dresult_t *d_res, int32_t *d_errc, void *d_ws, size_t ws_bytes,
+               void *stream) {
+  return decode_impl(L, mode, d_wire, wire_len, d_msg_offsets, n_msgs, 0, d_recs, rec_cap,
+                     d_heaps, heap_caps, d_res, d_errc, d_ws, ws_bytes, stream);
+}
+
+int spk_decode_framed(const spk_layout *L, const void *d_wire, uint64_t wire_len,
+                      const uint64_t *d_msg_offsets, uint64_t n_msgs, uint32_t prefix_len,
+                      void *d_recs, uint64_t rec_cap, void *const *d_heaps,
+                      const uint64_t *heap_caps, spk_dresult_t *d_res, int32_t *d_errc,
+                      void *d_ws, size_t ws_bytes, void *stream) {
+  if (prefix_len > SPK_MAX_FRAME || (n_msgs && !d_msg_offsets)) return SPK_E_ARG;
+  return decode_impl(L, SPK_MODE_MESSAGES, d_wire, wire_len, d_msg_offsets, n_msgs,
+                     prefix_len, d_recs, rec_cap, d_heaps, heap_caps, d_res, d_errc, d_ws,
+                     ws_bytes, stream);
 }
 
 int spk_encode_body(const spk_layout *L, uint64_t n, const void *d_recs,

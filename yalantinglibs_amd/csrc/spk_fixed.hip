@@ -248,12 +248,24 @@ hipError_t launch_fixed_decode_vector(const spk_layout *L, const void *d_wire,
 
 // ---------------------------------------------------------------------------
 // SPK_MODE_MESSAGES, trivial records: message i = [hdr (H bytes)][record].
+constexpr uint32_t kMsgHdrMax = 320;  // frame prefix (<= 64) + struct_pack header
+
 struct MsgEncArgs {
   uint64_t n;
-  uint32_t stride;  // bytes
-  uint32_t hlen;    // header bytes
-  uint8_t hdr[256];
+  uint32_t stride;    // bytes
+  uint32_t hlen;      // header bytes (frame prefix + struct_pack header)
+  uint32_t seq_off;   // frame sequence field (u32 LE = seq_base + i) or ~0u
+  uint32_t seq_base;
+  uint8_t hdr[kMsgHdrMax];
 };
+
+// byte r (< hlen) of message i's header: the template, with the frame's
+// sequence number field patched in
+__device__ __forceinline__ uint8_t msg_hdr_byte(const uint8_t *hdr, uint32_t r, uint64_t i,
+                                                uint32_t seq_off, uint32_t seq_base) {
+  const uint32_t q = r - seq_off;
+  return r >= seq_off && q < 4 ? (uint8_t)((seq_base + (uint32_t)i) >> (8 * q)) : hdr[r];
+}
 
 // dword gather: out dword d -> message i = d / Mw, word r = d % Mw
 __global__ __launch_bounds__(256) void fixed_msg_encode_w4(
@@ -274,7 +286,7 @@ __global__ __launch_bounds__(256) void fixed_msg_encode_w4(
       if (r < Hw) {
         uint32_t h;
         __builtin_memcpy(&h, a.hdr + 4 * r, 4);
-        v[j] = h;
+        v[j] = 4 * r == a.seq_off ? a.seq_base + (uint32_t)i : h;
       } else {
         v[j] = (d0 + j < total_w) ? in[i * Sw + (r - Hw)] : 0u;
       }
@@ -309,7 +321,8 @@ __global__ __launch_bounds__(256) void fixed_msg_encode_b1(
        b += gstride) {
     const uint64_t i = b / M;
     const uint32_t r = (uint32_t)(b - i * M);
-    out[b] = r < a.hlen ? a.hdr[r] : in[i * a.stride + (r - a.hlen)];
+    out[b] = r < a.hlen ? msg_hdr_byte(a.hdr, r, i, a.seq_off, a.seq_base)
+                        : in[i * a.stride + (r - a.hlen)];
   }
   if (offs)
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= a.n;
@@ -351,8 +364,10 @@ struct MsgLdsArgs {
   uint32_t R;       // messages per block
   uint32_t cap;     // staging bytes (decode)
   uint32_t fixed_M; // implicit message stride when offsets == nullptr
-  uint32_t pad_;
-  uint8_t hdr[256];
+  uint32_t prefix;  // decode: frame bytes before each message
+  uint32_t seq_off; // encode: frame sequence field or ~0u
+  uint32_t seq_base;
+  uint8_t hdr[kMsgHdrMax];
 };
 
 __device__ __forceinline__ uint32_t lds_u32_at(const uint8_t *lds, uint32_t pos) {
@@ -370,14 +385,14 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_encode_lds(
     uint64_t *__restrict__ offs) {
   extern __shared__ v4u smem_v4[];
   uint8_t *hdr = reinterpret_cast<uint8_t *>(smem_v4);
-  uint8_t *inl = hdr + 256;
+  uint8_t *inl = hdr + kMsgHdrMax;
   const uint32_t tid = threadIdx.x;
   const uint32_t S = a.stride, H = a.hlen, M = H + S;
   const uint64_t first = (uint64_t)blockIdx.x * a.R;
   if (offs && blockIdx.x == gridDim.x - 1 && tid == 0) offs[a.n] = a.n * M;
   if (first >= a.n) return;
   const uint32_t nR = (uint32_t)((a.n - first) < a.R ? (a.n - first) : a.R);
-  if (tid < H) hdr[tid] = a.hdr[tid];
+  for (uint32_t k = tid; k < H; k += kMsgThreads) hdr[k] = a.hdr[k];
   const uint8_t *src = in + first * S;
   const uint32_t bin = nR * S;  // multiple of 4
   for (uint32_t c = tid; c < bin / 16; c += kMsgThreads)
@@ -391,6 +406,7 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_encode_lds(
   const uint32_t bout = nR * M;
   if constexpr (DW) {
     const uint32_t Mw = M / 4, Hw = H / 4, Sw = S / 4, nq = bout / 4;
+    const uint32_t seq_w = a.seq_off / 4;  // dword-aligned (host-checked) or huge
     const uint32_t *hw = reinterpret_cast<const uint32_t *>(hdr);
     const uint32_t *iw = reinterpret_cast<const uint32_t *>(inl);
     for (uint32_t t = tid; 4 * t < nq; t += kMsgThreads) {
@@ -399,7 +415,8 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_encode_lds(
       uint32_t v[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        v[k] = r < Hw ? hw[r] : iw[i * Sw + (r - Hw)];
+        v[k] = r < Hw ? (r == seq_w ? a.seq_base + (uint32_t)(first + i) : hw[r])
+                      : iw[i * Sw + (r - Hw)];
         if (++r == Mw) {
           r = 0;
           ++i;
@@ -416,7 +433,8 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_encode_lds(
   } else {
     for (uint32_t j = tid; j < bout; j += kMsgThreads) {
       const uint32_t i = j / M, r = j - i * M;
-      dst[j] = r < H ? hdr[r] : inl[i * S + (r - H)];
+      dst[j] = r < H ? msg_hdr_byte(hdr, r, first + i, a.seq_off, a.seq_base)
+                     : inl[i * S + (r - H)];
     }
   }
 }
@@ -444,7 +462,8 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
       const uint64_t i = first + tid;
       b = offs ? offs[i] : i * a.fixed_M;
       e = offs ? offs[i + 1] : (i + 1) * a.fixed_M;
-      inr = e >= b && e <= a.wire_len;
+      inr = e >= b && e <= a.wire_len && e - b >= a.prefix;
+      b += a.prefix;  // the struct_pack message starts after the frame prefix
     }
     // block min of starts / max of ends over in-range messages
     uint64_t mn = inr ? b : ~0ull, mx = inr ? e : 0;
@@ -559,20 +578,46 @@ static uint32_t msg_block_R(uint32_t M) {
   return R & ~15u;
 }
 
+// frame prefix + struct_pack header of one message into hdr; returns the
+// length. The frame's length field is constant for trivial records.
+static uint32_t msg_header(const spk_layout *L, const spk_frame *F, uint8_t *hdr,
+                           uint32_t *seq_off, uint32_t *seq_base) {
+  uint32_t P = 0;
+  *seq_off = ~0u;
+  *seq_base = 0;
+  if (F) {
+    P = F->prefix_len;
+    for (uint32_t k = 0; k < P; ++k) hdr[k] = F->tmpl[k];
+  }
+  const uint32_t H = write_hdr(hdr + P, L->fmt_one, 1);
+  if (F) {
+    const uint32_t len = H + L->rec_stride;
+    if (F->len_off != SPK_FRAME_NONE)
+      for (int k = 0; k < 4; ++k) hdr[F->len_off + k] = (uint8_t)(len >> (8 * k));
+    if (F->seq_off != SPK_FRAME_NONE) {
+      *seq_off = F->seq_off;
+      *seq_base = F->seq_base;
+    }
+  }
+  return P + H;
+}
+
 hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
                                         const void *d_recs, void *d_out,
-                                        uint64_t *d_offsets, hipStream_t s) {
+                                        uint64_t *d_offsets, const spk_frame *F,
+                                        hipStream_t s) {
   {
     MsgLdsArgs b = {};
     b.n = n;
     b.stride = L->rec_stride;
-    b.hlen = write_hdr(b.hdr, L->fmt_one, 1);
+    b.hlen = msg_header(L, F, b.hdr, &b.seq_off, &b.seq_base);
     const uint32_t M = b.hlen + b.stride;
     b.R = msg_block_R(M);
-    const bool dw = (b.hlen % 4 == 0) && ((uintptr_t)d_out % 16 == 0);
-    if (b.R && b.hlen <= 256 && (uintptr_t)d_recs % 4 == 0) {
+    const bool dw = (b.hlen % 4 == 0) && (b.seq_off == ~0u || b.seq_off % 4 == 0) &&
+                    ((uintptr_t)d_out % 16 == 0);
+    if (b.R && (uintptr_t)d_recs % 4 == 0) {
       const uint64_t blocks = n ? (n + b.R - 1) / b.R : 1;
-      const size_t lds = 256 + (size_t)b.R * b.stride + 16;
+      const size_t lds = kMsgHdrMax + (size_t)b.R * b.stride + 16;
       if (dw)
         hipLaunchKernelGGL(fixed_msg_encode_lds<true>, dim3((unsigned)blocks),
                            dim3(kMsgThreads), lds, s, b, (const uint8_t *)d_recs,
@@ -587,8 +632,9 @@ hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
   MsgEncArgs a = {};
   a.n = n;
   a.stride = L->rec_stride;
-  a.hlen = write_hdr(a.hdr, L->fmt_one, 1);
+  a.hlen = msg_header(L, F, a.hdr, &a.seq_off, &a.seq_base);
   const bool w4 = (a.hlen % 4 == 0) && (a.stride % 4 == 0) &&
+                  (a.seq_off == ~0u || a.seq_off % 4 == 0) &&
                   ((uintptr_t)d_recs % 4 == 0) && ((uintptr_t)d_out % 16 == 0);
   if (w4) {
     const uint64_t chunks = (n * ((a.hlen + a.stride) / 4) + 3) / 4;
@@ -612,6 +658,7 @@ struct MsgDecArgs {
   uint64_t rec_cap;
   uint32_t stride;
   uint32_t fixed_M;  // implicit message stride when offsets == nullptr
+  uint32_t prefix;   // frame bytes before each message
 };
 
 __global__ __launch_bounds__(256) void fixed_msg_parse(
@@ -627,7 +674,9 @@ __global__ __launch_bounds__(256) void fixed_msg_parse(
     int32_t ec = SPK_ERRC_OK;
     uint64_t pos = 0, dl = 0;
     uint32_t w = 1;
-    if (e < b || e > a.wire_len) {
+    const bool inr = e >= b && e <= a.wire_len && e - b >= a.prefix;
+    b += a.prefix;
+    if (!inr) {
       ec = SPK_ERRC_NO_BUFFER_SPACE;
     } else {
       ec = parse_hdr(a.fmt, wire + b, e - b, &pos, &w, &dl);
@@ -693,17 +742,18 @@ __global__ __launch_bounds__(256) void fixed_msg_gather(
 
 hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
                                            uint64_t wire_len, const uint64_t *d_offsets,
-                                           uint64_t n, void *d_recs, uint64_t rec_cap,
-                                           spk_dresult_t *d_res, int32_t *d_errc,
-                                           void *d_ws, hipStream_t s) {
+                                           uint64_t n, uint32_t prefix, void *d_recs,
+                                           uint64_t rec_cap, spk_dresult_t *d_res,
+                                           int32_t *d_errc, void *d_ws, hipStream_t s) {
   MsgDecArgs a;
+  a.prefix = prefix;
   a.fmt = L->fmt_one;
   a.n = n;
   a.wire_len = wire_len;
   a.rec_cap = rec_cap;
   a.stride = L->rec_stride;
   uint8_t hb[4 + 1 + SPK_MAX_LITERAL + 1];
-  a.fixed_M = write_hdr(hb, L->fmt_one, 1) + L->rec_stride;
+  a.fixed_M = prefix + write_hdr(hb, L->fmt_one, 1) + L->rec_stride;
   uint64_t *payload = reinterpret_cast<uint64_t *>((uint8_t *)d_ws + kWsScratch);
   hipError_t e = hipMemsetAsync(d_res, 0, sizeof(spk_dresult_t), s);
   if (e != hipSuccess) return e;
@@ -715,6 +765,7 @@ hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
     b.rec_cap = rec_cap;
     b.stride = L->rec_stride;
     b.fixed_M = a.fixed_M;
+    b.prefix = prefix;
     b.R = msg_block_R(a.fixed_M);
     if (b.R && (uintptr_t)d_recs % 16 == 0 && n > 0) {
       b.cap = b.R * a.fixed_M + 32;

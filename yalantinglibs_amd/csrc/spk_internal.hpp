@@ -171,7 +171,8 @@ hipError_t launch_fixed_encode_vector(const spk_layout *L, uint64_t n,
                                       const void *d_ws, hipStream_t s);
 hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
                                         const void *d_recs, void *d_out,
-                                        uint64_t *d_offsets, hipStream_t s);
+                                        uint64_t *d_offsets, const spk_frame *F,
+                                        hipStream_t s);
 hipError_t launch_fixed_decode_vector(const spk_layout *L, const void *d_wire,
                                       uint64_t wire_len, void *d_recs,
                                       uint64_t rec_cap, spk_dresult_t *d_res,
@@ -179,7 +180,7 @@ hipError_t launch_fixed_decode_vector(const spk_layout *L, const void *d_wire,
 hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
                                         uint64_t wire_len,
                                         const uint64_t *d_offsets, uint64_t n,
-                                        void *d_recs, uint64_t rec_cap,
+                                        uint32_t prefix, void *d_recs, uint64_t rec_cap,
                                         spk_dresult_t *d_res, int32_t *d_errc,
                                         void *d_ws, hipStream_t s);
 // spk_var.hip
@@ -191,15 +192,15 @@ hipError_t launch_var_plan(const spk_layout *L, int mode, uint64_t n,
 hipError_t launch_var_encode(const spk_layout *L, int mode, uint64_t n,
                              const void *d_recs, const void *const *d_heaps,
                              const spk_plan_t *d_plan, void *d_out,
-                             uint64_t out_cap, uint64_t *d_offsets, void *d_ws,
-                             size_t ws_bytes, hipStream_t s);
+                             uint64_t out_cap, uint64_t *d_offsets, const spk_frame *F,
+                             void *d_ws, size_t ws_bytes, hipStream_t s);
 hipError_t launch_var_encode_body(const spk_layout *L, uint64_t n, const void *d_recs,
                                   const void *const *d_heaps, uint32_t width, void *d_out,
                                   uint64_t out_cap, void *d_ws, size_t ws_bytes,
                                   hipStream_t s);
 hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
                              uint64_t wire_len, const uint64_t *d_offsets,
-                             uint64_t n_msgs, void *d_recs, uint64_t rec_cap,
+                             uint64_t n_msgs, uint32_t prefix, void *d_recs, uint64_t rec_cap,
                              void *const *d_heaps, const uint64_t *heap_caps,
                              spk_dresult_t *d_res, int32_t *d_errc, void *d_ws,
                              size_t ws_bytes, hipStream_t s);

@@ -48,8 +48,13 @@ struct VarArgs {
   KLayout L;
   uint64_t n;
   int mode;
-  uint32_t pad_;
+  uint32_t fpre;      // MESSAGES: frame prefix bytes before every message
   const uint8_t *heaps[SPK_MAX_SPANS];
+  uint32_t fseq_off;  // frame u32 fields (SPK_FRAME_NONE: absent)
+  uint32_t flen_off;
+  uint32_t fseq_base;
+  uint32_t pad_;
+  uint8_t ftmpl[SPK_MAX_FRAME];
 };
 
 static KLayout make_klayout(const spk_layout *L) {
@@ -349,6 +354,21 @@ __device__ __forceinline__ void win_record(const VarArgs &a, const uint8_t *rec,
   }
 }
 
+// frame prefix of message i (payload length plen) at output position pos:
+// the template with the sequence number and length fields patched
+__device__ __forceinline__ void win_frame(const VarArgs &a, const Win &W, uint64_t pos,
+                                          uint64_t i, uint64_t plen) {
+  for (uint32_t x = 0; x < a.fpre; ++x) {
+    const uint64_t y = pos + x;
+    if (y < W.lo || y >= W.hi) continue;
+    uint8_t v = a.ftmpl[x];
+    if (x >= a.fseq_off && x - a.fseq_off < 4)
+      v = (uint8_t)((a.fseq_base + (uint32_t)i) >> (8 * (x - a.fseq_off)));
+    if (x >= a.flen_off && x - a.flen_off < 4) v = (uint8_t)(plen >> (8 * (x - a.flen_off)));
+    W.lds[y - W.lo] = v;
+  }
+}
+
 constexpr uint32_t kEncWin = 20 * 1024;  // LDS assembly window per block
 
 // Write pass: records r0 + j*kThreads + tid (consecutive lanes on consecutive
@@ -360,7 +380,8 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
     const spk_plan_t *__restrict__ plan, uint64_t *__restrict__ offs) {
   __shared__ __align__(16) uint8_t lds[kEncWin];
   __shared__ uint64_t sh[kThreads / 64];
-  const uint64_t total = plan->total_bytes;
+  const uint64_t total =
+      plan->total_bytes + (a.mode == SPK_MODE_MESSAGES ? a.n * (uint64_t)a.fpre : 0);
   if (total > out_cap) return;  // caller reads plan->total_bytes
   const uint32_t w_vec = plan->width;
   const uint32_t hdr_vec = plan->header_bytes;
@@ -371,7 +392,7 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
   for (uint32_t j = 0; j < blockIdx.x % kPlanSub; ++j) gb += pb.sub[j];
   const uint64_t g0 = a.mode == SPK_MODE_VECTOR
                           ? hdr_vec + gb + r0 * (uint64_t)a.L.n_spans * w_vec
-                          : gb;
+                          : gb + r0 * (uint64_t)a.fpre;
   if (a.mode == SPK_MODE_VECTOR && blockIdx.x == 0)
     for (uint32_t i = threadIdx.x; i < hdr_vec; i += blockDim.x) out[i] = ws[kWsHdrVec + i];
   uint64_t pj[kIPT], szj[kIPT];
@@ -388,7 +409,8 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
         sz = var + (uint64_t)a.L.n_spans * w_vec;
       } else {
         w = width_of(maxc);
-        sz = ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + wlog(w)] + var + (uint64_t)a.L.n_spans * w;
+        sz = a.fpre + ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + wlog(w)] + var +
+             (uint64_t)a.L.n_spans * w;
       }
     }
     uint64_t btot;
@@ -409,6 +431,10 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
       if (i >= a.n || pj[j] >= W.hi || pj[j] + szj[j] <= W.lo) continue;
       uint64_t q = pj[j];
       if (a.mode == SPK_MODE_MESSAGES) {
+        if (a.fpre) {
+          win_frame(a, W, q, i, szj[j] - a.fpre);
+          q += a.fpre;
+        }
         const uint32_t sl = wlog(wj[j]);
         const uint32_t hl = ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + sl];
         win_put(W, q, ws + kWsHdrMsg + sl * kWsHdrSlot, hl);
@@ -508,6 +534,8 @@ struct DecArgs {
   uint64_t rec_cap;
   uint64_t heap_cap[SPK_MAX_SPANS];
   uint8_t *heaps[SPK_MAX_SPANS];
+  uint32_t prefix;  // MESSAGES: frame bytes before every message
+  uint32_t pad_;
 };
 
 
@@ -532,9 +560,10 @@ __global__ __launch_bounds__(kThreads) void var_msg_parse(
   uint64_t cnt[SPK_MAX_SPANS] = {};
   uint64_t ok = 0, consumed = 0;
   if (i < a.n_msgs) {
-    const uint64_t b = offs[i], e = offs[i + 1];
+    const uint64_t f = offs[i], e = offs[i + 1];
+    const uint64_t b = f + a.prefix;  // struct_pack message after the frame prefix
     MsgState s{~0ull, 1, SPK_ERRC_OK};
-    if (e < b || e > a.wire_len) {
+    if (e < f || e > a.wire_len || e - f < a.prefix) {
       s.errc = SPK_ERRC_NO_BUFFER_SPACE;
     } else {
       uint64_t pos, dl;
@@ -1611,6 +1640,7 @@ static VarArgs make_varargs(const spk_layout *L, int mode, uint64_t n,
   a.L = make_klayout(L);
   a.n = n;
   a.mode = mode;
+  a.fseq_off = a.flen_off = SPK_FRAME_NONE;
   for (uint32_t k = 0; k < a.L.n_spans && k < SPK_MAX_SPANS; ++k)
     a.heaps[k] = heaps ? (const uint8_t *)heaps[k] : nullptr;
   return a;
@@ -1649,9 +1679,16 @@ hipError_t launch_var_plan(const spk_layout *L, int mode, uint64_t n, const void
 hipError_t launch_var_encode(const spk_layout *L, int mode, uint64_t n,
                              const void *d_recs, const void *const *d_heaps,
                              const spk_plan_t *d_plan, void *d_out, uint64_t out_cap,
-                             uint64_t *d_offsets, void *d_ws, size_t ws_bytes,
-                             hipStream_t s) {
+                             uint64_t *d_offsets, const spk_frame *F, void *d_ws,
+                             size_t ws_bytes, hipStream_t s) {
   VarArgs a = make_varargs(L, mode, n, d_heaps);
+  if (F && mode == SPK_MODE_MESSAGES) {
+    a.fpre = F->prefix_len;
+    a.fseq_off = F->seq_off;
+    a.flen_off = F->len_off;
+    a.fseq_base = F->seq_base;
+    for (uint32_t k = 0; k < F->prefix_len; ++k) a.ftmpl[k] = F->tmpl[k];
+  }
   uint8_t *ws = (uint8_t *)d_ws;
   if (n == 0) {
     // header (+ zero count) only; reuse the write kernel with one block
@@ -1686,16 +1723,17 @@ hipError_t launch_var_encode_body(const spk_layout *L, uint64_t n, const void *d
   for (uint32_t i = 0; i < L->n_ops; ++i) ns += L->ops[i].kind == SPK_OP_SPAN;
   hipLaunchKernelGGL(body_plan_kernel, dim3(1), dim3(64), 0, s, plan, n, ns, width);
   return launch_var_encode(L, SPK_MODE_VECTOR, n, d_recs, d_heaps, plan, d_out, out_cap,
-                           nullptr, d_ws, ws_bytes, s);
+                           nullptr, nullptr, d_ws, ws_bytes, s);
 }
 
 hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
                              uint64_t wire_len, const uint64_t *d_offsets,
-                             uint64_t n_msgs, void *d_recs, uint64_t rec_cap,
-                             void *const *d_heaps, const uint64_t *heap_caps,
-                             spk_dresult_t *d_res, int32_t *d_errc, void *d_ws,
-                             size_t ws_bytes, hipStream_t s) {
+                             uint64_t n_msgs, uint32_t prefix, void *d_recs,
+                             uint64_t rec_cap, void *const *d_heaps,
+                             const uint64_t *heap_caps, spk_dresult_t *d_res,
+                             int32_t *d_errc, void *d_ws, size_t ws_bytes, hipStream_t s) {
   DecArgs a = {};
+  a.prefix = prefix;
   a.L = make_klayout(L);
   a.fmt = mode == SPK_MODE_VECTOR ? L->fmt_vector : L->fmt_one;
   a.wire_len = wire_len;

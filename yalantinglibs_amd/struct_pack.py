@@ -122,11 +122,21 @@ class Codec:
 
     def serialize_to(self, out: torch.Tensor, batch: RecordBatch, mode: int = MODE_VECTOR,
                      offsets: Optional[torch.Tensor] = None, stream=None,
-                     planned: bool = False):
-        """Plan + write into a caller-owned device buffer (no host sync)."""
+                     planned: bool = False, frame: Optional[C.spk_frame] = None):
+        """Plan + write into a caller-owned device buffer (no host sync).
+        `frame` (MODE_MESSAGES only) reserves and fills a per-message prefix
+        such as coro_rpc's req_header (see yalantinglibs_amd.coro_rpc)."""
         if not planned:
             self.plan(batch, mode, stream)
         ws = self.workspace(mode, batch.n)
+        if frame is not None:
+            if mode != MODE_MESSAGES:
+                raise ValueError("frames apply to MODE_MESSAGES batches")
+            self._check(self.lib.spk_encode_framed(
+                self.L.ptr, batch.n, _p(batch.recs), self._heap_ptrs(batch.heaps),
+                _p(self.plan_buf), ct.byref(frame), _p(out), out.numel(), _p(offsets),
+                _p(ws), ws.numel(), _stream(stream)), "spk_encode_framed")
+            return
         self._check(self.lib.spk_encode(self.L.ptr, mode, batch.n, _p(batch.recs),
                                         self._heap_ptrs(batch.heaps), _p(self.plan_buf),
                                         _p(out), out.numel(), _p(offsets), _p(ws),
@@ -145,14 +155,23 @@ class Codec:
     def deserialize_to(self, out: RecordBatch, wire: torch.Tensor, mode: int = MODE_VECTOR,
                        offsets: Optional[torch.Tensor] = None, n_msgs: int = 0,
                        errc_out: Optional[torch.Tensor] = None, heap_caps=None,
-                       stream=None) -> torch.Tensor:
+                       stream=None, prefix: int = 0) -> torch.Tensor:
         """Decode into caller-owned buffers; returns the device result
-        (spk_dresult_t bytes). Stream-ordered, no host sync."""
+        (spk_dresult_t bytes). Stream-ordered, no host sync. `prefix`
+        (MODE_MESSAGES only) skips a frame header before every message."""
         cap = out.n
         ws = self.workspace(mode, cap if mode == MODE_VECTOR else n_msgs, wire.numel())
         caps = heap_caps or [h.numel() // sp.elem.size
                              for h, sp in zip(out.heaps, self.L.dev.spans)]
         hc = (ct.c_uint64 * max(len(caps), 1))(*(caps or [0]))
+        if prefix:
+            if mode != MODE_MESSAGES:
+                raise ValueError("frames apply to MODE_MESSAGES batches")
+            self._check(self.lib.spk_decode_framed(
+                self.L.ptr, _p(wire), wire.numel(), _p(offsets), n_msgs, prefix, _p(out.recs),
+                cap, self._heap_ptrs(out.heaps), hc, _p(self.res_buf), _p(errc_out), _p(ws),
+                ws.numel(), _stream(stream)), "spk_decode_framed")
+            return self.res_buf
         self._check(self.lib.spk_decode(self.L.ptr, mode, _p(wire), wire.numel(), _p(offsets),
                                         n_msgs, _p(out.recs), cap, self._heap_ptrs(out.heaps),
                                         hc, _p(self.res_buf), _p(errc_out), _p(ws),
