@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS) + ["c5"])
     ap.add_argument("--records", type=int, default=0, help="override records per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--settle", type=float, default=1.0,
@@ -92,6 +92,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
+    if args.config == "c5":
+        return run_c5(args, torch, dist, world, rank, dev)
 
     case, n, param, modech, desc = CONFIGS[args.config]
     if args.records:
@@ -244,6 +246,151 @@ def main():
         }
         if host:
             line["host_path"] = host
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+C5_TYPES = [  # (case, share of messages, param, rpc function name) — coro_rpc bench shapes
+    ("rpcrect", 1, 0, "echo_rect"),          # rect{point p1, p2}   (api/Rect.h)
+    ("person", 1, 48, "echo_person"),        # person{id, name, age, salary}
+    ("ints", 1, 2000, "array_1K_int"),       # std::vector<int>, ~1K elements (data_gen.cpp:61)
+]
+C5_SEEDS = {"rpcrect": 0x5EED0007, "person": 0x5EED0008, "ints": 0x5EED0009}
+
+
+def run_c5(args, torch, dist, world, rank, dev):
+    """C5: a coro_rpc server step over a batch of framed requests of three
+    record types (grouped by function id, one launch per type): decode every
+    [req_header][args] frame, echo, encode every [resp_header][ret] frame.
+    Device-resident `value`; the host-inclusive rate (H2D of the socket
+    buffers + offsets, D2H of the responses) goes in `host_path`."""
+    from yalantinglibs_amd import coro_rpc as RPC
+    from yalantinglibs_amd import layout as LY
+    from yalantinglibs_amd import struct_pack as SP
+    n_total = args.records or 1_000_000
+    shares = sum(s for _, s, _, _ in C5_TYPES)
+    stream = torch.cuda.current_stream(dev)
+    groups = []
+    for case, share, param, fname in C5_TYPES:
+        n = n_total * share // shares
+        cd = SP.Codec(LY.case_layout(case), device=dev)
+        src = SP.synth_batch(cd, case, n, C5_SEEDS[case], param, first=rank * n)
+        plan = cd.get_needed_size(src, SP.MODE_MESSAGES)
+        fid = RPC.func_id(fname)
+        rq = RPC.req_frame(fid, seq_base=rank * n)
+        rs = RPC.resp_frame(seq_base=rank * n)
+        req_len = plan.total_bytes + n * rq.prefix_len
+        req = torch.empty(req_len + 64, dtype=torch.uint8, device=dev)
+        req_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        cd.serialize_to(req, src, SP.MODE_MESSAGES, req_offs, planned=True, frame=rq)
+        elems = [int(h.numel()) // sp.elem.size for h, sp in zip(src.heaps, cd.L.dev.spans)]
+        args_b = cd.alloc_batch(n, elems)
+        resp_len = plan.total_bytes + n * rs.prefix_len
+        resp = torch.empty(resp_len + 64, dtype=torch.uint8, device=dev)
+        resp_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        rec_bytes = src.recs.numel() + sum(int(h.numel()) for h in src.heaps)
+        groups.append(dict(case=case, n=n, cd=cd, src=src, req=req[:req_len],
+                           req_offs=req_offs, args=args_b, resp=resp, resp_offs=resp_offs,
+                           rq=rq, rs=rs, rec_bytes=rec_bytes, req_len=req_len,
+                           resp_len=resp_len))
+
+    def step():
+        for g in groups:
+            cd = g["cd"]
+            cd.deserialize_to(g["args"], g["req"], SP.MODE_MESSAGES, g["req_offs"], g["n"],
+                              stream=stream, prefix=g["rq"].prefix_len)
+            cd.serialize_to(g["resp"], g["args"], SP.MODE_MESSAGES, g["resp_offs"],
+                            stream=stream, frame=g["rs"])
+
+    step()
+    torch.cuda.synchronize(dev)
+    for g in groups:  # correctness gate: every request decoded, echo == source
+        r = g["cd"].result()
+        if (r.errc != 0 or r.count != g["n"] or not torch.equal(g["args"].recs, g["src"].recs)
+                or int(g["resp_offs"][-1].item()) != g["resp_len"]):
+            print(json.dumps({"error": "c5 round trip mismatch", "case": g["case"]}), flush=True)
+            sys.exit(3)
+    t_settle = time.perf_counter()
+    while time.perf_counter() - t_settle < args.settle:
+        step()
+        torch.cuda.synchronize(dev)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    # algorithmic bytes: request frames in + records/heaps out (decode),
+    # records/heaps in + response frames out (encode)
+    algo = sum(g["req_len"] + 2 * g["rec_bytes"] + g["resp_len"] for g in groups)
+    n_msgs = sum(g["n"] for g in groups)
+    ms_step = dt * 1e3 / args.steps
+    value = algo * world * args.steps / dt / 2**30
+
+    host = None
+    if rank == 0:
+        # host-inclusive: socket buffers live in (pinned) host memory
+        h_req = [torch.empty(g["req_len"], dtype=torch.uint8).pin_memory() for g in groups]
+        h_ro = [torch.empty(g["n"] + 1, dtype=torch.int64).pin_memory() for g in groups]
+        h_resp = [torch.empty(g["resp_len"], dtype=torch.uint8).pin_memory() for g in groups]
+        h_so = [torch.empty(g["n"] + 1, dtype=torch.int64).pin_memory() for g in groups]
+        for g, a, b in zip(groups, h_req, h_ro):
+            a.copy_(g["req"])
+            b.copy_(g["req_offs"])
+        torch.cuda.synchronize(dev)
+        reps = 3
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            for g, a, b in zip(groups, h_req, h_ro):
+                g["req"].copy_(a, non_blocking=True)
+                g["req_offs"].copy_(b, non_blocking=True)
+            step()
+            for g, a, b in zip(groups, h_resp, h_so):
+                a.copy_(g["resp"][:g["resp_len"]], non_blocking=True)
+                b.copy_(g["resp_offs"], non_blocking=True)
+        torch.cuda.synchronize(dev)
+        ht = (time.perf_counter() - t1) / reps
+        host = {"ms_per_step": round(ht * 1e3, 3), "gib_s": round(algo / ht / 2**30, 3),
+                "mmsg_per_s": round(n_msgs / ht / 1e6, 3),
+                "note": "H2D of request frames + offsets, decode, echo encode, D2H of "
+                        "response frames + offsets (pinned host buffers)"}
+    if rank == 0:
+        line = {
+            "metric": "struct_pack encode+decode throughput, device-resident (GiB/s)",
+            "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "u8", "data": "synthetic (spk_synth seeded rpcrect/person/ints)",
+            "config": {"workload": "C5: coro_rpc server step, %d framed requests per GPU "
+                                   "(rect / person / vector<int>~1K, one launch per type): "
+                                   "decode [req_header][args], encode [resp_header][ret]"
+                                   % n_msgs,
+                       "messages_per_gpu": n_msgs,
+                       "per_type": {g["case"]: g["n"] for g in groups},
+                       "algorithmic_bytes_per_step_per_gpu": algo,
+                       "parallelism": f"message-range shards x{world}, no data-path collective"},
+            "mmsg_per_s": round(n_msgs * world * args.steps / dt / 1e6, 3),
+            "roofline": {"bound": "hbm", "kernel": "whole step",
+                         "achieved": round(algo / (ms_step * 1e-3) / 1e9, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(algo / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic": None},
+            "cpu_baseline": None,
+            "host_path": host,
+        }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

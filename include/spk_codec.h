@@ -254,6 +254,9 @@ int spk_vector_header(const spk_layout *L, uint64_t total_n, uint32_t width,
 #define SPK_SYNTH_REC64 1
 #define SPK_SYNTH_RECS 2
 #define SPK_SYNTH_OUTER 3
+#define SPK_SYNTH_RPCRECT 4 /* C5 coro_rpc payload shapes */
+#define SPK_SYNTH_PERSON 5
+#define SPK_SYNTH_INTS 6
 int spk_synth(int kind, uint64_t seed, uint64_t first, uint64_t n,
               uint32_t param, void *d_recs, void *d_heap,
               const uint64_t *d_heap_offsets, void *stream);

@@ -45,6 +45,9 @@ SPK_LAYOUT_TRIVIAL = 0x1
 SPK_SYNTH_REC64 = 1
 SPK_SYNTH_RECS = 2
 SPK_SYNTH_OUTER = 3
+SPK_SYNTH_RPCRECT = 4
+SPK_SYNTH_PERSON = 5
+SPK_SYNTH_INTS = 6
 
 
 class spk_op(ct.Structure):

@@ -100,6 +100,64 @@ __global__ void synth_outer(uint64_t seed, uint64_t first, uint64_t n, uint32_t 
   }
 }
 
+// ---- C5 coro_rpc payload shapes (types.hpp rpcb::rect / person, make_ints)
+struct PersonDev {  // schema.flatten(person): id, name.n, name.off, age, salary
+  int32_t id;
+  uint32_t n;
+  uint64_t off;
+  int32_t age;
+  uint32_t pad;
+  double salary;
+};
+struct IntsDev {  // schema.flatten(std::vector<int32_t>): value.n, value.off
+  uint32_t n;
+  uint32_t pad;
+  uint64_t off;
+};
+
+__global__ void synth_rpcrect(uint64_t seed, uint64_t first, uint64_t n, double *out) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gs)
+    for (int k = 0; k < 4; ++k) out[4 * t + k] = rd(rnd(seed, first + t, k));
+}
+
+__global__ void synth_person(uint64_t seed, uint64_t first, uint64_t n, uint32_t param,
+                             PersonDev *out, uint8_t *heap, const uint64_t *hoff) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gs) {
+    const uint64_t i = first + t;
+    PersonDev r;
+    r.id = (int32_t)(uint32_t)rnd(seed, i, 0);
+    r.n = (uint32_t)(rnd(seed, i, 1) % (uint64_t)(param + 1));
+    r.off = hoff[t];
+    r.age = (int32_t)(rnd(seed, i, 60) % 100);
+    r.pad = 0;
+    r.salary = rd(rnd(seed, i, 61));
+    out[t] = r;
+    uint8_t *dst = heap + r.off;
+    for (uint32_t j = 0; j < r.n; ++j) {
+      const uint64_t w = rnd(seed, i, 2 + (j >> 3) % 56);
+      dst[j] = (uint8_t)('a' + ((w >> ((j & 7) * 8)) & 0xFF) % 26);
+    }
+  }
+}
+
+__global__ void synth_ints(uint64_t seed, uint64_t first, uint64_t n, uint32_t param,
+                           IntsDev *out, uint8_t *heap, const uint64_t *hoff) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gs) {
+    const uint64_t i = first + t;
+    IntsDev r;
+    r.n = (uint32_t)(rnd(seed, i, 1) % (uint64_t)(param + 1));
+    r.pad = 0;
+    r.off = hoff[t];
+    out[t] = r;
+    int32_t *dst = reinterpret_cast<int32_t *>(heap + r.off * 4);
+    const uint64_t base = rnd(seed, i, 2);
+    for (uint32_t j = 0; j < r.n; ++j) dst[j] = (int32_t)(uint32_t)mix64(base + j);
+  }
+}
+
 unsigned grid_of(uint64_t n) {
   uint64_t b = (n + 255) / 256;
   if (b > 8192) b = 8192;
@@ -110,7 +168,9 @@ unsigned grid_of(uint64_t n) {
 
 extern "C" int spk_synth_counts(int kind, uint64_t seed, uint64_t first, uint64_t n,
                                 uint32_t param, uint64_t *d_counts, void *stream) {
-  if (!d_counts || (kind != SPK_SYNTH_RECS && kind != SPK_SYNTH_OUTER)) return SPK_E_ARG;
+  if (!d_counts || (kind != SPK_SYNTH_RECS && kind != SPK_SYNTH_OUTER &&
+                    kind != SPK_SYNTH_PERSON && kind != SPK_SYNTH_INTS))
+    return SPK_E_ARG;
   hipLaunchKernelGGL(synth_counts, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, kind,
                      seed, first, n, param, d_counts);
   return hipGetLastError() == hipSuccess ? SPK_OK : SPK_E_HIP;
@@ -135,6 +195,20 @@ extern "C" int spk_synth(int kind, uint64_t seed, uint64_t first, uint64_t n, ui
       if (!d_heap_offsets) return SPK_E_ARG;
       hipLaunchKernelGGL(synth_outer, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n, param,
                          (OuterDev *)d_recs, (uint8_t *)d_heap, d_heap_offsets);
+      break;
+    case SPK_SYNTH_RPCRECT:
+      hipLaunchKernelGGL(synth_rpcrect, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n,
+                         (double *)d_recs);
+      break;
+    case SPK_SYNTH_PERSON:
+      if (!d_heap_offsets) return SPK_E_ARG;
+      hipLaunchKernelGGL(synth_person, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n,
+                         param, (PersonDev *)d_recs, (uint8_t *)d_heap, d_heap_offsets);
+      break;
+    case SPK_SYNTH_INTS:
+      if (!d_heap_offsets) return SPK_E_ARG;
+      hipLaunchKernelGGL(synth_ints, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n, param,
+                         (IntsDev *)d_recs, (uint8_t *)d_heap, d_heap_offsets);
       break;
     default:
       return SPK_E_ARG;

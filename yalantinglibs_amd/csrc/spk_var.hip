@@ -333,9 +333,10 @@ __device__ __forceinline__ void win_put_le(const Win &W, uint64_t pos, uint64_t 
   }
 }
 
-// one record at output position pos (width w) into the window
+// one record at output position pos (width w) into the window; span payloads
+// whose bit is set in `skip` are copied cooperatively by the block instead
 __device__ __forceinline__ void win_record(const VarArgs &a, const uint8_t *rec, uint32_t w,
-                                           uint64_t pos, const Win &W) {
+                                           uint64_t pos, const Win &W, uint32_t skip = 0) {
   uint32_t sk = 0;
   for (uint32_t o = 0; o < a.L.n_ops; ++o) {
     const spk_op op = a.L.ops[o];
@@ -347,11 +348,58 @@ __device__ __forceinline__ void win_record(const VarArgs &a, const uint8_t *rec,
       win_put_le(W, pos, c, w);
       pos += w;
       const uint64_t nb = c * op.size;
-      if (nb) win_put(W, pos, a.heaps[sk] + rec_u64(rec, op.aux) * op.size, nb);
+      if (nb && !(skip >> sk & 1)) win_put(W, pos, a.heaps[sk] + rec_u64(rec, op.aux) * op.size, nb);
       pos += nb;
       ++sk;
     }
   }
+}
+
+// ---- block-cooperative copies of large span payloads --------------------------
+// One lane copying a multi-KiB string / vector payload serialises the block
+// (e.g. the std::vector<int>(1K) messages of C5). Payloads of at least
+// kBigBytes are listed per block (in record order, via a block scan) and
+// copied by all lanes together: aligned 16-B destination chunks fed by
+// unaligned 16-B source loads.
+constexpr uint32_t kBigBytes = 256;
+constexpr uint32_t kBigMax = 256;  // list capacity per block (overflow: lane copies)
+
+struct BigSeg {
+  uint64_t dst;        // encode: output byte position; decode: unused
+  uint8_t *dptr;       // decode: destination pointer
+  const uint8_t *src;
+  uint64_t n;
+};
+
+// bytes [pos, pos+n) of the output come from src: the part inside the window,
+// written by the whole block (16-B aligned LDS chunks, bytes at the edges)
+__device__ __forceinline__ void win_put_coop(const Win &W, uint64_t pos, const uint8_t *src,
+                                             uint64_t n) {
+  const uint64_t a = pos > W.lo ? pos : W.lo;
+  const uint64_t b = pos + n < W.hi ? pos + n : W.hi;
+  if (a >= b) return;
+  const uint64_t ca = (a + 15) & ~15ull, cb = b & ~15ull;  // W.lo is 16-aligned
+  if (ca >= cb) {
+    for (uint64_t x = a + threadIdx.x; x < b; x += blockDim.x) W.lds[x - W.lo] = src[x - pos];
+    return;
+  }
+  for (uint64_t x = a + threadIdx.x; x < ca; x += blockDim.x) W.lds[x - W.lo] = src[x - pos];
+  for (uint64_t x = cb + threadIdx.x; x < b; x += blockDim.x) W.lds[x - W.lo] = src[x - pos];
+  for (uint64_t c = ca + 16 * (uint64_t)threadIdx.x; c < cb; c += 16 * (uint64_t)blockDim.x)
+    *reinterpret_cast<v4u_t *>(W.lds + (c - W.lo)) =
+        *reinterpret_cast<const v4u_una *>(src + (c - pos));
+}
+
+// d[0, n) = s[0, n) by the whole block
+__device__ __forceinline__ void coop_copy(uint8_t *d, const uint8_t *s, uint64_t n) {
+  uint64_t head = (16 - ((uintptr_t)d & 15)) & 15;
+  if (head > n) head = n;
+  const uint64_t body = (n - head) & ~15ull;
+  for (uint64_t x = threadIdx.x; x < head; x += blockDim.x) d[x] = s[x];
+  for (uint64_t x = head + body + threadIdx.x; x < n; x += blockDim.x) d[x] = s[x];
+  for (uint64_t c = threadIdx.x; c < body / 16; c += blockDim.x)
+    *reinterpret_cast<v4u_t *>(d + head + 16 * c) =
+        *reinterpret_cast<const v4u_una *>(s + head + 16 * c);
 }
 
 // frame prefix of message i (payload length plen) at output position pos:
@@ -380,6 +428,7 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
     const spk_plan_t *__restrict__ plan, uint64_t *__restrict__ offs) {
   __shared__ __align__(16) uint8_t lds[kEncWin];
   __shared__ uint64_t sh[kThreads / 64];
+  __shared__ BigSeg big[kBigMax];
   const uint64_t total =
       plan->total_bytes + (a.mode == SPK_MODE_MESSAGES ? a.n * (uint64_t)a.fpre : 0);
   if (total > out_cap) return;  // caller reads plan->total_bytes
@@ -424,6 +473,47 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
     offs[a.n] = total;
   const uint64_t g1 = g;
   if (g1 == g0) return;
+  // large span payloads of this block's records -> cooperative list
+  static_assert(kIPT == 1, "one record per lane below");
+  uint32_t skip = 0;
+  uint64_t nbig_tot;
+  {
+    const uint64_t i = r0 + threadIdx.x;
+    uint32_t nbig = 0;
+    if (i < a.n) {
+      const uint8_t *rec = recs + i * a.L.stride;
+      for (uint32_t o = 0; o < a.L.n_ops; ++o)
+        if (a.L.ops[o].kind == SPK_OP_SPAN &&
+            (uint64_t)rec_u32(rec, a.L.ops[o].rec_off) * a.L.ops[o].size >= kBigBytes)
+          ++nbig;
+    }
+    uint64_t slot = block_excl_scan(nbig, &nbig_tot, sh);
+    if (nbig && slot + nbig <= kBigMax) {
+      const uint8_t *rec = recs + i * a.L.stride;
+      uint64_t q = pj[0];
+      if (a.mode == SPK_MODE_MESSAGES)
+        q += a.fpre + ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + wlog(wj[0])];
+      uint32_t sk = 0;
+      for (uint32_t o = 0; o < a.L.n_ops; ++o) {
+        const spk_op op = a.L.ops[o];
+        if (op.kind == SPK_OP_COPY) {
+          q += op.size;
+          continue;
+        }
+        const uint64_t nb = (uint64_t)rec_u32(rec, op.rec_off) * op.size;
+        q += wj[0];
+        if (nb >= kBigBytes) {
+          big[slot++] = BigSeg{q, nullptr, a.heaps[sk] + rec_u64(rec, op.aux) * op.size, nb};
+          skip |= 1u << sk;
+        }
+        q += nb;
+        ++sk;
+      }
+    }
+    if (nbig_tot > kBigMax) nbig_tot = kBigMax;
+    __syncthreads();
+  }
+  uint32_t k0 = 0;  // first list entry that may reach the current window
   for (uint64_t wlo = g0 & ~15ull; wlo < g1; wlo += kEncWin) {
     const Win W{lds, wlo, wlo + kEncWin < g1 ? wlo + kEncWin : g1};
     for (int j = 0; j < kIPT; ++j) {
@@ -440,8 +530,12 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
         win_put(W, q, ws + kWsHdrMsg + sl * kWsHdrSlot, hl);
         q += hl;
       }
-      win_record(a, recs + i * a.L.stride, wj[j], q, W);
+      win_record(a, recs + i * a.L.stride, wj[j], q, W, skip);
     }
+    // listed payloads are in output order: walk the ones touching the window
+    while (k0 < nbig_tot && big[k0].dst + big[k0].n <= W.lo) ++k0;
+    for (uint32_t k = k0; k < nbig_tot && big[k].dst < W.hi; ++k)
+      win_put_coop(W, big[k].dst, big[k].src, big[k].n);
     __syncthreads();
     // flush [max(W.lo, g0), W.hi): aligned 16-B chunks, bytes at the edges
     for (uint64_t c = W.lo + (uint64_t)threadIdx.x * 16; c < W.hi; c += kThreads * 16) {
@@ -490,7 +584,7 @@ __device__ __forceinline__ uint64_t rec_wire_len(const KLayout &L, const uint8_t
 // heap_off[k] = element offset where this record's span k goes.
 __device__ void decode_record(const KLayout &L, const uint8_t *wire, uint64_t pos,
                               uint32_t w, uint8_t *rec, uint8_t *const *heaps,
-                              const uint64_t *heap_off) {
+                              const uint64_t *heap_off, uint32_t skip = 0) {
   uint32_t sk = 0;
   for (uint32_t o = 0; o < L.n_ops; ++o) {
     const spk_op op = L.ops[o];
@@ -503,7 +597,7 @@ __device__ void decode_record(const KLayout &L, const uint8_t *wire, uint64_t po
       *reinterpret_cast<uint32_t *>(rec + op.rec_off) = (uint32_t)c;
       *reinterpret_cast<uint64_t *>(rec + op.aux) = heap_off[sk];
       const uint64_t nb = c * op.size;
-      copy_bytes(heaps[sk] + heap_off[sk] * op.size, wire + pos, nb);
+      if (!(skip >> sk & 1)) copy_bytes(heaps[sk] + heap_off[sk] * op.size, wire + pos, nb);
       pos += nb;
       ++sk;
     }
@@ -656,8 +750,43 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
     uint64_t tot;
     hoff[k] = bsum[(uint64_t)blockIdx.x * SPK_MAX_SPANS + k] + block_excl_scan(cnt[k], &tot, sh);
   }
-  if (s.pos == ~0ull || s.errc) return;
-  decode_record(a.L, wire, s.pos, s.w, recs + i * a.L.stride, a.heaps, hoff);
+  const bool live = s.pos != ~0ull && !s.errc;
+  // large payloads go to the block's cooperative list (record order)
+  __shared__ BigSeg big[kBigMax];
+  uint32_t nbig = 0, skip = 0;
+  if (live) {
+    uint32_t sk = 0;
+    for (uint32_t o = 0; o < a.L.n_ops; ++o)
+      if (a.L.ops[o].kind == SPK_OP_SPAN) {
+        if (cnt[sk] * a.L.ops[o].size >= kBigBytes) ++nbig;
+        ++sk;
+      }
+  }
+  uint64_t nbig_tot;
+  uint64_t slot = block_excl_scan(nbig, &nbig_tot, sh);
+  if (nbig && slot + nbig <= kBigMax) {
+    uint64_t pos = s.pos;
+    uint32_t sk = 0;
+    for (uint32_t o = 0; o < a.L.n_ops; ++o) {
+      const spk_op op = a.L.ops[o];
+      if (op.kind == SPK_OP_COPY) {
+        pos += op.size;
+        continue;
+      }
+      pos += s.w;
+      const uint64_t nb = cnt[sk] * op.size;
+      if (nb >= kBigBytes) {
+        big[slot++] = BigSeg{0, a.heaps[sk] + hoff[sk] * op.size, wire + pos, nb};
+        skip |= 1u << sk;
+      }
+      pos += nb;
+      ++sk;
+    }
+  }
+  if (live) decode_record(a.L, wire, s.pos, s.w, recs + i * a.L.stride, a.heaps, hoff, skip);
+  __syncthreads();
+  if (nbig_tot > kBigMax) nbig_tot = kBigMax;
+  for (uint32_t k = 0; k < nbig_tot; ++k) coop_copy(big[k].dptr, big[k].src, big[k].n);
 }
 
 // ===========================================================================

@@ -211,14 +211,17 @@ class Codec:
 
 def synth_batch(codec: Codec, kind: str, n: int, seed: int, param: int = 48,
                 first: int = 0, stream=None) -> RecordBatch:
-    """Device-generated synthetic batch (spk_synth) for rec64 / recs / outer."""
+    """Device-generated synthetic batch (spk_synth) for rec64 / recs / outer
+    and the C5 coro_rpc shapes rpcrect / person / ints."""
     lib = codec.lib
     dev = codec.device
-    kinds = {"rec64": C.SPK_SYNTH_REC64, "recs": C.SPK_SYNTH_RECS, "outer": C.SPK_SYNTH_OUTER}
+    kinds = {"rec64": C.SPK_SYNTH_REC64, "recs": C.SPK_SYNTH_RECS, "outer": C.SPK_SYNTH_OUTER,
+             "rpcrect": C.SPK_SYNTH_RPCRECT, "person": C.SPK_SYNTH_PERSON,
+             "ints": C.SPK_SYNTH_INTS}
     k = kinds[kind]
     recs = torch.empty((n, codec.L.stride), dtype=torch.uint8, device=dev)
     st = _stream(stream)
-    if k == C.SPK_SYNTH_REC64:
+    if k in (C.SPK_SYNTH_REC64, C.SPK_SYNTH_RPCRECT):
         Codec._check(lib.spk_synth(k, seed, first, n, param, _p(recs), None, None, st),
                      "spk_synth")
         return RecordBatch(codec.L, recs, [])
