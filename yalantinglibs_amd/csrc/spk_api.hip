@@ -63,7 +63,9 @@ int spk_layout_check(const spk_layout *L) {
 
 size_t spk_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len) {
   if (spk_layout_check(L) != SPK_OK) return 0;
-  if (is_trivial(L)) return kWsScratch + (n + 1) * 8 + 256;
+  // trivial: per-message payload positions (fallback gather) or 2 words per
+  // decode block (<= 4096 blocks), whichever is larger
+  if (is_trivial(L)) return kWsScratch + ((n + 1) * 8 > 65536 ? (n + 1) * 8 : 65536) + 256;
   return var_workspace_bytes(L, mode, n, wire_len);
 }
 

@@ -441,7 +441,8 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_encode_lds(
 
 __global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
     MsgLdsArgs a, const uint8_t *__restrict__ wire, const uint64_t *__restrict__ offs,
-    int32_t *__restrict__ errc, spk_dresult_t *__restrict__ res, uint8_t *__restrict__ out) {
+    int32_t *__restrict__ errc, spk_dresult_t *__restrict__ res, uint8_t *__restrict__ out,
+    uint64_t *__restrict__ part) {
   extern __shared__ v4u smem_v4[];
   uint8_t *stage = reinterpret_cast<uint8_t *>(smem_v4);
   __shared__ uint64_t s_lo[kMsgThreads / 64], s_hi[kMsgThreads / 64];
@@ -558,15 +559,55 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
     }
     __syncthreads();  // stage / s_pay are reused by the next group
   }
+  // per-block partials (summed by msg_sum_partials): same-address atomics
+  // from thousands of blocks would serialise in L2
   for (int o = 32; o > 0; o >>= 1) {
     ok += __shfl_down(ok, o);
     consumed += __shfl_down(consumed, o);
   }
-  if ((tid & 63) == 0 && (ok || consumed)) {
-    atomicAdd((unsigned long long *)&res->count, ok);
-    atomicAdd((unsigned long long *)&res->consumed, consumed);
+  if ((tid & 63) == 0) {
+    s_lo[tid >> 6] = ok;
+    s_hi[tid >> 6] = consumed;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t o = 0, c = 0;
+    for (int k = 0; k < kMsgThreads / 64; ++k) {
+      o += s_lo[k];
+      c += s_hi[k];
+    }
+    part[2 * blockIdx.x] = o;
+    part[2 * blockIdx.x + 1] = c;
   }
   if (__any(cap_hit) && (tid & 63) == 0) atomicExch(&res->errc, SPK_ERRC_CAPACITY);
+}
+
+__global__ __launch_bounds__(1024) void msg_sum_partials(const uint64_t *__restrict__ part,
+                                                         uint32_t nblocks,
+                                                         spk_dresult_t *__restrict__ res) {
+  __shared__ uint64_t sh[2][1024 / 64];
+  uint64_t o = 0, c = 0;
+  for (uint32_t b = threadIdx.x; b < nblocks; b += blockDim.x) {
+    o += part[2 * b];
+    c += part[2 * b + 1];
+  }
+  for (int k = 32; k > 0; k >>= 1) {
+    o += __shfl_down(o, k);
+    c += __shfl_down(c, k);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    sh[0][threadIdx.x >> 6] = o;
+    sh[1][threadIdx.x >> 6] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t k = 1; k < blockDim.x / 64; ++k) {
+      o += sh[0][k];
+      c += sh[1][k];
+    }
+    res->count = o;
+    res->consumed = c;
+  }
 }
 
 // messages per block for the LDS-staged kernels: a multiple of 16 whose
@@ -771,9 +812,12 @@ hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
       b.cap = b.R * a.fixed_M + 32;
       uint64_t blocks = (n + b.R - 1) / b.R;
       if (blocks > 4096) blocks = 4096;  // groups are strided over the grid
+      uint64_t *part = payload;  // workspace scratch: 2 words per block
       hipLaunchKernelGGL(fixed_msg_decode_lds, dim3((unsigned)blocks), dim3(kMsgThreads),
                          (size_t)b.cap + 16, s, b, (const uint8_t *)d_wire, d_offsets, d_errc,
-                         d_res, (uint8_t *)d_recs);
+                         d_res, (uint8_t *)d_recs, part);
+      hipLaunchKernelGGL(msg_sum_partials, dim3(1), dim3(1024), 0, s, (const uint64_t *)part,
+                         (uint32_t)blocks, d_res);
       return hipGetLastError();
     }
   }

@@ -637,6 +637,11 @@ struct DecArgs {
 // DECODE, SPK_MODE_MESSAGES
 // ===========================================================================
 // per-message state in workspace: u64 payload_pos (~0 = failed) | width
+// per-block slots of the MESSAGES decode scan buffer: span totals, then the
+// block's ok-message count and consumed bytes (summed by var_scan_blocks:
+// no same-address atomics across thousands of blocks)
+constexpr uint32_t kBs = SPK_MAX_SPANS + 2;
+
 struct MsgState {
   uint64_t pos;    // absolute payload position, ~0 if the message failed
   uint32_t w;
@@ -690,15 +695,14 @@ __global__ __launch_bounds__(kThreads) void var_msg_parse(
   for (uint32_t k = 0; k < a.L.n_spans; ++k) {
     uint64_t tot;
     block_excl_scan(cnt[k], &tot, sh);
-    if (threadIdx.x == 0) bsum[(uint64_t)blockIdx.x * SPK_MAX_SPANS + k] = tot;
+    if (threadIdx.x == 0) bsum[(uint64_t)blockIdx.x * kBs + k] = tot;
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    ok += __shfl_down(ok, o);
-    consumed += __shfl_down(consumed, o);
-  }
-  if ((threadIdx.x & 63) == 0 && (ok | consumed)) {
-    atomicAdd((unsigned long long *)&res->count, (unsigned long long)ok);
-    atomicAdd((unsigned long long *)&res->consumed, (unsigned long long)consumed);
+  uint64_t tok, tcons;
+  block_excl_scan(ok, &tok, sh);
+  block_excl_scan(consumed, &tcons, sh);
+  if (threadIdx.x == 0) {
+    bsum[(uint64_t)blockIdx.x * kBs + SPK_MAX_SPANS] = tok;
+    bsum[(uint64_t)blockIdx.x * kBs + SPK_MAX_SPANS + 1] = tcons;
   }
 }
 
@@ -714,15 +718,31 @@ __global__ __launch_bounds__(1024) void var_scan_blocks(uint64_t nblocks,
     uint64_t carry = 0;
     for (uint64_t b0 = 0; b0 < nblocks; b0 += blockDim.x) {
       const uint64_t b = b0 + threadIdx.x;
-      const uint64_t v = b < nblocks ? bsum[b * SPK_MAX_SPANS + k] : 0;
+      const uint64_t v = b < nblocks ? bsum[b * kBs + k] : 0;
       uint64_t tot;
       const uint64_t ex = block_excl_scan(v, &tot, sh);
-      if (b < nblocks) bsum[b * SPK_MAX_SPANS + k] = carry + ex;
+      if (b < nblocks) bsum[b * kBs + k] = carry + ex;
       carry += tot;
     }
     if (threadIdx.x == 0) {
       res->heap_used[k] = carry;
       if (carry > a.heap_cap[k] && res->errc == 0) res->errc = SPK_ERRC_CAPACITY;
+    }
+  }
+  // count / consumed: sums of the per-block partials
+  for (uint32_t k = SPK_MAX_SPANS; k < kBs; ++k) {
+    uint64_t carry = 0;
+    for (uint64_t b0 = 0; b0 < nblocks; b0 += blockDim.x) {
+      const uint64_t b = b0 + threadIdx.x;
+      uint64_t tot;
+      block_excl_scan(b < nblocks ? bsum[b * kBs + k] : 0, &tot, sh);
+      carry += tot;
+    }
+    if (threadIdx.x == 0) {
+      if (k == SPK_MAX_SPANS)
+        res->count = carry;
+      else
+        res->consumed = carry;
     }
   }
 }
@@ -748,7 +768,7 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
   uint64_t hoff[SPK_MAX_SPANS] = {};
   for (uint32_t k = 0; k < a.L.n_spans; ++k) {
     uint64_t tot;
-    hoff[k] = bsum[(uint64_t)blockIdx.x * SPK_MAX_SPANS + k] + block_excl_scan(cnt[k], &tot, sh);
+    hoff[k] = bsum[(uint64_t)blockIdx.x * kBs + k] + block_excl_scan(cnt[k], &tot, sh);
   }
   const bool live = s.pos != ~0ull && !s.errc;
   // large payloads go to the block's cooperative list (record order)
@@ -1755,7 +1775,7 @@ static hipError_t launch_vec_decode_ns(const DecArgs &a, const WalkProg &P, cons
 size_t var_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len) {
   size_t enc = kWsScratch + (grid_for(n, kPlanRPB) + 1) * sizeof(Partial) + 256;
   size_t dec_msg = kWsScratch + n * sizeof(MsgState) +
-                   (grid_for(n, kThreads) + 1) * SPK_MAX_SPANS * 8 + 256;
+                   (grid_for(n, kThreads) + 1) * kBs * 8 + 256;
   size_t dec_vec = vec_ws_layout(L, wire_len, n).end + 256;
   size_t m = enc;
   if (mode == SPK_MODE_MESSAGES) m = m > dec_msg ? m : dec_msg;
