@@ -184,10 +184,24 @@ def main():
     value = total_bytes / dt / 2**30
     mrec = n * world * args.steps / dt / 1e6
 
-    # dominant kernel: the encode write pass (C2: shift_copy_kernel), which
-    # moves record bytes in and wire bytes out; per launch algorithmic bytes
-    enc_bytes = rec_bytes + wire_bytes
-    roof_ach = enc_bytes / (enc_ms * 1e-3) / 1e9
+    # dominant kernel and its per-launch algorithmic bytes / duration:
+    #   trivially serializable records in one vector message (C2): every
+    #   step is two launches of shift_copy_kernel (encode: records -> wire
+    #   body, decode: wire body -> records), each moving 2 x record bytes; its
+    #   average duration is the mean of the encode and decode phases (HIP
+    #   events on the launch stream; the decode phase also holds the ~4 us
+    #   header kernel, so this slightly understates the kernel's rate);
+    #   otherwise: the encode write pass (record + heap bytes in, wire out).
+    if cd.L.dev.trivial and mode == SP.MODE_VECTOR:
+        roof_kernel = "shift_copy_kernel (encode + decode launches)"
+        launch_bytes = 2 * rec_bytes
+        launch_ms = (enc_ms + dec_ms) / 2
+    else:
+        roof_kernel = ("fixed_msg_encode_lds" if cd.L.dev.trivial else "var_encode_write") \
+            + " (encode phase)"
+        launch_bytes = rec_bytes + wire_bytes
+        launch_ms = enc_ms
+    roof_ach = launch_bytes / (launch_ms * 1e-3) / 1e9
     # HBM bytes per launch of the same kernel from a separate rocprofv3 PMC run
     # of this command (scripts/gpu_pmc.sh -> profiles/r01/pmc_<config>.json;
     # FETCH_SIZE doubled per the gfx950 correction, WRITE_SIZE exact)
@@ -236,7 +250,8 @@ def main():
             "mrec_per_s": round(mrec, 2),
             "phase_ms": {"plan": round(plan_ms, 4), "encode": round(enc_ms, 4),
                          "decode": round(dec_ms, 4)},
-            "roofline": {"bound": "hbm", "kernel": "encode write pass",
+            "roofline": {"bound": "hbm", "kernel": roof_kernel,
+                         "bytes_per_launch": launch_bytes, "ms_per_launch": round(launch_ms, 4),
                          "achieved": round(roof_ach, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(roof_ach / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
@@ -397,31 +412,38 @@ def run_c5(args, torch, dist, world, rank, dev):
 
 
 def host_path(cd, batch, mode, plan, wire, dec, offs, n, stream, dev):
-    """PCIe-inclusive rate: pinned host records -> H2D -> encode -> D2H wire;
-    pinned host wire -> H2D -> decode -> D2H records."""
+    """PCIe-inclusive rate: pinned host records (+ heaps) -> H2D -> encode ->
+    D2H wire; pinned host wire -> H2D -> decode -> D2H records (+ heaps)
+    (DESIGN.md). The coro_rpc socket buffers this models live in host memory."""
     import torch
     from yalantinglibs_amd import struct_pack as SP
-    h_recs = torch.empty_like(batch.recs, device="cpu").pin_memory()
-    h_recs.copy_(batch.recs)
+    srcs = [batch.recs] + list(batch.heaps)
+    dsts = [dec.recs] + list(dec.heaps)
+    h_in = [torch.empty_like(t, device="cpu").pin_memory() for t in srcs]
+    for h, t in zip(h_in, srcs):
+        h.copy_(t)
     h_wire = torch.empty(plan.total_bytes, dtype=torch.uint8).pin_memory()
-    h_dec = torch.empty_like(dec.recs, device="cpu").pin_memory()
+    h_out = [torch.empty_like(t, device="cpu").pin_memory() for t in dsts]
     torch.cuda.synchronize(dev)
     reps = 3
     t0 = time.perf_counter()
     for _ in range(reps):
-        batch.recs.copy_(h_recs, non_blocking=True)
+        for t, h in zip(srcs, h_in):
+            t.copy_(h, non_blocking=True)
         cd.plan(batch, mode, stream)
         cd.serialize_to(wire, batch, mode, offs, stream=stream, planned=True)
         h_wire.copy_(wire[:plan.total_bytes], non_blocking=True)
         wire[:plan.total_bytes].copy_(h_wire, non_blocking=True)
         cd.deserialize_to(dec, wire[:plan.total_bytes], mode, offs,
                           n if mode == SP.MODE_MESSAGES else 0, stream=stream)
-        h_dec.copy_(dec.recs, non_blocking=True)
+        for t, h in zip(dsts, h_out):
+            h.copy_(t, non_blocking=True)
     torch.cuda.synchronize(dev)
     dt = (time.perf_counter() - t0) / reps
-    algo = 2 * batch.recs.numel() + 2 * plan.total_bytes
+    algo = 2 * sum(int(t.numel()) for t in srcs) + 2 * plan.total_bytes
     return {"ms_per_step": round(dt * 1e3, 3), "gib_s": round(algo / dt / 2**30, 3),
-            "note": "includes H2D of records and wire, D2H of wire and decoded records"}
+            "note": "includes H2D of records (+heaps) and wire, D2H of wire and decoded "
+                    "records (+heaps); pinned host buffers"}
 
 
 if __name__ == "__main__":

@@ -11,9 +11,10 @@ import sys
 from collections import defaultdict
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
+base = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out"
 out = {}
 for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-    files = glob.glob(f"gpurun_out/pmc_{cfg}_{ctr}/**/*counter_collection.csv", recursive=True)
+    files = glob.glob(f"{base}/pmc_{cfg}_{ctr}/**/*counter_collection.csv", recursive=True)
     acc = defaultdict(list)
     for f in files:
         for r in csv.DictReader(open(f)):
