@@ -88,10 +88,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    dev = torch.device(f"cuda:{local}")
+    # one rank per GPU; the modulo only matters when rehearsing several ranks
+    # on fewer GPUs (BENCH_DIST_BACKEND=gloo: RCCL refuses two ranks per GPU)
+    dev = torch.device(f"cuda:{local % max(1, torch.cuda.device_count())}")
     torch.cuda.set_device(dev)
+    if world > 1:
+        backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     if args.config == "c5":
         return run_c5(args, torch, dist, world, rank, dev)
 
