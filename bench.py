@@ -63,10 +63,10 @@ def cpu_baseline(case, param):
     if not os.path.exists(exe):
         return None
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    n = {"rec64": 20_000_000, "recs": 4_000_000, "outer": 4_000_000}[case]
+    n = {"rec64": 20_000_000, "recs": 4_000_000, "outer": 4_000_000, "c5": 600_000}[case]
     out = {}
     for t in sorted({1, threads}):
-        r = subprocess.run([exe, case, str(n), str(SEEDS[case]), str(param), str(t), "10"],
+        r = subprocess.run([exe, case, str(n), str(SEEDS.get(case, 0)), str(param), str(t), "10"],
                            capture_output=True, text=True, timeout=600)
         if r.returncode != 0:
             return None
@@ -361,6 +361,24 @@ def run_c5(args, torch, dist, world, rank, dev):
     ms_step = dt * 1e3 / args.steps
     value = algo * world * args.steps / dt / 2**30
 
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cb = cpu_baseline("c5", 0)
+        if cb:
+            runs, cn, threads = cb
+            per_msg = algo / n_msgs
+            best, single = runs[threads], runs[1]
+            cpu = {"value": round(per_msg * cn / (best["encode_s"] + best["decode_s"]) / 2**30, 3),
+                   "unit": "GiB/s", "cores": threads, "kind": "reference",
+                   "sample": f"{cn} framed requests (rect/person/vector<int> thirds), reference "
+                             "struct_pack deserialize_to of each request + resp_header/"
+                             "serialize of each echo response (-O3 -DNDEBUG "
+                             f"-DSTRUCT_PACK_OPTIMIZE), {threads} threads x message slices, "
+                             "best of 10",
+                   "single_thread_gib_s": round(per_msg * cn / (single["encode_s"] +
+                                                                single["decode_s"]) / 2**30, 3),
+                   "mmsg_per_s": round(cn / (best["encode_s"] + best["decode_s"]) / 1e6, 3)}
+
     host = None
     if rank == 0:
         # host-inclusive: socket buffers live in (pinned) host memory
@@ -409,7 +427,7 @@ def run_c5(args, torch, dist, world, rank, dev):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(algo / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "traffic": None},
-            "cpu_baseline": None,
+            "cpu_baseline": cpu,
             "host_path": host,
         }
         print(json.dumps(line), flush=True)

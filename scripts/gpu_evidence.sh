@@ -13,8 +13,9 @@ step() { local name=$1; shift; local t=$1; shift
   echo "[$name] rc=$rc"; tail -1 "$OUT/$name.log" | cut -c1-400
   if [ $rc -ne 0 ]; then tail -20 "$OUT/$name.log"; exit $rc; fi; }
 step bench_c2 600 python bench.py --config c2 --host-path
-for c in c2b c3 c4 c5; do
-  step bench_$c 600 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --host-path
+step bench_c2b 600 python bench.py --config c2b --steps 10 --warmup 2 --no-cpu-baseline --host-path
+for c in c3 c4 c5; do
+  step bench_$c 600 python bench.py --config $c --steps 10 --warmup 2 --host-path
 done
 for c in ${PROF_CONFIGS:-c2 c2b c3 c4 c5}; do
   step prof_$c 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o run --output-format csv -- python bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline
