@@ -39,7 +39,9 @@
 namespace spk {
 
 constexpr int kThreads = 256;
-constexpr int kIPT = 1;                     // records per thread (encode write)
+constexpr int kIPT = 1;                     // records per thread (encode write; 2 measured
+                                            // slower: C3 +19 %, C5 3x as big payloads
+                                            // overflow the cooperative list)
 constexpr uint64_t kRPB = kThreads * kIPT;  // records per block (encode write)
 constexpr int kPlanSub = 4;                 // write blocks per plan block
 constexpr uint64_t kPlanRPB = kRPB * kPlanSub;  // records per plan block
@@ -185,21 +187,26 @@ __global__ __launch_bounds__(kThreads) void var_plan_reduce(
   __shared__ uint64_t sh[kThreads / 64];
   const uint64_t r0 = (uint64_t)blockIdx.x * kPlanRPB;
   uint64_t mx = 0, tot = 0, sub[kPlanSub];
-  for (int j = 0; j < kPlanSub; ++j) {
-    const uint64_t i = r0 + (uint64_t)j * kThreads + threadIdx.x;  // coalesced
-    uint64_t sum = 0;
-    if (i < a.n) {
-      uint64_t var, maxc;
-      rec_sizes(a.L, recs + i * a.L.stride, var, maxc);
-      if (a.mode == SPK_MODE_VECTOR) {
-        sum = var;
-      } else {
-        const uint32_t w = width_of(maxc);
-        sum = hdrlen_tbl[wlog(w)] + var + (uint64_t)a.L.n_spans * w;
+  for (int j = 0; j < kPlanSub; ++j) {  // write block j: kIPT rounds of kThreads records
+    sub[j] = 0;
+    for (int q = 0; q < kIPT; ++q) {
+      const uint64_t i = r0 + (uint64_t)j * kRPB + (uint64_t)q * kThreads + threadIdx.x;
+      uint64_t sum = 0;
+      if (i < a.n) {
+        uint64_t var, maxc;
+        rec_sizes(a.L, recs + i * a.L.stride, var, maxc);
+        if (a.mode == SPK_MODE_VECTOR) {
+          sum = var;
+        } else {
+          const uint32_t w = width_of(maxc);
+          sum = hdrlen_tbl[wlog(w)] + var + (uint64_t)a.L.n_spans * w;
+        }
+        mx = maxc > mx ? maxc : mx;
       }
-      mx = maxc > mx ? maxc : mx;
+      uint64_t t;
+      block_excl_scan(sum, &t, sh);
+      sub[j] += t;
     }
-    block_excl_scan(sum, &sub[j], sh);
     tot += sub[j];
   }
   const uint64_t m = block_max(mx, sh);
@@ -474,11 +481,11 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
   const uint64_t g1 = g;
   if (g1 == g0) return;
   // large span payloads of this block's records -> cooperative list
-  static_assert(kIPT == 1, "one record per lane below");
-  uint32_t skip = 0;
-  uint64_t nbig_tot;
-  {
-    const uint64_t i = r0 + threadIdx.x;
+  uint32_t skip[kIPT];
+  uint64_t nbig_tot = 0;
+  for (int j = 0; j < kIPT; ++j) {  // list order = record order = output order
+    skip[j] = 0;
+    const uint64_t i = r0 + (uint64_t)j * kThreads + threadIdx.x;
     uint32_t nbig = 0;
     if (i < a.n) {
       const uint8_t *rec = recs + i * a.L.stride;
@@ -487,12 +494,14 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
             (uint64_t)rec_u32(rec, a.L.ops[o].rec_off) * a.L.ops[o].size >= kBigBytes)
           ++nbig;
     }
-    uint64_t slot = block_excl_scan(nbig, &nbig_tot, sh);
+    uint64_t round_tot;
+    uint64_t slot = nbig_tot + block_excl_scan(nbig, &round_tot, sh);
+    nbig_tot += round_tot;
     if (nbig && slot + nbig <= kBigMax) {
       const uint8_t *rec = recs + i * a.L.stride;
-      uint64_t q = pj[0];
+      uint64_t q = pj[j];
       if (a.mode == SPK_MODE_MESSAGES)
-        q += a.fpre + ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + wlog(wj[0])];
+        q += a.fpre + ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + wlog(wj[j])];
       uint32_t sk = 0;
       for (uint32_t o = 0; o < a.L.n_ops; ++o) {
         const spk_op op = a.L.ops[o];
@@ -501,18 +510,18 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
           continue;
         }
         const uint64_t nb = (uint64_t)rec_u32(rec, op.rec_off) * op.size;
-        q += wj[0];
+        q += wj[j];
         if (nb >= kBigBytes) {
           big[slot++] = BigSeg{q, nullptr, a.heaps[sk] + rec_u64(rec, op.aux) * op.size, nb};
-          skip |= 1u << sk;
+          skip[j] |= 1u << sk;
         }
         q += nb;
         ++sk;
       }
     }
-    if (nbig_tot > kBigMax) nbig_tot = kBigMax;
-    __syncthreads();
   }
+  if (nbig_tot > kBigMax) nbig_tot = kBigMax;
+  __syncthreads();
   uint32_t k0 = 0;  // first list entry that may reach the current window
   for (uint64_t wlo = g0 & ~15ull; wlo < g1; wlo += kEncWin) {
     const Win W{lds, wlo, wlo + kEncWin < g1 ? wlo + kEncWin : g1};
@@ -530,7 +539,7 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
         win_put(W, q, ws + kWsHdrMsg + sl * kWsHdrSlot, hl);
         q += hl;
       }
-      win_record(a, recs + i * a.L.stride, wj[j], q, W, skip);
+      win_record(a, recs + i * a.L.stride, wj[j], q, W, skip[j]);
     }
     // listed payloads are in output order: walk the ones touching the window
     while (k0 < nbig_tot && big[k0].dst + big[k0].n <= W.lo) ++k0;
