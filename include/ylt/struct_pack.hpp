@@ -13,6 +13,8 @@
 //   deserialize_to(std::vector<T>&, const char*, size_t[, size_t& consume])
 //   deserialize<std::vector<T>>(const char*, size_t)  -> result<T>
 //   serialize_messages / deserialize_messages         coro_rpc payload batches
+//   serialize_frames / deserialize_frames             ... in coro_rpc's framing
+//                                                      ([req|resp header][payload])
 //   device::codec<T>                                   device-resident batches
 //
 // Build: hipcc -std=c++20 -I include ... -L yalantinglibs_amd -lspk_codec
@@ -231,10 +233,21 @@ class codec {
                          ws_.size(), s_), "spk_encode");
   }
 
-  // decode into `out` (capacities from out.n / out.heap_elems)
+  // after plan(SPK_MODE_MESSAGES): n framed messages [prefix][serialize(rec)]
+  void encode_framed(const batch<T> &b, const spk_frame &f, void *d_out, std::size_t cap,
+                     uint64_t *d_offsets = nullptr) {
+    std::vector<const void *> hp(n_spans() ? n_spans() : 1, nullptr);
+    for (uint32_t k = 0; k < n_spans(); ++k) hp[k] = b.heaps[k].data();
+    check_spk(spk_encode_framed(&layout(), b.n, b.recs.data(), hp.data(),
+                                (const spk_plan_t *)plan_.data(), &f, d_out, cap, d_offsets,
+                                ws_.data(), ws_.size(), s_), "spk_encode_framed");
+  }
+
+  // decode into `out` (capacities from out.n / out.heap_elems); `prefix` =
+  // frame bytes before each message (MESSAGES mode only)
   spk_dresult_t decode(batch<T> &out, const void *d_wire, std::size_t len, int mode,
                        const uint64_t *d_offsets = nullptr, std::size_t n_msgs = 0,
-                       int32_t *d_errc = nullptr) {
+                       int32_t *d_errc = nullptr, uint32_t prefix = 0) {
     const uint64_t nrec = mode == SPK_MODE_VECTOR ? out.n : n_msgs;
     ws_.resize(spk_workspace_bytes(&layout(), mode, nrec, len));
     res_.resize(sizeof(spk_dresult_t));
@@ -244,9 +257,15 @@ class codec {
       hp[k] = out.heaps[k].data();
       caps[k] = out.heap_elems[k];
     }
-    check_spk(spk_decode(&layout(), mode, d_wire, len, d_offsets, n_msgs, out.recs.data(),
-                         out.n, hp.data(), caps.data(), (spk_dresult_t *)res_.data(), d_errc,
-                         ws_.data(), ws_.size(), s_), "spk_decode");
+    if (prefix)
+      check_spk(spk_decode_framed(&layout(), d_wire, len, d_offsets, n_msgs, prefix,
+                                  out.recs.data(), out.n, hp.data(), caps.data(),
+                                  (spk_dresult_t *)res_.data(), d_errc, ws_.data(), ws_.size(),
+                                  s_), "spk_decode_framed");
+    else
+      check_spk(spk_decode(&layout(), mode, d_wire, len, d_offsets, n_msgs, out.recs.data(),
+                           out.n, hp.data(), caps.data(), (spk_dresult_t *)res_.data(), d_errc,
+                           ws_.data(), ws_.size(), s_), "spk_decode");
     spk_dresult_t r{};
     check(hipMemcpyAsync(&r, res_.data(), sizeof(r), hipMemcpyDeviceToHost, s_), "D2H");
     check(hipStreamSynchronize(s_), "sync");
@@ -400,11 +419,13 @@ std::vector<char> serialize_messages(const std::vector<T> &v, std::vector<uint64
   return bytes;
 }
 
-// decodes message i = data[offsets[i], offsets[i+1]) into out[i]; returns per-message errc
+// decodes message i = data[offsets[i] + prefix, offsets[i+1]) into out[i];
+// returns per-message errc
 template <uint64_t conf = sp_config::DEFAULT, typename T>
 std::vector<err_code> deserialize_messages(std::vector<T> &out, const char *data,
                                            std::size_t size,
-                                           const std::vector<uint64_t> &offsets) {
+                                           const std::vector<uint64_t> &offsets,
+                                           uint32_t prefix = 0) {
   auto &c = device::thread_codec<T, conf>();
   const std::size_t n = offsets.empty() ? 0 : offsets.size() - 1;
   device::buffer wire(size + 16), offs(offsets.size() * 8 + 8), ec(n * 4 + 4);
@@ -413,7 +434,7 @@ std::vector<err_code> deserialize_messages(std::vector<T> &out, const char *data
                                hipMemcpyHostToDevice, c.stream()), "H2D");
   auto b = c.alloc_for_wire(size, n);
   spk_dresult_t r = c.decode(b, wire.data(), size, SPK_MODE_MESSAGES, (uint64_t *)offs.data(), n,
-                             (int32_t *)ec.data());
+                             (int32_t *)ec.data(), prefix);
   if (r.errc == SPK_ERRC_CAPACITY) throw spk_error("struct_pack: decode capacity exceeded");
   std::vector<int32_t> e(n);
   device::check(hipMemcpyAsync(e.data(), ec.data(), n * 4, hipMemcpyDeviceToHost, c.stream()),
@@ -425,6 +446,72 @@ std::vector<err_code> deserialize_messages(std::vector<T> &out, const char *data
   std::vector<err_code> res(n);
   for (std::size_t i = 0; i < n; ++i) res[i] = static_cast<errc>(e[i]);
   return res;
+}
+
+// ---- coro_rpc framing ------------------------------------------------------
+// coro_rpc puts a 20-byte req_header before every request payload and a
+// 16-byte resp_header before every response (ref coro_rpc_protocol.hpp:60-79;
+// written with DISABLE_ALL_META_INFO = the raw struct bytes, client
+// coro_rpc_client.hpp:1285-1335, server coro_rpc_protocol.hpp:191-240).
+namespace rpc_frame {
+inline constexpr uint8_t magic_number = 21;  // coro_rpc_protocol.hpp:250
+inline constexpr uint32_t req_head_len = 20, resp_head_len = 16;
+
+// requests of function `function_id`; message i carries seq_num = seq_base + i
+inline spk_frame request(uint32_t function_id, uint32_t seq_base = 0,
+                         uint32_t attach_length = 0) {
+  spk_frame f{};
+  f.prefix_len = req_head_len;
+  f.seq_off = 4;
+  f.len_off = 12;
+  f.seq_base = seq_base;
+  f.tmpl[0] = magic_number;  // version, serialize_type, msg_type = 0
+  for (int k = 0; k < 4; ++k) {
+    f.tmpl[8 + k] = (uint8_t)(function_id >> (8 * k));
+    f.tmpl[16 + k] = (uint8_t)(attach_length >> (8 * k));
+  }
+  return f;
+}
+
+// responses echoing seq_num = seq_base + i
+inline spk_frame response(uint32_t seq_base = 0, uint8_t err_code = 0) {
+  spk_frame f{};
+  f.prefix_len = resp_head_len;
+  f.seq_off = 4;
+  f.len_off = 8;
+  f.seq_base = seq_base;
+  f.tmpl[0] = magic_number;
+  f.tmpl[2] = err_code;
+  return f;
+}
+}  // namespace rpc_frame
+
+// n framed messages [frame prefix][serialize(v[i])]; offsets = frame starts
+template <uint64_t conf = sp_config::DEFAULT, typename T>
+std::vector<char> serialize_frames(const std::vector<T> &v, const spk_frame &f,
+                                   std::vector<uint64_t> &offsets) {
+  auto &c = device::thread_codec<T, conf>();
+  auto b = c.upload(v.data(), v.size());
+  spk_plan_t p = c.plan(b, SPK_MODE_MESSAGES);
+  const std::size_t total = p.total_bytes + v.size() * (std::size_t)f.prefix_len;
+  device::buffer out(total), offs((v.size() + 1) * sizeof(uint64_t));
+  c.encode_framed(b, f, out.data(), out.size(), (uint64_t *)offs.data());
+  std::vector<char> bytes(total);
+  offsets.resize(v.size() + 1);
+  device::check(hipMemcpyAsync(bytes.data(), out.data(), bytes.size(), hipMemcpyDeviceToHost,
+                               c.stream()), "D2H");
+  device::check(hipMemcpyAsync(offsets.data(), offs.data(), offsets.size() * 8,
+                               hipMemcpyDeviceToHost, c.stream()), "D2H");
+  device::check(hipStreamSynchronize(c.stream()), "sync");
+  return bytes;
+}
+
+// frames data[offsets[i], offsets[i+1]) with a prefix_len-byte header each
+template <uint64_t conf = sp_config::DEFAULT, typename T>
+std::vector<err_code> deserialize_frames(std::vector<T> &out, const char *data, std::size_t size,
+                                         const std::vector<uint64_t> &offsets,
+                                         uint32_t prefix_len) {
+  return deserialize_messages<conf>(out, data, size, offsets, prefix_len);
 }
 
 }  // namespace struct_pack

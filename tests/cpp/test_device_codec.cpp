@@ -39,6 +39,7 @@ bool operator==(const RecS &a, const RecS &b) { return a.id == b.id && a.name ==
 bool operator==(const Inner &a, const Inner &b) { return a.x == b.x && a.y == b.y; }
 bool operator==(const Outer &a, const Outer &b) { return a.key == b.key && a.items == b.items; }
 namespace rpcb {
+bool operator==(const rect &a, const rect &b) { return std::memcmp(&a, &b, sizeof a) == 0; }
 bool operator==(const person &a, const person &b) {
   return a.id == b.id && a.name == b.name && a.age == b.age && a.salary == b.salary;
 }
@@ -94,6 +95,38 @@ static void roundtrip_messages(const char *fixture, const char *lens, std::size_
   CHECK(back == v);
 }
 
+// coro_rpc framing, against frames built by golden_gen the way coro_rpc does
+template <typename T, typename Gen>
+static void roundtrip_frames(const char *fixture, const char *lens, std::size_t n, bool req,
+                             uint32_t fid, uint32_t seq, Gen gen) {
+  std::vector<T> v(n);
+  for (std::size_t i = 0; i < n; ++i) gen(v[i], i);
+  const std::string want = golden(fixture);
+  CHECK(!want.empty());
+  const spk_frame f = req ? rpc_frame::request(fid, seq) : rpc_frame::response(seq);
+  std::vector<uint64_t> offs;
+  auto bytes = serialize_frames(v, f, offs);
+  CHECK(std::string(bytes.begin(), bytes.end()) == want);
+  auto l = golden_lens(lens);
+  CHECK(offs.size() == n + 1);
+  for (std::size_t i = 0; i < n && i < l.size(); ++i) CHECK(offs[i + 1] - offs[i] == l[i]);
+  std::vector<T> back;
+  auto errs = deserialize_frames(back, want.data(), want.size(), offs, f.prefix_len);
+  bool all_ok = true;
+  for (auto &e : errs) all_ok &= !e;
+  CHECK(all_ok);
+  CHECK(back == v);
+}
+
+static uint32_t fid_of(const char *name) {  // frames.json function_id (MD5Hash32 of the name)
+  std::ifstream f(std::string(SPK_GOLDEN_DIR) + "/frames.json");
+  std::string js((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  auto p = js.find(std::string("\"function\": \"") + name + "\"");
+  if (p == std::string::npos) return 0;
+  p = js.find("\"function_id\": ", p);
+  return (uint32_t)std::strtoul(js.c_str() + p + 15, nullptr, 10);
+}
+
 int main() {
   using namespace spk_gold;
   const uint64_t S2 = 0x5EED0002, S3 = 0x5EED0003, S4 = 0x5EED0004, S8 = 0x5EED0008;
@@ -124,6 +157,18 @@ int main() {
                            [&](RecS &o, uint64_t i) { o = make_recs(S3, i, 300); });
   roundtrip_messages<Rec64>("rec64_B_n300_p0_default.bin", "rec64_B_n300_p0_default.lens", 300,
                             [&](Rec64 &o, uint64_t i) { o = make_rec64(S2, i); });
+  const uint64_t S7 = 0x5EED0007, S9 = 0x5EED0009;
+  roundtrip_frames<rpcb::rect>("frames_rpcrect_req_n100_p0.bin", "frames_rpcrect_req_n100_p0.lens",
+                               100, true, fid_of("echo_rect"), 1,
+                               [&](rpcb::rect &o, uint64_t i) { o = make_rpc_rect(S7, i); });
+  roundtrip_frames<rpcb::person>("frames_person_resp_n120_p48.bin",
+                                 "frames_person_resp_n120_p48.lens", 120, false, 0, 7,
+                                 [&](rpcb::person &o, uint64_t i) { o = make_person(S8, i, 48); });
+  roundtrip_frames<rpcb::person>("frames_person_req_n120_p48.bin",
+                                 "frames_person_req_n120_p48.lens", 120, true,
+                                 fid_of("echo_person"), 7,
+                                 [&](rpcb::person &o, uint64_t i) { o = make_person(S8, i, 48); });
+  CHECK(fid_of("array_1K_int") != 0);
   std::printf("{\"checks\": %d, \"failures\": %d}\n", g_checks, g_fail);
   return g_fail ? 1 : 0;
 }
