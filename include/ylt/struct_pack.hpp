@@ -190,7 +190,11 @@ class codec {
       check(hipStreamSynchronize(s_), "sync");
     } else {
       std::vector<uint8_t> recs(n * L.rec_stride);
-      std::vector<std::vector<uint8_t>> heaps(n_spans());
+      // kept in the codec: string_view / span members of the decoded objects
+      // alias these host heaps, valid until this thread's next decode of T
+      // (the reference's views alias its input buffer, unpacker.hpp:1135-1145)
+      std::vector<std::vector<uint8_t>> &heaps = view_heaps_;
+      heaps.assign(n_spans(), {});
       if (n) check(hipMemcpyAsync(recs.data(), b.recs.data(), recs.size(),
                                   hipMemcpyDeviceToHost, s_), "D2H");
       std::vector<const uint8_t *> hp(n_spans());
@@ -305,6 +309,7 @@ class codec {
  private:
   hipStream_t s_;
   buffer ws_, plan_, res_;
+  std::vector<std::vector<uint8_t>> view_heaps_;
 };
 
 template <typename T, uint64_t conf>

@@ -84,15 +84,15 @@ int main() {
   const uint64_t nk = bytes / 16 - 1024;
   const uint64_t full8 = nk / (64 * 8) / 4, full16 = nk / (64 * 16) / 4;
   for (int blocks : {32768}) {
-    run<1, 16, 0, 0, 7>("unaligned R7 U16 dst+0", (v4u*)d, s, nk, blocks);
+    run<1, 16, 0, 0, 7>("unaligned R7 U16 dst+16 (warm)", (v4u*)(d + 16), s, nk, blocks);
     run<1, 16, 0, 0, 7>("unaligned R7 U16 dst+16", (v4u*)(d + 16), s, nk, blocks);
-    run<1, 16, 0, 0, 7>("unaligned R7 U16 dst+64", (v4u*)(d + 64), s, nk, blocks);
-    run<1, 16, 0, 0, 7>("unaligned R7 U16 dst+128", (v4u*)(d + 128), s, nk, blocks);
-    run<1, 16, 0, 0, 9>("unaligned R9 U16 dst+0", (v4u*)d, s, nk, blocks);
-    run<1, 16, 0, 0, 7>("unaligned R7 U16 dst+0", (v4u*)d, s, nk, blocks);
-    run<1, 16, 0, 0, 7>("unaligned R7 U16 dst+16", (v4u*)(d + 16), s, nk, blocks);
+    run<1, 16, 1, 0, 7>("unaligned R7 U16 dst+16 ntload", (v4u*)(d + 16), s, nk, blocks);
+    run<1, 16, 0, 1, 7>("unaligned R7 U16 dst+16 ntstore", (v4u*)(d + 16), s, nk, blocks);
+    run<1, 16, 1, 1, 7>("unaligned R7 U16 dst+16 nt both", (v4u*)(d + 16), s, nk, blocks);
     run<2, 16, 0, 0, 0>("pure copy U16 dst+16", (v4u*)(d + 16), s, nk, blocks);
-    run<2, 16, 0, 0, 0>("pure copy U16 dst+0", (v4u*)(d), s, nk, blocks);
+    run<2, 16, 0, 1, 0>("pure copy U16 dst+16 ntstore", (v4u*)(d + 16), s, nk, blocks);
+    run<2, 16, 1, 1, 0>("pure copy U16 dst+16 nt both", (v4u*)(d + 16), s, nk, blocks);
+    run<1, 16, 0, 0, 7>("unaligned R7 U16 dst+16 (again)", (v4u*)(d + 16), s, nk, blocks);
   }
   return 0;
 }
