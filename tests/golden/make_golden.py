@@ -84,25 +84,41 @@ FRAMES = [
 ]
 
 
+# full-size C5 frames (bench.py --config c5: 333,333 messages per type): digests only
+FRAMES_BIG = [
+    ("rpcrect_B", 333333, 0, "req", "echo_rect", 0), ("rpcrect_B", 333333, 0, "resp", "", 0),
+    ("person_B", 333333, 48, "req", "echo_person", 0), ("person_B", 333333, 48, "resp", "", 0),
+    ("ints_B", 333333, 2000, "req", "array_1K_int", 0), ("ints_B", 333333, 2000, "resp", "", 0),
+]
+
+
 def func_id(name):
     """router.hpp:121-127: MD5Hash32Constexpr(function name)"""
     return int.from_bytes(hashlib.md5(name.encode()).digest()[:4], "big") if name else 0
 
 
-def make_frames(tmp):
+def make_frames(tmp, big=False):
     out = []
-    for cm, n, param, kind, fname, seq in FRAMES:
+    for cm, n, param, kind, fname, seq in FRAMES + (FRAMES_BIG if big else []):
         case = cm[:-2]
         name = f"frames_{case}_{kind}_n{n}_p{param}"
-        wire = os.path.join(HERE, name + ".bin")
-        lens = os.path.join(HERE, name + ".lens")
+        keep = (cm, n, param, kind, fname, seq) in FRAMES
+        d = HERE if keep else tmp
+        wire = os.path.join(d, name + ".bin")
+        lens = os.path.join(d, name + ".lens")
         fid = func_id(fname)
         subprocess.run([GEN, "frames", cm, str(n), str(SEED[case]), str(param), kind, str(fid),
                         str(seq), wire, lens], check=True, stdout=subprocess.DEVNULL)
-        out.append({"name": name, "case": case, "n": n, "seed": SEED[case], "param": param,
-                    "kind": kind, "function": fname, "function_id": fid, "seq_base": seq,
-                    "file": name + ".bin", "lens": name + ".lens",
-                    "wire_len": os.path.getsize(wire), "sha256": sha256_file(wire)})
+        ent = {"name": name, "case": case, "n": n, "seed": SEED[case], "param": param,
+               "kind": kind, "function": fname, "function_id": fid, "seq_base": seq,
+               "wire_len": os.path.getsize(wire), "sha256": sha256_file(wire),
+               "lens_sha256": sha256_file(lens)}
+        if keep:
+            ent.update({"file": name + ".bin", "lens": name + ".lens"})
+        else:
+            os.remove(wire)
+            os.remove(lens)
+        out.append(ent)
     return out
 
 
@@ -239,7 +255,12 @@ def main():
         with open(man_path, "w") as f:
             json.dump(ents, f, indent=1)
         errs = make_errs(tmp)
-        frames = make_frames(tmp)
+        frames = make_frames(tmp, args.big)
+        if not args.big:  # keep the full-size digests of an earlier --big run
+            fp = os.path.join(HERE, "frames.json")
+            if os.path.exists(fp):
+                with open(fp) as f:
+                    frames += [e for e in json.load(f) if "file" not in e]
     with open(os.path.join(HERE, "frames.json"), "w") as f:
         json.dump(frames, f, indent=1)
     with open(os.path.join(HERE, "errs.json"), "w") as f:

@@ -21,7 +21,9 @@ from yalantinglibs_amd import synth
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 with open(os.path.join(GOLD, "frames.json")) as _f:
-    FRAMES = json.load(_f)
+    _ALL = json.load(_f)
+FRAMES = [e for e in _ALL if "file" in e]          # byte fixtures
+FRAMES_BIG = [e for e in _ALL if "file" not in e]  # full-size C5 digests
 
 
 def _fixture(ent):
@@ -157,3 +159,41 @@ def test_gpu_framed_decode_short_frames():
         assert e[6] != 0  # starts one byte early: head check fails
         bad = {2, 3, 5, 6}
         assert all(e[i] == 0 for i in range(n) if i not in bad)
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+@pytest.mark.parametrize("ent", FRAMES_BIG, ids=[e["name"] for e in FRAMES_BIG])
+def test_gpu_framed_full_size(ent):
+    """bench.py --config c5 sizes (333,333 messages per type, device-generated
+    inputs): framed encode == digest of the reference-built frames, and the
+    framed decode gives the inputs back."""
+    import hashlib
+    import torch
+    from yalantinglibs_amd import struct_pack as SP
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    n = ent["n"]
+    cd = SP.Codec(LY.case_layout(ent["case"]))
+    b = SP.synth_batch(cd, ent["case"], n, ent["seed"], ent["param"])
+    plan = cd.get_needed_size(b, SP.MODE_MESSAGES)
+    fr = _frame_of(ent)
+    total = plan.total_bytes + n * fr.prefix_len
+    assert total == ent["wire_len"]
+    out = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+    offs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    cd.serialize_to(out, b, SP.MODE_MESSAGES, offs, planned=True, frame=fr)
+    h = hashlib.sha256()
+    for i in range(0, total, 1 << 28):
+        h.update(out[i:min(total, i + (1 << 28))].cpu().numpy().tobytes())
+    assert h.hexdigest() == ent["sha256"]
+    lens = torch.diff(offs).cpu().numpy().astype(np.uint64).tobytes()
+    assert hashlib.sha256(lens).hexdigest() == ent["lens_sha256"]
+    elems = [int(x.numel()) // sp.elem.size for x, sp in zip(b.heaps, cd.L.dev.spans)]
+    dec = cd.alloc_batch(n, elems)
+    cd.deserialize_to(dec, out[:total], SP.MODE_MESSAGES, offs, n, prefix=fr.prefix_len)
+    res = cd.result()
+    assert res.errc == 0 and res.count == n
+    assert torch.equal(dec.recs, b.recs)
+    for k in range(len(b.heaps)):
+        assert torch.equal(dec.heaps[k], b.heaps[k])
