@@ -36,7 +36,10 @@ CONFIGS = {
     "c4": ("outer", 10_000_000, 16, "A",
            "C4: 10M Outer{int64, vector<Inner{int32,float}> n U[0,16]} per GPU, one vector message"),
 }
-DOMINANT = {"c2": "spk::shift_copy_kernel"}  # dominant kernel per config (rocprof name)
+# kernel the roofline object describes, per config (rocprof name prefix, for
+# the PMC traffic lookup in profiles/r01/pmc_<config>.json)
+DOMINANT = {"c2": "spk::shift_copy_kernel", "c2b": "void spk::fixed_msg_encode_lds<true>",
+            "c3": "spk::var_encode_write", "c4": "spk::var_encode_write"}
 SEEDS = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
