@@ -227,7 +227,7 @@ def main():
         host = host_path(cd, batch, mode, plan, wire, dec, offs, n, stream, dev)
 
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # N=1 only
         cb = cpu_baseline(case, param)
         if cb:
             runs, cn, threads = cb
@@ -365,7 +365,7 @@ def run_c5(args, torch, dist, world, rank, dev):
     value = algo * world * args.steps / dt / 2**30
 
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:  # N=1 only
         cb = cpu_baseline("c5", 0)
         if cb:
             runs, cn, threads = cb
