@@ -353,3 +353,32 @@ def test_sharded_bodies_concatenate_to_reference(case, n, param):
         assert rc == 0
         parts.append(out[:size].cpu().numpy().tobytes())
     assert b"".join(parts) == exp
+
+
+@pytest.mark.parametrize("case,n,param", [("recs", 5000, 48), ("rec64", 3000, 0)])
+def test_sharded_encoder_rccl_world1(case, n, param):
+    """ShardedVectorEncoder end to end over RCCL (backend "nccl") with one
+    rank: width/size agreement collectives on device tensors, the body
+    encode, the header, the root's assembly and the host-buffer variant, all
+    equal to the reference bytes (via the pinned oracle)."""
+    import socket
+    import torch.distributed as dist
+    from yalantinglibs_amd import parallel as PAR
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                            world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        cd = codec_for(case)
+        _, recs, heaps = synth.make_batch(case, n, 99, param)
+        exp, _, _ = H.oracle_encode(cd.L, C.SPK_MODE_VECTOR, recs, heaps)
+        enc = PAR.ShardedVectorEncoder(cd)
+        out = enc.encode(to_dev(cd, recs, heaps))
+        assert out.cpu().numpy().tobytes() == exp
+        host = torch.zeros(len(exp) + 16, dtype=torch.uint8).pin_memory()
+        sp = enc.encode_to_host(to_dev(cd, recs, heaps), host)
+        assert sp.total_bytes == len(exp) and host[:len(exp)].numpy().tobytes() == exp
+    finally:
+        dist.destroy_process_group()
