@@ -1723,6 +1723,21 @@ struct VecWs {
   uint32_t lp;
 };
 
+// chunk counts past the device-side chunk total must read as zero; span sums
+// start at zero; re-verification stamps start as "never listed"
+__global__ __launch_bounds__(256) void vec_init(VecBufs B, uint64_t nch, uint32_t ns,
+                                                uint64_t *__restrict__ tot) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (uint64_t i = t0; i < nch; i += gs) {
+    B.cnt[i] = 0;
+    B.dirty[i] = 0xFFFFFFFFu;
+    B.dirty[nch + i] = 0xFFFFFFFFu;
+  }
+  for (uint64_t i = t0; i < (uint64_t)ns * nch; i += gs) B.hs[i] = 0;
+  if (t0 < 16) tot[t0] = 0;
+}
+
 static VecWs vec_ws_layout(const spk_layout *L, uint64_t wire_len, uint64_t rec_cap) {
   VecWs v = {};
   v.nch = wire_len / kSpec + 2;
@@ -1802,15 +1817,14 @@ static hipError_t launch_vec_decode_ns(const DecArgs &a, const WalkProg &P, cons
   VecBufs B = vec_bufs(ws, v);
   hipError_t e;
   const uint32_t ns = P.ns;
-  // chunk counts past the device-side chunk total must read as zero
-  if ((e = hipMemsetAsync(B.cnt, 0, v.nch * 4, s)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(B.hs, 0, (uint64_t)(ns ? ns : 1) * v.nch * 8, s)) != hipSuccess) return e;
+  // one launch initialises cnt / hs / tot / dirty (four memsets cost ~20 us)
+  hipLaunchKernelGGL(vec_init, dim3(grid_for(v.nch, 256) < 4096 ? grid_for(v.nch, 256) : 4096),
+                     dim3(256), 0, s, B, v.nch, ns ? ns : 1u,
+                     reinterpret_cast<uint64_t *>(ws + v.tot));
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   uint64_t *tot = reinterpret_cast<uint64_t *>(ws + v.tot);
-  if ((e = hipMemsetAsync(tot, 0, 16 * 8, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, v.lp, v.nch);
   const unsigned cg = grid_for(v.nch, 256);
-  // re-verification stamps start as "never listed"
-  if ((e = hipMemsetAsync(B.dirty, 0xFF, 2 * v.nch * 4, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(vec_spec<NS>, dim3(grid_for(v.nch, (uint64_t)kSpecStep * kSpecWaves)),
                      dim3(64 * kSpecWaves), 0, s, a, P, wire, ws, B);
   for (uint32_t r = 1; r < (uint32_t)kRounds; ++r)
