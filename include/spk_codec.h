@@ -28,6 +28,16 @@
  *                                           rec_off and a u64 element offset into
  *                                           this span's heap at aux; `size` =
  *                                           sizeof(U). Wire: [count:w][bytes].
+ *   SPK_OP_OPTION {rec_off, size, aux}     a std::optional<U> with U trivially
+ *                                           serializable: same record fields as
+ *                                           SPAN with a count of 0 or 1 (the
+ *                                           value sits in this member's heap).
+ *                                           Wire: [has_value:1][U if present]
+ *                                           (packer.hpp:382-388; any non-zero
+ *                                           byte decodes as present like
+ *                                           unpacker.hpp:1251-1275). It is not
+ *                                           a container: it never sets the
+ *                                           width (calculate_size.hpp:100-105).
  * A trivially-serializable T (SPK_LAYOUT_TRIVIAL) is a single COPY of the
  * whole record (reference packer.hpp:418-421, unpacker.hpp:1300-1312).
  *
@@ -82,6 +92,7 @@ extern "C" {
 
 #define SPK_OP_COPY 1u
 #define SPK_OP_SPAN 2u
+#define SPK_OP_OPTION 3u
 
 #define SPK_MODE_VECTOR 0
 #define SPK_MODE_MESSAGES 1
@@ -96,7 +107,7 @@ extern "C" {
 #define SPK_LAYOUT_TRIVIAL 0x1u   /* is_trivial_serializable<T>: 1 COPY op  */
 
 typedef struct spk_op {
-  uint32_t kind;    /* SPK_OP_COPY | SPK_OP_SPAN                             */
+  uint32_t kind;    /* SPK_OP_COPY | SPK_OP_SPAN | SPK_OP_OPTION             */
   uint32_t rec_off; /* COPY: source byte offset; SPAN: u32 count offset      */
   uint32_t size;    /* COPY: byte length;       SPAN: element size (bytes)   */
   uint32_t aux;     /* SPAN: u64 heap element-offset field offset; COPY: 0   */

@@ -84,6 +84,11 @@ static int cmd_kat() {
   kat_one<rpcb::req_header>(os, "req_header", first);
   kat_one<rpcb::resp_header>(os, "resp_header", first);
   kat_one<std::monostate>(os, "monostate", first);
+  kat_one<Opt>(os, "Opt", first);
+  kat_one<std::vector<Opt>>(os, "vector<Opt>", first);
+  kat_one<OptP>(os, "OptP", first);
+  kat_one<std::vector<OptP>>(os, "vector<OptP>", first);
+  kat_one<std::optional<int32_t>>(os, "optional<int32_t>", first);
   kat_one<std::array<int16_t, 3>>(os, "array<int16_t,3>", first);
   kat_one<std::vector<std::string>>(os, "vector<string>", first);
   kat_one<uint8_t, uint16_t, uint32_t, uint64_t, int8_t, int16_t, int64_t,
@@ -152,6 +157,10 @@ static bool with_case(const Args &a, F &&f) {
     return f.template operator()<Pad>([=](Pad &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "mixed")
     return f.template operator()<Mixed>([=](Mixed &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "opt")
+    return f.template operator()<Opt>([=](Opt &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "optp")
+    return f.template operator()<OptP>([=](OptP &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "rect")  // C1: benchmark rect<int> default values
     return f.template operator()<rect<int>>([=](rect<int> &o, uint64_t) { o = rect<int>{}; });
   if (k == "rpcrect")

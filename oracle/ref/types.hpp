@@ -14,6 +14,7 @@
 #include <array>
 #include <cstdint>
 #include <cstring>
+#include <optional>
 #include <string>
 #include <vector>
 
@@ -70,6 +71,14 @@ struct Mixed {  // non-trivial: raw Pad (with padding), raw array, two spans
   std::array<int16_t, 3> arr;
   std::string s;
   std::vector<int32_t> v;
+};
+
+// ---- optional members: [has_value:1][value?] -----
+struct Opt {  // optional first member (no screening byte for the walker)
+  int32_t id;
+  std::optional<double> score;
+  std::string tag;
+  std::optional<Pad> pad;  // trivially serializable value incl. padding
 };
 
 // ---- C1: src/struct_pack/benchmark/data_def.hpp rect<int> --------------
@@ -197,6 +206,31 @@ inline void fill(Mixed &m, uint64_t seed, uint64_t i, uint32_t maxlen) {
   m.v.resize(n);
   for (uint32_t j = 0; j < n; ++j)
     m.v[j] = (int32_t)(uint32_t)mix64(rnd(seed, i, 62) + j);
+}
+
+inline void fill(Opt &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
+  o.id = (int32_t)(uint32_t)rnd(seed, i, 0);
+  const uint64_t bits = rnd(seed, i, 3);
+  if (bits & 1) o.score = rd(rnd(seed, i, 60));
+  o.tag = make_chars(seed, i, maxlen);
+  if (bits & 2) {
+    o.pad.emplace();
+    fill(*o.pad, seed, i, 0);
+  }
+}
+
+// only optional members: no container, so no metainfo byte per message
+struct OptP {
+  int64_t k;
+  std::optional<int32_t> a;
+  std::optional<rpcb::point> b;
+};
+
+inline void fill(OptP &o, uint64_t seed, uint64_t i, uint32_t) {
+  o.k = (int64_t)rnd(seed, i, 0);
+  const uint64_t bits = rnd(seed, i, 3);
+  if (bits & 1) o.a = (int32_t)(uint32_t)rnd(seed, i, 4);
+  if (bits & 4) o.b = rpcb::point{rd(rnd(seed, i, 5)), rd(rnd(seed, i, 6))};
 }
 
 inline rpcb::rect make_rpc_rect(uint64_t seed, uint64_t i) {

@@ -29,7 +29,13 @@ static unsigned n_spans(const spk_layout *L) {
 static uint64_t rec_count(const uint8_t *rec, const spk_op *op) {
   uint32_t c;
   memcpy(&c, rec + op->rec_off, 4);
+  if (op->kind == SPK_OP_OPTION) return c != 0; /* has_value() */
   return c;
+}
+/* prefix bytes of a SPAN (container length, width w) or an OPTION (the bool
+ * has_value: write_wrapper<sizeof(bool)>, packer.hpp:382-388) */
+static unsigned op_pw(const spk_op *op, unsigned w) {
+  return op->kind == SPK_OP_OPTION ? 1u : w;
 }
 static uint64_t rec_heapoff(const uint8_t *rec, const spk_op *op) {
   uint64_t o;
@@ -94,7 +100,7 @@ static uint64_t rec_wire_size(const spk_layout *L, const uint8_t *rec,
     if (op->kind == SPK_OP_COPY)
       s += op->size;
     else
-      s += w + rec_count(rec, op) * op->size;
+      s += op_pw(op, w) + rec_count(rec, op) * op->size;
   }
   return s;
 }
@@ -123,10 +129,11 @@ static uint8_t *write_record(const spk_layout *L, const uint8_t *rec,
       memcpy(p, rec + op->rec_off, op->size);
       p += op->size;
     }
-    else { /* container: low_bytes_write_wrapper<w> + memcpy (:304-363) */
+    else { /* container: low_bytes_write_wrapper<w> + memcpy (:304-363);
+              optional: bool has_value + the value (:382-388) */
       uint64_t c = rec_count(rec, op);
-      put_le(p, c, w);
-      p += w;
+      put_le(p, c, op_pw(op, w));
+      p += op_pw(op, w);
       uint64_t nb = c * op->size;
       if (nb) {
         const uint8_t *src =
@@ -309,9 +316,18 @@ static int32_t read_record(dctx_t *c, rd_t *r, unsigned w, uint8_t *rec) {
       if (rec) memcpy(rec + op->rec_off, p, op->size);
       continue;
     }
-    if (!rd_take(r, w, &p)) return SPK_ERRC_NO_BUFFER_SPACE; /* :905-979 */
-    uint64_t cnt = get_le(p, w);
-    if (cnt) { /* size==0 returns early (:980-982) */
+    /* container length :905-979; optional: read_wrapper<sizeof(bool)>, any
+       non-zero byte is "has value" (unpacker.hpp:1251-1275) */
+    if (!rd_take(r, op_pw(op, w), &p)) return SPK_ERRC_NO_BUFFER_SPACE;
+    uint64_t cnt = op->kind == SPK_OP_OPTION ? (uint64_t)(p[0] != 0) : get_le(p, w);
+    int unreadable = 0;
+    if (cnt && op->kind == SPK_OP_OPTION) {
+      /* deserialize_one(*item)'s errc is dropped (unpacker.hpp:1271-1273):
+         a value that does not fit leaves the reader in place and the value
+         value-initialised */
+      if (!rd_take(r, op->size, &p)) unreadable = 1;
+    }
+    else if (cnt) { /* size==0 returns early (:980-982) */
       if (op->size > 1 && cnt > UINT64_MAX / op->size) /* :1128-1132 */
         return SPK_ERRC_NO_BUFFER_SPACE;
       if (!rd_take(r, cnt * op->size, &p)) /* check(mem_sz) :1147-1149 */
@@ -326,7 +342,9 @@ static int32_t read_record(dctx_t *c, rd_t *r, unsigned w, uint8_t *rec) {
         uint32_t c32 = (uint32_t)cnt;
         memcpy(rec + op->rec_off, &c32, 4);
         memcpy(rec + op->aux, &off, 8);
-        if (cnt)
+        if (unreadable)
+          memset((uint8_t *)c->heaps[sk] + off * op->size, 0, op->size);
+        else if (cnt)
           memcpy((uint8_t *)c->heaps[sk] + off * op->size, p, cnt * op->size);
         c->used[sk] = off + cnt;
       }

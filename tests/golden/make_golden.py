@@ -29,7 +29,7 @@ GEN = os.path.join(ROOT, "oracle", "_ref", "golden_gen")
 
 SEED = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004,
         "pad": 0x5EED0005, "mixed": 0x5EED0006, "rect": 0, "rpcrect": 0x5EED0007,
-        "person": 0x5EED0008, "ints": 0x5EED0009}
+        "person": 0x5EED0008, "ints": 0x5EED0009, "opt": 0x5EED000A, "optp": 0x5EED000B}
 
 # (case_mode, n, param, conf, keep_bin)
 SMALL = [
@@ -58,6 +58,11 @@ SMALL = [
     ("rpcrect_A", 100, 0, "default"), ("rpcrect_B", 100, 0, "default"),
     ("person_A", 100, 64, "default"), ("person_B", 100, 300, "default"),
     ("ints_B", 100, 300, "default"), ("ints_B", 20, 3000, "default"),
+    ("opt_A", 0, 16, "default"), ("opt_A", 1, 16, "default"),
+    ("opt_A", 300, 16, "default"), ("opt_A", 40, 400, "default"),
+    ("opt_A", 100, 48, "typeinfo"), ("opt_B", 200, 300, "default"),
+    ("optp_A", 300, 0, "default"), ("optp_B", 200, 0, "default"),
+    ("optp_B", 50, 0, "typeinfo"), ("optp_A", 20, 0, "nometa"),
 ]
 MEDIUM = [  # digest only (wire > ~1 MB)
     ("rec64_A", 65535, 0, "default"), ("rec64_A", 65536, 0, "default"),
@@ -65,6 +70,8 @@ MEDIUM = [  # digest only (wire > ~1 MB)
     ("outer_A", 70000, 16, "default"), ("mixed_A", 20000, 40, "default"),
     ("recs_B", 70000, 48, "default"), ("outer_B", 70000, 16, "default"),
     ("ints_B", 3, 70000, "default"), ("ints_B", 20, 70000, "default"),
+    ("opt_A", 70000, 48, "default"), ("optp_A", 70000, 0, "default"),
+    ("opt_B", 70000, 48, "default"),
 ]
 BIG = [  # BASELINE.json full-size configs (digest only)
     ("rec64_A", 100_000_000, 0, "default"),
@@ -173,6 +180,7 @@ ERR_BASES = [
     ("rect_A", 3, 0, "default"), ("outer_A", 4, 8, "default"),
     ("rec64_A", 300, 0, "default"), ("recs_B", 1, 300, "default"),
     ("rec64_B", 1, 0, "default"), ("mixed_A", 3, 300, "default"),
+    ("opt_A", 6, 10, "default"), ("optp_B", 1, 0, "default"), ("opt_B", 1, 20, "default"),
 ]
 
 

@@ -34,6 +34,7 @@ ERRC_CAPACITY = 100
 
 SPK_OP_COPY = 1
 SPK_OP_SPAN = 2
+SPK_OP_OPTION = 3
 SPK_MODE_VECTOR = 0
 SPK_MODE_MESSAGES = 1
 

@@ -42,22 +42,24 @@ int spk_layout_check(const spk_layout *L) {
     if (L->fmt_one.flags & SPK_MF_HAS_CONTAINER) return SPK_E_LAYOUT;
     return SPK_OK;
   }
-  uint32_t spans = 0;
+  uint32_t spans = 0, conts = 0;
   for (uint32_t i = 0; i < L->n_ops; ++i) {
     const spk_op &o = L->ops[i];
     if (o.kind == SPK_OP_COPY) {
       if (o.size == 0 || (uint64_t)o.rec_off + o.size > L->rec_stride) return SPK_E_LAYOUT;
-    } else if (o.kind == SPK_OP_SPAN) {
+    } else if (o.kind == SPK_OP_SPAN || o.kind == SPK_OP_OPTION) {
       if (o.size == 0 || o.rec_off % 4 || o.aux % 8 || o.rec_off + 4 > L->rec_stride ||
           o.aux + 8 > L->rec_stride)
         return SPK_E_LAYOUT;
       ++spans;
+      conts += o.kind == SPK_OP_SPAN;
     } else {
       return SPK_E_LAYOUT;
     }
   }
   if (spans == 0 || spans > SPK_MAX_SPANS || L->rec_stride % 8) return SPK_E_LAYOUT;
-  if (!(L->fmt_one.flags & SPK_MF_HAS_CONTAINER)) return SPK_E_LAYOUT;
+  // check_if_has_container<T>: a container member (an optional alone is none)
+  if (!(L->fmt_one.flags & SPK_MF_HAS_CONTAINER) != !conts) return SPK_E_LAYOUT;
   return SPK_OK;
 }
 
@@ -117,7 +119,7 @@ static int encode_impl(const spk_layout *L, int mode, uint64_t n, const void *d_
   }
   if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
   uint32_t spans = 0;
-  for (uint32_t i = 0; i < L->n_ops; ++i) spans += L->ops[i].kind == SPK_OP_SPAN;
+  for (uint32_t i = 0; i < L->n_ops; ++i) spans += L->ops[i].kind != SPK_OP_COPY;
   if (!d_heaps) return SPK_E_ARG;
   for (uint32_t k = 0; k < spans; ++k)
     if (!d_heaps[k] && n) return SPK_E_ARG;

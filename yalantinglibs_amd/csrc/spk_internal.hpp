@@ -22,9 +22,9 @@ struct KLayout {
   uint32_t stride;
   uint32_t n_ops;
   uint32_t trivial;
-  uint32_t n_spans;
-  uint32_t fixed_bytes;  // sum of COPY sizes (== stride when trivial)
-  uint32_t pad_;
+  uint32_t n_spans;      // SPAN + OPTION members (one heap each)
+  uint32_t fixed_bytes;  // sum of COPY sizes + one has_value byte per OPTION
+  uint32_t n_cont;       // SPAN members: the ones with a width-w count
   spk_op ops[SPK_MAX_OPS];
 };
 

@@ -66,10 +66,15 @@ static KLayout make_klayout(const spk_layout *L) {
   k.trivial = (L->flags & SPK_LAYOUT_TRIVIAL) ? 1 : 0;
   for (uint32_t i = 0; i < L->n_ops && i < SPK_MAX_OPS; ++i) {
     k.ops[i] = L->ops[i];
-    if (L->ops[i].kind == SPK_OP_COPY)
+    if (L->ops[i].kind == SPK_OP_COPY) {
       k.fixed_bytes += L->ops[i].size;
-    else
+    } else {
       ++k.n_spans;
+      if (L->ops[i].kind == SPK_OP_SPAN)
+        ++k.n_cont;
+      else
+        k.fixed_bytes += 1;  // OPTION: has_value byte
+    }
   }
   return k;
 }
@@ -113,6 +118,25 @@ __device__ __forceinline__ void store_le(uint8_t *d, uint64_t v, uint32_t w) {
   }
 }
 
+// SPAN/OPTION helpers: an OPTION's count is 0/1 and its prefix one byte
+__device__ __forceinline__ uint32_t op_pw(const spk_op &op, uint32_t w) {
+  return op.kind == SPK_OP_OPTION ? 1u : w;
+}
+__device__ __forceinline__ uint64_t op_rec_count(const spk_op &op, const uint8_t *rec) {
+  const uint32_t c = rec_u32(rec, op.rec_off);
+  return op.kind == SPK_OP_OPTION ? (uint64_t)(c != 0) : (uint64_t)c;
+}
+
+// Payload bytes a SPAN/OPTION with count c consumes at pos (message end
+// `end`). An OPTION's value read status is ignored by the reference
+// (unpacker.hpp:1271-1273 drops deserialize_one's errc): a present value that
+// does not fit leaves the reader where it was and the value value-initialised.
+__device__ __forceinline__ uint64_t opt_nb(const spk_op &op, uint64_t c, uint64_t pos,
+                                           uint64_t end) {
+  const uint64_t nb = c * op.size;
+  return (op.kind == SPK_OP_OPTION && nb > end - pos) ? 0 : nb;
+}
+
 // w-independent bytes of one record (fixed + span payloads) and its max count
 __device__ __forceinline__ void rec_sizes(const KLayout &L, const uint8_t *rec,
                                           uint64_t &var, uint64_t &maxc) {
@@ -124,6 +148,8 @@ __device__ __forceinline__ void rec_sizes(const KLayout &L, const uint8_t *rec,
       const uint64_t c = rec_u32(rec, op.rec_off);
       var += c * op.size;
       maxc = c > maxc ? c : maxc;
+    } else if (op.kind == SPK_OP_OPTION) {
+      var += op_rec_count(op, rec) * op.size;  // not a container: no width
     }
   }
 }
@@ -199,7 +225,7 @@ __global__ __launch_bounds__(kThreads) void var_plan_reduce(
           sum = var;
         } else {
           const uint32_t w = width_of(maxc);
-          sum = hdrlen_tbl[wlog(w)] + var + (uint64_t)a.L.n_spans * w;
+          sum = hdrlen_tbl[wlog(w)] + var + (uint64_t)a.L.n_cont * w;
         }
         mx = maxc > mx ? maxc : mx;
       }
@@ -224,7 +250,7 @@ struct FinArgs {
   spk_msgfmt fmt;
   uint64_t n;
   uint64_t nblocks;
-  uint32_t n_spans;
+  uint32_t n_cont;  // width-w count fields per record
   int mode;
 };
 
@@ -256,7 +282,7 @@ __global__ __launch_bounds__(1024) void var_plan_finalize(FinArgs a,
     uint8_t *hb = ws + kWsHdrVec;
     const uint32_t len = write_hdr(hb, a.fmt, w);
     for (uint32_t i = 0; i < w; ++i) hb[len + i] = (uint8_t)(a.n >> (8 * i));
-    r.total_bytes = len + w + carry + a.n * (uint64_t)a.n_spans * w;
+    r.total_bytes = len + w + carry + a.n * (uint64_t)a.n_cont * w;
     r.max_count = maxc;
     r.var_bytes = carry;
     r.width = w;
@@ -351,9 +377,10 @@ __device__ __forceinline__ void win_record(const VarArgs &a, const uint8_t *rec,
       win_put(W, pos, rec + op.rec_off, op.size);
       pos += op.size;
     } else {
-      const uint64_t c = rec_u32(rec, op.rec_off);
-      win_put_le(W, pos, c, w);
-      pos += w;
+      const uint64_t c = op_rec_count(op, rec);
+      const uint32_t pw = op_pw(op, w);
+      win_put_le(W, pos, c, pw);
+      pos += pw;
       const uint64_t nb = c * op.size;
       if (nb && !(skip >> sk & 1)) win_put(W, pos, a.heaps[sk] + rec_u64(rec, op.aux) * op.size, nb);
       pos += nb;
@@ -486,7 +513,7 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
   uint64_t gb = pb.sum;
   for (uint32_t j = 0; j < blockIdx.x % kPlanSub; ++j) gb += pb.sub[j];
   const uint64_t g0 = a.mode == SPK_MODE_VECTOR
-                          ? hdr_vec + gb + r0 * (uint64_t)a.L.n_spans * w_vec
+                          ? hdr_vec + gb + r0 * (uint64_t)a.L.n_cont * w_vec
                           : gb + r0 * (uint64_t)a.fpre;
   if (a.mode == SPK_MODE_VECTOR && blockIdx.x == 0)
     for (uint32_t i = threadIdx.x; i < hdr_vec; i += blockDim.x) out[i] = ws[kWsHdrVec + i];
@@ -501,11 +528,11 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
       uint64_t var, maxc;
       rec_sizes(a.L, recs + i * a.L.stride, var, maxc);
       if (a.mode == SPK_MODE_VECTOR) {
-        sz = var + (uint64_t)a.L.n_spans * w_vec;
+        sz = var + (uint64_t)a.L.n_cont * w_vec;
       } else {
         w = width_of(maxc);
         sz = a.fpre + ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + wlog(w)] + var +
-             (uint64_t)a.L.n_spans * w;
+             (uint64_t)a.L.n_cont * w;
       }
     }
     uint64_t btot;
@@ -529,8 +556,8 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
     if (i < a.n) {
       const uint8_t *rec = recs + i * a.L.stride;
       for (uint32_t o = 0; o < a.L.n_ops; ++o)
-        if (a.L.ops[o].kind == SPK_OP_SPAN &&
-            (uint64_t)rec_u32(rec, a.L.ops[o].rec_off) * a.L.ops[o].size >= kBigBytes)
+        if (a.L.ops[o].kind != SPK_OP_COPY &&
+            op_rec_count(a.L.ops[o], rec) * a.L.ops[o].size >= kBigBytes)
           ++nbig;
     }
     uint64_t round_tot;
@@ -548,8 +575,8 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
           q += op.size;
           continue;
         }
-        const uint64_t nb = (uint64_t)rec_u32(rec, op.rec_off) * op.size;
-        q += wj[j];
+        const uint64_t nb = op_rec_count(op, rec) * op.size;
+        q += op_pw(op, wj[j]);
         if (nb >= kBigBytes) {
           big[slot++] = BigSeg{q, nullptr, a.heaps[sk] + rec_u64(rec, op.aux) * op.size, nb};
           skip[j] |= 1u << sk;
@@ -616,14 +643,18 @@ __device__ __forceinline__ uint64_t rec_wire_len(const KLayout &L, const uint8_t
       pos += op.size;
       if (pos > len) return 0;
     } else {
-      if (pos + w > len) return 0;
-      const uint64_t c = ld_le(wire + pos, w);
-      pos += w;
+      const uint32_t pw = op_pw(op, w);
+      if (pos + pw > len) return 0;
+      const uint64_t c = op.kind == SPK_OP_OPTION ? (uint64_t)(wire[pos] != 0) : ld_le(wire + pos, w);
+      pos += pw;
       if (c) {
         if (op.size > 1 && c > ~0ull / op.size) return 0;
         const uint64_t nb = c * op.size;
-        if (nb > len - pos) return 0;
-        pos += nb;
+        if (nb > len - pos) {
+          if (op.kind != SPK_OP_OPTION) return 0;
+        } else {
+          pos += nb;
+        }
       }
     }
   }
@@ -634,7 +665,7 @@ __device__ __forceinline__ uint64_t rec_wire_len(const KLayout &L, const uint8_t
 // heap_off[k] = element offset where this record's span k goes.
 __device__ void decode_record(const KLayout &L, const uint8_t *wire, uint64_t pos,
                               uint32_t w, uint8_t *rec, uint8_t *const *heaps,
-                              const uint64_t *heap_off, uint32_t skip = 0) {
+                              const uint64_t *heap_off, uint64_t end, uint32_t skip = 0) {
   uint32_t sk = 0;
   for (uint32_t o = 0; o < L.n_ops; ++o) {
     const spk_op op = L.ops[o];
@@ -642,12 +673,16 @@ __device__ void decode_record(const KLayout &L, const uint8_t *wire, uint64_t po
       copy_bytes(rec + op.rec_off, wire + pos, op.size);
       pos += op.size;
     } else {
-      const uint64_t c = ld_le(wire + pos, w);
-      pos += w;
+      const uint64_t c = op.kind == SPK_OP_OPTION ? (uint64_t)(wire[pos] != 0) : ld_le(wire + pos, w);
+      pos += op_pw(op, w);
       *reinterpret_cast<uint32_t *>(rec + op.rec_off) = (uint32_t)c;
       *reinterpret_cast<uint64_t *>(rec + op.aux) = heap_off[sk];
-      const uint64_t nb = c * op.size;
-      if (!(skip >> sk & 1)) copy_bytes(heaps[sk] + heap_off[sk] * op.size, wire + pos, nb);
+      const uint64_t nb = opt_nb(op, c, pos, end);
+      uint8_t *hp = heaps[sk] + heap_off[sk] * op.size;
+      if (c && !nb && op.kind == SPK_OP_OPTION)
+        for (uint32_t b = 0; b < op.size; ++b) hp[b] = 0;  // unreadable value
+      else if (!(skip >> sk & 1))
+        copy_bytes(hp, wire + pos, nb);
       pos += nb;
       ++sk;
     }
@@ -656,16 +691,18 @@ __device__ void decode_record(const KLayout &L, const uint8_t *wire, uint64_t po
 
 // counts of the record at pos (assumes it is complete)
 __device__ __forceinline__ void rec_counts(const KLayout &L, const uint8_t *wire,
-                                           uint64_t pos, uint32_t w, uint64_t *cnt) {
+                                           uint64_t pos, uint32_t w, uint64_t *cnt,
+                                           uint64_t end) {
   uint32_t sk = 0;
   for (uint32_t o = 0; o < L.n_ops; ++o) {
     const spk_op op = L.ops[o];
     if (op.kind == SPK_OP_COPY) {
       pos += op.size;
     } else {
-      const uint64_t c = ld_le(wire + pos, w);
+      const uint64_t c = op.kind == SPK_OP_OPTION ? (uint64_t)(wire[pos] != 0) : ld_le(wire + pos, w);
       cnt[sk++] = c;
-      pos += w + c * op.size;
+      pos += op_pw(op, w);
+      pos += opt_nb(op, c, pos, end);
     }
   }
 }
@@ -726,7 +763,7 @@ __global__ __launch_bounds__(kThreads) void var_msg_parse(
           if (i >= a.rec_cap) s.errc = SPK_ERRC_CAPACITY;
           s.pos = b + pos;
           s.w = w;
-          rec_counts(a.L, wire, b + pos, w, cnt);
+          rec_counts(a.L, wire, b + pos, w, cnt, e);
           ok = 1;
           consumed = pos + rl > dl ? pos + rl : dl;
         }
@@ -798,8 +835,8 @@ __global__ __launch_bounds__(1024) void var_scan_blocks(uint64_t nblocks,
 }
 
 __global__ __launch_bounds__(kThreads) void var_msg_write(
-    DecArgs a, const uint8_t *__restrict__ wire, const uint8_t *__restrict__ ws,
-    uint8_t *__restrict__ recs, const spk_dresult_t *res) {
+    DecArgs a, const uint8_t *__restrict__ wire, const uint64_t *__restrict__ offs,
+    const uint8_t *__restrict__ ws, uint8_t *__restrict__ recs, const spk_dresult_t *res) {
   __shared__ uint64_t sh[kThreads / 64];
   const MsgState *st = reinterpret_cast<const MsgState *>(ws + kWsScratch);
   const uint64_t *bsum = reinterpret_cast<const uint64_t *>(ws + kWsScratch +
@@ -811,9 +848,13 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
   const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
   MsgState s{~0ull, 1, 1};
   uint64_t cnt[SPK_MAX_SPANS] = {};
+  uint64_t end = 0;
   if (i < a.n_msgs) {
     s = st[i];
-    if (s.pos != ~0ull) rec_counts(a.L, wire, s.pos, s.w, cnt);
+    if (s.pos != ~0ull) {
+      end = offs[i + 1];
+      rec_counts(a.L, wire, s.pos, s.w, cnt, end);
+    }
   }
   uint64_t hoff[SPK_MAX_SPANS] = {};
   for (uint32_t k = 0; k < a.L.n_spans; ++k) {
@@ -827,8 +868,8 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
   if (live) {
     uint32_t sk = 0;
     for (uint32_t o = 0; o < a.L.n_ops; ++o)
-      if (a.L.ops[o].kind == SPK_OP_SPAN) {
-        if (cnt[sk] * a.L.ops[o].size >= kBigBytes) ++nbig;
+      if (a.L.ops[o].kind != SPK_OP_COPY) {  // OPTION values: never listed
+        if (a.L.ops[o].kind == SPK_OP_SPAN && cnt[sk] * a.L.ops[o].size >= kBigBytes) ++nbig;
         ++sk;
       }
   }
@@ -843,9 +884,9 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
         pos += op.size;
         continue;
       }
-      pos += s.w;
-      const uint64_t nb = cnt[sk] * op.size;
-      if (nb >= kBigBytes) {
+      pos += op_pw(op, s.w);
+      const uint64_t nb = opt_nb(op, cnt[sk], pos, end);
+      if (op.kind == SPK_OP_SPAN && nb >= kBigBytes) {
         big[slot++] = BigSeg{0, a.heaps[sk] + hoff[sk] * op.size, wire + pos, nb};
         skip |= 1u << sk;
       }
@@ -853,7 +894,7 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
       ++sk;
     }
   }
-  if (live) decode_record(a.L, wire, s.pos, s.w, recs + i * a.L.stride, a.heaps, hoff, skip);
+  if (live) decode_record(a.L, wire, s.pos, s.w, recs + i * a.L.stride, a.heaps, hoff, end, skip);
   __syncthreads();
   if (nbig_tot > kBigMax) nbig_tot = kBigMax;
   if (nbig_tot == 0) return;  // block-uniform
@@ -932,6 +973,7 @@ struct WalkProg {
   uint32_t esz[SPK_MAX_SPANS];
   uint32_t c0max;                  // largest first count of a plausible record
   uint64_t cmax[SPK_MAX_SPANS];    // largest count whose byte size fits 64 bits
+  uint32_t optm;                   // bit k: span k is an OPTION ([has_value:1][U?])
 };
 
 static WalkProg make_walkprog(const spk_layout *L) {
@@ -942,12 +984,15 @@ static WalkProg make_walkprog(const spk_layout *L) {
       p.skip[k] += L->ops[i].size;
     } else {
       p.esz[k] = L->ops[i].size;
+      if (L->ops[i].kind == SPK_OP_OPTION) p.optm |= 1u << k;
       ++k;
     }
   }
   p.ns = k;
   for (uint32_t j = 0; j < k; ++j) p.cmax[j] = ~0ull / (p.esz[j] ? p.esz[j] : 1);
   p.c0max = k ? (kPlaus > p.skip[0] ? (kPlaus - p.skip[0]) / (p.esz[0] ? p.esz[0] : 1) : 0) : 0;
+  // an OPTION's has_value byte is not a w-byte count: no screening on it
+  if (p.optm & 1u) p.c0max = 0xFFFFFFFFu;
   return p;
 }
 
@@ -972,14 +1017,19 @@ __device__ __forceinline__ uint64_t wlen(const WalkProg &P, const uint8_t *wire,
 #pragma unroll
   for (uint32_t k = 0; k < (NS > 0 ? (uint32_t)NS : SPK_MAX_SPANS); ++k) {
     if (NS == 0 && k >= ns) break;
-    if (p + w > len) return 0;
-    const uint64_t c = wire_le(wire, p, w);
-    p += w;
+    const bool opt = (P.optm >> k) & 1u;
+    const uint32_t pw = opt ? 1u : w;
+    if (p + pw > len) return 0;
+    const uint64_t c = opt ? (uint64_t)(wire[p] != 0) : wire_le(wire, p, w);
+    p += pw;
     if (c) {
       if (c > P.cmax[k]) return 0;
       const uint64_t nb = c * P.esz[k];
-      if (nb > len - p) return 0;
-      p += nb;
+      if (nb > len - p) {
+        if (!opt) return 0;  // OPTION: value unreadable, reader stays (opt_nb)
+      } else {
+        p += nb;
+      }
     }
     p += P.skip[k + 1];
   }
@@ -996,14 +1046,19 @@ __device__ __forceinline__ uint64_t wlen_rd(const WalkProg &P, const Rd &rd, uin
 #pragma unroll
   for (uint32_t k = 0; k < (NS > 0 ? (uint32_t)NS : SPK_MAX_SPANS); ++k) {
     if (NS == 0 && k >= ns) break;
-    if (p + w > len) return 0;
-    const uint64_t c = rd(p);
-    p += w;
+    const bool opt = (P.optm >> k) & 1u;
+    const uint32_t pw = opt ? 1u : w;
+    if (p + pw > len) return 0;
+    const uint64_t c = opt ? (uint64_t)(rd.byte(p) != 0) : rd(p);
+    p += pw;
     if (c) {
       if (c > P.cmax[k]) return 0;
       const uint64_t nb = c * P.esz[k];
-      if (nb > len - p) return 0;
-      p += nb;
+      if (nb > len - p) {
+        if (!opt) return 0;  // OPTION: value unreadable, reader stays (opt_nb)
+      } else {
+        p += nb;
+      }
     }
     if (cnt) cnt[k] = c;
     p += P.skip[k + 1];
@@ -1017,6 +1072,7 @@ struct GReader {
   const uint8_t *wire;
   uint32_t w;
   __device__ __forceinline__ uint64_t operator()(uint64_t x) const { return wire_le(wire, x, w); }
+  __device__ __forceinline__ uint32_t byte(uint64_t x) const { return wire[x]; }
 };
 
 __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
@@ -1039,7 +1095,7 @@ __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
     // every record needs at least fixed + n_spans*w bytes: a payload that
     // cannot hold n of them fails in the reference's record loop with
     // no_buffer_space (unpacker.hpp:1208-1226)
-    const uint64_t min_rec = a.L.fixed_bytes + (uint64_t)a.L.n_spans * w;
+    const uint64_t min_rec = a.L.fixed_bytes + (uint64_t)a.L.n_cont * w;
     const uint64_t payload = a.wire_len - pos;
     if (n > payload / (min_rec ? min_rec : 1)) e = SPK_ERRC_NO_BUFFER_SPACE;
   }
@@ -1106,6 +1162,13 @@ struct WinReader {
       return lo | ((uint64_t)__builtin_amdgcn_alignbyte(d[i + 2], d1, sh) << 32);
     }
     return wire_le(wire, x, w);
+  }
+  __device__ __forceinline__ uint32_t byte(uint64_t x) const {
+    if (x < wend) {
+      const uint32_t o = (uint32_t)(x - cs);
+      return (d[o >> 2] >> (8 * (o & 3))) & 0xFFu;
+    }
+    return wire[x];
   }
 };
 
@@ -1315,6 +1378,7 @@ __global__ __launch_bounds__(64 * kSpecWaves) void vec_spec(DecArgs a, WalkProg 
           m |= (cv <= P.c0max ? 1u : 0u) << k;
         }
       }
+      if (P.optm & 1u) m = 0xFFu;  // first span is an OPTION: every byte may start a record
       const uint64_t rem = ce - (cs + t);  // candidates must start in the chunk
       if (rem < 8) m &= (1u << rem) - 1u;
       if (!m) {
@@ -1610,7 +1674,7 @@ __global__ void vec_finish(DecArgs a, uint8_t *__restrict__ ws, spk_dresult_t *r
 // decode_record with piecewise copies; off[k] = heap element offset of span k
 __device__ __forceinline__ void emit_record(const KLayout &L, const uint8_t *wire, uint64_t pos,
                                             uint32_t w, uint8_t *rec, uint8_t *const *heaps,
-                                            const uint64_t *off) {
+                                            const uint64_t *off, uint64_t end) {
   uint32_t sk = 0;
   for (uint32_t o = 0; o < L.n_ops; ++o) {
     const spk_op op = L.ops[o];
@@ -1618,12 +1682,16 @@ __device__ __forceinline__ void emit_record(const KLayout &L, const uint8_t *wir
       copy_bytes(rec + op.rec_off, wire + pos, op.size);
       pos += op.size;
     } else {
-      const uint64_t cnt = wire_le(wire, pos, w);
-      pos += w;
+      const uint64_t cnt = op.kind == SPK_OP_OPTION ? (uint64_t)(wire[pos] != 0) : wire_le(wire, pos, w);
+      pos += op_pw(op, w);
       *reinterpret_cast<uint32_t *>(rec + op.rec_off) = (uint32_t)cnt;
       *reinterpret_cast<uint64_t *>(rec + op.aux) = off[sk];
-      const uint64_t nb = cnt * op.size;
-      copy_bytes(heaps[sk] + off[sk] * op.size, wire + pos, nb);
+      const uint64_t nb = opt_nb(op, cnt, pos, end);
+      uint8_t *hp = heaps[sk] + off[sk] * op.size;
+      if (cnt && !nb && op.kind == SPK_OP_OPTION)
+        for (uint32_t b = 0; b < op.size; ++b) hp[b] = 0;  // unreadable value
+      else
+        copy_bytes(hp, wire + pos, nb);
       pos += nb;
       ++sk;
     }
@@ -1704,7 +1772,7 @@ __global__ __launch_bounds__(64 * kEmitWaves) void vec_emit(DecArgs a, WalkProg 
       off[q] = carry[q] + wave_excl_scan_u64(act ? rc[q] : 0, lane, &tot);
       carry[q] += tot;
     }
-    if (act) emit_record(a.L, wire, pos, w, recs + (R0 + i) * a.L.stride, a.heaps, off);
+    if (act) emit_record(a.L, wire, pos, w, recs + (R0 + i) * a.L.stride, a.heaps, off, a.wire_len);
   }
 }
 
@@ -1897,7 +1965,7 @@ hipError_t launch_var_plan(const spk_layout *L, int mode, uint64_t n, const void
   f.fmt = mode == SPK_MODE_VECTOR ? L->fmt_vector : L->fmt_one;
   f.n = n;
   f.nblocks = n ? nb : 0;
-  f.n_spans = a.L.n_spans;
+  f.n_cont = a.L.n_cont;
   f.mode = mode;
   hipLaunchKernelGGL(var_plan_finalize, dim3(1), dim3(1024), 0, s, f, ws, d_plan);
   (void)ws_bytes;
@@ -1948,7 +2016,7 @@ hipError_t launch_var_encode_body(const spk_layout *L, uint64_t n, const void *d
   hipError_t e = launch_var_plan(L, SPK_MODE_VECTOR, n, d_recs, plan, d_ws, ws_bytes, s);
   if (e != hipSuccess) return e;
   uint32_t ns = 0;
-  for (uint32_t i = 0; i < L->n_ops; ++i) ns += L->ops[i].kind == SPK_OP_SPAN;
+  for (uint32_t i = 0; i < L->n_ops; ++i) ns += L->ops[i].kind == SPK_OP_SPAN;  // width-w counts
   hipLaunchKernelGGL(body_plan_kernel, dim3(1), dim3(64), 0, s, plan, n, ns, width);
   return launch_var_encode(L, SPK_MODE_VECTOR, n, d_recs, d_heaps, plan, d_out, out_cap,
                            nullptr, nullptr, d_ws, ws_bytes, s);
@@ -1983,7 +2051,7 @@ hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
     uint64_t *bsum = reinterpret_cast<uint64_t *>(ws + kWsScratch + sizeof(MsgState) * n_msgs);
     hipLaunchKernelGGL(var_scan_blocks, dim3(1), dim3(1024), 0, s, (uint64_t)nb,
                        a.L.n_spans, bsum, a, d_res);
-    hipLaunchKernelGGL(var_msg_write, dim3(nb), dim3(kThreads), 0, s, a, wire,
+    hipLaunchKernelGGL(var_msg_write, dim3(nb), dim3(kThreads), 0, s, a, wire, d_offsets,
                        (const uint8_t *)ws, (uint8_t *)d_recs, (const spk_dresult_t *)d_res);
     (void)ws_bytes;
     return hipGetLastError();

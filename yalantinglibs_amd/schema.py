@@ -13,7 +13,7 @@ Computes, exactly as the reference does at compile time:
   * the sp_config resolution that decides hash head / type literal
     (type_calculate.hpp:158-172, 744-891);
 and flattens a record type into the spk_layout descriptor of
-include/spk_codec.h (COPY / SPAN ops over a "device record").
+include/spk_codec.h (COPY / SPAN / OPTION ops over a "device record").
 """
 from __future__ import annotations
 
@@ -161,6 +161,25 @@ class String(SpType):
     @property
     def has_container(self):
         return True
+
+
+class Optional(SpType):
+    """std::optional<T> (optional_t): wire [has_value:1][T if present]
+    (ref packer.hpp:382-388, unpacker.hpp:1251-1275); its literal is
+    optional_t + literal(T) (type_calculate.hpp:273-278); a container only if
+    T holds one (type_calculate.hpp:846-849)."""
+
+    def __init__(self, elem: SpType):
+        self.elem = elem
+        self.name = f"std::optional<{elem.name}>"
+        self.config = DEFAULT
+
+    def literal(self):
+        return bytes([TID_OPTIONAL]) + self.elem.literal()
+
+    @property
+    def has_container(self):
+        return self.elem.has_container
 
 
 class Array(SpType):
@@ -350,6 +369,17 @@ def flatten(rtype: SpType) -> DeviceLayout:
             coff = place(4, 4)
             ooff = place(8, 8)
             ops.append((C.SPK_OP_SPAN, coff, t.elem.size, ooff))
+            spans.append(SpanField(path, t.elem, coff, ooff))
+            npf.append((path + ".n", "<u4", coff))
+            npf.append((path + ".off", "<u8", ooff))
+        elif isinstance(t, Optional):
+            if not t.elem.trivial:
+                raise NotImplementedError(
+                    f"{path}: optional of non-trivially-serializable "
+                    f"{t.elem.name} is outside the flat record model")
+            coff = place(4, 4)
+            ooff = place(8, 8)
+            ops.append((C.SPK_OP_OPTION, coff, t.elem.size, ooff))
             spans.append(SpanField(path, t.elem, coff, ooff))
             npf.append((path + ".n", "<u4", coff))
             npf.append((path + ".off", "<u8", ooff))

@@ -77,9 +77,14 @@ RespHeader = S.Struct("resp_header", [("magic", S.uint8), ("version", S.uint8),
                                       ("seq_num", S.uint32), ("length", S.uint32),
                                       ("attach_length", S.uint32)])
 
+Opt = S.Struct("Opt", [("id", S.int32), ("score", S.Optional(S.float64)),
+                       ("tag", S.String()), ("pad", S.Optional(Pad))])
+OptP = S.Struct("OptP", [("k", S.int64), ("a", S.Optional(S.int32)),
+                         ("b", S.Optional(Point))])
+
 CASE_TYPES = {"rec64": Rec64, "recs": RecS, "outer": Outer, "pad": Pad,
               "mixed": Mixed, "rect": RectInt, "rpcrect": RpcRect,
-              "person": Person, "ints": Ints}
+              "person": Person, "ints": Ints, "opt": Opt, "optp": OptP}
 # vector<rect<int>> has its own ADL set_sp_config (benchmark data_def.hpp:69-72)
 VECTOR_CONFIG = {"rect": S.DISABLE_ALL_META_INFO}
 
@@ -93,6 +98,20 @@ def _chars(seed, idx, lens):
     w = rnd(seed, rec, np.uint64(2) + (j >> np.uint64(3)) % np.uint64(56))
     b = (w >> ((j & np.uint64(7)) * np.uint64(8))) & np.uint64(0xFF)
     return (np.uint64(ord("a")) + b % np.uint64(26)).astype(np.uint8)
+
+
+def _excl(cnt):
+    return np.concatenate([[0], np.cumsum(cnt)[:-1]]) if len(cnt) else np.zeros(0, np.int64)
+
+
+def _pad_raw(w):
+    """fill(Pad&): a = w & 0xFF, b = w >> 8, c = w >> 40, zero padding."""
+    m = len(w)
+    raw = np.zeros((m, 12), np.uint8)
+    raw[:, 0] = (w & np.uint64(0xFF)).astype(np.uint8)
+    raw[:, 4:8] = (w >> np.uint64(8)).astype(np.uint32)[:, None].view(np.uint8).reshape(m, 4)
+    raw[:, 8:10] = (w >> np.uint64(40)).astype(np.uint16)[:, None].view(np.uint8).reshape(m, 2)
+    return raw
 
 
 def make_batch(case: str, n: int, seed: int, param: int = 48):
@@ -188,6 +207,35 @@ def make_batch(case: str, n: int, seed: int, param: int = 48):
         with np.errstate(over="ignore"):
             vals = mix64(rnd(seed, rec, 2) + j)
         heaps.append(i32(vals).view(np.uint8))
+    elif case == "opt":  # fill(Opt&): optional members (types.hpp)
+        bits = rnd(seed, idx, 3)
+        recs["id"] = i32(rnd(seed, idx, 0))
+        has_s = (bits & np.uint64(1)).astype(np.int64)
+        recs["score.n"] = has_s
+        recs["score.off"] = _excl(has_s)
+        heaps.append(rd(rnd(seed, idx[has_s == 1], 60)).astype("<f8").view(np.uint8))
+        lens = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+        recs["tag.n"] = lens
+        recs["tag.off"] = _excl(lens)
+        heaps.append(_chars(seed, idx, lens))
+        has_p = ((bits >> np.uint64(1)) & np.uint64(1)).astype(np.int64)
+        recs["pad.n"] = has_p
+        recs["pad.off"] = _excl(has_p)
+        heaps.append(_pad_raw(rnd(seed, idx[has_p == 1], 0)).reshape(-1))
+    elif case == "optp":  # fill(OptP&)
+        bits = rnd(seed, idx, 3)
+        recs["k"] = rnd(seed, idx, 0).view(np.int64)
+        has_a = (bits & np.uint64(1)).astype(np.int64)
+        recs["a.n"] = has_a
+        recs["a.off"] = _excl(has_a)
+        heaps.append(i32(rnd(seed, idx[has_a == 1], 4)).view(np.uint8))
+        has_b = ((bits >> np.uint64(2)) & np.uint64(1)).astype(np.int64)
+        recs["b.n"] = has_b
+        recs["b.off"] = _excl(has_b)
+        sel = idx[has_b == 1]
+        pts = np.stack([rd(rnd(seed, sel, 5)), rd(rnd(seed, sel, 6))], 1) if len(sel) \
+            else np.zeros((0, 2))
+        heaps.append(pts.astype("<f8").view(np.uint8).reshape(-1))
     else:
         raise KeyError(case)
     return L, recs, heaps
