@@ -282,7 +282,8 @@ class codec {
     b.n = max_records;
     b.recs.resize(max_records * layout().rec_stride);
     for (uint32_t k = 0; k < n_spans(); ++k) {
-      b.heap_elems.push_back(len / span_elem(k) + 1);
+      // an OPTION holds at most one value per record, readable or not
+      b.heap_elems.push_back(span_is_option(k) ? max_records : len / span_elem(k) + 1);
       b.heaps.emplace_back(b.heap_elems.back() * span_elem(k));
     }
     return b;
@@ -290,13 +291,19 @@ class codec {
 
   static uint32_t n_spans() {
     uint32_t k = 0;
-    for (uint32_t i = 0; i < layout().n_ops; ++i) k += layout().ops[i].kind == SPK_OP_SPAN;
+    for (uint32_t i = 0; i < layout().n_ops; ++i) k += layout().ops[i].kind != SPK_OP_COPY;  // SPAN + OPTION: one heap each
     return k;
   }
   static uint32_t span_elem(uint32_t k) {
     for (uint32_t i = 0, s = 0; i < layout().n_ops; ++i)
-      if (layout().ops[i].kind == SPK_OP_SPAN && s++ == k) return layout().ops[i].size;
+      if (layout().ops[i].kind != SPK_OP_COPY && s++ == k) return layout().ops[i].size;
     return 1;
+  }
+  static bool span_is_option(uint32_t k) {
+    for (uint32_t i = 0, s = 0; i < layout().n_ops; ++i)
+      if (layout().ops[i].kind != SPK_OP_COPY && s++ == k)
+        return layout().ops[i].kind == SPK_OP_OPTION;
+    return false;
   }
   static std::size_t min_record_wire() {
     std::size_t m = 0;

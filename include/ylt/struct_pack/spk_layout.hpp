@@ -9,8 +9,9 @@
 //     packer.hpp:432-447): trivially serializable members become COPY ops at
 //     a C-like offset of the device record; std::string / std::vector<U>
 //     (U trivially serializable) become a SPAN op {u32 count; u64 element
-//     offset into that member's heap}. Nested non-trivial aggregates are
-//     flattened inline.
+//     offset into that member's heap}; std::optional<U> (U trivially
+//     serializable) an OPTION op with the same fields and a count of 0/1.
+//     Nested non-trivial aggregates are flattened inline.
 // This is the same flattening as yalantinglibs_amd/schema.py:flatten, so
 // Python and C++ front ends produce identical descriptors.
 #pragma once
@@ -44,11 +45,11 @@ struct layout_builder {
     if (L.n_ops >= SPK_MAX_OPS) throw std::length_error("struct_pack: too many members");
     L.ops[L.n_ops++] = spk_op{SPK_OP_COPY, o, size, 0};
   }
-  void span(uint32_t esz) {
+  void span(uint32_t esz, uint32_t kind = SPK_OP_SPAN) {
     const uint32_t c = place(4, 4), a = place(8, 8);
     if (L.n_ops >= SPK_MAX_OPS || spans >= SPK_MAX_SPANS)
       throw std::length_error("struct_pack: too many variable-length members");
-    L.ops[L.n_ops++] = spk_op{SPK_OP_SPAN, c, esz, a};
+    L.ops[L.n_ops++] = spk_op{kind, c, esz, a};
     ++spans;
   }
 };
@@ -65,6 +66,12 @@ void flatten_into(layout_builder &b) {
                   "MI355X codec: containers of non-trivially-serializable elements are "
                   "outside the flat record model");
     b.span(sizeof(E));
+  } else if constexpr (is_std_optional<T>::value) {
+    using E = remove_cvref_t<typename T::value_type>;
+    static_assert(is_trivially_serializable<E>(),
+                  "MI355X codec: optional of a non-trivially-serializable value is "
+                  "outside the flat record model");
+    b.span(sizeof(E), SPK_OP_OPTION);
   } else if constexpr (is_std_array<T>::value) {
     for (std::size_t i = 0; i < std::tuple_size_v<T>; ++i)
       flatten_into<typename T::value_type>(b);
@@ -162,6 +169,17 @@ void to_device(const T &v, marshal_state &s) {
     std::memcpy(s.rec + op.aux, &eoff, 8);
     const auto *p = reinterpret_cast<const uint8_t *>(v.data());
     heap.insert(heap.end(), p, p + static_cast<std::size_t>(cnt) * op.size);
+  } else if constexpr (is_std_optional<T>::value) {
+    const spk_op &op = s.L->ops[s.op++];
+    auto &heap = (*s.heaps)[s.span++];
+    const uint32_t cnt = v.has_value() ? 1u : 0u;
+    const uint64_t eoff = heap.size() / op.size;
+    std::memcpy(s.rec + op.rec_off, &cnt, 4);
+    std::memcpy(s.rec + op.aux, &eoff, 8);
+    if (cnt) {
+      const auto *p = reinterpret_cast<const uint8_t *>(&*v);
+      heap.insert(heap.end(), p, p + op.size);
+    }
   } else if constexpr (is_std_array<T>::value) {
     for (const auto &e : v) to_device(e, s);
   } else {
@@ -205,6 +223,19 @@ void from_device(T &v, unmarshal_state &s) {
     } else {
       v.resize(cnt);
       if (cnt) std::memcpy(v.data(), src, static_cast<std::size_t>(cnt) * op.size);
+    }
+  } else if constexpr (is_std_optional<T>::value) {
+    const spk_op &op = s.L->ops[s.op++];
+    const uint8_t *heap = s.heaps[s.span++];
+    uint32_t cnt;
+    uint64_t eoff;
+    std::memcpy(&cnt, s.rec + op.rec_off, 4);
+    std::memcpy(&eoff, s.rec + op.aux, 8);
+    if (cnt) {
+      v.emplace();
+      std::memcpy(static_cast<void *>(&*v), heap + eoff * op.size, op.size);
+    } else {
+      v.reset();
     }
   } else if constexpr (is_std_array<T>::value) {
     for (auto &e : v) from_device(e, s);

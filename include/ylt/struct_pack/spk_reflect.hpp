@@ -11,6 +11,7 @@
 #include <array>
 #include <cstddef>
 #include <cstdint>
+#include <optional>
 #include <span>
 #include <string>
 #include <string_view>
@@ -40,6 +41,8 @@ template <typename T> struct is_std_vector : std::false_type {};
 template <typename T, typename A> struct is_std_vector<std::vector<T, A>> : std::true_type {};
 template <typename T> struct is_std_span : std::false_type {};
 template <typename T, std::size_t E> struct is_std_span<std::span<T, E>> : std::bool_constant<E == std::dynamic_extent> {};
+template <typename T> struct is_std_optional : std::false_type {};
+template <typename T> struct is_std_optional<std::optional<T>> : std::true_type {};
 template <typename T> struct is_std_array : std::false_type {};
 template <typename T, std::size_t N> struct is_std_array<std::array<T, N>> : std::true_type {};
 
@@ -51,7 +54,8 @@ template <typename T>
 constexpr bool is_fundamental_v = std::is_arithmetic_v<T> || std::is_enum_v<T>;
 template <typename T>
 constexpr bool is_record_v = std::is_aggregate_v<T> && std::is_class_v<T> &&
-                             !is_std_array<T>::value && !is_string_v<T> && !is_container_v<T>;
+                             !is_std_array<T>::value && !is_string_v<T> && !is_container_v<T> &&
+                             !is_std_optional<T>::value;
 
 // ---- aggregate member count (brace-init probing) ----------------------------
 struct any_init {

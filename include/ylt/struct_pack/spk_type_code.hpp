@@ -31,7 +31,7 @@ enum : uint8_t {
   TID_INT32 = 1, TID_UINT32 = 2, TID_INT64 = 3, TID_UINT64 = 4, TID_INT8 = 5,
   TID_UINT8 = 6, TID_INT16 = 7, TID_UINT16 = 8, TID_BOOL = 11, TID_CHAR8 = 12,
   TID_CHAR16 = 13, TID_CHAR32 = 14, TID_FLOAT32 = 17, TID_FLOAT64 = 18,
-  TID_STRING = 128, TID_ARRAY = 129, TID_CONTAINER = 132, TID_STRUCT = 253,
+  TID_STRING = 128, TID_ARRAY = 129, TID_CONTAINER = 132, TID_OPTIONAL = 133, TID_STRUCT = 253,
   TID_END = 255
 };
 
@@ -85,8 +85,8 @@ constexpr bool is_trivially_serializable() {
     return true;
   } else if constexpr (is_std_array<T>::value) {
     return is_trivially_serializable<typename T::value_type>();
-  } else if constexpr (is_string_v<T> || is_container_v<T>) {
-    return false;
+  } else if constexpr (is_string_v<T> || is_container_v<T> || is_std_optional<T>::value) {
+    return false;  // reflection.hpp:899-901
   } else {
     static_assert(is_record_v<T>, "unsupported member type");
     using M = members_tuple_t<T>;
@@ -104,8 +104,8 @@ template <typename T>
 constexpr bool has_container() {
   if constexpr (is_string_v<T> || is_container_v<T>)
     return true;
-  else if constexpr (is_std_array<T>::value)
-    return has_container<typename T::value_type>();
+  else if constexpr (is_std_array<T>::value || is_std_optional<T>::value)
+    return has_container<typename T::value_type>();  // type_calculate.hpp:846-849
   else if constexpr (is_record_v<T>) {
     using M = members_tuple_t<T>;
     return any_container<M>(std::make_index_sequence<std::tuple_size_v<M>>{});
@@ -147,6 +147,9 @@ constexpr lit_t type_literal() {
     l.push(TID_CHAR8);
   } else if constexpr (is_container_v<T>) {
     l.push(TID_CONTAINER);
+    l.append(type_literal<remove_cvref_t<typename T::value_type>>());
+  } else if constexpr (is_std_optional<T>::value) {  // type_calculate.hpp:273-278
+    l.push(TID_OPTIONAL);
     l.append(type_literal<remove_cvref_t<typename T::value_type>>());
   } else if constexpr (is_std_array<T>::value) {
     l.push(TID_ARRAY);

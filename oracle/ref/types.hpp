@@ -133,6 +133,13 @@ struct resp_header {
 };
 }  // namespace rpcb
 
+// only optional members: no container, so no metainfo byte per message
+struct OptP {
+  int64_t k;
+  std::optional<int32_t> a;
+  std::optional<rpcb::point> b;
+};
+
 namespace spk_gold {
 
 inline Rec64 make_rec64(uint64_t seed, uint64_t i) {
@@ -218,13 +225,6 @@ inline void fill(Opt &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
     fill(*o.pad, seed, i, 0);
   }
 }
-
-// only optional members: no container, so no metainfo byte per message
-struct OptP {
-  int64_t k;
-  std::optional<int32_t> a;
-  std::optional<rpcb::point> b;
-};
 
 inline void fill(OptP &o, uint64_t seed, uint64_t i, uint32_t) {
   o.k = (int64_t)rnd(seed, i, 0);

@@ -38,14 +38,23 @@ bool operator==(const Rec64 &a, const Rec64 &b) { return std::memcmp(&a, &b, siz
 bool operator==(const RecS &a, const RecS &b) { return a.id == b.id && a.name == b.name && a.v == b.v; }
 bool operator==(const Inner &a, const Inner &b) { return a.x == b.x && a.y == b.y; }
 bool operator==(const Outer &a, const Outer &b) { return a.key == b.key && a.items == b.items; }
+bool operator==(const Pad &a, const Pad &b) { return a.a == b.a && a.b == b.b && a.c == b.c; }
+bool operator==(const Opt &a, const Opt &b) {
+  return a.id == b.id && a.score == b.score && a.tag == b.tag && a.pad == b.pad;
+}
 namespace rpcb {
+bool operator==(const point &a, const point &b) { return a.x == b.x && a.y == b.y; }
 bool operator==(const rect &a, const rect &b) { return std::memcmp(&a, &b, sizeof a) == 0; }
 bool operator==(const person &a, const person &b) {
   return a.id == b.id && a.name == b.name && a.age == b.age && a.salary == b.salary;
 }
 }  // namespace rpcb
+bool operator==(const OptP &a, const OptP &b) { return a.k == b.k && a.a == b.a && a.b == b.b; }
 
-template <typename T, typename Gen>
+// check_trunc: a record type whose last member may be an optional value is
+// exempt from the "one byte short -> no_buffer_space" check: the reference
+// drops the value read's errc (unpacker.hpp:1271-1273; errs.json pins it)
+template <typename T, typename Gen, bool check_trunc = true>
 static void roundtrip_vector(const char *fixture, std::size_t n, Gen gen) {
   std::vector<T> v(n);
   for (std::size_t i = 0; i < n; ++i) gen(v[i], i);
@@ -62,7 +71,7 @@ static void roundtrip_vector(const char *fixture, std::size_t n, Gen gen) {
   CHECK(consumed == want.size());
   CHECK(back == v);
   // truncation: the reference reports no_buffer_space (test_serialize.cpp:816-845)
-  if (want.size() > 5) {
+  if (check_trunc && want.size() > 5) {
     std::vector<T> t;
     auto e2 = deserialize_to(t, want.data(), want.size() - 1);
     CHECK(e2.ec == errc::no_buffer_space);
@@ -169,6 +178,17 @@ int main() {
                                  fid_of("echo_person"), 7,
                                  [&](rpcb::person &o, uint64_t i) { o = make_person(S8, i, 48); });
   CHECK(fid_of("array_1K_int") != 0);
+  // std::optional members (SPK_OP_OPTION)
+  const uint64_t SA = 0x5EED000A, SB = 0x5EED000B;
+  auto gen_opt = [&](uint32_t p) { return [=](Opt &o, uint64_t i) { fill(o, SA, i, p); }; };
+  auto gen_optp = [&](OptP &o, uint64_t i) { fill(o, SB, i, 0); };
+  roundtrip_vector<Opt, decltype(gen_opt(16)), false>("opt_A_n300_p16_default.bin", 300,
+                                                      gen_opt(16));
+  roundtrip_vector<OptP, decltype(gen_optp), false>("optp_A_n300_p0_default.bin", 300, gen_optp);
+  roundtrip_messages<Opt>("opt_B_n200_p300_default.bin", "opt_B_n200_p300_default.lens", 200,
+                          gen_opt(300));
+  roundtrip_messages<OptP>("optp_B_n200_p0_default.bin", "optp_B_n200_p0_default.lens", 200,
+                           gen_optp);
   std::printf("{\"checks\": %d, \"failures\": %d}\n", g_checks, g_fail);
   return g_fail ? 1 : 0;
 }

@@ -21,6 +21,10 @@ static_assert(get_type_code<std::vector<rect<int>>>() == 0xe8fa8a7cu);
 static_assert(spk_detail::is_trivially_serializable<Rec64>());
 static_assert(!spk_detail::is_trivially_serializable<RecS>());
 static_assert(spk_detail::members_count_v<Mixed> == 5);
+static_assert(spk_detail::members_count_v<Opt> == 4);
+static_assert(get_type_code<Opt>() == 3223865924u);   // kat.json "Opt"
+static_assert(get_type_code<OptP>() == 3947683952u);  // kat.json "OptP"
+static_assert(!spk_detail::has_container<OptP>());
 
 template <typename T>
 static void lit_json(const char *name, bool &first) {
@@ -73,6 +77,11 @@ int main() {
   lit_json<rpcb::req_header>("req_header", first);
   lit_json<rpcb::resp_header>("resp_header", first);
   lit_json<std::array<int16_t, 3>>("array<int16_t,3>", first);
+  lit_json<Opt>("Opt", first);
+  lit_json<std::vector<Opt>>("vector<Opt>", first);
+  lit_json<OptP>("OptP", first);
+  lit_json<std::vector<OptP>>("vector<OptP>", first);
+  lit_json<std::optional<int32_t>>("optional<int32_t>", first);
   printf("},\n\"layout\": {\n");
   first = true;
   layout_json<Rec64>("rec64", first);
@@ -84,6 +93,8 @@ int main() {
   layout_json<rpcb::rect>("rpcrect", first);
   layout_json<rpcb::person>("person", first);
   layout_json<std::vector<int32_t>>("ints", first);
+  layout_json<Opt>("opt", first);
+  layout_json<OptP>("optp", first);
   layout_json<RecS, sp_config::ENABLE_TYPE_INFO>("recs_typeinfo", first);
   layout_json<Rec64, sp_config::DISABLE_ALL_META_INFO>("rec64_nometa", first);
   printf("}}\n");

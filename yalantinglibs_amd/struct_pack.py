@@ -198,7 +198,9 @@ class Codec:
         min_rec = max(1, sum(op[2] for op in self.L.dev.ops if op[0] == C.SPK_OP_COPY) +
                       len(self.L.dev.spans))
         cap = (wl // min_rec + 1) if mode == MODE_VECTOR else n_msgs
-        elems = [wl // sp.elem.size + 1 for sp in self.L.dev.spans]
+        # an OPTION holds at most one value per record, readable or not
+        opt = [op[0] == C.SPK_OP_OPTION for op in self.L.dev.ops if op[0] != C.SPK_OP_COPY]
+        elems = [cap if o else wl // sp.elem.size + 1 for o, sp in zip(opt, self.L.dev.spans)]
         out = self.alloc_batch(cap, elems)
         ec = (torch.zeros(max(n_msgs, 1), dtype=torch.int32, device=self.device)
               if mode == MODE_MESSAGES else None)
