@@ -38,6 +38,17 @@
  *                                           unpacker.hpp:1251-1275). It is not
  *                                           a container: it never sets the
  *                                           width (calculate_size.hpp:100-105).
+ *   SPK_OP_VARINT {rec_off, size, aux}     a struct_pack::var_uint32_t /
+ *                                           var_uint64_t (aux 0) or var_int32_t /
+ *                                           var_int64_t (aux SPK_VARINT_ZIGZAG)
+ *                                           held as a plain `size`-byte (4/8)
+ *                                           integer at rec_off. Wire: LEB128 of
+ *                                           the value (zigzag-mapped first for
+ *                                           the signed types), 1-10 bytes
+ *                                           (varint.hpp:245-330). Decode: a
+ *                                           10th byte with its high bit set is
+ *                                           invalid_buffer; a truncated varint
+ *                                           is no_buffer_space. Not a container.
  * A trivially-serializable T (SPK_LAYOUT_TRIVIAL) is a single COPY of the
  * whole record (reference packer.hpp:418-421, unpacker.hpp:1300-1312).
  *
@@ -93,6 +104,11 @@ extern "C" {
 #define SPK_OP_COPY 1u
 #define SPK_OP_SPAN 2u
 #define SPK_OP_OPTION 3u
+#define SPK_OP_VARINT 4u
+
+/* spk_op.aux of an SPK_OP_VARINT */
+#define SPK_VARINT_ZIGZAG 0x1u /* var_int32_t / var_int64_t (sint<T>): zigzag */
+#define SPK_MAX_VARINTS 16u    /* varint members per record                  */
 
 #define SPK_MODE_VECTOR 0
 #define SPK_MODE_MESSAGES 1
@@ -107,7 +123,7 @@ extern "C" {
 #define SPK_LAYOUT_TRIVIAL 0x1u   /* is_trivial_serializable<T>: 1 COPY op  */
 
 typedef struct spk_op {
-  uint32_t kind;    /* SPK_OP_COPY | SPK_OP_SPAN | SPK_OP_OPTION             */
+  uint32_t kind;    /* SPK_OP_COPY | SPK_OP_SPAN | SPK_OP_OPTION | VARINT    */
   uint32_t rec_off; /* COPY: source byte offset; SPAN: u32 count offset      */
   uint32_t size;    /* COPY: byte length;       SPAN: element size (bytes)   */
   uint32_t aux;     /* SPAN: u64 heap element-offset field offset; COPY: 0   */

@@ -89,6 +89,12 @@ static int cmd_kat() {
   kat_one<OptP>(os, "OptP", first);
   kat_one<std::vector<OptP>>(os, "vector<OptP>", first);
   kat_one<std::optional<int32_t>>(os, "optional<int32_t>", first);
+  kat_one<Var>(os, "Var", first);
+  kat_one<std::vector<Var>>(os, "vector<Var>", first);
+  kat_one<VarP>(os, "VarP", first);
+  kat_one<std::vector<VarP>>(os, "vector<VarP>", first);
+  kat_one<struct_pack::var_int32_t, struct_pack::var_int64_t, struct_pack::var_uint32_t,
+          struct_pack::var_uint64_t>(os, "varints", first);
   kat_one<std::array<int16_t, 3>>(os, "array<int16_t,3>", first);
   kat_one<std::vector<std::string>>(os, "vector<string>", first);
   kat_one<uint8_t, uint16_t, uint32_t, uint64_t, int8_t, int16_t, int64_t,
@@ -161,6 +167,10 @@ static bool with_case(const Args &a, F &&f) {
     return f.template operator()<Opt>([=](Opt &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "optp")
     return f.template operator()<OptP>([=](OptP &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "var")
+    return f.template operator()<Var>([=](Var &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "varp")
+    return f.template operator()<VarP>([=](VarP &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "rect")  // C1: benchmark rect<int> default values
     return f.template operator()<rect<int>>([=](rect<int> &o, uint64_t) { o = rect<int>{}; });
   if (k == "rpcrect")

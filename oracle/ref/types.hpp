@@ -18,6 +18,23 @@
 #include <string>
 #include <vector>
 
+// ---- varint members: LEB128, zigzag for var_int* --
+struct Var {  // a varint first: no count field to screen candidates on
+  struct_pack::var_int32_t a;
+  std::string s;
+  struct_pack::var_uint64_t b;
+  double d;
+  struct_pack::var_int64_t c;
+  struct_pack::var_uint32_t e;
+};
+
+// varints and fixed members only: no container, no span
+struct VarP {
+  int32_t id;
+  struct_pack::var_int64_t x;
+  struct_pack::var_uint32_t y;
+};
+
 namespace spk_gold {
 
 inline uint64_t mix64(uint64_t z) {
@@ -231,6 +248,30 @@ inline void fill(OptP &o, uint64_t seed, uint64_t i, uint32_t) {
   const uint64_t bits = rnd(seed, i, 3);
   if (bits & 1) o.a = (int32_t)(uint32_t)rnd(seed, i, 4);
   if (bits & 4) o.b = rpcb::point{rd(rnd(seed, i, 5)), rd(rnd(seed, i, 6))};
+}
+
+// magnitudes from 0 to 64 bits, so every LEB128 length 1..10 occurs
+inline uint64_t spread(uint64_t w) { return w >> ((w >> 58) & 63); }
+
+inline void fill(Var &v, uint64_t seed, uint64_t i, uint32_t maxlen) {
+  const uint64_t r0 = rnd(seed, i, 0), r3 = rnd(seed, i, 3), r4 = rnd(seed, i, 4),
+                 r5 = rnd(seed, i, 5);
+  const uint32_t a = (uint32_t)spread(r0);
+  v.a = (int32_t)((r0 & 1) ? ~a : a);
+  v.s = make_chars(seed, i, maxlen);
+  v.b = spread(r3);
+  v.d = rd(rnd(seed, i, 60));
+  const uint64_t c = spread(r4);
+  v.c = (int64_t)((r4 & 1) ? ~c : c);
+  v.e = (uint32_t)spread(r5);
+}
+
+inline void fill(VarP &v, uint64_t seed, uint64_t i, uint32_t) {
+  const uint64_t r0 = rnd(seed, i, 0), r1 = rnd(seed, i, 1), r2 = rnd(seed, i, 2);
+  v.id = (int32_t)(uint32_t)r0;
+  const uint64_t x = spread(r1);
+  v.x = (int64_t)((r1 & 1) ? ~x : x);
+  v.y = (uint32_t)spread(r2);
 }
 
 inline rpcb::rect make_rpc_rect(uint64_t seed, uint64_t i) {

@@ -20,6 +20,39 @@ static uint64_t get_le(const uint8_t *p, unsigned w) {
   return v;
 }
 
+/* ---- varints: struct_pack/varint.hpp ------------------------------------ */
+/* the unsigned value serialize_varint puts on the wire (varint.hpp:245-268):
+ * sint<T> is zigzag-mapped at its own width (encode_zigzag, :194-210),
+ * varint<T> is the value itself */
+static uint64_t vi_value(const uint8_t *rec, const spk_op *op) {
+  if (op->size == 4) {
+    uint32_t u;
+    memcpy(&u, rec + op->rec_off, 4);
+    if (op->aux & SPK_VARINT_ZIGZAG) u = (u << 1) ^ (uint32_t)(-(int32_t)(u >> 31));
+    return u;
+  }
+  uint64_t u;
+  memcpy(&u, rec + op->rec_off, 8);
+  if (op->aux & SPK_VARINT_ZIGZAG) u = (u << 1) ^ (uint64_t)(-(int64_t)(u >> 63));
+  return u;
+}
+/* calculate_varint_size (varint.hpp:212-239) */
+static unsigned vi_len(uint64_t v) {
+  unsigned n = 1;
+  while (v >= 0x80) {
+    v >>= 7;
+    ++n;
+  }
+  return n;
+}
+/* deserialize_varint (varint.hpp:270-330): LEB128 of at most 10 bytes; the
+ * value is truncated to the member width, zigzag-decoded at 64 bits first
+ * for the signed types */
+static void vi_store(uint8_t *rec, const spk_op *op, uint64_t v) {
+  if (op->aux & SPK_VARINT_ZIGZAG) v = (v >> 1) ^ (uint64_t)(-(int64_t)(v & 1));
+  put_le(rec + op->rec_off, v, op->size);
+}
+
 /* ---- layout helpers ---------------------------------------------------- */
 static unsigned n_spans(const spk_layout *L) {
   unsigned k = 0;
@@ -99,6 +132,8 @@ static uint64_t rec_wire_size(const spk_layout *L, const uint8_t *rec,
     const spk_op *op = &L->ops[i];
     if (op->kind == SPK_OP_COPY)
       s += op->size;
+    else if (op->kind == SPK_OP_VARINT)
+      s += vi_len(vi_value(rec, op));
     else
       s += op_pw(op, w) + rec_count(rec, op) * op->size;
   }
@@ -128,6 +163,14 @@ static uint8_t *write_record(const spk_layout *L, const uint8_t *rec,
     if (op->kind == SPK_OP_COPY) { /* write_wrapper<sizeof(T)> :264-267 */
       memcpy(p, rec + op->rec_off, op->size);
       p += op->size;
+    }
+    else if (op->kind == SPK_OP_VARINT) { /* serialize_varint :245-268 */
+      uint64_t v = vi_value(rec, op);
+      while (v >= 0x80) {
+        *p++ = (uint8_t)(v | 0x80u);
+        v >>= 7;
+      }
+      *p++ = (uint8_t)v;
     }
     else { /* container: low_bytes_write_wrapper<w> + memcpy (:304-363);
               optional: bool has_value + the value (:382-388) */
@@ -314,6 +357,18 @@ static int32_t read_record(dctx_t *c, rd_t *r, unsigned w, uint8_t *rec) {
     if (op->kind == SPK_OP_COPY) {
       if (!rd_take(r, op->size, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
       if (rec) memcpy(rec + op->rec_off, p, op->size);
+      continue;
+    }
+    if (op->kind == SPK_OP_VARINT) { /* deserialize_varint_impl :270-292 */
+      uint64_t v = 0;
+      int i = 0;
+      for (; i < 10; ++i) {
+        if (!rd_take(r, 1, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
+        v |= (uint64_t)(p[0] & 0x7fu) << (i * 7);
+        if (!(p[0] & 0x80u)) break;
+      }
+      if (i == 10) return SPK_ERRC_INVALID_BUFFER;
+      if (rec) vi_store(rec, op, v);
       continue;
     }
     /* container length :905-979; optional: read_wrapper<sizeof(bool)>, any

@@ -29,7 +29,8 @@ GEN = os.path.join(ROOT, "oracle", "_ref", "golden_gen")
 
 SEED = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004,
         "pad": 0x5EED0005, "mixed": 0x5EED0006, "rect": 0, "rpcrect": 0x5EED0007,
-        "person": 0x5EED0008, "ints": 0x5EED0009, "opt": 0x5EED000A, "optp": 0x5EED000B}
+        "person": 0x5EED0008, "ints": 0x5EED0009, "opt": 0x5EED000A, "optp": 0x5EED000B,
+        "var": 0x5EED000C, "varp": 0x5EED000D}
 
 # (case_mode, n, param, conf, keep_bin)
 SMALL = [
@@ -63,6 +64,12 @@ SMALL = [
     ("opt_A", 100, 48, "typeinfo"), ("opt_B", 200, 300, "default"),
     ("optp_A", 300, 0, "default"), ("optp_B", 200, 0, "default"),
     ("optp_B", 50, 0, "typeinfo"), ("optp_A", 20, 0, "nometa"),
+    ("var_A", 0, 16, "default"), ("var_A", 1, 16, "default"),
+    ("var_A", 300, 16, "default"), ("var_A", 40, 400, "default"),
+    ("var_A", 100, 48, "typeinfo"), ("var_B", 200, 300, "default"),
+    ("var_A", 3000, 8, "default"), ("var_A", 50, 8, "nometa"),
+    ("varp_A", 300, 0, "default"), ("varp_B", 200, 0, "default"),
+    ("varp_B", 50, 0, "typeinfo"), ("varp_A", 20, 0, "nometa"),
 ]
 MEDIUM = [  # digest only (wire > ~1 MB)
     ("rec64_A", 65535, 0, "default"), ("rec64_A", 65536, 0, "default"),
@@ -72,6 +79,8 @@ MEDIUM = [  # digest only (wire > ~1 MB)
     ("ints_B", 3, 70000, "default"), ("ints_B", 20, 70000, "default"),
     ("opt_A", 70000, 48, "default"), ("optp_A", 70000, 0, "default"),
     ("opt_B", 70000, 48, "default"),
+    ("var_A", 70000, 48, "default"), ("varp_A", 70000, 0, "default"),
+    ("var_B", 70000, 48, "default"),
 ]
 BIG = [  # BASELINE.json full-size configs (digest only)
     ("rec64_A", 100_000_000, 0, "default"),
@@ -181,6 +190,7 @@ ERR_BASES = [
     ("rec64_A", 300, 0, "default"), ("recs_B", 1, 300, "default"),
     ("rec64_B", 1, 0, "default"), ("mixed_A", 3, 300, "default"),
     ("opt_A", 6, 10, "default"), ("optp_B", 1, 0, "default"), ("opt_B", 1, 20, "default"),
+    ("var_A", 6, 10, "default"), ("varp_B", 1, 0, "default"), ("varp_A", 4, 0, "default"),
 ]
 
 
@@ -212,6 +222,12 @@ def make_errs(tmp):
         with open(wire, "rb") as f:
             base = f.read()
         muts = mutations(len(base), rng)
+        if case in ("var", "varp"):  # overlong / 10-byte / unterminated varints
+            for p0 in range(0, min(len(base), 48), 3):
+                run = " ".join(f"set {p0 + j} 255" for j in range(10))
+                muts.append(run)
+                muts.append(" ".join(f"set {p0 + j} 255" for j in range(9)) + f" set {p0 + 9} 1")
+                muts.append(run + f" trunc {p0 + 6}")
         mfile = os.path.join(tmp, "muts.txt")
         with open(mfile, "w") as f:
             f.write("\n".join(muts) + "\n")

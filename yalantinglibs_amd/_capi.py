@@ -35,6 +35,9 @@ ERRC_CAPACITY = 100
 SPK_OP_COPY = 1
 SPK_OP_SPAN = 2
 SPK_OP_OPTION = 3
+SPK_OP_VARINT = 4
+SPK_VARINT_ZIGZAG = 1
+SPK_MAX_VARINTS = 16
 SPK_MODE_VECTOR = 0
 SPK_MODE_MESSAGES = 1
 

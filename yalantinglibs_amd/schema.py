@@ -34,6 +34,7 @@ TID_INT32, TID_UINT32, TID_INT64, TID_UINT64 = 1, 2, 3, 4
 TID_INT8, TID_UINT8, TID_INT16, TID_UINT16 = 5, 6, 7, 8
 TID_BOOL, TID_CHAR8 = 11, 12
 TID_FLOAT32, TID_FLOAT64 = 17, 18
+TID_VINT32, TID_VINT64, TID_VUINT32, TID_VUINT64 = 20, 21, 22, 23
 TID_STRING, TID_ARRAY, TID_MAP, TID_SET, TID_CONTAINER = 128, 129, 130, 131, 132
 TID_OPTIONAL, TID_VARIANT = 133, 134
 TID_MONOSTATE = 250
@@ -115,6 +116,29 @@ boolean = Fund("bool", TID_BOOL, 1, "<u1")
 char = Fund("char", TID_CHAR8, 1, "<u1")
 float32 = Fund("float", TID_FLOAT32, 4, "<f4")
 float64 = Fund("double", TID_FLOAT64, 8, "<f8")
+
+
+class VarInt(SpType):
+    """struct_pack::var_int32_t / var_int64_t (sint<T>, zigzag) and
+    var_uint32_t / var_uint64_t (varint<T>) (ref varint.hpp:352-355): held
+    as a plain integer in the device record, LEB128 on the wire. Not
+    trivially serializable (reflection.hpp:872), so a struct holding one is
+    written member by member."""
+
+    def __init__(self, name: str, tid: int, size: int, npdt: str, zigzag: bool):
+        self.name, self.tid, self.size, self.npdt = name, tid, size, npdt
+        self.align = size
+        self.zigzag = zigzag
+        self.config = DEFAULT
+
+    def literal(self):
+        return bytes([self.tid])
+
+
+var_int32 = VarInt("var_int32_t", TID_VINT32, 4, "<i4", True)
+var_int64 = VarInt("var_int64_t", TID_VINT64, 8, "<i8", True)
+var_uint32 = VarInt("var_uint32_t", TID_VUINT32, 4, "<u4", False)
+var_uint64 = VarInt("var_uint64_t", TID_VUINT64, 8, "<u8", False)
 
 
 class Monostate(SpType):
@@ -383,6 +407,11 @@ def flatten(rtype: SpType) -> DeviceLayout:
             spans.append(SpanField(path, t.elem, coff, ooff))
             npf.append((path + ".n", "<u4", coff))
             npf.append((path + ".off", "<u8", ooff))
+        elif isinstance(t, VarInt):
+            off = place(t.size, t.size)
+            ops.append((C.SPK_OP_VARINT, off, t.size,
+                        C.SPK_VARINT_ZIGZAG if t.zigzag else 0))
+            npf.append((path, t.npdt, off))
         elif isinstance(t, Struct):
             for fname, ft in t.fields:
                 visit(ft, f"{path}.{fname}" if path else fname)
@@ -395,6 +424,8 @@ def flatten(rtype: SpType) -> DeviceLayout:
     visit(rtype, "" if isinstance(rtype, Struct) else "value")
     if len(spans) > C.SPK_MAX_SPANS:
         raise NotImplementedError("too many variable-length members")
+    if sum(op[0] == C.SPK_OP_VARINT for op in ops) > C.SPK_MAX_VARINTS:
+        raise NotImplementedError("too many varint members")
     # merge COPY runs contiguous in the record (always contiguous on the wire)
     merged: List[Tuple[int, int, int, int]] = []
     for op in ops:

@@ -82,9 +82,14 @@ Opt = S.Struct("Opt", [("id", S.int32), ("score", S.Optional(S.float64)),
 OptP = S.Struct("OptP", [("k", S.int64), ("a", S.Optional(S.int32)),
                          ("b", S.Optional(Point))])
 
+Var = S.Struct("Var", [("a", S.var_int32), ("s", S.String()), ("b", S.var_uint64),
+                       ("d", S.float64), ("c", S.var_int64), ("e", S.var_uint32)])
+VarP = S.Struct("VarP", [("id", S.int32), ("x", S.var_int64), ("y", S.var_uint32)])
+
 CASE_TYPES = {"rec64": Rec64, "recs": RecS, "outer": Outer, "pad": Pad,
               "mixed": Mixed, "rect": RectInt, "rpcrect": RpcRect,
-              "person": Person, "ints": Ints, "opt": Opt, "optp": OptP}
+              "person": Person, "ints": Ints, "opt": Opt, "optp": OptP,
+              "var": Var, "varp": VarP}
 # vector<rect<int>> has its own ADL set_sp_config (benchmark data_def.hpp:69-72)
 VECTOR_CONFIG = {"rect": S.DISABLE_ALL_META_INFO}
 
@@ -236,6 +241,32 @@ def make_batch(case: str, n: int, seed: int, param: int = 48):
         pts = np.stack([rd(rnd(seed, sel, 5)), rd(rnd(seed, sel, 6))], 1) if len(sel) \
             else np.zeros((0, 2))
         heaps.append(pts.astype("<f8").view(np.uint8).reshape(-1))
+    elif case == "var":  # fill(Var&): varint members (types.hpp)
+        r0 = rnd(seed, idx, 0)
+        a = _spread(r0) & np.uint64(0xFFFFFFFF)
+        a = np.where(r0 & np.uint64(1), ~a & np.uint64(0xFFFFFFFF), a)
+        recs["a"] = a.astype(np.uint32).view(np.int32)
+        lens = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+        recs["s.n"] = lens
+        recs["s.off"] = _excl(lens)
+        heaps.append(_chars(seed, idx, lens))
+        recs["b"] = _spread(rnd(seed, idx, 3))
+        recs["d"] = rd(rnd(seed, idx, 60))
+        r4 = rnd(seed, idx, 4)
+        c = _spread(r4)
+        recs["c"] = np.where(r4 & np.uint64(1), ~c, c).view(np.int64)
+        recs["e"] = (_spread(rnd(seed, idx, 5)) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    elif case == "varp":  # fill(VarP&)
+        recs["id"] = i32(rnd(seed, idx, 0))
+        r1 = rnd(seed, idx, 1)
+        x = _spread(r1)
+        recs["x"] = np.where(r1 & np.uint64(1), ~x, x).view(np.int64)
+        recs["y"] = (_spread(rnd(seed, idx, 2)) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
     else:
         raise KeyError(case)
     return L, recs, heaps
+
+
+def _spread(w):
+    """spread() of types.hpp: magnitudes from 0 to 64 bits."""
+    return w >> ((w >> np.uint64(58)) & np.uint64(63))
