@@ -291,17 +291,21 @@ class codec {
 
   static uint32_t n_spans() {
     uint32_t k = 0;
-    for (uint32_t i = 0; i < layout().n_ops; ++i) k += layout().ops[i].kind != SPK_OP_COPY;  // SPAN + OPTION: one heap each
+    for (uint32_t i = 0; i < layout().n_ops; ++i) k += has_heap(layout().ops[i]);
     return k;
+  }
+  // SPAN + OPTION members: one heap each (COPY and VARINT live in the record)
+  static bool has_heap(const spk_op &o) {
+    return o.kind == SPK_OP_SPAN || o.kind == SPK_OP_OPTION;
   }
   static uint32_t span_elem(uint32_t k) {
     for (uint32_t i = 0, s = 0; i < layout().n_ops; ++i)
-      if (layout().ops[i].kind != SPK_OP_COPY && s++ == k) return layout().ops[i].size;
+      if (has_heap(layout().ops[i]) && s++ == k) return layout().ops[i].size;
     return 1;
   }
   static bool span_is_option(uint32_t k) {
     for (uint32_t i = 0, s = 0; i < layout().n_ops; ++i)
-      if (layout().ops[i].kind != SPK_OP_COPY && s++ == k)
+      if (has_heap(layout().ops[i]) && s++ == k)
         return layout().ops[i].kind == SPK_OP_OPTION;
     return false;
   }

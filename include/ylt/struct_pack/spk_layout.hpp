@@ -27,7 +27,7 @@ namespace spk_detail {
 
 struct layout_builder {
   spk_layout L{};
-  uint32_t off = 0, align = 1, spans = 0;
+  uint32_t off = 0, align = 1, spans = 0, vars = 0;
   uint32_t place(uint32_t size, uint32_t al) {
     off = (off + al - 1) / al * al;
     const uint32_t o = off;
@@ -45,6 +45,12 @@ struct layout_builder {
     if (L.n_ops >= SPK_MAX_OPS) throw std::length_error("struct_pack: too many members");
     L.ops[L.n_ops++] = spk_op{SPK_OP_COPY, o, size, 0};
   }
+  void varint(uint32_t size, uint32_t zigzag) {
+    const uint32_t o = place(size, size);
+    if (L.n_ops >= SPK_MAX_OPS || ++vars > SPK_MAX_VARINTS)
+      throw std::length_error("struct_pack: too many varint members");
+    L.ops[L.n_ops++] = spk_op{SPK_OP_VARINT, o, size, zigzag ? SPK_VARINT_ZIGZAG : 0u};
+  }
   void span(uint32_t esz, uint32_t kind = SPK_OP_SPAN) {
     const uint32_t c = place(4, 4), a = place(8, 8);
     if (L.n_ops >= SPK_MAX_OPS || spans >= SPK_MAX_SPANS)
@@ -58,6 +64,8 @@ template <typename T>
 void flatten_into(layout_builder &b) {
   if constexpr (is_trivially_serializable<T>()) {
     b.copy(sizeof(T), alignof(T));
+  } else if constexpr (is_varint<T>::value) {
+    b.varint(sizeof(typename T::value_type), T::zigzag);
   } else if constexpr (is_string_v<T>) {
     b.span(1);
   } else if constexpr (is_container_v<T>) {
@@ -160,6 +168,9 @@ template <typename T>
 void to_device(const T &v, marshal_state &s) {
   if constexpr (is_trivially_serializable<T>()) {
     put_copy(s, &v, sizeof(T));
+  } else if constexpr (is_varint<T>::value) {
+    const spk_op &op = s.L->ops[s.op++];
+    std::memcpy(s.rec + op.rec_off, &v.get(), op.size);
   } else if constexpr (is_string_v<T> || is_container_v<T>) {
     const spk_op &op = s.L->ops[s.op++];
     auto &heap = (*s.heaps)[s.span++];
@@ -209,6 +220,9 @@ template <typename T>
 void from_device(T &v, unmarshal_state &s) {
   if constexpr (is_trivially_serializable<T>()) {
     get_copy(s, &v, sizeof(T));
+  } else if constexpr (is_varint<T>::value) {
+    const spk_op &op = s.L->ops[s.op++];
+    std::memcpy(&v.get(), s.rec + op.rec_off, op.size);
   } else if constexpr (is_string_v<T> || is_container_v<T>) {
     const spk_op &op = s.L->ops[s.op++];
     const uint8_t *heap = s.heaps[s.span++];

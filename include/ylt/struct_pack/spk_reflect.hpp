@@ -34,6 +34,41 @@ enum sp_config : uint64_t {
 
 namespace spk_detail {
 
+// var_int32_t / var_int64_t (zigzag) and var_uint32_t / var_uint64_t: an
+// integer wrapper with the reference's interface (varint.hpp:79-185,352-355)
+template <typename T, bool ZigZag>
+class varint_value {
+ public:
+  using value_type = T;
+  static constexpr bool zigzag = ZigZag;
+  varint_value() noexcept = default;
+  varint_value(T t) noexcept : val(t) {}
+  [[nodiscard]] operator T() const noexcept { return val; }
+  varint_value &operator=(T t) noexcept {
+    val = t;
+    return *this;
+  }
+  [[nodiscard]] bool operator==(const varint_value &o) const noexcept { return val == o.val; }
+  [[nodiscard]] bool operator==(T t) const noexcept { return val == t; }
+  [[nodiscard]] bool operator<(const varint_value &o) const noexcept { return val < o.val; }
+  const T &get() const noexcept { return val; }
+  T &get() noexcept { return val; }
+
+ private:
+  T val{};
+};
+template <typename T> struct is_varint : std::false_type {};
+template <typename T, bool Z> struct is_varint<varint_value<T, Z>> : std::true_type {};
+
+}  // namespace spk_detail
+
+using var_int32_t = spk_detail::varint_value<int32_t, true>;
+using var_int64_t = spk_detail::varint_value<int64_t, true>;
+using var_uint32_t = spk_detail::varint_value<uint32_t, false>;
+using var_uint64_t = spk_detail::varint_value<uint64_t, false>;
+
+namespace spk_detail {
+
 template <typename T>
 using remove_cvref_t = std::remove_cv_t<std::remove_reference_t<T>>;
 
@@ -55,7 +90,7 @@ constexpr bool is_fundamental_v = std::is_arithmetic_v<T> || std::is_enum_v<T>;
 template <typename T>
 constexpr bool is_record_v = std::is_aggregate_v<T> && std::is_class_v<T> &&
                              !is_std_array<T>::value && !is_string_v<T> && !is_container_v<T> &&
-                             !is_std_optional<T>::value;
+                             !is_std_optional<T>::value && !is_varint<T>::value;
 
 // ---- aggregate member count (brace-init probing) ----------------------------
 struct any_init {

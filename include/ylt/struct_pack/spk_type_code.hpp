@@ -31,6 +31,7 @@ enum : uint8_t {
   TID_INT32 = 1, TID_UINT32 = 2, TID_INT64 = 3, TID_UINT64 = 4, TID_INT8 = 5,
   TID_UINT8 = 6, TID_INT16 = 7, TID_UINT16 = 8, TID_BOOL = 11, TID_CHAR8 = 12,
   TID_CHAR16 = 13, TID_CHAR32 = 14, TID_FLOAT32 = 17, TID_FLOAT64 = 18,
+  TID_VINT32 = 20, TID_VINT64 = 21, TID_VUINT32 = 22, TID_VUINT64 = 23,
   TID_STRING = 128, TID_ARRAY = 129, TID_CONTAINER = 132, TID_OPTIONAL = 133, TID_STRUCT = 253,
   TID_END = 255
 };
@@ -85,8 +86,9 @@ constexpr bool is_trivially_serializable() {
     return true;
   } else if constexpr (is_std_array<T>::value) {
     return is_trivially_serializable<typename T::value_type>();
-  } else if constexpr (is_string_v<T> || is_container_v<T> || is_std_optional<T>::value) {
-    return false;  // reflection.hpp:899-901
+  } else if constexpr (is_string_v<T> || is_container_v<T> || is_std_optional<T>::value ||
+                       is_varint<T>::value) {
+    return false;  // reflection.hpp:872,899-901
   } else {
     static_assert(is_record_v<T>, "unsupported member type");
     using M = members_tuple_t<T>;
@@ -148,6 +150,10 @@ constexpr lit_t type_literal() {
   } else if constexpr (is_container_v<T>) {
     l.push(TID_CONTAINER);
     l.append(type_literal<remove_cvref_t<typename T::value_type>>());
+  } else if constexpr (is_varint<T>::value) {  // get_varint_type (type_id.hpp:84-125)
+    using V = typename T::value_type;
+    l.push(sizeof(V) == 4 ? (T::zigzag ? TID_VINT32 : TID_VUINT32)
+                          : (T::zigzag ? TID_VINT64 : TID_VUINT64));
   } else if constexpr (is_std_optional<T>::value) {  // type_calculate.hpp:273-278
     l.push(TID_OPTIONAL);
     l.append(type_literal<remove_cvref_t<typename T::value_type>>());

@@ -50,6 +50,10 @@ bool operator==(const person &a, const person &b) {
 }
 }  // namespace rpcb
 bool operator==(const OptP &a, const OptP &b) { return a.k == b.k && a.a == b.a && a.b == b.b; }
+bool operator==(const Var &a, const Var &b) {
+  return a.a == b.a && a.s == b.s && a.b == b.b && a.d == b.d && a.c == b.c && a.e == b.e;
+}
+bool operator==(const VarP &a, const VarP &b) { return a.id == b.id && a.x == b.x && a.y == b.y; }
 
 // check_trunc: a record type whose last member may be an optional value is
 // exempt from the "one byte short -> no_buffer_space" check: the reference
@@ -189,6 +193,16 @@ int main() {
                           gen_opt(300));
   roundtrip_messages<OptP>("optp_B_n200_p0_default.bin", "optp_B_n200_p0_default.lens", 200,
                            gen_optp);
+  // varint members (SPK_OP_VARINT)
+  const uint64_t SC = 0x5EED000C, SD = 0x5EED000D;
+  auto gen_var = [&](uint32_t p) { return [=](Var &o, uint64_t i) { fill(o, SC, i, p); }; };
+  auto gen_varp = [&](VarP &o, uint64_t i) { fill(o, SD, i, 0); };
+  roundtrip_vector<Var>("var_A_n300_p16_default.bin", 300, gen_var(16));
+  roundtrip_vector<VarP>("varp_A_n300_p0_default.bin", 300, gen_varp);
+  roundtrip_messages<Var>("var_B_n200_p300_default.bin", "var_B_n200_p300_default.lens", 200,
+                          gen_var(300));
+  roundtrip_messages<VarP>("varp_B_n200_p0_default.bin", "varp_B_n200_p0_default.lens", 200,
+                           gen_varp);
   std::printf("{\"checks\": %d, \"failures\": %d}\n", g_checks, g_fail);
   return g_fail ? 1 : 0;
 }

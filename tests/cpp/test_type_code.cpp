@@ -25,6 +25,10 @@ static_assert(spk_detail::members_count_v<Opt> == 4);
 static_assert(get_type_code<Opt>() == 3223865924u);   // kat.json "Opt"
 static_assert(get_type_code<OptP>() == 3947683952u);  // kat.json "OptP"
 static_assert(!spk_detail::has_container<OptP>());
+static_assert(get_type_code<Var>() == 3170970548u);    // kat.json "Var"
+static_assert(get_type_code<VarP>() == 2257901056u);  // kat.json "VarP"
+static_assert(!spk_detail::is_trivially_serializable<VarP>());
+static_assert(!spk_detail::has_container<VarP>());
 
 template <typename T>
 static void lit_json(const char *name, bool &first) {
@@ -82,6 +86,10 @@ int main() {
   lit_json<OptP>("OptP", first);
   lit_json<std::vector<OptP>>("vector<OptP>", first);
   lit_json<std::optional<int32_t>>("optional<int32_t>", first);
+  lit_json<Var>("Var", first);
+  lit_json<std::vector<Var>>("vector<Var>", first);
+  lit_json<VarP>("VarP", first);
+  lit_json<std::vector<VarP>>("vector<VarP>", first);
   printf("},\n\"layout\": {\n");
   first = true;
   layout_json<Rec64>("rec64", first);
@@ -95,6 +103,8 @@ int main() {
   layout_json<std::vector<int32_t>>("ints", first);
   layout_json<Opt>("opt", first);
   layout_json<OptP>("optp", first);
+  layout_json<Var>("var", first);
+  layout_json<VarP>("varp", first);
   layout_json<RecS, sp_config::ENABLE_TYPE_INFO>("recs_typeinfo", first);
   layout_json<Rec64, sp_config::DISABLE_ALL_META_INFO>("rec64_nometa", first);
   printf("}}\n");

@@ -167,7 +167,8 @@ def test_error_parity(base):
 RANDOM = [("recs", 1, 300), ("recs", 257, 5), ("recs", 5000, 48), ("recs", 20000, 200),
           ("outer", 3000, 16), ("outer", 500, 300), ("mixed", 700, 70), ("person", 999, 30),
           ("pad", 12345, 0), ("rec64", 4099, 0), ("rpcrect", 77, 0), ("ints", 400, 100),
-          ("opt", 5000, 48), ("opt", 300, 400), ("optp", 20000, 0)]
+          ("opt", 5000, 48), ("opt", 300, 400), ("optp", 20000, 0),
+          ("var", 5000, 48), ("var", 300, 400), ("var", 20000, 4), ("varp", 20000, 0)]
 
 
 @pytest.mark.parametrize("case,n,param", RANDOM)
@@ -223,7 +224,8 @@ def _irregular_messages(cd, case, n, seed, param):
 @pytest.mark.parametrize("case,n,param", [("rec64", 1000, 0), ("pad", 777, 0),
                                           ("rpcrect", 300, 0), ("person", 500, 40),
                                           ("ints", 200, 60), ("opt", 500, 40),
-                                          ("optp", 400, 0)])
+                                          ("optp", 400, 0), ("var", 500, 40),
+                                          ("varp", 400, 0)])
 @pytest.mark.parametrize("cap_frac", [1.0, 0.6])
 def test_messages_irregular_vs_oracle(case, n, param, cap_frac):
     """Mode B decode of non-canonical message batches: per-message errc,

@@ -42,7 +42,7 @@ int spk_layout_check(const spk_layout *L) {
     if (L->fmt_one.flags & SPK_MF_HAS_CONTAINER) return SPK_E_LAYOUT;
     return SPK_OK;
   }
-  uint32_t spans = 0, conts = 0;
+  uint32_t spans = 0, conts = 0, vars = 0;
   for (uint32_t i = 0; i < L->n_ops; ++i) {
     const spk_op &o = L->ops[i];
     if (o.kind == SPK_OP_COPY) {
@@ -53,11 +53,19 @@ int spk_layout_check(const spk_layout *L) {
         return SPK_E_LAYOUT;
       ++spans;
       conts += o.kind == SPK_OP_SPAN;
+    } else if (o.kind == SPK_OP_VARINT) {  // var_(u)int32_t / var_(u)int64_t member
+      if ((o.size != 4 && o.size != 8) || o.rec_off % o.size || o.rec_off + o.size > L->rec_stride ||
+          (o.aux & ~SPK_VARINT_ZIGZAG))
+        return SPK_E_LAYOUT;
+      ++vars;
     } else {
       return SPK_E_LAYOUT;
     }
   }
-  if (spans == 0 || spans > SPK_MAX_SPANS || L->rec_stride % 8) return SPK_E_LAYOUT;
+  // a non-trivial record has a variable-length member: a span/option or a varint
+  if ((spans == 0 && vars == 0) || spans > SPK_MAX_SPANS || vars > SPK_MAX_VARINTS ||
+      L->rec_stride % 8)
+    return SPK_E_LAYOUT;
   // check_if_has_container<T>: a container member (an optional alone is none)
   if (!(L->fmt_one.flags & SPK_MF_HAS_CONTAINER) != !conts) return SPK_E_LAYOUT;
   return SPK_OK;
@@ -119,8 +127,9 @@ static int encode_impl(const spk_layout *L, int mode, uint64_t n, const void *d_
   }
   if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
   uint32_t spans = 0;
-  for (uint32_t i = 0; i < L->n_ops; ++i) spans += L->ops[i].kind != SPK_OP_COPY;
-  if (!d_heaps) return SPK_E_ARG;
+  for (uint32_t i = 0; i < L->n_ops; ++i)
+    spans += L->ops[i].kind == SPK_OP_SPAN || L->ops[i].kind == SPK_OP_OPTION;
+  if (!d_heaps && spans) return SPK_E_ARG;
   for (uint32_t k = 0; k < spans; ++k)
     if (!d_heaps[k] && n) return SPK_E_ARG;
   return hip_rc(launch_var_encode(L, mode, n, d_recs, d_heaps, d_plan, d_out, out_cap,
@@ -169,7 +178,10 @@ static int decode_impl(const spk_layout *L, int mode, const void *d_wire, uint64
                                                s));
   }
   if (d_recs && (uintptr_t)d_recs % 8) return SPK_E_ARG;
-  if (!d_heaps || !heap_caps) return SPK_E_ARG;
+  uint32_t spans = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i)
+    spans += L->ops[i].kind == SPK_OP_SPAN || L->ops[i].kind == SPK_OP_OPTION;
+  if (spans && (!d_heaps || !heap_caps)) return SPK_E_ARG;
   if (mode == SPK_MODE_MESSAGES && n_msgs && !d_msg_offsets) return SPK_E_ARG;
   return hip_rc(launch_var_decode(L, mode, d_wire, wire_len, d_msg_offsets, n_msgs, prefix,
                                   d_recs, rec_cap, d_heaps, heap_caps, d_res, d_errc, d_ws,

@@ -25,6 +25,8 @@ struct KLayout {
   uint32_t n_spans;      // SPAN + OPTION members (one heap each)
   uint32_t fixed_bytes;  // sum of COPY sizes + one has_value byte per OPTION
   uint32_t n_cont;       // SPAN members: the ones with a width-w count
+  uint32_t n_var;        // VARINT members (LEB128, 1-10 wire bytes each)
+  uint32_t pad_;
   spk_op ops[SPK_MAX_OPS];
 };
 

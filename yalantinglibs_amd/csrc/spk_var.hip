@@ -68,6 +68,8 @@ static KLayout make_klayout(const spk_layout *L) {
     k.ops[i] = L->ops[i];
     if (L->ops[i].kind == SPK_OP_COPY) {
       k.fixed_bytes += L->ops[i].size;
+    } else if (L->ops[i].kind == SPK_OP_VARINT) {
+      ++k.n_var;
     } else {
       ++k.n_spans;
       if (L->ops[i].kind == SPK_OP_SPAN)
@@ -137,6 +139,57 @@ __device__ __forceinline__ uint64_t opt_nb(const spk_op &op, uint64_t c, uint64_
   return (op.kind == SPK_OP_OPTION && nb > end - pos) ? 0 : nb;
 }
 
+// ---- varint members (struct_pack/varint.hpp) ---------------------------------
+// The unsigned value serialize_varint writes (varint.hpp:245-268): sint<T>
+// (var_int32_t / var_int64_t) is zigzag-mapped at its own width
+// (encode_zigzag :194-210), varint<T> is the value itself.
+__device__ __forceinline__ uint64_t vi_value(const spk_op &op, const uint8_t *rec) {
+  if (op.size == 4) {
+    uint32_t u = rec_u32(rec, op.rec_off);
+    if (op.aux & SPK_VARINT_ZIGZAG) u = (u << 1) ^ (uint32_t)(-(int32_t)(u >> 31));
+    return u;
+  }
+  uint64_t u = rec_u64(rec, op.rec_off);
+  if (op.aux & SPK_VARINT_ZIGZAG) u = (u << 1) ^ (uint64_t)(-(int64_t)(u >> 63));
+  return u;
+}
+// LEB128 byte count, calculate_varint_size (varint.hpp:212-239)
+__device__ __forceinline__ uint32_t vi_len(uint64_t v) {
+  return (70u - (uint32_t)__builtin_clzll(v | 1)) / 7u;
+}
+constexpr uint32_t kViBad = 0xFFu;
+// deserialize_varint_impl (varint.hpp:270-292) at pos (message end len):
+// the byte count, 0 when truncated (no_buffer_space), kViBad after ten bytes
+// that all carry the continuation bit (invalid_buffer)
+template <typename ByteFn>
+__device__ __forceinline__ uint32_t vi_read(ByteFn byte, uint64_t pos, uint64_t len,
+                                            uint64_t *v) {
+  uint64_t x = 0;
+  for (uint32_t i = 0; i < 10; ++i) {
+    if (pos + i >= len) return 0;
+    const uint32_t b = byte(pos + i);
+    x |= (uint64_t)(b & 0x7fu) << (7 * i);
+    if (!(b & 0x80u)) {
+      *v = x;
+      return i + 1;
+    }
+  }
+  return kViBad;
+}
+// the decoded value truncated to the member (deserialize_varint :294-330:
+// zigzag decoded at 64 bits for the signed types)
+__device__ __forceinline__ void vi_store(const spk_op &op, uint8_t *rec, uint64_t v) {
+  if (op.aux & SPK_VARINT_ZIGZAG) v = (v >> 1) ^ (uint64_t)(-(int64_t)(v & 1));
+  if (op.size == 4)
+    *reinterpret_cast<uint32_t *>(rec + op.rec_off) = (uint32_t)v;
+  else
+    *reinterpret_cast<uint64_t *>(rec + op.rec_off) = v;
+}
+struct WireBytes {
+  const uint8_t *wire;
+  __device__ __forceinline__ uint32_t operator()(uint64_t x) const { return wire[x]; }
+};
+
 // w-independent bytes of one record (fixed + span payloads) and its max count
 __device__ __forceinline__ void rec_sizes(const KLayout &L, const uint8_t *rec,
                                           uint64_t &var, uint64_t &maxc) {
@@ -150,6 +203,8 @@ __device__ __forceinline__ void rec_sizes(const KLayout &L, const uint8_t *rec,
       maxc = c > maxc ? c : maxc;
     } else if (op.kind == SPK_OP_OPTION) {
       var += op_rec_count(op, rec) * op.size;  // not a container: no width
+    } else if (op.kind == SPK_OP_VARINT) {
+      var += vi_len(vi_value(op, rec));
     }
   }
 }
@@ -376,6 +431,15 @@ __device__ __forceinline__ void win_record(const VarArgs &a, const uint8_t *rec,
     if (op.kind == SPK_OP_COPY) {
       win_put(W, pos, rec + op.rec_off, op.size);
       pos += op.size;
+    } else if (op.kind == SPK_OP_VARINT) {  // serialize_varint (varint.hpp:245-268)
+      uint64_t v = vi_value(op, rec);
+      for (;;) {
+        const uint8_t b = (uint8_t)(v >= 0x80 ? (v | 0x80u) : v);
+        if (pos >= W.lo && pos < W.hi) W.lds[pos - W.lo] = b;
+        ++pos;
+        if (v < 0x80) break;
+        v >>= 7;
+      }
     } else {
       const uint64_t c = op_rec_count(op, rec);
       const uint32_t pw = op_pw(op, w);
@@ -556,7 +620,7 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
     if (i < a.n) {
       const uint8_t *rec = recs + i * a.L.stride;
       for (uint32_t o = 0; o < a.L.n_ops; ++o)
-        if (a.L.ops[o].kind != SPK_OP_COPY &&
+        if ((a.L.ops[o].kind == SPK_OP_SPAN || a.L.ops[o].kind == SPK_OP_OPTION) &&
             op_rec_count(a.L.ops[o], rec) * a.L.ops[o].size >= kBigBytes)
           ++nbig;
     }
@@ -573,6 +637,10 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
         const spk_op op = a.L.ops[o];
         if (op.kind == SPK_OP_COPY) {
           q += op.size;
+          continue;
+        }
+        if (op.kind == SPK_OP_VARINT) {
+          q += vi_len(vi_value(op, rec));
           continue;
         }
         const uint64_t nb = op_rec_count(op, rec) * op.size;
@@ -634,14 +702,22 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
 
 // Size of the record starting at `pos` (absolute), reading counts from
 // `wire` (length len). Returns 0 if the record does not fit (incomplete).
+// A bad varint sets *ec to invalid_buffer (otherwise a 0 is no_buffer_space).
 __device__ __forceinline__ uint64_t rec_wire_len(const KLayout &L, const uint8_t *wire,
-                                                 uint64_t len, uint64_t pos, uint32_t w) {
+                                                 uint64_t len, uint64_t pos, uint32_t w,
+                                                 int32_t *ec = nullptr) {
   const uint64_t p0 = pos;
   for (uint32_t o = 0; o < L.n_ops; ++o) {
     const spk_op op = L.ops[o];
     if (op.kind == SPK_OP_COPY) {
       pos += op.size;
       if (pos > len) return 0;
+    } else if (op.kind == SPK_OP_VARINT) {
+      uint64_t v;
+      const uint32_t l = vi_read(WireBytes{wire}, pos, len, &v);
+      if (l == kViBad && ec) *ec = SPK_ERRC_INVALID_BUFFER;
+      if (!l || l == kViBad) return 0;
+      pos += l;
     } else {
       const uint32_t pw = op_pw(op, w);
       if (pos + pw > len) return 0;
@@ -672,6 +748,10 @@ __device__ void decode_record(const KLayout &L, const uint8_t *wire, uint64_t po
     if (op.kind == SPK_OP_COPY) {
       copy_bytes(rec + op.rec_off, wire + pos, op.size);
       pos += op.size;
+    } else if (op.kind == SPK_OP_VARINT) {
+      uint64_t v = 0;
+      pos += vi_read(WireBytes{wire}, pos, end, &v);
+      vi_store(op, rec, v);
     } else {
       const uint64_t c = op.kind == SPK_OP_OPTION ? (uint64_t)(wire[pos] != 0) : ld_le(wire + pos, w);
       pos += op_pw(op, w);
@@ -698,6 +778,9 @@ __device__ __forceinline__ void rec_counts(const KLayout &L, const uint8_t *wire
     const spk_op op = L.ops[o];
     if (op.kind == SPK_OP_COPY) {
       pos += op.size;
+    } else if (op.kind == SPK_OP_VARINT) {
+      uint64_t v;
+      pos += vi_read(WireBytes{wire}, pos, end, &v);
     } else {
       const uint64_t c = op.kind == SPK_OP_OPTION ? (uint64_t)(wire[pos] != 0) : ld_le(wire + pos, w);
       cnt[sk++] = c;
@@ -756,9 +839,10 @@ __global__ __launch_bounds__(kThreads) void var_msg_parse(
       uint32_t w;
       s.errc = parse_hdr(a.fmt, wire + b, e - b, &pos, &w, &dl);
       if (!s.errc) {
-        const uint64_t rl = rec_wire_len(a.L, wire + b, e - b, pos, w);
+        int32_t ec = SPK_ERRC_NO_BUFFER_SPACE;
+        const uint64_t rl = rec_wire_len(a.L, wire + b, e - b, pos, w, &ec);
         if (!rl) {
-          s.errc = SPK_ERRC_NO_BUFFER_SPACE;
+          s.errc = ec;
         } else {
           if (i >= a.rec_cap) s.errc = SPK_ERRC_CAPACITY;
           s.pos = b + pos;
@@ -868,7 +952,7 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
   if (live) {
     uint32_t sk = 0;
     for (uint32_t o = 0; o < a.L.n_ops; ++o)
-      if (a.L.ops[o].kind != SPK_OP_COPY) {  // OPTION values: never listed
+      if (a.L.ops[o].kind == SPK_OP_SPAN || a.L.ops[o].kind == SPK_OP_OPTION) {  // OPTION values: never listed
         if (a.L.ops[o].kind == SPK_OP_SPAN && cnt[sk] * a.L.ops[o].size >= kBigBytes) ++nbig;
         ++sk;
       }
@@ -882,6 +966,11 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
       const spk_op op = a.L.ops[o];
       if (op.kind == SPK_OP_COPY) {
         pos += op.size;
+        continue;
+      }
+      if (op.kind == SPK_OP_VARINT) {
+        uint64_t v;
+        pos += vi_read(WireBytes{wire}, pos, end, &v);
         continue;
       }
       pos += op_pw(op, s.w);
@@ -974,25 +1063,41 @@ struct WalkProg {
   uint32_t c0max;                  // largest first count of a plausible record
   uint64_t cmax[SPK_MAX_SPANS];    // largest count whose byte size fits 64 bits
   uint32_t optm;                   // bit k: span k is an OPTION ([has_value:1][U?])
+  uint32_t pf_all;                 // no first-count screening of candidate starts
+  uint32_t nv;                     // varint members
+  uint8_t vfirst[SPK_MAX_SPANS + 2];  // segment k's varints: [vfirst[k], vfirst[k+1])
+  uint32_t vafter[SPK_MAX_VARINTS];   // fixed bytes after varint j (same segment)
 };
 
 static WalkProg make_walkprog(const spk_layout *L) {
   WalkProg p = {};
   uint32_t k = 0;
+  // segment k (before span k; the last one after every span) = skip[k] fixed
+  // bytes, then per varint j of the segment: [LEB128][vafter[j] fixed bytes]
   for (uint32_t i = 0; i < L->n_ops; ++i) {
     if (L->ops[i].kind == SPK_OP_COPY) {
-      p.skip[k] += L->ops[i].size;
+      if (p.nv > p.vfirst[k])
+        p.vafter[p.nv - 1] += L->ops[i].size;
+      else
+        p.skip[k] += L->ops[i].size;
+    } else if (L->ops[i].kind == SPK_OP_VARINT) {
+      ++p.nv;
     } else {
       p.esz[k] = L->ops[i].size;
       if (L->ops[i].kind == SPK_OP_OPTION) p.optm |= 1u << k;
       ++k;
+      p.vfirst[k] = (uint8_t)p.nv;
     }
   }
   p.ns = k;
+  for (uint32_t j = k + 1; j < SPK_MAX_SPANS + 2; ++j) p.vfirst[j] = (uint8_t)p.nv;
   for (uint32_t j = 0; j < k; ++j) p.cmax[j] = ~0ull / (p.esz[j] ? p.esz[j] : 1);
   p.c0max = k ? (kPlaus > p.skip[0] ? (kPlaus - p.skip[0]) / (p.esz[0] ? p.esz[0] : 1) : 0) : 0;
   // an OPTION's has_value byte is not a w-byte count: no screening on it
   if (p.optm & 1u) p.c0max = 0xFFFFFFFFu;
+  // a varint before the first count (or no count at all): the first count's
+  // position is data-dependent, so every byte may start a record
+  p.pf_all = (p.optm & 1u) || p.vfirst[1] > 0 || k == 0;
   return p;
 }
 
@@ -1007,6 +1112,20 @@ __device__ __forceinline__ uint64_t wire_le(const uint8_t *wire, uint64_t x, uin
   }
 }
 
+// the varints of segment k at p (advanced past them and their fixed bytes);
+// false when one is truncated or overlong
+template <typename ByteFn>
+__device__ __forceinline__ bool vi_seg(const WalkProg &P, uint32_t k, ByteFn byte,
+                                       uint64_t len, uint64_t &p) {
+  for (uint32_t j = P.vfirst[k]; j < P.vfirst[k + 1]; ++j) {
+    uint64_t v;
+    const uint32_t l = vi_read(byte, p, len, &v);
+    if (!l || l == kViBad) return false;
+    p += l + P.vafter[j];
+  }
+  return true;
+}
+
 // Wire length of the record at `pos` (0 = incomplete: the reference fails it
 // with no_buffer_space). NS > 0: compile-time span count.
 template <int NS>
@@ -1014,6 +1133,7 @@ __device__ __forceinline__ uint64_t wlen(const WalkProg &P, const uint8_t *wire,
                                          uint64_t pos, uint32_t w) {
   uint64_t p = pos + P.skip[0];
   const uint32_t ns = NS > 0 ? (uint32_t)NS : P.ns;
+  if (!vi_seg(P, 0, WireBytes{wire}, len, p)) return 0;
 #pragma unroll
   for (uint32_t k = 0; k < (NS > 0 ? (uint32_t)NS : SPK_MAX_SPANS); ++k) {
     if (NS == 0 && k >= ns) break;
@@ -1032,6 +1152,7 @@ __device__ __forceinline__ uint64_t wlen(const WalkProg &P, const uint8_t *wire,
       }
     }
     p += P.skip[k + 1];
+    if (!vi_seg(P, k + 1, WireBytes{wire}, len, p)) return 0;
   }
   if (p > len) return 0;
   return p - pos;
@@ -1043,6 +1164,8 @@ __device__ __forceinline__ uint64_t wlen_rd(const WalkProg &P, const Rd &rd, uin
                                             uint64_t pos, uint32_t w, uint64_t *cnt = nullptr) {
   uint64_t p = pos + P.skip[0];
   const uint32_t ns = NS > 0 ? (uint32_t)NS : P.ns;
+  auto byte = [&rd](uint64_t x) { return rd.byte(x); };
+  if (!vi_seg(P, 0, byte, len, p)) return 0;
 #pragma unroll
   for (uint32_t k = 0; k < (NS > 0 ? (uint32_t)NS : SPK_MAX_SPANS); ++k) {
     if (NS == 0 && k >= ns) break;
@@ -1062,6 +1185,7 @@ __device__ __forceinline__ uint64_t wlen_rd(const WalkProg &P, const Rd &rd, uin
     }
     if (cnt) cnt[k] = c;
     p += P.skip[k + 1];
+    if (!vi_seg(P, k + 1, byte, len, p)) return 0;
   }
   if (p > len) return 0;
   return p - pos;
@@ -1091,10 +1215,11 @@ __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
       n = ld_le(wire + pos, w);
     pos += w;
   }
-  if (!e && n) {
+  if (!e && n && !a.L.n_var) {
     // every record needs at least fixed + n_spans*w bytes: a payload that
     // cannot hold n of them fails in the reference's record loop with
-    // no_buffer_space (unpacker.hpp:1208-1226)
+    // no_buffer_space (unpacker.hpp:1208-1226). Not with varints: an
+    // overlong one before the payload runs out is invalid_buffer.
     const uint64_t min_rec = a.L.fixed_bytes + (uint64_t)a.L.n_cont * w;
     const uint64_t payload = a.wire_len - pos;
     if (n > payload / (min_rec ? min_rec : 1)) e = SPK_ERRC_NO_BUFFER_SPACE;
@@ -1378,7 +1503,7 @@ __global__ __launch_bounds__(64 * kSpecWaves) void vec_spec(DecArgs a, WalkProg 
           m |= (cv <= P.c0max ? 1u : 0u) << k;
         }
       }
-      if (P.optm & 1u) m = 0xFFu;  // first span is an OPTION: every byte may start a record
+      if (P.pf_all) m = 0xFFu;  // first span an OPTION / varint first: any byte may start a record
       const uint64_t rem = ce - (cs + t);  // candidates must start in the chunk
       if (rem < 8) m &= (1u << rem) - 1u;
       if (!m) {
@@ -1671,6 +1796,43 @@ __global__ void vec_finish(DecArgs a, uint8_t *__restrict__ ws, spk_dresult_t *r
   *res = r;
 }
 
+// Layouts with varints: the true path can also end on an overlong varint,
+// which the reference reports as invalid_buffer (varint.hpp:290-291), not
+// no_buffer_space. One lane finds the chunk of the last complete record
+// (binary search over the record bases), re-walks to the failing record
+// and classifies it.
+template <int NS>
+__global__ void vec_vi_errc(DecArgs a, WalkProg P, const uint8_t *__restrict__ wire,
+                            const uint8_t *__restrict__ ws, VecBufs B, spk_dresult_t *res) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
+  if (c->errc || res->errc != SPK_ERRC_NO_BUFFER_SPACE) return;
+  const uint64_t total = c->total;  // complete records on the true path (< n)
+  uint64_t pos = c->p0;
+  if (total) {
+    // the chunk holding record total-1: the last with base <= total-1
+    const uint64_t r = total - 1;
+    uint64_t lo = 0, hi = c->nchunks - 1;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi + 1) / 2;
+      if (B.base[mid] <= r) lo = mid; else hi = mid - 1;
+    }
+    const uint64_t ch = lo;
+    const uint32_t mj = B.mj[ch], k0 = mj >> 16, j0 = mj & 0xFFFFu;
+    const uint64_t cs = c->p0 + ch * kSpec;
+    const uint16_t *Pl = B.P + ch * c->lp;
+    pos = B.T[ch];
+    for (uint64_t q = 0; q <= r - B.base[ch]; ++q) {
+      if (q >= k0) pos = cs + Pl[j0 + (q - k0)];
+      pos += wlen<NS>(P, wire, a.wire_len, pos, c->w);
+    }
+  }
+  if (pos >= a.wire_len) return;
+  int32_t ec = SPK_ERRC_NO_BUFFER_SPACE;
+  rec_wire_len(a.L, wire, a.wire_len, pos, c->w, &ec);
+  if (ec == SPK_ERRC_INVALID_BUFFER) res->errc = ec;
+}
+
 // decode_record with piecewise copies; off[k] = heap element offset of span k
 __device__ __forceinline__ void emit_record(const KLayout &L, const uint8_t *wire, uint64_t pos,
                                             uint32_t w, uint8_t *rec, uint8_t *const *heaps,
@@ -1681,6 +1843,10 @@ __device__ __forceinline__ void emit_record(const KLayout &L, const uint8_t *wir
     if (op.kind == SPK_OP_COPY) {
       copy_bytes(rec + op.rec_off, wire + pos, op.size);
       pos += op.size;
+    } else if (op.kind == SPK_OP_VARINT) {
+      uint64_t v = 0;
+      pos += vi_read(WireBytes{wire}, pos, end, &v);
+      vi_store(op, rec, v);
     } else {
       const uint64_t cnt = op.kind == SPK_OP_OPTION ? (uint64_t)(wire[pos] != 0) : wire_le(wire, pos, w);
       pos += op_pw(op, w);
@@ -1811,7 +1977,9 @@ static VecWs vec_ws_layout(const spk_layout *L, uint64_t wire_len, uint64_t rec_
   v.nch = wire_len / kSpec + 2;
   uint32_t min_rec = 0, ns = 0;
   for (uint32_t i = 0; i < L->n_ops; ++i) {
-    if (L->ops[i].kind == SPK_OP_COPY) min_rec += L->ops[i].size; else { ++min_rec; ++ns; }
+    if (L->ops[i].kind == SPK_OP_COPY) min_rec += L->ops[i].size;
+    else if (L->ops[i].kind == SPK_OP_VARINT) ++min_rec;
+    else { ++min_rec; ++ns; }
   }
   if (!min_rec) min_rec = 1;
   v.lp = kSpec / min_rec + 2;
@@ -1910,6 +2078,9 @@ static hipError_t launch_vec_decode_ns(const DecArgs &a, const WalkProg &P, cons
   hipLaunchKernelGGL(vec_total<NS>, dim3(cg), dim3(256), 0, s, a, P, wire, ws, B, tot + 1);
   hipLaunchKernelGGL(vec_finish, dim3(1), dim3(64), 0, s, a, ws, d_res,
                      (const uint64_t *)(tot + 1));
+  if (P.nv)
+    hipLaunchKernelGGL(vec_vi_errc<NS>, dim3(1), dim3(64), 0, s, a, P, wire,
+                       (const uint8_t *)ws, B, d_res);
   uint32_t G = kEmitRecs / v.lp;
   if (G > 64) G = 64;
   if (G < 1) G = 1;

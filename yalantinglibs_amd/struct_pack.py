@@ -195,11 +195,11 @@ class Codec:
         """Allocating decode: capacities bounded by the wire length.
         Returns (result, RecordBatch, errc tensor or None)."""
         wl = wire.numel()
-        min_rec = max(1, sum(op[2] for op in self.L.dev.ops if op[0] == C.SPK_OP_COPY) +
-                      len(self.L.dev.spans))
+        min_rec = max(1, sum(op[2] if op[0] == C.SPK_OP_COPY else 1 for op in self.L.dev.ops))
         cap = (wl // min_rec + 1) if mode == MODE_VECTOR else n_msgs
         # an OPTION holds at most one value per record, readable or not
-        opt = [op[0] == C.SPK_OP_OPTION for op in self.L.dev.ops if op[0] != C.SPK_OP_COPY]
+        opt = [op[0] == C.SPK_OP_OPTION for op in self.L.dev.ops
+               if op[0] in (C.SPK_OP_SPAN, C.SPK_OP_OPTION)]
         elems = [cap if o else wl // sp.elem.size + 1 for o, sp in zip(opt, self.L.dev.spans)]
         out = self.alloc_batch(cap, elems)
         ec = (torch.zeros(max(n_msgs, 1), dtype=torch.int32, device=self.device)
