@@ -1127,16 +1127,17 @@ __device__ __forceinline__ bool vi_seg(const WalkProg &P, uint32_t k, ByteFn byt
 }
 
 // Wire length of the record at `pos` (0 = incomplete: the reference fails it
-// with no_buffer_space). NS > 0: compile-time span count.
+// with no_buffer_space). NS > 0: compile-time span count; 0: runtime count;
+// -1: runtime count and the record has varints.
 template <int NS>
 __device__ __forceinline__ uint64_t wlen(const WalkProg &P, const uint8_t *wire, uint64_t len,
                                          uint64_t pos, uint32_t w) {
   uint64_t p = pos + P.skip[0];
   const uint32_t ns = NS > 0 ? (uint32_t)NS : P.ns;
-  if (!vi_seg(P, 0, WireBytes{wire}, len, p)) return 0;
+  if (NS < 0 && !vi_seg(P, 0, WireBytes{wire}, len, p)) return 0;
 #pragma unroll
   for (uint32_t k = 0; k < (NS > 0 ? (uint32_t)NS : SPK_MAX_SPANS); ++k) {
-    if (NS == 0 && k >= ns) break;
+    if (NS <= 0 && k >= ns) break;
     const bool opt = (P.optm >> k) & 1u;
     const uint32_t pw = opt ? 1u : w;
     if (p + pw > len) return 0;
@@ -1152,7 +1153,7 @@ __device__ __forceinline__ uint64_t wlen(const WalkProg &P, const uint8_t *wire,
       }
     }
     p += P.skip[k + 1];
-    if (!vi_seg(P, k + 1, WireBytes{wire}, len, p)) return 0;
+    if (NS < 0 && !vi_seg(P, k + 1, WireBytes{wire}, len, p)) return 0;
   }
   if (p > len) return 0;
   return p - pos;
@@ -1165,10 +1166,10 @@ __device__ __forceinline__ uint64_t wlen_rd(const WalkProg &P, const Rd &rd, uin
   uint64_t p = pos + P.skip[0];
   const uint32_t ns = NS > 0 ? (uint32_t)NS : P.ns;
   auto byte = [&rd](uint64_t x) { return rd.byte(x); };
-  if (!vi_seg(P, 0, byte, len, p)) return 0;
+  if (NS < 0 && !vi_seg(P, 0, byte, len, p)) return 0;
 #pragma unroll
   for (uint32_t k = 0; k < (NS > 0 ? (uint32_t)NS : SPK_MAX_SPANS); ++k) {
-    if (NS == 0 && k >= ns) break;
+    if (NS <= 0 && k >= ns) break;
     const bool opt = (P.optm >> k) & 1u;
     const uint32_t pw = opt ? 1u : w;
     if (p + pw > len) return 0;
@@ -1185,7 +1186,7 @@ __device__ __forceinline__ uint64_t wlen_rd(const WalkProg &P, const Rd &rd, uin
     }
     if (cnt) cnt[k] = c;
     p += P.skip[k + 1];
-    if (!vi_seg(P, k + 1, byte, len, p)) return 0;
+    if (NS < 0 && !vi_seg(P, k + 1, byte, len, p)) return 0;
   }
   if (p > len) return 0;
   return p - pos;
@@ -2232,6 +2233,9 @@ hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
   const WalkProg P = make_walkprog(L);
   (void)e;
   (void)ws_bytes;
+  // NS = -1: the walkers read varints (kept out of the other instantiations:
+  // the inlined LEB128 loops cost registers in the hot walks)
+  if (P.nv) return launch_vec_decode_ns<-1>(a, P, wire, ws, v, d_res, (uint8_t *)d_recs, s);
   if (P.ns == 1) return launch_vec_decode_ns<1>(a, P, wire, ws, v, d_res, (uint8_t *)d_recs, s);
   if (P.ns == 2) return launch_vec_decode_ns<2>(a, P, wire, ws, v, d_res, (uint8_t *)d_recs, s);
   return launch_vec_decode_ns<0>(a, P, wire, ws, v, d_res, (uint8_t *)d_recs, s);
