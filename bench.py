@@ -35,12 +35,16 @@ CONFIGS = {
            "C3: 10M RecS{int32, std::string len U[0,48], double} per GPU, one vector message"),
     "c4": ("outer", 10_000_000, 16, "A",
            "C4: 10M Outer{int64, vector<Inner{int32,float}> n U[0,16]} per GPU, one vector message"),
+    "cv": ("var", 10_000_000, 16, "A",
+           "varint records: 10M Var{var_int32_t, std::string len U[0,16], var_uint64_t, double, "
+           "var_int64_t, var_uint32_t} per GPU (LEB128 lengths 1-10 B), one vector message"),
 }
 # kernel the roofline object describes, per config (rocprof name prefix, for
 # the PMC traffic lookup in profiles/r01/pmc_<config>.json)
 DOMINANT = {"c2": "spk::shift_copy_kernel", "c2b": "void spk::fixed_msg_encode_lds<true>",
-            "c3": "spk::var_encode_write", "c4": "spk::var_encode_write"}
-SEEDS = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004}
+            "c3": "spk::var_encode_write", "c4": "spk::var_encode_write",
+            "cv": "spk::var_encode_write"}
+SEEDS = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004, "var": 0x5EED000C}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -66,7 +70,8 @@ def cpu_baseline(case, param):
     if not os.path.exists(exe):
         return None
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    n = {"rec64": 20_000_000, "recs": 4_000_000, "outer": 4_000_000, "c5": 600_000}[case]
+    n = {"rec64": 20_000_000, "recs": 4_000_000, "outer": 4_000_000, "c5": 600_000,
+         "var": 4_000_000}[case]
     out = {}
     for t in sorted({1, threads}):
         r = subprocess.run([exe, case, str(n), str(SEEDS.get(case, 0)), str(param), str(t), "10"],
@@ -110,7 +115,17 @@ def main():
     mode = SP.MODE_VECTOR if modech == "A" else SP.MODE_MESSAGES
     cd = SP.Codec(LY.case_layout(case), device=dev)
     # this rank's shard: global records [rank*n, (rank+1)*n)
-    batch = SP.synth_batch(cd, case, n, SEEDS[case], param, first=rank * n)
+    if case in ("rec64", "recs", "outer"):
+        batch = SP.synth_batch(cd, case, n, SEEDS[case], param, first=rank * n)
+    else:  # host generator (yalantinglibs_amd/synth.py), uploaded before timing;
+        # every rank gets the same n records (same shape and bytes per rank)
+        import numpy as np
+        from yalantinglibs_amd import synth as SY
+        _, recs_np, heaps_np = SY.make_batch(case, n, SEEDS[case], param)
+        batch = SP.RecordBatch(
+            cd.L, torch.from_numpy(recs_np.view(np.uint8).reshape(n, cd.L.stride)).to(dev),
+            [torch.from_numpy(np.ascontiguousarray(h).view(np.uint8).reshape(-1)).to(dev)
+             for h in heaps_np])
     plan = cd.get_needed_size(batch, mode)
     wire = torch.empty(plan.total_bytes + 64, dtype=torch.uint8, device=dev)
     offs = torch.empty(n + 1, dtype=torch.int64, device=dev) if mode == SP.MODE_MESSAGES else None
@@ -250,7 +265,8 @@ def main():
             "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "u8", "data": f"synthetic (spk_synth seeded {case}, seed {SEEDS[case]:#x})",
+            "dtype": "u8", "data": (f"synthetic ({'spk_synth' if case in ('rec64', 'recs', 'outer') else 'host synth.py'} "
+                                     f"seeded {case}, seed {SEEDS[case]:#x})"),
             "config": {"workload": desc, "records_per_gpu": n,
                        "mode": "vector" if modech == "A" else "messages",
                        "wire_bytes_per_gpu": wire_bytes, "record_bytes_per_gpu": rec_bytes,

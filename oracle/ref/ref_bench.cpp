@@ -206,6 +206,8 @@ int main(int argc, char **argv) {
   if (k == "outer")
     return run<Outer>("outer", n, threads, reps,
                       [=](Outer &o, uint64_t i) { o = make_outer(s, i, p); });
+  if (k == "var")
+    return run<Var>("var", n, threads, reps, [=](Var &o, uint64_t i) { fill(o, s, i, p); });
   fprintf(stderr, "unknown case\n");
   return 2;
 }
