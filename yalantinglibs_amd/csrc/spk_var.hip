@@ -1064,6 +1064,7 @@ struct WalkProg {
   uint64_t cmax[SPK_MAX_SPANS];    // largest count whose byte size fits 64 bits
   uint32_t optm;                   // bit k: span k is an OPTION ([has_value:1][U?])
   uint32_t pf_all;                 // no first-count screening of candidate starts
+  uint32_t pf_var;                 // screening past segment 0's varints (NS = -1 walks)
   uint32_t nv;                     // varint members
   uint8_t vfirst[SPK_MAX_SPANS + 2];  // segment k's varints: [vfirst[k], vfirst[k+1])
   uint32_t vafter[SPK_MAX_VARINTS];   // fixed bytes after varint j (same segment)
@@ -1097,7 +1098,8 @@ static WalkProg make_walkprog(const spk_layout *L) {
   if (p.optm & 1u) p.c0max = 0xFFFFFFFFu;
   // a varint before the first count (or no count at all): the first count's
   // position is data-dependent, so every byte may start a record
-  p.pf_all = (p.optm & 1u) || p.vfirst[1] > 0 || k == 0;
+  p.pf_all = (p.optm & 1u) || k == 0;
+  p.pf_var = !p.pf_all && p.vfirst[1] > 0;
   return p;
 }
 
@@ -1480,7 +1482,26 @@ __global__ __launch_bounds__(64 * kSpecWaves) void vec_spec(DecArgs a, WalkProg 
     if (searching) {
       const uint64_t b0 = cs + t + s0;  // first count field of candidate cs+t
       uint32_t m = 0;
-      if (b0 + 20 <= wend) {
+      if (NS < 0 && P.pf_var) {
+        // varints before the first count: parse them per candidate, then
+        // screen the count that follows
+        auto byte = [&rd](uint64_t q) { return rd.byte(q); };
+        for (int k = 0; k < 8; ++k) {
+          uint64_t q = b0 + k;
+          bool ok = true;
+          for (uint32_t j = 0; j < P.vfirst[1]; ++j) {
+            uint64_t v;
+            const uint32_t l = vi_read(byte, q, len, &v);
+            if (!l || l == kViBad) {
+              ok = false;
+              break;
+            }
+            q += l + P.vafter[j];
+          }
+          if (ok) ok = (q + w <= len ? rd(q) : ~0ull) <= P.c0max;
+          m |= (ok ? 1u : 0u) << k;
+        }
+      } else if (b0 + 20 <= wend) {
         const uint32_t o0 = (uint32_t)(b0 - rs), i = o0 >> 2, sh = o0 & 3;
         const lds_u32 *d = rd.d;
         const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2], d3 = d[i + 3], d4 = d[i + 4];
@@ -1504,7 +1525,7 @@ __global__ __launch_bounds__(64 * kSpecWaves) void vec_spec(DecArgs a, WalkProg 
           m |= (cv <= P.c0max ? 1u : 0u) << k;
         }
       }
-      if (P.pf_all) m = 0xFFu;  // first span an OPTION / varint first: any byte may start a record
+      if (P.pf_all) m = 0xFFu;  // first span an OPTION / no span: any byte may start a record
       const uint64_t rem = ce - (cs + t);  // candidates must start in the chunk
       if (rem < 8) m &= (1u << rem) - 1u;
       if (!m) {
