@@ -64,6 +64,20 @@ def test_layout_check_rejects_malformed():
     assert lib.spk_layout_check(L.ptr) == C.SPK_E_LAYOUT
 
 
+def test_layout_check_varint_ops():
+    lib = C.load_codec()
+    L = LY.case_layout("var")
+    vi = [i for i in range(L.c.n_ops) if L.c.ops[i].kind == C.SPK_OP_VARINT]
+    assert len(vi) == 4 and L.c.ops[vi[0]].aux == C.SPK_VARINT_ZIGZAG
+    assert [L.c.ops[i].aux for i in vi] == [1, 0, 1, 0]  # var_int32, var_uint64, var_int64, var_uint32
+    for field, bad in (("size", 2), ("size", 16), ("rec_off", 2), ("aux", 4)):
+        L = LY.case_layout("var")
+        setattr(L.c.ops[vi[0]], field, bad)
+        assert lib.spk_layout_check(L.ptr) == C.SPK_E_LAYOUT, (field, bad)
+    # varints alone (no span / option) make a valid non-trivial record
+    assert lib.spk_layout_check(LY.case_layout("varp").ptr) == 0
+
+
 def test_encode_rejects_bad_args_without_device_work():
     lib = C.load_codec()
     L = LY.case_layout("rec64")

@@ -386,3 +386,25 @@ def test_sharded_encoder_rccl_world1(case, n, param):
         assert sp.total_bytes == len(exp) and host[:len(exp)].numpy().tobytes() == exp
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_varint_edge_values_gpu():
+    """INT64_MIN / INT64_MAX / UINT32_MAX / 7-bit boundaries through the HIP
+    codec, messages and vector mode, against hand-checked LEB128 bytes and
+    the oracle."""
+    from test_oracle_golden import varp_edge_records, varp_edge_wire
+    L, recs = varp_edge_records()
+    cd = codec_for("varp")
+    msgs = varp_edge_wire(L)
+    out, offs = cd.serialize(to_dev(cd, recs, []), C.SPK_MODE_MESSAGES)
+    assert out.cpu().numpy().tobytes() == b"".join(msgs)
+    res, back, ec = cd.deserialize(out, C.SPK_MODE_MESSAGES, offs, len(msgs))
+    assert res.errc == 0 and (ec.cpu().numpy()[:len(msgs)] == 0).all()
+    assert back.recs.cpu().numpy().tobytes() == recs.tobytes()
+    out, _ = cd.serialize(to_dev(cd, recs, []), C.SPK_MODE_VECTOR)
+    want, _, _ = H.oracle_encode(L, C.SPK_MODE_VECTOR, recs, [])
+    assert out.cpu().numpy().tobytes() == want
+    res, back, _ = cd.deserialize(out, C.SPK_MODE_VECTOR)
+    assert res.errc == 0 and res.count == len(msgs)
+    assert back.recs.cpu().numpy().tobytes() == recs.tobytes()

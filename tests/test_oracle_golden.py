@@ -142,3 +142,42 @@ def test_oracle_error_parity(base):
             if H.sha256(re) != t["reenc_sha256"]:
                 bad.append((t["mut"], "reenc"))
     assert not bad, bad[:10]
+
+
+# ---- varint edge values (LEB128 / zigzag KATs, varint.hpp:194-330) ----------
+VARP_EDGE = [  # (x: var_int64_t, y: var_uint32_t, expected LEB128 bytes of x, of y)
+    (-(1 << 63), 0xFFFFFFFF, "ff" * 9 + "01", "ffffffff0f"),
+    ((1 << 63) - 1, 0, "fe" + "ff" * 8 + "01", "00"),
+    (-1, 127, "01", "7f"),
+    (0, 128, "00", "8001"),
+    (63, 16383, "7e", "ff7f"),
+    (-64, 16384, "7f", "808001"),
+    (64, 1 << 28, "8001", "8080808001"),
+]
+
+
+def varp_edge_records():
+    from yalantinglibs_amd import layout as LY
+    L = LY.case_layout("varp")
+    recs = np.zeros(len(VARP_EDGE), L.dev.dtype)
+    recs["id"] = np.arange(len(VARP_EDGE), dtype=np.int32) - 3
+    recs["x"] = [e[0] for e in VARP_EDGE]
+    recs["y"] = [e[1] for e in VARP_EDGE]
+    return L, recs
+
+
+def varp_edge_wire(L):
+    head = (L.c.fmt_one.code & ~1).to_bytes(4, "little")  # no container: no meta byte
+    return [head + int(i - 3).to_bytes(4, "little", signed=True) + bytes.fromhex(xb)
+            + bytes.fromhex(yb) for i, (_, _, xb, yb) in enumerate(VARP_EDGE)]
+
+
+def test_oracle_varint_edge_values():
+    L, recs = varp_edge_records()
+    wire, offs, _ = H.oracle_encode(L, C.SPK_MODE_MESSAGES, recs, [])
+    msgs = varp_edge_wire(L)
+    assert wire == b"".join(msgs)
+    assert list(np.diff(offs.astype(np.int64))) == [len(m) for m in msgs]
+    res, back, _, ec = H.oracle_decode(L, C.SPK_MODE_MESSAGES, wire, offs, len(msgs))
+    assert res.errc == 0 and (ec == 0).all()
+    assert back[:len(msgs)].tobytes() == recs.tobytes()
