@@ -326,7 +326,8 @@ def test_full_size_configs(ent):
 
 @pytest.mark.parametrize("case,n,param", [("rec64", 3000, 0), ("recs", 5000, 48),
                                           ("recs", 600, 300), ("outer", 2000, 16),
-                                          ("mixed", 300, 300)])
+                                          ("mixed", 300, 300), ("opt", 500, 40),
+                                          ("var", 700, 40), ("varp", 400, 0)])
 def test_sharded_bodies_concatenate_to_reference(case, n, param):
     """Multi-GPU single message on one device: shard bodies encoded with the
     agreed global width + rank-0 header == serialize(vector<T>) of all."""
@@ -348,7 +349,7 @@ def test_sharded_bodies_concatenate_to_reference(case, n, param):
     parts = [bytes(buf[:hl])]
     for (lo, hi), p in zip(zip(cuts[:-1], cuts[1:]), plans):
         sub = SP.RecordBatch(cd.L, full.recs[lo:hi], full.heaps)
-        size = p.var_bytes + (hi - lo) * cd.L.n_spans * w
+        size = p.var_bytes + (hi - lo) * cd.L.n_cont * w
         out = torch.empty(max(size, 1), dtype=torch.uint8, device="cuda")
         ws = cd.workspace(C.SPK_MODE_VECTOR, hi - lo)
         rc = cd.lib.spk_encode_body(cd.L.ptr, hi - lo, SP._p(sub.recs), cd._heap_ptrs(sub.heaps),

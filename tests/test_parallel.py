@@ -57,7 +57,7 @@ def _worker(rank, world, port, case, n, param, q):
         o = C.load_oracle()
         plan = C.spk_plan_t()
         assert o.spko_plan(L.ptr, C.SPK_MODE_VECTOR, len(sub), H._ptr(sub), ct.byref(plan)) == 0
-        sp = PAR.agree_shard_plan(len(sub), plan.max_count, plan.var_bytes, L.n_spans,
+        sp = PAR.agree_shard_plan(len(sub), plan.max_count, plan.var_bytes, L.n_cont,
                                   lambda gn, w: _oracle_header(L, gn, w))
         hp = (ct.c_void_p * max(len(sh), 1))(*[h.ctypes.data if h.size else 0 for h in sh])
         body = np.zeros(max(sp.body_bytes[rank], 1), np.uint8)
@@ -77,7 +77,8 @@ def _worker(rank, world, port, case, n, param, q):
 
 @pytest.mark.parametrize("case,n,param", [("rec64", 1000, 0), ("recs", 3000, 48),
                                           ("recs", 300, 400), ("outer", 700, 16),
-                                          ("mixed", 200, 300)])
+                                          ("mixed", 200, 300), ("opt", 300, 40),
+                                          ("var", 300, 40), ("varp", 200, 0)])
 def test_sharded_vector_message_gloo(case, n, param):
     world = 2
     ctx = mp.get_context("spawn")

@@ -34,6 +34,13 @@ class Layout:
     def n_spans(self):
         return len(self.dev.spans)
 
+    @property
+    def n_cont(self):
+        """Members with a width-w count on the wire (SPAN: string / vector);
+        an OPTION's 1-byte has_value and varints are in the plan's var_bytes."""
+        from . import _capi as C
+        return sum(op[0] == C.SPK_OP_SPAN for op in self.dev.ops)
+
 
 def make_layout(rtype: S.SpType, conf: int = S.DEFAULT, debug: bool = False,
                 vector_config: Optional[int] = None) -> Layout:

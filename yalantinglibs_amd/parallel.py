@@ -46,7 +46,7 @@ def width_of(max_count: int) -> int:
 
 
 def agree_shard_plan(local_n: int, local_max_count: int, local_var_bytes: int,
-                     n_spans: int, header_fn, group=None, device=None) -> ShardPlan:
+                     n_cont: int, header_fn, group=None, device=None) -> ShardPlan:
     """Collective part of the sharded encode (works on gloo or nccl):
     all-reduce(SUM) of record counts, all-reduce(MAX) of the largest element
     count, all-gather of body sizes."""
@@ -58,7 +58,7 @@ def agree_shard_plan(local_n: int, local_max_count: int, local_var_bytes: int,
     dist.all_reduce(s[1:], op=dist.ReduceOp.MAX, group=group)
     global_n, gmax = int(s[0].item()), int(s[1].item())
     w = width_of(max(global_n, gmax))
-    body = local_var_bytes + local_n * n_spans * w
+    body = local_var_bytes + local_n * n_cont * w
     sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
     dist.all_gather(sizes, torch.tensor([body], dtype=torch.int64, device=dev), group=group)
     body_bytes = [int(x.item()) for x in sizes]
@@ -89,7 +89,7 @@ class ShardedVectorEncoder:
 
     def plan(self, batch: RecordBatch) -> ShardPlan:
         p = self.cd.get_needed_size(batch, C.SPK_MODE_VECTOR)
-        return agree_shard_plan(batch.n, p.max_count, p.var_bytes, self.cd.L.n_spans,
+        return agree_shard_plan(batch.n, p.max_count, p.var_bytes, self.cd.L.n_cont,
                                 self.header, self.group, self.cd.device)
 
     def encode_body(self, batch: RecordBatch, width: int, out: torch.Tensor, stream=None):
