@@ -1026,7 +1026,8 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
 constexpr uint32_t kSpec = 256;        // payload bytes per speculation chunk
 constexpr uint32_t kWinExtra = 512;    // extension bytes staged past a wave's chunks
 constexpr uint32_t kPlaus = 4096;      // longest record a speculative walk accepts
-constexpr int kRounds = 6;             // parallel re-verification rounds
+constexpr int kRounds = 6;             // parallel re-verification rounds (default)
+constexpr int kRoundsMax = 16;         // ... for varint layouts (WalkProg::rounds)
 constexpr uint32_t kExt = 4;           // records a spec walk continues past its chunk
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
 
@@ -1048,7 +1049,7 @@ struct VCtl {
   uint32_t n_unver;  // chunks left for the sequential fixup (diagnostic)
   uint32_t term_chunk;  // first chunk where the true path terminates (kNone32)
   uint32_t overflow;    // a P list overflowed (records < 1 B impossible; guard)
-  uint32_t wl_n[kRounds + 1];  // re-verification worklist length per round
+  uint32_t wl_n[kRoundsMax + 1];  // re-verification worklist length per round
   uint32_t pad_;
   uint64_t cap;                // chunk capacity: stride of the per-span chunk arrays
 };
@@ -1065,6 +1066,7 @@ struct WalkProg {
   uint32_t optm;                   // bit k: span k is an OPTION ([has_value:1][U?])
   uint32_t pf_all;                 // no first-count screening of candidate starts
   uint32_t pf_var;                 // screening past segment 0's varints (NS = -1 walks)
+  uint32_t rounds;                 // parallel re-verification rounds before the fixup
   uint32_t nv;                     // varint members
   uint8_t vfirst[SPK_MAX_SPANS + 2];  // segment k's varints: [vfirst[k], vfirst[k+1])
   uint32_t vafter[SPK_MAX_VARINTS];   // fixed bytes after varint j (same segment)
@@ -1100,6 +1102,9 @@ static WalkProg make_walkprog(const spk_layout *L) {
   // position is data-dependent, so every byte may start a record
   p.pf_all = (p.optm & 1u) || k == 0;
   p.pf_var = !p.pf_all && p.vfirst[1] > 0;
+  // varint walks leave longer chains of unverified chunks: more parallel
+  // rounds keep the one-lane fixup short
+  p.rounds = p.nv ? kRoundsMax : kRounds;
   return p;
 }
 
@@ -1237,7 +1242,7 @@ __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
   c->lp = lp;
   c->cap = cap;
   c->n_unver = 0;
-  for (int r = 0; r <= kRounds; ++r) c->wl_n[r] = 0;
+  for (int r = 0; r <= kRoundsMax; ++r) c->wl_n[r] = 0;
   c->term_chunk = kNone32;
   c->overflow = 0;
   const uint64_t payload = (!e && a.wire_len > pos) ? a.wire_len - pos : 0;
@@ -1408,7 +1413,7 @@ __device__ __forceinline__ void verify_chunk(const DecArgs &a, const WalkProg &P
   B.T[ch] = T;
   B.cnt[ch] = count;
   B.flags[ch] = flags;
-  if (r < (uint32_t)kRounds && ch + 1 < c->nchunks && exit != next_used)
+  if (r < P.rounds && ch + 1 < c->nchunks && exit != next_used)
     mark_dirty(c, B, ch + 1, r + 1);
 }
 
@@ -1633,11 +1638,11 @@ __global__ __launch_bounds__(1024) void vec_fixup(DecArgs a, WalkProg P,
                                                   uint8_t *__restrict__ ws, VecBufs B) {
   __shared__ uint32_t sh[kFixSort];
   VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
-  const uint32_t n = c->wl_n[kRounds];
+  const uint32_t n = c->wl_n[P.rounds];
   if (threadIdx.x == 0) c->n_unver = n;
   if (!n) return;
   const uint64_t nch = c->nchunks;
-  const uint32_t *list = B.wl + (kRounds & 1) * nch;
+  const uint32_t *list = B.wl + (P.rounds & 1) * nch;
   uint32_t m = 2;  // sort size: next power of two >= n
   while (m < n) m <<= 1;
   if (n <= kFixSort) {
@@ -1668,14 +1673,14 @@ __global__ __launch_bounds__(1024) void vec_fixup(DecArgs a, WalkProg P,
       for (; ch < nch; ++ch) {
         const uint64_t entry = B.exitp[ch - 1];
         if (entry == B.used[ch]) break;
-        verify_chunk<NS>(a, P, wire, c, B, ch, entry, 0, kRounds);
+        verify_chunk<NS>(a, P, wire, c, B, ch, entry, 0, P.rounds);
       }
       done_to = ch + 1;
     }
   } else {
     for (uint64_t ch = 1; ch < nch; ++ch) {  // long list: scan every chunk
       const uint64_t entry = B.exitp[ch - 1];
-      if (entry != B.used[ch]) verify_chunk<NS>(a, P, wire, c, B, ch, entry, 0, kRounds);
+      if (entry != B.used[ch]) verify_chunk<NS>(a, P, wire, c, B, ch, entry, 0, P.rounds);
     }
   }
 }
@@ -2085,7 +2090,7 @@ static hipError_t launch_vec_decode_ns(const DecArgs &a, const WalkProg &P, cons
   const unsigned cg = grid_for(v.nch, 256);
   hipLaunchKernelGGL(vec_spec<NS>, dim3(grid_for(v.nch, (uint64_t)kSpecStep * kSpecWaves)),
                      dim3(64 * kSpecWaves), 0, s, a, P, wire, ws, B);
-  for (uint32_t r = 1; r < (uint32_t)kRounds; ++r)
+  for (uint32_t r = 1; r < P.rounds; ++r)
     hipLaunchKernelGGL(vec_verify_round<NS>, dim3(256), dim3(256), 0, s, a, P, wire, ws, B, r);
   hipLaunchKernelGGL(vec_fixup<NS>, dim3(1), dim3(1024), 0, s, a, P, wire, ws, B);
   hipLaunchKernelGGL(vec_term_min, dim3(cg), dim3(256), 0, s, ws, B);
