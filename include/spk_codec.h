@@ -2,7 +2,7 @@
  * spk_codec.h — C ABI of the MI355X struct_pack batch codec.
  *
  * This is the drop-in boundary between a host-side struct_pack front end
- * (our C++20 header include/ylt/struct_pack.hpp, or the Python mirror
+ * (our C++20 header include/ylt/struct_pack_gpu.hpp, or the Python mirror
  * yalantinglibs_amd/struct_pack.py) and the hand-written gfx950 HIP kernels
  * in yalantinglibs_amd/csrc/ (spk_api.hip, spk_fixed.hip, spk_var.hip). Plain C: no HIP/torch types, all
  * buffers are raw pointers + sizes, streams are opaque `void*` (hipStream_t).
@@ -290,6 +290,22 @@ int spk_synth(int kind, uint64_t seed, uint64_t first, uint64_t n,
 /* per-record span counts for variable kinds (to size/prefix the heap) */
 int spk_synth_counts(int kind, uint64_t seed, uint64_t first, uint64_t n,
                      uint32_t param, uint64_t *d_counts, void *stream);
+
+/* ---- runtime helpers ----------------------------------------------------
+ * Device / pinned-host memory, async copies and streams, so that a front end
+ * (our C++ header, a cgo / JNI / ctypes binding) needs no HIP headers of its
+ * own. Return SPK_OK or SPK_E_ARG / SPK_E_HIP. */
+#define SPK_COPY_H2D 1
+#define SPK_COPY_D2H 2
+#define SPK_COPY_D2D 3
+int spk_device_alloc(void **d_ptr, size_t bytes);
+int spk_device_free(void *d_ptr);
+int spk_host_alloc_pinned(void **h_ptr, size_t bytes);
+int spk_host_free_pinned(void *h_ptr);
+int spk_copy_async(void *dst, const void *src, size_t bytes, int kind, void *stream);
+int spk_stream_create(void **stream); /* non-blocking stream */
+int spk_stream_destroy(void *stream);
+int spk_stream_sync(void *stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,836 @@
+// struct_pack_gpu.hpp — MI355X-native struct_pack front end (our
+// implementation), namespace struct_pack::gpu.
+//
+// Keeps the reference's entry-point names, argument order, argument meaning
+// and error values (reference include/ylt/struct_pack.hpp:75-658,
+// error_code.hpp:21-64) and produces the reference's wire bytes exactly. The
+// byte work runs in the gfx950 HIP kernels of libspk_codec.so behind the C
+// ABI of include/spk_codec.h; this header reflects types, builds the layout
+// descriptor, stages host objects and calls the ABI. There is no CPU codec
+// and no HIP header here: device memory, copies and streams also go through
+// the C ABI, so any C++20 compiler can build a caller.
+//
+// It compiles next to the reference header (then struct_pack::errc,
+// sp_config, var_int32_t ... ARE the reference's, see config.hpp) or alone.
+//
+//   get_type_code<T>() / get_type_literal<T>()          compile time
+//   get_needed_size(t)                                   size pass (device)
+//   serialize(t) / serialize<Buffer>(t) / serialize<conf, Buffer>(t)
+//   serialize_to(buffer|writer, t) / serialize_to(char*, serialize_buffer_size, t)
+//   serialize_to_with_offset(buffer, offset, t) / serialize_with_offset(offset, t)
+//   deserialize_to(t, view|data,size [, consume_len])
+//   deserialize_to_with_offset(t, view|data,size, offset)
+//   deserialize<T>(view|data,size [, consume_len]) / deserialize<conf, T>(...)
+//   get_field<T, I>(view|data,size)
+//       t = std::vector<R> (or std::span<R> to serialize): one message of
+//           records, SPK_MODE_VECTOR; t = R: one record message
+//           (SPK_MODE_MESSAGES with one message)
+//   serialize_messages / deserialize_messages           coro_rpc payload batches
+//   serialize_frames / deserialize_frames               ... in coro_rpc's framing
+//   device::codec<R>                                     device-resident batches
+//
+// Build: <c++20 compiler> -I include ... -L yalantinglibs_amd -lspk_codec
+#pragma once
+#include <cstring>
+#include <memory>
+#include <span>
+#include <stdexcept>
+#include <string>
+#include <string_view>
+#include <type_traits>
+#include <vector>
+
+#include "../spk_codec.h"
+#include "struct_pack_gpu/layout.hpp"
+
+namespace struct_pack::gpu {
+
+// Device / ABI failures (not wire errors: those come back as errc, never as
+// exceptions, like the reference's decoder)
+class spk_error : public std::runtime_error {
+ public:
+  using std::runtime_error::runtime_error;
+};
+
+// serialize_buffer_size (calculate_size.hpp:391-405): message length and
+// metainfo byte of a planned message
+struct serialize_buffer_size {
+  std::size_t len_ = 0;
+  unsigned char metainfo_ = 0;
+  constexpr std::size_t size() const { return len_; }
+  constexpr unsigned char metainfo() const { return metainfo_; }
+  constexpr operator std::size_t() const { return len_; }
+};
+
+namespace detail {
+
+// ---- what the batch model covers (compile-time, SFINAE-friendly) -----------
+template <typename T>
+constexpr bool supported();
+template <typename M, std::size_t... I>
+constexpr bool all_supported(std::index_sequence<I...>) {
+  return (supported<std::tuple_element_t<I, M>>() && ...);
+}
+template <typename T>
+constexpr bool elem_supported() {  // container / optional element
+  if constexpr (supported<T>())
+    return is_trivially_serializable<T>();
+  else
+    return false;
+}
+template <typename T>
+constexpr bool supported() {
+  if constexpr (is_fundamental_v<T> || is_string_v<T> || is_varint_v<T>) {
+    return true;
+  } else if constexpr (is_container_v<T> || is_std_optional<T>::value) {
+    return elem_supported<remove_cvref_t<typename T::value_type>>();
+  } else if constexpr (is_std_array<T>::value) {
+    return supported<typename T::value_type>();
+  } else if constexpr (is_record_v<T>) {
+    using M = members_tuple_t<T>;
+    return all_supported<M>(std::make_index_sequence<std::tuple_size_v<M>>{});
+  } else {
+    return false;
+  }
+}
+// a record type the batch codec encodes as the element of a message
+template <typename R>
+constexpr bool record_supported() {
+  if constexpr (is_record_v<R> || is_fundamental_v<R> || is_std_array<R>::value)
+    return supported<R>();
+  else
+    return false;
+}
+
+// the argument of serialize / deserialize_to: std::vector<R> / std::span<R>
+// (a VECTOR message) or a record R (one message)
+template <typename T>
+struct msg_traits {
+  static constexpr bool vector = false, record = record_supported<T>();
+  using rec = T;
+};
+template <typename R, typename A>
+struct msg_traits<std::vector<R, A>> {
+  static constexpr bool vector = record_supported<R>(), record = false;
+  using rec = R;
+};
+template <typename R, std::size_t E>
+struct msg_traits<std::span<R, E>> {
+  static constexpr bool vector = E == std::dynamic_extent && record_supported<remove_cvref_t<R>>(),
+                        record = false;
+  using rec = remove_cvref_t<R>;
+};
+
+}  // namespace detail
+
+// true when the GPU front end handles `T` as a whole message
+template <typename T>
+constexpr bool is_gpu_message_v =
+    detail::msg_traits<detail::remove_cvref_t<T>>::vector ||
+    detail::msg_traits<detail::remove_cvref_t<T>>::record;
+// true for a batch message: std::vector<R> / std::span<R> of records
+template <typename T>
+constexpr bool is_gpu_batch_v = detail::msg_traits<detail::remove_cvref_t<T>>::vector;
+
+namespace device {
+
+inline void check(int rc, const char *what) {
+  if (rc != SPK_OK) throw spk_error(std::string("struct_pack::gpu: ") + what + " failed (" +
+                                    std::to_string(rc) + ")");
+}
+
+// RAII device allocation (spk_device_alloc)
+class buffer {
+ public:
+  buffer() = default;
+  explicit buffer(std::size_t n) { resize(n); }
+  buffer(const buffer &) = delete;
+  buffer &operator=(const buffer &) = delete;
+  buffer(buffer &&o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr, o.n_ = 0; }
+  buffer &operator=(buffer &&o) noexcept {
+    std::swap(p_, o.p_);
+    std::swap(n_, o.n_);
+    return *this;
+  }
+  ~buffer() {
+    if (p_) (void)spk_device_free(p_);
+  }
+  void resize(std::size_t n) {  // grows only; contents not preserved
+    if (n <= n_ && p_) return;
+    if (p_) check(spk_device_free(p_), "spk_device_free");
+    p_ = nullptr;
+    n_ = 0;
+    check(spk_device_alloc(&p_, n ? n : 1), "spk_device_alloc");
+    n_ = n;
+  }
+  void *data() const { return p_; }
+  std::size_t size() const { return n_; }
+
+ private:
+  void *p_ = nullptr;
+  std::size_t n_ = 0;
+};
+
+inline void copy(void *dst, const void *src, std::size_t n, int kind, void *s) {
+  check(spk_copy_async(dst, src, n, kind, s), "spk_copy_async");
+}
+inline void sync(void *s) { check(spk_stream_sync(s), "spk_stream_sync"); }
+
+// A batch of R in device memory: device records + one heap per span.
+template <typename R>
+struct batch {
+  buffer recs;
+  std::vector<buffer> heaps;
+  std::vector<uint64_t> heap_elems;
+  std::size_t n = 0;
+};
+
+template <typename R, uint64_t conf = sp_config::DEFAULT>
+class codec {
+ public:
+  explicit codec(void *stream = nullptr) : s_(stream) {}
+
+  static const spk_layout &layout() {
+    static const spk_layout L = [] {
+      spk_layout l = make_spk_layout<R, conf>();
+      check(spk_layout_check(&l), "spk_layout_check");
+      return l;
+    }();
+    return L;
+  }
+  static constexpr bool trivial = detail::is_trivially_serializable<R>();
+
+  // ---- staging (host <-> device) -----------------------------------------
+  batch<R> upload(const R *v, std::size_t n) {
+    const spk_layout &L = layout();
+    batch<R> b;
+    b.n = n;
+    b.recs.resize(n * L.rec_stride);
+    if constexpr (trivial) {
+      copy(b.recs.data(), v, n * sizeof(R), SPK_COPY_H2D, s_);
+      sync(s_);
+    } else {
+      std::vector<uint8_t> recs(n * L.rec_stride, 0);
+      std::vector<std::vector<uint8_t>> heaps(n_spans());
+      for (std::size_t i = 0; i < n; ++i) {
+        detail::marshal_state st{&L, recs.data() + i * L.rec_stride, 0, 0, &heaps, 0};
+        detail::to_device(v[i], st);
+      }
+      copy(b.recs.data(), recs.data(), recs.size(), SPK_COPY_H2D, s_);
+      for (uint32_t k = 0; k < n_spans(); ++k) {
+        b.heaps.emplace_back(heaps[k].size());
+        b.heap_elems.push_back(heaps[k].size() / span_elem(k));
+        copy(b.heaps[k].data(), heaps[k].data(), heaps[k].size(), SPK_COPY_H2D, s_);
+      }
+      sync(s_);  // host staging buffers die here
+    }
+    return b;
+  }
+
+  // ok(i) selects the records to materialise (failed messages stay default)
+  template <typename Pred = std::nullptr_t>
+  void download(const batch<R> &b, std::size_t n, R *out, Pred ok = nullptr) {
+    const spk_layout &L = layout();
+    if constexpr (trivial) {
+      copy(out, b.recs.data(), n * sizeof(R), SPK_COPY_D2H, s_);
+      sync(s_);
+    } else {
+      std::vector<uint8_t> recs(n * L.rec_stride);
+      // kept in the codec: string_view / span members of the decoded objects
+      // alias these host heaps, valid until this thread's next decode of R
+      // (the reference's views alias its input buffer, unpacker.hpp:1135-1145)
+      std::vector<std::vector<uint8_t>> &heaps = view_heaps_;
+      heaps.assign(n_spans(), {});
+      copy(recs.data(), b.recs.data(), recs.size(), SPK_COPY_D2H, s_);
+      std::vector<const uint8_t *> hp(n_spans());
+      for (uint32_t k = 0; k < n_spans(); ++k) {
+        heaps[k].resize(b.heap_elems[k] * span_elem(k));
+        copy(heaps[k].data(), b.heaps[k].data(), heaps[k].size(), SPK_COPY_D2H, s_);
+        hp[k] = heaps[k].data();
+      }
+      sync(s_);
+      for (std::size_t i = 0; i < n; ++i) {
+        if constexpr (!std::is_same_v<Pred, std::nullptr_t>)
+          if (!ok(i)) continue;
+        detail::unmarshal_state st{&L, recs.data() + i * L.rec_stride, 0, 0, hp.data(), 0};
+        detail::from_device(out[i], st);
+      }
+    }
+  }
+
+  // ---- device-resident codec ----------------------------------------------
+  spk_plan_t plan(const batch<R> &b, int mode) {
+    ws_.resize(spk_workspace_bytes(&layout(), mode, b.n, 0));
+    plan_.resize(sizeof(spk_plan_t));
+    check(spk_plan(&layout(), mode, b.n, b.recs.data(), (spk_plan_t *)plan_.data(), ws_.data(),
+                   ws_.size(), s_), "spk_plan");
+    spk_plan_t p{};
+    copy(&p, plan_.data(), sizeof(p), SPK_COPY_D2H, s_);
+    sync(s_);
+    return p;
+  }
+
+  // after plan(): write into d_out (device). Stream-ordered, no sync.
+  void encode(const batch<R> &b, int mode, void *d_out, std::size_t cap,
+              uint64_t *d_offsets = nullptr) {
+    std::vector<const void *> hp = heap_ptrs(b);
+    check(spk_encode(&layout(), mode, b.n, b.recs.data(), hp.data(),
+                     (const spk_plan_t *)plan_.data(), d_out, cap, d_offsets, ws_.data(),
+                     ws_.size(), s_), "spk_encode");
+  }
+
+  // after plan(SPK_MODE_MESSAGES): n framed messages [prefix][serialize(rec)]
+  void encode_framed(const batch<R> &b, const spk_frame &f, void *d_out, std::size_t cap,
+                     uint64_t *d_offsets = nullptr) {
+    std::vector<const void *> hp = heap_ptrs(b);
+    check(spk_encode_framed(&layout(), b.n, b.recs.data(), hp.data(),
+                            (const spk_plan_t *)plan_.data(), &f, d_out, cap, d_offsets,
+                            ws_.data(), ws_.size(), s_), "spk_encode_framed");
+  }
+
+  // decode into `out` (capacities from out.n / out.heap_elems); `prefix` =
+  // frame bytes before each message (MESSAGES mode only)
+  spk_dresult_t decode(batch<R> &out, const void *d_wire, std::size_t len, int mode,
+                       const uint64_t *d_offsets = nullptr, std::size_t n_msgs = 0,
+                       int32_t *d_errc = nullptr, uint32_t prefix = 0) {
+    const uint64_t nrec = mode == SPK_MODE_VECTOR ? out.n : n_msgs;
+    ws_.resize(spk_workspace_bytes(&layout(), mode, nrec, len));
+    res_.resize(sizeof(spk_dresult_t));
+    std::vector<void *> hp(n_spans() ? n_spans() : 1, nullptr);
+    std::vector<uint64_t> caps(n_spans() ? n_spans() : 1, 0);
+    for (uint32_t k = 0; k < n_spans(); ++k) {
+      hp[k] = out.heaps[k].data();
+      caps[k] = out.heap_elems[k];
+    }
+    if (prefix)
+      check(spk_decode_framed(&layout(), d_wire, len, d_offsets, n_msgs, prefix, out.recs.data(),
+                              out.n, hp.data(), caps.data(), (spk_dresult_t *)res_.data(), d_errc,
+                              ws_.data(), ws_.size(), s_), "spk_decode_framed");
+    else
+      check(spk_decode(&layout(), mode, d_wire, len, d_offsets, n_msgs, out.recs.data(), out.n,
+                       hp.data(), caps.data(), (spk_dresult_t *)res_.data(), d_errc, ws_.data(),
+                       ws_.size(), s_), "spk_decode");
+    spk_dresult_t r{};
+    copy(&r, res_.data(), sizeof(r), SPK_COPY_D2H, s_);
+    sync(s_);
+    return r;
+  }
+
+  // a batch able to hold the decode of a `len`-byte wire buffer into at most
+  // max_records records: every heap can hold the whole wire
+  batch<R> alloc_for_wire(std::size_t len, std::size_t max_records) {
+    batch<R> b;
+    b.n = max_records;
+    b.recs.resize(max_records * layout().rec_stride);
+    for (uint32_t k = 0; k < n_spans(); ++k) {
+      // an OPTION holds at most one value per record, readable or not
+      b.heap_elems.push_back(span_is_option(k) ? max_records : len / span_elem(k) + 1);
+      b.heaps.emplace_back(b.heap_elems.back() * span_elem(k));
+    }
+    return b;
+  }
+
+  static uint32_t n_spans() {
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < layout().n_ops; ++i) k += has_heap(layout().ops[i]);
+    return k;
+  }
+  // SPAN + OPTION members: one heap each (COPY and VARINT live in the record)
+  static bool has_heap(const spk_op &o) {
+    return o.kind == SPK_OP_SPAN || o.kind == SPK_OP_OPTION;
+  }
+  static uint32_t span_elem(uint32_t k) {
+    for (uint32_t i = 0, s = 0; i < layout().n_ops; ++i)
+      if (has_heap(layout().ops[i]) && s++ == k) return layout().ops[i].size;
+    return 1;
+  }
+  static bool span_is_option(uint32_t k) {
+    for (uint32_t i = 0, s = 0; i < layout().n_ops; ++i)
+      if (has_heap(layout().ops[i]) && s++ == k)
+        return layout().ops[i].kind == SPK_OP_OPTION;
+    return false;
+  }
+  // fewest wire bytes a record can take: a bound on the records in a buffer
+  static std::size_t min_record_wire() {
+    std::size_t m = 0;
+    for (uint32_t i = 0; i < layout().n_ops; ++i)
+      m += layout().ops[i].kind == SPK_OP_COPY ? layout().ops[i].size : 1;
+    return m ? m : 1;
+  }
+  void *stream() const { return s_; }
+
+ private:
+  std::vector<const void *> heap_ptrs(const batch<R> &b) const {
+    std::vector<const void *> hp(n_spans() ? n_spans() : 1, nullptr);
+    for (uint32_t k = 0; k < n_spans(); ++k) hp[k] = b.heaps[k].data();
+    return hp;
+  }
+  void *s_;
+  buffer ws_, plan_, res_;
+  std::vector<std::vector<uint8_t>> view_heaps_;
+};
+
+template <typename R, uint64_t conf>
+codec<R, conf> &thread_codec() {
+  thread_local codec<R, conf> c;
+  return c;
+}
+
+}  // namespace device
+
+namespace detail {
+
+template <typename T>
+concept byte_view = requires(const T &v) {
+  v.data();
+  v.size();
+} && sizeof(*std::declval<const T &>().data()) == 1;
+
+template <typename T>
+concept resizable_buffer = requires(T &b, std::size_t n) {
+  b.resize(n);
+  b.data();
+  b.size();
+} && sizeof(*std::declval<T &>().data()) == 1;
+
+template <typename T>
+concept byte_writer = requires(T &w, const char *p, std::size_t n) { w.write(p, n); };
+
+// One planned message of `t` staged on the device (plan + encode); the bytes
+// stay in `out` until copied to the caller.
+template <uint64_t conf, typename T>
+struct staged_message {
+  using tr = msg_traits<remove_cvref_t<T>>;
+  using R = typename tr::rec;
+  device::buffer out, offs;
+  spk_plan_t plan{};
+  std::size_t len = 0;
+
+  explicit staged_message(const T &t) {
+    auto &c = device::thread_codec<R, conf>();
+    if constexpr (tr::vector) {
+      auto b = c.upload(t.data(), t.size());
+      plan = c.plan(b, SPK_MODE_VECTOR);
+      len = plan.total_bytes;
+      out.resize(len);
+      c.encode(b, SPK_MODE_VECTOR, out.data(), out.size());
+    } else {
+      auto b = c.upload(&t, 1);
+      plan = c.plan(b, SPK_MODE_MESSAGES);
+      len = plan.total_bytes;
+      out.resize(len);
+      offs.resize(2 * sizeof(uint64_t));
+      c.encode(b, SPK_MODE_MESSAGES, out.data(), out.size(), (uint64_t *)offs.data());
+    }
+  }
+  void copy_to(void *dst) {
+    auto &c = device::thread_codec<R, conf>();
+    device::copy(dst, out.data(), len, SPK_COPY_D2H, c.stream());
+    device::sync(c.stream());
+  }
+};
+
+template <typename T>
+constexpr void check_message_type() {
+  static_assert(is_gpu_message_v<T>,
+                "struct_pack::gpu handles one std::vector<R> / std::span<R> of records or one "
+                "record R whose members are fundamentals, enums, std::array, std::string, "
+                "containers / optionals of trivially serializable types, varints and nested "
+                "records; use the reference's CPU struct_pack for anything else");
+}
+
+// decode of one message into t: VECTOR for std::vector<R>, one MESSAGES
+// message for a record. errc / consume_len as the reference
+// (struct_pack.hpp:326-357); `t` is left unchanged on an error.
+template <uint64_t conf, typename T>
+err_code decode_one(T &t, const char *data, std::size_t size, std::size_t &consume_len) {
+  check_message_type<T>();
+  using tr = msg_traits<T>;
+  using R = typename tr::rec;
+  static_assert(!std::is_same_v<T, std::span<R>>, "deserialize into std::vector<R>");
+  auto &c = device::thread_codec<R, conf>();
+  consume_len = 0;
+  device::buffer wire(size + 16);
+  device::copy(wire.data(), data, size, SPK_COPY_H2D, c.stream());
+  std::size_t cap = tr::vector ? size / c.min_record_wire() + 1 : 1;
+  for (;;) {
+    // the capacities are upper bounds by construction (every record takes at
+    // least min_record_wire bytes, no heap exceeds the wire); the loop only
+    // guards that invariant and never surfaces a non-reference errc
+    auto b = c.alloc_for_wire(size, cap);
+    spk_dresult_t r;
+    if constexpr (tr::vector) {
+      r = c.decode(b, wire.data(), size, SPK_MODE_VECTOR);
+    } else {
+      device::buffer offs(2 * sizeof(uint64_t)), ec(sizeof(int32_t));
+      const uint64_t o[2] = {0, size};
+      device::copy(offs.data(), o, sizeof o, SPK_COPY_H2D, c.stream());
+      r = c.decode(b, wire.data(), size, SPK_MODE_MESSAGES, (const uint64_t *)offs.data(), 1,
+                   (int32_t *)ec.data());
+      int32_t e = 0;
+      device::copy(&e, ec.data(), sizeof e, SPK_COPY_D2H, c.stream());
+      device::sync(c.stream());
+      r.errc = e;
+    }
+    if (r.errc == SPK_ERRC_CAPACITY) {
+      cap = cap * 2 + 1;
+      continue;
+    }
+    if (r.errc) return static_cast<errc>(r.errc);
+    for (uint32_t k = 0; k < c.n_spans(); ++k) b.heap_elems[k] = r.heap_used[k];
+    if constexpr (tr::vector) {
+      T out(r.count);
+      c.download(b, r.count, out.data());
+      t = std::move(out);
+    } else {
+      c.download(b, 1, &t);
+    }
+    consume_len = r.consumed;
+    return {};
+  }
+}
+
+}  // namespace detail
+
+// ===========================================================================
+// Reference-named entry points (host data in, host bytes out)
+// ===========================================================================
+
+// get_needed_size (struct_pack.hpp:131-135)
+template <uint64_t conf = sp_config::DEFAULT, typename T>
+serialize_buffer_size get_needed_size(const T &t) {
+  detail::check_message_type<T>();
+  using tr = detail::msg_traits<detail::remove_cvref_t<T>>;
+  using R = typename tr::rec;
+  auto &c = device::thread_codec<R, conf>();
+  spk_plan_t p;
+  if constexpr (tr::vector) {
+    auto b = c.upload(t.data(), t.size());
+    p = c.plan(b, SPK_MODE_VECTOR);
+  } else {
+    auto b = c.upload(&t, 1);
+    p = c.plan(b, SPK_MODE_MESSAGES);
+  }
+  serialize_buffer_size r;
+  r.len_ = p.total_bytes;
+  if constexpr (tr::vector) {
+    r.metainfo_ = static_cast<unsigned char>(p.has_meta ? p.metainfo : 0);
+  } else {  // one message: its header shape at the record's own width
+    const spk_msgfmt &f = c.layout().fmt_one;
+    const bool head = f.flags & SPK_MF_HASH_HEAD, lit = head && (f.flags & SPK_MF_TYPE_LITERAL);
+    const bool cont = f.flags & SPK_MF_HAS_CONTAINER;
+    const uint32_t w = cont ? p.width : 1;
+    const bool meta = lit || (!head && cont) || w > 1;
+    const unsigned char wb = w == 1 ? 0 : w == 2 ? 0x08 : w == 4 ? 0x10 : 0x18;
+    r.metainfo_ = meta ? static_cast<unsigned char>(wb | (lit ? 0x04 : 0)) : 0;
+  }
+  return r;
+}
+
+// serialize_to(Buffer& | Writer&, t): appends to a byte buffer or writes to
+// a writer (struct_pack.hpp:137-159)
+template <uint64_t conf = sp_config::DEFAULT, typename Writer, typename T>
+void serialize_to(Writer &writer, const T &t) {
+  detail::check_message_type<T>();
+  detail::staged_message<conf, T> m(t);
+  if constexpr (detail::resizable_buffer<Writer>) {
+    const std::size_t old = writer.size();
+    writer.resize(old + m.len);
+    m.copy_to(writer.data() + old);
+  } else {
+    static_assert(detail::byte_writer<Writer>,
+                  "serialize_to needs a contiguous byte buffer or a writer with "
+                  "write(const char*, size_t)");
+    std::vector<char> tmp(m.len);
+    m.copy_to(tmp.data());
+    writer.write(tmp.data(), tmp.size());
+  }
+}
+
+// serialize_to(char*, serialize_buffer_size, t): the caller sized the buffer
+// with get_needed_size (struct_pack.hpp:161-167)
+template <uint64_t conf = sp_config::DEFAULT, typename T>
+void serialize_to(char *buffer, serialize_buffer_size info, const T &t) {
+  detail::check_message_type<T>();
+  detail::staged_message<conf, T> m(t);
+  if (m.len != info.size())
+    throw spk_error("struct_pack::gpu::serialize_to: serialize_buffer_size does not match t");
+  m.copy_to(buffer);
+}
+#if SPK_GPU_WITH_REFERENCE
+// ... with the size object of the reference's own get_needed_size
+template <uint64_t conf = sp_config::DEFAULT, typename T>
+void serialize_to(char *buffer, struct_pack::serialize_buffer_size info, const T &t) {
+  serialize_buffer_size s;
+  s.len_ = info.size();
+  s.metainfo_ = info.metainfo();
+  serialize_to<conf>(buffer, s, t);
+}
+#endif
+
+// serialize_to_with_offset(buffer, offset, t): `offset` bytes reserved
+// before the message, e.g. coro_rpc's req_header (struct_pack.hpp:169-189)
+template <uint64_t conf = sp_config::DEFAULT, typename Buffer, typename T>
+void serialize_to_with_offset(Buffer &buffer, std::size_t offset, const T &t) {
+  detail::check_message_type<T>();
+  static_assert(detail::resizable_buffer<Buffer>, "a contiguous byte buffer");
+  detail::staged_message<conf, T> m(t);
+  const std::size_t old = buffer.size();
+  buffer.resize(old + offset + m.len);
+  m.copy_to(buffer.data() + old + offset);
+}
+
+// serialize<Buffer>(t) and serialize<conf, Buffer>(t) (struct_pack.hpp:191-262)
+template <typename Buffer = std::vector<char>, typename T>
+  requires detail::resizable_buffer<Buffer>
+[[nodiscard]] Buffer serialize(const T &t) {
+  Buffer b;
+  serialize_to<sp_config::DEFAULT>(b, t);
+  return b;
+}
+template <uint64_t conf, typename Buffer = std::vector<char>, typename T>
+  requires detail::resizable_buffer<Buffer>
+[[nodiscard]] Buffer serialize(const T &t) {
+  Buffer b;
+  serialize_to<conf>(b, t);
+  return b;
+}
+template <typename Buffer = std::vector<char>, typename T>
+  requires detail::resizable_buffer<Buffer>
+[[nodiscard]] Buffer serialize_with_offset(std::size_t offset, const T &t) {
+  Buffer b;
+  serialize_to_with_offset<sp_config::DEFAULT>(b, offset, t);
+  return b;
+}
+template <uint64_t conf, typename Buffer = std::vector<char>, typename T>
+  requires detail::resizable_buffer<Buffer>
+[[nodiscard]] Buffer serialize_with_offset(std::size_t offset, const T &t) {
+  Buffer b;
+  serialize_to_with_offset<conf>(b, offset, t);
+  return b;
+}
+
+// deserialize_to (struct_pack.hpp:266-357): errc as the reference; with
+// consume_len the message end (or the compatible-data length if larger), 0 on
+// an error
+template <uint64_t conf = sp_config::DEFAULT, typename T>
+[[nodiscard]] err_code deserialize_to(T &t, const char *data, std::size_t size,
+                                      std::size_t &consume_len) {
+  return detail::decode_one<conf>(t, data, size, consume_len);
+}
+template <uint64_t conf = sp_config::DEFAULT, typename T>
+[[nodiscard]] err_code deserialize_to(T &t, const char *data, std::size_t size) {
+  std::size_t consumed;
+  return detail::decode_one<conf>(t, data, size, consumed);
+}
+template <uint64_t conf = sp_config::DEFAULT, typename T, detail::byte_view View>
+[[nodiscard]] err_code deserialize_to(T &t, const View &v) {
+  std::size_t consumed;
+  return detail::decode_one<conf>(t, reinterpret_cast<const char *>(v.data()), v.size(),
+                                  consumed);
+}
+template <uint64_t conf = sp_config::DEFAULT, typename T, detail::byte_view View>
+[[nodiscard]] err_code deserialize_to(T &t, const View &v, std::size_t &consume_len) {
+  return detail::decode_one<conf>(t, reinterpret_cast<const char *>(v.data()), v.size(),
+                                  consume_len);
+}
+
+// deserialize_to_with_offset: decode at data + offset, advance offset by the
+// bytes consumed (struct_pack.hpp:359-385)
+template <uint64_t conf = sp_config::DEFAULT, typename T>
+[[nodiscard]] err_code deserialize_to_with_offset(T &t, const char *data, std::size_t size,
+                                                  std::size_t &offset) {
+  std::size_t sz;
+  auto e = detail::decode_one<conf>(t, data + offset, size - offset, sz);
+  offset += sz;
+  return e;
+}
+template <uint64_t conf = sp_config::DEFAULT, typename T, detail::byte_view View>
+[[nodiscard]] err_code deserialize_to_with_offset(T &t, const View &v, std::size_t &offset) {
+  return deserialize_to_with_offset<conf>(t, reinterpret_cast<const char *>(v.data()), v.size(),
+                                          offset);
+}
+
+// deserialize<T>(...) and deserialize<conf, T>(...) -> expected<T, err_code>
+// (struct_pack.hpp:387-533; one message type)
+template <typename T, detail::byte_view View>
+[[nodiscard]] expected<T> deserialize(const View &v) {
+  T t{};
+  if (auto e = deserialize_to(t, v)) return make_unexpected<T>(e);
+  return t;
+}
+template <typename T>
+[[nodiscard]] expected<T> deserialize(const char *data, std::size_t size) {
+  T t{};
+  if (auto e = deserialize_to(t, data, size)) return make_unexpected<T>(e);
+  return t;
+}
+template <typename T, detail::byte_view View>
+[[nodiscard]] expected<T> deserialize(const View &v, std::size_t &consume_len) {
+  T t{};
+  if (auto e = deserialize_to(t, v, consume_len)) return make_unexpected<T>(e);
+  return t;
+}
+template <typename T>
+[[nodiscard]] expected<T> deserialize(const char *data, std::size_t size,
+                                      std::size_t &consume_len) {
+  T t{};
+  if (auto e = deserialize_to(t, data, size, consume_len)) return make_unexpected<T>(e);
+  return t;
+}
+template <uint64_t conf, typename T, detail::byte_view View>
+[[nodiscard]] expected<T> deserialize(const View &v) {
+  T t{};
+  if (auto e = deserialize_to<conf>(t, v)) return make_unexpected<T>(e);
+  return t;
+}
+template <uint64_t conf, typename T>
+[[nodiscard]] expected<T> deserialize(const char *data, std::size_t size) {
+  T t{};
+  if (auto e = deserialize_to<conf>(t, data, size)) return make_unexpected<T>(e);
+  return t;
+}
+template <uint64_t conf, typename T, detail::byte_view View>
+[[nodiscard]] expected<T> deserialize(const View &v, std::size_t &consume_len) {
+  T t{};
+  if (auto e = deserialize_to<conf>(t, v, consume_len)) return make_unexpected<T>(e);
+  return t;
+}
+
+// get_field<T, I>: member I of a T message (struct_pack.hpp:565-658). The
+// whole record is decoded on the device, member I returned.
+template <typename T, std::size_t I>
+using field_t = std::tuple_element_t<I, detail::members_tuple_t<T>>;
+
+template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT>
+[[nodiscard]] expected<field_t<T, I>> get_field(const char *data, std::size_t size) {
+  static_assert(detail::is_record_v<T>, "get_field reads a member of a record message");
+  T t{};
+  std::size_t consumed;
+  if (auto e = detail::decode_one<conf>(t, data, size, consumed))
+    return make_unexpected<field_t<T, I>>(e);
+  return expected<field_t<T, I>>(std::get<I>(detail::tie_members(t)));
+}
+template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT, detail::byte_view View>
+[[nodiscard]] expected<field_t<T, I>> get_field(const View &v) {
+  return get_field<T, I, conf>(reinterpret_cast<const char *>(v.data()), v.size());
+}
+
+// ---- coro_rpc payload batches: n independent serialize(R) messages --------
+template <uint64_t conf = sp_config::DEFAULT, typename R>
+std::vector<char> serialize_messages(const std::vector<R> &v, std::vector<uint64_t> &offsets) {
+  auto &c = device::thread_codec<R, conf>();
+  auto b = c.upload(v.data(), v.size());
+  spk_plan_t p = c.plan(b, SPK_MODE_MESSAGES);
+  device::buffer out(p.total_bytes), offs((v.size() + 1) * sizeof(uint64_t));
+  c.encode(b, SPK_MODE_MESSAGES, out.data(), out.size(), (uint64_t *)offs.data());
+  std::vector<char> bytes(p.total_bytes);
+  offsets.resize(v.size() + 1);
+  device::copy(bytes.data(), out.data(), bytes.size(), SPK_COPY_D2H, c.stream());
+  device::copy(offsets.data(), offs.data(), offsets.size() * 8, SPK_COPY_D2H, c.stream());
+  device::sync(c.stream());
+  return bytes;
+}
+
+// decodes message i = data[offsets[i] + prefix, offsets[i+1]) into out[i];
+// returns per-message errc
+template <uint64_t conf = sp_config::DEFAULT, typename R>
+std::vector<err_code> deserialize_messages(std::vector<R> &out, const char *data,
+                                           std::size_t size,
+                                           const std::vector<uint64_t> &offsets,
+                                           uint32_t prefix = 0) {
+  auto &c = device::thread_codec<R, conf>();
+  const std::size_t n = offsets.empty() ? 0 : offsets.size() - 1;
+  device::buffer wire(size + 16), offs(offsets.size() * 8 + 8), ec(n * 4 + 4);
+  device::copy(wire.data(), data, size, SPK_COPY_H2D, c.stream());
+  device::copy(offs.data(), offsets.data(), offsets.size() * 8, SPK_COPY_H2D, c.stream());
+  auto b = c.alloc_for_wire(size, n);
+  spk_dresult_t r = c.decode(b, wire.data(), size, SPK_MODE_MESSAGES, (uint64_t *)offs.data(), n,
+                             (int32_t *)ec.data(), prefix);
+  if (r.errc == SPK_ERRC_CAPACITY)  // heaps hold the whole wire: unreachable
+    throw std::logic_error("struct_pack::gpu: decode capacity invariant broken");
+  std::vector<int32_t> e(n);
+  device::copy(e.data(), ec.data(), n * 4, SPK_COPY_D2H, c.stream());
+  for (uint32_t k = 0; k < c.n_spans(); ++k) b.heap_elems[k] = r.heap_used[k];
+  device::sync(c.stream());
+  out.assign(n, R{});
+  c.download(b, n, out.data(), [&](std::size_t i) { return e[i] == 0; });
+  std::vector<err_code> res(n);
+  for (std::size_t i = 0; i < n; ++i) res[i] = static_cast<errc>(e[i]);
+  return res;
+}
+
+// ---- coro_rpc framing ------------------------------------------------------
+// coro_rpc puts a 20-byte req_header before every request payload and a
+// 16-byte resp_header before every response (ref coro_rpc_protocol.hpp:60-79;
+// written with DISABLE_ALL_META_INFO = the raw struct bytes, client
+// coro_rpc_client.hpp:1285-1335, server coro_rpc_protocol.hpp:191-240).
+namespace rpc_frame {
+inline constexpr uint8_t magic_number = 21;  // coro_rpc_protocol.hpp:250
+inline constexpr uint32_t req_head_len = 20, resp_head_len = 16;
+
+// requests of function `function_id`; message i carries seq_num = seq_base + i
+inline spk_frame request(uint32_t function_id, uint32_t seq_base = 0,
+                         uint32_t attach_length = 0) {
+  spk_frame f{};
+  f.prefix_len = req_head_len;
+  f.seq_off = 4;
+  f.len_off = 12;
+  f.seq_base = seq_base;
+  f.tmpl[0] = magic_number;  // version, serialize_type, msg_type = 0
+  for (int k = 0; k < 4; ++k) {
+    f.tmpl[8 + k] = (uint8_t)(function_id >> (8 * k));
+    f.tmpl[16 + k] = (uint8_t)(attach_length >> (8 * k));
+  }
+  return f;
+}
+
+// responses echoing seq_num = seq_base + i
+inline spk_frame response(uint32_t seq_base = 0, uint8_t err_code = 0) {
+  spk_frame f{};
+  f.prefix_len = resp_head_len;
+  f.seq_off = 4;
+  f.len_off = 8;
+  f.seq_base = seq_base;
+  f.tmpl[0] = magic_number;
+  f.tmpl[2] = err_code;
+  return f;
+}
+}  // namespace rpc_frame
+
+// n framed messages [frame prefix][serialize(v[i])]; offsets = frame starts
+template <uint64_t conf = sp_config::DEFAULT, typename R>
+std::vector<char> serialize_frames(const std::vector<R> &v, const spk_frame &f,
+                                   std::vector<uint64_t> &offsets) {
+  auto &c = device::thread_codec<R, conf>();
+  auto b = c.upload(v.data(), v.size());
+  spk_plan_t p = c.plan(b, SPK_MODE_MESSAGES);
+  const std::size_t total = p.total_bytes + v.size() * (std::size_t)f.prefix_len;
+  device::buffer out(total), offs((v.size() + 1) * sizeof(uint64_t));
+  c.encode_framed(b, f, out.data(), out.size(), (uint64_t *)offs.data());
+  std::vector<char> bytes(total);
+  offsets.resize(v.size() + 1);
+  device::copy(bytes.data(), out.data(), bytes.size(), SPK_COPY_D2H, c.stream());
+  device::copy(offsets.data(), offs.data(), offsets.size() * 8, SPK_COPY_D2H, c.stream());
+  device::sync(c.stream());
+  return bytes;
+}
+
+// frames data[offsets[i], offsets[i+1]) with a prefix_len-byte header each
+template <uint64_t conf = sp_config::DEFAULT, typename R>
+std::vector<err_code> deserialize_frames(std::vector<R> &out, const char *data, std::size_t size,
+                                         const std::vector<uint64_t> &offsets,
+                                         uint32_t prefix_len) {
+  return deserialize_messages<conf>(out, data, size, offsets, prefix_len);
+}
+
+#if SPK_GPU_WITH_REFERENCE
+// next to the reference our constexpr type hash must be the reference's:
+// checked at compile time for every message type the GPU path sees
+template <typename T>
+constexpr bool hash_matches_reference() {
+  return get_type_code<T>() == struct_pack::get_type_code<T>();
+}
+#endif
+
+}  // namespace struct_pack::gpu

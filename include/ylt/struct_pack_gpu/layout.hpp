@@ -1,4 +1,4 @@
-// spk_layout.hpp — host C++20 reflection -> spk_layout descriptor, and the
+// layout.hpp — host C++20 reflection -> spk_layout descriptor, and the
 // host-object <-> device-record marshalling used when a batch starts or ends
 // in host memory (coro_rpc socket buffers).
 //
@@ -20,10 +20,10 @@
 #include <vector>
 
 #include "../../spk_codec.h"
-#include "spk_type_code.hpp"
+#include "type_code.hpp"
 
-namespace struct_pack {
-namespace spk_detail {
+namespace struct_pack::gpu {
+namespace detail {
 
 struct layout_builder {
   spk_layout L{};
@@ -64,8 +64,8 @@ template <typename T>
 void flatten_into(layout_builder &b) {
   if constexpr (is_trivially_serializable<T>()) {
     b.copy(sizeof(T), alignof(T));
-  } else if constexpr (is_varint<T>::value) {
-    b.varint(sizeof(typename T::value_type), T::zigzag);
+  } else if constexpr (is_varint_v<T>) {
+    b.varint(sizeof(typename varint_traits<T>::value_type), varint_traits<T>::zigzag);
   } else if constexpr (is_string_v<T>) {
     b.span(1);
   } else if constexpr (is_container_v<T>) {
@@ -120,12 +120,12 @@ constexpr uint32_t msg_flags() {
   return f;
 }
 
-}  // namespace spk_detail
+}  // namespace detail
 
 // Descriptor of record type T for the batch codec (cacheable, immutable).
 template <typename T, uint64_t conf = sp_config::DEFAULT>
 spk_layout make_spk_layout() {
-  using namespace spk_detail;
+  using namespace detail;
   layout_builder b;
   b.L.abi = SPK_ABI_VERSION;
   flatten_into<T>(b);
@@ -133,7 +133,9 @@ spk_layout make_spk_layout() {
     b.L.flags = SPK_LAYOUT_TRIVIAL;
     b.L.rec_stride = sizeof(T);
   } else {
-    const uint32_t al = b.align < 4 ? 4 : b.align;
+    // non-trivial device records are 8-byte aligned (the kernels read span
+    // offsets as u64): a record of 4-byte members and varints rounds up too
+    const uint32_t al = b.align < 8 ? 8 : b.align;
     b.L.rec_stride = (b.off + al - 1) / al * al;
   }
   fill_fmt(b.L.fmt_vector, get_type_code<std::vector<T>>(),
@@ -142,7 +144,7 @@ spk_layout make_spk_layout() {
   return b.L;
 }
 
-namespace spk_detail {
+namespace detail {
 
 // ---- host object <-> device record ----------------------------------------
 struct marshal_state {
@@ -168,9 +170,10 @@ template <typename T>
 void to_device(const T &v, marshal_state &s) {
   if constexpr (is_trivially_serializable<T>()) {
     put_copy(s, &v, sizeof(T));
-  } else if constexpr (is_varint<T>::value) {
+  } else if constexpr (is_varint_v<T>) {
     const spk_op &op = s.L->ops[s.op++];
-    std::memcpy(s.rec + op.rec_off, &v.get(), op.size);
+    const typename varint_traits<T>::value_type x = v;
+    std::memcpy(s.rec + op.rec_off, &x, op.size);
   } else if constexpr (is_string_v<T> || is_container_v<T>) {
     const spk_op &op = s.L->ops[s.op++];
     auto &heap = (*s.heaps)[s.span++];
@@ -220,9 +223,11 @@ template <typename T>
 void from_device(T &v, unmarshal_state &s) {
   if constexpr (is_trivially_serializable<T>()) {
     get_copy(s, &v, sizeof(T));
-  } else if constexpr (is_varint<T>::value) {
+  } else if constexpr (is_varint_v<T>) {
     const spk_op &op = s.L->ops[s.op++];
-    std::memcpy(&v.get(), s.rec + op.rec_off, op.size);
+    typename varint_traits<T>::value_type x;
+    std::memcpy(&x, s.rec + op.rec_off, op.size);
+    v = x;
   } else if constexpr (is_string_v<T> || is_container_v<T>) {
     const spk_op &op = s.L->ops[s.op++];
     const uint8_t *heap = s.heaps[s.span++];
@@ -258,5 +263,5 @@ void from_device(T &v, unmarshal_state &s) {
   }
 }
 
-}  // namespace spk_detail
-}  // namespace struct_pack
+}  // namespace detail
+}  // namespace struct_pack::gpu

@@ -1,12 +1,15 @@
-// spk_reflect.hpp — compile-time reflection for the MI355X struct_pack front
-// end (our own implementation; behaviour follows the reference's
-// ylt::reflection member_count.hpp:158-209 / member_ptr.hpp:95-137 for
-// aggregates): member count by brace-initialisation probing, member access
-// by structured bindings.
+// reflect.hpp — compile-time reflection for the MI355X struct_pack front end
+// (our own implementation; behaviour follows the reference's ylt::reflection,
+// member_count.hpp:158-209 / member_ptr.hpp:95-137): aggregates by
+// brace-initialisation member counting and structured bindings; non-aggregate
+// types (or a chosen member list) through YLT_REFL(Type, member...), whose
+// members are whatever refl_object_to_tuple ties (data members or accessor
+// calls, user_reflect_macro.hpp:27-57).
 //
 // Supported members: fundamentals, enums, std::string / std::string_view,
-// std::vector<T> / std::span<T>, std::array<T, N>, and nested aggregates.
-// (C arrays inside aggregates defeat brace-init counting — use std::array.)
+// std::vector<T> / std::span<T>, std::array<T, N>, std::optional<T>, the
+// varint types, and nested records. (C arrays inside aggregates defeat
+// brace-init counting -- use std::array.)
 #pragma once
 #include <array>
 #include <cstddef>
@@ -20,54 +23,9 @@
 #include <utility>
 #include <vector>
 
-namespace struct_pack {
+#include "config.hpp"
 
-// sp_config (ref include/ylt/struct_pack/reflection.hpp:53-60)
-enum sp_config : uint64_t {
-  DEFAULT = 0,
-  DISABLE_TYPE_INFO = 0b1,
-  ENABLE_TYPE_INFO = 0b10,
-  DISABLE_ALL_META_INFO = 0b11,
-  ENCODING_WITH_VARINT = 0b100,
-  USE_FAST_VARINT = 0b1000
-};
-
-namespace spk_detail {
-
-// var_int32_t / var_int64_t (zigzag) and var_uint32_t / var_uint64_t: an
-// integer wrapper with the reference's interface (varint.hpp:79-185,352-355)
-template <typename T, bool ZigZag>
-class varint_value {
- public:
-  using value_type = T;
-  static constexpr bool zigzag = ZigZag;
-  varint_value() noexcept = default;
-  varint_value(T t) noexcept : val(t) {}
-  [[nodiscard]] operator T() const noexcept { return val; }
-  varint_value &operator=(T t) noexcept {
-    val = t;
-    return *this;
-  }
-  [[nodiscard]] bool operator==(const varint_value &o) const noexcept { return val == o.val; }
-  [[nodiscard]] bool operator==(T t) const noexcept { return val == t; }
-  [[nodiscard]] bool operator<(const varint_value &o) const noexcept { return val < o.val; }
-  const T &get() const noexcept { return val; }
-  T &get() noexcept { return val; }
-
- private:
-  T val{};
-};
-template <typename T> struct is_varint : std::false_type {};
-template <typename T, bool Z> struct is_varint<varint_value<T, Z>> : std::true_type {};
-
-}  // namespace spk_detail
-
-using var_int32_t = spk_detail::varint_value<int32_t, true>;
-using var_int64_t = spk_detail::varint_value<int64_t, true>;
-using var_uint32_t = spk_detail::varint_value<uint32_t, false>;
-using var_uint64_t = spk_detail::varint_value<uint64_t, false>;
-
-namespace spk_detail {
+namespace struct_pack::gpu::detail {
 
 template <typename T>
 using remove_cvref_t = std::remove_cv_t<std::remove_reference_t<T>>;
@@ -88,14 +46,19 @@ constexpr bool is_container_v = is_std_vector<T>::value || is_std_span<T>::value
 template <typename T>
 constexpr bool is_fundamental_v = std::is_arithmetic_v<T> || std::is_enum_v<T>;
 template <typename T>
-constexpr bool is_record_v = std::is_aggregate_v<T> && std::is_class_v<T> &&
-                             !is_std_array<T>::value && !is_string_v<T> && !is_container_v<T> &&
-                             !is_std_optional<T>::value && !is_varint<T>::value;
+constexpr bool is_varint_v = varint_traits<T>::value;
+template <typename T>
+constexpr bool is_aggregate_record_v = std::is_aggregate_v<T> && std::is_class_v<T> &&
+                                       !is_std_array<T>::value && !is_string_v<T> &&
+                                       !is_container_v<T> && !is_std_optional<T>::value &&
+                                       !is_varint_v<T> && !is_ylt_refl_v<T>;
+template <typename T>
+constexpr bool is_record_v = is_aggregate_record_v<T> || (std::is_class_v<T> && is_ylt_refl_v<T>);
 
 // ---- aggregate member count (brace-init probing) ----------------------------
 struct any_init {
   template <typename T>
-  constexpr operator T() const noexcept;  // unevaluated only
+  operator T() const noexcept;  // unevaluated only (never defined)
 };
 
 template <typename T, std::size_t... I>
@@ -117,7 +80,8 @@ constexpr std::size_t members_count_impl() {
 template <typename T>
 constexpr std::size_t members_count_v = members_count_impl<T>();
 
-// ---- tie members by structured bindings --------------------------------------
+// ---- tie members: refl_object_to_tuple for YLT_REFL types, structured
+// bindings for aggregates ------------------------------------------------------
 #define SPK_TIE_CASE(N, ...)                   \
   else if constexpr (n == N) {                 \
     auto &&[__VA_ARGS__] = obj;                \
@@ -125,7 +89,7 @@ constexpr std::size_t members_count_v = members_count_impl<T>();
   }
 
 template <typename T>
-constexpr auto tie_members(T &&obj) {
+constexpr auto tie_aggregate(T &obj) {
   using U = remove_cvref_t<T>;
   constexpr std::size_t n = members_count_v<U>;
   static_assert(n <= 24, "struct_pack MI355X front end: at most 24 members per aggregate");
@@ -166,16 +130,24 @@ constexpr auto tie_members(T &&obj) {
 }
 #undef SPK_TIE_CASE
 
-// member types as a tuple of values (for compile-time walks)
 template <typename T>
-using members_tuple_t =
-    decltype(std::apply([](auto &...m) { return std::tuple<remove_cvref_t<decltype(m)>...>{}; },
-                        tie_members(std::declval<T &>())));
-
-template <typename T, typename F>
-constexpr void visit_members(T &obj, F &&f) {
-  std::apply([&](auto &...m) { (f(m), ...); }, tie_members(obj));
+constexpr auto tie_members(T &obj) {
+  if constexpr (is_ylt_refl_v<remove_cvref_t<T>>)
+    return refl_tuple(obj);
+  else
+    return tie_aggregate(obj);
 }
+
+// member types as a tuple of values (for compile-time walks; no lambda in
+// the unevaluated operand, which g++ 11 does not survive)
+template <typename Tup>
+struct decay_tuple;
+template <typename... A>
+struct decay_tuple<std::tuple<A...>> {
+  using type = std::tuple<remove_cvref_t<A>...>;
+};
+template <typename T>
+using members_tuple_t = typename decay_tuple<decltype(tie_members(std::declval<T &>()))>::type;
 
 // ---- per-type sp_config: ADL set_sp_config(T*) or T::struct_pack_config
 // (ref type_calculate.hpp:158-172) -----------------------------------------
@@ -194,5 +166,4 @@ constexpr uint64_t type_config() {
     return sp_config::DEFAULT;
 }
 
-}  // namespace spk_detail
-}  // namespace struct_pack
+}  // namespace struct_pack::gpu::detail

@@ -1,4 +1,4 @@
-// spk_type_code.hpp — compile-time type literal and 32-bit type code of the
+// type_code.hpp — compile-time type literal and 32-bit type code of the
 // MI355X struct_pack front end (our own implementation of the reference's
 // wire contract):
 //   type_id bytes           ref include/ylt/struct_pack/type_id.hpp:25-81
@@ -7,15 +7,17 @@
 //   code = MD5_32 & ~1       ref type_calculate.hpp:507-516, md5_constexpr.hpp
 //   is_trivial_serializable  ref reflection.hpp:851-922
 //   check_if_has_container   ref type_calculate.hpp:793-857
+//   pack / alignment literal ref alignment.hpp:23-122 (user overrides
+//                            struct_pack::pack_alignment_v / alignment_v)
 // The MD5 below is a straightforward constexpr RFC 1321 implementation.
 #pragma once
 #include <array>
 #include <cstdint>
 
-#include "spk_reflect.hpp"
+#include "reflect.hpp"
 
-namespace struct_pack {
-namespace spk_detail {
+namespace struct_pack::gpu {
+namespace detail {
 
 // ---- fixed-capacity constexpr byte string ----------------------------------
 struct lit_t {
@@ -87,8 +89,10 @@ constexpr bool is_trivially_serializable() {
   } else if constexpr (is_std_array<T>::value) {
     return is_trivially_serializable<typename T::value_type>();
   } else if constexpr (is_string_v<T> || is_container_v<T> || is_std_optional<T>::value ||
-                       is_varint<T>::value) {
+                       is_varint_v<T>) {
     return false;  // reflection.hpp:872,899-901
+  } else if constexpr (is_ylt_refl_v<T>) {
+    return false;  // user_defined_refl: member by member (reflection.hpp:896-898)
   } else {
     static_assert(is_record_v<T>, "unsupported member type");
     using M = members_tuple_t<T>;
@@ -115,17 +119,56 @@ constexpr bool has_container() {
     return false;
 }
 
-// alignment_v (alignment.hpp:90-122) without alignas/pragma-pack overrides
+// max over the members' alignment (alignment.hpp:33-41,63-71)
+template <typename T>
+constexpr std::size_t alignment_of();
+template <typename M, std::size_t... I>
+constexpr std::size_t max_member_alignment(std::index_sequence<I...>) {
+  std::size_t a = 0;
+  ((a = alignment_of<std::tuple_element_t<I, M>>() > a ? alignment_of<std::tuple_element_t<I, M>>()
+                                                        : a),
+   ...);
+  return a;
+}
+
+// pack_alignment_v (alignment.hpp:72-88): the user's struct_pack::
+// pack_alignment_v<T> when set (#pragma pack), else the largest member
+// alignment
+template <typename T>
+constexpr std::size_t pack_alignment_of() {
+  constexpr std::size_t user = user_pack_alignment<T>;
+  static_assert(user == 0 || user == 1 || user == 2 || user == 4 || user == 8 || user == 16,
+                "struct_pack::pack_alignment_v must be 0, 1, 2, 4, 8 or 16");
+  if constexpr (user != 0) {
+    return user;
+  } else {
+    using M = members_tuple_t<T>;
+    return max_member_alignment<M>(std::make_index_sequence<std::tuple_size_v<M>>{});
+  }
+}
+
+// alignment_v (alignment.hpp:90-122): the user's struct_pack::alignment_v<T>
+// when set (it must equal alignof for a trivially serializable type);
+// otherwise alignof for trivially serializable / non-record types and, for a
+// non-trivial record, the user's pack alignment or the largest member
+// alignment
 template <typename T>
 constexpr std::size_t alignment_of() {
-  if constexpr (is_record_v<T> && !is_trivially_serializable<T>()) {
-    using M = members_tuple_t<T>;
-    return []<std::size_t... I>(std::index_sequence<I...>) {
-      std::size_t a = 0;
-      ((a = alignment_of<std::tuple_element_t<I, M>>() > a
-                ? alignment_of<std::tuple_element_t<I, M>>() : a), ...);
-      return a;
-    }(std::make_index_sequence<std::tuple_size_v<M>>{});
+  if constexpr (is_record_v<T>) {
+    constexpr std::size_t user = user_alignment<T>;
+    if constexpr (user != 0) {
+      static_assert((user & (user - 1)) == 0, "alignment should be power of 2");
+      if constexpr (is_trivially_serializable<T>())
+        static_assert(user == alignof(T), "struct_pack::alignment_v must equal alignof(T)");
+      return user;
+    } else if constexpr (is_trivially_serializable<T>()) {
+      return alignof(T);
+    } else if constexpr (user_pack_alignment<T> != 0) {
+      return user_pack_alignment<T>;
+    } else {
+      using M = members_tuple_t<T>;
+      return max_member_alignment<M>(std::make_index_sequence<std::tuple_size_v<M>>{});
+    }
   } else {
     return alignof(T);
   }
@@ -150,10 +193,10 @@ constexpr lit_t type_literal() {
   } else if constexpr (is_container_v<T>) {
     l.push(TID_CONTAINER);
     l.append(type_literal<remove_cvref_t<typename T::value_type>>());
-  } else if constexpr (is_varint<T>::value) {  // get_varint_type (type_id.hpp:84-125)
-    using V = typename T::value_type;
-    l.push(sizeof(V) == 4 ? (T::zigzag ? TID_VINT32 : TID_VUINT32)
-                          : (T::zigzag ? TID_VINT64 : TID_VUINT64));
+  } else if constexpr (is_varint_v<T>) {  // get_varint_type (type_id.hpp:84-125)
+    using V = typename varint_traits<T>::value_type;
+    constexpr bool zz = varint_traits<T>::zigzag;
+    l.push(sizeof(V) == 4 ? (zz ? TID_VINT32 : TID_VUINT32) : (zz ? TID_VINT64 : TID_VUINT64));
   } else if constexpr (is_std_optional<T>::value) {  // type_calculate.hpp:273-278
     l.push(TID_OPTIONAL);
     l.append(type_literal<remove_cvref_t<typename T::value_type>>());
@@ -166,14 +209,12 @@ constexpr lit_t type_literal() {
     using M = members_tuple_t<T>;
     l.push(TID_STRUCT);
     append_members<M>(l, std::make_index_sequence<std::tuple_size_v<M>>{});
-    if constexpr (is_trivially_serializable<T>()) {
-      std::size_t pack = 1;
-      [&]<std::size_t... I>(std::index_sequence<I...>) {
-        ((pack = alignment_of<std::tuple_element_t<I, M>>() > pack
-                     ? alignment_of<std::tuple_element_t<I, M>>() : pack), ...);
-      }(std::make_index_sequence<std::tuple_size_v<M>>{});
-      l.append(size_literal(pack));
-      l.append(size_literal(alignof(T)));
+    if constexpr (is_trivially_serializable<T>()) {  // type_calculate.hpp:229-239
+      static_assert(pack_alignment_of<T>() <= alignment_of<T>(),
+                    "If you add #pragma pack to a struct, please specify "
+                    "struct_pack::pack_alignment_v<T>.");
+      l.append(size_literal(pack_alignment_of<T>()));
+      l.append(size_literal(alignment_of<T>()));
     }
     l.push(TID_END);
   }
@@ -243,16 +284,16 @@ constexpr uint32_t md5_hash32(const lit_t &l) {
          (static_cast<uint32_t>(d[2]) << 8) | static_cast<uint32_t>(d[3]);
 }
 
-}  // namespace spk_detail
+}  // namespace detail
 
 // Public: get_type_literal / get_type_code of one type (struct_pack.hpp:75-110)
 template <typename T>
 constexpr auto get_type_literal() {
-  return spk_detail::type_literal<spk_detail::remove_cvref_t<T>>();
+  return detail::type_literal<detail::remove_cvref_t<T>>();
 }
 template <typename T>
 constexpr uint32_t get_type_code() {
-  return spk_detail::md5_hash32(get_type_literal<T>()) & 0xFFFFFFFEu;
+  return detail::md5_hash32(get_type_literal<T>()) & 0xFFFFFFFEu;
 }
 
-}  // namespace struct_pack
+}  // namespace struct_pack::gpu

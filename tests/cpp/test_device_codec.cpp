@@ -9,10 +9,14 @@
 #include <string>
 #include <vector>
 
-#include "ylt/struct_pack.hpp"
+#include "ylt/struct_pack_gpu.hpp"
 #include "../../oracle/ref/types.hpp"
 
-using namespace struct_pack;
+// the GPU front end's names; compiled both standalone and next to the
+// reference header (then errc / sp_config / var_int*_t are the reference's)
+using namespace struct_pack::gpu;
+using struct_pack::errc;
+using struct_pack::sp_config;
 static int g_fail = 0, g_checks = 0;
 #define CHECK(c)                                                        \
   do {                                                                  \

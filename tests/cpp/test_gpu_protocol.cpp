@@ -1,0 +1,191 @@
+// GPU: coro_rpc's serialize-protocol seam with the MI355X codec behind it.
+//
+// Built NEXT TO THE REFERENCE (-I /root/reference/include ...): the reference's
+// coro_rpc handler executor (rpc_execute.hpp:56-179) runs a batch handler with
+// struct_pack_gpu_protocol as its serialize protocol, and every byte is
+// compared with the reference's own struct_pack_protocol on the same values
+// (computed in this process by the reference's CPU struct_pack) and with the
+// committed reference-built fixtures. Also checks that the front end's type
+// codes equal the reference's at compile time. The binary is built by
+// __graft_entry__.build() into oracle/_ref/ (it contains reference code) and
+// run by tests/test_gpu_cpp.py on the GPU box.
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iterator>
+#include <string>
+#include <vector>
+
+#include <ylt/coro_rpc/impl/protocol/coro_rpc_protocol.hpp>
+#include <ylt/coro_rpc/impl/protocol/struct_pack_gpu_protocol.hpp>
+#include <ylt/coro_rpc/impl/rpc_execute.hpp>
+
+#include "../../oracle/ref/types.hpp"
+
+static_assert(SPK_GPU_WITH_REFERENCE, "build with the reference on the include path");
+
+using coro_rpc::protocol::struct_pack_gpu_protocol;
+using coro_rpc::protocol::struct_pack_protocol;
+using rpc_protocol = coro_rpc::protocol::coro_rpc_protocol;
+
+static int g_fail = 0, g_checks = 0;
+#define CHECK(c)                                                                 \
+  do {                                                                           \
+    ++g_checks;                                                                  \
+    if (!(c)) {                                                                  \
+      ++g_fail;                                                                  \
+      std::fprintf(stderr, "%s:%d: CHECK(%s) failed\n", __FILE__, __LINE__, #c); \
+    }                                                                            \
+  } while (0)
+
+// our constexpr type hash == the reference's, for every type the tests use
+template <typename... T>
+constexpr bool all_match() {
+  return (struct_pack::gpu::hash_matches_reference<T>() && ...);
+}
+static_assert(all_match<Rec64, RecS, Inner, Outer, Pad, Mixed, Opt, OptP, Var, VarP,
+                        rpcb::point, rpcb::rect, rpcb::person, rect<int>>());
+static_assert(all_match<std::vector<Rec64>, std::vector<RecS>, std::vector<Outer>,
+                        std::vector<Mixed>, std::vector<Opt>, std::vector<Var>,
+                        std::vector<rpcb::person>, std::vector<rect<int>>>());
+
+static std::string golden(const std::string &name) {
+  std::ifstream f(std::string(SPK_GOLDEN_DIR) + "/" + name, std::ios::binary);
+  return std::string((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+}
+
+bool operator==(const RecS &a, const RecS &b) { return a.id == b.id && a.name == b.name && a.v == b.v; }
+bool operator==(const Inner &a, const Inner &b) { return a.x == b.x && a.y == b.y; }
+bool operator==(const Outer &a, const Outer &b) { return a.key == b.key && a.items == b.items; }
+namespace rpcb {
+bool operator==(const person &a, const person &b) {
+  return a.id == b.id && a.name == b.name && a.age == b.age && a.salary == b.salary;
+}
+}  // namespace rpcb
+
+// ---- handlers: what a coro_rpc service registers ------------------------------
+std::vector<RecS> echo_recs(std::vector<RecS> v) { return v; }
+std::vector<Outer> reverse_outer(std::vector<Outer> v) {
+  std::reverse(v.begin(), v.end());
+  return v;
+}
+int count_people(std::vector<rpcb::person> v) { return (int)v.size(); }  // batch in, int out
+std::string greet(rpcb::person p, int times) {                           // not a batch: CPU path
+  std::string s;
+  for (int i = 0; i < times; ++i) s += p.name;
+  return s;
+}
+
+// the executor as coro_rpc's router calls it (router.hpp:155-163)
+template <auto func, typename Proto>
+std::pair<coro_rpc::err_code, std::string> run(std::string_view args) {
+  coro_rpc::rpc_context<rpc_protocol> ctx;  // handlers above take no context
+  return coro_rpc::internal::execute<rpc_protocol, Proto, func>(args, ctx);
+}
+
+template <auto func, typename Arg>
+void same_as_reference(const Arg &arg, const char *what) {
+  // the request payload a coro_rpc client sends (rpc_execute / client pack:
+  // one argument -> serialize(arg))
+  const std::string req = struct_pack::serialize<std::string>(arg);
+  auto ref = run<func, struct_pack_protocol>(req);
+  auto gpu = run<func, struct_pack_gpu_protocol>(req);
+  CHECK(!ref.first && !gpu.first);
+  CHECK(ref.second == gpu.second);
+  if (ref.second != gpu.second) std::fprintf(stderr, "  mismatch in %s\n", what);
+}
+
+int main() {
+  using namespace spk_gold;
+  // force the GPU path for every batch size in this test
+  struct_pack_gpu_protocol::min_gpu_bytes = 0;
+  struct_pack_gpu_protocol::min_gpu_records = 0;
+  const uint64_t S3 = 0x5EED0003, S4 = 0x5EED0004, S8 = 0x5EED0008;
+
+  // 1. the protocol statics against the reference protocol and fixtures
+  {
+    std::vector<RecS> v(300);
+    for (uint64_t i = 0; i < v.size(); ++i) v[i] = make_recs(S3, i, 48);
+    const std::string want = golden("recs_A_n300_p48_default.bin");
+    CHECK(!want.empty());
+    const std::string g = struct_pack_gpu_protocol::serialize(v);
+    CHECK(g == want);
+    CHECK(g == struct_pack_protocol::serialize(v));
+    std::tuple<std::vector<RecS>> args;
+    CHECK(struct_pack_gpu_protocol::deserialize_to(args, want));
+    CHECK(std::get<0>(args) == v);
+    // a corrupted head: the protocol reports failure like the reference's
+    std::string bad = want;
+    bad[0] ^= 0x10;
+    std::tuple<std::vector<RecS>> args2;
+    CHECK(!struct_pack_gpu_protocol::deserialize_to(args2, bad));
+    CHECK(!struct_pack_protocol::deserialize_to(args2, bad));
+    // truncated: no_buffer_space on both
+    std::tuple<std::vector<RecS>> args3;
+    CHECK(!struct_pack_gpu_protocol::deserialize_to(args3, std::string_view(want).substr(0, want.size() - 3)));
+  }
+  {
+    std::vector<Outer> v(1000);
+    for (uint64_t i = 0; i < v.size(); ++i) v[i] = make_outer(S4, i, 16);
+    const std::string want = golden("outer_A_n1000_p16_default.bin");
+    CHECK(struct_pack_gpu_protocol::serialize(v) == want);
+    std::tuple<std::vector<Outer>> args;
+    CHECK(struct_pack_gpu_protocol::deserialize_to(args, want));
+    CHECK(std::get<0>(args) == v);
+  }
+  // 2. the reference's handler executor with the GPU protocol
+  {
+    std::vector<RecS> v(5000);
+    for (uint64_t i = 0; i < v.size(); ++i) v[i] = make_recs(S3, i, 48);
+    same_as_reference<echo_recs>(v, "echo_recs");
+    std::vector<Outer> o(3000);
+    for (uint64_t i = 0; i < o.size(); ++i) o[i] = make_outer(S4, i, 16);
+    same_as_reference<reverse_outer>(o, "reverse_outer");
+    std::vector<rpcb::person> p(700);
+    for (uint64_t i = 0; i < p.size(); ++i) p[i] = make_person(S8, i, 64);
+    same_as_reference<count_people>(p, "count_people");
+    // an empty batch and a one-record batch
+    same_as_reference<echo_recs>(std::vector<RecS>{}, "echo_recs(empty)");
+    same_as_reference<echo_recs>(std::vector<RecS>{make_recs(S3, 7, 48)}, "echo_recs(1)");
+    // two arguments: not a batch message, served by the reference codec
+    const std::string req =
+        struct_pack::serialize<std::string>(std::make_tuple(make_person(S8, 1, 10), 3));
+    auto ref = run<greet, struct_pack_protocol>(req);
+    auto gpu = run<greet, struct_pack_gpu_protocol>(req);
+    CHECK(!ref.first && !gpu.first && ref.second == gpu.second);
+    // a malformed request: coro_rpc's invalid_rpc_arguments on both paths
+    std::string bad = struct_pack::serialize<std::string>(v);
+    bad.resize(bad.size() / 2);
+    auto rb = run<echo_recs, struct_pack_protocol>(bad);
+    auto gb = run<echo_recs, struct_pack_gpu_protocol>(bad);
+    CHECK(rb.first && gb.first && rb.first.val() == gb.first.val());
+  }
+  // 3. the front end's single-record and reference-order entry points next to
+  // the reference: identical bytes for one record message, deserialize<conf, T>
+  {
+    const rpcb::person p = make_person(S8, 3, 64);
+    const auto want = struct_pack::serialize<std::string>(p);
+    CHECK(struct_pack::gpu::serialize<std::string>(p) == want);
+    auto sz = struct_pack::gpu::get_needed_size(p);
+    auto rsz = struct_pack::get_needed_size(p);
+    CHECK(sz.size() == rsz.size() && sz.metainfo() == rsz.metainfo());
+    std::string buf(sz.size(), '\0');
+    struct_pack::gpu::serialize_to(buf.data(), sz, p);
+    CHECK(buf == want);
+    std::string buf2(rsz.size(), '\0');
+    struct_pack::gpu::serialize_to(buf2.data(), rsz, p);  // the reference's size object
+    CHECK(buf2 == want);
+    auto r = struct_pack::gpu::deserialize<struct_pack::sp_config::DEFAULT, rpcb::person>(want);
+    CHECK(r.has_value() && r.value() == p);
+    auto f = struct_pack::gpu::get_field<rpcb::person, 1>(want);
+    auto rf = struct_pack::get_field<rpcb::person, 1>(want);
+    CHECK(f.has_value() && rf.has_value() && f.value() == rf.value());
+    std::string off;
+    struct_pack::gpu::serialize_to_with_offset(off, 20, p);
+    std::string roff;
+    struct_pack::serialize_to_with_offset(roff, 20, p);
+    CHECK(off.size() == roff.size() && off.substr(20) == roff.substr(20));
+  }
+  std::printf("{\"checks\": %d, \"failures\": %d}\n", g_checks, g_fail);
+  return g_fail ? 1 : 0;
+}

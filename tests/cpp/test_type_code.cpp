@@ -5,10 +5,11 @@
 #include <cstdio>
 #include <string>
 
-#include "ylt/struct_pack/spk_layout.hpp"
+#include "ylt/struct_pack_gpu/layout.hpp"
 #include "../../oracle/ref/types.hpp"
 
 using namespace struct_pack;
+using namespace struct_pack::gpu;
 
 // compile-time checks against the reference's KATs
 static_assert(get_type_code<Rec64>() == 0xd3e789e0u);
@@ -18,17 +19,17 @@ static_assert(get_type_code<std::vector<RecS>>() == 0xd2c6fa72u);
 static_assert(get_type_code<std::vector<Outer>>() == 0xfea939d6u);
 static_assert(get_type_code<rect<int>>() == 0x5d2be0aau);
 static_assert(get_type_code<std::vector<rect<int>>>() == 0xe8fa8a7cu);
-static_assert(spk_detail::is_trivially_serializable<Rec64>());
-static_assert(!spk_detail::is_trivially_serializable<RecS>());
-static_assert(spk_detail::members_count_v<Mixed> == 5);
-static_assert(spk_detail::members_count_v<Opt> == 4);
+static_assert(gpu::detail::is_trivially_serializable<Rec64>());
+static_assert(!gpu::detail::is_trivially_serializable<RecS>());
+static_assert(gpu::detail::members_count_v<Mixed> == 5);
+static_assert(gpu::detail::members_count_v<Opt> == 4);
 static_assert(get_type_code<Opt>() == 3223865924u);   // kat.json "Opt"
 static_assert(get_type_code<OptP>() == 3947683952u);  // kat.json "OptP"
-static_assert(!spk_detail::has_container<OptP>());
+static_assert(!gpu::detail::has_container<OptP>());
 static_assert(get_type_code<Var>() == 3170970548u);    // kat.json "Var"
 static_assert(get_type_code<VarP>() == 2257901056u);  // kat.json "VarP"
-static_assert(!spk_detail::is_trivially_serializable<VarP>());
-static_assert(!spk_detail::has_container<VarP>());
+static_assert(!gpu::detail::is_trivially_serializable<VarP>());
+static_assert(!gpu::detail::has_container<VarP>());
 
 template <typename T>
 static void lit_json(const char *name, bool &first) {

@@ -76,6 +76,11 @@ def test_layout_check_varint_ops():
         assert lib.spk_layout_check(L.ptr) == C.SPK_E_LAYOUT, (field, bad)
     # varints alone (no span / option) make a valid non-trivial record
     assert lib.spk_layout_check(LY.case_layout("varp").ptr) == 0
+    # ... also with only 4-byte neighbours: {int32; var_uint32_t; int32} has
+    # no 8-byte member, its device stride still rounds up to 8 (12 -> 16)
+    t = S.Struct("V4", [("a", S.int32), ("b", S.var_uint32), ("c", S.int32)])
+    L4 = LY.make_layout(t)
+    assert L4.stride == 16 and lib.spk_layout_check(L4.ptr) == 0
 
 
 def test_encode_rejects_bad_args_without_device_work():

@@ -1,4 +1,4 @@
-"""CPU: the C++20 front end (include/ylt/struct_pack.hpp and friends).
+"""CPU: the C++20 front end (include/ylt/struct_pack_gpu.hpp and friends).
 
 Compiles tests/cpp/test_type_code.cpp host-only (it static_asserts the
 reference's type-code KATs at compile time) and checks its JSON against the
@@ -52,3 +52,73 @@ def test_cpp_and_python_descriptors_agree(cpp_json, case, conf):
                         for i in range(L.n_ops)]
     assert c["vec"] == [L.fmt_vector.code, L.fmt_vector.flags, L.fmt_vector.literal_len]
     assert c["one"] == [L.fmt_one.code, L.fmt_one.flags, L.fmt_one.literal_len]
+
+
+# ---- the front end compiles with the reference's toolchain and next to the
+# reference headers (the coro_rpc drop-in case) --------------------------------
+REF_INC = "/root/reference/include"
+
+
+def _compile(cxx, src, extra=(), syntax_only=True):
+    cmd = [cxx, "-std=c++20", "-DNDEBUG", "-I", os.path.join(ROOT, "include"), *extra]
+    cmd += ["-fsyntax-only", "-x", "c++", "-"] if syntax_only else []
+    return subprocess.run(cmd, input=src, capture_output=True, text=True)
+
+
+USE_FRONT_END = """
+#include <ylt/struct_pack_gpu.hpp>
+struct person { int64_t id; std::string name; int age; double salary; };
+struct refl_point { int x, y, z; };
+YLT_REFL(refl_point, x, y, z);
+struct with_varint { struct_pack::var_int32_t a; std::vector<int> b; };
+void use() {
+  std::vector<person> v;
+  auto buf = struct_pack::gpu::serialize(v);
+  auto r = struct_pack::gpu::deserialize<std::vector<person>>(buf);
+  auto r2 = struct_pack::gpu::deserialize<struct_pack::sp_config::DEFAULT, person>(buf);
+  std::size_t consumed = 0;
+  person p;
+  struct_pack::err_code ec = struct_pack::gpu::deserialize_to(p, buf, consumed);
+  (void)r; (void)r2; (void)ec;
+  static_assert(struct_pack::gpu::is_gpu_batch_v<std::vector<with_varint>>);
+  static_assert(!struct_pack::gpu::detail::is_trivially_serializable<refl_point>());
+  static_assert(struct_pack::gpu::get_type_code<refl_point>() !=
+                struct_pack::gpu::get_type_code<std::array<int, 3>>());
+}
+"""
+
+
+@pytest.mark.parametrize("cxx", ["g++", CLANG])
+def test_front_end_standalone_compiles(cxx):
+    """No HIP header and no reference needed: g++ 11 and clang both build a
+    caller of the front end (SPK_GPU_STANDALONE: our own vocabulary types)."""
+    r = _compile(cxx, USE_FRONT_END, ["-DSPK_GPU_STANDALONE"])
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_INC), reason="reference headers absent")
+@pytest.mark.parametrize("cxx", ["g++", CLANG])
+def test_protocol_compiles_next_to_reference(cxx):
+    """struct_pack_gpu_protocol.hpp with the reference's coro_rpc headers in
+    one translation unit: the GPU front end reuses the reference's errc /
+    sp_config / var_int types (no redefinition), and its constexpr type
+    codes equal the reference's (hash_matches_reference static_asserts)."""
+    src = USE_FRONT_END.replace(
+        "#include <ylt/struct_pack_gpu.hpp>",
+        "#include <ylt/coro_rpc/impl/protocol/coro_rpc_protocol.hpp>\n"
+        "#include <ylt/coro_rpc/impl/protocol/struct_pack_gpu_protocol.hpp>") + """
+static_assert(SPK_GPU_WITH_REFERENCE);
+static_assert(std::is_same_v<struct_pack::errc, decltype(struct_pack::err_code{}.ec)>);
+static_assert(struct_pack::gpu::hash_matches_reference<std::vector<person>>());
+static_assert(struct_pack::gpu::hash_matches_reference<refl_point>());
+static_assert(struct_pack::gpu::hash_matches_reference<std::vector<with_varint>>());
+void use_protocol() {
+  std::tuple<std::vector<person>> args;
+  (void)coro_rpc::protocol::struct_pack_gpu_protocol::deserialize_to(args, std::string_view{});
+  (void)coro_rpc::protocol::struct_pack_gpu_protocol::serialize(std::get<0>(args));
+  (void)coro_rpc::protocol::struct_pack_gpu_protocol::serialize(42);
+}
+"""
+    r = _compile(cxx, src, ["-I", REF_INC, "-I", REF_INC + "/ylt/thirdparty",
+                            "-I", REF_INC + "/ylt/standalone"])
+    assert r.returncode == 0, r.stderr[-3000:]

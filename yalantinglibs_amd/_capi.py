@@ -103,7 +103,11 @@ ORACLE_PATH = os.path.join(_ROOT, "oracle", "libspk_oracle.so")
 CODEC_SYMBOLS = ["spk_abi_version", "spk_errc_message", "spk_layout_check",
                  "spk_workspace_bytes", "spk_plan", "spk_encode", "spk_decode",
                  "spk_synth", "spk_synth_counts", "spk_encode_body",
-                 "spk_vector_header", "spk_encode_framed", "spk_decode_framed"]
+                 "spk_vector_header", "spk_encode_framed", "spk_decode_framed",
+                 # runtime helpers (front ends without HIP headers)
+                 "spk_device_alloc", "spk_device_free", "spk_host_alloc_pinned",
+                 "spk_host_free_pinned", "spk_copy_async", "spk_stream_create",
+                 "spk_stream_destroy", "spk_stream_sync"]
 
 _codec = None
 _oracle = None

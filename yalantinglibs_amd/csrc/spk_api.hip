@@ -101,6 +101,19 @@ static int frame_check(const spk_frame *F) {
   return SPK_OK;
 }
 
+// SPAN / OPTION members read their payloads from d_heaps[k]: a non-empty
+// batch needs every one of them (a layout of varints only may pass NULL)
+static int heaps_check(const spk_layout *L, uint64_t n, const void *const *d_heaps) {
+  uint32_t spans = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i)
+    spans += L->ops[i].kind == SPK_OP_SPAN || L->ops[i].kind == SPK_OP_OPTION;
+  if (!spans || !n) return SPK_OK;
+  if (!d_heaps) return SPK_E_ARG;
+  for (uint32_t k = 0; k < spans; ++k)
+    if (!d_heaps[k]) return SPK_E_ARG;
+  return SPK_OK;
+}
+
 static int encode_impl(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
                        const void *const *d_heaps, const spk_plan_t *d_plan, void *d_out,
                        uint64_t out_cap, uint64_t *d_msg_offsets, const spk_frame *F,
@@ -126,12 +139,7 @@ static int encode_impl(const spk_layout *L, int mode, uint64_t n, const void *d_
     return hip_rc(launch_fixed_encode_messages(L, n, d_recs, d_out, d_msg_offsets, F, s));
   }
   if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
-  uint32_t spans = 0;
-  for (uint32_t i = 0; i < L->n_ops; ++i)
-    spans += L->ops[i].kind == SPK_OP_SPAN || L->ops[i].kind == SPK_OP_OPTION;
-  if (!d_heaps && spans) return SPK_E_ARG;
-  for (uint32_t k = 0; k < spans; ++k)
-    if (!d_heaps[k] && n) return SPK_E_ARG;
+  if ((rc = heaps_check(L, n, d_heaps))) return rc;
   return hip_rc(launch_var_encode(L, mode, n, d_recs, d_heaps, d_plan, d_out, out_cap,
                                   d_msg_offsets, F, d_ws, ws_bytes, s));
 }
@@ -222,7 +230,8 @@ int spk_encode_body(const spk_layout *L, uint64_t n, const void *d_recs,
     if (nb > out_cap) return SPK_E_CAPACITY;
     return hip_rc(hipMemcpyAsync(d_out, d_recs, nb, hipMemcpyDeviceToDevice, s));
   }
-  if ((uintptr_t)d_recs % 8 || !d_heaps) return SPK_E_ARG;
+  if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
+  if ((rc = heaps_check(L, n, d_heaps))) return rc;
   return hip_rc(launch_var_encode_body(L, n, d_recs, d_heaps, width, d_out, out_cap, d_ws,
                                        ws_bytes, s));
 }
@@ -241,5 +250,43 @@ int spk_vector_header(const spk_layout *L, uint64_t total_n, uint32_t width, uin
   for (uint32_t i = 0; i < len; ++i) h_out[i] = hb[i];
   return (int)len;
 }
+
+// ---- runtime helpers: front ends in any language stage batches through
+// these, so none of them needs the HIP headers --------------------------------
+int spk_device_alloc(void **d_ptr, size_t bytes) {
+  if (!d_ptr) return SPK_E_ARG;
+  *d_ptr = nullptr;
+  return hip_rc(hipMalloc(d_ptr, bytes ? bytes : 1));
+}
+int spk_device_free(void *d_ptr) { return d_ptr ? hip_rc(hipFree(d_ptr)) : SPK_OK; }
+int spk_host_alloc_pinned(void **h_ptr, size_t bytes) {
+  if (!h_ptr) return SPK_E_ARG;
+  *h_ptr = nullptr;
+  return hip_rc(hipHostMalloc(h_ptr, bytes ? bytes : 1, hipHostMallocDefault));
+}
+int spk_host_free_pinned(void *h_ptr) { return h_ptr ? hip_rc(hipHostFree(h_ptr)) : SPK_OK; }
+int spk_copy_async(void *dst, const void *src, size_t bytes, int kind, void *stream) {
+  if (!bytes) return SPK_OK;
+  if (!dst || !src) return SPK_E_ARG;
+  hipMemcpyKind k;
+  switch (kind) {
+    case SPK_COPY_H2D: k = hipMemcpyHostToDevice; break;
+    case SPK_COPY_D2H: k = hipMemcpyDeviceToHost; break;
+    case SPK_COPY_D2D: k = hipMemcpyDeviceToDevice; break;
+    default: return SPK_E_ARG;
+  }
+  return hip_rc(hipMemcpyAsync(dst, src, bytes, k, (hipStream_t)stream));
+}
+int spk_stream_create(void **stream) {
+  if (!stream) return SPK_E_ARG;
+  hipStream_t s = nullptr;
+  const int rc = hip_rc(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  *stream = s;
+  return rc;
+}
+int spk_stream_destroy(void *stream) {
+  return stream ? hip_rc(hipStreamDestroy((hipStream_t)stream)) : SPK_OK;
+}
+int spk_stream_sync(void *stream) { return hip_rc(hipStreamSynchronize((hipStream_t)stream)); }
 
 }  // extern "C"

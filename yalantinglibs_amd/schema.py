@@ -1,5 +1,5 @@
 """Host-side type model for struct_pack records (Python mirror of the C++20
-reflection in include/ylt/struct_pack/spk_reflect.hpp).
+reflection in include/ylt/struct_pack_gpu/reflect.hpp).
 
 Computes, exactly as the reference does at compile time:
   * the type literal  — get_type_literal (ref include/ylt/struct_pack/
@@ -435,6 +435,9 @@ def flatten(rtype: SpType) -> DeviceLayout:
             merged[-1] = (k, o, s + op[2], a)
         else:
             merged.append(op)
-    align = max(cur[1], 4)
+    # non-trivial device records are 8-byte aligned (the kernels read span
+    # offsets as u64; spk_layout_check rejects other strides), also when the
+    # record has only 4-byte members and varints
+    align = max(cur[1], 8)
     stride = (cur[0] + align - 1) // align * align
     return DeviceLayout(rtype, stride, merged, spans, npf, False)
