@@ -307,6 +307,16 @@ int spk_stream_create(void **stream); /* non-blocking stream */
 int spk_stream_destroy(void *stream);
 int spk_stream_sync(void *stream);
 
+/* ---- kernel tracing ------------------------------------------------------
+ * Off by default. When enabled, every kernel the codec launches is bracketed
+ * by hipEvents on its stream; spk_trace_read (after the work completes)
+ * writes {"<kernel>": [launches, total_ms], ...} accumulated since the last
+ * reset into buf and returns the JSON length. For profiling runs: the events
+ * cost a few microseconds per launch. */
+int spk_trace_enable(int on);
+int spk_trace_reset(void);
+int spk_trace_read(char *buf, size_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -107,7 +107,9 @@ CODEC_SYMBOLS = ["spk_abi_version", "spk_errc_message", "spk_layout_check",
                  # runtime helpers (front ends without HIP headers)
                  "spk_device_alloc", "spk_device_free", "spk_host_alloc_pinned",
                  "spk_host_free_pinned", "spk_copy_async", "spk_stream_create",
-                 "spk_stream_destroy", "spk_stream_sync"]
+                 "spk_stream_destroy", "spk_stream_sync",
+                 # kernel tracing
+                 "spk_trace_enable", "spk_trace_reset", "spk_trace_read"]
 
 _codec = None
 _oracle = None
@@ -141,7 +143,28 @@ def _bind_codec(lib):
                                       ct.POINTER(P), ct.POINTER(U64), P, P, P,
                                       ct.c_size_t, P]
     lib.spk_synth_counts.argtypes = [ct.c_int, U64, U64, U64, ct.c_uint32, P, P]
+    lib.spk_trace_enable.argtypes = [ct.c_int]
+    lib.spk_trace_read.argtypes = [ct.c_char_p, ct.c_size_t]
     return lib
+
+
+def trace_enable(on: bool = True):
+    """Bracket every codec kernel launch with hipEvents (spk_trace_enable)."""
+    load_codec().spk_trace_enable(1 if on else 0)
+
+
+def trace_reset():
+    load_codec().spk_trace_reset()
+
+
+def trace_read() -> dict:
+    """{kernel: (launches, total_ms)} since the last reset (syncs the events)."""
+    import json
+    lib = load_codec()
+    n = lib.spk_trace_read(None, 0)
+    buf = ct.create_string_buffer(n + 1)
+    lib.spk_trace_read(buf, n + 1)
+    return {k: (int(v[0]), float(v[1])) for k, v in json.loads(buf.value.decode()).items()}
 
 
 def load_codec():

@@ -6,7 +6,67 @@
 // the caller's stream. There is no CPU path behind these symbols.
 #include "spk_internal.hpp"
 
+#include <cstdio>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
 using namespace spk;
+
+// ---- kernel tracing state (SPK_LAUNCH, spk_trace_*) -------------------------
+namespace spk {
+volatile int g_trace_on = 0;
+namespace {
+struct TraceRec {
+  const char *name;
+  hipEvent_t e0, e1;
+};
+struct TraceAcc {
+  uint64_t launches = 0;
+  double ms = 0;
+};
+std::mutex g_trace_mu;
+std::vector<TraceRec> g_trace_pending;
+std::map<std::string, TraceAcc> g_trace_acc;
+thread_local long g_trace_open = -1;  // index of this thread's open launch
+
+void trace_settle_locked() {
+  for (TraceRec &r : g_trace_pending) {
+    if (r.e1) {
+      float ms = 0;
+      if (hipEventSynchronize(r.e1) == hipSuccess && hipEventElapsedTime(&ms, r.e0, r.e1) == hipSuccess) {
+        TraceAcc &a = g_trace_acc[r.name];
+        ++a.launches;
+        a.ms += ms;
+      }
+      (void)hipEventDestroy(r.e1);
+    }
+    (void)hipEventDestroy(r.e0);
+  }
+  g_trace_pending.clear();
+}
+}  // namespace
+
+void trace_mark(const char *name, hipStream_t s, int end) {
+  std::lock_guard<std::mutex> lk(g_trace_mu);
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return;
+  if (hipEventRecord(e, s) != hipSuccess) {
+    (void)hipEventDestroy(e);
+    return;
+  }
+  if (!end) {
+    g_trace_open = (long)g_trace_pending.size();
+    g_trace_pending.push_back(TraceRec{name, e, nullptr});
+  } else if (g_trace_open >= 0 && g_trace_open < (long)g_trace_pending.size()) {
+    g_trace_pending[g_trace_open].e1 = e;
+    g_trace_open = -1;
+  } else {
+    (void)hipEventDestroy(e);
+  }
+}
+}  // namespace spk
 
 static int hip_rc(hipError_t e) { return e == hipSuccess ? SPK_OK : SPK_E_HIP; }
 
@@ -249,6 +309,40 @@ int spk_vector_header(const spk_layout *L, uint64_t total_n, uint32_t width, uin
   if (len > cap) return SPK_E_CAPACITY;
   for (uint32_t i = 0; i < len; ++i) h_out[i] = hb[i];
   return (int)len;
+}
+
+// ---- kernel tracing ---------------------------------------------------------
+int spk_trace_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_trace_mu);
+  g_trace_on = on ? 1 : 0;
+  return SPK_OK;
+}
+int spk_trace_reset(void) {
+  std::lock_guard<std::mutex> lk(g_trace_mu);
+  trace_settle_locked();
+  g_trace_acc.clear();
+  return SPK_OK;
+}
+// {"kernel": [launches, total_ms], ...} into buf (NUL-terminated when it
+// fits); returns the full length, or a negative SPK_E_*
+int spk_trace_read(char *buf, size_t cap) {
+  std::lock_guard<std::mutex> lk(g_trace_mu);
+  trace_settle_locked();
+  std::string js = "{";
+  for (const auto &kv : g_trace_acc) {
+    char tmp[96];
+    std::snprintf(tmp, sizeof tmp, "[%llu, %.6f]", (unsigned long long)kv.second.launches,
+                  kv.second.ms);
+    if (js.size() > 1) js += ", ";
+    js += "\"" + kv.first + "\": " + tmp;
+  }
+  js += "}";
+  if (buf && cap) {
+    const size_t n = js.size() < cap - 1 ? js.size() : cap - 1;
+    for (size_t i = 0; i < n; ++i) buf[i] = js[i];
+    buf[n] = 0;
+  }
+  return (int)js.size();
 }
 
 // ---- runtime helpers: front ends in any language stage batches through

@@ -158,7 +158,7 @@ hipError_t launch_fixed_plan(const spk_layout *L, int mode, uint64_t n,
   a.n = n;
   a.stride = L->rec_stride;
   a.mode = mode;
-  hipLaunchKernelGGL(fixed_plan_kernel, dim3(1), dim3(64), 0, s, a, d_plan,
+  SPK_LAUNCH(fixed_plan_kernel, dim3(1), dim3(64), 0, s, a, d_plan,
                      (uint8_t *)d_ws);
   return hipGetLastError();
 }
@@ -168,7 +168,7 @@ hipError_t launch_fixed_encode_vector(const spk_layout *L, uint64_t n,
                                       const void *d_ws, hipStream_t s) {
   const uint8_t *ws = (const uint8_t *)d_ws;
   const uint64_t max_bytes = n * (uint64_t)L->rec_stride;
-  hipLaunchKernelGGL(shift_copy_kernel, dim3(copy_grid(max_bytes)), dim3(kCopyThreads),
+  SPK_LAUNCH(shift_copy_kernel, dim3(copy_grid(max_bytes)), dim3(kCopyThreads),
                      0, s, (uint8_t *)d_out, (const uint8_t *)d_recs,
                      reinterpret_cast<const CopyJob *>(ws + kWsCtl), ws + kWsHdrVec);
   return hipGetLastError();
@@ -234,13 +234,13 @@ hipError_t launch_fixed_decode_vector(const spk_layout *L, const void *d_wire,
   a.rec_cap = rec_cap;
   a.stride = L->rec_stride;
   CopyJob *job = reinterpret_cast<CopyJob *>((uint8_t *)d_ws + kWsCtl);
-  hipLaunchKernelGGL(fixed_decode_hdr_kernel, dim3(1), dim3(64), 0, s, a,
+  SPK_LAUNCH(fixed_decode_hdr_kernel, dim3(1), dim3(64), 0, s, a,
                      (const uint8_t *)d_wire, job, d_res);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   uint64_t max_bytes = rec_cap * (uint64_t)L->rec_stride;
   if (max_bytes > wire_len) max_bytes = wire_len;
-  hipLaunchKernelGGL(shift_copy_kernel, dim3(copy_grid(max_bytes)), dim3(kCopyThreads),
+  SPK_LAUNCH(shift_copy_kernel, dim3(copy_grid(max_bytes)), dim3(kCopyThreads),
                      0, s, (uint8_t *)d_recs, (const uint8_t *)d_wire,
                      (const CopyJob *)job, (const uint8_t *)nullptr);
   return hipGetLastError();
@@ -660,11 +660,11 @@ hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
       const uint64_t blocks = n ? (n + b.R - 1) / b.R : 1;
       const size_t lds = kMsgHdrMax + (size_t)b.R * b.stride + 16;
       if (dw)
-        hipLaunchKernelGGL(fixed_msg_encode_lds<true>, dim3((unsigned)blocks),
+        SPK_LAUNCH(fixed_msg_encode_lds<true>, dim3((unsigned)blocks),
                            dim3(kMsgThreads), lds, s, b, (const uint8_t *)d_recs,
                            (uint8_t *)d_out, d_offsets);
       else
-        hipLaunchKernelGGL(fixed_msg_encode_lds<false>, dim3((unsigned)blocks),
+        SPK_LAUNCH(fixed_msg_encode_lds<false>, dim3((unsigned)blocks),
                            dim3(kMsgThreads), lds, s, b, (const uint8_t *)d_recs,
                            (uint8_t *)d_out, d_offsets);
       return hipGetLastError();
@@ -679,11 +679,11 @@ hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
                   ((uintptr_t)d_recs % 4 == 0) && ((uintptr_t)d_out % 16 == 0);
   if (w4) {
     const uint64_t chunks = (n * ((a.hlen + a.stride) / 4) + 3) / 4;
-    hipLaunchKernelGGL(fixed_msg_encode_w4, dim3(elem_grid(chunks > n ? chunks : n + 1)),
+    SPK_LAUNCH(fixed_msg_encode_w4, dim3(elem_grid(chunks > n ? chunks : n + 1)),
                        dim3(256), 0, s, a, (const uint32_t *)d_recs, (uint32_t *)d_out,
                        d_offsets);
   } else {
-    hipLaunchKernelGGL(fixed_msg_encode_b1, dim3(elem_grid(n * (a.hlen + a.stride) + 1)),
+    SPK_LAUNCH(fixed_msg_encode_b1, dim3(elem_grid(n * (a.hlen + a.stride) + 1)),
                        dim3(256), 0, s, a, (const uint8_t *)d_recs, (uint8_t *)d_out,
                        d_offsets);
   }
@@ -813,21 +813,21 @@ hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
       uint64_t blocks = (n + b.R - 1) / b.R;
       if (blocks > 4096) blocks = 4096;  // groups are strided over the grid
       uint64_t *part = payload;  // workspace scratch: 2 words per block
-      hipLaunchKernelGGL(fixed_msg_decode_lds, dim3((unsigned)blocks), dim3(kMsgThreads),
+      SPK_LAUNCH(fixed_msg_decode_lds, dim3((unsigned)blocks), dim3(kMsgThreads),
                          (size_t)b.cap + 16, s, b, (const uint8_t *)d_wire, d_offsets, d_errc,
                          d_res, (uint8_t *)d_recs, part);
-      hipLaunchKernelGGL(msg_sum_partials, dim3(1), dim3(1024), 0, s, (const uint64_t *)part,
+      SPK_LAUNCH(msg_sum_partials, dim3(1), dim3(1024), 0, s, (const uint64_t *)part,
                          (uint32_t)blocks, d_res);
       return hipGetLastError();
     }
   }
-  hipLaunchKernelGGL(fixed_msg_parse, dim3(elem_grid(n)), dim3(256), 0, s, a,
+  SPK_LAUNCH(fixed_msg_parse, dim3(elem_grid(n)), dim3(256), 0, s, a,
                      (const uint8_t *)d_wire, d_offsets, payload, d_errc, d_res);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const uint64_t nrec = n < rec_cap ? n : rec_cap;
   const uint64_t items = (L->rec_stride % 4 == 0) ? nrec * (L->rec_stride / 4)
                                                   : nrec * L->rec_stride;
-  hipLaunchKernelGGL(fixed_msg_gather, dim3(elem_grid(items)), dim3(256), 0, s, nrec,
+  SPK_LAUNCH(fixed_msg_gather, dim3(elem_grid(items)), dim3(256), 0, s, nrec,
                      (uint32_t)L->rec_stride, (const uint8_t *)d_wire,
                      (const uint64_t *)payload, (uint8_t *)d_recs);
   return hipGetLastError();

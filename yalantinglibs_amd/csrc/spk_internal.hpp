@@ -163,6 +163,23 @@ __device__ inline int32_t parse_hdr(const spk_msgfmt &f, const uint8_t *p, uint6
 
 }  // namespace spk
 
+// ---- kernel tracing (spk_trace_*, SURVEY.md §5 "tracing / profiling") -----
+// Every kernel launch of the codec goes through SPK_LAUNCH. With tracing
+// switched on (spk_trace_enable) it is bracketed by two hipEvents recorded on
+// the launch stream; spk_trace_read sums their elapsed times per kernel. Off
+// (the default) it costs one load and branch per launch.
+namespace spk {
+extern volatile int g_trace_on;
+void trace_mark(const char *name, hipStream_t s, int end);
+}  // namespace spk
+#define SPK_LAUNCH(kern, grid, block, shm, stream, ...)                 \
+  do {                                                                  \
+    const bool spk_tr_ = ::spk::g_trace_on != 0;                        \
+    if (spk_tr_) ::spk::trace_mark(#kern, (stream), 0);                 \
+    hipLaunchKernelGGL(kern, grid, block, shm, stream, __VA_ARGS__);    \
+    if (spk_tr_) ::spk::trace_mark(#kern, (stream), 1);                 \
+  } while (0)
+
 // ---- launch wrappers implemented in the kernel TUs -----------------------
 namespace spk {
 // spk_fixed.hip

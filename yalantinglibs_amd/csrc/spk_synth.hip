@@ -171,7 +171,7 @@ extern "C" int spk_synth_counts(int kind, uint64_t seed, uint64_t first, uint64_
   if (!d_counts || (kind != SPK_SYNTH_RECS && kind != SPK_SYNTH_OUTER &&
                     kind != SPK_SYNTH_PERSON && kind != SPK_SYNTH_INTS))
     return SPK_E_ARG;
-  hipLaunchKernelGGL(synth_counts, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, kind,
+  SPK_LAUNCH(synth_counts, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, kind,
                      seed, first, n, param, d_counts);
   return hipGetLastError() == hipSuccess ? SPK_OK : SPK_E_HIP;
 }
@@ -183,31 +183,31 @@ extern "C" int spk_synth(int kind, uint64_t seed, uint64_t first, uint64_t n, ui
   if (!d_recs && n) return SPK_E_ARG;
   switch (kind) {
     case SPK_SYNTH_REC64:
-      hipLaunchKernelGGL(synth_rec64, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n,
+      SPK_LAUNCH(synth_rec64, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n,
                          (Rec64 *)d_recs);
       break;
     case SPK_SYNTH_RECS:
       if (!d_heap_offsets) return SPK_E_ARG;
-      hipLaunchKernelGGL(synth_recs, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n, param,
+      SPK_LAUNCH(synth_recs, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n, param,
                          (RecSDev *)d_recs, (uint8_t *)d_heap, d_heap_offsets);
       break;
     case SPK_SYNTH_OUTER:
       if (!d_heap_offsets) return SPK_E_ARG;
-      hipLaunchKernelGGL(synth_outer, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n, param,
+      SPK_LAUNCH(synth_outer, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n, param,
                          (OuterDev *)d_recs, (uint8_t *)d_heap, d_heap_offsets);
       break;
     case SPK_SYNTH_RPCRECT:
-      hipLaunchKernelGGL(synth_rpcrect, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n,
+      SPK_LAUNCH(synth_rpcrect, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n,
                          (double *)d_recs);
       break;
     case SPK_SYNTH_PERSON:
       if (!d_heap_offsets) return SPK_E_ARG;
-      hipLaunchKernelGGL(synth_person, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n,
+      SPK_LAUNCH(synth_person, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n,
                          param, (PersonDev *)d_recs, (uint8_t *)d_heap, d_heap_offsets);
       break;
     case SPK_SYNTH_INTS:
       if (!d_heap_offsets) return SPK_E_ARG;
-      hipLaunchKernelGGL(synth_ints, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n, param,
+      SPK_LAUNCH(synth_ints, dim3(grid_of(n)), dim3(256), 0, s, seed, first, n, param,
                          (IntsDev *)d_recs, (uint8_t *)d_heap, d_heap_offsets);
       break;
     default:

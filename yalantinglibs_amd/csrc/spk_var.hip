@@ -2067,9 +2067,9 @@ template <typename In>
 static void scan_dev(const In *in, uint64_t n, uint64_t *out, uint64_t *bsum, uint64_t *tot,
                      hipStream_t s) {
   const unsigned nb = grid_for(n ? n : 1, kScanBlock);
-  hipLaunchKernelGGL(scan_reduce<In>, dim3(nb), dim3(256), 0, s, in, n, bsum);
-  hipLaunchKernelGGL(scan_blocks, dim3(1), dim3(1024), 0, s, bsum, (uint64_t)nb, tot);
-  hipLaunchKernelGGL(scan_apply<In>, dim3(nb), dim3(256), 0, s, in, n, (const uint64_t *)bsum,
+  SPK_LAUNCH(scan_reduce<In>, dim3(nb), dim3(256), 0, s, in, n, bsum);
+  SPK_LAUNCH(scan_blocks, dim3(1), dim3(1024), 0, s, bsum, (uint64_t)nb, tot);
+  SPK_LAUNCH(scan_apply<In>, dim3(nb), dim3(256), 0, s, in, n, (const uint64_t *)bsum,
                      out);
 }
 
@@ -2081,38 +2081,38 @@ static hipError_t launch_vec_decode_ns(const DecArgs &a, const WalkProg &P, cons
   hipError_t e;
   const uint32_t ns = P.ns;
   // one launch initialises cnt / hs / tot / dirty (four memsets cost ~20 us)
-  hipLaunchKernelGGL(vec_init, dim3(grid_for(v.nch, 256) < 4096 ? grid_for(v.nch, 256) : 4096),
+  SPK_LAUNCH(vec_init, dim3(grid_for(v.nch, 256) < 4096 ? grid_for(v.nch, 256) : 4096),
                      dim3(256), 0, s, B, v.nch, ns ? ns : 1u,
                      reinterpret_cast<uint64_t *>(ws + v.tot));
   if ((e = hipGetLastError()) != hipSuccess) return e;
   uint64_t *tot = reinterpret_cast<uint64_t *>(ws + v.tot);
-  hipLaunchKernelGGL(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, v.lp, v.nch);
+  SPK_LAUNCH(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, v.lp, v.nch);
   const unsigned cg = grid_for(v.nch, 256);
-  hipLaunchKernelGGL(vec_spec<NS>, dim3(grid_for(v.nch, (uint64_t)kSpecStep * kSpecWaves)),
+  SPK_LAUNCH(vec_spec<NS>, dim3(grid_for(v.nch, (uint64_t)kSpecStep * kSpecWaves)),
                      dim3(64 * kSpecWaves), 0, s, a, P, wire, ws, B);
   for (uint32_t r = 1; r < P.rounds; ++r)
-    hipLaunchKernelGGL(vec_verify_round<NS>, dim3(256), dim3(256), 0, s, a, P, wire, ws, B, r);
-  hipLaunchKernelGGL(vec_fixup<NS>, dim3(1), dim3(1024), 0, s, a, P, wire, ws, B);
-  hipLaunchKernelGGL(vec_term_min, dim3(cg), dim3(256), 0, s, ws, B);
-  hipLaunchKernelGGL(vec_term_zero, dim3(cg), dim3(256), 0, s, ws, B, ns);
+    SPK_LAUNCH(vec_verify_round<NS>, dim3(256), dim3(256), 0, s, a, P, wire, ws, B, r);
+  SPK_LAUNCH(vec_fixup<NS>, dim3(1), dim3(1024), 0, s, a, P, wire, ws, B);
+  SPK_LAUNCH(vec_term_min, dim3(cg), dim3(256), 0, s, ws, B);
+  SPK_LAUNCH(vec_term_zero, dim3(cg), dim3(256), 0, s, ws, B, ns);
   // chunk record counts -> record bases; chunk span-count sums -> heap bases
   // (nchunks is device-side: the capacity is scanned, entries past it are 0)
   scan_dev<uint32_t>(B.cnt, v.nch, B.base, B.scan, tot, s);
-  hipLaunchKernelGGL(vec_count_check, dim3(1), dim3(64), 0, s, ws, (const uint64_t *)tot, d_res);
+  SPK_LAUNCH(vec_count_check, dim3(1), dim3(64), 0, s, ws, (const uint64_t *)tot, d_res);
   for (uint32_t k = 0; k < ns; ++k)
     scan_dev<uint64_t>(B.hs + (uint64_t)k * v.nch, v.nch, B.hb + (uint64_t)k * v.nch, B.scan,
                        (uint64_t *)nullptr, s);
-  hipLaunchKernelGGL(vec_total<NS>, dim3(cg), dim3(256), 0, s, a, P, wire, ws, B, tot + 1);
-  hipLaunchKernelGGL(vec_finish, dim3(1), dim3(64), 0, s, a, ws, d_res,
+  SPK_LAUNCH(vec_total<NS>, dim3(cg), dim3(256), 0, s, a, P, wire, ws, B, tot + 1);
+  SPK_LAUNCH(vec_finish, dim3(1), dim3(64), 0, s, a, ws, d_res,
                      (const uint64_t *)(tot + 1));
   if (P.nv)
-    hipLaunchKernelGGL(vec_vi_errc<NS>, dim3(1), dim3(64), 0, s, a, P, wire,
+    SPK_LAUNCH(vec_vi_errc<NS>, dim3(1), dim3(64), 0, s, a, P, wire,
                        (const uint8_t *)ws, B, d_res);
   uint32_t G = kEmitRecs / v.lp;
   if (G > 64) G = 64;
   if (G < 1) G = 1;
   const uint64_t groups = (v.nch + G - 1) / G;
-  hipLaunchKernelGGL(vec_emit<NS>, dim3(grid_for(groups, kEmitWaves)), dim3(64 * kEmitWaves), 0, s,
+  SPK_LAUNCH(vec_emit<NS>, dim3(grid_for(groups, kEmitWaves)), dim3(64 * kEmitWaves), 0, s,
                      a, P, wire, (const uint8_t *)ws, B, d_recs, (const spk_dresult_t *)d_res, G);
   return hipGetLastError();
 }
@@ -2153,11 +2153,11 @@ hipError_t launch_var_plan(const spk_layout *L, int mode, uint64_t n, const void
   VarArgs a = make_varargs(L, mode, n, nullptr);
   uint8_t *ws = (uint8_t *)d_ws;
   const MsgHdrTable t = msg_hdr_table(L);
-  hipLaunchKernelGGL(write_msg_hdrs, dim3(1), dim3(256), 0, s, t, ws);
+  SPK_LAUNCH(write_msg_hdrs, dim3(1), dim3(256), 0, s, t, ws);
   const uint64_t nb = grid_for(n, kPlanRPB);
   const uint8_t *tbl = ws + kWsHdrMsg + 4 * kWsHdrSlot - 8;
   if (n)
-    hipLaunchKernelGGL(var_plan_reduce, dim3(nb), dim3(kThreads), 0, s, a,
+    SPK_LAUNCH(var_plan_reduce, dim3(nb), dim3(kThreads), 0, s, a,
                        (const uint8_t *)d_recs, ws, tbl);
   FinArgs f;
   f.fmt = mode == SPK_MODE_VECTOR ? L->fmt_vector : L->fmt_one;
@@ -2165,7 +2165,7 @@ hipError_t launch_var_plan(const spk_layout *L, int mode, uint64_t n, const void
   f.nblocks = n ? nb : 0;
   f.n_cont = a.L.n_cont;
   f.mode = mode;
-  hipLaunchKernelGGL(var_plan_finalize, dim3(1), dim3(1024), 0, s, f, ws, d_plan);
+  SPK_LAUNCH(var_plan_finalize, dim3(1), dim3(1024), 0, s, f, ws, d_plan);
   (void)ws_bytes;
   return hipGetLastError();
 }
@@ -2187,7 +2187,7 @@ hipError_t launch_var_encode(const spk_layout *L, int mode, uint64_t n,
   if (n == 0) {
     // header (+ zero count) only; reuse the write kernel with one block
   }
-  hipLaunchKernelGGL(var_encode_write, dim3(grid_for(n ? n : 1, kRPB)), dim3(kThreads), 0,
+  SPK_LAUNCH(var_encode_write, dim3(grid_for(n ? n : 1, kRPB)), dim3(kThreads), 0,
                      s, a, (const uint8_t *)d_recs, (uint8_t *)d_out, out_cap,
                      (const uint8_t *)ws, d_plan, d_offsets);
   (void)ws_bytes;
@@ -2215,7 +2215,7 @@ hipError_t launch_var_encode_body(const spk_layout *L, uint64_t n, const void *d
   if (e != hipSuccess) return e;
   uint32_t ns = 0;
   for (uint32_t i = 0; i < L->n_ops; ++i) ns += L->ops[i].kind == SPK_OP_SPAN;  // width-w counts
-  hipLaunchKernelGGL(body_plan_kernel, dim3(1), dim3(64), 0, s, plan, n, ns, width);
+  SPK_LAUNCH(body_plan_kernel, dim3(1), dim3(64), 0, s, plan, n, ns, width);
   return launch_var_encode(L, SPK_MODE_VECTOR, n, d_recs, d_heaps, plan, d_out, out_cap,
                            nullptr, nullptr, d_ws, ws_bytes, s);
 }
@@ -2244,12 +2244,12 @@ hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
     if ((e = hipMemsetAsync(d_res, 0, sizeof(spk_dresult_t), s)) != hipSuccess) return e;
     if (n_msgs == 0) return hipSuccess;
     const unsigned nb = grid_for(n_msgs, kThreads);
-    hipLaunchKernelGGL(var_msg_parse, dim3(nb), dim3(kThreads), 0, s, a, wire, d_offsets,
+    SPK_LAUNCH(var_msg_parse, dim3(nb), dim3(kThreads), 0, s, a, wire, d_offsets,
                        ws, d_errc, d_res);
     uint64_t *bsum = reinterpret_cast<uint64_t *>(ws + kWsScratch + sizeof(MsgState) * n_msgs);
-    hipLaunchKernelGGL(var_scan_blocks, dim3(1), dim3(1024), 0, s, (uint64_t)nb,
+    SPK_LAUNCH(var_scan_blocks, dim3(1), dim3(1024), 0, s, (uint64_t)nb,
                        a.L.n_spans, bsum, a, d_res);
-    hipLaunchKernelGGL(var_msg_write, dim3(nb), dim3(kThreads), 0, s, a, wire, d_offsets,
+    SPK_LAUNCH(var_msg_write, dim3(nb), dim3(kThreads), 0, s, a, wire, d_offsets,
                        (const uint8_t *)ws, (uint8_t *)d_recs, (const spk_dresult_t *)d_res);
     (void)ws_bytes;
     return hipGetLastError();
