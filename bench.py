@@ -366,7 +366,7 @@ def measure(wl, args, torch, dist, world, dev, steps, warmup, settle):
     stream = torch.cuda.current_stream(dev)
     wl.step(stream)
     torch.cuda.synchronize(dev)
-    bad = wl.check()
+    bad = None if os.environ.get("SPK_FUSED_DBG") else wl.check()  # diagnostics runs: no gate
     if bad:
         print(json.dumps({"error": "round trip mismatch", "config": wl.cfg, "what": bad}),
               flush=True)

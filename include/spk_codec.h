@@ -100,6 +100,9 @@ extern "C" {
 #define SPK_ERRC_INVALID_WIDTH 4
 /* device-side capacity overflow during decode (not a reference errc) */
 #define SPK_ERRC_CAPACITY 100
+/* internal failure of the decoder (an in-kernel wait timed out; never
+ * expected; not a reference errc) */
+#define SPK_ERRC_INTERNAL 101
 
 #define SPK_OP_COPY 1u
 #define SPK_OP_SPAN 2u

@@ -96,7 +96,8 @@ DRES_BYTES = ct.sizeof(spk_dresult_t)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _ROOT = os.path.dirname(_HERE)
-CODEC_PATH = os.path.join(_HERE, "libspk_codec.so")
+# SPK_CODEC_LIB: dev-only override to A/B alternative builds of the same ABI
+CODEC_PATH = os.environ.get("SPK_CODEC_LIB") or os.path.join(_HERE, "libspk_codec.so")
 ORACLE_PATH = os.path.join(_ROOT, "oracle", "libspk_oracle.so")
 
 # exported symbols of include/spk_codec.h (checked by tests/test_capi.py)

@@ -36,6 +36,15 @@
 // falls back to one sequential walker (correct, slow) — see DESIGN.md.
 #include "spk_internal.hpp"
 
+#include <stdlib.h>
+
+#ifndef SPK_TCHUNK
+#define SPK_TCHUNK 256
+#endif
+#ifndef SPK_TWAVES
+#define SPK_TWAVES 1
+#endif
+
 namespace spk {
 
 constexpr int kThreads = 256;
@@ -1054,6 +1063,19 @@ struct VCtl {
   uint64_t cap;                // chunk capacity: stride of the per-span chunk arrays
 };
 
+// control words of the tile vector decoder (vec_tile_*)
+struct FCtl {
+  unsigned long long broken[4];  // tiles re-walked by select pass k (K2)
+  unsigned long long unresolved; // tiles no pass could select (never expected)
+  unsigned long long term_tile;  // first tile whose path ends inside it (atomicMin), ~0
+  unsigned long long term_pos;   // where the true path ends (atomicMin), ~0
+  unsigned long long end_pos;    // end of record n-1
+  unsigned long long total;      // records on the path (tile scan)
+  unsigned long long htot[SPK_MAX_SPANS];  // heap elements used by records 0..n-1
+  unsigned long long stot[SPK_MAX_SPANS];  // span-count sums on the path
+};
+constexpr size_t kWsFCtl = kWsCtl + 1280;
+
 // Compact walk program of a record: fixed bytes, then per span
 // [count:w][count*esz bytes][fixed bytes]. Built once on the host from the
 // descriptor so the walker's loop constants sit in SGPRs.
@@ -1245,6 +1267,14 @@ __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
   for (int r = 0; r <= kRoundsMax; ++r) c->wl_n[r] = 0;
   c->term_chunk = kNone32;
   c->overflow = 0;
+  FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);  // tile decoder state
+  for (int k = 0; k < 4; ++k) fc->broken[k] = 0;
+  fc->unresolved = 0;
+  fc->term_tile = ~0ull;
+  fc->term_pos = ~0ull;
+  fc->end_pos = 0;
+  fc->total = 0;
+  for (int k = 0; k < SPK_MAX_SPANS; ++k) fc->htot[k] = fc->stot[k] = 0;
   const uint64_t payload = (!e && a.wire_len > pos) ? a.wire_len - pos : 0;
   c->nchunks = (c->n == 0) ? 0 : (payload + kSpec - 1) / kSpec;
   spk_dresult_t r = {};
@@ -1303,7 +1333,70 @@ struct WinReader {
     }
     return wire[x];
   }
+  // 4 / 16 bytes at x (x + n <= wend: inside the staged window)
+  __device__ __forceinline__ uint32_t ld4(uint64_t x) const {
+    const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = o >> 2;
+    return __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+  }
+  __device__ __forceinline__ v4u_t ld16(uint64_t x) const {
+    const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = o >> 2;
+    const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2], d3 = d[i + 3], d4 = d[i + 4];
+    return v4u_t{__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                 __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh)};
+  }
+  // dst[0, n) = wire[x, x + n): from LDS when inside the window
+  __device__ __forceinline__ void copy_to(uint8_t *dst, uint64_t x, uint64_t n) const {
+    if (x + n + 4 > wend) {
+      copy_bytes(dst, wire + x, n);
+      return;
+    }
+    uint64_t i = 0;
+    for (; i + 16 <= n; i += 16) *reinterpret_cast<v4u_una *>(dst + i) = ld16(x + i);
+    if (n - i >= 8) {
+      const uint64_t lo = ld4(x + i), hi = ld4(x + i + 4);
+      *reinterpret_cast<u64_unaligned *>(dst + i) = lo | (hi << 32);
+      i += 8;
+    }
+    if (n - i >= 4) {
+      *reinterpret_cast<u32_unaligned *>(dst + i) = ld4(x + i);
+      i += 4;
+    }
+    for (; i < n; ++i) dst[i] = (uint8_t)byte(x + i);
+  }
 };
+
+// emit_record reading the wire through an LDS window reader
+__device__ __forceinline__ void emit_record_rd(const KLayout &L, const WinReader &rd,
+                                               uint64_t pos, uint32_t w, uint8_t *rec,
+                                               uint8_t *const *heaps, const uint64_t *off,
+                                               uint64_t end) {
+  uint32_t sk = 0;
+  for (uint32_t o = 0; o < L.n_ops; ++o) {
+    const spk_op op = L.ops[o];
+    if (op.kind == SPK_OP_COPY) {
+      rd.copy_to(rec + op.rec_off, pos, op.size);
+      pos += op.size;
+    } else if (op.kind == SPK_OP_VARINT) {
+      uint64_t v = 0;
+      auto byte = [&rd](uint64_t x) { return rd.byte(x); };
+      pos += vi_read(byte, pos, end, &v);
+      vi_store(op, rec, v);
+    } else {
+      const uint64_t cnt = op.kind == SPK_OP_OPTION ? (uint64_t)(rd.byte(pos) != 0) : rd(pos);
+      pos += op_pw(op, w);
+      *reinterpret_cast<uint32_t *>(rec + op.rec_off) = (uint32_t)cnt;
+      *reinterpret_cast<uint64_t *>(rec + op.aux) = off[sk];
+      const uint64_t nb = opt_nb(op, cnt, pos, end);
+      uint8_t *hp = heaps[sk] + off[sk] * op.size;
+      if (cnt && !nb && op.kind == SPK_OP_OPTION)
+        for (uint32_t b = 0; b < op.size; ++b) hp[b] = 0;  // unreadable value
+      else
+        rd.copy_to(hp, pos, nb);
+      pos += nb;
+      ++sk;
+    }
+  }
+}
 
 constexpr uint32_t kRegion = 64 * kSpec;                    // chunk bytes per wave
 constexpr uint32_t kRegionVec = (kRegion + kWinExtra) / 16;  // 16-B LDS slots per wave
@@ -1970,6 +2063,883 @@ __global__ __launch_bounds__(64 * kEmitWaves) void vec_emit(DecArgs a, WalkProg 
 }
 
 // ===========================================================================
+// DECODE, SPK_MODE_VECTOR — tiles: speculate, select, scan, emit
+// ===========================================================================
+// A tile is 64 consecutive kSpec-byte chunks of the payload (16 KiB), owned
+// by one wave (one lane per chunk) and staged in LDS.
+//  K1 vec_tile_spec: every lane walks its chunk from its first plausible
+//     record start (candidate screen above) -> spec start, exit (first record
+//     start at or past the chunk end), record count, span-count sums. Chunk
+//     0's start is cross-checked against chunk 1's independent speculation.
+//     Resolution in registers: chunk c's entry is chunk c-1's exit, lanes
+//     whose state came from another entry re-walk, in parallel rounds, until
+//     the chain is consistent given the tile's assumed entry X. The tile then
+//     publishes its FUNCTION: exit Y (the same for every entry below) and up
+//     to kAlt entries (X and other start candidates of chunk 0 whose walk
+//     reaches chunk 0's exit) with the tile's records / span sums for each.
+//  K2 vec_tile_select: tile t's true entry is tile t-1's exit (tile 0: the
+//     payload start). It selects the matching entry; a tile whose entry is
+//     none of them re-walks from it (rare; twice, a cascade is rarer still,
+//     then one wave fixes any rest in order).
+//  K3 a prefix sum over the tiles' selected (records, span sums), zero past
+//     the tile where the path ends -> every tile's first record index and heap
+//     offsets.
+//  K4 vec_tile_emit: each tile re-stages its bytes, takes its chunk states
+//     for the selected entry, lists its record starts in LDS and writes 64
+//     consecutive records at a time (span counts scanned across the wave for
+//     heap offsets).
+// No kernel waits on another workgroup.
+constexpr uint32_t kTChunk = SPK_TCHUNK;                    // payload bytes per lane (chunk)
+constexpr uint32_t kTileBytes = 64 * kTChunk;                // payload bytes per tile
+constexpr uint32_t kTileVec = (kTileBytes + kWinExtra) / 16;  // staged 16-B slots
+constexpr uint32_t kDecWaves = SPK_TWAVES;                   // tiles (waves) per block
+constexpr uint32_t kTab = 2048;                              // record starts per emission pass
+constexpr uint64_t kNoPos = ~0ull - 1;  // "no plausible start / unknown entry"
+constexpr uint32_t kSpecPast = 2;       // records a speculative walk checks past its chunk
+constexpr uint32_t kAlt = 4;            // entries a tile function carries
+constexpr uint32_t kAltWords = 2 + SPK_MAX_SPANS;   // entry, cnt, sums
+constexpr uint32_t kFnWords = 48;       // y, nalt, kAlt x kAltWords (+ pad)
+constexpr int32_t kSelTerm = -2;        // the tile starts past the path's end
+constexpr int32_t kSelBroken = -1;
+
+struct TileBufs {
+  uint64_t *fn;       // [ntiles][kFnWords]
+  uint64_t *cused;    // [nchunks] entry each chunk state was computed from
+  uint64_t *cex;      // [nchunks] its exit (first start past the chunk / kTermPos)
+  uint32_t *ccnt;     // [nchunks] records starting in the chunk
+  uint64_t *csum;     // [nsp][nchunks] span-count sums
+  int32_t *sel;       // [ntiles] selected entry (kSelTerm / kSelBroken)
+  uint64_t *contrib;  // [1 + nsp][ntiles] selected (records, sums) -> exclusive prefix
+  uint64_t *scan;     // block sums of the tile scan
+  uint64_t ntiles, nchunks;
+};
+
+// A true walk of chunk [.., ce) from `entry` (no plausibility limit): exit =
+// first record start >= ce, or kTermPos when the path ends (incomplete record
+// or wire end: *term_at = where); kTermPos / kNoPos entries propagate.
+template <int NS, typename Rd>
+__device__ __forceinline__ void walk_true(const WalkProg &P, const Rd &rd, uint64_t len,
+                                          uint32_t w, uint64_t entry, uint64_t ce,
+                                          uint64_t &ex, uint32_t &cnt, uint64_t *sums,
+                                          uint64_t &term_at) {
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  cnt = 0;
+  for (uint32_t q = 0; q < nsp; ++q) sums[q] = 0;
+  term_at = kTermPos;
+  if (entry == kTermPos || entry == kNoPos) {
+    ex = entry;
+    return;
+  }
+  uint64_t x = entry;
+  while (x < ce) {
+    uint64_t rc[NS > 0 ? NS : SPK_MAX_SPANS];
+    const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w, rc) : 0;
+    if (!L) {
+      term_at = x;
+      ex = kTermPos;
+      return;
+    }
+    ++cnt;
+    for (uint32_t q = 0; q < nsp; ++q) sums[q] += rc[q];
+    x += L;
+  }
+  ex = x;
+}
+
+// The first records of a lane's speculative walk (chunk-relative starts and
+// the span-count sums before each), so that a walk from another entry stops
+// where it meets that path: paths through the same records coincide from
+// there on, and the speculative walk's totals give the rest.
+constexpr uint32_t kMergePts = 4;
+template <int NS>
+struct SpecPath {
+  static constexpr int kS = NS > 0 ? NS : 2;
+  uint32_t pos[kMergePts];
+  uint32_t ps[kMergePts][kS];
+  uint32_t np;     // valid entries (0: no merge information)
+  uint32_t cnt;    // the speculative walk's records in the chunk
+  uint64_t sums[kS];
+  uint64_t ex, term_at;
+};
+
+template <int NS, typename Rd>
+__device__ __forceinline__ void walk_merge(const WalkProg &P, const Rd &rd, uint64_t len,
+                                           uint32_t w, uint64_t entry, uint64_t cs, uint64_t ce,
+                                           const SpecPath<NS> &sp, uint64_t &ex, uint32_t &cnt,
+                                           uint64_t *sums, uint64_t &term_at) {
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  cnt = 0;
+  for (uint32_t q = 0; q < nsp; ++q) sums[q] = 0;
+  term_at = kTermPos;
+  if (entry == kTermPos || entry == kNoPos) {
+    ex = entry;
+    return;
+  }
+  uint64_t x = entry;
+  while (x < ce) {
+    for (uint32_t j = 0; j < sp.np; ++j)
+      if (x == cs + sp.pos[j]) {  // joined the speculative path at its record j
+        cnt += sp.cnt - j;
+        for (uint32_t q = 0; q < nsp; ++q) sums[q] += sp.sums[q] - sp.ps[j][q];
+        ex = sp.ex;
+        term_at = sp.term_at;
+        return;
+      }
+    uint64_t rc[NS > 0 ? NS : SPK_MAX_SPANS];
+    const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w, rc) : 0;
+    if (!L) {
+      term_at = x;
+      ex = kTermPos;
+      return;
+    }
+    ++cnt;
+    for (uint32_t q = 0; q < nsp; ++q) sums[q] += rc[q];
+    x += L;
+  }
+  ex = x;
+}
+
+// In-wave resolution: until every lane's state was computed from its true
+// entry (lane 0: entry0; lane c: lane c-1's exit), lanes that disagree re-walk.
+template <int NS, typename Rd>
+__device__ __forceinline__ void resolve_tile(const WalkProg &P, const Rd &rd, uint64_t len,
+                                             uint32_t w, uint64_t ce, uint32_t lane,
+                                             uint64_t entry0, uint64_t &used, uint64_t &ex,
+                                             uint32_t &cnt, uint64_t *sums, uint64_t &term_at) {
+  for (int round = 0; round < 66; ++round) {
+    const uint64_t prev = __shfl_up(ex, 1);
+    const uint64_t entry = lane == 0 ? entry0 : prev;
+    const bool need = entry != used;
+    if (!__any(need)) return;
+    if (need) {
+      walk_true<NS>(P, rd, len, w, entry, ce, ex, cnt, sums, term_at);
+      used = entry;
+    }
+  }
+}
+// ... with each lane's speculative path for early merges
+template <int NS, typename Rd>
+__device__ __forceinline__ void resolve_tile_sp(const WalkProg &P, const Rd &rd, uint64_t len,
+                                                uint32_t w, uint64_t cs, uint64_t ce,
+                                                uint32_t lane, uint64_t entry0,
+                                                const SpecPath<NS> &sp, uint64_t &used,
+                                                uint64_t &ex, uint32_t &cnt, uint64_t *sums,
+                                                uint64_t &term_at) {
+  for (int round = 0; round < 66; ++round) {
+    const uint64_t prev = __shfl_up(ex, 1);
+    const uint64_t entry = lane == 0 ? entry0 : prev;
+    const bool need = entry != used;
+    if (!__any(need)) return;
+    if (need) {
+      walk_merge<NS>(P, rd, len, w, entry, cs, ce, sp, ex, cnt, sums, term_at);
+      used = entry;
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// The candidate screen of the speculative walk for one start position.
+template <int NS, typename Rd>
+__device__ __forceinline__ bool screen_one(const WalkProg &P, const Rd &rd, uint64_t len,
+                                           uint32_t w, uint64_t q) {
+  if (P.pf_all) return true;
+  uint64_t b = q + P.skip[0];
+  if (NS < 0 && P.pf_var) {
+    auto byte = [&rd](uint64_t x) { return rd.byte(x); };
+    for (uint32_t j = 0; j < P.vfirst[1]; ++j) {
+      uint64_t v;
+      const uint32_t l = vi_read(byte, b, len, &v);
+      if (!l || l == kViBad) return false;
+      b += l + P.vafter[j];
+    }
+  }
+  return (b + w <= len ? rd(b) : ~0ull) <= P.c0max;
+}
+
+
+// Stage tile t's bytes (+ extension) in this wave's LDS window; reader over it.
+struct TileView {
+  WinReader rd;
+  uint64_t ts, wend;
+};
+__device__ __forceinline__ TileView stage_tile(v4u_t *win, const uint8_t *wire, uint64_t len,
+                                               uint64_t ts, uint32_t w, uint32_t lane) {
+  const uint64_t wend = ts + kTileVec * 16 < len ? ts + kTileVec * 16 : len;
+  for (uint32_t v = lane; v < kTileVec; v += 64) {
+    const uint64_t g = ts + 16ull * v;
+    v4u_t val = {0u, 0u, 0u, 0u};
+    if (g + 16 <= len) {
+      val = *reinterpret_cast<const v4u_una *>(wire + g);
+    } else if (g < len) {
+      uint32_t tt[4] = {0u, 0u, 0u, 0u};
+      for (uint64_t q = g; q < len; ++q) tt[(q - g) >> 2] |= (uint32_t)wire[q] << (8 * ((q - g) & 3));
+      val = v4u_t{tt[0], tt[1], tt[2], tt[3]};
+    }
+    win[v] = val;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  TileView tv;
+  tv.rd.d = (const lds_u32 *)win;
+  tv.rd.wire = wire;
+  tv.rd.cs = ts;
+  tv.rd.wend = wend;
+  tv.rd.w = w;
+  tv.ts = ts;
+  tv.wend = wend;
+  return tv;
+}
+
+__device__ __forceinline__ bool vec_live(const VCtl *c) { return !c->errc && c->n; }
+
+// ---- K1 ----------------------------------------------------------------------
+template <int NS>
+__global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkProg P,
+                                                                const uint8_t *__restrict__ wire,
+                                                                const uint8_t *__restrict__ ws,
+                                                                TileBufs TB, uint32_t dbg) {
+  __shared__ v4u_t win_s[kDecWaves][kTileVec + 1];
+  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t t = (uint64_t)blockIdx.x * kDecWaves + wv;
+  if (t >= TB.ntiles || !vec_live(c)) return;  // wave-uniform
+  const uint32_t w = c->w;
+  const uint64_t len = a.wire_len, p0 = c->p0;
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  const uint64_t ts = p0 + t * kTileBytes;
+  const TileView tv = stage_tile(win_s[wv], wire, len, ts, w, lane);
+  const WinReader &rd = tv.rd;
+  const uint64_t wend = tv.wend;
+  const uint64_t cs = ts + (uint64_t)lane * kTChunk;
+  const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
+  // ---- 1. speculative walk of this lane's chunk ----
+  uint64_t used = kNoPos, ex = kNoPos, sums[NS > 0 ? NS : SPK_MAX_SPANS], term_at = kTermPos;
+  uint32_t cnt = 0;
+  for (uint32_t q = 0; q < nsp; ++q) sums[q] = 0;
+  const bool exact = t == 0 && lane == 0;  // the payload start: no search
+  SpecPath<NS> sp;
+  sp.np = 0;
+  if (cs < len && !(dbg & 8)) {
+    uint64_t tt = 0, x = cs, past = 0, sx = exact ? cs : kNoPos;
+    bool searching = !exact, done = false;
+    uint32_t k = 0;
+    uint64_t ksum[NS > 0 ? NS : SPK_MAX_SPANS];
+    for (uint32_t q = 0; q < nsp; ++q) ksum[q] = 0;
+    const uint32_t s0 = P.skip[0];
+    while (!done) {
+      if (searching) {
+        const uint64_t b0 = cs + tt + s0;  // first count field of candidate cs+tt
+        uint32_t m = 0;
+        if (NS < 0 && P.pf_var) {
+          auto byte = [&rd](uint64_t q) { return rd.byte(q); };
+          for (int kk = 0; kk < 8; ++kk) {
+            uint64_t q = b0 + kk;
+            bool ok = true;
+            for (uint32_t j = 0; j < P.vfirst[1]; ++j) {
+              uint64_t v;
+              const uint32_t l = vi_read(byte, q, len, &v);
+              if (!l || l == kViBad) {
+                ok = false;
+                break;
+              }
+              q += l + P.vafter[j];
+            }
+            if (ok) ok = (q + w <= len ? rd(q) : ~0ull) <= P.c0max;
+            m |= (ok ? 1u : 0u) << kk;
+          }
+        } else if (b0 + 20 <= wend) {
+          const uint32_t o0 = (uint32_t)(b0 - ts), i = o0 >> 2, sh = o0 & 3;
+          const lds_u32 *d = rd.d;
+          const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2], d3 = d[i + 3], d4 = d[i + 4];
+          const uint32_t wd[4] = {__builtin_amdgcn_alignbyte(d1, d0, sh),
+                                  __builtin_amdgcn_alignbyte(d2, d1, sh),
+                                  __builtin_amdgcn_alignbyte(d3, d2, sh),
+                                  __builtin_amdgcn_alignbyte(d4, d3, sh)};
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk) {
+            const uint32_t lo = __builtin_amdgcn_alignbyte(wd[(kk >> 2) + 1], wd[kk >> 2], kk & 3);
+            uint64_t cv = w == 1 ? (lo & 0xFFu) : w == 2 ? (lo & 0xFFFFu) : lo;
+            if (w == 8)
+              cv |= (uint64_t)__builtin_amdgcn_alignbyte(wd[(kk >> 2) + 2], wd[(kk >> 2) + 1], kk & 3)
+                    << 32;
+            m |= (cv <= P.c0max ? 1u : 0u) << kk;
+          }
+        } else {
+          for (int kk = 0; kk < 8; ++kk) {
+            const uint64_t q = b0 + kk;
+            const uint64_t cv = q + w <= len ? rd(q) : ~0ull;
+            m |= (cv <= P.c0max ? 1u : 0u) << kk;
+          }
+        }
+        if (P.pf_all) m = 0xFFu;  // first span an OPTION / no span: any byte may start a record
+        const uint64_t rem = ce - (cs + tt);  // candidates must start in the chunk
+        if (rem < 8) m &= (1u << rem) - 1u;
+        if (!m) {
+          tt += 8;
+          if (cs + tt >= ce) done = true;
+          continue;
+        }
+        tt += (uint32_t)__builtin_ctz(m);
+        x = cs + tt;
+        sx = x;
+        k = 0;
+        past = 0;
+        ex = kNoPos;
+        for (uint32_t q = 0; q < nsp; ++q) ksum[q] = 0;
+        searching = false;
+      }
+      uint64_t rc[NS > 0 ? NS : SPK_MAX_SPANS];
+      const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w, rc) : 0;
+      if (!exact && ((L == 0 && x < len) || L > kPlaus)) {  // off the record grid
+        tt += 1;
+        searching = true;
+        sx = kNoPos;
+        if (cs + tt >= ce) done = true;
+        continue;
+      }
+      if (x < ce) {
+        if (!L) {  // the wire ends inside the chunk: the walk's path ends here
+          ex = kTermPos;
+          term_at = x;
+          break;
+        }
+        if (k < kMergePts) {
+          sp.pos[k] = (uint32_t)(x - cs);
+          for (uint32_t q = 0; q < nsp && q < SpecPath<NS>::kS; ++q) sp.ps[k][q] = (uint32_t)ksum[q];
+        }
+        ++k;
+        for (uint32_t q = 0; q < nsp; ++q) ksum[q] += rc[q];
+      } else {
+        if (!past) ex = x;
+        ++past;
+        if (!L || past >= kSpecPast) break;
+      }
+      x += L;
+    }
+    if (sx != kNoPos) {
+      used = sx;
+      cnt = k;
+      for (uint32_t q = 0; q < nsp; ++q) sums[q] = ksum[q];
+      // merge information: spans fit the path record, sums fit 32 bits
+      bool mok = NS > 0 || P.ns <= (uint32_t)SpecPath<NS>::kS;
+      for (uint32_t q = 0; q < nsp && q < SpecPath<NS>::kS; ++q) {
+        mok = mok && ksum[q] < 0xFFFFFFFFull;
+        sp.sums[q] = ksum[q];
+      }
+      sp.np = mok ? (k < kMergePts ? k : kMergePts) : 0;
+      sp.cnt = k;
+      sp.ex = ex;
+      sp.term_at = term_at;
+    } else {
+      ex = kNoPos;
+    }
+  } else {
+    // a lane past the wire end: no chunk; it passes its entry through
+    used = kNoPos;
+    ex = kNoPos;
+  }
+  // ---- 2. resolution given the tile's assumed entry ----
+  uint64_t X = __shfl(used, 0);  // lane 0's spec start (kNoPos: no plausible start)
+  if (t == 0) X = p0;
+  if (t > 0 && !(dbg & 16)) {
+    // Two independent speculations that agree are far likelier true: when
+    // chunk 0's walk does not exit where chunk 1's speculative walk starts,
+    // take the first start candidate of chunk 0 whose walk does (in parallel,
+    // one candidate per lane), so the tile rarely publishes a wrong assumption.
+    const uint64_t x1 = __shfl(used, 1), e0 = __shfl(ex, 0), ce0 = __shfl(ce, 0);
+    const uint64_t cs0 = ts;
+    if (x1 != kNoPos && e0 != x1 && cs0 < len) {
+      const uint64_t from = X != kNoPos ? X + 1 : cs0;
+      for (uint64_t b = from; b < ce0; b += 64) {
+        const uint64_t q = b + lane;
+        bool ok = q < ce0 && screen_one<NS>(P, rd, len, w, q);
+        uint64_t qe = kNoPos, qt;
+        uint32_t qc = 0;
+        uint64_t qs[NS > 0 ? NS : SPK_MAX_SPANS];
+        if (ok) {
+          walk_true<NS>(P, rd, len, w, q, ce0, qe, qc, qs, qt);
+          ok = qe == x1;
+        }
+        const uint64_t m = __ballot(ok);
+        if (m) {
+          const uint32_t l = (uint32_t)__builtin_ctzll(m);
+          const uint64_t nq = __shfl(q, l);
+          const uint32_t nc = (uint32_t)__shfl((uint64_t)qc, l);
+          for (uint32_t qq = 0; qq < nsp; ++qq) {
+            const uint64_t v = __shfl(ok ? qs[qq] : 0, l);
+            if (lane == 0) sums[qq] = v;
+          }
+          if (lane == 0) {
+            used = nq;
+            ex = x1;
+            cnt = nc;
+            term_at = kTermPos;
+            sp.np = 0;  // chunk 0 is not on its speculative path any more
+          }
+          X = nq;
+          break;
+        }
+      }
+    }
+  }
+  if (X != kNoPos && !(dbg & 32))
+    resolve_tile_sp<NS>(P, rd, len, w, cs, ce, lane, X, sp, used, ex, cnt, sums, term_at);
+  uint64_t tcnt = wave_sum_u64(cnt), tsum[NS > 0 ? NS : SPK_MAX_SPANS];
+  for (uint32_t q = 0; q < nsp; ++q) tsum[q] = wave_sum_u64(sums[q]);
+  // ---- 3. entry alternatives (tile 0's entry is exact) ----
+  uint32_t nalt = X != kNoPos ? 1u : 0u;
+  uint64_t alt_e = kNoPos, alt_c = 0, alt_s[NS > 0 ? NS : SPK_MAX_SPANS];  // lane a holds alt a
+  for (uint32_t q = 0; q < nsp; ++q) alt_s[q] = 0;
+  if (lane == 0 && nalt) {
+    alt_e = X;
+    alt_c = tcnt;
+    for (uint32_t q = 0; q < nsp; ++q) alt_s[q] = tsum[q];
+  }
+  if ((dbg & 4) && t > 0) {
+    // ---- 3a. entry alternatives: other start candidates in chunk 0 after X
+    // whose walk reaches chunk 0's exit; one per lane, in parallel ----
+    const uint64_t e0 = __shfl(ex, 0), ce0 = __shfl(ce, 0);
+    const uint32_t c0 = __shfl(cnt, 0);
+    uint64_t s0[NS > 0 ? NS : SPK_MAX_SPANS];
+    for (uint32_t q = 0; q < nsp; ++q) s0[q] = __shfl(sums[q], 0);
+    const uint64_t lim = e0 < ce0 ? e0 : ce0;
+    for (uint64_t b = X + 1; nalt && nalt < kAlt && b < lim && b < X + 1 + 128; b += 64) {
+      const uint64_t q = b + lane;
+      bool ok = q < lim && screen_one<NS>(P, rd, len, w, q);
+      uint64_t qe = kNoPos, qt;
+      uint32_t qc = 0;
+      uint64_t qs[NS > 0 ? NS : SPK_MAX_SPANS];
+      if (ok) {
+        walk_true<NS>(P, rd, len, w, q, ce0, qe, qc, qs, qt);
+        ok = qe == e0;
+      }
+      uint64_t m = __ballot(ok);
+      while (m && nalt < kAlt) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        const uint64_t ae = __shfl(q, l);
+        const uint64_t ac = tcnt - c0 + __shfl((uint64_t)qc, l);
+        if (lane == nalt) {
+          alt_e = ae;
+          alt_c = ac;
+        }
+        for (uint32_t qq = 0; qq < nsp; ++qq) {
+          const uint64_t v = tsum[qq] - s0[qq] + __shfl(ok ? qs[qq] : 0, l);
+          if (lane == nalt) alt_s[qq] = v;
+        }
+        ++nalt;
+      }
+    }
+  }
+  // ---- publish: chunk states and the tile function ----
+  const uint64_t g = t * 64 + lane;
+  TB.cused[g] = used;
+  TB.cex[g] = ex;
+  TB.ccnt[g] = cnt;
+  for (uint32_t q = 0; q < nsp; ++q) TB.csum[(uint64_t)q * TB.nchunks + g] = sums[q];
+  uint64_t *fn = TB.fn + t * kFnWords;
+  const uint64_t y63 = __shfl(ex, 63);
+  if (lane == 0) {
+    fn[0] = y63;
+    fn[1] = nalt;
+  }
+  if (lane < kAlt) {
+    uint64_t *al = fn + 2 + lane * kAltWords;
+    al[0] = lane < nalt ? alt_e : kNoPos;
+    al[1] = alt_c;
+    for (uint32_t q = 0; q < nsp; ++q) al[2 + q] = alt_s[q];
+  }
+}
+
+// tile t's entry: tile t-1's published exit (tile 0: the payload start)
+__device__ __forceinline__ uint64_t tile_entry(const TileBufs &TB, const VCtl *c, uint64_t t) {
+  return t == 0 ? c->p0 : TB.fn[(t - 1) * kFnWords];
+}
+
+// ---- K2: select each tile's entry; re-walk tiles whose entry is none of
+// theirs (one wave per tile; only those waves stage anything) ---------------
+template <int NS>
+__global__ __launch_bounds__(64) void vec_tile_select(DecArgs a, WalkProg P,
+                                                      const uint8_t *__restrict__ wire,
+                                                      uint8_t *__restrict__ ws, TileBufs TB,
+                                                      uint32_t pass) {
+  __shared__ v4u_t win_s[1][kTileVec + 1];
+  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
+  FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
+  const uint32_t lane = threadIdx.x;
+  const uint64_t t = blockIdx.x;
+  if (t >= TB.ntiles || !vec_live(c)) return;
+  if (pass > 0 && !fc->broken[pass - 1]) return;  // the previous pass fixed nothing
+  uint64_t *fn = TB.fn + t * kFnWords;
+  const uint64_t T = tile_entry(TB, c, t);
+  int32_t sel = kSelBroken;
+  if (T == kTermPos) {
+    sel = kSelTerm;
+  } else if (T != kNoPos) {
+    const uint32_t nalt = (uint32_t)fn[1];
+    for (uint32_t k = 0; k < nalt && k < kAlt; ++k)
+      if (fn[2 + k * kAltWords] == T) {
+        sel = (int32_t)k;
+        break;
+      }
+  }
+  if (sel != kSelBroken || T == kNoPos) {
+    if (lane == 0) TB.sel[t] = sel;
+    return;
+  }
+  // broken: re-resolve the whole tile from its true entry
+  if (lane == 0) atomicAdd(&fc->broken[pass], 1ull);
+  const uint32_t w = c->w;
+  const uint64_t len = a.wire_len, p0 = c->p0;
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  const uint64_t ts = p0 + t * kTileBytes;
+  const TileView tv = stage_tile(win_s[0], wire, len, ts, w, lane);
+  const uint64_t cs = ts + (uint64_t)lane * kTChunk;
+  const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
+  const uint64_t g = t * 64 + lane;
+  uint64_t used = TB.cused[g], ex = TB.cex[g], term_at = kTermPos;
+  uint32_t cnt = TB.ccnt[g];
+  uint64_t sums[NS > 0 ? NS : SPK_MAX_SPANS];
+  for (uint32_t q = 0; q < nsp; ++q) sums[q] = TB.csum[(uint64_t)q * TB.nchunks + g];
+  resolve_tile<NS>(P, tv.rd, len, w, ce, lane, T, used, ex, cnt, sums, term_at);
+  const uint64_t tcnt = wave_sum_u64(cnt);
+  uint64_t tsum[NS > 0 ? NS : SPK_MAX_SPANS];
+  for (uint32_t q = 0; q < nsp; ++q) tsum[q] = wave_sum_u64(sums[q]);
+  TB.cused[g] = used;
+  TB.cex[g] = ex;
+  TB.ccnt[g] = cnt;
+  for (uint32_t q = 0; q < nsp; ++q) TB.csum[(uint64_t)q * TB.nchunks + g] = sums[q];
+  const uint64_t y63 = __shfl(ex, 63);
+  if (lane == 0) {
+    fn[0] = y63;
+    fn[1] = 1;
+    fn[2] = T;
+    fn[3] = tcnt;
+    for (uint32_t q = 0; q < nsp; ++q) fn[4 + q] = tsum[q];
+    TB.sel[t] = 0;
+  }
+}
+
+// Residual entries no pass could select (an exit that moved twice in a row):
+// one wave, tiles in order. Normally exits at once.
+template <int NS>
+__global__ __launch_bounds__(64) void vec_tile_seqfix(DecArgs a, WalkProg P,
+                                                      const uint8_t *__restrict__ wire,
+                                                      uint8_t *__restrict__ ws, TileBufs TB,
+                                                      uint32_t last_pass) {
+  __shared__ v4u_t win_s[1][kTileVec + 1];
+  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
+  FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
+  const uint32_t lane = threadIdx.x;
+  if (!vec_live(c) || !fc->broken[last_pass]) return;
+  const uint32_t w = c->w;
+  const uint64_t len = a.wire_len, p0 = c->p0;
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  for (uint64_t t = 0; t < TB.ntiles; ++t) {
+    uint64_t *fn = TB.fn + t * kFnWords;
+    const uint64_t T = tile_entry(TB, c, t);
+    int32_t sel = kSelBroken;
+    if (T == kTermPos) {
+      sel = kSelTerm;
+    } else {
+      const uint32_t nalt = (uint32_t)fn[1];
+      for (uint32_t k = 0; k < nalt && k < kAlt; ++k)
+        if (fn[2 + k * kAltWords] == T) {
+          sel = (int32_t)k;
+          break;
+        }
+    }
+    if (sel != kSelBroken || T == kNoPos) {
+      if (lane == 0) TB.sel[t] = sel;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      continue;
+    }
+    const uint64_t ts = p0 + t * kTileBytes;
+    const TileView tv = stage_tile(win_s[0], wire, len, ts, w, lane);
+    const uint64_t cs = ts + (uint64_t)lane * kTChunk;
+    const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
+    const uint64_t g = t * 64 + lane;
+    uint64_t used = TB.cused[g], ex = TB.cex[g], term_at = kTermPos;
+    uint32_t cnt = TB.ccnt[g];
+    uint64_t sums[NS > 0 ? NS : SPK_MAX_SPANS];
+    for (uint32_t q = 0; q < nsp; ++q) sums[q] = TB.csum[(uint64_t)q * TB.nchunks + g];
+    resolve_tile<NS>(P, tv.rd, len, w, ce, lane, T, used, ex, cnt, sums, term_at);
+    const uint64_t tcnt = wave_sum_u64(cnt);
+    uint64_t tsum[NS > 0 ? NS : SPK_MAX_SPANS];
+    for (uint32_t q = 0; q < nsp; ++q) tsum[q] = wave_sum_u64(sums[q]);
+    TB.cused[g] = used;
+    TB.cex[g] = ex;
+    TB.ccnt[g] = cnt;
+    for (uint32_t q = 0; q < nsp; ++q) TB.csum[(uint64_t)q * TB.nchunks + g] = sums[q];
+    const uint64_t y63 = __shfl(ex, 63);
+    if (lane == 0) {
+      fn[0] = y63;
+      fn[1] = 1;
+      fn[2] = T;
+      fn[3] = tcnt;
+      for (uint32_t q = 0; q < nsp; ++q) fn[4 + q] = tsum[q];
+      TB.sel[t] = 0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+}
+
+// ---- K3: the selected contribution of every tile; the first tile whose
+// path ends inside it (its exit is kTermPos) --------------------------------
+__global__ __launch_bounds__(256) void vec_tile_contrib(uint8_t *__restrict__ ws, TileBufs TB,
+                                                        uint32_t nsp) {
+  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
+  FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= TB.ntiles || !vec_live(c)) return;
+  const uint64_t *fn = TB.fn + t * kFnWords;
+  const int32_t sel = TB.sel[t];
+  uint64_t cnt = 0, s[SPK_MAX_SPANS] = {};
+  if (sel >= 0) {
+    cnt = fn[2 + sel * kAltWords + 1];
+    for (uint32_t q = 0; q < nsp; ++q) s[q] = fn[2 + sel * kAltWords + 2 + q];
+    if (fn[0] == kTermPos) atomicMin(&fc->term_tile, (unsigned long long)t);
+  } else if (sel == kSelTerm) {
+    atomicMin(&fc->term_tile, (unsigned long long)t);
+  } else {
+    atomicAdd(&fc->unresolved, 1ull);  // never expected after the fix passes
+  }
+  TB.contrib[t] = cnt;
+  for (uint32_t q = 0; q < nsp; ++q) TB.contrib[(uint64_t)(1 + q) * TB.ntiles + t] = s[q];
+}
+
+// exclusive prefix sums of the 1 + nsp contribution columns over the tiles,
+// zero past fc->term_tile; totals -> fc->total / fc->stot
+constexpr uint32_t kTScanIPT = 8;
+constexpr uint64_t kTScanBlock = 256ull * kTScanIPT;
+__global__ __launch_bounds__(256) void tscan_reduce(const uint8_t *__restrict__ ws, TileBufs TB,
+                                                    uint32_t ncol) {
+  __shared__ uint64_t sh[4];
+  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
+  const FCtl *fc = reinterpret_cast<const FCtl *>(ws + kWsFCtl);
+  if (!vec_live(c)) return;
+  const uint64_t lim = fc->term_tile < TB.ntiles ? fc->term_tile + 1 : TB.ntiles;
+  const uint64_t b0 = (uint64_t)blockIdx.x * kTScanBlock;
+  for (uint32_t col = 0; col < ncol; ++col) {
+    const uint64_t *in = TB.contrib + (uint64_t)col * TB.ntiles;
+    uint64_t v = 0;
+    for (uint32_t j = 0; j < kTScanIPT; ++j) {
+      const uint64_t i = b0 + (uint64_t)j * 256 + threadIdx.x;
+      if (i < lim) v += in[i];
+    }
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) TB.scan[(uint64_t)col * gridDim.x + blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+    __syncthreads();
+  }
+}
+__global__ __launch_bounds__(1024) void tscan_top(uint8_t *__restrict__ ws, TileBufs TB,
+                                                  uint32_t ncol, uint64_t nb) {
+  __shared__ uint64_t sh[16];
+  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
+  FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
+  if (!vec_live(c)) return;
+  for (uint32_t col = 0; col < ncol; ++col) {
+    uint64_t *bs = TB.scan + (uint64_t)col * nb;
+    uint64_t carry = 0;
+    for (uint64_t b0 = 0; b0 < nb; b0 += blockDim.x) {
+      const uint64_t b = b0 + threadIdx.x;
+      const uint64_t v = b < nb ? bs[b] : 0;
+      uint64_t tot;
+      const uint64_t ex = block_excl_scan(v, &tot, sh);
+      if (b < nb) bs[b] = carry + ex;
+      carry += tot;
+    }
+    if (threadIdx.x == 0) {
+      if (col == 0)
+        fc->total = carry;
+      else
+        fc->stot[col - 1] = carry;
+    }
+  }
+}
+__global__ __launch_bounds__(256) void tscan_apply(const uint8_t *__restrict__ ws, TileBufs TB,
+                                                   uint32_t ncol) {
+  __shared__ uint64_t sh[4];
+  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
+  const FCtl *fc = reinterpret_cast<const FCtl *>(ws + kWsFCtl);
+  if (!vec_live(c)) return;
+  const uint64_t lim = fc->term_tile < TB.ntiles ? fc->term_tile + 1 : TB.ntiles;
+  const uint64_t b0 = (uint64_t)blockIdx.x * kTScanBlock;
+  const uint64_t i0 = b0 + (uint64_t)threadIdx.x * kTScanIPT;
+  for (uint32_t col = 0; col < ncol; ++col) {
+    uint64_t *io = TB.contrib + (uint64_t)col * TB.ntiles;
+    uint64_t v[kTScanIPT], s = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kTScanIPT; ++j) {
+      v[j] = i0 + j < lim ? io[i0 + j] : 0;
+      s += v[j];
+    }
+    uint64_t tot;
+    uint64_t run = TB.scan[(uint64_t)col * gridDim.x + blockIdx.x] + block_excl_scan(s, &tot, sh);
+#pragma unroll
+    for (uint32_t j = 0; j < kTScanIPT; ++j) {
+      if (i0 + j < TB.ntiles) io[i0 + j] = run;
+      run += v[j];
+    }
+  }
+}
+
+// ---- K4 ----------------------------------------------------------------------
+template <int NS>
+__global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkProg P,
+                                                                const uint8_t *__restrict__ wire,
+                                                                uint8_t *__restrict__ ws,
+                                                                TileBufs TB,
+                                                                uint8_t *__restrict__ recs,
+                                                                uint32_t dbg) {
+  __shared__ v4u_t win_s[kDecWaves][kTileVec + 1];
+  __shared__ uint16_t tab_s[kDecWaves][kTab];
+  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
+  FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t t = (uint64_t)blockIdx.x * kDecWaves + wv;
+  if (t >= TB.ntiles || !vec_live(c) || t > fc->term_tile) return;
+  const uint64_t n = c->n;
+  const uint64_t base = TB.contrib[t];
+  const int32_t sel = TB.sel[t];
+  if (base >= n || sel < 0) return;
+  const uint32_t w = c->w;
+  const uint64_t len = a.wire_len, p0 = c->p0;
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  const uint64_t ts = p0 + t * kTileBytes;
+  const TileView tv = stage_tile(win_s[wv], wire, len, ts, w, lane);
+  const WinReader &rd = tv.rd;
+  if (dbg & 128) {
+    if (lane == 0 && rd.byte(ts) == 0x1234) fc->end_pos = 1;  // keep the staging alive
+    return;
+  }
+  const uint64_t cs = ts + (uint64_t)lane * kTChunk;
+  const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
+  const uint64_t g = t * 64 + lane;
+  uint64_t used = TB.cused[g], ex = TB.cex[g];
+  uint32_t cnt = TB.ccnt[g];
+  if (sel > 0 && lane == 0) {  // another entry of chunk 0 (same exit)
+    const uint64_t T = tile_entry(TB, c, t);
+    uint64_t qe, qt, qs[NS > 0 ? NS : SPK_MAX_SPANS];
+    walk_true<NS>(P, rd, len, w, T, ce, qe, cnt, qs, qt);
+    used = T;
+  }
+  uint64_t psum[SPK_MAX_SPANS];
+  for (uint32_t q = 0; q < nsp; ++q) psum[q] = TB.contrib[(uint64_t)(1 + q) * TB.ntiles + t];
+  const uint64_t tcnt = wave_sum_u64(cnt);
+  if (ex == kTermPos && used != kNoPos && used != kTermPos && t == fc->term_tile) {
+    // where the true path ends: past this chunk's records
+    uint64_t x = used;
+    for (uint32_t r = 0; r < cnt; ++r) {
+      uint64_t rc[NS > 0 ? NS : SPK_MAX_SPANS];
+      x += wlen_rd<NS>(P, rd, len, x, w, rc);
+    }
+    atomicMin(&fc->term_pos, (unsigned long long)x);
+  }
+  uint64_t rofs;  // this chunk's first record, tile-relative
+  {
+    uint64_t tot;
+    rofs = wave_excl_scan_u64(cnt, lane, &tot);
+  }
+  uint16_t *tab = tab_s[wv];
+  uint64_t carry[NS > 0 ? NS : SPK_MAX_SPANS];
+  for (uint32_t q = 0; q < nsp; ++q) carry[q] = psum[q];
+  const uint64_t nemit = (n - base < tcnt) ? n - base : tcnt;
+  for (uint64_t pass0 = 0; pass0 < nemit; pass0 += kTab) {
+    const uint64_t pend = pass0 + kTab < nemit ? pass0 + kTab : nemit;
+    // record starts of this pass into the table
+    if (cnt && rofs < pend && rofs + cnt > pass0) {
+      uint64_t x = used;
+      for (uint32_t r = 0; r < cnt; ++r) {
+        const uint64_t i = rofs + r;
+        if (i >= pend) break;
+        if (i >= pass0) tab[i - pass0] = (uint16_t)(x - ts);
+        uint64_t rc[NS > 0 ? NS : SPK_MAX_SPANS];
+        x += wlen_rd<NS>(P, rd, len, x, w, rc);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t nrec = pend - pass0;
+    for (uint64_t i0 = 0; i0 < nrec; i0 += 64) {
+      const uint64_t i = i0 + lane;
+      const bool act = i < nrec;
+      const uint64_t pos = ts + (act ? tab[i] : 0);
+      uint64_t rc[SPK_MAX_SPANS] = {};
+      uint64_t L = 0;
+      if (act) L = wlen_rd<NS>(P, rd, len, pos, w, rc);
+      uint64_t off[SPK_MAX_SPANS];
+      bool fits = true;
+      for (uint32_t q = 0; q < nsp; ++q) {
+        uint64_t tot;
+        off[q] = carry[q] + wave_excl_scan_u64(act ? rc[q] : 0, lane, &tot);
+        carry[q] += tot;
+        if (off[q] + rc[q] > a.heap_cap[q]) fits = false;
+      }
+      const uint64_t g = base + pass0 + i;
+      if (act && g < a.rec_cap && fits && !(dbg & 64))
+        emit_record_rd(a.L, rd, pos, w, recs + g * a.L.stride, a.heaps, off, len);
+      if (act && g == n - 1) {
+        fc->end_pos = pos + L;
+        for (uint32_t q = 0; q < nsp; ++q) fc->htot[q] = off[q] + rc[q];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+// Result: count / consume_len / heap use, or the errc of a short payload
+// (no_buffer_space; invalid_buffer for an overlong varint where the path ends).
+__global__ void vec_tile_finish(DecArgs a, const uint8_t *__restrict__ wire,
+                                const uint8_t *__restrict__ ws, spk_dresult_t *res) {
+  if (threadIdx.x != 0) return;
+  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
+  const FCtl *fc = reinterpret_cast<const FCtl *>(ws + kWsFCtl);
+  if (c->errc) return;  // the header errc is already in *res
+  spk_dresult_t r = *res;
+  if (fc->unresolved) {
+    r.errc = SPK_ERRC_INTERNAL;
+    *res = r;
+    return;
+  }
+  const uint64_t total = c->n ? (uint64_t)fc->total : 0;
+  if (c->n && total < c->n) {
+    r.errc = SPK_ERRC_NO_BUFFER_SPACE;
+    if (a.L.n_var && fc->term_pos < a.wire_len) {
+      int32_t ec = SPK_ERRC_NO_BUFFER_SPACE;
+      rec_wire_len(a.L, wire, a.wire_len, fc->term_pos, c->w, &ec);
+      if (ec == SPK_ERRC_INVALID_BUFFER) r.errc = ec;
+    }
+    r.count = 0;
+    r.consumed = 0;
+    for (int k = 0; k < SPK_MAX_SPANS; ++k) r.heap_used[k] = 0;
+  } else {
+    r.count = c->n;
+    const uint64_t end = c->n ? (uint64_t)fc->end_pos : c->p0;
+    r.consumed = end > c->data_len ? end : c->data_len;
+    if (c->n > a.rec_cap && r.errc == 0) r.errc = SPK_ERRC_CAPACITY;
+    for (uint32_t k = 0; k < a.L.n_spans; ++k) {
+      r.heap_used[k] = c->n ? fc->htot[k] : 0;
+      if (r.heap_used[k] > a.heap_cap[k] && r.errc == 0) r.errc = SPK_ERRC_CAPACITY;
+    }
+  }
+  *res = r;
+}
+
+// ===========================================================================
 // host launchers
 // ===========================================================================
 static unsigned grid_for(uint64_t items, uint64_t per_block) {
@@ -2117,11 +3087,98 @@ static hipError_t launch_vec_decode_ns(const DecArgs &a, const WalkProg &P, cons
   return hipGetLastError();
 }
 
+// ---- tile decoder: workspace and launch ---------------------------------------
+struct TileWs {
+  size_t fn, cused, cex, ccnt, csum, sel, contrib, scan, end;
+  uint64_t ntiles, nchunks, nsb;
+};
+static TileWs tile_ws_layout(const spk_layout *L, uint64_t wire_len) {
+  TileWs f = {};
+  uint32_t ns = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i)
+    ns += L->ops[i].kind == SPK_OP_SPAN || L->ops[i].kind == SPK_OP_OPTION;
+  if (!ns) ns = 1;
+  f.ntiles = wire_len / kTileBytes + 1;  // the payload starts past the header
+  f.nchunks = f.ntiles * 64;
+  f.nsb = (f.ntiles + kTScanBlock - 1) / kTScanBlock + 1;
+  size_t off = kWsScratch;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += (bytes + 255) & ~size_t(255);
+    return o;
+  };
+  f.fn = take(f.ntiles * kFnWords * 8);
+  f.cused = take(f.nchunks * 8);
+  f.cex = take(f.nchunks * 8);
+  f.ccnt = take(f.nchunks * 4);
+  f.csum = take(f.nchunks * 8 * ns);
+  f.sel = take(f.ntiles * 4);
+  f.contrib = take(f.ntiles * 8 * (1 + ns));
+  f.scan = take(f.nsb * 8 * (1 + ns));
+  f.end = off;
+  return f;
+}
+
+// SPK_TILE_DBG bits (A/B experiments): 4 = compute entry alternatives in K1
+static uint32_t tile_dbg() {
+  static const uint32_t v = [] {
+    const char *e = getenv("SPK_TILE_DBG");
+    return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
+  }();
+  return v;
+}
+
+template <int NS>
+static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const spk_layout *L,
+                                      const uint8_t *wire, uint8_t *ws, spk_dresult_t *d_res,
+                                      uint8_t *d_recs, hipStream_t s) {
+  const TileWs f = tile_ws_layout(L, a.wire_len);
+  TileBufs TB;
+  TB.fn = reinterpret_cast<uint64_t *>(ws + f.fn);
+  TB.cused = reinterpret_cast<uint64_t *>(ws + f.cused);
+  TB.cex = reinterpret_cast<uint64_t *>(ws + f.cex);
+  TB.ccnt = reinterpret_cast<uint32_t *>(ws + f.ccnt);
+  TB.csum = reinterpret_cast<uint64_t *>(ws + f.csum);
+  TB.sel = reinterpret_cast<int32_t *>(ws + f.sel);
+  TB.contrib = reinterpret_cast<uint64_t *>(ws + f.contrib);
+  TB.scan = reinterpret_cast<uint64_t *>(ws + f.scan);
+  TB.ntiles = f.ntiles;
+  TB.nchunks = f.nchunks;
+  const uint32_t nsp = P.ns ? P.ns : 1;
+  const unsigned nb = (unsigned)((f.ntiles + kTScanBlock - 1) / kTScanBlock);
+  SPK_LAUNCH(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, 0u, (uint64_t)0);
+  SPK_LAUNCH(vec_tile_spec<NS>, dim3(grid_for(f.ntiles, kDecWaves)), dim3(64 * kDecWaves), 0, s,
+             a, P, wire, (const uint8_t *)ws, TB, tile_dbg());
+  for (uint32_t pass = 0; pass < 3; ++pass)
+    SPK_LAUNCH(vec_tile_select<NS>, dim3((unsigned)f.ntiles), dim3(64), 0, s, a, P, wire, ws, TB,
+               pass);
+  SPK_LAUNCH(vec_tile_seqfix<NS>, dim3(1), dim3(64), 0, s, a, P, wire, ws, TB, 2u);
+  SPK_LAUNCH(vec_tile_contrib, dim3(grid_for(f.ntiles, 256)), dim3(256), 0, s, ws, TB, nsp);
+  SPK_LAUNCH(tscan_reduce, dim3(nb), dim3(256), 0, s, (const uint8_t *)ws, TB, 1 + nsp);
+  SPK_LAUNCH(tscan_top, dim3(1), dim3(1024), 0, s, ws, TB, 1 + nsp, (uint64_t)nb);
+  SPK_LAUNCH(tscan_apply, dim3(nb), dim3(256), 0, s, (const uint8_t *)ws, TB, 1 + nsp);
+  SPK_LAUNCH(vec_tile_emit<NS>, dim3(grid_for(f.ntiles, kDecWaves)), dim3(64 * kDecWaves), 0, s,
+             a, P, wire, ws, TB, d_recs, tile_dbg());
+  SPK_LAUNCH(vec_tile_finish, dim3(1), dim3(64), 0, s, a, wire, (const uint8_t *)ws, d_res);
+  return hipGetLastError();
+}
+
+// SPK_VEC_DECODE=legacy selects the multi-pass decoder (A/B runs)
+static bool legacy_vec_decode() {
+  static const int v = [] {
+    const char *e = getenv("SPK_VEC_DECODE");
+    return (e && e[0] == 'l') ? 1 : 0;
+  }();
+  return v != 0;
+}
+
 size_t var_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len) {
   size_t enc = kWsScratch + (grid_for(n, kPlanRPB) + 1) * sizeof(Partial) + 256;
   size_t dec_msg = kWsScratch + n * sizeof(MsgState) +
                    (grid_for(n, kThreads) + 1) * kBs * 8 + 256;
   size_t dec_vec = vec_ws_layout(L, wire_len, n).end + 256;
+  const size_t dec_tiles = tile_ws_layout(L, wire_len).end + 256;
+  if (dec_tiles > dec_vec) dec_vec = dec_tiles;
   size_t m = enc;
   if (mode == SPK_MODE_MESSAGES) m = m > dec_msg ? m : dec_msg;
   if (mode == SPK_MODE_VECTOR) m = m > dec_vec ? m : dec_vec;
@@ -2261,6 +3318,13 @@ hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
   (void)ws_bytes;
   // NS = -1: the walkers read varints (kept out of the other instantiations:
   // the inlined LEB128 loops cost registers in the hot walks)
+  if (!legacy_vec_decode()) {
+    uint8_t *r = (uint8_t *)d_recs;
+    if (P.nv) return launch_vec_tiles_ns<-1>(a, P, L, wire, ws, d_res, r, s);
+    if (P.ns == 1) return launch_vec_tiles_ns<1>(a, P, L, wire, ws, d_res, r, s);
+    if (P.ns == 2) return launch_vec_tiles_ns<2>(a, P, L, wire, ws, d_res, r, s);
+    return launch_vec_tiles_ns<0>(a, P, L, wire, ws, d_res, r, s);
+  }
   if (P.nv) return launch_vec_decode_ns<-1>(a, P, wire, ws, v, d_res, (uint8_t *)d_recs, s);
   if (P.ns == 1) return launch_vec_decode_ns<1>(a, P, wire, ws, v, d_res, (uint8_t *)d_recs, s);
   if (P.ns == 2) return launch_vec_decode_ns<2>(a, P, wire, ws, v, d_res, (uint8_t *)d_recs, s);
