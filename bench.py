@@ -75,6 +75,10 @@ def parse():
     ap.add_argument("--host-path", action="store_true",
                     help="also time H2D + encode + decode + D2H from pinned host buffers")
     ap.add_argument("--pmc-dir", default="", help="directory of pmc_<config>.json summaries")
+    ap.add_argument("--no-concat", action="store_true",
+                    help="N>1: skip the one-message concatenation timing (concat_*)")
+    ap.add_argument("--concat-records", type=int, default=8_000_000,
+                    help="N>1: Rec64 records per rank of the one-message concatenation")
     return ap.parse_args()
 
 
@@ -513,6 +517,82 @@ def host_path(wl, torch, dev):
                     "D2H of decoded records (+heaps); pinned host buffers, one stream"}
 
 
+def concat_bench(torch, dist, world, rank, dev, n, reps=3):
+    """N>1 only: ONE serialize(vector<Rec64>) message over the records of all
+    ranks (yalantinglibs_amd/parallel.py ShardedVectorEncoder), the data-path
+    collective the weak-scaling headline does not have. Times, max over ranks,
+    best of `reps`: the plan agreement (all-reduce SUM/MAX + all-gather of body
+    sizes), each rank's body encode, and three concatenations of the bodies —
+    P2P gather into rank 0's message buffer (grouped RCCL send/recv over
+    xGMI), all-gather (every rank gets the whole message), and each rank's D2H
+    of its body into pinned host memory (the coro_rpc destination). Checked
+    once: rank 0 decodes the gathered message and compares it with the global
+    synthetic batch."""
+    from yalantinglibs_amd import layout as LY
+    from yalantinglibs_amd import parallel as PAR
+    from yalantinglibs_amd import struct_pack as SP
+    cd = SP.Codec(LY.case_layout("rec64"), device=dev)
+    batch = SP.synth_batch(cd, "rec64", n, SEEDS["rec64"], 0, first=rank * n)
+    enc = PAR.ShardedVectorEncoder(cd)
+    red_dev = torch.device("cpu") if dist.get_backend() == "gloo" else dev
+
+    def timed(fn):
+        best = None
+        for i in range(reps + 1):
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize(dev)
+            dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=red_dev)
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+            if i:  # the first run is a warmup
+                best = dt.item() if best is None else min(best, dt.item())
+        return best
+
+    sp = enc.plan(batch)
+    t_plan = timed(lambda: enc.plan(batch))
+    mine = sp.body_bytes[rank]
+    body = torch.empty(max(mine, 1), dtype=torch.uint8, device=dev)
+    t_enc = timed(lambda: enc.encode_body(batch, sp.width, body))
+    out = torch.empty(sp.total_bytes, dtype=torch.uint8, device=dev) if rank == 0 else None
+    t_p2p = timed(lambda: enc.gather(sp, body, out))
+    check = "skipped"
+    if rank == 0:
+        res, back, _ = cd.deserialize(out)
+        want = SP.synth_batch(cd, "rec64", world * n, SEEDS["rec64"], 0, first=0)
+        check = "ok" if (res.errc == 0 and res.count == world * n and
+                         torch.equal(back.recs, want.recs)) else f"FAILED errc {res.errc}"
+        del back, want
+    del out
+    torch.cuda.empty_cache()
+    full = torch.empty(sp.total_bytes, dtype=torch.uint8, device=dev)
+    slab = [None]
+
+    def ag():
+        slab[0] = enc.all_gather(sp, body, full, slab[0])
+    t_ag = timed(ag)
+    del full, slab
+    host = torch.empty(max(mine, 1), dtype=torch.uint8).pin_memory()
+    t_d2h = timed(lambda: host.copy_(body[:mine], non_blocking=True))
+    total = sp.total_bytes
+    gbs = lambda b, t: round(b / t / 1e9, 2)
+    return {
+        "workload": f"one serialize(vector<Rec64>) message of {world} x {n} records "
+                    f"({total / 2**30:.2f} GiB), bodies encoded on their own ranks",
+        "records_per_rank": n, "message_bytes": total, "width": sp.width,
+        "plan_ms": round(t_plan * 1e3, 3), "encode_body_ms": round(t_enc * 1e3, 3),
+        "p2p_gather_ms": round(t_p2p * 1e3, 3),
+        "p2p_gather_gbs": gbs(total - sp.body_bytes[0], t_p2p),
+        "all_gather_ms": round(t_ag * 1e3, 3), "all_gather_gbs": gbs(total * (world - 1), t_ag),
+        "d2h_pinned_ms": round(t_d2h * 1e3, 3), "d2h_pinned_gbs_per_rank": gbs(mine, t_d2h),
+        "check": check,
+        "note": "p2p_gather_gbs = bytes received by rank 0 / time; all_gather_gbs = bytes "
+                "received over all ranks / time; times are max over ranks, best of "
+                f"{reps} after a warmup",
+    }
+
+
 def main():
     args = parse()
     import torch
@@ -536,6 +616,12 @@ def main():
 
     head = run_config(args.config, args, torch, dist, world, rank, dev, args.steps,
                       args.warmup, args.settle, cpu=True)
+    concat = None
+    if world > 1 and not args.no_concat:
+        try:
+            concat = concat_bench(torch, dist, world, rank, dev, args.concat_records)
+        except Exception as e:  # never lose the headline line
+            concat = {"error": f"{type(e).__name__}: {e}"}
     extra = {}
     if world == 1 and not args.no_extra and args.config == "c2":
         for cfg in EXTRA:
@@ -561,6 +647,10 @@ def main():
         }
         if "host_path" in head:
             line["host_path"] = head["host_path"]
+        if concat is not None:
+            line["concat_ms"] = concat.get("p2p_gather_ms")
+            line["concat_gbs"] = concat.get("p2p_gather_gbs")
+            line["concat"] = concat
         if extra:
             line["extra"] = {"configs": extra}
         print(json.dumps(line), flush=True)

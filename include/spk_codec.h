@@ -49,6 +49,28 @@
  *                                           10th byte with its high bit set is
  *                                           invalid_buffer; a truncated varint
  *                                           is no_buffer_space. Not a container.
+ *   SPK_OP_ARRAY {rec_off, size, aux}      a std::vector<U> / std::string-like
+ *                                           container whose element U is NOT
+ *                                           trivially serializable (e.g.
+ *                                           vector<string>, vector<struct with
+ *                                           a string>): the record holds a u32
+ *                                           element count at rec_off and a u64
+ *                                           element offset at aux into this
+ *                                           op's heap of `size`-byte element
+ *                                           records; the ops that follow, up
+ *                                           to the matching SPK_OP_END, are
+ *                                           U's flattened layout (offsets
+ *                                           relative to an element record; they
+ *                                           may nest further ARRAYs). Wire:
+ *                                           [count:w] then each element as
+ *                                           serialize_one(U) (packer.hpp:
+ *                                           365-367; decode: unpacker.hpp:
+ *                                           1208-1226, stops at the first
+ *                                           failing element).
+ *   SPK_OP_END {0, 0, 0, 0}                closes the innermost open ARRAY.
+ * Heaps are numbered in op order over SPAN, OPTION and ARRAY ops at every
+ * nesting level; heap k of an ARRAY holds element records, counted in
+ * elements like the others. Decode writes every heap packed in wire order.
  * A trivially-serializable T (SPK_LAYOUT_TRIVIAL) is a single COPY of the
  * whole record (reference packer.hpp:418-421, unpacker.hpp:1300-1312).
  *
@@ -108,6 +130,9 @@ extern "C" {
 #define SPK_OP_SPAN 2u
 #define SPK_OP_OPTION 3u
 #define SPK_OP_VARINT 4u
+#define SPK_OP_ARRAY 5u
+#define SPK_OP_END 6u
+#define SPK_MAX_DEPTH 4u       /* ARRAY nesting levels                       */
 
 /* spk_op.aux of an SPK_OP_VARINT */
 #define SPK_VARINT_ZIGZAG 0x1u /* var_int32_t / var_int64_t (sint<T>): zigzag */
@@ -126,7 +151,7 @@ extern "C" {
 #define SPK_LAYOUT_TRIVIAL 0x1u   /* is_trivial_serializable<T>: 1 COPY op  */
 
 typedef struct spk_op {
-  uint32_t kind;    /* SPK_OP_COPY | SPK_OP_SPAN | SPK_OP_OPTION | VARINT    */
+  uint32_t kind;    /* SPK_OP_COPY | SPAN | OPTION | VARINT | ARRAY | END    */
   uint32_t rec_off; /* COPY: source byte offset; SPAN: u32 count offset      */
   uint32_t size;    /* COPY: byte length;       SPAN: element size (bytes)   */
   uint32_t aux;     /* SPAN: u64 heap element-offset field offset; COPY: 0   */
@@ -164,6 +189,13 @@ typedef struct spk_plan_t {
   uint32_t has_meta;
 } spk_plan_t;
 
+/* spk_plan with the span heaps: required for layouts with SPK_OP_ARRAY
+ * (their sizes depend on the element records; spk_plan rejects such a
+ * non-empty batch with SPK_E_ARG), accepted for every layout. */
+int spk_plan_ex(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
+                const void *const *d_heaps, spk_plan_t *d_plan, void *d_ws,
+                size_t ws_bytes, void *stream);
+
 /* Decode result (device memory, written by spk_decode). */
 typedef struct spk_dresult_t {
   int32_t errc;         /* reference errc, or SPK_ERRC_CAPACITY            */
@@ -171,6 +203,13 @@ typedef struct spk_dresult_t {
   uint64_t count;       /* records decoded (VECTOR) / messages ok (MESSAGES)*/
   uint64_t consumed;    /* consume_len (struct_pack.hpp:343-357)           */
   uint64_t heap_used[SPK_MAX_SPANS]; /* elements written per span heap     */
+  /* diagnostics of the SPK_MODE_VECTOR decoder for variable-size records
+   * (zero otherwise; not part of the reference's result): 16 KiB tiles whose
+   * speculated record grid missed and were re-resolved in parallel, and tiles
+   * the one-wave sequential fixer then had to visit (a record spanning k
+   * tiles counts k). */
+  uint32_t tiles_repaired;
+  uint32_t tiles_sequential;
 } spk_dresult_t;
 
 /* ------------------------------------------------------------------------ */

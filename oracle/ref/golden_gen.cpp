@@ -97,6 +97,12 @@ static int cmd_kat() {
           struct_pack::var_uint64_t>(os, "varints", first);
   kat_one<std::array<int16_t, 3>>(os, "array<int16_t,3>", first);
   kat_one<std::vector<std::string>>(os, "vector<string>", first);
+  kat_one<Tags>(os, "Tags", first);
+  kat_one<std::vector<Tags>>(os, "vector<Tags>", first);
+  kat_one<Group>(os, "Group", first);
+  kat_one<std::vector<Group>>(os, "vector<Group>", first);
+  kat_one<Deep>(os, "Deep", first);
+  kat_one<std::vector<Deep>>(os, "vector<Deep>", first);
   kat_one<uint8_t, uint16_t, uint32_t, uint64_t, int8_t, int16_t, int64_t,
           bool, char, float, double>(os, "fundamentals", first);
   os << "\n}\n";
@@ -171,6 +177,12 @@ static bool with_case(const Args &a, F &&f) {
     return f.template operator()<Var>([=](Var &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "varp")
     return f.template operator()<VarP>([=](VarP &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "tags")
+    return f.template operator()<Tags>([=](Tags &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "group")
+    return f.template operator()<Group>([=](Group &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "deep")
+    return f.template operator()<Deep>([=](Deep &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "rect")  // C1: benchmark rect<int> default values
     return f.template operator()<rect<int>>([=](rect<int> &o, uint64_t) { o = rect<int>{}; });
   if (k == "rpcrect")

@@ -157,6 +157,22 @@ struct OptP {
   std::optional<rpcb::point> b;
 };
 
+// ---- containers of non-trivially-serializable elements (SPK_OP_ARRAY) ----
+struct Tags {  // vector<string>
+  int32_t id;
+  std::vector<std::string> tags;
+  double w;
+};
+struct Group {  // vector<struct with a string>, then a string
+  int64_t gid;
+  std::vector<RecS> members;
+  std::string label;
+};
+struct Deep {  // two nesting levels: vector<vector<string>>
+  uint16_t k;
+  std::vector<std::vector<std::string>> m;
+};
+
 namespace spk_gold {
 
 inline Rec64 make_rec64(uint64_t seed, uint64_t i) {
@@ -295,6 +311,47 @@ inline std::vector<int32_t> make_ints(uint64_t seed, uint64_t i,
   for (uint32_t j = 0; j < n; ++j)
     v[j] = (int32_t)(uint32_t)mix64(rnd(seed, i, 2) + j);
   return v;
+}
+
+// element j of a record's list: a short string from word h (len h % 13)
+inline std::string tag_chars(uint64_t h) {
+  std::string s((size_t)(h % 13), '\0');
+  for (size_t k = 0; k < s.size(); ++k) {
+    uint64_t w = mix64(h + (k >> 3));
+    s[k] = (char)('a' + ((w >> ((k & 7) * 8)) & 0xFF) % 26);
+  }
+  return s;
+}
+inline uint64_t elem_word(uint64_t seed, uint64_t i, uint64_t j) {
+  return mix64(rnd(seed, i, 2 + j % 56) ^ j);
+}
+
+inline void fill(Tags &t, uint64_t seed, uint64_t i, uint32_t maxn) {
+  t.id = (int32_t)(uint32_t)rnd(seed, i, 0);
+  const uint32_t n = (uint32_t)(rnd(seed, i, 1) % (uint64_t)(maxn + 1));
+  t.tags.resize(n);
+  for (uint32_t j = 0; j < n; ++j) t.tags[j] = tag_chars(elem_word(seed, i, j));
+  t.w = rd(rnd(seed, i, 60));
+}
+
+inline void fill(Group &g, uint64_t seed, uint64_t i, uint32_t maxn) {
+  g.gid = (int64_t)rnd(seed, i, 0);
+  const uint32_t n = (uint32_t)(rnd(seed, i, 1) % (uint64_t)(maxn + 1));
+  const uint64_t s2 = mix64(seed + i);  // member j = RecS j of seed s2
+  g.members.resize(n);
+  for (uint32_t j = 0; j < n; ++j) g.members[j] = make_recs(s2, j, 20);
+  g.label = make_chars(seed, i, 12);
+}
+
+inline void fill(Deep &d, uint64_t seed, uint64_t i, uint32_t maxn) {
+  d.k = (uint16_t)rnd(seed, i, 0);
+  const uint32_t n = (uint32_t)(rnd(seed, i, 1) % (uint64_t)(maxn + 1));
+  d.m.resize(n);
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint64_t h = elem_word(seed, i, j);
+    d.m[j].resize((size_t)(h % 5));
+    for (size_t q = 0; q < d.m[j].size(); ++q) d.m[j][q] = tag_chars(mix64(h + q + 1));
+  }
 }
 
 }  // namespace spk_gold

@@ -54,10 +54,26 @@ static void vi_store(uint8_t *rec, const spk_op *op, uint64_t v) {
 }
 
 /* ---- layout helpers ---------------------------------------------------- */
-static unsigned n_spans(const spk_layout *L) {
+/* Heaps are numbered in op order over SPAN, OPTION and ARRAY ops at every
+ * nesting level; an ARRAY's element ops run to its matching END. */
+static int is_heap_op(uint32_t k) {
+  return k == SPK_OP_SPAN || k == SPK_OP_OPTION || k == SPK_OP_ARRAY;
+}
+static unsigned heap_of(const spk_layout *L, uint32_t i) {
   unsigned k = 0;
-  for (uint32_t i = 0; i < L->n_ops; ++i) k += L->ops[i].kind == SPK_OP_SPAN;
+  for (uint32_t j = 0; j < i; ++j) k += is_heap_op(L->ops[j].kind);
   return k;
+}
+static uint32_t end_of(const spk_layout *L, uint32_t i) { /* ARRAY at i -> its END */
+  unsigned depth = 0;
+  for (uint32_t j = i + 1; j < L->n_ops; ++j) {
+    if (L->ops[j].kind == SPK_OP_ARRAY) ++depth;
+    if (L->ops[j].kind == SPK_OP_END) {
+      if (!depth) return j;
+      --depth;
+    }
+  }
+  return L->n_ops;
 }
 static uint64_t rec_count(const uint8_t *rec, const spk_op *op) {
   uint32_t c;
@@ -65,8 +81,8 @@ static uint64_t rec_count(const uint8_t *rec, const spk_op *op) {
   if (op->kind == SPK_OP_OPTION) return c != 0; /* has_value() */
   return c;
 }
-/* prefix bytes of a SPAN (container length, width w) or an OPTION (the bool
- * has_value: write_wrapper<sizeof(bool)>, packer.hpp:382-388) */
+/* prefix bytes of a SPAN / ARRAY (container length, width w) or an OPTION
+ * (the bool has_value: write_wrapper<sizeof(bool)>, packer.hpp:382-388) */
 static unsigned op_pw(const spk_op *op, unsigned w) {
   return op->kind == SPK_OP_OPTION ? 1u : w;
 }
@@ -123,42 +139,55 @@ static uint8_t *write_header(uint8_t *p, const spk_msgfmt *f, const hdr_t *h) {
   return p;
 }
 
-/* per-record wire bytes: calculate_one_size (calculate_size.hpp:39-183) */
-static uint64_t rec_wire_size(const spk_layout *L, const uint8_t *rec,
-                              unsigned w) {
-  if (L->flags & SPK_LAYOUT_TRIVIAL) return L->rec_stride;
-  uint64_t s = 0;
-  for (uint32_t i = 0; i < L->n_ops; ++i) {
+/* calculate_one_size (calculate_size.hpp:39-183) of ops [i0, i1) over one
+ * (element) record: payload bytes without count fields in *bytes, count
+ * fields (size_cnt) in *cnts, the largest container length (max_size) in
+ * *maxc; a container of non-trivially-serializable elements sums its
+ * elements (calculate_size.hpp:76-87) */
+static void ops_size(const spk_layout *L, uint32_t i0, uint32_t i1, const uint8_t *rec,
+                     const void *const *heaps, uint64_t *bytes, uint64_t *cnts,
+                     uint64_t *maxc) {
+  for (uint32_t i = i0; i < i1; ++i) {
     const spk_op *op = &L->ops[i];
-    if (op->kind == SPK_OP_COPY)
-      s += op->size;
-    else if (op->kind == SPK_OP_VARINT)
-      s += vi_len(vi_value(rec, op));
-    else
-      s += op_pw(op, w) + rec_count(rec, op) * op->size;
-  }
-  return s;
-}
-
-static uint64_t rec_max_count(const spk_layout *L, const uint8_t *rec) {
-  uint64_t m = 0;
-  for (uint32_t i = 0; i < L->n_ops; ++i)
-    if (L->ops[i].kind == SPK_OP_SPAN) {
-      uint64_t c = rec_count(rec, &L->ops[i]);
-      if (c > m) m = c;
+    if (op->kind == SPK_OP_COPY) {
+      *bytes += op->size;
+    } else if (op->kind == SPK_OP_VARINT) {
+      *bytes += vi_len(vi_value(rec, op));
+    } else if (op->kind == SPK_OP_OPTION) {
+      *bytes += 1 + rec_count(rec, op) * op->size;
+    } else if (op->kind == SPK_OP_SPAN) {
+      uint64_t c = rec_count(rec, op);
+      *cnts += 1;
+      *bytes += c * op->size;
+      if (c > *maxc) *maxc = c;
+    } else if (op->kind == SPK_OP_ARRAY) {
+      const uint32_t e = end_of(L, i);
+      const uint64_t c = rec_count(rec, op);
+      const uint8_t *el = (const uint8_t *)heaps[heap_of(L, i)] + rec_heapoff(rec, op) * op->size;
+      *cnts += 1;
+      if (c > *maxc) *maxc = c;
+      for (uint64_t j = 0; j < c; ++j) ops_size(L, i + 1, e, el + j * op->size, heaps, bytes, cnts, maxc);
+      i = e;
     }
-  return m;
+  }
 }
 
-/* serialize_one (packer.hpp:237-527) for one flattened record */
-static uint8_t *write_record(const spk_layout *L, const uint8_t *rec,
-                             const void *const *heaps, unsigned w, uint8_t *p) {
-  if (L->flags & SPK_LAYOUT_TRIVIAL) { /* packer.hpp:418-421 (incl. padding) */
-    memcpy(p, rec, L->rec_stride);
-    return p + L->rec_stride;
+static void rec_size(const spk_layout *L, const uint8_t *rec, const void *const *heaps,
+                     uint64_t *bytes, uint64_t *cnts, uint64_t *maxc) {
+  *bytes = *cnts = *maxc = 0;
+  if (L->flags & SPK_LAYOUT_TRIVIAL) {
+    *bytes = L->rec_stride;
+    return;
   }
-  unsigned sk = 0;
-  for (uint32_t i = 0; i < L->n_ops; ++i) {
+  ops_size(L, 0, L->n_ops, rec, heaps, bytes, cnts, maxc);
+}
+
+/* serialize_one (packer.hpp:237-527) of ops [i0, i1) over one (element)
+ * record; a container of non-trivially-serializable elements writes its
+ * length then each element (packer.hpp:365-367) */
+static uint8_t *ops_write(const spk_layout *L, uint32_t i0, uint32_t i1, const uint8_t *rec,
+                          const void *const *heaps, unsigned w, uint8_t *p) {
+  for (uint32_t i = i0; i < i1; ++i) {
     const spk_op *op = &L->ops[i];
     if (op->kind == SPK_OP_COPY) { /* write_wrapper<sizeof(T)> :264-267 */
       memcpy(p, rec + op->rec_off, op->size);
@@ -172,6 +201,15 @@ static uint8_t *write_record(const spk_layout *L, const uint8_t *rec,
       }
       *p++ = (uint8_t)v;
     }
+    else if (op->kind == SPK_OP_ARRAY) {
+      const uint32_t e = end_of(L, i);
+      const uint64_t c = rec_count(rec, op);
+      const uint8_t *el = (const uint8_t *)heaps[heap_of(L, i)] + rec_heapoff(rec, op) * op->size;
+      put_le(p, c, w);
+      p += w;
+      for (uint64_t j = 0; j < c; ++j) p = ops_write(L, i + 1, e, el + j * op->size, heaps, w, p);
+      i = e;
+    }
     else { /* container: low_bytes_write_wrapper<w> + memcpy (:304-363);
               optional: bool has_value + the value (:382-388) */
       uint64_t c = rec_count(rec, op);
@@ -180,29 +218,38 @@ static uint8_t *write_record(const spk_layout *L, const uint8_t *rec,
       uint64_t nb = c * op->size;
       if (nb) {
         const uint8_t *src =
-            (const uint8_t *)heaps[sk] + rec_heapoff(rec, op) * op->size;
+            (const uint8_t *)heaps[heap_of(L, i)] + rec_heapoff(rec, op) * op->size;
         memcpy(p, src, nb);
         p += nb;
       }
-      ++sk;
     }
   }
   return p;
 }
 
+static uint8_t *write_record(const spk_layout *L, const uint8_t *rec,
+                             const void *const *heaps, unsigned w, uint8_t *p) {
+  if (L->flags & SPK_LAYOUT_TRIVIAL) { /* packer.hpp:418-421 (incl. padding) */
+    memcpy(p, rec, L->rec_stride);
+    return p + L->rec_stride;
+  }
+  return ops_write(L, 0, L->n_ops, rec, heaps, w, p);
+}
+
 int spko_plan(const spk_layout *L, int mode, uint64_t n, const void *recs,
-              spk_plan_t *plan) {
+              const void *const *heaps, spk_plan_t *plan) {
   if (!L || !plan || (n && !recs)) return SPK_E_ARG;
   const uint8_t *r = (const uint8_t *)recs;
   memset(plan, 0, sizeof(*plan));
   if (mode == SPK_MODE_VECTOR) {
     /* calculate_one_size container branch: size_cnt += 1, max_size = n */
-    uint64_t maxc = n, var = 0, nsp = n_spans(L);
+    uint64_t maxc = n, var = 0, cnts = 0;
     for (uint64_t i = 0; i < n; ++i) {
-      const uint8_t *rec = r + i * L->rec_stride;
-      uint64_t m = rec_max_count(L, rec);
+      uint64_t b, c, m;
+      rec_size(L, r + i * L->rec_stride, heaps, &b, &c, &m);
       if (m > maxc) maxc = m;
-      var += rec_wire_size(L, rec, 0);
+      var += b;
+      cnts += c;
     }
     unsigned w = width_of(maxc);
     hdr_t h = header_shape(&L->fmt_vector, w);
@@ -212,18 +259,18 @@ int spko_plan(const spk_layout *L, int mode, uint64_t n, const void *recs,
     plan->header_bytes = h.len + w;
     plan->metainfo = h.meta;
     plan->has_meta = h.has_meta;
-    plan->total_bytes = h.len + w + var + nsp * n * w;
+    plan->total_bytes = h.len + w + var + cnts * w;
   }
   else if (mode == SPK_MODE_MESSAGES) {
     uint64_t tot = 0, maxc = 0, var = 0;
     for (uint64_t i = 0; i < n; ++i) {
-      const uint8_t *rec = r + i * L->rec_stride;
-      uint64_t m = rec_max_count(L, rec);
+      uint64_t b, c, m;
+      rec_size(L, r + i * L->rec_stride, heaps, &b, &c, &m);
       unsigned w = width_of(m);
       hdr_t h = header_shape(&L->fmt_one, w);
       if (m > maxc) maxc = m;
-      var += rec_wire_size(L, rec, 0);
-      tot += h.len + rec_wire_size(L, rec, w);
+      var += b;
+      tot += h.len + b + c * w;
     }
     plan->max_count = maxc;
     plan->var_bytes = var;
@@ -239,7 +286,7 @@ int spko_encode(const spk_layout *L, int mode, uint64_t n, const void *recs,
                 const void *const *heaps, void *out, uint64_t out_cap,
                 uint64_t *msg_offsets, uint64_t *written) {
   spk_plan_t plan;
-  int rc = spko_plan(L, mode, n, recs, &plan);
+  int rc = spko_plan(L, mode, n, recs, heaps, &plan);
   if (rc) return rc;
   if (written) *written = plan.total_bytes;
   if (plan.total_bytes > out_cap) return SPK_E_CAPACITY;
@@ -258,7 +305,9 @@ int spko_encode(const spk_layout *L, int mode, uint64_t n, const void *recs,
     uint8_t *base = p;
     for (uint64_t i = 0; i < n; ++i) {
       const uint8_t *rec = r + i * L->rec_stride;
-      unsigned w = width_of(rec_max_count(L, rec));
+      uint64_t b, c, m;
+      rec_size(L, rec, heaps, &b, &c, &m);
+      unsigned w = width_of(m);
       hdr_t h = header_shape(&L->fmt_one, w);
       if (msg_offsets) msg_offsets[i] = (uint64_t)(p - base);
       p = write_header(p, &L->fmt_one, &h);
@@ -276,7 +325,11 @@ int spko_encode_body(const spk_layout *L, uint64_t n, const void *recs,
     return SPK_E_ARG;
   const uint8_t *r = (const uint8_t *)recs;
   uint64_t tot = 0;
-  for (uint64_t i = 0; i < n; ++i) tot += rec_wire_size(L, r + i * L->rec_stride, width);
+  for (uint64_t i = 0; i < n; ++i) {
+    uint64_t b, c, m;
+    rec_size(L, r + i * L->rec_stride, heaps, &b, &c, &m);
+    tot += b + c * width;
+  }
   if (written) *written = tot;
   if (tot > out_cap) return SPK_E_CAPACITY;
   uint8_t *p = (uint8_t *)out;
@@ -341,18 +394,17 @@ typedef struct dctx_t {
   int overflow;
 } dctx_t;
 
-/* deserialize_one for one flattened record (unpacker.hpp:780-1349):
- * every payload failure is no_buffer_space (memory_reader::read/check). */
-static int32_t read_record(dctx_t *c, rd_t *r, unsigned w, uint8_t *rec) {
+/* deserialize_one of ops [i0, i1) over one (element) record
+ * (unpacker.hpp:780-1349): every payload failure is no_buffer_space
+ * (memory_reader::read/check). A container of non-trivially-serializable
+ * elements reads its length, then emplaces and decodes element after element,
+ * stopping at the first failure (unpacker.hpp:1208-1226). `rec` NULL: parse
+ * only (no output slot). */
+static int32_t ops_read(dctx_t *c, rd_t *r, unsigned w, uint32_t i0, uint32_t i1,
+                        uint8_t *rec) {
   const spk_layout *L = c->L;
   const uint8_t *p;
-  if (L->flags & SPK_LAYOUT_TRIVIAL) {
-    if (!rd_take(r, L->rec_stride, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
-    if (rec) memcpy(rec, p, L->rec_stride);
-    return SPK_ERRC_OK;
-  }
-  unsigned sk = 0;
-  for (uint32_t i = 0; i < L->n_ops; ++i) {
+  for (uint32_t i = i0; i < i1; ++i) {
     const spk_op *op = &L->ops[i];
     if (op->kind == SPK_OP_COPY) {
       if (!rd_take(r, op->size, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
@@ -361,14 +413,40 @@ static int32_t read_record(dctx_t *c, rd_t *r, unsigned w, uint8_t *rec) {
     }
     if (op->kind == SPK_OP_VARINT) { /* deserialize_varint_impl :270-292 */
       uint64_t v = 0;
-      int i = 0;
-      for (; i < 10; ++i) {
+      int k = 0;
+      for (; k < 10; ++k) {
         if (!rd_take(r, 1, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
-        v |= (uint64_t)(p[0] & 0x7fu) << (i * 7);
+        v |= (uint64_t)(p[0] & 0x7fu) << (k * 7);
         if (!(p[0] & 0x80u)) break;
       }
-      if (i == 10) return SPK_ERRC_INVALID_BUFFER;
+      if (k == 10) return SPK_ERRC_INVALID_BUFFER;
       if (rec) vi_store(rec, op, v);
+      continue;
+    }
+    const unsigned hk = heap_of(L, i);
+    if (op->kind == SPK_OP_ARRAY) {
+      const uint32_t e = end_of(L, i);
+      if (!rd_take(r, w, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
+      const uint64_t cnt = get_le(p, w);
+      uint8_t *el = NULL;
+      if (rec) {
+        const uint64_t off = c->used[hk];
+        if (cnt > 0xFFFFFFFFull || cnt > c->heap_caps[hk] - off) {
+          c->overflow = 1;
+          rec = NULL;
+        } else {
+          uint32_t c32 = (uint32_t)cnt;
+          memcpy(rec + op->rec_off, &c32, 4);
+          memcpy(rec + op->aux, &off, 8);
+          c->used[hk] = off + cnt;
+          el = (uint8_t *)c->heaps[hk] + off * op->size;
+        }
+      }
+      for (uint64_t j = 0; j < cnt; ++j) {
+        int32_t ec = ops_read(c, r, w, i + 1, e, el ? el + j * op->size : NULL);
+        if (ec) return ec;
+      }
+      i = e;
       continue;
     }
     /* container length :905-979; optional: read_wrapper<sizeof(bool)>, any
@@ -389,8 +467,8 @@ static int32_t read_record(dctx_t *c, rd_t *r, unsigned w, uint8_t *rec) {
         return SPK_ERRC_NO_BUFFER_SPACE;
     }
     if (rec) {
-      uint64_t off = c->used[sk];
-      if (cnt > 0xFFFFFFFFull || off + cnt > c->heap_caps[sk]) {
+      uint64_t off = c->used[hk];
+      if (cnt > 0xFFFFFFFFull || off + cnt > c->heap_caps[hk]) {
         c->overflow = 1;
       }
       else {
@@ -398,15 +476,25 @@ static int32_t read_record(dctx_t *c, rd_t *r, unsigned w, uint8_t *rec) {
         memcpy(rec + op->rec_off, &c32, 4);
         memcpy(rec + op->aux, &off, 8);
         if (unreadable)
-          memset((uint8_t *)c->heaps[sk] + off * op->size, 0, op->size);
+          memset((uint8_t *)c->heaps[hk] + off * op->size, 0, op->size);
         else if (cnt)
-          memcpy((uint8_t *)c->heaps[sk] + off * op->size, p, cnt * op->size);
-        c->used[sk] = off + cnt;
+          memcpy((uint8_t *)c->heaps[hk] + off * op->size, p, cnt * op->size);
+        c->used[hk] = off + cnt;
       }
     }
-    ++sk;
   }
   return SPK_ERRC_OK;
+}
+
+static int32_t read_record(dctx_t *c, rd_t *r, unsigned w, uint8_t *rec) {
+  const spk_layout *L = c->L;
+  const uint8_t *p;
+  if (L->flags & SPK_LAYOUT_TRIVIAL) {
+    if (!rd_take(r, L->rec_stride, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
+    if (rec) memcpy(rec, p, L->rec_stride);
+    return SPK_ERRC_OK;
+  }
+  return ops_read(c, r, w, 0, L->n_ops, rec);
 }
 
 int spko_decode(const spk_layout *L, int mode, const void *wire,

@@ -22,7 +22,7 @@ extern "C" {
 
 /* Host pointers throughout. Return SPK_OK / SPK_E_*. */
 int spko_plan(const spk_layout *L, int mode, uint64_t n, const void *recs,
-              spk_plan_t *plan);
+              const void *const *heaps, spk_plan_t *plan);
 int spko_encode(const spk_layout *L, int mode, uint64_t n, const void *recs,
                 const void *const *heaps, void *out, uint64_t out_cap,
                 uint64_t *msg_offsets, uint64_t *written);

@@ -30,7 +30,8 @@ GEN = os.path.join(ROOT, "oracle", "_ref", "golden_gen")
 SEED = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004,
         "pad": 0x5EED0005, "mixed": 0x5EED0006, "rect": 0, "rpcrect": 0x5EED0007,
         "person": 0x5EED0008, "ints": 0x5EED0009, "opt": 0x5EED000A, "optp": 0x5EED000B,
-        "var": 0x5EED000C, "varp": 0x5EED000D}
+        "var": 0x5EED000C, "varp": 0x5EED000D, "tags": 0x5EED000E, "group": 0x5EED000F,
+        "deep": 0x5EED0010}
 
 # (case_mode, n, param, conf, keep_bin)
 SMALL = [
@@ -70,6 +71,15 @@ SMALL = [
     ("var_A", 3000, 8, "default"), ("var_A", 50, 8, "nometa"),
     ("varp_A", 300, 0, "default"), ("varp_B", 200, 0, "default"),
     ("varp_B", 50, 0, "typeinfo"), ("varp_A", 20, 0, "nometa"),
+    # containers of non-trivially-serializable elements (SPK_OP_ARRAY)
+    ("tags_A", 0, 4, "default"), ("tags_A", 1, 4, "default"),
+    ("tags_A", 200, 6, "default"), ("tags_A", 30, 300, "default"),
+    ("tags_B", 200, 6, "default"), ("tags_B", 20, 300, "default"),
+    ("tags_A", 100, 6, "typeinfo"), ("tags_A", 50, 6, "nometa"),
+    ("group_A", 0, 5, "default"), ("group_A", 100, 5, "default"),
+    ("group_B", 100, 5, "default"), ("group_A", 3, 300, "default"),
+    ("deep_A", 100, 4, "default"), ("deep_B", 100, 4, "default"),
+    ("deep_A", 20, 300, "default"), ("deep_B", 30, 4, "nometa"),
 ]
 MEDIUM = [  # digest only (wire > ~1 MB)
     ("rec64_A", 65535, 0, "default"), ("rec64_A", 65536, 0, "default"),
@@ -81,6 +91,8 @@ MEDIUM = [  # digest only (wire > ~1 MB)
     ("opt_B", 70000, 48, "default"),
     ("var_A", 70000, 48, "default"), ("varp_A", 70000, 0, "default"),
     ("var_B", 70000, 48, "default"),
+    ("tags_A", 70000, 6, "default"), ("tags_B", 20000, 6, "default"),
+    ("group_A", 20000, 5, "default"), ("deep_A", 20000, 4, "default"),
 ]
 BIG = [  # BASELINE.json full-size configs (digest only)
     ("rec64_A", 100_000_000, 0, "default"),
@@ -191,7 +203,55 @@ ERR_BASES = [
     ("rec64_B", 1, 0, "default"), ("mixed_A", 3, 300, "default"),
     ("opt_A", 6, 10, "default"), ("optp_B", 1, 0, "default"), ("opt_B", 1, 20, "default"),
     ("var_A", 6, 10, "default"), ("varp_B", 1, 0, "default"), ("varp_A", 4, 0, "default"),
+    ("tags_A", 5, 4, "default"), ("tags_B", 1, 6, "default"), ("group_A", 4, 3, "default"),
+    ("group_B", 1, 4, "default"), ("deep_A", 4, 3, "default"), ("deep_B", 1, 4, "default"),
+    # width-8 container lengths (metainfo 0x18): no reference encoder writes
+    # them below 2^32 elements, but every decoder must read them
+    # (unpacker.hpp:572-619); the base is our width-8 re-encoding, decoded by
+    # the reference
+    ("recs_A", 5, 10, "default", 8), ("outer_A", 4, 8, "default", 8),
+    ("recs_B", 1, 30, "default", 8), ("tags_A", 4, 4, "default", 8),
+    ("mixed_A", 3, 20, "default", 4), ("recs_A", 4, 10, "default", 2),
 ]
+
+
+def wide_wire(cm, n, param, conf, width):
+    """The message golden_gen would emit, with every container length (and the
+    outer vector count) written at `width` bytes and the metainfo byte saying
+    so: header from spk_vector_header, body from the oracle's encode_body."""
+    import ctypes as ct
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    from yalantinglibs_amd import _capi as C
+    from yalantinglibs_amd import layout as LY
+    from yalantinglibs_amd import schema as S
+    from yalantinglibs_amd import synth
+    case = cm[:-2]
+    confv = {"default": S.DEFAULT, "typeinfo": S.ENABLE_TYPE_INFO,
+             "nometa": S.DISABLE_ALL_META_INFO}[conf]
+    L = LY.case_layout(case, confv)
+    _, recs, heaps = synth.make_batch(case, n, SEED[case], param)
+    o = C.load_oracle()
+    hp = (ct.c_void_p * max(len(heaps), 1))(*[h.ctypes.data if h.size else 0 for h in heaps])
+    rp = ct.c_void_p(recs.ctypes.data if n else 0)
+    body = np.zeros(1 << 20, np.uint8)
+    wr = ct.c_uint64()
+    assert o.spko_encode_body(L.ptr, n, rp, hp, width, ct.c_void_p(body.ctypes.data),
+                              body.size, ct.byref(wr)) == 0
+    if cm.endswith("_B"):  # one message: the T header at this width
+        assert n == 1
+        lib = C.load_codec()
+        vb = (ct.c_uint8 * 512)()
+        k = lib.spk_vector_header(L.ptr, 0, width, vb, 512)
+        hdr = bytes(vb[:k - width])  # fmt_vector's header: swap in fmt_one's code
+        code = L.c.fmt_one.code
+        hdr = bytes([(code & 0xFE) | (hdr[0] & 1)]) + code.to_bytes(4, "little")[1:] + hdr[4:]
+        return hdr + body[:wr.value].tobytes()
+    lib = C.load_codec()
+    vb = (ct.c_uint8 * 512)()
+    k = lib.spk_vector_header(L.ptr, n, width, vb, 512)
+    assert k > 0
+    return bytes(vb[:k]) + body[:wr.value].tobytes()
 
 
 def mutations(wire_len, rng):
@@ -212,16 +272,24 @@ def mutations(wire_len, rng):
 def make_errs(tmp):
     rng = random.Random(1234)
     out = []
-    for cm, n, param, conf in ERR_BASES:
+    for eb in ERR_BASES:
+        cm, n, param, conf = eb[:4]
+        width = eb[4] if len(eb) > 4 else 0
         case = cm[:-2]
         seed = SEED[case]
         wire = os.path.join(tmp, "ewire.bin")
-        subprocess.run([GEN, "emit", cm, str(n), str(seed), str(param), conf, wire,
-                        os.path.join(tmp, "elens.bin")], check=True,
-                       stdout=subprocess.DEVNULL)
+        if width:
+            with open(wire, "wb") as f:
+                f.write(wide_wire(cm, n, param, conf, width))
+        else:
+            subprocess.run([GEN, "emit", cm, str(n), str(seed), str(param), conf, wire,
+                            os.path.join(tmp, "elens.bin")], check=True,
+                           stdout=subprocess.DEVNULL)
         with open(wire, "rb") as f:
             base = f.read()
         muts = mutations(len(base), rng)
+        if width:  # the unmutated wide message first
+            muts.insert(0, f"trunc {len(base)}")
         if case in ("var", "varp"):  # overlong / 10-byte / unterminated varints
             for p0 in range(0, min(len(base), 48), 3):
                 run = " ".join(f"set {p0 + j} 255" for j in range(10))
@@ -239,8 +307,10 @@ def make_errs(tmp):
             r["reenc_sha256"] = (hashlib.sha256(bytes.fromhex(re_hex)).hexdigest()
                                  if re_hex is not None else None)
         assert len(rows) == len(muts), (cm, len(rows), len(muts))
+        if width:
+            assert rows[0]["errc"] == 0, (cm, width, rows[0])  # the reference reads it
         out.append({"case": case, "mode": cm[-1], "n": n, "seed": seed, "param": param,
-                    "conf": conf, "base": base.hex(),
+                    "conf": conf, "width": width or None, "base": base.hex(),
                     "tests": [{"mut": m, **r} for m, r in zip(muts, rows)]})
     return out
 

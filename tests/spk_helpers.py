@@ -70,11 +70,11 @@ def oracle_encode(L, mode, recs, heaps):
     o = C.load_oracle()
     n = len(recs)
     plan = C.spk_plan_t()
-    rc = o.spko_plan(L.ptr, mode, n, _ptr(recs), ct.byref(plan))
+    hp = (ct.c_void_p * max(len(heaps), 1))(*[h.ctypes.data for h in heaps])
+    rc = o.spko_plan(L.ptr, mode, n, _ptr(recs), hp, ct.byref(plan))
     assert rc == 0, rc
     out = np.zeros(max(plan.total_bytes, 1), np.uint8)
     offs = np.zeros(n + 1, np.uint64)
-    hp = (ct.c_void_p * max(len(heaps), 1))(*[h.ctypes.data for h in heaps])
     written = ct.c_uint64(0)
     rc = o.spko_encode(L.ptr, mode, n, _ptr(recs), hp, _ptr(out), out.size,
                        _ptr(offs), ct.byref(written))
@@ -90,8 +90,9 @@ def oracle_decode(L, mode, wire: bytes, offsets=None, n_msgs=0, rec_cap=None,
         rec_cap = max(len(wire), 1) if mode == C.SPK_MODE_VECTOR else max(n_msgs, 1)
     recs = np.zeros(rec_cap, L.dev.dtype)
     heaps, caps = [], []
-    for sp in L.dev.spans:
-        cap = heap_caps or (len(wire) // max(sp.elem.size, 1) + 1)
+    wcaps = S.heap_caps_for_wire(L.dev, len(wire), rec_cap)
+    for sp, wc in zip(L.dev.spans, wcaps):
+        cap = heap_caps or max(wc, len(wire) // max(sp.elem.size, 1) + 1)
         heaps.append(np.zeros(cap * sp.elem.size, np.uint8))
         caps.append(cap)
     hp = (ct.c_void_p * max(len(heaps), 1))(*[h.ctypes.data for h in heaps])
@@ -111,12 +112,19 @@ def lens_to_offsets(lens):
     return offs
 
 
-def records_equal(L, a, b, heaps_a, heaps_b):
-    """Compare decoded records/heaps with the synth inputs (canonical heap)."""
+def records_equal(L, a, b, heaps_a, heaps_b, heap_used=None):
+    """Compare decoded records/heaps with the synth inputs (canonical heap).
+    heap_used: elements in use per heap (the decode result); needed for the
+    heaps of ARRAY elements, whose counts are not in the top-level records."""
     if L.dev.trivial:
         return a.tobytes() == b.tobytes()
     ok = a.tobytes() == b.tobytes()
     for k, sp in enumerate(L.dev.spans):
-        used = int(a[sp.path + ".n"].astype(np.uint64).sum()) * sp.elem.size
+        if heap_used is not None:
+            n = int(heap_used[k])
+        else:
+            n = int(a[sp.path + ".n"].astype(np.uint64).sum())
+        used = n * sp.elem.size
         ok = ok and heaps_a[k][:used].tobytes() == heaps_b[k][:used].tobytes()
+        ok = ok and len(heaps_b[k]) == used
     return ok

@@ -40,7 +40,7 @@ def test_struct_sizes_match_header():
     assert ct.sizeof(C.spk_op) == 16
     assert ct.sizeof(C.spk_msgfmt) == 16 + C.SPK_MAX_LITERAL
     assert ct.sizeof(C.spk_plan_t) == 40
-    assert ct.sizeof(C.spk_dresult_t) == 24 + 8 * C.SPK_MAX_SPANS
+    assert ct.sizeof(C.spk_dresult_t) == 32 + 8 * C.SPK_MAX_SPANS
 
 
 @pytest.mark.parametrize("case", sorted(synth.CASE_TYPES))

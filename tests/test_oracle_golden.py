@@ -87,7 +87,7 @@ def test_oracle_decode_roundtrip_reference(ent):
         res, out, oh, errc = H.oracle_decode(L, C.SPK_MODE_MESSAGES, wire, offs, ent["n"])
         assert res.errc == 0 and res.count == ent["n"]
         assert (errc[:ent["n"]] == 0).all()
-    assert H.records_equal(L, out[:ent["n"]], recs, oh, heaps)
+    assert H.records_equal(L, out[:ent["n"]], recs, oh, heaps, res.heap_used)
 
 
 @pytest.mark.parametrize("ent", MEDIUM, ids=[e["name"] for e in MEDIUM])

@@ -56,10 +56,11 @@ def _worker(rank, world, port, case, n, param, q):
             sh.append(np.ascontiguousarray(h, dtype=np.uint8))
         o = C.load_oracle()
         plan = C.spk_plan_t()
-        assert o.spko_plan(L.ptr, C.SPK_MODE_VECTOR, len(sub), H._ptr(sub), ct.byref(plan)) == 0
+        hp = (ct.c_void_p * max(len(sh), 1))(*[h.ctypes.data if h.size else 0 for h in sh])
+        assert o.spko_plan(L.ptr, C.SPK_MODE_VECTOR, len(sub), H._ptr(sub), hp,
+                           ct.byref(plan)) == 0
         sp = PAR.agree_shard_plan(len(sub), plan.max_count, plan.var_bytes, L.n_cont,
                                   lambda gn, w: _oracle_header(L, gn, w))
-        hp = (ct.c_void_p * max(len(sh), 1))(*[h.ctypes.data if h.size else 0 for h in sh])
         body = np.zeros(max(sp.body_bytes[rank], 1), np.uint8)
         wr = ct.c_uint64()
         assert o.spko_encode_body(L.ptr, len(sub), H._ptr(sub), hp, sp.width, H._ptr(body),

@@ -36,6 +36,9 @@ SPK_OP_COPY = 1
 SPK_OP_SPAN = 2
 SPK_OP_OPTION = 3
 SPK_OP_VARINT = 4
+SPK_OP_ARRAY = 5
+SPK_OP_END = 6
+SPK_MAX_DEPTH = 4
 SPK_VARINT_ZIGZAG = 1
 SPK_MAX_VARINTS = 16
 SPK_MODE_VECTOR = 0
@@ -82,7 +85,8 @@ class spk_plan_t(ct.Structure):
 class spk_dresult_t(ct.Structure):
     _fields_ = [("errc", ct.c_int32), ("width", ct.c_uint32),
                 ("count", ct.c_uint64), ("consumed", ct.c_uint64),
-                ("heap_used", ct.c_uint64 * SPK_MAX_SPANS)]
+                ("heap_used", ct.c_uint64 * SPK_MAX_SPANS),
+                ("tiles_repaired", ct.c_uint32), ("tiles_sequential", ct.c_uint32)]
 
 
 class spk_frame(ct.Structure):
@@ -102,7 +106,7 @@ ORACLE_PATH = os.path.join(_ROOT, "oracle", "libspk_oracle.so")
 
 # exported symbols of include/spk_codec.h (checked by tests/test_capi.py)
 CODEC_SYMBOLS = ["spk_abi_version", "spk_errc_message", "spk_layout_check",
-                 "spk_workspace_bytes", "spk_plan", "spk_encode", "spk_decode",
+                 "spk_workspace_bytes", "spk_plan", "spk_plan_ex", "spk_encode", "spk_decode",
                  "spk_synth", "spk_synth_counts", "spk_encode_body",
                  "spk_vector_header", "spk_encode_framed", "spk_decode_framed",
                  # runtime helpers (front ends without HIP headers)
@@ -128,6 +132,7 @@ def _bind_codec(lib):
     lib.spk_workspace_bytes.restype = ct.c_size_t
     lib.spk_workspace_bytes.argtypes = [PL, ct.c_int, U64, U64]
     lib.spk_plan.argtypes = [PL, ct.c_int, U64, P, P, P, ct.c_size_t, P]
+    lib.spk_plan_ex.argtypes = [PL, ct.c_int, U64, P, ct.POINTER(P), P, P, ct.c_size_t, P]
     lib.spk_encode.argtypes = [PL, ct.c_int, U64, P, ct.POINTER(P), P, P, U64,
                                P, P, ct.c_size_t, P]
     lib.spk_decode.argtypes = [PL, ct.c_int, P, U64, P, U64, P, U64,
@@ -189,7 +194,7 @@ def load_oracle():
         if not os.path.exists(ORACLE_PATH):
             raise RuntimeError(f"oracle not built ({ORACLE_PATH}); make -C oracle oracle")
         lib = ct.CDLL(ORACLE_PATH)
-        lib.spko_plan.argtypes = [PL, ct.c_int, U64, P, ct.POINTER(spk_plan_t)]
+        lib.spko_plan.argtypes = [PL, ct.c_int, U64, P, ct.POINTER(P), ct.POINTER(spk_plan_t)]
         lib.spko_encode.argtypes = [PL, ct.c_int, U64, P, ct.POINTER(P), P, U64,
                                     P, ct.POINTER(U64)]
         lib.spko_encode_body.argtypes = [PL, U64, P, ct.POINTER(P), ct.c_uint, P, U64,

@@ -103,18 +103,30 @@ int spk_layout_check(const spk_layout *L) {
     return SPK_OK;
   }
   uint32_t spans = 0, conts = 0, vars = 0;
+  // record strides of the open ARRAY element layouts (0: the top record)
+  uint32_t stride[SPK_MAX_DEPTH + 1] = {L->rec_stride}, depth = 0, nops[SPK_MAX_DEPTH + 1] = {0};
   for (uint32_t i = 0; i < L->n_ops; ++i) {
     const spk_op &o = L->ops[i];
+    const uint32_t rs = stride[depth];
+    ++nops[depth];
     if (o.kind == SPK_OP_COPY) {
-      if (o.size == 0 || (uint64_t)o.rec_off + o.size > L->rec_stride) return SPK_E_LAYOUT;
-    } else if (o.kind == SPK_OP_SPAN || o.kind == SPK_OP_OPTION) {
-      if (o.size == 0 || o.rec_off % 4 || o.aux % 8 || o.rec_off + 4 > L->rec_stride ||
-          o.aux + 8 > L->rec_stride)
+      if (o.size == 0 || (uint64_t)o.rec_off + o.size > rs) return SPK_E_LAYOUT;
+    } else if (o.kind == SPK_OP_SPAN || o.kind == SPK_OP_OPTION || o.kind == SPK_OP_ARRAY) {
+      if (o.size == 0 || o.rec_off % 4 || o.aux % 8 || o.rec_off + 4 > rs || o.aux + 8 > rs)
         return SPK_E_LAYOUT;
       ++spans;
-      conts += o.kind == SPK_OP_SPAN;
+      conts += o.kind != SPK_OP_OPTION;
+      if (o.kind == SPK_OP_ARRAY) {  // element records: 8-byte aligned, one more level
+        if (o.size % 8 || depth == SPK_MAX_DEPTH) return SPK_E_LAYOUT;
+        stride[++depth] = o.size;
+        nops[depth] = 0;
+      }
+    } else if (o.kind == SPK_OP_END) {
+      --nops[depth];
+      if (depth == 0 || nops[depth] == 0) return SPK_E_LAYOUT;  // unmatched / empty element
+      --depth;
     } else if (o.kind == SPK_OP_VARINT) {  // var_(u)int32_t / var_(u)int64_t member
-      if ((o.size != 4 && o.size != 8) || o.rec_off % o.size || o.rec_off + o.size > L->rec_stride ||
+      if ((o.size != 4 && o.size != 8) || o.rec_off % o.size || o.rec_off + o.size > rs ||
           (o.aux & ~SPK_VARINT_ZIGZAG))
         return SPK_E_LAYOUT;
       ++vars;
@@ -122,6 +134,7 @@ int spk_layout_check(const spk_layout *L) {
       return SPK_E_LAYOUT;
     }
   }
+  if (depth) return SPK_E_LAYOUT;  // an ARRAY without its END
   // a non-trivial record has a variable-length member: a span/option or a varint
   if ((spans == 0 && vars == 0) || spans > SPK_MAX_SPANS || vars > SPK_MAX_VARINTS ||
       L->rec_stride % 8)
@@ -136,11 +149,32 @@ size_t spk_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t w
   // trivial: per-message payload positions (fallback gather) or 2 words per
   // decode block (<= 4096 blocks), whichever is larger
   if (is_trivial(L)) return kWsScratch + ((n + 1) * 8 > 65536 ? (n + 1) * 8 : 65536) + 256;
+  if (layout_has_array(L)) return nested_workspace_bytes(L, mode, n, wire_len);
   return var_workspace_bytes(L, mode, n, wire_len);
 }
 
-int spk_plan(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
-             spk_plan_t *d_plan, void *d_ws, size_t ws_bytes, void *stream) {
+// SPAN / OPTION / ARRAY members read their payloads from d_heaps[k]: a
+// non-empty batch needs every one of them (a layout of varints only may pass
+// NULL); ARRAY heaps hold element records, read and written as u32/u64 fields
+static int heaps_check(const spk_layout *L, uint64_t n, const void *const *d_heaps) {
+  uint32_t spans = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i) {
+    const uint32_t k = L->ops[i].kind;
+    if (k != SPK_OP_SPAN && k != SPK_OP_OPTION && k != SPK_OP_ARRAY) continue;
+    if (n && d_heaps && k == SPK_OP_ARRAY && d_heaps[spans] && (uintptr_t)d_heaps[spans] % 8)
+      return SPK_E_ARG;
+    ++spans;
+  }
+  if (!spans || !n) return SPK_OK;
+  if (!d_heaps) return SPK_E_ARG;
+  for (uint32_t k = 0; k < spans; ++k)
+    if (!d_heaps[k]) return SPK_E_ARG;
+  return SPK_OK;
+}
+
+int spk_plan_ex(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
+                const void *const *d_heaps, spk_plan_t *d_plan, void *d_ws, size_t ws_bytes,
+                void *stream) {
   int rc = spk_layout_check(L);
   if (rc) return rc;
   if ((mode != SPK_MODE_VECTOR && mode != SPK_MODE_MESSAGES) || !d_plan || !d_ws)
@@ -150,7 +184,17 @@ int spk_plan(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
   hipStream_t s = (hipStream_t)stream;
   if (is_trivial(L)) return hip_rc(launch_fixed_plan(L, mode, n, d_plan, d_ws, s));
   if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
+  if (layout_has_array(L)) {  // the sizes live in the element records
+    if ((rc = heaps_check(L, n, d_heaps))) return rc;
+    return hip_rc(launch_nested_plan(L, mode, n, d_recs, d_heaps, d_plan, d_ws, s));
+  }
   return hip_rc(launch_var_plan(L, mode, n, d_recs, d_plan, d_ws, ws_bytes, s));
+}
+
+int spk_plan(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
+             spk_plan_t *d_plan, void *d_ws, size_t ws_bytes, void *stream) {
+  if (L && spk_layout_check(L) == SPK_OK && layout_has_array(L) && n) return SPK_E_ARG;
+  return spk_plan_ex(L, mode, n, d_recs, nullptr, d_plan, d_ws, ws_bytes, stream);
 }
 
 static int frame_check(const spk_frame *F) {
@@ -158,19 +202,6 @@ static int frame_check(const spk_frame *F) {
   if (F->prefix_len > SPK_MAX_FRAME) return SPK_E_ARG;
   if (F->seq_off != SPK_FRAME_NONE && (uint64_t)F->seq_off + 4 > F->prefix_len) return SPK_E_ARG;
   if (F->len_off != SPK_FRAME_NONE && (uint64_t)F->len_off + 4 > F->prefix_len) return SPK_E_ARG;
-  return SPK_OK;
-}
-
-// SPAN / OPTION members read their payloads from d_heaps[k]: a non-empty
-// batch needs every one of them (a layout of varints only may pass NULL)
-static int heaps_check(const spk_layout *L, uint64_t n, const void *const *d_heaps) {
-  uint32_t spans = 0;
-  for (uint32_t i = 0; i < L->n_ops; ++i)
-    spans += L->ops[i].kind == SPK_OP_SPAN || L->ops[i].kind == SPK_OP_OPTION;
-  if (!spans || !n) return SPK_OK;
-  if (!d_heaps) return SPK_E_ARG;
-  for (uint32_t k = 0; k < spans; ++k)
-    if (!d_heaps[k]) return SPK_E_ARG;
   return SPK_OK;
 }
 
@@ -200,6 +231,9 @@ static int encode_impl(const spk_layout *L, int mode, uint64_t n, const void *d_
   }
   if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
   if ((rc = heaps_check(L, n, d_heaps))) return rc;
+  if (layout_has_array(L))
+    return hip_rc(launch_nested_encode(L, mode, n, d_recs, d_heaps, d_out, d_msg_offsets, F, 0,
+                                       d_ws, s));
   return hip_rc(launch_var_encode(L, mode, n, d_recs, d_heaps, d_plan, d_out, out_cap,
                                   d_msg_offsets, F, d_ws, ws_bytes, s));
 }
@@ -248,9 +282,17 @@ static int decode_impl(const spk_layout *L, int mode, const void *d_wire, uint64
   if (d_recs && (uintptr_t)d_recs % 8) return SPK_E_ARG;
   uint32_t spans = 0;
   for (uint32_t i = 0; i < L->n_ops; ++i)
-    spans += L->ops[i].kind == SPK_OP_SPAN || L->ops[i].kind == SPK_OP_OPTION;
+    spans += L->ops[i].kind == SPK_OP_SPAN || L->ops[i].kind == SPK_OP_OPTION ||
+             L->ops[i].kind == SPK_OP_ARRAY;
   if (spans && (!d_heaps || !heap_caps)) return SPK_E_ARG;
   if (mode == SPK_MODE_MESSAGES && n_msgs && !d_msg_offsets) return SPK_E_ARG;
+  if (layout_has_array(L)) {
+    for (uint32_t k = 0; k < spans; ++k)
+      if (!d_heaps[k] || (uintptr_t)d_heaps[k] % 8) return SPK_E_ARG;
+    return hip_rc(launch_nested_decode(L, mode, d_wire, wire_len, d_msg_offsets, n_msgs, prefix,
+                                       d_recs, rec_cap, d_heaps, heap_caps, d_res, d_errc, d_ws,
+                                       s));
+  }
   return hip_rc(launch_var_decode(L, mode, d_wire, wire_len, d_msg_offsets, n_msgs, prefix,
                                   d_recs, rec_cap, d_heaps, heap_caps, d_res, d_errc, d_ws,
                                   ws_bytes, s));
@@ -292,6 +334,9 @@ int spk_encode_body(const spk_layout *L, uint64_t n, const void *d_recs,
   }
   if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
   if ((rc = heaps_check(L, n, d_heaps))) return rc;
+  if (layout_has_array(L))
+    return hip_rc(launch_nested_encode(L, SPK_MODE_VECTOR, n, d_recs, d_heaps, d_out, nullptr,
+                                       nullptr, width, d_ws, s));
   return hip_rc(launch_var_encode_body(L, n, d_recs, d_heaps, width, d_out, out_cap, d_ws,
                                        ws_bytes, s));
 }

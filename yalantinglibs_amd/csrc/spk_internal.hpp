@@ -182,6 +182,22 @@ void trace_mark(const char *name, hipStream_t s, int end);
 
 // ---- launch wrappers implemented in the kernel TUs -----------------------
 namespace spk {
+// spk_nested.hip: layouts with SPK_OP_ARRAY
+bool layout_has_array(const spk_layout *L);
+size_t nested_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len);
+hipError_t launch_nested_plan(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
+                              const void *const *d_heaps, spk_plan_t *d_plan, void *d_ws,
+                              hipStream_t s);
+hipError_t launch_nested_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
+                                const void *const *d_heaps, void *d_out,
+                                uint64_t *d_msg_offsets, const spk_frame *F, uint32_t fixed_w,
+                                void *d_ws, hipStream_t s);
+hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wire,
+                                uint64_t wire_len, const uint64_t *d_msg_offsets,
+                                uint64_t n_msgs, uint32_t prefix, void *d_recs, uint64_t rec_cap,
+                                void *const *d_heaps, const uint64_t *heap_caps,
+                                spk_dresult_t *d_res, int32_t *d_errc, void *d_ws,
+                                hipStream_t s);
 // spk_fixed.hip
 hipError_t launch_fixed_plan(const spk_layout *L, int mode, uint64_t n,
                              spk_plan_t *d_plan, void *d_ws, hipStream_t s);

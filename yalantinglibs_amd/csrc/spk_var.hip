@@ -1067,6 +1067,8 @@ struct VCtl {
 struct FCtl {
   unsigned long long broken[4];  // tiles re-walked by select pass k (K2)
   unsigned long long unresolved; // tiles no pass could select (never expected)
+  unsigned long long seq;        // tiles the sequential fixer re-resolved or passed through
+  unsigned long long njobs;      // deferred long-span copies (BigQ)
   unsigned long long term_tile;  // first tile whose path ends inside it (atomicMin), ~0
   unsigned long long term_pos;   // where the true path ends (atomicMin), ~0
   unsigned long long end_pos;    // end of record n-1
@@ -1075,6 +1077,7 @@ struct FCtl {
   unsigned long long stot[SPK_MAX_SPANS];  // span-count sums on the path
 };
 constexpr size_t kWsFCtl = kWsCtl + 1280;
+static_assert(kWsFCtl + sizeof(FCtl) <= kWsScratch, "FCtl overlaps the scratch area");
 
 // Compact walk program of a record: fixed bytes, then per span
 // [count:w][count*esz bytes][fixed bytes]. Built once on the host from the
@@ -1270,6 +1273,8 @@ __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);  // tile decoder state
   for (int k = 0; k < 4; ++k) fc->broken[k] = 0;
   fc->unresolved = 0;
+  fc->seq = 0;
+  fc->njobs = 0;
   fc->term_tile = ~0ull;
   fc->term_pos = ~0ull;
   fc->end_pos = 0;
@@ -1365,11 +1370,29 @@ struct WinReader {
   }
 };
 
+// Long spans are not copied by the lane that emits their record: the lane
+// queues them in <= kBigPiece pieces and vec_big_copy moves every piece with
+// a whole block (a multi-MiB string would otherwise be one lane's serial copy).
+constexpr uint64_t kBigCopy = 4096;
+constexpr uint64_t kBigPiece = 64 * 1024;
+struct BigJob {
+  uint64_t src, n;
+  uint8_t *dst;
+};
+struct BigQ {
+  BigJob *jobs;
+  unsigned long long *n;
+  uint64_t cap;
+};
+__host__ __device__ constexpr uint64_t big_jobs_cap(uint64_t wire_len) {
+  return wire_len / kBigCopy + wire_len / kBigPiece + 1;
+}
+
 // emit_record reading the wire through an LDS window reader
 __device__ __forceinline__ void emit_record_rd(const KLayout &L, const WinReader &rd,
                                                uint64_t pos, uint32_t w, uint8_t *rec,
                                                uint8_t *const *heaps, const uint64_t *off,
-                                               uint64_t end) {
+                                               uint64_t end, const BigQ &bq) {
   uint32_t sk = 0;
   for (uint32_t o = 0; o < L.n_ops; ++o) {
     const spk_op op = L.ops[o];
@@ -1388,10 +1411,21 @@ __device__ __forceinline__ void emit_record_rd(const KLayout &L, const WinReader
       *reinterpret_cast<uint64_t *>(rec + op.aux) = off[sk];
       const uint64_t nb = opt_nb(op, cnt, pos, end);
       uint8_t *hp = heaps[sk] + off[sk] * op.size;
-      if (cnt && !nb && op.kind == SPK_OP_OPTION)
+      if (cnt && !nb && op.kind == SPK_OP_OPTION) {
         for (uint32_t b = 0; b < op.size; ++b) hp[b] = 0;  // unreadable value
-      else
+      } else if (nb >= kBigCopy) {
+        const uint64_t np = (nb + kBigPiece - 1) / kBigPiece;
+        const uint64_t j0 = atomicAdd(bq.n, (unsigned long long)np);
+        for (uint64_t p = 0; p < np; ++p) {
+          const uint64_t o = p * kBigPiece, m = nb - o < kBigPiece ? nb - o : kBigPiece;
+          if (j0 + p < bq.cap)
+            bq.jobs[j0 + p] = BigJob{pos + o, m, hp + o};
+          else
+            copy_bytes(hp + o, rd.wire + pos + o, m);  // (the cap is never reached)
+        }
+      } else {
         rd.copy_to(hp, pos, nb);
+      }
       pos += nb;
       ++sk;
     }
@@ -2562,6 +2596,45 @@ __device__ __forceinline__ uint64_t tile_entry(const TileBufs &TB, const VCtl *c
   return t == 0 ? c->p0 : TB.fn[(t - 1) * kFnWords];
 }
 
+// Tile t whose entry lies at or past its end (inside a record that spans it):
+// no records, exit = entry.
+__device__ __forceinline__ void tile_pass_through(const TileBufs &TB, uint64_t t, uint64_t T,
+                                                  uint32_t nsp) {
+  uint64_t *fn = TB.fn + t * kFnWords;
+  fn[0] = T;
+  fn[1] = 1;
+  fn[2] = T;
+  fn[3] = 0;
+  for (uint32_t q = 0; q < nsp; ++q) fn[4 + q] = 0;
+  TB.sel[t] = 0;
+}
+
+// Tile t's exit E lies past tile t+1: the tiles a record spans, t+1 ..
+// tile(E)-1, pass E through (written here so that a long record costs one
+// select pass, not one per tile; any race with those tiles' own waves is
+// settled by the next pass and the sequential check).
+__device__ __forceinline__ void tile_jump(const TileBufs &TB, uint64_t p0, uint64_t t, uint64_t E,
+                                          uint32_t nsp, uint32_t lane,
+                                          unsigned long long *changed) {
+  if (E == kTermPos || E == kNoPos || E < p0) return;
+  const uint64_t e0 = (E - p0) / kTileBytes;
+  const uint64_t e = e0 < TB.ntiles ? e0 : TB.ntiles;
+  if (t + 1 >= e) return;
+  // the pass changed other tiles' functions: the next pass re-checks them
+  if (lane == 0) atomicAdd(changed, 1ull);
+  for (uint64_t v = t + 1 + lane; v < e; v += 64) tile_pass_through(TB, v, E, nsp);
+}
+
+// tile t's selection given its current entry T (kSelBroken: none fits)
+__device__ __forceinline__ int32_t tile_select_for(const TileBufs &TB, uint64_t t, uint64_t T) {
+  if (T == kTermPos) return kSelTerm;
+  const uint64_t *fn = TB.fn + t * kFnWords;
+  const uint32_t nalt = (uint32_t)fn[1];
+  for (uint32_t k = 0; k < nalt && k < kAlt; ++k)
+    if (fn[2 + k * kAltWords] == T) return (int32_t)k;
+  return kSelBroken;
+}
+
 // ---- K2: select each tile's entry; re-walk tiles whose entry is none of
 // theirs (one wave per tile; only those waves stage anything) ---------------
 template <int NS>
@@ -2578,19 +2651,11 @@ __global__ __launch_bounds__(64) void vec_tile_select(DecArgs a, WalkProg P,
   if (pass > 0 && !fc->broken[pass - 1]) return;  // the previous pass fixed nothing
   uint64_t *fn = TB.fn + t * kFnWords;
   const uint64_t T = tile_entry(TB, c, t);
-  int32_t sel = kSelBroken;
-  if (T == kTermPos) {
-    sel = kSelTerm;
-  } else if (T != kNoPos) {
-    const uint32_t nalt = (uint32_t)fn[1];
-    for (uint32_t k = 0; k < nalt && k < kAlt; ++k)
-      if (fn[2 + k * kAltWords] == T) {
-        sel = (int32_t)k;
-        break;
-      }
-  }
+  const int32_t sel = T == kNoPos ? kSelBroken : tile_select_for(TB, t, T);
   if (sel != kSelBroken || T == kNoPos) {
     if (lane == 0) TB.sel[t] = sel;
+    if (sel >= 0)
+      tile_jump(TB, c->p0, t, fn[0], NS > 0 ? (uint32_t)NS : P.ns, lane, &fc->broken[pass]);
     return;
   }
   // broken: re-resolve the whole tile from its true entry
@@ -2599,6 +2664,11 @@ __global__ __launch_bounds__(64) void vec_tile_select(DecArgs a, WalkProg P,
   const uint64_t len = a.wire_len, p0 = c->p0;
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
   const uint64_t ts = p0 + t * kTileBytes;
+  if (T >= ts + kTileBytes) {  // inside a record that spans the tile
+    if (lane == 0) tile_pass_through(TB, t, T, nsp);
+    tile_jump(TB, p0, t, T, nsp, lane, &fc->broken[pass]);
+    return;
+  }
   const TileView tv = stage_tile(win_s[0], wire, len, ts, w, lane);
   const uint64_t cs = ts + (uint64_t)lane * kTChunk;
   const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
@@ -2624,10 +2694,14 @@ __global__ __launch_bounds__(64) void vec_tile_select(DecArgs a, WalkProg P,
     for (uint32_t q = 0; q < nsp; ++q) fn[4 + q] = tsum[q];
     TB.sel[t] = 0;
   }
+  tile_jump(TB, p0, t, y63, nsp, lane, &fc->broken[pass]);
 }
 
-// Residual entries no pass could select (an exit that moved twice in a row):
-// one wave, tiles in order. Normally exits at once.
+// Residual entries no pass could select (an exit that moved twice in a row,
+// or a chain of tiles inside records longer than a tile): one wave, in tile
+// order. It checks 64 tiles per step, jumps a run of tiles that a record
+// spans in one step, and re-resolves only the tiles still broken. Normally
+// exits at once.
 template <int NS>
 __global__ __launch_bounds__(64) void vec_tile_seqfix(DecArgs a, WalkProg P,
                                                       const uint8_t *__restrict__ wire,
@@ -2641,50 +2715,62 @@ __global__ __launch_bounds__(64) void vec_tile_seqfix(DecArgs a, WalkProg P,
   const uint32_t w = c->w;
   const uint64_t len = a.wire_len, p0 = c->p0;
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
-  for (uint64_t t = 0; t < TB.ntiles; ++t) {
-    uint64_t *fn = TB.fn + t * kFnWords;
-    const uint64_t T = tile_entry(TB, c, t);
-    int32_t sel = kSelBroken;
-    if (T == kTermPos) {
-      sel = kSelTerm;
-    } else {
-      const uint32_t nalt = (uint32_t)fn[1];
-      for (uint32_t k = 0; k < nalt && k < kAlt; ++k)
-        if (fn[2 + k * kAltWords] == T) {
-          sel = (int32_t)k;
-          break;
-        }
+  uint64_t t = 0;
+  while (t < TB.ntiles) {
+    // 64 tiles at once: the first whose entry none of its alternatives takes
+    const uint64_t u = t + lane;
+    int32_t sel = kSelTerm;
+    bool bad = false;
+    if (u < TB.ntiles) {
+      const uint64_t T = tile_entry(TB, c, u);
+      sel = tile_select_for(TB, u, T);
+      bad = sel == kSelBroken && T != kNoPos;
     }
-    if (sel != kSelBroken || T == kNoPos) {
-      if (lane == 0) TB.sel[t] = sel;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    const uint64_t m = __ballot(bad);
+    const uint64_t f = m ? t + (uint64_t)__builtin_ctzll(m) : ~0ull;
+    if (u < TB.ntiles && u < f) TB.sel[u] = sel;
+    if (!m) {
+      t += 64;
       continue;
     }
-    const uint64_t ts = p0 + t * kTileBytes;
-    const TileView tv = stage_tile(win_s[0], wire, len, ts, w, lane);
-    const uint64_t cs = ts + (uint64_t)lane * kTChunk;
-    const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
-    const uint64_t g = t * 64 + lane;
-    uint64_t used = TB.cused[g], ex = TB.cex[g], term_at = kTermPos;
-    uint32_t cnt = TB.ccnt[g];
-    uint64_t sums[NS > 0 ? NS : SPK_MAX_SPANS];
-    for (uint32_t q = 0; q < nsp; ++q) sums[q] = TB.csum[(uint64_t)q * TB.nchunks + g];
-    resolve_tile<NS>(P, tv.rd, len, w, ce, lane, T, used, ex, cnt, sums, term_at);
-    const uint64_t tcnt = wave_sum_u64(cnt);
-    uint64_t tsum[NS > 0 ? NS : SPK_MAX_SPANS];
-    for (uint32_t q = 0; q < nsp; ++q) tsum[q] = wave_sum_u64(sums[q]);
-    TB.cused[g] = used;
-    TB.cex[g] = ex;
-    TB.ccnt[g] = cnt;
-    for (uint32_t q = 0; q < nsp; ++q) TB.csum[(uint64_t)q * TB.nchunks + g] = sums[q];
-    const uint64_t y63 = __shfl(ex, 63);
-    if (lane == 0) {
-      fn[0] = y63;
-      fn[1] = 1;
-      fn[2] = T;
-      fn[3] = tcnt;
-      for (uint32_t q = 0; q < nsp; ++q) fn[4 + q] = tsum[q];
-      TB.sel[t] = 0;
+    const uint64_t T = tile_entry(TB, c, f);
+    const uint64_t ts = p0 + f * kTileBytes;
+    if (T >= ts + kTileBytes) {
+      // a record spans tiles f .. e-1: all pass the entry through
+      const uint64_t e0 = (T - p0) / kTileBytes;
+      const uint64_t e = e0 < TB.ntiles ? e0 : TB.ntiles;
+      for (uint64_t v = f + lane; v < e; v += 64) tile_pass_through(TB, v, T, nsp);
+      if (lane == 0) fc->seq += e - f;
+      t = e;
+    } else {
+      const TileView tv = stage_tile(win_s[0], wire, len, ts, w, lane);
+      const uint64_t cs = ts + (uint64_t)lane * kTChunk;
+      const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
+      const uint64_t g = f * 64 + lane;
+      uint64_t used = TB.cused[g], ex = TB.cex[g], term_at = kTermPos;
+      uint32_t cnt = TB.ccnt[g];
+      uint64_t sums[NS > 0 ? NS : SPK_MAX_SPANS];
+      for (uint32_t q = 0; q < nsp; ++q) sums[q] = TB.csum[(uint64_t)q * TB.nchunks + g];
+      resolve_tile<NS>(P, tv.rd, len, w, ce, lane, T, used, ex, cnt, sums, term_at);
+      const uint64_t tcnt = wave_sum_u64(cnt);
+      uint64_t tsum[NS > 0 ? NS : SPK_MAX_SPANS];
+      for (uint32_t q = 0; q < nsp; ++q) tsum[q] = wave_sum_u64(sums[q]);
+      TB.cused[g] = used;
+      TB.cex[g] = ex;
+      TB.ccnt[g] = cnt;
+      for (uint32_t q = 0; q < nsp; ++q) TB.csum[(uint64_t)q * TB.nchunks + g] = sums[q];
+      const uint64_t y63 = __shfl(ex, 63);
+      if (lane == 0) {
+        uint64_t *fn = TB.fn + f * kFnWords;
+        fn[0] = y63;
+        fn[1] = 1;
+        fn[2] = T;
+        fn[3] = tcnt;
+        for (uint32_t q = 0; q < nsp; ++q) fn[4 + q] = tsum[q];
+        TB.sel[f] = 0;
+        fc->seq += 1;
+      }
+      t = f + 1;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -2801,7 +2887,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
                                                                 uint8_t *__restrict__ ws,
                                                                 TileBufs TB,
                                                                 uint8_t *__restrict__ recs,
-                                                                uint32_t dbg) {
+                                                                BigQ bq, uint32_t dbg) {
   __shared__ v4u_t win_s[kDecWaves][kTileVec + 1];
   __shared__ uint16_t tab_s[kDecWaves][kTab];
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
@@ -2812,7 +2898,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
   const uint64_t n = c->n;
   const uint64_t base = TB.contrib[t];
   const int32_t sel = TB.sel[t];
-  if (base >= n || sel < 0) return;
+  if (base >= n || sel < 0 || !TB.fn[t * kFnWords + 2 + sel * kAltWords + 1]) return;
   const uint32_t w = c->w;
   const uint64_t len = a.wire_len, p0 = c->p0;
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
@@ -2889,7 +2975,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
       }
       const uint64_t g = base + pass0 + i;
       if (act && g < a.rec_cap && fits && !(dbg & 64))
-        emit_record_rd(a.L, rd, pos, w, recs + g * a.L.stride, a.heaps, off, len);
+        emit_record_rd(a.L, rd, pos, w, recs + g * a.L.stride, a.heaps, off, len, bq);
       if (act && g == n - 1) {
         fc->end_pos = pos + L;
         for (uint32_t q = 0; q < nsp; ++q) fc->htot[q] = off[q] + rc[q];
@@ -2898,6 +2984,26 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+// The queued long-span pieces: one block per piece, 16-B aligned stores.
+__global__ __launch_bounds__(256) void vec_big_copy(const uint8_t *__restrict__ wire,
+                                                    const uint8_t *__restrict__ ws, BigQ bq) {
+  const FCtl *fc = reinterpret_cast<const FCtl *>(ws + kWsFCtl);
+  const uint64_t nj = fc->njobs < bq.cap ? fc->njobs : bq.cap;
+  for (uint64_t j = blockIdx.x; j < nj; j += gridDim.x) {
+    const BigJob jb = bq.jobs[j];
+    const uint8_t *src = wire + jb.src;
+    uint8_t *dst = jb.dst;
+    const uint64_t head = (16 - ((uintptr_t)dst & 15)) & 15;
+    const uint64_t h = head < jb.n ? head : jb.n;
+    if (threadIdx.x < h) dst[threadIdx.x] = src[threadIdx.x];
+    const uint64_t nv = (jb.n - h) / 16;
+    for (uint64_t v = threadIdx.x; v < nv; v += blockDim.x)
+      *reinterpret_cast<v4u_t *>(dst + h + 16 * v) =
+          *reinterpret_cast<const v4u_una *>(src + h + 16 * v);
+    for (uint64_t b = h + 16 * nv + threadIdx.x; b < jb.n; b += blockDim.x) dst[b] = src[b];
   }
 }
 
@@ -2910,6 +3016,10 @@ __global__ void vec_tile_finish(DecArgs a, const uint8_t *__restrict__ wire,
   const FCtl *fc = reinterpret_cast<const FCtl *>(ws + kWsFCtl);
   if (c->errc) return;  // the header errc is already in *res
   spk_dresult_t r = *res;
+  uint64_t rep = 0;
+  for (int k = 0; k < 4; ++k) rep += fc->broken[k];
+  r.tiles_repaired = (uint32_t)(rep < 0xFFFFFFFFull ? rep : 0xFFFFFFFFull);
+  r.tiles_sequential = (uint32_t)(fc->seq < 0xFFFFFFFFull ? fc->seq : 0xFFFFFFFFull);
   if (fc->unresolved) {
     r.errc = SPK_ERRC_INTERNAL;
     *res = r;
@@ -3089,7 +3199,7 @@ static hipError_t launch_vec_decode_ns(const DecArgs &a, const WalkProg &P, cons
 
 // ---- tile decoder: workspace and launch ---------------------------------------
 struct TileWs {
-  size_t fn, cused, cex, ccnt, csum, sel, contrib, scan, end;
+  size_t fn, cused, cex, ccnt, csum, sel, contrib, scan, jobs, end;
   uint64_t ntiles, nchunks, nsb;
 };
 static TileWs tile_ws_layout(const spk_layout *L, uint64_t wire_len) {
@@ -3115,6 +3225,7 @@ static TileWs tile_ws_layout(const spk_layout *L, uint64_t wire_len) {
   f.sel = take(f.ntiles * 4);
   f.contrib = take(f.ntiles * 8 * (1 + ns));
   f.scan = take(f.nsb * 8 * (1 + ns));
+  f.jobs = take(big_jobs_cap(wire_len) * sizeof(BigJob));
   f.end = off;
   return f;
 }
@@ -3157,8 +3268,16 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
   SPK_LAUNCH(tscan_reduce, dim3(nb), dim3(256), 0, s, (const uint8_t *)ws, TB, 1 + nsp);
   SPK_LAUNCH(tscan_top, dim3(1), dim3(1024), 0, s, ws, TB, 1 + nsp, (uint64_t)nb);
   SPK_LAUNCH(tscan_apply, dim3(nb), dim3(256), 0, s, (const uint8_t *)ws, TB, 1 + nsp);
+  BigQ bq;
+  bq.jobs = reinterpret_cast<BigJob *>(ws + f.jobs);
+  bq.n = &reinterpret_cast<FCtl *>(ws + kWsFCtl)->njobs;
+  bq.cap = big_jobs_cap(a.wire_len);
   SPK_LAUNCH(vec_tile_emit<NS>, dim3(grid_for(f.ntiles, kDecWaves)), dim3(64 * kDecWaves), 0, s,
-             a, P, wire, ws, TB, d_recs, tile_dbg());
+             a, P, wire, ws, TB, d_recs, bq, tile_dbg());
+  if (P.ns) {
+    const uint64_t gb = bq.cap < 2048 ? bq.cap : 2048;
+    SPK_LAUNCH(vec_big_copy, dim3((unsigned)gb), dim3(256), 0, s, wire, (const uint8_t *)ws, bq);
+  }
   SPK_LAUNCH(vec_tile_finish, dim3(1), dim3(64), 0, s, a, wire, (const uint8_t *)ws, d_res);
   return hipGetLastError();
 }

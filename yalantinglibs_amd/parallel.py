@@ -90,7 +90,8 @@ class ShardedVectorEncoder:
     def plan(self, batch: RecordBatch) -> ShardPlan:
         p = self.cd.get_needed_size(batch, C.SPK_MODE_VECTOR)
         return agree_shard_plan(batch.n, p.max_count, p.var_bytes, self.cd.L.n_cont,
-                                self.header, self.group, self.cd.device)
+                                self.header, self.group,
+                                None if self._host_staged() else self.cd.device)
 
     def encode_body(self, batch: RecordBatch, width: int, out: torch.Tensor, stream=None):
         ws = self.cd.workspace(C.SPK_MODE_VECTOR, batch.n)
@@ -100,6 +101,63 @@ class ShardedVectorEncoder:
         if rc != 0:
             raise RuntimeError(f"spk_encode_body failed ({rc})")
 
+    def _host_staged(self) -> bool:
+        # gloo moves host tensors only (CPU rehearsals); RCCL moves HBM directly
+        return dist.get_backend(self.group) == "gloo"
+
+    def gather(self, sp: ShardPlan, body: torch.Tensor, out: Optional[torch.Tensor],
+               root: int = 0) -> None:
+        """P2P concatenation: every rank's body goes into its slice of root's
+        message buffer `out` (grouped RCCL send/recv over xGMI; root also
+        writes the header and its own body). `out` is ignored off root."""
+        mine = sp.body_bytes[self.rank]
+        staged = self._host_staged()
+        if self.rank == root:
+            o = sp.offsets[self.rank]
+            out[:len(sp.header)].copy_(torch.frombuffer(bytearray(sp.header), dtype=torch.uint8))
+            out[o:o + mine].copy_(body[:mine])
+            ops, bufs = [], []
+            for r in range(self.world):
+                if r != root and sp.body_bytes[r]:
+                    o = sp.offsets[r]
+                    dst = out[o:o + sp.body_bytes[r]]
+                    if staged:
+                        dst = torch.empty(sp.body_bytes[r], dtype=torch.uint8)
+                        bufs.append((o, dst))
+                    ops.append(dist.P2POp(dist.irecv, dst, r, self.group))
+            if ops:
+                for req in dist.batch_isend_irecv(ops):
+                    req.wait()
+            for o, b in bufs:
+                out[o:o + b.numel()].copy_(b)
+        elif mine:
+            src = body[:mine].cpu() if staged else body[:mine]
+            for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, src, root, self.group)]):
+                req.wait()
+
+    def all_gather(self, sp: ShardPlan, body: torch.Tensor, out: torch.Tensor,
+                   slab: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Every rank receives the whole message: one RCCL all-gather of the
+        bodies padded to the largest, then an on-device compaction behind the
+        header. `slab` (world x max body bytes) may be passed to reuse it."""
+        mb = max(max(sp.body_bytes), 1)
+        mine = sp.body_bytes[self.rank]
+        staged = self._host_staged()
+        dev = torch.device("cpu") if staged else body.device
+        if slab is None or slab.device != dev:
+            slab = torch.empty(self.world * mb, dtype=torch.uint8, device=dev)
+        send = torch.zeros(mb, dtype=torch.uint8, device=dev)
+        send[:mine].copy_(body[:mine])
+        if staged:
+            dist.all_gather(list(slab.view(self.world, mb).unbind(0)), send, group=self.group)
+        else:
+            dist.all_gather_into_tensor(slab, send, group=self.group)
+        out[:len(sp.header)].copy_(torch.frombuffer(bytearray(sp.header), dtype=torch.uint8))
+        for r in range(self.world):
+            o, b = sp.offsets[r], sp.body_bytes[r]
+            out[o:o + b].copy_(slab[r * mb:r * mb + b])
+        return slab
+
     def encode(self, batch: RecordBatch, root: int = 0) -> Optional[torch.Tensor]:
         """Returns the whole message on `root` (None elsewhere). The bodies
         move to root with grouped RCCL point-to-point transfers straight into
@@ -108,27 +166,10 @@ class ShardedVectorEncoder:
         mine = sp.body_bytes[self.rank]
         body = torch.empty(max(mine, 1), dtype=torch.uint8, device=self.cd.device)
         self.encode_body(batch, sp.width, body)
-        if self.rank == root:
-            out = torch.empty(sp.total_bytes, dtype=torch.uint8, device=self.cd.device)
-            hdr = torch.frombuffer(bytearray(sp.header), dtype=torch.uint8)
-            out[:len(sp.header)].copy_(hdr)
-            o = sp.offsets[self.rank]
-            out[o:o + mine].copy_(body[:mine])
-            ops = []
-            for r in range(self.world):
-                if r != root and sp.body_bytes[r]:
-                    o = sp.offsets[r]
-                    ops.append(dist.P2POp(dist.irecv, out[o:o + sp.body_bytes[r]], r,
-                                          self.group))
-            if ops:
-                for req in dist.batch_isend_irecv(ops):
-                    req.wait()
-            return out
-        if mine:
-            for req in dist.batch_isend_irecv([dist.P2POp(dist.isend, body[:mine], root,
-                                                          self.group)]):
-                req.wait()
-        return None
+        out = (torch.empty(sp.total_bytes, dtype=torch.uint8, device=self.cd.device)
+               if self.rank == root else None)
+        self.gather(sp, body, out, root)
+        return out
 
     def encode_to_host(self, batch: RecordBatch, host_out: torch.Tensor) -> ShardPlan:
         """coro_rpc destination: every rank copies its body D2H straight into

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import hashlib
 from dataclasses import dataclass, field
+from typing import Optional as Optional_
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -331,6 +332,19 @@ class SpanField:
     elem: SpType
     count_off: int
     off_off: int
+    sub: "Optional_[DeviceLayout]" = None  # ARRAY: the element record layout
+
+
+class ElemRecord(SpType):
+    """The device record of a container element that is not trivially
+    serializable (an SPK_OP_ARRAY heap holds these)."""
+
+    def __init__(self, layout: "DeviceLayout"):
+        self.layout = layout
+        self.name = f"record<{layout.rtype.name}>"
+        self.size = layout.stride
+        self.align = 8
+        self.config = DEFAULT
 
 
 @dataclass
@@ -385,11 +399,23 @@ def flatten(rtype: SpType) -> DeviceLayout:
             off = place(t.size, t.align)
             ops.append((C.SPK_OP_COPY, off, t.size, 0))
             npf.append((path, _np_format(t), off))
+        elif isinstance(t, (String, Vector)) and not t.elem.trivial:
+            # container of non-trivially-serializable elements: SPK_OP_ARRAY
+            # over the element's own flattened layout (packer.hpp:365-367)
+            sub = flatten(t.elem)
+            coff = place(4, 4)
+            ooff = place(8, 8)
+            ops.append((C.SPK_OP_ARRAY, coff, sub.stride, ooff))
+            spans.append(SpanField(path, ElemRecord(sub), coff, ooff, sub))
+            npf.append((path + ".n", "<u4", coff))
+            npf.append((path + ".off", "<u8", ooff))
+            for op in (sub.ops if not sub.trivial else [(C.SPK_OP_COPY, 0, sub.stride, 0)]):
+                ops.append(op)
+            ops.append((C.SPK_OP_END, 0, 0, 0))
+            for sp in sub.spans:
+                spans.append(SpanField(f"{path}[].{sp.path}", sp.elem, sp.count_off, sp.off_off,
+                                       sp.sub))
         elif isinstance(t, (String, Vector)):
-            if not t.elem.trivial:
-                raise NotImplementedError(
-                    f"{path}: container of non-trivially-serializable "
-                    f"{t.elem.name} is outside the flat record model")
             coff = place(4, 4)
             ooff = place(8, 8)
             ops.append((C.SPK_OP_SPAN, coff, t.elem.size, ooff))
@@ -426,18 +452,64 @@ def flatten(rtype: SpType) -> DeviceLayout:
         raise NotImplementedError("too many variable-length members")
     if sum(op[0] == C.SPK_OP_VARINT for op in ops) > C.SPK_MAX_VARINTS:
         raise NotImplementedError("too many varint members")
-    # merge COPY runs contiguous in the record (always contiguous on the wire)
+    if len(ops) > C.SPK_MAX_OPS:
+        raise NotImplementedError("too many layout ops")
+    # merge COPY runs contiguous in the record (always contiguous on the wire);
+    # never across an ARRAY's element ops (they address another record)
     merged: List[Tuple[int, int, int, int]] = []
+    depth, last_depth = 0, -1
     for op in ops:
         if (merged and op[0] == C.SPK_OP_COPY and merged[-1][0] == C.SPK_OP_COPY
-                and merged[-1][1] + merged[-1][2] == op[1]):
+                and last_depth == depth and merged[-1][1] + merged[-1][2] == op[1]):
             k, o, s, a = merged[-1]
             merged[-1] = (k, o, s + op[2], a)
         else:
             merged.append(op)
+        last_depth = depth
+        if op[0] == C.SPK_OP_ARRAY:
+            depth += 1
+            last_depth = -1
+        elif op[0] == C.SPK_OP_END:
+            depth -= 1
+            last_depth = -1
     # non-trivial device records are 8-byte aligned (the kernels read span
     # offsets as u64; spk_layout_check rejects other strides), also when the
     # record has only 4-byte members and varints
     align = max(cur[1], 8)
     stride = (cur[0] + align - 1) // align * align
     return DeviceLayout(rtype, stride, merged, spans, npf, False)
+
+
+def min_record_wire_bytes(dev: DeviceLayout) -> int:
+    """Fewest wire bytes one top-level record can take (each container count
+    >= 1 byte): bounds a decode's record capacity by the wire length."""
+    from . import _capi as C
+    total, depth = 0, 0
+    for k, _, sz, _ in dev.ops:
+        if k == C.SPK_OP_END:
+            depth -= 1
+            continue
+        if depth == 0:
+            total += sz if k == C.SPK_OP_COPY else 1
+        if k == C.SPK_OP_ARRAY:
+            depth += 1
+    return max(total, 1)
+
+
+def heap_caps_for_wire(dev: DeviceLayout, wire_len: int, rec_cap: int) -> List[int]:
+    """Per-heap element capacities no decode of `wire_len` bytes can exceed:
+    a SPAN's elements take their size in wire bytes; an ARRAY element and a
+    nested OPTION at least one byte; a top-level OPTION one per record."""
+    from . import _capi as C
+    caps, depth = [], 0
+    for k, _, sz, _ in dev.ops:
+        if k == C.SPK_OP_SPAN:
+            caps.append(wire_len // max(sz, 1) + 1)
+        elif k == C.SPK_OP_OPTION:
+            caps.append(rec_cap if depth == 0 else wire_len + 1)
+        elif k == C.SPK_OP_ARRAY:
+            caps.append(wire_len + 1)
+            depth += 1
+        elif k == C.SPK_OP_END:
+            depth -= 1
+    return caps

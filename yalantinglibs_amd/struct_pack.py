@@ -110,9 +110,9 @@ class Codec:
     def plan(self, batch: RecordBatch, mode: int, stream=None) -> torch.Tensor:
         """Size pass (stream-ordered): writes spk_plan_t into self.plan_buf."""
         ws = self.workspace(mode, batch.n)
-        self._check(self.lib.spk_plan(self.L.ptr, mode, batch.n, _p(batch.recs),
-                                      _p(self.plan_buf), _p(ws), ws.numel(),
-                                      _stream(stream)), "spk_plan")
+        self._check(self.lib.spk_plan_ex(self.L.ptr, mode, batch.n, _p(batch.recs),
+                                         self._heap_ptrs(batch.heaps), _p(self.plan_buf),
+                                         _p(ws), ws.numel(), _stream(stream)), "spk_plan_ex")
         return self.plan_buf
 
     def get_needed_size(self, batch: RecordBatch, mode: int = MODE_VECTOR) -> C.spk_plan_t:
@@ -195,12 +195,9 @@ class Codec:
         """Allocating decode: capacities bounded by the wire length.
         Returns (result, RecordBatch, errc tensor or None)."""
         wl = wire.numel()
-        min_rec = max(1, sum(op[2] if op[0] == C.SPK_OP_COPY else 1 for op in self.L.dev.ops))
+        min_rec = S.min_record_wire_bytes(self.L.dev)
         cap = (wl // min_rec + 1) if mode == MODE_VECTOR else n_msgs
-        # an OPTION holds at most one value per record, readable or not
-        opt = [op[0] == C.SPK_OP_OPTION for op in self.L.dev.ops
-               if op[0] in (C.SPK_OP_SPAN, C.SPK_OP_OPTION)]
-        elems = [cap if o else wl // sp.elem.size + 1 for o, sp in zip(opt, self.L.dev.spans)]
+        elems = S.heap_caps_for_wire(self.L.dev, wl, cap)
         out = self.alloc_batch(cap, elems)
         ec = (torch.zeros(max(n_msgs, 1), dtype=torch.int32, device=self.device)
               if mode == MODE_MESSAGES else None)

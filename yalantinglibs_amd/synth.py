@@ -26,11 +26,11 @@ def mix64(z):
     return z ^ (z >> np.uint64(31))
 
 
-def rnd(seed: int, i, k):
+def rnd(seed, i, k):
     i = np.asarray(i, dtype=np.uint64)
     k = np.asarray(k, dtype=np.uint64)
     with np.errstate(over="ignore"):
-        x = np.uint64(seed) + (i * np.uint64(64) + k + np.uint64(1)) * GOLD
+        x = np.asarray(seed, dtype=np.uint64) + (i * np.uint64(64) + k + np.uint64(1)) * GOLD
     return mix64(x)
 
 
@@ -86,10 +86,16 @@ Var = S.Struct("Var", [("a", S.var_int32), ("s", S.String()), ("b", S.var_uint64
                        ("d", S.float64), ("c", S.var_int64), ("e", S.var_uint32)])
 VarP = S.Struct("VarP", [("id", S.int32), ("x", S.var_int64), ("y", S.var_uint32)])
 
+# containers of non-trivially-serializable elements (SPK_OP_ARRAY)
+Tags = S.Struct("Tags", [("id", S.int32), ("tags", S.Vector(S.String())), ("w", S.float64)])
+Group = S.Struct("Group", [("gid", S.int64), ("members", S.Vector(RecS)),
+                           ("label", S.String())])
+Deep = S.Struct("Deep", [("k", S.uint16), ("m", S.Vector(S.Vector(S.String())))])
+
 CASE_TYPES = {"rec64": Rec64, "recs": RecS, "outer": Outer, "pad": Pad,
               "mixed": Mixed, "rect": RectInt, "rpcrect": RpcRect,
               "person": Person, "ints": Ints, "opt": Opt, "optp": OptP,
-              "var": Var, "varp": VarP}
+              "var": Var, "varp": VarP, "tags": Tags, "group": Group, "deep": Deep}
 # vector<rect<int>> has its own ADL set_sp_config (benchmark data_def.hpp:69-72)
 VECTOR_CONFIG = {"rect": S.DISABLE_ALL_META_INFO}
 
@@ -103,6 +109,40 @@ def _chars(seed, idx, lens):
     w = rnd(seed, rec, np.uint64(2) + (j >> np.uint64(3)) % np.uint64(56))
     b = (w >> ((j & np.uint64(7)) * np.uint64(8))) & np.uint64(0xFF)
     return (np.uint64(ord("a")) + b % np.uint64(26)).astype(np.uint8)
+
+
+def _seg(cnt):
+    """(owner index, index within the owner) of every element of lists with
+    counts `cnt`."""
+    cnt = np.asarray(cnt, np.int64)
+    owner = np.repeat(np.arange(len(cnt)), cnt)
+    j = np.arange(int(cnt.sum()), dtype=np.int64) - np.repeat(_excl(cnt), cnt)
+    return owner, j.astype(np.uint64)
+
+
+def _tag_strings(h):
+    """tag_chars(h) of types.hpp for every word in h: (lengths, chars)."""
+    h = np.asarray(h, np.uint64)
+    lens = (h % np.uint64(13)).astype(np.int64)
+    owner, k = _seg(lens)
+    with np.errstate(over="ignore"):
+        w = mix64(h[owner] + (k >> np.uint64(3)))
+    b = (w >> ((k & np.uint64(7)) * np.uint64(8))) & np.uint64(0xFF)
+    return lens, (np.uint64(ord("a")) + b % np.uint64(26)).astype(np.uint8)
+
+
+def _elem_word(seed, i, j):
+    """elem_word(seed, i, j) of types.hpp."""
+    return mix64(rnd(seed, i, np.uint64(2) + np.asarray(j, np.uint64) % np.uint64(56))
+                 ^ np.asarray(j, np.uint64))
+
+
+def _str_records(sub, lens):
+    """element records of a std::string element layout (value.n / value.off)."""
+    e = np.zeros(len(lens), dtype=sub.dtype)
+    e["value.n"] = lens
+    e["value.off"] = _excl(lens)
+    return e
 
 
 def _excl(cnt):
@@ -262,6 +302,56 @@ def make_batch(case: str, n: int, seed: int, param: int = 48):
         x = _spread(r1)
         recs["x"] = np.where(r1 & np.uint64(1), ~x, x).view(np.int64)
         recs["y"] = (_spread(rnd(seed, idx, 2)) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    elif case == "tags":  # fill(Tags&)
+        recs["id"] = i32(rnd(seed, idx, 0))
+        cnt = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+        recs["tags.n"] = cnt
+        recs["tags.off"] = _excl(cnt)
+        recs["w"] = rd(rnd(seed, idx, 60))
+        owner, j = _seg(cnt)
+        lens, chars = _tag_strings(_elem_word(seed, idx[owner], j))
+        heaps.append(_str_records(L.spans[0].sub, lens).view(np.uint8))
+        heaps.append(chars)
+    elif case == "group":  # fill(Group&): member j = make_recs(mix64(seed + i), j, 20)
+        recs["gid"] = rnd(seed, idx, 0).view(np.int64)
+        cnt = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+        recs["members.n"] = cnt
+        recs["members.off"] = _excl(cnt)
+        owner, j = _seg(cnt)
+        with np.errstate(over="ignore"):
+            s2 = mix64(np.uint64(seed) + idx[owner])
+        m = np.zeros(len(j), dtype=L.spans[0].sub.dtype)
+        m["id"] = i32(rnd(s2, j, 0))
+        mlen = (rnd(s2, j, 1) % np.uint64(21)).astype(np.int64)
+        m["name.n"] = mlen
+        m["name.off"] = _excl(mlen)
+        m["v"] = rd(rnd(s2, j, 60))
+        mo, c = _seg(mlen)
+        w = rnd(s2[mo], j[mo], np.uint64(2) + (c >> np.uint64(3)) % np.uint64(56))
+        b = (w >> ((c & np.uint64(7)) * np.uint64(8))) & np.uint64(0xFF)
+        heaps.append(m.view(np.uint8))
+        heaps.append((np.uint64(ord("a")) + b % np.uint64(26)).astype(np.uint8))
+        lens = (rnd(seed, idx, 1) % np.uint64(13)).astype(np.int64)
+        recs["label.n"] = lens
+        recs["label.off"] = _excl(lens)
+        heaps.append(_chars(seed, idx, lens))
+    elif case == "deep":  # fill(Deep&): list j of record i has h % 5 strings
+        recs["k"] = rnd(seed, idx, 0).astype(np.uint16)
+        cnt = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+        recs["m.n"] = cnt
+        recs["m.off"] = _excl(cnt)
+        owner, j = _seg(cnt)
+        h = _elem_word(seed, idx[owner], j)
+        m = (h % np.uint64(5)).astype(np.int64)
+        lists = np.zeros(len(j), dtype=L.spans[0].sub.dtype)
+        lists["value.n"] = m
+        lists["value.off"] = _excl(m)
+        lo, q = _seg(m)
+        with np.errstate(over="ignore"):
+            lens, chars = _tag_strings(mix64(h[lo] + q + np.uint64(1)))
+        heaps.append(lists.view(np.uint8))
+        heaps.append(_str_records(L.spans[1].sub, lens).view(np.uint8))
+        heaps.append(chars)
     else:
         raise KeyError(case)
     return L, recs, heaps
