@@ -471,6 +471,12 @@ def run_config(cfg, args, torch, dist, world, rank, dev, steps, warmup, settle, 
         host = host_path(wl, torch, dev)
     if host:
         out["host_path"] = host
+        try:
+            hp = host_path_pipelined(wl, torch, dev)
+        except Exception as e:  # never lose the line
+            hp = {"error": f"{type(e).__name__}: {e}"}
+        if hp:
+            out["host_path_pipelined"] = hp
     out["cpu_baseline"] = None
     if cpu and rank == 0 and world == 1 and not args.no_cpu_baseline and wl.cpu_case():
         out["cpu_baseline"] = cpu_baseline(wl.cpu_case(), wl.units,
@@ -593,6 +599,94 @@ def concat_bench(torch, dist, world, rank, dev, n, reps=3):
     }
 
 
+def host_path_pipelined(wl, torch, dev, chunk_records=4_000_000, reps=3):
+    """The host path of a trivially-serializable VECTOR config (C2) as a
+    pipeline: the batch moves in record chunks over three HIP streams (H2D,
+    compute, D2H) with pinned host buffers. Chunk c of the step's encode leg
+    (H2D records -> spk_encode_body -> D2H wire) and of its decode leg (H2D
+    wire -> spk_decode_body -> D2H records, header parsed on the host by
+    spk_parse_vector_header) run beside chunk c+1's transfers, so both PCIe
+    directions stay busy. Same bytes as host_path (the serial form)."""
+    import ctypes as ct
+    SP = wl.SP
+    cd = wl.cd
+    if not cd.L.dev.trivial or wl.mode != SP.MODE_VECTOR:
+        return None
+    n, stride = wl.n, cd.L.stride
+    plan = cd.get_needed_size(wl.batch, SP.MODE_VECTOR)
+    w, hl, total = plan.width, plan.header_bytes, plan.total_bytes
+    hb = (ct.c_uint8 * 512)()
+    k = cd.lib.spk_vector_header(cd.L.ptr, n, w, hb, 512)
+    assert k == hl
+    recs_b = n * stride
+    h_recs = torch.empty(recs_b, dtype=torch.uint8).pin_memory()
+    h_recs.copy_(wl.batch.recs.view(-1))
+    h_wire_in = torch.empty(total, dtype=torch.uint8).pin_memory()   # decode input
+    h_wire_out = torch.empty(total, dtype=torch.uint8).pin_memory()  # encode output
+    h_out = torch.empty(recs_b, dtype=torch.uint8).pin_memory()
+    cd.serialize_to(wl.wire, wl.batch, SP.MODE_VECTOR, planned=False)
+    h_wire_in.copy_(wl.wire[:total])
+    d_recs = wl.batch.recs.view(-1)
+    d_wire_out = wl.wire
+    d_wire_in = torch.empty(total, dtype=torch.uint8, device=dev)
+    d_dec = wl.dec.recs.view(-1)
+    s_in, s_cmp, s_out = (torch.cuda.Stream(dev) for _ in range(3))
+    ws = cd.workspace(SP.MODE_VECTOR, max(chunk_records, 1), total)
+    chunks = [(r, min(r + chunk_records, n)) for r in range(0, n, chunk_records)]
+    nullh = (ct.c_void_p * 1)(0)
+    caps0 = (ct.c_uint64 * 1)(0)
+
+    def step():
+        h_wire_out[:hl].copy_(torch.frombuffer(bytearray(bytes(hb[:hl])), dtype=torch.uint8))
+        e, nn, ww, hh = cd.parse_vector_header(bytes(h_wire_in[:64].numpy()))
+        assert e == 0 and nn == n and ww == w and hh == hl
+        for r0, r1 in chunks:
+            b0, b1 = r0 * stride, r1 * stride
+            # encode leg
+            with torch.cuda.stream(s_in):
+                d_recs[b0:b1].copy_(h_recs[b0:b1], non_blocking=True)
+                ev_in = torch.cuda.Event()
+                ev_in.record(s_in)
+                d_wire_in[hl + b0:hl + b1].copy_(h_wire_in[hl + b0:hl + b1], non_blocking=True)
+                ev_win = torch.cuda.Event()
+                ev_win.record(s_in)
+            s_cmp.wait_event(ev_in)
+            rc = cd.lib.spk_encode_body(cd.L.ptr, r1 - r0, SP._p(d_recs[b0:]), nullh, w,
+                                        SP._p(d_wire_out[hl + b0:]), b1 - b0, SP._p(ws),
+                                        ws.numel(), SP._stream(s_cmp))
+            assert rc == 0
+            ev_enc = torch.cuda.Event()
+            ev_enc.record(s_cmp)
+            s_cmp.wait_event(ev_win)
+            rc = cd.lib.spk_decode_body(cd.L.ptr, SP._p(d_wire_in[hl + b0:]), b1 - b0, w,
+                                        r1 - r0, SP._p(d_dec[b0:]), r1 - r0, nullh, caps0,
+                                        SP._p(cd.res_buf), SP._p(ws), ws.numel(),
+                                        SP._stream(s_cmp))
+            assert rc == 0
+            ev_dec = torch.cuda.Event()
+            ev_dec.record(s_cmp)
+            s_out.wait_event(ev_enc)
+            with torch.cuda.stream(s_out):
+                h_wire_out[hl + b0:hl + b1].copy_(d_wire_out[hl + b0:hl + b1], non_blocking=True)
+            s_out.wait_event(ev_dec)
+            with torch.cuda.stream(s_out):
+                h_out[b0:b1].copy_(d_dec[b0:b1], non_blocking=True)
+        for st in (s_in, s_cmp, s_out):
+            st.synchronize()
+
+    step()  # warmup
+    ok = bool(torch.equal(h_out, h_recs)) and bool(torch.equal(h_wire_out, h_wire_in))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    dt = (time.perf_counter() - t0) / reps
+    return {"ms_per_step": round(dt * 1e3, 3), "gib_s": round(wl.algo_bytes / dt / 2**30, 3),
+            "chunk_records": chunk_records, "check": "ok" if ok else "FAILED",
+            "note": "pipelined: per record chunk H2D records -> spk_encode_body -> D2H wire and "
+                    "H2D wire -> spk_decode_body -> D2H records, three HIP streams, pinned "
+                    "host buffers, header parsed on the host (spk_parse_vector_header)"}
+
+
 def main():
     args = parse()
     import torch
@@ -647,6 +741,8 @@ def main():
         }
         if "host_path" in head:
             line["host_path"] = head["host_path"]
+        if "host_path_pipelined" in head:
+            line["host_path_pipelined"] = head["host_path_pipelined"]
         if concat is not None:
             line["concat_ms"] = concat.get("p2p_gather_ms")
             line["concat_gbs"] = concat.get("p2p_gather_gbs")

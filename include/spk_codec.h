@@ -67,7 +67,20 @@
  *                                           365-367; decode: unpacker.hpp:
  *                                           1208-1226, stops at the first
  *                                           failing element).
- *   SPK_OP_END {0, 0, 0, 0}                closes the innermost open ARRAY.
+ *   SPK_OP_VARIANT {rec_off, size, 0}      a std::variant of `size` (1..255)
+ *                                           alternatives: the record holds the
+ *                                           u32 active index at rec_off; the
+ *                                           ops that follow are `size` groups,
+ *                                           each closed by SPK_OP_END: the
+ *                                           flattened alternatives, placed in
+ *                                           the same record (an empty group is
+ *                                           std::monostate). Wire: [index:1]
+ *                                           then the active alternative
+ *                                           (packer.hpp:389-398); decode: an
+ *                                           index >= size is invalid_buffer
+ *                                           (unpacker.hpp:1278-1292).
+ *   SPK_OP_END {0, 0, 0, 0}                closes the innermost open ARRAY or
+ *                                           VARIANT alternative.
  * Heaps are numbered in op order over SPAN, OPTION and ARRAY ops at every
  * nesting level; heap k of an ARRAY holds element records, counted in
  * elements like the others. Decode writes every heap packed in wire order.
@@ -132,7 +145,8 @@ extern "C" {
 #define SPK_OP_VARINT 4u
 #define SPK_OP_ARRAY 5u
 #define SPK_OP_END 6u
-#define SPK_MAX_DEPTH 4u       /* ARRAY nesting levels                       */
+#define SPK_OP_VARIANT 7u
+#define SPK_MAX_DEPTH 4u       /* ARRAY / VARIANT nesting levels             */
 
 /* spk_op.aux of an SPK_OP_VARINT */
 #define SPK_VARINT_ZIGZAG 0x1u /* var_int32_t / var_int64_t (sint<T>): zigzag */
@@ -151,7 +165,7 @@ extern "C" {
 #define SPK_LAYOUT_TRIVIAL 0x1u   /* is_trivial_serializable<T>: 1 COPY op  */
 
 typedef struct spk_op {
-  uint32_t kind;    /* SPK_OP_COPY | SPAN | OPTION | VARINT | ARRAY | END    */
+  uint32_t kind;    /* SPK_OP_COPY | SPAN | OPTION | VARINT | ARRAY | END | VARIANT */
   uint32_t rec_off; /* COPY: source byte offset; SPAN: u32 count offset      */
   uint32_t size;    /* COPY: byte length;       SPAN: element size (bytes)   */
   uint32_t aux;     /* SPAN: u64 heap element-offset field offset; COPY: 0   */
@@ -311,6 +325,24 @@ int spk_decode_framed(const spk_layout *L, const void *d_wire, uint64_t wire_len
 int spk_encode_body(const spk_layout *L, uint64_t n, const void *d_recs,
                     const void *const *d_heaps, uint32_t width, void *d_out,
                     uint64_t out_cap, void *d_ws, size_t ws_bytes, void *stream);
+/* Decode exactly n records from a message BODY — the bytes after the header
+ * and the container count of a SPK_MODE_VECTOR message of width `width` —
+ * into d_recs / d_heaps: the counterpart of spk_encode_body, for pipelined
+ * (chunked H2D) and sharded decodes where the front end has parsed the
+ * header already (spk_parse_vector_header). Errors and d_res as spk_decode;
+ * d_res->consumed counts body bytes. Heaps are written from element 0. */
+int spk_decode_body(const spk_layout *L, const void *d_body, uint64_t body_len,
+                    uint32_t width, uint64_t n, void *d_recs, uint64_t rec_cap,
+                    void *const *d_heaps, const uint64_t *heap_caps,
+                    spk_dresult_t *d_res, void *d_ws, size_t ws_bytes, void *stream);
+
+/* HOST function: deserialize_metainfo of a SPK_MODE_VECTOR message in host
+ * memory (unpacker.hpp:548-619) plus its container count. Returns the
+ * reference errc (0 ok) or a negative SPK_E_*; on success *n = records,
+ * *width, *header_len = bytes before the first record. */
+int32_t spk_parse_vector_header(const spk_layout *L, const void *h_wire, uint64_t len,
+                                uint64_t *n, uint32_t *width, uint32_t *header_len);
+
 /* Host-side: header + count prefix of a VECTOR message of total_n records at
  * `width` into h_out (HOST memory, capacity cap). Returns its length, or a
  * negative SPK_E_*. (packer.hpp:100-139) */

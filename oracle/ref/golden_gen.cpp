@@ -102,6 +102,9 @@ static int cmd_kat() {
   kat_one<Group>(os, "Group", first);
   kat_one<std::vector<Group>>(os, "vector<Group>", first);
   kat_one<Deep>(os, "Deep", first);
+  kat_one<Vnt>(os, "Vnt", first);
+  kat_one<std::vector<Vnt>>(os, "vector<Vnt>", first);
+  kat_one<std::variant<int32_t, std::string>>(os, "variant<int32_t,string>", first);
   kat_one<std::vector<Deep>>(os, "vector<Deep>", first);
   kat_one<uint8_t, uint16_t, uint32_t, uint64_t, int8_t, int16_t, int64_t,
           bool, char, float, double>(os, "fundamentals", first);
@@ -181,6 +184,8 @@ static bool with_case(const Args &a, F &&f) {
     return f.template operator()<Tags>([=](Tags &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "group")
     return f.template operator()<Group>([=](Group &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "vnt")
+    return f.template operator()<Vnt>([=](Vnt &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "deep")
     return f.template operator()<Deep>([=](Deep &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "rect")  // C1: benchmark rect<int> default values

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <optional>
 #include <string>
+#include <variant>
 #include <vector>
 
 // ---- varint members: LEB128, zigzag for var_int* --
@@ -171,6 +172,14 @@ struct Group {  // vector<struct with a string>, then a string
 struct Deep {  // two nesting levels: vector<vector<string>>
   uint16_t k;
   std::vector<std::vector<std::string>> m;
+};
+
+// ---- std::variant members (SPK_OP_VARIANT) ----------------------------
+struct Vnt {
+  int32_t id;
+  std::variant<int32_t, double, std::string, Inner> v;
+  std::variant<std::monostate, std::vector<int32_t>> w;
+  std::vector<std::variant<int64_t, std::string>> list;
 };
 
 namespace spk_gold {
@@ -351,6 +360,30 @@ inline void fill(Deep &d, uint64_t seed, uint64_t i, uint32_t maxn) {
     const uint64_t h = elem_word(seed, i, j);
     d.m[j].resize((size_t)(h % 5));
     for (size_t q = 0; q < d.m[j].size(); ++q) d.m[j][q] = tag_chars(mix64(h + q + 1));
+  }
+}
+
+inline void fill(Vnt &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
+  o.id = (int32_t)(uint32_t)rnd(seed, i, 0);
+  switch (rnd(seed, i, 1) % 4) {
+    case 0: o.v = (int32_t)(uint32_t)rnd(seed, i, 2); break;
+    case 1: o.v = rd(rnd(seed, i, 3)); break;
+    case 2: o.v = make_chars(seed, i, maxlen); break;
+    default: o.v = Inner{(int32_t)(uint32_t)rnd(seed, i, 4), rf(rnd(seed, i, 5))};
+  }
+  if (rnd(seed, i, 6) & 1) {
+    std::vector<int32_t> v((size_t)(rnd(seed, i, 7) % (uint64_t)(maxlen + 1)));
+    for (size_t j = 0; j < v.size(); ++j) v[j] = (int32_t)(uint32_t)mix64(rnd(seed, i, 8) + j);
+    o.w = std::move(v);
+  }
+  const uint64_t n = rnd(seed, i, 9) % 5;
+  o.list.clear();
+  for (uint64_t j = 0; j < n; ++j) {
+    const uint64_t h = elem_word(seed, i, j);
+    if (h & 1)
+      o.list.emplace_back(tag_chars(h >> 1));
+    else
+      o.list.emplace_back((int64_t)(h >> 1));
   }
 }
 

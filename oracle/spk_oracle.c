@@ -64,16 +64,32 @@ static unsigned heap_of(const spk_layout *L, uint32_t i) {
   for (uint32_t j = 0; j < i; ++j) k += is_heap_op(L->ops[j].kind);
   return k;
 }
-static uint32_t end_of(const spk_layout *L, uint32_t i) { /* ARRAY at i -> its END */
-  unsigned depth = 0;
-  for (uint32_t j = i + 1; j < L->n_ops; ++j) {
-    if (L->ops[j].kind == SPK_OP_ARRAY) ++depth;
-    if (L->ops[j].kind == SPK_OP_END) {
-      if (!depth) return j;
-      --depth;
+static uint32_t end_of(const spk_layout *L, uint32_t i);
+/* the END closing the op group (element layout / alternative) starting at j */
+static uint32_t group_end(const spk_layout *L, uint32_t j) {
+  while (j < L->n_ops) {
+    const uint32_t k = L->ops[j].kind;
+    if (k == SPK_OP_ARRAY || k == SPK_OP_VARIANT) {
+      j = end_of(L, j) + 1;
+      continue;
     }
+    if (k == SPK_OP_END) return j;
+    ++j;
   }
   return L->n_ops;
+}
+/* ARRAY at i -> its END; VARIANT at i -> the END of its last alternative */
+static uint32_t end_of(const spk_layout *L, uint32_t i) {
+  if (L->ops[i].kind == SPK_OP_ARRAY) return group_end(L, i + 1);
+  uint32_t j = i + 1;
+  for (uint32_t a = 0; a < L->ops[i].size; ++a) j = group_end(L, j) + 1;
+  return j - 1;
+}
+/* first op of alternative a of the VARIANT at i */
+static uint32_t alt_start(const spk_layout *L, uint32_t i, uint32_t a) {
+  uint32_t j = i + 1;
+  while (a--) j = group_end(L, j) + 1;
+  return j;
 }
 static uint64_t rec_count(const uint8_t *rec, const spk_op *op) {
   uint32_t c;
@@ -160,6 +176,13 @@ static void ops_size(const spk_layout *L, uint32_t i0, uint32_t i1, const uint8_
       *cnts += 1;
       *bytes += c * op->size;
       if (c > *maxc) *maxc = c;
+    } else if (op->kind == SPK_OP_VARIANT) { /* index byte + the active alternative */
+      uint32_t idx;
+      memcpy(&idx, rec + op->rec_off, 4);
+      const uint32_t a0 = alt_start(L, i, idx);
+      *bytes += 1;
+      ops_size(L, a0, group_end(L, a0), rec, heaps, bytes, cnts, maxc);
+      i = end_of(L, i);
     } else if (op->kind == SPK_OP_ARRAY) {
       const uint32_t e = end_of(L, i);
       const uint64_t c = rec_count(rec, op);
@@ -200,6 +223,14 @@ static uint8_t *ops_write(const spk_layout *L, uint32_t i0, uint32_t i1, const u
         v >>= 7;
       }
       *p++ = (uint8_t)v;
+    }
+    else if (op->kind == SPK_OP_VARIANT) { /* packer.hpp:389-398 */
+      uint32_t idx;
+      memcpy(&idx, rec + op->rec_off, 4);
+      const uint32_t a0 = alt_start(L, i, idx);
+      *p++ = (uint8_t)idx;
+      p = ops_write(L, a0, group_end(L, a0), rec, heaps, w, p);
+      i = end_of(L, i);
     }
     else if (op->kind == SPK_OP_ARRAY) {
       const uint32_t e = end_of(L, i);
@@ -423,6 +454,19 @@ static int32_t ops_read(dctx_t *c, rd_t *r, unsigned w, uint32_t i0, uint32_t i1
       if (rec) vi_store(rec, op, v);
       continue;
     }
+    if (op->kind == SPK_OP_VARIANT) { /* unpacker.hpp:1278-1292 */
+      if (!rd_take(r, 1, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
+      const uint32_t idx = p[0];
+      if (idx >= op->size) return SPK_ERRC_INVALID_BUFFER;
+      if (rec) memcpy(rec + op->rec_off, &idx, 4);
+      const uint32_t a0 = alt_start(L, i, idx);
+      /* variant_construct_helper::run (unpacker.hpp:476-490) drops the
+         alternative's errc: the reader stays wherever its decode stopped and
+         the alternative keeps what was decoded */
+      (void)ops_read(c, r, w, a0, group_end(L, a0), rec);
+      i = end_of(L, i);
+      continue;
+    }
     const unsigned hk = heap_of(L, i);
     if (op->kind == SPK_OP_ARRAY) {
       const uint32_t e = end_of(L, i);
@@ -444,7 +488,15 @@ static int32_t ops_read(dctx_t *c, rd_t *r, unsigned w, uint32_t i0, uint32_t i1
       }
       for (uint64_t j = 0; j < cnt; ++j) {
         int32_t ec = ops_read(c, r, w, i + 1, e, el ? el + j * op->size : NULL);
-        if (ec) return ec;
+        if (ec) { /* emplace_back + decode (unpacker.hpp:1208-1226): the failing
+                     element stays in the container */
+          if (el) {
+            uint32_t c32 = (uint32_t)(j + 1);
+            memcpy(rec + op->rec_off, &c32, 4);
+            c->used[hk] -= cnt - (j + 1);
+          }
+          return ec;
+        }
       }
       i = e;
       continue;

@@ -31,7 +31,7 @@ SEED = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004,
         "pad": 0x5EED0005, "mixed": 0x5EED0006, "rect": 0, "rpcrect": 0x5EED0007,
         "person": 0x5EED0008, "ints": 0x5EED0009, "opt": 0x5EED000A, "optp": 0x5EED000B,
         "var": 0x5EED000C, "varp": 0x5EED000D, "tags": 0x5EED000E, "group": 0x5EED000F,
-        "deep": 0x5EED0010}
+        "deep": 0x5EED0010, "vnt": 0x5EED0011}
 
 # (case_mode, n, param, conf, keep_bin)
 SMALL = [
@@ -80,6 +80,10 @@ SMALL = [
     ("group_B", 100, 5, "default"), ("group_A", 3, 300, "default"),
     ("deep_A", 100, 4, "default"), ("deep_B", 100, 4, "default"),
     ("deep_A", 20, 300, "default"), ("deep_B", 30, 4, "nometa"),
+    # std::variant members (SPK_OP_VARIANT), also inside a vector element
+    ("vnt_A", 0, 6, "default"), ("vnt_A", 1, 6, "default"), ("vnt_A", 200, 6, "default"),
+    ("vnt_B", 200, 6, "default"), ("vnt_A", 40, 300, "default"),
+    ("vnt_A", 50, 6, "typeinfo"), ("vnt_B", 60, 6, "nometa"),
 ]
 MEDIUM = [  # digest only (wire > ~1 MB)
     ("rec64_A", 65535, 0, "default"), ("rec64_A", 65536, 0, "default"),
@@ -93,6 +97,7 @@ MEDIUM = [  # digest only (wire > ~1 MB)
     ("var_B", 70000, 48, "default"),
     ("tags_A", 70000, 6, "default"), ("tags_B", 20000, 6, "default"),
     ("group_A", 20000, 5, "default"), ("deep_A", 20000, 4, "default"),
+    ("vnt_A", 30000, 8, "default"), ("vnt_B", 20000, 8, "default"),
 ]
 BIG = [  # BASELINE.json full-size configs (digest only)
     ("rec64_A", 100_000_000, 0, "default"),
@@ -205,6 +210,7 @@ ERR_BASES = [
     ("var_A", 6, 10, "default"), ("varp_B", 1, 0, "default"), ("varp_A", 4, 0, "default"),
     ("tags_A", 5, 4, "default"), ("tags_B", 1, 6, "default"), ("group_A", 4, 3, "default"),
     ("group_B", 1, 4, "default"), ("deep_A", 4, 3, "default"), ("deep_B", 1, 4, "default"),
+    ("vnt_A", 6, 4, "default"), ("vnt_B", 1, 4, "default"), ("vnt_B", 1, 40, "default"),
     # width-8 container lengths (metainfo 0x18): no reference encoder writes
     # them below 2^32 elements, but every decoder must read them
     # (unpacker.hpp:572-619); the base is our width-8 re-encoding, decoded by

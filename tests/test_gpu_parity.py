@@ -170,7 +170,7 @@ RANDOM = [("recs", 1, 300), ("recs", 257, 5), ("recs", 5000, 48), ("recs", 20000
           ("opt", 5000, 48), ("opt", 300, 400), ("optp", 20000, 0),
           ("var", 5000, 48), ("var", 300, 400), ("var", 20000, 4), ("varp", 20000, 0),
           ("tags", 3000, 6), ("tags", 200, 300), ("group", 500, 5), ("group", 3, 2000),
-          ("deep", 700, 4)]
+          ("deep", 700, 4), ("vnt", 3000, 8), ("vnt", 100, 400)]
 
 
 @pytest.mark.parametrize("case,n,param", RANDOM)
@@ -228,7 +228,8 @@ def _irregular_messages(cd, case, n, seed, param):
                                           ("ints", 200, 60), ("opt", 500, 40),
                                           ("optp", 400, 0), ("var", 500, 40),
                                           ("varp", 400, 0), ("tags", 300, 6),
-                                          ("group", 200, 4), ("deep", 200, 3)])
+                                          ("group", 200, 4), ("deep", 200, 3),
+                                          ("vnt", 300, 6)])
 @pytest.mark.parametrize("cap_frac", [1.0, 0.6])
 def test_messages_irregular_vs_oracle(case, n, param, cap_frac):
     """Mode B decode of non-canonical message batches: per-message errc,
@@ -516,3 +517,67 @@ def test_varint_edge_values_gpu():
     res, back, _ = cd.deserialize(out, C.SPK_MODE_VECTOR)
     assert res.errc == 0 and res.count == len(msgs)
     assert back.recs.cpu().numpy().tobytes() == recs.tobytes()
+
+
+@pytest.mark.parametrize("case,n,param", [("rec64", 5000, 0), ("recs", 4000, 48),
+                                          ("outer", 3000, 16), ("var", 3000, 16),
+                                          ("tags", 2000, 6), ("opt", 2000, 20),
+                                          ("vnt", 2000, 6)])
+def test_decode_body_chunks(case, n, param):
+    """spk_parse_vector_header (host) + spk_decode_body: the message body cut
+    at record boundaries into chunks, each decoded on its own, equals the
+    records (the pipelined host path / sharded decode building block)."""
+    cd = codec_for(case)
+    L, recs, heaps = synth.make_batch(case, n, 0xB0D1 + n, param)
+    exp, _, _ = H.oracle_encode(cd.L, C.SPK_MODE_VECTOR, recs, heaps)
+    e, nn, w, hl = cd.parse_vector_header(exp[:600])
+    assert e == 0 and nn == n
+    # record boundaries from the oracle's own per-record encodings
+    cuts = [0, n // 3, n // 3 + 1, n]
+    body = wire_dev(exp[hl:])
+    for a, b in zip(cuts, cuts[1:]):
+        ra = recs[a:b].copy()
+        sub_heaps = []
+        if not cd.L.dev.trivial and not any("[]" in sp.path for sp in cd.L.dev.spans):
+            for k, sp in enumerate(cd.L.dev.spans):
+                cnt = ra[sp.path + ".n"].astype(np.int64)
+                off = ra[sp.path + ".off"].astype(np.int64)
+                parts = [heaps[k][o * sp.elem.size:(o + c) * sp.elem.size]
+                         for o, c in zip(off, cnt)]
+                sub_heaps.append(np.concatenate(parts) if parts else np.zeros(0, np.uint8))
+                ra[sp.path + ".off"] = np.concatenate([[0], np.cumsum(cnt)[:-1]]) if len(cnt) else []
+        else:
+            sub_heaps = heaps
+        # the chunk's bytes: encode_body of its records at width w (oracle)
+        import ctypes as ct
+        o = C.load_oracle()
+        hp = (ct.c_void_p * max(len(sub_heaps), 1))(*[h.ctypes.data if h.size else 0
+                                                       for h in sub_heaps])
+        buf = np.zeros(len(exp) + 16, np.uint8)
+        wr = ct.c_uint64()
+        assert o.spko_encode_body(cd.L.ptr, b - a, H._ptr(ra), hp, w, H._ptr(buf), buf.size,
+                                  ct.byref(wr)) == 0
+        chunk = wire_dev(buf[:wr.value].tobytes())
+        caps = [max(c, 1) for c in S.heap_caps_for_wire(cd.L.dev, wr.value, b - a + 1)]
+        out = cd.alloc_batch(b - a + 1, caps)
+        cd.deserialize_body(out, chunk, w, b - a)
+        r = cd.result()
+        assert r.errc == 0 and r.count == b - a and r.consumed == wr.value, (a, b, r.errc)
+        if cd.L.dev.trivial or not any("[]" in sp.path for sp in cd.L.dev.spans):
+            assert out.recs[:b - a].cpu().numpy().tobytes() == \
+                np.ascontiguousarray(ra).view(np.uint8).tobytes()
+        # and back: the decoded chunk re-encodes to the same body bytes
+        rb = SP.RecordBatch(cd.L, out.recs[:b - a], out.heaps)
+        ws = cd.workspace(C.SPK_MODE_VECTOR, b - a)
+        dst = torch.zeros(wr.value + 16, dtype=torch.uint8, device="cuda")
+        assert cd.lib.spk_encode_body(cd.L.ptr, b - a, SP._p(rb.recs), cd._heap_ptrs(rb.heaps),
+                                      w, SP._p(dst), dst.numel(), SP._p(ws), ws.numel(),
+                                      None) == 0
+        assert dst[:wr.value].cpu().numpy().tobytes() == buf[:wr.value].tobytes()
+    # a body too short for n records: no_buffer_space
+    out = cd.alloc_batch(n + 1, [max(c, 1) for c in S.heap_caps_for_wire(cd.L.dev, len(exp), n + 1)])
+    cd.deserialize_body(out, body[:len(exp) - hl - 3], w, n)
+    assert cd.result().errc == C.ERRC_NO_BUFFER_SPACE
+    cd.deserialize_body(out, body, w, n)
+    r = cd.result()
+    assert r.errc == 0 and r.count == n and r.consumed == len(exp) - hl

@@ -47,7 +47,12 @@ def _worker(rank, world, port, case, n, param, q):
         # this rank's shard, re-based heaps (a real rank owns its own heap)
         sub = recs[lo:hi].copy()
         sh = []
+        if any("[]" in sp.path for sp in L.dev.spans):
+            # ARRAY layouts: the shard keeps the global heaps (offsets stay valid)
+            sh = [np.ascontiguousarray(h).view(np.uint8) for h in heaps]
         for k, sp in enumerate(L.dev.spans):
+            if sh and len(sh) == len(L.dev.spans):
+                break
             cnt = sub[sp.path + ".n"].astype(np.int64)
             off = sub[sp.path + ".off"].astype(np.int64)
             parts = [heaps[k][o * sp.elem.size:(o + c) * sp.elem.size] for o, c in zip(off, cnt)]
@@ -59,8 +64,9 @@ def _worker(rank, world, port, case, n, param, q):
         hp = (ct.c_void_p * max(len(sh), 1))(*[h.ctypes.data if h.size else 0 for h in sh])
         assert o.spko_plan(L.ptr, C.SPK_MODE_VECTOR, len(sub), H._ptr(sub), hp,
                            ct.byref(plan)) == 0
-        sp = PAR.agree_shard_plan(len(sub), plan.max_count, plan.var_bytes, L.n_cont,
-                                  lambda gn, w: _oracle_header(L, gn, w))
+        sp = PAR.agree_shard_plan(len(sub), plan.max_count, plan.var_bytes, 0,
+                                  lambda gn, w: _oracle_header(L, gn, w),
+                                  local_fields=PAR.count_fields(plan))
         body = np.zeros(max(sp.body_bytes[rank], 1), np.uint8)
         wr = ct.c_uint64()
         assert o.spko_encode_body(L.ptr, len(sub), H._ptr(sub), hp, sp.width, H._ptr(body),
@@ -79,7 +85,9 @@ def _worker(rank, world, port, case, n, param, q):
 @pytest.mark.parametrize("case,n,param", [("rec64", 1000, 0), ("recs", 3000, 48),
                                           ("recs", 300, 400), ("outer", 700, 16),
                                           ("mixed", 200, 300), ("opt", 300, 40),
-                                          ("var", 300, 40), ("varp", 200, 0)])
+                                          ("var", 300, 40), ("varp", 200, 0),
+                                          ("tags", 300, 6), ("group", 100, 4),
+                                          ("deep", 100, 3), ("vnt", 200, 6)])
 def test_sharded_vector_message_gloo(case, n, param):
     world = 2
     ctx = mp.get_context("spawn")

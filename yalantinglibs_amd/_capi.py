@@ -38,6 +38,7 @@ SPK_OP_OPTION = 3
 SPK_OP_VARINT = 4
 SPK_OP_ARRAY = 5
 SPK_OP_END = 6
+SPK_OP_VARIANT = 7
 SPK_MAX_DEPTH = 4
 SPK_VARINT_ZIGZAG = 1
 SPK_MAX_VARINTS = 16
@@ -109,6 +110,7 @@ CODEC_SYMBOLS = ["spk_abi_version", "spk_errc_message", "spk_layout_check",
                  "spk_workspace_bytes", "spk_plan", "spk_plan_ex", "spk_encode", "spk_decode",
                  "spk_synth", "spk_synth_counts", "spk_encode_body",
                  "spk_vector_header", "spk_encode_framed", "spk_decode_framed",
+                 "spk_decode_body", "spk_parse_vector_header",
                  # runtime helpers (front ends without HIP headers)
                  "spk_device_alloc", "spk_device_free", "spk_host_alloc_pinned",
                  "spk_host_free_pinned", "spk_copy_async", "spk_stream_create",
@@ -143,6 +145,11 @@ def _bind_codec(lib):
                                     ct.c_size_t, P]
     lib.spk_vector_header.argtypes = [PL, U64, ct.c_uint32, ct.POINTER(ct.c_uint8),
                                       ct.c_uint32]
+    lib.spk_decode_body.argtypes = [PL, P, U64, ct.c_uint32, U64, P, U64, ct.POINTER(P),
+                                    ct.POINTER(U64), P, P, ct.c_size_t, P]
+    lib.spk_parse_vector_header.argtypes = [PL, P, U64, ct.POINTER(U64),
+                                            ct.POINTER(ct.c_uint32), ct.POINTER(ct.c_uint32)]
+    lib.spk_parse_vector_header.restype = ct.c_int32
     lib.spk_encode_framed.argtypes = [PL, U64, P, ct.POINTER(P), P, ct.POINTER(spk_frame),
                                       P, U64, P, P, ct.c_size_t, P]
     lib.spk_decode_framed.argtypes = [PL, P, U64, P, U64, ct.c_uint32, P, U64,

@@ -103,12 +103,29 @@ int spk_layout_check(const spk_layout *L) {
     return SPK_OK;
   }
   uint32_t spans = 0, conts = 0, vars = 0;
-  // record strides of the open ARRAY element layouts (0: the top record)
+  // open ARRAY element layouts / VARIANT alternatives (level 0: the top
+  // record): the record stride, ops seen, alternatives still to close
   uint32_t stride[SPK_MAX_DEPTH + 1] = {L->rec_stride}, depth = 0, nops[SPK_MAX_DEPTH + 1] = {0};
+  uint32_t alts[SPK_MAX_DEPTH + 1] = {0};
   for (uint32_t i = 0; i < L->n_ops; ++i) {
     const spk_op &o = L->ops[i];
     const uint32_t rs = stride[depth];
     ++nops[depth];
+    if (o.kind == SPK_OP_VARIANT) {  // u32 index in this record; groups follow
+      if (o.size == 0 || o.size > 255 || o.aux || o.rec_off % 4 || o.rec_off + 4 > rs ||
+          depth == SPK_MAX_DEPTH)
+        return SPK_E_LAYOUT;
+      ++vars;  // a variable-length member
+      stride[++depth] = rs;
+      nops[depth] = 0;
+      alts[depth] = o.size;
+      continue;
+    }
+    if (o.kind == SPK_OP_END && depth && alts[depth]) {  // closes one alternative
+      nops[depth] = 0;
+      if (--alts[depth] == 0) --depth;
+      continue;
+    }
     if (o.kind == SPK_OP_COPY) {
       if (o.size == 0 || (uint64_t)o.rec_off + o.size > rs) return SPK_E_LAYOUT;
     } else if (o.kind == SPK_OP_SPAN || o.kind == SPK_OP_OPTION || o.kind == SPK_OP_ARRAY) {
@@ -120,6 +137,7 @@ int spk_layout_check(const spk_layout *L) {
         if (o.size % 8 || depth == SPK_MAX_DEPTH) return SPK_E_LAYOUT;
         stride[++depth] = o.size;
         nops[depth] = 0;
+        alts[depth] = 0;
       }
     } else if (o.kind == SPK_OP_END) {
       --nops[depth];
@@ -134,7 +152,7 @@ int spk_layout_check(const spk_layout *L) {
       return SPK_E_LAYOUT;
     }
   }
-  if (depth) return SPK_E_LAYOUT;  // an ARRAY without its END
+  if (depth) return SPK_E_LAYOUT;  // an ARRAY / VARIANT without its END(s)
   // a non-trivial record has a variable-length member: a span/option or a varint
   if ((spans == 0 && vars == 0) || spans > SPK_MAX_SPANS || vars > SPK_MAX_VARINTS ||
       L->rec_stride % 8)
@@ -149,7 +167,7 @@ size_t spk_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t w
   // trivial: per-message payload positions (fallback gather) or 2 words per
   // decode block (<= 4096 blocks), whichever is larger
   if (is_trivial(L)) return kWsScratch + ((n + 1) * 8 > 65536 ? (n + 1) * 8 : 65536) + 256;
-  if (layout_has_array(L)) return nested_workspace_bytes(L, mode, n, wire_len);
+  if (layout_nested(L)) return nested_workspace_bytes(L, mode, n, wire_len);
   return var_workspace_bytes(L, mode, n, wire_len);
 }
 
@@ -184,7 +202,7 @@ int spk_plan_ex(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
   hipStream_t s = (hipStream_t)stream;
   if (is_trivial(L)) return hip_rc(launch_fixed_plan(L, mode, n, d_plan, d_ws, s));
   if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
-  if (layout_has_array(L)) {  // the sizes live in the element records
+  if (layout_nested(L)) {  // the sizes live in the element records
     if ((rc = heaps_check(L, n, d_heaps))) return rc;
     return hip_rc(launch_nested_plan(L, mode, n, d_recs, d_heaps, d_plan, d_ws, s));
   }
@@ -193,7 +211,7 @@ int spk_plan_ex(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
 
 int spk_plan(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
              spk_plan_t *d_plan, void *d_ws, size_t ws_bytes, void *stream) {
-  if (L && spk_layout_check(L) == SPK_OK && layout_has_array(L) && n) return SPK_E_ARG;
+  if (L && spk_layout_check(L) == SPK_OK && layout_nested(L) && n) return SPK_E_ARG;
   return spk_plan_ex(L, mode, n, d_recs, nullptr, d_plan, d_ws, ws_bytes, stream);
 }
 
@@ -231,7 +249,7 @@ static int encode_impl(const spk_layout *L, int mode, uint64_t n, const void *d_
   }
   if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
   if ((rc = heaps_check(L, n, d_heaps))) return rc;
-  if (layout_has_array(L))
+  if (layout_nested(L))
     return hip_rc(launch_nested_encode(L, mode, n, d_recs, d_heaps, d_out, d_msg_offsets, F, 0,
                                        d_ws, s));
   return hip_rc(launch_var_encode(L, mode, n, d_recs, d_heaps, d_plan, d_out, out_cap,
@@ -286,7 +304,7 @@ static int decode_impl(const spk_layout *L, int mode, const void *d_wire, uint64
              L->ops[i].kind == SPK_OP_ARRAY;
   if (spans && (!d_heaps || !heap_caps)) return SPK_E_ARG;
   if (mode == SPK_MODE_MESSAGES && n_msgs && !d_msg_offsets) return SPK_E_ARG;
-  if (layout_has_array(L)) {
+  if (layout_nested(L)) {
     for (uint32_t k = 0; k < spans; ++k)
       if (!d_heaps[k] || (uintptr_t)d_heaps[k] % 8) return SPK_E_ARG;
     return hip_rc(launch_nested_decode(L, mode, d_wire, wire_len, d_msg_offsets, n_msgs, prefix,
@@ -334,11 +352,59 @@ int spk_encode_body(const spk_layout *L, uint64_t n, const void *d_recs,
   }
   if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
   if ((rc = heaps_check(L, n, d_heaps))) return rc;
-  if (layout_has_array(L))
+  if (layout_nested(L))
     return hip_rc(launch_nested_encode(L, SPK_MODE_VECTOR, n, d_recs, d_heaps, d_out, nullptr,
                                        nullptr, width, d_ws, s));
   return hip_rc(launch_var_encode_body(L, n, d_recs, d_heaps, width, d_out, out_cap, d_ws,
                                        ws_bytes, s));
+}
+
+int spk_decode_body(const spk_layout *L, const void *d_body, uint64_t body_len, uint32_t width,
+                    uint64_t n, void *d_recs, uint64_t rec_cap, void *const *d_heaps,
+                    const uint64_t *heap_caps, spk_dresult_t *d_res, void *d_ws,
+                    size_t ws_bytes, void *stream) {
+  int rc = spk_layout_check(L);
+  if (rc) return rc;
+  if (width != 1 && width != 2 && width != 4 && width != 8) return SPK_E_ARG;
+  if (!d_res || !d_ws || (body_len && !d_body) || (rec_cap && !d_recs)) return SPK_E_ARG;
+  if (ws_bytes < spk_workspace_bytes(L, SPK_MODE_VECTOR, rec_cap, body_len))
+    return SPK_E_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  if (is_trivial(L))
+    return hip_rc(launch_fixed_decode_vector(L, d_body, body_len, d_recs, rec_cap, d_res, d_ws,
+                                             s, width, n));
+  if (d_recs && (uintptr_t)d_recs % 8) return SPK_E_ARG;
+  uint32_t spans = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i)
+    spans += L->ops[i].kind == SPK_OP_SPAN || L->ops[i].kind == SPK_OP_OPTION ||
+             L->ops[i].kind == SPK_OP_ARRAY;
+  if (spans && (!d_heaps || !heap_caps)) return SPK_E_ARG;
+  if (layout_nested(L)) {
+    for (uint32_t k = 0; k < spans; ++k)
+      if (!d_heaps[k] || (uintptr_t)d_heaps[k] % 8) return SPK_E_ARG;
+    return hip_rc(launch_nested_decode(L, SPK_MODE_VECTOR, d_body, body_len, nullptr, 0, 0,
+                                       d_recs, rec_cap, d_heaps, heap_caps, d_res, nullptr, d_ws,
+                                       s, width, n));
+  }
+  return hip_rc(launch_var_decode(L, SPK_MODE_VECTOR, d_body, body_len, nullptr, 0, 0, d_recs,
+                                  rec_cap, d_heaps, heap_caps, d_res, nullptr, d_ws, ws_bytes, s,
+                                  width, n));
+}
+
+int32_t spk_parse_vector_header(const spk_layout *L, const void *h_wire, uint64_t len,
+                                uint64_t *n, uint32_t *width, uint32_t *header_len) {
+  if (spk_layout_check(L) != SPK_OK) return SPK_E_LAYOUT;
+  if ((len && !h_wire) || !n || !width || !header_len) return SPK_E_ARG;
+  const uint8_t *p = (const uint8_t *)h_wire;
+  uint64_t pos, dl;
+  uint32_t w;
+  int32_t e = parse_hdr(L->fmt_vector, p, len, &pos, &w, &dl);
+  if (e) return e;
+  if (len < pos + w) return SPK_ERRC_NO_BUFFER_SPACE;
+  *n = ld_le(p + pos, w);
+  *width = w;
+  *header_len = (uint32_t)(pos + w);
+  return SPK_ERRC_OK;
 }
 
 int spk_vector_header(const spk_layout *L, uint64_t total_n, uint32_t width, uint8_t *h_out,

@@ -185,21 +185,23 @@ struct FixedDecArgs {
   uint64_t wire_len;
   uint64_t rec_cap;
   uint32_t stride;
+  uint32_t body_w;   // spk_decode_body: no header, body_n records at this width
+  uint64_t body_n;
 };
 
 __global__ void fixed_decode_hdr_kernel(FixedDecArgs a, const uint8_t *wire,
                                         CopyJob *job, spk_dresult_t *res) {
   if (threadIdx.x != 0) return;
-  uint64_t pos, data_len;
-  uint32_t w;
-  int32_t e = parse_hdr(a.fmt, wire, a.wire_len, &pos, &w, &data_len);
+  uint64_t pos = 0, data_len = 0;
+  uint32_t w = a.body_w;
+  int32_t e = a.body_w ? SPK_ERRC_OK : parse_hdr(a.fmt, wire, a.wire_len, &pos, &w, &data_len);
   uint64_t n = 0;
   if (!e) {
-    if (a.wire_len < pos + w) {
+    if (!a.body_w && a.wire_len < pos + w) {
       e = SPK_ERRC_NO_BUFFER_SPACE;
     } else {
-      n = ld_le(wire + pos, w);
-      pos += w;
+      n = a.body_w ? a.body_n : ld_le(wire + pos, w);
+      pos += a.body_w ? 0 : w;
       // overflow guard + check(mem_sz) (unpacker.hpp:1128-1149)
       if (n > ~0ull / a.stride || a.wire_len - pos < n * a.stride)
         e = SPK_ERRC_NO_BUFFER_SPACE;
@@ -227,8 +229,11 @@ __global__ void fixed_decode_hdr_kernel(FixedDecArgs a, const uint8_t *wire,
 hipError_t launch_fixed_decode_vector(const spk_layout *L, const void *d_wire,
                                          uint64_t wire_len, void *d_recs,
                                          uint64_t rec_cap, spk_dresult_t *d_res,
-                                         void *d_ws, hipStream_t s) {
+                                         void *d_ws, hipStream_t s, uint32_t body_w,
+                                         uint64_t body_n) {
   FixedDecArgs a;
+  a.body_w = body_w;
+  a.body_n = body_n;
   a.fmt = L->fmt_vector;
   a.wire_len = wire_len;
   a.rec_cap = rec_cap;

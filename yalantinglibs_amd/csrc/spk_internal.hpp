@@ -110,7 +110,7 @@ struct Ctl {
   uint32_t pad;
 };
 
-__device__ __forceinline__ uint64_t ld_le(const uint8_t *p, uint32_t w) {
+__host__ __device__ __forceinline__ uint64_t ld_le(const uint8_t *p, uint32_t w) {
   uint64_t v = 0;
   for (uint32_t i = 0; i < w; ++i) v |= (uint64_t)p[i] << (8 * i);
   return v;
@@ -118,7 +118,7 @@ __device__ __forceinline__ uint64_t ld_le(const uint8_t *p, uint32_t w) {
 
 // Parse a message header at p[0..len). Returns errc; sets *pos to the first
 // payload byte, *w to the width, *data_len to the compatible length field.
-__device__ inline int32_t parse_hdr(const spk_msgfmt &f, const uint8_t *p, uint64_t len,
+__host__ __device__ inline int32_t parse_hdr(const spk_msgfmt &f, const uint8_t *p, uint64_t len,
                              uint64_t *pos, uint32_t *w, uint64_t *data_len) {
   *w = 1;
   *data_len = 0;
@@ -183,7 +183,7 @@ void trace_mark(const char *name, hipStream_t s, int end);
 // ---- launch wrappers implemented in the kernel TUs -----------------------
 namespace spk {
 // spk_nested.hip: layouts with SPK_OP_ARRAY
-bool layout_has_array(const spk_layout *L);
+bool layout_nested(const spk_layout *L);
 size_t nested_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len);
 hipError_t launch_nested_plan(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
                               const void *const *d_heaps, spk_plan_t *d_plan, void *d_ws,
@@ -197,7 +197,7 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
                                 uint64_t n_msgs, uint32_t prefix, void *d_recs, uint64_t rec_cap,
                                 void *const *d_heaps, const uint64_t *heap_caps,
                                 spk_dresult_t *d_res, int32_t *d_errc, void *d_ws,
-                                hipStream_t s);
+                                hipStream_t s, uint32_t body_w = 0, uint64_t body_n = 0);
 // spk_fixed.hip
 hipError_t launch_fixed_plan(const spk_layout *L, int mode, uint64_t n,
                              spk_plan_t *d_plan, void *d_ws, hipStream_t s);
@@ -208,10 +208,13 @@ hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
                                         const void *d_recs, void *d_out,
                                         uint64_t *d_offsets, const spk_frame *F,
                                         hipStream_t s);
+// body_w != 0: d_wire is a message BODY of body_n records at width body_w
+// (no header / count: spk_decode_body)
 hipError_t launch_fixed_decode_vector(const spk_layout *L, const void *d_wire,
                                       uint64_t wire_len, void *d_recs,
                                       uint64_t rec_cap, spk_dresult_t *d_res,
-                                      void *d_ws, hipStream_t s);
+                                      void *d_ws, hipStream_t s, uint32_t body_w = 0,
+                                      uint64_t body_n = 0);
 hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
                                         uint64_t wire_len,
                                         const uint64_t *d_offsets, uint64_t n,
@@ -238,5 +241,5 @@ hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
                              uint64_t n_msgs, uint32_t prefix, void *d_recs, uint64_t rec_cap,
                              void *const *d_heaps, const uint64_t *heap_caps,
                              spk_dresult_t *d_res, int32_t *d_errc, void *d_ws,
-                             size_t ws_bytes, hipStream_t s);
+                             size_t ws_bytes, hipStream_t s, uint32_t body_w = 0, uint64_t body_n = 0);
 }  // namespace spk

@@ -24,13 +24,14 @@ namespace spk {
 struct NLayout {
   spk_op ops[SPK_MAX_OPS];
   uint8_t heap[SPK_MAX_OPS];  // heap index of a SPAN / OPTION / ARRAY op
-  uint8_t end[SPK_MAX_OPS];   // ARRAY: index of its END
+  uint8_t end[SPK_MAX_OPS];   // ARRAY: its END; VARIANT: the END of its last alternative
   uint32_t n_ops, stride, n_heaps, pad_;
 };
 
-bool layout_has_array(const spk_layout *L) {
+// layouts the interpreter runs: an ARRAY (element layouts) or a VARIANT
+bool layout_nested(const spk_layout *L) {
   for (uint32_t i = 0; i < L->n_ops; ++i)
-    if (L->ops[i].kind == SPK_OP_ARRAY) return true;
+    if (L->ops[i].kind == SPK_OP_ARRAY || L->ops[i].kind == SPK_OP_VARIANT) return true;
   return false;
 }
 
@@ -38,13 +39,17 @@ static NLayout make_nlayout(const spk_layout *L) {
   NLayout N = {};
   N.n_ops = L->n_ops;
   N.stride = L->rec_stride;
-  uint32_t stack[SPK_MAX_DEPTH + 1], d = 0, h = 0;
+  // open ARRAYs / VARIANTs and the alternatives a VARIANT still has to close
+  uint32_t stack[SPK_MAX_DEPTH + 1], left[SPK_MAX_DEPTH + 1], d = 0, h = 0;
   for (uint32_t i = 0; i < L->n_ops; ++i) {
     N.ops[i] = L->ops[i];
     const uint32_t k = L->ops[i].kind;
     if (k == SPK_OP_SPAN || k == SPK_OP_OPTION || k == SPK_OP_ARRAY) N.heap[i] = (uint8_t)h++;
-    if (k == SPK_OP_ARRAY) stack[d++] = i;
-    if (k == SPK_OP_END && d) N.end[stack[--d]] = (uint8_t)i;
+    if (k == SPK_OP_ARRAY || k == SPK_OP_VARIANT) {
+      stack[d] = i;
+      left[d++] = k == SPK_OP_VARIANT ? L->ops[i].size : 1;
+    }
+    if (k == SPK_OP_END && d && --left[d - 1] == 0) N.end[stack[--d]] = (uint8_t)i;
   }
   N.n_heaps = h;
   return N;
@@ -80,11 +85,39 @@ __device__ __forceinline__ void n_copy(uint8_t *d, const uint8_t *s, uint64_t n)
 
 // one open ARRAY on the interpreter's stack
 struct NFrame {
-  uint32_t aop, pend;      // the ARRAY op; the op range end to resume
-  uint64_t j, cnt;         // element index, element count
+  uint32_t aop, pend;      // the ARRAY / VARIANT op; the op range end to resume
+  uint64_t j, cnt;         // element index, element count (a VARIANT: 0 of 1)
   const uint8_t *el;       // element records (encode) / output slots (decode)
   const uint8_t *prec;     // record to resume
+  uint32_t first, ret;     // first op of an element / alternative; op to resume at
 };
+
+// first op of alternative `a` of the VARIANT at i (groups closed by END)
+__device__ __forceinline__ uint32_t n_alt_start(const NLayout &N, uint32_t i, uint32_t a) {
+  uint32_t j = i + 1;
+  while (a) {
+    const uint32_t k = N.ops[j].kind;
+    if (k == SPK_OP_ARRAY || k == SPK_OP_VARIANT) {
+      j = N.end[j] + 1;  // skip a nested one whole
+      continue;
+    }
+    if (k == SPK_OP_END) --a;
+    ++j;
+  }
+  return j;
+}
+// the END that closes the alternative starting at j
+__device__ __forceinline__ uint32_t n_alt_end(const NLayout &N, uint32_t j) {
+  for (;;) {
+    const uint32_t k = N.ops[j].kind;
+    if (k == SPK_OP_ARRAY || k == SPK_OP_VARIANT) {
+      j = N.end[j] + 1;
+      continue;
+    }
+    if (k == SPK_OP_END) return j;
+    ++j;
+  }
+}
 
 // ---- encode: size of one record -----------------------------------------------
 struct NSize {
@@ -101,10 +134,10 @@ __device__ NSize n_size(const NLayout &N, const uint8_t *rec, const uint8_t *con
       NFrame &f = st[d - 1];
       if (++f.j < f.cnt) {
         r = f.el + f.j * N.ops[f.aop].size;
-        i = f.aop + 1;
+        i = f.first;
         continue;
       }
-      i = N.end[f.aop] + 1;
+      i = f.ret;
       iend = f.pend;
       r = f.prec;
       --d;
@@ -119,6 +152,15 @@ __device__ NSize n_size(const NLayout &N, const uint8_t *rec, const uint8_t *con
       ++i;
     } else {
       const uint64_t c = *reinterpret_cast<const uint32_t *>(r + op.rec_off);
+      if (op.kind == SPK_OP_VARIANT) {  // [index:1] + the active alternative
+        s.bytes += 1;
+        const uint32_t a0 = n_alt_start(N, i, (uint32_t)c);
+        st[d] = NFrame{i, iend, 0, 1, r, r, a0, (uint32_t)N.end[i] + 1u};
+        ++d;
+        iend = n_alt_end(N, a0);
+        i = a0;
+        continue;
+      }
       if (op.kind == SPK_OP_OPTION) {
         s.bytes += 1 + (c ? op.size : 0);
         ++i;
@@ -133,7 +175,7 @@ __device__ NSize n_size(const NLayout &N, const uint8_t *rec, const uint8_t *con
         i = N.end[i] + 1;
       } else {
         const uint64_t off = *reinterpret_cast<const uint64_t *>(r + op.aux);
-        st[d] = NFrame{i, iend, 0, c, heaps[N.heap[i]] + off * op.size, r};
+        st[d] = NFrame{i, iend, 0, c, heaps[N.heap[i]] + off * op.size, r, i + 1, (uint32_t)N.end[i] + 1u};
         r = st[d].el;
         ++d;
         iend = N.end[i];
@@ -156,10 +198,10 @@ __device__ uint8_t *n_write(const NLayout &N, const uint8_t *rec, const uint8_t 
       NFrame &f = st[d - 1];
       if (++f.j < f.cnt) {
         r = f.el + f.j * N.ops[f.aop].size;
-        i = f.aop + 1;
+        i = f.first;
         continue;
       }
-      i = N.end[f.aop] + 1;
+      i = f.ret;
       iend = f.pend;
       r = f.prec;
       --d;
@@ -180,6 +222,15 @@ __device__ uint8_t *n_write(const NLayout &N, const uint8_t *rec, const uint8_t 
       ++i;
     } else {
       const uint64_t c = *reinterpret_cast<const uint32_t *>(r + op.rec_off);
+      if (op.kind == SPK_OP_VARIANT) {
+        *p++ = (uint8_t)c;
+        const uint32_t a0 = n_alt_start(N, i, (uint32_t)c);
+        st[d] = NFrame{i, iend, 0, 1, r, r, a0, (uint32_t)N.end[i] + 1u};
+        ++d;
+        iend = n_alt_end(N, a0);
+        i = a0;
+        continue;
+      }
       const uint64_t off = *reinterpret_cast<const uint64_t *>(r + op.aux);
       if (op.kind == SPK_OP_OPTION) {
         *p++ = c ? 1 : 0;
@@ -199,7 +250,7 @@ __device__ uint8_t *n_write(const NLayout &N, const uint8_t *rec, const uint8_t 
       } else if (!c) {
         i = N.end[i] + 1;
       } else {
-        st[d] = NFrame{i, iend, 0, c, heaps[N.heap[i]] + off * op.size, r};
+        st[d] = NFrame{i, iend, 0, c, heaps[N.heap[i]] + off * op.size, r, i + 1, (uint32_t)N.end[i] + 1u};
         r = st[d].el;
         ++d;
         iend = N.end[i];
@@ -223,16 +274,42 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
   NFrame st[SPK_MAX_DEPTH];
   uint32_t d = 0, i = 0, iend = N.n_ops;
   uint8_t *r = rec;
+  int32_t ec = SPK_ERRC_OK;
   for (;;) {
+    if (ec) {
+      // unwind to the innermost VARIANT: variant_construct_helper::run
+      // (unpacker.hpp:476-490) drops its alternative's errc; an ARRAY keeps
+      // its failing element (emplace_back, unpacker.hpp:1208-1226)
+      bool dropped = false;
+      while (d) {
+        NFrame &f = st[d - 1];
+        const spk_op &fo = N.ops[f.aop];
+        if (fo.kind == SPK_OP_VARIANT) {
+          i = f.ret;
+          iend = f.pend;
+          r = const_cast<uint8_t *>(f.prec);
+          --d;
+          dropped = true;
+          break;
+        }
+        used[N.heap[f.aop]] -= f.cnt - (f.j + 1);
+        if (f.el) *reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(f.prec) + fo.rec_off) =
+            (uint32_t)(f.j + 1);
+        --d;
+      }
+      if (!dropped) return ec;
+      ec = SPK_ERRC_OK;
+      continue;
+    }
     if (i >= iend) {
       if (!d) break;
       NFrame &f = st[d - 1];
       if (++f.j < f.cnt) {
         r = f.el ? const_cast<uint8_t *>(f.el) + f.j * N.ops[f.aop].size : nullptr;
-        i = f.aop + 1;
+        i = f.first;
         continue;
       }
-      i = N.end[f.aop] + 1;
+      i = f.ret;
       iend = f.pend;
       r = const_cast<uint8_t *>(f.prec);
       --d;
@@ -240,7 +317,7 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
     }
     const spk_op op = N.ops[i];
     if (op.kind == SPK_OP_COPY) {
-      if (end - pos < op.size) return SPK_ERRC_NO_BUFFER_SPACE;
+      if (end - pos < op.size) { ec = SPK_ERRC_NO_BUFFER_SPACE; continue; }
       if (r) n_copy(r + op.rec_off, wire + pos, op.size);
       pos += op.size;
       ++i;
@@ -248,13 +325,22 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
     }
     if (op.kind == SPK_OP_VARINT) {  // deserialize_varint (varint.hpp:270-330)
       uint64_t v = 0;
-      uint32_t k = 0;
-      for (;; ++k) {
-        if (k == 10) return SPK_ERRC_INVALID_BUFFER;
-        if (pos >= end) return SPK_ERRC_NO_BUFFER_SPACE;
+      int32_t vec = SPK_ERRC_INVALID_BUFFER;  // 10 bytes, all continued
+      for (uint32_t k = 0; k < 10; ++k) {
+        if (pos >= end) {
+          vec = SPK_ERRC_NO_BUFFER_SPACE;  // (the bytes read stay consumed)
+          break;
+        }
         const uint8_t b = wire[pos++];
         v |= (uint64_t)(b & 0x7fu) << (7 * k);
-        if (!(b & 0x80u)) break;
+        if (!(b & 0x80u)) {
+          vec = SPK_ERRC_OK;
+          break;
+        }
+      }
+      if (vec) {
+        ec = vec;
+        continue;
       }
       if (r) {
         if (op.aux & SPK_VARINT_ZIGZAG) v = (v >> 1) ^ (uint64_t)(-(int64_t)(v & 1));
@@ -266,9 +352,21 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
       ++i;
       continue;
     }
+    if (op.kind == SPK_OP_VARIANT) {  // unpacker.hpp:1278-1292
+      if (pos >= end) { ec = SPK_ERRC_NO_BUFFER_SPACE; continue; }
+      const uint32_t idx = wire[pos++];
+      if (idx >= op.size) { ec = SPK_ERRC_INVALID_BUFFER; continue; }
+      if (r) *reinterpret_cast<uint32_t *>(r + op.rec_off) = idx;
+      const uint32_t a0 = n_alt_start(N, i, idx);
+      st[d] = NFrame{i, iend, 0, 1, r, r, a0, (uint32_t)N.end[i] + 1};
+      ++d;
+      iend = n_alt_end(N, a0);
+      i = a0;
+      continue;
+    }
     const uint32_t hk = N.heap[i];
     const uint32_t pw = op.kind == SPK_OP_OPTION ? 1u : w;
-    if (end - pos < pw) return SPK_ERRC_NO_BUFFER_SPACE;
+    if (end - pos < pw) { ec = SPK_ERRC_NO_BUFFER_SPACE; continue; }
     uint64_t cnt;
     if (op.kind == SPK_OP_OPTION) {
       cnt = wire[pos] != 0;
@@ -293,7 +391,8 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
         i = N.end[i] + 1;
         continue;
       }
-      st[d] = NFrame{i, iend, 0, cnt, put ? heaps[hk] + off * op.size : nullptr, r};
+      st[d] = NFrame{i, iend, 0, cnt, put ? heaps[hk] + off * op.size : nullptr, r, i + 1,
+                     (uint32_t)N.end[i] + 1};
       r = put ? heaps[hk] + off * op.size : nullptr;
       ++d;
       iend = N.end[i];
@@ -317,9 +416,9 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
     }
     // SPAN (unpacker.hpp:1127-1156): the whole payload must be present
     if (cnt) {
-      if (op.size > 1 && cnt > ~0ull / op.size) return SPK_ERRC_NO_BUFFER_SPACE;
+      if (op.size > 1 && cnt > ~0ull / op.size) { ec = SPK_ERRC_NO_BUFFER_SPACE; continue; }
       const uint64_t nb = cnt * op.size;
-      if (end - pos < nb) return SPK_ERRC_NO_BUFFER_SPACE;
+      if (end - pos < nb) { ec = SPK_ERRC_NO_BUFFER_SPACE; continue; }
       if (put) n_copy(heaps[hk] + off * op.size, wire + pos, nb);
       pos += nb;
     }
@@ -691,7 +790,8 @@ struct NDec {
   NLayout N;
   spk_msgfmt fmt;
   uint64_t wire_len, n_msgs, rec_cap;
-  uint32_t prefix, pad_;
+  uint32_t prefix, body_w;  // body_w: spk_decode_body (no header, body_n records)
+  uint64_t body_n;
   uint8_t *heaps[SPK_MAX_SPANS];
   uint64_t heap_cap[SPK_MAX_SPANS];
 };
@@ -720,8 +820,15 @@ __global__ __launch_bounds__(64) void nest_vec_walk(NDec a, const uint8_t *__res
   struct Fr {
     uint32_t aop, pend;
     uint64_t j, cnt;
+    uint32_t first, ret;
   } st[SPK_MAX_DEPTH];
-  if (lane == 0) {
+  if (lane == 0 && a.body_w) {
+    w = a.body_w;
+    n = a.body_n;
+    s_pos = 0;
+    s_done = n == 0;
+    if (n && a.rec_cap) starts[0] = 0;
+  } else if (lane == 0) {
     uint64_t p0;
     errc = parse_hdr(a.fmt, wire, len, &p0, &w, &data_len);
     pos = p0;
@@ -752,16 +859,34 @@ __global__ __launch_bounds__(64) void nest_vec_walk(NDec a, const uint8_t *__res
     if (lane == 0) {
       const uint64_t wend = wbase + kNWin < len ? wbase + kNWin : len;
       auto byte = [&](uint64_t x) -> uint32_t { return win[x - wbase]; };
+      // an error inside a VARIANT alternative is dropped (the walk goes on
+      // after the variant, unpacker.hpp:476-490); an ARRAY keeps its failing
+      // element. Returns false when the error ends the message.
+      auto fail = [&](int32_t e) -> bool {
+        while (d) {
+          Fr &f = st[d - 1];
+          if (N.ops[f.aop].kind == SPK_OP_VARIANT) {
+            i = f.ret;
+            iend = f.pend;
+            --d;
+            return true;
+          }
+          used[N.heap[f.aop]] -= f.cnt - (f.j + 1);
+          --d;
+        }
+        errc = e;
+        return false;
+      };
       bool stall = false, done = false;
       while (!stall && !done) {
         if (i >= iend) {
           if (d) {
             Fr &f = st[d - 1];
             if (++f.j < f.cnt) {
-              i = f.aop + 1;
+              i = f.first;
               continue;
             }
-            i = N.end[f.aop] + 1;
+            i = f.ret;
             iend = f.pend;
             --d;
             continue;
@@ -783,9 +908,11 @@ __global__ __launch_bounds__(64) void nest_vec_walk(NDec a, const uint8_t *__res
         const spk_op op = N.ops[i];
         if (op.kind == SPK_OP_COPY) {
           if (len - pos < op.size) {
-            errc = SPK_ERRC_NO_BUFFER_SPACE;
-            done = true;
-            break;
+            if (!fail(SPK_ERRC_NO_BUFFER_SPACE)) {
+              done = true;
+              break;
+            }
+            continue;
           }
           pos += op.size;  // skipped, not read
           ++i;
@@ -793,38 +920,65 @@ __global__ __launch_bounds__(64) void nest_vec_walk(NDec a, const uint8_t *__res
         }
         // every other op reads at most 10 bytes: refill when the window (not
         // the wire) ends before them
-        const uint64_t need = op.kind == SPK_OP_VARINT ? 10 : (op.kind == SPK_OP_OPTION ? 1 : w);
+        const uint64_t need = op.kind == SPK_OP_VARINT ? 10
+                              : (op.kind == SPK_OP_OPTION || op.kind == SPK_OP_VARIANT) ? 1
+                                                                                          : w;
         if (wend < len && pos + need > wend) {
           stall = true;
           break;
         }
         if (op.kind == SPK_OP_VARINT) {
-          uint32_t k = 0;
-          for (;; ++k) {
-            if (k == 10) {
-              errc = SPK_ERRC_INVALID_BUFFER;
-              break;
-            }
+          int32_t vec = SPK_ERRC_INVALID_BUFFER;
+          for (uint32_t k = 0; k < 10; ++k) {
             if (pos >= len) {
-              errc = SPK_ERRC_NO_BUFFER_SPACE;
+              vec = SPK_ERRC_NO_BUFFER_SPACE;
               break;
             }
-            const uint32_t b = byte(pos++);
-            if (!(b & 0x80u)) break;
+            if (!(byte(pos++) & 0x80u)) {
+              vec = SPK_ERRC_OK;
+              break;
+            }
           }
-          if (errc) {
-            done = true;
-            break;
+          if (vec) {
+            if (!fail(vec)) {
+              done = true;
+              break;
+            }
+            continue;
           }
           ++i;
+          continue;
+        }
+        if (op.kind == SPK_OP_VARIANT) {
+          if (pos >= len) {
+            if (!fail(SPK_ERRC_NO_BUFFER_SPACE)) {
+              done = true;
+              break;
+            }
+            continue;
+          }
+          const uint32_t idx = byte(pos++);
+          if (idx >= op.size || d == SPK_MAX_DEPTH) {
+            if (!fail(SPK_ERRC_INVALID_BUFFER)) {
+              done = true;
+              break;
+            }
+            continue;
+          }
+          const uint32_t a0 = n_alt_start(N, i, idx);
+          st[d++] = Fr{i, iend, 0, 1, a0, (uint32_t)N.end[i] + 1};
+          iend = n_alt_end(N, a0);
+          i = a0;
           continue;
         }
         const uint32_t hk = N.heap[i];
         const uint32_t pw = op.kind == SPK_OP_OPTION ? 1u : w;
         if (len - pos < pw) {
-          errc = SPK_ERRC_NO_BUFFER_SPACE;
-          done = true;
-          break;
+          if (!fail(SPK_ERRC_NO_BUFFER_SPACE)) {
+            done = true;
+            break;
+          }
+          continue;
         }
         uint64_t cnt = 0;
         if (op.kind == SPK_OP_OPTION)
@@ -839,11 +993,13 @@ __global__ __launch_bounds__(64) void nest_vec_walk(NDec a, const uint8_t *__res
             continue;
           }
           if (d == SPK_MAX_DEPTH) {  // (layout_check bounds the depth)
-            errc = SPK_ERRC_INVALID_BUFFER;
-            done = true;
-            break;
+            if (!fail(SPK_ERRC_INVALID_BUFFER)) {
+              done = true;
+              break;
+            }
+            continue;
           }
-          st[d++] = Fr{i, iend, 0, cnt};
+          st[d++] = Fr{i, iend, 0, cnt, i + 1, (uint32_t)N.end[i] + 1};
           iend = N.end[i];
           ++i;
           continue;
@@ -855,9 +1011,11 @@ __global__ __launch_bounds__(64) void nest_vec_walk(NDec a, const uint8_t *__res
         }
         if (cnt) {
           if ((op.size > 1 && cnt > ~0ull / op.size) || len - pos < cnt * op.size) {
-            errc = SPK_ERRC_NO_BUFFER_SPACE;
-            done = true;
-            break;
+            if (!fail(SPK_ERRC_NO_BUFFER_SPACE)) {
+              done = true;
+              break;
+            }
+            continue;
           }
           pos += cnt * op.size;
         }
@@ -1004,8 +1162,10 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
                                 uint64_t n_msgs, uint32_t prefix, void *d_recs, uint64_t rec_cap,
                                 void *const *d_heaps, const uint64_t *heap_caps,
                                 spk_dresult_t *d_res, int32_t *d_errc, void *d_ws,
-                                hipStream_t s) {
+                                hipStream_t s, uint32_t body_w, uint64_t body_n) {
   NDec a = {};
+  a.body_w = body_w;
+  a.body_n = body_n;
   a.N = make_nlayout(L);
   a.fmt = mode == SPK_MODE_VECTOR ? L->fmt_vector : L->fmt_one;
   a.wire_len = wire_len;

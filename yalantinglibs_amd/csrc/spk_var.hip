@@ -808,7 +808,8 @@ struct DecArgs {
   uint64_t heap_cap[SPK_MAX_SPANS];
   uint8_t *heaps[SPK_MAX_SPANS];
   uint32_t prefix;  // MESSAGES: frame bytes before every message
-  uint32_t pad_;
+  uint32_t body_w;  // VECTOR, spk_decode_body: no header, body_n records at this width
+  uint64_t body_n;
 };
 
 
@@ -1237,11 +1238,13 @@ __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
                                uint64_t cap) {
   if (threadIdx.x != 0) return;
   VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
-  uint64_t pos, dl;
-  uint32_t w;
-  int32_t e = parse_hdr(a.fmt, wire, a.wire_len, &pos, &w, &dl);
+  uint64_t pos = 0, dl = 0;
+  uint32_t w = a.body_w;
+  int32_t e = a.body_w ? SPK_ERRC_OK : parse_hdr(a.fmt, wire, a.wire_len, &pos, &w, &dl);
   uint64_t n = 0;
-  if (!e) {
+  if (a.body_w) {
+    n = a.body_n;
+  } else if (!e) {
     if (a.wire_len < pos + w)
       e = SPK_ERRC_NO_BUFFER_SPACE;
     else
@@ -3401,9 +3404,12 @@ hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
                              uint64_t n_msgs, uint32_t prefix, void *d_recs,
                              uint64_t rec_cap, void *const *d_heaps,
                              const uint64_t *heap_caps, spk_dresult_t *d_res,
-                             int32_t *d_errc, void *d_ws, size_t ws_bytes, hipStream_t s) {
+                             int32_t *d_errc, void *d_ws, size_t ws_bytes, hipStream_t s,
+                             uint32_t body_w, uint64_t body_n) {
   DecArgs a = {};
   a.prefix = prefix;
+  a.body_w = body_w;
+  a.body_n = body_n;
   a.L = make_klayout(L);
   a.fmt = mode == SPK_MODE_VECTOR ? L->fmt_vector : L->fmt_one;
   a.wire_len = wire_len;
@@ -3437,7 +3443,7 @@ hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
   (void)ws_bytes;
   // NS = -1: the walkers read varints (kept out of the other instantiations:
   // the inlined LEB128 loops cost registers in the hot walks)
-  if (!legacy_vec_decode()) {
+  if (!legacy_vec_decode() || body_w) {
     uint8_t *r = (uint8_t *)d_recs;
     if (P.nv) return launch_vec_tiles_ns<-1>(a, P, L, wire, ws, d_res, r, s);
     if (P.ns == 1) return launch_vec_tiles_ns<1>(a, P, L, wire, ws, d_res, r, s);

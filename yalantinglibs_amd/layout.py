@@ -39,6 +39,9 @@ class Layout:
         """Members with a width-w count on the wire (SPAN: string / vector);
         an OPTION's 1-byte has_value and varints are in the plan's var_bytes."""
         from . import _capi as C
+        if any(op[0] == C.SPK_OP_ARRAY for op in self.dev.ops):
+            raise ValueError("count fields of an ARRAY layout depend on the data: "
+                             "use parallel.count_fields(plan)")
         return sum(op[0] == C.SPK_OP_SPAN for op in self.dev.ops)
 
 

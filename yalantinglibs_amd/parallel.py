@@ -45,11 +45,21 @@ def width_of(max_count: int) -> int:
     return 1 if max_count < 1 << 8 else 2 if max_count < 1 << 16 else 4 if max_count < 1 << 32 else 8
 
 
+def count_fields(plan) -> int:
+    """Width-w count fields in the body of a local VECTOR plan (every SPAN and
+    ARRAY length, at every nesting level): total = header + var + fields * w."""
+    if plan.width == 0:
+        return 0
+    return (plan.total_bytes - plan.header_bytes - plan.var_bytes) // plan.width
+
+
 def agree_shard_plan(local_n: int, local_max_count: int, local_var_bytes: int,
-                     n_cont: int, header_fn, group=None, device=None) -> ShardPlan:
+                     n_cont: int, header_fn, group=None, device=None,
+                     local_fields: Optional[int] = None) -> ShardPlan:
     """Collective part of the sharded encode (works on gloo or nccl):
     all-reduce(SUM) of record counts, all-reduce(MAX) of the largest element
-    count, all-gather of body sizes."""
+    count, all-gather of body sizes. The body holds local_fields count fields
+    (n_cont per record for flat layouts; count_fields(plan) in general)."""
     world = dist.get_world_size(group)
     dev = device if device is not None else torch.device("cpu")
     t = torch.tensor([local_n, local_max_count], dtype=torch.int64, device=dev)
@@ -58,7 +68,8 @@ def agree_shard_plan(local_n: int, local_max_count: int, local_var_bytes: int,
     dist.all_reduce(s[1:], op=dist.ReduceOp.MAX, group=group)
     global_n, gmax = int(s[0].item()), int(s[1].item())
     w = width_of(max(global_n, gmax))
-    body = local_var_bytes + local_n * n_cont * w
+    fields = local_n * n_cont if local_fields is None else local_fields
+    body = local_var_bytes + fields * w
     sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
     dist.all_gather(sizes, torch.tensor([body], dtype=torch.int64, device=dev), group=group)
     body_bytes = [int(x.item()) for x in sizes]
@@ -89,9 +100,10 @@ class ShardedVectorEncoder:
 
     def plan(self, batch: RecordBatch) -> ShardPlan:
         p = self.cd.get_needed_size(batch, C.SPK_MODE_VECTOR)
-        return agree_shard_plan(batch.n, p.max_count, p.var_bytes, self.cd.L.n_cont,
+        return agree_shard_plan(batch.n, p.max_count, p.var_bytes, 0,
                                 self.header, self.group,
-                                None if self._host_staged() else self.cd.device)
+                                None if self._host_staged() else self.cd.device,
+                                local_fields=count_fields(p))
 
     def encode_body(self, batch: RecordBatch, width: int, out: torch.Tensor, stream=None):
         ws = self.cd.workspace(C.SPK_MODE_VECTOR, batch.n)

@@ -207,6 +207,29 @@ class Optional(SpType):
         return self.elem.has_container
 
 
+class Variant(SpType):
+    """std::variant<A, B, ...> (variant_t): wire [index:1][active
+    alternative] (ref packer.hpp:389-398; decode: an index past the last
+    alternative is invalid_buffer, unpacker.hpp:1278-1292); literal
+    variant_t + the alternatives' literals + end (type_calculate.hpp:245-253);
+    a container if any alternative holds one (type_calculate.hpp:785-815).
+    Device record: the u32 active index, then every alternative's fields side
+    by side (a decode writes only the active one's)."""
+
+    def __init__(self, *alts: SpType):
+        assert 0 < len(alts) < 256
+        self.alts = alts
+        self.name = "std::variant<" + ",".join(a.name for a in alts) + ">"
+        self.config = DEFAULT
+
+    def literal(self):
+        return bytes([TID_VARIANT]) + b"".join(a.literal() for a in self.alts) + bytes([TID_END])
+
+    @property
+    def has_container(self):
+        return any(a.has_container for a in self.alts)
+
+
 class Array(SpType):
     """std::array<T, n> / T[n] (array_t): no length prefix on the wire."""
 
@@ -433,6 +456,14 @@ def flatten(rtype: SpType) -> DeviceLayout:
             spans.append(SpanField(path, t.elem, coff, ooff))
             npf.append((path + ".n", "<u4", coff))
             npf.append((path + ".off", "<u8", ooff))
+        elif isinstance(t, Variant):
+            ioff = place(4, 4)
+            ops.append((C.SPK_OP_VARIANT, ioff, len(t.alts), 0))
+            npf.append((path + ".index", "<u4", ioff))
+            for a, alt in enumerate(t.alts):
+                if not isinstance(alt, Monostate):
+                    visit(alt, f"{path}.{a}")
+                ops.append((C.SPK_OP_END, 0, 0, 0))
         elif isinstance(t, VarInt):
             off = place(t.size, t.size)
             ops.append((C.SPK_OP_VARINT, off, t.size,

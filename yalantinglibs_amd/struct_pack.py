@@ -178,6 +178,28 @@ class Codec:
                                         ws.numel(), _stream(stream)), "spk_decode")
         return self.res_buf
 
+    def deserialize_body(self, out: RecordBatch, body: torch.Tensor, width: int, n: int,
+                         heap_caps=None, stream=None) -> torch.Tensor:
+        """spk_decode_body: n records from a VECTOR message body (after the
+        header and count) at `width` — chunked / sharded decodes."""
+        ws = self.workspace(MODE_VECTOR, out.n, body.numel())
+        caps = heap_caps or [h.numel() // sp.elem.size
+                             for h, sp in zip(out.heaps, self.L.dev.spans)]
+        hc = (ct.c_uint64 * max(len(caps), 1))(*(caps or [0]))
+        self._check(self.lib.spk_decode_body(self.L.ptr, _p(body), body.numel(), width, n,
+                                             _p(out.recs), out.n, self._heap_ptrs(out.heaps),
+                                             hc, _p(self.res_buf), _p(ws), ws.numel(),
+                                             _stream(stream)), "spk_decode_body")
+        return self.res_buf
+
+    def parse_vector_header(self, host_bytes: bytes):
+        """Host parse of a VECTOR message head: (errc, n, width, header_len)."""
+        n, w, hl = ct.c_uint64(), ct.c_uint32(), ct.c_uint32()
+        buf = (ct.c_uint8 * max(len(host_bytes), 1)).from_buffer_copy(host_bytes or b"\0")
+        e = self.lib.spk_parse_vector_header(self.L.ptr, buf, len(host_bytes), ct.byref(n),
+                                             ct.byref(w), ct.byref(hl))
+        return int(e), n.value, w.value, hl.value
+
     def result(self) -> C.spk_dresult_t:
         return C.spk_dresult_t.from_buffer_copy(bytes(self.res_buf.cpu().numpy()))
 

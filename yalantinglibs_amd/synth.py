@@ -92,10 +92,16 @@ Group = S.Struct("Group", [("gid", S.int64), ("members", S.Vector(RecS)),
                            ("label", S.String())])
 Deep = S.Struct("Deep", [("k", S.uint16), ("m", S.Vector(S.Vector(S.String())))])
 
+Vnt = S.Struct("Vnt", [("id", S.int32),
+                       ("v", S.Variant(S.int32, S.float64, S.String(), Inner)),
+                       ("w", S.Variant(S.Monostate(), S.Vector(S.int32))),
+                       ("list", S.Vector(S.Variant(S.int64, S.String())))])
+
 CASE_TYPES = {"rec64": Rec64, "recs": RecS, "outer": Outer, "pad": Pad,
               "mixed": Mixed, "rect": RectInt, "rpcrect": RpcRect,
               "person": Person, "ints": Ints, "opt": Opt, "optp": OptP,
-              "var": Var, "varp": VarP, "tags": Tags, "group": Group, "deep": Deep}
+              "var": Var, "varp": VarP, "tags": Tags, "group": Group, "deep": Deep,
+              "vnt": Vnt}
 # vector<rect<int>> has its own ADL set_sp_config (benchmark data_def.hpp:69-72)
 VECTOR_CONFIG = {"rect": S.DISABLE_ALL_META_INFO}
 
@@ -351,6 +357,47 @@ def make_batch(case: str, n: int, seed: int, param: int = 48):
             lens, chars = _tag_strings(mix64(h[lo] + q + np.uint64(1)))
         heaps.append(lists.view(np.uint8))
         heaps.append(_str_records(L.spans[1].sub, lens).view(np.uint8))
+        heaps.append(chars)
+    elif case == "vnt":  # fill(Vnt&)
+        recs["id"] = i32(rnd(seed, idx, 0))
+        a = (rnd(seed, idx, 1) % np.uint64(4)).astype(np.int64)
+        recs["v.index"] = a
+        recs["v.0"] = np.where(a == 0, i32(rnd(seed, idx, 2)), 0)
+        recs["v.1"] = np.where(a == 1, rd(rnd(seed, idx, 3)), 0.0)
+        lens = np.where(a == 2, (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64), 0)
+        recs["v.2.n"] = lens
+        recs["v.2.off"] = np.where(a == 2, _excl(lens), 0)
+        inner = np.zeros((n, 8), np.uint8)
+        sel = a == 3
+        inner.view(np.int32).reshape(-1, 2)[:, 0] = np.where(sel, i32(rnd(seed, idx, 4)), 0)
+        inner.view(np.float32).reshape(-1, 2)[:, 1] = np.where(sel, rf(rnd(seed, idx, 5)), 0)
+        recs["v.3"] = inner.view("V8").reshape(n)
+        heaps.append(_chars(seed, idx, lens))
+        has_w = (rnd(seed, idx, 6) & np.uint64(1)).astype(np.int64)
+        recs["w.index"] = has_w
+        cnt = np.where(has_w == 1, (rnd(seed, idx, 7) % np.uint64(param + 1)).astype(np.int64), 0)
+        recs["w.1.n"] = cnt
+        recs["w.1.off"] = np.where(has_w == 1, _excl(cnt), 0)
+        owner, j = _seg(cnt)
+        with np.errstate(over="ignore"):
+            vals = mix64(rnd(seed, idx[owner], 8) + j)
+        heaps.append(i32(vals).view(np.uint8))
+        m = (rnd(seed, idx, 9) % np.uint64(5)).astype(np.int64)
+        recs["list.n"] = m
+        recs["list.off"] = _excl(m)
+        lo, q = _seg(m)
+        h = _elem_word(seed, idx[lo], q)
+        sub = L.spans[2].sub
+        el = np.zeros(len(q), dtype=sub.dtype)
+        isstr = (h & np.uint64(1)).astype(np.int64)
+        el["value.index"] = isstr
+        el["value.0"] = np.where(isstr == 0, (h >> np.uint64(1)).view(np.int64), 0)
+        slen, chars = _tag_strings((h >> np.uint64(1))[isstr == 1])
+        sl = np.zeros(len(q), np.int64)
+        sl[isstr == 1] = slen
+        el["value.1.n"] = sl
+        el["value.1.off"] = np.where(isstr == 1, _excl(sl), 0)
+        heaps.append(el.view(np.uint8))
         heaps.append(chars)
     else:
         raise KeyError(case)
