@@ -381,7 +381,9 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
       *ovf = 1;
       put = false;
     }
-    if (put) {
+    // a SPAN's fields are set only once its payload is there (the reference
+    // checks before it resizes: a failing string stays empty)
+    if (put && op.kind != SPK_OP_SPAN) {
       *reinterpret_cast<uint32_t *>(r + op.rec_off) = (uint32_t)cnt;
       *reinterpret_cast<uint64_t *>(r + op.aux) = off;
     }
@@ -421,6 +423,10 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
       if (end - pos < nb) { ec = SPK_ERRC_NO_BUFFER_SPACE; continue; }
       if (put) n_copy(heaps[hk] + off * op.size, wire + pos, nb);
       pos += nb;
+    }
+    if (put) {
+      *reinterpret_cast<uint32_t *>(r + op.rec_off) = (uint32_t)cnt;
+      *reinterpret_cast<uint64_t *>(r + op.aux) = off;
     }
     used[hk] = off + cnt;
     ++i;
@@ -986,7 +992,7 @@ __global__ __launch_bounds__(64) void nest_vec_walk(NDec a, const uint8_t *__res
         else
           for (uint32_t b = 0; b < w; ++b) cnt |= (uint64_t)byte(pos + b) << (8 * b);
         pos += pw;
-        used[hk] += cnt;
+        if (op.kind != SPK_OP_SPAN) used[hk] += cnt;
         if (op.kind == SPK_OP_ARRAY) {
           if (!cnt) {
             i = N.end[i] + 1;
@@ -1019,6 +1025,7 @@ __global__ __launch_bounds__(64) void nest_vec_walk(NDec a, const uint8_t *__res
           }
           pos += cnt * op.size;
         }
+        used[hk] += cnt;
         ++i;
       }
       s_pos = pos;

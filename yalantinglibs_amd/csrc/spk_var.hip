@@ -2901,7 +2901,10 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
   const uint64_t n = c->n;
   const uint64_t base = TB.contrib[t];
   const int32_t sel = TB.sel[t];
-  if (base >= n || sel < 0 || !TB.fn[t * kFnWords + 2 + sel * kAltWords + 1]) return;
+  if (base >= n || sel < 0) return;
+  // a tile without records (inside a record that spans it) emits nothing,
+  // unless the path ends in it (term_pos below)
+  if (!TB.fn[t * kFnWords + 2 + sel * kAltWords + 1] && t != fc->term_tile) return;
   const uint32_t w = c->w;
   const uint64_t len = a.wire_len, p0 = c->p0;
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
