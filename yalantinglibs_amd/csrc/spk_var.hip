@@ -44,6 +44,9 @@
 #ifndef SPK_TWAVES
 #define SPK_TWAVES 1
 #endif
+#ifndef SPK_ESPLIT
+#define SPK_ESPLIT 2
+#endif
 
 namespace spk {
 
@@ -2304,10 +2307,11 @@ struct TileView {
   WinReader rd;
   uint64_t ts, wend;
 };
-__device__ __forceinline__ TileView stage_tile(v4u_t *win, const uint8_t *wire, uint64_t len,
-                                               uint64_t ts, uint32_t w, uint32_t lane) {
-  const uint64_t wend = ts + kTileVec * 16 < len ? ts + kTileVec * 16 : len;
-  for (uint32_t v = lane; v < kTileVec; v += 64) {
+template <uint32_t NV>
+__device__ __forceinline__ TileView stage_win(v4u_t *win, const uint8_t *wire, uint64_t len,
+                                              uint64_t ts, uint32_t w, uint32_t lane) {
+  const uint64_t wend = ts + NV * 16 < len ? ts + NV * 16 : len;
+  for (uint32_t v = lane; v < NV; v += 64) {
     const uint64_t g = ts + 16ull * v;
     v4u_t val = {0u, 0u, 0u, 0u};
     if (g + 16 <= len) {
@@ -2331,6 +2335,10 @@ __device__ __forceinline__ TileView stage_tile(v4u_t *win, const uint8_t *wire, 
   tv.ts = ts;
   tv.wend = wend;
   return tv;
+}
+__device__ __forceinline__ TileView stage_tile(v4u_t *win, const uint8_t *wire, uint64_t len,
+                                               uint64_t ts, uint32_t w, uint32_t lane) {
+  return stage_win<kTileVec>(win, wire, len, ts, w, lane);
 }
 
 __device__ __forceinline__ bool vec_live(const VCtl *c) { return !c->errc && c->n; }
@@ -2884,6 +2892,16 @@ __global__ __launch_bounds__(256) void tscan_apply(const uint8_t *__restrict__ w
 }
 
 // ---- K4 ----------------------------------------------------------------------
+// kEmitSplit waves per tile, each on kEmitChunks consecutive chunks: half the
+// LDS per wave of a whole tile, so twice the waves per CU hide the walks'
+// LDS latencies. A later part's first record and heap offsets are the
+// tile's selected totals minus what its own and later parts hold.
+constexpr uint32_t kEmitSplit = SPK_ESPLIT;
+constexpr uint32_t kEmitChunks = 64 / kEmitSplit;
+constexpr uint32_t kEmitBytes = kEmitChunks * kTChunk;
+constexpr uint32_t kEmitVec = (kEmitBytes + kWinExtra) / 16;
+constexpr uint32_t kEmitTab = kTab / kEmitSplit;  // record starts per emission pass
+
 template <int NS>
 __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkProg P,
                                                                 const uint8_t *__restrict__ wire,
@@ -2891,45 +2909,63 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
                                                                 TileBufs TB,
                                                                 uint8_t *__restrict__ recs,
                                                                 BigQ bq, uint32_t dbg) {
-  __shared__ v4u_t win_s[kDecWaves][kTileVec + 1];
-  __shared__ uint16_t tab_s[kDecWaves][kTab];
+  __shared__ v4u_t win_s[kDecWaves][kEmitVec + 1];
+  __shared__ uint16_t tab_s[kDecWaves][kEmitTab];
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t t = (uint64_t)blockIdx.x * kDecWaves + wv;
+  const uint64_t gw = (uint64_t)blockIdx.x * kDecWaves + wv;
+  const uint64_t t = gw / kEmitSplit;
+  const uint32_t part = (uint32_t)(gw % kEmitSplit);
   if (t >= TB.ntiles || !vec_live(c) || t > fc->term_tile) return;
   const uint64_t n = c->n;
-  const uint64_t base = TB.contrib[t];
+  const uint64_t tbase = TB.contrib[t];
   const int32_t sel = TB.sel[t];
-  if (base >= n || sel < 0) return;
+  if (tbase >= n || sel < 0) return;
+  const uint64_t *alt = TB.fn + t * kFnWords + 2 + sel * kAltWords;  // entry, cnt, sums
   // a tile without records (inside a record that spans it) emits nothing,
   // unless the path ends in it (term_pos below)
-  if (!TB.fn[t * kFnWords + 2 + sel * kAltWords + 1] && t != fc->term_tile) return;
+  if (!alt[1] && t != fc->term_tile) return;
   const uint32_t w = c->w;
   const uint64_t len = a.wire_len, p0 = c->p0;
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
   const uint64_t ts = p0 + t * kTileBytes;
-  const TileView tv = stage_tile(win_s[wv], wire, len, ts, w, lane);
+  const uint64_t wb = ts + (uint64_t)part * kEmitBytes;  // this part's window
+  const TileView tv = stage_win<kEmitVec>(win_s[wv], wire, len, wb, w, lane);
   const WinReader &rd = tv.rd;
   if (dbg & 128) {
-    if (lane == 0 && rd.byte(ts) == 0x1234) fc->end_pos = 1;  // keep the staging alive
+    if (lane == 0 && rd.byte(wb) == 0x1234) fc->end_pos = 1;  // keep the staging alive
     return;
   }
-  const uint64_t cs = ts + (uint64_t)lane * kTChunk;
+  const bool own = lane < kEmitChunks;
+  const uint32_t ch = part * kEmitChunks + lane;  // tile-relative chunk
+  const uint64_t cs = ts + (uint64_t)ch * kTChunk;
   const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
-  const uint64_t g = t * 64 + lane;
-  uint64_t used = TB.cused[g], ex = TB.cex[g];
-  uint32_t cnt = TB.ccnt[g];
-  if (sel > 0 && lane == 0) {  // another entry of chunk 0 (same exit)
-    const uint64_t T = tile_entry(TB, c, t);
+  const uint64_t g = t * 64 + ch;
+  uint64_t used = own ? TB.cused[g] : kNoPos, ex = own ? TB.cex[g] : kNoPos;
+  uint32_t cnt = own ? TB.ccnt[g] : 0;
+  if (sel > 0 && part == 0 && lane == 0) {  // another entry of chunk 0 (same exit)
+    const uint64_t T = alt[0];
     uint64_t qe, qt, qs[NS > 0 ? NS : SPK_MAX_SPANS];
     walk_true<NS>(P, rd, len, w, T, ce, qe, cnt, qs, qt);
     used = T;
   }
-  uint64_t psum[SPK_MAX_SPANS];
+  const uint64_t pcnt = wave_sum_u64(cnt);  // records starting in this part
+  uint64_t base = tbase, psum[SPK_MAX_SPANS];
   for (uint32_t q = 0; q < nsp; ++q) psum[q] = TB.contrib[(uint64_t)(1 + q) * TB.ntiles + t];
-  const uint64_t tcnt = wave_sum_u64(cnt);
-  if (ex == kTermPos && used != kNoPos && used != kTermPos && t == fc->term_tile) {
+  if (part > 0) {
+    // everything from this part to the tile's end (chunk 0 is not among it)
+    uint64_t rest = 0;
+    for (uint32_t cc = ch; cc < 64; cc += kEmitChunks) rest += TB.ccnt[t * 64 + cc];
+    base += alt[1] - wave_sum_u64(own ? rest : 0);
+    for (uint32_t q = 0; q < nsp; ++q) {
+      uint64_t rs = 0;
+      for (uint32_t cc = ch; cc < 64; cc += kEmitChunks)
+        rs += TB.csum[(uint64_t)q * TB.nchunks + t * 64 + cc];
+      psum[q] += alt[2 + q] - wave_sum_u64(own ? rs : 0);
+    }
+  }
+  if (own && ex == kTermPos && used != kNoPos && used != kTermPos && t == fc->term_tile) {
     // where the true path ends: past this chunk's records
     uint64_t x = used;
     for (uint32_t r = 0; r < cnt; ++r) {
@@ -2938,7 +2974,8 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
     }
     atomicMin(&fc->term_pos, (unsigned long long)x);
   }
-  uint64_t rofs;  // this chunk's first record, tile-relative
+  if (base >= n) return;
+  uint64_t rofs;  // this chunk's first record, part-relative
   {
     uint64_t tot;
     rofs = wave_excl_scan_u64(cnt, lane, &tot);
@@ -2946,16 +2983,16 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
   uint16_t *tab = tab_s[wv];
   uint64_t carry[NS > 0 ? NS : SPK_MAX_SPANS];
   for (uint32_t q = 0; q < nsp; ++q) carry[q] = psum[q];
-  const uint64_t nemit = (n - base < tcnt) ? n - base : tcnt;
-  for (uint64_t pass0 = 0; pass0 < nemit; pass0 += kTab) {
-    const uint64_t pend = pass0 + kTab < nemit ? pass0 + kTab : nemit;
+  const uint64_t nemit = (n - base < pcnt) ? n - base : pcnt;
+  for (uint64_t pass0 = 0; pass0 < nemit; pass0 += kEmitTab) {
+    const uint64_t pend = pass0 + kEmitTab < nemit ? pass0 + kEmitTab : nemit;
     // record starts of this pass into the table
     if (cnt && rofs < pend && rofs + cnt > pass0) {
       uint64_t x = used;
       for (uint32_t r = 0; r < cnt; ++r) {
         const uint64_t i = rofs + r;
         if (i >= pend) break;
-        if (i >= pass0) tab[i - pass0] = (uint16_t)(x - ts);
+        if (i >= pass0) tab[i - pass0] = (uint16_t)(x - wb);
         uint64_t rc[NS > 0 ? NS : SPK_MAX_SPANS];
         x += wlen_rd<NS>(P, rd, len, x, w, rc);
       }
@@ -2967,7 +3004,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
     for (uint64_t i0 = 0; i0 < nrec; i0 += 64) {
       const uint64_t i = i0 + lane;
       const bool act = i < nrec;
-      const uint64_t pos = ts + (act ? tab[i] : 0);
+      const uint64_t pos = wb + (act ? tab[i] : 0);
       uint64_t rc[SPK_MAX_SPANS] = {};
       uint64_t L = 0;
       if (act) L = wlen_rd<NS>(P, rd, len, pos, w, rc);
@@ -2979,10 +3016,10 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
         carry[q] += tot;
         if (off[q] + rc[q] > a.heap_cap[q]) fits = false;
       }
-      const uint64_t g = base + pass0 + i;
-      if (act && g < a.rec_cap && fits && !(dbg & 64))
-        emit_record_rd(a.L, rd, pos, w, recs + g * a.L.stride, a.heaps, off, len, bq);
-      if (act && g == n - 1) {
+      const uint64_t gr = base + pass0 + i;
+      if (act && gr < a.rec_cap && fits && !(dbg & 64))
+        emit_record_rd(a.L, rd, pos, w, recs + gr * a.L.stride, a.heaps, off, len, bq);
+      if (act && gr == n - 1) {
         fc->end_pos = pos + L;
         for (uint32_t q = 0; q < nsp; ++q) fc->htot[q] = off[q] + rc[q];
       }
@@ -3278,8 +3315,8 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
   bq.jobs = reinterpret_cast<BigJob *>(ws + f.jobs);
   bq.n = &reinterpret_cast<FCtl *>(ws + kWsFCtl)->njobs;
   bq.cap = big_jobs_cap(a.wire_len);
-  SPK_LAUNCH(vec_tile_emit<NS>, dim3(grid_for(f.ntiles, kDecWaves)), dim3(64 * kDecWaves), 0, s,
-             a, P, wire, ws, TB, d_recs, bq, tile_dbg());
+  SPK_LAUNCH(vec_tile_emit<NS>, dim3(grid_for(f.ntiles * kEmitSplit, kDecWaves)),
+             dim3(64 * kDecWaves), 0, s, a, P, wire, ws, TB, d_recs, bq, tile_dbg());
   if (P.ns) {
     const uint64_t gb = bq.cap < 2048 ? bq.cap : 2048;
     SPK_LAUNCH(vec_big_copy, dim3((unsigned)gb), dim3(256), 0, s, wire, (const uint8_t *)ws, bq);
