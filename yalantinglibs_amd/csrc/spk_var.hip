@@ -2311,6 +2311,23 @@ template <uint32_t NV>
 __device__ __forceinline__ TileView stage_win(v4u_t *win, const uint8_t *wire, uint64_t len,
                                               uint64_t ts, uint32_t w, uint32_t lane) {
   const uint64_t wend = ts + NV * 16 < len ? ts + NV * 16 : len;
+  if (ts + NV * 16 <= len) {
+    // the whole window exists: every lane issues all its 16-B loads before
+    // the first LDS write, so the wave waits for one load latency, not one
+    // per 1 KiB (an un-unrolled loop serialises them)
+    constexpr uint32_t kPer = (NV + 63) / 64;
+    v4u_t val[kPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+      const uint32_t v = lane + 64 * k;
+      if (NV % 64 == 0 || v < NV) val[k] = *reinterpret_cast<const v4u_una *>(wire + ts + 16ull * v);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+      const uint32_t v = lane + 64 * k;
+      if (NV % 64 == 0 || v < NV) win[v] = val[k];
+    }
+  } else
   for (uint32_t v = lane; v < NV; v += 64) {
     const uint64_t g = ts + 16ull * v;
     v4u_t val = {0u, 0u, 0u, 0u};
