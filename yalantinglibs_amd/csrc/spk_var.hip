@@ -1398,23 +1398,25 @@ __host__ __device__ constexpr uint64_t big_jobs_cap(uint64_t wire_len) {
 __device__ __forceinline__ void emit_record_rd(const KLayout &L, const WinReader &rd,
                                                uint64_t pos, uint32_t w, uint8_t *rec,
                                                uint8_t *const *heaps, const uint64_t *off,
-                                               uint64_t end, const BigQ &bq) {
+                                               uint64_t end, const BigQ &bq, uint32_t dbg = 0) {
   uint32_t sk = 0;
   for (uint32_t o = 0; o < L.n_ops; ++o) {
     const spk_op op = L.ops[o];
     if (op.kind == SPK_OP_COPY) {
-      rd.copy_to(rec + op.rec_off, pos, op.size);
+      if (!(dbg & 512)) rd.copy_to(rec + op.rec_off, pos, op.size);
       pos += op.size;
     } else if (op.kind == SPK_OP_VARINT) {
       uint64_t v = 0;
       auto byte = [&rd](uint64_t x) { return rd.byte(x); };
       pos += vi_read(byte, pos, end, &v);
-      vi_store(op, rec, v);
+      if (!(dbg & 512)) vi_store(op, rec, v);
     } else {
       const uint64_t cnt = op.kind == SPK_OP_OPTION ? (uint64_t)(rd.byte(pos) != 0) : rd(pos);
       pos += op_pw(op, w);
-      *reinterpret_cast<uint32_t *>(rec + op.rec_off) = (uint32_t)cnt;
-      *reinterpret_cast<uint64_t *>(rec + op.aux) = off[sk];
+      if (!(dbg & 512)) {
+        *reinterpret_cast<uint32_t *>(rec + op.rec_off) = (uint32_t)cnt;
+        *reinterpret_cast<uint64_t *>(rec + op.aux) = off[sk];
+      }
       const uint64_t nb = opt_nb(op, cnt, pos, end);
       uint8_t *hp = heaps[sk] + off[sk] * op.size;
       if (cnt && !nb && op.kind == SPK_OP_OPTION) {
@@ -1429,7 +1431,7 @@ __device__ __forceinline__ void emit_record_rd(const KLayout &L, const WinReader
           else
             copy_bytes(hp + o, rd.wire + pos + o, m);  // (the cap is never reached)
         }
-      } else {
+      } else if (!(dbg & 256)) {
         rd.copy_to(hp, pos, nb);
       }
       pos += nb;
@@ -3035,7 +3037,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
       }
       const uint64_t gr = base + pass0 + i;
       if (act && gr < a.rec_cap && fits && !(dbg & 64))
-        emit_record_rd(a.L, rd, pos, w, recs + gr * a.L.stride, a.heaps, off, len, bq);
+        emit_record_rd(a.L, rd, pos, w, recs + gr * a.L.stride, a.heaps, off, len, bq, dbg);
       if (act && gr == n - 1) {
         fc->end_pos = pos + L;
         for (uint32_t q = 0; q < nsp; ++q) fc->htot[q] = off[q] + rc[q];
