@@ -103,6 +103,11 @@ static int cmd_kat() {
   kat_one<std::vector<Group>>(os, "vector<Group>", first);
   kat_one<Deep>(os, "Deep", first);
   kat_one<Vnt>(os, "Vnt", first);
+  kat_one<Al8>(os, "Al8", first);
+  kat_one<AlOuter>(os, "AlOuter", first);
+  kat_one<Packed>(os, "Packed", first);
+  kat_one<AlRec>(os, "AlRec", first);
+  kat_one<std::vector<AlRec>>(os, "vector<AlRec>", first);
   kat_one<std::vector<Vnt>>(os, "vector<Vnt>", first);
   kat_one<std::variant<int32_t, std::string>>(os, "variant<int32_t,string>", first);
   kat_one<std::vector<Deep>>(os, "vector<Deep>", first);
@@ -184,6 +189,14 @@ static bool with_case(const Args &a, F &&f) {
     return f.template operator()<Tags>([=](Tags &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "group")
     return f.template operator()<Group>([=](Group &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "al8")
+    return f.template operator()<Al8>([=](Al8 &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "alout")
+    return f.template operator()<AlOuter>([=](AlOuter &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "packed")
+    return f.template operator()<Packed>([=](Packed &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "alrec")
+    return f.template operator()<AlRec>([=](AlRec &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "vnt")
     return f.template operator()<Vnt>([=](Vnt &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "deep")

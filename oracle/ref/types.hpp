@@ -174,6 +174,39 @@ struct Deep {  // two nesting levels: vector<vector<string>>
   std::vector<std::vector<std::string>> m;
 };
 
+// ---- alignment overrides (ref alignment.hpp:72-122, tests/test_alignas.cpp) --
+struct alignas(8) Al8 {  // alignas on a trivially serializable struct: 8 B
+  char a;
+  short b;
+};
+struct alignas(4) AlA {
+  char a;
+  short b;
+};
+struct alignas(8) AlB {
+  char a;
+  int b;
+};
+struct alignas(16) AlOuter {  // nesting: pack_alignment 8, alignment 16
+  AlA a;
+  AlB b;
+};
+#pragma pack(push, 1)
+struct Packed {  // #pragma pack(1) + struct_pack::pack_alignment_v = 1
+  char a;
+  int32_t b;
+  int16_t c;
+};
+#pragma pack(pop)
+template <>
+constexpr inline std::size_t struct_pack::pack_alignment_v<Packed> = 1;
+struct AlRec {  // non-trivial record holding aligned / packed members verbatim
+  AlOuter o;
+  std::string s;
+  Packed p;
+  Al8 e;
+};
+
 // ---- std::variant members (SPK_OP_VARIANT) ----------------------------
 struct Vnt {
   int32_t id;
@@ -385,6 +418,34 @@ inline void fill(Vnt &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
     else
       o.list.emplace_back((int64_t)(h >> 1));
   }
+}
+
+inline void fill(Al8 &o, uint64_t seed, uint64_t i, uint32_t) {
+  std::memset((void *)&o, 0, sizeof(o));
+  const uint64_t r = rnd(seed, i, 0);
+  o.a = (char)r;
+  o.b = (short)(r >> 8);
+}
+inline void fill(AlOuter &o, uint64_t seed, uint64_t i, uint32_t) {
+  std::memset((void *)&o, 0, sizeof(o));
+  const uint64_t r = rnd(seed, i, 1);
+  o.a.a = (char)r;
+  o.a.b = (short)(r >> 8);
+  o.b.a = (char)(r >> 24);
+  o.b.b = (int)(r >> 32);
+}
+inline void fill(Packed &o, uint64_t seed, uint64_t i, uint32_t) {
+  std::memset((void *)&o, 0, sizeof(o));
+  const uint64_t r = rnd(seed, i, 2);
+  o.a = (char)r;
+  o.b = (int32_t)(r >> 8);
+  o.c = (int16_t)(r >> 40);
+}
+inline void fill(AlRec &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
+  fill(o.o, seed, i, 0);
+  o.s = make_chars(seed, i, maxlen);
+  fill(o.p, seed, i, 0);
+  fill(o.e, seed, i, 0);
 }
 
 }  // namespace spk_gold

@@ -45,6 +45,8 @@ constexpr bool all_match() {
 }
 static_assert(all_match<Rec64, RecS, Inner, Outer, Pad, Mixed, Opt, OptP, Var, VarP,
                         rpcb::point, rpcb::rect, rpcb::person, rect<int>>());
+// alignment overrides (alignas, nested alignas, #pragma pack + pack_alignment_v)
+static_assert(all_match<Al8, AlOuter, Packed, AlRec, std::vector<AlRec>, std::vector<Packed>>());
 static_assert(all_match<std::vector<Rec64>, std::vector<RecS>, std::vector<Outer>,
                         std::vector<Mixed>, std::vector<Opt>, std::vector<Var>,
                         std::vector<rpcb::person>, std::vector<rect<int>>>());

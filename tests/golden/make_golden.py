@@ -31,7 +31,8 @@ SEED = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004,
         "pad": 0x5EED0005, "mixed": 0x5EED0006, "rect": 0, "rpcrect": 0x5EED0007,
         "person": 0x5EED0008, "ints": 0x5EED0009, "opt": 0x5EED000A, "optp": 0x5EED000B,
         "var": 0x5EED000C, "varp": 0x5EED000D, "tags": 0x5EED000E, "group": 0x5EED000F,
-        "deep": 0x5EED0010, "vnt": 0x5EED0011}
+        "deep": 0x5EED0010, "vnt": 0x5EED0011, "al8": 0x5EED0012, "alout": 0x5EED0013,
+        "packed": 0x5EED0014, "alrec": 0x5EED0015}
 
 # (case_mode, n, param, conf, keep_bin)
 SMALL = [
@@ -84,6 +85,14 @@ SMALL = [
     ("vnt_A", 0, 6, "default"), ("vnt_A", 1, 6, "default"), ("vnt_A", 200, 6, "default"),
     ("vnt_B", 200, 6, "default"), ("vnt_A", 40, 300, "default"),
     ("vnt_A", 50, 6, "typeinfo"), ("vnt_B", 60, 6, "nometa"),
+    # alignment overrides: alignas(8), nested alignas(4/8/16), #pragma pack(1) +
+    # pack_alignment_v = 1, and a non-trivial record holding all three
+    ("al8_A", 300, 0, "default"), ("al8_B", 50, 0, "default"), ("al8_A", 40, 0, "typeinfo"),
+    ("alout_A", 300, 0, "default"), ("alout_B", 50, 0, "default"),
+    ("alout_A", 40, 0, "typeinfo"), ("packed_A", 300, 0, "default"),
+    ("packed_B", 50, 0, "default"), ("packed_A", 40, 0, "typeinfo"),
+    ("alrec_A", 200, 20, "default"), ("alrec_B", 100, 20, "default"),
+    ("alrec_A", 40, 20, "typeinfo"),
 ]
 MEDIUM = [  # digest only (wire > ~1 MB)
     ("rec64_A", 65535, 0, "default"), ("rec64_A", 65536, 0, "default"),
@@ -211,6 +220,7 @@ ERR_BASES = [
     ("tags_A", 5, 4, "default"), ("tags_B", 1, 6, "default"), ("group_A", 4, 3, "default"),
     ("group_B", 1, 4, "default"), ("deep_A", 4, 3, "default"), ("deep_B", 1, 4, "default"),
     ("vnt_A", 6, 4, "default"), ("vnt_B", 1, 4, "default"), ("vnt_B", 1, 40, "default"),
+    ("alout_A", 5, 0, "default"), ("packed_B", 1, 0, "default"), ("alrec_A", 4, 10, "default"),
     # width-8 container lengths (metainfo 0x18): no reference encoder writes
     # them below 2^32 elements, but every decoder must read them
     # (unpacker.hpp:572-619); the base is our width-8 re-encoding, decoded by

@@ -170,7 +170,8 @@ RANDOM = [("recs", 1, 300), ("recs", 257, 5), ("recs", 5000, 48), ("recs", 20000
           ("opt", 5000, 48), ("opt", 300, 400), ("optp", 20000, 0),
           ("var", 5000, 48), ("var", 300, 400), ("var", 20000, 4), ("varp", 20000, 0),
           ("tags", 3000, 6), ("tags", 200, 300), ("group", 500, 5), ("group", 3, 2000),
-          ("deep", 700, 4), ("vnt", 3000, 8), ("vnt", 100, 400)]
+          ("deep", 700, 4), ("vnt", 3000, 8), ("vnt", 100, 400), ("al8", 5000, 0),
+          ("alout", 3000, 0), ("packed", 4097, 0), ("alrec", 3000, 30)]
 
 
 @pytest.mark.parametrize("case,n,param", RANDOM)

@@ -661,7 +661,9 @@ hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
     b.R = msg_block_R(M);
     const bool dw = (b.hlen % 4 == 0) && (b.seq_off == ~0u || b.seq_off % 4 == 0) &&
                     ((uintptr_t)d_out % 16 == 0);
-    if (b.R && (uintptr_t)d_recs % 4 == 0) {
+    // the LDS kernels move records in dwords: a packed stride (e.g. 7 B,
+    // #pragma pack) takes the byte kernels below
+    if (b.R && (uintptr_t)d_recs % 4 == 0 && b.stride % 4 == 0) {
       const uint64_t blocks = n ? (n + b.R - 1) / b.R : 1;
       const size_t lds = kMsgHdrMax + (size_t)b.R * b.stride + 16;
       if (dw)
@@ -813,7 +815,7 @@ hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
     b.fixed_M = a.fixed_M;
     b.prefix = prefix;
     b.R = msg_block_R(a.fixed_M);
-    if (b.R && (uintptr_t)d_recs % 16 == 0 && n > 0) {
+    if (b.R && (uintptr_t)d_recs % 16 == 0 && n > 0 && b.stride % 4 == 0) {
       b.cap = b.R * a.fixed_M + 32;
       uint64_t blocks = (n + b.R - 1) / b.R;
       if (blocks > 4096) blocks = 4096;  // groups are strided over the grid

@@ -257,17 +257,21 @@ class Struct(SpType):
     """An aggregate: members in declaration order (visit_members)."""
 
     def __init__(self, name: str, fields: Sequence[Tuple[str, SpType]],
-                 config: int = DEFAULT, alignas: int = 0):
+                 config: int = DEFAULT, alignas: int = 0, pack: int = 0):
+        """alignas: alignas(N) on the struct; pack: #pragma pack(N) together
+        with the user override struct_pack::pack_alignment_v<T> = N
+        (ref alignment.hpp:72-122; tests/test_alignas.cpp)."""
         self.name = name
         self.fields = list(fields)
         self.config = config
         self._alignas = alignas
+        self._pack = pack
         # C layout
         off = 0
         al = 1
         self.offsets = []
         for _, t in self.fields:
-            a = t.align
+            a = min(t.align, pack) if pack else t.align
             off = (off + a - 1) // a * a
             self.offsets.append(off)
             off += t.size
@@ -290,7 +294,7 @@ class Struct(SpType):
         if self.trivial:
             # pack_alignment_v (max member alignment_v) and alignment_v
             # (alignof) literals: type_calculate.hpp:232-239, alignment.hpp
-            pack = max((t.align for _, t in self.fields), default=1)
+            pack = self._pack or max((t.align for _, t in self.fields), default=1)
             return (bytes([TID_STRUCT]) + body + size_literal(pack) +
                     size_literal(self.align) + bytes([TID_END]))
         return bytes([TID_STRUCT]) + body + bytes([TID_END])

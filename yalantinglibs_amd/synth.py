@@ -97,11 +97,19 @@ Vnt = S.Struct("Vnt", [("id", S.int32),
                        ("w", S.Variant(S.Monostate(), S.Vector(S.int32))),
                        ("list", S.Vector(S.Variant(S.int64, S.String())))])
 
+# alignment overrides (types.hpp; ref alignment.hpp, tests/test_alignas.cpp)
+Al8 = S.Struct("Al8", [("a", S.char), ("b", S.int16)], alignas=8)
+AlA = S.Struct("AlA", [("a", S.char), ("b", S.int16)], alignas=4)
+AlB = S.Struct("AlB", [("a", S.char), ("b", S.int32)], alignas=8)
+AlOuter = S.Struct("AlOuter", [("a", AlA), ("b", AlB)], alignas=16)
+Packed = S.Struct("Packed", [("a", S.char), ("b", S.int32), ("c", S.int16)], pack=1)
+AlRec = S.Struct("AlRec", [("o", AlOuter), ("s", S.String()), ("p", Packed), ("e", Al8)])
+
 CASE_TYPES = {"rec64": Rec64, "recs": RecS, "outer": Outer, "pad": Pad,
               "mixed": Mixed, "rect": RectInt, "rpcrect": RpcRect,
               "person": Person, "ints": Ints, "opt": Opt, "optp": OptP,
               "var": Var, "varp": VarP, "tags": Tags, "group": Group, "deep": Deep,
-              "vnt": Vnt}
+              "vnt": Vnt, "al8": Al8, "alout": AlOuter, "packed": Packed, "alrec": AlRec}
 # vector<rect<int>> has its own ADL set_sp_config (benchmark data_def.hpp:69-72)
 VECTOR_CONFIG = {"rect": S.DISABLE_ALL_META_INFO}
 
@@ -358,6 +366,41 @@ def make_batch(case: str, n: int, seed: int, param: int = 48):
         heaps.append(lists.view(np.uint8))
         heaps.append(_str_records(L.spans[1].sub, lens).view(np.uint8))
         heaps.append(chars)
+    elif case in ("al8", "alout", "packed", "alrec"):  # fill(Al8& / AlOuter& / Packed& / AlRec&)
+        def al8_raw(r):
+            raw = np.zeros((n, 8), np.uint8)
+            raw[:, 0] = (r & np.uint64(0xFF)).astype(np.uint8)
+            raw[:, 2:4] = (r >> np.uint64(8)).astype(np.uint16)[:, None].view(np.uint8).reshape(n, 2)
+            return raw
+
+        def alout_raw(r):
+            raw = np.zeros((n, 16), np.uint8)
+            raw[:, 0] = (r & np.uint64(0xFF)).astype(np.uint8)
+            raw[:, 2:4] = (r >> np.uint64(8)).astype(np.uint16)[:, None].view(np.uint8).reshape(n, 2)
+            raw[:, 8] = ((r >> np.uint64(24)) & np.uint64(0xFF)).astype(np.uint8)
+            raw[:, 12:16] = (r >> np.uint64(32)).astype(np.uint32)[:, None].view(np.uint8).reshape(n, 4)
+            return raw
+
+        def packed_raw(r):
+            raw = np.zeros((n, 7), np.uint8)
+            raw[:, 0] = (r & np.uint64(0xFF)).astype(np.uint8)
+            raw[:, 1:5] = (r >> np.uint64(8)).astype(np.uint32)[:, None].view(np.uint8).reshape(n, 4)
+            raw[:, 5:7] = (r >> np.uint64(40)).astype(np.uint16)[:, None].view(np.uint8).reshape(n, 2)
+            return raw
+        if case == "al8":
+            recs = al8_raw(rnd(seed, idx, 0)).view(L.dtype).reshape(n)
+        elif case == "alout":
+            recs = alout_raw(rnd(seed, idx, 1)).view(L.dtype).reshape(n)
+        elif case == "packed":
+            recs = packed_raw(rnd(seed, idx, 2)).view(L.dtype).reshape(n)
+        else:
+            recs["o"] = alout_raw(rnd(seed, idx, 1)).view("V16").reshape(n)
+            lens = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+            recs["s.n"] = lens
+            recs["s.off"] = _excl(lens)
+            heaps.append(_chars(seed, idx, lens))
+            recs["p"] = packed_raw(rnd(seed, idx, 2)).view("V7").reshape(n)
+            recs["e"] = al8_raw(rnd(seed, idx, 0)).view("V8").reshape(n)
     elif case == "vnt":  # fill(Vnt&)
         recs["id"] = i32(rnd(seed, idx, 0))
         a = (rnd(seed, idx, 1) % np.uint64(4)).astype(np.int64)
