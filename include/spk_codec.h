@@ -336,6 +336,49 @@ int spk_decode_body(const spk_layout *L, const void *d_body, uint64_t body_len,
                     void *const *d_heaps, const uint64_t *heap_caps,
                     spk_dresult_t *d_res, void *d_ws, size_t ws_bytes, void *stream);
 
+/* ---- sharded decode of one SPK_MODE_VECTOR message ----------------------
+ * Every rank holds the message; rank r decodes the records that START in
+ * its tiles [tile_lo, tile_hi) of the body (SPK_DECODE_TILE_BYTES each,
+ * counted from the first byte after the header and count). Records are
+ * self-delimiting only from a known start, so:
+ *   1. spk_decode_shard_index: speculative index of the range from `entry`
+ *      (the wire offset of the range's first record start; SPK_ENTRY_UNKNOWN
+ *      lets the range guess it) -> *d_summary: the entry used, the exit
+ *      (first record start at or past the range end), the records and heap
+ *      elements on that path;
+ *   2. the ranks exchange summaries: the range is right when its entry is
+ *      the previous range's exit (range 0's entry is exact); a wrong one is
+ *      indexed again from that exit (normally never);
+ *   3. spk_decode_shard_emit (same workspace, same tiles): the range's
+ *      records into rank-local buffers (record 0 = global record `first`,
+ *      heaps from element 0), clipped at the message's count; `last` marks
+ *      the range holding the message's end (its shortfall is the errc).
+ * Layouts with SPK_OP_ARRAY / SPK_OP_VARIANT, and trivially-serializable
+ * records (plain offset arithmetic, spk_decode_body), are rejected
+ * (SPK_E_LAYOUT). */
+#define SPK_DECODE_TILE_BYTES 16384u
+#define SPK_ENTRY_UNKNOWN (~0ull)
+typedef struct spk_shard_t {
+  int32_t errc;         /* header errc                                       */
+  uint32_t width;
+  uint64_t n;           /* the message's record count                        */
+  uint64_t entry;       /* first record start the range was indexed from     */
+  uint64_t exit;        /* first record start at/past the range end; ~0 when
+                           the path ends inside the range                    */
+  uint64_t count;       /* records starting in the range on that path        */
+  uint64_t heap[SPK_MAX_SPANS]; /* their heap elements per span            */
+  uint64_t tiles_repaired;
+} spk_shard_t;
+int spk_decode_shard_index(const spk_layout *L, const void *d_wire, uint64_t wire_len,
+                           uint64_t tile_lo, uint64_t tile_hi, uint64_t entry,
+                           spk_shard_t *d_summary, void *d_ws, size_t ws_bytes,
+                           void *stream);
+int spk_decode_shard_emit(const spk_layout *L, const void *d_wire, uint64_t wire_len,
+                          uint64_t tile_lo, uint64_t tile_hi, uint64_t first, int last,
+                          void *d_recs, uint64_t rec_cap, void *const *d_heaps,
+                          const uint64_t *heap_caps, spk_dresult_t *d_res, void *d_ws,
+                          size_t ws_bytes, void *stream);
+
 /* HOST function: deserialize_metainfo of a SPK_MODE_VECTOR message in host
  * memory (unpacker.hpp:548-619) plus its container count. Returns the
  * reference errc (0 ok) or a negative SPK_E_*; on success *n = records,

@@ -593,3 +593,63 @@ def test_decode_body_chunks(case, n, param):
     cd.deserialize_body(out, body, w, n)
     r = cd.result()
     assert r.errc == 0 and r.count == n and r.consumed == len(exp) - hl
+
+
+@pytest.mark.parametrize("case,n,param,world", [("outer", 200000, 16, 4), ("recs", 300000, 48, 3),
+                                                ("var", 100000, 16, 5), ("opt", 50000, 40, 2),
+                                                ("recs", 5, 48, 4), ("mixed", 30000, 30, 3)])
+def test_sharded_decode_simulated(case, n, param, world):
+    """spk_decode_shard_index / _emit with `world` ranks simulated in one
+    process (one workspace each): the ranks' records re-encoded at the
+    message width and concatenated are the message body, byte for byte, and
+    the first-record indices tile [0, n)."""
+    from yalantinglibs_amd import layout as LY
+    from yalantinglibs_amd import parallel as PAR
+    cds = [SP.Codec(LY.case_layout(case)) for _ in range(world)]
+    _, recs, heaps = synth.make_batch(case, n, 0x5A5A + n, param)
+    exp, _, _ = H.oracle_encode(cds[0].L, C.SPK_MODE_VECTOR, recs, heaps)
+    _check_sharded(cds, exp, n, world)
+
+
+def _check_sharded(cds, exp, n, world):
+    from yalantinglibs_amd import parallel as PAR
+    wire = wire_dev(exp)
+    out, rounds = PAR.shard_decode([PAR.DeviceShardBackend(c) for c in cds], wire, world,
+                                   lambda mine: mine)
+    e, nn, w, hl = cds[0].parse_vector_header(exp[:1024])
+    assert e == 0 and nn == n
+    chunks, total = [], 0
+    for (b, first, res), cd in zip(out, cds):
+        assert res.errc == 0, (res.errc, first)
+        assert first == total and res.count == b.n
+        total += b.n
+        if not b.n:
+            continue
+        # the rank's records re-encoded at the message width = its body slice
+        pl = cd.get_needed_size(b, C.SPK_MODE_VECTOR)
+        blen = pl.total_bytes - pl.header_bytes + _fields(pl) * (w - pl.width)
+        ws = cd.workspace(C.SPK_MODE_VECTOR, b.n)
+        dst = torch.zeros(blen + 16, dtype=torch.uint8, device="cuda")
+        assert cd.lib.spk_encode_body(cd.L.ptr, b.n, SP._p(b.recs), cd._heap_ptrs(b.heaps), w,
+                                      SP._p(dst), dst.numel(), SP._p(ws), ws.numel(), None) == 0
+        chunks.append(dst[:blen].cpu().numpy().tobytes())
+    assert total == n
+    got = b"".join(chunks)
+    assert got == exp[hl:], (len(got), len(exp) - hl, rounds)
+    print(f"world {world}: {n} records, {rounds} exchange rounds")
+
+
+def _fields(plan):
+    return (plan.total_bytes - plan.header_bytes - plan.var_bytes) // plan.width
+
+
+def test_sharded_decode_long_records_boundaries():
+    """Ranges whose boundaries fall inside multi-MiB strings: the ranks'
+    guesses are wrong and the exchange re-indexes them from their neighbour's
+    exit; the result is still the message, byte for byte."""
+    from yalantinglibs_amd import layout as LY
+    lens = [3 << 20, 5, 1 << 20, 0, (2 << 20) + 7, 40000, 3] * 2
+    recs, heaps = _recs_with_lens(lens, 21)
+    cds = [SP.Codec(LY.case_layout("recs")) for _ in range(6)]
+    exp, _, _ = H.oracle_encode(cds[0].L, C.SPK_MODE_VECTOR, recs, heaps)
+    _check_sharded(cds, exp, len(recs), 6)

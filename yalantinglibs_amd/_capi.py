@@ -90,6 +90,15 @@ class spk_dresult_t(ct.Structure):
                 ("tiles_repaired", ct.c_uint32), ("tiles_sequential", ct.c_uint32)]
 
 
+class spk_shard_t(ct.Structure):
+    _fields_ = [("errc", ct.c_int32), ("width", ct.c_uint32), ("n", ct.c_uint64),
+                ("entry", ct.c_uint64), ("exit", ct.c_uint64), ("count", ct.c_uint64),
+                ("heap", ct.c_uint64 * SPK_MAX_SPANS), ("tiles_repaired", ct.c_uint64)]
+
+
+SPK_DECODE_TILE_BYTES = 16384
+
+
 class spk_frame(ct.Structure):
     _fields_ = [("prefix_len", ct.c_uint32), ("seq_off", ct.c_uint32),
                 ("len_off", ct.c_uint32), ("seq_base", ct.c_uint32),
@@ -111,6 +120,7 @@ CODEC_SYMBOLS = ["spk_abi_version", "spk_errc_message", "spk_layout_check",
                  "spk_synth", "spk_synth_counts", "spk_encode_body",
                  "spk_vector_header", "spk_encode_framed", "spk_decode_framed",
                  "spk_decode_body", "spk_parse_vector_header",
+                 "spk_decode_shard_index", "spk_decode_shard_emit",
                  # runtime helpers (front ends without HIP headers)
                  "spk_device_alloc", "spk_device_free", "spk_host_alloc_pinned",
                  "spk_host_free_pinned", "spk_copy_async", "spk_stream_create",
@@ -150,6 +160,9 @@ def _bind_codec(lib):
     lib.spk_parse_vector_header.argtypes = [PL, P, U64, ct.POINTER(U64),
                                             ct.POINTER(ct.c_uint32), ct.POINTER(ct.c_uint32)]
     lib.spk_parse_vector_header.restype = ct.c_int32
+    lib.spk_decode_shard_index.argtypes = [PL, P, U64, U64, U64, U64, P, P, ct.c_size_t, P]
+    lib.spk_decode_shard_emit.argtypes = [PL, P, U64, U64, U64, U64, ct.c_int, P, U64,
+                                          ct.POINTER(P), ct.POINTER(U64), P, P, ct.c_size_t, P]
     lib.spk_encode_framed.argtypes = [PL, U64, P, ct.POINTER(P), P, ct.POINTER(spk_frame),
                                       P, U64, P, P, ct.c_size_t, P]
     lib.spk_decode_framed.argtypes = [PL, P, U64, P, U64, ct.c_uint32, P, U64,

@@ -391,6 +391,45 @@ int spk_decode_body(const spk_layout *L, const void *d_body, uint64_t body_len, 
                                   width, n));
 }
 
+static int shard_check(const spk_layout *L, const void *d_wire, uint64_t wire_len, void *d_ws,
+                       size_t ws_bytes, uint64_t rec_cap) {
+  int rc = spk_layout_check(L);
+  if (rc) return rc;
+  if (is_trivial(L) || layout_nested(L)) return SPK_E_LAYOUT;
+  if (!d_ws || (wire_len && !d_wire)) return SPK_E_ARG;
+  if (ws_bytes < spk_workspace_bytes(L, SPK_MODE_VECTOR, rec_cap, wire_len)) return SPK_E_WORKSPACE;
+  return SPK_OK;
+}
+
+int spk_decode_shard_index(const spk_layout *L, const void *d_wire, uint64_t wire_len,
+                           uint64_t tile_lo, uint64_t tile_hi, uint64_t entry,
+                           spk_shard_t *d_summary, void *d_ws, size_t ws_bytes, void *stream) {
+  int rc = shard_check(L, d_wire, wire_len, d_ws, ws_bytes, 0);
+  if (rc) return rc;
+  if (!d_summary || tile_hi < tile_lo) return SPK_E_ARG;
+  spk_dresult_t *scratch = (spk_dresult_t *)((uint8_t *)d_ws + kWsCtl - sizeof(spk_dresult_t));
+  return hip_rc(launch_var_shard(L, 0, d_wire, wire_len, tile_lo, tile_hi, entry, d_summary, 0, 0,
+                                 nullptr, 0, nullptr, nullptr, scratch, d_ws,
+                                 (hipStream_t)stream));
+}
+
+int spk_decode_shard_emit(const spk_layout *L, const void *d_wire, uint64_t wire_len,
+                          uint64_t tile_lo, uint64_t tile_hi, uint64_t first, int last,
+                          void *d_recs, uint64_t rec_cap, void *const *d_heaps,
+                          const uint64_t *heap_caps, spk_dresult_t *d_res, void *d_ws,
+                          size_t ws_bytes, void *stream) {
+  // the tile decoder's workspace does not depend on rec_cap
+  int rc = shard_check(L, d_wire, wire_len, d_ws, ws_bytes, 0);
+  if (rc) return rc;
+  if (!d_res || tile_hi < tile_lo || (rec_cap && !d_recs) || (d_recs && (uintptr_t)d_recs % 8))
+    return SPK_E_ARG;
+  if ((rc = heaps_check(L, rec_cap, d_heaps))) return rc;
+  if (!heap_caps) return SPK_E_ARG;
+  return hip_rc(launch_var_shard(L, 1, d_wire, wire_len, tile_lo, tile_hi, 0, nullptr, first,
+                                 last ? 1u : 0u, d_recs, rec_cap, d_heaps, heap_caps, d_res, d_ws,
+                                 (hipStream_t)stream));
+}
+
 int32_t spk_parse_vector_header(const spk_layout *L, const void *h_wire, uint64_t len,
                                 uint64_t *n, uint32_t *width, uint32_t *header_len) {
   if (spk_layout_check(L) != SPK_OK) return SPK_E_LAYOUT;

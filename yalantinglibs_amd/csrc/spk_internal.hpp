@@ -182,6 +182,12 @@ void trace_mark(const char *name, hipStream_t s, int end);
 
 // ---- launch wrappers implemented in the kernel TUs -----------------------
 namespace spk {
+// spk_var.hip: sharded VECTOR decode (phase 0 = index, 1 = emit)
+hipError_t launch_var_shard(const spk_layout *L, int phase, const void *d_wire, uint64_t wire_len,
+                            uint64_t tile_lo, uint64_t tile_hi, uint64_t entry,
+                            spk_shard_t *d_summary, uint64_t first, uint32_t last, void *d_recs,
+                            uint64_t rec_cap, void *const *d_heaps, const uint64_t *heap_caps,
+                            spk_dresult_t *d_res, void *d_ws, hipStream_t s);
 // spk_nested.hip: layouts with SPK_OP_ARRAY
 bool layout_nested(const spk_layout *L);
 size_t nested_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len);

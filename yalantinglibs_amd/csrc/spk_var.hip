@@ -813,6 +813,9 @@ struct DecArgs {
   uint32_t prefix;  // MESSAGES: frame bytes before every message
   uint32_t body_w;  // VECTOR, spk_decode_body: no header, body_n records at this width
   uint64_t body_n;
+  uint32_t range;   // spk_decode_shard_index: tiles [range_t0, ...) of the body
+  uint32_t pad2_;
+  uint64_t range_t0, range_entry;
 };
 
 
@@ -1078,6 +1081,10 @@ struct FCtl {
   unsigned long long end_pos;    // end of record n-1
   unsigned long long total;      // records on the path (tile scan)
   unsigned long long htot[SPK_MAX_SPANS];  // heap elements used by records 0..n-1
+  unsigned long long entry0;     // tile 0's entry (range mode: injected, or kNoPos = its own guess)
+  unsigned long long nglob;      // range mode: the message's record count
+  uint32_t range;                // the tiles are a byte range of the body (spk_decode_shard_*)
+  uint32_t last;                 // range mode: the range holds the message's end
   unsigned long long stot[SPK_MAX_SPANS];  // span-count sums on the path
 };
 constexpr size_t kWsFCtl = kWsCtl + 1280;
@@ -1265,6 +1272,17 @@ __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
   }
   c->p0 = pos;
   c->n = e ? 0 : n;
+  {
+    FCtl *f0 = reinterpret_cast<FCtl *>(ws + kWsFCtl);
+    f0->range = a.range;
+    f0->last = 0;
+    f0->nglob = c->n;
+    f0->entry0 = pos;
+    if (a.range) {  // the tiles start range_t0 tiles into the body
+      c->p0 = pos + a.range_t0 * (64ull * SPK_TCHUNK);  // kTileBytes
+      f0->entry0 = a.range_t0 == 0 ? pos : a.range_entry;
+    }
+  }
   c->w = w;
   c->errc = e;
   c->data_len = dl;
@@ -2133,6 +2151,7 @@ __global__ __launch_bounds__(64 * kEmitWaves) void vec_emit(DecArgs a, WalkProg 
 // No kernel waits on another workgroup.
 constexpr uint32_t kTChunk = SPK_TCHUNK;                    // payload bytes per lane (chunk)
 constexpr uint32_t kTileBytes = 64 * kTChunk;                // payload bytes per tile
+static_assert(kTileBytes == SPK_DECODE_TILE_BYTES, "shard ranges are counted in these tiles");
 constexpr uint32_t kTileVec = (kTileBytes + kWinExtra) / 16;  // staged 16-B slots
 constexpr uint32_t kDecWaves = SPK_TWAVES;                   // tiles (waves) per block
 constexpr uint32_t kTab = 2048;                              // record starts per emission pass
@@ -2386,7 +2405,8 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
   uint64_t used = kNoPos, ex = kNoPos, sums[NS > 0 ? NS : SPK_MAX_SPANS], term_at = kTermPos;
   uint32_t cnt = 0;
   for (uint32_t q = 0; q < nsp; ++q) sums[q] = 0;
-  const bool exact = t == 0 && lane == 0;  // the payload start: no search
+  const bool rng = reinterpret_cast<const FCtl *>(ws + kWsFCtl)->range != 0;
+  const bool exact = t == 0 && lane == 0 && !rng;  // the payload start: no search
   SpecPath<NS> sp;
   sp.np = 0;
   if (cs < len && !(dbg & 8)) {
@@ -2510,8 +2530,8 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
   }
   // ---- 2. resolution given the tile's assumed entry ----
   uint64_t X = __shfl(used, 0);  // lane 0's spec start (kNoPos: no plausible start)
-  if (t == 0) X = p0;
-  if (t > 0 && !(dbg & 16)) {
+  if (t == 0 && !rng) X = p0;
+  if ((t > 0 || rng) && !(dbg & 16)) {
     // Two independent speculations that agree are far likelier true: when
     // chunk 0's walk does not exit where chunk 1's speculative walk starts,
     // take the first start candidate of chunk 0 whose walk does (in parallel,
@@ -2622,8 +2642,14 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
 }
 
 // tile t's entry: tile t-1's published exit (tile 0: the payload start)
-__device__ __forceinline__ uint64_t tile_entry(const TileBufs &TB, const VCtl *c, uint64_t t) {
-  return t == 0 ? c->p0 : TB.fn[(t - 1) * kFnWords];
+__device__ __forceinline__ uint64_t tile_entry(const TileBufs &TB, const FCtl *fc, uint64_t t) {
+  return t == 0 ? fc->entry0 : TB.fn[(t - 1) * kFnWords];
+}
+
+// range mode, entry unknown: tile 0 assumes its own speculated entry
+__global__ void vec_range_entry(uint8_t *__restrict__ ws, TileBufs TB) {
+  FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
+  if (threadIdx.x == 0 && fc->range && fc->entry0 == kNoPos && TB.ntiles) fc->entry0 = TB.fn[2];
 }
 
 // Tile t whose entry lies at or past its end (inside a record that spans it):
@@ -2680,7 +2706,7 @@ __global__ __launch_bounds__(64) void vec_tile_select(DecArgs a, WalkProg P,
   if (t >= TB.ntiles || !vec_live(c)) return;
   if (pass > 0 && !fc->broken[pass - 1]) return;  // the previous pass fixed nothing
   uint64_t *fn = TB.fn + t * kFnWords;
-  const uint64_t T = tile_entry(TB, c, t);
+  const uint64_t T = tile_entry(TB, fc, t);
   const int32_t sel = T == kNoPos ? kSelBroken : tile_select_for(TB, t, T);
   if (sel != kSelBroken || T == kNoPos) {
     if (lane == 0) TB.sel[t] = sel;
@@ -2752,7 +2778,7 @@ __global__ __launch_bounds__(64) void vec_tile_seqfix(DecArgs a, WalkProg P,
     int32_t sel = kSelTerm;
     bool bad = false;
     if (u < TB.ntiles) {
-      const uint64_t T = tile_entry(TB, c, u);
+      const uint64_t T = tile_entry(TB, fc, u);
       sel = tile_select_for(TB, u, T);
       bad = sel == kSelBroken && T != kNoPos;
     }
@@ -2763,7 +2789,7 @@ __global__ __launch_bounds__(64) void vec_tile_seqfix(DecArgs a, WalkProg P,
       t += 64;
       continue;
     }
-    const uint64_t T = tile_entry(TB, c, f);
+    const uint64_t T = tile_entry(TB, fc, f);
     const uint64_t ts = p0 + f * kTileBytes;
     if (T >= ts + kTileBytes) {
       // a record spans tiles f .. e-1: all pass the entry through
@@ -3069,6 +3095,45 @@ __global__ __launch_bounds__(256) void vec_big_copy(const uint8_t *__restrict__ 
   }
 }
 
+// spk_decode_shard_index's summary of the range
+__global__ void vec_shard_summary(const uint8_t *__restrict__ ws, TileBufs TB, uint32_t nsp,
+                                  spk_shard_t *out) {
+  if (threadIdx.x != 0) return;
+  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
+  const FCtl *fc = reinterpret_cast<const FCtl *>(ws + kWsFCtl);
+  spk_shard_t r = {};
+  r.errc = c->errc;
+  r.width = c->w;
+  r.n = fc->nglob;
+  r.entry = fc->entry0;
+  if (!c->errc && c->n) {
+    const bool term = fc->term_tile < TB.ntiles;
+    r.exit = term ? ~0ull : (TB.ntiles ? TB.fn[(TB.ntiles - 1) * kFnWords] : fc->entry0);
+    r.count = fc->total;
+    for (uint32_t q = 0; q < nsp && q < SPK_MAX_SPANS; ++q) r.heap[q] = fc->stot[q];
+    r.tiles_repaired = fc->broken[0] + fc->broken[1] + fc->broken[2] + fc->broken[3];
+  }
+  *out = r;
+}
+
+// spk_decode_shard_emit: the range's share of the message's count
+__global__ void vec_shard_setn(uint8_t *__restrict__ ws, uint64_t first, uint32_t last,
+                               spk_dresult_t *res) {
+  if (threadIdx.x != 0) return;
+  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
+  FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
+  spk_dresult_t r0 = {};
+  r0.errc = c->errc;
+  r0.width = c->w;
+  *res = r0;
+  if (c->errc) return;
+  c->n = fc->nglob > first ? fc->nglob - first : 0;
+  fc->last = last;
+  fc->end_pos = 0;
+  fc->njobs = 0;
+  for (int k = 0; k < SPK_MAX_SPANS; ++k) fc->htot[k] = 0;
+}
+
 // Result: count / consume_len / heap use, or the errc of a short payload
 // (no_buffer_space; invalid_buffer for an overlong varint where the path ends).
 __global__ void vec_tile_finish(DecArgs a, const uint8_t *__restrict__ wire,
@@ -3088,6 +3153,18 @@ __global__ void vec_tile_finish(DecArgs a, const uint8_t *__restrict__ wire,
     return;
   }
   const uint64_t total = c->n ? (uint64_t)fc->total : 0;
+  if (fc->range && !fc->last) {  // a middle shard: its records, up to the message's count
+    const uint64_t k = total < c->n ? total : c->n;
+    r.count = k;
+    r.consumed = k == c->n && k ? (uint64_t)fc->end_pos : 0;
+    for (uint32_t q = 0; q < a.L.n_spans; ++q) {
+      r.heap_used[q] = k == c->n && k ? fc->htot[q] : fc->stot[q];
+      if (r.heap_used[q] > a.heap_cap[q] && r.errc == 0) r.errc = SPK_ERRC_CAPACITY;
+    }
+    if (k > a.rec_cap && r.errc == 0) r.errc = SPK_ERRC_CAPACITY;
+    *res = r;
+    return;
+  }
   if (c->n && total < c->n) {
     r.errc = SPK_ERRC_NO_BUFFER_SPACE;
     if (a.L.n_var && fc->term_pos < a.wire_len) {
@@ -3301,11 +3378,24 @@ static uint32_t tile_dbg() {
   return v;
 }
 
+// phase: kTilesAll (one decode), kTilesIndex (spk_decode_shard_index: K1-K3
+// over tiles [a.range_t0, +ntiles) and the summary), kTilesEmit
+// (spk_decode_shard_emit: K4 + finish over the same tiles)
+constexpr int kTilesAll = 0, kTilesIndex = 1, kTilesEmit = 2;
+struct ShardCall {
+  uint64_t ntiles;     // range tiles (0: the whole message)
+  spk_shard_t *summary;
+  uint64_t first;      // emit: global index of the range's first record
+  uint32_t last;
+};
+
 template <int NS>
 static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const spk_layout *L,
                                       const uint8_t *wire, uint8_t *ws, spk_dresult_t *d_res,
-                                      uint8_t *d_recs, hipStream_t s) {
-  const TileWs f = tile_ws_layout(L, a.wire_len);
+                                      uint8_t *d_recs, hipStream_t s, int phase = kTilesAll,
+                                      const ShardCall &sc = ShardCall{}) {
+  TileWs f = tile_ws_layout(L, a.wire_len);
+  if (phase != kTilesAll) f.ntiles = sc.ntiles < f.ntiles ? sc.ntiles : f.ntiles;
   TileBufs TB;
   TB.fn = reinterpret_cast<uint64_t *>(ws + f.fn);
   TB.cused = reinterpret_cast<uint64_t *>(ws + f.cused);
@@ -3319,9 +3409,22 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
   TB.nchunks = f.nchunks;
   const uint32_t nsp = P.ns ? P.ns : 1;
   const unsigned nb = (unsigned)((f.ntiles + kTScanBlock - 1) / kTScanBlock);
+  if (phase != kTilesAll && f.ntiles == 0) {  // an empty range: header + summary only
+    if (phase == kTilesIndex) {
+      SPK_LAUNCH(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, 0u, (uint64_t)0);
+      SPK_LAUNCH(vec_shard_summary, dim3(1), dim3(64), 0, s, (const uint8_t *)ws, TB, nsp,
+                 sc.summary);
+    } else {
+      SPK_LAUNCH(vec_shard_setn, dim3(1), dim3(64), 0, s, ws, sc.first, sc.last, d_res);
+      SPK_LAUNCH(vec_tile_finish, dim3(1), dim3(64), 0, s, a, wire, (const uint8_t *)ws, d_res);
+    }
+    return hipGetLastError();
+  }
+  if (phase != kTilesEmit) {
   SPK_LAUNCH(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, 0u, (uint64_t)0);
   SPK_LAUNCH(vec_tile_spec<NS>, dim3(grid_for(f.ntiles, kDecWaves)), dim3(64 * kDecWaves), 0, s,
              a, P, wire, (const uint8_t *)ws, TB, tile_dbg());
+  if (phase == kTilesIndex) SPK_LAUNCH(vec_range_entry, dim3(1), dim3(64), 0, s, ws, TB);
   for (uint32_t pass = 0; pass < 3; ++pass)
     SPK_LAUNCH(vec_tile_select<NS>, dim3((unsigned)f.ntiles), dim3(64), 0, s, a, P, wire, ws, TB,
                pass);
@@ -3330,6 +3433,14 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
   SPK_LAUNCH(tscan_reduce, dim3(nb), dim3(256), 0, s, (const uint8_t *)ws, TB, 1 + nsp);
   SPK_LAUNCH(tscan_top, dim3(1), dim3(1024), 0, s, ws, TB, 1 + nsp, (uint64_t)nb);
   SPK_LAUNCH(tscan_apply, dim3(nb), dim3(256), 0, s, (const uint8_t *)ws, TB, 1 + nsp);
+  }
+  if (phase == kTilesIndex) {
+    SPK_LAUNCH(vec_shard_summary, dim3(1), dim3(64), 0, s, (const uint8_t *)ws, TB, nsp,
+               sc.summary);
+    return hipGetLastError();
+  }
+  if (phase == kTilesEmit)
+    SPK_LAUNCH(vec_shard_setn, dim3(1), dim3(64), 0, s, ws, sc.first, sc.last, d_res);
   BigQ bq;
   bq.jobs = reinterpret_cast<BigJob *>(ws + f.jobs);
   bq.n = &reinterpret_cast<FCtl *>(ws + kWsFCtl)->njobs;
@@ -3342,6 +3453,38 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
   }
   SPK_LAUNCH(vec_tile_finish, dim3(1), dim3(64), 0, s, a, wire, (const uint8_t *)ws, d_res);
   return hipGetLastError();
+}
+
+hipError_t launch_var_shard(const spk_layout *L, int phase, const void *d_wire, uint64_t wire_len,
+                            uint64_t tile_lo, uint64_t tile_hi, uint64_t entry,
+                            spk_shard_t *d_summary, uint64_t first, uint32_t last, void *d_recs,
+                            uint64_t rec_cap, void *const *d_heaps, const uint64_t *heap_caps,
+                            spk_dresult_t *d_res, void *d_ws, hipStream_t s) {
+  DecArgs a = {};
+  a.L = make_klayout(L);
+  a.fmt = L->fmt_vector;
+  a.wire_len = wire_len;
+  a.rec_cap = rec_cap;
+  for (uint32_t k = 0; k < a.L.n_spans; ++k) {
+    a.heaps[k] = d_heaps ? (uint8_t *)d_heaps[k] : nullptr;
+    a.heap_cap[k] = heap_caps ? heap_caps[k] : 0;
+  }
+  a.range = 1;
+  a.range_t0 = tile_lo;
+  a.range_entry = entry == ~0ull ? kNoPos : entry;
+  ShardCall sc;
+  sc.ntiles = tile_hi > tile_lo ? tile_hi - tile_lo : 0;
+  sc.summary = d_summary;
+  sc.first = first;
+  sc.last = last;
+  const int ph = phase == 0 ? kTilesIndex : kTilesEmit;
+  const WalkProg P = make_walkprog(L);
+  const uint8_t *wire = (const uint8_t *)d_wire;
+  uint8_t *ws = (uint8_t *)d_ws, *r = (uint8_t *)d_recs;
+  if (P.nv) return launch_vec_tiles_ns<-1>(a, P, L, wire, ws, d_res, r, s, ph, sc);
+  if (P.ns == 1) return launch_vec_tiles_ns<1>(a, P, L, wire, ws, d_res, r, s, ph, sc);
+  if (P.ns == 2) return launch_vec_tiles_ns<2>(a, P, L, wire, ws, d_res, r, s, ph, sc);
+  return launch_vec_tiles_ns<0>(a, P, L, wire, ws, d_res, r, s, ph, sc);
 }
 
 // SPK_VEC_DECODE=legacy selects the multi-pass decoder (A/B runs)

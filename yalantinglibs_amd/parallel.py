@@ -200,3 +200,156 @@ class ShardedVectorEncoder:
         torch.cuda.synchronize(self.cd.device)
         dist.barrier(self.group)
         return sp
+
+
+# ---------------------------------------------------------------------------
+# Sharded decode of ONE vector message (spk_decode_shard_index / _emit)
+# ---------------------------------------------------------------------------
+TILE_BYTES = C.SPK_DECODE_TILE_BYTES
+ENTRY_UNKNOWN = (1 << 64) - 1
+
+
+@dataclass
+class ShardSummary:
+    errc: int
+    width: int
+    n: int
+    entry: int
+    exit: int
+    count: int
+    heap: List[int]
+
+    def as_list(self) -> List[int]:
+        return [self.errc, self.width, self.n, self.entry, self.exit, self.count] + list(self.heap)
+
+    @staticmethod
+    def from_list(v) -> "ShardSummary":
+        v = [int(x) for x in v]
+        return ShardSummary(v[0], v[1], v[2], v[3], v[4], v[5], v[6:])
+
+
+def tile_ranges(n_tiles: int, world: int) -> List[tuple]:
+    """Even split of the body's tiles over the ranks."""
+    return [(n_tiles * r // world, n_tiles * (r + 1) // world) for r in range(world)]
+
+
+def settle_entries(sums: List[ShardSummary]) -> List[Optional[int]]:
+    """The exchange step: range r stands when its entry is range r-1's exit
+    (range 0 starts at the payload: exact). Returns, per rank, None when its
+    summary stands, else the entry to index it again from: the previous
+    range's current exit. A chain of k wrong ranges settles in at most k
+    rounds; a range after the one where the path ends is left alone (it
+    holds no records)."""
+    redo: List[Optional[int]] = [None] * len(sums)
+    for r in range(1, len(sums)):
+        want = sums[r - 1].exit
+        if want != ENTRY_UNKNOWN and sums[r].entry != want:
+            redo[r] = want
+    return redo
+
+
+def shard_plan(sums: List[ShardSummary]):
+    """(first record index, records, last flag) per rank from settled
+    summaries: a range after the one where the path ends holds nothing; the
+    message's count clips the ranges."""
+    n = sums[0].n
+    out, first, ended = [], 0, False
+    for s in sums:
+        if ended or first >= n:
+            out.append((min(first, n), 0, False))
+            continue
+        k = min(s.count, n - first)
+        out.append((first, k, False))
+        first += k
+        if s.exit == ENTRY_UNKNOWN:
+            ended = True
+    # the range holding the message's end (or the last one that has records)
+    last = max((i for i, (_, k, _) in enumerate(out) if k), default=0)
+    f, k, _ = out[last]
+    out[last] = (f, k, True)
+    return out
+
+
+class DeviceShardBackend:
+    """The HIP kernels behind ShardedVectorDecoder (one Codec = one
+    workspace: an index and its emit must use the same one)."""
+
+    def __init__(self, codec: Codec):
+        self.cd = codec
+
+    def header(self, wire):
+        return self.cd.parse_vector_header(bytes(wire[:1024].cpu().numpy()))
+
+    def wire_len(self, wire) -> int:
+        return int(wire.numel())
+
+    def index(self, wire, lo, hi, entry) -> ShardSummary:
+        return self.cd.shard_index(wire, lo, hi, entry)
+
+    def emit(self, wire, lo, hi, first, last, count, summary):
+        cd = self.cd
+        out = cd.alloc_batch(count + 1, [max(h, 1) for h in summary.heap[:len(cd.L.dev.spans)]])
+        res = cd.shard_emit(out, wire, lo, hi, first, last)
+        return RecordBatch(cd.L, out.recs[:count], out.heaps), res
+
+
+def shard_decode(backends, wire, world: int, gather, rank: Optional[int] = None):
+    """The protocol of ShardedVectorDecoder. `backends[r]` runs rank r's
+    kernels (one entry when `rank` is given: this process is that rank);
+    `gather(list_of_my_summaries) -> all ranks' summaries`. Returns
+    [(batch, first, result)] for the ranks this process runs."""
+    mine_ranks = [rank] if rank is not None else list(range(world))
+    be0 = backends[0]
+    e, n, w, hl = be0.header(wire)
+    if e:
+        raise ValueError(f"header errc {e}")
+    n_tiles = max(1, (be0.wire_len(wire) - hl + TILE_BYTES - 1) // TILE_BYTES)
+    rng = tile_ranges(n_tiles, world)
+    local = {r: backends[i].index(wire, rng[r][0], rng[r][1], ENTRY_UNKNOWN)
+             for i, r in enumerate(mine_ranks)}
+    rounds = 0
+    for _ in range(world):
+        sums = gather([local[r] for r in mine_ranks])
+        redo = settle_entries(sums)
+        if not any(x is not None for x in redo):
+            break
+        rounds += 1
+        for i, r in enumerate(mine_ranks):
+            if redo[r] is not None:
+                local[r] = backends[i].index(wire, rng[r][0], rng[r][1], redo[r])
+    plan = shard_plan(sums)
+    out = []
+    for i, r in enumerate(mine_ranks):
+        first, k, last = plan[r]
+        b, res = backends[i].emit(wire, rng[r][0], rng[r][1], first, last, k, local[r])
+        out.append((b, first, res))
+    return out, rounds
+
+
+class ShardedVectorDecoder:
+    """Decode of one serialize(std::vector<T>) message that every rank holds
+    (one GPU per rank): rank r decodes the records that start in its share of
+    the body's 16 KiB tiles into rank-local buffers (record 0 = global record
+    `first`; heaps from element 0). One all-gather of a ~100-byte summary per
+    rank per round (normally one round) is the only collective."""
+
+    def __init__(self, codec: Codec, group=None, backend=None):
+        self.be = backend or DeviceShardBackend(codec)
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.rounds = 0
+
+    def _gather(self, mine: List[ShardSummary]) -> List[ShardSummary]:
+        v = mine[0].as_list()
+        t = torch.tensor([x - (1 << 64) if x >= (1 << 63) else x for x in v], dtype=torch.int64)
+        if dist.get_backend(self.group) != "gloo":
+            t = t.to(self.be.cd.device)
+        outs = [torch.zeros_like(t) for _ in range(self.world)]
+        dist.all_gather(outs, t, group=self.group)
+        return [ShardSummary.from_list([x & ((1 << 64) - 1) for x in o.tolist()]) for o in outs]
+
+    def decode(self, wire):
+        """Returns (RecordBatch of this rank's records, first, result)."""
+        out, self.rounds = shard_decode([self.be], wire, self.world, self._gather, self.rank)
+        return out[0]

@@ -192,6 +192,32 @@ class Codec:
                                              _stream(stream)), "spk_decode_body")
         return self.res_buf
 
+    def shard_index(self, wire: torch.Tensor, tile_lo: int, tile_hi: int, entry: int,
+                    stream=None):
+        """spk_decode_shard_index -> host ShardSummary (synchronises)."""
+        from .parallel import ShardSummary
+        ws = self.workspace(MODE_VECTOR, 0, wire.numel())
+        if not hasattr(self, "_shard_buf"):
+            self._shard_buf = torch.zeros(ct.sizeof(C.spk_shard_t), dtype=torch.uint8,
+                                          device=self.device)
+        self._check(self.lib.spk_decode_shard_index(
+            self.L.ptr, _p(wire), wire.numel(), tile_lo, tile_hi, entry, _p(self._shard_buf),
+            _p(ws), ws.numel(), _stream(stream)), "spk_decode_shard_index")
+        r = C.spk_shard_t.from_buffer_copy(bytes(self._shard_buf.cpu().numpy()))
+        return ShardSummary(r.errc, r.width, r.n, r.entry, r.exit, r.count, list(r.heap))
+
+    def shard_emit(self, out: RecordBatch, wire: torch.Tensor, tile_lo: int, tile_hi: int,
+                   first: int, last: bool, stream=None) -> C.spk_dresult_t:
+        """spk_decode_shard_emit into `out` (same workspace as shard_index)."""
+        ws = self.workspace(MODE_VECTOR, 0, wire.numel())  # the index pass's buffer
+        caps = [h.numel() // sp.elem.size for h, sp in zip(out.heaps, self.L.dev.spans)]
+        hc = (ct.c_uint64 * max(len(caps), 1))(*(caps or [0]))
+        self._check(self.lib.spk_decode_shard_emit(
+            self.L.ptr, _p(wire), wire.numel(), tile_lo, tile_hi, first, 1 if last else 0,
+            _p(out.recs), out.n, self._heap_ptrs(out.heaps), hc, _p(self.res_buf), _p(ws),
+            ws.numel(), _stream(stream)), "spk_decode_shard_emit")
+        return self.result()
+
     def parse_vector_header(self, host_bytes: bytes):
         """Host parse of a VECTOR message head: (errc, n, width, header_len)."""
         n, w, hl = ct.c_uint64(), ct.c_uint32(), ct.c_uint32()
