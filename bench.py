@@ -587,7 +587,13 @@ def concat_bench(torch, dist, world, rank, dev, n, reps=3):
     t_d2h = timed(lambda: host.copy_(body[:mine], non_blocking=True))
     total = sp.total_bytes
     gbs = lambda b, t: round(b / t / 1e9, 2)
+    dec = None
+    try:
+        dec = sharded_decode_bench(torch, dist, world, rank, dev, timed)
+    except Exception as e:  # never lose the concat numbers
+        dec = {"error": f"{type(e).__name__}: {e}"}
     return {
+        "sharded_decode": dec,
         "workload": f"one serialize(vector<Rec64>) message of {world} x {n} records "
                     f"({total / 2**30:.2f} GiB), bodies encoded on their own ranks",
         "records_per_rank": n, "message_bytes": total, "width": sp.width,
@@ -689,6 +695,52 @@ def host_path_pipelined(wl, torch, dev, chunk_records=4_000_000, reps=3):
             "note": "pipelined: per record chunk H2D records -> spk_encode_body -> D2H wire and "
                     "H2D wire -> spk_decode_body -> D2H records, three HIP streams, pinned "
                     "host buffers, header parsed on the host (spk_parse_vector_header)"}
+
+
+def sharded_decode_bench(torch, dist, world, rank, dev, timed, per_rank=2_000_000):
+    """N>1: ONE C4-shaped message (vector<Outer>, world x 2M records) that
+    every rank holds, decoded by ShardedVectorDecoder (each rank indexes and
+    emits the records starting in its 1/world of the body; one all-gather of
+    summaries) vs the whole message decoded by one GPU (rank 0)."""
+    from yalantinglibs_amd import layout as LY
+    from yalantinglibs_amd import parallel as PAR
+    from yalantinglibs_amd import struct_pack as SP
+    cd = SP.Codec(LY.case_layout("outer"), device=dev)
+    n = per_rank * world
+    batch = SP.synth_batch(cd, "outer", n, SEEDS["outer"], 16)
+    wire, _ = cd.serialize(batch, SP.MODE_VECTOR)
+    del batch
+    torch.cuda.empty_cache()
+    dec = PAR.ShardedVectorDecoder(cd)
+    out = [None]
+
+    def run():
+        out[0] = dec.decode(wire)
+    t_sh = timed(run)
+    b, first, res = out[0]
+    counts = torch.tensor([b.n, int(res.errc)], dtype=torch.int64,
+                          device=torch.device("cpu") if dist.get_backend() == "gloo" else dev)
+    dist.all_reduce(counts)
+    del out, b
+    torch.cuda.empty_cache()
+    single = None
+    if rank == 0:
+        one = cd.alloc_batch(n, [int(wire.numel())])
+        ts = []
+        for _ in range(3):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            cd.deserialize_to(one, wire, SP.MODE_VECTOR)
+            torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - t0)
+        single = min(ts[1:])
+        del one
+    return {"records": n, "message_bytes": int(wire.numel()), "ms": round(t_sh * 1e3, 3),
+            "exchange_rounds": dec.rounds, "records_decoded": int(counts[0].item()),
+            "errc_sum": int(counts[1].item()),
+            "single_gpu_ms": round(single * 1e3, 3) if single else None,
+            "note": "sharded: header parse + index + summary all-gather + emit on every rank, "
+                    "max over ranks; single_gpu_ms: rank 0 decodes the whole message"}
 
 
 def main():

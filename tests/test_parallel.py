@@ -108,3 +108,131 @@ def test_width_agreement_uses_global_count():
     # 200 records per shard: each shard alone would use width 1, the message
     # of 400 records needs width 2 (calculate_size.hpp:79,426-447)
     assert PAR.width_of(200) == 1 and PAR.width_of(400) == 2
+
+
+# ---- sharded decode of one vector message: the exchange protocol ----------
+class _OracleShardBackend:
+    """CPU stand-in for the kernels behind ShardedVectorDecoder (checker
+    only): exact from a true record start; from an unknown entry it guesses
+    WRONG (start + 1, exit + 1) so that the protocol has to repair it."""
+
+    def __init__(self, L, recs, heaps, wire):
+        self.L, self.wire = L, wire
+        o = C.load_oracle()
+        self.hl = None
+        lib = C.load_codec()
+        n, w, hl = ct.c_uint64(), ct.c_uint32(), ct.c_uint32()
+        buf = (ct.c_uint8 * len(wire)).from_buffer_copy(wire)
+        assert lib.spk_parse_vector_header(L.ptr, buf, len(wire), ct.byref(n), ct.byref(w),
+                                           ct.byref(hl)) == 0
+        self.n, self.w, self.hl = n.value, w.value, hl.value
+        # true record starts from the oracle's per-record body sizes
+        hp = (ct.c_void_p * max(len(heaps), 1))(*[h.ctypes.data if h.size else 0 for h in heaps])
+        sizes = []
+        tmp = np.zeros(len(wire) + 16, np.uint8)
+        for i in range(len(recs)):
+            wr = ct.c_uint64()
+            assert o.spko_encode_body(L.ptr, 1, H._ptr(recs[i:i + 1]), hp, self.w,
+                                      H._ptr(tmp), tmp.size, ct.byref(wr)) == 0
+            sizes.append(wr.value)
+        self.starts = np.concatenate([[self.hl], self.hl + np.cumsum(sizes)]).astype(np.int64)
+
+    def header(self, wire):
+        return 0, self.n, self.w, self.hl
+
+    def wire_len(self, wire):
+        return len(self.wire)
+
+    def _next(self, pos):
+        """first true record start >= pos, or None past the last record"""
+        i = int(np.searchsorted(self.starts, pos))
+        if i >= len(self.starts) or self.starts[i] >= len(self.wire):
+            return None
+        return int(self.starts[i])
+
+    def index(self, wire, lo, hi, entry):
+        b0, b1 = self.hl + lo * PAR.TILE_BYTES, self.hl + hi * PAR.TILE_BYTES
+        ns = len(self.L.dev.spans)
+        if lo == 0:
+            entry = self.hl
+        true_starts = set(int(x) for x in self.starts[:-1])
+        if entry == PAR.ENTRY_UNKNOWN or (entry not in true_starts and entry < len(self.wire)):
+            # a wrong path: entry, exit and count all off
+            e0 = entry if entry != PAR.ENTRY_UNKNOWN else (self._next(b0) or b0) + 1
+            ex = self._next(b1)
+            return PAR.ShardSummary(0, self.w, self.n, e0,
+                                    PAR.ENTRY_UNKNOWN if ex is None else ex + 1, 7, [7] * ns)
+        s = self.starts[:-1]
+        end = max(b1, entry)
+        k = int(((s >= entry) & (s < end)).sum())
+        ex = self._next(end)
+        return PAR.ShardSummary(0, self.w, self.n, entry,
+                                PAR.ENTRY_UNKNOWN if ex is None else ex, k, [0] * ns)
+
+    def emit(self, wire, lo, hi, first, last, count, summary):
+        # decode records [first, first + count) from their body bytes with the oracle
+        a, b = int(self.starts[first]), int(self.starts[first + count])
+        lib = C.load_codec()
+        hb = (ct.c_uint8 * 512)()
+        k = lib.spk_vector_header(self.L.ptr, count, self.w, hb, 512)
+        msg = bytes(hb[:k]) + bytes(self.wire[a:b])
+        res, recs, heaps, _ = H.oracle_decode(self.L, C.SPK_MODE_VECTOR, msg)
+        assert res.errc == 0 and res.count == count
+        used = [int(res.heap_used[q]) * sp.elem.size for q, sp in enumerate(self.L.dev.spans)]
+        return (recs[:count].tobytes(), [h[:u].tobytes() for h, u in zip(heaps, used)]), res
+
+
+def _shard_worker(rank, world, port, case, n, param, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        L = LY.case_layout(case)
+        _, recs, heaps = synth.make_batch(case, n, 0x5EED + n, param)
+        wire, _, _ = H.oracle_encode(L, C.SPK_MODE_VECTOR, recs, heaps)
+        be = _OracleShardBackend(L, recs, heaps, wire)
+        dec = PAR.ShardedVectorDecoder(None, backend=be)
+        (rec_bytes, heap_bytes), first, res = dec.decode(wire)
+        parts = [None] * world
+        dist.all_gather_object(parts, (first, rec_bytes, heap_bytes, dec.rounds))
+        if rank == 0:
+            # every rank's records re-encoded at the message width, in order == the body
+            o = C.load_oracle()
+            body = b""
+            total = 0
+            for f, rb, hb, _ in parts:
+                assert f == total
+                rr = np.frombuffer(rb, dtype=L.dev.dtype).copy()
+                total += len(rr)
+                if not len(rr):
+                    continue
+                hs = [np.frombuffer(h, np.uint8).copy() for h in hb]
+                hp = (ct.c_void_p * max(len(hs), 1))(*[h.ctypes.data if h.size else 0 for h in hs])
+                buf = np.zeros(len(wire) + 16, np.uint8)
+                wr = ct.c_uint64()
+                assert o.spko_encode_body(L.ptr, len(rr), H._ptr(rr), hp, be.w, H._ptr(buf),
+                                          buf.size, ct.byref(wr)) == 0
+                body += buf[:wr.value].tobytes()
+            q.put((total == n and body == wire[be.hl:], parts[0][3]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,n,param", [("outer", 4000, 16), ("recs", 3000, 300),
+                                          ("var", 3000, 40), ("recs", 40, 20000)])
+def test_sharded_vector_decode_gloo(case, n, param):
+    """ShardedVectorDecoder over gloo (world 2): wrong guesses are repaired by
+    the exchange and the two ranks' records are the message, byte for byte."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, case, n, param, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    ok, rounds = q.get(timeout=10)
+    assert ok and rounds >= 1
