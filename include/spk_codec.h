@@ -81,7 +81,37 @@
  *                                           (unpacker.hpp:1278-1292).
  *   SPK_OP_END {0, 0, 0, 0}                closes the innermost open ARRAY or
  *                                           VARIANT alternative.
- * Heaps are numbered in op order over SPAN, OPTION and ARRAY ops at every
+ *   SPK_OP_COMPAT {rec_off, size, aux}     a struct_pack::compatible<U, ver>
+ *                                           member (U trivially serializable) of
+ *                                           the top-level record: record fields
+ *                                           as OPTION. kind = SPK_OP_COMPAT |
+ *                                           rank << 8, rank = index of `ver` in
+ *                                           the record's sorted distinct versions
+ *                                           (only the order reaches the wire). It
+ *                                           is skipped by the main pass; after
+ *                                           it, one pass per rank writes
+ *                                           [has_value:1][U if present] for that
+ *                                           rank's members of every record, in
+ *                                           record then op order (packer.hpp:
+ *                                           66-78,453-461). Excluded from the
+ *                                           type literal / hash (type_calculate
+ *                                           .hpp:298-303); the message gets a
+ *                                           metainfo byte and a total-length
+ *                                           field of 2/4/8 bytes after it
+ *                                           (calculate_size.hpp:457-470, packer
+ *                                           .hpp:108-130). Decode stops the
+ *                                           version passes, with no error, at the
+ *                                           first member whose has byte would
+ *                                           start at or past that length (an
+ *                                           older writer); members never reached
+ *                                           read as absent; the value read's errc
+ *                                           is dropped as for OPTION; consumed =
+ *                                           max(position, length), skipping
+ *                                           newer versions (unpacker.hpp:
+ *                                           292-366,1354-1376). Requires
+ *                                           SPK_MF_HASH_HEAD and a non-trivial
+ *                                           layout (type_calculate.hpp:868-876).
+ * Heaps are numbered in op order over SPAN, OPTION, ARRAY and COMPAT ops at every
  * nesting level; heap k of an ARRAY holds element records, counted in
  * elements like the others. Decode writes every heap packed in wire order.
  * A trivially-serializable T (SPK_LAYOUT_TRIVIAL) is a single COPY of the
@@ -146,6 +176,9 @@ extern "C" {
 #define SPK_OP_ARRAY 5u
 #define SPK_OP_END 6u
 #define SPK_OP_VARIANT 7u
+#define SPK_OP_COMPAT 8u       /* | rank << 8 (see above)                    */
+#define SPK_OP_KIND(k) ((k) & 0xFFu)
+#define SPK_OP_RANK(k) ((k) >> 8)
 #define SPK_MAX_DEPTH 4u       /* ARRAY / VARIANT nesting levels             */
 
 /* spk_op.aux of an SPK_OP_VARINT */
@@ -165,7 +198,7 @@ extern "C" {
 #define SPK_LAYOUT_TRIVIAL 0x1u   /* is_trivial_serializable<T>: 1 COPY op  */
 
 typedef struct spk_op {
-  uint32_t kind;    /* SPK_OP_COPY | SPAN | OPTION | VARINT | ARRAY | END | VARIANT */
+  uint32_t kind;    /* SPK_OP_COPY | SPAN | OPTION | VARINT | ARRAY | END | VARIANT | COMPAT */
   uint32_t rec_off; /* COPY: source byte offset; SPAN: u32 count offset      */
   uint32_t size;    /* COPY: byte length;       SPAN: element size (bytes)   */
   uint32_t aux;     /* SPAN: u64 heap element-offset field offset; COPY: 0   */

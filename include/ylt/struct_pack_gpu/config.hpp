@@ -117,6 +117,25 @@ using var_int64_t = detail::sint<int64_t>;
 using var_uint32_t = detail::varint<uint32_t>;
 using var_uint64_t = detail::varint<uint64_t>;
 
+// compatible.hpp:21-154: an optional member that is written after the main
+// pass, in the pass of its version (forward / backward compatible fields)
+template <typename T, uint64_t version = 0>
+struct compatible : public std::optional<T> {
+  constexpr compatible() = default;
+  constexpr compatible(const compatible &) = default;
+  constexpr compatible(compatible &&) = default;
+  constexpr compatible(std::optional<T> &&o) : std::optional<T>(std::move(o)) {}
+  constexpr compatible(const std::optional<T> &o) : std::optional<T>(o) {}
+  using std::optional<T>::optional;
+  constexpr compatible &operator=(const compatible &) = default;
+  constexpr compatible &operator=(compatible &&) = default;
+  static constexpr uint64_t version_number = version;
+};
+template <typename T, uint64_t v1, uint64_t v2>
+inline bool operator==(const compatible<T, v1> &a, const compatible<T, v2> &b) {
+  return static_cast<bool>(a) == static_cast<bool>(b) && (!a || *a == *b);
+}
+
 }  // namespace struct_pack
 
 // ---- YLT_REFL(Type, member...) ---------------------------------------------
@@ -227,6 +246,15 @@ template <typename T>
 struct varint_traits<struct_pack::detail::sint<T>> : std::true_type {
   using value_type = T;
   static constexpr bool zigzag = true;
+};
+
+// ---- compatible<T, version> members (compatible.hpp:21-154) ------------------
+template <typename T>
+struct compat_traits : std::false_type {};
+template <typename T, uint64_t V>
+struct compat_traits<struct_pack::compatible<T, V>> : std::true_type {
+  using value_type = T;
+  static constexpr uint64_t version = V;
 };
 
 // ---- YLT_REFL detection: refl_object_to_tuple found by ADL (macro at

@@ -28,6 +28,9 @@ namespace detail {
 struct layout_builder {
   spk_layout L{};
   uint32_t off = 0, align = 1, spans = 0, vars = 0;
+  uint32_t depth = 0;           // record nesting (1: members of the top-level record)
+  uint64_t vers[SPK_MAX_OPS];   // sorted distinct compatible versions of the record
+  uint32_t n_vers = 0;
   uint32_t place(uint32_t size, uint32_t al) {
     off = (off + al - 1) / al * al;
     const uint32_t o = off;
@@ -80,14 +83,52 @@ void flatten_into(layout_builder &b) {
                   "MI355X codec: optional of a non-trivially-serializable value is "
                   "outside the flat record model");
     b.span(sizeof(E), SPK_OP_OPTION);
+  } else if constexpr (is_compat_v<T>) {
+    using E = remove_cvref_t<typename T::value_type>;
+    static_assert(is_trivially_serializable<E>(),
+                  "MI355X codec: compatible of a non-trivially-serializable value is "
+                  "outside the flat record model");
+    if (b.depth != 1)
+      throw std::logic_error("MI355X codec: compatible members only at the top level");
+    uint32_t rank = 0;
+    while (b.vers[rank] != compat_traits<T>::version) ++rank;
+    b.span(sizeof(E), SPK_OP_COMPAT | rank << 8);
   } else if constexpr (is_std_array<T>::value) {
     for (std::size_t i = 0; i < std::tuple_size_v<T>; ++i)
       flatten_into<typename T::value_type>(b);
   } else {
     using M = members_tuple_t<T>;
+    ++b.depth;
     [&]<std::size_t... I>(std::index_sequence<I...>) {
       (flatten_into<std::tuple_element_t<I, M>>(b), ...);
     }(std::make_index_sequence<std::tuple_size_v<M>>{});
+    --b.depth;
+  }
+}
+
+// the sorted distinct versions of T's compatible members (type_calculate.hpp:
+// 531-556: the order of the version passes)
+template <typename F>
+void add_version(layout_builder &b) {
+  if constexpr (is_compat_v<F>) {
+    constexpr uint64_t v = compat_traits<F>::version;
+    uint32_t j = 0;
+    while (j < b.n_vers && b.vers[j] < v) ++j;
+    if (j < b.n_vers && b.vers[j] == v) return;
+    for (uint32_t k = b.n_vers; k > j; --k) b.vers[k] = b.vers[k - 1];
+    b.vers[j] = v;
+    ++b.n_vers;
+  }
+}
+template <typename M, std::size_t... I>
+void add_versions(layout_builder &b, std::index_sequence<I...>) {
+  (add_version<std::tuple_element_t<I, M>>(b), ...);
+}
+template <typename T>
+void collect_versions(layout_builder &b) {
+  if constexpr (is_record_v<T> && !is_trivially_serializable<T>()) {
+    using M = members_tuple_t<T>;
+    add_versions<M>(b, std::make_index_sequence<std::tuple_size_v<M>>{});
   }
 }
 
@@ -128,6 +169,7 @@ spk_layout make_spk_layout() {
   using namespace detail;
   layout_builder b;
   b.L.abi = SPK_ABI_VERSION;
+  collect_versions<T>(b);
   flatten_into<T>(b);
   if constexpr (is_trivially_serializable<T>()) {
     b.L.flags = SPK_LAYOUT_TRIVIAL;
@@ -183,7 +225,7 @@ void to_device(const T &v, marshal_state &s) {
     std::memcpy(s.rec + op.aux, &eoff, 8);
     const auto *p = reinterpret_cast<const uint8_t *>(v.data());
     heap.insert(heap.end(), p, p + static_cast<std::size_t>(cnt) * op.size);
-  } else if constexpr (is_std_optional<T>::value) {
+  } else if constexpr (is_std_optional<T>::value || is_compat_v<T>) {
     const spk_op &op = s.L->ops[s.op++];
     auto &heap = (*s.heaps)[s.span++];
     const uint32_t cnt = v.has_value() ? 1u : 0u;
@@ -243,7 +285,7 @@ void from_device(T &v, unmarshal_state &s) {
       v.resize(cnt);
       if (cnt) std::memcpy(v.data(), src, static_cast<std::size_t>(cnt) * op.size);
     }
-  } else if constexpr (is_std_optional<T>::value) {
+  } else if constexpr (is_std_optional<T>::value || is_compat_v<T>) {
     const spk_op &op = s.L->ops[s.op++];
     const uint8_t *heap = s.heaps[s.span++];
     uint32_t cnt;

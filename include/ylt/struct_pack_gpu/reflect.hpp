@@ -48,10 +48,12 @@ constexpr bool is_fundamental_v = std::is_arithmetic_v<T> || std::is_enum_v<T>;
 template <typename T>
 constexpr bool is_varint_v = varint_traits<T>::value;
 template <typename T>
+constexpr bool is_compat_v = compat_traits<T>::value;
+template <typename T>
 constexpr bool is_aggregate_record_v = std::is_aggregate_v<T> && std::is_class_v<T> &&
                                        !is_std_array<T>::value && !is_string_v<T> &&
                                        !is_container_v<T> && !is_std_optional<T>::value &&
-                                       !is_varint_v<T> && !is_ylt_refl_v<T>;
+                                       !is_varint_v<T> && !is_compat_v<T> && !is_ylt_refl_v<T>;
 template <typename T>
 constexpr bool is_record_v = is_aggregate_record_v<T> || (std::is_class_v<T> && is_ylt_refl_v<T>);
 

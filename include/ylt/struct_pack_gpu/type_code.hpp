@@ -89,8 +89,8 @@ constexpr bool is_trivially_serializable() {
   } else if constexpr (is_std_array<T>::value) {
     return is_trivially_serializable<typename T::value_type>();
   } else if constexpr (is_string_v<T> || is_container_v<T> || is_std_optional<T>::value ||
-                       is_varint_v<T>) {
-    return false;  // reflection.hpp:872,899-901
+                       is_varint_v<T> || is_compat_v<T>) {
+    return false;  // reflection.hpp:872-876,899-901
   } else if constexpr (is_ylt_refl_v<T>) {
     return false;  // user_defined_refl: member by member (reflection.hpp:896-898)
   } else {
@@ -110,7 +110,7 @@ template <typename T>
 constexpr bool has_container() {
   if constexpr (is_string_v<T> || is_container_v<T>)
     return true;
-  else if constexpr (is_std_array<T>::value || is_std_optional<T>::value)
+  else if constexpr (is_std_array<T>::value || is_std_optional<T>::value || is_compat_v<T>)
     return has_container<typename T::value_type>();  // type_calculate.hpp:846-849
   else if constexpr (is_record_v<T>) {
     using M = members_tuple_t<T>;
@@ -197,6 +197,7 @@ constexpr lit_t type_literal() {
     using V = typename varint_traits<T>::value_type;
     constexpr bool zz = varint_traits<T>::zigzag;
     l.push(sizeof(V) == 4 ? (zz ? TID_VINT32 : TID_VUINT32) : (zz ? TID_VINT64 : TID_VUINT64));
+  } else if constexpr (is_compat_v<T>) {  // not in the literal (type_calculate.hpp:298-303)
   } else if constexpr (is_std_optional<T>::value) {  // type_calculate.hpp:273-278
     l.push(TID_OPTIONAL);
     l.append(type_literal<remove_cvref_t<typename T::value_type>>());

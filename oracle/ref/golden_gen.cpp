@@ -111,6 +111,10 @@ static int cmd_kat() {
   kat_one<std::vector<Vnt>>(os, "vector<Vnt>", first);
   kat_one<std::variant<int32_t, std::string>>(os, "variant<int32_t,string>", first);
   kat_one<std::vector<Deep>>(os, "vector<Deep>", first);
+  kat_one<Cmp>(os, "Cmp", first);
+  kat_one<std::vector<Cmp>>(os, "vector<Cmp>", first);
+  kat_one<CmpOld>(os, "CmpOld", first);
+  kat_one<CmpNew>(os, "CmpNew", first);
   kat_one<uint8_t, uint16_t, uint32_t, uint64_t, int8_t, int16_t, int64_t,
           bool, char, float, double>(os, "fundamentals", first);
   os << "\n}\n";
@@ -126,9 +130,28 @@ struct Args {
   std::string conf;
 };
 
+template <typename T>
+struct elem_of {
+  using type = T;
+};
+template <typename T>
+struct elem_of<std::vector<T>> {
+  using type = T;
+};
+// DISABLE_ALL_META_INFO is a compile error with compatible members
+// (type_calculate.hpp:868-876): such cases fall back to the default config
+template <uint64_t conf, typename T>
+static constexpr uint64_t conf_for() {
+  if constexpr (conf == sp_config::DISABLE_ALL_META_INFO &&
+                kHasCompat<typename elem_of<T>::type>)
+    return sp_config::DEFAULT;
+  else
+    return conf;
+}
+
 template <uint64_t conf, typename T>
 static void ser_append(std::string &out, const T &v) {
-  struct_pack::serialize_to<conf>(out, v);
+  struct_pack::serialize_to<conf_for<conf, T>()>(out, v);
 }
 
 template <typename T, typename Gen>
@@ -199,6 +222,12 @@ static bool with_case(const Args &a, F &&f) {
     return f.template operator()<AlRec>([=](AlRec &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "vnt")
     return f.template operator()<Vnt>([=](Vnt &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "cmp")
+    return f.template operator()<Cmp>([=](Cmp &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "cmpold")
+    return f.template operator()<CmpOld>([=](CmpOld &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "cmpnew")
+    return f.template operator()<CmpNew>([=](CmpNew &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "deep")
     return f.template operator()<Deep>([=](Deep &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "rect")  // C1: benchmark rect<int> default values
@@ -289,8 +318,9 @@ static int cmd_frames(const Args &a, bool req, uint32_t fid, uint32_t seq_base,
 //   trunc <len>            keep the first <len> bytes
 //   set <pos> <byte>       overwrite one byte
 // Output: one JSON object per line {errc, consume, reenc_hex|null}
-template <uint64_t conf, typename T>
+template <uint64_t conf0, typename T>
 static void decode_report(const std::string &buf, std::ostream &os) {
+  constexpr uint64_t conf = conf_for<conf0, T>();
   T obj{};
   size_t consume = 0;
   auto ec = struct_pack::deserialize_to<conf>(obj, buf.data(), buf.size(),

@@ -215,6 +215,36 @@ struct Vnt {
   std::vector<std::variant<int64_t, std::string>> list;
 };
 
+// ---- struct_pack::compatible<T, version> members (SPK_OP_COMPAT) --------
+// Cmp is the record; CmpOld is an older writer without the compatible members
+// and CmpNew a newer one with an extra version: all three share one type
+// code (compatible members are not in the literal).
+struct Cmp {
+  int32_t id;
+  struct_pack::compatible<int64_t, 20210101> a;
+  std::string name;
+  struct_pack::compatible<double, 20240101> c;
+  struct_pack::compatible<int16_t, 20210101> b;
+};
+struct CmpOld {
+  int32_t id;
+  std::string name;
+};
+struct CmpNew {
+  int32_t id;
+  struct_pack::compatible<int64_t, 20210101> a;
+  std::string name;
+  struct_pack::compatible<double, 20240101> c;
+  struct_pack::compatible<int16_t, 20210101> b;
+  struct_pack::compatible<int32_t, 20250101> d;
+};
+template <typename T>
+constexpr bool kHasCompat = false;
+template <>
+inline constexpr bool kHasCompat<Cmp> = true;
+template <>
+inline constexpr bool kHasCompat<CmpNew> = true;
+
 namespace spk_gold {
 
 inline Rec64 make_rec64(uint64_t seed, uint64_t i) {
@@ -418,6 +448,27 @@ inline void fill(Vnt &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
     else
       o.list.emplace_back((int64_t)(h >> 1));
   }
+}
+
+template <typename C>
+inline void fill_cmp(C &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
+  o.id = (int32_t)(uint32_t)rnd(seed, i, 0);
+  const uint64_t m = rnd(seed, i, 6);
+  if (m & 1) o.a = (int64_t)rnd(seed, i, 2);
+  o.name = make_chars(seed, i, maxlen);
+  if (m & 2) o.c = rd(rnd(seed, i, 3));
+  if (m & 4) o.b = (int16_t)rnd(seed, i, 4);
+}
+inline void fill(Cmp &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
+  fill_cmp(o, seed, i, maxlen);
+}
+inline void fill(CmpNew &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
+  fill_cmp(o, seed, i, maxlen);
+  if (rnd(seed, i, 6) & 8) o.d = (int32_t)(uint32_t)rnd(seed, i, 5);
+}
+inline void fill(CmpOld &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
+  o.id = (int32_t)(uint32_t)rnd(seed, i, 0);
+  o.name = make_chars(seed, i, maxlen);
 }
 
 inline void fill(Al8 &o, uint64_t seed, uint64_t i, uint32_t) {

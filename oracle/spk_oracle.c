@@ -57,7 +57,18 @@ static void vi_store(uint8_t *rec, const spk_op *op, uint64_t v) {
 /* Heaps are numbered in op order over SPAN, OPTION and ARRAY ops at every
  * nesting level; an ARRAY's element ops run to its matching END. */
 static int is_heap_op(uint32_t k) {
-  return k == SPK_OP_SPAN || k == SPK_OP_OPTION || k == SPK_OP_ARRAY;
+  k = SPK_OP_KIND(k);
+  return k == SPK_OP_SPAN || k == SPK_OP_OPTION || k == SPK_OP_ARRAY || k == SPK_OP_COMPAT;
+}
+/* compatible<U, ver> members: top-level ops only (include/spk_codec.h) */
+static int is_compat(uint32_t k) { return SPK_OP_KIND(k) == SPK_OP_COMPAT; }
+/* number of distinct version ranks (max rank + 1), 0 without compat members */
+static unsigned compat_ranks(const spk_layout *L) {
+  unsigned r = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i)
+    if (is_compat(L->ops[i].kind) && SPK_OP_RANK(L->ops[i].kind) + 1 > r)
+      r = SPK_OP_RANK(L->ops[i].kind) + 1;
+  return r;
 }
 static unsigned heap_of(const spk_layout *L, uint32_t i) {
   unsigned k = 0;
@@ -94,13 +105,13 @@ static uint32_t alt_start(const spk_layout *L, uint32_t i, uint32_t a) {
 static uint64_t rec_count(const uint8_t *rec, const spk_op *op) {
   uint32_t c;
   memcpy(&c, rec + op->rec_off, 4);
-  if (op->kind == SPK_OP_OPTION) return c != 0; /* has_value() */
+  if (op->kind == SPK_OP_OPTION || is_compat(op->kind)) return c != 0; /* has_value() */
   return c;
 }
 /* prefix bytes of a SPAN / ARRAY (container length, width w) or an OPTION
  * (the bool has_value: write_wrapper<sizeof(bool)>, packer.hpp:382-388) */
 static unsigned op_pw(const spk_op *op, unsigned w) {
-  return op->kind == SPK_OP_OPTION ? 1u : w;
+  return (op->kind == SPK_OP_OPTION || is_compat(op->kind)) ? 1u : w;
 }
 static uint64_t rec_heapoff(const uint8_t *rec, const spk_op *op) {
   uint64_t o;
@@ -121,23 +132,35 @@ static unsigned width_bits(unsigned w) {
 
 /* Header shape: check_has_metainfo (type_calculate.hpp:884-891),
  * get_serialize_runtime_info (calculate_size.hpp:407-474) and
- * serialize_metainfo (packer.hpp:100-139). Compatible fields unsupported. */
+ * serialize_metainfo (packer.hpp:100-139). With compatible members the
+ * metainfo byte is always present and is followed by the total message
+ * length in 2/4/8 bytes; `body` = every byte after the header. */
 typedef struct hdr_t {
-  unsigned head, lit, has_meta, len;
+  unsigned head, lit, has_meta, len, lenw;
   uint8_t meta;
+  uint64_t total;
 } hdr_t;
 
-static hdr_t header_shape(const spk_msgfmt *f, unsigned w) {
+static hdr_t header_shape(const spk_msgfmt *f, unsigned w, int compat, uint64_t body) {
   hdr_t h;
   unsigned has_container = (f->flags & SPK_MF_HAS_CONTAINER) != 0;
   h.head = (f->flags & SPK_MF_HASH_HEAD) != 0;
   h.lit = h.head && (f->flags & SPK_MF_TYPE_LITERAL);
-  unsigned meta_fixed = h.lit || (!h.head && has_container);
+  unsigned meta_fixed = compat || h.lit || (!h.head && has_container);
   if (!has_container) w = 1;
   h.has_meta = meta_fixed || w > 1;
   h.meta = (uint8_t)(width_bits(w) | (h.lit ? 0x04u : 0u));
   h.len = (h.head ? 4u : 0u) + (h.has_meta ? 1u : 0u) +
           (h.lit ? f->literal_len + 1u : 0u);
+  h.lenw = 0;
+  if (compat && h.head) { /* calculate_size.hpp:457-470 */
+    const uint64_t l = h.len + body;
+    if (l + 2 < (1ull << 16)) h.lenw = 2, h.meta |= 1;
+    else if (l + 4 < (1ull << 32)) h.lenw = 4, h.meta |= 2;
+    else h.lenw = 8, h.meta |= 3;
+  }
+  h.len += h.lenw;
+  h.total = h.len + body;
   return h;
 }
 
@@ -147,6 +170,10 @@ static uint8_t *write_header(uint8_t *p, const spk_msgfmt *f, const hdr_t *h) {
     p += 4;
   }
   if (h->has_meta) *p++ = h->meta; /* packer.hpp:108-110 */
+  if (h->lenw) {                   /* packer.hpp:111-130: info_.size() */
+    put_le(p, h->total, h->lenw);
+    p += h->lenw;
+  }
   if (h->lit) {                    /* packer.hpp:132-137: literal + NUL */
     memcpy(p, f->literal, f->literal_len);
     p += f->literal_len;
@@ -167,6 +194,8 @@ static void ops_size(const spk_layout *L, uint32_t i0, uint32_t i1, const uint8_
     const spk_op *op = &L->ops[i];
     if (op->kind == SPK_OP_COPY) {
       *bytes += op->size;
+    } else if (is_compat(op->kind)) { /* calculate_size.hpp:100-105 (optional) */
+      *bytes += 1 + rec_count(rec, op) * op->size;
     } else if (op->kind == SPK_OP_VARINT) {
       *bytes += vi_len(vi_value(rec, op));
     } else if (op->kind == SPK_OP_OPTION) {
@@ -215,6 +244,8 @@ static uint8_t *ops_write(const spk_layout *L, uint32_t i0, uint32_t i1, const u
     if (op->kind == SPK_OP_COPY) { /* write_wrapper<sizeof(T)> :264-267 */
       memcpy(p, rec + op->rec_off, op->size);
       p += op->size;
+    }
+    else if (is_compat(op->kind)) { /* version UINT64_MAX: nothing (:246-249) */
     }
     else if (op->kind == SPK_OP_VARINT) { /* serialize_varint :245-268 */
       uint64_t v = vi_value(rec, op);
@@ -267,6 +298,24 @@ static uint8_t *write_record(const spk_layout *L, const uint8_t *rec,
   return ops_write(L, 0, L->n_ops, rec, heaps, w, p);
 }
 
+/* the version pass of rank `rk` over one record (packer.hpp:453-461):
+ * [has_value][U] for each compatible member of that version */
+static uint8_t *write_compat(const spk_layout *L, unsigned rk, const uint8_t *rec,
+                             const void *const *heaps, uint8_t *p) {
+  for (uint32_t i = 0; i < L->n_ops; ++i) {
+    const spk_op *op = &L->ops[i];
+    if (!is_compat(op->kind) || SPK_OP_RANK(op->kind) != rk) continue;
+    const uint64_t c = rec_count(rec, op);
+    *p++ = (uint8_t)c;
+    if (c) {
+      memcpy(p, (const uint8_t *)heaps[heap_of(L, i)] + rec_heapoff(rec, op) * op->size,
+             op->size);
+      p += op->size;
+    }
+  }
+  return p;
+}
+
 int spko_plan(const spk_layout *L, int mode, uint64_t n, const void *recs,
               const void *const *heaps, spk_plan_t *plan) {
   if (!L || !plan || (n && !recs)) return SPK_E_ARG;
@@ -283,14 +332,14 @@ int spko_plan(const spk_layout *L, int mode, uint64_t n, const void *recs,
       cnts += c;
     }
     unsigned w = width_of(maxc);
-    hdr_t h = header_shape(&L->fmt_vector, w);
+    hdr_t h = header_shape(&L->fmt_vector, w, compat_ranks(L) > 0, w + var + cnts * w);
     plan->max_count = maxc;
     plan->var_bytes = var;
     plan->width = w;
     plan->header_bytes = h.len + w;
     plan->metainfo = h.meta;
     plan->has_meta = h.has_meta;
-    plan->total_bytes = h.len + w + var + cnts * w;
+    plan->total_bytes = h.total;
   }
   else if (mode == SPK_MODE_MESSAGES) {
     uint64_t tot = 0, maxc = 0, var = 0;
@@ -298,10 +347,10 @@ int spko_plan(const spk_layout *L, int mode, uint64_t n, const void *recs,
       uint64_t b, c, m;
       rec_size(L, r + i * L->rec_stride, heaps, &b, &c, &m);
       unsigned w = width_of(m);
-      hdr_t h = header_shape(&L->fmt_one, w);
+      hdr_t h = header_shape(&L->fmt_one, w, compat_ranks(L) > 0, b + c * w);
       if (m > maxc) maxc = m;
       var += b;
-      tot += h.len + b + c * w;
+      tot += h.total;
     }
     plan->max_count = maxc;
     plan->var_bytes = var;
@@ -325,12 +374,16 @@ int spko_encode(const spk_layout *L, int mode, uint64_t n, const void *recs,
   uint8_t *p = (uint8_t *)out;
   if (mode == SPK_MODE_VECTOR) {
     unsigned w = plan.width;
-    hdr_t h = header_shape(&L->fmt_vector, w);
+    hdr_t h = header_shape(&L->fmt_vector, w, compat_ranks(L) > 0,
+                           plan.total_bytes - plan.header_bytes + w);
     p = write_header(p, &L->fmt_vector, &h);
     put_le(p, n, w); /* outer vector length prefix */
     p += w;
     for (uint64_t i = 0; i < n; ++i)
       p = write_record(L, r + i * L->rec_stride, heaps, w, p);
+    for (unsigned rk = 0; rk < compat_ranks(L); ++rk) /* packer.hpp:66-78 */
+      for (uint64_t i = 0; i < n; ++i)
+        p = write_compat(L, rk, r + i * L->rec_stride, heaps, p);
   }
   else {
     uint8_t *base = p;
@@ -339,10 +392,11 @@ int spko_encode(const spk_layout *L, int mode, uint64_t n, const void *recs,
       uint64_t b, c, m;
       rec_size(L, rec, heaps, &b, &c, &m);
       unsigned w = width_of(m);
-      hdr_t h = header_shape(&L->fmt_one, w);
+      hdr_t h = header_shape(&L->fmt_one, w, compat_ranks(L) > 0, b + c * w);
       if (msg_offsets) msg_offsets[i] = (uint64_t)(p - base);
       p = write_header(p, &L->fmt_one, &h);
       p = write_record(L, rec, heaps, w, p);
+      for (unsigned rk = 0; rk < compat_ranks(L); ++rk) p = write_compat(L, rk, rec, heaps, p);
     }
     if (msg_offsets) msg_offsets[n] = (uint64_t)(p - base);
   }
@@ -352,7 +406,8 @@ int spko_encode(const spk_layout *L, int mode, uint64_t n, const void *recs,
 int spko_encode_body(const spk_layout *L, uint64_t n, const void *recs,
                      const void *const *heaps, unsigned width, void *out,
                      uint64_t out_cap, uint64_t *written) {
-  if (!L || (n && !recs) || (width != 1 && width != 2 && width != 4 && width != 8))
+  if (!L || (n && !recs) || (width != 1 && width != 2 && width != 4 && width != 8) ||
+      compat_ranks(L)) /* the version passes trail the whole body */
     return SPK_E_ARG;
   const uint8_t *r = (const uint8_t *)recs;
   uint64_t tot = 0;
@@ -440,6 +495,15 @@ static int32_t ops_read(dctx_t *c, rd_t *r, unsigned w, uint32_t i0, uint32_t i1
     if (op->kind == SPK_OP_COPY) {
       if (!rd_take(r, op->size, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
       if (rec) memcpy(rec + op->rec_off, p, op->size);
+      continue;
+    }
+    if (is_compat(op->kind)) { /* main pass: absent until its version pass */
+      if (rec) {
+        const uint32_t z = 0;
+        const uint64_t off = c->used[heap_of(L, i)];
+        memcpy(rec + op->rec_off, &z, 4);
+        memcpy(rec + op->aux, &off, 8);
+      }
       continue;
     }
     if (op->kind == SPK_OP_VARINT) { /* deserialize_varint_impl :270-292 */
@@ -549,6 +613,43 @@ static int32_t read_record(dctx_t *c, rd_t *r, unsigned w, uint8_t *rec) {
   return ops_read(c, r, w, 0, L->n_ops, rec);
 }
 
+/* the version pass of rank `rk` over one record (unpacker.hpp:1354-1376).
+ * Returns 1 when the reader reached data_len before a member: the legal end
+ * of an older writer's message (size_type_ = UCHAR_MAX, :360-365). */
+static int read_compat(dctx_t *c, rd_t *r, const uint8_t *msg, uint64_t data_len,
+                       unsigned rk, uint8_t *rec, int32_t *err) {
+  const spk_layout *L = c->L;
+  const uint8_t *p;
+  for (uint32_t i = 0; i < L->n_ops; ++i) {
+    const spk_op *op = &L->ops[i];
+    if (!is_compat(op->kind) || SPK_OP_RANK(op->kind) != rk) continue;
+    if ((uint64_t)(r->now - msg) >= data_len) return 1;
+    if (!rd_take(r, 1, &p)) {
+      *err = SPK_ERRC_NO_BUFFER_SPACE;
+      return 1;
+    }
+    if (!p[0]) continue;
+    /* item = U{}; deserialize_one(*item) with its errc dropped */
+    const uint8_t *v = NULL;
+    if (!rd_take(r, op->size, &v)) v = NULL;
+    if (!rec) continue;
+    const unsigned hk = heap_of(L, i);
+    const uint64_t off = c->used[hk];
+    if (off + 1 > c->heap_caps[hk]) {
+      c->overflow = 1;
+      continue;
+    }
+    const uint32_t one = 1;
+    memcpy(rec + op->rec_off, &one, 4);
+    memcpy(rec + op->aux, &off, 8);
+    uint8_t *dst = (uint8_t *)c->heaps[hk] + off * op->size;
+    if (v) memcpy(dst, v, op->size);
+    else memset(dst, 0, op->size);
+    c->used[hk] = off + 1;
+  }
+  return 0;
+}
+
 int spko_decode(const spk_layout *L, int mode, const void *wire,
                 uint64_t wire_len, const uint64_t *msg_offsets, uint64_t n_msgs,
                 void *recs, uint64_t rec_cap, void *const *heaps,
@@ -594,6 +695,31 @@ int spko_decode(const spk_layout *L, int mode, const void *wire,
         return SPK_OK;
       }
     }
+    /* deserialize_compatibles (unpacker.hpp:292-366): version by version,
+       record by record */
+    int stop = 0;
+    for (unsigned rk = 0; rk < compat_ranks(L) && !stop; ++rk)
+      for (uint64_t i = 0; i < n && !stop; ++i)
+        stop = read_compat(&c, &r, base, data_len, rk,
+                           (i < rec_cap && out) ? out + i * L->rec_stride : NULL, &e);
+    if (e) {
+      res->errc = e;
+      return SPK_OK;
+    }
+    /* an absent member's heap offset: the values before its record (as for
+       an absent optional, and what the device decoder's per-record bases give) */
+    for (uint32_t k = 0; k < L->n_ops && compat_ranks(L); ++k) {
+      if (!is_compat(L->ops[k].kind)) continue;
+      uint64_t run = 0;
+      for (uint64_t i = 0; i < n && i < rec_cap && out; ++i) {
+        uint8_t *rec = out + i * L->rec_stride;
+        if (rec_count(rec, &L->ops[k])) {
+          ++run;
+          continue;
+        }
+        memcpy(rec + L->ops[k].aux, &run, 8);
+      }
+    }
     res->count = n;
     uint64_t pos = (uint64_t)(r.now - base);
     res->consumed = pos > data_len ? pos : data_len;
@@ -624,8 +750,10 @@ int spko_decode(const spk_layout *L, int mode, const void *wire,
     if (!e) {
       uint64_t save[SPK_MAX_SPANS];
       memcpy(save, c.used, sizeof(save));
-      e = read_record(&c, &r, w,
-                      (i < rec_cap && out) ? out + i * L->rec_stride : NULL);
+      uint8_t *rec = (i < rec_cap && out) ? out + i * L->rec_stride : NULL;
+      e = read_record(&c, &r, w, rec);
+      for (unsigned rk = 0; !e && rk < compat_ranks(L); ++rk)
+        if (read_compat(&c, &r, base + a, data_len, rk, rec, &e)) break;
       if (!e && i >= rec_cap) {
         e = SPK_ERRC_CAPACITY;
         c.overflow = 1;

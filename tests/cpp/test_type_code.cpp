@@ -30,6 +30,11 @@ static_assert(get_type_code<Var>() == 3170970548u);    // kat.json "Var"
 static_assert(get_type_code<VarP>() == 2257901056u);  // kat.json "VarP"
 static_assert(!gpu::detail::is_trivially_serializable<VarP>());
 static_assert(!gpu::detail::has_container<VarP>());
+// compatible members: not in the literal, so all writer versions share a code
+static_assert(get_type_code<Cmp>() == 2242444774u);  // kat.json "Cmp"
+static_assert(get_type_code<CmpOld>() == get_type_code<Cmp>());
+static_assert(get_type_code<CmpNew>() == get_type_code<Cmp>());
+static_assert(!gpu::detail::is_trivially_serializable<Cmp>());
 
 template <typename T>
 static void lit_json(const char *name, bool &first) {
@@ -91,6 +96,9 @@ int main() {
   lit_json<std::vector<Var>>("vector<Var>", first);
   lit_json<VarP>("VarP", first);
   lit_json<std::vector<VarP>>("vector<VarP>", first);
+  lit_json<Cmp>("Cmp", first);
+  lit_json<std::vector<Cmp>>("vector<Cmp>", first);
+  lit_json<CmpNew>("CmpNew", first);
   printf("},\n\"layout\": {\n");
   first = true;
   layout_json<Rec64>("rec64", first);
@@ -106,6 +114,8 @@ int main() {
   layout_json<OptP>("optp", first);
   layout_json<Var>("var", first);
   layout_json<VarP>("varp", first);
+  layout_json<Cmp>("cmp", first);
+  layout_json<CmpNew>("cmpnew", first);
   layout_json<RecS, sp_config::ENABLE_TYPE_INFO>("recs_typeinfo", first);
   layout_json<Rec64, sp_config::DISABLE_ALL_META_INFO>("rec64_nometa", first);
   printf("}}\n");

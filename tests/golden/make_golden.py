@@ -32,7 +32,9 @@ SEED = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004,
         "person": 0x5EED0008, "ints": 0x5EED0009, "opt": 0x5EED000A, "optp": 0x5EED000B,
         "var": 0x5EED000C, "varp": 0x5EED000D, "tags": 0x5EED000E, "group": 0x5EED000F,
         "deep": 0x5EED0010, "vnt": 0x5EED0011, "al8": 0x5EED0012, "alout": 0x5EED0013,
-        "packed": 0x5EED0014, "alrec": 0x5EED0015}
+        "packed": 0x5EED0014, "alrec": 0x5EED0015,
+        # one seed for the three writer versions of Cmp (same records)
+        "cmp": 0x5EED0016, "cmpold": 0x5EED0016, "cmpnew": 0x5EED0016}
 
 # (case_mode, n, param, conf, keep_bin)
 SMALL = [
@@ -93,6 +95,13 @@ SMALL = [
     ("packed_B", 50, 0, "default"), ("packed_A", 40, 0, "typeinfo"),
     ("alrec_A", 200, 20, "default"), ("alrec_B", 100, 20, "default"),
     ("alrec_A", 40, 20, "typeinfo"),
+    # struct_pack::compatible members: total-length field of 2 and 4 bytes,
+    # and the older / newer writers of the same type code
+    ("cmp_A", 0, 8, "default"), ("cmp_A", 1, 8, "default"), ("cmp_A", 200, 8, "default"),
+    ("cmp_A", 40, 300, "default"), ("cmp_A", 50, 8, "typeinfo"), ("cmp_B", 200, 8, "default"),
+    ("cmp_B", 30, 300, "default"), ("cmp_A", 3000, 30, "default"),
+    ("cmpold_A", 200, 8, "default"), ("cmpold_B", 100, 8, "default"),
+    ("cmpnew_A", 200, 8, "default"), ("cmpnew_B", 100, 8, "default"),
 ]
 MEDIUM = [  # digest only (wire > ~1 MB)
     ("rec64_A", 65535, 0, "default"), ("rec64_A", 65536, 0, "default"),
@@ -107,6 +116,8 @@ MEDIUM = [  # digest only (wire > ~1 MB)
     ("tags_A", 70000, 6, "default"), ("tags_B", 20000, 6, "default"),
     ("group_A", 20000, 5, "default"), ("deep_A", 20000, 4, "default"),
     ("vnt_A", 30000, 8, "default"), ("vnt_B", 20000, 8, "default"),
+    ("cmp_A", 30000, 48, "default"), ("cmp_B", 20000, 48, "default"),
+    ("recs_A", 200, 20000, "default"), ("outer_A", 100, 2000, "default"),
 ]
 BIG = [  # BASELINE.json full-size configs (digest only)
     ("rec64_A", 100_000_000, 0, "default"),
@@ -228,6 +239,15 @@ ERR_BASES = [
     ("recs_A", 5, 10, "default", 8), ("outer_A", 4, 8, "default", 8),
     ("recs_B", 1, 30, "default", 8), ("tags_A", 4, 4, "default", 8),
     ("mixed_A", 3, 20, "default", 4), ("recs_A", 4, 10, "default", 2),
+    ("cmp_A", 6, 10, "default"), ("cmp_B", 1, 20, "default"), ("cmp_A", 3, 10, "typeinfo"),
+    ("cmp_B", 1, 300, "default"),
+]
+# compatible members across writer versions: (writer, reader, n, param) — the
+# writer's message mutated and decoded as the reader's type (one type code)
+XERR_BASES = [
+    ("cmpold_A", "cmp_A", 6, 10), ("cmpnew_A", "cmp_A", 6, 10), ("cmp_A", "cmpold_A", 6, 10),
+    ("cmp_A", "cmpnew_A", 6, 10), ("cmpold_B", "cmp_B", 1, 10), ("cmpnew_B", "cmp_B", 1, 10),
+    ("cmp_B", "cmpold_B", 1, 10),
 ]
 
 
@@ -288,9 +308,10 @@ def mutations(wire_len, rng):
 def make_errs(tmp):
     rng = random.Random(1234)
     out = []
-    for eb in ERR_BASES:
+    for eb in ERR_BASES + [(r, n, p, "default", 0, w) for w, r, n, p in XERR_BASES]:
         cm, n, param, conf = eb[:4]
         width = eb[4] if len(eb) > 4 else 0
+        writer = eb[5] if len(eb) > 5 else cm
         case = cm[:-2]
         seed = SEED[case]
         wire = os.path.join(tmp, "ewire.bin")
@@ -298,13 +319,13 @@ def make_errs(tmp):
             with open(wire, "wb") as f:
                 f.write(wide_wire(cm, n, param, conf, width))
         else:
-            subprocess.run([GEN, "emit", cm, str(n), str(seed), str(param), conf, wire,
+            subprocess.run([GEN, "emit", writer, str(n), str(seed), str(param), conf, wire,
                             os.path.join(tmp, "elens.bin")], check=True,
                            stdout=subprocess.DEVNULL)
         with open(wire, "rb") as f:
             base = f.read()
         muts = mutations(len(base), rng)
-        if width:  # the unmutated wide message first
+        if width or writer != cm:  # the unmutated message first
             muts.insert(0, f"trunc {len(base)}")
         if case in ("var", "varp"):  # overlong / 10-byte / unterminated varints
             for p0 in range(0, min(len(base), 48), 3):
@@ -325,8 +346,11 @@ def make_errs(tmp):
         assert len(rows) == len(muts), (cm, len(rows), len(muts))
         if width:
             assert rows[0]["errc"] == 0, (cm, width, rows[0])  # the reference reads it
+        if writer != cm:
+            assert rows[0]["errc"] == 0, (writer, cm, rows[0])
         out.append({"case": case, "mode": cm[-1], "n": n, "seed": seed, "param": param,
-                    "conf": conf, "width": width or None, "base": base.hex(),
+                    "conf": conf, "width": width or None, "writer": writer[:-2],
+                    "base": base.hex(),
                     "tests": [{"mut": m, **r} for m, r in zip(muts, rows)]})
     return out
 

@@ -84,6 +84,42 @@ def test_layout_check_varint_ops():
     assert L4.stride == 16 and lib.spk_layout_check(L4.ptr) == 0
 
 
+def test_layout_check_compat_ops():
+    """compatible<T, ver> members: one SPK_OP_COMPAT per member with its
+    version rank in kind >> 8; top-level only, the hash head required, and no
+    body / sharded entry point (the version passes trail the whole message)."""
+    lib = C.load_codec()
+    L = LY.case_layout("cmpnew")
+    ks = [L.c.ops[i].kind for i in range(L.c.n_ops) if (L.c.ops[i].kind & 0xFF) == C.SPK_OP_COMPAT]
+    assert [k >> 8 for k in ks] == [0, 1, 0, 2]  # 20210101, 20240101, 20210101, 20250101
+    assert lib.spk_layout_check(L.ptr) == 0
+    for field, bad in (("rec_off", 2), ("aux", 4), ("size", 0), ("kind", C.SPK_OP_COMPAT | 1 << 16)):
+        Lb = LY.case_layout("cmp")
+        setattr(Lb.c.ops[1], field, bad)
+        assert lib.spk_layout_check(Lb.ptr) == C.SPK_E_LAYOUT, (field, bad)
+    Lb = LY.case_layout("cmp")
+    Lb.c.fmt_one.flags &= ~C.SPK_MF_HASH_HEAD
+    assert lib.spk_layout_check(Lb.ptr) == C.SPK_E_LAYOUT
+    with pytest.raises(ValueError):  # DISABLE_ALL_META_INFO: a static_assert in the reference
+        LY.case_layout("cmp", S.DISABLE_ALL_META_INFO)
+    # inside a container element: outside the flat model (host) / E_LAYOUT (C ABI)
+    with pytest.raises(NotImplementedError):
+        LY.make_layout(S.Struct("W", [("v", S.Vector(synth.Cmp))]))
+    Lt = LY.case_layout("tags")
+    el = next(i for i in range(Lt.c.n_ops) if Lt.c.ops[i].kind == C.SPK_OP_ARRAY)
+    Lt.c.ops[el + 1].kind = C.SPK_OP_COMPAT
+    Lt.c.ops[el + 1].aux = 8
+    assert lib.spk_layout_check(Lt.ptr) == C.SPK_E_LAYOUT
+    # trivially serializable apart from the compatible member (packer.hpp:422-431)
+    with pytest.raises(NotImplementedError):
+        LY.make_layout(S.Struct("T", [("a", S.int32), ("c", S.Compatible(S.int32, 1))]))
+    vb = (ct.c_uint8 * 64)()
+    assert lib.spk_vector_header(L.ptr, 3, 1, vb, 64) == C.SPK_E_LAYOUT
+    assert lib.spk_encode_body(L.ptr, 0, None, None, 1, vb, 64, vb, 1 << 20, None) == C.SPK_E_LAYOUT
+    assert lib.spk_decode_body(L.ptr, vb, 0, 1, 0, None, 0, None, None, vb, vb, 1 << 20,
+                               None) == C.SPK_E_LAYOUT
+
+
 def test_encode_rejects_bad_args_without_device_work():
     lib = C.load_codec()
     L = LY.case_layout("rec64")

@@ -71,6 +71,16 @@ void trace_mark(const char *name, hipStream_t s, int end) {
 static int hip_rc(hipError_t e) { return e == hipSuccess ? SPK_OK : SPK_E_HIP; }
 
 static bool is_trivial(const spk_layout *L) { return (L->flags & SPK_LAYOUT_TRIVIAL) != 0; }
+static bool has_compat(const spk_layout *L) {
+  for (uint32_t i = 0; i < L->n_ops; ++i)
+    if (SPK_OP_KIND(L->ops[i].kind) == SPK_OP_COMPAT) return true;
+  return false;
+}
+static uint32_t heap_count(const spk_layout *L) {
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i) k += op_has_heap(L->ops[i].kind);
+  return k;
+}
 
 extern "C" {
 
@@ -139,6 +149,15 @@ int spk_layout_check(const spk_layout *L) {
         nops[depth] = 0;
         alts[depth] = 0;
       }
+    } else if (SPK_OP_KIND(o.kind) == SPK_OP_COMPAT) {
+      // compatible<U, ver> of the top-level record only; OPTION's fields;
+      // DISABLE_ALL_META_INFO is a compile error in the reference
+      // (type_calculate.hpp:868-876)
+      if (depth || (o.kind & ~0xFFFFu) || o.size == 0 || o.rec_off % 4 || o.aux % 8 ||
+          o.rec_off + 4 > rs || o.aux + 8 > rs || !(L->fmt_one.flags & SPK_MF_HASH_HEAD) ||
+          !(L->fmt_vector.flags & SPK_MF_HASH_HEAD))
+        return SPK_E_LAYOUT;
+      ++spans;
     } else if (o.kind == SPK_OP_END) {
       --nops[depth];
       if (depth == 0 || nops[depth] == 0) return SPK_E_LAYOUT;  // unmatched / empty element
@@ -178,7 +197,7 @@ static int heaps_check(const spk_layout *L, uint64_t n, const void *const *d_hea
   uint32_t spans = 0;
   for (uint32_t i = 0; i < L->n_ops; ++i) {
     const uint32_t k = L->ops[i].kind;
-    if (k != SPK_OP_SPAN && k != SPK_OP_OPTION && k != SPK_OP_ARRAY) continue;
+    if (!op_has_heap(k)) continue;
     if (n && d_heaps && k == SPK_OP_ARRAY && d_heaps[spans] && (uintptr_t)d_heaps[spans] % 8)
       return SPK_E_ARG;
     ++spans;
@@ -298,10 +317,7 @@ static int decode_impl(const spk_layout *L, int mode, const void *d_wire, uint64
                                                s));
   }
   if (d_recs && (uintptr_t)d_recs % 8) return SPK_E_ARG;
-  uint32_t spans = 0;
-  for (uint32_t i = 0; i < L->n_ops; ++i)
-    spans += L->ops[i].kind == SPK_OP_SPAN || L->ops[i].kind == SPK_OP_OPTION ||
-             L->ops[i].kind == SPK_OP_ARRAY;
+  const uint32_t spans = heap_count(L);
   if (spans && (!d_heaps || !heap_caps)) return SPK_E_ARG;
   if (mode == SPK_MODE_MESSAGES && n_msgs && !d_msg_offsets) return SPK_E_ARG;
   if (layout_nested(L)) {
@@ -341,6 +357,7 @@ int spk_encode_body(const spk_layout *L, uint64_t n, const void *d_recs,
                     uint64_t out_cap, void *d_ws, size_t ws_bytes, void *stream) {
   int rc = spk_layout_check(L);
   if (rc) return rc;
+  if (has_compat(L)) return SPK_E_LAYOUT;  // the version passes trail the whole message
   if (width != 1 && width != 2 && width != 4 && width != 8) return SPK_E_ARG;
   if ((n && !d_recs) || !d_out || !d_ws) return SPK_E_ARG;
   if (ws_bytes < spk_workspace_bytes(L, SPK_MODE_VECTOR, n, 0)) return SPK_E_WORKSPACE;
@@ -365,6 +382,7 @@ int spk_decode_body(const spk_layout *L, const void *d_body, uint64_t body_len, 
                     size_t ws_bytes, void *stream) {
   int rc = spk_layout_check(L);
   if (rc) return rc;
+  if (has_compat(L)) return SPK_E_LAYOUT;
   if (width != 1 && width != 2 && width != 4 && width != 8) return SPK_E_ARG;
   if (!d_res || !d_ws || (body_len && !d_body) || (rec_cap && !d_recs)) return SPK_E_ARG;
   if (ws_bytes < spk_workspace_bytes(L, SPK_MODE_VECTOR, rec_cap, body_len))
@@ -374,10 +392,7 @@ int spk_decode_body(const spk_layout *L, const void *d_body, uint64_t body_len, 
     return hip_rc(launch_fixed_decode_vector(L, d_body, body_len, d_recs, rec_cap, d_res, d_ws,
                                              s, width, n));
   if (d_recs && (uintptr_t)d_recs % 8) return SPK_E_ARG;
-  uint32_t spans = 0;
-  for (uint32_t i = 0; i < L->n_ops; ++i)
-    spans += L->ops[i].kind == SPK_OP_SPAN || L->ops[i].kind == SPK_OP_OPTION ||
-             L->ops[i].kind == SPK_OP_ARRAY;
+  const uint32_t spans = heap_count(L);
   if (spans && (!d_heaps || !heap_caps)) return SPK_E_ARG;
   if (layout_nested(L)) {
     for (uint32_t k = 0; k < spans; ++k)
@@ -450,6 +465,7 @@ int spk_vector_header(const spk_layout *L, uint64_t total_n, uint32_t width, uin
                       uint32_t cap) {
   int rc = spk_layout_check(L);
   if (rc) return rc;
+  if (has_compat(L)) return SPK_E_LAYOUT;
   if ((width != 1 && width != 2 && width != 4 && width != 8) || !h_out) return SPK_E_ARG;
   if (width < width_of(total_n)) return SPK_E_ARG;  // the count itself must fit
   uint8_t hb[4 + 1 + SPK_MAX_LITERAL + 1 + 8];

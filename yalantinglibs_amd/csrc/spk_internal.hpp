@@ -68,6 +68,37 @@ __host__ __device__ inline HdrShape hdr_shape(uint32_t flags, uint32_t lit_len,
   return h;
 }
 
+// compatible<T> members (SPK_OP_COMPAT): the metainfo byte is always there
+// and is followed by the message's total length in 2/4/8 bytes
+// (calculate_size.hpp:457-470; packer.hpp:111-130). `body` = the bytes after
+// the header. Returns the header length; writes it into dst when set.
+__host__ __device__ inline uint32_t compat_hdr(uint8_t *dst, const spk_msgfmt &f, uint32_t w,
+                                               uint64_t body) {
+  const HdrShape h = hdr_shape(f.flags, f.literal_len, w);
+  const uint32_t base = h.len + (h.has_meta ? 0u : 1u);
+  const uint64_t l = base + body;
+  const uint32_t lw = l + 2 < (1ull << 16) ? 2u : l + 4 < (1ull << 32) ? 4u : 8u;
+  if (dst) {
+    uint32_t p = 0;
+    const uint32_t head = f.code | 1u;
+    for (uint32_t b = 0; b < 4; ++b) dst[p++] = (uint8_t)(head >> (8 * b));
+    dst[p++] = (uint8_t)(h.meta | (lw == 2 ? 1u : lw == 4 ? 2u : 3u));
+    const uint64_t total = l + lw;
+    for (uint32_t b = 0; b < lw; ++b) dst[p++] = (uint8_t)(total >> (8 * b));
+    if (h.lit) {
+      for (uint32_t i = 0; i < f.literal_len; ++i) dst[p++] = f.literal[i];
+      dst[p++] = 0;
+    }
+  }
+  return base + lw;
+}
+
+__host__ __device__ inline bool op_has_heap(uint32_t kind) {
+  kind = SPK_OP_KIND(kind);
+  return kind == SPK_OP_SPAN || kind == SPK_OP_OPTION || kind == SPK_OP_ARRAY ||
+         kind == SPK_OP_COMPAT;
+}
+
 // Writes the header bytes (at most 4+1+SPK_MAX_LITERAL+1) into dst.
 __host__ __device__ inline uint32_t write_hdr(uint8_t *dst, const spk_msgfmt &f,
                                               uint32_t w) {

@@ -17,6 +17,12 @@
 // message's record boundaries come from one wave that walks the counts
 // through an LDS window (payload bytes are skipped, not read), then every
 // record is decoded by its own lane into heap offsets from a per-heap scan.
+//
+// compatible<U, ver> members (SPK_OP_COMPAT, top-level record only) run here
+// too: the main pass skips them, then one version pass per rank writes
+// [has][U] of every record (packer.hpp:66-78,453-461; unpacker.hpp:292-366,
+// 1354-1376). A VECTOR decode's walker records where each record's group of
+// each version starts; the record's lane decodes its groups from there.
 #include "spk_internal.hpp"
 
 namespace spk {
@@ -25,13 +31,17 @@ struct NLayout {
   spk_op ops[SPK_MAX_OPS];
   uint8_t heap[SPK_MAX_OPS];  // heap index of a SPAN / OPTION / ARRAY op
   uint8_t end[SPK_MAX_OPS];   // ARRAY: its END; VARIANT: the END of its last alternative
-  uint32_t n_ops, stride, n_heaps, pad_;
+  uint8_t crank[SPK_MAX_OPS]; // COMPAT: its version rank (ops[i].kind is SPK_OP_COMPAT)
+  uint32_t n_ops, stride, n_heaps, n_ranks;
 };
 
-// layouts the interpreter runs: an ARRAY (element layouts) or a VARIANT
+// layouts the interpreter runs: an ARRAY (element layouts), a VARIANT or a
+// compatible member
 bool layout_nested(const spk_layout *L) {
-  for (uint32_t i = 0; i < L->n_ops; ++i)
-    if (L->ops[i].kind == SPK_OP_ARRAY || L->ops[i].kind == SPK_OP_VARIANT) return true;
+  for (uint32_t i = 0; i < L->n_ops; ++i) {
+    const uint32_t k = SPK_OP_KIND(L->ops[i].kind);
+    if (k == SPK_OP_ARRAY || k == SPK_OP_VARIANT || k == SPK_OP_COMPAT) return true;
+  }
   return false;
 }
 
@@ -43,8 +53,13 @@ static NLayout make_nlayout(const spk_layout *L) {
   uint32_t stack[SPK_MAX_DEPTH + 1], left[SPK_MAX_DEPTH + 1], d = 0, h = 0;
   for (uint32_t i = 0; i < L->n_ops; ++i) {
     N.ops[i] = L->ops[i];
-    const uint32_t k = L->ops[i].kind;
-    if (k == SPK_OP_SPAN || k == SPK_OP_OPTION || k == SPK_OP_ARRAY) N.heap[i] = (uint8_t)h++;
+    const uint32_t k = SPK_OP_KIND(L->ops[i].kind);
+    if (k == SPK_OP_COMPAT) {
+      N.ops[i].kind = k;
+      N.crank[i] = (uint8_t)SPK_OP_RANK(L->ops[i].kind);
+      if (N.crank[i] + 1u > N.n_ranks) N.n_ranks = N.crank[i] + 1u;
+    }
+    if (op_has_heap(k)) N.heap[i] = (uint8_t)h++;
     if (k == SPK_OP_ARRAY || k == SPK_OP_VARIANT) {
       stack[d] = i;
       left[d++] = k == SPK_OP_VARIANT ? L->ops[i].size : 1;
@@ -122,9 +137,10 @@ __device__ __forceinline__ uint32_t n_alt_end(const NLayout &N, uint32_t j) {
 // ---- encode: size of one record -----------------------------------------------
 struct NSize {
   uint64_t bytes, cnts, maxc;  // payload bytes w/o counts, count fields, longest container
+  uint64_t cbytes;             // of which in the version passes (compatible members)
 };
 __device__ NSize n_size(const NLayout &N, const uint8_t *rec, const uint8_t *const *heaps) {
-  NSize s = {0, 0, 0};
+  NSize s = {0, 0, 0, 0};
   NFrame st[SPK_MAX_DEPTH];
   uint32_t d = 0, i = 0, iend = N.n_ops;
   const uint8_t *r = rec;
@@ -161,8 +177,10 @@ __device__ NSize n_size(const NLayout &N, const uint8_t *rec, const uint8_t *con
         i = a0;
         continue;
       }
-      if (op.kind == SPK_OP_OPTION) {
-        s.bytes += 1 + (c ? op.size : 0);
+      if (op.kind == SPK_OP_OPTION || op.kind == SPK_OP_COMPAT) {  // calculate_size.hpp:100-105
+        const uint64_t b = 1 + (c ? op.size : 0);
+        s.bytes += b;
+        if (op.kind == SPK_OP_COMPAT) s.cbytes += b;
         ++i;
         continue;
       }
@@ -231,6 +249,10 @@ __device__ uint8_t *n_write(const NLayout &N, const uint8_t *rec, const uint8_t 
         i = a0;
         continue;
       }
+      if (op.kind == SPK_OP_COMPAT) {  // version UINT64_MAX: nothing (packer.hpp:246-249)
+        ++i;
+        continue;
+      }
       const uint64_t off = *reinterpret_cast<const uint64_t *>(r + op.aux);
       if (op.kind == SPK_OP_OPTION) {
         *p++ = c ? 1 : 0;
@@ -259,6 +281,69 @@ __device__ uint8_t *n_write(const NLayout &N, const uint8_t *rec, const uint8_t 
     }
   }
   return p;
+}
+
+// ---- compatible members: the version pass of rank rk over one top-level record ----
+__device__ uint64_t n_compat_size(const NLayout &N, const uint8_t *rec, uint32_t rk) {
+  uint64_t b = 0;
+  for (uint32_t i = 0; i < N.n_ops; ++i)
+    if (N.ops[i].kind == SPK_OP_COMPAT && N.crank[i] == rk)
+      b += 1 + (*reinterpret_cast<const uint32_t *>(rec + N.ops[i].rec_off) ? N.ops[i].size : 0);
+  return b;
+}
+// packer.hpp:453-461: [has_value:1][U if present] per member of that version
+__device__ uint8_t *n_write_compat(const NLayout &N, const uint8_t *rec,
+                                   const uint8_t *const *heaps, uint32_t rk, uint8_t *p) {
+  for (uint32_t i = 0; i < N.n_ops; ++i) {
+    const spk_op op = N.ops[i];
+    if (op.kind != SPK_OP_COMPAT || N.crank[i] != rk) continue;
+    const uint32_t c = *reinterpret_cast<const uint32_t *>(rec + op.rec_off);
+    *p++ = c ? 1 : 0;
+    if (c) {
+      const uint64_t off = *reinterpret_cast<const uint64_t *>(rec + op.aux);
+      n_copy(p, heaps[N.heap[i]] + off * op.size, op.size);
+      p += op.size;
+    }
+  }
+  return p;
+}
+// unpacker.hpp:1354-1376 over one record: a member whose has byte would start
+// at or past data_end ends every version pass without an error (returns 1,
+// size_type_ = UCHAR_MAX, :360-365); a missing has byte before it is
+// no_buffer_space (*ec, returns 1); a value that does not fit reads as present
+// and zero (its errc is dropped). The main pass left every member absent.
+__device__ int n_read_compat(const NLayout &N, const uint8_t *wire, uint64_t &pos, uint64_t end,
+                             uint64_t data_end, uint32_t rk, uint8_t *rec, uint8_t *const *heaps,
+                             uint64_t *used, const uint64_t *heap_cap, uint32_t *ovf,
+                             int32_t *ec) {
+  for (uint32_t i = 0; i < N.n_ops; ++i) {
+    const spk_op op = N.ops[i];
+    if (op.kind != SPK_OP_COMPAT || N.crank[i] != rk) continue;
+    if (pos >= data_end) return 1;
+    if (pos >= end) {
+      *ec = SPK_ERRC_NO_BUFFER_SPACE;
+      return 1;
+    }
+    if (!wire[pos++]) continue;
+    const bool fits = end - pos >= op.size;
+    const uint32_t hk = N.heap[i];
+    const uint64_t off = used[hk];
+    if (rec) {
+      if (off >= heap_cap[hk]) {
+        *ovf = 1;
+      } else {
+        *reinterpret_cast<uint32_t *>(rec + op.rec_off) = 1;
+        *reinterpret_cast<uint64_t *>(rec + op.aux) = off;
+        if (fits)
+          n_copy(heaps[hk] + off * op.size, wire + pos, op.size);
+        else
+          for (uint32_t b = 0; b < op.size; ++b) heaps[hk][off * op.size + b] = 0;
+      }
+    }
+    used[hk] = off + 1;
+    if (fits) pos += op.size;
+  }
+  return 0;
 }
 
 // ---- decode: one record from the wire -------------------------------------------
@@ -365,6 +450,14 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
       continue;
     }
     const uint32_t hk = N.heap[i];
+    if (op.kind == SPK_OP_COMPAT) {  // absent until its version pass
+      if (r) {
+        *reinterpret_cast<uint32_t *>(r + op.rec_off) = 0;
+        *reinterpret_cast<uint64_t *>(r + op.aux) = used[hk];
+      }
+      ++i;
+      continue;
+    }
     const uint32_t pw = op.kind == SPK_OP_OPTION ? 1u : w;
     if (end - pos < pw) { ec = SPK_ERRC_NO_BUFFER_SPACE; continue; }
     uint64_t cnt;
@@ -540,9 +633,9 @@ static size_t nscan_part_bytes(uint64_t n, uint32_t ncols) {
 
 // ---- workspace ------------------------------------------------------------------
 struct NWs {
-  size_t a, b, part, starts, end;  // a/b: [C][n] u64 columns; starts: [n] u64
-};
-static NWs nws_layout(uint64_t n, uint32_t n_heaps) {
+  size_t a, b, part, starts, cpos, end;  // a/b: [C][n] u64 columns; starts: [n] u64
+};                                       // cpos: [ranks][n] u64 version-group starts
+static NWs nws_layout(uint64_t n, uint32_t n_heaps, uint32_t n_ranks) {
   NWs f = {};
   size_t off = kWsScratch;
   auto take = [&](size_t bytes) {
@@ -555,13 +648,14 @@ static NWs nws_layout(uint64_t n, uint32_t n_heaps) {
   f.b = take((n + 1) * 8);
   f.part = take(nscan_part_bytes(n + 1, cols));
   f.starts = take((n + 1) * 8);
+  f.cpos = take((n + 1) * 8 * (n_ranks ? n_ranks : 1));
   f.end = off;
   return f;
 }
 
 size_t nested_workspace_bytes(const spk_layout *L, int, uint64_t n, uint64_t) {
   const NLayout N = make_nlayout(L);
-  return nws_layout(n, N.n_heaps).end + 256;
+  return nws_layout(n, N.n_heaps, N.n_ranks).end + 256;
 }
 
 // control block of the nested path (at kWsCtl)
@@ -598,12 +692,17 @@ __global__ __launch_bounds__(256) void nest_size(NEnc e, const uint8_t *__restri
     m = s.maxc;
     if (e.mode == SPK_MODE_MESSAGES) {
       const uint32_t w = width_of(s.maxc);
-      const HdrShape h = hdr_shape(e.fmt.flags, e.fmt.literal_len, w);
-      a[i] = e.fpre + h.len + s.bytes + s.cnts * w;
+      const uint64_t body = s.bytes + s.cnts * w;
+      const uint32_t hl = e.N.n_ranks ? compat_hdr(nullptr, e.fmt, w, body)
+                                      : hdr_shape(e.fmt.flags, e.fmt.literal_len, w).len;
+      a[i] = e.fpre + hl + body;
       a[e.n + i] = s.bytes;
     } else {
-      a[i] = s.bytes;
+      // main pass bytes; count fields; then one column per version pass
+      a[i] = s.bytes - s.cbytes;
       a[e.n + i] = s.cnts;
+      for (uint32_t rk = 0; rk < e.N.n_ranks; ++rk)
+        a[(2 + rk) * e.n + i] = n_compat_size(e.N, recs + i * e.N.stride, rk);
     }
   }
   // block max -> one atomic per wave
@@ -647,13 +746,23 @@ __global__ void nest_plan_fin(NEnc e, const uint64_t *__restrict__ a,
     const uint64_t mx = ctl->maxc > e.n ? ctl->maxc : e.n;
     const uint32_t w = width_of(mx);
     const HdrShape h = hdr_shape(e.fmt.flags, e.fmt.literal_len, w);
+    uint64_t totc = 0;  // the version passes
+    for (uint32_t rk = 0; rk < e.N.n_ranks; ++rk)
+      totc += e.n ? part[(2 + rk) * (nb + 1) + nb] : 0;
+    uint32_t hl = h.len, meta = h.meta, has_meta = h.has_meta;
+    if (e.N.n_ranks) {
+      uint8_t hb[4 + 1 + 8 + SPK_MAX_LITERAL + 1];
+      hl = compat_hdr(hb, e.fmt, w, w + tot0 + totc);
+      meta = hb[4];
+      has_meta = 1;
+    }
     p.max_count = mx;
     p.width = w;
-    p.header_bytes = h.len + w;
-    p.metainfo = h.meta;
-    p.has_meta = h.has_meta;
-    p.var_bytes = tot0 - tot1 * w;  // column 0 holds bytes + counts * w
-    p.total_bytes = h.len + w + tot0;
+    p.header_bytes = hl + w;
+    p.metainfo = meta;
+    p.has_meta = has_meta;
+    p.var_bytes = tot0 - tot1 * w + totc;  // column 0 holds bytes + counts * w
+    p.total_bytes = hl + w + tot0 + totc;
   } else {
     p.max_count = ctl->maxc;
     p.width = width_of(ctl->maxc);
@@ -677,16 +786,28 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
     const uint64_t mx = ctl->maxc > e.n ? ctl->maxc : e.n;
     const uint32_t w = e.fixed_w ? e.fixed_w : width_of(mx);
     uint32_t hl = 0;
+    const uint64_t tot0 = e.n ? part[nb] : 0;
+    uint64_t totc = 0;
+    for (uint32_t rk = 0; rk < e.N.n_ranks; ++rk) totc += e.n ? part[(2 + rk) * (nb + 1) + nb] : 0;
     if (with_header) {
-      uint8_t hb[4 + 1 + SPK_MAX_LITERAL + 1];
-      hl = write_hdr(hb, e.fmt, w);
+      uint8_t hb[4 + 1 + 8 + SPK_MAX_LITERAL + 1];
+      hl = e.N.n_ranks ? compat_hdr(hb, e.fmt, w, w + tot0 + totc) : write_hdr(hb, e.fmt, w);
       if (i == 0) {
         for (uint32_t b = 0; b < hl; ++b) out[b] = hb[b];
         for (uint32_t b = 0; b < w; ++b) out[hl + b] = (uint8_t)(e.n >> (8 * b));
       }
       hl += w;
     }
-    if (i < e.n) n_write(e.N, recs + i * e.N.stride, e.heaps, w, out + hl + off[i]);
+    if (i < e.n) {
+      const uint8_t *rec = recs + i * e.N.stride;
+      n_write(e.N, rec, e.heaps, w, out + hl + off[i]);
+      // version passes after every record's main pass (packer.hpp:66-78)
+      uint64_t sec = hl + tot0;
+      for (uint32_t rk = 0; rk < e.N.n_ranks; ++rk) {
+        n_write_compat(e.N, rec, e.heaps, rk, out + sec + off[(2 + rk) * e.n + i]);
+        sec += part[(2 + rk) * (nb + 1) + nb];
+      }
+    }
     return;
   }
   if (i == 0 && msg_offsets) msg_offsets[e.n] = e.n ? part[nb] : 0;
@@ -697,10 +818,12 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
   uint8_t *p = out + off[i];
   if (msg_offsets) msg_offsets[i] = off[i];
   uint8_t *m = p + e.fpre;
-  uint8_t hb[4 + 1 + SPK_MAX_LITERAL + 1];
-  const uint32_t hl = write_hdr(hb, e.fmt, w);
+  uint8_t hb[4 + 1 + 8 + SPK_MAX_LITERAL + 1];
+  const uint32_t hl = e.N.n_ranks ? compat_hdr(hb, e.fmt, w, s.bytes + s.cnts * w)
+                                  : write_hdr(hb, e.fmt, w);
   for (uint32_t b = 0; b < hl; ++b) m[b] = hb[b];
   uint8_t *q = n_write(e.N, rec, e.heaps, w, m + hl);
+  for (uint32_t rk = 0; rk < e.N.n_ranks; ++rk) q = n_write_compat(e.N, rec, e.heaps, rk, q);
   if (e.fpre) {
     for (uint32_t b = 0; b < e.fpre; ++b) p[b] = e.ftmpl[b];
     const uint32_t mlen = (uint32_t)(q - m);
@@ -733,7 +856,7 @@ static NEnc make_nenc(const spk_layout *L, int mode, uint64_t n, const void *con
 // size pass + scan; leaves per-record offsets in column a[0]
 static hipError_t nest_size_scan(const NEnc &e, const void *d_recs, uint8_t *ws, hipStream_t s,
                                  uint64_t **a_out, uint64_t **part_out, uint64_t *nb_out) {
-  const NWs f = nws_layout(e.n, e.N.n_heaps);
+  const NWs f = nws_layout(e.n, e.N.n_heaps, e.N.n_ranks);
   uint64_t *a = reinterpret_cast<uint64_t *>(ws + f.a);
   uint64_t *part = reinterpret_cast<uint64_t *>(ws + f.part);
   SPK_LAUNCH(nest_ctl_init, dim3(1), dim3(1), 0, s, ws);
@@ -746,9 +869,11 @@ static hipError_t nest_size_scan(const NEnc &e, const void *d_recs, uint8_t *ws,
   }
   hipError_t er = hipGetLastError();
   if (er != hipSuccess) return er;
-  // VECTOR: column 0 = sizes at w, column 1 = count fields; MESSAGES: column 0
-  // = message sizes, column 1 = payload bytes. Both scanned (totals in part).
-  if ((er = nscan(a, e.n, 2, part, s)) != hipSuccess) return er;
+  // VECTOR: column 0 = sizes at w, column 1 = count fields, 2.. = version
+  // passes; MESSAGES: column 0 = message sizes, column 1 = payload bytes. All
+  // scanned (totals in part).
+  const uint32_t cols = e.mode == SPK_MODE_VECTOR ? 2 + e.N.n_ranks : 2;
+  if ((er = nscan(a, e.n, cols, part, s)) != hipSuccess) return er;
   *a_out = a;
   *part_out = part;
   *nb_out = (e.n + kNScanBlk - 1) / kNScanBlk;
@@ -810,6 +935,7 @@ constexpr uint32_t kNWin = 4096;
 __global__ __launch_bounds__(64) void nest_vec_walk(NDec a, const uint8_t *__restrict__ wire,
                                                     uint8_t *ws, uint64_t *__restrict__ U,
                                                     uint64_t *__restrict__ starts,
+                                                    uint64_t *__restrict__ cpos,
                                                     spk_dresult_t *res) {
   __shared__ uint8_t win[kNWin + 16];
   __shared__ unsigned long long s_pos;
@@ -823,6 +949,9 @@ __global__ __launch_bounds__(64) void nest_vec_walk(NDec a, const uint8_t *__res
   uint32_t w = 1, i = 0, iend = N.n_ops, d = 0;
   int32_t errc = 0;
   uint64_t data_len = 0;
+  // the version passes of compatible members (ph 1): rank rk, record crec, op ci
+  uint32_t ph = 0, rk = 0, ci = 0;
+  uint64_t crec = 0;
   struct Fr {
     uint32_t aop, pend;
     uint64_t j, cnt;
@@ -885,6 +1014,44 @@ __global__ __launch_bounds__(64) void nest_vec_walk(NDec a, const uint8_t *__res
       };
       bool stall = false, done = false;
       while (!stall && !done) {
+        if (ph) {  // unpacker.hpp:292-366,1354-1376
+          if (rk >= N.n_ranks) {
+            done = true;
+            break;
+          }
+          if (crec >= n) {
+            ++rk;
+            crec = 0;
+            ci = 0;
+            continue;
+          }
+          if (ci == 0 && crec < a.rec_cap) cpos[(uint64_t)rk * a.rec_cap + crec] = pos;
+          while (ci < N.n_ops && !(N.ops[ci].kind == SPK_OP_COMPAT && N.crank[ci] == rk)) ++ci;
+          if (ci >= N.n_ops) {
+            ++crec;
+            ci = 0;
+            continue;
+          }
+          if (pos >= data_len) {  // an older writer: the legal end
+            done = true;
+            break;
+          }
+          if (wend < len && pos + 1 > wend) {
+            stall = true;
+            break;
+          }
+          if (pos >= len) {
+            errc = SPK_ERRC_NO_BUFFER_SPACE;
+            done = true;
+            break;
+          }
+          if (byte(pos++)) {
+            if (crec < a.rec_cap) U[(uint64_t)N.heap[ci] * a.rec_cap + crec] = 1;
+            if (len - pos >= N.ops[ci].size) pos += N.ops[ci].size;
+          }
+          ++ci;
+          continue;
+        }
         if (i >= iend) {
           if (d) {
             Fr &f = st[d - 1];
@@ -903,6 +1070,10 @@ __global__ __launch_bounds__(64) void nest_vec_walk(NDec a, const uint8_t *__res
           for (uint32_t k = 0; k < N.n_heaps; ++k) base[k] = used[k];
           ++rec;
           if (rec == n) {
+            if (N.n_ranks) {
+              ph = 1;
+              continue;
+            }
             done = true;
             break;
           }
@@ -912,6 +1083,10 @@ __global__ __launch_bounds__(64) void nest_vec_walk(NDec a, const uint8_t *__res
           continue;
         }
         const spk_op op = N.ops[i];
+        if (op.kind == SPK_OP_COMPAT) {  // main pass: nothing on the wire
+          ++i;
+          continue;
+        }
         if (op.kind == SPK_OP_COPY) {
           if (len - pos < op.size) {
             if (!fail(SPK_ERRC_NO_BUFFER_SPACE)) {
@@ -1070,6 +1245,10 @@ __global__ __launch_bounds__(256) void nest_msg_count(NDec a, const uint8_t *__r
       uint64_t pos = m0 + p0;
       uint32_t ovf = 0;
       errc = n_read(N, wire, pos, e, w, nullptr, nullptr, used, a.heap_cap, &ovf);
+      for (uint32_t rk = 0; !errc && rk < N.n_ranks; ++rk)
+        if (n_read_compat(N, wire, pos, e, m0 + dl, rk, nullptr, nullptr, used, a.heap_cap, &ovf,
+                          &errc))
+          break;
       consumed = pos - m0 > dl ? pos - m0 : dl;  // consume_len (struct_pack.hpp:343-357)
     }
     if (!errc && i >= a.rec_cap) errc = SPK_ERRC_CAPACITY;
@@ -1085,17 +1264,19 @@ __global__ __launch_bounds__(256) void nest_emit(NDec a, const uint8_t *__restri
                                                  const uint64_t *__restrict__ starts,
                                                  const uint64_t *__restrict__ B, uint64_t nrows,
                                                  const int32_t *__restrict__ ec, uint8_t *ws,
+                                                 const uint64_t *__restrict__ cpos,
                                                  uint8_t *__restrict__ recs, int mode) {
   NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const NLayout &N = a.N;
-  uint64_t pos, end;
+  uint64_t pos, end, data_end;
   uint32_t w;
   if (mode == SPK_MODE_VECTOR) {
     if (ctl->errc || i >= ctl->nrec || i >= a.rec_cap) return;
     pos = starts[i];
     end = a.wire_len;
     w = ctl->w;
+    data_end = ctl->data_len;
   } else {
     if (i >= a.n_msgs || i >= a.rec_cap || ec[i]) return;
     const uint64_t m0 = offs[i] + a.prefix;
@@ -1103,11 +1284,22 @@ __global__ __launch_bounds__(256) void nest_emit(NDec a, const uint8_t *__restri
     uint64_t p0, dl;
     parse_hdr(a.fmt, wire + m0, end - m0, &p0, &w, &dl);
     pos = m0 + p0;
+    data_end = m0 + dl;
   }
   uint64_t used[SPK_MAX_SPANS];
   for (uint32_t k = 0; k < N.n_heaps; ++k) used[k] = B[(uint64_t)k * nrows + i];
   uint32_t ovf = 0;
-  n_read(N, wire, pos, end, w, recs + i * N.stride, a.heaps, used, a.heap_cap, &ovf);
+  uint8_t *rec = recs + i * N.stride;
+  n_read(N, wire, pos, end, w, rec, a.heaps, used, a.heap_cap, &ovf);
+  int32_t cec = 0;
+  for (uint32_t rk = 0; rk < N.n_ranks; ++rk) {
+    if (mode == SPK_MODE_VECTOR) {  // this record's group of version rk (walker)
+      pos = cpos[(uint64_t)rk * a.rec_cap + i];
+      if (pos == ~0ull) break;
+    }
+    if (n_read_compat(N, wire, pos, end, data_end, rk, rec, a.heaps, used, a.heap_cap, &ovf, &cec))
+      break;
+  }
   if (ovf) atomicAdd(&ctl->ovf, 1ull);
 }
 
@@ -1185,7 +1377,8 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
   }
   uint8_t *ws = (uint8_t *)d_ws;
   const uint64_t rows = mode == SPK_MODE_VECTOR ? rec_cap : n_msgs;
-  const NWs f = nws_layout(rows, a.N.n_heaps);
+  const NWs f = nws_layout(rows, a.N.n_heaps, a.N.n_ranks);
+  uint64_t *cpos = reinterpret_cast<uint64_t *>(ws + f.cpos);
   uint64_t *U = reinterpret_cast<uint64_t *>(ws + f.a);
   uint64_t *cons = reinterpret_cast<uint64_t *>(ws + f.b);
   uint64_t *part = reinterpret_cast<uint64_t *>(ws + f.part);
@@ -1197,13 +1390,16 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
   SPK_LAUNCH(nest_ctl_init, dim3(1), dim3(1), 0, s, ws);
   if (mode == SPK_MODE_VECTOR) {
     if (rows && (er = hipMemsetAsync(U, 0, rows * 8 * a.N.n_heaps, s)) != hipSuccess) return er;
+    if (rows && a.N.n_ranks &&
+        (er = hipMemsetAsync(cpos, 0xFF, rows * 8 * a.N.n_ranks, s)) != hipSuccess)
+      return er;
     SPK_LAUNCH(nest_vec_walk, dim3(1), dim3(64), 0, s, a, (const uint8_t *)d_wire, ws, U, starts,
-               d_res);
+               cpos, d_res);
     if ((er = nscan(U, rows, a.N.n_heaps, part, s)) != hipSuccess) return er;
     if (rows)
       SPK_LAUNCH(nest_emit, dim3(nblocks(rows, 256)), dim3(256), 0, s, a, (const uint8_t *)d_wire,
                  d_msg_offsets, (const uint64_t *)starts, (const uint64_t *)U, rows,
-                 (const int32_t *)ec, ws, (uint8_t *)d_recs, mode);
+                 (const int32_t *)ec, ws, (const uint64_t *)cpos, (uint8_t *)d_recs, mode);
     SPK_LAUNCH(nest_finish, dim3(1), dim3(256), 0, s, a, (const uint64_t *)part, nb,
                (const int32_t *)ec, ws, mode, d_res, (int32_t *)nullptr);
     return hipGetLastError();
@@ -1214,7 +1410,7 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
   if ((er = nscan(U, rows, a.N.n_heaps, part, s)) != hipSuccess) return er;
   SPK_LAUNCH(nest_emit, dim3(nblocks(rows, 256)), dim3(256), 0, s, a, (const uint8_t *)d_wire,
              d_msg_offsets, (const uint64_t *)starts, (const uint64_t *)U, rows,
-             (const int32_t *)ec, ws, (uint8_t *)d_recs, mode);
+             (const int32_t *)ec, ws, (const uint64_t *)cpos, (uint8_t *)d_recs, mode);
   SPK_LAUNCH(nest_finish, dim3(1), dim3(256), 0, s, a, (const uint64_t *)part, nb,
              (const int32_t *)ec, ws, mode, d_res, d_errc);
   uint64_t *cpart = reinterpret_cast<uint64_t *>(ws + f.part) + (nb + 1) * a.N.n_heaps;

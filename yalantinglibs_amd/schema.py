@@ -207,6 +207,38 @@ class Optional(SpType):
         return self.elem.has_container
 
 
+class Compatible(SpType):
+    """struct_pack::compatible<T, version> (compatible_t, ref compatible.hpp:
+    21-154): an optional written after the main pass, in the version pass of
+    its version (packer.hpp:66-78,453-461); not in the type literal nor the
+    hash (type_calculate.hpp:298-303); the message gets a total-length field
+    (calculate_size.hpp:457-470). Only a member of the top-level record with a
+    trivially serializable T is in the flat record model."""
+
+    def __init__(self, elem: SpType, version: int = 0):
+        self.elem, self.version = elem, version
+        self.name = f"struct_pack::compatible<{elem.name},{version}>"
+        self.config = DEFAULT
+
+    def literal(self):
+        return b""
+
+    @property
+    def has_container(self):
+        return self.elem.has_container
+
+
+def has_compatible(t: SpType) -> bool:
+    """serialize_static_config<T>::has_compatible (type_calculate.hpp:746)."""
+    if isinstance(t, Compatible):
+        return True
+    if isinstance(t, Struct):
+        return any(has_compatible(ft) for _, ft in t.fields)
+    if isinstance(t, (Vector, Optional)):
+        return has_compatible(t.elem)
+    return False
+
+
 class Variant(SpType):
     """std::variant<A, B, ...> (variant_t): wire [index:1][active
     alternative] (ref packer.hpp:389-398; decode: an index past the last
@@ -286,6 +318,11 @@ class Struct(SpType):
         return all(t.trivial for _, t in self.fields)
 
     @property
+    def trivial_ignoring_compatible(self):
+        """is_trivial_serializable<T, true> (reflection.hpp:851-921)."""
+        return all(isinstance(t, Compatible) or t.trivial for _, t in self.fields)
+
+    @property
     def has_container(self):
         return any(t.has_container for _, t in self.fields)
 
@@ -338,6 +375,9 @@ def resolve_flags(msg: SpType, conf: int = DEFAULT, debug: bool = False) -> int:
     if c == DEFAULT:
         c = msg.config & 0b11
     disable_head = c == DISABLE_ALL_META_INFO
+    if disable_head and has_compatible(msg):  # a static_assert in the reference
+        raise ValueError("compatible members need the hash head "
+                         "(type_calculate.hpp:868-876)")
     if c == DEFAULT:
         type_lit = debug
     else:
@@ -410,6 +450,12 @@ def flatten(rtype: SpType) -> DeviceLayout:
     if rtype.trivial:
         return DeviceLayout(rtype, rtype.size, [(C.SPK_OP_COPY, 0, rtype.size, 0)],
                             [], [("raw", f"V{rtype.size}", 0)], True)
+    if isinstance(rtype, Struct) and has_compatible(rtype) and rtype.trivial_ignoring_compatible:
+        # packer.hpp:422-431 writes such a struct field by field WITH padding
+        raise NotImplementedError(f"{rtype.name}: trivially serializable apart from "
+                                  "compatible members is outside the flat record model")
+    versions = sorted({ft.version for _, ft in getattr(rtype, "fields", [])
+                       if isinstance(ft, Compatible)})
     ops: List[Tuple[int, int, int, int]] = []
     spans: List[SpanField] = []
     npf: List[Tuple[str, str, int]] = []
@@ -429,6 +475,9 @@ def flatten(rtype: SpType) -> DeviceLayout:
         elif isinstance(t, (String, Vector)) and not t.elem.trivial:
             # container of non-trivially-serializable elements: SPK_OP_ARRAY
             # over the element's own flattened layout (packer.hpp:365-367)
+            if has_compatible(t.elem):
+                raise NotImplementedError(f"{path}: compatible members inside container "
+                                          "elements are outside the flat record model")
             sub = flatten(t.elem)
             coff = place(4, 4)
             ooff = place(8, 8)
@@ -457,6 +506,18 @@ def flatten(rtype: SpType) -> DeviceLayout:
             coff = place(4, 4)
             ooff = place(8, 8)
             ops.append((C.SPK_OP_OPTION, coff, t.elem.size, ooff))
+            spans.append(SpanField(path, t.elem, coff, ooff))
+            npf.append((path + ".n", "<u4", coff))
+            npf.append((path + ".off", "<u8", ooff))
+        elif isinstance(t, Compatible):
+            if t.elem.trivial is False or path.count(".") or path.count("["):
+                raise NotImplementedError(
+                    f"{path}: compatible<{t.elem.name}> is only in the flat record model "
+                    "as a top-level member with a trivially serializable value")
+            coff = place(4, 4)
+            ooff = place(8, 8)
+            rank = versions.index(t.version)
+            ops.append((C.SPK_OP_COMPAT | (rank << 8), coff, t.elem.size, ooff))
             spans.append(SpanField(path, t.elem, coff, ooff))
             npf.append((path + ".n", "<u4", coff))
             npf.append((path + ".off", "<u8", ooff))
@@ -524,7 +585,7 @@ def min_record_wire_bytes(dev: DeviceLayout) -> int:
         if k == C.SPK_OP_END:
             depth -= 1
             continue
-        if depth == 0:
+        if depth == 0 and (k & 0xFF) != C.SPK_OP_COMPAT:  # an older writer has none
             total += sz if k == C.SPK_OP_COPY else 1
         if k == C.SPK_OP_ARRAY:
             depth += 1
@@ -542,6 +603,8 @@ def heap_caps_for_wire(dev: DeviceLayout, wire_len: int, rec_cap: int) -> List[i
             caps.append(wire_len // max(sz, 1) + 1)
         elif k == C.SPK_OP_OPTION:
             caps.append(rec_cap if depth == 0 else wire_len + 1)
+        elif (k & 0xFF) == C.SPK_OP_COMPAT:
+            caps.append(rec_cap)
         elif k == C.SPK_OP_ARRAY:
             caps.append(wire_len + 1)
             depth += 1

@@ -97,6 +97,14 @@ Vnt = S.Struct("Vnt", [("id", S.int32),
                        ("w", S.Variant(S.Monostate(), S.Vector(S.int32))),
                        ("list", S.Vector(S.Variant(S.int64, S.String())))])
 
+# struct_pack::compatible members (types.hpp Cmp / CmpOld / CmpNew: one type
+# code, three writer versions)
+Cmp = S.Struct("Cmp", [("id", S.int32), ("a", S.Compatible(S.int64, 20210101)),
+                       ("name", S.String()), ("c", S.Compatible(S.float64, 20240101)),
+                       ("b", S.Compatible(S.int16, 20210101))])
+CmpOld = S.Struct("CmpOld", [("id", S.int32), ("name", S.String())])
+CmpNew = S.Struct("CmpNew", Cmp.fields + [("d", S.Compatible(S.int32, 20250101))])
+
 # alignment overrides (types.hpp; ref alignment.hpp, tests/test_alignas.cpp)
 Al8 = S.Struct("Al8", [("a", S.char), ("b", S.int16)], alignas=8)
 AlA = S.Struct("AlA", [("a", S.char), ("b", S.int16)], alignas=4)
@@ -109,7 +117,7 @@ CASE_TYPES = {"rec64": Rec64, "recs": RecS, "outer": Outer, "pad": Pad,
               "mixed": Mixed, "rect": RectInt, "rpcrect": RpcRect,
               "person": Person, "ints": Ints, "opt": Opt, "optp": OptP,
               "var": Var, "varp": VarP, "tags": Tags, "group": Group, "deep": Deep,
-              "vnt": Vnt, "al8": Al8, "alout": AlOuter, "packed": Packed, "alrec": AlRec}
+              "vnt": Vnt, "cmp": Cmp, "cmpold": CmpOld, "cmpnew": CmpNew, "al8": Al8, "alout": AlOuter, "packed": Packed, "alrec": AlRec}
 # vector<rect<int>> has its own ADL set_sp_config (benchmark data_def.hpp:69-72)
 VECTOR_CONFIG = {"rect": S.DISABLE_ALL_META_INFO}
 
@@ -401,6 +409,26 @@ def make_batch(case: str, n: int, seed: int, param: int = 48):
             heaps.append(_chars(seed, idx, lens))
             recs["p"] = packed_raw(rnd(seed, idx, 2)).view("V7").reshape(n)
             recs["e"] = al8_raw(rnd(seed, idx, 0)).view("V8").reshape(n)
+    elif case in ("cmp", "cmpold", "cmpnew"):  # fill(Cmp& / CmpOld& / CmpNew&)
+        recs["id"] = i32(rnd(seed, idx, 0))
+        m = rnd(seed, idx, 6)
+
+        def compat(field, bit, vals):
+            has = ((m >> np.uint64(bit)) & np.uint64(1)).astype(np.int64)
+            recs[field + ".n"] = has
+            recs[field + ".off"] = _excl(has)
+            heaps.append(np.ascontiguousarray(vals[has == 1]).view(np.uint8))
+        if case != "cmpold":
+            compat("a", 0, rnd(seed, idx, 2).view(np.int64))
+        lens = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+        recs["name.n"] = lens
+        recs["name.off"] = _excl(lens)
+        heaps.append(_chars(seed, idx, lens))
+        if case != "cmpold":
+            compat("c", 1, rd(rnd(seed, idx, 3)).astype("<f8"))
+            compat("b", 2, rnd(seed, idx, 4).astype(np.uint16).view(np.int16))
+        if case == "cmpnew":
+            compat("d", 3, i32(rnd(seed, idx, 5)))
     elif case == "vnt":  # fill(Vnt&)
         recs["id"] = i32(rnd(seed, idx, 0))
         a = (rnd(seed, idx, 1) % np.uint64(4)).astype(np.int64)
