@@ -1169,6 +1169,19 @@ __device__ __forceinline__ bool vi_seg(const WalkProg &P, uint32_t k, ByteFn byt
   return true;
 }
 
+// vi_seg through a reader's vread (the LDS window reads 8 bytes at once)
+template <typename Rd>
+__device__ __forceinline__ bool vi_seg_rd(const WalkProg &P, uint32_t k, const Rd &rd,
+                                          uint64_t len, uint64_t &p) {
+  for (uint32_t j = P.vfirst[k]; j < P.vfirst[k + 1]; ++j) {
+    uint64_t v;
+    const uint32_t l = rd.vread(p, len, &v);
+    if (!l || l == kViBad) return false;
+    p += l + P.vafter[j];
+  }
+  return true;
+}
+
 // Wire length of the record at `pos` (0 = incomplete: the reference fails it
 // with no_buffer_space). NS > 0: compile-time span count; 0: runtime count;
 // -1: runtime count and the record has varints.
@@ -1208,8 +1221,7 @@ __device__ __forceinline__ uint64_t wlen_rd(const WalkProg &P, const Rd &rd, uin
                                             uint64_t pos, uint32_t w, uint64_t *cnt = nullptr) {
   uint64_t p = pos + P.skip[0];
   const uint32_t ns = NS > 0 ? (uint32_t)NS : P.ns;
-  auto byte = [&rd](uint64_t x) { return rd.byte(x); };
-  if (NS < 0 && !vi_seg(P, 0, byte, len, p)) return 0;
+  if (NS < 0 && !vi_seg_rd(P, 0, rd, len, p)) return 0;
 #pragma unroll
   for (uint32_t k = 0; k < (NS > 0 ? (uint32_t)NS : SPK_MAX_SPANS); ++k) {
     if (NS <= 0 && k >= ns) break;
@@ -1229,7 +1241,7 @@ __device__ __forceinline__ uint64_t wlen_rd(const WalkProg &P, const Rd &rd, uin
     }
     if (cnt) cnt[k] = c;
     p += P.skip[k + 1];
-    if (NS < 0 && !vi_seg(P, k + 1, byte, len, p)) return 0;
+    if (NS < 0 && !vi_seg_rd(P, k + 1, rd, len, p)) return 0;
   }
   if (p > len) return 0;
   return p - pos;
@@ -1241,6 +1253,9 @@ struct GReader {
   uint32_t w;
   __device__ __forceinline__ uint64_t operator()(uint64_t x) const { return wire_le(wire, x, w); }
   __device__ __forceinline__ uint32_t byte(uint64_t x) const { return wire[x]; }
+  __device__ __forceinline__ uint32_t vread(uint64_t x, uint64_t len, uint64_t *v) const {
+    return vi_read(WireBytes{wire}, x, len, v);
+  }
 };
 
 __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
@@ -1362,6 +1377,30 @@ struct WinReader {
     }
     return wire[x];
   }
+  // LEB128 at x (message end len), as vi_read: eight bytes from the window at
+  // once -- the terminator is the first byte without its high bit, the value
+  // gathers the 7-bit groups -- and the byte loop for longer / edge varints
+  __device__ __forceinline__ uint32_t vread(uint64_t x, uint64_t len, uint64_t *v) const {
+    if (x + 12 <= wend) {
+      const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = o >> 2;
+      const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2];
+      const uint64_t b = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
+                         ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
+      const uint64_t t = ~b & 0x8080808080808080ull;
+      if (t) {
+        const uint32_t l = ((uint32_t)__builtin_ctzll(t) >> 3) + 1;
+        uint64_t m = b & 0x7F7F7F7F7F7F7F7Full;
+        if (l < 8) m &= (1ull << (8 * l)) - 1;
+        *v = (m & 0x7Full) | ((m >> 1) & (0x7Full << 7)) | ((m >> 2) & (0x7Full << 14)) |
+             ((m >> 3) & (0x7Full << 21)) | ((m >> 4) & (0x7Full << 28)) |
+             ((m >> 5) & (0x7Full << 35)) | ((m >> 6) & (0x7Full << 42)) |
+             ((m >> 7) & (0x7Full << 49));
+        return l;
+      }
+    }
+    auto bf = [this](uint64_t q) { return byte(q); };
+    return vi_read(bf, x, len, v);
+  }
   // 4 / 16 bytes at x (x + n <= wend: inside the staged window)
   __device__ __forceinline__ uint32_t ld4(uint64_t x) const {
     const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = o >> 2;
@@ -1425,8 +1464,7 @@ __device__ __forceinline__ void emit_record_rd(const KLayout &L, const WinReader
       pos += op.size;
     } else if (op.kind == SPK_OP_VARINT) {
       uint64_t v = 0;
-      auto byte = [&rd](uint64_t x) { return rd.byte(x); };
-      pos += vi_read(byte, pos, end, &v);
+      pos += rd.vread(pos, end, &v);
       if (!(dbg & 512)) vi_store(op, rec, v);
     } else {
       const uint64_t cnt = op.kind == SPK_OP_OPTION ? (uint64_t)(rd.byte(pos) != 0) : rd(pos);
@@ -1643,13 +1681,12 @@ __global__ __launch_bounds__(64 * kSpecWaves) void vec_spec(DecArgs a, WalkProg 
       if (NS < 0 && P.pf_var) {
         // varints before the first count: parse them per candidate, then
         // screen the count that follows
-        auto byte = [&rd](uint64_t q) { return rd.byte(q); };
         for (int k = 0; k < 8; ++k) {
           uint64_t q = b0 + k;
           bool ok = true;
           for (uint32_t j = 0; j < P.vfirst[1]; ++j) {
             uint64_t v;
-            const uint32_t l = vi_read(byte, q, len, &v);
+            const uint32_t l = rd.vread(q, len, &v);
             if (!l || l == kViBad) {
               ok = false;
               break;
@@ -2311,10 +2348,9 @@ __device__ __forceinline__ bool screen_one(const WalkProg &P, const Rd &rd, uint
   if (P.pf_all) return true;
   uint64_t b = q + P.skip[0];
   if (NS < 0 && P.pf_var) {
-    auto byte = [&rd](uint64_t x) { return rd.byte(x); };
     for (uint32_t j = 0; j < P.vfirst[1]; ++j) {
       uint64_t v;
-      const uint32_t l = vi_read(byte, b, len, &v);
+      const uint32_t l = rd.vread(b, len, &v);
       if (!l || l == kViBad) return false;
       b += l + P.vafter[j];
     }
@@ -2421,13 +2457,12 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
         const uint64_t b0 = cs + tt + s0;  // first count field of candidate cs+tt
         uint32_t m = 0;
         if (NS < 0 && P.pf_var) {
-          auto byte = [&rd](uint64_t q) { return rd.byte(q); };
           for (int kk = 0; kk < 8; ++kk) {
             uint64_t q = b0 + kk;
             bool ok = true;
             for (uint32_t j = 0; j < P.vfirst[1]; ++j) {
               uint64_t v;
-              const uint32_t l = vi_read(byte, q, len, &v);
+              const uint32_t l = rd.vread(q, len, &v);
               if (!l || l == kViBad) {
                 ok = false;
                 break;
