@@ -45,7 +45,12 @@
  *                                           integer at rec_off. Wire: LEB128 of
  *                                           the value (zigzag-mapped first for
  *                                           the signed types), 1-10 bytes
- *                                           (varint.hpp:245-330). Decode: a
+ *                                           (varint.hpp:245-330); aux
+ *                                           SPK_VARINT_SEXT: a plain int32_t of an
+ *                                           ENCODING_WITH_VARINT record, sign-
+ *                                           extended to 64 bits, no zigzag
+ *                                           (reflection.hpp:843, varint.hpp:
+ *                                           249-259). Decode: a
  *                                           10th byte with its high bit set is
  *                                           invalid_buffer; a truncated varint
  *                                           is no_buffer_space. Not a container.
@@ -81,6 +86,24 @@
  *                                           (unpacker.hpp:1278-1292).
  *   SPK_OP_END {0, 0, 0, 0}                closes the innermost open ARRAY or
  *                                           VARIANT alternative.
+ *   SPK_OP_FVAR {rec_off, size, aux}       a varint member of a top-level record
+ *                                           whose sp_config has USE_FAST_VARINT
+ *                                           (var_* types; with ENCODING_WITH_VARINT
+ *                                           also plain (u)int32/64): a `size`-byte
+ *                                           integer at rec_off, aux
+ *                                           SPK_FVAR_SIGNED for the signed types.
+ *                                           Wire: before the record's other
+ *                                           members, a bitset of ceil((k+2)/8)
+ *                                           bytes (bit j: FVAR j is non-zero; bits
+ *                                           k, k+1: width code c) then every
+ *                                           non-zero FVAR in op order as its low
+ *                                           min(2^c, size) bytes; c from the
+ *                                           largest unsigned value / signed
+ *                                           magnitude (v<0: -(v+1)) (packer.hpp:
+ *                                           152-235). Decode sign-extends the
+ *                                           signed ones; c = 3 without a 64-bit
+ *                                           FVAR is invalid_buffer (unpacker.hpp:
+ *                                           642-747).
  *   SPK_OP_COMPAT {rec_off, size, aux}     a struct_pack::compatible<U, ver>
  *                                           member (U trivially serializable) of
  *                                           the top-level record: record fields
@@ -177,12 +200,16 @@ extern "C" {
 #define SPK_OP_END 6u
 #define SPK_OP_VARIANT 7u
 #define SPK_OP_COMPAT 8u       /* | rank << 8 (see above)                    */
+#define SPK_OP_FVAR 9u
 #define SPK_OP_KIND(k) ((k) & 0xFFu)
 #define SPK_OP_RANK(k) ((k) >> 8)
 #define SPK_MAX_DEPTH 4u       /* ARRAY / VARIANT nesting levels             */
 
 /* spk_op.aux of an SPK_OP_VARINT */
 #define SPK_VARINT_ZIGZAG 0x1u /* var_int32_t / var_int64_t (sint<T>): zigzag */
+#define SPK_VARINT_SEXT 0x2u   /* plain int32_t under ENCODING_WITH_VARINT     */
+/* spk_op.aux of an SPK_OP_FVAR */
+#define SPK_FVAR_SIGNED 0x1u
 #define SPK_MAX_VARINTS 16u    /* varint members per record                  */
 
 #define SPK_MODE_VECTOR 0
@@ -198,7 +225,7 @@ extern "C" {
 #define SPK_LAYOUT_TRIVIAL 0x1u   /* is_trivial_serializable<T>: 1 COPY op  */
 
 typedef struct spk_op {
-  uint32_t kind;    /* SPK_OP_COPY | SPAN | OPTION | VARINT | ARRAY | END | VARIANT | COMPAT */
+  uint32_t kind;    /* SPK_OP_COPY | SPAN | OPTION | VARINT | ARRAY | END | VARIANT | COMPAT | FVAR */
   uint32_t rec_off; /* COPY: source byte offset; SPAN: u32 count offset      */
   uint32_t size;    /* COPY: byte length;       SPAN: element size (bytes)   */
   uint32_t aux;     /* SPAN: u64 heap element-offset field offset; COPY: 0   */

@@ -167,6 +167,10 @@ constexpr uint32_t msg_flags() {
 template <typename T, uint64_t conf = sp_config::DEFAULT>
 spk_layout make_spk_layout() {
   using namespace detail;
+  static_assert((type_config<T>() & (sp_config::ENCODING_WITH_VARINT | sp_config::USE_FAST_VARINT)) == 0,
+                "MI355X codec C++ front end: records with ENCODING_WITH_VARINT / USE_FAST_VARINT "
+                "are described through the C ABI (SPK_OP_FVAR, SPK_VARINT_SEXT) by the Python "
+                "mirror; this front end does not flatten them yet");
   layout_builder b;
   b.L.abi = SPK_ABI_VERSION;
   collect_versions<T>(b);

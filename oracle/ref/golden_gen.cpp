@@ -115,6 +115,12 @@ static int cmd_kat() {
   kat_one<std::vector<Cmp>>(os, "vector<Cmp>", first);
   kat_one<CmpOld>(os, "CmpOld", first);
   kat_one<CmpNew>(os, "CmpNew", first);
+  kat_one<FV>(os, "FV", first);
+  kat_one<std::vector<FV>>(os, "vector<FV>", first);
+  kat_one<FVE>(os, "FVE", first);
+  kat_one<FV32>(os, "FV32", first);
+  kat_one<EV>(os, "EV", first);
+  kat_one<std::vector<EV>>(os, "vector<EV>", first);
   kat_one<uint8_t, uint16_t, uint32_t, uint64_t, int8_t, int16_t, int64_t,
           bool, char, float, double>(os, "fundamentals", first);
   os << "\n}\n";
@@ -228,6 +234,14 @@ static bool with_case(const Args &a, F &&f) {
     return f.template operator()<CmpOld>([=](CmpOld &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "cmpnew")
     return f.template operator()<CmpNew>([=](CmpNew &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "fv")
+    return f.template operator()<FV>([=](FV &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "fve")
+    return f.template operator()<FVE>([=](FVE &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "fv32")
+    return f.template operator()<FV32>([=](FV32 &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "ev")
+    return f.template operator()<EV>([=](EV &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "deep")
     return f.template operator()<Deep>([=](Deep &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "rect")  // C1: benchmark rect<int> default values

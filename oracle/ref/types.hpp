@@ -238,6 +238,54 @@ struct CmpNew {
   struct_pack::compatible<int16_t, 20210101> b;
   struct_pack::compatible<int32_t, 20250101> d;
 };
+// ---- sp_config varint encodings of the record (reflection.hpp:53-60) ------
+// USE_FAST_VARINT: [bitset: non-zero flags + 2 width bits][non-zero varints at
+// one width] before the other members (packer.hpp:200-235);
+// ENCODING_WITH_VARINT: plain int32/64 and uint32/64 members are varints
+// (reflection.hpp:843), LEB128 without zigzag.
+struct FV {
+  struct_pack::var_int32_t a;
+  std::string s;
+  struct_pack::var_uint64_t b;
+  double d;
+  struct_pack::var_int64_t c;
+  struct_pack::var_uint32_t e;
+};
+constexpr struct_pack::sp_config set_sp_config(FV *) {
+  return struct_pack::sp_config::USE_FAST_VARINT;
+}
+struct FVE {
+  int32_t a;
+  std::string s;
+  uint64_t b;
+  double d;
+  int64_t c;
+  uint32_t e;
+  int16_t f;
+};
+constexpr struct_pack::sp_config set_sp_config(FVE *) {
+  return static_cast<struct_pack::sp_config>(struct_pack::sp_config::ENCODING_WITH_VARINT |
+                                             struct_pack::sp_config::USE_FAST_VARINT);
+}
+struct FV32 {  // 32-bit varints only: width code 3 is invalid_buffer on decode
+  struct_pack::var_uint32_t a;
+  int16_t x;
+  struct_pack::var_int32_t b;
+};
+constexpr struct_pack::sp_config set_sp_config(FV32 *) {
+  return struct_pack::sp_config::USE_FAST_VARINT;
+}
+struct EV {
+  int32_t a;
+  std::string s;
+  uint64_t b;
+  int64_t c;
+  uint32_t e;
+};
+constexpr struct_pack::sp_config set_sp_config(EV *) {
+  return struct_pack::sp_config::ENCODING_WITH_VARINT;
+}
+
 template <typename T>
 constexpr bool kHasCompat = false;
 template <>
@@ -448,6 +496,52 @@ inline void fill(Vnt &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
     else
       o.list.emplace_back((int64_t)(h >> 1));
   }
+}
+
+// varint values with one magnitude per record (64 - sh bits), member j zero
+// when bit j of z is set, signed ones negated (~x) on bit 0 of their word
+struct FvGen {
+  uint64_t seed, i;
+  uint32_t sh, z;
+  FvGen(uint64_t s, uint64_t i_) : seed(s), i(i_) {
+    const uint64_t r7 = rnd(s, i_, 7);
+    sh = (uint32_t)(r7 >> 58);
+    z = (uint32_t)r7;
+  }
+  uint64_t u(uint32_t j) const { return ((z >> j) & 1) ? 0 : rnd(seed, i, j) >> sh; }
+  uint64_t sg(uint32_t j) const {
+    const uint64_t x = u(j);
+    return ((z >> j) & 1) ? 0 : (rnd(seed, i, j) & 1) ? ~x : x;
+  }
+};
+template <typename F>
+inline void fill_fv(F &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
+  const FvGen g(seed, i);
+  o.a = (int32_t)(uint32_t)g.sg(0);
+  o.s = make_chars(seed, i, maxlen);
+  o.b = g.u(2);
+  o.d = rd(rnd(seed, i, 60));
+  o.c = (int64_t)g.sg(3);
+  o.e = (uint32_t)g.u(4);
+}
+inline void fill(FV &o, uint64_t seed, uint64_t i, uint32_t maxlen) { fill_fv(o, seed, i, maxlen); }
+inline void fill(FVE &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
+  fill_fv(o, seed, i, maxlen);
+  o.f = (int16_t)rnd(seed, i, 5);
+}
+inline void fill(FV32 &o, uint64_t seed, uint64_t i, uint32_t) {
+  const FvGen g(seed, i);
+  o.a = (uint32_t)g.u(0);
+  o.x = (int16_t)rnd(seed, i, 5);
+  o.b = (int32_t)(uint32_t)g.sg(1);
+}
+inline void fill(EV &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
+  const FvGen g(seed, i);
+  o.a = (int32_t)(uint32_t)g.sg(0);
+  o.s = make_chars(seed, i, maxlen);
+  o.b = g.u(2);
+  o.c = (int64_t)g.sg(3);
+  o.e = (uint32_t)g.u(4);
 }
 
 template <typename C>

@@ -28,6 +28,7 @@ static uint64_t vi_value(const uint8_t *rec, const spk_op *op) {
   if (op->size == 4) {
     uint32_t u;
     memcpy(&u, rec + op->rec_off, 4);
+    if (op->aux & SPK_VARINT_SEXT) return (uint64_t)(int64_t)(int32_t)u; /* v = t */
     if (op->aux & SPK_VARINT_ZIGZAG) u = (u << 1) ^ (uint32_t)(-(int32_t)(u >> 31));
     return u;
   }
@@ -102,6 +103,96 @@ static uint32_t alt_start(const spk_layout *L, uint32_t i, uint32_t a) {
   while (a--) j = group_end(L, j) + 1;
   return j;
 }
+/* ---- USE_FAST_VARINT group of the top-level record (packer.hpp:152-235,
+ * calculate_size.hpp:191-390, unpacker.hpp:642-747) ---------------------- */
+typedef struct fv_t {
+  unsigned cnt, has64, bits; /* FVAR ops, any 64-bit one, bitset bytes */
+} fv_t;
+static fv_t fv_shape(const spk_layout *L) {
+  fv_t f = {0, 0, 0};
+  for (uint32_t i = 0; i < L->n_ops; ++i)
+    if (L->ops[i].kind == SPK_OP_FVAR) {
+      ++f.cnt;
+      f.has64 |= L->ops[i].size == 8;
+    }
+  f.bits = f.cnt ? (f.cnt + 2 + 7) / 8 : 0;
+  return f;
+}
+static int64_t fv_signed(const uint8_t *rec, const spk_op *op) {
+  if (op->size == 4) {
+    int32_t v;
+    memcpy(&v, rec + op->rec_off, 4);
+    return v;
+  }
+  int64_t v;
+  memcpy(&v, rec + op->rec_off, 8);
+  return v;
+}
+static uint64_t fv_raw(const uint8_t *rec, const spk_op *op) {
+  uint64_t v = 0;
+  memcpy(&v, rec + op->rec_off, op->size);
+  return v;
+}
+/* get_fast_varint_width_from_max: 0..3 from the largest unsigned value and
+   the largest signed magnitude (v > 0 ? v : -(v + 1)) of the non-zero ones */
+static unsigned fv_code(const spk_layout *L, const uint8_t *rec) {
+  uint64_t um = 0, sm = 0;
+  int hu = 0, hs = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i) {
+    const spk_op *op = &L->ops[i];
+    if (op->kind != SPK_OP_FVAR) continue;
+    if (op->aux & SPK_FVAR_SIGNED) {
+      hs = 1;
+      const int64_t v = fv_signed(rec, op);
+      const uint64_t m = v > 0 ? (uint64_t)v : (uint64_t)(-(v + 1));
+      if (v && m > sm) sm = m;
+    } else {
+      hu = 1;
+      const uint64_t v = fv_raw(rec, op);
+      if (v > um) um = v;
+    }
+  }
+  unsigned cu = um <= 0xFFull ? 0 : um <= 0xFFFFull ? 1 : um <= 0xFFFFFFFFull ? 2 : 3;
+  unsigned cs = sm <= 0x7Full ? 0 : sm <= 0x7FFFull ? 1 : sm <= 0x7FFFFFFFull ? 2 : 3;
+  if (!hu) cu = 0;
+  if (!hs) cs = 0;
+  return cu > cs ? cu : cs;
+}
+static uint64_t fv_size(const spk_layout *L, const uint8_t *rec) {
+  const fv_t f = fv_shape(L);
+  if (!f.cnt) return 0;
+  const unsigned wb = 1u << fv_code(L, rec);
+  uint64_t b = f.bits;
+  for (uint32_t i = 0; i < L->n_ops; ++i)
+    if (L->ops[i].kind == SPK_OP_FVAR && fv_raw(rec, &L->ops[i]))
+      b += wb < L->ops[i].size ? wb : L->ops[i].size;
+  return b;
+}
+static uint8_t *fv_write(const spk_layout *L, const uint8_t *rec, uint8_t *p) {
+  const fv_t f = fv_shape(L);
+  if (!f.cnt) return p;
+  const unsigned code = fv_code(L, rec), wb = 1u << code;
+  uint8_t *bs = p;
+  memset(bs, 0, f.bits);
+  p += f.bits;
+  unsigned j = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i) {
+    const spk_op *op = &L->ops[i];
+    if (op->kind != SPK_OP_FVAR) continue;
+    const uint64_t v = fv_raw(rec, op);
+    if (v) {
+      bs[j / 8] |= (uint8_t)(1u << (j % 8));
+      const unsigned rw = wb < op->size ? wb : op->size;
+      put_le(p, v, rw); /* low_bytes_write_wrapper */
+      p += rw;
+    }
+    ++j;
+  }
+  bs[f.cnt / 8] |= (uint8_t)((code & 1u) << (f.cnt % 8));
+  bs[(f.cnt + 1) / 8] |= (uint8_t)(((code >> 1) & 1u) << ((f.cnt + 1) % 8));
+  return p;
+}
+
 static uint64_t rec_count(const uint8_t *rec, const spk_op *op) {
   uint32_t c;
   memcpy(&c, rec + op->rec_off, 4);
@@ -232,6 +323,7 @@ static void rec_size(const spk_layout *L, const uint8_t *rec, const void *const 
     return;
   }
   ops_size(L, 0, L->n_ops, rec, heaps, bytes, cnts, maxc);
+  *bytes += fv_size(L, rec);
 }
 
 /* serialize_one (packer.hpp:237-527) of ops [i0, i1) over one (element)
@@ -245,7 +337,8 @@ static uint8_t *ops_write(const spk_layout *L, uint32_t i0, uint32_t i1, const u
       memcpy(p, rec + op->rec_off, op->size);
       p += op->size;
     }
-    else if (is_compat(op->kind)) { /* version UINT64_MAX: nothing (:246-249) */
+    else if (is_compat(op->kind) || op->kind == SPK_OP_FVAR) {
+      /* version UINT64_MAX: nothing (:246-249); fast varints: in the group */
     }
     else if (op->kind == SPK_OP_VARINT) { /* serialize_varint :245-268 */
       uint64_t v = vi_value(rec, op);
@@ -295,6 +388,7 @@ static uint8_t *write_record(const spk_layout *L, const uint8_t *rec,
     memcpy(p, rec, L->rec_stride);
     return p + L->rec_stride;
   }
+  p = fv_write(L, rec, p); /* before the members (packer.hpp:432-440) */
   return ops_write(L, 0, L->n_ops, rec, heaps, w, p);
 }
 
@@ -497,6 +591,7 @@ static int32_t ops_read(dctx_t *c, rd_t *r, unsigned w, uint32_t i0, uint32_t i1
       if (rec) memcpy(rec + op->rec_off, p, op->size);
       continue;
     }
+    if (op->kind == SPK_OP_FVAR) continue; /* read with the record's group */
     if (is_compat(op->kind)) { /* main pass: absent until its version pass */
       if (rec) {
         const uint32_t z = 0;
@@ -609,6 +704,30 @@ static int32_t read_record(dctx_t *c, rd_t *r, unsigned w, uint8_t *rec) {
     if (!rd_take(r, L->rec_stride, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
     if (rec) memcpy(rec, p, L->rec_stride);
     return SPK_ERRC_OK;
+  }
+  const fv_t f = fv_shape(L);
+  if (f.cnt) { /* deserialize_fast_varint (unpacker.hpp:702-747) */
+    if (!rd_take(r, f.bits, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
+    const uint8_t *bs = p;
+    const unsigned code = ((bs[f.cnt / 8] >> (f.cnt % 8)) & 1u) |
+                          (((bs[(f.cnt + 1) / 8] >> ((f.cnt + 1) % 8)) & 1u) << 1);
+    if (code == 3 && !f.has64) return SPK_ERRC_INVALID_BUFFER;
+    const unsigned wb = 1u << code;
+    unsigned j = 0;
+    for (uint32_t i = 0; i < L->n_ops; ++i) {
+      const spk_op *op = &L->ops[i];
+      if (op->kind != SPK_OP_FVAR) continue;
+      uint64_t v = 0;
+      if ((bs[j / 8] >> (j % 8)) & 1u) { /* deserialize_one_fast_varint :642-682 */
+        const unsigned rw = wb < op->size ? wb : op->size;
+        if (!rd_take(r, rw, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
+        v = get_le(p, rw);
+        if ((op->aux & SPK_FVAR_SIGNED) && rw < 8 && (v >> (8 * rw - 1)) & 1u)
+          v |= ~0ull << (8 * rw); /* int_t<real_width> -> the member */
+      }
+      if (rec) put_le(rec + op->rec_off, v, op->size);
+      ++j;
+    }
   }
   return ops_read(c, r, w, 0, L->n_ops, rec);
 }

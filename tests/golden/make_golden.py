@@ -34,7 +34,8 @@ SEED = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004,
         "deep": 0x5EED0010, "vnt": 0x5EED0011, "al8": 0x5EED0012, "alout": 0x5EED0013,
         "packed": 0x5EED0014, "alrec": 0x5EED0015,
         # one seed for the three writer versions of Cmp (same records)
-        "cmp": 0x5EED0016, "cmpold": 0x5EED0016, "cmpnew": 0x5EED0016}
+        "cmp": 0x5EED0016, "cmpold": 0x5EED0016, "cmpnew": 0x5EED0016,
+        "fv": 0x5EED0017, "fve": 0x5EED0018, "fv32": 0x5EED0019, "ev": 0x5EED001A}
 
 # (case_mode, n, param, conf, keep_bin)
 SMALL = [
@@ -102,6 +103,12 @@ SMALL = [
     ("cmp_B", 30, 300, "default"), ("cmp_A", 3000, 30, "default"),
     ("cmpold_A", 200, 8, "default"), ("cmpold_B", 100, 8, "default"),
     ("cmpnew_A", 200, 8, "default"), ("cmpnew_B", 100, 8, "default"),
+    # sp_config USE_FAST_VARINT / ENCODING_WITH_VARINT records
+    ("fv_A", 0, 8, "default"), ("fv_A", 1, 8, "default"), ("fv_A", 300, 8, "default"),
+    ("fv_A", 40, 300, "default"), ("fv_A", 50, 8, "typeinfo"), ("fv_B", 300, 8, "default"),
+    ("fv_A", 30, 8, "nometa"), ("fve_A", 300, 8, "default"), ("fve_B", 200, 8, "default"),
+    ("fv32_A", 300, 0, "default"), ("fv32_B", 200, 0, "default"),
+    ("ev_A", 300, 8, "default"), ("ev_B", 200, 8, "default"), ("ev_A", 30, 8, "nometa"),
 ]
 MEDIUM = [  # digest only (wire > ~1 MB)
     ("rec64_A", 65535, 0, "default"), ("rec64_A", 65536, 0, "default"),
@@ -117,6 +124,8 @@ MEDIUM = [  # digest only (wire > ~1 MB)
     ("group_A", 20000, 5, "default"), ("deep_A", 20000, 4, "default"),
     ("vnt_A", 30000, 8, "default"), ("vnt_B", 20000, 8, "default"),
     ("cmp_A", 30000, 48, "default"), ("cmp_B", 20000, 48, "default"),
+    ("fv_A", 70000, 48, "default"), ("fve_B", 20000, 16, "default"),
+    ("ev_A", 70000, 16, "default"),
     ("recs_A", 200, 20000, "default"), ("outer_A", 100, 2000, "default"),
 ]
 BIG = [  # BASELINE.json full-size configs (digest only)
@@ -241,6 +250,9 @@ ERR_BASES = [
     ("mixed_A", 3, 20, "default", 4), ("recs_A", 4, 10, "default", 2),
     ("cmp_A", 6, 10, "default"), ("cmp_B", 1, 20, "default"), ("cmp_A", 3, 10, "typeinfo"),
     ("cmp_B", 1, 300, "default"),
+    ("fv_A", 6, 10, "default"), ("fv_B", 1, 10, "default"), ("fve_A", 5, 6, "default"),
+    ("fv32_A", 8, 0, "default"), ("fv32_B", 1, 0, "default"), ("ev_A", 5, 6, "default"),
+    ("ev_B", 1, 6, "default"),
 ]
 # compatible members across writer versions: (writer, reader, n, param) — the
 # writer's message mutated and decoded as the reader's type (one type code)

@@ -120,6 +120,33 @@ def test_layout_check_compat_ops():
                                None) == C.SPK_E_LAYOUT
 
 
+def test_layout_check_fast_varint_ops():
+    """USE_FAST_VARINT: one SPK_OP_FVAR per varint member of the top-level
+    record (signed flag for var_int* / int*); ENCODING_WITH_VARINT alone turns
+    plain ints into VARINT ops (int32_t sign-extended, no zigzag)."""
+    lib = C.load_codec()
+    L = LY.case_layout("fve")
+    fv = [(L.c.ops[i].kind, L.c.ops[i].size, L.c.ops[i].aux) for i in range(L.c.n_ops)
+          if L.c.ops[i].kind == C.SPK_OP_FVAR]
+    assert fv == [(9, 4, 1), (9, 8, 0), (9, 8, 1), (9, 4, 0)]  # int32, uint64, int64, uint32
+    assert lib.spk_layout_check(L.ptr) == 0
+    i0 = next(i for i in range(L.c.n_ops) if L.c.ops[i].kind == C.SPK_OP_FVAR)
+    for field, bad in (("size", 2), ("rec_off", 2), ("aux", 2)):
+        Lb = LY.case_layout("fve")
+        setattr(Lb.c.ops[i0], field, bad)
+        assert lib.spk_layout_check(Lb.ptr) == C.SPK_E_LAYOUT, (field, bad)
+    Le = LY.case_layout("ev")
+    vi = [(Le.c.ops[i].size, Le.c.ops[i].aux) for i in range(Le.c.n_ops)
+          if Le.c.ops[i].kind == C.SPK_OP_VARINT]
+    assert vi == [(4, C.SPK_VARINT_SEXT), (8, 0), (8, 0), (4, 0)]
+    Lb = LY.case_layout("ev")
+    k = next(i for i in range(Lb.c.n_ops) if Lb.c.ops[i].kind == C.SPK_OP_VARINT)
+    Lb.c.ops[k].aux = C.SPK_VARINT_SEXT | C.SPK_VARINT_ZIGZAG
+    assert lib.spk_layout_check(Lb.ptr) == C.SPK_E_LAYOUT
+    with pytest.raises(NotImplementedError):  # the tag on a nested struct
+        LY.make_layout(S.Struct("W", [("k", S.int32), ("v", synth.FV)]))
+
+
 def test_encode_rejects_bad_args_without_device_work():
     lib = C.load_codec()
     L = LY.case_layout("rec64")

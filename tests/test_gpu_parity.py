@@ -172,7 +172,9 @@ RANDOM = [("recs", 1, 300), ("recs", 257, 5), ("recs", 5000, 48), ("recs", 20000
           ("tags", 3000, 6), ("tags", 200, 300), ("group", 500, 5), ("group", 3, 2000),
           ("deep", 700, 4), ("vnt", 3000, 8), ("vnt", 100, 400), ("al8", 5000, 0),
           ("alout", 3000, 0), ("packed", 4097, 0), ("alrec", 3000, 30),
-          ("cmp", 5000, 48), ("cmp", 300, 400), ("cmpnew", 20000, 8), ("cmp", 1, 8)]
+          ("cmp", 5000, 48), ("cmp", 300, 400), ("cmpnew", 20000, 8), ("cmp", 1, 8),
+          ("fv", 5000, 48), ("fv", 200, 400), ("fve", 3000, 8), ("fv32", 4000, 0),
+          ("ev", 5000, 16), ("ev", 30000, 4)]
 
 
 @pytest.mark.parametrize("case,n,param", RANDOM)
@@ -232,7 +234,8 @@ def _irregular_messages(cd, case, n, seed, param):
                                           ("varp", 400, 0), ("tags", 300, 6),
                                           ("group", 200, 4), ("deep", 200, 3),
                                           ("vnt", 300, 6), ("cmp", 300, 8),
-                                          ("cmpnew", 300, 8)])
+                                          ("cmpnew", 300, 8), ("fv", 300, 8),
+                                          ("fv32", 300, 0), ("ev", 300, 8)])
 @pytest.mark.parametrize("cap_frac", [1.0, 0.6])
 def test_messages_irregular_vs_oracle(case, n, param, cap_frac):
     """Mode B decode of non-canonical message batches: per-message errc,

@@ -40,6 +40,9 @@ SPK_OP_ARRAY = 5
 SPK_OP_END = 6
 SPK_OP_VARIANT = 7
 SPK_OP_COMPAT = 8  # | version rank << 8
+SPK_OP_FVAR = 9
+SPK_FVAR_SIGNED = 1
+SPK_VARINT_SEXT = 2
 SPK_MAX_DEPTH = 4
 SPK_VARINT_ZIGZAG = 1
 SPK_MAX_VARINTS = 16

@@ -112,7 +112,7 @@ int spk_layout_check(const spk_layout *L) {
     if (L->fmt_one.flags & SPK_MF_HAS_CONTAINER) return SPK_E_LAYOUT;
     return SPK_OK;
   }
-  uint32_t spans = 0, conts = 0, vars = 0;
+  uint32_t spans = 0, conts = 0, vars = 0, fvars = 0;
   // open ARRAY element layouts / VARIANT alternatives (level 0: the top
   // record): the record stride, ops seen, alternatives still to close
   uint32_t stride[SPK_MAX_DEPTH + 1] = {L->rec_stride}, depth = 0, nops[SPK_MAX_DEPTH + 1] = {0};
@@ -164,7 +164,13 @@ int spk_layout_check(const spk_layout *L) {
       --depth;
     } else if (o.kind == SPK_OP_VARINT) {  // var_(u)int32_t / var_(u)int64_t member
       if ((o.size != 4 && o.size != 8) || o.rec_off % o.size || o.rec_off + o.size > rs ||
-          (o.aux & ~SPK_VARINT_ZIGZAG))
+          (o.aux & ~(SPK_VARINT_ZIGZAG | SPK_VARINT_SEXT)) ||
+          ((o.aux & SPK_VARINT_SEXT) && (o.size != 4 || (o.aux & SPK_VARINT_ZIGZAG))))
+        return SPK_E_LAYOUT;
+      ++vars;
+    } else if (o.kind == SPK_OP_FVAR) {  // the top-level record's fast-varint group
+      if (depth || (o.size != 4 && o.size != 8) || o.rec_off % o.size ||
+          o.rec_off + o.size > rs || (o.aux & ~SPK_FVAR_SIGNED) || ++fvars > SPK_MAX_VARINTS)
         return SPK_E_LAYOUT;
       ++vars;
     } else {

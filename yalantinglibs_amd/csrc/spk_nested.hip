@@ -33,6 +33,7 @@ struct NLayout {
   uint8_t end[SPK_MAX_OPS];   // ARRAY: its END; VARIANT: the END of its last alternative
   uint8_t crank[SPK_MAX_OPS]; // COMPAT: its version rank (ops[i].kind is SPK_OP_COMPAT)
   uint32_t n_ops, stride, n_heaps, n_ranks;
+  uint32_t fv_cnt, fv_has64, fv_bits;  // USE_FAST_VARINT group: FVAR ops, a 64-bit one, bitset bytes
 };
 
 // layouts the interpreter runs: an ARRAY (element layouts), a VARIANT or a
@@ -40,7 +41,8 @@ struct NLayout {
 bool layout_nested(const spk_layout *L) {
   for (uint32_t i = 0; i < L->n_ops; ++i) {
     const uint32_t k = SPK_OP_KIND(L->ops[i].kind);
-    if (k == SPK_OP_ARRAY || k == SPK_OP_VARIANT || k == SPK_OP_COMPAT) return true;
+    if (k == SPK_OP_ARRAY || k == SPK_OP_VARIANT || k == SPK_OP_COMPAT || k == SPK_OP_FVAR)
+      return true;
   }
   return false;
 }
@@ -60,6 +62,10 @@ static NLayout make_nlayout(const spk_layout *L) {
       if (N.crank[i] + 1u > N.n_ranks) N.n_ranks = N.crank[i] + 1u;
     }
     if (op_has_heap(k)) N.heap[i] = (uint8_t)h++;
+    if (k == SPK_OP_FVAR) {
+      ++N.fv_cnt;
+      N.fv_has64 |= L->ops[i].size == 8;
+    }
     if (k == SPK_OP_ARRAY || k == SPK_OP_VARIANT) {
       stack[d] = i;
       left[d++] = k == SPK_OP_VARIANT ? L->ops[i].size : 1;
@@ -67,6 +73,7 @@ static NLayout make_nlayout(const spk_layout *L) {
     if (k == SPK_OP_END && d && --left[d - 1] == 0) N.end[stack[--d]] = (uint8_t)i;
   }
   N.n_heaps = h;
+  N.fv_bits = N.fv_cnt ? (N.fv_cnt + 2 + 7) / 8 : 0;
   return N;
 }
 
@@ -75,6 +82,7 @@ __device__ __forceinline__ uint64_t n_vi_value(const spk_op &op, const uint8_t *
   // serialize_varint (varint.hpp:245-268): sint<T> zigzag at its own width
   if (op.size == 4) {
     uint32_t u = *reinterpret_cast<const uint32_t *>(rec + op.rec_off);
+    if (op.aux & SPK_VARINT_SEXT) return (uint64_t)(int64_t)(int32_t)u;  // plain int32_t: v = t
     if (op.aux & SPK_VARINT_ZIGZAG) u = (u << 1) ^ (uint32_t)(-(int32_t)(u >> 31));
     return u;
   }
@@ -134,6 +142,116 @@ __device__ __forceinline__ uint32_t n_alt_end(const NLayout &N, uint32_t j) {
   }
 }
 
+// ---- USE_FAST_VARINT group of the top-level record (packer.hpp:152-235,
+// calculate_size.hpp:191-390, unpacker.hpp:642-747): a bitset of non-zero
+// flags + 2 width bits, then the non-zero values at min(2^code, size) bytes --
+__device__ __forceinline__ uint64_t n_fv_raw(const spk_op &op, const uint8_t *rec) {
+  return op.size == 4 ? *reinterpret_cast<const uint32_t *>(rec + op.rec_off)
+                      : *reinterpret_cast<const uint64_t *>(rec + op.rec_off);
+}
+__device__ uint32_t n_fv_code(const NLayout &N, const uint8_t *rec) {
+  uint64_t um = 0, sm = 0;
+  bool hu = false, hs = false;
+  for (uint32_t i = 0; i < N.n_ops; ++i) {
+    const spk_op op = N.ops[i];
+    if (op.kind != SPK_OP_FVAR) continue;
+    const uint64_t r = n_fv_raw(op, rec);
+    if (op.aux & SPK_FVAR_SIGNED) {
+      hs = true;
+      const int64_t v = op.size == 4 ? (int64_t)(int32_t)(uint32_t)r : (int64_t)r;
+      const uint64_t m = v > 0 ? (uint64_t)v : (uint64_t)(-(v + 1));
+      if (v && m > sm) sm = m;
+    } else {
+      hu = true;
+      if (r > um) um = r;
+    }
+  }
+  const uint32_t cu = !hu ? 0u : um <= 0xFFull ? 0u : um <= 0xFFFFull ? 1u : um <= 0xFFFFFFFFull ? 2u : 3u;
+  const uint32_t cs = !hs ? 0u : sm <= 0x7Full ? 0u : sm <= 0x7FFFull ? 1u : sm <= 0x7FFFFFFFull ? 2u : 3u;
+  return cu > cs ? cu : cs;
+}
+__device__ uint64_t n_fv_size(const NLayout &N, const uint8_t *rec) {
+  if (!N.fv_cnt) return 0;
+  const uint32_t wb = 1u << n_fv_code(N, rec);
+  uint64_t b = N.fv_bits;
+  for (uint32_t i = 0; i < N.n_ops; ++i)
+    if (N.ops[i].kind == SPK_OP_FVAR && n_fv_raw(N.ops[i], rec))
+      b += wb < N.ops[i].size ? wb : N.ops[i].size;
+  return b;
+}
+__device__ uint8_t *n_fv_write(const NLayout &N, const uint8_t *rec, uint8_t *p) {
+  if (!N.fv_cnt) return p;
+  const uint32_t code = n_fv_code(N, rec), wb = 1u << code;
+  uint8_t bs[(SPK_MAX_VARINTS + 2 + 7) / 8] = {};
+  uint8_t *q = p + N.fv_bits;
+  uint32_t j = 0;
+  for (uint32_t i = 0; i < N.n_ops; ++i) {
+    const spk_op op = N.ops[i];
+    if (op.kind != SPK_OP_FVAR) continue;
+    const uint64_t v = n_fv_raw(op, rec);
+    if (v) {
+      bs[j / 8] |= (uint8_t)(1u << (j % 8));
+      const uint32_t rw = wb < op.size ? wb : op.size;
+      for (uint32_t b = 0; b < rw; ++b) q[b] = (uint8_t)(v >> (8 * b));
+      q += rw;
+    }
+    ++j;
+  }
+  bs[N.fv_cnt / 8] |= (uint8_t)((code & 1u) << (N.fv_cnt % 8));
+  bs[(N.fv_cnt + 1) / 8] |= (uint8_t)(((code >> 1) & 1u) << ((N.fv_cnt + 1) % 8));
+  for (uint32_t b = 0; b < N.fv_bits; ++b) p[b] = bs[b];
+  return q;
+}
+// the group's wire length from its bitset at wire[pos] (the caller checked
+// the bitset is there); 0 for the invalid width code
+__device__ __forceinline__ uint64_t n_fv_len(const NLayout &N, const uint8_t *bs) {
+  const uint32_t code = ((bs[N.fv_cnt / 8] >> (N.fv_cnt % 8)) & 1u) |
+                        (((bs[(N.fv_cnt + 1) / 8] >> ((N.fv_cnt + 1) % 8)) & 1u) << 1);
+  if (code == 3 && !N.fv_has64) return 0;
+  const uint32_t wb = 1u << code;
+  uint64_t b = N.fv_bits;
+  uint32_t j = 0;
+  for (uint32_t i = 0; i < N.n_ops; ++i) {
+    if (N.ops[i].kind != SPK_OP_FVAR) continue;
+    if ((bs[j / 8] >> (j % 8)) & 1u) b += wb < N.ops[i].size ? wb : N.ops[i].size;
+    ++j;
+  }
+  return b;
+}
+// deserialize_fast_varint: errc; values into rec (zero when the bit is clear)
+__device__ int32_t n_fv_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, uint64_t end,
+                             uint8_t *rec) {
+  if (end - pos < N.fv_bits) return SPK_ERRC_NO_BUFFER_SPACE;
+  uint8_t bs[(SPK_MAX_VARINTS + 2 + 7) / 8];
+  for (uint32_t b = 0; b < N.fv_bits; ++b) bs[b] = wire[pos + b];
+  pos += N.fv_bits;
+  const uint32_t code = ((bs[N.fv_cnt / 8] >> (N.fv_cnt % 8)) & 1u) |
+                        (((bs[(N.fv_cnt + 1) / 8] >> ((N.fv_cnt + 1) % 8)) & 1u) << 1);
+  if (code == 3 && !N.fv_has64) return SPK_ERRC_INVALID_BUFFER;
+  const uint32_t wb = 1u << code;
+  uint32_t j = 0;
+  for (uint32_t i = 0; i < N.n_ops; ++i) {
+    const spk_op op = N.ops[i];
+    if (op.kind != SPK_OP_FVAR) continue;
+    uint64_t v = 0;
+    if ((bs[j / 8] >> (j % 8)) & 1u) {
+      const uint32_t rw = wb < op.size ? wb : op.size;
+      if (end - pos < rw) return SPK_ERRC_NO_BUFFER_SPACE;
+      for (uint32_t b = 0; b < rw; ++b) v |= (uint64_t)wire[pos + b] << (8 * b);
+      pos += rw;
+      if ((op.aux & SPK_FVAR_SIGNED) && rw < 8 && ((v >> (8 * rw - 1)) & 1u)) v |= ~0ull << (8 * rw);
+    }
+    if (rec) {
+      if (op.size == 4)
+        *reinterpret_cast<uint32_t *>(rec + op.rec_off) = (uint32_t)v;
+      else
+        *reinterpret_cast<uint64_t *>(rec + op.rec_off) = v;
+    }
+    ++j;
+  }
+  return SPK_ERRC_OK;
+}
+
 // ---- encode: size of one record -----------------------------------------------
 struct NSize {
   uint64_t bytes, cnts, maxc;  // payload bytes w/o counts, count fields, longest container
@@ -141,6 +259,7 @@ struct NSize {
 };
 __device__ NSize n_size(const NLayout &N, const uint8_t *rec, const uint8_t *const *heaps) {
   NSize s = {0, 0, 0, 0};
+  s.bytes = n_fv_size(N, rec);
   NFrame st[SPK_MAX_DEPTH];
   uint32_t d = 0, i = 0, iend = N.n_ops;
   const uint8_t *r = rec;
@@ -160,7 +279,9 @@ __device__ NSize n_size(const NLayout &N, const uint8_t *rec, const uint8_t *con
       continue;
     }
     const spk_op op = N.ops[i];
-    if (op.kind == SPK_OP_COPY) {
+    if (op.kind == SPK_OP_FVAR) {  // in the group
+      ++i;
+    } else if (op.kind == SPK_OP_COPY) {
       s.bytes += op.size;
       ++i;
     } else if (op.kind == SPK_OP_VARINT) {
@@ -210,6 +331,7 @@ __device__ uint8_t *n_write(const NLayout &N, const uint8_t *rec, const uint8_t 
   NFrame st[SPK_MAX_DEPTH];
   uint32_t d = 0, i = 0, iend = N.n_ops;
   const uint8_t *r = rec;
+  p = n_fv_write(N, rec, p);  // before the members (packer.hpp:432-440)
   for (;;) {
     if (i >= iend) {
       if (!d) break;
@@ -226,7 +348,9 @@ __device__ uint8_t *n_write(const NLayout &N, const uint8_t *rec, const uint8_t 
       continue;
     }
     const spk_op op = N.ops[i];
-    if (op.kind == SPK_OP_COPY) {
+    if (op.kind == SPK_OP_FVAR) {
+      ++i;
+    } else if (op.kind == SPK_OP_COPY) {
       n_copy(p, r + op.rec_off, op.size);
       p += op.size;
       ++i;
@@ -360,6 +484,7 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
   uint32_t d = 0, i = 0, iend = N.n_ops;
   uint8_t *r = rec;
   int32_t ec = SPK_ERRC_OK;
+  if (N.fv_cnt && (ec = n_fv_read(N, wire, pos, end, rec))) return ec;
   for (;;) {
     if (ec) {
       // unwind to the innermost VARIANT: variant_construct_helper::run
@@ -401,6 +526,10 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
       continue;
     }
     const spk_op op = N.ops[i];
+    if (op.kind == SPK_OP_FVAR) {  // read with the group
+      ++i;
+      continue;
+    }
     if (op.kind == SPK_OP_COPY) {
       if (end - pos < op.size) { ec = SPK_ERRC_NO_BUFFER_SPACE; continue; }
       if (r) n_copy(r + op.rec_off, wire + pos, op.size);
@@ -952,6 +1081,7 @@ __global__ __launch_bounds__(64) void nest_vec_walk(NDec a, const uint8_t *__res
   // the version passes of compatible members (ph 1): rank rk, record crec, op ci
   uint32_t ph = 0, rk = 0, ci = 0;
   uint64_t crec = 0;
+  bool fvg = false;  // this record's fast-varint group is behind the walk
   struct Fr {
     uint32_t aop, pend;
     uint64_t j, cnt;
@@ -1080,9 +1210,40 @@ __global__ __launch_bounds__(64) void nest_vec_walk(NDec a, const uint8_t *__res
           if (rec < a.rec_cap) starts[rec] = pos;
           i = 0;
           iend = N.n_ops;
+          fvg = false;
+          continue;
+        }
+        if (N.fv_cnt && !fvg) {  // the record's USE_FAST_VARINT group comes first
+          if (wend < len && pos + N.fv_bits > wend) {
+            stall = true;
+            break;
+          }
+          int32_t ge = SPK_ERRC_OK;
+          uint64_t g = 0;
+          if (len - pos < N.fv_bits) {
+            ge = SPK_ERRC_NO_BUFFER_SPACE;
+          } else {
+            uint8_t bs[(SPK_MAX_VARINTS + 2 + 7) / 8];
+            for (uint32_t b = 0; b < N.fv_bits; ++b) bs[b] = (uint8_t)byte(pos + b);
+            g = n_fv_len(N, bs);
+            ge = !g ? SPK_ERRC_INVALID_BUFFER : len - pos < g ? SPK_ERRC_NO_BUFFER_SPACE : 0;
+          }
+          if (ge) {
+            if (!fail(ge)) {
+              done = true;
+              break;
+            }
+            continue;
+          }
+          pos += g;
+          fvg = true;
           continue;
         }
         const spk_op op = N.ops[i];
+        if (op.kind == SPK_OP_FVAR) {  // in the group
+          ++i;
+          continue;
+        }
         if (op.kind == SPK_OP_COMPAT) {  // main pass: nothing on the wire
           ++i;
           continue;

@@ -158,6 +158,7 @@ __device__ __forceinline__ uint64_t opt_nb(const spk_op &op, uint64_t c, uint64_
 __device__ __forceinline__ uint64_t vi_value(const spk_op &op, const uint8_t *rec) {
   if (op.size == 4) {
     uint32_t u = rec_u32(rec, op.rec_off);
+    if (op.aux & SPK_VARINT_SEXT) return (uint64_t)(int64_t)(int32_t)u;  // plain int32_t: v = t
     if (op.aux & SPK_VARINT_ZIGZAG) u = (u << 1) ^ (uint32_t)(-(int32_t)(u >> 31));
     return u;
   }

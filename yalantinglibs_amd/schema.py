@@ -141,6 +141,25 @@ var_int64 = VarInt("var_int64_t", TID_VINT64, 8, "<i8", True)
 var_uint32 = VarInt("var_uint32_t", TID_VUINT32, 4, "<u4", False)
 var_uint64 = VarInt("var_uint64_t", TID_VUINT64, 8, "<u8", False)
 
+# sp_config bits of a record type (reflection.hpp:53-60)
+ENCODING_WITH_VARINT, USE_FAST_VARINT = 0b100, 0b1000
+_PLAIN_VAR = {TID_INT32: TID_VINT32, TID_UINT32: TID_VUINT32, TID_INT64: TID_VINT64,
+              TID_UINT64: TID_VUINT64}
+
+
+def varint_tid(t: SpType, tag: int):
+    """get_varint_type<T, parent_tag> (type_id.hpp:83-125): the type id of a
+    varint member under its struct's sp_config tag, or None (reflection.hpp:
+    843: with ENCODING_WITH_VARINT plain (u)int32/64 are varints too);
+    USE_FAST_VARINT selects the fast_v* ids."""
+    if isinstance(t, VarInt):
+        tid = t.tid
+    elif isinstance(t, Fund) and tag & ENCODING_WITH_VARINT and t.tid in _PLAIN_VAR:
+        tid = _PLAIN_VAR[t.tid]
+    else:
+        return None
+    return tid + 4 if tag & USE_FAST_VARINT else tid
+
 
 class Monostate(SpType):
     name = "std::monostate"
@@ -315,7 +334,7 @@ class Struct(SpType):
 
     @property
     def trivial(self):
-        return all(t.trivial for _, t in self.fields)
+        return all(t.trivial and varint_tid(t, self.config) is None for _, t in self.fields)
 
     @property
     def trivial_ignoring_compatible(self):
@@ -327,7 +346,8 @@ class Struct(SpType):
         return any(t.has_container for _, t in self.fields)
 
     def literal(self):
-        body = b"".join(t.literal() for _, t in self.fields)
+        body = b"".join(bytes([varint_tid(t, self.config)]) if varint_tid(t, self.config)
+                        else t.literal() for _, t in self.fields)
         if self.trivial:
             # pack_alignment_v (max member alignment_v) and alignment_v
             # (alignof) literals: type_calculate.hpp:232-239, alignment.hpp
@@ -534,6 +554,26 @@ def flatten(rtype: SpType) -> DeviceLayout:
             ops.append((C.SPK_OP_VARINT, off, t.size,
                         C.SPK_VARINT_ZIGZAG if t.zigzag else 0))
             npf.append((path, t.npdt, off))
+        elif isinstance(t, Struct) and t.config & (ENCODING_WITH_VARINT | USE_FAST_VARINT):
+            if path:
+                raise NotImplementedError(f"{path}: varint sp_config bits are only in the "
+                                          "flat record model on the top-level record")
+            for fname, ft in t.fields:
+                tid = varint_tid(ft, t.config)
+                if tid is None:
+                    visit(ft, fname)
+                    continue
+                off = place(ft.size, ft.size)
+                npf.append((fname, ft.npdt, off))
+                signed = tid in (TID_VINT32, TID_VINT64, TID_VINT32 + 4, TID_VINT64 + 4)
+                if t.config & USE_FAST_VARINT:  # the record's fast-varint group
+                    ops.append((C.SPK_OP_FVAR, off, ft.size, C.SPK_FVAR_SIGNED if signed else 0))
+                elif isinstance(ft, VarInt):
+                    ops.append((C.SPK_OP_VARINT, off, ft.size,
+                                C.SPK_VARINT_ZIGZAG if ft.zigzag else 0))
+                else:  # plain (u)int under ENCODING_WITH_VARINT: v = t, no zigzag
+                    ops.append((C.SPK_OP_VARINT, off, ft.size,
+                                C.SPK_VARINT_SEXT if (signed and ft.size == 4) else 0))
         elif isinstance(t, Struct):
             for fname, ft in t.fields:
                 visit(ft, f"{path}.{fname}" if path else fname)
@@ -546,7 +586,8 @@ def flatten(rtype: SpType) -> DeviceLayout:
     visit(rtype, "" if isinstance(rtype, Struct) else "value")
     if len(spans) > C.SPK_MAX_SPANS:
         raise NotImplementedError("too many variable-length members")
-    if sum(op[0] == C.SPK_OP_VARINT for op in ops) > C.SPK_MAX_VARINTS:
+    if (sum(op[0] == C.SPK_OP_VARINT for op in ops) > C.SPK_MAX_VARINTS or
+            sum(op[0] == C.SPK_OP_FVAR for op in ops) > C.SPK_MAX_VARINTS):
         raise NotImplementedError("too many varint members")
     if len(ops) > C.SPK_MAX_OPS:
         raise NotImplementedError("too many layout ops")

@@ -105,6 +105,18 @@ Cmp = S.Struct("Cmp", [("id", S.int32), ("a", S.Compatible(S.int64, 20210101)),
 CmpOld = S.Struct("CmpOld", [("id", S.int32), ("name", S.String())])
 CmpNew = S.Struct("CmpNew", Cmp.fields + [("d", S.Compatible(S.int32, 20250101))])
 
+# sp_config varint encodings (types.hpp FV / FVE / FV32 / EV)
+FV = S.Struct("FV", [("a", S.var_int32), ("s", S.String()), ("b", S.var_uint64),
+                     ("d", S.float64), ("c", S.var_int64), ("e", S.var_uint32)],
+              config=S.USE_FAST_VARINT)
+FVE = S.Struct("FVE", [("a", S.int32), ("s", S.String()), ("b", S.uint64), ("d", S.float64),
+                       ("c", S.int64), ("e", S.uint32), ("f", S.int16)],
+               config=S.ENCODING_WITH_VARINT | S.USE_FAST_VARINT)
+FV32 = S.Struct("FV32", [("a", S.var_uint32), ("x", S.int16), ("b", S.var_int32)],
+                config=S.USE_FAST_VARINT)
+EV = S.Struct("EV", [("a", S.int32), ("s", S.String()), ("b", S.uint64), ("c", S.int64),
+                     ("e", S.uint32)], config=S.ENCODING_WITH_VARINT)
+
 # alignment overrides (types.hpp; ref alignment.hpp, tests/test_alignas.cpp)
 Al8 = S.Struct("Al8", [("a", S.char), ("b", S.int16)], alignas=8)
 AlA = S.Struct("AlA", [("a", S.char), ("b", S.int16)], alignas=4)
@@ -117,7 +129,8 @@ CASE_TYPES = {"rec64": Rec64, "recs": RecS, "outer": Outer, "pad": Pad,
               "mixed": Mixed, "rect": RectInt, "rpcrect": RpcRect,
               "person": Person, "ints": Ints, "opt": Opt, "optp": OptP,
               "var": Var, "varp": VarP, "tags": Tags, "group": Group, "deep": Deep,
-              "vnt": Vnt, "cmp": Cmp, "cmpold": CmpOld, "cmpnew": CmpNew, "al8": Al8, "alout": AlOuter, "packed": Packed, "alrec": AlRec}
+              "vnt": Vnt, "cmp": Cmp, "cmpold": CmpOld, "cmpnew": CmpNew, "fv": FV, "fve": FVE,
+              "fv32": FV32, "ev": EV, "al8": Al8, "alout": AlOuter, "packed": Packed, "alrec": AlRec}
 # vector<rect<int>> has its own ADL set_sp_config (benchmark data_def.hpp:69-72)
 VECTOR_CONFIG = {"rect": S.DISABLE_ALL_META_INFO}
 
@@ -409,6 +422,37 @@ def make_batch(case: str, n: int, seed: int, param: int = 48):
             heaps.append(_chars(seed, idx, lens))
             recs["p"] = packed_raw(rnd(seed, idx, 2)).view("V7").reshape(n)
             recs["e"] = al8_raw(rnd(seed, idx, 0)).view("V8").reshape(n)
+    elif case in ("fv", "fve", "fv32", "ev"):  # FvGen of types.hpp
+        r7 = rnd(seed, idx, 7)
+        sh = r7 >> np.uint64(58)
+        z = r7 & np.uint64(0xFFFFFFFF)
+
+        def u(j):
+            return np.where((z >> np.uint64(j)) & np.uint64(1), np.uint64(0),
+                            rnd(seed, idx, j) >> sh).astype(np.uint64)
+
+        def sg(j):
+            x = u(j)
+            neg = rnd(seed, idx, j) & np.uint64(1)
+            return np.where((z >> np.uint64(j)) & np.uint64(1), np.uint64(0),
+                            np.where(neg, ~x, x)).astype(np.uint64)
+        if case == "fv32":
+            recs["a"] = (u(0) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+            recs["x"] = rnd(seed, idx, 5).astype(np.uint16).view(np.int16)
+            recs["b"] = (sg(1) & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32)
+        else:
+            recs["a"] = (sg(0) & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32)
+            lens = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+            recs["s.n"] = lens
+            recs["s.off"] = _excl(lens)
+            heaps.append(_chars(seed, idx, lens))
+            recs["b"] = u(2)
+            if case != "ev":
+                recs["d"] = rd(rnd(seed, idx, 60))
+            recs["c"] = sg(3).view(np.int64)
+            recs["e"] = (u(4) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+            if case == "fve":
+                recs["f"] = rnd(seed, idx, 5).astype(np.uint16).view(np.int16)
     elif case in ("cmp", "cmpold", "cmpnew"):  # fill(Cmp& / CmpOld& / CmpNew&)
         recs["id"] = i32(rnd(seed, idx, 0))
         m = rnd(seed, idx, 6)
