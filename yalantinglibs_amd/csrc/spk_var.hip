@@ -1351,6 +1351,7 @@ struct VecBufs {
 };
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
 // Count-field reader over a chunk's LDS window: bytes [cs, wend) of the wire
 // are staged in LDS; reads past the window go to global memory.
@@ -1361,6 +1362,7 @@ struct WinReader {
   uint32_t w;
   __device__ __forceinline__ uint64_t operator()(uint64_t x) const {
     if (x + w <= wend) {
+      if (w == 1) return reinterpret_cast<const lds_u8 *>(d)[(uint32_t)(x - cs)];  // ds_read_u8
       const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = o >> 2;
       const uint32_t d0 = d[i], d1 = d[i + 1];
       const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
@@ -1372,10 +1374,7 @@ struct WinReader {
     return wire_le(wire, x, w);
   }
   __device__ __forceinline__ uint32_t byte(uint64_t x) const {
-    if (x < wend) {
-      const uint32_t o = (uint32_t)(x - cs);
-      return (d[o >> 2] >> (8 * (o & 3))) & 0xFFu;
-    }
+    if (x < wend) return reinterpret_cast<const lds_u8 *>(d)[(uint32_t)(x - cs)];
     return wire[x];
   }
   // LEB128 at x (message end len), as vi_read: eight bytes from the window at
