@@ -252,19 +252,25 @@ class VecWorkload:
 
 
 class C5Workload:
-    """C5: a coro_rpc server step over a batch of framed requests of three
-    record types (grouped by function id, one launch per type): decode every
-    [req_header][args] frame, echo, encode every [resp_header][ret] frame."""
+    """C5: a coro_rpc server step over one batch of request frames of three
+    record types whose function ids arrive interleaved (seeded order, each
+    type's own order kept): route the frames by function id (spk_route_frames,
+    the handler lookup of router.hpp:226-240 for the whole batch), read the
+    per-type counts, decode each type's [req_header][args] frames where they
+    lie (spk_decode_frames), echo, encode each type's [resp_header][ret]
+    frames and copy every request's seq_num into its response."""
 
     def __init__(self, torch, n_total, rank, dev):
+        import numpy as np
         from yalantinglibs_amd import coro_rpc as RPC
         from yalantinglibs_amd import layout as LY
         from yalantinglibs_amd import struct_pack as SP
-        self.torch, self.SP, self.dev = torch, SP, dev
+        self.torch, self.SP, self.RPC, self.dev = torch, SP, RPC, dev
         self.cfg = "c5"
         n_total = n_total or 1_000_000
         shares = sum(s for _, s, _, _ in C5_TYPES)
         self.groups = []
+        host_frames = []
         for case, share, param, fname in C5_TYPES:
             n = n_total * share // shares
             cd = SP.Codec(LY.case_layout(case), device=dev)
@@ -272,57 +278,100 @@ class C5Workload:
             plan = cd.get_needed_size(src, SP.MODE_MESSAGES)
             fid = RPC.func_id(fname)
             rq = RPC.req_frame(fid, seq_base=rank * n)
-            rs = RPC.resp_frame(seq_base=rank * n)
+            rs = RPC.resp_frame(seq_base=0)  # seq_num copied from the requests
             req_len = plan.total_bytes + n * rq.prefix_len
             req = torch.empty(req_len + 64, dtype=torch.uint8, device=dev)
             req_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
             cd.serialize_to(req, src, SP.MODE_MESSAGES, req_offs, planned=True, frame=rq)
+            host_frames.append((req[:req_len].cpu().numpy(), req_offs.cpu().numpy()))
+            del req, req_offs
             elems = [int(h.numel()) // sp.elem.size for h, sp in zip(src.heaps, cd.L.dev.spans)]
             args_b = cd.alloc_batch(n, elems)
             resp_len = plan.total_bytes + n * rs.prefix_len
             resp = torch.empty(resp_len + 64, dtype=torch.uint8, device=dev)
             resp_offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
             rec_bytes = src.recs.numel() + sum(int(h.numel()) for h in src.heaps)
-            self.groups.append(dict(case=case, n=n, cd=cd, src=src, req=req[:req_len],
-                                    req_offs=req_offs, args=args_b, resp=resp,
-                                    resp_offs=resp_offs, rq=rq, rs=rs, rec_bytes=rec_bytes,
-                                    req_len=req_len, resp_len=resp_len))
+            self.groups.append(dict(case=case, n=n, cd=cd, src=src, fid=fid, args=args_b,
+                                    resp=resp, resp_offs=resp_offs, rq=rq, rs=rs,
+                                    rec_bytes=rec_bytes, req_len=req_len, resp_len=resp_len))
+        # the connection's byte stream: frames of all types in a seeded arrival order
+        rng = np.random.default_rng(0x5EED000C5 + rank)
+        tags = np.concatenate([np.full(g["n"], k, np.int8) for k, g in enumerate(self.groups)])
+        rng.shuffle(tags)
+        nxt = [0] * len(self.groups)
+        lens = np.empty(len(tags), np.int64)
+        for k, (_, offs) in enumerate(host_frames):
+            lens[tags == k] = np.diff(offs)
+        moffs = np.zeros(len(tags) + 1, np.int64)
+        moffs[1:] = np.cumsum(lens)
+        buf = np.empty(int(moffs[-1]), np.uint8)
+        for j, k in enumerate(tags.tolist()):
+            w, offs = host_frames[k]
+            i = nxt[k]
+            nxt[k] = i + 1
+            buf[moffs[j]:moffs[j + 1]] = w[offs[i]:offs[i + 1]]
+        del host_frames
+        self.nframes = len(tags)
+        self.wire = torch.from_numpy(buf).to(dev)
+        self.offs = torch.from_numpy(moffs).to(dev)
+        del buf
+        self.router = RPC.FrameRouter([g["fid"] for g in self.groups], self.nframes, device=dev)
+        self.counts_pinned = torch.empty(len(self.groups) + 1, dtype=torch.int64).pin_memory()
         # request frames in + records/heaps out (decode), records/heaps in +
         # response frames out (encode)
         self.algo_bytes = sum(g["req_len"] + 2 * g["rec_bytes"] + g["resp_len"] for g in self.groups)
         self.units = sum(g["n"] for g in self.groups)
         self.n = self.units
-        self.data = "spk_synth seeded rpcrect/person/ints"
+        self.data = "spk_synth seeded rpcrect/person/ints, frames interleaved in a seeded order"
 
     def phases(self):
-        return ("decode", "encode")
+        return ("route", "decode", "encode")
 
     def step(self, stream, marks=None):
-        SP = self.SP
+        SP, RPC = self.SP, self.RPC
         if marks is not None:
             marks[0].record(stream)
-        for g in self.groups:
-            g["cd"].deserialize_to(g["args"], g["req"], SP.MODE_MESSAGES, g["req_offs"], g["n"],
-                                   stream=stream, prefix=g["rq"].prefix_len)
+        self.router.route(self.wire, self.offs, self.nframes, stream=stream)
+        self.counts_pinned.copy_(self.router.counts, non_blocking=True)
+        stream.synchronize()  # the per-type counts size the decode launches
+        counts = self.counts_pinned.tolist()
         if marks is not None:
             marks[1].record(stream)
-        for g in self.groups:
-            g["cd"].serialize_to(g["resp"], g["args"], SP.MODE_MESSAGES, g["resp_offs"],
-                                 stream=stream, frame=g["rs"])
+        rt = self.router
+        for k, g in enumerate(self.groups):
+            g["m"] = int(counts[k])
+            g["cd"].deserialize_frames(g["args"], self.wire, rt.begins[k], rt.ends[k], g["m"],
+                                       g["rq"].prefix_len, stream=stream)
         if marks is not None:
             marks[2].record(stream)
+        for k, g in enumerate(self.groups):
+            g["cd"].serialize_to(g["resp"], g["args"], SP.MODE_MESSAGES, g["resp_offs"],
+                                 stream=stream, frame=g["rs"])
+            RPC.copy_frame_field(g["resp"], g["resp_offs"], RPC.RESP_SEQ_OFF, self.wire,
+                                 rt.begins[k], RPC.REQ_SEQ_OFF, 4, g["m"], stream=stream)
+        if marks is not None:
+            marks[3].record(stream)
 
     def check(self):
         torch = self.torch
-        for g in self.groups:
+        for k, g in enumerate(self.groups):
             r = g["cd"].result()
-            if (r.errc != 0 or r.count != g["n"] or not torch.equal(g["args"].recs, g["src"].recs)
+            if (r.errc != 0 or r.count != g["n"] or g["m"] != g["n"]
+                    or not torch.equal(g["args"].recs, g["src"].recs)
                     or int(g["resp_offs"][-1].item()) != g["resp_len"]):
                 return f"c5 {g['case']}"
-            for k, (h_in, h_out) in enumerate(zip(g["src"].heaps, g["args"].heaps)):
-                used = int(r.heap_used[k]) * g["cd"].L.dev.spans[k].elem.size
+            for q, (h_in, h_out) in enumerate(zip(g["src"].heaps, g["args"].heaps)):
+                used = int(r.heap_used[q]) * g["cd"].L.dev.spans[q].elem.size
                 if not torch.equal(h_out[:used], h_in[:used]):
-                    return f"c5 {g['case']} heap {k}"
+                    return f"c5 {g['case']} heap {q}"
+            # response j echoes request j's seq_num (the request's rank*n + j)
+            ro = g["resp_offs"][:-1]
+            seq = torch.stack([g["resp"][ro + self.RPC.RESP_SEQ_OFF + b].to(torch.int64) << (8 * b)
+                               for b in range(4)]).sum(0)
+            if not torch.equal(seq, torch.arange(g["n"], device=seq.device) + g["rq"].seq_base):
+                return f"c5 {g['case']} seq_num"
+        if self.router.counts_host()[-1] != 0:
+            return "c5 unrouted frames"
         return None
 
     def kernel_bytes(self):
@@ -333,17 +382,20 @@ class C5Workload:
         for g in self.groups:
             ob = 8 * (g["n"] + 1)
             if g["cd"].L.dev.trivial:
-                add("fixed_msg_decode_lds", g["req_len"] + ob + g["rec_bytes"])
+                add("fixed_msg_decode_lds", g["req_len"] + 2 * ob + g["rec_bytes"])
                 add("fixed_msg_encode_lds", g["rec_bytes"] + g["resp_len"] + ob)
             else:
-                add("var_msg_write", g["req_len"] + ob + g["rec_bytes"])
+                add("var_msg_write", g["req_len"] + 2 * ob + g["rec_bytes"])
                 add("var_encode_write", g["rec_bytes"] + g["resp_len"] + ob)
+        # routing: frame offsets and keys in, begins / ends / arrival index out
+        add("route_scatter", 8 * (self.nframes + 1) + self.nframes + 24 * self.nframes)
         return kb
 
     def config(self):
-        return {"workload": "C5: coro_rpc server step, %d framed requests per GPU "
-                            "(rect / person / vector<int>~1K, one launch per type): "
-                            "decode [req_header][args], encode [resp_header][ret]" % self.units,
+        return {"workload": "C5: coro_rpc server step, %d framed requests per GPU in arrival "
+                            "order (rect / person / vector<int>~1K interleaved): route by "
+                            "function id, decode [req_header][args] per type, encode "
+                            "[resp_header][ret] with the request's seq_num" % self.units,
                 "messages_per_gpu": self.units,
                 "per_type": {g["case"]: g["n"] for g in self.groups},
                 "algorithmic_bytes_per_step_per_gpu": self.algo_bytes}

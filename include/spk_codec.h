@@ -372,6 +372,46 @@ int spk_decode_framed(const spk_layout *L, const void *d_wire, uint64_t wire_len
                       spk_dresult_t *d_res, int32_t *d_errc, void *d_ws,
                       size_t ws_bytes, void *stream);
 
+/* ---- mixed-type request batches in arrival order (coro_rpc server) -------
+ * A connection's request frames interleave function ids; the reference
+ * server looks each one up in its handler map and decodes it with that
+ * handler's argument types (router.hpp:226-240, coro_rpc_protocol.hpp:60-95).
+ * spk_route_frames does the lookup for a whole batch in one pass: frame i is
+ * d_wire[d_frame_offsets[i] .. d_frame_offsets[i+1]); its u32 LE key at byte
+ * key_off (req_header.function_id: key_off 8) is looked up in h_keys[0..n_keys)
+ * (n_keys <= SPK_MAX_ROUTES, distinct). For every key k the frames carrying it
+ * are listed IN ARRIVAL ORDER: d_begins[k][j] / d_ends[k][j] = the j-th such
+ * frame's bounds, d_index[k][j] (nullable) = its arrival index i;
+ * d_counts[k] = how many. Frames with another key, or shorter than
+ * key_off + 4 bytes, are counted in d_counts[n_keys] and listed in list
+ * n_keys when d_begins[n_keys] is non-null (host arrays of n_keys + 1 device
+ * pointers, each list with room for n_frames entries). d_counts (device,
+ * n_keys + 1 words) is written in stream order: read it before launching the
+ * per-type decodes (spk_decode_frames). */
+#define SPK_MAX_ROUTES 16u
+size_t spk_route_workspace_bytes(uint64_t n_frames, uint32_t n_keys);
+int spk_route_frames(const void *d_wire, uint64_t wire_len, const uint64_t *d_frame_offsets,
+                     uint64_t n_frames, uint32_t key_off, const uint32_t *h_keys,
+                     uint32_t n_keys, uint64_t *const *d_begins, uint64_t *const *d_ends,
+                     uint64_t *const *d_index, uint64_t *d_counts, void *d_ws,
+                     size_t ws_bytes, void *stream);
+/* spk_decode_framed over frames that need not be adjacent: frame i is
+ * d_wire[d_begins[i] .. d_ends[i]) (one type's lists from spk_route_frames). */
+int spk_decode_frames(const spk_layout *L, const void *d_wire, uint64_t wire_len,
+                      const uint64_t *d_begins, const uint64_t *d_ends, uint64_t n_msgs,
+                      uint32_t prefix_len, void *d_recs, uint64_t rec_cap,
+                      void *const *d_heaps, const uint64_t *heap_caps,
+                      spk_dresult_t *d_res, int32_t *d_errc, void *d_ws,
+                      size_t ws_bytes, void *stream);
+/* For i < n: copy `bytes` (1..8) from d_src[d_src_offsets[i] + src_off] to
+ * d_dst[d_dst_offsets[i] + dst_off]: the response header echoes its request's
+ * seq_num (coro_rpc_protocol.hpp:191-201) when responses were encoded per
+ * type (spk_encode_framed numbers them seq_base + j): src = the request
+ * frames at d_begins[k] (seq_num at 4), dst = the response frames (at 4). */
+int spk_copy_frame_field(void *d_dst, const uint64_t *d_dst_offsets, uint32_t dst_off,
+                         const void *d_src, const uint64_t *d_src_offsets, uint32_t src_off,
+                         uint32_t bytes, uint64_t n, void *stream);
+
 /* ---- sharded single-message encode (multi-GPU, SPK_MODE_VECTOR) --------
  * One std::vector<T> message whose records are spread over several GPUs:
  * every shard encodes only its records' bytes ("body") with the GLOBAL

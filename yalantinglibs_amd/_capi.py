@@ -16,6 +16,7 @@ SPK_MAX_OPS = 64
 SPK_MAX_SPANS = 8
 SPK_MAX_LITERAL = 240
 SPK_MAX_FRAME = 64
+SPK_MAX_ROUTES = 16
 SPK_FRAME_NONE = 0xFFFFFFFF
 
 SPK_OK = 0
@@ -125,6 +126,9 @@ CODEC_SYMBOLS = ["spk_abi_version", "spk_errc_message", "spk_layout_check",
                  "spk_vector_header", "spk_encode_framed", "spk_decode_framed",
                  "spk_decode_body", "spk_parse_vector_header",
                  "spk_decode_shard_index", "spk_decode_shard_emit",
+                 # mixed-type frame batches in arrival order
+                 "spk_route_workspace_bytes", "spk_route_frames", "spk_decode_frames",
+                 "spk_copy_frame_field",
                  # runtime helpers (front ends without HIP headers)
                  "spk_device_alloc", "spk_device_free", "spk_host_alloc_pinned",
                  "spk_host_free_pinned", "spk_copy_async", "spk_stream_create",
@@ -173,6 +177,16 @@ def _bind_codec(lib):
                                       ct.POINTER(P), ct.POINTER(U64), P, P, P,
                                       ct.c_size_t, P]
     lib.spk_synth_counts.argtypes = [ct.c_int, U64, U64, U64, ct.c_uint32, P, P]
+    lib.spk_route_workspace_bytes.restype = ct.c_size_t
+    lib.spk_route_workspace_bytes.argtypes = [U64, ct.c_uint32]
+    lib.spk_route_frames.argtypes = [P, U64, P, U64, ct.c_uint32, ct.POINTER(ct.c_uint32),
+                                     ct.c_uint32, ct.POINTER(P), ct.POINTER(P), ct.POINTER(P),
+                                     P, P, ct.c_size_t, P]
+    lib.spk_decode_frames.argtypes = [PL, P, U64, P, P, U64, ct.c_uint32, P, U64,
+                                      ct.POINTER(P), ct.POINTER(U64), P, P, P,
+                                      ct.c_size_t, P]
+    lib.spk_copy_frame_field.argtypes = [P, P, ct.c_uint32, P, P, ct.c_uint32, ct.c_uint32,
+                                         U64, P]
     lib.spk_trace_enable.argtypes = [ct.c_int]
     lib.spk_trace_read.argtypes = [ct.c_char_p, ct.c_size_t]
     return lib

@@ -16,11 +16,16 @@ name (router.hpp:121-127).
 On MI355X a batch of such calls is one spk_encode_framed / spk_decode_framed
 launch per record type (include/spk_codec.h): the kernels write the header
 template with the per-message sequence number and payload length patched in,
-and skip it on decode. This module builds those frame descriptors and
-restates the header layout for host-side checks.
+and skip it on decode. A connection's frames arrive with their function ids
+interleaved: FrameRouter splits such a batch per function id in one pass
+(spk_route_frames, arrival order kept per id) for spk_decode_frames, and
+echoes each request's seq_num into its response (spk_copy_frame_field).
+This module builds those frame descriptors and restates the header layout
+for host-side checks.
 """
 from __future__ import annotations
 
+import ctypes as ct
 import struct
 
 from . import _capi as C
@@ -28,6 +33,7 @@ from . import schema as S
 
 # coro_rpc_protocol.hpp:45, 250 and the header structs at :60-79
 MAGIC_NUMBER = 21
+REQ_SEQ_OFF, REQ_FID_OFF, RESP_SEQ_OFF = 4, 8, 4
 VERSION_NUMBER = 0
 REQ_HEAD_LEN = 20
 RESP_HEAD_LEN = 16
@@ -92,3 +98,65 @@ def frame_offsets_from_stream(buf: bytes, head_len: int = REQ_HEAD_LEN, len_off:
         p += head_len + ln
         offs.append(p)
     return offs
+
+
+def _stream(stream=None):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ct.c_void_p(s.cuda_stream)
+
+
+class FrameRouter:
+    """Dispatch of a batch of request frames by function id, as the server's
+    handler lookup does frame by frame (router.hpp:226-240): for function id
+    k the frames are listed in arrival order (begins[k] / ends[k] / index[k]),
+    frames with unknown ids in the extra list n_keys. counts (device) holds
+    n_keys + 1 sizes after route(); counts_host() reads them."""
+
+    def __init__(self, function_ids, capacity: int, device="cuda"):
+        import torch
+        if len(function_ids) > C.SPK_MAX_ROUTES:
+            raise ValueError(f"at most {C.SPK_MAX_ROUTES} function ids per router")
+        self.lib = C.load_codec()
+        self.keys = [int(f) & 0xFFFFFFFF for f in function_ids]
+        self.capacity = capacity
+        self.device = device
+        nk = len(self.keys)
+        mk = lambda: [torch.empty(max(capacity, 1), dtype=torch.int64, device=device)
+                      for _ in range(nk + 1)]
+        self.begins, self.ends, self.index = mk(), mk(), mk()
+        self.counts = torch.zeros(nk + 1, dtype=torch.int64, device=device)
+        need = int(self.lib.spk_route_workspace_bytes(capacity, nk))
+        self._ws = torch.empty(need, dtype=torch.uint8, device=device)
+        ptrs = lambda ts: (ct.c_void_p * (nk + 1))(*[t.data_ptr() for t in ts])
+        self._pb, self._pe, self._pi = ptrs(self.begins), ptrs(self.ends), ptrs(self.index)
+        self._keys = (ct.c_uint32 * max(nk, 1))(*(self.keys or [0]))
+
+    def route(self, wire, offsets, n: int, stream=None):
+        """Stream-ordered: frame i = wire[offsets[i] .. offsets[i+1])."""
+        if n > self.capacity:
+            raise ValueError("more frames than the router's capacity")
+        rc = self.lib.spk_route_frames(
+            ct.c_void_p(wire.data_ptr()), wire.numel(), ct.c_void_p(offsets.data_ptr()), n,
+            REQ_FID_OFF, self._keys, len(self.keys), self._pb, self._pe, self._pi,
+            ct.c_void_p(self.counts.data_ptr()), ct.c_void_p(self._ws.data_ptr()),
+            self._ws.numel(), _stream(stream))
+        if rc != 0:
+            raise RuntimeError(f"spk_route_frames failed with {rc}")
+        return self.counts
+
+    def counts_host(self):
+        return [int(x) for x in self.counts.cpu().tolist()]
+
+
+def copy_frame_field(dst, dst_offsets, dst_off: int, src, src_offsets, src_off: int,
+                     nbytes: int, n: int, stream=None):
+    """spk_copy_frame_field: dst[dst_offsets[i] + dst_off ..] = src[src_offsets[i] +
+    src_off ..] (nbytes) for i < n — e.g. response seq_num = request seq_num."""
+    lib = C.load_codec()
+    rc = lib.spk_copy_frame_field(ct.c_void_p(dst.data_ptr()), ct.c_void_p(dst_offsets.data_ptr()),
+                                  dst_off, ct.c_void_p(src.data_ptr()),
+                                  ct.c_void_p(src_offsets.data_ptr()), src_off, nbytes, n,
+                                  _stream(stream))
+    if rc != 0:
+        raise RuntimeError(f"spk_copy_frame_field failed with {rc}")

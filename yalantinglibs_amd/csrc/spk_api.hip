@@ -304,7 +304,8 @@ static int decode_impl(const spk_layout *L, int mode, const void *d_wire, uint64
                        const uint64_t *d_msg_offsets, uint64_t n_msgs, uint32_t prefix,
                        void *d_recs, uint64_t rec_cap, void *const *d_heaps,
                        const uint64_t *heap_caps, spk_dresult_t *d_res, int32_t *d_errc,
-                       void *d_ws, size_t ws_bytes, void *stream) {
+                       void *d_ws, size_t ws_bytes, void *stream,
+                       const uint64_t *d_msg_ends = nullptr) {
   int rc = spk_layout_check(L);
   if (rc) return rc;
   if ((mode != SPK_MODE_VECTOR && mode != SPK_MODE_MESSAGES) || !d_res || !d_ws)
@@ -320,7 +321,7 @@ static int decode_impl(const spk_layout *L, int mode, const void *d_wire, uint64
                                                d_ws, s));
     return hip_rc(launch_fixed_decode_messages(L, d_wire, wire_len, d_msg_offsets, n_msgs,
                                                prefix, d_recs, rec_cap, d_res, d_errc, d_ws,
-                                               s));
+                                               s, d_msg_ends));
   }
   if (d_recs && (uintptr_t)d_recs % 8) return SPK_E_ARG;
   const uint32_t spans = heap_count(L);
@@ -331,11 +332,11 @@ static int decode_impl(const spk_layout *L, int mode, const void *d_wire, uint64
       if (!d_heaps[k] || (uintptr_t)d_heaps[k] % 8) return SPK_E_ARG;
     return hip_rc(launch_nested_decode(L, mode, d_wire, wire_len, d_msg_offsets, n_msgs, prefix,
                                        d_recs, rec_cap, d_heaps, heap_caps, d_res, d_errc, d_ws,
-                                       s));
+                                       s, 0, 0, d_msg_ends));
   }
   return hip_rc(launch_var_decode(L, mode, d_wire, wire_len, d_msg_offsets, n_msgs, prefix,
                                   d_recs, rec_cap, d_heaps, heap_caps, d_res, d_errc, d_ws,
-                                  ws_bytes, s));
+                                  ws_bytes, s, 0, 0, d_msg_ends));
 }
 
 int spk_decode(const spk_layout *L, int mode, const void *d_wire, uint64_t wire_len,
@@ -356,6 +357,17 @@ int spk_decode_framed(const spk_layout *L, const void *d_wire, uint64_t wire_len
   return decode_impl(L, SPK_MODE_MESSAGES, d_wire, wire_len, d_msg_offsets, n_msgs,
                      prefix_len, d_recs, rec_cap, d_heaps, heap_caps, d_res, d_errc, d_ws,
                      ws_bytes, stream);
+}
+
+int spk_decode_frames(const spk_layout *L, const void *d_wire, uint64_t wire_len,
+                      const uint64_t *d_begins, const uint64_t *d_ends, uint64_t n_msgs,
+                      uint32_t prefix_len, void *d_recs, uint64_t rec_cap,
+                      void *const *d_heaps, const uint64_t *heap_caps, spk_dresult_t *d_res,
+                      int32_t *d_errc, void *d_ws, size_t ws_bytes, void *stream) {
+  if (prefix_len > SPK_MAX_FRAME || (n_msgs && (!d_begins || !d_ends))) return SPK_E_ARG;
+  return decode_impl(L, SPK_MODE_MESSAGES, d_wire, wire_len, d_begins, n_msgs, prefix_len,
+                     d_recs, rec_cap, d_heaps, heap_caps, d_res, d_errc, d_ws, ws_bytes, stream,
+                     d_ends);
 }
 
 int spk_encode_body(const spk_layout *L, uint64_t n, const void *d_recs,

@@ -372,6 +372,7 @@ struct MsgLdsArgs {
   uint32_t prefix;  // decode: frame bytes before each message
   uint32_t seq_off; // encode: frame sequence field or ~0u
   uint32_t seq_base;
+  const uint64_t *ends;  // decode: message i ends at ends[i] (null: offs[i + 1])
   uint8_t hdr[kMsgHdrMax];
 };
 
@@ -467,7 +468,7 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
     if (tid < nR) {
       const uint64_t i = first + tid;
       b = offs ? offs[i] : i * a.fixed_M;
-      e = offs ? offs[i + 1] : (i + 1) * a.fixed_M;
+      e = offs ? (a.ends ? a.ends[i] : offs[i + 1]) : (i + 1) * a.fixed_M;
       inr = e >= b && e <= a.wire_len && e - b >= a.prefix;
       b += a.prefix;  // the struct_pack message starts after the frame prefix
     }
@@ -707,6 +708,7 @@ struct MsgDecArgs {
   uint32_t stride;
   uint32_t fixed_M;  // implicit message stride when offsets == nullptr
   uint32_t prefix;   // frame bytes before each message
+  const uint64_t *ends;  // message i ends at ends[i] (null: offs[i + 1])
 };
 
 __global__ __launch_bounds__(256) void fixed_msg_parse(
@@ -718,7 +720,7 @@ __global__ __launch_bounds__(256) void fixed_msg_parse(
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n;
        i += gstride) {
     uint64_t b = offs ? offs[i] : i * a.fixed_M;
-    uint64_t e = offs ? offs[i + 1] : (i + 1) * a.fixed_M;
+    uint64_t e = offs ? (a.ends ? a.ends[i] : offs[i + 1]) : (i + 1) * a.fixed_M;
     int32_t ec = SPK_ERRC_OK;
     uint64_t pos = 0, dl = 0;
     uint32_t w = 1;
@@ -792,9 +794,11 @@ hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
                                            uint64_t wire_len, const uint64_t *d_offsets,
                                            uint64_t n, uint32_t prefix, void *d_recs,
                                            uint64_t rec_cap, spk_dresult_t *d_res,
-                                           int32_t *d_errc, void *d_ws, hipStream_t s) {
+                                           int32_t *d_errc, void *d_ws, hipStream_t s,
+                                           const uint64_t *d_msg_ends) {
   MsgDecArgs a;
   a.prefix = prefix;
+  a.ends = d_msg_ends;
   a.fmt = L->fmt_one;
   a.n = n;
   a.wire_len = wire_len;
@@ -814,6 +818,7 @@ hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
     b.stride = L->rec_stride;
     b.fixed_M = a.fixed_M;
     b.prefix = prefix;
+    b.ends = d_msg_ends;
     b.R = msg_block_R(a.fixed_M);
     if (b.R && (uintptr_t)d_recs % 16 == 0 && n > 0 && b.stride % 4 == 0) {
       b.cap = b.R * a.fixed_M + 32;

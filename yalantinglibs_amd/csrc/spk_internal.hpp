@@ -234,7 +234,8 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
                                 uint64_t n_msgs, uint32_t prefix, void *d_recs, uint64_t rec_cap,
                                 void *const *d_heaps, const uint64_t *heap_caps,
                                 spk_dresult_t *d_res, int32_t *d_errc, void *d_ws,
-                                hipStream_t s, uint32_t body_w = 0, uint64_t body_n = 0);
+                                hipStream_t s, uint32_t body_w = 0, uint64_t body_n = 0,
+                                const uint64_t *d_msg_ends = nullptr);
 // spk_fixed.hip
 hipError_t launch_fixed_plan(const spk_layout *L, int mode, uint64_t n,
                              spk_plan_t *d_plan, void *d_ws, hipStream_t s);
@@ -257,7 +258,8 @@ hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
                                         const uint64_t *d_offsets, uint64_t n,
                                         uint32_t prefix, void *d_recs, uint64_t rec_cap,
                                         spk_dresult_t *d_res, int32_t *d_errc,
-                                        void *d_ws, hipStream_t s);
+                                        void *d_ws, hipStream_t s,
+                                        const uint64_t *d_msg_ends = nullptr);
 // spk_var.hip
 size_t var_workspace_bytes(const spk_layout *L, int mode, uint64_t n,
                            uint64_t wire_len);
@@ -278,5 +280,6 @@ hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
                              uint64_t n_msgs, uint32_t prefix, void *d_recs, uint64_t rec_cap,
                              void *const *d_heaps, const uint64_t *heap_caps,
                              spk_dresult_t *d_res, int32_t *d_errc, void *d_ws,
-                             size_t ws_bytes, hipStream_t s, uint32_t body_w = 0, uint64_t body_n = 0);
+                             size_t ws_bytes, hipStream_t s, uint32_t body_w = 0, uint64_t body_n = 0,
+                             const uint64_t *d_msg_ends = nullptr);
 }  // namespace spk

@@ -1054,6 +1054,7 @@ struct NDec {
   uint64_t body_n;
   uint8_t *heaps[SPK_MAX_SPANS];
   uint64_t heap_cap[SPK_MAX_SPANS];
+  const uint64_t *ends;  // MESSAGES: message i ends at ends[i] (null: offs[i + 1])
 };
 
 // VECTOR boundary walk: one wave; lane 0 interprets the record counts while
@@ -1392,7 +1393,7 @@ __global__ __launch_bounds__(256) void nest_msg_count(NDec a, const uint8_t *__r
   if (i >= a.n_msgs) return;
   const NLayout &N = a.N;
   uint64_t used[SPK_MAX_SPANS] = {};
-  const uint64_t b = offs[i], e = offs[i + 1];
+  const uint64_t b = offs[i], e = a.ends ? a.ends[i] : offs[i + 1];
   int32_t errc = SPK_ERRC_OK;
   uint64_t consumed = 0;
   if (e < b || e > a.wire_len || e - b < a.prefix) {
@@ -1441,7 +1442,7 @@ __global__ __launch_bounds__(256) void nest_emit(NDec a, const uint8_t *__restri
   } else {
     if (i >= a.n_msgs || i >= a.rec_cap || ec[i]) return;
     const uint64_t m0 = offs[i] + a.prefix;
-    end = offs[i + 1];
+    end = a.ends ? a.ends[i] : offs[i + 1];
     uint64_t p0, dl;
     parse_hdr(a.fmt, wire + m0, end - m0, &p0, &w, &dl);
     pos = m0 + p0;
@@ -1522,8 +1523,10 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
                                 uint64_t n_msgs, uint32_t prefix, void *d_recs, uint64_t rec_cap,
                                 void *const *d_heaps, const uint64_t *heap_caps,
                                 spk_dresult_t *d_res, int32_t *d_errc, void *d_ws,
-                                hipStream_t s, uint32_t body_w, uint64_t body_n) {
+                                hipStream_t s, uint32_t body_w, uint64_t body_n,
+                                const uint64_t *d_msg_ends) {
   NDec a = {};
+  a.ends = d_msg_ends;
   a.body_w = body_w;
   a.body_n = body_n;
   a.N = make_nlayout(L);

@@ -501,42 +501,37 @@ __device__ __forceinline__ void win_put_coop(const Win &W, uint64_t pos, const u
         *reinterpret_cast<const v4u_una *>(src + (c - pos));
 }
 
-constexpr int kCoopU = 4;  // loads in flight per lane in coop_copy_all
+constexpr int kCoopU = 8;       // loads in flight per lane in wave_copy_all
+constexpr unsigned kYSplit = 8;  // blocks sharing one write block's output
 
-// All m listed payloads (B[k].dptr <- B[k].src, B[k].n bytes) copied by the
-// whole block over one flattened index of their aligned 16-B destination
-// chunks (c0s: exclusive prefix of per-payload chunk counts, in LDS), kCoopU
-// loads in flight per lane; head/tail bytes by one lane per payload.
-__device__ __forceinline__ void coop_copy_all(const BigSeg *B, uint32_t m, const uint32_t *c0s) {
-  if (threadIdx.x < m) {
-    const BigSeg e = B[threadIdx.x];
+// All m listed payloads (B[k].dptr <- B[k].src, B[k].n bytes), one wave per
+// payload (payload k by wave k mod the waves of all nparts blocks): aligned
+// 16-B destination chunks fed by unaligned 16-B source loads, kCoopU loads in
+// flight per lane, head/tail bytes by single lanes. (A block-wide flattened
+// chunk index over all payloads, searched per chunk, measured 13 % slower on
+// C5's vector<int> messages.)
+__device__ __forceinline__ void wave_copy_all(const BigSeg *B, uint32_t m, uint32_t part,
+                                              uint32_t nparts) {
+  const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const uint32_t gw = part * nw + (threadIdx.x >> 6), W = nparts * nw;
+  for (uint32_t k = gw; k < m; k += W) {
+    const BigSeg e = B[k];
     uint64_t head = (16 - ((uintptr_t)e.dptr & 15)) & 15;
     if (head > e.n) head = e.n;
-    const uint64_t body = (e.n - head) & ~15ull;
-    for (uint64_t x = 0; x < head; ++x) e.dptr[x] = e.src[x];
-    for (uint64_t x = head + body; x < e.n; ++x) e.dptr[x] = e.src[x];
-  }
-  const uint32_t total = c0s[m];
-  uint32_t k = 0;
-  for (uint32_t c0 = threadIdx.x; c0 < total; c0 += blockDim.x * kCoopU) {
-    v4u_t v[kCoopU];
-    uint8_t *d[kCoopU];
+    const uint64_t nc = (e.n - head) >> 4, tail = head + 16 * nc;
+    if (lane < head) e.dptr[lane] = e.src[lane];
+    if (lane < e.n - tail) e.dptr[tail + lane] = e.src[tail + lane];
+    const uint8_t *src = e.src + head;
+    uint8_t *dst = e.dptr + head;
+    for (uint64_t c0 = lane; c0 < nc; c0 += 64 * kCoopU) {
+      v4u_t v[kCoopU];
 #pragma unroll
-    for (int u = 0; u < kCoopU; ++u) {
-      const uint32_t c = c0 + u * blockDim.x;
-      d[u] = nullptr;
-      if (c < total) {
-        while (c0s[k + 1] <= c) ++k;
-        const BigSeg &e = B[k];
-        uint64_t head = (16 - ((uintptr_t)e.dptr & 15)) & 15;
-        const uint64_t off = head + 16ull * (c - c0s[k]);
-        v[u] = *reinterpret_cast<const v4u_una *>(e.src + off);
-        d[u] = e.dptr + off;
-      }
+      for (int u = 0; u < kCoopU; ++u)
+        if (c0 + 64 * u < nc) v[u] = *reinterpret_cast<const v4u_una *>(src + 16 * (c0 + 64 * u));
+#pragma unroll
+      for (int u = 0; u < kCoopU; ++u)
+        if (c0 + 64 * u < nc) *reinterpret_cast<v4u_t *>(dst + 16 * (c0 + 64 * u)) = v[u];
     }
-#pragma unroll
-    for (int u = 0; u < kCoopU; ++u)
-      if (d[u]) *reinterpret_cast<v4u_t *>(d[u]) = v[u];
   }
 }
 
@@ -572,7 +567,7 @@ constexpr uint32_t kEncWin = 20 * 1024;  // LDS assembly window per block
 // Write pass: records r0 + j*kThreads + tid (consecutive lanes on consecutive
 // records), byte offsets from a block scan per round on top of the block's
 // planned base; the block's output range is assembled window by window.
-__global__ __launch_bounds__(kThreads) void var_encode_write(
+__global__ __launch_bounds__(kThreads, 5) void var_encode_write(
     VarArgs a, const uint8_t *__restrict__ recs, uint8_t *__restrict__ out,
     uint64_t out_cap, const uint8_t *__restrict__ ws,
     const spk_plan_t *__restrict__ plan, uint64_t *__restrict__ offs) {
@@ -586,13 +581,28 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
   const uint32_t hdr_vec = plan->header_bytes;
   const Partial *part = reinterpret_cast<const Partial *>(ws + kWsScratch);
   const uint64_t r0 = (uint64_t)blockIdx.x * kRPB;
-  const Partial &pb = part[blockIdx.x / kPlanSub];
-  uint64_t gb = pb.sum;
-  for (uint32_t j = 0; j < blockIdx.x % kPlanSub; ++j) gb += pb.sub[j];
-  const uint64_t g0 = a.mode == SPK_MODE_VECTOR
-                          ? hdr_vec + gb + r0 * (uint64_t)a.L.n_cont * w_vec
-                          : gb + r0 * (uint64_t)a.fpre;
-  if (a.mode == SPK_MODE_VECTOR && blockIdx.x == 0)
+  // output base of write block b (b == gridDim.x: the end of the output)
+  auto base_of = [&](uint64_t b) -> uint64_t {
+    if (b >= gridDim.x) return total;
+    const Partial &pb = part[b / kPlanSub];
+    uint64_t gb = pb.sum;
+    for (uint32_t j = 0; j < b % kPlanSub; ++j) gb += pb.sub[j];
+    const uint64_t rb = b * kRPB;
+    return a.mode == SPK_MODE_VECTOR ? hdr_vec + gb + rb * (uint64_t)a.L.n_cont * w_vec
+                                     : gb + rb * (uint64_t)a.fpre;
+  };
+  const uint64_t g0 = base_of(blockIdx.x);
+  // Window split: gridDim.y blocks share one write block's output range, block
+  // y assembling windows y, y + gridDim.y, ... (a few blocks of multi-KiB
+  // messages would otherwise leave most CUs idle). The range end comes from
+  // the next block's base, so a block without windows leaves before reading
+  // any record.
+  const uint32_t ysub = blockIdx.y, ny = gridDim.y;
+  if (ysub > 0) {
+    const uint64_t ge = base_of((uint64_t)blockIdx.x + 1);
+    if ((g0 & ~15ull) + (uint64_t)ysub * kEncWin >= ge) return;
+  }
+  if (a.mode == SPK_MODE_VECTOR && blockIdx.x == 0 && ysub == 0)
     for (uint32_t i = threadIdx.x; i < hdr_vec; i += blockDim.x) out[i] = ws[kWsHdrVec + i];
   uint64_t pj[kIPT], szj[kIPT];
   uint32_t wj[kIPT];
@@ -617,15 +627,16 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
     szj[j] = sz;
     wj[j] = w;
     g += btot;
-    if (a.mode == SPK_MODE_MESSAGES && offs && i < a.n) offs[i] = pj[j];
+    if (a.mode == SPK_MODE_MESSAGES && offs && i < a.n && ysub == 0) offs[i] = pj[j];
   }
-  if (a.mode == SPK_MODE_MESSAGES && offs && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+  if (a.mode == SPK_MODE_MESSAGES && offs && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 &&
+      ysub == 0)
     offs[a.n] = total;
   const uint64_t g1 = g;
   if (g1 == g0) return;
   // large span payloads of this block's records -> cooperative list
   uint32_t skip[kIPT];
-  uint64_t nbig_tot = 0;
+  uint64_t nbig_tot = 0, big_bytes = 0;
   for (int j = 0; j < kIPT; ++j) {  // list order = record order = output order
     skip[j] = 0;
     const uint64_t i = r0 + (uint64_t)j * kThreads + threadIdx.x;
@@ -659,18 +670,55 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
         const uint64_t nb = op_rec_count(op, rec) * op.size;
         q += op_pw(op, wj[j]);
         if (nb >= kBigBytes) {
-          big[slot++] = BigSeg{q, nullptr, a.heaps[sk] + rec_u64(rec, op.aux) * op.size, nb};
+          big[slot++] = BigSeg{q, out + q, a.heaps[sk] + rec_u64(rec, op.aux) * op.size, nb};
           skip[j] |= 1u << sk;
+          big_bytes += nb;
         }
         q += nb;
         ++sk;
       }
     }
   }
+  // Direct mode: when the listed payloads are >= 7/8 of the block's output
+  // (multi-KiB strings / vectors, e.g. C5's vector<int>), the LDS windows would
+  // only relay payload bytes. The record bytes around them are then stored
+  // straight to HBM by their lanes (a few partial stores per record) and the
+  // payloads are copied HBM to HBM with aligned 16-B stores, the copy split
+  // over the gridDim.y blocks of this write block.
+  if (nbig_tot && nbig_tot <= kBigMax) {
+    uint64_t bb_tot;
+    block_excl_scan(big_bytes, &bb_tot, sh);
+    if (bb_tot * 8 >= (g1 - g0) * 7) {
+      if (ysub == 0) {
+        const Win D{out, 0, ~0ull};
+        for (int j = 0; j < kIPT; ++j) {
+          const uint64_t i = r0 + (uint64_t)j * kThreads + threadIdx.x;
+          if (i >= a.n) continue;
+          uint64_t q = pj[j];
+          if (a.mode == SPK_MODE_MESSAGES) {
+            if (a.fpre) {
+              win_frame(a, D, q, i, szj[j] - a.fpre);
+              q += a.fpre;
+            }
+            const uint32_t sl = wlog(wj[j]);
+            const uint32_t hl = ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + sl];
+            win_put(D, q, ws + kWsHdrMsg + sl * kWsHdrSlot, hl);
+            q += hl;
+          }
+          win_record(a, recs + i * a.L.stride, wj[j], q, D, skip[j]);
+        }
+      }
+      __syncthreads();  // the payload list
+      // the blocks of this write block that did not leave at the top
+      const uint64_t nwin = ((g1 - (g0 & ~15ull)) + kEncWin - 1) / kEncWin;
+      wave_copy_all(big, (uint32_t)nbig_tot, ysub, nwin < ny ? (uint32_t)nwin : ny);
+      return;
+    }
+  }
   if (nbig_tot > kBigMax) nbig_tot = kBigMax;
   __syncthreads();
   uint32_t k0 = 0;  // first list entry that may reach the current window
-  for (uint64_t wlo = g0 & ~15ull; wlo < g1; wlo += kEncWin) {
+  for (uint64_t wlo = (g0 & ~15ull) + (uint64_t)ysub * kEncWin; wlo < g1; wlo += ny * kEncWin) {
     const Win W{lds, wlo, wlo + kEncWin < g1 ? wlo + kEncWin : g1};
     for (int j = 0; j < kIPT; ++j) {
       const uint64_t i = r0 + (uint64_t)j * kThreads + threadIdx.x;
@@ -688,9 +736,7 @@ __global__ __launch_bounds__(kThreads) void var_encode_write(
       }
       win_record(a, recs + i * a.L.stride, wj[j], q, W, skip[j]);
     }
-    // listed payloads are in output order: walk the ones touching the window
-    // (win_fill_big, one flattened chunk index with 4 loads in flight per
-    // lane, measured slower here: C5 encode 0.79 -> 0.89 ms, C3 +13 %)
+    // listed payloads are in output order: fill the window slots they cover
     while (k0 < nbig_tot && big[k0].dst + big[k0].n <= W.lo) ++k0;
     for (uint32_t k = k0; k < nbig_tot && big[k].dst < W.hi; ++k)
       win_put_coop(W, big[k].dst, big[k].src, big[k].n);
@@ -817,6 +863,7 @@ struct DecArgs {
   uint32_t range;   // spk_decode_shard_index: tiles [range_t0, ...) of the body
   uint32_t pad2_;
   uint64_t range_t0, range_entry;
+  const uint64_t *ends;  // MESSAGES: message i ends at ends[i] (null: offs[i + 1])
 };
 
 
@@ -846,7 +893,7 @@ __global__ __launch_bounds__(kThreads) void var_msg_parse(
   uint64_t cnt[SPK_MAX_SPANS] = {};
   uint64_t ok = 0, consumed = 0;
   if (i < a.n_msgs) {
-    const uint64_t f = offs[i], e = offs[i + 1];
+    const uint64_t f = offs[i], e = a.ends ? a.ends[i] : offs[i + 1];
     const uint64_t b = f + a.prefix;  // struct_pack message after the frame prefix
     MsgState s{~0ull, 1, SPK_ERRC_OK};
     if (e < f || e > a.wire_len || e - f < a.prefix) {
@@ -953,7 +1000,7 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
   if (i < a.n_msgs) {
     s = st[i];
     if (s.pos != ~0ull) {
-      end = offs[i + 1];
+      end = a.ends ? a.ends[i] : offs[i + 1];
       rec_counts(a.L, wire, s.pos, s.w, cnt, end);
     }
   }
@@ -1000,25 +1047,14 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
       ++sk;
     }
   }
-  if (live) decode_record(a.L, wire, s.pos, s.w, recs + i * a.L.stride, a.heaps, hoff, end, skip);
+  // copy split: gridDim.y blocks share the block's listed payloads; block 0
+  // also writes the records and the short payloads
+  if (live && blockIdx.y == 0)
+    decode_record(a.L, wire, s.pos, s.w, recs + i * a.L.stride, a.heaps, hoff, end, skip);
   __syncthreads();
   if (nbig_tot > kBigMax) nbig_tot = kBigMax;
   if (nbig_tot == 0) return;  // block-uniform
-  // per-payload aligned destination chunk counts -> exclusive prefix (LDS)
-  __shared__ uint32_t c0s[kBigMax + 1];
-  uint64_t nc = 0;
-  if (threadIdx.x < nbig_tot) {
-    const BigSeg &e = big[threadIdx.x];
-    uint64_t head = (16 - ((uintptr_t)e.dptr & 15)) & 15;
-    if (head > e.n) head = e.n;
-    nc = (e.n - head) >> 4;
-  }
-  uint64_t nct;
-  const uint64_t cx = block_excl_scan(nc, &nct, sh);
-  if (threadIdx.x < nbig_tot) c0s[threadIdx.x] = (uint32_t)cx;
-  if (threadIdx.x == 0) c0s[nbig_tot] = (uint32_t)nct;
-  __syncthreads();
-  coop_copy_all(big, (uint32_t)nbig_tot, c0s);
+  wave_copy_all(big, (uint32_t)nbig_tot, blockIdx.y, gridDim.y);
 }
 
 // ===========================================================================
@@ -3603,7 +3639,11 @@ hipError_t launch_var_encode(const spk_layout *L, int mode, uint64_t n,
   if (n == 0) {
     // header (+ zero count) only; reuse the write kernel with one block
   }
-  SPK_LAUNCH(var_encode_write, dim3(grid_for(n ? n : 1, kRPB)), dim3(kThreads), 0,
+  // window split (var_encode_write): up to 8 blocks per write block while the
+  // grid stays under ~8K blocks, i.e. for batches of a few thousand blocks
+  const unsigned nb = grid_for(n ? n : 1, kRPB);
+  const unsigned ny = nb >= 8192 ? 1u : (8192u / nb < kYSplit ? 8192u / nb : kYSplit);
+  SPK_LAUNCH(var_encode_write, dim3(nb, ny), dim3(kThreads), 0,
                      s, a, (const uint8_t *)d_recs, (uint8_t *)d_out, out_cap,
                      (const uint8_t *)ws, d_plan, d_offsets);
   (void)ws_bytes;
@@ -3642,8 +3682,9 @@ hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
                              uint64_t rec_cap, void *const *d_heaps,
                              const uint64_t *heap_caps, spk_dresult_t *d_res,
                              int32_t *d_errc, void *d_ws, size_t ws_bytes, hipStream_t s,
-                             uint32_t body_w, uint64_t body_n) {
+                             uint32_t body_w, uint64_t body_n, const uint64_t *d_msg_ends) {
   DecArgs a = {};
+  a.ends = d_msg_ends;
   a.prefix = prefix;
   a.body_w = body_w;
   a.body_n = body_n;
@@ -3668,7 +3709,9 @@ hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
     uint64_t *bsum = reinterpret_cast<uint64_t *>(ws + kWsScratch + sizeof(MsgState) * n_msgs);
     SPK_LAUNCH(var_scan_blocks, dim3(1), dim3(1024), 0, s, (uint64_t)nb,
                        a.L.n_spans, bsum, a, d_res);
-    SPK_LAUNCH(var_msg_write, dim3(nb), dim3(kThreads), 0, s, a, wire, d_offsets,
+    // (a copy split over gridDim.y blocks, as the encode's, measured no faster
+    // here with one wave per payload: C5 vector<int> decode 0.682 / 0.686 ms)
+    SPK_LAUNCH(var_msg_write, dim3(nb, 1), dim3(kThreads), 0, s, a, wire, d_offsets,
                        (const uint8_t *)ws, (uint8_t *)d_recs, (const spk_dresult_t *)d_res);
     (void)ws_bytes;
     return hipGetLastError();

@@ -178,6 +178,23 @@ class Codec:
                                         ws.numel(), _stream(stream)), "spk_decode")
         return self.res_buf
 
+    def deserialize_frames(self, out: RecordBatch, wire: torch.Tensor, begins: torch.Tensor,
+                           ends: torch.Tensor, n_msgs: int, prefix: int,
+                           errc_out: Optional[torch.Tensor] = None, heap_caps=None,
+                           stream=None) -> torch.Tensor:
+        """spk_decode_frames: message i = wire[begins[i] + prefix .. ends[i]) —
+        one record type's frames routed out of a mixed batch
+        (coro_rpc.FrameRouter). Stream-ordered, no host sync."""
+        ws = self.workspace(MODE_MESSAGES, n_msgs, wire.numel())
+        caps = heap_caps or [h.numel() // sp.elem.size
+                             for h, sp in zip(out.heaps, self.L.dev.spans)]
+        hc = (ct.c_uint64 * max(len(caps), 1))(*(caps or [0]))
+        self._check(self.lib.spk_decode_frames(
+            self.L.ptr, _p(wire), wire.numel(), _p(begins), _p(ends), n_msgs, prefix,
+            _p(out.recs), out.n, self._heap_ptrs(out.heaps), hc, _p(self.res_buf),
+            _p(errc_out), _p(ws), ws.numel(), _stream(stream)), "spk_decode_frames")
+        return self.res_buf
+
     def deserialize_body(self, out: RecordBatch, body: torch.Tensor, width: int, n: int,
                          heap_caps=None, stream=None) -> torch.Tensor:
         """spk_decode_body: n records from a VECTOR message body (after the
