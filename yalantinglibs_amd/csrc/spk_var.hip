@@ -1123,6 +1123,7 @@ struct FCtl {
   uint32_t range;                // the tiles are a byte range of the body (spk_decode_shard_*)
   uint32_t last;                 // range mode: the range holds the message's end
   unsigned long long stot[SPK_MAX_SPANS];  // span-count sums on the path
+  unsigned long long nlist[4];   // tiles listed for re-resolution by select pass k
 };
 constexpr size_t kWsFCtl = kWsCtl + 1280;
 static_assert(kWsFCtl + sizeof(FCtl) <= kWsScratch, "FCtl overlaps the scratch area");
@@ -1347,7 +1348,7 @@ __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
   c->term_chunk = kNone32;
   c->overflow = 0;
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);  // tile decoder state
-  for (int k = 0; k < 4; ++k) fc->broken[k] = 0;
+  for (int k = 0; k < 4; ++k) fc->broken[k] = fc->nlist[k] = 0;
   fc->unresolved = 0;
   fc->seq = 0;
   fc->njobs = 0;
@@ -2210,7 +2211,7 @@ __global__ __launch_bounds__(64 * kEmitWaves) void vec_emit(DecArgs a, WalkProg 
 //     publishes its FUNCTION: exit Y (the same for every entry below) and up
 //     to kAlt entries (X and other start candidates of chunk 0 whose walk
 //     reaches chunk 0's exit) with the tile's records / span sums for each.
-//  K2 vec_tile_select: tile t's true entry is tile t-1's exit (tile 0: the
+//  K2 vec_tile_pick / vec_tile_repair: tile t's true entry is tile t-1's exit (tile 0: the
 //     payload start). It selects the matching entry; a tile whose entry is
 //     none of them re-walks from it (rare; twice, a cascade is rarer still,
 //     then one wave fixes any rest in order).
@@ -2245,6 +2246,7 @@ struct TileBufs {
   int32_t *sel;       // [ntiles] selected entry (kSelTerm / kSelBroken)
   uint64_t *contrib;  // [1 + nsp][ntiles] selected (records, sums) -> exclusive prefix
   uint64_t *scan;     // block sums of the tile scan
+  uint32_t *blist;    // [ntiles] tiles a select pass found broken
   uint64_t ntiles, nchunks;
 };
 
@@ -2742,14 +2744,14 @@ __device__ __forceinline__ void tile_pass_through(const TileBufs &TB, uint64_t t
 // settled by the next pass and the sequential check).
 __device__ __forceinline__ void tile_jump(const TileBufs &TB, uint64_t p0, uint64_t t, uint64_t E,
                                           uint32_t nsp, uint32_t lane,
-                                          unsigned long long *changed) {
+                                          unsigned long long *changed, uint32_t step = 64) {
   if (E == kTermPos || E == kNoPos || E < p0) return;
   const uint64_t e0 = (E - p0) / kTileBytes;
   const uint64_t e = e0 < TB.ntiles ? e0 : TB.ntiles;
   if (t + 1 >= e) return;
   // the pass changed other tiles' functions: the next pass re-checks them
   if (lane == 0) atomicAdd(changed, 1ull);
-  for (uint64_t v = t + 1 + lane; v < e; v += 64) tile_pass_through(TB, v, E, nsp);
+  for (uint64_t v = t + 1 + lane; v < e; v += step) tile_pass_through(TB, v, E, nsp);
 }
 
 // tile t's selection given its current entry T (kSelBroken: none fits)
@@ -2762,10 +2764,36 @@ __device__ __forceinline__ int32_t tile_select_for(const TileBufs &TB, uint64_t 
   return kSelBroken;
 }
 
-// ---- K2: select each tile's entry; re-walk tiles whose entry is none of
-// theirs (one wave per tile; only those waves stage anything) ---------------
+// ---- K2: select each tile's entry (one thread per tile); tiles whose entry
+// is none of theirs are listed and re-walked by vec_tile_repair (one wave per
+// listed tile, a fixed grid striding over the list) -------------------------
+__global__ __launch_bounds__(256) void vec_tile_pick(uint8_t *__restrict__ ws, TileBufs TB,
+                                                     uint32_t nsp, uint32_t pass) {
+  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
+  FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= TB.ntiles || !vec_live(c)) return;
+  if (pass > 0 && !fc->broken[pass - 1]) return;  // the previous pass fixed nothing
+  const uint64_t T = tile_entry(TB, fc, t);
+  const int32_t sel = T == kNoPos ? kSelBroken : tile_select_for(TB, t, T);
+  if (sel != kSelBroken || T == kNoPos) {
+    TB.sel[t] = sel;
+    if (sel >= 0) tile_jump(TB, c->p0, t, TB.fn[t * kFnWords], nsp, 0, &fc->broken[pass], 1);
+    return;
+  }
+  atomicAdd(&fc->broken[pass], 1ull);
+  const uint64_t ts = c->p0 + t * kTileBytes;
+  if (T >= ts + kTileBytes) {  // inside a record that spans the tile
+    tile_pass_through(TB, t, T, nsp);
+    tile_jump(TB, c->p0, t, T, nsp, 0, &fc->broken[pass], 1);
+    return;
+  }
+  TB.blist[atomicAdd(&fc->nlist[pass], 1ull)] = (uint32_t)t;
+}
+
+constexpr unsigned kRepairGrid = 2048;
 template <int NS>
-__global__ __launch_bounds__(64) void vec_tile_select(DecArgs a, WalkProg P,
+__global__ __launch_bounds__(64) void vec_tile_repair(DecArgs a, WalkProg P,
                                                       const uint8_t *__restrict__ wire,
                                                       uint8_t *__restrict__ ws, TileBufs TB,
                                                       uint32_t pass) {
@@ -2773,55 +2801,56 @@ __global__ __launch_bounds__(64) void vec_tile_select(DecArgs a, WalkProg P,
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
   const uint32_t lane = threadIdx.x;
-  const uint64_t t = blockIdx.x;
-  if (t >= TB.ntiles || !vec_live(c)) return;
-  if (pass > 0 && !fc->broken[pass - 1]) return;  // the previous pass fixed nothing
-  uint64_t *fn = TB.fn + t * kFnWords;
-  const uint64_t T = tile_entry(TB, fc, t);
-  const int32_t sel = T == kNoPos ? kSelBroken : tile_select_for(TB, t, T);
-  if (sel != kSelBroken || T == kNoPos) {
-    if (lane == 0) TB.sel[t] = sel;
-    if (sel >= 0)
-      tile_jump(TB, c->p0, t, fn[0], NS > 0 ? (uint32_t)NS : P.ns, lane, &fc->broken[pass]);
-    return;
-  }
-  // broken: re-resolve the whole tile from its true entry
-  if (lane == 0) atomicAdd(&fc->broken[pass], 1ull);
+  if (!vec_live(c)) return;
+  const uint64_t nl = fc->nlist[pass];
   const uint32_t w = c->w;
   const uint64_t len = a.wire_len, p0 = c->p0;
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
-  const uint64_t ts = p0 + t * kTileBytes;
-  if (T >= ts + kTileBytes) {  // inside a record that spans the tile
-    if (lane == 0) tile_pass_through(TB, t, T, nsp);
-    tile_jump(TB, p0, t, T, nsp, lane, &fc->broken[pass]);
-    return;
+  for (uint64_t j = blockIdx.x; j < nl; j += gridDim.x) {
+    const uint64_t t = TB.blist[j];
+    uint64_t *fn = TB.fn + t * kFnWords;
+    const uint64_t T = tile_entry(TB, fc, t);  // (re-read: a predecessor may have moved)
+    const uint64_t ts = p0 + t * kTileBytes;
+    if (T == kNoPos) {
+      if (lane == 0) TB.sel[t] = kSelBroken;
+      continue;
+    }
+    if (T >= ts + kTileBytes) {
+      if (lane == 0) tile_pass_through(TB, t, T, nsp);
+      tile_jump(TB, p0, t, T, nsp, lane, &fc->broken[pass]);
+      continue;
+    }
+    const TileView tv = stage_tile(win_s[0], wire, len, ts, w, lane);
+    const uint64_t cs = ts + (uint64_t)lane * kTChunk;
+    const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
+    const uint64_t g = t * 64 + lane;
+    uint64_t used = TB.cused[g], ex = TB.cex[g], term_at = kTermPos;
+    uint32_t cnt = TB.ccnt[g];
+    uint64_t sums[NS > 0 ? NS : SPK_MAX_SPANS];
+    for (uint32_t q = 0; q < nsp; ++q) sums[q] = TB.csum[(uint64_t)q * TB.nchunks + g];
+    resolve_tile<NS>(P, tv.rd, len, w, ce, lane, T, used, ex, cnt, sums, term_at);
+    const uint64_t tcnt = wave_sum_u64(cnt);
+    uint64_t tsum[NS > 0 ? NS : SPK_MAX_SPANS];
+    for (uint32_t q = 0; q < nsp; ++q) tsum[q] = wave_sum_u64(sums[q]);
+    TB.cused[g] = used;
+    TB.cex[g] = ex;
+    TB.ccnt[g] = cnt;
+    for (uint32_t q = 0; q < nsp; ++q) TB.csum[(uint64_t)q * TB.nchunks + g] = sums[q];
+    const uint64_t y63 = __shfl(ex, 63);
+    if (lane == 0) {
+      fn[0] = y63;
+      fn[1] = 1;
+      fn[2] = T;
+      fn[3] = tcnt;
+      for (uint32_t q = 0; q < nsp; ++q) fn[4 + q] = tsum[q];
+      TB.sel[t] = 0;
+    }
+    tile_jump(TB, p0, t, y63, nsp, lane, &fc->broken[pass]);
+    // the window is restaged for the next listed tile
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   }
-  const TileView tv = stage_tile(win_s[0], wire, len, ts, w, lane);
-  const uint64_t cs = ts + (uint64_t)lane * kTChunk;
-  const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
-  const uint64_t g = t * 64 + lane;
-  uint64_t used = TB.cused[g], ex = TB.cex[g], term_at = kTermPos;
-  uint32_t cnt = TB.ccnt[g];
-  uint64_t sums[NS > 0 ? NS : SPK_MAX_SPANS];
-  for (uint32_t q = 0; q < nsp; ++q) sums[q] = TB.csum[(uint64_t)q * TB.nchunks + g];
-  resolve_tile<NS>(P, tv.rd, len, w, ce, lane, T, used, ex, cnt, sums, term_at);
-  const uint64_t tcnt = wave_sum_u64(cnt);
-  uint64_t tsum[NS > 0 ? NS : SPK_MAX_SPANS];
-  for (uint32_t q = 0; q < nsp; ++q) tsum[q] = wave_sum_u64(sums[q]);
-  TB.cused[g] = used;
-  TB.cex[g] = ex;
-  TB.ccnt[g] = cnt;
-  for (uint32_t q = 0; q < nsp; ++q) TB.csum[(uint64_t)q * TB.nchunks + g] = sums[q];
-  const uint64_t y63 = __shfl(ex, 63);
-  if (lane == 0) {
-    fn[0] = y63;
-    fn[1] = 1;
-    fn[2] = T;
-    fn[3] = tcnt;
-    for (uint32_t q = 0; q < nsp; ++q) fn[4 + q] = tsum[q];
-    TB.sel[t] = 0;
-  }
-  tile_jump(TB, p0, t, y63, nsp, lane, &fc->broken[pass]);
 }
 
 // Residual entries no pass could select (an exit that moved twice in a row,
@@ -3409,7 +3438,7 @@ static hipError_t launch_vec_decode_ns(const DecArgs &a, const WalkProg &P, cons
 
 // ---- tile decoder: workspace and launch ---------------------------------------
 struct TileWs {
-  size_t fn, cused, cex, ccnt, csum, sel, contrib, scan, jobs, end;
+  size_t fn, cused, cex, ccnt, csum, sel, contrib, scan, blist, jobs, end;
   uint64_t ntiles, nchunks, nsb;
 };
 static TileWs tile_ws_layout(const spk_layout *L, uint64_t wire_len) {
@@ -3435,6 +3464,7 @@ static TileWs tile_ws_layout(const spk_layout *L, uint64_t wire_len) {
   f.sel = take(f.ntiles * 4);
   f.contrib = take(f.ntiles * 8 * (1 + ns));
   f.scan = take(f.nsb * 8 * (1 + ns));
+  f.blist = take(f.ntiles * 4);
   f.jobs = take(big_jobs_cap(wire_len) * sizeof(BigJob));
   f.end = off;
   return f;
@@ -3476,6 +3506,7 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
   TB.sel = reinterpret_cast<int32_t *>(ws + f.sel);
   TB.contrib = reinterpret_cast<uint64_t *>(ws + f.contrib);
   TB.scan = reinterpret_cast<uint64_t *>(ws + f.scan);
+  TB.blist = reinterpret_cast<uint32_t *>(ws + f.blist);
   TB.ntiles = f.ntiles;
   TB.nchunks = f.nchunks;
   const uint32_t nsp = P.ns ? P.ns : 1;
@@ -3496,9 +3527,10 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
   SPK_LAUNCH(vec_tile_spec<NS>, dim3(grid_for(f.ntiles, kDecWaves)), dim3(64 * kDecWaves), 0, s,
              a, P, wire, (const uint8_t *)ws, TB, tile_dbg());
   if (phase == kTilesIndex) SPK_LAUNCH(vec_range_entry, dim3(1), dim3(64), 0, s, ws, TB);
-  for (uint32_t pass = 0; pass < 3; ++pass)
-    SPK_LAUNCH(vec_tile_select<NS>, dim3((unsigned)f.ntiles), dim3(64), 0, s, a, P, wire, ws, TB,
-               pass);
+  for (uint32_t pass = 0; pass < 3; ++pass) {
+    SPK_LAUNCH(vec_tile_pick, dim3(grid_for(f.ntiles, 256)), dim3(256), 0, s, ws, TB, nsp, pass);
+    SPK_LAUNCH(vec_tile_repair<NS>, dim3(kRepairGrid), dim3(64), 0, s, a, P, wire, ws, TB, pass);
+  }
   SPK_LAUNCH(vec_tile_seqfix<NS>, dim3(1), dim3(64), 0, s, a, P, wire, ws, TB, 2u);
   SPK_LAUNCH(vec_tile_contrib, dim3(grid_for(f.ntiles, 256)), dim3(256), 0, s, ws, TB, nsp);
   SPK_LAUNCH(tscan_reduce, dim3(nb), dim3(256), 0, s, (const uint8_t *)ws, TB, 1 + nsp);
