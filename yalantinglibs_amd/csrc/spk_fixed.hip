@@ -358,6 +358,7 @@ static unsigned elem_grid(uint64_t items, unsigned threads = 256) {
 // global loads inside the same kernel, so results never depend on the path.
 constexpr int kMsgThreads = 256;
 constexpr uint32_t kMsgStageMax = 32768;  // staging bytes per block
+constexpr uint32_t kStagePer = 5;  // 16-B staging loads in flight per lane (decode)
 
 struct MsgLdsArgs {
   spk_msgfmt fmt;   // decode only
@@ -401,8 +402,20 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_encode_lds(
   for (uint32_t k = tid; k < H; k += kMsgThreads) hdr[k] = a.hdr[k];
   const uint8_t *src = in + first * S;
   const uint32_t bin = nR * S;  // multiple of 4
-  for (uint32_t c = tid; c < bin / 16; c += kMsgThreads)
-    reinterpret_cast<v4u *>(inl)[c] = *reinterpret_cast<const v4u_unaligned *>(src + 16 * c);
+  // kStagePer 16-B loads in flight per lane before their LDS writes
+  for (uint32_t c0 = 0; c0 < bin / 16; c0 += kStagePer * kMsgThreads) {
+    v4u val[kStagePer];
+#pragma unroll
+    for (uint32_t k = 0; k < kStagePer; ++k) {
+      const uint32_t c = c0 + tid + k * kMsgThreads;
+      if (c < bin / 16) val[k] = *reinterpret_cast<const v4u_unaligned *>(src + 16 * c);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < kStagePer; ++k) {
+      const uint32_t c = c0 + tid + k * kMsgThreads;
+      if (c < bin / 16) reinterpret_cast<v4u *>(inl)[c] = val[k];
+    }
+  }
   for (uint32_t d = (bin / 16) * 4 + tid; d < bin / 4; d += kMsgThreads)
     reinterpret_cast<uint32_t *>(inl)[d] = reinterpret_cast<const uint32_t *>(src)[d];
   if (offs)
@@ -460,15 +473,23 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
   // the end (same-address atomics per group would serialise in L2)
   unsigned long long ok = 0, consumed = 0;
   bool cap_hit = false;
+  // message bounds of this lane in group g (prefetched one group ahead)
+  auto bounds = [&](uint64_t g, uint64_t &b, uint64_t &e) {
+    const uint64_t i = g * a.R + tid;
+    if (g >= ngroups || tid >= a.R || i >= a.n) return;
+    b = offs ? offs[i] : i * a.fixed_M;
+    e = offs ? (a.ends ? a.ends[i] : offs[i + 1]) : (i + 1) * a.fixed_M;
+  };
+  uint64_t b_nx = 0, e_nx = 0;
+  bounds(blockIdx.x, b_nx, e_nx);
   for (uint64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
     const uint64_t first = g * a.R;
     const uint32_t nR = (uint32_t)((a.n - first) < a.R ? (a.n - first) : a.R);
-    uint64_t b = 0, e = 0;
+    uint64_t b = b_nx, e = e_nx;
+    b_nx = e_nx = 0;
+    bounds(g + gridDim.x, b_nx, e_nx);
     bool inr = false;
     if (tid < nR) {
-      const uint64_t i = first + tid;
-      b = offs ? offs[i] : i * a.fixed_M;
-      e = offs ? (a.ends ? a.ends[i] : offs[i + 1]) : (i + 1) * a.fixed_M;
       inr = e >= b && e <= a.wire_len && e - b >= a.prefix;
       b += a.prefix;  // the struct_pack message starts after the frame prefix
     }
@@ -494,13 +515,33 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
     if (staged) {
       const uint32_t nb = (uint32_t)(hi - lo);
       const uint64_t full = (a.wire_len - lo) / 16;  // 16-B chunks inside the wire
-      for (uint32_t c = tid; 16 * c < nb; c += kMsgThreads) {
-        if (c < full) {
-          reinterpret_cast<v4u *>(stage)[c] =
-              *reinterpret_cast<const v4u_unaligned *>(wire + lo + 16 * (uint64_t)c);
-        } else {
-          for (uint32_t k = 0; k < 16 && 16 * c + k < nb; ++k)
-            stage[16 * c + k] = wire[lo + 16 * (uint64_t)c + k];
+      const uint32_t nc = (nb + 15) / 16;
+      if (nc <= full) {
+        // each lane issues kStagePer 16-B loads before its LDS writes (a
+        // load / store loop waits one load latency per 4 KiB); one round
+        // covers 256 68-B messages
+        for (uint32_t c0 = 0; c0 < nc; c0 += kStagePer * kMsgThreads) {
+          v4u val[kStagePer];
+#pragma unroll
+          for (uint32_t k = 0; k < kStagePer; ++k) {
+            const uint32_t c = c0 + tid + k * kMsgThreads;
+            if (c < nc) val[k] = *reinterpret_cast<const v4u_unaligned *>(wire + lo + 16 * (uint64_t)c);
+          }
+#pragma unroll
+          for (uint32_t k = 0; k < kStagePer; ++k) {
+            const uint32_t c = c0 + tid + k * kMsgThreads;
+            if (c < nc) reinterpret_cast<v4u *>(stage)[c] = val[k];
+          }
+        }
+      } else {
+        for (uint32_t c = tid; 16 * c < nb; c += kMsgThreads) {
+          if (c < full) {
+            reinterpret_cast<v4u *>(stage)[c] =
+                *reinterpret_cast<const v4u_unaligned *>(wire + lo + 16 * (uint64_t)c);
+          } else {
+            for (uint32_t k = 0; k < 16 && 16 * c + k < nb; ++k)
+              stage[16 * c + k] = wire[lo + 16 * (uint64_t)c + k];
+          }
         }
       }
     }
