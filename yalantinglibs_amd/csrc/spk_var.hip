@@ -2346,8 +2346,12 @@ __device__ __forceinline__ void resolve_tile(const WalkProg &P, const Rd &rd, ui
     const uint64_t prev = __shfl_up(ex, 1);
     const uint64_t entry = lane == 0 ? entry0 : prev;
     const bool need = entry != used;
-    if (!__any(need)) return;
-    if (need) {
+    const uint64_t m = __ballot(need);
+    if (!m) return;
+    // a lane waits while its predecessor re-walks (that exit is about to
+    // change): walks from an exit that is itself wrong would only pass the
+    // error on, one lane per round (the first mismatch always proceeds)
+    if (need && !(lane > 0 && ((m >> (lane - 1)) & 1))) {
       walk_true<NS>(P, rd, len, w, entry, ce, ex, cnt, sums, term_at);
       used = entry;
     }
@@ -2365,8 +2369,9 @@ __device__ __forceinline__ void resolve_tile_sp(const WalkProg &P, const Rd &rd,
     const uint64_t prev = __shfl_up(ex, 1);
     const uint64_t entry = lane == 0 ? entry0 : prev;
     const bool need = entry != used;
-    if (!__any(need)) return;
-    if (need) {
+    const uint64_t m = __ballot(need);
+    if (!m) return;
+    if (need && !(lane > 0 && ((m >> (lane - 1)) & 1))) {  // as resolve_tile
       walk_merge<NS>(P, rd, len, w, entry, cs, ce, sp, ex, cnt, sums, term_at);
       used = entry;
     }
