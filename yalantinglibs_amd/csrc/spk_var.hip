@@ -227,14 +227,33 @@ __device__ __forceinline__ uint32_t wlog(uint32_t w) {
 }
 
 // ---- block-wide helpers ----------------------------------------------------
+// v of the lane selected by DPP control CTRL in the rows of ROW_MASK, 0 where
+// the source lane is outside the row / the row is masked (both halves moved
+// by the same lane permutation)
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, ROW_MASK,
+                                                             0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL,
+                                                             ROW_MASK, 0xf, false);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+// Inclusive wave64 prefix sum on the DPP network (no LDS round trips, unlike
+// __shfl_up's ds_bpermute): row_shr 1/2/4/8 within each row of 16 lanes, then
+// row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3).
 __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
-  const uint32_t lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint64_t u = __shfl_up(v, o);
-    if (lane >= (uint32_t)o) v += u;
-  }
+  v += dpp_u64<0x111, 0xf>(v);
+  v += dpp_u64<0x112, 0xf>(v);
+  v += dpp_u64<0x114, 0xf>(v);
+  v += dpp_u64<0x118, 0xf>(v);
+  v += dpp_u64<0x142, 0xa>(v);
+  v += dpp_u64<0x143, 0xc>(v);
   return v;
+}
+__device__ __forceinline__ uint64_t wave_lane63(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
 // exclusive scan over the block; returns prefix, sets *total
@@ -2119,13 +2138,9 @@ __device__ __forceinline__ void emit_record(const KLayout &L, const uint8_t *wir
 }
 
 __device__ __forceinline__ uint64_t wave_excl_scan_u64(uint64_t v, uint32_t lane, uint64_t *tot) {
-  uint64_t x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t y = __shfl_up(x, d);
-    if (lane >= (uint32_t)d) x += y;
-  }
-  *tot = __shfl(x, 63);
+  (void)lane;
+  const uint64_t x = wave_incl_scan(v);
+  *tot = wave_lane63(x);
   return x - v;
 }
 
@@ -2379,9 +2394,7 @@ __device__ __forceinline__ void resolve_tile_sp(const WalkProg &P, const Rd &rd,
 }
 
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  return wave_lane63(wave_incl_scan(v));
 }
 
 // The candidate screen of the speculative walk for one start position.
