@@ -258,7 +258,7 @@ class C5Workload:
     the handler lookup of router.hpp:226-240 for the whole batch), read the
     per-type counts, decode each type's [req_header][args] frames where they
     lie (spk_decode_frames), echo, encode each type's [resp_header][ret]
-    frames and copy every request's seq_num into its response."""
+    frames carrying every request's seq_num (spk_encode_framed_echo)."""
 
     def __init__(self, torch, n_total, rank, dev):
         import numpy as np
@@ -345,10 +345,9 @@ class C5Workload:
         if marks is not None:
             marks[2].record(stream)
         for k, g in enumerate(self.groups):
-            g["cd"].serialize_to(g["resp"], g["args"], SP.MODE_MESSAGES, g["resp_offs"],
-                                 stream=stream, frame=g["rs"])
-            RPC.copy_frame_field(g["resp"], g["resp_offs"], RPC.RESP_SEQ_OFF, self.wire,
-                                 rt.begins[k], RPC.REQ_SEQ_OFF, 4, g["m"], stream=stream)
+            # responses carry their requests' seq_num (spk_encode_framed_echo)
+            g["cd"].serialize_echo(g["resp"], g["args"], g["resp_offs"], g["rs"], self.wire,
+                                   rt.begins[k], RPC.REQ_SEQ_OFF, stream=stream)
         if marks is not None:
             marks[3].record(stream)
 

@@ -403,6 +403,18 @@ int spk_decode_frames(const spk_layout *L, const void *d_wire, uint64_t wire_len
                       void *const *d_heaps, const uint64_t *heap_caps,
                       spk_dresult_t *d_res, int32_t *d_errc, void *d_ws,
                       size_t ws_bytes, void *stream);
+/* spk_encode_framed whose message i carries, instead of seq_base + i, the
+ * u32 LE at d_seq_src[d_seq_offsets[i] + seq_src_off] in its frame's seq
+ * field: responses encoded per type echo their requests' seq_num
+ * (coro_rpc_protocol.hpp:191-201) with d_seq_src = the request frames and
+ * d_seq_offsets = that type's d_begins from spk_route_frames, seq_src_off = 4.
+ * F->seq_off must name the field. */
+int spk_encode_framed_echo(const spk_layout *L, uint64_t n, const void *d_recs,
+                           const void *const *d_heaps, const spk_plan_t *d_plan,
+                           const spk_frame *F, const void *d_seq_src,
+                           const uint64_t *d_seq_offsets, uint32_t seq_src_off, void *d_out,
+                           uint64_t out_cap, uint64_t *d_msg_offsets, void *d_ws,
+                           size_t ws_bytes, void *stream);
 /* For i < n: copy `bytes` (1..8) from d_src[d_src_offsets[i] + src_off] to
  * d_dst[d_dst_offsets[i] + dst_off]: the response header echoes its request's
  * seq_num (coro_rpc_protocol.hpp:191-201) when responses were encoded per

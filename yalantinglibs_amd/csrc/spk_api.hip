@@ -251,7 +251,8 @@ static int frame_check(const spk_frame *F) {
 static int encode_impl(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
                        const void *const *d_heaps, const spk_plan_t *d_plan, void *d_out,
                        uint64_t out_cap, uint64_t *d_msg_offsets, const spk_frame *F,
-                       void *d_ws, size_t ws_bytes, void *stream) {
+                       void *d_ws, size_t ws_bytes, void *stream,
+                       const SeqEcho *echo = nullptr) {
   int rc = spk_layout_check(L);
   if (rc) return rc;
   if ((mode != SPK_MODE_VECTOR && mode != SPK_MODE_MESSAGES) || !d_plan || !d_ws || !d_out)
@@ -270,15 +271,15 @@ static int encode_impl(const spk_layout *L, int mode, uint64_t n, const void *d_
     const uint32_t P = F ? F->prefix_len : 0;
     const uint64_t total = n * (uint64_t)(P + write_hdr(hb, L->fmt_one, 1) + L->rec_stride);
     if (total > out_cap) return SPK_E_CAPACITY;
-    return hip_rc(launch_fixed_encode_messages(L, n, d_recs, d_out, d_msg_offsets, F, s));
+    return hip_rc(launch_fixed_encode_messages(L, n, d_recs, d_out, d_msg_offsets, F, s, echo));
   }
   if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
   if ((rc = heaps_check(L, n, d_heaps))) return rc;
   if (layout_nested(L))
     return hip_rc(launch_nested_encode(L, mode, n, d_recs, d_heaps, d_out, d_msg_offsets, F, 0,
-                                       d_ws, s));
+                                       d_ws, s, echo));
   return hip_rc(launch_var_encode(L, mode, n, d_recs, d_heaps, d_plan, d_out, out_cap,
-                                  d_msg_offsets, F, d_ws, ws_bytes, s));
+                                  d_msg_offsets, F, d_ws, ws_bytes, s, echo));
 }
 
 int spk_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
@@ -298,6 +299,21 @@ int spk_encode_framed(const spk_layout *L, uint64_t n, const void *d_recs,
   if (rc) return rc;
   return encode_impl(L, SPK_MODE_MESSAGES, n, d_recs, d_heaps, d_plan, d_out, out_cap,
                      d_msg_offsets, F, d_ws, ws_bytes, stream);
+}
+
+int spk_encode_framed_echo(const spk_layout *L, uint64_t n, const void *d_recs,
+                           const void *const *d_heaps, const spk_plan_t *d_plan,
+                           const spk_frame *F, const void *d_seq_src,
+                           const uint64_t *d_seq_offsets, uint32_t seq_src_off, void *d_out,
+                           uint64_t out_cap, uint64_t *d_msg_offsets, void *d_ws,
+                           size_t ws_bytes, void *stream) {
+  if (!F || F->seq_off == SPK_FRAME_NONE) return SPK_E_ARG;
+  if (n && (!d_seq_src || !d_seq_offsets)) return SPK_E_ARG;
+  int rc = frame_check(F);
+  if (rc) return rc;
+  const SeqEcho echo{(const uint8_t *)d_seq_src, d_seq_offsets, seq_src_off, 0};
+  return encode_impl(L, SPK_MODE_MESSAGES, n, d_recs, d_heaps, d_plan, d_out, out_cap,
+                     d_msg_offsets, F, d_ws, ws_bytes, stream, n ? &echo : nullptr);
 }
 
 static int decode_impl(const spk_layout *L, int mode, const void *d_wire, uint64_t wire_len,

@@ -261,15 +261,17 @@ struct MsgEncArgs {
   uint32_t hlen;      // header bytes (frame prefix + struct_pack header)
   uint32_t seq_off;   // frame sequence field (u32 LE = seq_base + i) or ~0u
   uint32_t seq_base;
+  SeqEcho echo;
   uint8_t hdr[kMsgHdrMax];
 };
 
 // byte r (< hlen) of message i's header: the template, with the frame's
 // sequence number field patched in
 __device__ __forceinline__ uint8_t msg_hdr_byte(const uint8_t *hdr, uint32_t r, uint64_t i,
-                                                uint32_t seq_off, uint32_t seq_base) {
+                                                uint32_t seq_off, uint32_t seq_base,
+                                                const SeqEcho &echo) {
   const uint32_t q = r - seq_off;
-  return r >= seq_off && q < 4 ? (uint8_t)((seq_base + (uint32_t)i) >> (8 * q)) : hdr[r];
+  return r >= seq_off && q < 4 ? (uint8_t)(seq_value(echo, seq_base, i) >> (8 * q)) : hdr[r];
 }
 
 // dword gather: out dword d -> message i = d / Mw, word r = d % Mw
@@ -291,7 +293,8 @@ __global__ __launch_bounds__(256) void fixed_msg_encode_w4(
       if (r < Hw) {
         uint32_t h;
         __builtin_memcpy(&h, a.hdr + 4 * r, 4);
-        v[j] = 4 * r == a.seq_off ? a.seq_base + (uint32_t)i : h;
+        // (i == n: the padding past the last message; an echo has no entry)
+        v[j] = 4 * r == a.seq_off && i < a.n ? seq_value(a.echo, a.seq_base, i) : h;
       } else {
         v[j] = (d0 + j < total_w) ? in[i * Sw + (r - Hw)] : 0u;
       }
@@ -326,7 +329,7 @@ __global__ __launch_bounds__(256) void fixed_msg_encode_b1(
        b += gstride) {
     const uint64_t i = b / M;
     const uint32_t r = (uint32_t)(b - i * M);
-    out[b] = r < a.hlen ? msg_hdr_byte(a.hdr, r, i, a.seq_off, a.seq_base)
+    out[b] = r < a.hlen ? msg_hdr_byte(a.hdr, r, i, a.seq_off, a.seq_base, a.echo)
                         : in[i * a.stride + (r - a.hlen)];
   }
   if (offs)
@@ -373,6 +376,7 @@ struct MsgLdsArgs {
   uint32_t prefix;  // decode: frame bytes before each message
   uint32_t seq_off; // encode: frame sequence field or ~0u
   uint32_t seq_base;
+  SeqEcho echo;     // encode: seq_num echoed from request frames
   const uint64_t *ends;  // decode: message i ends at ends[i] (null: offs[i + 1])
   uint8_t hdr[kMsgHdrMax];
 };
@@ -434,7 +438,7 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_encode_lds(
       uint32_t v[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        v[k] = r < Hw ? (r == seq_w ? a.seq_base + (uint32_t)(first + i) : hw[r])
+        v[k] = r < Hw ? (r == seq_w && i < nR ? seq_value(a.echo, a.seq_base, first + i) : hw[r])
                       : iw[i * Sw + (r - Hw)];
         if (++r == Mw) {
           r = 0;
@@ -452,7 +456,7 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_encode_lds(
   } else {
     for (uint32_t j = tid; j < bout; j += kMsgThreads) {
       const uint32_t i = j / M, r = j - i * M;
-      dst[j] = r < H ? msg_hdr_byte(hdr, r, first + i, a.seq_off, a.seq_base)
+      dst[j] = r < H ? msg_hdr_byte(hdr, r, first + i, a.seq_off, a.seq_base, a.echo)
                      : inl[i * S + (r - H)];
     }
   }
@@ -693,9 +697,10 @@ static uint32_t msg_header(const spk_layout *L, const spk_frame *F, uint8_t *hdr
 hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
                                         const void *d_recs, void *d_out,
                                         uint64_t *d_offsets, const spk_frame *F,
-                                        hipStream_t s) {
+                                        hipStream_t s, const SeqEcho *echo) {
   {
     MsgLdsArgs b = {};
+    if (echo) b.echo = *echo;
     b.n = n;
     b.stride = L->rec_stride;
     b.hlen = msg_header(L, F, b.hdr, &b.seq_off, &b.seq_base);
@@ -720,6 +725,7 @@ hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
     }
   }
   MsgEncArgs a = {};
+  if (echo) a.echo = *echo;
   a.n = n;
   a.stride = L->rec_stride;
   a.hlen = msg_header(L, F, a.hdr, &a.seq_off, &a.seq_base);

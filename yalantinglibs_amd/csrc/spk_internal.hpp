@@ -211,6 +211,23 @@ void trace_mark(const char *name, hipStream_t s, int end);
     if (spk_tr_) ::spk::trace_mark(#kern, (stream), 1);                 \
   } while (0)
 
+// ---- frame sequence numbers ------------------------------------------------
+namespace spk {
+// A framed encode writes message i's seq_num as seq_base + i, or, echoing
+// requests (spk_encode_framed_echo), as the u32 LE at src[offs[i] + off].
+struct SeqEcho {
+  const uint8_t *src;
+  const uint64_t *offs;
+  uint32_t off;
+  uint32_t pad_;
+};
+__device__ __forceinline__ uint32_t seq_value(const SeqEcho &e, uint32_t base, uint64_t i) {
+  if (!e.src) return base + (uint32_t)i;
+  const uint8_t *p = e.src + e.offs[i] + e.off;
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+}  // namespace spk
+
 // ---- launch wrappers implemented in the kernel TUs -----------------------
 namespace spk {
 // spk_var.hip: sharded VECTOR decode (phase 0 = index, 1 = emit)
@@ -228,7 +245,7 @@ hipError_t launch_nested_plan(const spk_layout *L, int mode, uint64_t n, const v
 hipError_t launch_nested_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
                                 const void *const *d_heaps, void *d_out,
                                 uint64_t *d_msg_offsets, const spk_frame *F, uint32_t fixed_w,
-                                void *d_ws, hipStream_t s);
+                                void *d_ws, hipStream_t s, const SeqEcho *echo = nullptr);
 hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wire,
                                 uint64_t wire_len, const uint64_t *d_msg_offsets,
                                 uint64_t n_msgs, uint32_t prefix, void *d_recs, uint64_t rec_cap,
@@ -245,7 +262,7 @@ hipError_t launch_fixed_encode_vector(const spk_layout *L, uint64_t n,
 hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
                                         const void *d_recs, void *d_out,
                                         uint64_t *d_offsets, const spk_frame *F,
-                                        hipStream_t s);
+                                        hipStream_t s, const SeqEcho *echo = nullptr);
 // body_w != 0: d_wire is a message BODY of body_n records at width body_w
 // (no header / count: spk_decode_body)
 hipError_t launch_fixed_decode_vector(const spk_layout *L, const void *d_wire,
@@ -270,7 +287,8 @@ hipError_t launch_var_encode(const spk_layout *L, int mode, uint64_t n,
                              const void *d_recs, const void *const *d_heaps,
                              const spk_plan_t *d_plan, void *d_out,
                              uint64_t out_cap, uint64_t *d_offsets, const spk_frame *F,
-                             void *d_ws, size_t ws_bytes, hipStream_t s);
+                             void *d_ws, size_t ws_bytes, hipStream_t s,
+                             const SeqEcho *echo = nullptr);
 hipError_t launch_var_encode_body(const spk_layout *L, uint64_t n, const void *d_recs,
                                   const void *const *d_heaps, uint32_t width, void *d_out,
                                   uint64_t out_cap, void *d_ws, size_t ws_bytes,

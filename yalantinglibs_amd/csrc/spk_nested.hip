@@ -804,6 +804,7 @@ struct NEnc {
   int mode;
   uint32_t fixed_w;        // spk_encode_body: imposed width (0: from the plan)
   uint32_t fpre, fseq_off, flen_off, fseq_base;
+  SeqEcho echo;
   uint8_t ftmpl[SPK_MAX_FRAME];
   spk_msgfmt fmt;          // the message format of `mode`
   const uint8_t *heaps[SPK_MAX_SPANS];
@@ -957,7 +958,7 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
     for (uint32_t b = 0; b < e.fpre; ++b) p[b] = e.ftmpl[b];
     const uint32_t mlen = (uint32_t)(q - m);
     if (e.fseq_off != SPK_FRAME_NONE) {
-      const uint32_t sq = e.fseq_base + (uint32_t)i;
+      const uint32_t sq = seq_value(e.echo, e.fseq_base, i);
       for (uint32_t b = 0; b < 4; ++b) p[e.fseq_off + b] = (uint8_t)(sq >> (8 * b));
     }
     if (e.flen_off != SPK_FRAME_NONE)
@@ -1025,8 +1026,9 @@ hipError_t launch_nested_plan(const spk_layout *L, int mode, uint64_t n, const v
 hipError_t launch_nested_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
                                 const void *const *d_heaps, void *d_out,
                                 uint64_t *d_msg_offsets, const spk_frame *F, uint32_t fixed_w,
-                                void *d_ws, hipStream_t s) {
+                                void *d_ws, hipStream_t s, const SeqEcho *echo) {
   NEnc e = make_nenc(L, mode, n, d_heaps);
+  if (echo) e.echo = *echo;
   e.fixed_w = fixed_w;
   if (F) {
     e.fpre = F->prefix_len;

@@ -43,7 +43,7 @@ __device__ __forceinline__ uint32_t frame_slot(const RouteArgs &a, const uint8_t
   return a.nk;
 }
 
-// per block: frames per key slot -> bcnt[block][slot]; slots -> tslot[i]
+// per block: frames per key slot -> bcnt[slot][block]; slots -> tslot[i]
 __global__ __launch_bounds__(kRT) void route_count(RouteArgs a, const uint8_t *__restrict__ wire,
                                                    const uint64_t *__restrict__ offs,
                                                    uint8_t *__restrict__ tslot,
@@ -61,39 +61,62 @@ __global__ __launch_bounds__(kRT) void route_count(RouteArgs a, const uint8_t *_
   if (threadIdx.x <= a.nk) {
     uint64_t s = 0;
     for (uint32_t w = 0; w < kRW; ++w) s += wc[w][threadIdx.x];
-    bcnt[(uint64_t)blockIdx.x * kRK + threadIdx.x] = s;
+    bcnt[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = s;
   }
 }
 
-// one block: per slot, exclusive prefix over blocks (in place) and the total
-__global__ __launch_bounds__(1024) void route_scan(uint64_t nblocks, uint32_t nk,
-                                                   uint64_t *__restrict__ bcnt,
-                                                   uint64_t *__restrict__ counts) {
-  __shared__ uint64_t sh[1024 / 64];
+// inclusive wave64 prefix sum on the DPP network (row_shr 1/2/4/8, then
+// row_bcast 15 / 31)
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, ROW_MASK,
+                                                             0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL,
+                                                             ROW_MASK, 0xf, false);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ uint64_t incl_scan64(uint64_t v) {
+  v += dpp64<0x111, 0xf>(v);
+  v += dpp64<0x112, 0xf>(v);
+  v += dpp64<0x114, 0xf>(v);
+  v += dpp64<0x118, 0xf>(v);
+  v += dpp64<0x142, 0xa>(v);
+  v += dpp64<0x143, 0xc>(v);
+  return v;
+}
+
+// one block: per slot, exclusive prefix over blocks (in place) and the total.
+// Thread j owns a run of consecutive blocks (summed serially), so each slot
+// takes one block-wide scan however many routing blocks there are.
+constexpr uint32_t kScanT = 1024;
+__global__ __launch_bounds__(kScanT) void route_scan(uint64_t nblocks, uint32_t nk,
+                                                     uint64_t *__restrict__ bcnt,
+                                                     uint64_t *__restrict__ counts) {
+  __shared__ uint64_t sh[kScanT / 64];
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t per = (nblocks + kScanT - 1) / kScanT;
+  const uint64_t b0 = (uint64_t)threadIdx.x * per;
+  const uint64_t b1 = b0 + per < nblocks ? b0 + per : nblocks;
   for (uint32_t k = 0; k <= nk; ++k) {
-    uint64_t carry = 0;
-    for (uint64_t b0 = 0; b0 < nblocks; b0 += blockDim.x) {
-      const uint64_t b = b0 + threadIdx.x;
-      const uint64_t v = b < nblocks ? bcnt[b * kRK + k] : 0;
-      uint64_t x = v;  // inclusive wave scan
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t y = __shfl_up(x, o);
-        if ((int)lane >= o) x += y;
-      }
-      if (lane == 63) sh[wv] = x;
-      __syncthreads();
-      uint64_t wbase = 0, tot = 0;
-      for (uint32_t w = 0; w < blockDim.x / 64; ++w) {
-        if (w < wv) wbase += sh[w];
-        tot += sh[w];
-      }
-      if (b < nblocks) bcnt[b * kRK + k] = carry + wbase + x - v;
-      carry += tot;
-      __syncthreads();
+    uint64_t run = 0;
+    uint64_t *col = bcnt + (uint64_t)k * nblocks;
+    for (uint64_t b = b0; b < b1; ++b) run += col[b];
+    const uint64_t inc = incl_scan64(run);
+    if (lane == 63) sh[wv] = inc;
+    __syncthreads();
+    uint64_t wbase = 0, tot = 0;
+    for (uint32_t w = 0; w < kScanT / 64; ++w) {
+      if (w < wv) wbase += sh[w];
+      tot += sh[w];
     }
-    if (threadIdx.x == 0) counts[k] = carry;
+    __syncthreads();
+    uint64_t x = wbase + inc - run;  // exclusive prefix of this thread's run
+    for (uint64_t b = b0; b < b1; ++b) {
+      const uint64_t c = col[b];
+      col[b] = x;
+      x += c;
+    }
+    if (threadIdx.x == 0) counts[k] = tot;
   }
 }
 
@@ -114,7 +137,7 @@ __global__ __launch_bounds__(kRT) void route_scatter(RouteArgs a,
   }
   __syncthreads();
   if (t >= kRK || !a.beg[t]) return;
-  uint64_t pos = bcnt[(uint64_t)blockIdx.x * kRK + t] + rank;
+  uint64_t pos = bcnt[(uint64_t)t * gridDim.x + blockIdx.x] + rank;
   for (uint32_t w = 0; w < wv; ++w) pos += wc[w][t];
   a.beg[t][pos] = offs[i];
   if (a.end[t]) a.end[t][pos] = offs[i + 1];
@@ -180,7 +203,7 @@ extern "C" int spk_route_frames(const void *d_wire, uint64_t wire_len,
   const uint8_t *wire = (const uint8_t *)d_wire;
   SPK_LAUNCH(route_count, dim3((unsigned)nb), dim3(kRT), 0, s, a, wire, d_frame_offsets, tslot,
              bcnt);
-  SPK_LAUNCH(route_scan, dim3(1), dim3(1024), 0, s, nb, n_keys, bcnt, d_counts);
+  SPK_LAUNCH(route_scan, dim3(1), dim3(kScanT), 0, s, nb, n_keys, bcnt, d_counts);
   SPK_LAUNCH(route_scatter, dim3((unsigned)nb), dim3(kRT), 0, s, a, d_frame_offsets,
              (const uint8_t *)tslot, (const uint64_t *)bcnt);
   return hipGetLastError() == hipSuccess ? SPK_OK : SPK_E_HIP;

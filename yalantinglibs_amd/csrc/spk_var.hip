@@ -68,6 +68,7 @@ struct VarArgs {
   uint32_t flen_off;
   uint32_t fseq_base;
   uint32_t pad_;
+  SeqEcho echo;       // MESSAGES: seq_num echoed from request frames
   uint8_t ftmpl[SPK_MAX_FRAME];
 };
 
@@ -575,7 +576,7 @@ __device__ __forceinline__ void win_frame(const VarArgs &a, const Win &W, uint64
     if (y < W.lo || y >= W.hi) continue;
     uint8_t v = a.ftmpl[x];
     if (x >= a.fseq_off && x - a.fseq_off < 4)
-      v = (uint8_t)((a.fseq_base + (uint32_t)i) >> (8 * (x - a.fseq_off)));
+      v = (uint8_t)(seq_value(a.echo, a.fseq_base, i) >> (8 * (x - a.fseq_off)));
     if (x >= a.flen_off && x - a.flen_off < 4) v = (uint8_t)(plen >> (8 * (x - a.flen_off)));
     W.lds[y - W.lo] = v;
   }
@@ -3676,8 +3677,9 @@ hipError_t launch_var_encode(const spk_layout *L, int mode, uint64_t n,
                              const void *d_recs, const void *const *d_heaps,
                              const spk_plan_t *d_plan, void *d_out, uint64_t out_cap,
                              uint64_t *d_offsets, const spk_frame *F, void *d_ws,
-                             size_t ws_bytes, hipStream_t s) {
+                             size_t ws_bytes, hipStream_t s, const SeqEcho *echo) {
   VarArgs a = make_varargs(L, mode, n, d_heaps);
+  if (echo) a.echo = *echo;
   if (F && mode == SPK_MODE_MESSAGES) {
     a.fpre = F->prefix_len;
     a.fseq_off = F->seq_off;

@@ -142,6 +142,20 @@ class Codec:
                                         _p(out), out.numel(), _p(offsets), _p(ws),
                                         ws.numel(), _stream(stream)), "spk_encode")
 
+    def serialize_echo(self, out: torch.Tensor, batch: RecordBatch, offsets: torch.Tensor,
+                       frame: C.spk_frame, seq_src: torch.Tensor, seq_offsets: torch.Tensor,
+                       seq_src_off: int = 4, stream=None):
+        """spk_encode_framed_echo (plan + write, no host sync): message i's
+        frame carries seq_src[seq_offsets[i] + seq_src_off ..+4] as its
+        seq_num — responses echoing their routed requests."""
+        self.plan(batch, MODE_MESSAGES, stream)
+        ws = self.workspace(MODE_MESSAGES, batch.n)
+        self._check(self.lib.spk_encode_framed_echo(
+            self.L.ptr, batch.n, _p(batch.recs), self._heap_ptrs(batch.heaps),
+            _p(self.plan_buf), ct.byref(frame), _p(seq_src), _p(seq_offsets), seq_src_off,
+            _p(out), out.numel(), _p(offsets), _p(ws), ws.numel(), _stream(stream)),
+            "spk_encode_framed_echo")
+
     def serialize(self, batch: RecordBatch, mode: int = MODE_VECTOR):
         """Returns (wire uint8 tensor, message offsets or None)."""
         plan = self.get_needed_size(batch, mode)
