@@ -288,6 +288,41 @@ class codec {
                             ws_.data(), ws_.size(), s_), "spk_encode_framed");
   }
 
+  // after plan(SPK_MODE_MESSAGES): framed messages whose seq_num is the u32 at
+  // d_seq_src[d_seq_offsets[i] + seq_src_off] (responses echoing the routed
+  // requests, coro_rpc_protocol.hpp:191-201)
+  void encode_framed_echo(const batch<R> &b, const spk_frame &f, const void *d_seq_src,
+                          const uint64_t *d_seq_offsets, uint32_t seq_src_off, void *d_out,
+                          std::size_t cap, uint64_t *d_offsets = nullptr) {
+    std::vector<const void *> hp = heap_ptrs(b);
+    check(spk_encode_framed_echo(&layout(), b.n, b.recs.data(), hp.data(),
+                                 (const spk_plan_t *)plan_.data(), &f, d_seq_src, d_seq_offsets,
+                                 seq_src_off, d_out, cap, d_offsets, ws_.data(), ws_.size(), s_),
+          "spk_encode_framed_echo");
+  }
+
+  // decode frames that need not be adjacent: message i = d_wire[d_begins[i] +
+  // prefix, d_ends[i]) (one function id's lists from a frame_router)
+  spk_dresult_t decode_frames(batch<R> &out, const void *d_wire, std::size_t len,
+                              const uint64_t *d_begins, const uint64_t *d_ends, std::size_t n,
+                              uint32_t prefix, int32_t *d_errc = nullptr) {
+    ws_.resize(spk_workspace_bytes(&layout(), SPK_MODE_MESSAGES, n, len));
+    res_.resize(sizeof(spk_dresult_t));
+    std::vector<void *> hp(n_spans() ? n_spans() : 1, nullptr);
+    std::vector<uint64_t> caps(n_spans() ? n_spans() : 1, 0);
+    for (uint32_t k = 0; k < n_spans(); ++k) {
+      hp[k] = out.heaps[k].data();
+      caps[k] = out.heap_elems[k];
+    }
+    check(spk_decode_frames(&layout(), d_wire, len, d_begins, d_ends, n, prefix, out.recs.data(),
+                            out.n, hp.data(), caps.data(), (spk_dresult_t *)res_.data(), d_errc,
+                            ws_.data(), ws_.size(), s_), "spk_decode_frames");
+    spk_dresult_t r{};
+    copy(&r, res_.data(), sizeof(r), SPK_COPY_D2H, s_);
+    sync(s_);
+    return r;
+  }
+
   // decode into `out` (capacities from out.n / out.heap_elems); `prefix` =
   // frame bytes before each message (MESSAGES mode only)
   spk_dresult_t decode(batch<R> &out, const void *d_wire, std::size_t len, int mode,
@@ -368,6 +403,56 @@ class codec {
   void *s_;
   buffer ws_, plan_, res_;
   std::vector<std::vector<uint8_t>> view_heaps_;
+};
+
+// A connection's request frames in arrival order, function ids interleaved:
+// the handler lookup of the reference server (router.hpp:226-240) for the
+// whole batch. After route(), list k (function_ids[k]; the last list: ids in
+// no handler map) holds its frames' bounds and arrival indices, in arrival
+// order, for codec<Args>::decode_frames and encode_framed_echo.
+class frame_router {
+ public:
+  frame_router(std::vector<uint32_t> function_ids, std::size_t capacity, void *stream = nullptr)
+      : ids_(std::move(function_ids)), cap_(capacity), s_(stream) {
+    const std::size_t lists = ids_.size() + 1;
+    for (std::size_t k = 0; k < lists; ++k) {
+      beg_.emplace_back((capacity ? capacity : 1) * 8);
+      end_.emplace_back((capacity ? capacity : 1) * 8);
+      idx_.emplace_back((capacity ? capacity : 1) * 8);
+    }
+    counts_.resize(lists * 8);
+    ws_.resize(spk_route_workspace_bytes(capacity, (uint32_t)ids_.size()));
+  }
+  // frame i = d_wire[d_offsets[i], d_offsets[i+1]); returns the list sizes
+  std::vector<uint64_t> route(const void *d_wire, std::size_t len, const uint64_t *d_offsets,
+                              std::size_t n) {
+    if (n > cap_) throw spk_error("struct_pack::gpu::frame_router: more frames than capacity");
+    std::vector<uint64_t *> b, e, x;
+    for (std::size_t k = 0; k <= ids_.size(); ++k) {
+      b.push_back((uint64_t *)beg_[k].data());
+      e.push_back((uint64_t *)end_[k].data());
+      x.push_back((uint64_t *)idx_[k].data());
+    }
+    check(spk_route_frames(d_wire, len, d_offsets, n, rpc_key_off, ids_.data(),
+                           (uint32_t)ids_.size(), b.data(), e.data(), x.data(),
+                           (uint64_t *)counts_.data(), ws_.data(), ws_.size(), s_),
+          "spk_route_frames");
+    std::vector<uint64_t> c(ids_.size() + 1);
+    copy(c.data(), counts_.data(), c.size() * 8, SPK_COPY_D2H, s_);
+    sync(s_);
+    return c;
+  }
+  const uint64_t *begins(std::size_t k) const { return (const uint64_t *)beg_[k].data(); }
+  const uint64_t *ends(std::size_t k) const { return (const uint64_t *)end_[k].data(); }
+  const uint64_t *index(std::size_t k) const { return (const uint64_t *)idx_[k].data(); }
+  static constexpr uint32_t rpc_key_off = 8;  // req_header.function_id
+
+ private:
+  std::vector<uint32_t> ids_;
+  std::size_t cap_;
+  void *s_;
+  std::vector<buffer> beg_, end_, idx_;
+  buffer counts_, ws_;
 };
 
 template <typename R, uint64_t conf>

@@ -3,7 +3,9 @@
 // from /root/reference). Reads like the reference's doctest suites
 // (src/struct_pack/tests/test_serialize.cpp): serialize -> compare bytes,
 // deserialize -> compare objects, truncated / corrupted buffers -> errc.
+#include <algorithm>
 #include <cstdio>
+#include <type_traits>
 #include <fstream>
 #include <iterator>
 #include <string>
@@ -135,6 +137,101 @@ static void roundtrip_frames(const char *fixture, const char *lens, std::size_t 
   CHECK(back == v);
 }
 
+static uint32_t fid_of(const char *name);
+
+// A mixed batch in arrival order: reference-built request frames of rect and
+// person interleaved (plus one frame of an unregistered id), routed by
+// function id on the GPU, each type decoded where its frames lie, and the
+// responses encoded with their requests' seq_num == the reference-built
+// response frames.
+template <typename T>
+static std::vector<std::string> split_frames(const char *fixture, const char *lens) {
+  const std::string w = golden(fixture);
+  auto l = golden_lens(lens);
+  std::vector<std::string> f;
+  std::size_t p = 0;
+  for (auto x : l) {
+    f.push_back(w.substr(p, x));
+    p += x;
+  }
+  return f;
+}
+static void routed_mixed_batch() {
+  using namespace spk_gold;
+  using rect_t = rpcb::rect;
+  using person_t = rpcb::person;
+  auto fr = split_frames<rect_t>("frames_rpcrect_req_n100_p0.bin", "frames_rpcrect_req_n100_p0.lens");
+  auto fp = split_frames<person_t>("frames_person_req_n120_p48.bin",
+                                   "frames_person_req_n120_p48.lens");
+  CHECK(fr.size() == 100 && fp.size() == 120);
+  std::string wire;
+  std::vector<uint64_t> offs{0};
+  std::vector<int> who;  // 0 rect, 1 person, 2 unknown id
+  std::size_t ir = 0, ip = 0;
+  for (std::size_t j = 0; ir < fr.size() || ip < fp.size(); ++j) {
+    std::string f;
+    if (j == 57) {
+      f = fp[0];
+      f[8] = 0x7F;  // an id no handler has
+      who.push_back(2);
+    } else if (ip >= fp.size() || (ir < fr.size() && (j * 7) % 11 < 5)) {
+      f = fr[ir++];
+      who.push_back(0);
+    } else {
+      f = fp[ip++];
+      who.push_back(1);
+    }
+    wire += f;
+    offs.push_back(wire.size());
+  }
+  const std::size_t n = who.size();
+  void *s = nullptr;
+  device::buffer dw(wire.size() + 16), doffs(offs.size() * 8);
+  device::copy(dw.data(), wire.data(), wire.size(), SPK_COPY_H2D, s);
+  device::copy(doffs.data(), offs.data(), offs.size() * 8, SPK_COPY_H2D, s);
+  device::frame_router rt({fid_of("echo_rect"), fid_of("echo_person")}, n, s);
+  auto counts = rt.route(dw.data(), wire.size(), (const uint64_t *)doffs.data(), n);
+  CHECK(counts.size() == 3 && counts[0] == 100 && counts[1] == 120 && counts[2] == 1);
+  // arrival order within each id (the stable partition)
+  std::vector<uint64_t> idx(n);
+  device::copy(idx.data(), rt.index(1), counts[1] * 8, SPK_COPY_D2H, s);
+  device::sync(s);
+  std::vector<uint64_t> want;
+  for (std::size_t i = 0; i < n; ++i)
+    if (who[i] == 1) want.push_back(i);
+  CHECK(std::equal(want.begin(), want.end(), idx.begin()));
+  auto check_type = [&](auto tag, std::size_t k, const char *resp_fixture, auto gen) {
+    using T = typename decltype(tag)::type;
+    auto &c = device::thread_codec<T, sp_config::DEFAULT>();
+    auto b = c.alloc_for_wire(wire.size(), counts[k]);
+    spk_dresult_t r = c.decode_frames(b, dw.data(), wire.size(), rt.begins(k), rt.ends(k),
+                                      counts[k], rpc_frame::req_head_len);
+    CHECK(r.errc == 0 && r.count == counts[k]);
+    for (uint32_t q = 0; q < c.n_spans(); ++q) b.heap_elems[q] = r.heap_used[q];
+    std::vector<T> got(counts[k]);
+    c.download(b, counts[k], got.data());
+    bool same = true;
+    for (std::size_t i = 0; i < got.size(); ++i) same &= got[i] == gen(i);
+    CHECK(same);
+    // responses: the echo encode writes each request's seq_num
+    b.n = counts[k];
+    spk_plan_t p = c.plan(b, SPK_MODE_MESSAGES);
+    const spk_frame f = rpc_frame::response(0);
+    const std::size_t total = p.total_bytes + counts[k] * f.prefix_len;
+    device::buffer out(total + 16);
+    c.encode_framed_echo(b, f, dw.data(), rt.begins(k), 4, out.data(), out.size());
+    std::string bytes(total, '\0');
+    device::copy(bytes.data(), out.data(), total, SPK_COPY_D2H, s);
+    device::sync(s);
+    CHECK(bytes == golden(resp_fixture));
+  };
+  const uint64_t S7 = 0x5EED0007, S8 = 0x5EED0008;
+  check_type(std::type_identity<rect_t>{}, 0, "frames_rpcrect_resp_n100_p0.bin",
+             [&](std::size_t i) { return make_rpc_rect(S7, i); });
+  check_type(std::type_identity<person_t>{}, 1, "frames_person_resp_n120_p48.bin",
+             [&](std::size_t i) { return make_person(S8, i, 48); });
+}
+
 static uint32_t fid_of(const char *name) {  // frames.json function_id (MD5Hash32 of the name)
   std::ifstream f(std::string(SPK_GOLDEN_DIR) + "/frames.json");
   std::string js((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
@@ -207,6 +304,7 @@ int main() {
                           gen_var(300));
   roundtrip_messages<VarP>("varp_B_n200_p0_default.bin", "varp_B_n200_p0_default.lens", 200,
                            gen_varp);
+  routed_mixed_batch();
   std::printf("{\"checks\": %d, \"failures\": %d}\n", g_checks, g_fail);
   return g_fail ? 1 : 0;
 }
