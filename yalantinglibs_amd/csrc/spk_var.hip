@@ -2364,10 +2364,12 @@ __device__ __forceinline__ void resolve_tile(const WalkProg &P, const Rd &rd, ui
     const bool need = entry != used;
     const uint64_t m = __ballot(need);
     if (!m) return;
-    // a lane waits while its predecessor re-walks (that exit is about to
-    // change): walks from an exit that is itself wrong would only pass the
-    // error on, one lane per round (the first mismatch always proceeds)
-    if (need && !(lane > 0 && ((m >> (lane - 1)) & 1))) {
+    // a lane with a start of its own waits while its predecessor re-walks
+    // (that exit is about to change): walks from an exit that is itself wrong
+    // would only pass the error on, one lane per round (the first mismatch
+    // always proceeds). A lane without any start walks anyway: records
+    // resynchronise, so its walk from a wrong entry is often already right.
+    if (need && (used == kNoPos || !(lane > 0 && ((m >> (lane - 1)) & 1)))) {
       walk_true<NS>(P, rd, len, w, entry, ce, ex, cnt, sums, term_at);
       used = entry;
     }
@@ -2387,7 +2389,7 @@ __device__ __forceinline__ void resolve_tile_sp(const WalkProg &P, const Rd &rd,
     const bool need = entry != used;
     const uint64_t m = __ballot(need);
     if (!m) return;
-    if (need && !(lane > 0 && ((m >> (lane - 1)) & 1))) {  // as resolve_tile
+    if (need && (used == kNoPos || !(lane > 0 && ((m >> (lane - 1)) & 1)))) {  // as resolve_tile
       walk_merge<NS>(P, rd, len, w, entry, cs, ce, sp, ex, cnt, sums, term_at);
       used = entry;
     }
