@@ -223,16 +223,15 @@ class VecWorkload:
     def kernel_bytes(self):
         """Algorithmic bytes per step of the byte-moving kernels (SURVEY.md
         §8d per-unit figures x units per launch); scratch-only kernels
-        (plan reductions, scans, verification rounds) carry none."""
+        (plan reductions, scans, tile selection) carry none."""
         rb, wb = self.rec_bytes, self.wire_bytes
         if self.mode == self.SP.MODE_VECTOR:
             if self.cd.L.dev.trivial:  # one shift_copy per phase: records <-> body
                 return {"shift_copy_kernel": 4 * rb}
             # wait-free tile decoder: K1 reads the wire once, K4 reads it again
-            # and writes the records + heaps (SURVEY.md §8d); the legacy
-            # multi-pass decoder (SPK_VEC_DECODE=legacy) under its own names
+            # and writes the records + heaps (SURVEY.md §8d)
             return {"var_encode_write": rb + wb, "vec_tile_emit": wb + rb,
-                    "vec_tile_spec": wb, "vec_emit": wb + rb, "vec_spec": wb}
+                    "vec_tile_spec": wb}
         ob = 8 * (self.n + 1)
         if self.cd.L.dev.trivial:
             return {"fixed_msg_encode_lds": rb + wb + ob, "fixed_msg_decode_lds": wb + ob + rb}

@@ -1080,34 +1080,18 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
 // ===========================================================================
 // DECODE, SPK_MODE_VECTOR — speculative chunk walks
 // ===========================================================================
-// Record k's start depends on every earlier length field, so the payload is
-// cut into kSpec-byte chunks and each chunk is parsed speculatively by one
-// lane, in parallel: the walk starts at the chunk's first byte (the next
-// candidate byte when the first records it would parse are implausibly long)
-// and records the positions it visits in the chunk (P list) and in the next
-// kExt records past it (E list). Chunk 0 starts at the true payload start,
-// so its walk is exact. Chunk c's walk is on the true path from the first
-// position it shares with chunk c-1's extension (E_{c-1} is the true path
-// when chunk c-1 is verified), which a second parallel pass finds by merging
-// the two sorted lists. Chunks without such a meeting point (records larger
-// than the extension window, pathological data) are re-walked in order by a
-// single fixup lane from the true position, until the path meets a
-// speculative walk again. Then per-chunk record counts are scanned into
-// record indices, one lane per chunk re-walks its true records to place
-// their starts, a device-wide scan turns span counts into heap offsets, and
-// one thread per record decodes it.
+// Record k's start depends on every earlier length field. The decoder below
+// (the tile pipeline, vec_tile_*) cuts the payload into 16 KiB tiles of
+// kSpec-byte chunks, walks every chunk speculatively in parallel and joins
+// the walks; see the pipeline overview before kTChunk. (Round 1's multi-pass
+// chunk walker with P/E lists and verification rounds was removed in round 2
+// after the tile pipeline replaced it.)
 constexpr uint32_t kSpec = 256;        // payload bytes per speculation chunk
 constexpr uint32_t kWinExtra = 512;    // extension bytes staged past a wave's chunks
 constexpr uint32_t kPlaus = 4096;      // longest record a speculative walk accepts
 constexpr int kRounds = 6;             // parallel re-verification rounds (default)
 constexpr int kRoundsMax = 16;         // ... for varint layouts (WalkProg::rounds)
-constexpr uint32_t kExt = 4;           // records a spec walk continues past its chunk
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
-
-// per-chunk verification flags
-constexpr uint32_t kOk = 1u;           // true records of the chunk are known
-constexpr uint32_t kTerm = 2u;         // the true path terminates inside this chunk
-constexpr uint32_t kWalkTerm = 4u;     // the spec walk itself ended (INC / wire end)
 
 struct VCtl {
   uint64_t p0;       // payload start (after header + count)
@@ -1553,590 +1537,7 @@ __device__ __forceinline__ void emit_record_rd(const KLayout &L, const WinReader
   }
 }
 
-constexpr uint32_t kRegion = 64 * kSpec;                    // chunk bytes per wave
-constexpr uint32_t kRegionVec = (kRegion + kWinExtra) / 16;  // 16-B LDS slots per wave
-constexpr uint32_t kSpecWaves = 2;                           // waves per block
-
 constexpr uint64_t kTermPos = ~0ull;  // "the true path ended before this chunk"
-
-// Walk the true path of chunk `ch` from `entry` until it meets the chunk's
-// speculative walk (two-pointer merge against the sorted P list) or leaves
-// the chunk. Returns the chunk's exit (first true start past it, or
-// kTermPos when the path ends inside) and its complete-record count.
-template <int NS>
-__device__ void walk_chunk(const DecArgs &a, const WalkProg &P, const uint8_t *wire,
-                           const VCtl *c, const VecBufs &B, uint64_t ch, uint64_t entry,
-                           uint64_t *exit, uint32_t *count, uint32_t *flags, uint64_t *T,
-                           uint32_t *mj, uint64_t *hs) {
-  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
-  for (uint32_t q = 0; q < nsp; ++q) hs[q] = 0;
-  const uint64_t len = a.wire_len;
-  const uint64_t cs = c->p0 + ch * kSpec;
-  const uint64_t ce = cs + kSpec < len ? cs + kSpec : len;
-  const uint16_t *Pl = B.P + ch * c->lp;
-  const uint32_t np = B.Pn[ch], en = B.En[ch];
-  const bool walk_term = B.flags[ch] & kWalkTerm;
-  *T = entry < ce ? entry : ~0ull;
-  uint32_t fl = B.flags[ch] & kWalkTerm;
-  if (entry == kTermPos) {
-    *exit = kTermPos;
-    *count = 0;
-    *flags = fl | kOk;
-    *T = ~0ull;
-    *mj = 0;
-    return;
-  }
-  uint32_t j = 0, k = 0;
-  uint64_t pos = entry;
-  bool merged = false, term = false;
-  while (pos < ce) {
-    while (j < np && cs + Pl[j] < pos) ++j;
-    if (j < np && cs + Pl[j] == pos) {
-      merged = true;
-      break;
-    }
-    uint64_t rc[SPK_MAX_SPANS];
-    const uint64_t L = pos < len ? wlen_rd<NS>(P, GReader{wire, c->w}, len, pos, c->w, rc) : 0;
-    if (!L) {
-      term = true;
-      break;
-    }
-    ++k;
-    for (uint32_t q = 0; q < nsp; ++q) hs[q] += rc[q];
-    pos += L;
-  }
-  const uint32_t k0 = k;  // records walked before the meeting point
-  if (merged) {
-    k += np - j;
-    if (walk_term && en == 0) {  // the merged walk ends inside this chunk
-      k -= 1;
-      term = true;
-    }
-    if (j == 0) {  // the whole spec walk is true: its count sums hold
-      for (uint32_t q = 0; q < nsp; ++q) hs[q] += B.psum[q * c->cap + ch];
-    } else {
-      for (uint32_t i = j; i < np; ++i) {
-        uint64_t rc[SPK_MAX_SPANS];
-        if (wlen_rd<NS>(P, GReader{wire, c->w}, len, cs + Pl[i], c->w, rc))
-          for (uint32_t q = 0; q < nsp; ++q) hs[q] += rc[q];
-      }
-    }
-  }
-  if (term) {
-    *exit = kTermPos;
-    fl |= kTerm;
-  } else if (merged) {
-    *exit = cs + B.E[ch * kExt];  // E lists are relative to the chunk start
-  } else {
-    *exit = pos;
-  }
-  *count = k;
-  *flags = fl | kOk;
-  *mj = (merged ? j : np) | (k0 << 16);
-}
-
-// list chunk x for round r (once)
-__device__ __forceinline__ void mark_dirty(VCtl *c, const VecBufs &B, uint64_t x, uint32_t r) {
-  const uint64_t nch = c->nchunks;
-  uint32_t *stamp = B.dirty + (r & 1) * nch;
-  if (atomicExch(&stamp[x], r) != r) {
-    const uint32_t slot = atomicAdd(&c->wl_n[r], 1u);
-    B.wl[(r & 1) * nch + slot] = (uint32_t)x;
-  }
-}
-
-template <int NS>
-__device__ __forceinline__ void verify_chunk(const DecArgs &a, const WalkProg &P,
-                                             const uint8_t *wire, VCtl *c, const VecBufs &B,
-                                             uint64_t ch, uint64_t entry, uint64_t next_used,
-                                             uint32_t r) {
-  uint64_t exit, T, hs[SPK_MAX_SPANS];
-  uint32_t count, flags, mj;
-  walk_chunk<NS>(a, P, wire, c, B, ch, entry, &exit, &count, &flags, &T, &mj, hs);
-  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
-  for (uint32_t q = 0; q < nsp; ++q) B.hs[q * c->cap + ch] = hs[q];
-  B.mj[ch] = mj;
-  B.used[ch] = entry;
-  B.exitp[ch] = exit;
-  B.T[ch] = T;
-  B.cnt[ch] = count;
-  B.flags[ch] = flags;
-  if (r < P.rounds && ch + 1 < c->nchunks && exit != next_used)
-    mark_dirty(c, B, ch + 1, r + 1);
-}
-
-// One lane per chunk; a wave stages its 64 consecutive chunks (plus the head
-// of the extension) in LDS with coalesced 16-B loads, then every lane walks
-// its own chunk there. Lane 0 re-walks the last chunk of the previous wave
-// (63 new chunks per wave) so that every other lane gets its predecessor's
-// first extension position by a lane shuffle: round 0 of the verification
-// runs here, with the common case -- that position is the chunk's first
-// spec position -- settled in registers. A candidate start byte is plausible when no record of
-// its walk -- in the chunk or in the extension -- is implausible (longer than
-// kPlaus, or incomplete before the wire end); the lane takes the first
-// plausible candidate and records its walk: positions in the chunk (P) and
-// kExt positions past it (E). Chunk 0 starts at the payload start (exact).
-constexpr uint32_t kSpecStep = 63;  // new chunks per wave
-template <int NS>
-__global__ __launch_bounds__(64 * kSpecWaves) void vec_spec(DecArgs a, WalkProg P,
-                                                            const uint8_t *__restrict__ wire,
-                                                            uint8_t *__restrict__ ws, VecBufs B) {
-  __shared__ v4u_t reg_s[kSpecWaves][kRegionVec + 1];
-  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t ch0 = ((uint64_t)blockIdx.x * kSpecWaves + wv) * kSpecStep;
-  const uint64_t nch = c->nchunks;
-  if (ch0 >= nch) return;  // wave-uniform; only wave-level sync below
-  const uint32_t w = c->w, lp = c->lp;
-  const uint64_t len = a.wire_len;
-  const uint64_t chf = ch0 ? ch0 - 1 : 0;  // first chunk in the region
-  const uint64_t rs = c->p0 + chf * kSpec;
-  const uint64_t wend = rs + kRegionVec * 16 < len ? rs + kRegionVec * 16 : len;
-  v4u_t *reg = reg_s[wv];
-  for (uint32_t v = lane; v < kRegionVec; v += 64) {
-    const uint64_t g = rs + 16ull * v;
-    v4u_t val = {0u, 0u, 0u, 0u};
-    if (g + 16 <= len) {
-      val = *reinterpret_cast<const v4u_una *>(wire + g);
-    } else if (g < len) {
-      uint32_t t[4] = {0u, 0u, 0u, 0u};
-      for (uint64_t q = g; q < len; ++q) t[(q - g) >> 2] |= (uint32_t)wire[q] << (8 * ((q - g) & 3));
-      val = v4u_t{t[0], t[1], t[2], t[3]};
-    }
-    reg[v] = val;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // lane l walks chunk ch0 - 1 + l (lane 0 of wave 0 has none)
-  const bool live = (ch0 > 0 || lane > 0) && ch0 + lane - 1 < nch;
-  const uint64_t ch = live ? ch0 + lane - 1 : chf;
-  WinReader rd;
-  rd.d = (const lds_u32 *)(reg);
-  rd.wire = wire;
-  rd.cs = rs;
-  rd.wend = wend;
-  rd.w = w;
-  const uint64_t cs = c->p0 + ch * kSpec;
-  const uint64_t ce = cs + kSpec < len ? cs + kSpec : len;
-  uint16_t *Pl = B.P + ch * lp;
-  uint32_t *El = B.E + ch * kExt;
-  uint32_t np = 0, ne = 0, fl = 0, p0rel = 0, e0rel = 0;
-  // One record step per iteration for every lane (a nested try/walk loop
-  // would make the wave wait for each lane's walk in turn). While searching,
-  // 8 candidate start bytes are screened per iteration on their first count.
-  uint64_t t = 0, x = cs;
-  bool searching = ch != 0, done = !live;
-  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
-  uint64_t ps[NS > 0 ? NS : SPK_MAX_SPANS];
-  for (uint32_t k = 0; k < nsp; ++k) ps[k] = 0;
-  const uint32_t s0 = P.skip[0];
-  while (!done) {
-    if (searching) {
-      const uint64_t b0 = cs + t + s0;  // first count field of candidate cs+t
-      uint32_t m = 0;
-      if (NS < 0 && P.pf_var) {
-        // varints before the first count: parse them per candidate, then
-        // screen the count that follows
-        for (int k = 0; k < 8; ++k) {
-          uint64_t q = b0 + k;
-          bool ok = true;
-          for (uint32_t j = 0; j < P.vfirst[1]; ++j) {
-            uint64_t v;
-            const uint32_t l = rd.vread(q, len, &v);
-            if (!l || l == kViBad) {
-              ok = false;
-              break;
-            }
-            q += l + P.vafter[j];
-          }
-          if (ok) ok = (q + w <= len ? rd(q) : ~0ull) <= P.c0max;
-          m |= (ok ? 1u : 0u) << k;
-        }
-      } else if (b0 + 20 <= wend) {
-        const uint32_t o0 = (uint32_t)(b0 - rs), i = o0 >> 2, sh = o0 & 3;
-        const lds_u32 *d = rd.d;
-        const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2], d3 = d[i + 3], d4 = d[i + 4];
-        const uint32_t wd[4] = {__builtin_amdgcn_alignbyte(d1, d0, sh),
-                                __builtin_amdgcn_alignbyte(d2, d1, sh),
-                                __builtin_amdgcn_alignbyte(d3, d2, sh),
-                                __builtin_amdgcn_alignbyte(d4, d3, sh)};
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const uint32_t lo = __builtin_amdgcn_alignbyte(wd[(k >> 2) + 1], wd[k >> 2], k & 3);
-          uint64_t cv = w == 1 ? (lo & 0xFFu) : w == 2 ? (lo & 0xFFFFu) : lo;
-          if (w == 8)
-            cv |= (uint64_t)__builtin_amdgcn_alignbyte(wd[(k >> 2) + 2], wd[(k >> 2) + 1], k & 3)
-                  << 32;
-          m |= (cv <= P.c0max ? 1u : 0u) << k;
-        }
-      } else {
-        for (int k = 0; k < 8; ++k) {
-          const uint64_t q = b0 + k;
-          const uint64_t cv = q + w <= len ? rd(q) : ~0ull;
-          m |= (cv <= P.c0max ? 1u : 0u) << k;
-        }
-      }
-      if (P.pf_all) m = 0xFFu;  // first span an OPTION / no span: any byte may start a record
-      const uint64_t rem = ce - (cs + t);  // candidates must start in the chunk
-      if (rem < 8) m &= (1u << rem) - 1u;
-      if (!m) {
-        t += 8;
-        if (cs + t >= ce) done = true;
-        continue;
-      }
-      t += (uint32_t)__builtin_ctz(m);
-      x = cs + t;
-      np = ne = 0;
-      for (uint32_t k = 0; k < nsp; ++k) ps[k] = 0;
-      searching = false;
-    }
-    uint64_t rc[NS > 0 ? NS : SPK_MAX_SPANS];
-    const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w, rc) : 0;
-    if (ch != 0 && ((L == 0 && x < len) || L > kPlaus)) {  // off the record grid
-      t += 1;
-      searching = true;
-      if (cs + t >= ce) done = true;
-      continue;
-    }
-    if (x < ce) {
-      if (!np) p0rel = (uint32_t)(x - cs);
-      if (np < lp && lane) Pl[np] = (uint16_t)(x - cs);
-      ++np;
-      if (L)
-        for (uint32_t k = 0; k < nsp; ++k) ps[k] += rc[k];
-    } else {
-      const uint32_t er = (x - cs) < 0xFFFFFFFFull ? (uint32_t)(x - cs) : 0xFFFFFFFEu;
-      if (!ne) e0rel = er;
-      if (lane) El[ne] = er;
-      ++ne;
-    }
-    if (!L) {  // incomplete record or the wire end: the walk terminates here
-      fl = kWalkTerm;
-      break;
-    }
-    x += L;
-    if (x >= ce && ne == kExt) done = true;
-  }
-  if (searching) np = ne = fl = 0;  // no plausible start in the chunk
-  if (np > lp) {
-    atomicOr(&c->overflow, 1u);
-    np = lp;
-  }
-  // ---- round 0 of the verification ----
-  const uint64_t e0 = ne ? cs + e0rel : kTermPos;  // this chunk's first position past it
-  const uint64_t prev_e0 = __shfl_up(e0, 1);
-  if (!live || lane == 0) return;  // lane 0 only fed lane 1
-  B.Pn[ch] = np;
-  B.En[ch] = ne;
-  B.flags[ch] = fl;
-  // a later round may re-walk this chunk and meet the walk at its start
-  for (uint32_t k = 0; k < nsp; ++k) B.psum[k * c->cap + ch] = searching ? 0 : ps[k];
-  const uint64_t entry = ch == 0 ? c->p0 : prev_e0;
-  if (np && entry == cs + p0rel) {
-    // the true path enters at the spec walk's first position: all of it holds
-    const bool term = fl == kWalkTerm && ne == 0;  // the walk ends inside the chunk
-    B.mj[ch] = 0;
-    B.used[ch] = entry;
-    B.exitp[ch] = term ? kTermPos : e0;
-    B.T[ch] = entry;
-    B.cnt[ch] = term ? np - 1 : np;
-    B.flags[ch] = fl | kOk | (term ? kTerm : 0u);
-    for (uint32_t k = 0; k < nsp; ++k) B.hs[k * c->cap + ch] = ps[k];
-    return;
-  }
-  // otherwise the chunk is re-walked in round 1 (after its predecessor is
-  // final): one slow lane here would stall its whole wave
-  B.used[ch] = kTermPos - 1;  // no true entry equals this: "never verified"
-  mark_dirty(c, B, ch, 1);
-}
-
-// Round r >= 1 over round r's worklist: a listed chunk whose predecessor is
-// listed too waits for the next round; otherwise it is re-walked from its
-// predecessor's (now final) exit.
-template <int NS>
-__global__ __launch_bounds__(256) void vec_verify_round(DecArgs a, WalkProg P,
-                                                        const uint8_t *__restrict__ wire,
-                                                        uint8_t *__restrict__ ws, VecBufs B,
-                                                        uint32_t r) {
-  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
-  const uint64_t nch = c->nchunks;
-  const uint32_t n_in = c->wl_n[r];
-  const uint32_t *list = B.wl + (r & 1) * nch;
-  const uint32_t *stamp = B.dirty + (r & 1) * nch;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_in; i += gridDim.x * blockDim.x) {
-    const uint64_t ch = list[i];
-    if (stamp[ch - 1] == r) {  // predecessor not final yet (chunk 0 is never listed)
-      mark_dirty(c, B, ch, r + 1);
-      continue;
-    }
-    const uint64_t next_used = ch + 1 < nch ? B.used[ch + 1] : 0;
-    verify_chunk<NS>(a, P, wire, c, B, ch, B.exitp[ch - 1], next_used, r);
-  }
-}
-
-// Last resort, one block: chunks still listed after kRounds rounds, in
-// ascending order (bitonic sort in LDS), each re-walked with its cascade
-// until a chunk's state matches its predecessor's exit.
-constexpr uint32_t kFixSort = 4096;
-template <int NS>
-__global__ __launch_bounds__(1024) void vec_fixup(DecArgs a, WalkProg P,
-                                                  const uint8_t *__restrict__ wire,
-                                                  uint8_t *__restrict__ ws, VecBufs B) {
-  __shared__ uint32_t sh[kFixSort];
-  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
-  const uint32_t n = c->wl_n[P.rounds];
-  if (threadIdx.x == 0) c->n_unver = n;
-  if (!n) return;
-  const uint64_t nch = c->nchunks;
-  const uint32_t *list = B.wl + (P.rounds & 1) * nch;
-  uint32_t m = 2;  // sort size: next power of two >= n
-  while (m < n) m <<= 1;
-  if (n <= kFixSort) {
-    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) sh[i] = i < n ? list[i] : kNone32;
-    __syncthreads();
-    for (uint32_t k = 2; k <= m; k <<= 1) {
-      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-          const uint32_t l = i ^ j;
-          if (l > i) {
-            const uint32_t x = sh[i], y = sh[l];
-            if (((i & k) == 0) == (x > y)) {
-              sh[i] = y;
-              sh[l] = x;
-            }
-          }
-        }
-        __syncthreads();
-      }
-    }
-  }
-  if (threadIdx.x != 0) return;
-  if (n <= kFixSort) {
-    uint64_t done_to = 0;  // chunks < done_to are final
-    for (uint32_t i = 0; i < n; ++i) {
-      uint64_t ch = sh[i];
-      if (ch < done_to) continue;
-      for (; ch < nch; ++ch) {
-        const uint64_t entry = B.exitp[ch - 1];
-        if (entry == B.used[ch]) break;
-        verify_chunk<NS>(a, P, wire, c, B, ch, entry, 0, P.rounds);
-      }
-      done_to = ch + 1;
-    }
-  } else {
-    for (uint64_t ch = 1; ch < nch; ++ch) {  // long list: scan every chunk
-      const uint64_t entry = B.exitp[ch - 1];
-      if (entry != B.used[ch]) verify_chunk<NS>(a, P, wire, c, B, ch, entry, 0, P.rounds);
-    }
-  }
-}
-
-// first chunk where the true path terminates; zero the counts after it
-__global__ void vec_term_min(uint8_t *__restrict__ ws, const VecBufs B) {
-  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
-  const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch < c->nchunks && (B.flags[ch] & kTerm)) atomicMin(&c->term_chunk, (uint32_t)ch);
-}
-__global__ void vec_term_zero(uint8_t *__restrict__ ws, VecBufs B, uint32_t ns) {
-  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
-  const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch < c->nchunks && c->term_chunk != kNone32 && ch > c->term_chunk) {
-    B.cnt[ch] = 0;
-    for (uint32_t q = 0; q < ns; ++q) B.hs[q * c->cap + ch] = 0;
-  }
-}
-
-// ---- device-wide exclusive scan u32 -> u64 (3 phases) ----------------------
-constexpr uint32_t kScanIPT = 16;
-constexpr uint64_t kScanBlock = 256ull * kScanIPT;
-
-template <typename In>
-__global__ __launch_bounds__(256) void scan_reduce(const In *__restrict__ in, uint64_t n,
-                                                   uint64_t *__restrict__ bsum) {
-  __shared__ uint64_t sh[4];
-  const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock;
-  uint64_t s = 0;
-  for (uint32_t j = 0; j < kScanIPT; ++j) {
-    const uint64_t i = b0 + (uint64_t)j * 256 + threadIdx.x;
-    if (i < n) s += in[i];
-  }
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) bsum[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
-}
-
-// exclusive scan of bsum in place; *total = sum (one block)
-__global__ __launch_bounds__(1024) void scan_blocks(uint64_t *__restrict__ bsum, uint64_t nb,
-                                                    uint64_t *__restrict__ total) {
-  __shared__ uint64_t sh[16];
-  uint64_t carry = 0;
-  for (uint64_t b0 = 0; b0 < nb; b0 += blockDim.x) {
-    const uint64_t b = b0 + threadIdx.x;
-    const uint64_t v = b < nb ? bsum[b] : 0;
-    uint64_t tot;
-    const uint64_t ex = block_excl_scan(v, &tot, sh);
-    if (b < nb) bsum[b] = carry + ex;
-    carry += tot;
-  }
-  if (threadIdx.x == 0 && total) *total = carry;
-}
-
-template <typename In>
-__global__ __launch_bounds__(256) void scan_apply(const In *__restrict__ in, uint64_t n,
-                                                  const uint64_t *__restrict__ bsum,
-                                                  uint64_t *__restrict__ out) {
-  __shared__ uint64_t sh[4];
-  // thread t handles kScanIPT consecutive elements
-  const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock;
-  const uint64_t i0 = b0 + (uint64_t)threadIdx.x * kScanIPT;
-  In v[kScanIPT];
-  uint64_t s = 0;
-#pragma unroll
-  for (uint32_t j = 0; j < kScanIPT; ++j) {
-    v[j] = i0 + j < n ? in[i0 + j] : 0;
-    s += v[j];
-  }
-  uint64_t tot;
-  uint64_t run = bsum[blockIdx.x] + block_excl_scan(s, &tot, sh);
-#pragma unroll
-  for (uint32_t j = 0; j < kScanIPT; ++j) {
-    if (i0 + j < n) out[i0 + j] = run;
-    run += v[j];
-  }
-}
-
-// total records on the true path and the short-payload check
-__global__ void vec_count_check(uint8_t *__restrict__ ws, const uint64_t *__restrict__ total,
-                                spk_dresult_t *res) {
-  if (threadIdx.x != 0) return;
-  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
-  if (c->errc) return;
-  c->total = *total;
-  if (c->n && *total < c->n) res->errc = SPK_ERRC_NO_BUFFER_SPACE;
-}
-
-// The chunk holding record n-1 (one lane): the message end (consume_len)
-// and the heap elements used by records 0..n-1, for the capacity checks.
-template <int NS>
-__global__ __launch_bounds__(256) void vec_total(DecArgs a, WalkProg P,
-                                                 const uint8_t *__restrict__ wire,
-                                                 uint8_t *__restrict__ ws, VecBufs B,
-                                                 uint64_t *heap_tot) {
-  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
-  const uint64_t ch = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= c->nchunks || c->errc) return;
-  const uint64_t n = c->n, base = B.base[ch];
-  const uint32_t k = B.cnt[ch];
-  if (!n || !k || n - 1 < base || n - 1 >= base + k) return;
-  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
-  uint64_t h[SPK_MAX_SPANS];
-  for (uint32_t q = 0; q < nsp; ++q) h[q] = B.hb[q * c->cap + ch];
-  const uint32_t mj = B.mj[ch], k0 = mj >> 16, j0 = mj & 0xFFFFu;
-  const uint64_t cs = c->p0 + ch * kSpec;
-  const uint16_t *Pl = B.P + ch * c->lp;
-  uint64_t pos = B.T[ch];
-  for (uint32_t r = 0; r <= n - 1 - base; ++r) {
-    if (r >= k0) pos = cs + Pl[j0 + (r - k0)];
-    uint64_t rc[SPK_MAX_SPANS];
-    pos += wlen_rd<NS>(P, GReader{wire, c->w}, a.wire_len, pos, c->w, rc);
-    for (uint32_t q = 0; q < nsp; ++q) h[q] += rc[q];
-  }
-  c->end_pos = pos;
-  for (uint32_t q = 0; q < nsp; ++q) heap_tot[q] = h[q];
-}
-
-__global__ void vec_finish(DecArgs a, uint8_t *__restrict__ ws, spk_dresult_t *res,
-                           const uint64_t *__restrict__ heap_tot) {
-  if (threadIdx.x != 0) return;
-  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
-  if (c->errc) return;
-  spk_dresult_t r = *res;
-  if (r.errc == SPK_ERRC_NO_BUFFER_SPACE) {
-    r.count = 0;
-    r.consumed = 0;
-    for (int k = 0; k < SPK_MAX_SPANS; ++k) r.heap_used[k] = 0;
-  } else {
-    r.count = c->n;
-    const uint64_t end = c->n ? (uint64_t)c->end_pos : c->p0;
-    r.consumed = end > c->data_len ? end : c->data_len;
-    if (c->n > a.rec_cap && r.errc == 0) r.errc = SPK_ERRC_CAPACITY;
-    for (uint32_t k = 0; k < a.L.n_spans; ++k) {
-      r.heap_used[k] = c->n ? heap_tot[k] : 0;
-      if (r.heap_used[k] > a.heap_cap[k] && r.errc == 0) r.errc = SPK_ERRC_CAPACITY;
-    }
-  }
-  *res = r;
-}
-
-// Layouts with varints: the true path can also end on an overlong varint,
-// which the reference reports as invalid_buffer (varint.hpp:290-291), not
-// no_buffer_space. One lane finds the chunk of the last complete record
-// (binary search over the record bases), re-walks to the failing record
-// and classifies it.
-template <int NS>
-__global__ void vec_vi_errc(DecArgs a, WalkProg P, const uint8_t *__restrict__ wire,
-                            const uint8_t *__restrict__ ws, VecBufs B, spk_dresult_t *res) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
-  if (c->errc || res->errc != SPK_ERRC_NO_BUFFER_SPACE) return;
-  const uint64_t total = c->total;  // complete records on the true path (< n)
-  uint64_t pos = c->p0;
-  if (total) {
-    // the chunk holding record total-1: the last with base <= total-1
-    const uint64_t r = total - 1;
-    uint64_t lo = 0, hi = c->nchunks - 1;
-    while (lo < hi) {
-      const uint64_t mid = (lo + hi + 1) / 2;
-      if (B.base[mid] <= r) lo = mid; else hi = mid - 1;
-    }
-    const uint64_t ch = lo;
-    const uint32_t mj = B.mj[ch], k0 = mj >> 16, j0 = mj & 0xFFFFu;
-    const uint64_t cs = c->p0 + ch * kSpec;
-    const uint16_t *Pl = B.P + ch * c->lp;
-    pos = B.T[ch];
-    for (uint64_t q = 0; q <= r - B.base[ch]; ++q) {
-      if (q >= k0) pos = cs + Pl[j0 + (q - k0)];
-      pos += wlen<NS>(P, wire, a.wire_len, pos, c->w);
-    }
-  }
-  if (pos >= a.wire_len) return;
-  int32_t ec = SPK_ERRC_NO_BUFFER_SPACE;
-  rec_wire_len(a.L, wire, a.wire_len, pos, c->w, &ec);
-  if (ec == SPK_ERRC_INVALID_BUFFER) res->errc = ec;
-}
-
-// decode_record with piecewise copies; off[k] = heap element offset of span k
-__device__ __forceinline__ void emit_record(const KLayout &L, const uint8_t *wire, uint64_t pos,
-                                            uint32_t w, uint8_t *rec, uint8_t *const *heaps,
-                                            const uint64_t *off, uint64_t end) {
-  uint32_t sk = 0;
-  for (uint32_t o = 0; o < L.n_ops; ++o) {
-    const spk_op op = L.ops[o];
-    if (op.kind == SPK_OP_COPY) {
-      copy_bytes(rec + op.rec_off, wire + pos, op.size);
-      pos += op.size;
-    } else if (op.kind == SPK_OP_VARINT) {
-      uint64_t v = 0;
-      pos += vi_read(WireBytes{wire}, pos, end, &v);
-      vi_store(op, rec, v);
-    } else {
-      const uint64_t cnt = op.kind == SPK_OP_OPTION ? (uint64_t)(wire[pos] != 0) : wire_le(wire, pos, w);
-      pos += op_pw(op, w);
-      *reinterpret_cast<uint32_t *>(rec + op.rec_off) = (uint32_t)cnt;
-      *reinterpret_cast<uint64_t *>(rec + op.aux) = off[sk];
-      const uint64_t nb = opt_nb(op, cnt, pos, end);
-      uint8_t *hp = heaps[sk] + off[sk] * op.size;
-      if (cnt && !nb && op.kind == SPK_OP_OPTION)
-        for (uint32_t b = 0; b < op.size; ++b) hp[b] = 0;  // unreadable value
-      else
-        copy_bytes(hp, wire + pos, nb);
-      pos += nb;
-      ++sk;
-    }
-  }
-}
 
 __device__ __forceinline__ uint64_t wave_excl_scan_u64(uint64_t v, uint32_t lane, uint64_t *tot) {
   (void)lane;
@@ -2150,68 +1551,6 @@ __device__ __forceinline__ uint64_t wave_excl_scan_u64(uint64_t v, uint32_t lane
 // before it), then lanes take 64 consecutive records at a time, scan their
 // span counts across the wave for heap offsets (group base from the chunk
 // scan) and write the device records and heap bytes.
-constexpr uint32_t kEmitRecs = 4096;  // record slots per wave
-constexpr uint32_t kEmitWaves = 4;
-template <int NS>
-__global__ __launch_bounds__(64 * kEmitWaves) void vec_emit(DecArgs a, WalkProg P,
-                                                            const uint8_t *__restrict__ wire,
-                                                            const uint8_t *__restrict__ ws,
-                                                            VecBufs B, uint8_t *__restrict__ recs,
-                                                            const spk_dresult_t *res, uint32_t G) {
-  __shared__ uint16_t tab_s[kEmitWaves][kEmitRecs];
-  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
-  if (c->errc || res->errc) return;
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t nch = c->nchunks;
-  const uint64_t g0 = ((uint64_t)blockIdx.x * kEmitWaves + wv) * G;
-  if (g0 >= nch) return;  // wave-uniform
-  const uint64_t n = c->n, R0 = B.base[g0];
-  if (R0 >= n) return;
-  const uint64_t gend = g0 + G < nch ? g0 + G : nch;
-  uint64_t R1 = B.base[gend - 1] + B.cnt[gend - 1];
-  if (R1 > n) R1 = n;
-  const uint32_t w = c->w;
-  const uint64_t gs = c->p0 + g0 * kSpec;
-  uint16_t *tab = tab_s[wv];
-  if (lane < gend - g0) {
-    const uint64_t ch = g0 + lane, base = B.base[ch];
-    const uint32_t k = B.cnt[ch];
-    const uint64_t lim = R1 > base ? (R1 - base < k ? R1 - base : k) : 0;
-    const uint32_t mj = B.mj[ch], k0 = mj >> 16, j0 = mj & 0xFFFFu;
-    const uint16_t *Pl = B.P + ch * c->lp;
-    const uint16_t rel = (uint16_t)(ch - g0) * (uint16_t)kSpec;
-    uint16_t *dst = tab + (base - R0);
-    uint64_t pos = B.T[ch];
-    uint32_t r = 0;
-    for (; r < k0 && r < lim; ++r) {  // records before the meeting point
-      dst[r] = (uint16_t)(pos - gs);
-      pos += wlen<NS>(P, wire, a.wire_len, pos, w);
-    }
-    for (; r < lim; ++r) dst[r] = (uint16_t)(rel + Pl[j0 + (r - k0)]);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const uint32_t nsp = NS > 0 ? (uint32_t)NS : a.L.n_spans;
-  uint64_t carry[NS > 0 ? NS : SPK_MAX_SPANS];
-  for (uint32_t q = 0; q < nsp; ++q) carry[q] = B.hb[q * c->cap + g0];
-  const uint64_t nrec = R1 - R0;
-  for (uint64_t i0 = 0; i0 < nrec; i0 += 64) {
-    const uint64_t i = i0 + lane;
-    const bool act = i < nrec;
-    const uint64_t pos = gs + (act ? tab[i] : 0);
-    uint64_t rc[SPK_MAX_SPANS] = {};
-    if (act) wlen_rd<NS>(P, GReader{wire, w}, a.wire_len, pos, w, rc);
-    uint64_t off[SPK_MAX_SPANS];
-    for (uint32_t q = 0; q < nsp; ++q) {
-      uint64_t tot;
-      off[q] = carry[q] + wave_excl_scan_u64(act ? rc[q] : 0, lane, &tot);
-      carry[q] += tot;
-    }
-    if (act) emit_record(a.L, wire, pos, w, recs + (R0 + i) * a.L.stride, a.heaps, off, a.wire_len);
-  }
-}
-
 // ===========================================================================
 // DECODE, SPK_MODE_VECTOR — tiles: speculate, select, scan, emit
 // ===========================================================================
@@ -3317,146 +2656,6 @@ static unsigned grid_for(uint64_t items, uint64_t per_block) {
   return (unsigned)(b ? b : 1);
 }
 
-struct VecWs {
-  size_t P, Pn, E, En, flags, T, cnt, base, wl, exitp, used, dirty, mj, psum, hs, hb, scan, tot,
-      end;
-  uint64_t nch;
-  uint32_t lp;
-};
-
-// chunk counts past the device-side chunk total must read as zero; span sums
-// start at zero; re-verification stamps start as "never listed"
-__global__ __launch_bounds__(256) void vec_init(VecBufs B, uint64_t nch, uint32_t ns,
-                                                uint64_t *__restrict__ tot) {
-  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
-  const uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (uint64_t i = t0; i < nch; i += gs) {
-    B.cnt[i] = 0;
-    B.dirty[i] = 0xFFFFFFFFu;
-    B.dirty[nch + i] = 0xFFFFFFFFu;
-  }
-  for (uint64_t i = t0; i < (uint64_t)ns * nch; i += gs) B.hs[i] = 0;
-  if (t0 < 16) tot[t0] = 0;
-}
-
-static VecWs vec_ws_layout(const spk_layout *L, uint64_t wire_len, uint64_t rec_cap) {
-  VecWs v = {};
-  v.nch = wire_len / kSpec + 2;
-  uint32_t min_rec = 0, ns = 0;
-  for (uint32_t i = 0; i < L->n_ops; ++i) {
-    if (L->ops[i].kind == SPK_OP_COPY) min_rec += L->ops[i].size;
-    else if (L->ops[i].kind == SPK_OP_VARINT) ++min_rec;
-    else { ++min_rec; ++ns; }
-  }
-  if (!min_rec) min_rec = 1;
-  v.lp = kSpec / min_rec + 2;
-  size_t off = kWsScratch;
-  auto take = [&](size_t bytes) {
-    size_t o = off;
-    off += (bytes + 255) & ~size_t(255);
-    return o;
-  };
-  v.P = take(v.nch * v.lp * 2);
-  v.Pn = take(v.nch * 4);
-  v.E = take(v.nch * kExt * 4);
-  v.En = take(v.nch * 4);
-  v.flags = take(v.nch * 4);
-  v.T = take(v.nch * 8);
-  v.cnt = take(v.nch * 4);
-  v.base = take(v.nch * 8);
-  v.wl = take(2 * v.nch * 4);
-  v.exitp = take(v.nch * 8);
-  v.used = take(v.nch * 8);
-  v.dirty = take(2 * v.nch * 4);
-  v.mj = take(v.nch * 4);
-  v.psum = take((uint64_t)(ns ? ns : 1) * v.nch * 8);
-  v.hs = take((uint64_t)(ns ? ns : 1) * v.nch * 8);
-  v.hb = take((uint64_t)(ns ? ns : 1) * v.nch * 8);
-  (void)rec_cap;
-  const uint64_t nsb = v.nch / kScanBlock + 2;
-  v.scan = take(nsb * 8);
-  v.tot = take(16 * 8);
-  v.end = off;
-  return v;
-}
-
-static VecBufs vec_bufs(uint8_t *ws, const VecWs &v) {
-  VecBufs B;
-  B.P = reinterpret_cast<uint16_t *>(ws + v.P);
-  B.Pn = reinterpret_cast<uint32_t *>(ws + v.Pn);
-  B.E = reinterpret_cast<uint32_t *>(ws + v.E);
-  B.En = reinterpret_cast<uint32_t *>(ws + v.En);
-  B.flags = reinterpret_cast<uint32_t *>(ws + v.flags);
-  B.T = reinterpret_cast<uint64_t *>(ws + v.T);
-  B.cnt = reinterpret_cast<uint32_t *>(ws + v.cnt);
-  B.base = reinterpret_cast<uint64_t *>(ws + v.base);
-  B.wl = reinterpret_cast<uint32_t *>(ws + v.wl);
-  B.exitp = reinterpret_cast<uint64_t *>(ws + v.exitp);
-  B.used = reinterpret_cast<uint64_t *>(ws + v.used);
-  B.dirty = reinterpret_cast<uint32_t *>(ws + v.dirty);
-  B.mj = reinterpret_cast<uint32_t *>(ws + v.mj);
-  B.psum = reinterpret_cast<uint64_t *>(ws + v.psum);
-  B.hs = reinterpret_cast<uint64_t *>(ws + v.hs);
-  B.hb = reinterpret_cast<uint64_t *>(ws + v.hb);
-  B.scan = reinterpret_cast<uint64_t *>(ws + v.scan);
-  return B;
-}
-
-// exclusive scan in[0..n) -> out, total -> *tot (device)
-template <typename In>
-static void scan_dev(const In *in, uint64_t n, uint64_t *out, uint64_t *bsum, uint64_t *tot,
-                     hipStream_t s) {
-  const unsigned nb = grid_for(n ? n : 1, kScanBlock);
-  SPK_LAUNCH(scan_reduce<In>, dim3(nb), dim3(256), 0, s, in, n, bsum);
-  SPK_LAUNCH(scan_blocks, dim3(1), dim3(1024), 0, s, bsum, (uint64_t)nb, tot);
-  SPK_LAUNCH(scan_apply<In>, dim3(nb), dim3(256), 0, s, in, n, (const uint64_t *)bsum,
-                     out);
-}
-
-template <int NS>
-static hipError_t launch_vec_decode_ns(const DecArgs &a, const WalkProg &P, const uint8_t *wire,
-                                       uint8_t *ws, const VecWs &v, spk_dresult_t *d_res,
-                                       uint8_t *d_recs, hipStream_t s) {
-  VecBufs B = vec_bufs(ws, v);
-  hipError_t e;
-  const uint32_t ns = P.ns;
-  // one launch initialises cnt / hs / tot / dirty (four memsets cost ~20 us)
-  SPK_LAUNCH(vec_init, dim3(grid_for(v.nch, 256) < 4096 ? grid_for(v.nch, 256) : 4096),
-                     dim3(256), 0, s, B, v.nch, ns ? ns : 1u,
-                     reinterpret_cast<uint64_t *>(ws + v.tot));
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  uint64_t *tot = reinterpret_cast<uint64_t *>(ws + v.tot);
-  SPK_LAUNCH(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, v.lp, v.nch);
-  const unsigned cg = grid_for(v.nch, 256);
-  SPK_LAUNCH(vec_spec<NS>, dim3(grid_for(v.nch, (uint64_t)kSpecStep * kSpecWaves)),
-                     dim3(64 * kSpecWaves), 0, s, a, P, wire, ws, B);
-  for (uint32_t r = 1; r < P.rounds; ++r)
-    SPK_LAUNCH(vec_verify_round<NS>, dim3(256), dim3(256), 0, s, a, P, wire, ws, B, r);
-  SPK_LAUNCH(vec_fixup<NS>, dim3(1), dim3(1024), 0, s, a, P, wire, ws, B);
-  SPK_LAUNCH(vec_term_min, dim3(cg), dim3(256), 0, s, ws, B);
-  SPK_LAUNCH(vec_term_zero, dim3(cg), dim3(256), 0, s, ws, B, ns);
-  // chunk record counts -> record bases; chunk span-count sums -> heap bases
-  // (nchunks is device-side: the capacity is scanned, entries past it are 0)
-  scan_dev<uint32_t>(B.cnt, v.nch, B.base, B.scan, tot, s);
-  SPK_LAUNCH(vec_count_check, dim3(1), dim3(64), 0, s, ws, (const uint64_t *)tot, d_res);
-  for (uint32_t k = 0; k < ns; ++k)
-    scan_dev<uint64_t>(B.hs + (uint64_t)k * v.nch, v.nch, B.hb + (uint64_t)k * v.nch, B.scan,
-                       (uint64_t *)nullptr, s);
-  SPK_LAUNCH(vec_total<NS>, dim3(cg), dim3(256), 0, s, a, P, wire, ws, B, tot + 1);
-  SPK_LAUNCH(vec_finish, dim3(1), dim3(64), 0, s, a, ws, d_res,
-                     (const uint64_t *)(tot + 1));
-  if (P.nv)
-    SPK_LAUNCH(vec_vi_errc<NS>, dim3(1), dim3(64), 0, s, a, P, wire,
-                       (const uint8_t *)ws, B, d_res);
-  uint32_t G = kEmitRecs / v.lp;
-  if (G > 64) G = 64;
-  if (G < 1) G = 1;
-  const uint64_t groups = (v.nch + G - 1) / G;
-  SPK_LAUNCH(vec_emit<NS>, dim3(grid_for(groups, kEmitWaves)), dim3(64 * kEmitWaves), 0, s,
-                     a, P, wire, (const uint8_t *)ws, B, d_recs, (const spk_dresult_t *)d_res, G);
-  return hipGetLastError();
-}
-
 // ---- tile decoder: workspace and launch ---------------------------------------
 struct TileWs {
   size_t fn, cused, cex, ccnt, csum, sel, contrib, scan, blist, jobs, end;
@@ -3611,22 +2810,11 @@ hipError_t launch_var_shard(const spk_layout *L, int phase, const void *d_wire, 
   return launch_vec_tiles_ns<0>(a, P, L, wire, ws, d_res, r, s, ph, sc);
 }
 
-// SPK_VEC_DECODE=legacy selects the multi-pass decoder (A/B runs)
-static bool legacy_vec_decode() {
-  static const int v = [] {
-    const char *e = getenv("SPK_VEC_DECODE");
-    return (e && e[0] == 'l') ? 1 : 0;
-  }();
-  return v != 0;
-}
-
 size_t var_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len) {
   size_t enc = kWsScratch + (grid_for(n, kPlanRPB) + 1) * sizeof(Partial) + 256;
   size_t dec_msg = kWsScratch + n * sizeof(MsgState) +
                    (grid_for(n, kThreads) + 1) * kBs * 8 + 256;
-  size_t dec_vec = vec_ws_layout(L, wire_len, n).end + 256;
-  const size_t dec_tiles = tile_ws_layout(L, wire_len).end + 256;
-  if (dec_tiles > dec_vec) dec_vec = dec_tiles;
+  const size_t dec_vec = tile_ws_layout(L, wire_len).end + 256;
   size_t m = enc;
   if (mode == SPK_MODE_MESSAGES) m = m > dec_msg ? m : dec_msg;
   if (mode == SPK_MODE_VECTOR) m = m > dec_vec ? m : dec_vec;
@@ -3771,23 +2959,16 @@ hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
     return hipGetLastError();
   }
   // ---- VECTOR ----
-  const VecWs v = vec_ws_layout(L, wire_len, rec_cap);
   const WalkProg P = make_walkprog(L);
   (void)e;
   (void)ws_bytes;
   // NS = -1: the walkers read varints (kept out of the other instantiations:
   // the inlined LEB128 loops cost registers in the hot walks)
-  if (!legacy_vec_decode() || body_w) {
-    uint8_t *r = (uint8_t *)d_recs;
-    if (P.nv) return launch_vec_tiles_ns<-1>(a, P, L, wire, ws, d_res, r, s);
-    if (P.ns == 1) return launch_vec_tiles_ns<1>(a, P, L, wire, ws, d_res, r, s);
-    if (P.ns == 2) return launch_vec_tiles_ns<2>(a, P, L, wire, ws, d_res, r, s);
-    return launch_vec_tiles_ns<0>(a, P, L, wire, ws, d_res, r, s);
-  }
-  if (P.nv) return launch_vec_decode_ns<-1>(a, P, wire, ws, v, d_res, (uint8_t *)d_recs, s);
-  if (P.ns == 1) return launch_vec_decode_ns<1>(a, P, wire, ws, v, d_res, (uint8_t *)d_recs, s);
-  if (P.ns == 2) return launch_vec_decode_ns<2>(a, P, wire, ws, v, d_res, (uint8_t *)d_recs, s);
-  return launch_vec_decode_ns<0>(a, P, wire, ws, v, d_res, (uint8_t *)d_recs, s);
+  uint8_t *r = (uint8_t *)d_recs;
+  if (P.nv) return launch_vec_tiles_ns<-1>(a, P, L, wire, ws, d_res, r, s);
+  if (P.ns == 1) return launch_vec_tiles_ns<1>(a, P, L, wire, ws, d_res, r, s);
+  if (P.ns == 2) return launch_vec_tiles_ns<2>(a, P, L, wire, ws, d_res, r, s);
+  return launch_vec_tiles_ns<0>(a, P, L, wire, ws, d_res, r, s);
 }
 
 }  // namespace spk
