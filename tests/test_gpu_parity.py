@@ -658,3 +658,61 @@ def test_sharded_decode_long_records_boundaries():
     cds = [SP.Codec(LY.case_layout("recs")) for _ in range(6)]
     exp, _, _ = H.oracle_encode(cds[0].L, C.SPK_MODE_VECTOR, recs, heaps)
     _check_sharded(cds, exp, len(recs), 6)
+
+
+@pytest.mark.parametrize("case,param", [("tags", 6), ("vnt", 6), ("cmp", 8), ("deep", 3),
+                                        ("fv", 8), ("recs", 48), ("rec64", 0)])
+@pytest.mark.parametrize("modech", ["A", "B"])
+def test_encode_respects_out_cap(case, param, modech):
+    """An output buffer one byte (or half) too small: the encode either
+    returns SPK_E_CAPACITY (sizes known on the host) or writes nothing
+    (sizes known on the device; the plan tells the caller the size), and the
+    bytes past the buffer stay untouched. With the exact size the bytes are
+    the reference's (via the pinned oracle)."""
+    cd = codec_for(case)
+    n = 300
+    _, recs, heaps = synth.make_batch(case, n, 0x0CA9 + n, param)
+    mode = C.SPK_MODE_VECTOR if modech == "A" else C.SPK_MODE_MESSAGES
+    b = to_dev(cd, recs, heaps)
+    total = cd.get_needed_size(b, mode).total_bytes
+    exp, _, _ = H.oracle_encode(cd.L, mode, recs, heaps)
+    assert total == len(exp)
+    guard = 4096
+    for cap in (total - 1, total // 2, 1):
+        buf = torch.full((total + guard,), 0xA5, dtype=torch.uint8, device="cuda")
+        offs = torch.full((n + 1,), -7, dtype=torch.int64, device="cuda")
+        try:
+            cd.serialize_to(buf[:cap], b, mode, offs if mode == C.SPK_MODE_MESSAGES else None)
+        except RuntimeError as e:
+            assert str(C.SPK_E_CAPACITY) in str(e)
+        torch.cuda.synchronize()
+        assert bool((buf == 0xA5).all()), (cap, int((buf != 0xA5).sum()))
+        assert bool((offs == -7).all())
+    buf = torch.full((total + guard,), 0xA5, dtype=torch.uint8, device="cuda")
+    cd.serialize_to(buf[:total], b, mode, None)
+    assert buf[:total].cpu().numpy().tobytes() == exp
+    assert bool((buf[total:] == 0xA5).all())
+
+
+@pytest.mark.parametrize("case,param", [("tags", 6), ("vnt", 6), ("recs", 48)])
+def test_encode_body_respects_out_cap(case, param):
+    """spk_encode_body with a buffer one byte short writes nothing."""
+    from yalantinglibs_amd import parallel as PAR
+    cd = codec_for(case)
+    n = 200
+    _, recs, heaps = synth.make_batch(case, n, 0xB0DC, param)
+    b = to_dev(cd, recs, heaps)
+    w = 4
+    pl = cd.get_needed_size(b, C.SPK_MODE_VECTOR)
+    size = pl.var_bytes + PAR.count_fields(pl) * w
+    ws = cd.workspace(C.SPK_MODE_VECTOR, n)
+    buf = torch.full((size + 1024,), 0xA5, dtype=torch.uint8, device="cuda")
+    rc = cd.lib.spk_encode_body(cd.L.ptr, n, SP._p(b.recs), cd._heap_ptrs(b.heaps), w,
+                                SP._p(buf), size - 1, SP._p(ws), ws.numel(), None)
+    torch.cuda.synchronize()
+    assert rc in (0, C.SPK_E_CAPACITY)
+    assert bool((buf == 0xA5).all())
+    rc = cd.lib.spk_encode_body(cd.L.ptr, n, SP._p(b.recs), cd._heap_ptrs(b.heaps), w,
+                                SP._p(buf), size, SP._p(ws), ws.numel(), None)
+    torch.cuda.synchronize()
+    assert rc == 0 and bool((buf[size:] == 0xA5).all()) and not bool((buf[:size] == 0xA5).all())

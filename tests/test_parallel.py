@@ -169,6 +169,9 @@ class _OracleShardBackend:
         return PAR.ShardSummary(0, self.w, self.n, entry,
                                 PAR.ENTRY_UNKNOWN if ex is None else ex, k, [0] * ns)
 
+    def empty(self, first):
+        return (b"", [b""] * len(self.L.dev.spans)), C.spk_dresult_t()
+
     def emit(self, wire, lo, hi, first, last, count, summary):
         # decode records [first, first + count) from their body bytes with the oracle
         a, b = int(self.starts[first]), int(self.starts[first + count])
@@ -236,3 +239,70 @@ def test_sharded_vector_decode_gloo(case, n, param):
         assert p.exitcode == 0
     ok, rounds = q.get(timeout=10)
     assert ok and rounds >= 1
+
+
+class _ScriptedBackend:
+    """Backend whose ranges report scripted summaries and emit results: the
+    message's path ends inside range `end_rank` with records missing."""
+
+    def __init__(self, n, world, end_rank, errc, short):
+        self.n, self.world, self.end_rank, self.errc, self.short = n, world, end_rank, errc, short
+        self.emitted, self.emptied = [], []
+
+    def header(self, wire):
+        return 0, self.n, 4, 9
+
+    def wire_len(self, wire):
+        return 9 + self.world * PAR.TILE_BYTES
+
+    def index(self, wire, lo, hi, entry):
+        r = lo  # one tile per rank
+        per = self.n // self.world
+        if r < self.end_rank:
+            return PAR.ShardSummary(0, 4, self.n, 9 + r * 100, 9 + (r + 1) * 100, per, [per])
+        if r == self.end_rank:  # the path ends here, `short` records before n
+            return PAR.ShardSummary(0, 4, self.n, 9 + r * 100, PAR.ENTRY_UNKNOWN,
+                                    self.n - r * per - self.short, [1])
+        # past the end: a guessed path of records that are not the message's
+        return PAR.ShardSummary(0, 4, self.n, 9 + r * 100 + 3, 9 + (r + 1) * 100 + 3, 5, [5])
+
+    def empty(self, first):
+        self.emptied.append(first)
+        return "empty", C.spk_dresult_t()
+
+    def emit(self, wire, lo, hi, first, last, count, summary):
+        self.emitted.append((lo, first, count, last))
+        res = C.spk_dresult_t()
+        res.count = count
+        res.errc = self.errc if last else 0
+        return "batch", res
+
+
+@pytest.mark.parametrize("end_rank,errc", [(1, C.ERRC_NO_BUFFER_SPACE), (0, C.ERRC_INVALID_BUFFER),
+                                           (3, C.ERRC_NO_BUFFER_SPACE)])
+def test_sharded_decode_one_verdict_on_a_short_message(end_rank, errc):
+    """A truncated / corrupt message: the ranges after the one where the path
+    ends emit nothing (their guessed paths are not the message's), and every
+    rank returns the errc the range holding the shortfall found."""
+    world, n = 4, 400
+    be = _ScriptedBackend(n, world, end_rank, errc, short=7)
+    out, rounds = PAR.shard_decode([be] * world, None, world, lambda mine: mine)
+    assert [res.errc for _, _, res in out] == [errc] * world
+    assert all(e[0] <= end_rank for e in be.emitted)
+    assert [e[3] for e in be.emitted] == [False] * end_rank + [True]
+    assert len(be.emptied) == world - 1 - end_rank
+    firsts = [f for _, f, _ in out]
+    assert firsts == sorted(firsts)
+
+
+def test_sharded_decode_settles_or_raises():
+    """Entries that never settle are an error, not a silent mismatch."""
+    class Flaky(_ScriptedBackend):
+        def index(self, wire, lo, hi, entry):
+            s = super().index(wire, lo, hi, entry)
+            if lo == 2:  # always claims an entry its neighbour's exit is not
+                s.entry += 1
+            return s
+    be = Flaky(400, 4, 3, 0, 0)
+    with pytest.raises(RuntimeError):
+        PAR.shard_decode([be] * 4, None, 4, lambda mine: mine)

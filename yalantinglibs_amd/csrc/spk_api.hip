@@ -276,7 +276,7 @@ static int encode_impl(const spk_layout *L, int mode, uint64_t n, const void *d_
   if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
   if ((rc = heaps_check(L, n, d_heaps))) return rc;
   if (layout_nested(L))
-    return hip_rc(launch_nested_encode(L, mode, n, d_recs, d_heaps, d_out, d_msg_offsets, F, 0,
+    return hip_rc(launch_nested_encode(L, mode, n, d_recs, d_heaps, d_out, out_cap, d_msg_offsets, F, 0,
                                        d_ws, s, echo));
   return hip_rc(launch_var_encode(L, mode, n, d_recs, d_heaps, d_plan, d_out, out_cap,
                                   d_msg_offsets, F, d_ws, ws_bytes, s, echo));
@@ -404,7 +404,7 @@ int spk_encode_body(const spk_layout *L, uint64_t n, const void *d_recs,
   if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
   if ((rc = heaps_check(L, n, d_heaps))) return rc;
   if (layout_nested(L))
-    return hip_rc(launch_nested_encode(L, SPK_MODE_VECTOR, n, d_recs, d_heaps, d_out, nullptr,
+    return hip_rc(launch_nested_encode(L, SPK_MODE_VECTOR, n, d_recs, d_heaps, d_out, out_cap, nullptr,
                                        nullptr, width, d_ws, s));
   return hip_rc(launch_var_encode_body(L, n, d_recs, d_heaps, width, d_out, out_cap, d_ws,
                                        ws_bytes, s));

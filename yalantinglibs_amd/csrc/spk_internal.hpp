@@ -243,7 +243,7 @@ hipError_t launch_nested_plan(const spk_layout *L, int mode, uint64_t n, const v
                               const void *const *d_heaps, spk_plan_t *d_plan, void *d_ws,
                               hipStream_t s);
 hipError_t launch_nested_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
-                                const void *const *d_heaps, void *d_out,
+                                const void *const *d_heaps, void *d_out, uint64_t out_cap,
                                 uint64_t *d_msg_offsets, const spk_frame *F, uint32_t fixed_w,
                                 void *d_ws, hipStream_t s, const SeqEcho *echo = nullptr);
 hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wire,

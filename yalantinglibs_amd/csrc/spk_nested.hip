@@ -909,7 +909,7 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
                                                   const uint64_t *__restrict__ part, uint64_t nb,
                                                   uint8_t *ws, uint8_t *__restrict__ out,
                                                   uint64_t *__restrict__ msg_offsets,
-                                                  uint32_t with_header) {
+                                                  uint32_t with_header, uint64_t out_cap) {
   const NCtl *ctl = reinterpret_cast<const NCtl *>(ws + kWsCtl);
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e.mode == SPK_MODE_VECTOR) {
@@ -919,9 +919,13 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
     const uint64_t tot0 = e.n ? part[nb] : 0;
     uint64_t totc = 0;
     for (uint32_t rk = 0; rk < e.N.n_ranks; ++rk) totc += e.n ? part[(2 + rk) * (nb + 1) + nb] : 0;
-    if (with_header) {
-      uint8_t hb[4 + 1 + 8 + SPK_MAX_LITERAL + 1];
+    uint8_t hb[4 + 1 + 8 + SPK_MAX_LITERAL + 1];
+    if (with_header)
       hl = e.N.n_ranks ? compat_hdr(hb, e.fmt, w, w + tot0 + totc) : write_hdr(hb, e.fmt, w);
+    // the whole message must fit, or nothing is written (spk_encode's
+    // contract; the caller reads the plan's total_bytes)
+    if ((with_header ? hl + w : 0) + tot0 + totc > out_cap) return;
+    if (with_header) {
       if (i == 0) {
         for (uint32_t b = 0; b < hl; ++b) out[b] = hb[b];
         for (uint32_t b = 0; b < w; ++b) out[hl + b] = (uint8_t)(e.n >> (8 * b));
@@ -940,6 +944,7 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
     }
     return;
   }
+  if ((e.n ? part[nb] : 0) > out_cap) return;  // every message with its frame
   if (i == 0 && msg_offsets) msg_offsets[e.n] = e.n ? part[nb] : 0;
   if (i >= e.n) return;
   const uint8_t *rec = recs + i * e.N.stride;
@@ -1024,7 +1029,7 @@ hipError_t launch_nested_plan(const spk_layout *L, int mode, uint64_t n, const v
 }
 
 hipError_t launch_nested_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
-                                const void *const *d_heaps, void *d_out,
+                                const void *const *d_heaps, void *d_out, uint64_t out_cap,
                                 uint64_t *d_msg_offsets, const spk_frame *F, uint32_t fixed_w,
                                 void *d_ws, hipStream_t s, const SeqEcho *echo) {
   NEnc e = make_nenc(L, mode, n, d_heaps);
@@ -1043,7 +1048,7 @@ hipError_t launch_nested_encode(const spk_layout *L, int mode, uint64_t n, const
   if (er != hipSuccess) return er;
   SPK_LAUNCH(nest_write, dim3(nblocks(n, 256)), dim3(256), 0, s, e, (const uint8_t *)d_recs,
              (const uint64_t *)a, (const uint64_t *)part, nb, ws, (uint8_t *)d_out,
-             d_msg_offsets, fixed_w ? 0u : 1u);
+             d_msg_offsets, fixed_w ? 0u : 1u, out_cap);
   return hipGetLastError();
 }
 

@@ -286,6 +286,12 @@ class DeviceShardBackend:
     def index(self, wire, lo, hi, entry) -> ShardSummary:
         return self.cd.shard_index(wire, lo, hi, entry)
 
+    def empty(self, first):
+        """The batch and result of a rank that holds no records."""
+        cd = self.cd
+        out = cd.alloc_batch(1, [1] * len(cd.L.dev.spans))
+        return RecordBatch(cd.L, out.recs[:0], out.heaps), C.spk_dresult_t()
+
     def emit(self, wire, lo, hi, first, last, count, summary):
         cd = self.cd
         out = cd.alloc_batch(count + 1, [max(h, 1) for h in summary.heap[:len(cd.L.dev.spans)]])
@@ -297,7 +303,13 @@ def shard_decode(backends, wire, world: int, gather, rank: Optional[int] = None)
     """The protocol of ShardedVectorDecoder. `backends[r]` runs rank r's
     kernels (one entry when `rank` is given: this process is that rank);
     `gather(list_of_my_summaries) -> all ranks' summaries`. Returns
-    [(batch, first, result)] for the ranks this process runs."""
+    [(batch, first, result)] for the ranks this process runs.
+
+    Every rank returns the same verdict: after the emits the ranks exchange
+    their results, and the errc of the lowest rank that failed (the range
+    holding the message's shortfall reports no_buffer_space / invalid_buffer
+    like the reference, unpacker.hpp:1208-1226; a rank out of output capacity
+    SPK_ERRC_CAPACITY) is written into every rank's result."""
     mine_ranks = [rank] if rank is not None else list(range(world))
     be0 = backends[0]
     e, n, w, hl = be0.header(wire)
@@ -308,21 +320,36 @@ def shard_decode(backends, wire, world: int, gather, rank: Optional[int] = None)
     local = {r: backends[i].index(wire, rng[r][0], rng[r][1], ENTRY_UNKNOWN)
              for i, r in enumerate(mine_ranks)}
     rounds = 0
-    for _ in range(world):
+    settled = False
+    for _ in range(world + 1):
         sums = gather([local[r] for r in mine_ranks])
         redo = settle_entries(sums)
         if not any(x is not None for x in redo):
+            settled = True
             break
         rounds += 1
         for i, r in enumerate(mine_ranks):
             if redo[r] is not None:
                 local[r] = backends[i].index(wire, rng[r][0], rng[r][1], redo[r])
+    if not settled:  # k wrong ranges settle in <= k rounds (range 0 is exact)
+        raise RuntimeError(f"sharded decode: range entries did not settle in {world} rounds")
     plan = shard_plan(sums)
     out = []
     for i, r in enumerate(mine_ranks):
         first, k, last = plan[r]
-        b, res = backends[i].emit(wire, rng[r][0], rng[r][1], first, last, k, local[r])
+        if k == 0 and not last:
+            # a range past the message's end (or past the point where the path
+            # ends) holds none of its records: nothing to emit
+            b, res = backends[i].empty(first)
+        else:
+            b, res = backends[i].emit(wire, rng[r][0], rng[r][1], first, last, k, local[r])
         out.append((b, first, res))
+    # one verdict on every rank
+    verdicts = gather([ShardSummary(int(res.errc), int(res.width), n, 0, 0, int(res.count),
+                                    [0] * C.SPK_MAX_SPANS) for _, _, res in out])
+    errc = next((v.errc for v in verdicts if v.errc), 0)
+    for _, _, res in out:
+        res.errc = errc
     return out, rounds
 
 
