@@ -84,8 +84,8 @@
  *                                           (packer.hpp:389-398); decode: an
  *                                           index >= size is invalid_buffer
  *                                           (unpacker.hpp:1278-1292).
- *   SPK_OP_END {0, 0, 0, 0}                closes the innermost open ARRAY or
- *                                           VARIANT alternative.
+ *   SPK_OP_END {0, 0, 0, 0}                closes the innermost open ARRAY, VARIANT
+ *                                           alternative, OPTGROUP group or CGROUP.
  *   SPK_OP_FVAR {rec_off, size, aux}       a varint member of a top-level record
  *                                           whose sp_config has USE_FAST_VARINT
  *                                           (var_* types; with ENCODING_WITH_VARINT
@@ -134,6 +134,36 @@
  *                                           292-366,1354-1376). Requires
  *                                           SPK_MF_HASH_HEAD and a non-trivial
  *                                           layout (type_calculate.hpp:868-876).
+ *   SPK_OP_OPTGROUP {rec_off, size, 0}     a std::optional<U> (size 1) or
+ *                                           std::expected<U, E> (size 2) whose
+ *                                           value is NOT trivially serializable
+ *                                           (optional<string>, optional<struct
+ *                                           with a string> ...): the record holds
+ *                                           a u32 has_value at rec_off (0 / 1);
+ *                                           the ops that follow are `size`
+ *                                           groups closed by SPK_OP_END, placed
+ *                                           in the same record like VARIANT
+ *                                           alternatives: group 0 = U (present),
+ *                                           group 1 = E (expected without a
+ *                                           value). Wire: [has_value:1] then
+ *                                           U if present (packer.hpp:382-388),
+ *                                           else E for an expected (:400-410).
+ *                                           Decode: any non-zero byte is
+ *                                           present; the errc of the group's
+ *                                           decode is dropped and the reader
+ *                                           stays where it stopped
+ *                                           (unpacker.hpp:1251-1277). Not a
+ *                                           container; its value may hold some.
+ *   SPK_OP_CGROUP {rec_off, 1, 0}          a struct_pack::compatible<U, ver>
+ *                                           member of the top-level record with a
+ *                                           U that is NOT trivially serializable:
+ *                                           kind = SPK_OP_CGROUP | rank << 8 (as
+ *                                           COMPAT); a u32 has_value at rec_off,
+ *                                           then U's ops closed by SPK_OP_END,
+ *                                           in the same record. Written, read
+ *                                           and skipped like COMPAT ([has:1][U]
+ *                                           in its version pass), U's containers
+ *                                           at the message width.
  * Heaps are numbered in op order over SPAN, OPTION, ARRAY and COMPAT ops at every
  * nesting level; heap k of an ARRAY holds element records, counted in
  * elements like the others. Decode writes every heap packed in wire order.
@@ -167,9 +197,9 @@
 extern "C" {
 #endif
 
-#define SPK_ABI_VERSION 1u
+#define SPK_ABI_VERSION 2u
 #define SPK_MAX_OPS 64u
-#define SPK_MAX_SPANS 8u
+#define SPK_MAX_SPANS 16u  /* heaps (variable-length members) per layout */
 #define SPK_MAX_LITERAL 240u
 
 /* return codes (host-side; negative) */
@@ -201,6 +231,8 @@ extern "C" {
 #define SPK_OP_VARIANT 7u
 #define SPK_OP_COMPAT 8u       /* | rank << 8 (see above)                    */
 #define SPK_OP_FVAR 9u
+#define SPK_OP_OPTGROUP 10u
+#define SPK_OP_CGROUP 11u      /* | rank << 8                                */
 #define SPK_OP_KIND(k) ((k) & 0xFFu)
 #define SPK_OP_RANK(k) ((k) >> 8)
 #define SPK_MAX_DEPTH 4u       /* ARRAY / VARIANT nesting levels             */

@@ -11,9 +11,9 @@ from __future__ import annotations
 import ctypes as ct
 import os
 
-SPK_ABI_VERSION = 1
+SPK_ABI_VERSION = 2
 SPK_MAX_OPS = 64
-SPK_MAX_SPANS = 8
+SPK_MAX_SPANS = 16
 SPK_MAX_LITERAL = 240
 SPK_MAX_FRAME = 64
 SPK_MAX_ROUTES = 16
@@ -42,6 +42,8 @@ SPK_OP_END = 6
 SPK_OP_VARIANT = 7
 SPK_OP_COMPAT = 8  # | version rank << 8
 SPK_OP_FVAR = 9
+SPK_OP_OPTGROUP = 10
+SPK_OP_CGROUP = 11  # | version rank << 8
 SPK_FVAR_SIGNED = 1
 SPK_VARINT_SEXT = 2
 SPK_MAX_DEPTH = 4

@@ -73,7 +73,9 @@ static int hip_rc(hipError_t e) { return e == hipSuccess ? SPK_OK : SPK_E_HIP; }
 static bool is_trivial(const spk_layout *L) { return (L->flags & SPK_LAYOUT_TRIVIAL) != 0; }
 static bool has_compat(const spk_layout *L) {
   for (uint32_t i = 0; i < L->n_ops; ++i)
-    if (SPK_OP_KIND(L->ops[i].kind) == SPK_OP_COMPAT) return true;
+    if (SPK_OP_KIND(L->ops[i].kind) == SPK_OP_COMPAT ||
+        SPK_OP_KIND(L->ops[i].kind) == SPK_OP_CGROUP)
+      return true;
   return false;
 }
 static uint32_t heap_count(const spk_layout *L) {
@@ -121,9 +123,19 @@ int spk_layout_check(const spk_layout *L) {
     const spk_op &o = L->ops[i];
     const uint32_t rs = stride[depth];
     ++nops[depth];
-    if (o.kind == SPK_OP_VARIANT) {  // u32 index in this record; groups follow
-      if (o.size == 0 || o.size > 255 || o.aux || o.rec_off % 4 || o.rec_off + 4 > rs ||
-          depth == SPK_MAX_DEPTH)
+    const uint32_t kk = SPK_OP_KIND(o.kind);
+    if (kk == SPK_OP_VARIANT || kk == SPK_OP_OPTGROUP || kk == SPK_OP_CGROUP) {
+      // u32 index / has_value in this record; the groups follow in it:
+      // variant 1..255 alternatives, optional 1 group / expected 2, compatible
+      // 1 (top-level record only, with the hash head: type_calculate.hpp:
+      // 868-876)
+      const uint32_t maxg = kk == SPK_OP_VARIANT ? 255u : kk == SPK_OP_OPTGROUP ? 2u : 1u;
+      if (o.size == 0 || o.size > maxg || o.aux || o.rec_off % 4 || o.rec_off + 4 > rs ||
+          depth == SPK_MAX_DEPTH || (kk != SPK_OP_CGROUP && (o.kind >> 8)))
+        return SPK_E_LAYOUT;
+      if (kk == SPK_OP_CGROUP &&
+          (depth || (o.kind & ~0xFFFFu) || !(L->fmt_one.flags & SPK_MF_HASH_HEAD) ||
+           !(L->fmt_vector.flags & SPK_MF_HASH_HEAD)))
         return SPK_E_LAYOUT;
       ++vars;  // a variable-length member
       stride[++depth] = rs;

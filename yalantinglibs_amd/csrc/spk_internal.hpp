@@ -16,6 +16,10 @@ namespace spk {
 
 constexpr int kWave = 64;
 
+// Heaps the flat-record kernels (spk_var.hip) carry per record; layouts with
+// more run the op-list interpreter (spk_nested.hip).
+#define SPK_FLAT_SPANS 8u
+
 // Kernel-argument copy of the descriptor, without the literal tables (the
 // type literal lives in the device header buffer produced by the plan).
 struct KLayout {

@@ -36,27 +36,37 @@ struct NLayout {
   uint32_t fv_cnt, fv_has64, fv_bits;  // USE_FAST_VARINT group: FVAR ops, a 64-bit one, bitset bytes
 };
 
-// layouts the interpreter runs: an ARRAY (element layouts), a VARIANT or a
-// compatible member
+// layouts the interpreter runs: an ARRAY (element layouts), a VARIANT, an
+// OPTGROUP, a compatible member, a fast-varint group, or more heaps than the
+// flat-record kernels carry
 bool layout_nested(const spk_layout *L) {
+  uint32_t heaps = 0;
   for (uint32_t i = 0; i < L->n_ops; ++i) {
     const uint32_t k = SPK_OP_KIND(L->ops[i].kind);
-    if (k == SPK_OP_ARRAY || k == SPK_OP_VARIANT || k == SPK_OP_COMPAT || k == SPK_OP_FVAR)
+    if (k == SPK_OP_ARRAY || k == SPK_OP_VARIANT || k == SPK_OP_COMPAT || k == SPK_OP_FVAR ||
+        k == SPK_OP_OPTGROUP || k == SPK_OP_CGROUP)
       return true;
+    heaps += op_has_heap(k);
   }
-  return false;
+  return heaps > SPK_FLAT_SPANS;  // more heaps than the flat kernels carry
+}
+
+// VARIANT / OPTGROUP / CGROUP: groups placed in the same record, each closed
+// by an END (an ARRAY's element ops are one group too, in another record)
+__host__ __device__ __forceinline__ bool n_group(uint32_t k) {
+  return k == SPK_OP_VARIANT || k == SPK_OP_OPTGROUP || k == SPK_OP_CGROUP;
 }
 
 static NLayout make_nlayout(const spk_layout *L) {
   NLayout N = {};
   N.n_ops = L->n_ops;
   N.stride = L->rec_stride;
-  // open ARRAYs / VARIANTs and the alternatives a VARIANT still has to close
+  // open ARRAYs / groups and the groups each one still has to close
   uint32_t stack[SPK_MAX_DEPTH + 1], left[SPK_MAX_DEPTH + 1], d = 0, h = 0;
   for (uint32_t i = 0; i < L->n_ops; ++i) {
     N.ops[i] = L->ops[i];
     const uint32_t k = SPK_OP_KIND(L->ops[i].kind);
-    if (k == SPK_OP_COMPAT) {
+    if (k == SPK_OP_COMPAT || k == SPK_OP_CGROUP) {
       N.ops[i].kind = k;
       N.crank[i] = (uint8_t)SPK_OP_RANK(L->ops[i].kind);
       if (N.crank[i] + 1u > N.n_ranks) N.n_ranks = N.crank[i] + 1u;
@@ -66,9 +76,9 @@ static NLayout make_nlayout(const spk_layout *L) {
       ++N.fv_cnt;
       N.fv_has64 |= L->ops[i].size == 8;
     }
-    if (k == SPK_OP_ARRAY || k == SPK_OP_VARIANT) {
+    if (k == SPK_OP_ARRAY || n_group(k)) {
       stack[d] = i;
-      left[d++] = k == SPK_OP_VARIANT ? L->ops[i].size : 1;
+      left[d++] = k == SPK_OP_ARRAY ? 1 : L->ops[i].size;
     }
     if (k == SPK_OP_END && d && --left[d - 1] == 0) N.end[stack[--d]] = (uint8_t)i;
   }
@@ -106,21 +116,21 @@ __device__ __forceinline__ void n_copy(uint8_t *d, const uint8_t *s, uint64_t n)
   for (; i < n; ++i) d[i] = s[i];
 }
 
-// one open ARRAY on the interpreter's stack
+// one open ARRAY or group on the interpreter's stack
 struct NFrame {
-  uint32_t aop, pend;      // the ARRAY / VARIANT op; the op range end to resume
-  uint64_t j, cnt;         // element index, element count (a VARIANT: 0 of 1)
+  uint32_t aop, pend;      // the ARRAY / group op; the op range end to resume
+  uint64_t j, cnt;         // element index, element count (a group: 0 of 1)
   const uint8_t *el;       // element records (encode) / output slots (decode)
   const uint8_t *prec;     // record to resume
-  uint32_t first, ret;     // first op of an element / alternative; op to resume at
+  uint32_t first, ret;     // first op of an element / group; op to resume at
 };
 
-// first op of alternative `a` of the VARIANT at i (groups closed by END)
+// first op of group `a` of the VARIANT / OPTGROUP at i (groups closed by END)
 __device__ __forceinline__ uint32_t n_alt_start(const NLayout &N, uint32_t i, uint32_t a) {
   uint32_t j = i + 1;
   while (a) {
     const uint32_t k = N.ops[j].kind;
-    if (k == SPK_OP_ARRAY || k == SPK_OP_VARIANT) {
+    if (k == SPK_OP_ARRAY || n_group(k)) {
       j = N.end[j] + 1;  // skip a nested one whole
       continue;
     }
@@ -129,17 +139,25 @@ __device__ __forceinline__ uint32_t n_alt_start(const NLayout &N, uint32_t i, ui
   }
   return j;
 }
-// the END that closes the alternative starting at j
+// the END that closes the group starting at j
 __device__ __forceinline__ uint32_t n_alt_end(const NLayout &N, uint32_t j) {
   for (;;) {
     const uint32_t k = N.ops[j].kind;
-    if (k == SPK_OP_ARRAY || k == SPK_OP_VARIANT) {
+    if (k == SPK_OP_ARRAY || n_group(k)) {
       j = N.end[j] + 1;
       continue;
     }
     if (k == SPK_OP_END) return j;
     ++j;
   }
+}
+// the group a VARIANT / OPTGROUP / CGROUP at i writes for record r: the
+// variant's index; group 0 (the value) when has_value, else group 1 of an
+// expected (its error) or none (-1) (packer.hpp:382-410)
+__device__ __forceinline__ int n_active(const NLayout &N, uint32_t i, const uint8_t *r) {
+  const uint32_t v = *reinterpret_cast<const uint32_t *>(r + N.ops[i].rec_off);
+  if (N.ops[i].kind == SPK_OP_VARIANT) return (int)v;
+  return v ? 0 : (N.ops[i].size == 2 ? 1 : -1);
 }
 
 // ---- USE_FAST_VARINT group of the top-level record (packer.hpp:152-235,
@@ -252,16 +270,20 @@ __device__ int32_t n_fv_read(const NLayout &N, const uint8_t *wire, uint64_t &po
   return SPK_ERRC_OK;
 }
 
-// ---- encode: size of one record -----------------------------------------------
+// ---- encode: size of one record (or of an op range of it) ----------------------
 struct NSize {
   uint64_t bytes, cnts, maxc;  // payload bytes w/o counts, count fields, longest container
-  uint64_t cbytes;             // of which in the version passes (compatible members)
+  uint64_t cbytes, ccnts;      // of which in the version passes (compatible members)
 };
-__device__ NSize n_size(const NLayout &N, const uint8_t *rec, const uint8_t *const *heaps) {
-  NSize s = {0, 0, 0, 0};
-  s.bytes = n_fv_size(N, rec);
+// calculate_one_size (calculate_size.hpp:39-183) of ops [i0, i1) of `rec`;
+// `top`: the whole top-level record (its fast-varint group counts too)
+__device__ NSize n_size(const NLayout &N, const uint8_t *rec, const uint8_t *const *heaps,
+                        uint32_t i0, uint32_t i1, bool top) {
+  NSize s = {0, 0, 0, 0, 0};
+  if (top) s.bytes = n_fv_size(N, rec);
   NFrame st[SPK_MAX_DEPTH];
-  uint32_t d = 0, i = 0, iend = N.n_ops;
+  uint32_t d = 0, i = i0, iend = i1;
+  uint32_t cd = 0;  // depth of an open compatible group (its bytes are version-pass bytes)
   const uint8_t *r = rec;
   for (;;) {
     if (i >= iend) {
@@ -275,6 +297,7 @@ __device__ NSize n_size(const NLayout &N, const uint8_t *rec, const uint8_t *con
       i = f.ret;
       iend = f.pend;
       r = f.prec;
+      if (cd == d) cd = 0;
       --d;
       continue;
     }
@@ -283,32 +306,42 @@ __device__ NSize n_size(const NLayout &N, const uint8_t *rec, const uint8_t *con
       ++i;
     } else if (op.kind == SPK_OP_COPY) {
       s.bytes += op.size;
+      if (cd) s.cbytes += op.size;
       ++i;
     } else if (op.kind == SPK_OP_VARINT) {
-      s.bytes += n_vi_len(n_vi_value(op, r));
+      const uint32_t b = n_vi_len(n_vi_value(op, r));
+      s.bytes += b;
+      if (cd) s.cbytes += b;
       ++i;
-    } else {
-      const uint64_t c = *reinterpret_cast<const uint32_t *>(r + op.rec_off);
-      if (op.kind == SPK_OP_VARIANT) {  // [index:1] + the active alternative
-        s.bytes += 1;
-        const uint32_t a0 = n_alt_start(N, i, (uint32_t)c);
-        st[d] = NFrame{i, iend, 0, 1, r, r, a0, (uint32_t)N.end[i] + 1u};
-        ++d;
-        iend = n_alt_end(N, a0);
-        i = a0;
+    } else if (n_group(op.kind)) {  // [index / has_value:1] + the active group
+      s.bytes += 1;
+      if (cd || op.kind == SPK_OP_CGROUP) s.cbytes += 1;
+      const int a = n_active(N, i, r);
+      if (a < 0) {
+        i = N.end[i] + 1u;
         continue;
       }
+      const uint32_t a0 = n_alt_start(N, i, (uint32_t)a);
+      st[d] = NFrame{i, iend, 0, 1, r, r, a0, (uint32_t)N.end[i] + 1u};
+      ++d;
+      if (op.kind == SPK_OP_CGROUP) cd = d;
+      iend = n_alt_end(N, a0);
+      i = a0;
+    } else {
+      const uint64_t c = *reinterpret_cast<const uint32_t *>(r + op.rec_off);
       if (op.kind == SPK_OP_OPTION || op.kind == SPK_OP_COMPAT) {  // calculate_size.hpp:100-105
         const uint64_t b = 1 + (c ? op.size : 0);
         s.bytes += b;
-        if (op.kind == SPK_OP_COMPAT) s.cbytes += b;
+        if (cd || op.kind == SPK_OP_COMPAT) s.cbytes += b;
         ++i;
         continue;
       }
       s.cnts += 1;
+      if (cd) s.ccnts += 1;
       if (c > s.maxc) s.maxc = c;
       if (op.kind == SPK_OP_SPAN) {
         s.bytes += c * op.size;
+        if (cd) s.cbytes += c * op.size;
         ++i;
       } else if (!c) {
         i = N.end[i] + 1;
@@ -325,13 +358,13 @@ __device__ NSize n_size(const NLayout &N, const uint8_t *rec, const uint8_t *con
   return s;
 }
 
-// ---- encode: bytes of one record ----------------------------------------------
+// ---- encode: bytes of one record (or of an op range of it) ---------------------
 __device__ uint8_t *n_write(const NLayout &N, const uint8_t *rec, const uint8_t *const *heaps,
-                            uint32_t w, uint8_t *p) {
+                            uint32_t w, uint8_t *p, uint32_t i0, uint32_t i1, bool top) {
   NFrame st[SPK_MAX_DEPTH];
-  uint32_t d = 0, i = 0, iend = N.n_ops;
+  uint32_t d = 0, i = i0, iend = i1;
   const uint8_t *r = rec;
-  p = n_fv_write(N, rec, p);  // before the members (packer.hpp:432-440)
+  if (top) p = n_fv_write(N, rec, p);  // before the members (packer.hpp:432-440)
   for (;;) {
     if (i >= iend) {
       if (!d) break;
@@ -362,21 +395,27 @@ __device__ uint8_t *n_write(const NLayout &N, const uint8_t *rec, const uint8_t 
       }
       *p++ = (uint8_t)v;
       ++i;
+    } else if (op.kind == SPK_OP_COMPAT || op.kind == SPK_OP_CGROUP) {
+      // version UINT64_MAX: nothing (packer.hpp:246-249); written by the
+      // version pass of its version
+      i = op.kind == SPK_OP_CGROUP ? N.end[i] + 1u : i + 1u;
+    } else if (n_group(op.kind)) {
+      // variant: [index:1] (packer.hpp:389-398); optional / expected:
+      // [has_value:1] (:382-388, :400-410); then the active group
+      const uint32_t v = *reinterpret_cast<const uint32_t *>(r + op.rec_off);
+      *p++ = op.kind == SPK_OP_VARIANT ? (uint8_t)v : (uint8_t)(v ? 1 : 0);
+      const int a = n_active(N, i, r);
+      if (a < 0) {
+        i = N.end[i] + 1u;
+        continue;
+      }
+      const uint32_t a0 = n_alt_start(N, i, (uint32_t)a);
+      st[d] = NFrame{i, iend, 0, 1, r, r, a0, (uint32_t)N.end[i] + 1u};
+      ++d;
+      iend = n_alt_end(N, a0);
+      i = a0;
     } else {
       const uint64_t c = *reinterpret_cast<const uint32_t *>(r + op.rec_off);
-      if (op.kind == SPK_OP_VARIANT) {
-        *p++ = (uint8_t)c;
-        const uint32_t a0 = n_alt_start(N, i, (uint32_t)c);
-        st[d] = NFrame{i, iend, 0, 1, r, r, a0, (uint32_t)N.end[i] + 1u};
-        ++d;
-        iend = n_alt_end(N, a0);
-        i = a0;
-        continue;
-      }
-      if (op.kind == SPK_OP_COMPAT) {  // version UINT64_MAX: nothing (packer.hpp:246-249)
-        ++i;
-        continue;
-      }
       const uint64_t off = *reinterpret_cast<const uint64_t *>(r + op.aux);
       if (op.kind == SPK_OP_OPTION) {
         *p++ = c ? 1 : 0;
@@ -408,22 +447,38 @@ __device__ uint8_t *n_write(const NLayout &N, const uint8_t *rec, const uint8_t 
 }
 
 // ---- compatible members: the version pass of rank rk over one top-level record ----
-__device__ uint64_t n_compat_size(const NLayout &N, const uint8_t *rec, uint32_t rk) {
+// (COMPAT / CGROUP ops sit at the top level only: spk_layout_check)
+__device__ uint64_t n_compat_size(const NLayout &N, const uint8_t *rec,
+                                  const uint8_t *const *heaps, uint32_t rk, uint32_t w) {
   uint64_t b = 0;
-  for (uint32_t i = 0; i < N.n_ops; ++i)
-    if (N.ops[i].kind == SPK_OP_COMPAT && N.crank[i] == rk)
-      b += 1 + (*reinterpret_cast<const uint32_t *>(rec + N.ops[i].rec_off) ? N.ops[i].size : 0);
+  for (uint32_t i = 0; i < N.n_ops; ++i) {
+    if (N.crank[i] != rk) continue;
+    const uint32_t has = *reinterpret_cast<const uint32_t *>(rec + N.ops[i].rec_off);
+    if (N.ops[i].kind == SPK_OP_COMPAT) {
+      b += 1 + (has ? N.ops[i].size : 0);
+    } else if (N.ops[i].kind == SPK_OP_CGROUP) {
+      b += 1;
+      if (has) {
+        const NSize g = n_size(N, rec, heaps, i + 1, N.end[i], false);
+        b += g.bytes + g.cnts * w;
+      }
+    }
+  }
   return b;
 }
 // packer.hpp:453-461: [has_value:1][U if present] per member of that version
 __device__ uint8_t *n_write_compat(const NLayout &N, const uint8_t *rec,
-                                   const uint8_t *const *heaps, uint32_t rk, uint8_t *p) {
+                                   const uint8_t *const *heaps, uint32_t rk, uint32_t w,
+                                   uint8_t *p) {
   for (uint32_t i = 0; i < N.n_ops; ++i) {
     const spk_op op = N.ops[i];
-    if (op.kind != SPK_OP_COMPAT || N.crank[i] != rk) continue;
+    if ((op.kind != SPK_OP_COMPAT && op.kind != SPK_OP_CGROUP) || N.crank[i] != rk) continue;
     const uint32_t c = *reinterpret_cast<const uint32_t *>(rec + op.rec_off);
     *p++ = c ? 1 : 0;
-    if (c) {
+    if (!c) continue;
+    if (op.kind == SPK_OP_CGROUP) {
+      p = n_write(N, rec, heaps, w, p, i + 1, N.end[i], false);
+    } else {
       const uint64_t off = *reinterpret_cast<const uint64_t *>(rec + op.aux);
       n_copy(p, heaps[N.heap[i]] + off * op.size, op.size);
       p += op.size;
@@ -431,70 +486,40 @@ __device__ uint8_t *n_write_compat(const NLayout &N, const uint8_t *rec,
   }
   return p;
 }
-// unpacker.hpp:1354-1376 over one record: a member whose has byte would start
-// at or past data_end ends every version pass without an error (returns 1,
-// size_type_ = UCHAR_MAX, :360-365); a missing has byte before it is
-// no_buffer_space (*ec, returns 1); a value that does not fit reads as present
-// and zero (its errc is dropped). The main pass left every member absent.
-__device__ int n_read_compat(const NLayout &N, const uint8_t *wire, uint64_t &pos, uint64_t end,
-                             uint64_t data_end, uint32_t rk, uint8_t *rec, uint8_t *const *heaps,
-                             uint64_t *used, const uint64_t *heap_cap, uint32_t *ovf,
-                             int32_t *ec) {
-  for (uint32_t i = 0; i < N.n_ops; ++i) {
-    const spk_op op = N.ops[i];
-    if (op.kind != SPK_OP_COMPAT || N.crank[i] != rk) continue;
-    if (pos >= data_end) return 1;
-    if (pos >= end) {
-      *ec = SPK_ERRC_NO_BUFFER_SPACE;
-      return 1;
-    }
-    if (!wire[pos++]) continue;
-    const bool fits = end - pos >= op.size;
-    const uint32_t hk = N.heap[i];
-    const uint64_t off = used[hk];
-    if (rec) {
-      if (off >= heap_cap[hk]) {
-        *ovf = 1;
-      } else {
-        *reinterpret_cast<uint32_t *>(rec + op.rec_off) = 1;
-        *reinterpret_cast<uint64_t *>(rec + op.aux) = off;
-        if (fits)
-          n_copy(heaps[hk] + off * op.size, wire + pos, op.size);
-        else
-          for (uint32_t b = 0; b < op.size; ++b) heaps[hk][off * op.size + b] = 0;
-      }
-    }
-    used[hk] = off + 1;
-    if (fits) pos += op.size;
-  }
-  return 0;
-}
 
-// ---- decode: one record from the wire -------------------------------------------
+// ---- decode: one record (or an op range of it) from the wire ---------------------
+// A bounded walk (speculation from a guessed start, `end` short of the wire's
+// end) gives up with kNLimit wherever a read would need bytes past `end`: its
+// result is then unknown, never a different decode.
+constexpr int32_t kNLimit = 0x7FFF0001;
 // Parses wire[pos, end) and advances pos. used[k]: next element slot of heap
 // k (counted even when nothing is written). With `rec` set, writes the record,
 // its element records and heap payloads, skipping (and flagging in *ovf) what
-// does not fit heap_cap. Any non-zero OPTION byte is "has value"; a value that
-// does not fit leaves the reader in place and is zero-filled
-// (unpacker.hpp:1251-1275).
+// does not fit heap_cap. Any non-zero OPTION / OPTGROUP byte is "has value";
+// a value that does not fit leaves the reader in place (a trivially
+// serializable one zero-filled) (unpacker.hpp:1251-1277). `top`: the whole
+// top-level record, its fast-varint group first.
 __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, uint64_t end,
                           uint32_t w, uint8_t *rec, uint8_t *const *heaps, uint64_t *used,
-                          const uint64_t *heap_cap, uint32_t *ovf) {
+                          const uint64_t *heap_cap, uint32_t *ovf, uint32_t i0, uint32_t i1,
+                          bool top, bool bounded = false) {
   NFrame st[SPK_MAX_DEPTH];
-  uint32_t d = 0, i = 0, iend = N.n_ops;
+  uint32_t d = 0, i = i0, iend = i1;
   uint8_t *r = rec;
   int32_t ec = SPK_ERRC_OK;
-  if (N.fv_cnt && (ec = n_fv_read(N, wire, pos, end, rec))) return ec;
+  if (top && N.fv_cnt && (ec = n_fv_read(N, wire, pos, end, rec)))
+    return bounded && ec == SPK_ERRC_NO_BUFFER_SPACE ? kNLimit : ec;
   for (;;) {
     if (ec) {
-      // unwind to the innermost VARIANT: variant_construct_helper::run
-      // (unpacker.hpp:476-490) drops its alternative's errc; an ARRAY keeps
-      // its failing element (emplace_back, unpacker.hpp:1208-1226)
+      // unwind to the innermost variant / optional / expected group: their
+      // decode's errc is dropped (variant_construct_helper::run,
+      // unpacker.hpp:476-490; optional / expected, :1251-1277); an ARRAY
+      // keeps its failing element (emplace_back, unpacker.hpp:1208-1226)
       bool dropped = false;
       while (d) {
         NFrame &f = st[d - 1];
         const spk_op &fo = N.ops[f.aop];
-        if (fo.kind == SPK_OP_VARIANT) {
+        if (fo.kind == SPK_OP_VARIANT || fo.kind == SPK_OP_OPTGROUP) {
           i = f.ret;
           iend = f.pend;
           r = const_cast<uint8_t *>(f.prec);
@@ -531,7 +556,11 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
       continue;
     }
     if (op.kind == SPK_OP_COPY) {
-      if (end - pos < op.size) { ec = SPK_ERRC_NO_BUFFER_SPACE; continue; }
+      if (end - pos < op.size) {
+        if (bounded) return kNLimit;
+        ec = SPK_ERRC_NO_BUFFER_SPACE;
+        continue;
+      }
       if (r) n_copy(r + op.rec_off, wire + pos, op.size);
       pos += op.size;
       ++i;
@@ -542,6 +571,7 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
       int32_t vec = SPK_ERRC_INVALID_BUFFER;  // 10 bytes, all continued
       for (uint32_t k = 0; k < 10; ++k) {
         if (pos >= end) {
+          if (bounded) return kNLimit;
           vec = SPK_ERRC_NO_BUFFER_SPACE;  // (the bytes read stay consumed)
           break;
         }
@@ -566,16 +596,37 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
       ++i;
       continue;
     }
-    if (op.kind == SPK_OP_VARIANT) {  // unpacker.hpp:1278-1292
-      if (pos >= end) { ec = SPK_ERRC_NO_BUFFER_SPACE; continue; }
-      const uint32_t idx = wire[pos++];
-      if (idx >= op.size) { ec = SPK_ERRC_INVALID_BUFFER; continue; }
-      if (r) *reinterpret_cast<uint32_t *>(r + op.rec_off) = idx;
-      const uint32_t a0 = n_alt_start(N, i, idx);
+    if (op.kind == SPK_OP_VARIANT || op.kind == SPK_OP_OPTGROUP) {
+      // variant: unpacker.hpp:1278-1292; optional / expected: :1251-1277
+      if (pos >= end) {
+        if (bounded) return kNLimit;
+        ec = SPK_ERRC_NO_BUFFER_SPACE;
+        continue;
+      }
+      const uint32_t b = wire[pos++];
+      int a;
+      if (op.kind == SPK_OP_VARIANT) {
+        if (b >= op.size) { ec = SPK_ERRC_INVALID_BUFFER; continue; }
+        a = (int)b;
+        if (r) *reinterpret_cast<uint32_t *>(r + op.rec_off) = b;
+      } else {
+        a = b ? 0 : (op.size == 2 ? 1 : -1);
+        if (r) *reinterpret_cast<uint32_t *>(r + op.rec_off) = b ? 1u : 0u;
+      }
+      if (a < 0) {
+        i = N.end[i] + 1u;
+        continue;
+      }
+      const uint32_t a0 = n_alt_start(N, i, (uint32_t)a);
       st[d] = NFrame{i, iend, 0, 1, r, r, a0, (uint32_t)N.end[i] + 1};
       ++d;
       iend = n_alt_end(N, a0);
       i = a0;
+      continue;
+    }
+    if (op.kind == SPK_OP_CGROUP) {  // absent until its version pass
+      if (r) *reinterpret_cast<uint32_t *>(r + op.rec_off) = 0;
+      i = N.end[i] + 1u;
       continue;
     }
     const uint32_t hk = N.heap[i];
@@ -588,7 +639,11 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
       continue;
     }
     const uint32_t pw = op.kind == SPK_OP_OPTION ? 1u : w;
-    if (end - pos < pw) { ec = SPK_ERRC_NO_BUFFER_SPACE; continue; }
+    if (end - pos < pw) {
+      if (bounded) return kNLimit;
+      ec = SPK_ERRC_NO_BUFFER_SPACE;
+      continue;
+    }
     uint64_t cnt;
     if (op.kind == SPK_OP_OPTION) {
       cnt = wire[pos] != 0;
@@ -610,11 +665,15 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
       *reinterpret_cast<uint64_t *>(r + op.aux) = off;
     }
     if (op.kind == SPK_OP_ARRAY) {
+      // (an element takes at least one wire byte: a bounded walk gives up on
+      // a count the bytes left cannot hold)
+      if (bounded && cnt > end - pos) return kNLimit;
       used[hk] = off + cnt;
       if (!cnt) {
         i = N.end[i] + 1;
         continue;
       }
+      if (d == SPK_MAX_DEPTH) { ec = SPK_ERRC_INVALID_BUFFER; continue; }  // (layout_check bounds it)
       st[d] = NFrame{i, iend, 0, cnt, put ? heaps[hk] + off * op.size : nullptr, r, i + 1,
                      (uint32_t)N.end[i] + 1};
       r = put ? heaps[hk] + off * op.size : nullptr;
@@ -626,6 +685,7 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
     if (op.kind == SPK_OP_OPTION) {
       if (cnt) {
         const bool fits = end - pos >= op.size;
+        if (!fits && bounded) return kNLimit;
         if (put) {
           if (fits)
             n_copy(heaps[hk] + off * op.size, wire + pos, op.size);
@@ -640,9 +700,12 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
     }
     // SPAN (unpacker.hpp:1127-1156): the whole payload must be present
     if (cnt) {
-      if (op.size > 1 && cnt > ~0ull / op.size) { ec = SPK_ERRC_NO_BUFFER_SPACE; continue; }
+      if ((op.size > 1 && cnt > ~0ull / op.size) || end - pos < cnt * op.size) {
+        if (bounded) return kNLimit;
+        ec = SPK_ERRC_NO_BUFFER_SPACE;
+        continue;
+      }
       const uint64_t nb = cnt * op.size;
-      if (end - pos < nb) { ec = SPK_ERRC_NO_BUFFER_SPACE; continue; }
       if (put) n_copy(heaps[hk] + off * op.size, wire + pos, nb);
       pos += nb;
     }
@@ -654,6 +717,51 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
     ++i;
   }
   return SPK_ERRC_OK;
+}
+
+// unpacker.hpp:1354-1376 over one record: a member whose has byte would start
+// at or past data_end ends every version pass without an error (returns 1,
+// size_type_ = UCHAR_MAX, :360-365); a missing has byte before it is
+// no_buffer_space (*ec, returns 1); the value's errc is dropped (a trivially
+// serializable one that does not fit reads as present and zero; a group stops
+// where its decode stopped). The main pass left every member absent.
+__device__ int n_read_compat(const NLayout &N, const uint8_t *wire, uint64_t &pos, uint64_t end,
+                             uint64_t data_end, uint32_t rk, uint32_t w, uint8_t *rec,
+                             uint8_t *const *heaps, uint64_t *used, const uint64_t *heap_cap,
+                             uint32_t *ovf, int32_t *ec) {
+  for (uint32_t i = 0; i < N.n_ops; ++i) {
+    const spk_op op = N.ops[i];
+    if ((op.kind != SPK_OP_COMPAT && op.kind != SPK_OP_CGROUP) || N.crank[i] != rk) continue;
+    if (pos >= data_end) return 1;
+    if (pos >= end) {
+      *ec = SPK_ERRC_NO_BUFFER_SPACE;
+      return 1;
+    }
+    if (!wire[pos++]) continue;
+    if (op.kind == SPK_OP_CGROUP) {
+      if (rec) *reinterpret_cast<uint32_t *>(rec + op.rec_off) = 1;
+      (void)n_read(N, wire, pos, end, w, rec, heaps, used, heap_cap, ovf, i + 1, N.end[i], false);
+      continue;
+    }
+    const bool fits = end - pos >= op.size;
+    const uint32_t hk = N.heap[i];
+    const uint64_t off = used[hk];
+    if (rec) {
+      if (off >= heap_cap[hk]) {
+        *ovf = 1;
+      } else {
+        *reinterpret_cast<uint32_t *>(rec + op.rec_off) = 1;
+        *reinterpret_cast<uint64_t *>(rec + op.aux) = off;
+        if (fits)
+          n_copy(heaps[hk] + off * op.size, wire + pos, op.size);
+        else
+          for (uint32_t b = 0; b < op.size; ++b) heaps[hk][off * op.size + b] = 0;
+      }
+    }
+    used[hk] = off + 1;
+    if (fits) pos += op.size;
+  }
+  return 0;
 }
 
 // ---- device-wide exclusive scan of C u64 columns [C][n] (in place) ---------------
@@ -772,7 +880,8 @@ static NWs nws_layout(uint64_t n, uint32_t n_heaps, uint32_t n_ranks) {
     off += (bytes + 255) & ~size_t(255);
     return o;
   };
-  const uint32_t cols = n_heaps + 2;
+  // encode: 2 + n_ranks columns; decode: n_heaps
+  const uint32_t cols = (n_heaps > n_ranks ? n_heaps : n_ranks) + 2;
   f.a = take((n + 1) * 8 * cols);
   f.b = take((n + 1) * 8);
   f.part = take(nscan_part_bytes(n + 1, cols));
@@ -782,9 +891,55 @@ static NWs nws_layout(uint64_t n, uint32_t n_heaps, uint32_t n_ranks) {
   return f;
 }
 
-size_t nested_workspace_bytes(const spk_layout *L, int, uint64_t n, uint64_t) {
+// ---- chunked VECTOR decode (layouts without compatible members) -----------------
+// The body is cut into kNCh-byte chunks, one lane each. A record starts where
+// the previous one ends, so a chunk's first record start (its entry) is known
+// only from its predecessor; every lane therefore GUESSES its entry (the
+// first byte from which whole records parse up to the chunk's end, a bounded
+// walk) and walks its records from there. Records resynchronise, so a lane
+// that guessed wrong usually exits where the true path does. Rounds then
+// check every entry against the predecessor's exit and re-walk the chunks
+// that disagree from that exit (chunk 0's entry is exact), a one-wave fixer
+// settles what the rounds left, a scan over the chunks' record counts and heap
+// use gives every chunk its first record index and heap bases, and each lane
+// decodes its records into place.
+constexpr uint32_t kNCh = 1024;        // wire bytes per chunk
+constexpr uint32_t kNBound = 4096;     // a speculative walk's reach past its chunk
+constexpr int kNRounds = 4;            // parallel re-check rounds
+constexpr uint32_t kNT = 128;          // lanes per block of the chunk kernels
+constexpr uint64_t kNUnk = ~0ull - 1;  // entry / exit unknown (no plausible start; walk gave up)
+constexpr uint64_t kNFail = ~0ull;     // the path failed before this point
+
+struct CWs {
+  size_t ent, ext, err, cols, part, end;  // cols: [1 + heaps][nch] u64 (count, heap use)
+};
+static uint64_t cws_chunks(uint64_t wire_len) { return wire_len / kNCh + 2; }
+static CWs cws_layout(uint64_t wire_len, uint32_t n_heaps) {
+  CWs f = {};
+  size_t off = kWsScratch;
+  auto take = [&](size_t bytes) {
+    size_t o = off;
+    off += (bytes + 255) & ~size_t(255);
+    return o;
+  };
+  const uint64_t nch = cws_chunks(wire_len);
+  f.ent = take(nch * 8);
+  f.ext = take(nch * 8);
+  f.err = take(nch * 4);
+  f.cols = take(nch * 8 * (1 + n_heaps));
+  f.part = take(nscan_part_bytes(nch, 1 + n_heaps));
+  f.end = off;
+  return f;
+}
+
+size_t nested_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len) {
   const NLayout N = make_nlayout(L);
-  return nws_layout(n, N.n_heaps, N.n_ranks).end + 256;
+  size_t b = nws_layout(n, N.n_heaps, N.n_ranks).end;
+  if (mode == SPK_MODE_VECTOR && !N.n_ranks) {
+    const size_t c = cws_layout(wire_len, N.n_heaps).end;
+    if (c > b) b = c;
+  }
+  return b + 256;
 }
 
 // control block of the nested path (at kWsCtl)
@@ -794,8 +949,18 @@ struct NCtl {
   unsigned long long end;    // vector decode: position after the last record
   unsigned long long data_len;
   unsigned long long ovf;
-  uint32_t w, errc;
+  uint32_t w, errc;          // errc: the header's
+  // chunked vector decode
+  unsigned long long p0;                      // first record start
+  unsigned long long nch;                     // chunks
+  unsigned long long changed[kNRounds];       // round r moved an exit or left a chunk open
+  unsigned long long cmin, cmax, ndirty;      // chunks the rounds left open
+  unsigned long long rewalks, fixed;          // chunks re-walked by the rounds / the fixer
+  unsigned long long htot[SPK_MAX_SPANS];     // heap elements of records 0..n-1
+  int32_t werr;                               // the errc of the record the path fails at
+  uint32_t pad_;
 };
+static_assert(kWsCtl + sizeof(NCtl) <= kWsScratch, "NCtl overlaps the scratch area");
 
 // ---- encode kernels ------------------------------------------------------------------
 struct NEnc {
@@ -818,7 +983,7 @@ __global__ __launch_bounds__(256) void nest_size(NEnc e, const uint8_t *__restri
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t m = 0;
   if (i < e.n) {
-    const NSize s = n_size(e.N, recs + i * e.N.stride, e.heaps);
+    const NSize s = n_size(e.N, recs + i * e.N.stride, e.heaps, 0, e.N.n_ops, true);
     m = s.maxc;
     if (e.mode == SPK_MODE_MESSAGES) {
       const uint32_t w = width_of(s.maxc);
@@ -828,11 +993,10 @@ __global__ __launch_bounds__(256) void nest_size(NEnc e, const uint8_t *__restri
       a[i] = e.fpre + hl + body;
       a[e.n + i] = s.bytes;
     } else {
-      // main pass bytes; count fields; then one column per version pass
+      // main pass bytes and count fields (the version passes' columns
+      // need the width: nest_vec_sizes)
       a[i] = s.bytes - s.cbytes;
-      a[e.n + i] = s.cnts;
-      for (uint32_t rk = 0; rk < e.N.n_ranks; ++rk)
-        a[(2 + rk) * e.n + i] = n_compat_size(e.N, recs + i * e.N.stride, rk);
+      a[e.n + i] = s.cnts - s.ccnts;
     }
   }
   // block max -> one atomic per wave
@@ -854,14 +1018,19 @@ __global__ void nest_ctl_init(uint8_t *ws) {
   ctl->errc = 0;
 }
 
-// VECTOR: sizes[i] = bytes + cnts * w (in place over a[0]), w from maxc
-__global__ void nest_vec_sizes(NEnc e, uint64_t *__restrict__ a, uint8_t *ws) {
+// VECTOR: sizes[i] = bytes + cnts * w (in place over a[0]), w from maxc;
+// column 2 + rk: the bytes of record i in the version pass of rank rk
+__global__ void nest_vec_sizes(NEnc e, const uint8_t *__restrict__ recs,
+                               uint64_t *__restrict__ a, uint8_t *ws) {
   const NCtl *ctl = reinterpret_cast<const NCtl *>(ws + kWsCtl);
   const uint64_t mx = ctl->maxc > e.n ? ctl->maxc : e.n;
   const uint32_t w = e.fixed_w ? e.fixed_w : width_of(mx);
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < e.n;
-       i += (uint64_t)gridDim.x * blockDim.x)
+       i += (uint64_t)gridDim.x * blockDim.x) {
     a[i] = a[i] + a[e.n + i] * w;
+    for (uint32_t rk = 0; rk < e.N.n_ranks; ++rk)
+      a[(2 + rk) * e.n + i] = n_compat_size(e.N, recs + i * e.N.stride, e.heaps, rk, w);
+  }
 }
 
 // plan result from the column sums (part tables after the scan)
@@ -934,11 +1103,11 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
     }
     if (i < e.n) {
       const uint8_t *rec = recs + i * e.N.stride;
-      n_write(e.N, rec, e.heaps, w, out + hl + off[i]);
+      n_write(e.N, rec, e.heaps, w, out + hl + off[i], 0, e.N.n_ops, true);
       // version passes after every record's main pass (packer.hpp:66-78)
       uint64_t sec = hl + tot0;
       for (uint32_t rk = 0; rk < e.N.n_ranks; ++rk) {
-        n_write_compat(e.N, rec, e.heaps, rk, out + sec + off[(2 + rk) * e.n + i]);
+        n_write_compat(e.N, rec, e.heaps, rk, w, out + sec + off[(2 + rk) * e.n + i]);
         sec += part[(2 + rk) * (nb + 1) + nb];
       }
     }
@@ -948,7 +1117,7 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
   if (i == 0 && msg_offsets) msg_offsets[e.n] = e.n ? part[nb] : 0;
   if (i >= e.n) return;
   const uint8_t *rec = recs + i * e.N.stride;
-  const NSize s = n_size(e.N, rec, e.heaps);
+  const NSize s = n_size(e.N, rec, e.heaps, 0, e.N.n_ops, true);
   const uint32_t w = width_of(s.maxc);
   uint8_t *p = out + off[i];
   if (msg_offsets) msg_offsets[i] = off[i];
@@ -957,8 +1126,8 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
   const uint32_t hl = e.N.n_ranks ? compat_hdr(hb, e.fmt, w, s.bytes + s.cnts * w)
                                   : write_hdr(hb, e.fmt, w);
   for (uint32_t b = 0; b < hl; ++b) m[b] = hb[b];
-  uint8_t *q = n_write(e.N, rec, e.heaps, w, m + hl);
-  for (uint32_t rk = 0; rk < e.N.n_ranks; ++rk) q = n_write_compat(e.N, rec, e.heaps, rk, q);
+  uint8_t *q = n_write(e.N, rec, e.heaps, w, m + hl, 0, e.N.n_ops, true);
+  for (uint32_t rk = 0; rk < e.N.n_ranks; ++rk) q = n_write_compat(e.N, rec, e.heaps, rk, w, q);
   if (e.fpre) {
     for (uint32_t b = 0; b < e.fpre; ++b) p[b] = e.ftmpl[b];
     const uint32_t mlen = (uint32_t)(q - m);
@@ -1000,7 +1169,7 @@ static hipError_t nest_size_scan(const NEnc &e, const void *d_recs, uint8_t *ws,
                a, ws);
     if (e.mode == SPK_MODE_VECTOR)
       SPK_LAUNCH(nest_vec_sizes, dim3(nblocks(e.n, 256) < 4096 ? nblocks(e.n, 256) : 4096),
-                 dim3(256), 0, s, e, a, ws);
+                 dim3(256), 0, s, e, (const uint8_t *)d_recs, a, ws);
   }
   hipError_t er = hipGetLastError();
   if (er != hipSuccess) return er;
@@ -1064,47 +1233,20 @@ struct NDec {
   const uint64_t *ends;  // MESSAGES: message i ends at ends[i] (null: offs[i + 1])
 };
 
-// VECTOR boundary walk: one wave; lane 0 interprets the record counts while
-// the wave keeps a window of the wire in LDS (payload bytes are skipped).
-// Writes starts[i] (i < rec_cap) and the heap use U[k][i] of every record,
-// ctl->nrec / end / errc / w.
-constexpr uint32_t kNWin = 4096;
-__global__ __launch_bounds__(64) void nest_vec_walk(NDec a, const uint8_t *__restrict__ wire,
-                                                    uint8_t *ws, uint64_t *__restrict__ U,
-                                                    uint64_t *__restrict__ starts,
-                                                    uint64_t *__restrict__ cpos,
-                                                    spk_dresult_t *res) {
-  __shared__ uint8_t win[kNWin + 16];
-  __shared__ unsigned long long s_pos;
-  __shared__ int s_done;
+// VECTOR header (deserialize_metainfo, unpacker.hpp:548-619, + the count) or
+// the body of spk_decode_body; initialises the control block and *res
+__global__ void nest_vhdr(NDec a, const uint8_t *__restrict__ wire, uint8_t *ws,
+                          spk_dresult_t *res) {
   NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
-  const uint32_t lane = threadIdx.x;
   const uint64_t len = a.wire_len;
-  const NLayout &N = a.N;
-  // lane 0's interpreter state
-  uint64_t pos = 0, n = 0, rec = 0, used[SPK_MAX_SPANS] = {}, base[SPK_MAX_SPANS] = {};
-  uint32_t w = 1, i = 0, iend = N.n_ops, d = 0;
+  uint64_t pos = 0, n = 0, dl = 0;
+  uint32_t w = 1;
   int32_t errc = 0;
-  uint64_t data_len = 0;
-  // the version passes of compatible members (ph 1): rank rk, record crec, op ci
-  uint32_t ph = 0, rk = 0, ci = 0;
-  uint64_t crec = 0;
-  bool fvg = false;  // this record's fast-varint group is behind the walk
-  struct Fr {
-    uint32_t aop, pend;
-    uint64_t j, cnt;
-    uint32_t first, ret;
-  } st[SPK_MAX_DEPTH];
-  if (lane == 0 && a.body_w) {
+  if (a.body_w) {
     w = a.body_w;
     n = a.body_n;
-    s_pos = 0;
-    s_done = n == 0;
-    if (n && a.rec_cap) starts[0] = 0;
-  } else if (lane == 0) {
-    uint64_t p0;
-    errc = parse_hdr(a.fmt, wire, len, &p0, &w, &data_len);
-    pos = p0;
+  } else {
+    errc = parse_hdr(a.fmt, wire, len, &pos, &w, &dl);
     if (!errc) {
       if (len - pos < w) {
         errc = SPK_ERRC_NO_BUFFER_SPACE;
@@ -1113,281 +1255,302 @@ __global__ __launch_bounds__(64) void nest_vec_walk(NDec a, const uint8_t *__res
         pos += w;
       }
     }
-    s_pos = pos;
-    s_done = errc != 0 || n == 0;
-    if (!errc && n && a.rec_cap) starts[0] = pos;
   }
-  __syncthreads();
-  uint64_t wbase = ~0ull;
-  while (!s_done) {
-    // refill the window at the walk position
-    const uint64_t wp = s_pos;
-    if (wp != wbase) {
-      for (uint32_t b = lane * 16; b < kNWin; b += 64 * 16)
-        for (uint32_t q = 0; q < 16; ++q)
-          win[b + q] = wp + b + q < len ? wire[wp + b + q] : 0;
-      wbase = wp;
+  ctl->maxc = 0;
+  ctl->nrec = errc ? 0 : n;
+  ctl->end = pos;
+  ctl->data_len = dl;
+  ctl->ovf = 0;
+  ctl->w = w;
+  ctl->errc = (uint32_t)errc;
+  ctl->p0 = pos;
+  ctl->nch = (errc || !n || len <= pos) ? 0 : (len - pos + kNCh - 1) / kNCh;
+  for (int r = 0; r < kNRounds; ++r) ctl->changed[r] = 0;
+  ctl->cmin = ~0ull;
+  ctl->cmax = 0;
+  ctl->ndirty = 0;
+  ctl->rewalks = 0;
+  ctl->fixed = 0;
+  for (uint32_t k = 0; k < SPK_MAX_SPANS; ++k) ctl->htot[k] = 0;
+  ctl->werr = 0;
+  spk_dresult_t r = {};
+  r.errc = errc;
+  r.width = w;
+  *res = r;
+}
+
+struct CPtrs {
+  uint64_t *ent, *ext, *cols;  // cols[0][c]: records; cols[1 + k][c]: heap k use
+  int32_t *err;
+  uint64_t nch_cap;            // column stride = chunks the wire allows (the scan's length)
+};
+
+struct CWalk {
+  uint64_t ext, cnt;
+  int32_t err;
+};
+// the records of the path from s that start before c1; lim < wire_len makes
+// the walk speculative (kNUnk when a read would pass lim); hs += heap use
+__device__ CWalk nc_walk(const NDec &a, const uint8_t *__restrict__ wire, uint64_t s, uint64_t c1,
+                         uint64_t lim, uint32_t w, uint64_t *hs) {
+  CWalk r = {s, 0, 0};
+  if (s == kNFail || s == kNUnk) return r;
+  const bool bounded = lim < a.wire_len;
+  uint64_t pos = s;
+  uint32_t ovf = 0;
+  while (pos < c1) {
+    const uint64_t before = pos;
+    const int32_t ec = n_read(a.N, wire, pos, lim, w, nullptr, nullptr, hs, a.heap_cap, &ovf, 0,
+                              a.N.n_ops, true, bounded);
+    if (ec == kNLimit) {
+      r.ext = kNUnk;
+      return r;
     }
-    __syncthreads();
-    if (lane == 0) {
-      const uint64_t wend = wbase + kNWin < len ? wbase + kNWin : len;
-      auto byte = [&](uint64_t x) -> uint32_t { return win[x - wbase]; };
-      // an error inside a VARIANT alternative is dropped (the walk goes on
-      // after the variant, unpacker.hpp:476-490); an ARRAY keeps its failing
-      // element. Returns false when the error ends the message.
-      auto fail = [&](int32_t e) -> bool {
-        while (d) {
-          Fr &f = st[d - 1];
-          if (N.ops[f.aop].kind == SPK_OP_VARIANT) {
-            i = f.ret;
-            iend = f.pend;
-            --d;
-            return true;
-          }
-          used[N.heap[f.aop]] -= f.cnt - (f.j + 1);
-          --d;
-        }
-        errc = e;
-        return false;
-      };
-      bool stall = false, done = false;
-      while (!stall && !done) {
-        if (ph) {  // unpacker.hpp:292-366,1354-1376
-          if (rk >= N.n_ranks) {
-            done = true;
-            break;
-          }
-          if (crec >= n) {
-            ++rk;
-            crec = 0;
-            ci = 0;
-            continue;
-          }
-          if (ci == 0 && crec < a.rec_cap) cpos[(uint64_t)rk * a.rec_cap + crec] = pos;
-          while (ci < N.n_ops && !(N.ops[ci].kind == SPK_OP_COMPAT && N.crank[ci] == rk)) ++ci;
-          if (ci >= N.n_ops) {
-            ++crec;
-            ci = 0;
-            continue;
-          }
-          if (pos >= data_len) {  // an older writer: the legal end
-            done = true;
-            break;
-          }
-          if (wend < len && pos + 1 > wend) {
-            stall = true;
-            break;
-          }
-          if (pos >= len) {
-            errc = SPK_ERRC_NO_BUFFER_SPACE;
-            done = true;
-            break;
-          }
-          if (byte(pos++)) {
-            if (crec < a.rec_cap) U[(uint64_t)N.heap[ci] * a.rec_cap + crec] = 1;
-            if (len - pos >= N.ops[ci].size) pos += N.ops[ci].size;
-          }
-          ++ci;
-          continue;
-        }
-        if (i >= iend) {
-          if (d) {
-            Fr &f = st[d - 1];
-            if (++f.j < f.cnt) {
-              i = f.first;
-              continue;
-            }
-            i = f.ret;
-            iend = f.pend;
-            --d;
-            continue;
-          }
-          // record `rec` complete
-          if (rec < a.rec_cap)
-            for (uint32_t k = 0; k < N.n_heaps; ++k) U[(uint64_t)k * a.rec_cap + rec] = used[k] - base[k];
-          for (uint32_t k = 0; k < N.n_heaps; ++k) base[k] = used[k];
-          ++rec;
-          if (rec == n) {
-            if (N.n_ranks) {
-              ph = 1;
-              continue;
-            }
-            done = true;
-            break;
-          }
-          if (rec < a.rec_cap) starts[rec] = pos;
-          i = 0;
-          iend = N.n_ops;
-          fvg = false;
-          continue;
-        }
-        if (N.fv_cnt && !fvg) {  // the record's USE_FAST_VARINT group comes first
-          if (wend < len && pos + N.fv_bits > wend) {
-            stall = true;
-            break;
-          }
-          int32_t ge = SPK_ERRC_OK;
-          uint64_t g = 0;
-          if (len - pos < N.fv_bits) {
-            ge = SPK_ERRC_NO_BUFFER_SPACE;
-          } else {
-            uint8_t bs[(SPK_MAX_VARINTS + 2 + 7) / 8];
-            for (uint32_t b = 0; b < N.fv_bits; ++b) bs[b] = (uint8_t)byte(pos + b);
-            g = n_fv_len(N, bs);
-            ge = !g ? SPK_ERRC_INVALID_BUFFER : len - pos < g ? SPK_ERRC_NO_BUFFER_SPACE : 0;
-          }
-          if (ge) {
-            if (!fail(ge)) {
-              done = true;
-              break;
-            }
-            continue;
-          }
-          pos += g;
-          fvg = true;
-          continue;
-        }
-        const spk_op op = N.ops[i];
-        if (op.kind == SPK_OP_FVAR) {  // in the group
-          ++i;
-          continue;
-        }
-        if (op.kind == SPK_OP_COMPAT) {  // main pass: nothing on the wire
-          ++i;
-          continue;
-        }
-        if (op.kind == SPK_OP_COPY) {
-          if (len - pos < op.size) {
-            if (!fail(SPK_ERRC_NO_BUFFER_SPACE)) {
-              done = true;
-              break;
-            }
-            continue;
-          }
-          pos += op.size;  // skipped, not read
-          ++i;
-          continue;
-        }
-        // every other op reads at most 10 bytes: refill when the window (not
-        // the wire) ends before them
-        const uint64_t need = op.kind == SPK_OP_VARINT ? 10
-                              : (op.kind == SPK_OP_OPTION || op.kind == SPK_OP_VARIANT) ? 1
-                                                                                          : w;
-        if (wend < len && pos + need > wend) {
-          stall = true;
-          break;
-        }
-        if (op.kind == SPK_OP_VARINT) {
-          int32_t vec = SPK_ERRC_INVALID_BUFFER;
-          for (uint32_t k = 0; k < 10; ++k) {
-            if (pos >= len) {
-              vec = SPK_ERRC_NO_BUFFER_SPACE;
-              break;
-            }
-            if (!(byte(pos++) & 0x80u)) {
-              vec = SPK_ERRC_OK;
-              break;
-            }
-          }
-          if (vec) {
-            if (!fail(vec)) {
-              done = true;
-              break;
-            }
-            continue;
-          }
-          ++i;
-          continue;
-        }
-        if (op.kind == SPK_OP_VARIANT) {
-          if (pos >= len) {
-            if (!fail(SPK_ERRC_NO_BUFFER_SPACE)) {
-              done = true;
-              break;
-            }
-            continue;
-          }
-          const uint32_t idx = byte(pos++);
-          if (idx >= op.size || d == SPK_MAX_DEPTH) {
-            if (!fail(SPK_ERRC_INVALID_BUFFER)) {
-              done = true;
-              break;
-            }
-            continue;
-          }
-          const uint32_t a0 = n_alt_start(N, i, idx);
-          st[d++] = Fr{i, iend, 0, 1, a0, (uint32_t)N.end[i] + 1};
-          iend = n_alt_end(N, a0);
-          i = a0;
-          continue;
-        }
-        const uint32_t hk = N.heap[i];
-        const uint32_t pw = op.kind == SPK_OP_OPTION ? 1u : w;
-        if (len - pos < pw) {
-          if (!fail(SPK_ERRC_NO_BUFFER_SPACE)) {
-            done = true;
-            break;
-          }
-          continue;
-        }
-        uint64_t cnt = 0;
-        if (op.kind == SPK_OP_OPTION)
-          cnt = byte(pos) != 0;
-        else
-          for (uint32_t b = 0; b < w; ++b) cnt |= (uint64_t)byte(pos + b) << (8 * b);
-        pos += pw;
-        if (op.kind != SPK_OP_SPAN) used[hk] += cnt;
-        if (op.kind == SPK_OP_ARRAY) {
-          if (!cnt) {
-            i = N.end[i] + 1;
-            continue;
-          }
-          if (d == SPK_MAX_DEPTH) {  // (layout_check bounds the depth)
-            if (!fail(SPK_ERRC_INVALID_BUFFER)) {
-              done = true;
-              break;
-            }
-            continue;
-          }
-          st[d++] = Fr{i, iend, 0, cnt, i + 1, (uint32_t)N.end[i] + 1};
-          iend = N.end[i];
-          ++i;
-          continue;
-        }
-        if (op.kind == SPK_OP_OPTION) {
-          if (cnt && len - pos >= op.size) pos += op.size;  // else: unreadable, reader stays
-          ++i;
-          continue;
-        }
-        if (cnt) {
-          if ((op.size > 1 && cnt > ~0ull / op.size) || len - pos < cnt * op.size) {
-            if (!fail(SPK_ERRC_NO_BUFFER_SPACE)) {
-              done = true;
-              break;
-            }
-            continue;
-          }
-          pos += cnt * op.size;
-        }
-        used[hk] += cnt;
-        ++i;
+    if (ec) {
+      r.ext = kNFail;
+      r.err = ec;
+      return r;
+    }
+    if (pos == before) {  // (a record takes at least one byte: layout_check)
+      r.ext = kNFail;
+      r.err = SPK_ERRC_INTERNAL;
+      return r;
+    }
+    ++r.cnt;
+  }
+  r.ext = pos;
+  return r;
+}
+
+__device__ __forceinline__ void nc_store(const CPtrs &P, uint32_t H, uint64_t c, uint64_t ent,
+                                         const CWalk &r, const uint64_t *hs) {
+  P.ent[c] = ent;
+  P.ext[c] = r.ext;
+  P.err[c] = r.err;
+  P.cols[c] = r.cnt;
+  for (uint32_t k = 0; k < H; ++k) P.cols[(uint64_t)(1 + k) * P.nch_cap + c] = hs[k];
+}
+
+// speculation: chunk c's entry guessed (chunk 0's is exact) and its records walked
+__global__ __launch_bounds__(kNT) void nest_cspec(NDec a, const uint8_t *__restrict__ wire,
+                                                  const uint8_t *ws, CPtrs P) {
+  const NCtl *ctl = reinterpret_cast<const NCtl *>(ws + kWsCtl);
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t w = ctl->w, H = a.N.n_heaps;
+  uint64_t hs[SPK_MAX_SPANS];
+  for (uint32_t k = 0; k < H; ++k) hs[k] = 0;
+  if (c >= ctl->nch) {  // past the header's chunks: nothing in the scanned columns
+    if (c < P.nch_cap) nc_store(P, H, c, kNFail, CWalk{kNFail, 0, 0}, hs);
+    return;
+  }
+  const uint64_t len = a.wire_len, c0 = ctl->p0 + c * kNCh;
+  const uint64_t c1 = c0 + kNCh < len ? c0 + kNCh : len;
+  uint64_t ent = kNUnk;
+  CWalk r = {kNUnk, 0, 0};
+  if (c == 0) {
+    ent = c0;
+    r = nc_walk(a, wire, c0, c1, len, w, hs);
+  } else {
+    const uint64_t lim = c1 + kNBound < len ? c1 + kNBound : len;
+    for (uint64_t q = c0; q < c1; ++q) {
+      for (uint32_t k = 0; k < H; ++k) hs[k] = 0;
+      r = nc_walk(a, wire, q, c1, lim, w, hs);
+      if (r.ext != kNUnk && r.ext != kNFail) {  // whole records up to the chunk's end
+        ent = q;
+        break;
       }
-      s_pos = pos;
-      s_done = done;
     }
-    __syncthreads();
+    if (ent == kNUnk) {
+      r = CWalk{kNUnk, 0, 0};
+      for (uint32_t k = 0; k < H; ++k) hs[k] = 0;
+    }
   }
-  if (lane == 0) {
-    ctl->errc = (uint32_t)errc;
-    ctl->w = w;
-    ctl->nrec = errc ? 0 : n;
-    ctl->end = pos;
-    ctl->data_len = data_len;
-    spk_dresult_t r = {};
-    r.errc = errc;
-    r.width = w;
-    *res = r;
+  nc_store(P, H, c, ent, r, hs);
+}
+
+// round `round`: a chunk whose entry is not its predecessor's exit (or whose
+// walk gave up) is walked again from that exit
+__global__ __launch_bounds__(kNT) void nest_cround(NDec a, const uint8_t *__restrict__ wire,
+                                                   uint8_t *ws, CPtrs P, int round) {
+  NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
+  if (round > 0 && !ctl->changed[round - 1]) return;  // settled
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 || c >= ctl->nch) return;
+  const uint64_t E = __atomic_load_n(&P.ext[c - 1], __ATOMIC_RELAXED);
+  const uint64_t ent = P.ent[c], ext = P.ext[c];
+  if (E == ent && ext != kNUnk) return;
+  if (E == kNUnk) {  // the predecessor is open itself
+    atomicAdd(&ctl->changed[round], 1ull);
+    return;
   }
+  const uint64_t len = a.wire_len, c0 = ctl->p0 + c * kNCh;
+  const uint64_t c1 = c0 + kNCh < len ? c0 + kNCh : len;
+  const uint32_t H = a.N.n_heaps;
+  uint64_t hs[SPK_MAX_SPANS];
+  for (uint32_t k = 0; k < H; ++k) hs[k] = 0;
+  const CWalk r = nc_walk(a, wire, E, c1, len, ctl->w, hs);
+  nc_store(P, H, c, E, r, hs);
+  atomicAdd(&ctl->rewalks, 1ull);
+  if (r.ext != ext) atomicAdd(&ctl->changed[round], 1ull);
+}
+
+// after the rounds: the chunks still open (only when the last round moved something)
+__global__ __launch_bounds__(kNT) void nest_cverify(uint8_t *ws, CPtrs P) {
+  NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
+  if (!ctl->changed[kNRounds - 1]) return;
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 || c >= ctl->nch) return;
+  if (P.ext[c - 1] != P.ent[c] || P.ext[c] == kNUnk) {
+    atomicMin(&ctl->cmin, (unsigned long long)c);
+    atomicMax(&ctl->cmax, (unsigned long long)c);
+    atomicAdd(&ctl->ndirty, 1ull);
+  }
+}
+
+// one wave settles the open chunks in order: 64 chunks checked per step, the
+// first disagreeing one walked again from its predecessor's exit (carried in a
+// register, so the wave never re-reads what it wrote)
+__global__ __launch_bounds__(64) void nest_cfix(NDec a, const uint8_t *__restrict__ wire,
+                                                uint8_t *ws, CPtrs P) {
+  NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
+  if (!ctl->ndirty) return;
+  const uint32_t lane = threadIdx.x;
+  const uint64_t nch = ctl->nch, cmax = ctl->cmax, len = a.wire_len;
+  const uint32_t H = a.N.n_heaps;
+  uint64_t c = ctl->cmin;        // >= 1: chunk 0 is never open
+  uint64_t pext = P.ext[c - 1];  // exit of chunk c - 1 (settled)
+  uint64_t nfix = 0;
+  while (c < nch) {
+    const uint64_t cc = c + lane;
+    const bool valid = cc < nch;
+    const uint64_t my_ent = valid ? P.ent[cc] : 0, my_ext = valid ? P.ext[cc] : 0;
+    uint64_t prev = __shfl_up(my_ext, 1);  // lane l - 1's exit
+    if (lane == 0) prev = pext;
+    const bool bad = valid && (prev != my_ent || my_ext == kNUnk);
+    const uint64_t m = __ballot(bad);
+    if (!m) {
+      if (c + 64 > cmax) break;  // every chunk past cmax agreed, and still does
+      pext = __shfl(my_ext, 63);
+      c += 64;
+      continue;
+    }
+    const uint32_t l = (uint32_t)__ffsll((unsigned long long)m) - 1;
+    const uint64_t f = c + l;
+    const uint64_t E = __shfl(prev, (int)l), ext_old = __shfl(my_ext, (int)l);
+    uint64_t nx = 0;
+    if (lane == 0) {
+      const uint64_t c0 = ctl->p0 + f * kNCh;
+      const uint64_t c1 = c0 + kNCh < len ? c0 + kNCh : len;
+      uint64_t hs[SPK_MAX_SPANS];
+      for (uint32_t k = 0; k < H; ++k) hs[k] = 0;
+      // (E is settled: never kNUnk; guarded anyway)
+      const CWalk r = E == kNUnk ? CWalk{kNFail, 0, SPK_ERRC_INTERNAL}
+                                 : nc_walk(a, wire, E, c1, len, ctl->w, hs);
+      nc_store(P, H, f, E == kNUnk ? kNFail : E, r, hs);
+      nx = r.ext;
+    }
+    nx = __shfl(nx, 0);
+    ++nfix;
+    pext = nx;
+    c = f + 1;
+    if (nx == ext_old && c > cmax) break;  // nothing past cmax disagreed, nor does now
+  }
+  if (lane == 0) ctl->fixed = nfix;
+}
+
+// each chunk's records into place: record index and heap bases from the
+// scanned columns; the record the path fails at sets the errc
+__global__ __launch_bounds__(kNT) void nest_cemit(NDec a, const uint8_t *__restrict__ wire,
+                                                  uint8_t *ws, CPtrs P, uint8_t *__restrict__ recs) {
+  NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ctl->nch) return;
+  const uint64_t n = ctl->nrec, first = P.cols[c];
+  const uint64_t s = P.ent[c];
+  if (first >= n || s == kNFail || s == kNUnk) return;
+  const uint64_t len = a.wire_len, c0 = ctl->p0 + c * kNCh;
+  const uint64_t c1 = c0 + kNCh < len ? c0 + kNCh : len;
+  const uint32_t H = a.N.n_heaps, w = ctl->w;
+  uint64_t used[SPK_MAX_SPANS];
+  for (uint32_t k = 0; k < H; ++k) used[k] = P.cols[(uint64_t)(1 + k) * P.nch_cap + c];
+  uint32_t ovf = 0;
+  uint64_t pos = s;
+  for (uint64_t idx = first; pos < c1 && idx < n; ++idx) {
+    uint8_t *rec = idx < a.rec_cap ? recs + idx * a.N.stride : nullptr;
+    const int32_t ec = n_read(a.N, wire, pos, len, w, rec, a.heaps, used, a.heap_cap, &ovf, 0,
+                              a.N.n_ops, true);
+    if (ec) {
+      ctl->werr = ec;  // the one record of the path that fails before n
+      break;
+    }
+    if (idx == n - 1) {
+      ctl->end = pos;
+      for (uint32_t k = 0; k < H; ++k) ctl->htot[k] = used[k];
+    }
+  }
+  if (ovf) atomicAdd(&ctl->ovf, 1ull);
+}
+
+// result of the chunked decode: count, consume_len, heap use, capacity
+__global__ void nest_cfinish(NDec a, const uint64_t *__restrict__ part, uint64_t nb,
+                             const uint8_t *ws, spk_dresult_t *res) {
+  const NCtl *ctl = reinterpret_cast<const NCtl *>(ws + kWsCtl);
+  if (ctl->errc) return;  // the header errc is already in *res
+  spk_dresult_t r = *res;
+  const uint64_t n = ctl->nrec;
+  const uint64_t total = ctl->nch ? part[nb] : 0;  // records on the path (column 0)
+  r.tiles_repaired = (uint32_t)(ctl->rewalks < 0xFFFFFFFFull ? ctl->rewalks : 0xFFFFFFFFull);
+  r.tiles_sequential = (uint32_t)(ctl->fixed < 0xFFFFFFFFull ? ctl->fixed : 0xFFFFFFFFull);
+  if (ctl->werr || total < n) {
+    r.errc = ctl->werr ? ctl->werr : SPK_ERRC_NO_BUFFER_SPACE;
+  } else {
+    r.count = n;
+    r.consumed = ctl->end;
+    for (uint32_t k = 0; k < a.N.n_heaps; ++k) {
+      r.heap_used[k] = ctl->htot[k];
+      if (r.heap_used[k] > a.heap_cap[k]) r.errc = SPK_ERRC_CAPACITY;
+    }
+    if (n > a.rec_cap || ctl->ovf) r.errc = SPK_ERRC_CAPACITY;
+  }
+  *res = r;
+}
+
+// VECTOR layouts with compatible members: the version passes trail every
+// record's main pass, so one lane walks the message (main pass, then the
+// version passes, unpacker.hpp:292-366,1354-1376) and records each record's
+// start, its heap use U[k][i] and where its group of each version starts
+__global__ void nest_vec_serial(NDec a, const uint8_t *__restrict__ wire, uint8_t *ws,
+                                uint64_t *__restrict__ U, uint64_t *__restrict__ starts,
+                                uint64_t *__restrict__ cpos) {
+  NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
+  if (threadIdx.x || ctl->errc) return;
+  const NLayout &N = a.N;
+  const uint64_t n = ctl->nrec, len = a.wire_len, data_end = ctl->data_len;
+  const uint32_t w = ctl->w;
+  uint64_t pos = ctl->p0, used[SPK_MAX_SPANS] = {}, base[SPK_MAX_SPANS];
+  uint32_t ovf = 0;
+  int32_t errc = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (i < a.rec_cap) starts[i] = pos;
+    for (uint32_t k = 0; k < N.n_heaps; ++k) base[k] = used[k];
+    errc = n_read(N, wire, pos, len, w, nullptr, nullptr, used, a.heap_cap, &ovf, 0, N.n_ops, true);
+    if (errc) break;
+    if (i < a.rec_cap)
+      for (uint32_t k = 0; k < N.n_heaps; ++k) U[(uint64_t)k * a.rec_cap + i] = used[k] - base[k];
+  }
+  bool stop = errc != 0;
+  for (uint32_t rk = 0; rk < N.n_ranks && !stop; ++rk) {
+    for (uint64_t i = 0; i < n && !stop; ++i) {
+      if (i < a.rec_cap) cpos[(uint64_t)rk * a.rec_cap + i] = pos;
+      for (uint32_t k = 0; k < N.n_heaps; ++k) base[k] = used[k];
+      stop = n_read_compat(N, wire, pos, len, data_end, rk, w, nullptr, nullptr, used, a.heap_cap,
+                           &ovf, &errc) != 0;
+      if (i < a.rec_cap)
+        for (uint32_t k = 0; k < N.n_heaps; ++k) U[(uint64_t)k * a.rec_cap + i] += used[k] - base[k];
+    }
+  }
+  ctl->werr = errc;
+  ctl->end = pos;
 }
 
 // MESSAGES count pass: errc and heap use of every message (no writes)
@@ -1413,10 +1576,11 @@ __global__ __launch_bounds__(256) void nest_msg_count(NDec a, const uint8_t *__r
     if (!errc) {
       uint64_t pos = m0 + p0;
       uint32_t ovf = 0;
-      errc = n_read(N, wire, pos, e, w, nullptr, nullptr, used, a.heap_cap, &ovf);
+      errc = n_read(N, wire, pos, e, w, nullptr, nullptr, used, a.heap_cap, &ovf, 0, N.n_ops,
+                    true);
       for (uint32_t rk = 0; !errc && rk < N.n_ranks; ++rk)
-        if (n_read_compat(N, wire, pos, e, m0 + dl, rk, nullptr, nullptr, used, a.heap_cap, &ovf,
-                          &errc))
+        if (n_read_compat(N, wire, pos, e, m0 + dl, rk, w, nullptr, nullptr, used, a.heap_cap,
+                          &ovf, &errc))
           break;
       consumed = pos - m0 > dl ? pos - m0 : dl;  // consume_len (struct_pack.hpp:343-357)
     }
@@ -1427,7 +1591,8 @@ __global__ __launch_bounds__(256) void nest_msg_count(NDec a, const uint8_t *__r
   for (uint32_t k = 0; k < N.n_heaps; ++k) U[(uint64_t)k * a.n_msgs + i] = errc ? 0 : used[k];
 }
 
-// write pass (both modes): record i from its start with heap bases B[k][i]
+// write pass (MESSAGES, and VECTOR with compatible members): record i from
+// its start with heap bases B[k][i]
 __global__ __launch_bounds__(256) void nest_emit(NDec a, const uint8_t *__restrict__ wire,
                                                  const uint64_t *__restrict__ offs,
                                                  const uint64_t *__restrict__ starts,
@@ -1441,7 +1606,7 @@ __global__ __launch_bounds__(256) void nest_emit(NDec a, const uint8_t *__restri
   uint64_t pos, end, data_end;
   uint32_t w;
   if (mode == SPK_MODE_VECTOR) {
-    if (ctl->errc || i >= ctl->nrec || i >= a.rec_cap) return;
+    if (ctl->errc || ctl->werr || i >= ctl->nrec || i >= a.rec_cap) return;
     pos = starts[i];
     end = a.wire_len;
     w = ctl->w;
@@ -1459,14 +1624,15 @@ __global__ __launch_bounds__(256) void nest_emit(NDec a, const uint8_t *__restri
   for (uint32_t k = 0; k < N.n_heaps; ++k) used[k] = B[(uint64_t)k * nrows + i];
   uint32_t ovf = 0;
   uint8_t *rec = recs + i * N.stride;
-  n_read(N, wire, pos, end, w, rec, a.heaps, used, a.heap_cap, &ovf);
+  n_read(N, wire, pos, end, w, rec, a.heaps, used, a.heap_cap, &ovf, 0, N.n_ops, true);
   int32_t cec = 0;
   for (uint32_t rk = 0; rk < N.n_ranks; ++rk) {
     if (mode == SPK_MODE_VECTOR) {  // this record's group of version rk (walker)
       pos = cpos[(uint64_t)rk * a.rec_cap + i];
       if (pos == ~0ull) break;
     }
-    if (n_read_compat(N, wire, pos, end, data_end, rk, rec, a.heaps, used, a.heap_cap, &ovf, &cec))
+    if (n_read_compat(N, wire, pos, end, data_end, rk, w, rec, a.heaps, used, a.heap_cap, &ovf,
+                      &cec))
       break;
   }
   if (ovf) atomicAdd(&ctl->ovf, 1ull);
@@ -1499,6 +1665,11 @@ __global__ void nest_finish(NDec a, const uint64_t *__restrict__ part, uint64_t 
   const uint32_t nh = a.N.n_heaps;
   if (mode == SPK_MODE_VECTOR) {
     if (ctl->errc) return;  // errc already in *res
+    if (ctl->werr) {
+      r.errc = ctl->werr;
+      *res = r;
+      return;
+    }
     const uint64_t n = ctl->nrec;
     r.count = n;
     r.consumed = ctl->end > ctl->data_len ? ctl->end : ctl->data_len;
@@ -1547,6 +1718,39 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
     a.heap_cap[k] = heap_caps[k];
   }
   uint8_t *ws = (uint8_t *)d_ws;
+  hipError_t er;
+  if (mode == SPK_MODE_VECTOR && !a.N.n_ranks) {  // the chunked decode
+    const CWs f = cws_layout(wire_len, a.N.n_heaps);
+    const uint64_t cap = cws_chunks(wire_len);
+    CPtrs P;
+    P.ent = reinterpret_cast<uint64_t *>(ws + f.ent);
+    P.ext = reinterpret_cast<uint64_t *>(ws + f.ext);
+    P.err = reinterpret_cast<int32_t *>(ws + f.err);
+    P.cols = reinterpret_cast<uint64_t *>(ws + f.cols);
+    const uint64_t nch_max = (wire_len + kNCh - 1) / kNCh;
+    P.nch_cap = nch_max;
+    (void)cap;
+    uint64_t *part = reinterpret_cast<uint64_t *>(ws + f.part);
+    // the header decides the chunk count on the device: launch for the
+    // largest one the wire allows, lanes past it leave at once
+    const unsigned g = nblocks(nch_max, kNT);
+    SPK_LAUNCH(nest_vhdr, dim3(1), dim3(1), 0, s, a, (const uint8_t *)d_wire, ws, d_res);
+    SPK_LAUNCH(nest_cspec, dim3(g), dim3(kNT), 0, s, a, (const uint8_t *)d_wire,
+               (const uint8_t *)ws, P);
+    for (int r = 0; r < kNRounds; ++r)
+      SPK_LAUNCH(nest_cround, dim3(g), dim3(kNT), 0, s, a, (const uint8_t *)d_wire, ws, P, r);
+    SPK_LAUNCH(nest_cverify, dim3(g), dim3(kNT), 0, s, ws, P);
+    SPK_LAUNCH(nest_cfix, dim3(1), dim3(64), 0, s, a, (const uint8_t *)d_wire, ws, P);
+    // columns scanned over the chunks the wire allows (the speculation
+    // pass zeroed the ones past the header's count)
+    if ((er = nscan(P.cols, nch_max, 1 + a.N.n_heaps, part, s)) != hipSuccess) return er;
+    SPK_LAUNCH(nest_cemit, dim3(g), dim3(kNT), 0, s, a, (const uint8_t *)d_wire, ws, P,
+               (uint8_t *)d_recs);
+    const uint64_t nb = (nch_max + kNScanBlk - 1) / kNScanBlk;
+    SPK_LAUNCH(nest_cfinish, dim3(1), dim3(1), 0, s, a, (const uint64_t *)part, nb,
+               (const uint8_t *)ws, d_res);
+    return hipGetLastError();
+  }
   const uint64_t rows = mode == SPK_MODE_VECTOR ? rec_cap : n_msgs;
   const NWs f = nws_layout(rows, a.N.n_heaps, a.N.n_ranks);
   uint64_t *cpos = reinterpret_cast<uint64_t *>(ws + f.cpos);
@@ -1556,16 +1760,14 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
   uint64_t *starts = reinterpret_cast<uint64_t *>(ws + f.starts);
   int32_t *ec = reinterpret_cast<int32_t *>(ws + f.starts);  // MESSAGES: errc per message
   const uint64_t nb = (rows + kNScanBlk - 1) / kNScanBlk;
-  hipError_t er = hipMemsetAsync(d_res, 0, sizeof(spk_dresult_t), s);
-  if (er != hipSuccess) return er;
-  SPK_LAUNCH(nest_ctl_init, dim3(1), dim3(1), 0, s, ws);
-  if (mode == SPK_MODE_VECTOR) {
+  if ((er = hipMemsetAsync(d_res, 0, sizeof(spk_dresult_t), s)) != hipSuccess) return er;
+  if (mode == SPK_MODE_VECTOR) {  // compatible members: one lane walks the message
     if (rows && (er = hipMemsetAsync(U, 0, rows * 8 * a.N.n_heaps, s)) != hipSuccess) return er;
-    if (rows && a.N.n_ranks &&
-        (er = hipMemsetAsync(cpos, 0xFF, rows * 8 * a.N.n_ranks, s)) != hipSuccess)
+    if (rows && (er = hipMemsetAsync(cpos, 0xFF, rows * 8 * a.N.n_ranks, s)) != hipSuccess)
       return er;
-    SPK_LAUNCH(nest_vec_walk, dim3(1), dim3(64), 0, s, a, (const uint8_t *)d_wire, ws, U, starts,
-               cpos, d_res);
+    SPK_LAUNCH(nest_vhdr, dim3(1), dim3(1), 0, s, a, (const uint8_t *)d_wire, ws, d_res);
+    SPK_LAUNCH(nest_vec_serial, dim3(1), dim3(64), 0, s, a, (const uint8_t *)d_wire, ws, U,
+               starts, cpos);
     if ((er = nscan(U, rows, a.N.n_heaps, part, s)) != hipSuccess) return er;
     if (rows)
       SPK_LAUNCH(nest_emit, dim3(nblocks(rows, 256)), dim3(256), 0, s, a, (const uint8_t *)d_wire,
@@ -1575,6 +1777,7 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
                (const int32_t *)ec, ws, mode, d_res, (int32_t *)nullptr);
     return hipGetLastError();
   }
+  SPK_LAUNCH(nest_ctl_init, dim3(1), dim3(1), 0, s, ws);
   if (!n_msgs) return hipGetLastError();
   SPK_LAUNCH(nest_msg_count, dim3(nblocks(n_msgs, 256)), dim3(256), 0, s, a,
              (const uint8_t *)d_wire, d_msg_offsets, U, ec, cons);

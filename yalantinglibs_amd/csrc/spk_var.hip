@@ -50,6 +50,9 @@
 
 namespace spk {
 
+// Heaps of the flat-record kernels in this file: a flat layout with more
+// variable-length members runs the interpreter (spk_nested.hip).
+constexpr uint32_t kVS = SPK_FLAT_SPANS;
 constexpr int kThreads = 256;
 constexpr int kIPT = 1;                     // records per thread (encode write; 2 measured
                                             // slower: C3 +19 %, C5 3x as big payloads
@@ -63,7 +66,7 @@ struct VarArgs {
   uint64_t n;
   int mode;
   uint32_t fpre;      // MESSAGES: frame prefix bytes before every message
-  const uint8_t *heaps[SPK_MAX_SPANS];
+  const uint8_t *heaps[kVS];
   uint32_t fseq_off;  // frame u32 fields (SPK_FRAME_NONE: absent)
   uint32_t flen_off;
   uint32_t fseq_base;
@@ -875,8 +878,8 @@ struct DecArgs {
   uint64_t wire_len;
   uint64_t n_msgs;
   uint64_t rec_cap;
-  uint64_t heap_cap[SPK_MAX_SPANS];
-  uint8_t *heaps[SPK_MAX_SPANS];
+  uint64_t heap_cap[kVS];
+  uint8_t *heaps[kVS];
   uint32_t prefix;  // MESSAGES: frame bytes before every message
   uint32_t body_w;  // VECTOR, spk_decode_body: no header, body_n records at this width
   uint64_t body_n;
@@ -894,7 +897,7 @@ struct DecArgs {
 // per-block slots of the MESSAGES decode scan buffer: span totals, then the
 // block's ok-message count and consumed bytes (summed by var_scan_blocks:
 // no same-address atomics across thousands of blocks)
-constexpr uint32_t kBs = SPK_MAX_SPANS + 2;
+constexpr uint32_t kBs = kVS + 2;
 
 struct MsgState {
   uint64_t pos;    // absolute payload position, ~0 if the message failed
@@ -910,7 +913,7 @@ __global__ __launch_bounds__(kThreads) void var_msg_parse(
   uint64_t *bsum = reinterpret_cast<uint64_t *>(ws + kWsScratch +
                                                 sizeof(MsgState) * a.n_msgs);
   const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  uint64_t cnt[SPK_MAX_SPANS] = {};
+  uint64_t cnt[kVS] = {};
   uint64_t ok = 0, consumed = 0;
   if (i < a.n_msgs) {
     const uint64_t f = offs[i], e = a.ends ? a.ends[i] : offs[i + 1];
@@ -941,7 +944,7 @@ __global__ __launch_bounds__(kThreads) void var_msg_parse(
       s.pos = ~0ull;
       ok = 0;
       consumed = 0;
-      for (int k = 0; k < SPK_MAX_SPANS; ++k) cnt[k] = 0;
+      for (int k = 0; k < kVS; ++k) cnt[k] = 0;
     }
     st[i] = s;
     if (errc_out) errc_out[i] = s.errc;
@@ -956,8 +959,8 @@ __global__ __launch_bounds__(kThreads) void var_msg_parse(
   block_excl_scan(ok, &tok, sh);
   block_excl_scan(consumed, &tcons, sh);
   if (threadIdx.x == 0) {
-    bsum[(uint64_t)blockIdx.x * kBs + SPK_MAX_SPANS] = tok;
-    bsum[(uint64_t)blockIdx.x * kBs + SPK_MAX_SPANS + 1] = tcons;
+    bsum[(uint64_t)blockIdx.x * kBs + kVS] = tok;
+    bsum[(uint64_t)blockIdx.x * kBs + kVS + 1] = tcons;
   }
 }
 
@@ -985,7 +988,7 @@ __global__ __launch_bounds__(1024) void var_scan_blocks(uint64_t nblocks,
     }
   }
   // count / consumed: sums of the per-block partials
-  for (uint32_t k = SPK_MAX_SPANS; k < kBs; ++k) {
+  for (uint32_t k = kVS; k < kBs; ++k) {
     uint64_t carry = 0;
     for (uint64_t b0 = 0; b0 < nblocks; b0 += blockDim.x) {
       const uint64_t b = b0 + threadIdx.x;
@@ -994,7 +997,7 @@ __global__ __launch_bounds__(1024) void var_scan_blocks(uint64_t nblocks,
       carry += tot;
     }
     if (threadIdx.x == 0) {
-      if (k == SPK_MAX_SPANS)
+      if (k == kVS)
         res->count = carry;
       else
         res->consumed = carry;
@@ -1015,7 +1018,7 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
     if (res->heap_used[k] > a.heap_cap[k]) return;
   const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
   MsgState s{~0ull, 1, 1};
-  uint64_t cnt[SPK_MAX_SPANS] = {};
+  uint64_t cnt[kVS] = {};
   uint64_t end = 0;
   if (i < a.n_msgs) {
     s = st[i];
@@ -1024,7 +1027,7 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
       rec_counts(a.L, wire, s.pos, s.w, cnt, end);
     }
   }
-  uint64_t hoff[SPK_MAX_SPANS] = {};
+  uint64_t hoff[kVS] = {};
   for (uint32_t k = 0; k < a.L.n_spans; ++k) {
     uint64_t tot;
     hoff[k] = bsum[(uint64_t)blockIdx.x * kBs + k] + block_excl_scan(cnt[k], &tot, sh);
@@ -1121,12 +1124,12 @@ struct FCtl {
   unsigned long long term_pos;   // where the true path ends (atomicMin), ~0
   unsigned long long end_pos;    // end of record n-1
   unsigned long long total;      // records on the path (tile scan)
-  unsigned long long htot[SPK_MAX_SPANS];  // heap elements used by records 0..n-1
+  unsigned long long htot[kVS];  // heap elements used by records 0..n-1
   unsigned long long entry0;     // tile 0's entry (range mode: injected, or kNoPos = its own guess)
   unsigned long long nglob;      // range mode: the message's record count
   uint32_t range;                // the tiles are a byte range of the body (spk_decode_shard_*)
   uint32_t last;                 // range mode: the range holds the message's end
-  unsigned long long stot[SPK_MAX_SPANS];  // span-count sums on the path
+  unsigned long long stot[kVS];  // span-count sums on the path
   unsigned long long nlist[4];   // tiles listed for re-resolution by select pass k
 };
 constexpr size_t kWsFCtl = kWsCtl + 1280;
@@ -1137,16 +1140,16 @@ static_assert(kWsFCtl + sizeof(FCtl) <= kWsScratch, "FCtl overlaps the scratch a
 // descriptor so the walker's loop constants sit in SGPRs.
 struct WalkProg {
   uint32_t ns;
-  uint32_t skip[SPK_MAX_SPANS + 1];
-  uint32_t esz[SPK_MAX_SPANS];
+  uint32_t skip[kVS + 1];
+  uint32_t esz[kVS];
   uint32_t c0max;                  // largest first count of a plausible record
-  uint64_t cmax[SPK_MAX_SPANS];    // largest count whose byte size fits 64 bits
+  uint64_t cmax[kVS];    // largest count whose byte size fits 64 bits
   uint32_t optm;                   // bit k: span k is an OPTION ([has_value:1][U?])
   uint32_t pf_all;                 // no first-count screening of candidate starts
   uint32_t pf_var;                 // screening past segment 0's varints (NS = -1 walks)
   uint32_t rounds;                 // parallel re-verification rounds before the fixup
   uint32_t nv;                     // varint members
-  uint8_t vfirst[SPK_MAX_SPANS + 2];  // segment k's varints: [vfirst[k], vfirst[k+1])
+  uint8_t vfirst[kVS + 2];  // segment k's varints: [vfirst[k], vfirst[k+1])
   uint32_t vafter[SPK_MAX_VARINTS];   // fixed bytes after varint j (same segment)
 };
 
@@ -1171,7 +1174,7 @@ static WalkProg make_walkprog(const spk_layout *L) {
     }
   }
   p.ns = k;
-  for (uint32_t j = k + 1; j < SPK_MAX_SPANS + 2; ++j) p.vfirst[j] = (uint8_t)p.nv;
+  for (uint32_t j = k + 1; j < kVS + 2; ++j) p.vfirst[j] = (uint8_t)p.nv;
   for (uint32_t j = 0; j < k; ++j) p.cmax[j] = ~0ull / (p.esz[j] ? p.esz[j] : 1);
   p.c0max = k ? (kPlaus > p.skip[0] ? (kPlaus - p.skip[0]) / (p.esz[0] ? p.esz[0] : 1) : 0) : 0;
   // an OPTION's has_value byte is not a w-byte count: no screening on it
@@ -1234,7 +1237,7 @@ __device__ __forceinline__ uint64_t wlen(const WalkProg &P, const uint8_t *wire,
   const uint32_t ns = NS > 0 ? (uint32_t)NS : P.ns;
   if (NS < 0 && !vi_seg(P, 0, WireBytes{wire}, len, p)) return 0;
 #pragma unroll
-  for (uint32_t k = 0; k < (NS > 0 ? (uint32_t)NS : SPK_MAX_SPANS); ++k) {
+  for (uint32_t k = 0; k < (NS > 0 ? (uint32_t)NS : kVS); ++k) {
     if (NS <= 0 && k >= ns) break;
     const bool opt = (P.optm >> k) & 1u;
     const uint32_t pw = opt ? 1u : w;
@@ -1265,7 +1268,7 @@ __device__ __forceinline__ uint64_t wlen_rd(const WalkProg &P, const Rd &rd, uin
   const uint32_t ns = NS > 0 ? (uint32_t)NS : P.ns;
   if (NS < 0 && !vi_seg_rd(P, 0, rd, len, p)) return 0;
 #pragma unroll
-  for (uint32_t k = 0; k < (NS > 0 ? (uint32_t)NS : SPK_MAX_SPANS); ++k) {
+  for (uint32_t k = 0; k < (NS > 0 ? (uint32_t)NS : kVS); ++k) {
     if (NS <= 0 && k >= ns) break;
     const bool opt = (P.optm >> k) & 1u;
     const uint32_t pw = opt ? 1u : w;
@@ -1360,7 +1363,7 @@ __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
   fc->term_pos = ~0ull;
   fc->end_pos = 0;
   fc->total = 0;
-  for (int k = 0; k < SPK_MAX_SPANS; ++k) fc->htot[k] = fc->stot[k] = 0;
+  for (int k = 0; k < kVS; ++k) fc->htot[k] = fc->stot[k] = 0;
   const uint64_t payload = (!e && a.wire_len > pos) ? a.wire_len - pos : 0;
   c->nchunks = (c->n == 0) ? 0 : (payload + kSpec - 1) / kSpec;
   spk_dresult_t r = {};
@@ -1587,7 +1590,7 @@ constexpr uint32_t kTab = 2048;                              // record starts pe
 constexpr uint64_t kNoPos = ~0ull - 1;  // "no plausible start / unknown entry"
 constexpr uint32_t kSpecPast = 2;       // records a speculative walk checks past its chunk
 constexpr uint32_t kAlt = 4;            // entries a tile function carries
-constexpr uint32_t kAltWords = 2 + SPK_MAX_SPANS;   // entry, cnt, sums
+constexpr uint32_t kAltWords = 2 + kVS;   // entry, cnt, sums
 constexpr uint32_t kFnWords = 48;       // y, nalt, kAlt x kAltWords (+ pad)
 constexpr int32_t kSelTerm = -2;        // the tile starts past the path's end
 constexpr int32_t kSelBroken = -1;
@@ -1623,7 +1626,7 @@ __device__ __forceinline__ void walk_true(const WalkProg &P, const Rd &rd, uint6
   }
   uint64_t x = entry;
   while (x < ce) {
-    uint64_t rc[NS > 0 ? NS : SPK_MAX_SPANS];
+    uint64_t rc[NS > 0 ? NS : kVS];
     const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w, rc) : 0;
     if (!L) {
       term_at = x;
@@ -1676,7 +1679,7 @@ __device__ __forceinline__ void walk_merge(const WalkProg &P, const Rd &rd, uint
         term_at = sp.term_at;
         return;
       }
-    uint64_t rc[NS > 0 ? NS : SPK_MAX_SPANS];
+    uint64_t rc[NS > 0 ? NS : kVS];
     const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w, rc) : 0;
     if (!L) {
       term_at = x;
@@ -1836,7 +1839,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
   const uint64_t cs = ts + (uint64_t)lane * kTChunk;
   const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
   // ---- 1. speculative walk of this lane's chunk ----
-  uint64_t used = kNoPos, ex = kNoPos, sums[NS > 0 ? NS : SPK_MAX_SPANS], term_at = kTermPos;
+  uint64_t used = kNoPos, ex = kNoPos, sums[NS > 0 ? NS : kVS], term_at = kTermPos;
   uint32_t cnt = 0;
   for (uint32_t q = 0; q < nsp; ++q) sums[q] = 0;
   const bool rng = reinterpret_cast<const FCtl *>(ws + kWsFCtl)->range != 0;
@@ -1847,7 +1850,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
     uint64_t tt = 0, x = cs, past = 0, sx = exact ? cs : kNoPos;
     bool searching = !exact, done = false;
     uint32_t k = 0;
-    uint64_t ksum[NS > 0 ? NS : SPK_MAX_SPANS];
+    uint64_t ksum[NS > 0 ? NS : kVS];
     for (uint32_t q = 0; q < nsp; ++q) ksum[q] = 0;
     const uint32_t s0 = P.skip[0];
     while (!done) {
@@ -1911,7 +1914,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
         for (uint32_t q = 0; q < nsp; ++q) ksum[q] = 0;
         searching = false;
       }
-      uint64_t rc[NS > 0 ? NS : SPK_MAX_SPANS];
+      uint64_t rc[NS > 0 ? NS : kVS];
       const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w, rc) : 0;
       if (!exact && ((L == 0 && x < len) || L > kPlaus)) {  // off the record grid
         tt += 1;
@@ -1978,7 +1981,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
         bool ok = q < ce0 && screen_one<NS>(P, rd, len, w, q);
         uint64_t qe = kNoPos, qt;
         uint32_t qc = 0;
-        uint64_t qs[NS > 0 ? NS : SPK_MAX_SPANS];
+        uint64_t qs[NS > 0 ? NS : kVS];
         if (ok) {
           walk_true<NS>(P, rd, len, w, q, ce0, qe, qc, qs, qt);
           ok = qe == x1;
@@ -2007,11 +2010,11 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
   }
   if (X != kNoPos && !(dbg & 32))
     resolve_tile_sp<NS>(P, rd, len, w, cs, ce, lane, X, sp, used, ex, cnt, sums, term_at);
-  uint64_t tcnt = wave_sum_u64(cnt), tsum[NS > 0 ? NS : SPK_MAX_SPANS];
+  uint64_t tcnt = wave_sum_u64(cnt), tsum[NS > 0 ? NS : kVS];
   for (uint32_t q = 0; q < nsp; ++q) tsum[q] = wave_sum_u64(sums[q]);
   // ---- 3. entry alternatives (tile 0's entry is exact) ----
   uint32_t nalt = X != kNoPos ? 1u : 0u;
-  uint64_t alt_e = kNoPos, alt_c = 0, alt_s[NS > 0 ? NS : SPK_MAX_SPANS];  // lane a holds alt a
+  uint64_t alt_e = kNoPos, alt_c = 0, alt_s[NS > 0 ? NS : kVS];  // lane a holds alt a
   for (uint32_t q = 0; q < nsp; ++q) alt_s[q] = 0;
   if (lane == 0 && nalt) {
     alt_e = X;
@@ -2023,7 +2026,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
     // whose walk reaches chunk 0's exit; one per lane, in parallel ----
     const uint64_t e0 = __shfl(ex, 0), ce0 = __shfl(ce, 0);
     const uint32_t c0 = __shfl(cnt, 0);
-    uint64_t s0[NS > 0 ? NS : SPK_MAX_SPANS];
+    uint64_t s0[NS > 0 ? NS : kVS];
     for (uint32_t q = 0; q < nsp; ++q) s0[q] = __shfl(sums[q], 0);
     const uint64_t lim = e0 < ce0 ? e0 : ce0;
     for (uint64_t b = X + 1; nalt && nalt < kAlt && b < lim && b < X + 1 + 128; b += 64) {
@@ -2031,7 +2034,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
       bool ok = q < lim && screen_one<NS>(P, rd, len, w, q);
       uint64_t qe = kNoPos, qt;
       uint32_t qc = 0;
-      uint64_t qs[NS > 0 ? NS : SPK_MAX_SPANS];
+      uint64_t qs[NS > 0 ? NS : kVS];
       if (ok) {
         walk_true<NS>(P, rd, len, w, q, ce0, qe, qc, qs, qt);
         ok = qe == e0;
@@ -2186,11 +2189,11 @@ __global__ __launch_bounds__(64) void vec_tile_repair(DecArgs a, WalkProg P,
     const uint64_t g = t * 64 + lane;
     uint64_t used = TB.cused[g], ex = TB.cex[g], term_at = kTermPos;
     uint32_t cnt = TB.ccnt[g];
-    uint64_t sums[NS > 0 ? NS : SPK_MAX_SPANS];
+    uint64_t sums[NS > 0 ? NS : kVS];
     for (uint32_t q = 0; q < nsp; ++q) sums[q] = TB.csum[(uint64_t)q * TB.nchunks + g];
     resolve_tile<NS>(P, tv.rd, len, w, ce, lane, T, used, ex, cnt, sums, term_at);
     const uint64_t tcnt = wave_sum_u64(cnt);
-    uint64_t tsum[NS > 0 ? NS : SPK_MAX_SPANS];
+    uint64_t tsum[NS > 0 ? NS : kVS];
     for (uint32_t q = 0; q < nsp; ++q) tsum[q] = wave_sum_u64(sums[q]);
     TB.cused[g] = used;
     TB.cex[g] = ex;
@@ -2265,11 +2268,11 @@ __global__ __launch_bounds__(64) void vec_tile_seqfix(DecArgs a, WalkProg P,
       const uint64_t g = f * 64 + lane;
       uint64_t used = TB.cused[g], ex = TB.cex[g], term_at = kTermPos;
       uint32_t cnt = TB.ccnt[g];
-      uint64_t sums[NS > 0 ? NS : SPK_MAX_SPANS];
+      uint64_t sums[NS > 0 ? NS : kVS];
       for (uint32_t q = 0; q < nsp; ++q) sums[q] = TB.csum[(uint64_t)q * TB.nchunks + g];
       resolve_tile<NS>(P, tv.rd, len, w, ce, lane, T, used, ex, cnt, sums, term_at);
       const uint64_t tcnt = wave_sum_u64(cnt);
-      uint64_t tsum[NS > 0 ? NS : SPK_MAX_SPANS];
+      uint64_t tsum[NS > 0 ? NS : kVS];
       for (uint32_t q = 0; q < nsp; ++q) tsum[q] = wave_sum_u64(sums[q]);
       TB.cused[g] = used;
       TB.cex[g] = ex;
@@ -2304,7 +2307,7 @@ __global__ __launch_bounds__(256) void vec_tile_contrib(uint8_t *__restrict__ ws
   if (t >= TB.ntiles || !vec_live(c)) return;
   const uint64_t *fn = TB.fn + t * kFnWords;
   const int32_t sel = TB.sel[t];
-  uint64_t cnt = 0, s[SPK_MAX_SPANS] = {};
+  uint64_t cnt = 0, s[kVS] = {};
   if (sel >= 0) {
     cnt = fn[2 + sel * kAltWords + 1];
     for (uint32_t q = 0; q < nsp; ++q) s[q] = fn[2 + sel * kAltWords + 2 + q];
@@ -2451,12 +2454,12 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
   uint32_t cnt = own ? TB.ccnt[g] : 0;
   if (sel > 0 && part == 0 && lane == 0) {  // another entry of chunk 0 (same exit)
     const uint64_t T = alt[0];
-    uint64_t qe, qt, qs[NS > 0 ? NS : SPK_MAX_SPANS];
+    uint64_t qe, qt, qs[NS > 0 ? NS : kVS];
     walk_true<NS>(P, rd, len, w, T, ce, qe, cnt, qs, qt);
     used = T;
   }
   const uint64_t pcnt = wave_sum_u64(cnt);  // records starting in this part
-  uint64_t base = tbase, psum[SPK_MAX_SPANS];
+  uint64_t base = tbase, psum[kVS];
   for (uint32_t q = 0; q < nsp; ++q) psum[q] = TB.contrib[(uint64_t)(1 + q) * TB.ntiles + t];
   if (part > 0) {
     // everything from this part to the tile's end (chunk 0 is not among it)
@@ -2474,7 +2477,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
     // where the true path ends: past this chunk's records
     uint64_t x = used;
     for (uint32_t r = 0; r < cnt; ++r) {
-      uint64_t rc[NS > 0 ? NS : SPK_MAX_SPANS];
+      uint64_t rc[NS > 0 ? NS : kVS];
       x += wlen_rd<NS>(P, rd, len, x, w, rc);
     }
     atomicMin(&fc->term_pos, (unsigned long long)x);
@@ -2486,7 +2489,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
     rofs = wave_excl_scan_u64(cnt, lane, &tot);
   }
   uint16_t *tab = tab_s[wv];
-  uint64_t carry[NS > 0 ? NS : SPK_MAX_SPANS];
+  uint64_t carry[NS > 0 ? NS : kVS];
   for (uint32_t q = 0; q < nsp; ++q) carry[q] = psum[q];
   const uint64_t nemit = (n - base < pcnt) ? n - base : pcnt;
   for (uint64_t pass0 = 0; pass0 < nemit; pass0 += kEmitTab) {
@@ -2498,7 +2501,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
         const uint64_t i = rofs + r;
         if (i >= pend) break;
         if (i >= pass0) tab[i - pass0] = (uint16_t)(x - wb);
-        uint64_t rc[NS > 0 ? NS : SPK_MAX_SPANS];
+        uint64_t rc[NS > 0 ? NS : kVS];
         x += wlen_rd<NS>(P, rd, len, x, w, rc);
       }
     }
@@ -2510,10 +2513,10 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
       const uint64_t i = i0 + lane;
       const bool act = i < nrec;
       const uint64_t pos = wb + (act ? tab[i] : 0);
-      uint64_t rc[SPK_MAX_SPANS] = {};
+      uint64_t rc[kVS] = {};
       uint64_t L = 0;
       if (act) L = wlen_rd<NS>(P, rd, len, pos, w, rc);
-      uint64_t off[SPK_MAX_SPANS];
+      uint64_t off[kVS];
       bool fits = true;
       for (uint32_t q = 0; q < nsp; ++q) {
         uint64_t tot;
@@ -2570,7 +2573,7 @@ __global__ void vec_shard_summary(const uint8_t *__restrict__ ws, TileBufs TB, u
     const bool term = fc->term_tile < TB.ntiles;
     r.exit = term ? ~0ull : (TB.ntiles ? TB.fn[(TB.ntiles - 1) * kFnWords] : fc->entry0);
     r.count = fc->total;
-    for (uint32_t q = 0; q < nsp && q < SPK_MAX_SPANS; ++q) r.heap[q] = fc->stot[q];
+    for (uint32_t q = 0; q < nsp && q < kVS; ++q) r.heap[q] = fc->stot[q];
     r.tiles_repaired = fc->broken[0] + fc->broken[1] + fc->broken[2] + fc->broken[3];
   }
   *out = r;
@@ -2591,7 +2594,7 @@ __global__ void vec_shard_setn(uint8_t *__restrict__ ws, uint64_t first, uint32_
   fc->last = last;
   fc->end_pos = 0;
   fc->njobs = 0;
-  for (int k = 0; k < SPK_MAX_SPANS; ++k) fc->htot[k] = 0;
+  for (int k = 0; k < kVS; ++k) fc->htot[k] = 0;
 }
 
 // Result: count / consume_len / heap use, or the errc of a short payload
@@ -2634,7 +2637,7 @@ __global__ void vec_tile_finish(DecArgs a, const uint8_t *__restrict__ wire,
     }
     r.count = 0;
     r.consumed = 0;
-    for (int k = 0; k < SPK_MAX_SPANS; ++k) r.heap_used[k] = 0;
+    for (int k = 0; k < kVS; ++k) r.heap_used[k] = 0;
   } else {
     r.count = c->n;
     const uint64_t end = c->n ? (uint64_t)fc->end_pos : c->p0;
@@ -2828,7 +2831,7 @@ static VarArgs make_varargs(const spk_layout *L, int mode, uint64_t n,
   a.n = n;
   a.mode = mode;
   a.fseq_off = a.flen_off = SPK_FRAME_NONE;
-  for (uint32_t k = 0; k < a.L.n_spans && k < SPK_MAX_SPANS; ++k)
+  for (uint32_t k = 0; k < a.L.n_spans && k < kVS; ++k)
     a.heaps[k] = heaps ? (const uint8_t *)heaps[k] : nullptr;
   return a;
 }
