@@ -199,7 +199,7 @@ extern "C" {
 
 #define SPK_ABI_VERSION 2u
 #define SPK_MAX_OPS 64u
-#define SPK_MAX_SPANS 16u  /* heaps (variable-length members) per layout */
+#define SPK_MAX_SPANS 32u  /* heaps (variable-length members) per layout */
 #define SPK_MAX_LITERAL 240u
 
 /* return codes (host-side; negative) */

@@ -121,6 +121,27 @@ static int cmd_kat() {
   kat_one<FV32>(os, "FV32", first);
   kat_one<EV>(os, "EV", first);
   kat_one<std::vector<EV>>(os, "vector<EV>", first);
+  kat_one<ResponseCode>(os, "ResponseCode", first);
+  kat_one<AliMessage>(os, "AliMessage", first);
+  kat_one<ValidateRequest>(os, "ValidateRequest", first);
+  kat_one<std::vector<ValidateRequest>>(os, "vector<ValidateRequest>", first);
+  kat_one<Exp>(os, "Exp", first);
+  kat_one<std::vector<Exp>>(os, "vector<Exp>", first);
+  kat_one<struct_pack::expected<void, int32_t>>(os, "expected<void,int32_t>", first);
+  kat_one<CmpG>(os, "CmpG", first);
+  kat_one<Vec3>(os, "Vec3", first);
+  kat_one<Weapon>(os, "Weapon", first);
+  kat_one<Monster>(os, "Monster", first);
+  kat_one<std::vector<Monster>>(os, "vector<Monster>", first);
+  kat_one<rect2<int32_t>>(os, "rect2<int32_t>", first);
+  kat_one<std::vector<rect2<int32_t>>>(os, "vector<rect2<int32_t>>", first);
+  kat_one<Lists>(os, "Lists", first);
+  kat_one<Maps>(os, "Maps", first);
+  kat_one<std::vector<Maps>>(os, "vector<Maps>", first);
+  kat_one<std::map<int32_t, std::string>>(os, "map<int32_t,string>", first);
+  kat_one<std::unordered_multimap<int32_t, int32_t>>(os, "unordered_multimap<int32_t,int32_t>", first);
+  kat_one<std::pair<std::string, cpx::person>>(os, "pair<string,person>", first);
+  kat_one<cpx::complicated_object>(os, "complicated_object", first);
   kat_one<uint8_t, uint16_t, uint32_t, uint64_t, int8_t, int16_t, int64_t,
           bool, char, float, double>(os, "fundamentals", first);
   os << "\n}\n";
@@ -244,6 +265,23 @@ static bool with_case(const Args &a, F &&f) {
     return f.template operator()<EV>([=](EV &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "deep")
     return f.template operator()<Deep>([=](Deep &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "lists")
+    return f.template operator()<Lists>([=](Lists &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "maps")
+    return f.template operator()<Maps>([=](Maps &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "cplx")
+    return f.template operator()<cpx::complicated_object>(
+        [=](cpx::complicated_object &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "valreq")
+    return f.template operator()<ValidateRequest>([=](ValidateRequest &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "exp")
+    return f.template operator()<Exp>([=](Exp &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "cmpg")
+    return f.template operator()<CmpG>([=](CmpG &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "monster")
+    return f.template operator()<Monster>([=](Monster &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "rect2")
+    return f.template operator()<rect2<int32_t>>([=](rect2<int32_t> &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "rect")  // C1: benchmark rect<int> default values
     return f.template operator()<rect<int>>([=](rect<int> &o, uint64_t) { o = rect<int>{}; });
   if (k == "rpcrect")

@@ -14,7 +14,12 @@
 #include <array>
 #include <cstdint>
 #include <cstring>
+#include <deque>
+#include <list>
+#include <map>
 #include <optional>
+#include <set>
+#include <unordered_map>
 #include <string>
 #include <variant>
 #include <vector>
@@ -286,12 +291,146 @@ constexpr struct_pack::sp_config set_sp_config(EV *) {
   return struct_pack::sp_config::ENCODING_WITH_VARINT;
 }
 
+// ---- std::optional / expected / compatible of values that are not trivially
+// serializable (SPK_OP_OPTGROUP / SPK_OP_CGROUP) ---------------------------
+// the coro_rpc benchmark's request type, member for member as declared in
+// src/coro_rpc/benchmark/api/ValidateRequest.h
+struct ResponseCode {
+  int32_t retcode;
+  std::optional<std::string> error_message;
+};
+struct AliMessage {
+  int32_t message_type;
+  std::optional<std::string> session_no;
+  std::optional<bool> tint_flag;
+  std::optional<uint32_t> source_entity;
+  std::optional<uint32_t> dest_entity;
+  std::optional<std::string> client_ip;
+  std::optional<ResponseCode> rc;
+  std::optional<int32_t> version;
+};
+struct ValidateRequest {
+  AliMessage msg;
+  std::optional<int32_t> job_id;
+  std::vector<std::string> query_keys;
+  std::optional<bool> clean;
+};
+// struct_pack::expected<T, E> members (packer.hpp:400-410); the standalone
+// C++ front end (no reference on the include path) has no expected<T, E>
+#if !defined(SPK_GPU_WITH_REFERENCE) || SPK_GPU_WITH_REFERENCE
+#define SPK_TYPES_HAVE_EXPECTED 1
+struct Exp {
+  int32_t id;
+  struct_pack::expected<std::string, int32_t> r;
+  struct_pack::expected<Inner, std::string> q;
+  std::optional<std::vector<std::string>> l;
+  struct_pack::expected<int64_t, ResponseCode> e;
+};
+#endif
+// compatible<U, ver> with U not trivially serializable, beside a trivial one
+struct CmpG {
+  int32_t id;
+  struct_pack::compatible<std::string, 20230101> note;
+  std::string name;
+  struct_pack::compatible<std::vector<int32_t>, 20230101> ints;
+  struct_pack::compatible<Inner, 20240101> in;
+  struct_pack::compatible<ResponseCode, 20240101> rc;
+};
+
+// ---- the reference benchmark's shapes (src/struct_pack/benchmark/data_def.hpp)
+enum Color : uint8_t { Red, Green, Blue };
+struct Vec3 {
+  float x, y, z;
+};
+struct Weapon {
+  std::string name;
+  int16_t damage;
+};
+struct Monster {
+  Vec3 pos;
+  int16_t mana;
+  int16_t hp;
+  std::string name;
+  std::string inventory;
+  Color color;
+  std::vector<Weapon> weapons;
+  Weapon equipped;
+  std::vector<Vec3> path;
+};
+template <typename T>
+struct rect2 {
+  T x, y, width, height;
+};
+inline constexpr struct_pack::sp_config set_sp_config(rect2<int32_t> *) {
+  return struct_pack::sp_config{struct_pack::sp_config::DISABLE_ALL_META_INFO |
+                                struct_pack::sp_config::USE_FAST_VARINT |
+                                struct_pack::sp_config::ENCODING_WITH_VARINT};
+}
+inline constexpr struct_pack::sp_config set_sp_config(std::vector<rect2<int32_t>> *) {
+  return struct_pack::sp_config{struct_pack::DISABLE_ALL_META_INFO};
+}
+
+// ---- the other container kinds (reflection.hpp:328-350): list / deque are
+// container_t like vector; set_container_t / map_container_t hold their keys /
+// pairs in the container's order ----------------------------------------------
+struct Lists {
+  int32_t id;
+  std::list<std::string> names;
+  std::deque<int32_t> vals;
+  std::list<Inner> pts;
+};
+struct Maps {
+  int32_t id;
+  std::map<int32_t, std::string> m;
+  std::set<std::string> s;
+  std::multimap<int64_t, Inner> mm;  // pair<const int64_t, Inner>: 16 raw bytes
+  std::multiset<int32_t> ms;
+  std::map<std::string, RecS> mr;
+};
+
+// A mirror of complicated_object (src/struct_pack/tests/test_struct.hpp:17-103),
+// the type of the reference's own binary goldens (tests/binary_data/
+// test_cross_platform*.dat): same member types in the same order, so the same
+// type literal, code and bytes.
+namespace cpx {
+struct person {
+  int age;
+  std::string name;
+};
+enum class Color { red, black, white };
+struct trivial_one {
+  int a;
+  double b;
+  float c;
+};
+struct complicated_object {
+  Color color;
+  int a;
+  std::string b;
+  std::vector<person> c;
+  std::list<std::string> d;
+  std::deque<int> e;
+  std::map<int, person> f;
+  std::multimap<int, person> g;
+  std::set<std::string> h;
+  std::multiset<int> i;
+  std::unordered_map<int, person> j;
+  std::unordered_multimap<int, int> k;
+  std::array<person, 2> m;
+  person n[2];
+  std::pair<std::string, person> o;
+  std::vector<std::array<trivial_one, 2>> p;
+};
+}  // namespace cpx
+
 template <typename T>
 constexpr bool kHasCompat = false;
 template <>
 inline constexpr bool kHasCompat<Cmp> = true;
 template <>
 inline constexpr bool kHasCompat<CmpNew> = true;
+template <>
+inline constexpr bool kHasCompat<CmpG> = true;
 
 namespace spk_gold {
 
@@ -591,6 +730,169 @@ inline void fill(AlRec &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
   o.s = make_chars(seed, i, maxlen);
   fill(o.p, seed, i, 0);
   fill(o.e, seed, i, 0);
+}
+
+inline void fill(Lists &o, uint64_t seed, uint64_t i, uint32_t maxn) {
+  o.id = (int32_t)(uint32_t)rnd(seed, i, 0);
+  const uint32_t n = (uint32_t)(rnd(seed, i, 1) % (uint64_t)(maxn + 1));
+  for (uint32_t j = 0; j < n; ++j) o.names.push_back(tag_chars(elem_word(seed, i, j)));
+  const uint64_t r3 = rnd(seed, i, 3);
+  for (uint32_t j = 0; j < (uint32_t)((r3 >> 8) % 7); ++j)
+    o.vals.push_back((int32_t)(uint32_t)mix64(rnd(seed, i, 4) + j));
+  for (uint32_t j = 0; j < (uint32_t)(r3 % 5); ++j) {
+    const uint64_t w = mix64(rnd(seed, i, 5) + j);
+    o.pts.push_back(Inner{(int32_t)(uint32_t)w, rf(w >> 32)});
+  }
+}
+
+// keys drawn from small ranges, so maps and sets see repeated keys (a map /
+// set keeps the first, a multimap / multiset all of them)
+inline void fill(Maps &o, uint64_t seed, uint64_t i, uint32_t) {
+  o.id = (int32_t)(uint32_t)rnd(seed, i, 0);
+  const uint64_t b = rnd(seed, i, 3);
+  for (uint32_t j = 0; j < (uint32_t)(b % 5); ++j) {
+    const uint64_t h = elem_word(seed, i, j);
+    o.m.emplace((int32_t)(h % 7) - 3, tag_chars(h >> 8));
+  }
+  for (uint32_t j = 0; j < (uint32_t)((b >> 8) % 5); ++j)
+    o.s.insert(tag_chars(mix64(rnd(seed, i, 20) + j) % 5));
+  for (uint32_t j = 0; j < (uint32_t)((b >> 16) % 4); ++j) {
+    const uint64_t w = mix64(rnd(seed, i, 22) + j);
+    o.mm.emplace((int64_t)(mix64(rnd(seed, i, 21) + j) % 3) - 1,
+                 Inner{(int32_t)(uint32_t)w, rf(w >> 32)});
+  }
+  for (uint32_t j = 0; j < (uint32_t)((b >> 24) % 6); ++j)
+    o.ms.insert((int32_t)(mix64(rnd(seed, i, 23) + j) % 7) - 3);
+  for (uint32_t j = 0; j < (uint32_t)((b >> 32) % 3); ++j)
+    o.mr.emplace(tag_chars(mix64(rnd(seed, i, 24) + j) % 4 + 1), make_recs(mix64(seed + i), j, 10));
+}
+
+// create_complicated_object() (test_struct.hpp:82-103), padding bytes zero
+inline void fill(cpx::complicated_object &x, uint64_t, uint64_t, uint32_t) {
+  using cpx::person;
+  x.color = cpx::Color::red;
+  x.a = 42;
+  x.b = "hello";
+  x.c = {{20, "tom"}, {22, "jerry"}};
+  x.d = {"hello", "world"};
+  x.e = {1, 2};
+  x.f = {{1, {20, "tom"}}};
+  x.g = {{1, {20, "tom"}}, {1, {22, "jerry"}}};
+  x.h = {"aa", "bb"};
+  x.i = {1, 2};
+  x.j = {{1, {20, "tom"}}};
+  x.k = {{1, 2}};
+  x.m = {person{20, "tom"}, {22, "jerry"}};
+  x.n[0] = person{15, "tom"};
+  x.n[1] = person{31, "jerry"};
+  x.o = std::make_pair(std::string("aa"), person{20, "tom"});
+  const double bs[4] = {1.7, 1.4, 0.7, 11111.4};
+  const float cs[4] = {2.4f, 2.6f, 1.4f, 2213321.6f};
+  const int as[4] = {1232114, 12315, 4, 1123115};
+  x.p.resize(2);
+  std::memset((void *)x.p.data(), 0, 2 * sizeof(x.p[0]));
+  for (int q = 0; q < 4; ++q) {
+    cpx::trivial_one &t = x.p[q / 2][q % 2];
+    t.a = as[q];
+    t.b = bs[q];
+    t.c = cs[q];
+  }
+}
+
+inline void fill(ValidateRequest &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
+  const uint64_t b = rnd(seed, i, 3);
+  AliMessage &m = o.msg;
+  m.message_type = (int32_t)(uint32_t)rnd(seed, i, 0);
+  if (b & 1) m.session_no = make_chars(seed, i, maxlen);
+  if (b & 2) m.tint_flag = (rnd(seed, i, 4) & 1) != 0;
+  if (b & 4) m.source_entity = (uint32_t)rnd(seed, i, 5);
+  if (b & 8) m.dest_entity = (uint32_t)rnd(seed, i, 6);
+  if (b & 16) m.client_ip = tag_chars(rnd(seed, i, 7));
+  if (b & 32) {
+    m.rc.emplace();
+    m.rc->retcode = (int32_t)(uint32_t)rnd(seed, i, 8);
+    if (b & 64) m.rc->error_message = tag_chars(rnd(seed, i, 9));
+  }
+  if (b & 128) m.version = (int32_t)(uint32_t)rnd(seed, i, 10);
+  if (b & 256) o.job_id = (int32_t)(uint32_t)rnd(seed, i, 11);
+  const uint32_t n = (uint32_t)((b >> 16) % 5);
+  o.query_keys.resize(n);
+  for (uint32_t j = 0; j < n; ++j) o.query_keys[j] = tag_chars(elem_word(seed, i, j));
+  if (b & 512) o.clean = ((rnd(seed, i, 12) >> 1) & 1) != 0;
+}
+
+#ifdef SPK_TYPES_HAVE_EXPECTED
+inline void fill(Exp &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
+  const uint64_t b = rnd(seed, i, 3);
+  o.id = (int32_t)(uint32_t)rnd(seed, i, 0);
+  if (b & 1)
+    o.r = make_chars(seed, i, maxlen);
+  else
+    o.r = struct_pack::unexpected<int32_t>((int32_t)(uint32_t)rnd(seed, i, 4));
+  if (b & 2)
+    o.q = Inner{(int32_t)(uint32_t)rnd(seed, i, 5), rf(rnd(seed, i, 6))};
+  else
+    o.q = struct_pack::unexpected<std::string>(tag_chars(rnd(seed, i, 7)));
+  if (b & 4) {
+    o.l.emplace();
+    const uint32_t n = (uint32_t)((b >> 16) % 4);
+    for (uint32_t j = 0; j < n; ++j) o.l->push_back(tag_chars(elem_word(seed, i, j)));
+  }
+  if (b & 8) {
+    o.e = (int64_t)rnd(seed, i, 8);
+  } else {
+    ResponseCode rc{(int32_t)(uint32_t)rnd(seed, i, 9), std::nullopt};
+    if (b & 16) rc.error_message = tag_chars(rnd(seed, i, 10));
+    o.e = struct_pack::unexpected<ResponseCode>(rc);
+  }
+}
+#endif
+
+inline void fill(CmpG &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
+  const uint64_t m = rnd(seed, i, 6);
+  o.id = (int32_t)(uint32_t)rnd(seed, i, 0);
+  if (m & 1) o.note = tag_chars(rnd(seed, i, 2));
+  o.name = make_chars(seed, i, maxlen);
+  if (m & 2) {
+    std::vector<int32_t> v((size_t)((m >> 8) % 6));
+    for (size_t j = 0; j < v.size(); ++j) v[j] = (int32_t)(uint32_t)mix64(rnd(seed, i, 3) + j);
+    o.ints = std::move(v);
+  }
+  if (m & 4) o.in = Inner{(int32_t)(uint32_t)rnd(seed, i, 4), rf(rnd(seed, i, 5))};
+  if (m & 8) {
+    ResponseCode rc{(int32_t)(uint32_t)rnd(seed, i, 7), std::nullopt};
+    if (m & 16) rc.error_message = tag_chars(rnd(seed, i, 8));
+    o.rc = rc;
+  }
+}
+
+inline void fill(Monster &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
+  o.pos = Vec3{rf(rnd(seed, i, 4)), rf(rnd(seed, i, 5)), rf(rnd(seed, i, 6))};
+  const uint64_t r7 = rnd(seed, i, 7), r9 = rnd(seed, i, 9), r10 = rnd(seed, i, 10);
+  o.mana = (int16_t)r7;
+  o.hp = (int16_t)(r7 >> 16);
+  o.name = make_chars(seed, i, maxlen);
+  o.inventory = tag_chars(rnd(seed, i, 8));
+  o.color = (Color)(r9 % 3);
+  o.weapons.resize((size_t)((r9 >> 8) % 5));
+  for (size_t j = 0; j < o.weapons.size(); ++j) {
+    const uint64_t h = elem_word(seed, i, j);
+    o.weapons[j] = Weapon{tag_chars(h), (int16_t)(h >> 32)};
+  }
+  o.equipped = Weapon{tag_chars(r10), (int16_t)(r10 >> 40)};
+  o.path.resize((size_t)((r9 >> 16) % 9));
+  for (size_t j = 0; j < o.path.size(); ++j) {
+    const uint64_t w = mix64(rnd(seed, i, 11) + j);
+    o.path[j] = Vec3{rf(w), rf(w >> 32), rf(mix64(w))};
+  }
+}
+
+inline void fill(rect2<int32_t> &o, uint64_t seed, uint64_t i, uint32_t) {
+  const FvGen g(seed, i);
+  o.x = (int32_t)(uint32_t)g.sg(0);
+  o.y = (int32_t)(uint32_t)g.sg(1);
+  o.width = (int32_t)(uint32_t)g.sg(2);
+  o.height = (int32_t)(uint32_t)g.sg(3);
 }
 
 }  // namespace spk_gold

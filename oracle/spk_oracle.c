@@ -61,13 +61,21 @@ static int is_heap_op(uint32_t k) {
   k = SPK_OP_KIND(k);
   return k == SPK_OP_SPAN || k == SPK_OP_OPTION || k == SPK_OP_ARRAY || k == SPK_OP_COMPAT;
 }
-/* compatible<U, ver> members: top-level ops only (include/spk_codec.h) */
+/* compatible<U, ver> members: top-level ops only (include/spk_codec.h);
+ * COMPAT holds a trivially serializable U in a heap, CGROUP its ops inline */
 static int is_compat(uint32_t k) { return SPK_OP_KIND(k) == SPK_OP_COMPAT; }
+static int is_cgroup(uint32_t k) { return SPK_OP_KIND(k) == SPK_OP_CGROUP; }
+/* VARIANT / OPTGROUP / CGROUP: op groups closed by END in the same record */
+static int is_group(uint32_t k) {
+  k = SPK_OP_KIND(k);
+  return k == SPK_OP_VARIANT || k == SPK_OP_OPTGROUP || k == SPK_OP_CGROUP;
+}
 /* number of distinct version ranks (max rank + 1), 0 without compat members */
 static unsigned compat_ranks(const spk_layout *L) {
   unsigned r = 0;
   for (uint32_t i = 0; i < L->n_ops; ++i)
-    if (is_compat(L->ops[i].kind) && SPK_OP_RANK(L->ops[i].kind) + 1 > r)
+    if ((is_compat(L->ops[i].kind) || is_cgroup(L->ops[i].kind)) &&
+        SPK_OP_RANK(L->ops[i].kind) + 1 > r)
       r = SPK_OP_RANK(L->ops[i].kind) + 1;
   return r;
 }
@@ -81,7 +89,7 @@ static uint32_t end_of(const spk_layout *L, uint32_t i);
 static uint32_t group_end(const spk_layout *L, uint32_t j) {
   while (j < L->n_ops) {
     const uint32_t k = L->ops[j].kind;
-    if (k == SPK_OP_ARRAY || k == SPK_OP_VARIANT) {
+    if (k == SPK_OP_ARRAY || is_group(k)) {
       j = end_of(L, j) + 1;
       continue;
     }
@@ -90,18 +98,27 @@ static uint32_t group_end(const spk_layout *L, uint32_t j) {
   }
   return L->n_ops;
 }
-/* ARRAY at i -> its END; VARIANT at i -> the END of its last alternative */
+/* ARRAY at i -> its END; a group op at i -> the END of its last group */
 static uint32_t end_of(const spk_layout *L, uint32_t i) {
   if (L->ops[i].kind == SPK_OP_ARRAY) return group_end(L, i + 1);
   uint32_t j = i + 1;
   for (uint32_t a = 0; a < L->ops[i].size; ++a) j = group_end(L, j) + 1;
   return j - 1;
 }
-/* first op of alternative a of the VARIANT at i */
+/* first op of alternative a of the VARIANT (group a of the OPTGROUP) at i */
 static uint32_t alt_start(const spk_layout *L, uint32_t i, uint32_t a) {
   uint32_t j = i + 1;
   while (a--) j = group_end(L, j) + 1;
   return j;
+}
+/* the group a VARIANT / OPTGROUP writes: the variant's index; for an optional
+ * / expected (packer.hpp:382-388,400-410) group 0 (the value) when has_value,
+ * else group 1 of an expected (its error) or none (-1) */
+static int active_group(const spk_layout *L, uint32_t i, const uint8_t *rec) {
+  uint32_t v;
+  memcpy(&v, rec + L->ops[i].rec_off, 4);
+  if (L->ops[i].kind == SPK_OP_VARIANT) return (int)v;
+  return v ? 0 : (L->ops[i].size == 2 ? 1 : -1);
 }
 /* ---- USE_FAST_VARINT group of the top-level record (packer.hpp:152-235,
  * calculate_size.hpp:191-390, unpacker.hpp:642-747) ---------------------- */
@@ -296,12 +313,20 @@ static void ops_size(const spk_layout *L, uint32_t i0, uint32_t i1, const uint8_
       *cnts += 1;
       *bytes += c * op->size;
       if (c > *maxc) *maxc = c;
-    } else if (op->kind == SPK_OP_VARIANT) { /* index byte + the active alternative */
-      uint32_t idx;
-      memcpy(&idx, rec + op->rec_off, 4);
-      const uint32_t a0 = alt_start(L, i, idx);
+    } else if (op->kind == SPK_OP_VARIANT || op->kind == SPK_OP_OPTGROUP) {
+      /* index / has_value byte + the active group (calculate_size.hpp:100-105) */
+      const int a = active_group(L, i, rec);
       *bytes += 1;
-      ops_size(L, a0, group_end(L, a0), rec, heaps, bytes, cnts, maxc);
+      if (a >= 0) {
+        const uint32_t a0 = alt_start(L, i, (uint32_t)a);
+        ops_size(L, a0, group_end(L, a0), rec, heaps, bytes, cnts, maxc);
+      }
+      i = end_of(L, i);
+    } else if (is_cgroup(op->kind)) { /* [has_value] + U, in its version pass */
+      uint32_t has;
+      memcpy(&has, rec + op->rec_off, 4);
+      *bytes += 1;
+      if (has) ops_size(L, i + 1, end_of(L, i), rec, heaps, bytes, cnts, maxc);
       i = end_of(L, i);
     } else if (op->kind == SPK_OP_ARRAY) {
       const uint32_t e = end_of(L, i);
@@ -339,6 +364,20 @@ static uint8_t *ops_write(const spk_layout *L, uint32_t i0, uint32_t i1, const u
     }
     else if (is_compat(op->kind) || op->kind == SPK_OP_FVAR) {
       /* version UINT64_MAX: nothing (:246-249); fast varints: in the group */
+    }
+    else if (is_cgroup(op->kind)) {
+      i = end_of(L, i); /* written by its version pass */
+    }
+    else if (op->kind == SPK_OP_OPTGROUP) { /* packer.hpp:382-388,400-410 */
+      uint32_t has;
+      memcpy(&has, rec + op->rec_off, 4);
+      *p++ = has ? 1 : 0;
+      const int a = active_group(L, i, rec);
+      if (a >= 0) {
+        const uint32_t a0 = alt_start(L, i, (uint32_t)a);
+        p = ops_write(L, a0, group_end(L, a0), rec, heaps, w, p);
+      }
+      i = end_of(L, i);
     }
     else if (op->kind == SPK_OP_VARINT) { /* serialize_varint :245-268 */
       uint64_t v = vi_value(rec, op);
@@ -395,9 +434,17 @@ static uint8_t *write_record(const spk_layout *L, const uint8_t *rec,
 /* the version pass of rank `rk` over one record (packer.hpp:453-461):
  * [has_value][U] for each compatible member of that version */
 static uint8_t *write_compat(const spk_layout *L, unsigned rk, const uint8_t *rec,
-                             const void *const *heaps, uint8_t *p) {
+                             const void *const *heaps, unsigned w, uint8_t *p) {
   for (uint32_t i = 0; i < L->n_ops; ++i) {
     const spk_op *op = &L->ops[i];
+    if (is_cgroup(op->kind) && SPK_OP_RANK(op->kind) == rk) {
+      uint32_t has;
+      memcpy(&has, rec + op->rec_off, 4);
+      *p++ = has ? 1 : 0;
+      if (has) p = ops_write(L, i + 1, end_of(L, i), rec, heaps, w, p);
+      i = end_of(L, i);
+      continue;
+    }
     if (!is_compat(op->kind) || SPK_OP_RANK(op->kind) != rk) continue;
     const uint64_t c = rec_count(rec, op);
     *p++ = (uint8_t)c;
@@ -477,7 +524,7 @@ int spko_encode(const spk_layout *L, int mode, uint64_t n, const void *recs,
       p = write_record(L, r + i * L->rec_stride, heaps, w, p);
     for (unsigned rk = 0; rk < compat_ranks(L); ++rk) /* packer.hpp:66-78 */
       for (uint64_t i = 0; i < n; ++i)
-        p = write_compat(L, rk, r + i * L->rec_stride, heaps, p);
+        p = write_compat(L, rk, r + i * L->rec_stride, heaps, w, p);
   }
   else {
     uint8_t *base = p;
@@ -490,7 +537,7 @@ int spko_encode(const spk_layout *L, int mode, uint64_t n, const void *recs,
       if (msg_offsets) msg_offsets[i] = (uint64_t)(p - base);
       p = write_header(p, &L->fmt_one, &h);
       p = write_record(L, rec, heaps, w, p);
-      for (unsigned rk = 0; rk < compat_ranks(L); ++rk) p = write_compat(L, rk, rec, heaps, p);
+      for (unsigned rk = 0; rk < compat_ranks(L); ++rk) p = write_compat(L, rk, rec, heaps, w, p);
     }
     if (msg_offsets) msg_offsets[n] = (uint64_t)(p - base);
   }
@@ -613,6 +660,28 @@ static int32_t ops_read(dctx_t *c, rd_t *r, unsigned w, uint32_t i0, uint32_t i1
       if (rec) vi_store(rec, op, v);
       continue;
     }
+    if (is_cgroup(op->kind)) { /* main pass: absent until its version pass */
+      if (rec) {
+        const uint32_t z = 0;
+        memcpy(rec + op->rec_off, &z, 4);
+      }
+      i = end_of(L, i);
+      continue;
+    }
+    if (op->kind == SPK_OP_OPTGROUP) { /* unpacker.hpp:1251-1277 */
+      if (!rd_take(r, 1, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
+      const uint32_t has = p[0] != 0;
+      if (rec) memcpy(rec + op->rec_off, &has, 4);
+      const int a = has ? 0 : (op->size == 2 ? 1 : -1);
+      if (a >= 0) {
+        /* deserialize_one(*item) / (item.error()): the errc is dropped, the
+           reader stays where the decode stopped */
+        const uint32_t a0 = alt_start(L, i, (uint32_t)a);
+        (void)ops_read(c, r, w, a0, group_end(L, a0), rec);
+      }
+      i = end_of(L, i);
+      continue;
+    }
     if (op->kind == SPK_OP_VARIANT) { /* unpacker.hpp:1278-1292 */
       if (!rd_take(r, 1, &p)) return SPK_ERRC_NO_BUFFER_SPACE;
       const uint32_t idx = p[0];
@@ -634,7 +703,11 @@ static int32_t ops_read(dctx_t *c, rd_t *r, unsigned w, uint32_t i0, uint32_t i1
       uint8_t *el = NULL;
       if (rec) {
         const uint64_t off = c->used[hk];
-        if (cnt > 0xFFFFFFFFull || cnt > c->heap_caps[hk] - off) {
+        /* an element takes at least one byte: at most (bytes left + 1)
+           elements get decoded (the last one may fail and stay) */
+        const uint64_t left = (uint64_t)(r->end - r->now);
+        const uint64_t need = cnt < left + 1 ? cnt : left + 1;
+        if (need > 0xFFFFFFFFull || need > c->heap_caps[hk] - off) {
           c->overflow = 1;
           rec = NULL;
         } else {
@@ -736,11 +809,28 @@ static int32_t read_record(dctx_t *c, rd_t *r, unsigned w, uint8_t *rec) {
  * Returns 1 when the reader reached data_len before a member: the legal end
  * of an older writer's message (size_type_ = UCHAR_MAX, :360-365). */
 static int read_compat(dctx_t *c, rd_t *r, const uint8_t *msg, uint64_t data_len,
-                       unsigned rk, uint8_t *rec, int32_t *err) {
+                       unsigned rk, unsigned w, uint8_t *rec, int32_t *err) {
   const spk_layout *L = c->L;
   const uint8_t *p;
   for (uint32_t i = 0; i < L->n_ops; ++i) {
     const spk_op *op = &L->ops[i];
+    if (is_cgroup(op->kind) && SPK_OP_RANK(op->kind) == rk) {
+      const uint32_t e = end_of(L, i);
+      if ((uint64_t)(r->now - msg) >= data_len) return 1;
+      if (!rd_take(r, 1, &p)) {
+        *err = SPK_ERRC_NO_BUFFER_SPACE;
+        return 1;
+      }
+      if (p[0]) { /* item = U{}; deserialize_one(*item) with its errc dropped */
+        if (rec) {
+          const uint32_t one = 1;
+          memcpy(rec + op->rec_off, &one, 4);
+        }
+        (void)ops_read(c, r, w, i + 1, e, rec);
+      }
+      i = e;
+      continue;
+    }
     if (!is_compat(op->kind) || SPK_OP_RANK(op->kind) != rk) continue;
     if ((uint64_t)(r->now - msg) >= data_len) return 1;
     if (!rd_take(r, 1, &p)) {
@@ -819,7 +909,7 @@ int spko_decode(const spk_layout *L, int mode, const void *wire,
     int stop = 0;
     for (unsigned rk = 0; rk < compat_ranks(L) && !stop; ++rk)
       for (uint64_t i = 0; i < n && !stop; ++i)
-        stop = read_compat(&c, &r, base, data_len, rk,
+        stop = read_compat(&c, &r, base, data_len, rk, w,
                            (i < rec_cap && out) ? out + i * L->rec_stride : NULL, &e);
     if (e) {
       res->errc = e;
@@ -872,7 +962,7 @@ int spko_decode(const spk_layout *L, int mode, const void *wire,
       uint8_t *rec = (i < rec_cap && out) ? out + i * L->rec_stride : NULL;
       e = read_record(&c, &r, w, rec);
       for (unsigned rk = 0; !e && rk < compat_ranks(L); ++rk)
-        if (read_compat(&c, &r, base + a, data_len, rk, rec, &e)) break;
+        if (read_compat(&c, &r, base + a, data_len, rk, w, rec, &e)) break;
       if (!e && i >= rec_cap) {
         e = SPK_ERRC_CAPACITY;
         c.overflow = 1;

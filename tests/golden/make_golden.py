@@ -35,7 +35,9 @@ SEED = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004,
         "packed": 0x5EED0014, "alrec": 0x5EED0015,
         # one seed for the three writer versions of Cmp (same records)
         "cmp": 0x5EED0016, "cmpold": 0x5EED0016, "cmpnew": 0x5EED0016,
-        "fv": 0x5EED0017, "fve": 0x5EED0018, "fv32": 0x5EED0019, "ev": 0x5EED001A}
+        "fv": 0x5EED0017, "fve": 0x5EED0018, "fv32": 0x5EED0019, "ev": 0x5EED001A,
+        "valreq": 0x5EED001B, "exp": 0x5EED001C, "cmpg": 0x5EED001D, "monster": 0x5EED001E,
+        "rect2": 0x5EED001F, "lists": 0x5EED0020, "maps": 0x5EED0021, "cplx": 0}
 
 # (case_mode, n, param, conf, keep_bin)
 SMALL = [
@@ -109,6 +111,32 @@ SMALL = [
     ("fv_A", 30, 8, "nometa"), ("fve_A", 300, 8, "default"), ("fve_B", 200, 8, "default"),
     ("fv32_A", 300, 0, "default"), ("fv32_B", 200, 0, "default"),
     ("ev_A", 300, 8, "default"), ("ev_B", 200, 8, "default"), ("ev_A", 30, 8, "nometa"),
+    # optional / expected / compatible of values that are not trivially
+    # serializable: the coro_rpc benchmark's ValidateRequest, expected<T, E>
+    ("valreq_A", 0, 16, "default"), ("valreq_A", 1, 16, "default"),
+    ("valreq_A", 300, 16, "default"), ("valreq_A", 40, 300, "default"),
+    ("valreq_A", 50, 16, "typeinfo"), ("valreq_B", 200, 16, "default"),
+    ("valreq_B", 40, 16, "nometa"), ("exp_A", 0, 16, "default"), ("exp_A", 300, 16, "default"),
+    ("exp_B", 200, 16, "default"), ("exp_A", 50, 16, "typeinfo"), ("exp_A", 30, 300, "default"),
+    ("cmpg_A", 0, 8, "default"), ("cmpg_A", 200, 8, "default"), ("cmpg_B", 200, 8, "default"),
+    ("cmpg_A", 40, 300, "default"), ("cmpg_A", 50, 8, "typeinfo"),
+    # the reference benchmark's Monster (20 of them: its OBJECT_COUNT) and
+    # rect2<int32_t> with its ADL sp_config (fast varints, no meta info)
+    ("monster_A", 0, 20, "default"), ("monster_A", 1, 20, "default"),
+    ("monster_A", 20, 20, "default"), ("monster_A", 300, 20, "default"),
+    ("monster_B", 200, 20, "default"), ("monster_A", 40, 300, "default"),
+    ("monster_A", 50, 20, "typeinfo"), ("monster_B", 30, 20, "nometa"),
+    ("rect2_A", 0, 0, "default"), ("rect2_A", 20, 0, "default"), ("rect2_A", 300, 0, "default"),
+    ("rect2_B", 200, 0, "default"),
+    # list / deque / map / set / multimap / multiset; the reference's
+    # complicated_object (its cplx_B n1 typeinfo / default fixtures are the
+    # reference's own binary goldens, tests/golden/ref_test_cross_platform*.dat)
+    ("lists_A", 0, 6, "default"), ("lists_A", 1, 6, "default"), ("lists_A", 200, 6, "default"),
+    ("lists_A", 30, 300, "default"), ("lists_B", 200, 6, "default"),
+    ("lists_A", 50, 6, "typeinfo"), ("maps_A", 0, 0, "default"), ("maps_A", 1, 0, "default"),
+    ("maps_A", 200, 0, "default"), ("maps_B", 200, 0, "default"), ("maps_A", 50, 0, "typeinfo"),
+    ("cplx_B", 1, 0, "default"), ("cplx_B", 1, 0, "typeinfo"), ("cplx_A", 3, 0, "default"),
+    ("cplx_A", 2, 0, "typeinfo"), ("cplx_B", 5, 0, "nometa"),
 ]
 MEDIUM = [  # digest only (wire > ~1 MB)
     ("rec64_A", 65535, 0, "default"), ("rec64_A", 65536, 0, "default"),
@@ -127,6 +155,12 @@ MEDIUM = [  # digest only (wire > ~1 MB)
     ("fv_A", 70000, 48, "default"), ("fve_B", 20000, 16, "default"),
     ("ev_A", 70000, 16, "default"),
     ("recs_A", 200, 20000, "default"), ("outer_A", 100, 2000, "default"),
+    ("valreq_A", 30000, 16, "default"), ("valreq_B", 20000, 16, "default"),
+    ("exp_A", 30000, 16, "default"), ("cmpg_A", 30000, 16, "default"),
+    ("cmpg_B", 20000, 16, "default"), ("monster_A", 30000, 20, "default"),
+    ("monster_B", 20000, 20, "default"), ("rect2_A", 70000, 0, "default"),
+    ("lists_A", 30000, 6, "default"), ("maps_A", 20000, 0, "default"),
+    ("maps_B", 10000, 0, "default"), ("cplx_A", 3000, 0, "default"),
 ]
 BIG = [  # BASELINE.json full-size configs (digest only)
     ("rec64_A", 100_000_000, 0, "default"),
@@ -253,6 +287,13 @@ ERR_BASES = [
     ("fv_A", 6, 10, "default"), ("fv_B", 1, 10, "default"), ("fve_A", 5, 6, "default"),
     ("fv32_A", 8, 0, "default"), ("fv32_B", 1, 0, "default"), ("ev_A", 5, 6, "default"),
     ("ev_B", 1, 6, "default"),
+    ("valreq_A", 5, 10, "default"), ("valreq_B", 1, 10, "default"), ("valreq_A", 3, 10, "typeinfo"),
+    ("exp_A", 6, 10, "default"), ("exp_B", 1, 10, "default"),
+    ("cmpg_A", 6, 10, "default"), ("cmpg_B", 1, 10, "default"),
+    ("monster_A", 4, 10, "default"), ("monster_B", 1, 10, "default"),
+    ("rect2_A", 6, 0, "default"), ("rect2_B", 1, 0, "default"),
+    ("lists_A", 5, 4, "default"), ("lists_B", 1, 6, "default"),
+    ("maps_A", 4, 0, "default"), ("maps_B", 1, 0, "default"),
 ]
 # compatible members across writer versions: (writer, reader, n, param) — the
 # writer's message mutated and decoded as the reader's type (one type code)

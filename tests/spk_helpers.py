@@ -128,3 +128,63 @@ def records_equal(L, a, b, heaps_a, heaps_b, heap_used=None):
         ok = ok and heaps_a[k][:used].tobytes() == heaps_b[k][:used].tobytes()
         ok = ok and len(heaps_b[k]) == used
     return ok
+
+
+# ---- associative containers: the reference's insertion semantics ------------
+def _assoc_key(L, k, sub_rec, heaps, elem_bytes):
+    """Sort key of one element of top-level span k (a map's pair: its first;
+    a set: the element): signed integers by value, strings bytewise."""
+    sp = L.dev.spans[k]
+    t = sp.elem
+    key_t = getattr(getattr(L.rtype, "fields", None) and
+                    dict(L.rtype.fields).get(sp.path), "key", None)
+    kt = key_t if key_t is not None else getattr(dict(L.rtype.fields).get(sp.path), "elem", None)
+    if sp.sub is None:  # trivially serializable element bytes: the key's bytes first
+        return int.from_bytes(elem_bytes[:kt.size], "little", signed=kt.npdt[1] == "i")
+    name = "first" if sp.kind.endswith("map") else "value"
+    if isinstance(kt, S.String):
+        kk = [q for q, s2 in enumerate(L.dev.spans) if s2.path == f"{sp.path}[].{name}"][0]
+        n, o = int(sub_rec[name + ".n"]), int(sub_rec[name + ".off"])
+        return bytes(heaps[kk][o:o + n])
+    return int(sub_rec[name])
+
+
+def normalize_assoc(L, recs, heaps):
+    """What the reference's decode builds from a map / set on the wire
+    (unpacker.hpp:983-1122): a map / set keeps the first of repeated keys
+    (try_emplace / emplace), a multi container all of them, and iteration is
+    in key order (equal keys in insertion order). Our decode keeps the wire
+    order (the record model); this re-orders each top-level ordered
+    associative container's elements the same way so that re-encoding gives
+    the reference's canonical bytes. Returns new (recs, heaps)."""
+    recs = recs.copy()
+    heaps = [np.array(h, np.uint8, copy=True) for h in heaps]
+    for k, sp in enumerate(L.dev.spans):
+        if not sp.kind or "[]" in sp.path:
+            continue
+        assert sp.kind in ("map", "multimap", "set", "multiset"), sp.kind
+        esz = sp.elem.size
+        out = bytearray()
+        for i in range(len(recs)):
+            n, o = int(recs[i][sp.path + ".n"]), int(recs[i][sp.path + ".off"])
+            elems = [bytes(heaps[k][(o + j) * esz:(o + j + 1) * esz]) for j in range(n)]
+            subs = ([np.frombuffer(e, sp.sub.dtype)[0] for e in elems] if sp.sub is not None
+                    else [None] * n)
+            keys = [_assoc_key(L, k, sr, heaps, e) for sr, e in zip(subs, elems)]
+            order = sorted(range(n), key=lambda j: keys[j])  # stable
+            if not sp.kind.startswith("multi"):
+                seen, keep = set(), []
+                for j in range(n):  # the first of repeated keys stays
+                    if keys[j] not in seen:
+                        seen.add(keys[j])
+                        keep.append(j)
+                order = sorted(keep, key=lambda j: keys[j])
+            recs[sp.path + ".n"][i] = len(order)
+            recs[sp.path + ".off"][i] = len(out) // esz
+            out += b"".join(elems[j] for j in order)
+        heaps[k] = np.frombuffer(bytes(out), np.uint8).copy() if out else np.zeros(0, np.uint8)
+    return recs, heaps
+
+
+def has_assoc(L):
+    return any(sp.kind and "[]" not in sp.path for sp in L.dev.spans)

@@ -158,6 +158,10 @@ def test_error_parity(base):
             continue
         if e == 0:
             b2 = SP.RecordBatch(cd.L, out.recs, [h for h in out.heaps])
+            if H.has_assoc(cd.L):  # the reference's map / set from the decoded sequence
+                r_np = out.recs.cpu().numpy().reshape(-1).view(cd.L.dev.dtype)
+                r2, h2 = H.normalize_assoc(cd.L, r_np, [h.cpu().numpy() for h in out.heaps])
+                b2 = to_dev(cd, r2, h2)
             re, _ = cd.serialize(b2, mode)
             if H.sha256(re.cpu().numpy().tobytes()) != t["reenc_sha256"]:
                 bad.append((t["mut"], "reenc"))
@@ -174,7 +178,10 @@ RANDOM = [("recs", 1, 300), ("recs", 257, 5), ("recs", 5000, 48), ("recs", 20000
           ("alout", 3000, 0), ("packed", 4097, 0), ("alrec", 3000, 30),
           ("cmp", 5000, 48), ("cmp", 300, 400), ("cmpnew", 20000, 8), ("cmp", 1, 8),
           ("fv", 5000, 48), ("fv", 200, 400), ("fve", 3000, 8), ("fv32", 4000, 0),
-          ("ev", 5000, 16), ("ev", 30000, 4)]
+          ("ev", 5000, 16), ("ev", 30000, 4), ("valreq", 3000, 16), ("valreq", 100, 400),
+          ("exp", 3000, 16), ("cmpg", 3000, 16), ("cmpg", 100, 400), ("monster", 5000, 20),
+          ("monster", 200, 400), ("rect2", 20000, 0), ("lists", 3000, 6), ("lists", 100, 300),
+          ("maps", 2000, 0), ("cplx", 500, 0)]
 
 
 @pytest.mark.parametrize("case,n,param", RANDOM)
@@ -235,7 +242,11 @@ def _irregular_messages(cd, case, n, seed, param):
                                           ("group", 200, 4), ("deep", 200, 3),
                                           ("vnt", 300, 6), ("cmp", 300, 8),
                                           ("cmpnew", 300, 8), ("fv", 300, 8),
-                                          ("fv32", 300, 0), ("ev", 300, 8)])
+                                          ("fv32", 300, 0), ("ev", 300, 8),
+                                          ("valreq", 300, 16), ("exp", 300, 16),
+                                          ("cmpg", 300, 8), ("monster", 300, 20),
+                                          ("rect2", 300, 0), ("lists", 300, 6),
+                                          ("maps", 300, 0), ("cplx", 100, 0)])
 @pytest.mark.parametrize("cap_frac", [1.0, 0.6])
 def test_messages_irregular_vs_oracle(case, n, param, cap_frac):
     """Mode B decode of non-canonical message batches: per-message errc,
@@ -716,3 +727,62 @@ def test_encode_body_respects_out_cap(case, param):
                                 SP._p(buf), size, SP._p(ws), ws.numel(), None)
     torch.cuda.synchronize()
     assert rc == 0 and bool((buf[size:] == 0xA5).all()) and not bool((buf[:size] == 0xA5).all())
+
+
+@pytest.mark.parametrize("case,n,param", [("monster", 300000, 20), ("tags", 200000, 6),
+                                          ("valreq", 200000, 16), ("vnt", 100000, 8),
+                                          ("group", 3000, 300), ("deep", 2000, 300),
+                                          ("exp", 100000, 40), ("fv", 200000, 16)])
+def test_nested_vector_decode_chunked(case, n, param):
+    """The chunked decode of nested layouts (guessed chunk entries, rounds,
+    one-wave fixer, per-chunk emission) on messages of many chunks, incl.
+    records longer than a speculative walk's reach (group / deep with long
+    member lists): bit-exact with the oracle's bytes, round trip exact."""
+    cd = codec_for(case)
+    _, recs, heaps = synth.make_batch(case, n, 0xC4C4 + n, param)
+    exp, _, _ = H.oracle_encode(cd.L, C.SPK_MODE_VECTOR, recs, heaps)
+    out, _ = cd.serialize(to_dev(cd, recs, heaps), C.SPK_MODE_VECTOR)
+    assert out.cpu().numpy().tobytes() == exp
+    res, back, _ = cd.deserialize(out, C.SPK_MODE_VECTOR)
+    assert res.errc == 0 and res.count == n and res.consumed == len(exp)
+    assert back.recs.cpu().numpy().tobytes() == np.ascontiguousarray(recs).view(np.uint8).tobytes()
+    for k in range(len(heaps)):
+        nb = len(heaps[k])
+        assert res.heap_used[k] * cd.L.dev.spans[k].elem.size == nb
+        assert back.heaps[k][:nb].cpu().numpy().tobytes() == heaps[k].tobytes()
+    print(f"{case}: {len(exp) / 1e6:.1f} MB, chunks re-walked {res.tiles_repaired}, "
+          f"fixed by the wave {res.tiles_sequential}")
+    # truncations at many points: the errc and consume_len of the oracle
+    for cut in (len(exp) - 1, len(exp) * 2 // 3, len(exp) // 3, 9):
+        eres, _, _, _ = H.oracle_decode(cd.L, C.SPK_MODE_VECTOR, exp[:cut], rec_cap=n + 1,
+                                        heap_caps=max([len(h) // sp.elem.size + 2 for h, sp in
+                                                       zip(heaps, cd.L.dev.spans)] + [1]))
+        r, _, _ = cd.deserialize(wire_dev(exp[:cut]), C.SPK_MODE_VECTOR)
+        assert (r.errc, r.count, r.consumed) == (eres.errc, eres.count, eres.consumed), cut
+
+
+@pytest.mark.parametrize("ref,conf", [("ref_test_cross_platform.dat", "typeinfo"),
+                                      ("ref_test_cross_platform_without_debug_info.dat",
+                                       "default")])
+def test_gpu_decodes_reference_binary_goldens(ref, conf):
+    """The reference's own binary goldens (src/struct_pack/tests/binary_data/
+    test_cross_platform*.dat: complicated_object with list, deque, map,
+    multimap, set, multiset, unordered_map, unordered_multimap, array, pair
+    members; test_cross_platform.cpp:25-52) through the HIP decoder: the
+    decoded record == create_complicated_object(), and the HIP encoder
+    writes the file back byte for byte."""
+    import os
+    cd = codec_for("cplx", conf)
+    with open(os.path.join(H.GOLDEN, ref), "rb") as f:
+        wire = f.read()
+    _, recs, heaps = synth.make_batch("cplx", 1, 0, 0)
+    offs = torch.tensor([0, len(wire)], dtype=torch.int64, device="cuda")
+    res, out, ec = cd.deserialize(wire_dev(wire), C.SPK_MODE_MESSAGES, offs, 1)
+    assert res.errc == 0 and int(ec[0].item()) == 0 and res.consumed == len(wire)
+    assert out.recs.cpu().numpy().tobytes() == np.ascontiguousarray(recs).view(np.uint8).tobytes()
+    for k in range(len(heaps)):
+        nb = len(heaps[k])
+        assert res.heap_used[k] * cd.L.dev.spans[k].elem.size == nb
+        assert out.heaps[k][:nb].cpu().numpy().tobytes() == heaps[k].tobytes()
+    back, _ = cd.serialize(out, C.SPK_MODE_MESSAGES)
+    assert back.cpu().numpy().tobytes() == wire

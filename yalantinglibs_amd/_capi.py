@@ -13,7 +13,7 @@ import os
 
 SPK_ABI_VERSION = 2
 SPK_MAX_OPS = 64
-SPK_MAX_SPANS = 16
+SPK_MAX_SPANS = 32
 SPK_MAX_LITERAL = 240
 SPK_MAX_FRAME = 64
 SPK_MAX_ROUTES = 16

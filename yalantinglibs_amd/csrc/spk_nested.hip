@@ -654,7 +654,15 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
     pos += pw;
     const uint64_t off = used[hk];
     bool put = r != nullptr;
-    if (put && (cnt > 0xFFFFFFFFull || cnt > heap_cap[hk] - (off < heap_cap[hk] ? off : heap_cap[hk]))) {
+    // slots an ARRAY can fill: an element takes at least one byte, so at most
+    // (bytes left + 1) get decoded (the last one may fail and stay)
+    // (a SPAN whose payload is not there fails below without using its heap)
+    const uint64_t need = op.kind == SPK_OP_ARRAY ? (cnt > end - pos ? end - pos + 1 : cnt)
+                          : op.kind == SPK_OP_SPAN && ((op.size > 1 && cnt > ~0ull / op.size) ||
+                                                       end - pos < cnt * op.size)
+                              ? 0
+                              : cnt;
+    if (put && (need > 0xFFFFFFFFull || need > heap_cap[hk] - (off < heap_cap[hk] ? off : heap_cap[hk]))) {
       *ovf = 1;
       put = false;
     }

@@ -37,7 +37,7 @@ TID_BOOL, TID_CHAR8 = 11, 12
 TID_FLOAT32, TID_FLOAT64 = 17, 18
 TID_VINT32, TID_VINT64, TID_VUINT32, TID_VUINT64 = 20, 21, 22, 23
 TID_STRING, TID_ARRAY, TID_MAP, TID_SET, TID_CONTAINER = 128, 129, 130, 131, 132
-TID_OPTIONAL, TID_VARIANT = 133, 134
+TID_OPTIONAL, TID_VARIANT, TID_EXPECTED = 133, 134, 135
 TID_MONOSTATE = 250
 TID_STRUCT = 253
 TID_END = 255
@@ -190,6 +190,65 @@ class Vector(SpType):
         return True
 
 
+class List(Vector):
+    """std::list<T> / std::deque<T>: container_t like std::vector, the same
+    literal and bytes (type_id.hpp:334-336); decode appends in wire order."""
+
+    def __init__(self, elem: SpType, name: str = "std::list"):
+        super().__init__(elem)
+        self.name = f"{name}<{elem.name}>"
+
+
+class Set(Vector):
+    """std::set / multiset / unordered_set / unordered_multiset
+    (set_container_t): [count:w] then the keys in the container's iteration
+    order; literal set_container_t + literal(key) (type_calculate.hpp:280-283).
+    The record model keeps the elements in wire order: the reference inserts
+    them in that order (unpacker.hpp:1097-1122, emplace: a repeated key of a
+    set is dropped), so a host set built by inserting the array equals its."""
+
+    def __init__(self, key: SpType, multi: bool = False, ordered: bool = True):
+        super().__init__(key)
+        self.multi, self.ordered = multi, ordered
+        kind = ("std::multiset" if multi else "std::set") if ordered else \
+            ("std::unordered_multiset" if multi else "std::unordered_set")
+        self.name = f"{kind}<{key.name}>"
+        self.kind = ("multi" if multi else "") + ("set" if ordered else "uset")
+
+    def literal(self):
+        return bytes([TID_SET]) + self.elem.literal()
+
+
+class Map(Vector):
+    """std::map / multimap / unordered_map / unordered_multimap
+    (map_container_t): [count:w] then each std::pair<const K, V> in the
+    container's iteration order, written as a struct (first, second: raw
+    sizeof(pair) when both are trivially serializable, packer.hpp:411-421);
+    literal map_container_t + literal(K) + literal(V) (type_calculate.hpp:
+    284-290). The record model keeps the pairs in wire order: the reference
+    decodes them in that order with try_emplace (map: a repeated key keeps
+    the first value) / emplace (multimap) (unpacker.hpp:983-1095), so a host
+    map built that way from the array equals its."""
+
+    def __init__(self, key: SpType, value: SpType, multi: bool = False, ordered: bool = True):
+        super().__init__(Struct("std::pair", [("first", key), ("second", value)]))
+        self.key, self.value = key, value
+        self.multi, self.ordered = multi, ordered
+        kind = ("std::multimap" if multi else "std::map") if ordered else \
+            ("std::unordered_multimap" if multi else "std::unordered_map")
+        self.name = f"{kind}<{key.name},{value.name}>"
+        self.kind = ("multi" if multi else "") + ("map" if ordered else "umap")
+
+    def literal(self):
+        return bytes([TID_MAP]) + self.key.literal() + self.value.literal()
+
+
+def Pair(first: SpType, second: SpType) -> "Struct":
+    """std::pair<A, B>: a struct of first and second (type_id.hpp:360,
+    type_calculate.hpp:918-920), trivially serializable when both are."""
+    return Struct("std::pair", [("first", first), ("second", second)])
+
+
 class String(SpType):
     """std::string / std::string_view (string_t of char)."""
 
@@ -226,6 +285,28 @@ class Optional(SpType):
         return self.elem.has_container
 
 
+class Expected(SpType):
+    """struct_pack::expected<T, E> (tl / std::expected; expected_t): wire
+    [has_value:1] then T if present else E (ref packer.hpp:400-410; decode
+    unpacker.hpp:1251-1277 drops the value's / error's errc); literal
+    expected_t + literal(T) + literal(E) (type_calculate.hpp:291-297); T may be
+    Monostate() for expected<void, E>. Never trivially serializable
+    (reflection.hpp:903-905). Device record: u32 has_value, then T's fields
+    and E's fields side by side (SPK_OP_OPTGROUP with two groups)."""
+
+    def __init__(self, value: SpType, error: SpType):
+        self.value, self.error = value, error
+        self.name = f"struct_pack::expected<{value.name},{error.name}>"
+        self.config = DEFAULT
+
+    def literal(self):
+        return bytes([TID_EXPECTED]) + self.value.literal() + self.error.literal()
+
+    @property
+    def has_container(self):
+        return self.value.has_container or self.error.has_container
+
+
 class Compatible(SpType):
     """struct_pack::compatible<T, version> (compatible_t, ref compatible.hpp:
     21-154): an optional written after the main pass, in the version pass of
@@ -235,6 +316,8 @@ class Compatible(SpType):
     trivially serializable T is in the flat record model."""
 
     def __init__(self, elem: SpType, version: int = 0):
+        # (a U that is not trivially serializable is an SPK_OP_CGROUP: its
+        # ops inline in the record, [has][U] in the version pass)
         self.elem, self.version = elem, version
         self.name = f"struct_pack::compatible<{elem.name},{version}>"
         self.config = DEFAULT
@@ -255,6 +338,8 @@ def has_compatible(t: SpType) -> bool:
         return any(has_compatible(ft) for _, ft in t.fields)
     if isinstance(t, (Vector, Optional)):
         return has_compatible(t.elem)
+    if isinstance(t, Expected):
+        return has_compatible(t.value) or has_compatible(t.error)
     return False
 
 
@@ -420,6 +505,7 @@ class SpanField:
     count_off: int
     off_off: int
     sub: "Optional_[DeviceLayout]" = None  # ARRAY: the element record layout
+    kind: str = ""  # "map" / "multimap" / "umap" / "set" / ...: an associative container
 
 
 class ElemRecord(SpType):
@@ -502,7 +588,8 @@ def flatten(rtype: SpType) -> DeviceLayout:
             coff = place(4, 4)
             ooff = place(8, 8)
             ops.append((C.SPK_OP_ARRAY, coff, sub.stride, ooff))
-            spans.append(SpanField(path, ElemRecord(sub), coff, ooff, sub))
+            spans.append(SpanField(path, ElemRecord(sub), coff, ooff, sub,
+                                   getattr(t, "kind", "")))
             npf.append((path + ".n", "<u4", coff))
             npf.append((path + ".off", "<u8", ooff))
             for op in (sub.ops if not sub.trivial else [(C.SPK_OP_COPY, 0, sub.stride, 0)]):
@@ -515,25 +602,50 @@ def flatten(rtype: SpType) -> DeviceLayout:
             coff = place(4, 4)
             ooff = place(8, 8)
             ops.append((C.SPK_OP_SPAN, coff, t.elem.size, ooff))
-            spans.append(SpanField(path, t.elem, coff, ooff))
+            spans.append(SpanField(path, t.elem, coff, ooff, None, getattr(t, "kind", "")))
             npf.append((path + ".n", "<u4", coff))
             npf.append((path + ".off", "<u8", ooff))
+        elif isinstance(t, Optional) and not t.elem.trivial:
+            # SPK_OP_OPTGROUP: u32 has_value, U's fields inline (packer.hpp:
+            # 382-388; unpacker.hpp:1251-1275 drops U's errc)
+            ioff = place(4, 4)
+            ops.append((C.SPK_OP_OPTGROUP, ioff, 1, 0))
+            npf.append((path + ".has", "<u4", ioff))
+            visit(t.elem, path + ".value")
+            ops.append((C.SPK_OP_END, 0, 0, 0))
+        elif isinstance(t, Expected):
+            ioff = place(4, 4)
+            ops.append((C.SPK_OP_OPTGROUP, ioff, 2, 0))
+            npf.append((path + ".has", "<u4", ioff))
+            if not isinstance(t.value, Monostate):
+                visit(t.value, path + ".value")
+            ops.append((C.SPK_OP_END, 0, 0, 0))
+            if not isinstance(t.error, Monostate):
+                visit(t.error, path + ".error")
+            ops.append((C.SPK_OP_END, 0, 0, 0))
         elif isinstance(t, Optional):
-            if not t.elem.trivial:
-                raise NotImplementedError(
-                    f"{path}: optional of non-trivially-serializable "
-                    f"{t.elem.name} is outside the flat record model")
             coff = place(4, 4)
             ooff = place(8, 8)
             ops.append((C.SPK_OP_OPTION, coff, t.elem.size, ooff))
             spans.append(SpanField(path, t.elem, coff, ooff))
             npf.append((path + ".n", "<u4", coff))
             npf.append((path + ".off", "<u8", ooff))
-        elif isinstance(t, Compatible):
-            if t.elem.trivial is False or path.count(".") or path.count("["):
+        elif isinstance(t, Compatible) and not t.elem.trivial:
+            if path.count(".") or path.count("["):
                 raise NotImplementedError(
-                    f"{path}: compatible<{t.elem.name}> is only in the flat record model "
-                    "as a top-level member with a trivially serializable value")
+                    f"{path}: compatible<{t.elem.name}> is only in the record model "
+                    "as a member of the top-level record")
+            ioff = place(4, 4)
+            rank = versions.index(t.version)
+            ops.append((C.SPK_OP_CGROUP | (rank << 8), ioff, 1, 0))
+            npf.append((path + ".has", "<u4", ioff))
+            visit(t.elem, path + ".value")
+            ops.append((C.SPK_OP_END, 0, 0, 0))
+        elif isinstance(t, Compatible):
+            if path.count(".") or path.count("["):
+                raise NotImplementedError(
+                    f"{path}: compatible<{t.elem.name}> is only in the record model "
+                    "as a member of the top-level record")
             coff = place(4, 4)
             ooff = place(8, 8)
             rank = versions.index(t.version)
@@ -617,38 +729,58 @@ def flatten(rtype: SpType) -> DeviceLayout:
     return DeviceLayout(rtype, stride, merged, spans, npf, False)
 
 
+def _walk_levels(dev: DeviceLayout):
+    """(op, ARRAY nesting, group nesting) for every op but the ENDs: the
+    ops of an ARRAY element repeat per element; the ops of a VARIANT /
+    OPTGROUP / CGROUP group sit in the same record, present or not."""
+    from . import _capi as C
+    stack = []  # [kind, ENDs still to close]
+    for op in dev.ops:
+        k = op[0] & 0xFF
+        arr = sum(1 for s in stack if s[0] == C.SPK_OP_ARRAY)
+        grp = len(stack) - arr
+        if k == C.SPK_OP_END:
+            stack[-1][1] -= 1
+            if stack[-1][1] == 0:
+                stack.pop()
+            continue
+        yield op, arr, grp
+        if k == C.SPK_OP_ARRAY:
+            stack.append([k, 1])
+        elif k in (C.SPK_OP_VARIANT, C.SPK_OP_OPTGROUP, C.SPK_OP_CGROUP):
+            stack.append([k, op[2]])
+
+
 def min_record_wire_bytes(dev: DeviceLayout) -> int:
     """Fewest wire bytes one top-level record can take (each container count
-    >= 1 byte): bounds a decode's record capacity by the wire length."""
+    >= 1 byte; an absent optional / a variant's index 1 byte; compatible
+    members none: an older writer has none): bounds a decode's record
+    capacity by the wire length."""
     from . import _capi as C
-    total, depth = 0, 0
-    for k, _, sz, _ in dev.ops:
-        if k == C.SPK_OP_END:
-            depth -= 1
+    total = 0
+    for (k, _, sz, _), arr, grp in _walk_levels(dev):
+        k &= 0xFF
+        if arr or grp or k in (C.SPK_OP_COMPAT, C.SPK_OP_CGROUP):
             continue
-        if depth == 0 and (k & 0xFF) != C.SPK_OP_COMPAT:  # an older writer has none
-            total += sz if k == C.SPK_OP_COPY else 1
-        if k == C.SPK_OP_ARRAY:
-            depth += 1
+        total += sz if k == C.SPK_OP_COPY else 1
     return max(total, 1)
 
 
 def heap_caps_for_wire(dev: DeviceLayout, wire_len: int, rec_cap: int) -> List[int]:
     """Per-heap element capacities no decode of `wire_len` bytes can exceed:
-    a SPAN's elements take their size in wire bytes; an ARRAY element and a
-    nested OPTION at least one byte; a top-level OPTION one per record."""
+    a SPAN's elements take their size in wire bytes; an ARRAY element and an
+    OPTION inside an ARRAY element at least one byte; an OPTION / compatible
+    member of the top-level record one per record."""
     from . import _capi as C
-    caps, depth = [], 0
-    for k, _, sz, _ in dev.ops:
+    caps = []
+    for (k, _, sz, _), arr, grp in _walk_levels(dev):
+        k &= 0xFF
         if k == C.SPK_OP_SPAN:
             caps.append(wire_len // max(sz, 1) + 1)
         elif k == C.SPK_OP_OPTION:
-            caps.append(rec_cap if depth == 0 else wire_len + 1)
-        elif (k & 0xFF) == C.SPK_OP_COMPAT:
+            caps.append(rec_cap if arr == 0 else wire_len + 1)
+        elif k == C.SPK_OP_COMPAT:
             caps.append(rec_cap)
         elif k == C.SPK_OP_ARRAY:
             caps.append(wire_len + 1)
-            depth += 1
-        elif k == C.SPK_OP_END:
-            depth -= 1
     return caps

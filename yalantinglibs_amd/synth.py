@@ -125,14 +125,71 @@ AlOuter = S.Struct("AlOuter", [("a", AlA), ("b", AlB)], alignas=16)
 Packed = S.Struct("Packed", [("a", S.char), ("b", S.int32), ("c", S.int16)], pack=1)
 AlRec = S.Struct("AlRec", [("o", AlOuter), ("s", S.String()), ("p", Packed), ("e", Al8)])
 
+# optional / expected / compatible of values that are not trivially
+# serializable (SPK_OP_OPTGROUP / SPK_OP_CGROUP): the coro_rpc benchmark's
+# request type (ref src/coro_rpc/benchmark/api/ValidateRequest.h) and types.hpp
+ResponseCode = S.Struct("ResponseCode", [("retcode", S.int32),
+                                         ("error_message", S.Optional(S.String()))])
+AliMessage = S.Struct("AliMessage", [
+    ("message_type", S.int32), ("session_no", S.Optional(S.String())),
+    ("tint_flag", S.Optional(S.boolean)), ("source_entity", S.Optional(S.uint32)),
+    ("dest_entity", S.Optional(S.uint32)), ("client_ip", S.Optional(S.String())),
+    ("rc", S.Optional(ResponseCode)), ("version", S.Optional(S.int32))])
+ValidateRequest = S.Struct("ValidateRequest", [
+    ("msg", AliMessage), ("job_id", S.Optional(S.int32)),
+    ("query_keys", S.Vector(S.String())), ("clean", S.Optional(S.boolean))])
+Exp = S.Struct("Exp", [("id", S.int32), ("r", S.Expected(S.String(), S.int32)),
+                       ("q", S.Expected(Inner, S.String())),
+                       ("l", S.Optional(S.Vector(S.String()))),
+                       ("e", S.Expected(S.int64, ResponseCode))])
+CmpG = S.Struct("CmpG", [("id", S.int32), ("note", S.Compatible(S.String(), 20230101)),
+                         ("name", S.String()),
+                         ("ints", S.Compatible(S.Vector(S.int32), 20230101)),
+                         ("in", S.Compatible(Inner, 20240101)),
+                         ("rc", S.Compatible(ResponseCode, 20240101))])
+
+# the reference benchmark's shapes (ref src/struct_pack/benchmark/data_def.hpp)
+Vec3 = S.Struct("Vec3", [("x", S.float32), ("y", S.float32), ("z", S.float32)])
+Weapon = S.Struct("Weapon", [("name", S.String()), ("damage", S.int16)])
+Monster = S.Struct("Monster", [("pos", Vec3), ("mana", S.int16), ("hp", S.int16),
+                               ("name", S.String()), ("inventory", S.String()),
+                               ("color", S.uint8),  # enum Color : uint8_t
+                               ("weapons", S.Vector(Weapon)), ("equipped", Weapon),
+                               ("path", S.Vector(Vec3))])
+Rect2 = S.Struct("rect2<int32_t>", [("x", S.int32), ("y", S.int32), ("width", S.int32),
+                                    ("height", S.int32)],
+                 config=S.DISABLE_ALL_META_INFO | S.USE_FAST_VARINT | S.ENCODING_WITH_VARINT)
+
+# the other container kinds (types.hpp Lists / Maps) and the reference's
+# complicated_object (ref src/struct_pack/tests/test_struct.hpp:17-103)
+Lists = S.Struct("Lists", [("id", S.int32), ("names", S.List(S.String())),
+                           ("vals", S.List(S.int32, "std::deque")), ("pts", S.List(Inner))])
+Maps = S.Struct("Maps", [("id", S.int32), ("m", S.Map(S.int32, S.String())),
+                         ("s", S.Set(S.String())), ("mm", S.Map(S.int64, Inner, multi=True)),
+                         ("ms", S.Set(S.int32, multi=True)), ("mr", S.Map(S.String(), RecS))])
+CPerson = S.Struct("person", [("age", S.int32), ("name", S.String())])
+TrivialOne = S.Struct("trivial_one", [("a", S.int32), ("b", S.float64), ("c", S.float32)])
+Cplx = S.Struct("complicated_object", [
+    ("color", S.int32), ("a", S.int32), ("b", S.String()), ("c", S.Vector(CPerson)),
+    ("d", S.List(S.String())), ("e", S.List(S.int32, "std::deque")),
+    ("f", S.Map(S.int32, CPerson)), ("g", S.Map(S.int32, CPerson, multi=True)),
+    ("h", S.Set(S.String())), ("i", S.Set(S.int32, multi=True)),
+    ("j", S.Map(S.int32, CPerson, ordered=False)),
+    ("k", S.Map(S.int32, S.int32, multi=True, ordered=False)),
+    ("m", S.Array(CPerson, 2)), ("n", S.Array(CPerson, 2)), ("o", S.Pair(S.String(), CPerson)),
+    ("p", S.Vector(S.Array(TrivialOne, 2)))])
+
 CASE_TYPES = {"rec64": Rec64, "recs": RecS, "outer": Outer, "pad": Pad,
               "mixed": Mixed, "rect": RectInt, "rpcrect": RpcRect,
               "person": Person, "ints": Ints, "opt": Opt, "optp": OptP,
               "var": Var, "varp": VarP, "tags": Tags, "group": Group, "deep": Deep,
               "vnt": Vnt, "cmp": Cmp, "cmpold": CmpOld, "cmpnew": CmpNew, "fv": FV, "fve": FVE,
-              "fv32": FV32, "ev": EV, "al8": Al8, "alout": AlOuter, "packed": Packed, "alrec": AlRec}
-# vector<rect<int>> has its own ADL set_sp_config (benchmark data_def.hpp:69-72)
-VECTOR_CONFIG = {"rect": S.DISABLE_ALL_META_INFO}
+              "fv32": FV32, "ev": EV, "al8": Al8, "alout": AlOuter, "packed": Packed, "alrec": AlRec,
+              "valreq": ValidateRequest, "exp": Exp, "cmpg": CmpG, "monster": Monster,
+              "rect2": Rect2, "lists": Lists, "maps": Maps, "cplx": Cplx}
+# vector<rect<int>> / vector<rect2<int32_t>> have their own ADL set_sp_config
+# (benchmark data_def.hpp:69-72,90-94)
+VECTOR_CONFIG = {"rect": S.DISABLE_ALL_META_INFO, "rect2": S.DISABLE_ALL_META_INFO}
 
 
 def _chars(seed, idx, lens):
@@ -514,11 +571,422 @@ def make_batch(case: str, n: int, seed: int, param: int = 48):
         el["value.1.off"] = np.where(isstr == 1, _excl(sl), 0)
         heaps.append(el.view(np.uint8))
         heaps.append(chars)
+    elif case in ("valreq", "exp", "cmpg", "monster", "rect2"):
+        recs, heaps = _make_groups(case, L, recs, idx, seed, param)
+    elif case == "lists":  # fill(Lists&)
+        recs["id"] = i32(rnd(seed, idx, 0))
+        cnt = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+        recs["names.n"] = cnt
+        recs["names.off"] = _excl(cnt)
+        owner, j = _seg(cnt)
+        lens, chars = _tag_strings(_elem_word(seed, idx[owner], j))
+        heaps.append(_str_records(L.spans[0].sub, lens).view(np.uint8))
+        heaps.append(chars)
+        r3 = rnd(seed, idx, 3)
+        cnt = ((r3 >> np.uint64(8)) % np.uint64(7)).astype(np.int64)
+        recs["vals.n"] = cnt
+        recs["vals.off"] = _excl(cnt)
+        owner, j = _seg(cnt)
+        with np.errstate(over="ignore"):
+            heaps.append(i32(mix64(rnd(seed, idx[owner], 4) + j)).view(np.uint8))
+        cnt = (r3 % np.uint64(5)).astype(np.int64)
+        recs["pts.n"] = cnt
+        recs["pts.off"] = _excl(cnt)
+        owner, j = _seg(cnt)
+        with np.errstate(over="ignore"):
+            w = mix64(rnd(seed, idx[owner], 5) + j)
+        pts = np.zeros((len(w), 2), np.int32)
+        pts[:, 0] = i32(w)
+        pts.view(np.float32)[:, 1] = rf(w >> np.uint64(32))
+        heaps.append(pts.view(np.uint8).reshape(-1))
+    elif case == "maps":
+        recs, heaps = _make_maps(L, recs, idx, seed)
+    elif case == "cplx":
+        recs, heaps = _make_cplx(L, recs, n)
     else:
         raise KeyError(case)
     return L, recs, heaps
 
 
+def _opt_span(recs, path, has, lens):
+    """An optional / expected / compatible group holding a string at `path`:
+    the string's count and offset are set only where the group is present
+    (the decoder leaves an absent group's fields alone)."""
+    lens = np.where(has, lens, 0).astype(np.int64)
+    recs[path + ".n"] = lens
+    recs[path + ".off"] = np.where(has, _excl(lens), 0)
+    return lens
+
+
+def _opt_heap(recs, path, has, vals):
+    """A trivially serializable optional (SPK_OP_OPTION): count 0/1 and the
+    offset of the value among the present ones (absent ones too)."""
+    has = has.astype(np.int64)
+    recs[path + ".n"] = has
+    recs[path + ".off"] = _excl(has)
+    return np.ascontiguousarray(vals[has == 1]).view(np.uint8).reshape(-1)
+
+
+def _tag_heap(h, mask):
+    """Chars of tag_chars(h) where mask (lengths h % 13, else 0)."""
+    lens, chars = _tag_strings(h)
+    keep = np.repeat(mask, lens)
+    return np.where(mask, lens, 0).astype(np.int64), chars[keep]
+
+
+def _make_groups(case, L, recs, idx, seed, param):
+    n = len(idx)
+    heaps = []
+    bit = lambda w, k: ((w >> np.uint64(k)) & np.uint64(1)).astype(bool)  # noqa: E731
+    if case == "valreq":  # fill(ValidateRequest&)
+        b = rnd(seed, idx, 3)
+        recs["msg.message_type"] = i32(rnd(seed, idx, 0))
+        has = bit(b, 0)
+        recs["msg.session_no.has"] = has
+        lens = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+        lens = _opt_span(recs, "msg.session_no.value", has, lens)
+        heaps.append(_chars(seed, idx, lens))
+        heaps.append(_opt_heap(recs, "msg.tint_flag", bit(b, 1),
+                               (rnd(seed, idx, 4) & np.uint64(1)).astype(np.uint8)))
+        heaps.append(_opt_heap(recs, "msg.source_entity", bit(b, 2),
+                               rnd(seed, idx, 5).astype(np.uint32)))
+        heaps.append(_opt_heap(recs, "msg.dest_entity", bit(b, 3),
+                               rnd(seed, idx, 6).astype(np.uint32)))
+        has = bit(b, 4)
+        recs["msg.client_ip.has"] = has
+        lens, chars = _tag_heap(rnd(seed, idx, 7), has)
+        _opt_span(recs, "msg.client_ip.value", has, lens)
+        heaps.append(chars)
+        has = bit(b, 5)
+        recs["msg.rc.has"] = has
+        recs["msg.rc.value.retcode"] = np.where(has, i32(rnd(seed, idx, 8)), 0)
+        he = has & bit(b, 6)
+        recs["msg.rc.value.error_message.has"] = he
+        lens, chars = _tag_heap(rnd(seed, idx, 9), he)
+        _opt_span(recs, "msg.rc.value.error_message.value", he, lens)
+        heaps.append(chars)
+        heaps.append(_opt_heap(recs, "msg.version", bit(b, 7), i32(rnd(seed, idx, 10))))
+        heaps.append(_opt_heap(recs, "job_id", bit(b, 8), i32(rnd(seed, idx, 11))))
+        cnt = ((b >> np.uint64(16)) % np.uint64(5)).astype(np.int64)
+        recs["query_keys.n"] = cnt
+        recs["query_keys.off"] = _excl(cnt)
+        owner, j = _seg(cnt)
+        lens, chars = _tag_strings(_elem_word(seed, idx[owner], j))
+        heaps.append(_str_records(L.spans[8].sub, lens).view(np.uint8))
+        heaps.append(chars)
+        heaps.append(_opt_heap(recs, "clean", bit(b, 9),
+                               ((rnd(seed, idx, 12) >> np.uint64(1)) & np.uint64(1)).astype(np.uint8)))
+    elif case == "exp":  # fill(Exp&)
+        b = rnd(seed, idx, 3)
+        recs["id"] = i32(rnd(seed, idx, 0))
+        has = bit(b, 0)
+        recs["r.has"] = has
+        lens = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+        lens = _opt_span(recs, "r.value", has, lens)
+        heaps.append(_chars(seed, idx, lens))
+        recs["r.error"] = np.where(has, 0, i32(rnd(seed, idx, 4)))
+        has = bit(b, 1)
+        recs["q.has"] = has
+        inner = np.zeros((n, 8), np.uint8)
+        inner.view(np.int32).reshape(-1, 2)[:, 0] = np.where(has, i32(rnd(seed, idx, 5)), 0)
+        inner.view(np.float32).reshape(-1, 2)[:, 1] = np.where(has, rf(rnd(seed, idx, 6)), 0)
+        recs["q.value"] = inner.view("V8").reshape(n)
+        lens, chars = _tag_heap(rnd(seed, idx, 7), ~has)
+        _opt_span(recs, "q.error", ~has, lens)
+        heaps.append(chars)
+        has = bit(b, 2)
+        recs["l.has"] = has
+        cnt = np.where(has, ((b >> np.uint64(16)) % np.uint64(4)).astype(np.int64), 0)
+        recs["l.value.n"] = cnt
+        recs["l.value.off"] = np.where(has, _excl(cnt), 0)
+        owner, j = _seg(cnt)
+        lens, chars = _tag_strings(_elem_word(seed, idx[owner], j))
+        heaps.append(_str_records(L.spans[2].sub, lens).view(np.uint8))
+        heaps.append(chars)
+        has = bit(b, 3)
+        recs["e.has"] = has
+        recs["e.value"] = np.where(has, rnd(seed, idx, 8).view(np.int64), 0)
+        recs["e.error.retcode"] = np.where(has, 0, i32(rnd(seed, idx, 9)))
+        he = ~has & bit(b, 4)
+        recs["e.error.error_message.has"] = he
+        lens, chars = _tag_heap(rnd(seed, idx, 10), he)
+        _opt_span(recs, "e.error.error_message.value", he, lens)
+        heaps.append(chars)
+    elif case == "cmpg":  # fill(CmpG&)
+        m = rnd(seed, idx, 6)
+        recs["id"] = i32(rnd(seed, idx, 0))
+        has = bit(m, 0)
+        recs["note.has"] = has
+        lens, chars = _tag_heap(rnd(seed, idx, 2), has)
+        _opt_span(recs, "note.value", has, lens)
+        heaps.append(chars)
+        lens = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+        recs["name.n"] = lens
+        recs["name.off"] = _excl(lens)
+        heaps.append(_chars(seed, idx, lens))
+        has = bit(m, 1)
+        recs["ints.has"] = has
+        cnt = _opt_span(recs, "ints.value", has, ((m >> np.uint64(8)) % np.uint64(6)).astype(np.int64))
+        owner, j = _seg(cnt)
+        with np.errstate(over="ignore"):
+            vals = mix64(rnd(seed, idx[owner], 3) + j)
+        heaps.append(i32(vals).view(np.uint8))
+        has = bit(m, 2).astype(np.int64)
+        recs["in.n"] = has
+        recs["in.off"] = _excl(has)
+        sel = idx[has == 1]
+        inner = np.zeros((len(sel), 8), np.uint8)
+        inner.view(np.int32).reshape(-1, 2)[:, 0] = i32(rnd(seed, sel, 4))
+        inner.view(np.float32).reshape(-1, 2)[:, 1] = rf(rnd(seed, sel, 5))
+        heaps.append(inner.reshape(-1))
+        has = bit(m, 3)
+        recs["rc.has"] = has
+        recs["rc.value.retcode"] = np.where(has, i32(rnd(seed, idx, 7)), 0)
+        he = has & bit(m, 4)
+        recs["rc.value.error_message.has"] = he
+        lens, chars = _tag_heap(rnd(seed, idx, 8), he)
+        _opt_span(recs, "rc.value.error_message.value", he, lens)
+        heaps.append(chars)
+    elif case == "monster":  # fill(Monster&)
+        pos = np.zeros((n, 12), np.uint8)
+        pv = pos.view(np.float32).reshape(n, 3)
+        for k in range(3):
+            pv[:, k] = rf(rnd(seed, idx, 4 + k))
+        recs["pos"] = pos.view("V12").reshape(n)
+        r7, r9, r10 = rnd(seed, idx, 7), rnd(seed, idx, 9), rnd(seed, idx, 10)
+        recs["mana"] = r7.astype(np.uint16).view(np.int16)
+        recs["hp"] = (r7 >> np.uint64(16)).astype(np.uint16).view(np.int16)
+        lens = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+        recs["name.n"] = lens
+        recs["name.off"] = _excl(lens)
+        heaps.append(_chars(seed, idx, lens))
+        lens, chars = _tag_strings(rnd(seed, idx, 8))
+        recs["inventory.n"] = lens
+        recs["inventory.off"] = _excl(lens)
+        heaps.append(chars)
+        recs["color"] = (r9 % np.uint64(3)).astype(np.uint8)
+        cnt = ((r9 >> np.uint64(8)) % np.uint64(5)).astype(np.int64)
+        recs["weapons.n"] = cnt
+        recs["weapons.off"] = _excl(cnt)
+        owner, j = _seg(cnt)
+        h = _elem_word(seed, idx[owner], j)
+        wl, wc = _tag_strings(h)
+        el = np.zeros(len(h), dtype=L.spans[2].sub.dtype)
+        el["name.n"] = wl
+        el["name.off"] = _excl(wl)
+        el["damage"] = (h >> np.uint64(32)).astype(np.uint16).view(np.int16)
+        heaps.append(el.view(np.uint8))
+        heaps.append(wc)
+        lens, chars = _tag_strings(r10)
+        recs["equipped.name.n"] = lens
+        recs["equipped.name.off"] = _excl(lens)
+        heaps.append(chars)
+        recs["equipped.damage"] = (r10 >> np.uint64(40)).astype(np.uint16).view(np.int16)
+        cnt = ((r9 >> np.uint64(16)) % np.uint64(9)).astype(np.int64)
+        recs["path.n"] = cnt
+        recs["path.off"] = _excl(cnt)
+        owner, j = _seg(cnt)
+        with np.errstate(over="ignore"):
+            w = mix64(rnd(seed, idx[owner], 11) + j)
+        v = np.zeros((len(w), 3), np.float32)
+        v[:, 0] = rf(w)
+        v[:, 1] = rf(w >> np.uint64(32))
+        v[:, 2] = rf(mix64(w))
+        heaps.append(v.view(np.uint8).reshape(-1))
+    elif case == "rect2":  # fill(rect2<int32_t>&): FvGen of types.hpp
+        r7 = rnd(seed, idx, 7)
+        sh = r7 >> np.uint64(58)
+        z = r7 & np.uint64(0xFFFFFFFF)
+        for k, f in enumerate(("x", "y", "width", "height")):
+            x = np.where((z >> np.uint64(k)) & np.uint64(1), np.uint64(0), rnd(seed, idx, k) >> sh)
+            neg = rnd(seed, idx, k) & np.uint64(1)
+            v = np.where((z >> np.uint64(k)) & np.uint64(1), np.uint64(0), np.where(neg, ~x, x))
+            recs[f] = (v.astype(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.uint32).view(np.int32)
+    return recs, heaps
+
+
 def _spread(w):
     """spread() of types.hpp: magnitudes from 0 to 64 bits."""
     return w >> ((w >> np.uint64(58)) & np.uint64(63))
+
+
+# ---- per-record builders (associative containers and fixed objects) --------
+def _u64(x):
+    return int(np.uint64(x))
+
+
+def _mix(z):
+    return int(mix64(np.uint64(z & 0xFFFFFFFFFFFFFFFF)))
+
+
+def _rnd1(seed, i, k):
+    return int(rnd(seed, np.uint64(i), np.uint64(k)))
+
+
+def _tag1(h):
+    """tag_chars(h) of types.hpp for one word."""
+    h &= 0xFFFFFFFFFFFFFFFF
+    return bytes(ord("a") + ((_mix(h + (k >> 3)) >> ((k & 7) * 8)) & 0xFF) % 26
+                 for k in range(h % 13))
+
+
+def _s32(x):
+    x &= 0xFFFFFFFF
+    return x - (1 << 32) if x >> 31 else x
+
+
+class _Heaps:
+    """Device heaps built element by element (canonical: record order)."""
+
+    def __init__(self, L):
+        self.L = L
+        self.h = [bytearray() for _ in L.spans]
+
+    def put(self, k, data: bytes):
+        """append to heap k; returns the element offset"""
+        off = len(self.h[k]) // self.L.spans[k].elem.size
+        self.h[k] += data
+        return off
+
+    def string(self, k, s: bytes):
+        return len(s), self.put(k, s)
+
+    def out(self):
+        return [np.frombuffer(bytes(b), np.uint8).copy() for b in self.h]
+
+
+def _elem_records(sub, rows):
+    """element records of an ARRAY from per-element {field: value} dicts"""
+    e = np.zeros(len(rows), dtype=sub.dtype)
+    for j, r in enumerate(rows):
+        for f, v in r.items():
+            e[f][j] = v
+    return e.view(np.uint8).tobytes()
+
+
+def _make_maps(L, recs, idx, seed):
+    """fill(Maps&) of types.hpp with the containers' own order and key rules:
+    map / set keep the first of repeated keys, multimap / multiset all (equal
+    keys in insertion order), all sorted by key (std::less: signed integers,
+    strings bytewise)."""
+    H = _Heaps(L)
+    sp = {s.path: k for k, s in enumerate(L.spans)}
+    for i in map(int, idx):
+        recs["id"][i] = _s32(_rnd1(seed, i, 0))
+        b = _rnd1(seed, i, 3)
+        m = {}
+        for j in range(b % 5):
+            h = int(_elem_word(seed, np.uint64(i), np.uint64(j)))
+            m.setdefault((h % 7) - 3, _tag1(h >> 8))
+        rows = []
+        for key in sorted(m):
+            ln, off = H.string(sp["m[].second"], m[key])
+            rows.append({"first": key, "second.n": ln, "second.off": off})
+        recs["m.n"][i] = len(rows)
+        recs["m.off"][i] = H.put(sp["m"], _elem_records(L.spans[sp["m"]].sub, rows))
+        ss = sorted({_tag1(_mix(_rnd1(seed, i, 20) + j) % 5) for j in range((b >> 8) % 5)})
+        rows = []
+        for v in ss:
+            ln, off = H.string(sp["s[].value"], v)
+            rows.append({"value.n": ln, "value.off": off})
+        recs["s.n"][i] = len(rows)
+        recs["s.off"][i] = H.put(sp["s"], _elem_records(L.spans[sp["s"]].sub, rows))
+        mm = []
+        for j in range((b >> 16) % 4):
+            w = _mix(_rnd1(seed, i, 22) + j)
+            mm.append(((_mix(_rnd1(seed, i, 21) + j) % 3) - 1,
+                       np.array([_s32(w)], "<i4").tobytes() +
+                       rf(np.uint64(w >> 32)).astype("<f4").tobytes()))
+        mm.sort(key=lambda kv: kv[0])  # stable: equal keys keep insertion order
+        recs["mm.n"][i] = len(mm)
+        recs["mm.off"][i] = H.put(sp["mm"], b"".join(np.array([k], "<i8").tobytes() + v
+                                                    for k, v in mm))
+        ms = sorted((_mix(_rnd1(seed, i, 23) + j) % 7) - 3 for j in range((b >> 24) % 6))
+        recs["ms.n"][i] = len(ms)
+        recs["ms.off"][i] = H.put(sp["ms"], np.array(ms, "<i4").tobytes())
+        mr = {}
+        for j in range((b >> 32) % 3):
+            mr.setdefault(_tag1(_mix(_rnd1(seed, i, 24) + j) % 4 + 1), j)
+        rows = []
+        s2 = _mix(seed + i)
+        for key in sorted(mr):
+            j = mr[key]
+            kl, ko = H.string(sp["mr[].first"], key)
+            nm = bytes(_chars(np.uint64(s2), np.array([j], np.uint64),
+                              np.array([_rnd1(s2, j, 1) % 11], np.int64)))
+            nl, no = H.string(sp["mr[].second.name"], nm)
+            rows.append({"first.n": kl, "first.off": ko, "second.id": _s32(_rnd1(s2, j, 0)),
+                         "second.name.n": nl, "second.name.off": no,
+                         "second.v": float(rd(np.uint64(_rnd1(s2, j, 60))))})
+        recs["mr.n"][i] = len(rows)
+        recs["mr.off"][i] = H.put(sp["mr"], _elem_records(L.spans[sp["mr"]].sub, rows))
+    return recs, H.out()
+
+
+def _make_cplx(L, recs, n):
+    """create_complicated_object() (ref src/struct_pack/tests/test_struct.hpp:
+    82-103) in every record; padding bytes zero."""
+    H = _Heaps(L)
+    sp = {s.path: k for k, s in enumerate(L.spans)}
+
+    def person_rows(ps, path):
+        rows = []
+        for age, name in ps:
+            ln, off = H.string(sp[path], name)
+            rows.append({"age": age, "name.n": ln, "name.off": off})
+        return rows
+
+    def pair_rows(kvs, path):
+        rows = []
+        for k, (age, name) in kvs:
+            ln, off = H.string(sp[path], name)
+            rows.append({"first": k, "second.age": age, "second.name.n": ln, "second.name.off": off})
+        return rows
+
+    def arr(field, rows, k):
+        recs[field + ".n"][i] = len(rows)
+        recs[field + ".off"][i] = H.put(sp[field], _elem_records(L.spans[k].sub, rows))
+
+    def span(field, data: bytes):
+        esz = L.spans[sp[field]].elem.size
+        recs[field + ".n"][i] = len(data) // esz
+        recs[field + ".off"][i] = H.put(sp[field], data)
+
+    def string(field, s):
+        recs[field + ".n"][i], recs[field + ".off"][i] = H.string(sp[field], s)
+
+    for i in range(n):
+        recs["color"][i] = 0  # Color::red
+        recs["a"][i] = 42
+        string("b", b"hello")
+        arr("c", person_rows([(20, b"tom"), (22, b"jerry")], "c[].name"), sp["c"])
+        rows = []
+        for s_ in (b"hello", b"world"):
+            ln, off = H.string(sp["d[].value"], s_)
+            rows.append({"value.n": ln, "value.off": off})
+        arr("d", rows, sp["d"])
+        span("e", np.array([1, 2], "<i4").tobytes())
+        arr("f", pair_rows([(1, (20, b"tom"))], "f[].second.name"), sp["f"])
+        arr("g", pair_rows([(1, (20, b"tom")), (1, (22, b"jerry"))], "g[].second.name"), sp["g"])
+        rows = []
+        for s_ in (b"aa", b"bb"):
+            ln, off = H.string(sp["h[].value"], s_)
+            rows.append({"value.n": ln, "value.off": off})
+        arr("h", rows, sp["h"])
+        span("i", np.array([1, 2], "<i4").tobytes())
+        arr("j", pair_rows([(1, (20, b"tom"))], "j[].second.name"), sp["j"])
+        span("k", np.array([1, 2], "<i4").tobytes())
+        for f, ps in (("m", [(20, b"tom"), (22, b"jerry")]), ("n", [(15, b"tom"), (31, b"jerry")])):
+            for q, (age, name) in enumerate(ps):
+                recs[f"{f}[{q}].age"][i] = age
+                string(f"{f}[{q}].name", name)
+        string("o.first", b"aa")
+        recs["o.second.age"][i] = 20
+        string("o.second.name", b"tom")
+        t = np.zeros(4, dtype=np.dtype({"names": ["a", "b", "c"], "formats": ["<i4", "<f8", "<f4"],
+                                        "offsets": [0, 8, 16], "itemsize": 24}))
+        t["a"] = [1232114, 12315, 4, 1123115]
+        t["b"] = [1.7, 1.4, 0.7, 11111.4]
+        t["c"] = np.array([2.4, 2.6, 1.4, 2213321.6], np.float32)
+        span("p", t.tobytes())
+    return recs, H.out()
