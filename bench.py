@@ -19,7 +19,7 @@ At N=1 the same line carries `extra.configs`: the other BASELINE configs
 per-kernel times (HIP events around every codec launch, spk_trace_*), the
 dominant kernel's roofline and the reference CPU baseline on the same N.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2b|c3|c4|c5|cv]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2b|c3|c4|c5|cv|cm]
 """
 import argparse
 import json
@@ -45,11 +45,16 @@ CONFIGS = {
     "cv": ("var", 10_000_000, 16, "A",
            "varint records: 10M Var{var_int32_t, std::string len U[0,16], var_uint64_t, double, "
            "var_int64_t, var_uint32_t} per GPU (LEB128 lengths 1-10 B), one vector message"),
+    "cm": ("monster", 10_000_000, 20, "A",
+           "the reference benchmark's Monster (src/struct_pack/benchmark/data_def.hpp: Vec3, "
+           "2 x int16, 2 strings, enum, vector<Weapon{string,int16}>, Weapon, vector<Vec3>): "
+           "10M per GPU, one vector message"),
 }
-EXTRA = ["c2b", "c3", "c4", "c5", "cv"]  # timed beside the C2 headline at N=1
-SEEDS = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004, "var": 0x5EED000C}
+EXTRA = ["c2b", "c3", "c4", "c5", "cv", "cm"]  # timed beside the C2 headline at N=1
+SEEDS = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004, "var": 0x5EED000C,
+         "monster": 0x5EED001E}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PROFILE_ROUND = "r02"
+PROFILE_ROUND = "r03"
 
 C5_TYPES = [  # (case, share of messages, param, rpc function name) — coro_rpc bench shapes
     ("rpcrect", 1, 0, "echo_rect"),          # rect{point p1, p2}   (api/Rect.h)
@@ -97,6 +102,17 @@ def cpu_share():
     return max(1, min(aff, share) if share > 0 else aff), aff
 
 
+def cpu_quota():
+    """The cgroup CPU quota (cgroup v2 cpu.max, in CPUs), or None: the box
+    reports nproc / affinity of the whole machine, but its lease is a share."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -109,8 +125,10 @@ def cpu_model():
 
 
 def cpu_baseline(case, n, param, algo_bytes, per="record"):
-    """Reference CPU serialize+deserialize of the SAME n as the GPU leg
-    (threads = lease share, 10 reps: best and mean), plus one thread on n/10."""
+    """Reference CPU serialize+deserialize of the SAME n as the GPU leg on the
+    host cores this process may use (the lease's share: the pool sizes worker
+    pools to it, and its cgroup quota bounds them), median of 5 timed runs
+    after a warmup, plus one thread on n/10."""
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_bench")
     if not os.path.exists(exe):
         return None
@@ -124,27 +142,29 @@ def cpu_baseline(case, n, param, algo_bytes, per="record"):
             return None
         return json.loads(r.stdout.strip().splitlines()[-1])
 
-    full = run(n, threads, 10)
+    full = run(n, threads, 5)
     one = run(max(n // 10, 1), 1, 3)
     if not full:
         return None
     per_unit = algo_bytes / n
+    med = full["median_encode_s"] + full["median_decode_s"]
     best = full["encode_s"] + full["decode_s"]
     mean = full["mean_encode_s"] + full["mean_decode_s"]
-    out = {"value": round(per_unit * n / best / 2**30, 3), "unit": "GiB/s", "cores": threads,
+    out = {"value": round(per_unit * n / med / 2**30, 3), "unit": "GiB/s", "cores": threads,
            "kind": "reference",
            "sample": (f"{n} {case} {per}s (same N as the GPU leg), reference struct_pack "
                       f"serialize_to + deserialize_to (-O3 -DNDEBUG -DSTRUCT_PACK_OPTIMIZE), "
-                      f"{threads} threads x contiguous slices, best of 10"),
+                      f"{threads} threads x contiguous slices, median of 5 after a warmup"),
+           "best_gib_s": round(per_unit * n / best / 2**30, 3),
            "mean_gib_s": round(per_unit * n / mean / 2**30, 3),
-           f"m{per[:3]}_per_s": round(n / best / 1e6, 3),
-           "encode_s": full["encode_s"], "decode_s": full["decode_s"],
+           f"m{per[:3]}_per_s": round(n / med / 1e6, 3),
+           "encode_s": full["median_encode_s"], "decode_s": full["median_decode_s"],
            "host": {"cpu_model": cpu_model(), "nproc": os.cpu_count(), "affinity": aff,
-                    "threads_used": threads}}
+                    "cgroup_cpu_quota": cpu_quota(), "threads_used": threads}}
     if one:
         out["single_thread_gib_s"] = round(
-            per_unit * one["n"] / (one["encode_s"] + one["decode_s"]) / 2**30, 3)
-        out["single_thread_sample"] = f"{one['n']} {per}s, 1 thread, best of 3"
+            per_unit * one["n"] / (one["median_encode_s"] + one["median_decode_s"]) / 2**30, 3)
+        out["single_thread_sample"] = f"{one['n']} {per}s, 1 thread, median of 3"
     return out
 
 
@@ -166,7 +186,7 @@ class VecWorkload:
         self.cd = cd = SP.Codec(LY.case_layout(case), device=dev)
         n = self.n
         # this rank's shard: global records [rank*n, (rank+1)*n)
-        if case in ("rec64", "recs", "outer"):
+        if case in ("rec64", "recs", "outer", "monster"):
             self.batch = SP.synth_batch(cd, case, n, SEEDS[case], param, first=rank * n)
             self.data = f"spk_synth seeded {case}, seed {SEEDS[case]:#x}"
         else:  # host generator (yalantinglibs_amd/synth.py), uploaded before timing
@@ -228,6 +248,11 @@ class VecWorkload:
         if self.mode == self.SP.MODE_VECTOR:
             if self.cd.L.dev.trivial:  # one shift_copy per phase: records <-> body
                 return {"shift_copy_kernel": 4 * rb}
+            if any(op[0] & 0xFF in (5, 7, 8, 9, 10, 11) for op in self.cd.L.dev.ops):
+                # op-list interpreter (nested layouts): the encode writes each
+                # record's bytes; the chunked decode reads the wire to guess and
+                # walk the chunks, then again to write records + heaps
+                return {"nest_write": rb + wb, "nest_cemit": wb + rb, "nest_cspec": wb}
             # wait-free tile decoder: K1 reads the wire once, K4 reads it again
             # and writes the records + heaps
             return {"var_encode_write": rb + wb, "vec_tile_emit": wb + rb,
@@ -401,6 +426,45 @@ class C5Workload:
     def cpu_case(self):
         return "c5"
 
+    def host_path(self, torch, dev, reps=3):
+        """C5 with the coro_rpc socket buffers in host memory: the
+        connection's request bytes and frame offsets H2D from pinned buffers,
+        route + decode + encode as in the device step, then every type's
+        response frames and offsets D2H into pinned buffers. Serial, one
+        stream; the count read-back of the route stays in the step."""
+        stream = torch.cuda.current_stream(dev)
+        h_wire = torch.empty_like(self.wire, device="cpu").pin_memory()
+        h_wire.copy_(self.wire)
+        h_offs = torch.empty_like(self.offs, device="cpu").pin_memory()
+        h_offs.copy_(self.offs)
+        h_resp = [torch.empty(g["resp_len"], dtype=torch.uint8).pin_memory() for g in self.groups]
+        h_roff = [torch.empty_like(g["resp_offs"], device="cpu").pin_memory() for g in self.groups]
+        torch.cuda.synchronize(dev)
+
+        def one():
+            self.wire.copy_(h_wire, non_blocking=True)
+            self.offs.copy_(h_offs, non_blocking=True)
+            self.step(stream)
+            for g, hr, ho in zip(self.groups, h_resp, h_roff):
+                hr.copy_(g["resp"][:g["resp_len"]], non_blocking=True)
+                ho.copy_(g["resp_offs"], non_blocking=True)
+        one()
+        torch.cuda.synchronize(dev)
+        bad = self.check()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            one()
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t0) / reps
+        moved = int(self.wire.numel()) + 8 * int(self.offs.numel()) + sum(
+            g["resp_len"] + 8 * (g["n"] + 1) for g in self.groups)
+        return {"ms_per_step": round(dt * 1e3, 3), "gib_s": round(self.algo_bytes / dt / 2**30, 3),
+                "pcie_bytes": moved, "check": bad or "ok",
+                "note": "serial: H2D of the request stream + frame offsets (pinned), route, "
+                        "decode per type, encode the echo responses, D2H of every type's "
+                        "response frames + offsets (pinned); gib_s uses the device step's "
+                        "algorithmic bytes"}
+
 
 # ---------------------------------------------------------------------------
 # timing
@@ -521,12 +585,12 @@ def run_config(cfg, args, torch, dist, world, rank, dev, steps, warmup, settle, 
            "step_frac": round(wl.algo_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "detail": wl.config(), "data": wl.data}
     host = None
-    if args.host_path and rank == 0 and cfg != "c5":
-        host = host_path(wl, torch, dev)
+    if args.host_path and rank == 0:
+        host = wl.host_path(torch, dev) if cfg == "c5" else host_path(wl, torch, dev)
     if host:
         out["host_path"] = host
         try:
-            hp = host_path_pipelined(wl, torch, dev)
+            hp = None if cfg == "c5" else host_path_pipelined(wl, torch, dev)
         except Exception as e:  # never lose the line
             hp = {"error": f"{type(e).__name__}: {e}"}
         if hp:

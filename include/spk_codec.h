@@ -545,12 +545,21 @@ int spk_vector_header(const spk_layout *L, uint64_t total_n, uint32_t width,
 #define SPK_SYNTH_RPCRECT 4 /* C5 coro_rpc payload shapes */
 #define SPK_SYNTH_PERSON 5
 #define SPK_SYNTH_INTS 6
+#define SPK_SYNTH_MONSTER 7 /* the reference benchmark's Monster: six heaps */
 int spk_synth(int kind, uint64_t seed, uint64_t first, uint64_t n,
               uint32_t param, void *d_recs, void *d_heap,
               const uint64_t *d_heap_offsets, void *stream);
 /* per-record span counts for variable kinds (to size/prefix the heap) */
 int spk_synth_counts(int kind, uint64_t seed, uint64_t first, uint64_t n,
                      uint32_t param, uint64_t *d_counts, void *stream);
+/* kinds with several heaps (SPK_SYNTH_MONSTER): d_counts and d_heap_offsets
+ * are [heaps][n] columns (elements of each heap per record; their exclusive
+ * prefix sums); d_heaps a HOST array of the heaps' device pointers */
+int spk_synth_counts_ex(int kind, uint64_t seed, uint64_t first, uint64_t n,
+                        uint32_t param, uint64_t *d_counts, void *stream);
+int spk_synth_ex(int kind, uint64_t seed, uint64_t first, uint64_t n, uint32_t param,
+                 void *d_recs, void *const *d_heaps, const uint64_t *d_heap_offsets,
+                 void *stream);
 
 /* ---- runtime helpers ----------------------------------------------------
  * Device / pinned-host memory, async copies and streams, so that a front end

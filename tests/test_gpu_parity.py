@@ -393,7 +393,8 @@ def test_screen_defeating_payload_bounded_time():
 @pytest.mark.parametrize("kind,case,param", [("rec64", "rec64", 0), ("recs", "recs", 48),
                                               ("outer", "outer", 16), ("rpcrect", "rpcrect", 0),
                                               ("person", "person", 48),
-                                              ("ints", "ints", 1000)])
+                                              ("ints", "ints", 1000),
+                                              ("monster", "monster", 20)])
 def test_device_synth_matches_host_generator(kind, case, param):
     cd = codec_for(case)
     n = 3001

@@ -63,6 +63,7 @@ SPK_SYNTH_OUTER = 3
 SPK_SYNTH_RPCRECT = 4
 SPK_SYNTH_PERSON = 5
 SPK_SYNTH_INTS = 6
+SPK_SYNTH_MONSTER = 7
 
 
 class spk_op(ct.Structure):
@@ -124,7 +125,8 @@ ORACLE_PATH = os.path.join(_ROOT, "oracle", "libspk_oracle.so")
 # exported symbols of include/spk_codec.h (checked by tests/test_capi.py)
 CODEC_SYMBOLS = ["spk_abi_version", "spk_errc_message", "spk_layout_check",
                  "spk_workspace_bytes", "spk_plan", "spk_plan_ex", "spk_encode", "spk_decode",
-                 "spk_synth", "spk_synth_counts", "spk_encode_body",
+                 "spk_synth", "spk_synth_counts", "spk_synth_ex", "spk_synth_counts_ex",
+                 "spk_encode_body",
                  "spk_vector_header", "spk_encode_framed", "spk_decode_framed",
                  "spk_decode_body", "spk_parse_vector_header",
                  "spk_decode_shard_index", "spk_decode_shard_emit",
@@ -179,6 +181,8 @@ def _bind_codec(lib):
                                       ct.POINTER(P), ct.POINTER(U64), P, P, P,
                                       ct.c_size_t, P]
     lib.spk_synth_counts.argtypes = [ct.c_int, U64, U64, U64, ct.c_uint32, P, P]
+    lib.spk_synth_counts_ex.argtypes = [ct.c_int, U64, U64, U64, ct.c_uint32, P, P]
+    lib.spk_synth_ex.argtypes = [ct.c_int, U64, U64, U64, ct.c_uint32, P, ct.POINTER(P), P, P]
     lib.spk_route_workspace_bytes.restype = ct.c_size_t
     lib.spk_route_workspace_bytes.argtypes = [U64, ct.c_uint32]
     lib.spk_route_frames.argtypes = [P, U64, P, U64, ct.c_uint32, ct.POINTER(ct.c_uint32),

@@ -34,6 +34,10 @@ struct NLayout {
   uint8_t crank[SPK_MAX_OPS]; // COMPAT: its version rank (ops[i].kind is SPK_OP_COMPAT)
   uint32_t n_ops, stride, n_heaps, n_ranks;
   uint32_t fv_cnt, fv_has64, fv_bits;  // USE_FAST_VARINT group: FVAR ops, a 64-bit one, bitset bytes
+  // screen of a guessed record start: the first count (SPAN / ARRAY) sits
+  // scr_off fixed bytes into the record (~0: no such count before anything
+  // data-dependent); its elements take at least scr_esz bytes each
+  uint32_t scr_off, scr_esz;
 };
 
 // layouts the interpreter runs: an ARRAY (element layouts), a VARIANT, an
@@ -84,6 +88,20 @@ static NLayout make_nlayout(const spk_layout *L) {
   }
   N.n_heaps = h;
   N.fv_bits = N.fv_cnt ? (N.fv_cnt + 2 + 7) / 8 : 0;
+  N.scr_off = ~0u;
+  uint32_t pre = 0;
+  for (uint32_t i = 0; i < L->n_ops && !N.fv_cnt; ++i) {
+    const uint32_t k = SPK_OP_KIND(L->ops[i].kind);
+    if (k == SPK_OP_COPY) {
+      pre += L->ops[i].size;
+      continue;
+    }
+    if (k == SPK_OP_SPAN || k == SPK_OP_ARRAY) {
+      N.scr_off = pre;
+      N.scr_esz = k == SPK_OP_SPAN ? L->ops[i].size : 1;
+    }
+    break;
+  }
   return N;
 }
 
@@ -114,6 +132,16 @@ __device__ __forceinline__ void n_copy(uint8_t *d, const uint8_t *s, uint64_t n)
     for (; i + 8 <= n; i += 8)
       *reinterpret_cast<uint64_t *>(d + i) = *reinterpret_cast<const uint64_t *>(s + i);
   for (; i < n; ++i) d[i] = s[i];
+}
+
+// the layout in LDS: the interpreter reads an op per step, and a kernel
+// argument indexed per lane would be fetched from memory every time
+__device__ __forceinline__ void n_stage(NLayout &dst, const NLayout &src) {
+  static_assert(sizeof(NLayout) % 4 == 0, "NLayout staged as words");
+  const uint32_t *s = reinterpret_cast<const uint32_t *>(&src);
+  uint32_t *d = reinterpret_cast<uint32_t *>(&dst);
+  for (uint32_t k = threadIdx.x; k < sizeof(NLayout) / 4; k += blockDim.x) d[k] = s[k];
+  __syncthreads();
 }
 
 // one open ARRAY or group on the interpreter's stack
@@ -919,7 +947,7 @@ constexpr uint64_t kNUnk = ~0ull - 1;  // entry / exit unknown (no plausible sta
 constexpr uint64_t kNFail = ~0ull;     // the path failed before this point
 
 struct CWs {
-  size_t ent, ext, err, cols, part, end;  // cols: [1 + heaps][nch] u64 (count, heap use)
+  size_t ent, ext, err, dirty, cols, part, end;  // cols: [1 + heaps][nch] u64 (count, heap use)
 };
 static uint64_t cws_chunks(uint64_t wire_len) { return wire_len / kNCh + 2; }
 static CWs cws_layout(uint64_t wire_len, uint32_t n_heaps) {
@@ -934,6 +962,7 @@ static CWs cws_layout(uint64_t wire_len, uint32_t n_heaps) {
   f.ent = take(nch * 8);
   f.ext = take(nch * 8);
   f.err = take(nch * 4);
+  f.dirty = take((nch + 63) / 64 * 8);
   f.cols = take(nch * 8 * (1 + n_heaps));
   f.part = take(nscan_part_bytes(nch, 1 + n_heaps));
   f.end = off;
@@ -987,16 +1016,18 @@ struct NEnc {
 // message size (MESSAGES); the longest container into ctl->maxc
 __global__ __launch_bounds__(256) void nest_size(NEnc e, const uint8_t *__restrict__ recs,
                                                  uint64_t *__restrict__ a, uint8_t *ws) {
+  __shared__ NLayout N;
+  n_stage(N, e.N);
   NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t m = 0;
   if (i < e.n) {
-    const NSize s = n_size(e.N, recs + i * e.N.stride, e.heaps, 0, e.N.n_ops, true);
+    const NSize s = n_size(N, recs + i * N.stride, e.heaps, 0, N.n_ops, true);
     m = s.maxc;
     if (e.mode == SPK_MODE_MESSAGES) {
       const uint32_t w = width_of(s.maxc);
       const uint64_t body = s.bytes + s.cnts * w;
-      const uint32_t hl = e.N.n_ranks ? compat_hdr(nullptr, e.fmt, w, body)
+      const uint32_t hl = N.n_ranks ? compat_hdr(nullptr, e.fmt, w, body)
                                       : hdr_shape(e.fmt.flags, e.fmt.literal_len, w).len;
       a[i] = e.fpre + hl + body;
       a[e.n + i] = s.bytes;
@@ -1030,14 +1061,16 @@ __global__ void nest_ctl_init(uint8_t *ws) {
 // column 2 + rk: the bytes of record i in the version pass of rank rk
 __global__ void nest_vec_sizes(NEnc e, const uint8_t *__restrict__ recs,
                                uint64_t *__restrict__ a, uint8_t *ws) {
+  __shared__ NLayout N;
+  n_stage(N, e.N);
   const NCtl *ctl = reinterpret_cast<const NCtl *>(ws + kWsCtl);
   const uint64_t mx = ctl->maxc > e.n ? ctl->maxc : e.n;
   const uint32_t w = e.fixed_w ? e.fixed_w : width_of(mx);
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < e.n;
        i += (uint64_t)gridDim.x * blockDim.x) {
     a[i] = a[i] + a[e.n + i] * w;
-    for (uint32_t rk = 0; rk < e.N.n_ranks; ++rk)
-      a[(2 + rk) * e.n + i] = n_compat_size(e.N, recs + i * e.N.stride, e.heaps, rk, w);
+    for (uint32_t rk = 0; rk < N.n_ranks; ++rk)
+      a[(2 + rk) * e.n + i] = n_compat_size(N, recs + i * N.stride, e.heaps, rk, w);
   }
 }
 
@@ -1087,6 +1120,8 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
                                                   uint8_t *ws, uint8_t *__restrict__ out,
                                                   uint64_t *__restrict__ msg_offsets,
                                                   uint32_t with_header, uint64_t out_cap) {
+  __shared__ NLayout N;
+  n_stage(N, e.N);
   const NCtl *ctl = reinterpret_cast<const NCtl *>(ws + kWsCtl);
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e.mode == SPK_MODE_VECTOR) {
@@ -1095,10 +1130,10 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
     uint32_t hl = 0;
     const uint64_t tot0 = e.n ? part[nb] : 0;
     uint64_t totc = 0;
-    for (uint32_t rk = 0; rk < e.N.n_ranks; ++rk) totc += e.n ? part[(2 + rk) * (nb + 1) + nb] : 0;
+    for (uint32_t rk = 0; rk < N.n_ranks; ++rk) totc += e.n ? part[(2 + rk) * (nb + 1) + nb] : 0;
     uint8_t hb[4 + 1 + 8 + SPK_MAX_LITERAL + 1];
     if (with_header)
-      hl = e.N.n_ranks ? compat_hdr(hb, e.fmt, w, w + tot0 + totc) : write_hdr(hb, e.fmt, w);
+      hl = N.n_ranks ? compat_hdr(hb, e.fmt, w, w + tot0 + totc) : write_hdr(hb, e.fmt, w);
     // the whole message must fit, or nothing is written (spk_encode's
     // contract; the caller reads the plan's total_bytes)
     if ((with_header ? hl + w : 0) + tot0 + totc > out_cap) return;
@@ -1110,12 +1145,12 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
       hl += w;
     }
     if (i < e.n) {
-      const uint8_t *rec = recs + i * e.N.stride;
-      n_write(e.N, rec, e.heaps, w, out + hl + off[i], 0, e.N.n_ops, true);
+      const uint8_t *rec = recs + i * N.stride;
+      n_write(N, rec, e.heaps, w, out + hl + off[i], 0, N.n_ops, true);
       // version passes after every record's main pass (packer.hpp:66-78)
       uint64_t sec = hl + tot0;
-      for (uint32_t rk = 0; rk < e.N.n_ranks; ++rk) {
-        n_write_compat(e.N, rec, e.heaps, rk, w, out + sec + off[(2 + rk) * e.n + i]);
+      for (uint32_t rk = 0; rk < N.n_ranks; ++rk) {
+        n_write_compat(N, rec, e.heaps, rk, w, out + sec + off[(2 + rk) * e.n + i]);
         sec += part[(2 + rk) * (nb + 1) + nb];
       }
     }
@@ -1124,18 +1159,18 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
   if ((e.n ? part[nb] : 0) > out_cap) return;  // every message with its frame
   if (i == 0 && msg_offsets) msg_offsets[e.n] = e.n ? part[nb] : 0;
   if (i >= e.n) return;
-  const uint8_t *rec = recs + i * e.N.stride;
-  const NSize s = n_size(e.N, rec, e.heaps, 0, e.N.n_ops, true);
+  const uint8_t *rec = recs + i * N.stride;
+  const NSize s = n_size(N, rec, e.heaps, 0, N.n_ops, true);
   const uint32_t w = width_of(s.maxc);
   uint8_t *p = out + off[i];
   if (msg_offsets) msg_offsets[i] = off[i];
   uint8_t *m = p + e.fpre;
   uint8_t hb[4 + 1 + 8 + SPK_MAX_LITERAL + 1];
-  const uint32_t hl = e.N.n_ranks ? compat_hdr(hb, e.fmt, w, s.bytes + s.cnts * w)
+  const uint32_t hl = N.n_ranks ? compat_hdr(hb, e.fmt, w, s.bytes + s.cnts * w)
                                   : write_hdr(hb, e.fmt, w);
   for (uint32_t b = 0; b < hl; ++b) m[b] = hb[b];
-  uint8_t *q = n_write(e.N, rec, e.heaps, w, m + hl, 0, e.N.n_ops, true);
-  for (uint32_t rk = 0; rk < e.N.n_ranks; ++rk) q = n_write_compat(e.N, rec, e.heaps, rk, w, q);
+  uint8_t *q = n_write(N, rec, e.heaps, w, m + hl, 0, N.n_ops, true);
+  for (uint32_t rk = 0; rk < N.n_ranks; ++rk) q = n_write_compat(N, rec, e.heaps, rk, w, q);
   if (e.fpre) {
     for (uint32_t b = 0; b < e.fpre; ++b) p[b] = e.ftmpl[b];
     const uint32_t mlen = (uint32_t)(q - m);
@@ -1289,6 +1324,7 @@ __global__ void nest_vhdr(NDec a, const uint8_t *__restrict__ wire, uint8_t *ws,
 
 struct CPtrs {
   uint64_t *ent, *ext, *cols;  // cols[0][c]: records; cols[1 + k][c]: heap k use
+  unsigned long long *dirty;   // bitmap of the chunks the rounds left open
   int32_t *err;
   uint64_t nch_cap;            // column stride = chunks the wire allows (the scan's length)
 };
@@ -1297,10 +1333,11 @@ struct CWalk {
   uint64_t ext, cnt;
   int32_t err;
 };
+
 // the records of the path from s that start before c1; lim < wire_len makes
 // the walk speculative (kNUnk when a read would pass lim); hs += heap use
-__device__ CWalk nc_walk(const NDec &a, const uint8_t *__restrict__ wire, uint64_t s, uint64_t c1,
-                         uint64_t lim, uint32_t w, uint64_t *hs) {
+__device__ CWalk nc_walk(const NLayout &N, const NDec &a, const uint8_t *__restrict__ wire,
+                         uint64_t s, uint64_t c1, uint64_t lim, uint32_t w, uint64_t *hs) {
   CWalk r = {s, 0, 0};
   if (s == kNFail || s == kNUnk) return r;
   const bool bounded = lim < a.wire_len;
@@ -1308,8 +1345,8 @@ __device__ CWalk nc_walk(const NDec &a, const uint8_t *__restrict__ wire, uint64
   uint32_t ovf = 0;
   while (pos < c1) {
     const uint64_t before = pos;
-    const int32_t ec = n_read(a.N, wire, pos, lim, w, nullptr, nullptr, hs, a.heap_cap, &ovf, 0,
-                              a.N.n_ops, true, bounded);
+    const int32_t ec = n_read(N, wire, pos, lim, w, nullptr, nullptr, hs, a.heap_cap, &ovf, 0,
+                              N.n_ops, true, bounded);
     if (ec == kNLimit) {
       r.ext = kNUnk;
       return r;
@@ -1342,9 +1379,11 @@ __device__ __forceinline__ void nc_store(const CPtrs &P, uint32_t H, uint64_t c,
 // speculation: chunk c's entry guessed (chunk 0's is exact) and its records walked
 __global__ __launch_bounds__(kNT) void nest_cspec(NDec a, const uint8_t *__restrict__ wire,
                                                   const uint8_t *ws, CPtrs P) {
+  __shared__ NLayout N;
+  n_stage(N, a.N);
   const NCtl *ctl = reinterpret_cast<const NCtl *>(ws + kWsCtl);
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t w = ctl->w, H = a.N.n_heaps;
+  const uint32_t w = ctl->w, H = N.n_heaps;
   uint64_t hs[SPK_MAX_SPANS];
   for (uint32_t k = 0; k < H; ++k) hs[k] = 0;
   if (c >= ctl->nch) {  // past the header's chunks: nothing in the scanned columns
@@ -1357,21 +1396,29 @@ __global__ __launch_bounds__(kNT) void nest_cspec(NDec a, const uint8_t *__restr
   CWalk r = {kNUnk, 0, 0};
   if (c == 0) {
     ent = c0;
-    r = nc_walk(a, wire, c0, c1, len, w, hs);
+    r = nc_walk(N, a, wire, c0, c1, len, w, hs);
   } else {
+    // the first byte from which two whole records parse (a bounded walk)
     const uint64_t lim = c1 + kNBound < len ? c1 + kNBound : len;
-    for (uint64_t q = c0; q < c1; ++q) {
-      for (uint32_t k = 0; k < H; ++k) hs[k] = 0;
-      r = nc_walk(a, wire, q, c1, lim, w, hs);
-      if (r.ext != kNUnk && r.ext != kNFail) {  // whole records up to the chunk's end
-        ent = q;
-        break;
+    for (uint64_t q = c0; q < c1 && ent == kNUnk; ++q) {
+      if (N.scr_off != ~0u) {  // the first count must fit the bytes the walk may use
+        const uint64_t x = q + N.scr_off;
+        if (x + w > lim) continue;
+        const uint64_t cnt = ld_le(wire + x, w);
+        if (cnt > (lim - x - w) / N.scr_esz) continue;
       }
+      uint64_t p = q;
+      uint32_t ovf = 0;
+      int32_t ec = 0;
+      for (int k2 = 0; k2 < 2 && !ec && p < lim; ++k2)
+        ec = n_read(N, wire, p, lim, w, nullptr, nullptr, hs, a.heap_cap, &ovf, 0, N.n_ops,
+                    true, lim < len);
+      if (!ec) ent = q;
     }
-    if (ent == kNUnk) {
-      r = CWalk{kNUnk, 0, 0};
-      for (uint32_t k = 0; k < H; ++k) hs[k] = 0;
-    }
+    for (uint32_t k = 0; k < H; ++k) hs[k] = 0;
+    // its records up to the chunk's end (kNUnk / kNFail when that walk fails:
+    // the rounds walk the chunk again from its predecessor's exit)
+    if (ent != kNUnk) r = nc_walk(N, a, wire, ent, c1, lim, w, hs);
   }
   nc_store(P, H, c, ent, r, hs);
 }
@@ -1381,22 +1428,29 @@ __global__ __launch_bounds__(kNT) void nest_cspec(NDec a, const uint8_t *__restr
 __global__ __launch_bounds__(kNT) void nest_cround(NDec a, const uint8_t *__restrict__ wire,
                                                    uint8_t *ws, CPtrs P, int round) {
   NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
-  if (round > 0 && !ctl->changed[round - 1]) return;  // settled
+  if (round > 0 && !ctl->changed[round - 1]) return;  // settled (the same for every lane)
+  __shared__ NLayout N;
+  n_stage(N, a.N);
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c == 0 || c >= ctl->nch) return;
   const uint64_t E = __atomic_load_n(&P.ext[c - 1], __ATOMIC_RELAXED);
   const uint64_t ent = P.ent[c], ext = P.ext[c];
   if (E == ent && ext != kNUnk) return;
-  if (E == kNUnk) {  // the predecessor is open itself
+  // walk again only from the exit of a predecessor that agrees with its own
+  // predecessor: a predecessor that is about to change would hand a wrong
+  // entry on, and the wrong exit one chunk further each round
+  const bool pred_open =
+      E == kNUnk || (c >= 2 && (__atomic_load_n(&P.ext[c - 2], __ATOMIC_RELAXED) != P.ent[c - 1]));
+  if (pred_open) {
     atomicAdd(&ctl->changed[round], 1ull);
     return;
   }
   const uint64_t len = a.wire_len, c0 = ctl->p0 + c * kNCh;
   const uint64_t c1 = c0 + kNCh < len ? c0 + kNCh : len;
-  const uint32_t H = a.N.n_heaps;
+  const uint32_t H = N.n_heaps;
   uint64_t hs[SPK_MAX_SPANS];
   for (uint32_t k = 0; k < H; ++k) hs[k] = 0;
-  const CWalk r = nc_walk(a, wire, E, c1, len, ctl->w, hs);
+  const CWalk r = nc_walk(N, a, wire, E, c1, len, ctl->w, hs);
   nc_store(P, H, c, E, r, hs);
   atomicAdd(&ctl->rewalks, 1ull);
   if (r.ext != ext) atomicAdd(&ctl->changed[round], 1ull);
@@ -1412,56 +1466,69 @@ __global__ __launch_bounds__(kNT) void nest_cverify(uint8_t *ws, CPtrs P) {
     atomicMin(&ctl->cmin, (unsigned long long)c);
     atomicMax(&ctl->cmax, (unsigned long long)c);
     atomicAdd(&ctl->ndirty, 1ull);
+    atomicOr(&P.dirty[c >> 6], 1ull << (c & 63));
   }
 }
 
-// one wave settles the open chunks in order: 64 chunks checked per step, the
-// first disagreeing one walked again from its predecessor's exit (carried in a
-// register, so the wave never re-reads what it wrote)
+// one wave settles the open chunks in order: the next open chunk from the
+// bitmap (64 words = 4096 chunks per look), walked again from its
+// predecessor's exit; a walk that moves a chunk's exit makes the next chunk
+// open too. (A chunk is walked by lane 0 and its exit carried in a register,
+// so the wave never re-reads what it wrote.)
 __global__ __launch_bounds__(64) void nest_cfix(NDec a, const uint8_t *__restrict__ wire,
                                                 uint8_t *ws, CPtrs P) {
   NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
   if (!ctl->ndirty) return;
+  __shared__ NLayout N;
+  n_stage(N, a.N);
   const uint32_t lane = threadIdx.x;
-  const uint64_t nch = ctl->nch, cmax = ctl->cmax, len = a.wire_len;
-  const uint32_t H = a.N.n_heaps;
-  uint64_t c = ctl->cmin;        // >= 1: chunk 0 is never open
-  uint64_t pext = P.ext[c - 1];  // exit of chunk c - 1 (settled)
+  const uint64_t nch = ctl->nch, len = a.wire_len;
+  const uint64_t nwords = (nch + 63) >> 6;
+  const uint32_t H = N.n_heaps;
+  uint64_t c = ctl->cmin;  // >= 1: chunk 0 is never open
+  bool carry = false;      // chunk c follows a chunk whose exit moved
+  uint64_t cext = 0;       // that exit
   uint64_t nfix = 0;
   while (c < nch) {
-    const uint64_t cc = c + lane;
-    const bool valid = cc < nch;
-    const uint64_t my_ent = valid ? P.ent[cc] : 0, my_ext = valid ? P.ext[cc] : 0;
-    uint64_t prev = __shfl_up(my_ext, 1);  // lane l - 1's exit
-    if (lane == 0) prev = pext;
-    const bool bad = valid && (prev != my_ent || my_ext == kNUnk);
-    const uint64_t m = __ballot(bad);
-    if (!m) {
-      if (c + 64 > cmax) break;  // every chunk past cmax agreed, and still does
-      pext = __shfl(my_ext, 63);
-      c += 64;
-      continue;
+    if (!carry) {  // the next open chunk at or after c
+      uint64_t found = ~0ull;
+      for (uint64_t w0 = c >> 6; w0 < nwords && found == ~0ull; w0 += 64) {
+        const uint64_t wi = w0 + lane;
+        uint64_t bits = wi < nwords ? P.dirty[wi] : 0;
+        if (wi == (c >> 6)) bits &= ~0ull << (c & 63);
+        const uint64_t m = __ballot(bits != 0);
+        if (m) {
+          const uint32_t l = (uint32_t)__ffsll((unsigned long long)m) - 1;
+          const uint64_t b = __shfl(bits, (int)l);
+          found = ((w0 + l) << 6) + (uint64_t)(__ffsll((unsigned long long)b) - 1);
+        }
+      }
+      if (found == ~0ull || found >= nch) break;
+      c = found;
     }
-    const uint32_t l = (uint32_t)__ffsll((unsigned long long)m) - 1;
-    const uint64_t f = c + l;
-    const uint64_t E = __shfl(prev, (int)l), ext_old = __shfl(my_ext, (int)l);
-    uint64_t nx = 0;
+    uint64_t nx = 0, moved = 0;
     if (lane == 0) {
-      const uint64_t c0 = ctl->p0 + f * kNCh;
-      const uint64_t c1 = c0 + kNCh < len ? c0 + kNCh : len;
-      uint64_t hs[SPK_MAX_SPANS];
-      for (uint32_t k = 0; k < H; ++k) hs[k] = 0;
-      // (E is settled: never kNUnk; guarded anyway)
-      const CWalk r = E == kNUnk ? CWalk{kNFail, 0, SPK_ERRC_INTERNAL}
-                                 : nc_walk(a, wire, E, c1, len, ctl->w, hs);
-      nc_store(P, H, f, E == kNUnk ? kNFail : E, r, hs);
-      nx = r.ext;
+      const uint64_t E = carry ? cext : P.ext[c - 1];
+      const uint64_t ent = P.ent[c], old = P.ext[c];
+      if (E != ent || old == kNUnk) {
+        const uint64_t c0 = ctl->p0 + c * kNCh;
+        const uint64_t c1 = c0 + kNCh < len ? c0 + kNCh : len;
+        uint64_t hs[SPK_MAX_SPANS];
+        for (uint32_t k = 0; k < H; ++k) hs[k] = 0;
+        // (E is settled: never kNUnk; guarded anyway)
+        const CWalk r = E == kNUnk ? CWalk{kNFail, 0, SPK_ERRC_INTERNAL}
+                                   : nc_walk(N, a, wire, E, c1, len, ctl->w, hs);
+        nc_store(P, H, c, E == kNUnk ? kNFail : E, r, hs);
+        nx = r.ext;
+        moved = r.ext != old;
+        ++nfix;
+      }
     }
+    moved = __shfl(moved, 0);
     nx = __shfl(nx, 0);
-    ++nfix;
-    pext = nx;
-    c = f + 1;
-    if (nx == ext_old && c > cmax) break;  // nothing past cmax disagreed, nor does now
+    carry = moved != 0;
+    cext = nx;
+    ++c;
   }
   if (lane == 0) ctl->fixed = nfix;
 }
@@ -1470,6 +1537,8 @@ __global__ __launch_bounds__(64) void nest_cfix(NDec a, const uint8_t *__restric
 // scanned columns; the record the path fails at sets the errc
 __global__ __launch_bounds__(kNT) void nest_cemit(NDec a, const uint8_t *__restrict__ wire,
                                                   uint8_t *ws, CPtrs P, uint8_t *__restrict__ recs) {
+  __shared__ NLayout N;
+  n_stage(N, a.N);
   NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= ctl->nch) return;
@@ -1478,15 +1547,15 @@ __global__ __launch_bounds__(kNT) void nest_cemit(NDec a, const uint8_t *__restr
   if (first >= n || s == kNFail || s == kNUnk) return;
   const uint64_t len = a.wire_len, c0 = ctl->p0 + c * kNCh;
   const uint64_t c1 = c0 + kNCh < len ? c0 + kNCh : len;
-  const uint32_t H = a.N.n_heaps, w = ctl->w;
+  const uint32_t H = N.n_heaps, w = ctl->w;
   uint64_t used[SPK_MAX_SPANS];
   for (uint32_t k = 0; k < H; ++k) used[k] = P.cols[(uint64_t)(1 + k) * P.nch_cap + c];
   uint32_t ovf = 0;
   uint64_t pos = s;
   for (uint64_t idx = first; pos < c1 && idx < n; ++idx) {
-    uint8_t *rec = idx < a.rec_cap ? recs + idx * a.N.stride : nullptr;
-    const int32_t ec = n_read(a.N, wire, pos, len, w, rec, a.heaps, used, a.heap_cap, &ovf, 0,
-                              a.N.n_ops, true);
+    uint8_t *rec = idx < a.rec_cap ? recs + idx * N.stride : nullptr;
+    const int32_t ec = n_read(N, wire, pos, len, w, rec, a.heaps, used, a.heap_cap, &ovf, 0,
+                              N.n_ops, true);
     if (ec) {
       ctl->werr = ec;  // the one record of the path that fails before n
       break;
@@ -1734,6 +1803,8 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
     P.ent = reinterpret_cast<uint64_t *>(ws + f.ent);
     P.ext = reinterpret_cast<uint64_t *>(ws + f.ext);
     P.err = reinterpret_cast<int32_t *>(ws + f.err);
+    P.dirty = reinterpret_cast<unsigned long long *>(ws + f.dirty);
+    if ((er = hipMemsetAsync(P.dirty, 0, (cap + 63) / 64 * 8, s)) != hipSuccess) return er;
     P.cols = reinterpret_cast<uint64_t *>(ws + f.cols);
     const uint64_t nch_max = (wire_len + kNCh - 1) / kNCh;
     P.nch_cap = nch_max;

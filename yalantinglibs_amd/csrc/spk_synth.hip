@@ -158,6 +158,98 @@ __global__ void synth_ints(uint64_t seed, uint64_t first, uint64_t n, uint32_t p
   }
 }
 
+// ---- the reference benchmark's Monster (types.hpp fill(Monster&)) -----------
+// schema.flatten(Monster): 96-byte record, six heaps (name, inventory, weapon
+// element records, weapon names, equipped.name, path); Weapon element record
+// {u32 name.n, u64 name.off, i16 damage} = 24 bytes
+constexpr int kMonHeaps = 6;
+__device__ __forceinline__ uint32_t tag_len(uint64_t h) { return (uint32_t)(h % 13); }
+__device__ __forceinline__ void tag_fill(uint8_t *d, uint64_t h) {
+  for (uint32_t k = 0; k < tag_len(h); ++k) {
+    const uint64_t w = mix64(h + (k >> 3));
+    d[k] = (uint8_t)('a' + ((w >> ((k & 7) * 8)) & 0xFF) % 26);
+  }
+}
+__device__ __forceinline__ uint64_t elem_word(uint64_t seed, uint64_t i, uint64_t j) {
+  return mix64(rnd(seed, i, 2 + j % 56) ^ j);
+}
+// counts per record: [0] name chars, [1] inventory chars, [2] weapons,
+// [3] weapon-name chars, [4] equipped.name chars, [5] path points
+__global__ void synth_monster_counts(uint64_t seed, uint64_t first, uint64_t n, uint32_t param,
+                                     uint64_t *cnt) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gs) {
+    const uint64_t i = first + t, r9 = rnd(seed, i, 9);
+    const uint32_t nw = (uint32_t)((r9 >> 8) % 5);
+    uint64_t wl = 0;
+    for (uint32_t j = 0; j < nw; ++j) wl += tag_len(elem_word(seed, i, j));
+    cnt[t] = rnd(seed, i, 1) % (uint64_t)(param + 1);
+    cnt[n + t] = tag_len(rnd(seed, i, 8));
+    cnt[2 * n + t] = nw;
+    cnt[3 * n + t] = wl;
+    cnt[4 * n + t] = tag_len(rnd(seed, i, 10));
+    cnt[5 * n + t] = (r9 >> 16) % 9;
+  }
+}
+struct MonHeaps {
+  uint8_t *h[kMonHeaps];
+};
+__global__ void synth_monster(uint64_t seed, uint64_t first, uint64_t n, uint32_t param,
+                              uint8_t *recs, MonHeaps H, const uint64_t *off) {
+  const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gs) {
+    const uint64_t i = first + t;
+    uint8_t *r = recs + t * 96;
+    for (int q = 0; q < 12; ++q) reinterpret_cast<uint64_t *>(r)[q] = 0;
+    float *pos = reinterpret_cast<float *>(r);
+    for (int k = 0; k < 3; ++k) pos[k] = rf(rnd(seed, i, 4 + k));
+    const uint64_t r7 = rnd(seed, i, 7), r9 = rnd(seed, i, 9), r10 = rnd(seed, i, 10);
+    *reinterpret_cast<int16_t *>(r + 12) = (int16_t)r7;
+    *reinterpret_cast<int16_t *>(r + 14) = (int16_t)(r7 >> 16);
+    // name: make_chars (words 2.. of the record)
+    const uint32_t nl = (uint32_t)(rnd(seed, i, 1) % (uint64_t)(param + 1));
+    *reinterpret_cast<uint32_t *>(r + 16) = nl;
+    *reinterpret_cast<uint64_t *>(r + 24) = off[t];
+    for (uint32_t j = 0; j < nl; ++j) {
+      const uint64_t w = rnd(seed, i, 2 + (j >> 3) % 56);
+      H.h[0][off[t] + j] = (uint8_t)('a' + ((w >> ((j & 7) * 8)) & 0xFF) % 26);
+    }
+    const uint64_t r8 = rnd(seed, i, 8);
+    *reinterpret_cast<uint32_t *>(r + 32) = tag_len(r8);
+    *reinterpret_cast<uint64_t *>(r + 40) = off[n + t];
+    tag_fill(H.h[1] + off[n + t], r8);
+    r[48] = (uint8_t)(r9 % 3);
+    const uint32_t nw = (uint32_t)((r9 >> 8) % 5);
+    *reinterpret_cast<uint32_t *>(r + 52) = nw;
+    *reinterpret_cast<uint64_t *>(r + 56) = off[2 * n + t];
+    uint64_t wo = off[3 * n + t];
+    for (uint32_t j = 0; j < nw; ++j) {
+      const uint64_t h = elem_word(seed, i, j);
+      uint8_t *e = H.h[2] + (off[2 * n + t] + j) * 24;
+      for (int q = 0; q < 3; ++q) reinterpret_cast<uint64_t *>(e)[q] = 0;
+      *reinterpret_cast<uint32_t *>(e) = tag_len(h);
+      *reinterpret_cast<uint64_t *>(e + 8) = wo;
+      *reinterpret_cast<int16_t *>(e + 16) = (int16_t)(h >> 32);
+      tag_fill(H.h[3] + wo, h);
+      wo += tag_len(h);
+    }
+    *reinterpret_cast<uint32_t *>(r + 64) = tag_len(r10);
+    *reinterpret_cast<uint64_t *>(r + 72) = off[4 * n + t];
+    tag_fill(H.h[4] + off[4 * n + t], r10);
+    *reinterpret_cast<int16_t *>(r + 80) = (int16_t)(r10 >> 40);
+    const uint32_t np = (uint32_t)((r9 >> 16) % 9);
+    *reinterpret_cast<uint32_t *>(r + 84) = np;
+    *reinterpret_cast<uint64_t *>(r + 88) = off[5 * n + t];
+    float *pt = reinterpret_cast<float *>(H.h[5] + off[5 * n + t] * 12);
+    for (uint32_t j = 0; j < np; ++j) {
+      const uint64_t w = mix64(rnd(seed, i, 11) + j);
+      pt[3 * j] = rf(w);
+      pt[3 * j + 1] = rf(w >> 32);
+      pt[3 * j + 2] = rf(mix64(w));
+    }
+  }
+}
+
 unsigned grid_of(uint64_t n) {
   uint64_t b = (n + 255) / 256;
   if (b > 8192) b = 8192;
@@ -213,5 +305,27 @@ extern "C" int spk_synth(int kind, uint64_t seed, uint64_t first, uint64_t n, ui
     default:
       return SPK_E_ARG;
   }
+  return hipGetLastError() == hipSuccess ? SPK_OK : SPK_E_HIP;
+}
+
+// multi-heap kinds (SPK_SYNTH_MONSTER): d_counts / d_heap_offsets are
+// [heaps][n] columns (elements per record; exclusive prefix sums of them)
+extern "C" int spk_synth_counts_ex(int kind, uint64_t seed, uint64_t first, uint64_t n,
+                                   uint32_t param, uint64_t *d_counts, void *stream) {
+  if (kind != SPK_SYNTH_MONSTER || !d_counts) return SPK_E_ARG;
+  SPK_LAUNCH(synth_monster_counts, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, seed,
+             first, n, param, d_counts);
+  return hipGetLastError() == hipSuccess ? SPK_OK : SPK_E_HIP;
+}
+
+extern "C" int spk_synth_ex(int kind, uint64_t seed, uint64_t first, uint64_t n, uint32_t param,
+                            void *d_recs, void *const *d_heaps, const uint64_t *d_heap_offsets,
+                            void *stream) {
+  if (kind != SPK_SYNTH_MONSTER || (n && (!d_recs || !d_heaps || !d_heap_offsets)))
+    return SPK_E_ARG;
+  MonHeaps H;
+  for (int k = 0; k < kMonHeaps; ++k) H.h[k] = (uint8_t *)(d_heaps ? d_heaps[k] : nullptr);
+  SPK_LAUNCH(synth_monster, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, seed, first, n,
+             param, (uint8_t *)d_recs, H, d_heap_offsets);
   return hipGetLastError() == hipSuccess ? SPK_OK : SPK_E_HIP;
 }

@@ -296,6 +296,8 @@ def synth_batch(codec: Codec, kind: str, n: int, seed: int, param: int = 48,
     kinds = {"rec64": C.SPK_SYNTH_REC64, "recs": C.SPK_SYNTH_RECS, "outer": C.SPK_SYNTH_OUTER,
              "rpcrect": C.SPK_SYNTH_RPCRECT, "person": C.SPK_SYNTH_PERSON,
              "ints": C.SPK_SYNTH_INTS}
+    if kind == "monster":
+        return _synth_multi(codec, C.SPK_SYNTH_MONSTER, n, seed, param, first, stream)
     k = kinds[kind]
     recs = torch.empty((n, codec.L.stride), dtype=torch.uint8, device=dev)
     st = _stream(stream)
@@ -312,3 +314,25 @@ def synth_batch(codec: Codec, kind: str, n: int, seed: int, param: int = 48,
     Codec._check(lib.spk_synth(k, seed, first, n, param, _p(recs), _p(heap), _p(offs), st),
                  "spk_synth")
     return RecordBatch(codec.L, recs, [heap])
+
+
+def _synth_multi(codec: Codec, k: int, n: int, seed: int, param: int, first: int,
+                 stream=None) -> RecordBatch:
+    """spk_synth_ex: a kind with one heap per variable-length member
+    (counts pass, exclusive scans per heap, fill pass)."""
+    lib, dev, st = codec.lib, codec.device, _stream(stream)
+    nh = len(codec.L.dev.spans)
+    cnt = torch.empty((nh, max(n, 1)), dtype=torch.int64, device=dev)
+    Codec._check(lib.spk_synth_counts_ex(k, seed, first, n, param, _p(cnt), st),
+                 "spk_synth_counts_ex")
+    cnt = cnt[:, :n]
+    offs = (torch.cumsum(cnt, 1) - cnt).contiguous()
+    totals = cnt.sum(1).tolist() if n else [0] * nh
+    heaps = [torch.zeros(max(int(t), 1) * sp.elem.size, dtype=torch.uint8, device=dev)
+             for t, sp in zip(totals, codec.L.dev.spans)]
+    recs = torch.empty((n, codec.L.stride), dtype=torch.uint8, device=dev)
+    hp = (ct.c_void_p * nh)(*[h.data_ptr() for h in heaps])
+    Codec._check(lib.spk_synth_ex(k, seed, first, n, param, _p(recs), hp, _p(offs), st),
+                 "spk_synth_ex")
+    heaps = [h[:int(t) * sp.elem.size] for h, t, sp in zip(heaps, totals, codec.L.dev.spans)]
+    return RecordBatch(codec.L, recs, heaps)
