@@ -427,6 +427,31 @@ int spk_route_frames(const void *d_wire, uint64_t wire_len, const uint64_t *d_fr
                      uint32_t n_keys, uint64_t *const *d_begins, uint64_t *const *d_ends,
                      uint64_t *const *d_index, uint64_t *d_counts, void *d_ws,
                      size_t ws_bytes, void *stream);
+/* The frame header check the reference server makes before dispatching
+ * (coro_rpc_protocol.hpp:98-117 read_head: magic == 21, version <= 0;
+ * get_serialize_protocol: serialize_type == 0; read_payload: `length` body
+ * bytes then `attach_length` attachment bytes). With it, frame i is routed
+ * only if it holds head_len bytes, passes every check that is not -1 and
+ * head_len + length + attach_length == its size; the others go to the
+ * unrouted list n_keys. d_ends[k][j] is then the END OF THE MESSAGE,
+ * begin + head_len + length (the attachment, which follows it, is not
+ * struct_pack bytes), so spk_decode_frames sees only the message.
+ * attach_off = SPK_FRAME_NONE: the header has no attachment length. */
+typedef struct spk_route_hdr {
+  uint32_t head_len;       /* 20 (req_header)                        */
+  uint32_t len_off;        /* 12: u32 LE body length                 */
+  uint32_t attach_off;     /* 16: u32 LE attachment length, or NONE  */
+  int32_t magic;           /* byte 0 (21), or -1                     */
+  int32_t max_version;     /* byte 1 <= this (0), or -1              */
+  int32_t serialize_type;  /* byte 2 (0), or -1                      */
+} spk_route_hdr;
+/* spk_route_frames with the header check (hdr NULL = spk_route_frames). */
+int spk_route_frames_checked(const void *d_wire, uint64_t wire_len,
+                             const uint64_t *d_frame_offsets, uint64_t n_frames,
+                             uint32_t key_off, const uint32_t *h_keys, uint32_t n_keys,
+                             const spk_route_hdr *hdr, uint64_t *const *d_begins,
+                             uint64_t *const *d_ends, uint64_t *const *d_index,
+                             uint64_t *d_counts, void *d_ws, size_t ws_bytes, void *stream);
 /* spk_decode_framed over frames that need not be adjacent: frame i is
  * d_wire[d_begins[i] .. d_ends[i]) (one type's lists from spk_route_frames). */
 int spk_decode_frames(const spk_layout *L, const void *d_wire, uint64_t wire_len,

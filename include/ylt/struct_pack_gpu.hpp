@@ -71,19 +71,22 @@ template <typename M, std::size_t... I>
 constexpr bool all_supported(std::index_sequence<I...>) {
   return (supported<std::tuple_element_t<I, M>>() && ...);
 }
-template <typename T>
-constexpr bool elem_supported() {  // container / optional element
-  if constexpr (supported<T>())
-    return is_trivially_serializable<T>();
-  else
-    return false;
-}
+template <typename V>
+struct variant_supported;
+template <typename... A>
+struct variant_supported<std::variant<A...>> {
+  static constexpr bool value = ((is_monostate_v<A> || supported<A>()) && ...);
+};
 template <typename T>
 constexpr bool supported() {
   if constexpr (is_fundamental_v<T> || is_string_v<T> || is_varint_v<T>) {
     return true;
-  } else if constexpr (is_container_v<T> || is_std_optional<T>::value) {
-    return elem_supported<remove_cvref_t<typename T::value_type>>();
+  } else if constexpr (is_container_v<T>) {
+    return supported<elem_t<T>>();
+  } else if constexpr (is_std_optional<T>::value || is_compat_v<T>) {
+    return supported<remove_cvref_t<typename T::value_type>>();
+  } else if constexpr (is_std_variant<T>::value) {
+    return variant_supported<T>::value;
   } else if constexpr (is_std_array<T>::value) {
     return supported<typename T::value_type>();
   } else if constexpr (is_record_v<T>) {
@@ -262,8 +265,10 @@ class codec {
   spk_plan_t plan(const batch<R> &b, int mode) {
     ws_.resize(spk_workspace_bytes(&layout(), mode, b.n, 0));
     plan_.resize(sizeof(spk_plan_t));
-    check(spk_plan(&layout(), mode, b.n, b.recs.data(), (spk_plan_t *)plan_.data(), ws_.data(),
-                   ws_.size(), s_), "spk_plan");
+    std::vector<const void *> hp = heap_ptrs(b);
+    check(spk_plan_ex(&layout(), mode, b.n, b.recs.data(), hp.data(), (spk_plan_t *)plan_.data(),
+                      ws_.data(), ws_.size(), s_),
+          "spk_plan_ex");
     spk_plan_t p{};
     copy(&p, plan_.data(), sizeof(p), SPK_COPY_D2H, s_);
     sync(s_);
@@ -357,41 +362,30 @@ class codec {
     batch<R> b;
     b.n = max_records;
     b.recs.resize(max_records * layout().rec_stride);
+    const std::vector<uint64_t> caps = detail::heap_caps_for_wire(layout(), len, max_records);
     for (uint32_t k = 0; k < n_spans(); ++k) {
-      // an OPTION holds at most one value per record, readable or not
-      b.heap_elems.push_back(span_is_option(k) ? max_records : len / span_elem(k) + 1);
-      b.heaps.emplace_back(b.heap_elems.back() * span_elem(k));
+      b.heap_elems.push_back(caps[k]);
+      b.heaps.emplace_back(caps[k] * span_elem(k));
     }
     return b;
   }
 
+  // heaps: SPAN / OPTION / COMPAT values and ARRAY element records, in op
+  // order at every level (COPY, VARINT and group heads live in the record)
   static uint32_t n_spans() {
     uint32_t k = 0;
     for (uint32_t i = 0; i < layout().n_ops; ++i) k += has_heap(layout().ops[i]);
     return k;
   }
-  // SPAN + OPTION members: one heap each (COPY and VARINT live in the record)
-  static bool has_heap(const spk_op &o) {
-    return o.kind == SPK_OP_SPAN || o.kind == SPK_OP_OPTION;
-  }
+  static bool has_heap(const spk_op &o) { return detail::op_has_heap(o); }
+  // bytes per heap element (an ARRAY's: its element record stride)
   static uint32_t span_elem(uint32_t k) {
     for (uint32_t i = 0, s = 0; i < layout().n_ops; ++i)
       if (has_heap(layout().ops[i]) && s++ == k) return layout().ops[i].size;
     return 1;
   }
-  static bool span_is_option(uint32_t k) {
-    for (uint32_t i = 0, s = 0; i < layout().n_ops; ++i)
-      if (has_heap(layout().ops[i]) && s++ == k)
-        return layout().ops[i].kind == SPK_OP_OPTION;
-    return false;
-  }
   // fewest wire bytes a record can take: a bound on the records in a buffer
-  static std::size_t min_record_wire() {
-    std::size_t m = 0;
-    for (uint32_t i = 0; i < layout().n_ops; ++i)
-      m += layout().ops[i].kind == SPK_OP_COPY ? layout().ops[i].size : 1;
-    return m ? m : 1;
-  }
+  static std::size_t min_record_wire() { return detail::min_record_wire_bytes(layout()); }
   void *stream() const { return s_; }
 
  private:
@@ -520,8 +514,8 @@ constexpr void check_message_type() {
   static_assert(is_gpu_message_v<T>,
                 "struct_pack::gpu handles one std::vector<R> / std::span<R> of records or one "
                 "record R whose members are fundamentals, enums, std::array, std::string, "
-                "containers / optionals of trivially serializable types, varints and nested "
-                "records; use the reference's CPU struct_pack for anything else");
+                "sequence / set / map containers, optionals, variants, compatibles, varints "
+                "and nested records; use the reference's CPU struct_pack for anything else");
 }
 
 // decode of one message into t: VECTOR for std::vector<R>, one MESSAGES

@@ -7,12 +7,21 @@
 // calls, user_reflect_macro.hpp:27-57).
 //
 // Supported members: fundamentals, enums, std::string / std::string_view,
-// std::vector<T> / std::span<T>, std::array<T, N>, std::optional<T>, the
-// varint types, and nested records. (C arrays inside aggregates defeat
-// brace-init counting -- use std::array.)
+// std::vector<T> / std::span<T> / std::list<T> / std::deque<T>, the set and
+// map containers (ordered / unordered, multi or not), std::array<T, N>,
+// std::optional<T>, std::variant<...>, std::pair<A, B>, the varint types,
+// struct_pack::compatible<T, v>, and nested records. (C arrays inside
+// aggregates defeat brace-init counting -- use std::array.)
 #pragma once
 #include <array>
 #include <cstddef>
+#include <deque>
+#include <list>
+#include <map>
+#include <set>
+#include <unordered_map>
+#include <unordered_set>
+#include <variant>
 #include <cstdint>
 #include <optional>
 #include <span>
@@ -39,10 +48,60 @@ template <typename T> struct is_std_optional<std::optional<T>> : std::true_type 
 template <typename T> struct is_std_array : std::false_type {};
 template <typename T, std::size_t N> struct is_std_array<std::array<T, N>> : std::true_type {};
 
+template <typename T> struct is_std_list : std::false_type {};  // list / deque: container_t
+template <typename T, typename A> struct is_std_list<std::list<T, A>> : std::true_type {};
+template <typename T, typename A> struct is_std_list<std::deque<T, A>> : std::true_type {};
+template <typename T> struct is_std_variant : std::false_type {};
+template <typename... A> struct is_std_variant<std::variant<A...>> : std::true_type {};
+template <typename T> struct is_std_pair : std::false_type {};
+template <typename A, typename B> struct is_std_pair<std::pair<A, B>> : std::true_type {};
+
+// set_container_t (type_id.hpp: set, multiset, unordered_set, unordered_multiset)
+template <typename T> struct set_traits : std::false_type {};
+template <typename K, typename C, typename A>
+struct set_traits<std::set<K, C, A>> : std::true_type { static constexpr bool multi = false; };
+template <typename K, typename C, typename A>
+struct set_traits<std::multiset<K, C, A>> : std::true_type { static constexpr bool multi = true; };
+template <typename K, typename H, typename E, typename A>
+struct set_traits<std::unordered_set<K, H, E, A>> : std::true_type {
+  static constexpr bool multi = false;
+};
+template <typename K, typename H, typename E, typename A>
+struct set_traits<std::unordered_multiset<K, H, E, A>> : std::true_type {
+  static constexpr bool multi = true;
+};
+// map_container_t (map, multimap, unordered_map, unordered_multimap)
+template <typename T> struct map_traits : std::false_type {};
+template <typename K, typename V, typename C, typename A>
+struct map_traits<std::map<K, V, C, A>> : std::true_type { static constexpr bool multi = false; };
+template <typename K, typename V, typename C, typename A>
+struct map_traits<std::multimap<K, V, C, A>> : std::true_type {
+  static constexpr bool multi = true;
+};
+template <typename K, typename V, typename H, typename E, typename A>
+struct map_traits<std::unordered_map<K, V, H, E, A>> : std::true_type {
+  static constexpr bool multi = false;
+};
+template <typename K, typename V, typename H, typename E, typename A>
+struct map_traits<std::unordered_multimap<K, V, H, E, A>> : std::true_type {
+  static constexpr bool multi = true;
+};
+
 template <typename T>
 constexpr bool is_string_v = std::is_same_v<T, std::string> || std::is_same_v<T, std::string_view>;
 template <typename T>
-constexpr bool is_container_v = is_std_vector<T>::value || is_std_span<T>::value;
+constexpr bool is_set_v = set_traits<T>::value;
+template <typename T>
+constexpr bool is_map_v = map_traits<T>::value;
+// contiguous containers (memcpy of trivially serializable elements)
+template <typename T>
+constexpr bool is_contiguous_v = is_std_vector<T>::value || is_std_span<T>::value;
+// every [count][elements] container (string_t aside)
+template <typename T>
+constexpr bool is_container_v =
+    is_contiguous_v<T> || is_std_list<T>::value || is_set_v<T> || is_map_v<T>;
+template <typename T>
+constexpr bool is_monostate_v = std::is_same_v<T, std::monostate>;
 template <typename T>
 constexpr bool is_fundamental_v = std::is_arithmetic_v<T> || std::is_enum_v<T>;
 template <typename T>
@@ -53,9 +112,26 @@ template <typename T>
 constexpr bool is_aggregate_record_v = std::is_aggregate_v<T> && std::is_class_v<T> &&
                                        !is_std_array<T>::value && !is_string_v<T> &&
                                        !is_container_v<T> && !is_std_optional<T>::value &&
-                                       !is_varint_v<T> && !is_compat_v<T> && !is_ylt_refl_v<T>;
+                                       !is_varint_v<T> && !is_compat_v<T> && !is_ylt_refl_v<T> &&
+                                       !is_monostate_v<T>;
+// records: aggregates, YLT_REFL types, and std::pair (a struct of first,
+// second: type_id.hpp, the element of a map container)
 template <typename T>
-constexpr bool is_record_v = is_aggregate_record_v<T> || (std::is_class_v<T> && is_ylt_refl_v<T>);
+constexpr bool is_record_v = is_aggregate_record_v<T> || (std::is_class_v<T> && is_ylt_refl_v<T>) ||
+                             is_std_pair<T>::value;
+
+// element type of a container as its device record holds it (a map's
+// pair<const K, V> as pair<K, V>)
+template <typename T, bool = is_map_v<T>>
+struct elem_of {
+  using type = remove_cvref_t<typename T::value_type>;
+};
+template <typename T>
+struct elem_of<T, true> {
+  using type = std::pair<remove_cvref_t<typename T::key_type>, typename T::mapped_type>;
+};
+template <typename T>
+using elem_t = typename elem_of<T>::type;
 
 // ---- aggregate member count (brace-init probing) ----------------------------
 struct any_init {
@@ -134,7 +210,9 @@ constexpr auto tie_aggregate(T &obj) {
 
 template <typename T>
 constexpr auto tie_members(T &obj) {
-  if constexpr (is_ylt_refl_v<remove_cvref_t<T>>)
+  if constexpr (is_std_pair<remove_cvref_t<T>>::value)
+    return std::forward_as_tuple(obj.first, obj.second);
+  else if constexpr (is_ylt_refl_v<remove_cvref_t<T>>)
     return refl_tuple(obj);
   else
     return tie_aggregate(obj);

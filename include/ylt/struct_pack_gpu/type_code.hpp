@@ -34,9 +34,38 @@ enum : uint8_t {
   TID_UINT8 = 6, TID_INT16 = 7, TID_UINT16 = 8, TID_BOOL = 11, TID_CHAR8 = 12,
   TID_CHAR16 = 13, TID_CHAR32 = 14, TID_FLOAT32 = 17, TID_FLOAT64 = 18,
   TID_VINT32 = 20, TID_VINT64 = 21, TID_VUINT32 = 22, TID_VUINT64 = 23,
-  TID_STRING = 128, TID_ARRAY = 129, TID_CONTAINER = 132, TID_OPTIONAL = 133, TID_STRUCT = 253,
-  TID_END = 255
+  TID_STRING = 128, TID_ARRAY = 129, TID_MAP = 130, TID_SET = 131, TID_CONTAINER = 132,
+  TID_OPTIONAL = 133, TID_VARIANT = 134, TID_MONOSTATE = 250, TID_STRUCT = 253, TID_END = 255
 };
+
+// sp_config bits of a record that turn members into varints (reflection.hpp:
+// 53-60, 843): ENCODING_WITH_VARINT makes plain (u)int32/64 members varints,
+// USE_FAST_VARINT writes the record's varints as one fast-varint group
+inline constexpr uint64_t kCfgEncodingWithVarint = 0b100, kCfgUseFastVarint = 0b1000;
+inline constexpr uint64_t kCfgVarintBits = kCfgEncodingWithVarint | kCfgUseFastVarint;
+
+// a plain integer member that ENCODING_WITH_VARINT turns into a varint
+template <typename T>
+constexpr bool is_plain_varint_v = std::is_same_v<T, int32_t> || std::is_same_v<T, uint32_t> ||
+                                   std::is_same_v<T, int64_t> || std::is_same_v<T, uint64_t>;
+
+// get_varint_type<T, parent_tag> (type_id.hpp:83-125): the type id of member
+// T under its record's config `cfg`, or 0 when it is not a varint there;
+// USE_FAST_VARINT selects the fast_v* ids (varint id + 4)
+template <typename T, uint64_t cfg>
+constexpr uint8_t varint_tid() {
+  uint8_t t = 0;
+  if constexpr (is_varint_v<T>) {
+    using V = typename varint_traits<T>::value_type;
+    constexpr bool zz = varint_traits<T>::zigzag;
+    t = sizeof(V) == 4 ? (zz ? TID_VINT32 : TID_VUINT32) : (zz ? TID_VINT64 : TID_VUINT64);
+  } else if constexpr ((cfg & kCfgEncodingWithVarint) && is_plain_varint_v<T>) {
+    t = sizeof(T) == 4 ? (std::is_signed_v<T> ? TID_VINT32 : TID_VUINT32)
+                       : (std::is_signed_v<T> ? TID_VINT64 : TID_VUINT64);
+  }
+  if (t && (cfg & kCfgUseFastVarint)) t += 4;
+  return t;
+}
 
 template <typename T>
 constexpr uint8_t fundamental_id() {
@@ -77,28 +106,34 @@ constexpr lit_t size_literal(std::size_t n) {
 template <typename T>
 constexpr bool is_trivially_serializable();
 
-template <typename Tup, std::size_t... I>
+template <typename Tup, uint64_t cfg, std::size_t... I>
 constexpr bool all_trivial(std::index_sequence<I...>) {
-  return (is_trivially_serializable<std::tuple_element_t<I, Tup>>() && ...);
+  return ((is_trivially_serializable<std::tuple_element_t<I, Tup>>() &&
+           varint_tid<std::tuple_element_t<I, Tup>, cfg>() == 0) &&
+          ...);
 }
 
 template <typename T>
 constexpr bool is_trivially_serializable() {
-  if constexpr (is_fundamental_v<T>) {
+  if constexpr (is_fundamental_v<T> || is_monostate_v<T>) {
     return true;
   } else if constexpr (is_std_array<T>::value) {
     return is_trivially_serializable<typename T::value_type>();
   } else if constexpr (is_string_v<T> || is_container_v<T> || is_std_optional<T>::value ||
-                       is_varint_v<T> || is_compat_v<T>) {
-    return false;  // reflection.hpp:872-876,899-901
+                       is_varint_v<T> || is_compat_v<T> || is_std_variant<T>::value) {
+    return false;  // reflection.hpp:872-876,899-905
   } else if constexpr (is_ylt_refl_v<T>) {
     return false;  // user_defined_refl: member by member (reflection.hpp:896-898)
   } else {
     static_assert(is_record_v<T>, "unsupported member type");
     using M = members_tuple_t<T>;
-    return all_trivial<M>(std::make_index_sequence<std::tuple_size_v<M>>{});
+    return all_trivial<M, type_config<T>() & kCfgVarintBits>(
+        std::make_index_sequence<std::tuple_size_v<M>>{});
   }
 }
+
+template <typename V>
+struct variant_any_container;
 
 template <typename T>
 constexpr bool has_container();
@@ -110,6 +145,8 @@ template <typename T>
 constexpr bool has_container() {
   if constexpr (is_string_v<T> || is_container_v<T>)
     return true;
+  else if constexpr (is_std_variant<T>::value)  // type_calculate.hpp:785-815
+    return variant_any_container<T>::value;
   else if constexpr (is_std_array<T>::value || is_std_optional<T>::value || is_compat_v<T>)
     return has_container<typename T::value_type>();  // type_calculate.hpp:846-849
   else if constexpr (is_record_v<T>) {
@@ -118,6 +155,11 @@ constexpr bool has_container() {
   } else
     return false;
 }
+
+template <typename... A>
+struct variant_any_container<std::variant<A...>> {
+  static constexpr bool value = (has_container<A>() || ...);
+};
 
 // max over the members' alignment (alignment.hpp:33-41,63-71)
 template <typename T>
@@ -177,9 +219,24 @@ constexpr std::size_t alignment_of() {
 template <typename T>
 constexpr lit_t type_literal();
 
-template <typename Tup, std::size_t... I>
+// a member's literal under its record's config: a varint there is its type id
+template <typename F, uint64_t cfg>
+constexpr lit_t member_literal() {
+  if constexpr (varint_tid<F, cfg>() != 0) {
+    lit_t l;
+    l.push(varint_tid<F, cfg>());
+    return l;
+  } else {
+    return type_literal<F>();
+  }
+}
+template <typename Tup, uint64_t cfg, std::size_t... I>
 constexpr void append_members(lit_t &l, std::index_sequence<I...>) {
-  (l.append(type_literal<std::tuple_element_t<I, Tup>>()), ...);
+  (l.append(member_literal<std::tuple_element_t<I, Tup>, cfg>()), ...);
+}
+template <typename... A>
+constexpr void append_alternatives(lit_t &l, std::variant<A...> *) {
+  (l.append(type_literal<A>()), ...);
 }
 
 template <typename T>
@@ -190,9 +247,22 @@ constexpr lit_t type_literal() {
   } else if constexpr (is_string_v<T>) {
     l.push(TID_STRING);
     l.push(TID_CHAR8);
+  } else if constexpr (is_map_v<T>) {  // type_calculate.hpp:284-290
+    l.push(TID_MAP);
+    l.append(type_literal<remove_cvref_t<typename T::key_type>>());
+    l.append(type_literal<remove_cvref_t<typename T::mapped_type>>());
+  } else if constexpr (is_set_v<T>) {  // type_calculate.hpp:280-283
+    l.push(TID_SET);
+    l.append(type_literal<remove_cvref_t<typename T::key_type>>());
   } else if constexpr (is_container_v<T>) {
     l.push(TID_CONTAINER);
     l.append(type_literal<remove_cvref_t<typename T::value_type>>());
+  } else if constexpr (is_std_variant<T>::value) {  // type_calculate.hpp:245-253
+    l.push(TID_VARIANT);
+    append_alternatives(l, static_cast<T *>(nullptr));
+    l.push(TID_END);
+  } else if constexpr (is_monostate_v<T>) {
+    l.push(TID_MONOSTATE);
   } else if constexpr (is_varint_v<T>) {  // get_varint_type (type_id.hpp:84-125)
     using V = typename varint_traits<T>::value_type;
     constexpr bool zz = varint_traits<T>::zigzag;
@@ -209,7 +279,8 @@ constexpr lit_t type_literal() {
     static_assert(is_record_v<T>, "unsupported type");
     using M = members_tuple_t<T>;
     l.push(TID_STRUCT);
-    append_members<M>(l, std::make_index_sequence<std::tuple_size_v<M>>{});
+    append_members<M, type_config<T>() & kCfgVarintBits>(
+        l, std::make_index_sequence<std::tuple_size_v<M>>{});
     if constexpr (is_trivially_serializable<T>()) {  // type_calculate.hpp:229-239
       static_assert(pack_alignment_of<T>() <= alignment_of<T>(),
                     "If you add #pragma pack to a struct, please specify "

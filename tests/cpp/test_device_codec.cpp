@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <type_traits>
+#include <variant>
 #include <fstream>
 #include <iterator>
 #include <string>
@@ -60,6 +61,83 @@ bool operator==(const Var &a, const Var &b) {
   return a.a == b.a && a.s == b.s && a.b == b.b && a.d == b.d && a.c == b.c && a.e == b.e;
 }
 bool operator==(const VarP &a, const VarP &b) { return a.id == b.id && a.x == b.x && a.y == b.y; }
+
+// structural equality through the front end's own reflection (records,
+// containers, optionals, variants, compatibles), for the record types with
+// no operator==
+template <typename T>
+static bool same(const T &a, const T &b) {
+  namespace d = struct_pack::gpu::detail;
+  using U = d::remove_cvref_t<T>;
+  if constexpr (d::is_fundamental_v<U> || d::is_string_v<U> || d::is_monostate_v<U>) {
+    return a == b;
+  } else if constexpr (d::is_varint_v<U>) {
+    return typename d::varint_traits<U>::value_type(a) == typename d::varint_traits<U>::value_type(b);
+  } else if constexpr (d::is_std_optional<U>::value || d::is_compat_v<U>) {
+    return a.has_value() == b.has_value() && (!a.has_value() || same(*a, *b));
+  } else if constexpr (d::is_std_variant<U>::value) {
+    return a.index() == b.index() &&
+           std::visit([&](const auto &x) {
+             return same(x, *std::get_if<d::remove_cvref_t<decltype(x)>>(&b));
+           }, a);
+  } else if constexpr (d::is_container_v<U> || d::is_std_array<U>::value) {
+    if (a.size() != b.size()) return false;
+    auto i = a.begin();
+    auto j = b.begin();
+    for (; i != a.end(); ++i, ++j)
+      if (!same(*i, *j)) return false;
+    return true;
+  } else if constexpr (d::is_std_pair<U>::value) {
+    return same(a.first, b.first) && same(a.second, b.second);
+  } else {
+    auto ta = d::tie_members(const_cast<U &>(a));
+    auto tb = d::tie_members(const_cast<U &>(b));
+    return [&]<std::size_t... I>(std::index_sequence<I...>) {
+      return (same(std::get<I>(ta), std::get<I>(tb)) && ...);
+    }(std::make_index_sequence<std::tuple_size_v<decltype(ta)>>{});
+  }
+}
+
+// A vector message of a nested record type (ARRAY / VARIANT / OPTGROUP /
+// CGROUP / FVAR layouts and the other container kinds) through the C++ front
+// end: bytes == the reference's, decode == the records, and a truncated
+// buffer / broken hash reported as the reference does. trunc / hash: whether
+// the type's last member and head make those errc deterministic.
+template <typename T, typename Gen>
+static void roundtrip_nested(const char *fixture, std::size_t n, Gen gen, bool trunc = true,
+                             bool hash = true) {
+  std::vector<T> v(n);
+  for (std::size_t i = 0; i < n; ++i) gen(v[i], i);
+  const std::string want = golden(fixture);
+  CHECK(!want.empty());
+  auto sz = get_needed_size(v);
+  CHECK(sz.size() == want.size());
+  auto bytes = serialize<sp_config::DEFAULT, std::string>(v);
+  CHECK(bytes == want);
+  if (bytes != want) std::fprintf(stderr, "  %s: bytes differ (%zu vs %zu)\n", fixture,
+                                  bytes.size(), want.size());
+  std::vector<T> back;
+  std::size_t consumed = 0;
+  auto ec = deserialize_to(back, want.data(), want.size(), consumed);
+  CHECK(!ec);
+  CHECK(consumed == want.size());
+  bool eq = back.size() == v.size();
+  for (std::size_t i = 0; eq && i < n; ++i) eq = same(back[i], v[i]);
+  CHECK(eq);
+  if (!eq) std::fprintf(stderr, "  %s: decoded records differ\n", fixture);
+  // the decoded objects re-encode to the same bytes
+  CHECK((serialize<sp_config::DEFAULT, std::string>(back) == want));
+  if (trunc && n) {
+    std::vector<T> t;
+    CHECK(deserialize_to(t, want.data(), want.size() - 1).ec == errc::no_buffer_space);
+  }
+  if (hash && n) {
+    std::string bad = want;
+    bad[1] ^= 0x40;
+    std::vector<T> t2;
+    CHECK(deserialize_to(t2, bad.data(), bad.size()).ec == errc::invalid_buffer);
+  }
+}
 
 // check_trunc: a record type whose last member may be an optional value is
 // exempt from the "one byte short -> no_buffer_space" check: the reference
@@ -305,6 +383,30 @@ int main() {
   roundtrip_messages<VarP>("varp_B_n200_p0_default.bin", "varp_B_n200_p0_default.lens", 200,
                            gen_varp);
   routed_mixed_batch();
+  // nested layouts through the C++ front end (make_spk_layout flattens ARRAY,
+  // VARIANT, OPTGROUP, CGROUP, FVAR and the set / map / list containers)
+  auto gen = [](uint64_t seed, uint32_t p) {
+    return [=](auto &o, uint64_t i) { fill(o, seed, i, p); };
+  };
+  roundtrip_nested<Tags>("tags_A_n200_p6_default.bin", 200, gen(0x5EED000E, 6));
+  roundtrip_nested<Tags>("tags_A_n30_p300_default.bin", 30, gen(0x5EED000E, 300));
+  roundtrip_nested<Group>("group_A_n100_p5_default.bin", 100, gen(0x5EED000F, 5));
+  roundtrip_nested<Deep>("deep_A_n100_p4_default.bin", 100, gen(0x5EED0010, 4));
+  roundtrip_nested<Vnt>("vnt_A_n200_p6_default.bin", 200, gen(0x5EED0011, 6), false);
+  roundtrip_nested<FV>("fv_A_n300_p8_default.bin", 300, gen(0x5EED0017, 8));
+  roundtrip_nested<FVE>("fve_A_n300_p8_default.bin", 300, gen(0x5EED0018, 8));
+  roundtrip_nested<FV32>("fv32_A_n300_p0_default.bin", 300, gen(0x5EED0019, 0));
+  roundtrip_nested<EV>("ev_A_n300_p8_default.bin", 300, gen(0x5EED001A, 8));
+  roundtrip_nested<ValidateRequest>("valreq_A_n300_p16_default.bin", 300, gen(0x5EED001B, 16),
+                                    false);
+  roundtrip_nested<CmpG>("cmpg_A_n200_p8_default.bin", 200, gen(0x5EED001D, 8), false);
+  roundtrip_nested<Monster>("monster_A_n300_p20_default.bin", 300, gen(0x5EED001E, 20));
+  roundtrip_nested<Monster>("monster_A_n40_p300_default.bin", 40, gen(0x5EED001E, 300));
+  // vector<rect2<int32_t>>: DISABLE_ALL_META_INFO, no hash to break
+  roundtrip_nested<rect2<int32_t>>("rect2_A_n300_p0_default.bin", 300, gen(0x5EED001F, 0), true,
+                                   false);
+  roundtrip_nested<Lists>("lists_A_n200_p6_default.bin", 200, gen(0x5EED0020, 6));
+  roundtrip_nested<Maps>("maps_A_n200_p0_default.bin", 200, gen(0x5EED0021, 0));
   std::printf("{\"checks\": %d, \"failures\": %d}\n", g_checks, g_fail);
   return g_fail ? 1 : 0;
 }

@@ -14,6 +14,7 @@
 #include <fstream>
 #include <iterator>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include <ylt/coro_rpc/impl/protocol/coro_rpc_protocol.hpp>
@@ -51,6 +52,20 @@ static_assert(all_match<std::vector<Rec64>, std::vector<RecS>, std::vector<Outer
                         std::vector<Mixed>, std::vector<Opt>, std::vector<Var>,
                         std::vector<rpcb::person>, std::vector<rect<int>>>());
 
+// nested layouts: containers of non-trivial elements, variants, optional /
+// compatible values that are not trivially serializable, the varint sp_config
+// bits and the set / map / list containers
+static_assert(all_match<Tags, Group, Deep, Vnt, CmpG, FV, FVE, FV32, EV, ResponseCode, AliMessage,
+                        ValidateRequest, Vec3, Weapon, Monster, rect2<int32_t>, Lists, Maps>());
+static_assert(all_match<std::vector<Tags>, std::vector<Vnt>, std::vector<ValidateRequest>,
+                        std::vector<Monster>, std::vector<rect2<int32_t>>, std::vector<Maps>,
+                        std::vector<Lists>, std::vector<FV>>());
+static_assert(struct_pack::gpu::is_gpu_batch_v<std::vector<Monster>> &&
+              struct_pack::gpu::is_gpu_batch_v<std::vector<Tags>> &&
+              struct_pack::gpu::is_gpu_batch_v<std::vector<rect2<int32_t>>> &&
+              struct_pack::gpu::is_gpu_batch_v<std::vector<ValidateRequest>> &&
+              struct_pack::gpu::is_gpu_batch_v<std::vector<Maps>>);
+
 static std::string golden(const std::string &name) {
   std::ifstream f(std::string(SPK_GOLDEN_DIR) + "/" + name, std::ios::binary);
   return std::string((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
@@ -77,6 +92,22 @@ std::string greet(rpcb::person p, int times) {                           // not 
   for (int i = 0; i < times; ++i) s += p.name;
   return s;
 }
+
+// the reference benchmark's services (src/struct_pack/benchmark/data_def.hpp,
+// src/coro_rpc/benchmark/api/ValidateRequest.h)
+std::vector<Monster> echo_monsters(std::vector<Monster> v) { return v; }
+std::vector<rect2<int32_t>> grow_rects(std::vector<rect2<int32_t>> v) {
+  for (auto &r : v) r.width += 1;
+  return v;
+}
+int validate(std::vector<ValidateRequest> v) {
+  int ok = 0;
+  for (auto &r : v) ok += r.job_id.has_value() && !r.query_keys.empty();
+  return ok;
+}
+std::vector<Maps> echo_maps(std::vector<Maps> v) { return v; }
+std::vector<Tags> echo_tags(std::vector<Tags> v) { return v; }
+std::vector<Vnt> echo_vnt(std::vector<Vnt> v) { return v; }
 
 // the executor as coro_rpc's router calls it (router.hpp:155-163)
 template <auto func, typename Proto>
@@ -161,6 +192,27 @@ int main() {
     auto rb = run<echo_recs, struct_pack_protocol>(bad);
     auto gb = run<echo_recs, struct_pack_gpu_protocol>(bad);
     CHECK(rb.first && gb.first && rb.first.val() == gb.first.val());
+  }
+  // 2b. handlers over nested record types (C++ front end: ARRAY / VARIANT /
+  // OPTGROUP / FVAR layouts and map / set containers)
+  {
+    auto make = [](auto tag, std::size_t n, uint64_t seed, uint32_t p) {
+      std::vector<typename decltype(tag)::type> v(n);
+      for (uint64_t i = 0; i < n; ++i) fill(v[i], seed, i, p);
+      return v;
+    };
+    same_as_reference<echo_monsters>(make(std::type_identity<Monster>{}, 2000, 0x5EED001E, 20),
+                                     "echo_monsters");
+    same_as_reference<grow_rects>(make(std::type_identity<rect2<int32_t>>{}, 3000, 0x5EED001F, 0),
+                                  "grow_rects");
+    same_as_reference<validate>(
+        make(std::type_identity<ValidateRequest>{}, 1500, 0x5EED001B, 16), "validate");
+    same_as_reference<echo_maps>(make(std::type_identity<Maps>{}, 500, 0x5EED0021, 0),
+                                 "echo_maps");
+    same_as_reference<echo_tags>(make(std::type_identity<Tags>{}, 1000, 0x5EED000E, 6),
+                                 "echo_tags");
+    same_as_reference<echo_vnt>(make(std::type_identity<Vnt>{}, 1000, 0x5EED0011, 6), "echo_vnt");
+    same_as_reference<echo_monsters>(std::vector<Monster>{}, "echo_monsters(empty)");
   }
   // 3. the front end's single-record and reference-order entry points next to
   // the reference: identical bytes for one record message, deserialize<conf, T>

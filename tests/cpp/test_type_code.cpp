@@ -5,7 +5,7 @@
 #include <cstdio>
 #include <string>
 
-#include "ylt/struct_pack_gpu/layout.hpp"
+#include "ylt/struct_pack_gpu.hpp"
 #include "../../oracle/ref/types.hpp"
 
 using namespace struct_pack;
@@ -35,6 +35,18 @@ static_assert(get_type_code<Cmp>() == 2242444774u);  // kat.json "Cmp"
 static_assert(get_type_code<CmpOld>() == get_type_code<Cmp>());
 static_assert(get_type_code<CmpNew>() == get_type_code<Cmp>());
 static_assert(!gpu::detail::is_trivially_serializable<Cmp>());
+// containers of non-trivial elements, variants, optional / compatible groups,
+// varint configs and the other container kinds are batch records too
+static_assert(is_gpu_batch_v<std::vector<Tags>>);
+static_assert(is_gpu_batch_v<std::vector<Monster>>);
+static_assert(is_gpu_batch_v<std::vector<rect2<int32_t>>>);
+static_assert(is_gpu_batch_v<std::vector<Vnt>>);
+static_assert(is_gpu_batch_v<std::vector<ValidateRequest>>);
+static_assert(is_gpu_batch_v<std::vector<Maps>>);
+static_assert(is_gpu_batch_v<std::vector<Lists>>);
+static_assert(is_gpu_message_v<CmpG>);
+static_assert(!gpu::detail::is_trivially_serializable<rect2<int32_t>>());
+static_assert(!gpu::detail::is_trivially_serializable<std::variant<int, double>>());
 
 template <typename T>
 static void lit_json(const char *name, bool &first) {
@@ -99,6 +111,39 @@ int main() {
   lit_json<Cmp>("Cmp", first);
   lit_json<std::vector<Cmp>>("vector<Cmp>", first);
   lit_json<CmpNew>("CmpNew", first);
+  lit_json<Tags>("Tags", first);
+  lit_json<std::vector<Tags>>("vector<Tags>", first);
+  lit_json<Group>("Group", first);
+  lit_json<std::vector<Group>>("vector<Group>", first);
+  lit_json<Deep>("Deep", first);
+  lit_json<std::vector<Deep>>("vector<Deep>", first);
+  lit_json<Vnt>("Vnt", first);
+  lit_json<std::vector<Vnt>>("vector<Vnt>", first);
+  lit_json<std::variant<int32_t, std::string>>("variant<int32_t,string>", first);
+  lit_json<std::monostate>("monostate", first);
+  lit_json<CmpG>("CmpG", first);
+  lit_json<FV>("FV", first);
+  lit_json<std::vector<FV>>("vector<FV>", first);
+  lit_json<FVE>("FVE", first);
+  lit_json<FV32>("FV32", first);
+  lit_json<EV>("EV", first);
+  lit_json<std::vector<EV>>("vector<EV>", first);
+  lit_json<ResponseCode>("ResponseCode", first);
+  lit_json<AliMessage>("AliMessage", first);
+  lit_json<ValidateRequest>("ValidateRequest", first);
+  lit_json<std::vector<ValidateRequest>>("vector<ValidateRequest>", first);
+  lit_json<Vec3>("Vec3", first);
+  lit_json<Weapon>("Weapon", first);
+  lit_json<Monster>("Monster", first);
+  lit_json<std::vector<Monster>>("vector<Monster>", first);
+  lit_json<rect2<int32_t>>("rect2<int32_t>", first);
+  lit_json<std::vector<rect2<int32_t>>>("vector<rect2<int32_t>>", first);
+  lit_json<Lists>("Lists", first);
+  lit_json<Maps>("Maps", first);
+  lit_json<std::vector<Maps>>("vector<Maps>", first);
+  lit_json<std::map<int32_t, std::string>>("map<int32_t,string>", first);
+  lit_json<std::unordered_multimap<int32_t, int32_t>>("unordered_multimap<int32_t,int32_t>",
+                                                      first);
   printf("},\n\"layout\": {\n");
   first = true;
   layout_json<Rec64>("rec64", first);
@@ -116,6 +161,21 @@ int main() {
   layout_json<VarP>("varp", first);
   layout_json<Cmp>("cmp", first);
   layout_json<CmpNew>("cmpnew", first);
+  layout_json<Tags>("tags", first);
+  layout_json<Group>("group", first);
+  layout_json<Deep>("deep", first);
+  layout_json<Vnt>("vnt", first);
+  layout_json<CmpG>("cmpg", first);
+  layout_json<FV>("fv", first);
+  layout_json<FVE>("fve", first);
+  layout_json<FV32>("fv32", first);
+  layout_json<EV>("ev", first);
+  layout_json<ValidateRequest>("valreq", first);
+  layout_json<Monster>("monster", first);
+  layout_json<rect2<int32_t>>("rect2", first);
+  layout_json<Lists>("lists", first);
+  layout_json<Maps>("maps", first);
+  layout_json<AlRec>("alrec", first);
   layout_json<RecS, sp_config::ENABLE_TYPE_INFO>("recs_typeinfo", first);
   layout_json<Rec64, sp_config::DISABLE_ALL_META_INFO>("rec64_nometa", first);
   printf("}}\n");

@@ -40,7 +40,11 @@ def test_cpp_type_codes_match_reference_kats(cpp_json):
 @pytest.mark.parametrize("case,conf", [("rec64", 0), ("recs", 0), ("outer", 0), ("pad", 0),
                                        ("mixed", 0), ("rect", 0), ("rpcrect", 0),
                                        ("person", 0), ("ints", 0), ("opt", 0), ("optp", 0),
-                                       ("var", 0), ("varp", 0),
+                                       ("var", 0), ("varp", 0), ("tags", 0), ("group", 0),
+                                       ("deep", 0), ("vnt", 0), ("cmpg", 0), ("fv", 0),
+                                       ("fve", 0), ("fv32", 0), ("ev", 0), ("valreq", 0),
+                                       ("monster", 0), ("rect2", 0), ("lists", 0), ("maps", 0),
+                                       ("alrec", 0), ("cmp", 0), ("cmpnew", 0),
                                        ("recs", S.ENABLE_TYPE_INFO),
                                        ("rec64", S.DISABLE_ALL_META_INFO)])
 def test_cpp_and_python_descriptors_agree(cpp_json, case, conf):

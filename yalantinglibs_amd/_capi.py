@@ -113,6 +113,12 @@ class spk_frame(ct.Structure):
                 ("tmpl", ct.c_uint8 * SPK_MAX_FRAME)]
 
 
+class spk_route_hdr(ct.Structure):
+    _fields_ = [("head_len", ct.c_uint32), ("len_off", ct.c_uint32),
+                ("attach_off", ct.c_uint32), ("magic", ct.c_int32),
+                ("max_version", ct.c_int32), ("serialize_type", ct.c_int32)]
+
+
 PLAN_BYTES = ct.sizeof(spk_plan_t)
 DRES_BYTES = ct.sizeof(spk_dresult_t)
 
@@ -131,7 +137,7 @@ CODEC_SYMBOLS = ["spk_abi_version", "spk_errc_message", "spk_layout_check",
                  "spk_decode_body", "spk_parse_vector_header",
                  "spk_decode_shard_index", "spk_decode_shard_emit",
                  # mixed-type frame batches in arrival order
-                 "spk_route_workspace_bytes", "spk_route_frames", "spk_decode_frames",
+                 "spk_route_workspace_bytes", "spk_route_frames", "spk_route_frames_checked", "spk_decode_frames",
                  "spk_copy_frame_field", "spk_encode_framed_echo",
                  # runtime helpers (front ends without HIP headers)
                  "spk_device_alloc", "spk_device_free", "spk_host_alloc_pinned",
@@ -188,6 +194,10 @@ def _bind_codec(lib):
     lib.spk_route_frames.argtypes = [P, U64, P, U64, ct.c_uint32, ct.POINTER(ct.c_uint32),
                                      ct.c_uint32, ct.POINTER(P), ct.POINTER(P), ct.POINTER(P),
                                      P, P, ct.c_size_t, P]
+    lib.spk_route_frames_checked.argtypes = [P, U64, P, U64, ct.c_uint32,
+                                             ct.POINTER(ct.c_uint32), ct.c_uint32,
+                                             ct.POINTER(spk_route_hdr), ct.POINTER(P),
+                                             ct.POINTER(P), ct.POINTER(P), P, P, ct.c_size_t, P]
     lib.spk_decode_frames.argtypes = [PL, P, U64, P, P, U64, ct.c_uint32, P, U64,
                                       ct.POINTER(P), ct.POINTER(U64), P, P, P,
                                       ct.c_size_t, P]

@@ -88,16 +88,29 @@ def resp_frame(seq_base: int = 0, err_code: int = 0) -> C.spk_frame:
     return _frame(pack_resp_header(0, 0, 0, err_code), 4, 8, seq_base)
 
 
-def frame_offsets_from_stream(buf: bytes, head_len: int = REQ_HEAD_LEN, len_off: int = 12):
+def frame_offsets_from_stream(buf: bytes, head_len: int = REQ_HEAD_LEN, len_off: int = 12,
+                              attach_off: int | None = None):
     """Host walk of a received byte stream of frames (what coro_connection's
-    read_head / read_payload loop sees): returns the n+1 frame offsets."""
+    read_head / read_payload loop sees: `length` body bytes, then
+    `attach_length` attachment bytes, coro_rpc_protocol.hpp:138-159; the
+    attachment length follows the length in both headers): returns the n+1
+    frame offsets (attach_off -1: no attachment field)."""
+    if attach_off is None:
+        attach_off = len_off + 4
     offs = [0]
     p = 0
     while p + head_len <= len(buf):
         (ln,) = struct.unpack_from("<I", buf, p + len_off)
-        p += head_len + ln
+        (at,) = struct.unpack_from("<I", buf, p + attach_off) if attach_off >= 0 else (0,)
+        p += head_len + ln + at
         offs.append(p)
     return offs
+
+
+def req_route_hdr() -> C.spk_route_hdr:
+    """The server's check of a request header before dispatch (read_head,
+    coro_rpc_protocol.hpp:98-117; get_serialize_protocol :84-91)."""
+    return C.spk_route_hdr(REQ_HEAD_LEN, 12, 16, MAGIC_NUMBER, VERSION_NUMBER, 0)
 
 
 def _stream(stream=None):
@@ -113,7 +126,7 @@ class FrameRouter:
     frames with unknown ids in the extra list n_keys. counts (device) holds
     n_keys + 1 sizes after route(); counts_host() reads them."""
 
-    def __init__(self, function_ids, capacity: int, device="cuda"):
+    def __init__(self, function_ids, capacity: int, device="cuda", check=True):
         import torch
         if len(function_ids) > C.SPK_MAX_ROUTES:
             raise ValueError(f"at most {C.SPK_MAX_ROUTES} function ids per router")
@@ -131,14 +144,18 @@ class FrameRouter:
         ptrs = lambda ts: (ct.c_void_p * (nk + 1))(*[t.data_ptr() for t in ts])
         self._pb, self._pe, self._pi = ptrs(self.begins), ptrs(self.ends), ptrs(self.index)
         self._keys = (ct.c_uint32 * max(nk, 1))(*(self.keys or [0]))
+        # check: frames the server would reject (bad magic / version /
+        # serialize_type, sizes that disagree with length + attach_length) are
+        # unrouted, and ends[k] is where the message ends (attachment excluded)
+        self._hdr = ct.pointer(req_route_hdr()) if check else None
 
     def route(self, wire, offsets, n: int, stream=None):
         """Stream-ordered: frame i = wire[offsets[i] .. offsets[i+1])."""
         if n > self.capacity:
             raise ValueError("more frames than the router's capacity")
-        rc = self.lib.spk_route_frames(
+        rc = self.lib.spk_route_frames_checked(
             ct.c_void_p(wire.data_ptr()), wire.numel(), ct.c_void_p(offsets.data_ptr()), n,
-            REQ_FID_OFF, self._keys, len(self.keys), self._pb, self._pe, self._pi,
+            REQ_FID_OFF, self._keys, len(self.keys), self._hdr, self._pb, self._pe, self._pi,
             ct.c_void_p(self.counts.data_ptr()), ct.c_void_p(self._ws.data_ptr()),
             self._ws.numel(), _stream(stream))
         if rc != 0:

@@ -25,19 +25,38 @@ struct RouteArgs {
   uint64_t n, wire_len;
   uint32_t key_off, nk;  // nk = n_keys (list nk = unrouted)
   uint32_t keys[SPK_MAX_ROUTES];
+  uint32_t chk;          // header check on (spk_route_hdr)
+  spk_route_hdr h;
   uint64_t *beg[kRK];
   uint64_t *end[kRK];
   uint64_t *idx[kRK];
 };
 
+__device__ __forceinline__ uint32_t ld_u32le(const uint8_t *p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// the reference server's header checks (coro_rpc_protocol.hpp:98-117) and
+// the frame size they imply: head + length + attach_length
+__device__ __forceinline__ bool header_ok(const RouteArgs &a, const uint8_t *f, uint64_t size) {
+  const spk_route_hdr &h = a.h;
+  if (size < h.head_len) return false;
+  if (h.magic >= 0 && f[0] != (uint32_t)h.magic) return false;
+  if (h.max_version >= 0 && f[1] > (uint32_t)h.max_version) return false;
+  if (h.serialize_type >= 0 && f[2] != (uint32_t)h.serialize_type) return false;
+  uint64_t want = (uint64_t)h.head_len + ld_u32le(f + h.len_off);
+  if (h.attach_off != SPK_FRAME_NONE) want += ld_u32le(f + h.attach_off);
+  return want == size;
+}
+
 // key slot of frame i: 0..nk-1, or nk when the key is unknown / unreadable
+// (or, with the header check, the frame is not one the server would dispatch)
 __device__ __forceinline__ uint32_t frame_slot(const RouteArgs &a, const uint8_t *wire,
                                                const uint64_t *offs, uint64_t i) {
   const uint64_t b = offs[i], e = offs[i + 1];
   if (e < b || e > a.wire_len || e - b < (uint64_t)a.key_off + 4) return a.nk;
-  const uint8_t *p = wire + b + a.key_off;
-  const uint32_t key = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) |
-                       ((uint32_t)p[3] << 24);
+  if (a.chk && !header_ok(a, wire + b, e - b)) return a.nk;
+  const uint32_t key = ld_u32le(wire + b + a.key_off);
   for (uint32_t k = 0; k < a.nk; ++k)
     if (a.keys[k] == key) return k;
   return a.nk;
@@ -121,6 +140,7 @@ __global__ __launch_bounds__(kScanT) void route_scan(uint64_t nblocks, uint32_t 
 }
 
 __global__ __launch_bounds__(kRT) void route_scatter(RouteArgs a,
+                                                     const uint8_t *__restrict__ wire,
                                                      const uint64_t *__restrict__ offs,
                                                      const uint8_t *__restrict__ tslot,
                                                      const uint64_t *__restrict__ bcnt) {
@@ -139,8 +159,14 @@ __global__ __launch_bounds__(kRT) void route_scatter(RouteArgs a,
   if (t >= kRK || !a.beg[t]) return;
   uint64_t pos = bcnt[(uint64_t)t * gridDim.x + blockIdx.x] + rank;
   for (uint32_t w = 0; w < wv; ++w) pos += wc[w][t];
-  a.beg[t][pos] = offs[i];
-  if (a.end[t]) a.end[t][pos] = offs[i + 1];
+  const uint64_t b = offs[i];
+  a.beg[t][pos] = b;
+  if (a.end[t]) {
+    uint64_t e = offs[i + 1];
+    // checked frames: the message ends before the attachment
+    if (a.chk && t < a.nk) e = b + a.h.head_len + ld_u32le(wire + b + a.h.len_off);
+    a.end[t][pos] = e;
+  }
   if (a.idx[t]) a.idx[t][pos] = i;
 }
 
@@ -166,13 +192,18 @@ extern "C" size_t spk_route_workspace_bytes(uint64_t n_frames, uint32_t n_keys) 
   return (size_t)(((n_frames + 255) & ~255ull) + nb * kRK * 8 + 256);
 }
 
-extern "C" int spk_route_frames(const void *d_wire, uint64_t wire_len,
-                                const uint64_t *d_frame_offsets, uint64_t n_frames,
-                                uint32_t key_off, const uint32_t *h_keys, uint32_t n_keys,
-                                uint64_t *const *d_begins, uint64_t *const *d_ends,
-                                uint64_t *const *d_index, uint64_t *d_counts, void *d_ws,
-                                size_t ws_bytes, void *stream) {
+extern "C" int spk_route_frames_checked(const void *d_wire, uint64_t wire_len,
+                                        const uint64_t *d_frame_offsets, uint64_t n_frames,
+                                        uint32_t key_off, const uint32_t *h_keys,
+                                        uint32_t n_keys, const spk_route_hdr *hdr,
+                                        uint64_t *const *d_begins, uint64_t *const *d_ends,
+                                        uint64_t *const *d_index, uint64_t *d_counts,
+                                        void *d_ws, size_t ws_bytes, void *stream) {
   if (n_keys > SPK_MAX_ROUTES || (n_keys && !h_keys) || !d_counts || !d_begins) return SPK_E_ARG;
+  if (hdr && (hdr->head_len < 4 || hdr->len_off > hdr->head_len - 4 ||
+              (hdr->attach_off != SPK_FRAME_NONE && hdr->attach_off > hdr->head_len - 4) ||
+              key_off > hdr->head_len - 4))
+    return SPK_E_ARG;
   if (n_frames && (!d_frame_offsets || !d_wire || !d_ws)) return SPK_E_ARG;
   if (ws_bytes < spk_route_workspace_bytes(n_frames, n_keys)) return SPK_E_WORKSPACE;
   for (uint32_t k = 0; k < n_keys; ++k) {
@@ -186,6 +217,8 @@ extern "C" int spk_route_frames(const void *d_wire, uint64_t wire_len,
   a.wire_len = wire_len;
   a.key_off = key_off;
   a.nk = n_keys;
+  a.chk = hdr ? 1u : 0u;
+  if (hdr) a.h = *hdr;
   for (uint32_t k = 0; k < n_keys; ++k) a.keys[k] = h_keys[k];
   for (uint32_t k = 0; k <= n_keys; ++k) {
     a.beg[k] = d_begins[k];
@@ -204,9 +237,20 @@ extern "C" int spk_route_frames(const void *d_wire, uint64_t wire_len,
   SPK_LAUNCH(route_count, dim3((unsigned)nb), dim3(kRT), 0, s, a, wire, d_frame_offsets, tslot,
              bcnt);
   SPK_LAUNCH(route_scan, dim3(1), dim3(kScanT), 0, s, nb, n_keys, bcnt, d_counts);
-  SPK_LAUNCH(route_scatter, dim3((unsigned)nb), dim3(kRT), 0, s, a, d_frame_offsets,
+  SPK_LAUNCH(route_scatter, dim3((unsigned)nb), dim3(kRT), 0, s, a, wire, d_frame_offsets,
              (const uint8_t *)tslot, (const uint64_t *)bcnt);
   return hipGetLastError() == hipSuccess ? SPK_OK : SPK_E_HIP;
+}
+
+extern "C" int spk_route_frames(const void *d_wire, uint64_t wire_len,
+                                const uint64_t *d_frame_offsets, uint64_t n_frames,
+                                uint32_t key_off, const uint32_t *h_keys, uint32_t n_keys,
+                                uint64_t *const *d_begins, uint64_t *const *d_ends,
+                                uint64_t *const *d_index, uint64_t *d_counts, void *d_ws,
+                                size_t ws_bytes, void *stream) {
+  return spk_route_frames_checked(d_wire, wire_len, d_frame_offsets, n_frames, key_off, h_keys,
+                                  n_keys, nullptr, d_begins, d_ends, d_index, d_counts, d_ws,
+                                  ws_bytes, stream);
 }
 
 extern "C" int spk_copy_frame_field(void *d_dst, const uint64_t *d_dst_offsets, uint32_t dst_off,
