@@ -472,6 +472,33 @@ int spk_encode_framed_echo(const spk_layout *L, uint64_t n, const void *d_recs,
                            const uint64_t *d_seq_offsets, uint32_t seq_src_off, void *d_out,
                            uint64_t out_cap, uint64_t *d_msg_offsets, void *d_ws,
                            size_t ws_bytes, void *stream);
+/* ---- device-resident message counts (graph-capturable server steps) ------
+ * The _dn forms of the plan, the echo encode and the frames decode take the
+ * MESSAGES-mode message count from device memory: the count is
+ * min(*d_n, n_max), read by the kernels when they run. After
+ * spk_route_frames, d_n = &d_counts[k] sizes function id k's decode and
+ * response encode without the host reading the counts back, so route ->
+ * decode -> encode is one stream-ordered (and capturable) sequence. Grids,
+ * workspace and the trivial-record capacity check are sized for n_max (the
+ * caller's buffers: rec_cap / out_cap / offsets for n_max messages). A decode
+ * whose *d_n exceeds n_max decodes the first n_max frames and reports
+ * SPK_ERRC_CAPACITY. Flat layouts only (SPK_E_LAYOUT for ARRAY / VARIANT /
+ * group / FVAR layouts, whose kernels size on the host). */
+int spk_plan_dn(const spk_layout *L, const uint64_t *d_n, uint64_t n_max, const void *d_recs,
+                const void *const *d_heaps, spk_plan_t *d_plan, void *d_ws, size_t ws_bytes,
+                void *stream);
+int spk_decode_frames_dn(const spk_layout *L, const void *d_wire, uint64_t wire_len,
+                         const uint64_t *d_begins, const uint64_t *d_ends, const uint64_t *d_n,
+                         uint64_t n_max, uint32_t prefix_len, void *d_recs, uint64_t rec_cap,
+                         void *const *d_heaps, const uint64_t *heap_caps, spk_dresult_t *d_res,
+                         int32_t *d_errc, void *d_ws, size_t ws_bytes, void *stream);
+int spk_encode_framed_echo_dn(const spk_layout *L, const uint64_t *d_n, uint64_t n_max,
+                              const void *d_recs, const void *const *d_heaps,
+                              const spk_plan_t *d_plan, const spk_frame *F,
+                              const void *d_seq_src, const uint64_t *d_seq_offsets,
+                              uint32_t seq_src_off, void *d_out, uint64_t out_cap,
+                              uint64_t *d_msg_offsets, void *d_ws, size_t ws_bytes,
+                              void *stream);
 /* For i < n: copy `bytes` (1..8) from d_src[d_src_offsets[i] + src_off] to
  * d_dst[d_dst_offsets[i] + dst_off]: the response header echoes its request's
  * seq_num (coro_rpc_protocol.hpp:191-201) when responses were encoded per

@@ -342,7 +342,9 @@ def test_long_records_bounded_time(kind):
           f" tiles repaired {r.tiles_repaired}, sequential {r.tiles_sequential}")
     assert min(ts) < bound_ms, ts
     if kind == "huge":
-        assert r.tiles_sequential > 0  # the multi-MiB records are passed through by the fixer
+        # the tiles inside the multi-MiB records were entered wrongly and passed
+        # through (fused decode: re-composed blocks; tile pipeline: the fixer)
+        assert r.tiles_sequential + r.tiles_repaired > 0
 
 
 def test_screen_defeating_payload_bounded_time():

@@ -138,6 +138,7 @@ CODEC_SYMBOLS = ["spk_abi_version", "spk_errc_message", "spk_layout_check",
                  "spk_decode_shard_index", "spk_decode_shard_emit",
                  # mixed-type frame batches in arrival order
                  "spk_route_workspace_bytes", "spk_route_frames", "spk_route_frames_checked", "spk_decode_frames",
+                 "spk_plan_dn", "spk_decode_frames_dn", "spk_encode_framed_echo_dn",
                  "spk_copy_frame_field", "spk_encode_framed_echo",
                  # runtime helpers (front ends without HIP headers)
                  "spk_device_alloc", "spk_device_free", "spk_host_alloc_pinned",
@@ -203,6 +204,12 @@ def _bind_codec(lib):
                                       ct.c_size_t, P]
     lib.spk_encode_framed_echo.argtypes = [PL, U64, P, ct.POINTER(P), P, ct.POINTER(spk_frame),
                                            P, P, ct.c_uint32, P, U64, P, P, ct.c_size_t, P]
+    lib.spk_plan_dn.argtypes = [PL, P, U64, P, ct.POINTER(P), P, P, ct.c_size_t, P]
+    lib.spk_decode_frames_dn.argtypes = [PL, P, U64, P, P, P, U64, ct.c_uint32, P, U64,
+                                         ct.POINTER(P), ct.POINTER(U64), P, P, P, ct.c_size_t, P]
+    lib.spk_encode_framed_echo_dn.argtypes = [PL, P, U64, P, ct.POINTER(P), P,
+                                              ct.POINTER(spk_frame), P, P, ct.c_uint32, P, U64,
+                                              P, P, ct.c_size_t, P]
     lib.spk_copy_frame_field.argtypes = [P, P, ct.c_uint32, P, P, ct.c_uint32, ct.c_uint32,
                                          U64, P]
     lib.spk_trace_enable.argtypes = [ct.c_int]

@@ -246,6 +246,23 @@ int spk_plan_ex(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
   return hip_rc(launch_var_plan(L, mode, n, d_recs, d_plan, d_ws, ws_bytes, s));
 }
 
+int spk_plan_dn(const spk_layout *L, const uint64_t *d_n, uint64_t n_max, const void *d_recs,
+                const void *const *d_heaps, spk_plan_t *d_plan, void *d_ws, size_t ws_bytes,
+                void *stream) {
+  int rc = spk_layout_check(L);
+  if (rc) return rc;
+  if (!d_n || !d_plan || !d_ws || (n_max && !d_recs)) return SPK_E_ARG;
+  if (layout_nested(L)) return SPK_E_LAYOUT;
+  if (ws_bytes < spk_workspace_bytes(L, SPK_MODE_MESSAGES, n_max, 0)) return SPK_E_WORKSPACE;
+  hipStream_t s = (hipStream_t)stream;
+  if (is_trivial(L))
+    return hip_rc(launch_fixed_plan(L, SPK_MODE_MESSAGES, n_max, d_plan, d_ws, s, d_n));
+  if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
+  (void)d_heaps;
+  return hip_rc(launch_var_plan(L, SPK_MODE_MESSAGES, n_max, d_recs, d_plan, d_ws, ws_bytes, s,
+                                d_n));
+}
+
 int spk_plan(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
              spk_plan_t *d_plan, void *d_ws, size_t ws_bytes, void *stream) {
   if (L && spk_layout_check(L) == SPK_OK && layout_nested(L) && n) return SPK_E_ARG;
@@ -264,9 +281,10 @@ static int encode_impl(const spk_layout *L, int mode, uint64_t n, const void *d_
                        const void *const *d_heaps, const spk_plan_t *d_plan, void *d_out,
                        uint64_t out_cap, uint64_t *d_msg_offsets, const spk_frame *F,
                        void *d_ws, size_t ws_bytes, void *stream,
-                       const SeqEcho *echo = nullptr) {
+                       const SeqEcho *echo = nullptr, const uint64_t *d_n = nullptr) {
   int rc = spk_layout_check(L);
   if (rc) return rc;
+  if (d_n && layout_nested(L)) return SPK_E_LAYOUT;
   if ((mode != SPK_MODE_VECTOR && mode != SPK_MODE_MESSAGES) || !d_plan || !d_ws || !d_out)
     return SPK_E_ARG;
   if (n && !d_recs) return SPK_E_ARG;
@@ -283,7 +301,8 @@ static int encode_impl(const spk_layout *L, int mode, uint64_t n, const void *d_
     const uint32_t P = F ? F->prefix_len : 0;
     const uint64_t total = n * (uint64_t)(P + write_hdr(hb, L->fmt_one, 1) + L->rec_stride);
     if (total > out_cap) return SPK_E_CAPACITY;
-    return hip_rc(launch_fixed_encode_messages(L, n, d_recs, d_out, d_msg_offsets, F, s, echo));
+    return hip_rc(launch_fixed_encode_messages(L, n, d_recs, d_out, d_msg_offsets, F, s, echo,
+                                               d_n));
   }
   if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
   if ((rc = heaps_check(L, n, d_heaps))) return rc;
@@ -291,7 +310,7 @@ static int encode_impl(const spk_layout *L, int mode, uint64_t n, const void *d_
     return hip_rc(launch_nested_encode(L, mode, n, d_recs, d_heaps, d_out, out_cap, d_msg_offsets, F, 0,
                                        d_ws, s, echo));
   return hip_rc(launch_var_encode(L, mode, n, d_recs, d_heaps, d_plan, d_out, out_cap,
-                                  d_msg_offsets, F, d_ws, ws_bytes, s, echo));
+                                  d_msg_offsets, F, d_ws, ws_bytes, s, echo, d_n));
 }
 
 int spk_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
@@ -333,9 +352,10 @@ static int decode_impl(const spk_layout *L, int mode, const void *d_wire, uint64
                        void *d_recs, uint64_t rec_cap, void *const *d_heaps,
                        const uint64_t *heap_caps, spk_dresult_t *d_res, int32_t *d_errc,
                        void *d_ws, size_t ws_bytes, void *stream,
-                       const uint64_t *d_msg_ends = nullptr) {
+                       const uint64_t *d_msg_ends = nullptr, const uint64_t *d_n = nullptr) {
   int rc = spk_layout_check(L);
   if (rc) return rc;
+  if (d_n && layout_nested(L)) return SPK_E_LAYOUT;
   if ((mode != SPK_MODE_VECTOR && mode != SPK_MODE_MESSAGES) || !d_res || !d_ws)
     return SPK_E_ARG;
   if (wire_len && !d_wire) return SPK_E_ARG;
@@ -349,7 +369,7 @@ static int decode_impl(const spk_layout *L, int mode, const void *d_wire, uint64
                                                d_ws, s));
     return hip_rc(launch_fixed_decode_messages(L, d_wire, wire_len, d_msg_offsets, n_msgs,
                                                prefix, d_recs, rec_cap, d_res, d_errc, d_ws,
-                                               s, d_msg_ends));
+                                               s, d_msg_ends, d_n));
   }
   if (d_recs && (uintptr_t)d_recs % 8) return SPK_E_ARG;
   const uint32_t spans = heap_count(L);
@@ -364,7 +384,7 @@ static int decode_impl(const spk_layout *L, int mode, const void *d_wire, uint64
   }
   return hip_rc(launch_var_decode(L, mode, d_wire, wire_len, d_msg_offsets, n_msgs, prefix,
                                   d_recs, rec_cap, d_heaps, heap_caps, d_res, d_errc, d_ws,
-                                  ws_bytes, s, 0, 0, d_msg_ends));
+                                  ws_bytes, s, 0, 0, d_msg_ends, d_n));
 }
 
 int spk_decode(const spk_layout *L, int mode, const void *d_wire, uint64_t wire_len,
@@ -396,6 +416,33 @@ int spk_decode_frames(const spk_layout *L, const void *d_wire, uint64_t wire_len
   return decode_impl(L, SPK_MODE_MESSAGES, d_wire, wire_len, d_begins, n_msgs, prefix_len,
                      d_recs, rec_cap, d_heaps, heap_caps, d_res, d_errc, d_ws, ws_bytes, stream,
                      d_ends);
+}
+
+int spk_decode_frames_dn(const spk_layout *L, const void *d_wire, uint64_t wire_len,
+                         const uint64_t *d_begins, const uint64_t *d_ends, const uint64_t *d_n,
+                         uint64_t n_max, uint32_t prefix_len, void *d_recs, uint64_t rec_cap,
+                         void *const *d_heaps, const uint64_t *heap_caps, spk_dresult_t *d_res,
+                         int32_t *d_errc, void *d_ws, size_t ws_bytes, void *stream) {
+  if (!d_n || prefix_len > SPK_MAX_FRAME || (n_max && (!d_begins || !d_ends))) return SPK_E_ARG;
+  return decode_impl(L, SPK_MODE_MESSAGES, d_wire, wire_len, d_begins, n_max, prefix_len,
+                     d_recs, rec_cap, d_heaps, heap_caps, d_res, d_errc, d_ws, ws_bytes, stream,
+                     d_ends, d_n);
+}
+
+int spk_encode_framed_echo_dn(const spk_layout *L, const uint64_t *d_n, uint64_t n_max,
+                              const void *d_recs, const void *const *d_heaps,
+                              const spk_plan_t *d_plan, const spk_frame *F,
+                              const void *d_seq_src, const uint64_t *d_seq_offsets,
+                              uint32_t seq_src_off, void *d_out, uint64_t out_cap,
+                              uint64_t *d_msg_offsets, void *d_ws, size_t ws_bytes,
+                              void *stream) {
+  if (!d_n || !F || F->seq_off == SPK_FRAME_NONE) return SPK_E_ARG;
+  if (n_max && (!d_seq_src || !d_seq_offsets)) return SPK_E_ARG;
+  int rc = frame_check(F);
+  if (rc) return rc;
+  const SeqEcho echo{(const uint8_t *)d_seq_src, d_seq_offsets, seq_src_off, 0};
+  return encode_impl(L, SPK_MODE_MESSAGES, n_max, d_recs, d_heaps, d_plan, d_out, out_cap,
+                     d_msg_offsets, F, d_ws, ws_bytes, stream, n_max ? &echo : nullptr, d_n);
 }
 
 int spk_encode_body(const spk_layout *L, uint64_t n, const void *d_recs,

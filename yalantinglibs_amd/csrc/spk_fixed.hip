@@ -112,6 +112,7 @@ static unsigned copy_grid(uint64_t max_bytes) {
 struct FixedPlanArgs {
   spk_msgfmt fmt;  // message format (vector or one)
   uint64_t n;
+  const uint64_t *dn;  // MESSAGES: device count (min(*dn, n)) or null
   uint32_t stride;
   int mode;
 };
@@ -140,9 +141,10 @@ __global__ void fixed_plan_kernel(FixedPlanArgs a, spk_plan_t *plan, uint8_t *ws
   } else {
     const HdrShape h = hdr_shape(a.fmt.flags, a.fmt.literal_len, 1);
     write_hdr(ws + kWsHdrMsg, a.fmt, 1);
-    p.total_bytes = a.n * (h.len + a.stride);
+    const uint64_t n = dev_count(a.n, a.dn);
+    p.total_bytes = n * (h.len + a.stride);
     p.max_count = 0;
-    p.var_bytes = a.n * a.stride;
+    p.var_bytes = n * a.stride;
     p.width = 1;
     p.header_bytes = h.len;
     p.metainfo = h.meta;
@@ -152,10 +154,12 @@ __global__ void fixed_plan_kernel(FixedPlanArgs a, spk_plan_t *plan, uint8_t *ws
 }
 
 hipError_t launch_fixed_plan(const spk_layout *L, int mode, uint64_t n,
-                             spk_plan_t *d_plan, void *d_ws, hipStream_t s) {
+                             spk_plan_t *d_plan, void *d_ws, hipStream_t s,
+                             const uint64_t *d_n) {
   FixedPlanArgs a;
   a.fmt = mode == SPK_MODE_VECTOR ? L->fmt_vector : L->fmt_one;
   a.n = n;
+  a.dn = d_n;
   a.stride = L->rec_stride;
   a.mode = mode;
   SPK_LAUNCH(fixed_plan_kernel, dim3(1), dim3(64), 0, s, a, d_plan,
@@ -257,6 +261,7 @@ constexpr uint32_t kMsgHdrMax = 320;  // frame prefix (<= 64) + struct_pack head
 
 struct MsgEncArgs {
   uint64_t n;
+  const uint64_t *dn;  // device count (min(*dn, n)) or null
   uint32_t stride;    // bytes
   uint32_t hlen;      // header bytes (frame prefix + struct_pack header)
   uint32_t seq_off;   // frame sequence field (u32 LE = seq_base + i) or ~0u
@@ -278,8 +283,9 @@ __device__ __forceinline__ uint8_t msg_hdr_byte(const uint8_t *hdr, uint32_t r, 
 __global__ __launch_bounds__(256) void fixed_msg_encode_w4(
     MsgEncArgs a, const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
     uint64_t *__restrict__ offs) {
+  const uint64_t N = dev_count(a.n, a.dn);
   const uint32_t Hw = a.hlen >> 2, Sw = a.stride >> 2, Mw = Hw + Sw;
-  const uint64_t total_w = a.n * Mw;
+  const uint64_t total_w = N * Mw;
   const uint64_t nchunks = (total_w + 3) >> 2;
   const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks;
@@ -294,7 +300,7 @@ __global__ __launch_bounds__(256) void fixed_msg_encode_w4(
         uint32_t h;
         __builtin_memcpy(&h, a.hdr + 4 * r, 4);
         // (i == n: the padding past the last message; an echo has no entry)
-        v[j] = 4 * r == a.seq_off && i < a.n ? seq_value(a.echo, a.seq_base, i) : h;
+        v[j] = 4 * r == a.seq_off && i < N ? seq_value(a.echo, a.seq_base, i) : h;
       } else {
         v[j] = (d0 + j < total_w) ? in[i * Sw + (r - Hw)] : 0u;
       }
@@ -312,7 +318,7 @@ __global__ __launch_bounds__(256) void fixed_msg_encode_w4(
   }
   if (offs) {
     const uint64_t M = (uint64_t)Mw * 4;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= a.n;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= N;
          i += gstride)
       offs[i] = i * M;
   }
@@ -322,8 +328,9 @@ __global__ __launch_bounds__(256) void fixed_msg_encode_w4(
 __global__ __launch_bounds__(256) void fixed_msg_encode_b1(
     MsgEncArgs a, const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
     uint64_t *__restrict__ offs) {
+  const uint64_t N = dev_count(a.n, a.dn);
   const uint64_t M = (uint64_t)a.hlen + a.stride;
-  const uint64_t total = a.n * M;
+  const uint64_t total = N * M;
   const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < total;
        b += gstride) {
@@ -333,7 +340,7 @@ __global__ __launch_bounds__(256) void fixed_msg_encode_b1(
                         : in[i * a.stride + (r - a.hlen)];
   }
   if (offs)
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= a.n;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= N;
          i += gstride)
       offs[i] = i * M;
 }
@@ -366,6 +373,7 @@ constexpr uint32_t kStagePer = 5;  // 16-B staging loads in flight per lane (dec
 struct MsgLdsArgs {
   spk_msgfmt fmt;   // decode only
   uint64_t n;
+  const uint64_t *dn;  // device count (min(*dn, n)) or null
   uint64_t wire_len;
   uint64_t rec_cap;
   uint32_t stride;  // S (multiple of 4)
@@ -394,15 +402,16 @@ template <bool DW>
 __global__ __launch_bounds__(kMsgThreads) void fixed_msg_encode_lds(
     MsgLdsArgs a, const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
     uint64_t *__restrict__ offs) {
+  const uint64_t N = dev_count(a.n, a.dn);
   extern __shared__ v4u smem_v4[];
   uint8_t *hdr = reinterpret_cast<uint8_t *>(smem_v4);
   uint8_t *inl = hdr + kMsgHdrMax;
   const uint32_t tid = threadIdx.x;
   const uint32_t S = a.stride, H = a.hlen, M = H + S;
   const uint64_t first = (uint64_t)blockIdx.x * a.R;
-  if (offs && blockIdx.x == gridDim.x - 1 && tid == 0) offs[a.n] = a.n * M;
-  if (first >= a.n) return;
-  const uint32_t nR = (uint32_t)((a.n - first) < a.R ? (a.n - first) : a.R);
+  if (offs && blockIdx.x == gridDim.x - 1 && tid == 0) offs[N] = N * M;
+  if (first >= N) return;
+  const uint32_t nR = (uint32_t)((N - first) < a.R ? (N - first) : a.R);
   for (uint32_t k = tid; k < H; k += kMsgThreads) hdr[k] = a.hdr[k];
   const uint8_t *src = in + first * S;
   const uint32_t bin = nR * S;  // multiple of 4
@@ -466,13 +475,16 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
     MsgLdsArgs a, const uint8_t *__restrict__ wire, const uint64_t *__restrict__ offs,
     int32_t *__restrict__ errc, spk_dresult_t *__restrict__ res, uint8_t *__restrict__ out,
     uint64_t *__restrict__ part) {
+  const uint64_t N = dev_count(a.n, a.dn);
   extern __shared__ v4u smem_v4[];
   uint8_t *stage = reinterpret_cast<uint8_t *>(smem_v4);
   __shared__ uint64_t s_lo[kMsgThreads / 64], s_hi[kMsgThreads / 64];
   __shared__ uint64_t s_pay[kMsgThreads];  // payload position (staged: LDS offset)
   const uint32_t tid = threadIdx.x;
   const uint32_t S = a.stride;
-  const uint64_t ngroups = (a.n + a.R - 1) / a.R;
+  const uint64_t ngroups = (N + a.R - 1) / a.R;
+  // more frames than the caller's n_max: the excess is not decoded
+  if (a.dn && blockIdx.x == 0 && tid == 0 && *a.dn > a.n) atomicExch(&res->errc, SPK_ERRC_CAPACITY);
   // ok / consumed accumulate over the block's groups: one atomic per wave at
   // the end (same-address atomics per group would serialise in L2)
   unsigned long long ok = 0, consumed = 0;
@@ -480,7 +492,7 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
   // message bounds of this lane in group g (prefetched one group ahead)
   auto bounds = [&](uint64_t g, uint64_t &b, uint64_t &e) {
     const uint64_t i = g * a.R + tid;
-    if (g >= ngroups || tid >= a.R || i >= a.n) return;
+    if (g >= ngroups || tid >= a.R || i >= N) return;
     b = offs ? offs[i] : i * a.fixed_M;
     e = offs ? (a.ends ? a.ends[i] : offs[i + 1]) : (i + 1) * a.fixed_M;
   };
@@ -488,7 +500,7 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
   bounds(blockIdx.x, b_nx, e_nx);
   for (uint64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
     const uint64_t first = g * a.R;
-    const uint32_t nR = (uint32_t)((a.n - first) < a.R ? (a.n - first) : a.R);
+    const uint32_t nR = (uint32_t)((N - first) < a.R ? (N - first) : a.R);
     uint64_t b = b_nx, e = e_nx;
     b_nx = e_nx = 0;
     bounds(g + gridDim.x, b_nx, e_nx);
@@ -697,11 +709,13 @@ static uint32_t msg_header(const spk_layout *L, const spk_frame *F, uint8_t *hdr
 hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
                                         const void *d_recs, void *d_out,
                                         uint64_t *d_offsets, const spk_frame *F,
-                                        hipStream_t s, const SeqEcho *echo) {
+                                        hipStream_t s, const SeqEcho *echo,
+                                        const uint64_t *d_n) {
   {
     MsgLdsArgs b = {};
     if (echo) b.echo = *echo;
     b.n = n;
+    b.dn = d_n;
     b.stride = L->rec_stride;
     b.hlen = msg_header(L, F, b.hdr, &b.seq_off, &b.seq_base);
     const uint32_t M = b.hlen + b.stride;
@@ -727,6 +741,7 @@ hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
   MsgEncArgs a = {};
   if (echo) a.echo = *echo;
   a.n = n;
+  a.dn = d_n;
   a.stride = L->rec_stride;
   a.hlen = msg_header(L, F, a.hdr, &a.seq_off, &a.seq_base);
   const bool w4 = (a.hlen % 4 == 0) && (a.stride % 4 == 0) &&
@@ -750,6 +765,7 @@ hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
 struct MsgDecArgs {
   spk_msgfmt fmt;
   uint64_t n;
+  const uint64_t *dn;  // device count (min(*dn, n)) or null
   uint64_t wire_len;
   uint64_t rec_cap;
   uint32_t stride;
@@ -762,9 +778,12 @@ __global__ __launch_bounds__(256) void fixed_msg_parse(
     MsgDecArgs a, const uint8_t *__restrict__ wire, const uint64_t *__restrict__ offs,
     uint64_t *__restrict__ payload, int32_t *__restrict__ errc,
     spk_dresult_t *__restrict__ res) {
+  const uint64_t N = dev_count(a.n, a.dn);
   const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
   unsigned long long ok = 0, consumed = 0;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n;
+  if (a.dn && blockIdx.x == 0 && threadIdx.x == 0 && *a.dn > a.n)
+    atomicExch(&res->errc, SPK_ERRC_CAPACITY);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N;
        i += gstride) {
     uint64_t b = offs ? offs[i] : i * a.fixed_M;
     uint64_t e = offs ? (a.ends ? a.ends[i] : offs[i + 1]) : (i + 1) * a.fixed_M;
@@ -804,7 +823,8 @@ __global__ __launch_bounds__(256) void fixed_msg_parse(
 
 __global__ __launch_bounds__(256) void fixed_msg_gather(
     uint64_t n, uint32_t stride, const uint8_t *__restrict__ wire,
-    const uint64_t *__restrict__ payload, uint8_t *__restrict__ out) {
+    const uint64_t *__restrict__ payload, uint8_t *__restrict__ out, const uint64_t *dn) {
+  n = dev_count(n, dn);
   const uint64_t gstride = (uint64_t)gridDim.x * blockDim.x;
   if ((stride & 3) == 0) {
     const uint32_t Sw = stride >> 2;
@@ -842,8 +862,9 @@ hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
                                            uint64_t n, uint32_t prefix, void *d_recs,
                                            uint64_t rec_cap, spk_dresult_t *d_res,
                                            int32_t *d_errc, void *d_ws, hipStream_t s,
-                                           const uint64_t *d_msg_ends) {
+                                           const uint64_t *d_msg_ends, const uint64_t *d_n) {
   MsgDecArgs a;
+  a.dn = d_n;
   a.prefix = prefix;
   a.ends = d_msg_ends;
   a.fmt = L->fmt_one;
@@ -860,6 +881,7 @@ hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
     MsgLdsArgs b = {};
     b.fmt = L->fmt_one;
     b.n = n;
+    b.dn = d_n;
     b.wire_len = wire_len;
     b.rec_cap = rec_cap;
     b.stride = L->rec_stride;
@@ -888,7 +910,7 @@ hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
                                                   : nrec * L->rec_stride;
   SPK_LAUNCH(fixed_msg_gather, dim3(elem_grid(items)), dim3(256), 0, s, nrec,
                      (uint32_t)L->rec_stride, (const uint8_t *)d_wire,
-                     (const uint64_t *)payload, (uint8_t *)d_recs);
+                     (const uint64_t *)payload, (uint8_t *)d_recs, d_n);
   return hipGetLastError();
 }
 

@@ -258,15 +258,24 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
                                 hipStream_t s, uint32_t body_w = 0, uint64_t body_n = 0,
                                 const uint64_t *d_msg_ends = nullptr);
 // spk_fixed.hip
+// d_n (MESSAGES mode, nullable): the message count is min(*d_n, n), read on
+// the device (spk_*_dn); grids and workspace stay sized for n
+__device__ __forceinline__ uint64_t dev_count(uint64_t n, const uint64_t *d_n) {
+  if (!d_n) return n;
+  const uint64_t m = *d_n;
+  return m < n ? m : n;
+}
 hipError_t launch_fixed_plan(const spk_layout *L, int mode, uint64_t n,
-                             spk_plan_t *d_plan, void *d_ws, hipStream_t s);
+                             spk_plan_t *d_plan, void *d_ws, hipStream_t s,
+                             const uint64_t *d_n = nullptr);
 hipError_t launch_fixed_encode_vector(const spk_layout *L, uint64_t n,
                                       const void *d_recs, void *d_out,
                                       const void *d_ws, hipStream_t s);
 hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
                                         const void *d_recs, void *d_out,
                                         uint64_t *d_offsets, const spk_frame *F,
-                                        hipStream_t s, const SeqEcho *echo = nullptr);
+                                        hipStream_t s, const SeqEcho *echo = nullptr,
+                                        const uint64_t *d_n = nullptr);
 // body_w != 0: d_wire is a message BODY of body_n records at width body_w
 // (no header / count: spk_decode_body)
 hipError_t launch_fixed_decode_vector(const spk_layout *L, const void *d_wire,
@@ -280,19 +289,20 @@ hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
                                         uint32_t prefix, void *d_recs, uint64_t rec_cap,
                                         spk_dresult_t *d_res, int32_t *d_errc,
                                         void *d_ws, hipStream_t s,
-                                        const uint64_t *d_msg_ends = nullptr);
+                                        const uint64_t *d_msg_ends = nullptr,
+                                        const uint64_t *d_n = nullptr);
 // spk_var.hip
 size_t var_workspace_bytes(const spk_layout *L, int mode, uint64_t n,
                            uint64_t wire_len);
 hipError_t launch_var_plan(const spk_layout *L, int mode, uint64_t n,
                            const void *d_recs, spk_plan_t *d_plan, void *d_ws,
-                           size_t ws_bytes, hipStream_t s);
+                           size_t ws_bytes, hipStream_t s, const uint64_t *d_n = nullptr);
 hipError_t launch_var_encode(const spk_layout *L, int mode, uint64_t n,
                              const void *d_recs, const void *const *d_heaps,
                              const spk_plan_t *d_plan, void *d_out,
                              uint64_t out_cap, uint64_t *d_offsets, const spk_frame *F,
                              void *d_ws, size_t ws_bytes, hipStream_t s,
-                             const SeqEcho *echo = nullptr);
+                             const SeqEcho *echo = nullptr, const uint64_t *d_n = nullptr);
 hipError_t launch_var_encode_body(const spk_layout *L, uint64_t n, const void *d_recs,
                                   const void *const *d_heaps, uint32_t width, void *d_out,
                                   uint64_t out_cap, void *d_ws, size_t ws_bytes,
@@ -303,5 +313,6 @@ hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
                              void *const *d_heaps, const uint64_t *heap_caps,
                              spk_dresult_t *d_res, int32_t *d_errc, void *d_ws,
                              size_t ws_bytes, hipStream_t s, uint32_t body_w = 0, uint64_t body_n = 0,
-                             const uint64_t *d_msg_ends = nullptr);
+                             const uint64_t *d_msg_ends = nullptr,
+                             const uint64_t *d_n = nullptr);
 }  // namespace spk

@@ -64,6 +64,7 @@ constexpr uint64_t kPlanRPB = kRPB * kPlanSub;  // records per plan block
 struct VarArgs {
   KLayout L;
   uint64_t n;
+  const uint64_t *dn;  // MESSAGES: device count (min(*dn, n)) or null
   int mode;
   uint32_t fpre;      // MESSAGES: frame prefix bytes before every message
   const uint8_t *heaps[kVS];
@@ -301,6 +302,7 @@ struct Partial {
 __global__ __launch_bounds__(kThreads) void var_plan_reduce(
     VarArgs a, const uint8_t *__restrict__ recs, uint8_t *__restrict__ ws,
     const uint8_t *__restrict__ hdrlen_tbl) {
+  const uint64_t N = dev_count(a.n, a.dn);
   __shared__ uint64_t sh[kThreads / 64];
   const uint64_t r0 = (uint64_t)blockIdx.x * kPlanRPB;
   uint64_t mx = 0, tot = 0, sub[kPlanSub];
@@ -309,7 +311,7 @@ __global__ __launch_bounds__(kThreads) void var_plan_reduce(
     for (int q = 0; q < kIPT; ++q) {
       const uint64_t i = r0 + (uint64_t)j * kRPB + (uint64_t)q * kThreads + threadIdx.x;
       uint64_t sum = 0;
-      if (i < a.n) {
+      if (i < N) {
         uint64_t var, maxc;
         rec_sizes(a.L, recs + i * a.L.stride, var, maxc);
         if (a.mode == SPK_MODE_VECTOR) {
@@ -594,11 +596,12 @@ __global__ __launch_bounds__(kThreads, 5) void var_encode_write(
     VarArgs a, const uint8_t *__restrict__ recs, uint8_t *__restrict__ out,
     uint64_t out_cap, const uint8_t *__restrict__ ws,
     const spk_plan_t *__restrict__ plan, uint64_t *__restrict__ offs) {
+  const uint64_t N = dev_count(a.n, a.dn);
   __shared__ __align__(16) uint8_t lds[kEncWin];
   __shared__ uint64_t sh[kThreads / 64];
   __shared__ BigSeg big[kBigMax];
   const uint64_t total =
-      plan->total_bytes + (a.mode == SPK_MODE_MESSAGES ? a.n * (uint64_t)a.fpre : 0);
+      plan->total_bytes + (a.mode == SPK_MODE_MESSAGES ? N * (uint64_t)a.fpre : 0);
   if (total > out_cap) return;  // caller reads plan->total_bytes
   const uint32_t w_vec = plan->width;
   const uint32_t hdr_vec = plan->header_bytes;
@@ -634,7 +637,7 @@ __global__ __launch_bounds__(kThreads, 5) void var_encode_write(
     const uint64_t i = r0 + (uint64_t)j * kThreads + threadIdx.x;
     uint64_t sz = 0;
     uint32_t w = w_vec;
-    if (i < a.n) {
+    if (i < N) {
       uint64_t var, maxc;
       rec_sizes(a.L, recs + i * a.L.stride, var, maxc);
       if (a.mode == SPK_MODE_VECTOR) {
@@ -650,11 +653,11 @@ __global__ __launch_bounds__(kThreads, 5) void var_encode_write(
     szj[j] = sz;
     wj[j] = w;
     g += btot;
-    if (a.mode == SPK_MODE_MESSAGES && offs && i < a.n && ysub == 0) offs[i] = pj[j];
+    if (a.mode == SPK_MODE_MESSAGES && offs && i < N && ysub == 0) offs[i] = pj[j];
   }
   if (a.mode == SPK_MODE_MESSAGES && offs && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 &&
       ysub == 0)
-    offs[a.n] = total;
+    offs[N] = total;
   const uint64_t g1 = g;
   if (g1 == g0) return;
   // large span payloads of this block's records -> cooperative list
@@ -664,7 +667,7 @@ __global__ __launch_bounds__(kThreads, 5) void var_encode_write(
     skip[j] = 0;
     const uint64_t i = r0 + (uint64_t)j * kThreads + threadIdx.x;
     uint32_t nbig = 0;
-    if (i < a.n) {
+    if (i < N) {
       const uint8_t *rec = recs + i * a.L.stride;
       for (uint32_t o = 0; o < a.L.n_ops; ++o)
         if ((a.L.ops[o].kind == SPK_OP_SPAN || a.L.ops[o].kind == SPK_OP_OPTION) &&
@@ -716,7 +719,7 @@ __global__ __launch_bounds__(kThreads, 5) void var_encode_write(
         const Win D{out, 0, ~0ull};
         for (int j = 0; j < kIPT; ++j) {
           const uint64_t i = r0 + (uint64_t)j * kThreads + threadIdx.x;
-          if (i >= a.n) continue;
+          if (i >= N) continue;
           uint64_t q = pj[j];
           if (a.mode == SPK_MODE_MESSAGES) {
             if (a.fpre) {
@@ -745,7 +748,7 @@ __global__ __launch_bounds__(kThreads, 5) void var_encode_write(
     const Win W{lds, wlo, wlo + kEncWin < g1 ? wlo + kEncWin : g1};
     for (int j = 0; j < kIPT; ++j) {
       const uint64_t i = r0 + (uint64_t)j * kThreads + threadIdx.x;
-      if (i >= a.n || pj[j] >= W.hi || pj[j] + szj[j] <= W.lo) continue;
+      if (i >= N || pj[j] >= W.hi || pj[j] + szj[j] <= W.lo) continue;
       uint64_t q = pj[j];
       if (a.mode == SPK_MODE_MESSAGES) {
         if (a.fpre) {
@@ -887,6 +890,7 @@ struct DecArgs {
   uint32_t pad2_;
   uint64_t range_t0, range_entry;
   const uint64_t *ends;  // MESSAGES: message i ends at ends[i] (null: offs[i + 1])
+  const uint64_t *dn;    // MESSAGES: device count (min(*dn, n_msgs)) or null
 };
 
 
@@ -915,7 +919,9 @@ __global__ __launch_bounds__(kThreads) void var_msg_parse(
   const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
   uint64_t cnt[kVS] = {};
   uint64_t ok = 0, consumed = 0;
-  if (i < a.n_msgs) {
+  // more frames than the caller's n_max: the excess is not decoded
+  if (a.dn && i == 0 && *a.dn > a.n_msgs) atomicExch(&res->errc, SPK_ERRC_CAPACITY);
+  if (i < dev_count(a.n_msgs, a.dn)) {
     const uint64_t f = offs[i], e = a.ends ? a.ends[i] : offs[i + 1];
     const uint64_t b = f + a.prefix;  // struct_pack message after the frame prefix
     MsgState s{~0ull, 1, SPK_ERRC_OK};
@@ -1020,7 +1026,7 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
   MsgState s{~0ull, 1, 1};
   uint64_t cnt[kVS] = {};
   uint64_t end = 0;
-  if (i < a.n_msgs) {
+  if (i < dev_count(a.n_msgs, a.dn)) {
     s = st[i];
     if (s.pos != ~0ull) {
       end = a.ends ? a.ends[i] : offs[i + 1];
@@ -1818,34 +1824,39 @@ __device__ __forceinline__ TileView stage_tile(v4u_t *win, const uint8_t *wire, 
 
 __device__ __forceinline__ bool vec_live(const VCtl *c) { return !c->errc && c->n; }
 
-// ---- K1 ----------------------------------------------------------------------
+// One lane's chunk state after the speculative walk and the in-wave
+// resolution (K1 sections 1-2; also the fused decoder's first phase).
 template <int NS>
-__global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkProg P,
-                                                                const uint8_t *__restrict__ wire,
-                                                                const uint8_t *__restrict__ ws,
-                                                                TileBufs TB, uint32_t dbg) {
-  __shared__ v4u_t win_s[kDecWaves][kTileVec + 1];
-  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t t = (uint64_t)blockIdx.x * kDecWaves + wv;
-  if (t >= TB.ntiles || !vec_live(c)) return;  // wave-uniform
-  const uint32_t w = c->w;
-  const uint64_t len = a.wire_len, p0 = c->p0;
-  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
-  const uint64_t ts = p0 + t * kTileBytes;
-  const TileView tv = stage_tile(win_s[wv], wire, len, ts, w, lane);
-  const WinReader &rd = tv.rd;
-  const uint64_t wend = tv.wend;
-  const uint64_t cs = ts + (uint64_t)lane * kTChunk;
-  const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
-  // ---- 1. speculative walk of this lane's chunk ----
-  uint64_t used = kNoPos, ex = kNoPos, sums[NS > 0 ? NS : kVS], term_at = kTermPos;
-  uint32_t cnt = 0;
-  for (uint32_t q = 0; q < nsp; ++q) sums[q] = 0;
-  const bool rng = reinterpret_cast<const FCtl *>(ws + kWsFCtl)->range != 0;
-  const bool exact = t == 0 && lane == 0 && !rng;  // the payload start: no search
+struct TileLane {
+  uint64_t used, ex, term_at;
+  uint32_t cnt;
+  uint64_t sums[NS > 0 ? NS : kVS];
   SpecPath<NS> sp;
+};
+
+// Speculative walk of this lane's chunk [cs, ce) of the tile staged at ts,
+// the chunk-0 cross-check and the resolution under the tile's assumed entry;
+// returns that entry X (kNoPos: none plausible). exact0: the tile starts at
+// the payload start (its entry is p0, no search).
+template <int NS>
+__device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const WinReader &rd,
+                                                      uint64_t len, uint32_t w, uint64_t ts,
+                                                      uint64_t wend, uint64_t cs, uint64_t ce,
+                                                      uint32_t lane, bool exact0, uint64_t p0,
+                                                      uint32_t dbg, TileLane<NS> &st) {
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  uint64_t &used = st.used, &ex = st.ex, &term_at = st.term_at;
+  uint32_t &cnt = st.cnt;
+  uint64_t *sums = st.sums;
+  SpecPath<NS> &sp = st.sp;
+  used = kNoPos;
+  ex = kNoPos;
+  term_at = kTermPos;
+  cnt = 0;
+  for (uint32_t q = 0; q < nsp; ++q) sums[q] = 0;
+  const bool exact = exact0 && lane == 0;  // the payload start: no search
   sp.np = 0;
+  // ---- 1. speculative walk of this lane's chunk ----
   if (cs < len && !(dbg & 8)) {
     uint64_t tt = 0, x = cs, past = 0, sx = exact ? cs : kNoPos;
     bool searching = !exact, done = false;
@@ -1966,8 +1977,8 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
   }
   // ---- 2. resolution given the tile's assumed entry ----
   uint64_t X = __shfl(used, 0);  // lane 0's spec start (kNoPos: no plausible start)
-  if (t == 0 && !rng) X = p0;
-  if ((t > 0 || rng) && !(dbg & 16)) {
+  if (exact0) X = p0;
+  if (!exact0 && !(dbg & 16)) {
     // Two independent speculations that agree are far likelier true: when
     // chunk 0's walk does not exit where chunk 1's speculative walk starts,
     // take the first start candidate of chunk 0 whose walk does (in parallel,
@@ -2010,6 +2021,36 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
   }
   if (X != kNoPos && !(dbg & 32))
     resolve_tile_sp<NS>(P, rd, len, w, cs, ce, lane, X, sp, used, ex, cnt, sums, term_at);
+  return X;
+}
+
+// ---- K1 ----------------------------------------------------------------------
+template <int NS>
+__global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkProg P,
+                                                                const uint8_t *__restrict__ wire,
+                                                                const uint8_t *__restrict__ ws,
+                                                                TileBufs TB, uint32_t dbg) {
+  __shared__ v4u_t win_s[kDecWaves][kTileVec + 1];
+  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t t = (uint64_t)blockIdx.x * kDecWaves + wv;
+  if (t >= TB.ntiles || !vec_live(c)) return;  // wave-uniform
+  const uint32_t w = c->w;
+  const uint64_t len = a.wire_len, p0 = c->p0;
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  const uint64_t ts = p0 + t * kTileBytes;
+  const TileView tv = stage_tile(win_s[wv], wire, len, ts, w, lane);
+  const WinReader &rd = tv.rd;
+  const uint64_t wend = tv.wend;
+  const uint64_t cs = ts + (uint64_t)lane * kTChunk;
+  const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
+  const bool rng = reinterpret_cast<const FCtl *>(ws + kWsFCtl)->range != 0;
+  TileLane<NS> st;
+  const uint64_t X = tile_spec_resolve<NS>(P, rd, len, w, ts, wend, cs, ce, lane, t == 0 && !rng,
+                                           p0, dbg, st);
+  uint64_t &used = st.used, &ex = st.ex;
+  uint32_t &cnt = st.cnt;
+  uint64_t *sums = st.sums;
   uint64_t tcnt = wave_sum_u64(cnt), tsum[NS > 0 ? NS : kVS];
   for (uint32_t q = 0; q < nsp; ++q) tsum[q] = wave_sum_u64(sums[q]);
   // ---- 3. entry alternatives (tile 0's entry is exact) ----
@@ -2652,6 +2693,315 @@ __global__ void vec_tile_finish(DecArgs a, const uint8_t *__restrict__ wire,
 }
 
 // ===========================================================================
+// DECODE, SPK_MODE_VECTOR — one fused pass with a decoupled look-back
+// ===========================================================================
+// A block of kFW waves owns kFW consecutive tiles (64 KiB of payload), staged
+// once in LDS. Each wave speculates and resolves its tile (K1's phase); the
+// block composes its tiles (tile k's entry = tile k-1's exit, a tile whose
+// entry lies past its end passes it through) and publishes an AGGREGATE
+// under its assumed entry: (entry X, exit Y, records, span sums). Wave 0 then
+// looks back over the 64 preceding blocks (blocks take ordered ids, so every
+// predecessor is running or done): from the nearest block that published its
+// INCLUSIVE state (true exit, records and span sums up to it), the chain of
+// aggregates whose entries equal their predecessors' exits gives this block's
+// true entry and its first record / heap offsets; an aggregate that does not
+// fit is waited for until its block publishes its inclusive state. The block
+// re-resolves if its assumed entry was wrong, publishes its inclusive state
+// and emits its records from the same LDS window: the wire is read once and
+// no per-chunk state leaves the chip (K1 + K2-K4 in one kernel).
+// Published words carry a tag bit and are written / read with agent-scope
+// relaxed atomics (no ordering between words is needed: a reader takes a
+// block's words only once every one of them is tagged).
+constexpr uint32_t kFW = 4;                                  // tiles (waves) per block
+constexpr uint64_t kFBlockBytes = (uint64_t)kFW * kTileBytes;
+constexpr uint32_t kFTab = 1024;                             // record starts per emission pass
+constexpr uint32_t kAggWords = 16;                           // >= 3 + kVS
+constexpr uint64_t kFailPos = ~0ull - 2;                     // "the look-back gave up"
+constexpr uint32_t kLookSpin = 1u << 20;                     // polls before giving up
+struct FusedBufs {
+  uint64_t *aw;             // [nblk][kAggWords] X, Y, records, sums (tagged)
+  uint64_t *pw;             // [nblk][kAggWords] true Y, inclusive records, sums (tagged)
+  unsigned long long *ctr;  // ordered block ids
+  uint64_t nblk;
+};
+__device__ __forceinline__ uint64_t fz_tag(uint64_t v) {
+  // values < 2^62; kFailPos / kNoPos / kTermPos map to 2^63 - 3 / - 2 / - 1
+  const uint64_t e = v >= kFailPos ? 0x7FFFFFFFFFFFFFFFull - (~0ull - v) : v;
+  return (e << 1) | 1ull;
+}
+__device__ __forceinline__ uint64_t fz_untag(uint64_t t) {
+  const uint64_t e = t >> 1;
+  return e >= 0x7FFFFFFFFFFFFFFDull ? ~0ull - (0x7FFFFFFFFFFFFFFFull - e) : e;
+}
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+// words [0, nw) of a published block state once all are tagged (false: not yet)
+__device__ __forceinline__ bool fz_read(const uint64_t *p, uint32_t nw, uint64_t *v) {
+  for (uint32_t q = 0; q < nw; ++q) {
+    const uint64_t x = ld_agent(p + q);
+    if (!(x & 1)) return false;
+    v[q] = fz_untag(x);
+  }
+  return true;
+}
+
+// The block's tiles in order from entry e0: wave k re-resolves when its
+// entry differs from the one its lane states were computed under (tin); a
+// tile whose entry is past its end (inside a record spanning it), the path's
+// end or unknown passes it through (tpass: no records; the lane states are
+// kept for a later entry). Results per wave in sh_y / sh_c / sh_s.
+template <int NS>
+__device__ __forceinline__ void fz_compose(const WalkProg &P, const WinReader &rd, uint64_t len,
+                                           uint32_t w, uint64_t ts, uint64_t cs, uint64_t ce,
+                                           uint32_t wv, uint32_t lane, uint64_t e0,
+                                           TileLane<NS> &st, uint64_t &tin, bool &tpass,
+                                           uint64_t *sh_y, uint64_t *sh_c, uint64_t (*sh_s)[kVS]) {
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  for (uint32_t k = 0; k < kFW; ++k) {
+    if (wv == k) {
+      const uint64_t e = k ? sh_y[k - 1] : e0;
+      if (e != tin) {
+        tpass = e == kTermPos || e == kNoPos || e >= ts + kTileBytes;
+        if (!tpass)
+          resolve_tile_sp<NS>(P, rd, len, w, cs, ce, lane, e, st.sp, st.used, st.ex, st.cnt,
+                              st.sums, st.term_at);
+        tin = e;
+      }
+      const uint64_t y = tpass ? e : __shfl(st.ex, 63);
+      const uint64_t tc = wave_sum_u64(tpass ? 0u : st.cnt);
+      uint64_t tsq[NS > 0 ? NS : kVS];
+      for (uint32_t q = 0; q < nsp; ++q) tsq[q] = wave_sum_u64(tpass ? 0ull : st.sums[q]);
+      if (lane == 0) {
+        sh_y[k] = y;
+        sh_c[k] = tc;
+        for (uint32_t q = 0; q < nsp; ++q) sh_s[k][q] = tsq[q];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int NS>
+__global__ __launch_bounds__(64 * kFW) void vec_tile_fused(DecArgs a, WalkProg P,
+                                                          const uint8_t *__restrict__ wire,
+                                                          uint8_t *__restrict__ ws, FusedBufs FB,
+                                                          uint8_t *__restrict__ recs, BigQ bq,
+                                                          uint32_t dbg) {
+  __shared__ v4u_t win_s[kFW][kTileVec + 1];
+  __shared__ uint16_t tab_s[kFW][kFTab];
+  __shared__ uint64_t sh_y[kFW], sh_c[kFW], sh_s[kFW][kVS];
+  __shared__ uint64_t sh_x0, sh_e, sh_pc, sh_ps[kVS];
+  __shared__ unsigned long long sh_bid;
+  __shared__ uint32_t sh_fail;
+  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
+  FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
+  if (!vec_live(c)) return;  // block-uniform
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (threadIdx.x == 0) sh_bid = atomicAdd(FB.ctr, 1ull);
+  __syncthreads();
+  const uint64_t b = sh_bid;
+  const uint32_t w = c->w;
+  const uint64_t len = a.wire_len, p0 = c->p0;
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  const uint64_t t = b * kFW + wv;
+  const uint64_t ts = p0 + t * kTileBytes;
+  const TileView tv = stage_tile(win_s[wv], wire, len, ts, w, lane);
+  const WinReader &rd = tv.rd;
+  const uint64_t cs = ts + (uint64_t)lane * kTChunk;
+  const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
+  // ---- 1. speculate + resolve this tile under its own assumed entry ----
+  TileLane<NS> st;
+  uint64_t tin = tile_spec_resolve<NS>(P, rd, len, w, ts, tv.wend, cs, ce, lane, t == 0, p0, 0u,
+                                       st);
+  bool tpass = false;
+  if (wv == 0 && lane == 0) sh_x0 = tin;
+  __syncthreads();
+  const uint64_t x0 = sh_x0;
+  // ---- 2. the block under its assumed entry -> aggregate ----
+  fz_compose<NS>(P, rd, len, w, ts, cs, ce, wv, lane, x0, st, tin, tpass, sh_y, sh_c, sh_s);
+  const uint32_t na = 3 + nsp, np = 2 + nsp;
+  if (wv == 0 && x0 != kNoPos && lane < na) {
+    uint64_t v;
+    if (lane == 0) v = x0;
+    else if (lane == 1) v = sh_y[kFW - 1];
+    else if (lane == 2) { v = 0; for (uint32_t k = 0; k < kFW; ++k) v += sh_c[k]; }
+    else { v = 0; for (uint32_t k = 0; k < kFW; ++k) v += sh_s[k][lane - 3]; }
+    st_agent(FB.aw + b * kAggWords + lane, fz_tag(v));
+  }
+  // ---- 3. look-back (wave 0): true entry and first record / heap offsets ----
+  if (wv == 0 && (dbg & 1024)) {  // A/B timing only: no look-back (wrong offsets)
+    if (lane == 0) {
+      sh_e = b == 0 ? p0 : x0;
+      sh_pc = 0;
+      for (uint32_t q = 0; q < nsp; ++q) sh_ps[q] = 0;
+      sh_fail = 0;
+    }
+  } else if (wv == 0) {
+    uint64_t cur = kFailPos, pc = 0, ps[kVS] = {};
+    for (uint32_t spin = 0; spin < kLookSpin; ++spin) {
+      const int64_t j = (int64_t)b - 64 + (int64_t)lane;
+      uint32_t stt = 0;  // 0 nothing, 1 aggregate, 2 inclusive, 3 failed
+      uint64_t v[3 + kVS];
+      if (j == -1) {
+        stt = 2;
+        v[0] = p0;
+        for (uint32_t q = 1; q < np; ++q) v[q] = 0;
+      } else if (j >= 0) {
+        if (fz_read(FB.pw + (uint64_t)j * kAggWords, np, v))
+          stt = v[0] == kFailPos ? 3 : 2;
+        else if (fz_read(FB.aw + (uint64_t)j * kAggWords, na, v))
+          stt = 1;
+      }
+      const uint64_t mP = __ballot(stt >= 2);
+      if (mP) {
+        const uint32_t kp = 63 - (uint32_t)__builtin_clzll(mP);
+        if (__builtin_amdgcn_readlane((int)stt, (int)kp) == 3) break;  // a predecessor gave up
+        // inclusive lane kp: v = (Y, records, sums); aggregate lanes: (X, Y, records, sums)
+        uint64_t y = readlane64(v[0], kp), c0 = readlane64(v[1], kp), s0[kVS];
+        for (uint32_t q = 0; q < nsp; ++q) s0[q] = readlane64(v[2 + q], kp);
+        bool ok = true;
+        for (uint32_t l = kp + 1; l < 64 && ok; ++l) {
+          if (y == kTermPos) continue;  // the path ended: the rest adds nothing
+          const uint64_t bend = p0 + (b - 64 + l + 1) * kFBlockBytes;
+          if (y >= bend) continue;  // a record spans block l: it passes y through
+          const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)stt, (int)l);
+          if (sl != 1 || readlane64(v[0], l) != y) {
+            ok = false;
+            break;
+          }
+          c0 += readlane64(v[2], l);
+          for (uint32_t q = 0; q < nsp; ++q) s0[q] += readlane64(v[3 + q], l);
+          y = readlane64(v[1], l);
+        }
+        if (ok) {
+          cur = y;
+          pc = c0;
+          for (uint32_t q = 0; q < nsp; ++q) ps[q] = s0[q];
+          break;
+        }
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (lane == 0) {
+      sh_e = cur;
+      sh_pc = pc;
+      for (uint32_t q = 0; q < nsp; ++q) sh_ps[q] = ps[q];
+      sh_fail = cur == kFailPos ? 1u : 0u;
+    }
+  }
+  __syncthreads();
+  if (sh_fail) {  // never expected: the finish kernel reports an internal error
+    if (threadIdx.x < np) st_agent(FB.pw + b * kAggWords + threadIdx.x, fz_tag(kFailPos));
+    if (threadIdx.x == 0) atomicAdd(&fc->unresolved, 1ull);
+    return;
+  }
+  const uint64_t E = sh_e;
+  // ---- 4. the true block: re-resolve from E when it differs from x0 ----
+  if (E != x0) {
+    fz_compose<NS>(P, rd, len, w, ts, cs, ce, wv, lane, E, st, tin, tpass, sh_y, sh_c, sh_s);
+    if (threadIdx.x == 0) atomicAdd(&fc->broken[0], 1ull);
+  }
+  if (wv == 0 && lane < np) {
+    uint64_t v;
+    if (lane == 0) v = sh_y[kFW - 1];
+    else if (lane == 1) { v = sh_pc; for (uint32_t k = 0; k < kFW; ++k) v += sh_c[k]; }
+    else { v = sh_ps[lane - 2]; for (uint32_t k = 0; k < kFW; ++k) v += sh_s[k][lane - 2]; }
+    st_agent(FB.pw + b * kAggWords + lane, fz_tag(v));
+  }
+  if (b == FB.nblk - 1 && threadIdx.x == 0) {  // the path's totals
+    uint64_t v = sh_pc;
+    for (uint32_t k = 0; k < kFW; ++k) v += sh_c[k];
+    fc->total = v;
+    for (uint32_t q = 0; q < nsp; ++q) {
+      uint64_t sv = sh_ps[q];
+      for (uint32_t k = 0; k < kFW; ++k) sv += sh_s[k][q];
+      fc->stot[q] = sv;
+    }
+  }
+  // ---- 5. emission of this wave's tile ----
+  const uint64_t n = c->n;
+  uint64_t base = sh_pc, carry[NS > 0 ? NS : kVS];
+  for (uint32_t q = 0; q < nsp; ++q) carry[q] = sh_ps[q];
+  for (uint32_t k = 0; k < wv; ++k) {
+    base += sh_c[k];
+    for (uint32_t q = 0; q < nsp; ++q) carry[q] += sh_s[k][q];
+  }
+  const uint32_t cnt = st.cnt;
+  const uint64_t used = st.used;
+  if (!tpass && st.ex == kTermPos && used != kNoPos && used != kTermPos) {
+    // where the true path ends: past this chunk's records
+    uint64_t x = used;
+    for (uint32_t r = 0; r < cnt; ++r) {
+      uint64_t rc[NS > 0 ? NS : kVS];
+      x += wlen_rd<NS>(P, rd, len, x, w, rc);
+    }
+    atomicMin(&fc->term_pos, (unsigned long long)x);
+  }
+  const uint64_t tcnt = sh_c[wv];
+  if (!tcnt || base >= n || (dbg & 2048)) return;
+  uint64_t rofs;  // this chunk's first record, tile-relative
+  {
+    uint64_t tot;
+    rofs = wave_excl_scan_u64(cnt, lane, &tot);
+  }
+  uint16_t *tab = tab_s[wv];
+  const uint64_t nemit = (n - base < tcnt) ? n - base : tcnt;
+  for (uint64_t pass0 = 0; pass0 < nemit; pass0 += kFTab) {
+    const uint64_t pend = pass0 + kFTab < nemit ? pass0 + kFTab : nemit;
+    if (cnt && rofs < pend && rofs + cnt > pass0) {
+      uint64_t x = used;
+      for (uint32_t r = 0; r < cnt; ++r) {
+        const uint64_t i = rofs + r;
+        if (i >= pend) break;
+        if (i >= pass0) tab[i - pass0] = (uint16_t)(x - ts);
+        uint64_t rc[NS > 0 ? NS : kVS];
+        x += wlen_rd<NS>(P, rd, len, x, w, rc);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t nrec = pend - pass0;
+    for (uint64_t i0 = 0; i0 < nrec; i0 += 64) {
+      const uint64_t i = i0 + lane;
+      const bool act = i < nrec;
+      const uint64_t pos = ts + (act ? tab[i] : 0);
+      uint64_t rc[kVS] = {};
+      uint64_t L = 0;
+      if (act) L = wlen_rd<NS>(P, rd, len, pos, w, rc);
+      uint64_t off[kVS];
+      bool fits = true;
+      for (uint32_t q = 0; q < nsp; ++q) {
+        uint64_t tot;
+        off[q] = carry[q] + wave_excl_scan_u64(act ? rc[q] : 0, lane, &tot);
+        carry[q] += tot;
+        if (off[q] + rc[q] > a.heap_cap[q]) fits = false;
+      }
+      const uint64_t gr = base + pass0 + i;
+      if (act && gr < a.rec_cap && fits)
+        emit_record_rd(a.L, rd, pos, w, recs + gr * a.L.stride, a.heaps, off, len, bq);
+      if (act && gr == n - 1) {
+        fc->end_pos = pos + L;
+        for (uint32_t q = 0; q < nsp; ++q) fc->htot[q] = off[q] + rc[q];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+// ===========================================================================
 // host launchers
 // ===========================================================================
 static unsigned grid_for(uint64_t items, uint64_t per_block) {
@@ -2661,8 +3011,8 @@ static unsigned grid_for(uint64_t items, uint64_t per_block) {
 
 // ---- tile decoder: workspace and launch ---------------------------------------
 struct TileWs {
-  size_t fn, cused, cex, ccnt, csum, sel, contrib, scan, blist, jobs, end;
-  uint64_t ntiles, nchunks, nsb;
+  size_t fn, cused, cex, ccnt, csum, sel, contrib, scan, blist, jobs, agg, end;
+  uint64_t ntiles, nchunks, nsb, nblk;
 };
 static TileWs tile_ws_layout(const spk_layout *L, uint64_t wire_len) {
   TileWs f = {};
@@ -2689,8 +3039,20 @@ static TileWs tile_ws_layout(const spk_layout *L, uint64_t wire_len) {
   f.scan = take(f.nsb * 8 * (1 + ns));
   f.blist = take(f.ntiles * 4);
   f.jobs = take(big_jobs_cap(wire_len) * sizeof(BigJob));
+  f.nblk = (f.ntiles + kFW - 1) / kFW;
+  f.agg = take(2 * f.nblk * kAggWords * 8 + 64);  // fused decode: aggregates, inclusive, ids
   f.end = off;
   return f;
+}
+
+// SPK_FUSED=1: the fused look-back kernel for the whole-message decode
+// instead of the multi-kernel tile pipeline (K1-K4) (A/B)
+static bool tile_fused() {
+  static const bool v = [] {
+    const char *e = getenv("SPK_FUSED");
+    return e && e[0] == '1';
+  }();
+  return v;
 }
 
 // SPK_TILE_DBG bits (A/B experiments): 4 = compute entry alternatives in K1
@@ -2743,6 +3105,28 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
       SPK_LAUNCH(vec_shard_setn, dim3(1), dim3(64), 0, s, ws, sc.first, sc.last, d_res);
       SPK_LAUNCH(vec_tile_finish, dim3(1), dim3(64), 0, s, a, wire, (const uint8_t *)ws, d_res);
     }
+    return hipGetLastError();
+  }
+  if (phase == kTilesAll && tile_fused()) {
+    FusedBufs FB;
+    FB.nblk = f.nblk;
+    FB.aw = reinterpret_cast<uint64_t *>(ws + f.agg);
+    FB.pw = FB.aw + f.nblk * kAggWords;
+    FB.ctr = reinterpret_cast<unsigned long long *>(FB.pw + f.nblk * kAggWords);
+    BigQ bq;
+    bq.jobs = reinterpret_cast<BigJob *>(ws + f.jobs);
+    bq.n = &reinterpret_cast<FCtl *>(ws + kWsFCtl)->njobs;
+    bq.cap = big_jobs_cap(a.wire_len);
+    SPK_LAUNCH(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, 0u, (uint64_t)0);
+    hipError_t e = hipMemsetAsync(ws + f.agg, 0, 2 * f.nblk * kAggWords * 8 + 64, s);
+    if (e != hipSuccess) return e;
+    SPK_LAUNCH(vec_tile_fused<NS>, dim3((unsigned)f.nblk), dim3(64 * kFW), 0, s, a, P, wire, ws,
+               FB, d_recs, bq, tile_dbg());
+    if (P.ns) {
+      const uint64_t gb = bq.cap < 2048 ? bq.cap : 2048;
+      SPK_LAUNCH(vec_big_copy, dim3((unsigned)gb), dim3(256), 0, s, wire, (const uint8_t *)ws, bq);
+    }
+    SPK_LAUNCH(vec_tile_finish, dim3(1), dim3(64), 0, s, a, wire, (const uint8_t *)ws, d_res);
     return hipGetLastError();
   }
   if (phase != kTilesEmit) {
@@ -2845,8 +3229,9 @@ static MsgHdrTable msg_hdr_table(const spk_layout *L) {
 
 hipError_t launch_var_plan(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
                            spk_plan_t *d_plan, void *d_ws, size_t ws_bytes,
-                           hipStream_t s) {
+                           hipStream_t s, const uint64_t *d_n) {
   VarArgs a = make_varargs(L, mode, n, nullptr);
+  a.dn = d_n;
   uint8_t *ws = (uint8_t *)d_ws;
   const MsgHdrTable t = msg_hdr_table(L);
   SPK_LAUNCH(write_msg_hdrs, dim3(1), dim3(256), 0, s, t, ws);
@@ -2870,8 +3255,10 @@ hipError_t launch_var_encode(const spk_layout *L, int mode, uint64_t n,
                              const void *d_recs, const void *const *d_heaps,
                              const spk_plan_t *d_plan, void *d_out, uint64_t out_cap,
                              uint64_t *d_offsets, const spk_frame *F, void *d_ws,
-                             size_t ws_bytes, hipStream_t s, const SeqEcho *echo) {
+                             size_t ws_bytes, hipStream_t s, const SeqEcho *echo,
+                             const uint64_t *d_n) {
   VarArgs a = make_varargs(L, mode, n, d_heaps);
+  a.dn = d_n;
   if (echo) a.echo = *echo;
   if (F && mode == SPK_MODE_MESSAGES) {
     a.fpre = F->prefix_len;
@@ -2927,9 +3314,11 @@ hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
                              uint64_t rec_cap, void *const *d_heaps,
                              const uint64_t *heap_caps, spk_dresult_t *d_res,
                              int32_t *d_errc, void *d_ws, size_t ws_bytes, hipStream_t s,
-                             uint32_t body_w, uint64_t body_n, const uint64_t *d_msg_ends) {
+                             uint32_t body_w, uint64_t body_n, const uint64_t *d_msg_ends,
+                             const uint64_t *d_n) {
   DecArgs a = {};
   a.ends = d_msg_ends;
+  a.dn = d_n;
   a.prefix = prefix;
   a.body_w = body_w;
   a.body_n = body_n;

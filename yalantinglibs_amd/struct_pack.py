@@ -144,12 +144,25 @@ class Codec:
 
     def serialize_echo(self, out: torch.Tensor, batch: RecordBatch, offsets: torch.Tensor,
                        frame: C.spk_frame, seq_src: torch.Tensor, seq_offsets: torch.Tensor,
-                       seq_src_off: int = 4, stream=None):
+                       seq_src_off: int = 4, stream=None, d_count: Optional[torch.Tensor] = None):
         """spk_encode_framed_echo (plan + write, no host sync): message i's
         frame carries seq_src[seq_offsets[i] + seq_src_off ..+4] as its
-        seq_num — responses echoing their routed requests."""
-        self.plan(batch, MODE_MESSAGES, stream)
+        seq_num — responses echoing their routed requests. d_count (a device
+        int64 tensor, e.g. a FrameRouter count): encode its first
+        min(*d_count, batch.n) records (spk_plan_dn / spk_encode_framed_echo_dn)
+        without reading the count on the host."""
         ws = self.workspace(MODE_MESSAGES, batch.n)
+        if d_count is not None:
+            self._check(self.lib.spk_plan_dn(
+                self.L.ptr, _p(d_count), batch.n, _p(batch.recs), self._heap_ptrs(batch.heaps),
+                _p(self.plan_buf), _p(ws), ws.numel(), _stream(stream)), "spk_plan_dn")
+            self._check(self.lib.spk_encode_framed_echo_dn(
+                self.L.ptr, _p(d_count), batch.n, _p(batch.recs), self._heap_ptrs(batch.heaps),
+                _p(self.plan_buf), ct.byref(frame), _p(seq_src), _p(seq_offsets), seq_src_off,
+                _p(out), out.numel(), _p(offsets), _p(ws), ws.numel(), _stream(stream)),
+                "spk_encode_framed_echo_dn")
+            return
+        self.plan(batch, MODE_MESSAGES, stream)
         self._check(self.lib.spk_encode_framed_echo(
             self.L.ptr, batch.n, _p(batch.recs), self._heap_ptrs(batch.heaps),
             _p(self.plan_buf), ct.byref(frame), _p(seq_src), _p(seq_offsets), seq_src_off,
@@ -195,14 +208,22 @@ class Codec:
     def deserialize_frames(self, out: RecordBatch, wire: torch.Tensor, begins: torch.Tensor,
                            ends: torch.Tensor, n_msgs: int, prefix: int,
                            errc_out: Optional[torch.Tensor] = None, heap_caps=None,
-                           stream=None) -> torch.Tensor:
+                           stream=None, d_count: Optional[torch.Tensor] = None) -> torch.Tensor:
         """spk_decode_frames: message i = wire[begins[i] + prefix .. ends[i]) —
         one record type's frames routed out of a mixed batch
-        (coro_rpc.FrameRouter). Stream-ordered, no host sync."""
+        (coro_rpc.FrameRouter). Stream-ordered, no host sync. d_count (device
+        int64): the frame count read on the device, n_msgs its upper bound
+        (spk_decode_frames_dn)."""
         ws = self.workspace(MODE_MESSAGES, n_msgs, wire.numel())
         caps = heap_caps or [h.numel() // sp.elem.size
                              for h, sp in zip(out.heaps, self.L.dev.spans)]
         hc = (ct.c_uint64 * max(len(caps), 1))(*(caps or [0]))
+        if d_count is not None:
+            self._check(self.lib.spk_decode_frames_dn(
+                self.L.ptr, _p(wire), wire.numel(), _p(begins), _p(ends), _p(d_count), n_msgs,
+                prefix, _p(out.recs), out.n, self._heap_ptrs(out.heaps), hc, _p(self.res_buf),
+                _p(errc_out), _p(ws), ws.numel(), _stream(stream)), "spk_decode_frames_dn")
+            return self.res_buf
         self._check(self.lib.spk_decode_frames(
             self.L.ptr, _p(wire), wire.numel(), _p(begins), _p(ends), n_msgs, prefix,
             _p(out.recs), out.n, self._heap_ptrs(out.heaps), hc, _p(self.res_buf),
