@@ -240,6 +240,14 @@ hipError_t launch_var_shard(const spk_layout *L, int phase, const void *d_wire, 
                             spk_shard_t *d_summary, uint64_t first, uint32_t last, void *d_recs,
                             uint64_t rec_cap, void *const *d_heaps, const uint64_t *heap_caps,
                             spk_dresult_t *d_res, void *d_ws, hipStream_t s);
+// spk_var.hip: VECTOR decode of a nested layout (no compatible members, at
+// most SPK_FLAT_SPANS heaps) on the tile decoder
+bool var_nested_tile_ok(const spk_layout *L);
+size_t var_nested_tile_ws_bytes(const spk_layout *L, uint64_t wire_len);
+hipError_t launch_var_nested_decode(const spk_layout *L, const void *d_wire, uint64_t wire_len,
+                                    void *d_recs, uint64_t rec_cap, void *const *d_heaps,
+                                    const uint64_t *heap_caps, spk_dresult_t *d_res, void *d_ws,
+                                    hipStream_t s, uint32_t body_w, uint64_t body_n);
 // spk_nested.hip: layouts with SPK_OP_ARRAY
 bool layout_nested(const spk_layout *L);
 size_t nested_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len);

@@ -24,21 +24,15 @@
 // 1354-1376). A VECTOR decode's walker records where each record's group of
 // each version starts; the record's lane decodes its groups from there.
 #include "spk_internal.hpp"
+#include "spk_nlayout.hpp"
+
+#include <stdlib.h>
 
 namespace spk {
 
-struct NLayout {
-  spk_op ops[SPK_MAX_OPS];
-  uint8_t heap[SPK_MAX_OPS];  // heap index of a SPAN / OPTION / ARRAY op
-  uint8_t end[SPK_MAX_OPS];   // ARRAY: its END; VARIANT: the END of its last alternative
-  uint8_t crank[SPK_MAX_OPS]; // COMPAT: its version rank (ops[i].kind is SPK_OP_COMPAT)
-  uint32_t n_ops, stride, n_heaps, n_ranks;
-  uint32_t fv_cnt, fv_has64, fv_bits;  // USE_FAST_VARINT group: FVAR ops, a 64-bit one, bitset bytes
-  // screen of a guessed record start: the first count (SPAN / ARRAY) sits
-  // scr_off fixed bytes into the record (~0: no such count before anything
-  // data-dependent); its elements take at least scr_esz bytes each
-  uint32_t scr_off, scr_esz;
-};
+typedef uint32_t v4u_t __attribute__((ext_vector_type(4)));
+typedef v4u_t v4u_una __attribute__((aligned(1)));
+
 
 // layouts the interpreter runs: an ARRAY (element layouts), a VARIANT, an
 // OPTGROUP, a compatible member, a fast-varint group, or more heaps than the
@@ -53,56 +47,6 @@ bool layout_nested(const spk_layout *L) {
     heaps += op_has_heap(k);
   }
   return heaps > SPK_FLAT_SPANS;  // more heaps than the flat kernels carry
-}
-
-// VARIANT / OPTGROUP / CGROUP: groups placed in the same record, each closed
-// by an END (an ARRAY's element ops are one group too, in another record)
-__host__ __device__ __forceinline__ bool n_group(uint32_t k) {
-  return k == SPK_OP_VARIANT || k == SPK_OP_OPTGROUP || k == SPK_OP_CGROUP;
-}
-
-static NLayout make_nlayout(const spk_layout *L) {
-  NLayout N = {};
-  N.n_ops = L->n_ops;
-  N.stride = L->rec_stride;
-  // open ARRAYs / groups and the groups each one still has to close
-  uint32_t stack[SPK_MAX_DEPTH + 1], left[SPK_MAX_DEPTH + 1], d = 0, h = 0;
-  for (uint32_t i = 0; i < L->n_ops; ++i) {
-    N.ops[i] = L->ops[i];
-    const uint32_t k = SPK_OP_KIND(L->ops[i].kind);
-    if (k == SPK_OP_COMPAT || k == SPK_OP_CGROUP) {
-      N.ops[i].kind = k;
-      N.crank[i] = (uint8_t)SPK_OP_RANK(L->ops[i].kind);
-      if (N.crank[i] + 1u > N.n_ranks) N.n_ranks = N.crank[i] + 1u;
-    }
-    if (op_has_heap(k)) N.heap[i] = (uint8_t)h++;
-    if (k == SPK_OP_FVAR) {
-      ++N.fv_cnt;
-      N.fv_has64 |= L->ops[i].size == 8;
-    }
-    if (k == SPK_OP_ARRAY || n_group(k)) {
-      stack[d] = i;
-      left[d++] = k == SPK_OP_ARRAY ? 1 : L->ops[i].size;
-    }
-    if (k == SPK_OP_END && d && --left[d - 1] == 0) N.end[stack[--d]] = (uint8_t)i;
-  }
-  N.n_heaps = h;
-  N.fv_bits = N.fv_cnt ? (N.fv_cnt + 2 + 7) / 8 : 0;
-  N.scr_off = ~0u;
-  uint32_t pre = 0;
-  for (uint32_t i = 0; i < L->n_ops && !N.fv_cnt; ++i) {
-    const uint32_t k = SPK_OP_KIND(L->ops[i].kind);
-    if (k == SPK_OP_COPY) {
-      pre += L->ops[i].size;
-      continue;
-    }
-    if (k == SPK_OP_SPAN || k == SPK_OP_ARRAY) {
-      N.scr_off = pre;
-      N.scr_esz = k == SPK_OP_SPAN ? L->ops[i].size : 1;
-    }
-    break;
-  }
-  return N;
 }
 
 // ---- shared helpers ---------------------------------------------------------
@@ -225,29 +169,6 @@ __device__ uint64_t n_fv_size(const NLayout &N, const uint8_t *rec) {
       b += wb < N.ops[i].size ? wb : N.ops[i].size;
   return b;
 }
-__device__ uint8_t *n_fv_write(const NLayout &N, const uint8_t *rec, uint8_t *p) {
-  if (!N.fv_cnt) return p;
-  const uint32_t code = n_fv_code(N, rec), wb = 1u << code;
-  uint8_t bs[(SPK_MAX_VARINTS + 2 + 7) / 8] = {};
-  uint8_t *q = p + N.fv_bits;
-  uint32_t j = 0;
-  for (uint32_t i = 0; i < N.n_ops; ++i) {
-    const spk_op op = N.ops[i];
-    if (op.kind != SPK_OP_FVAR) continue;
-    const uint64_t v = n_fv_raw(op, rec);
-    if (v) {
-      bs[j / 8] |= (uint8_t)(1u << (j % 8));
-      const uint32_t rw = wb < op.size ? wb : op.size;
-      for (uint32_t b = 0; b < rw; ++b) q[b] = (uint8_t)(v >> (8 * b));
-      q += rw;
-    }
-    ++j;
-  }
-  bs[N.fv_cnt / 8] |= (uint8_t)((code & 1u) << (N.fv_cnt % 8));
-  bs[(N.fv_cnt + 1) / 8] |= (uint8_t)(((code >> 1) & 1u) << ((N.fv_cnt + 1) % 8));
-  for (uint32_t b = 0; b < N.fv_bits; ++b) p[b] = bs[b];
-  return q;
-}
 // the group's wire length from its bitset at wire[pos] (the caller checked
 // the bitset is there); 0 for the invalid width code
 __device__ __forceinline__ uint64_t n_fv_len(const NLayout &N, const uint8_t *bs) {
@@ -298,6 +219,110 @@ __device__ int32_t n_fv_read(const NLayout &N, const uint8_t *wire, uint64_t &po
   return SPK_ERRC_OK;
 }
 
+// ---- encode: the interpreter's element stack and output sinks ---------------------
+// The top frame lives in registers and D - 1 frames below it (D = the layout's
+// depth: 1, 2 or SPK_MAX_DEPTH); only D = SPK_MAX_DEPTH indexes them at run
+// time (a runtime index puts the stack in scratch memory).
+template <int D>
+struct NStk {
+  NFrame top;
+  NFrame sv[D > 1 ? D - 1 : 1];
+  __device__ __forceinline__ void push(uint32_t d, const NFrame &f) {  // d: depth before
+    if constexpr (D > 1) {
+      if (d) {
+        if constexpr (D == 2)
+          sv[0] = top;
+        else
+          sv[d - 1] = top;
+      }
+    }
+    top = f;
+  }
+  __device__ __forceinline__ void pop(uint32_t d) {  // d: depth after
+    if constexpr (D > 1) {
+      if (d) {
+        if constexpr (D == 2)
+          top = sv[0];
+        else
+          top = sv[d - 1];
+      }
+    }
+  }
+};
+// the kernels' D for a layout
+static inline int n_dclass(const NLayout &N) { return N.depth <= 1 ? 1 : N.depth <= 2 ? 2 : 4; }
+#define NEST_D(depth_class, ...)            \
+  do {                                      \
+    if ((depth_class) == 1) {               \
+      constexpr int D = 1;                  \
+      __VA_ARGS__;                          \
+    } else if ((depth_class) == 2) {        \
+      constexpr int D = 2;                  \
+      __VA_ARGS__;                          \
+    } else {                                \
+      constexpr int D = SPK_MAX_DEPTH;      \
+      __VA_ARGS__;                          \
+    }                                       \
+  } while (0)
+
+// output sinks of the write interpreter: output byte q
+struct NDirect {  // straight to memory at base + q
+  uint8_t *base;
+  __device__ __forceinline__ void put(uint64_t q, const uint8_t *src, uint64_t n) const {
+    n_copy(base + q, src, n);
+  }
+  __device__ __forceinline__ void byte(uint64_t q, uint32_t b) const { base[q] = (uint8_t)b; }
+};
+struct NWin {  // the part inside an LDS window holding output bytes [lo, hi)
+  uint8_t *lds;
+  uint64_t lo, hi;
+  __device__ __forceinline__ void put(uint64_t q, const uint8_t *src, uint64_t n) const {
+    const uint64_t a = q > lo ? q : lo;
+    const uint64_t b = q + n < hi ? q + n : hi;
+    if (a >= b) return;
+    uint64_t i = a - q;
+    const uint64_t e = b - q;
+    uint8_t *d = lds + (q - lo);
+    for (; i + 16 <= e; i += 16) {  // wide unaligned loads, byte stores into LDS
+      const v4u_t v = *reinterpret_cast<const v4u_una *>(src + i);
+      const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (uint32_t k = 0; k < 16; ++k) d[i + k] = (uint8_t)(x[k >> 2] >> (8 * (k & 3)));
+    }
+    for (; i < e; ++i) d[i] = src[i];
+  }
+  __device__ __forceinline__ void byte(uint64_t q, uint32_t b) const {
+    if (q >= lo && q < hi) lds[q - lo] = (uint8_t)b;
+  }
+};
+template <typename Sk>
+__device__ __forceinline__ void n_put_le(const Sk &sk, uint64_t q, uint64_t v, uint32_t w) {
+  for (uint32_t b = 0; b < w; ++b) sk.byte(q + b, (uint32_t)(v >> (8 * b)) & 0xFFu);
+}
+// the fast-varint group (packer.hpp:152-235) at q; returns the position past it
+template <typename Sk>
+__device__ uint64_t n_fv_write(const NLayout &N, const uint8_t *rec, const Sk &sk, uint64_t q0) {
+  if (!N.fv_cnt) return q0;
+  const uint32_t code = n_fv_code(N, rec), wb = 1u << code;
+  uint64_t bits = 0, q = q0 + N.fv_bits;
+  uint32_t j = 0;
+  for (uint32_t i = 0; i < N.n_ops; ++i) {
+    const spk_op op = N.ops[i];
+    if (op.kind != SPK_OP_FVAR) continue;
+    const uint64_t v = n_fv_raw(op, rec);
+    if (v) {
+      bits |= 1ull << j;
+      const uint32_t rw = wb < op.size ? wb : op.size;
+      n_put_le(sk, q, v, rw);
+      q += rw;
+    }
+    ++j;
+  }
+  bits |= (uint64_t)code << N.fv_cnt;
+  n_put_le(sk, q0, bits, N.fv_bits);
+  return q;
+}
+
 // ---- encode: size of one record (or of an op range of it) ----------------------
 struct NSize {
   uint64_t bytes, cnts, maxc;  // payload bytes w/o counts, count fields, longest container
@@ -305,18 +330,19 @@ struct NSize {
 };
 // calculate_one_size (calculate_size.hpp:39-183) of ops [i0, i1) of `rec`;
 // `top`: the whole top-level record (its fast-varint group counts too)
+template <int D>
 __device__ NSize n_size(const NLayout &N, const uint8_t *rec, const uint8_t *const *heaps,
                         uint32_t i0, uint32_t i1, bool top) {
   NSize s = {0, 0, 0, 0, 0};
   if (top) s.bytes = n_fv_size(N, rec);
-  NFrame st[SPK_MAX_DEPTH];
+  NStk<D> st;
   uint32_t d = 0, i = i0, iend = i1;
   uint32_t cd = 0;  // depth of an open compatible group (its bytes are version-pass bytes)
   const uint8_t *r = rec;
   for (;;) {
     if (i >= iend) {
       if (!d) break;
-      NFrame &f = st[d - 1];
+      NFrame &f = st.top;
       if (++f.j < f.cnt) {
         r = f.el + f.j * N.ops[f.aop].size;
         i = f.first;
@@ -326,7 +352,7 @@ __device__ NSize n_size(const NLayout &N, const uint8_t *rec, const uint8_t *con
       iend = f.pend;
       r = f.prec;
       if (cd == d) cd = 0;
-      --d;
+      st.pop(--d);
       continue;
     }
     const spk_op op = N.ops[i];
@@ -350,8 +376,7 @@ __device__ NSize n_size(const NLayout &N, const uint8_t *rec, const uint8_t *con
         continue;
       }
       const uint32_t a0 = n_alt_start(N, i, (uint32_t)a);
-      st[d] = NFrame{i, iend, 0, 1, r, r, a0, (uint32_t)N.end[i] + 1u};
-      ++d;
+      st.push(d++, NFrame{i, iend, 0, 1, r, r, a0, (uint32_t)N.end[i] + 1u});
       if (op.kind == SPK_OP_CGROUP) cd = d;
       iend = n_alt_end(N, a0);
       i = a0;
@@ -375,9 +400,9 @@ __device__ NSize n_size(const NLayout &N, const uint8_t *rec, const uint8_t *con
         i = N.end[i] + 1;
       } else {
         const uint64_t off = *reinterpret_cast<const uint64_t *>(r + op.aux);
-        st[d] = NFrame{i, iend, 0, c, heaps[N.heap[i]] + off * op.size, r, i + 1, (uint32_t)N.end[i] + 1u};
-        r = st[d].el;
-        ++d;
+        const uint8_t *el = heaps[N.heap[i]] + off * op.size;
+        st.push(d++, NFrame{i, iend, 0, c, el, r, i + 1, (uint32_t)N.end[i] + 1u});
+        r = el;
         iend = N.end[i];
         ++i;
       }
@@ -386,17 +411,19 @@ __device__ NSize n_size(const NLayout &N, const uint8_t *rec, const uint8_t *con
   return s;
 }
 
-// ---- encode: bytes of one record (or of an op range of it) ---------------------
-__device__ uint8_t *n_write(const NLayout &N, const uint8_t *rec, const uint8_t *const *heaps,
-                            uint32_t w, uint8_t *p, uint32_t i0, uint32_t i1, bool top) {
-  NFrame st[SPK_MAX_DEPTH];
+// ---- encode: bytes of one record (or of an op range of it) at output byte q ------
+template <int D, typename Sk>
+__device__ uint64_t n_write(const NLayout &N, const uint8_t *rec, const uint8_t *const *heaps,
+                            uint32_t w, const Sk &sk, uint64_t q, uint32_t i0, uint32_t i1,
+                            bool top) {
+  NStk<D> st;
   uint32_t d = 0, i = i0, iend = i1;
   const uint8_t *r = rec;
-  if (top) p = n_fv_write(N, rec, p);  // before the members (packer.hpp:432-440)
+  if (top) q = n_fv_write(N, rec, sk, q);  // before the members (packer.hpp:432-440)
   for (;;) {
     if (i >= iend) {
       if (!d) break;
-      NFrame &f = st[d - 1];
+      NFrame &f = st.top;
       if (++f.j < f.cnt) {
         r = f.el + f.j * N.ops[f.aop].size;
         i = f.first;
@@ -405,23 +432,23 @@ __device__ uint8_t *n_write(const NLayout &N, const uint8_t *rec, const uint8_t 
       i = f.ret;
       iend = f.pend;
       r = f.prec;
-      --d;
+      st.pop(--d);
       continue;
     }
     const spk_op op = N.ops[i];
     if (op.kind == SPK_OP_FVAR) {
       ++i;
     } else if (op.kind == SPK_OP_COPY) {
-      n_copy(p, r + op.rec_off, op.size);
-      p += op.size;
+      sk.put(q, r + op.rec_off, op.size);
+      q += op.size;
       ++i;
     } else if (op.kind == SPK_OP_VARINT) {
       uint64_t v = n_vi_value(op, r);
       while (v >= 0x80) {
-        *p++ = (uint8_t)(v | 0x80u);
+        sk.byte(q++, (uint32_t)(v | 0x80u) & 0xFFu);
         v >>= 7;
       }
-      *p++ = (uint8_t)v;
+      sk.byte(q++, (uint32_t)v);
       ++i;
     } else if (op.kind == SPK_OP_COMPAT || op.kind == SPK_OP_CGROUP) {
       // version UINT64_MAX: nothing (packer.hpp:246-249); written by the
@@ -431,51 +458,51 @@ __device__ uint8_t *n_write(const NLayout &N, const uint8_t *rec, const uint8_t 
       // variant: [index:1] (packer.hpp:389-398); optional / expected:
       // [has_value:1] (:382-388, :400-410); then the active group
       const uint32_t v = *reinterpret_cast<const uint32_t *>(r + op.rec_off);
-      *p++ = op.kind == SPK_OP_VARIANT ? (uint8_t)v : (uint8_t)(v ? 1 : 0);
+      sk.byte(q++, op.kind == SPK_OP_VARIANT ? (v & 0xFFu) : (v ? 1u : 0u));
       const int a = n_active(N, i, r);
       if (a < 0) {
         i = N.end[i] + 1u;
         continue;
       }
       const uint32_t a0 = n_alt_start(N, i, (uint32_t)a);
-      st[d] = NFrame{i, iend, 0, 1, r, r, a0, (uint32_t)N.end[i] + 1u};
-      ++d;
+      st.push(d++, NFrame{i, iend, 0, 1, r, r, a0, (uint32_t)N.end[i] + 1u});
       iend = n_alt_end(N, a0);
       i = a0;
     } else {
       const uint64_t c = *reinterpret_cast<const uint32_t *>(r + op.rec_off);
       const uint64_t off = *reinterpret_cast<const uint64_t *>(r + op.aux);
       if (op.kind == SPK_OP_OPTION) {
-        *p++ = c ? 1 : 0;
+        sk.byte(q++, c ? 1u : 0u);
         if (c) {
-          n_copy(p, heaps[N.heap[i]] + off * op.size, op.size);
-          p += op.size;
+          sk.put(q, heaps[N.heap[i]] + off * op.size, op.size);
+          q += op.size;
         }
         ++i;
         continue;
       }
-      for (uint32_t b = 0; b < w; ++b) p[b] = (uint8_t)(c >> (8 * b));
-      p += w;
+      n_put_le(sk, q, c, w);
+      q += w;
       if (op.kind == SPK_OP_SPAN) {
-        n_copy(p, heaps[N.heap[i]] + off * op.size, c * op.size);
-        p += c * op.size;
+        sk.put(q, heaps[N.heap[i]] + off * op.size, c * op.size);
+        q += c * op.size;
         ++i;
       } else if (!c) {
         i = N.end[i] + 1;
       } else {
-        st[d] = NFrame{i, iend, 0, c, heaps[N.heap[i]] + off * op.size, r, i + 1, (uint32_t)N.end[i] + 1u};
-        r = st[d].el;
-        ++d;
+        const uint8_t *el = heaps[N.heap[i]] + off * op.size;
+        st.push(d++, NFrame{i, iend, 0, c, el, r, i + 1, (uint32_t)N.end[i] + 1u});
+        r = el;
         iend = N.end[i];
         ++i;
       }
     }
   }
-  return p;
+  return q;
 }
 
 // ---- compatible members: the version pass of rank rk over one top-level record ----
 // (COMPAT / CGROUP ops sit at the top level only: spk_layout_check)
+template <int D>
 __device__ uint64_t n_compat_size(const NLayout &N, const uint8_t *rec,
                                   const uint8_t *const *heaps, uint32_t rk, uint32_t w) {
   uint64_t b = 0;
@@ -487,7 +514,7 @@ __device__ uint64_t n_compat_size(const NLayout &N, const uint8_t *rec,
     } else if (N.ops[i].kind == SPK_OP_CGROUP) {
       b += 1;
       if (has) {
-        const NSize g = n_size(N, rec, heaps, i + 1, N.end[i], false);
+        const NSize g = n_size<D>(N, rec, heaps, i + 1, N.end[i], false);
         b += g.bytes + g.cnts * w;
       }
     }
@@ -495,24 +522,25 @@ __device__ uint64_t n_compat_size(const NLayout &N, const uint8_t *rec,
   return b;
 }
 // packer.hpp:453-461: [has_value:1][U if present] per member of that version
-__device__ uint8_t *n_write_compat(const NLayout &N, const uint8_t *rec,
+template <int D, typename Sk>
+__device__ uint64_t n_write_compat(const NLayout &N, const uint8_t *rec,
                                    const uint8_t *const *heaps, uint32_t rk, uint32_t w,
-                                   uint8_t *p) {
+                                   const Sk &sk, uint64_t q) {
   for (uint32_t i = 0; i < N.n_ops; ++i) {
     const spk_op op = N.ops[i];
     if ((op.kind != SPK_OP_COMPAT && op.kind != SPK_OP_CGROUP) || N.crank[i] != rk) continue;
     const uint32_t c = *reinterpret_cast<const uint32_t *>(rec + op.rec_off);
-    *p++ = c ? 1 : 0;
+    sk.byte(q++, c ? 1u : 0u);
     if (!c) continue;
     if (op.kind == SPK_OP_CGROUP) {
-      p = n_write(N, rec, heaps, w, p, i + 1, N.end[i], false);
+      q = n_write<D>(N, rec, heaps, w, sk, q, i + 1, N.end[i], false);
     } else {
       const uint64_t off = *reinterpret_cast<const uint64_t *>(rec + op.aux);
-      n_copy(p, heaps[N.heap[i]] + off * op.size, op.size);
-      p += op.size;
+      sk.put(q, heaps[N.heap[i]] + off * op.size, op.size);
+      q += op.size;
     }
   }
-  return p;
+  return q;
 }
 
 // ---- decode: one record (or an op range of it) from the wire ---------------------
@@ -969,12 +997,36 @@ static CWs cws_layout(uint64_t wire_len, uint32_t n_heaps) {
   return f;
 }
 
+// SPK_NEST_DIRECT=1: nested VECTOR encodes store bytes straight to HBM
+// (nest_write) instead of through LDS windows (nest_write_win) (A/B)
+static bool nest_direct_write() {
+  static const bool v = [] {
+    const char *e = getenv("SPK_NEST_DIRECT");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+// SPK_NEST_CHUNKED=1: VECTOR decodes of nested layouts take the chunked
+// interpreter below instead of the tile decoder (A/B)
+static bool nest_chunked() {
+  static const bool v = [] {
+    const char *e = getenv("SPK_NEST_CHUNKED");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 size_t nested_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len) {
   const NLayout N = make_nlayout(L);
   size_t b = nws_layout(n, N.n_heaps, N.n_ranks).end;
   if (mode == SPK_MODE_VECTOR && !N.n_ranks) {
     const size_t c = cws_layout(wire_len, N.n_heaps).end;
     if (c > b) b = c;
+    if (var_nested_tile_ok(L)) {
+      const size_t t = var_nested_tile_ws_bytes(L, wire_len);
+      if (t > b) b = t;
+    }
   }
   return b + 256;
 }
@@ -1014,6 +1066,7 @@ struct NEnc {
 
 // a[0][i] = payload bytes, a[1][i] = count fields (VECTOR) or the whole
 // message size (MESSAGES); the longest container into ctl->maxc
+template <int D>
 __global__ __launch_bounds__(256) void nest_size(NEnc e, const uint8_t *__restrict__ recs,
                                                  uint64_t *__restrict__ a, uint8_t *ws) {
   __shared__ NLayout N;
@@ -1022,7 +1075,7 @@ __global__ __launch_bounds__(256) void nest_size(NEnc e, const uint8_t *__restri
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t m = 0;
   if (i < e.n) {
-    const NSize s = n_size(N, recs + i * N.stride, e.heaps, 0, N.n_ops, true);
+    const NSize s = n_size<D>(N, recs + i * N.stride, e.heaps, 0, N.n_ops, true);
     m = s.maxc;
     if (e.mode == SPK_MODE_MESSAGES) {
       const uint32_t w = width_of(s.maxc);
@@ -1059,6 +1112,7 @@ __global__ void nest_ctl_init(uint8_t *ws) {
 
 // VECTOR: sizes[i] = bytes + cnts * w (in place over a[0]), w from maxc;
 // column 2 + rk: the bytes of record i in the version pass of rank rk
+template <int D>
 __global__ void nest_vec_sizes(NEnc e, const uint8_t *__restrict__ recs,
                                uint64_t *__restrict__ a, uint8_t *ws) {
   __shared__ NLayout N;
@@ -1070,7 +1124,7 @@ __global__ void nest_vec_sizes(NEnc e, const uint8_t *__restrict__ recs,
        i += (uint64_t)gridDim.x * blockDim.x) {
     a[i] = a[i] + a[e.n + i] * w;
     for (uint32_t rk = 0; rk < N.n_ranks; ++rk)
-      a[(2 + rk) * e.n + i] = n_compat_size(N, recs + i * N.stride, e.heaps, rk, w);
+      a[(2 + rk) * e.n + i] = n_compat_size<D>(N, recs + i * N.stride, e.heaps, rk, w);
   }
 }
 
@@ -1114,6 +1168,7 @@ __global__ void nest_plan_fin(NEnc e, const uint64_t *__restrict__ a,
 
 // record i's bytes at its scanned offset (after the VECTOR header, or its
 // message with header and frame in MESSAGES mode)
+template <int D>
 __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restrict__ recs,
                                                   const uint64_t *__restrict__ off,
                                                   const uint64_t *__restrict__ part, uint64_t nb,
@@ -1146,11 +1201,12 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
     }
     if (i < e.n) {
       const uint8_t *rec = recs + i * N.stride;
-      n_write(N, rec, e.heaps, w, out + hl + off[i], 0, N.n_ops, true);
+      const NDirect sk{out};
+      n_write<D>(N, rec, e.heaps, w, sk, hl + off[i], 0, N.n_ops, true);
       // version passes after every record's main pass (packer.hpp:66-78)
       uint64_t sec = hl + tot0;
       for (uint32_t rk = 0; rk < N.n_ranks; ++rk) {
-        n_write_compat(N, rec, e.heaps, rk, w, out + sec + off[(2 + rk) * e.n + i]);
+        n_write_compat<D>(N, rec, e.heaps, rk, w, sk, sec + off[(2 + rk) * e.n + i]);
         sec += part[(2 + rk) * (nb + 1) + nb];
       }
     }
@@ -1160,7 +1216,7 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
   if (i == 0 && msg_offsets) msg_offsets[e.n] = e.n ? part[nb] : 0;
   if (i >= e.n) return;
   const uint8_t *rec = recs + i * N.stride;
-  const NSize s = n_size(N, rec, e.heaps, 0, N.n_ops, true);
+  const NSize s = n_size<D>(N, rec, e.heaps, 0, N.n_ops, true);
   const uint32_t w = width_of(s.maxc);
   uint8_t *p = out + off[i];
   if (msg_offsets) msg_offsets[i] = off[i];
@@ -1169,8 +1225,10 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
   const uint32_t hl = N.n_ranks ? compat_hdr(hb, e.fmt, w, s.bytes + s.cnts * w)
                                   : write_hdr(hb, e.fmt, w);
   for (uint32_t b = 0; b < hl; ++b) m[b] = hb[b];
-  uint8_t *q = n_write(N, rec, e.heaps, w, m + hl, 0, N.n_ops, true);
-  for (uint32_t rk = 0; rk < N.n_ranks; ++rk) q = n_write_compat(N, rec, e.heaps, rk, w, q);
+  const NDirect sk{m};
+  uint64_t qo = n_write<D>(N, rec, e.heaps, w, sk, hl, 0, N.n_ops, true);
+  for (uint32_t rk = 0; rk < N.n_ranks; ++rk) qo = n_write_compat<D>(N, rec, e.heaps, rk, w, sk, qo);
+  uint8_t *q = m + qo;
   if (e.fpre) {
     for (uint32_t b = 0; b < e.fpre; ++b) p[b] = e.ftmpl[b];
     const uint32_t mlen = (uint32_t)(q - m);
@@ -1180,6 +1238,56 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
     }
     if (e.flen_off != SPK_FRAME_NONE)
       for (uint32_t b = 0; b < 4; ++b) p[e.flen_off + b] = (uint8_t)(mlen >> (8 * b));
+  }
+}
+
+
+// VECTOR without compatible members: each block's contiguous output range
+// (its 256 records at their scanned offsets) is assembled in an LDS window,
+// kNEncWin bytes at a time (a lane writes the part of its record inside the
+// window), and flushed with aligned 16-B stores; unaligned byte stores
+// straight to HBM cost several times their bytes in write traffic.
+constexpr uint32_t kNEncWin = 24 * 1024;
+template <int D>
+__global__ __launch_bounds__(256) void nest_write_win(NEnc e, const uint8_t *__restrict__ recs,
+                                                      const uint64_t *__restrict__ off,
+                                                      const uint64_t *__restrict__ part,
+                                                      uint64_t nb, uint8_t *ws,
+                                                      uint8_t *__restrict__ out, uint64_t out_cap) {
+  __shared__ NLayout N;
+  __shared__ __align__(16) uint8_t lds[kNEncWin];
+  n_stage(N, e.N);
+  const NCtl *ctl = reinterpret_cast<const NCtl *>(ws + kWsCtl);
+  const uint64_t mx = ctl->maxc > e.n ? ctl->maxc : e.n;
+  const uint32_t w = width_of(mx);
+  const uint64_t tot0 = e.n ? part[nb] : 0;
+  const uint32_t hl = hdr_shape(e.fmt.flags, e.fmt.literal_len, w).len + w;
+  if (hl + tot0 > out_cap) return;  // nothing is written (the caller reads the plan)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    write_hdr(out, e.fmt, w);
+    for (uint32_t b = 0; b < w; ++b) out[hl - w + b] = (uint8_t)(e.n >> (8 * b));
+  }
+  const uint64_t r0 = (uint64_t)blockIdx.x * 256, i = r0 + threadIdx.x;
+  if (r0 >= e.n) return;
+  const uint64_t rend = r0 + 256 < e.n ? r0 + 256 : e.n;
+  const uint64_t g0 = hl + off[r0], g1 = hl + (rend < e.n ? off[rend] : tot0);
+  const uint64_t q0 = i < e.n ? hl + off[i] : 0;
+  const uint64_t q1 = i < e.n ? (i + 1 < e.n ? hl + off[i + 1] : hl + tot0) : 0;
+  const uint8_t *rec = recs + i * N.stride;
+  for (uint64_t wlo = g0 & ~15ull; wlo < g1; wlo += kNEncWin) {
+    const NWin W{lds, wlo, wlo + kNEncWin < g1 ? wlo + kNEncWin : g1};
+    if (i < e.n && q0 < W.hi && q1 > W.lo) n_write<D>(N, rec, e.heaps, w, W, q0, 0, N.n_ops, true);
+    __syncthreads();
+    // flush [max(W.lo, g0), W.hi): aligned 16-B chunks, bytes at the edges
+    for (uint64_t c = W.lo + (uint64_t)threadIdx.x * 16; c < W.hi; c += 256 * 16) {
+      const uint64_t lo = c > g0 ? c : g0;
+      const uint64_t hi = c + 16 < W.hi ? c + 16 : W.hi;
+      if (lo == c && hi == c + 16)
+        *reinterpret_cast<v4u_t *>(out + c) = *reinterpret_cast<const v4u_t *>(lds + (c - W.lo));
+      else
+        for (uint64_t x = lo; x < hi; ++x) out[x] = lds[x - W.lo];
+    }
+    __syncthreads();
   }
 }
 
@@ -1208,11 +1316,13 @@ static hipError_t nest_size_scan(const NEnc &e, const void *d_recs, uint8_t *ws,
   uint64_t *part = reinterpret_cast<uint64_t *>(ws + f.part);
   SPK_LAUNCH(nest_ctl_init, dim3(1), dim3(1), 0, s, ws);
   if (e.n) {
-    SPK_LAUNCH(nest_size, dim3(nblocks(e.n, 256)), dim3(256), 0, s, e, (const uint8_t *)d_recs,
-               a, ws);
+    NEST_D(n_dclass(e.N),
+           SPK_LAUNCH(nest_size<D>, dim3(nblocks(e.n, 256)), dim3(256), 0, s, e,
+                      (const uint8_t *)d_recs, a, ws));
     if (e.mode == SPK_MODE_VECTOR)
-      SPK_LAUNCH(nest_vec_sizes, dim3(nblocks(e.n, 256) < 4096 ? nblocks(e.n, 256) : 4096),
-                 dim3(256), 0, s, e, (const uint8_t *)d_recs, a, ws);
+      NEST_D(n_dclass(e.N),
+             SPK_LAUNCH(nest_vec_sizes<D>, dim3(nblocks(e.n, 256) < 4096 ? nblocks(e.n, 256) : 4096),
+                        dim3(256), 0, s, e, (const uint8_t *)d_recs, a, ws));
   }
   hipError_t er = hipGetLastError();
   if (er != hipSuccess) return er;
@@ -1258,9 +1368,17 @@ hipError_t launch_nested_encode(const spk_layout *L, int mode, uint64_t n, const
   uint64_t *a, *part, nb;
   hipError_t er = nest_size_scan(e, d_recs, ws, s, &a, &part, &nb);
   if (er != hipSuccess) return er;
-  SPK_LAUNCH(nest_write, dim3(nblocks(n, 256)), dim3(256), 0, s, e, (const uint8_t *)d_recs,
-             (const uint64_t *)a, (const uint64_t *)part, nb, ws, (uint8_t *)d_out,
-             d_msg_offsets, fixed_w ? 0u : 1u, out_cap);
+  if (mode == SPK_MODE_VECTOR && !e.N.n_ranks && !fixed_w && !nest_direct_write()) {
+    NEST_D(n_dclass(e.N),
+           SPK_LAUNCH(nest_write_win<D>, dim3(nblocks(n, 256)), dim3(256), 0, s, e,
+                      (const uint8_t *)d_recs, (const uint64_t *)a, (const uint64_t *)part, nb, ws,
+                      (uint8_t *)d_out, out_cap));
+    return hipGetLastError();
+  }
+  NEST_D(n_dclass(e.N),
+         SPK_LAUNCH(nest_write<D>, dim3(nblocks(n, 256)), dim3(256), 0, s, e,
+                    (const uint8_t *)d_recs, (const uint64_t *)a, (const uint64_t *)part, nb, ws,
+                    (uint8_t *)d_out, d_msg_offsets, fixed_w ? 0u : 1u, out_cap));
   return hipGetLastError();
 }
 
@@ -1780,6 +1898,11 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
                                 spk_dresult_t *d_res, int32_t *d_errc, void *d_ws,
                                 hipStream_t s, uint32_t body_w, uint64_t body_n,
                                 const uint64_t *d_msg_ends) {
+  // (the tile decoder counts heap slots in 32 bits: wires below 4 GiB)
+  if (mode == SPK_MODE_VECTOR && var_nested_tile_ok(L) && wire_len < (1ull << 32) &&
+      !nest_chunked())
+    return launch_var_nested_decode(L, d_wire, wire_len, d_recs, rec_cap, d_heaps, heap_caps,
+                                    d_res, d_ws, s, body_w, body_n);
   NDec a = {};
   a.ends = d_msg_ends;
   a.body_w = body_w;

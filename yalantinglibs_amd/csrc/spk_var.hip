@@ -35,6 +35,7 @@
 // straddling part exceeds 255 bytes defeat the 256-entry table: that case
 // falls back to one sequential walker (correct, slow) — see DESIGN.md.
 #include "spk_internal.hpp"
+#include "spk_nlayout.hpp"
 
 #include <stdlib.h>
 
@@ -53,6 +54,13 @@ namespace spk {
 // Heaps of the flat-record kernels in this file: a flat layout with more
 // variable-length members runs the interpreter (spk_nested.hip).
 constexpr uint32_t kVS = SPK_FLAT_SPANS;
+
+// Span loops q < nsp with a compile-time trip count (the arrays they index
+// stay in registers; a runtime bound would put them in scratch memory):
+// QFOR in functions templated on NS, QFORV elsewhere, QFORS over SpecPath.
+#define QFOR(q) _Pragma("unroll") for (uint32_t q = 0; q < (NS > 0 ? (uint32_t)NS : kVS); ++q) if (q < nsp)
+#define QFORV(q) _Pragma("unroll") for (uint32_t q = 0; q < kVS; ++q) if (q < nsp)
+#define QFORS(q) _Pragma("unroll") for (uint32_t q = 0; q < (uint32_t)SpecPath<NS>::kS; ++q) if (q < nsp)
 constexpr int kThreads = 256;
 constexpr int kIPT = 1;                     // records per thread (encode write; 2 measured
                                             // slower: C3 +19 %, C5 3x as big payloads
@@ -887,10 +895,11 @@ struct DecArgs {
   uint32_t body_w;  // VECTOR, spk_decode_body: no header, body_n records at this width
   uint64_t body_n;
   uint32_t range;   // spk_decode_shard_index: tiles [range_t0, ...) of the body
-  uint32_t pad2_;
+  uint32_t nested;  // VECTOR tile decode of a nested layout (NS = -2; the layout at nl)
   uint64_t range_t0, range_entry;
   const uint64_t *ends;  // MESSAGES: message i ends at ends[i] (null: offs[i + 1])
   const uint64_t *dn;    // MESSAGES: device count (min(*dn, n_msgs)) or null
+  const void *nl;        // nested: the NTLayout in device memory (workspace)
 };
 
 
@@ -1137,6 +1146,7 @@ struct FCtl {
   uint32_t last;                 // range mode: the range holds the message's end
   unsigned long long stot[kVS];  // span-count sums on the path
   unsigned long long nlist[4];   // tiles listed for re-resolution by select pass k
+  unsigned long long diag[8];    // SPK_TILE_DBG & 4096: K1 statistics (scripts/diag_tiles.py)
 };
 constexpr size_t kWsFCtl = kWsCtl + 1280;
 static_assert(kWsFCtl + sizeof(FCtl) <= kWsScratch, "FCtl overlaps the scratch area");
@@ -1233,9 +1243,15 @@ __device__ __forceinline__ bool vi_seg_rd(const WalkProg &P, uint32_t k, const R
   return true;
 }
 
+// the nested walker (NS = -2, defined with the tile decoder below)
+template <bool SIMPLE, typename Rd>
+__device__ uint64_t nt_len(const Rd &rd, uint64_t len, uint64_t pos, uint64_t *cnt,
+                           uint64_t reach);
+
 // Wire length of the record at `pos` (0 = incomplete: the reference fails it
 // with no_buffer_space). NS > 0: compile-time span count; 0: runtime count;
-// -1: runtime count and the record has varints.
+// -1: runtime count and the record has varints; -2: a nested layout (the
+// interpreter walk, nt_len).
 template <int NS>
 __device__ __forceinline__ uint64_t wlen(const WalkProg &P, const uint8_t *wire, uint64_t len,
                                          uint64_t pos, uint32_t w) {
@@ -1270,6 +1286,7 @@ __device__ __forceinline__ uint64_t wlen(const WalkProg &P, const uint8_t *wire,
 template <int NS, typename Rd>
 __device__ __forceinline__ uint64_t wlen_rd(const WalkProg &P, const Rd &rd, uint64_t len,
                                             uint64_t pos, uint32_t w, uint64_t *cnt = nullptr) {
+  if constexpr (NS <= -2) return nt_len<NS == -3>(rd, len, pos, cnt, 0);
   uint64_t p = pos + P.skip[0];
   const uint32_t ns = NS > 0 ? (uint32_t)NS : P.ns;
   if (NS < 0 && !vi_seg_rd(P, 0, rd, len, p)) return 0;
@@ -1363,6 +1380,7 @@ __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);  // tile decoder state
   for (int k = 0; k < 4; ++k) fc->broken[k] = fc->nlist[k] = 0;
   fc->unresolved = 0;
+  for (int k = 0; k < 8; ++k) fc->diag[k] = 0;
   fc->seq = 0;
   fc->njobs = 0;
   fc->term_tile = ~0ull;
@@ -1546,6 +1564,512 @@ __device__ __forceinline__ void emit_record_rd(const KLayout &L, const WinReader
   }
 }
 
+// ===========================================================================
+// Nested layouts on the tile decoder (NS = -2)
+// ===========================================================================
+// VECTOR messages of layouts with ARRAY / VARIANT / OPTGROUP / FVAR ops (no
+// compatible members, at most kVS heaps) run the tile pipeline below with the
+// op-list interpreter as the record walker: nt_read restates n_read
+// (spk_nested.hip; unpacker.hpp:1127-1292 for containers, optional, variant)
+// over the tile's LDS window, with the element stack in registers (static
+// indices over SPK_MAX_DEPTH frames) and the layout staged in LDS. A record's
+// heap use per heap takes the place of the flat walker's span counts, so the
+// speculation, selection, tile scan and the emission's wave scans are the flat
+// pipeline's; emission writes the record, its element records and its heap
+// payloads (long ones queued for vec_big_copy).
+struct NTLayout {
+  spk_op ops[SPK_MAX_OPS];
+  uint8_t heap[SPK_MAX_OPS];  // heap of a SPAN / OPTION / ARRAY op
+  uint8_t end[SPK_MAX_OPS];   // ARRAY: its END; VARIANT / OPTGROUP: the END of its last group
+  uint32_t n_ops, n_heaps, fv_cnt, fv_has64, fv_bits;
+  uint32_t groups;            // a VARIANT / OPTGROUP op: errors inside may be dropped
+  uint32_t wp_n;              // walk program length (0: walks run nt_read)
+  uint32_t pad_;
+  uint8_t *heaps[kVS];
+  // walk program of a layout of COPY / SPAN / OPTION / ARRAY ops only: one
+  // u32 per instruction, op | heap << 3 | arg << 8 (WP_*), consecutive COPYs
+  // merged; record lengths and heap use without the interpreter's bookkeeping
+  uint32_t wp[SPK_MAX_OPS];
+};
+constexpr uint32_t WP_SKIP = 1, WP_SPAN = 2, WP_OPT = 3, WP_ARR = 4, WP_END = 5;
+static_assert(sizeof(NTLayout) % 16 == 0, "NTLayout staged as 16-B words");
+static_assert(SPK_MAX_DEPTH == 4, "the walker's element stack has 4 register frames");
+
+__device__ __forceinline__ uint32_t nt_lane() {
+  return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+__device__ __forceinline__ NTLayout &nt_lds() {
+  __shared__ NTLayout s;
+  return s;
+}
+// each lane's heap slots in use during a walk (LDS, [heap][lane]: the
+// kernels of this path run one wave per block); u32: wires below 4 GiB
+__device__ __forceinline__ uint32_t *nt_used() {
+  __shared__ uint32_t u[kVS * 64];
+  return u + nt_lane();
+}
+// the layout into LDS by one wave (every lane of the calling wave takes part)
+__device__ __forceinline__ void nt_stage_wave(const void *src, uint32_t lane) {
+  const v4u_t *s = reinterpret_cast<const v4u_t *>(src);
+  v4u_t *d = reinterpret_cast<v4u_t *>(&nt_lds());
+  for (uint32_t k = lane; k < sizeof(NTLayout) / 16; k += 64) d[k] = s[k];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+template <int NS>
+__device__ __forceinline__ void nt_prologue(const DecArgs &a, uint32_t lane) {
+  if constexpr (NS <= -2) nt_stage_wave(a.nl, lane);
+}
+
+// the walker's element stack: the top frame lives in registers, the frames
+// below it in LDS ([frame][field][lane]); pointers only when emitting
+__device__ __forceinline__ uint32_t *nt_frames() {
+  __shared__ uint32_t f[(SPK_MAX_DEPTH - 1) * 3 * 64];
+  return f + nt_lane();
+}
+__device__ __forceinline__ uint8_t **nt_fptrs() {
+  __shared__ uint8_t *f[(SPK_MAX_DEPTH - 1) * 2 * 64];
+  return f + nt_lane();
+}
+// first op of group a of the VARIANT / OPTGROUP at i; the END closing the group at j
+__device__ __forceinline__ uint32_t nt_alt_start(const NTLayout &N, uint32_t i, uint32_t a) {
+  uint32_t j = i + 1;
+  while (a) {
+    const uint32_t k = N.ops[j].kind;
+    if (k == SPK_OP_ARRAY || k == SPK_OP_VARIANT || k == SPK_OP_OPTGROUP) {
+      j = N.end[j] + 1u;
+      continue;
+    }
+    if (k == SPK_OP_END) --a;
+    ++j;
+  }
+  return j;
+}
+__device__ __forceinline__ uint32_t nt_alt_end(const NTLayout &N, uint32_t j) {
+  for (;;) {
+    const uint32_t k = N.ops[j].kind;
+    if (k == SPK_OP_ARRAY || k == SPK_OP_VARIANT || k == SPK_OP_OPTGROUP) {
+      j = N.end[j] + 1u;
+      continue;
+    }
+    if (k == SPK_OP_END) return j;
+    ++j;
+  }
+}
+
+constexpr int32_t kNTLimit = 0x7FFF0001;  // a bounded walk needed bytes past its limit
+// a bounded (speculative) walk also gives up on a container of more elements:
+// from a false start, element counts read from payload bytes would have the
+// walk iterate up to its byte limit one element at a time
+constexpr uint64_t kNTSpecElems = 64;
+
+// deserialize_fast_varint of the top-level record (unpacker.hpp:642-747), as n_fv_read
+template <bool EMIT, typename Rd>
+__device__ __forceinline__ int32_t nt_fv_read(const NTLayout &N, const Rd &rd, uint64_t &pos,
+                                              uint64_t lim, uint8_t *rec) {
+  if (lim - pos < N.fv_bits) return SPK_ERRC_NO_BUFFER_SPACE;
+  uint64_t bits = 0;
+  for (uint32_t b = 0; b < N.fv_bits; ++b) bits |= (uint64_t)rd.byte(pos + b) << (8 * b);
+  pos += N.fv_bits;
+  const uint32_t code = (uint32_t)(bits >> N.fv_cnt) & 3u;
+  if (code == 3 && !N.fv_has64) return SPK_ERRC_INVALID_BUFFER;
+  const uint32_t wb = 1u << code;
+  uint32_t j = 0;
+  for (uint32_t i = 0; i < N.n_ops; ++i) {
+    const spk_op op = N.ops[i];
+    if (op.kind != SPK_OP_FVAR) continue;
+    uint64_t v = 0;
+    if ((bits >> j) & 1u) {
+      const uint32_t rw = wb < op.size ? wb : op.size;
+      if (lim - pos < rw) return SPK_ERRC_NO_BUFFER_SPACE;
+      for (uint32_t b = 0; b < rw; ++b) v |= (uint64_t)rd.byte(pos + b) << (8 * b);
+      pos += rw;
+      if ((op.aux & SPK_FVAR_SIGNED) && rw < 8 && ((v >> (8 * rw - 1)) & 1u)) v |= ~0ull << (8 * rw);
+    }
+    if constexpr (EMIT) {
+      if (op.size == 4)
+        *reinterpret_cast<uint32_t *>(rec + op.rec_off) = (uint32_t)v;
+      else
+        *reinterpret_cast<uint64_t *>(rec + op.rec_off) = v;
+    }
+    ++j;
+  }
+  return SPK_ERRC_OK;
+}
+
+// One record at pos (n_read over a reader; reads stop at lim, a bounded walk
+// (lim short of the wire's end) gives up there with kNTLimit). used[k]: next
+// slot of heap k. EMIT writes the record at rec, its element records and its
+// heap payloads (the caller checked the capacities). `quick`: a container
+// whose count exceeds the bytes left fails at once (exact for the walk's
+// outcome when no variant / optional group can drop the error; the errc of
+// a failing record is taken with quick = false).
+template <bool EMIT, typename Rd>
+__device__ int32_t nt_read(const NTLayout &N, const Rd &rd, uint64_t &pos, uint64_t lim,
+                           bool bounded, uint8_t *rec, const BigQ *bq, bool quick) {
+  uint32_t *const U = nt_used();  // U[64 * k]: heap k
+  const uint32_t w = rd.w;
+  // top frame: aop | pend << 8 | first << 16 | ret << 24, element index and
+  // count (a count past the bytes left is clamped to bytes left + 1: elements
+  // take at least one byte, so the walk fails at the same element; the tile
+  // decoder runs on wires below 4 GiB), element records and the record to
+  // resume (EMIT); the frames below it in LDS
+  uint32_t c_op = 0, c_j = 0, c_cnt = 0;
+  uint8_t *c_el = nullptr, *c_pr = nullptr;
+  uint32_t *const F = nt_frames();
+  uint8_t **const FP = EMIT ? nt_fptrs() : nullptr;
+  auto push = [&](uint32_t d0, uint32_t o, uint32_t cn, uint8_t *el, uint8_t *pr) {
+    if (d0) {
+      F[64 * (3 * (d0 - 1))] = c_op;
+      F[64 * (3 * (d0 - 1) + 1)] = c_j;
+      F[64 * (3 * (d0 - 1) + 2)] = c_cnt;
+      if constexpr (EMIT) {
+        FP[64 * (2 * (d0 - 1))] = c_el;
+        FP[64 * (2 * (d0 - 1) + 1)] = c_pr;
+      }
+    }
+    c_op = o;
+    c_j = 0;
+    c_cnt = cn;
+    c_el = el;
+    c_pr = pr;
+  };
+  auto pop = [&](uint32_t d1) {  // d1: the depth after the pop
+    if (d1) {
+      c_op = F[64 * (3 * (d1 - 1))];
+      c_j = F[64 * (3 * (d1 - 1) + 1)];
+      c_cnt = F[64 * (3 * (d1 - 1) + 2)];
+      if constexpr (EMIT) {
+        c_el = FP[64 * (2 * (d1 - 1))];
+        c_pr = FP[64 * (2 * (d1 - 1) + 1)];
+      }
+    }
+  };
+  uint32_t d = 0, i = 0, iend = N.n_ops;
+  uint8_t *r = rec;
+  int32_t ec = SPK_ERRC_OK;
+  if (N.fv_cnt && (ec = nt_fv_read<EMIT>(N, rd, pos, lim, r)))
+    return bounded && ec == SPK_ERRC_NO_BUFFER_SPACE ? kNTLimit : ec;
+  for (;;) {
+    if (ec) {
+      // unwind to the innermost variant / optional / expected group, whose
+      // errc is dropped (unpacker.hpp:476-490, 1251-1277); an ARRAY keeps its
+      // failing element and gives back the slots past it (:1208-1226)
+      bool dropped = false;
+      while (d) {
+        const uint32_t fo = c_op;
+        const spk_op &ao = N.ops[fo & 0xFFu];
+        if (ao.kind == SPK_OP_VARIANT || ao.kind == SPK_OP_OPTGROUP) {
+          i = fo >> 24;
+          iend = (fo >> 8) & 0xFFu;
+          if constexpr (EMIT) r = c_pr;
+          pop(--d);
+          dropped = true;
+          break;
+        }
+        const uint32_t hk = N.heap[fo & 0xFFu];
+        atomicSub(U + 64 * hk, c_cnt - (c_j + 1));
+        if constexpr (EMIT) *reinterpret_cast<uint32_t *>(c_pr + ao.rec_off) = c_j + 1;
+        pop(--d);
+      }
+      if (!dropped) return ec;
+      ec = SPK_ERRC_OK;
+      continue;
+    }
+    if (i >= iend) {
+      if (!d) break;
+      const uint32_t fo = c_op;
+      if (++c_j < c_cnt) {
+        if constexpr (EMIT) r = c_el + (uint64_t)c_j * N.ops[fo & 0xFFu].size;
+        i = (fo >> 16) & 0xFFu;
+        continue;
+      }
+      i = fo >> 24;
+      iend = (fo >> 8) & 0xFFu;
+      if constexpr (EMIT) r = c_pr;
+      pop(--d);
+      continue;
+    }
+    const spk_op op = N.ops[i];
+    const uint32_t kind = op.kind;
+    if (kind == SPK_OP_FVAR) {  // read with the group
+      ++i;
+      continue;
+    }
+    if (kind == SPK_OP_COPY) {
+      if (lim - pos < op.size) {
+        if (bounded) return kNTLimit;
+        ec = SPK_ERRC_NO_BUFFER_SPACE;
+        continue;
+      }
+      if constexpr (EMIT) rd.copy_to(r + op.rec_off, pos, op.size);
+      pos += op.size;
+      ++i;
+      continue;
+    }
+    if (kind == SPK_OP_VARINT) {  // deserialize_varint (varint.hpp:270-330)
+      uint64_t v = 0;
+      const uint32_t l = rd.vread(pos, lim, &v);
+      if (!l) {  // truncated: the bytes read stay consumed
+        if (bounded) return kNTLimit;
+        pos = lim;
+        ec = SPK_ERRC_NO_BUFFER_SPACE;
+        continue;
+      }
+      if (l == kViBad) {
+        pos += 10;
+        ec = SPK_ERRC_INVALID_BUFFER;
+        continue;
+      }
+      pos += l;
+      if constexpr (EMIT) vi_store(op, r, v);
+      ++i;
+      continue;
+    }
+    if (kind == SPK_OP_VARIANT || kind == SPK_OP_OPTGROUP) {
+      // variant: unpacker.hpp:1278-1292; optional / expected: :1251-1277
+      if (pos >= lim) {
+        if (bounded) return kNTLimit;
+        ec = SPK_ERRC_NO_BUFFER_SPACE;
+        continue;
+      }
+      const uint32_t b = rd.byte(pos++);
+      int a;
+      if (kind == SPK_OP_VARIANT) {
+        if (b >= op.size) {
+          ec = SPK_ERRC_INVALID_BUFFER;
+          continue;
+        }
+        a = (int)b;
+        if constexpr (EMIT) *reinterpret_cast<uint32_t *>(r + op.rec_off) = b;
+      } else {
+        a = b ? 0 : (op.size == 2 ? 1 : -1);
+        if constexpr (EMIT) *reinterpret_cast<uint32_t *>(r + op.rec_off) = b ? 1u : 0u;
+      }
+      if (a < 0) {
+        i = N.end[i] + 1u;
+        continue;
+      }
+      if (d == SPK_MAX_DEPTH) {  // (spk_layout_check bounds the nesting)
+        ec = SPK_ERRC_INVALID_BUFFER;
+        continue;
+      }
+      const uint32_t a0 = nt_alt_start(N, i, (uint32_t)a);
+      push(d++, i | (iend << 8) | (a0 << 16) | ((N.end[i] + 1u) << 24), 1u, r, r);
+      iend = nt_alt_end(N, a0);
+      i = a0;
+      continue;
+    }
+    // SPAN / OPTION / ARRAY
+    const uint32_t hk = N.heap[i];
+    const uint32_t pw = kind == SPK_OP_OPTION ? 1u : w;
+    if (lim - pos < pw) {
+      if (bounded) return kNTLimit;
+      ec = SPK_ERRC_NO_BUFFER_SPACE;
+      continue;
+    }
+    uint64_t cnt = kind == SPK_OP_OPTION ? (uint64_t)(rd.byte(pos) != 0) : rd(pos);
+    pos += pw;
+    uint64_t off = 0;
+    if constexpr (EMIT) off = U[64 * hk];
+    if (EMIT && kind != SPK_OP_SPAN) {
+      *reinterpret_cast<uint32_t *>(r + op.rec_off) = (uint32_t)cnt;
+      *reinterpret_cast<uint64_t *>(r + op.aux) = off;
+    }
+    if (kind == SPK_OP_ARRAY) {
+      // an element takes at least one wire byte
+      if (bounded && cnt > kNTSpecElems) return kNTLimit;
+      if (cnt > lim - pos) {
+        if (bounded) return kNTLimit;
+        if (quick && !N.groups) {
+          ec = SPK_ERRC_NO_BUFFER_SPACE;
+          continue;
+        }
+      }
+      if (cnt > lim - pos) cnt = lim - pos + 1;  // (the element past the bytes fails)
+      atomicAdd(U + 64 * hk, (uint32_t)cnt);
+      if (!cnt) {
+        i = N.end[i] + 1u;
+        continue;
+      }
+      if (d == SPK_MAX_DEPTH) {
+        ec = SPK_ERRC_INVALID_BUFFER;
+        continue;
+      }
+      uint8_t *el = EMIT ? N.heaps[hk] + off * op.size : nullptr;
+      push(d++, i | (iend << 8) | ((i + 1u) << 16) | ((N.end[i] + 1u) << 24), (uint32_t)cnt, el, r);
+      r = el;
+      iend = N.end[i];
+      ++i;
+      continue;
+    }
+    if (kind == SPK_OP_OPTION) {
+      if (cnt) {
+        const bool fits = lim - pos >= op.size;
+        if (!fits && bounded) return kNTLimit;
+        if constexpr (EMIT) {
+          uint8_t *hp = N.heaps[hk] + off * op.size;
+          if (fits)
+            rd.copy_to(hp, pos, op.size);
+          else
+            for (uint32_t b = 0; b < op.size; ++b) hp[b] = 0;  // unreadable value
+        }
+        if (fits) pos += op.size;
+      }
+      atomicAdd(U + 64 * hk, (uint32_t)cnt);
+      ++i;
+      continue;
+    }
+    // SPAN (unpacker.hpp:1127-1156): the whole payload must be present
+    if (cnt) {
+      if ((op.size > 1 && cnt > ~0ull / op.size) || lim - pos < cnt * op.size) {
+        if (bounded) return kNTLimit;
+        ec = SPK_ERRC_NO_BUFFER_SPACE;
+        continue;
+      }
+      const uint64_t nb = cnt * op.size;
+      if constexpr (EMIT) {
+        uint8_t *hp = N.heaps[hk] + off * op.size;
+        if (nb >= kBigCopy) {
+          const uint64_t np = (nb + kBigPiece - 1) / kBigPiece;
+          const uint64_t j0 = atomicAdd(bq->n, (unsigned long long)np);
+          for (uint64_t q = 0; q < np; ++q) {
+            const uint64_t o = q * kBigPiece, m = nb - o < kBigPiece ? nb - o : kBigPiece;
+            if (j0 + q < bq->cap)
+              bq->jobs[j0 + q] = BigJob{pos + o, m, hp + o};
+            else
+              copy_bytes(hp + o, rd.wire + pos + o, m);  // (the cap is never reached)
+          }
+        } else {
+          rd.copy_to(hp, pos, nb);
+        }
+      }
+      pos += nb;
+    }
+    if constexpr (EMIT) {
+      *reinterpret_cast<uint32_t *>(r + op.rec_off) = (uint32_t)cnt;
+      *reinterpret_cast<uint64_t *>(r + op.aux) = off;
+    }
+    atomicAdd(U + 64 * hk, (uint32_t)cnt);
+    ++i;
+  }
+  return SPK_ERRC_OK;
+}
+
+// A record's wire length through the walk program (0: the record fails, or a
+// bounded walk would need bytes past lim); heap use into the lane's LDS
+// counters. Exact for the walk's outcome: these layouts have no group that
+// could drop an error.
+template <typename Rd>
+__device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint64_t lim,
+                            bool bounded) {
+  uint32_t *const U = nt_used();
+  uint32_t *const F = nt_frames();
+  const uint32_t w = rd.w;
+  uint64_t p = pos;
+  uint32_t pc = 0, d = 0, body = 0, rem = 0;  // top loop frame: body start, elements left
+  while (pc < N.wp_n) {
+    const uint32_t ins = N.wp[pc];
+    const uint32_t op = ins & 7u, h = (ins >> 3) & 31u, arg = ins >> 8;
+    if (op == WP_SKIP) {
+      if (lim - p < arg) return 0;
+      p += arg;
+      ++pc;
+    } else if (op == WP_END) {
+      if (--rem) {
+        pc = body;
+      } else {
+        ++pc;
+        if (--d) {  // the enclosing loop's frame back from LDS
+          body = F[64 * (3 * (d - 1))];
+          rem = F[64 * (3 * (d - 1) + 1)];
+        }
+      }
+    } else if (op == WP_OPT) {  // [has_value:1][U if present]; an unreadable value leaves the reader
+      if (p >= lim) return 0;
+      const uint32_t b = rd.byte(p++);
+      if (b) {
+        if (lim - p >= arg) p += arg;
+        atomicAdd(U + 64 * h, 1u);
+      }
+      ++pc;
+    } else {  // WP_SPAN / WP_ARR: [count:w]
+      if (lim - p < w) return 0;
+      const uint64_t c = rd(p);
+      p += w;
+      if (op == WP_SPAN) {
+        if (c && c > (lim - p) / arg) return 0;
+        p += c * arg;
+        atomicAdd(U + 64 * h, (uint32_t)c);
+        ++pc;
+      } else {
+        if (c > lim - p || (bounded && c > kNTSpecElems)) return 0;  // elements take >= 1 byte
+        atomicAdd(U + 64 * h, (uint32_t)c);
+        if (!c) {
+          pc = arg;
+        } else {
+          if (d) {
+            F[64 * (3 * (d - 1))] = body;
+            F[64 * (3 * (d - 1) + 1)] = rem;
+          }
+          ++d;
+          body = ++pc;
+          rem = (uint32_t)c;
+        }
+      }
+    }
+  }
+  return p - pos;
+}
+
+// wlen_rd for NS = -2: the record's wire length (0: the path fails here) and
+// its heap use per heap; reach > 0 bounds a speculative walk (past it: longer
+// than a plausible record, kPlaus + 1)
+template <bool SIMPLE, typename Rd>
+__device__ uint64_t nt_len(const Rd &rd, uint64_t len, uint64_t pos, uint64_t *cnt,
+                           uint64_t reach) {
+  const NTLayout &N = nt_lds();
+  uint32_t *const U = nt_used();
+  const uint32_t nh = N.n_heaps;
+#pragma unroll
+  for (uint32_t q = 0; q < kVS; ++q)
+    if (q < nh) U[64 * q] = 0;
+  const uint64_t lim = reach && reach < len - pos ? pos + reach : len;
+  uint64_t p = pos;
+  if constexpr (SIMPLE) {
+    p += nt_walk(N, rd, pos, lim, lim < len);
+  } else {
+    const int32_t ec = nt_read<false>(N, rd, p, lim, lim < len, nullptr, nullptr, true);
+    if (ec == kNTLimit) return (uint64_t)kPlaus + 1;
+    if (ec) return 0;
+  }
+  if (p == pos) return 0;  // (a record takes at least one byte: spk_layout_check)
+  if (cnt) {
+#pragma unroll
+    for (uint32_t q = 0; q < kVS; ++q)
+      if (q < nh) cnt[q] = U[64 * q];
+  }
+  return p - pos;
+}
+// the speculative walk's record length (a nested walk is bounded)
+template <int NS, typename Rd>
+__device__ __forceinline__ uint64_t wlen_spec(const WalkProg &P, const Rd &rd, uint64_t len,
+                                              uint64_t pos, uint32_t w, uint64_t *cnt) {
+  if constexpr (NS <= -2) return nt_len<NS == -3>(rd, len, pos, cnt, (uint64_t)kPlaus + 1);
+  return wlen_rd<NS>(P, rd, len, pos, w, cnt);
+}
+// emission of the record at pos with heap bases off[]
+__device__ __forceinline__ void nt_emit(const WinReader &rd, uint64_t pos, uint64_t len,
+                                        uint8_t *rec, const uint64_t *off, const BigQ &bq) {
+  const NTLayout &N = nt_lds();
+  uint32_t *const U = nt_used();
+#pragma unroll
+  for (uint32_t q = 0; q < kVS; ++q)
+    if (q < N.n_heaps) U[64 * q] = (uint32_t)off[q];
+  nt_read<true>(N, rd, pos, len, false, rec, &bq, false);
+}
+
 constexpr uint64_t kTermPos = ~0ull;  // "the true path ended before this chunk"
 
 __device__ __forceinline__ uint64_t wave_excl_scan_u64(uint64_t v, uint32_t lane, uint64_t *tot) {
@@ -1624,7 +2148,7 @@ __device__ __forceinline__ void walk_true(const WalkProg &P, const Rd &rd, uint6
                                           uint64_t &term_at) {
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
   cnt = 0;
-  for (uint32_t q = 0; q < nsp; ++q) sums[q] = 0;
+  QFOR(q) sums[q] = 0;
   term_at = kTermPos;
   if (entry == kTermPos || entry == kNoPos) {
     ex = entry;
@@ -1640,7 +2164,7 @@ __device__ __forceinline__ void walk_true(const WalkProg &P, const Rd &rd, uint6
       return;
     }
     ++cnt;
-    for (uint32_t q = 0; q < nsp; ++q) sums[q] += rc[q];
+    QFOR(q) sums[q] += rc[q];
     x += L;
   }
   ex = x;
@@ -1669,7 +2193,7 @@ __device__ __forceinline__ void walk_merge(const WalkProg &P, const Rd &rd, uint
                                            uint64_t *sums, uint64_t &term_at) {
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
   cnt = 0;
-  for (uint32_t q = 0; q < nsp; ++q) sums[q] = 0;
+  QFOR(q) sums[q] = 0;
   term_at = kTermPos;
   if (entry == kTermPos || entry == kNoPos) {
     ex = entry;
@@ -1677,14 +2201,22 @@ __device__ __forceinline__ void walk_merge(const WalkProg &P, const Rd &rd, uint
   }
   uint64_t x = entry;
   while (x < ce) {
-    for (uint32_t j = 0; j < sp.np; ++j)
-      if (x == cs + sp.pos[j]) {  // joined the speculative path at its record j
-        cnt += sp.cnt - j;
-        for (uint32_t q = 0; q < nsp; ++q) sums[q] += sp.sums[q] - sp.ps[j][q];
-        ex = sp.ex;
-        term_at = sp.term_at;
-        return;
+    uint32_t jm = kMergePts;  // joined the speculative path at its record jm
+#pragma unroll
+    for (uint32_t j = 0; j < kMergePts; ++j)
+      if (jm == kMergePts && j < sp.np && x == cs + sp.pos[j]) jm = j;
+    if (jm < kMergePts) {
+      cnt += sp.cnt - jm;
+      QFORS(q) {
+        uint32_t pv = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kMergePts; ++j) pv = jm == j ? sp.ps[j][q] : pv;
+        sums[q] += sp.sums[q] - pv;
       }
+      ex = sp.ex;
+      term_at = sp.term_at;
+      return;
+    }
     uint64_t rc[NS > 0 ? NS : kVS];
     const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w, rc) : 0;
     if (!L) {
@@ -1693,7 +2225,7 @@ __device__ __forceinline__ void walk_merge(const WalkProg &P, const Rd &rd, uint
       return;
     }
     ++cnt;
-    for (uint32_t q = 0; q < nsp; ++q) sums[q] += rc[q];
+    QFOR(q) sums[q] += rc[q];
     x += L;
   }
   ex = x;
@@ -1730,14 +2262,16 @@ __device__ __forceinline__ void resolve_tile_sp(const WalkProg &P, const Rd &rd,
                                                 uint32_t lane, uint64_t entry0,
                                                 const SpecPath<NS> &sp, uint64_t &used,
                                                 uint64_t &ex, uint32_t &cnt, uint64_t *sums,
-                                                uint64_t &term_at) {
+                                                uint64_t &term_at, uint32_t *stat = nullptr) {
   for (int round = 0; round < 66; ++round) {
     const uint64_t prev = __shfl_up(ex, 1);
     const uint64_t entry = lane == 0 ? entry0 : prev;
     const bool need = entry != used;
     const uint64_t m = __ballot(need);
     if (!m) return;
+    if (stat) ++stat[0];
     if (need && (used == kNoPos || !(lane > 0 && ((m >> (lane - 1)) & 1)))) {  // as resolve_tile
+      if (stat) ++stat[1];
       walk_merge<NS>(P, rd, len, w, entry, cs, ce, sp, ex, cnt, sums, term_at);
       used = entry;
     }
@@ -1843,7 +2377,8 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
                                                       uint64_t len, uint32_t w, uint64_t ts,
                                                       uint64_t wend, uint64_t cs, uint64_t ce,
                                                       uint32_t lane, bool exact0, uint64_t p0,
-                                                      uint32_t dbg, TileLane<NS> &st) {
+                                                      uint32_t dbg, TileLane<NS> &st,
+                                                      uint32_t *stat = nullptr) {
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
   uint64_t &used = st.used, &ex = st.ex, &term_at = st.term_at;
   uint32_t &cnt = st.cnt;
@@ -1853,7 +2388,7 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
   ex = kNoPos;
   term_at = kTermPos;
   cnt = 0;
-  for (uint32_t q = 0; q < nsp; ++q) sums[q] = 0;
+  QFOR(q) sums[q] = 0;
   const bool exact = exact0 && lane == 0;  // the payload start: no search
   sp.np = 0;
   // ---- 1. speculative walk of this lane's chunk ----
@@ -1862,7 +2397,7 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
     bool searching = !exact, done = false;
     uint32_t k = 0;
     uint64_t ksum[NS > 0 ? NS : kVS];
-    for (uint32_t q = 0; q < nsp; ++q) ksum[q] = 0;
+    QFOR(q) ksum[q] = 0;
     const uint32_t s0 = P.skip[0];
     while (!done) {
       if (searching) {
@@ -1922,12 +2457,17 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
         k = 0;
         past = 0;
         ex = kNoPos;
-        for (uint32_t q = 0; q < nsp; ++q) ksum[q] = 0;
+        QFOR(q) ksum[q] = 0;
         searching = false;
       }
       uint64_t rc[NS > 0 ? NS : kVS];
-      const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w, rc) : 0;
+      // (the exact start of tile 0 walks unbounded: its records may be long)
+      const uint64_t L = x >= len ? 0
+                         : exact  ? wlen_rd<NS>(P, rd, len, x, w, rc)
+                                  : wlen_spec<NS>(P, rd, len, x, w, rc);
+      if (stat) ++stat[2];
       if (!exact && ((L == 0 && x < len) || L > kPlaus)) {  // off the record grid
+        if (stat) ++stat[3];
         tt += 1;
         searching = true;
         sx = kNoPos;
@@ -1940,12 +2480,14 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
           term_at = x;
           break;
         }
-        if (k < kMergePts) {
-          sp.pos[k] = (uint32_t)(x - cs);
-          for (uint32_t q = 0; q < nsp && q < SpecPath<NS>::kS; ++q) sp.ps[k][q] = (uint32_t)ksum[q];
-        }
+#pragma unroll
+        for (uint32_t j = 0; j < kMergePts; ++j)  // (static indices: sp stays in registers)
+          if (k == j) {
+            sp.pos[j] = (uint32_t)(x - cs);
+            QFORS(q) sp.ps[j][q] = (uint32_t)ksum[q];
+          }
         ++k;
-        for (uint32_t q = 0; q < nsp; ++q) ksum[q] += rc[q];
+        QFOR(q) ksum[q] += rc[q];
       } else {
         if (!past) ex = x;
         ++past;
@@ -1956,10 +2498,10 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
     if (sx != kNoPos) {
       used = sx;
       cnt = k;
-      for (uint32_t q = 0; q < nsp; ++q) sums[q] = ksum[q];
+      QFOR(q) sums[q] = ksum[q];
       // merge information: spans fit the path record, sums fit 32 bits
       bool mok = NS > 0 || P.ns <= (uint32_t)SpecPath<NS>::kS;
-      for (uint32_t q = 0; q < nsp && q < SpecPath<NS>::kS; ++q) {
+      QFORS(q) {
         mok = mok && ksum[q] < 0xFFFFFFFFull;
         sp.sums[q] = ksum[q];
       }
@@ -1976,6 +2518,7 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
     ex = kNoPos;
   }
   // ---- 2. resolution given the tile's assumed entry ----
+  const uint64_t used0 = used;
   uint64_t X = __shfl(used, 0);  // lane 0's spec start (kNoPos: no plausible start)
   if (exact0) X = p0;
   if (!exact0 && !(dbg & 16)) {
@@ -1986,6 +2529,7 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
     const uint64_t x1 = __shfl(used, 1), e0 = __shfl(ex, 0), ce0 = __shfl(ce, 0);
     const uint64_t cs0 = ts;
     if (x1 != kNoPos && e0 != x1 && cs0 < len) {
+      if (stat && lane == 0) ++stat[5];
       const uint64_t from = X != kNoPos ? X + 1 : cs0;
       for (uint64_t b = from; b < ce0; b += 64) {
         const uint64_t q = b + lane;
@@ -2002,7 +2546,7 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
           const uint32_t l = (uint32_t)__builtin_ctzll(m);
           const uint64_t nq = __shfl(q, l);
           const uint32_t nc = (uint32_t)__shfl((uint64_t)qc, l);
-          for (uint32_t qq = 0; qq < nsp; ++qq) {
+          QFOR(qq) {
             const uint64_t v = __shfl(ok ? qs[qq] : 0, l);
             if (lane == 0) sums[qq] = v;
           }
@@ -2020,7 +2564,8 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
     }
   }
   if (X != kNoPos && !(dbg & 32))
-    resolve_tile_sp<NS>(P, rd, len, w, cs, ce, lane, X, sp, used, ex, cnt, sums, term_at);
+    resolve_tile_sp<NS>(P, rd, len, w, cs, ce, lane, X, sp, used, ex, cnt, sums, term_at, stat);
+  if (stat && used != used0) ++stat[4];
   return X;
 }
 
@@ -2035,6 +2580,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t t = (uint64_t)blockIdx.x * kDecWaves + wv;
   if (t >= TB.ntiles || !vec_live(c)) return;  // wave-uniform
+  nt_prologue<NS>(a, lane);
   const uint32_t w = c->w;
   const uint64_t len = a.wire_len, p0 = c->p0;
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
@@ -2046,21 +2592,29 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
   const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
   const bool rng = reinterpret_cast<const FCtl *>(ws + kWsFCtl)->range != 0;
   TileLane<NS> st;
+  uint32_t stat[6] = {0, 0, 0, 0, 0, 0};
   const uint64_t X = tile_spec_resolve<NS>(P, rd, len, w, ts, wend, cs, ce, lane, t == 0 && !rng,
-                                           p0, dbg, st);
+                                           p0, dbg, st, (dbg & 4096) ? stat : nullptr);
+  if (dbg & 4096) {  // K1 statistics (scripts/diag_tiles.py)
+    FCtl *fcd = reinterpret_cast<FCtl *>(const_cast<uint8_t *>(ws) + kWsFCtl);
+    for (uint32_t k = 0; k < 6; ++k) {
+      const uint64_t v = wave_sum_u64(stat[k]);
+      if (lane == 0) atomicAdd(&fcd->diag[k], (unsigned long long)v);
+    }
+  }
   uint64_t &used = st.used, &ex = st.ex;
   uint32_t &cnt = st.cnt;
   uint64_t *sums = st.sums;
   uint64_t tcnt = wave_sum_u64(cnt), tsum[NS > 0 ? NS : kVS];
-  for (uint32_t q = 0; q < nsp; ++q) tsum[q] = wave_sum_u64(sums[q]);
+  QFOR(q) tsum[q] = wave_sum_u64(sums[q]);
   // ---- 3. entry alternatives (tile 0's entry is exact) ----
   uint32_t nalt = X != kNoPos ? 1u : 0u;
   uint64_t alt_e = kNoPos, alt_c = 0, alt_s[NS > 0 ? NS : kVS];  // lane a holds alt a
-  for (uint32_t q = 0; q < nsp; ++q) alt_s[q] = 0;
+  QFOR(q) alt_s[q] = 0;
   if (lane == 0 && nalt) {
     alt_e = X;
     alt_c = tcnt;
-    for (uint32_t q = 0; q < nsp; ++q) alt_s[q] = tsum[q];
+    QFOR(q) alt_s[q] = tsum[q];
   }
   if ((dbg & 4) && t > 0) {
     // ---- 3a. entry alternatives: other start candidates in chunk 0 after X
@@ -2068,7 +2622,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
     const uint64_t e0 = __shfl(ex, 0), ce0 = __shfl(ce, 0);
     const uint32_t c0 = __shfl(cnt, 0);
     uint64_t s0[NS > 0 ? NS : kVS];
-    for (uint32_t q = 0; q < nsp; ++q) s0[q] = __shfl(sums[q], 0);
+    QFOR(q) s0[q] = __shfl(sums[q], 0);
     const uint64_t lim = e0 < ce0 ? e0 : ce0;
     for (uint64_t b = X + 1; nalt && nalt < kAlt && b < lim && b < X + 1 + 128; b += 64) {
       const uint64_t q = b + lane;
@@ -2090,7 +2644,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
           alt_e = ae;
           alt_c = ac;
         }
-        for (uint32_t qq = 0; qq < nsp; ++qq) {
+        QFOR(qq) {
           const uint64_t v = tsum[qq] - s0[qq] + __shfl(ok ? qs[qq] : 0, l);
           if (lane == nalt) alt_s[qq] = v;
         }
@@ -2103,7 +2657,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
   TB.cused[g] = used;
   TB.cex[g] = ex;
   TB.ccnt[g] = cnt;
-  for (uint32_t q = 0; q < nsp; ++q) TB.csum[(uint64_t)q * TB.nchunks + g] = sums[q];
+  QFOR(q) TB.csum[(uint64_t)q * TB.nchunks + g] = sums[q];
   uint64_t *fn = TB.fn + t * kFnWords;
   const uint64_t y63 = __shfl(ex, 63);
   if (lane == 0) {
@@ -2114,7 +2668,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
     uint64_t *al = fn + 2 + lane * kAltWords;
     al[0] = lane < nalt ? alt_e : kNoPos;
     al[1] = alt_c;
-    for (uint32_t q = 0; q < nsp; ++q) al[2 + q] = alt_s[q];
+    QFOR(q) al[2 + q] = alt_s[q];
   }
 }
 
@@ -2138,7 +2692,7 @@ __device__ __forceinline__ void tile_pass_through(const TileBufs &TB, uint64_t t
   fn[1] = 1;
   fn[2] = T;
   fn[3] = 0;
-  for (uint32_t q = 0; q < nsp; ++q) fn[4 + q] = 0;
+  QFORV(q) fn[4 + q] = 0;
   TB.sel[t] = 0;
 }
 
@@ -2207,6 +2761,8 @@ __global__ __launch_bounds__(64) void vec_tile_repair(DecArgs a, WalkProg P,
   const uint32_t lane = threadIdx.x;
   if (!vec_live(c)) return;
   const uint64_t nl = fc->nlist[pass];
+  if (!nl) return;
+  nt_prologue<NS>(a, lane);
   const uint32_t w = c->w;
   const uint64_t len = a.wire_len, p0 = c->p0;
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
@@ -2231,22 +2787,22 @@ __global__ __launch_bounds__(64) void vec_tile_repair(DecArgs a, WalkProg P,
     uint64_t used = TB.cused[g], ex = TB.cex[g], term_at = kTermPos;
     uint32_t cnt = TB.ccnt[g];
     uint64_t sums[NS > 0 ? NS : kVS];
-    for (uint32_t q = 0; q < nsp; ++q) sums[q] = TB.csum[(uint64_t)q * TB.nchunks + g];
+    QFOR(q) sums[q] = TB.csum[(uint64_t)q * TB.nchunks + g];
     resolve_tile<NS>(P, tv.rd, len, w, ce, lane, T, used, ex, cnt, sums, term_at);
     const uint64_t tcnt = wave_sum_u64(cnt);
     uint64_t tsum[NS > 0 ? NS : kVS];
-    for (uint32_t q = 0; q < nsp; ++q) tsum[q] = wave_sum_u64(sums[q]);
+    QFOR(q) tsum[q] = wave_sum_u64(sums[q]);
     TB.cused[g] = used;
     TB.cex[g] = ex;
     TB.ccnt[g] = cnt;
-    for (uint32_t q = 0; q < nsp; ++q) TB.csum[(uint64_t)q * TB.nchunks + g] = sums[q];
+    QFOR(q) TB.csum[(uint64_t)q * TB.nchunks + g] = sums[q];
     const uint64_t y63 = __shfl(ex, 63);
     if (lane == 0) {
       fn[0] = y63;
       fn[1] = 1;
       fn[2] = T;
       fn[3] = tcnt;
-      for (uint32_t q = 0; q < nsp; ++q) fn[4 + q] = tsum[q];
+      QFOR(q) fn[4 + q] = tsum[q];
       TB.sel[t] = 0;
     }
     tile_jump(TB, p0, t, y63, nsp, lane, &fc->broken[pass]);
@@ -2272,6 +2828,7 @@ __global__ __launch_bounds__(64) void vec_tile_seqfix(DecArgs a, WalkProg P,
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
   const uint32_t lane = threadIdx.x;
   if (!vec_live(c) || !fc->broken[last_pass]) return;
+  nt_prologue<NS>(a, lane);
   const uint32_t w = c->w;
   const uint64_t len = a.wire_len, p0 = c->p0;
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
@@ -2310,15 +2867,15 @@ __global__ __launch_bounds__(64) void vec_tile_seqfix(DecArgs a, WalkProg P,
       uint64_t used = TB.cused[g], ex = TB.cex[g], term_at = kTermPos;
       uint32_t cnt = TB.ccnt[g];
       uint64_t sums[NS > 0 ? NS : kVS];
-      for (uint32_t q = 0; q < nsp; ++q) sums[q] = TB.csum[(uint64_t)q * TB.nchunks + g];
+      QFOR(q) sums[q] = TB.csum[(uint64_t)q * TB.nchunks + g];
       resolve_tile<NS>(P, tv.rd, len, w, ce, lane, T, used, ex, cnt, sums, term_at);
       const uint64_t tcnt = wave_sum_u64(cnt);
       uint64_t tsum[NS > 0 ? NS : kVS];
-      for (uint32_t q = 0; q < nsp; ++q) tsum[q] = wave_sum_u64(sums[q]);
+      QFOR(q) tsum[q] = wave_sum_u64(sums[q]);
       TB.cused[g] = used;
       TB.cex[g] = ex;
       TB.ccnt[g] = cnt;
-      for (uint32_t q = 0; q < nsp; ++q) TB.csum[(uint64_t)q * TB.nchunks + g] = sums[q];
+      QFOR(q) TB.csum[(uint64_t)q * TB.nchunks + g] = sums[q];
       const uint64_t y63 = __shfl(ex, 63);
       if (lane == 0) {
         uint64_t *fn = TB.fn + f * kFnWords;
@@ -2326,7 +2883,7 @@ __global__ __launch_bounds__(64) void vec_tile_seqfix(DecArgs a, WalkProg P,
         fn[1] = 1;
         fn[2] = T;
         fn[3] = tcnt;
-        for (uint32_t q = 0; q < nsp; ++q) fn[4 + q] = tsum[q];
+        QFOR(q) fn[4 + q] = tsum[q];
         TB.sel[f] = 0;
         fc->seq += 1;
       }
@@ -2351,7 +2908,7 @@ __global__ __launch_bounds__(256) void vec_tile_contrib(uint8_t *__restrict__ ws
   uint64_t cnt = 0, s[kVS] = {};
   if (sel >= 0) {
     cnt = fn[2 + sel * kAltWords + 1];
-    for (uint32_t q = 0; q < nsp; ++q) s[q] = fn[2 + sel * kAltWords + 2 + q];
+    QFORV(q) s[q] = fn[2 + sel * kAltWords + 2 + q];
     if (fn[0] == kTermPos) atomicMin(&fc->term_tile, (unsigned long long)t);
   } else if (sel == kSelTerm) {
     atomicMin(&fc->term_tile, (unsigned long long)t);
@@ -2359,7 +2916,7 @@ __global__ __launch_bounds__(256) void vec_tile_contrib(uint8_t *__restrict__ ws
     atomicAdd(&fc->unresolved, 1ull);  // never expected after the fix passes
   }
   TB.contrib[t] = cnt;
-  for (uint32_t q = 0; q < nsp; ++q) TB.contrib[(uint64_t)(1 + q) * TB.ntiles + t] = s[q];
+  QFORV(q) TB.contrib[(uint64_t)(1 + q) * TB.ntiles + t] = s[q];
 }
 
 // exclusive prefix sums of the 1 + nsp contribution columns over the tiles,
@@ -2480,6 +3037,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
   const uint64_t ts = p0 + t * kTileBytes;
   const uint64_t wb = ts + (uint64_t)part * kEmitBytes;  // this part's window
+  nt_prologue<NS>(a, lane);
   const TileView tv = stage_win<kEmitVec>(win_s[wv], wire, len, wb, w, lane);
   const WinReader &rd = tv.rd;
   if (dbg & 128) {
@@ -2501,13 +3059,13 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
   }
   const uint64_t pcnt = wave_sum_u64(cnt);  // records starting in this part
   uint64_t base = tbase, psum[kVS];
-  for (uint32_t q = 0; q < nsp; ++q) psum[q] = TB.contrib[(uint64_t)(1 + q) * TB.ntiles + t];
+  QFOR(q) psum[q] = TB.contrib[(uint64_t)(1 + q) * TB.ntiles + t];
   if (part > 0) {
     // everything from this part to the tile's end (chunk 0 is not among it)
     uint64_t rest = 0;
     for (uint32_t cc = ch; cc < 64; cc += kEmitChunks) rest += TB.ccnt[t * 64 + cc];
     base += alt[1] - wave_sum_u64(own ? rest : 0);
-    for (uint32_t q = 0; q < nsp; ++q) {
+    QFOR(q) {
       uint64_t rs = 0;
       for (uint32_t cc = ch; cc < 64; cc += kEmitChunks)
         rs += TB.csum[(uint64_t)q * TB.nchunks + t * 64 + cc];
@@ -2531,7 +3089,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
   }
   uint16_t *tab = tab_s[wv];
   uint64_t carry[NS > 0 ? NS : kVS];
-  for (uint32_t q = 0; q < nsp; ++q) carry[q] = psum[q];
+  QFOR(q) carry[q] = psum[q];
   const uint64_t nemit = (n - base < pcnt) ? n - base : pcnt;
   for (uint64_t pass0 = 0; pass0 < nemit; pass0 += kEmitTab) {
     const uint64_t pend = pass0 + kEmitTab < nemit ? pass0 + kEmitTab : nemit;
@@ -2559,18 +3117,22 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
       if (act) L = wlen_rd<NS>(P, rd, len, pos, w, rc);
       uint64_t off[kVS];
       bool fits = true;
-      for (uint32_t q = 0; q < nsp; ++q) {
+      QFOR(q) {
         uint64_t tot;
         off[q] = carry[q] + wave_excl_scan_u64(act ? rc[q] : 0, lane, &tot);
         carry[q] += tot;
         if (off[q] + rc[q] > a.heap_cap[q]) fits = false;
       }
       const uint64_t gr = base + pass0 + i;
-      if (act && gr < a.rec_cap && fits && !(dbg & 64))
-        emit_record_rd(a.L, rd, pos, w, recs + gr * a.L.stride, a.heaps, off, len, bq, dbg);
+      if (act && gr < a.rec_cap && fits && !(dbg & 64)) {
+        if constexpr (NS <= -2)
+          nt_emit(rd, pos, len, recs + gr * a.L.stride, off, bq);
+        else
+          emit_record_rd(a.L, rd, pos, w, recs + gr * a.L.stride, a.heaps, off, len, bq, dbg);
+      }
       if (act && gr == n - 1) {
         fc->end_pos = pos + L;
-        for (uint32_t q = 0; q < nsp; ++q) fc->htot[q] = off[q] + rc[q];
+        QFOR(q) fc->htot[q] = off[q] + rc[q];
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -2642,6 +3204,7 @@ __global__ void vec_shard_setn(uint8_t *__restrict__ ws, uint64_t first, uint32_
 // (no_buffer_space; invalid_buffer for an overlong varint where the path ends).
 __global__ void vec_tile_finish(DecArgs a, const uint8_t *__restrict__ wire,
                                 const uint8_t *__restrict__ ws, spk_dresult_t *res) {
+  if (a.nested) nt_stage_wave(a.nl, threadIdx.x);  // (launched with one wave)
   if (threadIdx.x != 0) return;
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   const FCtl *fc = reinterpret_cast<const FCtl *>(ws + kWsFCtl);
@@ -2671,7 +3234,13 @@ __global__ void vec_tile_finish(DecArgs a, const uint8_t *__restrict__ wire,
   }
   if (c->n && total < c->n) {
     r.errc = SPK_ERRC_NO_BUFFER_SPACE;
-    if (a.L.n_var && fc->term_pos < a.wire_len) {
+    if (a.nested && fc->term_pos < a.wire_len) {
+      // the errc of the record the path fails at (the exact walk, no quick exits)
+      uint64_t p = fc->term_pos;
+      const GReader g{wire, c->w};
+      const int32_t ec = nt_read<false>(nt_lds(), g, p, a.wire_len, false, nullptr, nullptr, false);
+      if (ec) r.errc = ec;
+    } else if (a.L.n_var && fc->term_pos < a.wire_len) {
       int32_t ec = SPK_ERRC_NO_BUFFER_SPACE;
       rec_wire_len(a.L, wire, a.wire_len, fc->term_pos, c->w, &ec);
       if (ec == SPK_ERRC_INVALID_BUFFER) r.errc = ec;
@@ -2780,11 +3349,11 @@ __device__ __forceinline__ void fz_compose(const WalkProg &P, const WinReader &r
       const uint64_t y = tpass ? e : __shfl(st.ex, 63);
       const uint64_t tc = wave_sum_u64(tpass ? 0u : st.cnt);
       uint64_t tsq[NS > 0 ? NS : kVS];
-      for (uint32_t q = 0; q < nsp; ++q) tsq[q] = wave_sum_u64(tpass ? 0ull : st.sums[q]);
+      QFOR(q) tsq[q] = wave_sum_u64(tpass ? 0ull : st.sums[q]);
       if (lane == 0) {
         sh_y[k] = y;
         sh_c[k] = tc;
-        for (uint32_t q = 0; q < nsp; ++q) sh_s[k][q] = tsq[q];
+        QFOR(q) sh_s[k][q] = tsq[q];
       }
     }
     __syncthreads();
@@ -2843,7 +3412,7 @@ __global__ __launch_bounds__(64 * kFW) void vec_tile_fused(DecArgs a, WalkProg P
     if (lane == 0) {
       sh_e = b == 0 ? p0 : x0;
       sh_pc = 0;
-      for (uint32_t q = 0; q < nsp; ++q) sh_ps[q] = 0;
+      QFOR(q) sh_ps[q] = 0;
       sh_fail = 0;
     }
   } else if (wv == 0) {
@@ -2868,7 +3437,7 @@ __global__ __launch_bounds__(64 * kFW) void vec_tile_fused(DecArgs a, WalkProg P
         if (__builtin_amdgcn_readlane((int)stt, (int)kp) == 3) break;  // a predecessor gave up
         // inclusive lane kp: v = (Y, records, sums); aggregate lanes: (X, Y, records, sums)
         uint64_t y = readlane64(v[0], kp), c0 = readlane64(v[1], kp), s0[kVS];
-        for (uint32_t q = 0; q < nsp; ++q) s0[q] = readlane64(v[2 + q], kp);
+        QFOR(q) s0[q] = readlane64(v[2 + q], kp);
         bool ok = true;
         for (uint32_t l = kp + 1; l < 64 && ok; ++l) {
           if (y == kTermPos) continue;  // the path ended: the rest adds nothing
@@ -2880,13 +3449,13 @@ __global__ __launch_bounds__(64 * kFW) void vec_tile_fused(DecArgs a, WalkProg P
             break;
           }
           c0 += readlane64(v[2], l);
-          for (uint32_t q = 0; q < nsp; ++q) s0[q] += readlane64(v[3 + q], l);
+          QFOR(q) s0[q] += readlane64(v[3 + q], l);
           y = readlane64(v[1], l);
         }
         if (ok) {
           cur = y;
           pc = c0;
-          for (uint32_t q = 0; q < nsp; ++q) ps[q] = s0[q];
+          QFOR(q) ps[q] = s0[q];
           break;
         }
       }
@@ -2895,7 +3464,7 @@ __global__ __launch_bounds__(64 * kFW) void vec_tile_fused(DecArgs a, WalkProg P
     if (lane == 0) {
       sh_e = cur;
       sh_pc = pc;
-      for (uint32_t q = 0; q < nsp; ++q) sh_ps[q] = ps[q];
+      QFOR(q) sh_ps[q] = ps[q];
       sh_fail = cur == kFailPos ? 1u : 0u;
     }
   }
@@ -2922,7 +3491,7 @@ __global__ __launch_bounds__(64 * kFW) void vec_tile_fused(DecArgs a, WalkProg P
     uint64_t v = sh_pc;
     for (uint32_t k = 0; k < kFW; ++k) v += sh_c[k];
     fc->total = v;
-    for (uint32_t q = 0; q < nsp; ++q) {
+    QFOR(q) {
       uint64_t sv = sh_ps[q];
       for (uint32_t k = 0; k < kFW; ++k) sv += sh_s[k][q];
       fc->stot[q] = sv;
@@ -2931,10 +3500,10 @@ __global__ __launch_bounds__(64 * kFW) void vec_tile_fused(DecArgs a, WalkProg P
   // ---- 5. emission of this wave's tile ----
   const uint64_t n = c->n;
   uint64_t base = sh_pc, carry[NS > 0 ? NS : kVS];
-  for (uint32_t q = 0; q < nsp; ++q) carry[q] = sh_ps[q];
+  QFOR(q) carry[q] = sh_ps[q];
   for (uint32_t k = 0; k < wv; ++k) {
     base += sh_c[k];
-    for (uint32_t q = 0; q < nsp; ++q) carry[q] += sh_s[k][q];
+    QFOR(q) carry[q] += sh_s[k][q];
   }
   const uint32_t cnt = st.cnt;
   const uint64_t used = st.used;
@@ -2981,7 +3550,7 @@ __global__ __launch_bounds__(64 * kFW) void vec_tile_fused(DecArgs a, WalkProg P
       if (act) L = wlen_rd<NS>(P, rd, len, pos, w, rc);
       uint64_t off[kVS];
       bool fits = true;
-      for (uint32_t q = 0; q < nsp; ++q) {
+      QFOR(q) {
         uint64_t tot;
         off[q] = carry[q] + wave_excl_scan_u64(act ? rc[q] : 0, lane, &tot);
         carry[q] += tot;
@@ -2992,7 +3561,7 @@ __global__ __launch_bounds__(64 * kFW) void vec_tile_fused(DecArgs a, WalkProg P
         emit_record_rd(a.L, rd, pos, w, recs + gr * a.L.stride, a.heaps, off, len, bq);
       if (act && gr == n - 1) {
         fc->end_pos = pos + L;
-        for (uint32_t q = 0; q < nsp; ++q) fc->htot[q] = off[q] + rc[q];
+        QFOR(q) fc->htot[q] = off[q] + rc[q];
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -3011,14 +3580,12 @@ static unsigned grid_for(uint64_t items, uint64_t per_block) {
 
 // ---- tile decoder: workspace and launch ---------------------------------------
 struct TileWs {
-  size_t fn, cused, cex, ccnt, csum, sel, contrib, scan, blist, jobs, agg, end;
+  size_t fn, cused, cex, ccnt, csum, sel, contrib, scan, blist, jobs, agg, nl, end;
   uint64_t ntiles, nchunks, nsb, nblk;
 };
-static TileWs tile_ws_layout(const spk_layout *L, uint64_t wire_len) {
+// ns: span counts per record (flat: SPAN + OPTION members; nested: heaps)
+static TileWs tile_ws_layout(uint32_t ns, uint64_t wire_len) {
   TileWs f = {};
-  uint32_t ns = 0;
-  for (uint32_t i = 0; i < L->n_ops; ++i)
-    ns += L->ops[i].kind == SPK_OP_SPAN || L->ops[i].kind == SPK_OP_OPTION;
   if (!ns) ns = 1;
   f.ntiles = wire_len / kTileBytes + 1;  // the payload starts past the header
   f.nchunks = f.ntiles * 64;
@@ -3041,6 +3608,7 @@ static TileWs tile_ws_layout(const spk_layout *L, uint64_t wire_len) {
   f.jobs = take(big_jobs_cap(wire_len) * sizeof(BigJob));
   f.nblk = (f.ntiles + kFW - 1) / kFW;
   f.agg = take(2 * f.nblk * kAggWords * 8 + 64);  // fused decode: aggregates, inclusive, ids
+  f.nl = take(sizeof(NTLayout));                  // nested layouts: the walker's layout
   f.end = off;
   return f;
 }
@@ -3080,7 +3648,7 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
                                       const uint8_t *wire, uint8_t *ws, spk_dresult_t *d_res,
                                       uint8_t *d_recs, hipStream_t s, int phase = kTilesAll,
                                       const ShardCall &sc = ShardCall{}) {
-  TileWs f = tile_ws_layout(L, a.wire_len);
+  TileWs f = tile_ws_layout(P.ns, a.wire_len);
   if (phase != kTilesAll) f.ntiles = sc.ntiles < f.ntiles ? sc.ntiles : f.ntiles;
   TileBufs TB;
   TB.fn = reinterpret_cast<uint64_t *>(ws + f.fn);
@@ -3107,7 +3675,7 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
     }
     return hipGetLastError();
   }
-  if (phase == kTilesAll && tile_fused()) {
+  if (NS > -2 && phase == kTilesAll && tile_fused()) {
     FusedBufs FB;
     FB.nblk = f.nblk;
     FB.aw = reinterpret_cast<uint64_t *>(ws + f.agg);
@@ -3120,8 +3688,8 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
     SPK_LAUNCH(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, 0u, (uint64_t)0);
     hipError_t e = hipMemsetAsync(ws + f.agg, 0, 2 * f.nblk * kAggWords * 8 + 64, s);
     if (e != hipSuccess) return e;
-    SPK_LAUNCH(vec_tile_fused<NS>, dim3((unsigned)f.nblk), dim3(64 * kFW), 0, s, a, P, wire, ws,
-               FB, d_recs, bq, tile_dbg());
+    SPK_LAUNCH(vec_tile_fused<NS <= -2 ? 0 : NS>, dim3((unsigned)f.nblk), dim3(64 * kFW), 0, s, a,
+               P, wire, ws, FB, d_recs, bq, tile_dbg());
     if (P.ns) {
       const uint64_t gb = bq.cap < 2048 ? bq.cap : 2048;
       SPK_LAUNCH(vec_big_copy, dim3((unsigned)gb), dim3(256), 0, s, wire, (const uint8_t *)ws, bq);
@@ -3197,11 +3765,115 @@ hipError_t launch_var_shard(const spk_layout *L, int phase, const void *d_wire, 
   return launch_vec_tiles_ns<0>(a, P, L, wire, ws, d_res, r, s, ph, sc);
 }
 
+
+// ---- nested layouts on the tile decoder -------------------------------------------
+static NTLayout make_ntlayout(const NLayout &N, void *const *heaps) {
+  NTLayout t = {};
+  for (uint32_t i = 0; i < N.n_ops; ++i) {
+    t.ops[i] = N.ops[i];
+    t.heap[i] = N.heap[i];
+    t.end[i] = N.end[i];
+    if (N.ops[i].kind == SPK_OP_VARIANT || N.ops[i].kind == SPK_OP_OPTGROUP) t.groups = 1;
+  }
+  t.n_ops = N.n_ops;
+  t.n_heaps = N.n_heaps;
+  t.fv_cnt = N.fv_cnt;
+  t.fv_has64 = N.fv_has64;
+  t.fv_bits = N.fv_bits;
+  for (uint32_t k = 0; k < N.n_heaps && k < kVS; ++k) t.heaps[k] = (uint8_t *)heaps[k];
+  // the walk program, when every op is COPY / SPAN / OPTION / ARRAY (+ END)
+  uint32_t n = 0, open[SPK_MAX_DEPTH + 1], d = 0;
+  bool ok = !N.fv_cnt;
+  for (uint32_t i = 0; i < N.n_ops && ok; ++i) {
+    const spk_op &op = N.ops[i];
+    if (op.kind == SPK_OP_COPY) {
+      if (n && (t.wp[n - 1] & 7u) == WP_SKIP && (t.wp[n - 1] >> 8) + op.size < (1u << 24))
+        t.wp[n - 1] += op.size << 8;
+      else
+        t.wp[n++] = WP_SKIP | (op.size << 8);
+    } else if (op.kind == SPK_OP_SPAN || op.kind == SPK_OP_OPTION) {
+      t.wp[n++] = (op.kind == SPK_OP_SPAN ? WP_SPAN : WP_OPT) | ((uint32_t)N.heap[i] << 3) |
+                  ((op.size ? op.size : 1u) << 8);
+    } else if (op.kind == SPK_OP_ARRAY && d < SPK_MAX_DEPTH) {
+      open[d++] = n;
+      t.wp[n++] = WP_ARR | ((uint32_t)N.heap[i] << 3);
+    } else if (op.kind == SPK_OP_END && d) {
+      t.wp[n++] = WP_END;
+      t.wp[open[--d]] |= n << 8;  // the loop's exit
+    } else {
+      ok = false;
+    }
+  }
+  t.wp_n = ok && !d ? n : 0;
+  return t;
+}
+// the tile pipeline's walk program for a nested layout: heap use as the span
+// sums; candidate starts screened on the first count (NLayout::scr_off)
+static WalkProg make_walkprog_nested(const NLayout &N) {
+  WalkProg p = {};
+  p.ns = N.n_heaps;
+  if (N.scr_off != ~0u) {
+    p.skip[0] = N.scr_off;
+    p.c0max = kPlaus > N.scr_off ? (kPlaus - N.scr_off) / (N.scr_esz ? N.scr_esz : 1) : 0;
+  } else {
+    p.pf_all = 1;
+  }
+  p.rounds = kRounds;
+  return p;
+}
+__global__ void nt_put(NTLayout t, uint8_t *dst) {
+  const uint32_t *src = reinterpret_cast<const uint32_t *>(&t);
+  for (uint32_t k = threadIdx.x; k < sizeof(NTLayout) / 4; k += blockDim.x)
+    reinterpret_cast<uint32_t *>(dst)[k] = src[k];
+}
+
+bool var_nested_tile_ok(const spk_layout *L) {
+  const NLayout N = make_nlayout(L);
+  return !N.n_ranks && N.n_heaps <= kVS;
+}
+size_t var_nested_tile_ws_bytes(const spk_layout *L, uint64_t wire_len) {
+  return tile_ws_layout(make_nlayout(L).n_heaps, wire_len).end + 256;
+}
+
+hipError_t launch_var_nested_decode(const spk_layout *L, const void *d_wire, uint64_t wire_len,
+                                    void *d_recs, uint64_t rec_cap, void *const *d_heaps,
+                                    const uint64_t *heap_caps, spk_dresult_t *d_res, void *d_ws,
+                                    hipStream_t s, uint32_t body_w, uint64_t body_n) {
+  const NLayout N = make_nlayout(L);
+  DecArgs a = {};
+  a.L.stride = N.stride;
+  a.L.n_spans = N.n_heaps;
+  a.L.n_var = 1;  // (no minimum-record-size screen in the header kernel)
+  a.fmt = L->fmt_vector;
+  a.wire_len = wire_len;
+  a.rec_cap = rec_cap;
+  a.body_w = body_w;
+  a.body_n = body_n;
+  for (uint32_t k = 0; k < N.n_heaps && k < kVS; ++k) {
+    a.heaps[k] = (uint8_t *)d_heaps[k];
+    a.heap_cap[k] = heap_caps[k];
+  }
+  a.nested = 1;
+  const WalkProg P = make_walkprog_nested(N);
+  uint8_t *ws = (uint8_t *)d_ws;
+  const TileWs f = tile_ws_layout(P.ns, wire_len);
+  a.nl = ws + f.nl;
+  SPK_LAUNCH(nt_put, dim3(1), dim3(256), 0, s, make_ntlayout(N, d_heaps), ws + f.nl);
+  // NS = -3: every walk runs the walk program; -2: the interpreter
+  const NTLayout t = make_ntlayout(N, d_heaps);
+  if (t.wp_n)
+    return launch_vec_tiles_ns<-3>(a, P, L, (const uint8_t *)d_wire, ws, d_res, (uint8_t *)d_recs, s);
+  return launch_vec_tiles_ns<-2>(a, P, L, (const uint8_t *)d_wire, ws, d_res, (uint8_t *)d_recs, s);
+}
+
 size_t var_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len) {
   size_t enc = kWsScratch + (grid_for(n, kPlanRPB) + 1) * sizeof(Partial) + 256;
   size_t dec_msg = kWsScratch + n * sizeof(MsgState) +
                    (grid_for(n, kThreads) + 1) * kBs * 8 + 256;
-  const size_t dec_vec = tile_ws_layout(L, wire_len).end + 256;
+  uint32_t ns = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i)
+    ns += L->ops[i].kind == SPK_OP_SPAN || L->ops[i].kind == SPK_OP_OPTION;
+  const size_t dec_vec = tile_ws_layout(ns, wire_len).end + 256;
   size_t m = enc;
   if (mode == SPK_MODE_MESSAGES) m = m > dec_msg ? m : dec_msg;
   if (mode == SPK_MODE_VECTOR) m = m > dec_vec ? m : dec_vec;
