@@ -342,7 +342,9 @@ int spk_plan(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
  * independent serialize_to calls for SPK_MODE_MESSAGES (then
  * d_msg_offsets[0..n] receives the message boundaries; nullable).
  * `d_heaps` is a HOST array of n_span DEVICE pointers. `d_plan` must come
- * from spk_plan on the same records (stream-ordered). Writes at most
+ * from spk_plan on the same records (stream-ordered), run on the same
+ * workspace: the write pass reads the size pass's partials (or, for layouts
+ * with element records, its per-record offsets) from it. Writes at most
  * out_cap bytes; if the plan exceeds out_cap nothing is written and
  * d_plan->total_bytes tells the caller the size needed. */
 int spk_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,

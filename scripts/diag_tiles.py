@@ -37,7 +37,7 @@ def main():
     diag = words[34:42]
     ntiles = (out.numel() + 16383) // 16384
     names = ["round-lanes (x64)", "re-walks", "spec walks", "spec off-grid", "wrong spec lanes",
-             "chunk0 cross-checks"]
+             "chunk0 cross-checks", "max tile cycles", "sum tile cycles"]
     print(f"{case} n={n} wire={out.numel() / 1e6:.1f} MB tiles={ntiles} errc={res.errc} "
           f"repaired={res.tiles_repaired} sequential={res.tiles_sequential}")
     for k, nm in enumerate(names):

@@ -616,12 +616,17 @@ def test_decode_body_chunks(case, n, param):
 
 @pytest.mark.parametrize("case,n,param,world", [("outer", 200000, 16, 4), ("recs", 300000, 48, 3),
                                                 ("var", 100000, 16, 5), ("opt", 50000, 40, 2),
-                                                ("recs", 5, 48, 4), ("mixed", 30000, 30, 3)])
+                                                ("recs", 5, 48, 4), ("mixed", 30000, 30, 3),
+                                                ("monster", 100000, 20, 4), ("tags", 100000, 6, 3),
+                                                ("vnt", 50000, 8, 3), ("rect2", 200000, 0, 3),
+                                                ("group", 300, 300, 4)])
 def test_sharded_decode_simulated(case, n, param, world):
     """spk_decode_shard_index / _emit with `world` ranks simulated in one
     process (one workspace each): the ranks' records re-encoded at the
     message width and concatenated are the message body, byte for byte, and
-    the first-record indices tile [0, n)."""
+    the first-record indices tile [0, n). Nested layouts (monster, tags:
+    the walk program; vnt, rect2: the interpreter walker; group: records
+    longer than a speculative walk's reach) shard on the same tiles."""
     from yalantinglibs_amd import layout as LY
     from yalantinglibs_amd import parallel as PAR
     cds = [SP.Codec(LY.case_layout(case)) for _ in range(world)]

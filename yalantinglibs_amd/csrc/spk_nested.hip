@@ -1066,16 +1066,34 @@ struct NEnc {
 
 // a[0][i] = payload bytes, a[1][i] = count fields (VECTOR) or the whole
 // message size (MESSAGES); the longest container into ctl->maxc
+// the block's records staged in LDS with coalesced 16-B loads when they fit:
+// the interpreter's reads of one record's count fields are dependent (one
+// load per op), so from LDS they cost LDS latencies, not HBM ones
+constexpr uint32_t kNSizeStage = 28 * 1024;
 template <int D>
 __global__ __launch_bounds__(256) void nest_size(NEnc e, const uint8_t *__restrict__ recs,
                                                  uint64_t *__restrict__ a, uint8_t *ws) {
   __shared__ NLayout N;
+  __shared__ __align__(16) uint8_t rs[kNSizeStage];
   n_stage(N, e.N);
   NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t r0 = (uint64_t)blockIdx.x * blockDim.x;
+  const uint64_t nb = r0 < e.n ? (e.n - r0 < blockDim.x ? e.n - r0 : blockDim.x) : 0;
+  const uint64_t bytes = nb * N.stride;
+  // (device records are 8-aligned, their stride a multiple of 8)
+  const bool staged = (uint64_t)blockDim.x * N.stride <= kNSizeStage && !(N.stride & 7) &&
+                      !((uintptr_t)recs & 7);
+  if (staged) {
+    const uint64_t *src = reinterpret_cast<const uint64_t *>(recs + r0 * N.stride);
+    uint64_t *dst = reinterpret_cast<uint64_t *>(rs);
+    for (uint64_t k = threadIdx.x; k < bytes / 8; k += blockDim.x) dst[k] = src[k];
+    __syncthreads();
+  }
   uint64_t m = 0;
   if (i < e.n) {
-    const NSize s = n_size<D>(N, recs + i * N.stride, e.heaps, 0, N.n_ops, true);
+    const uint8_t *rec = staged ? rs + (i - r0) * N.stride : recs + i * N.stride;
+    const NSize s = n_size<D>(N, rec, e.heaps, 0, N.n_ops, true);
     m = s.maxc;
     if (e.mode == SPK_MODE_MESSAGES) {
       const uint32_t w = width_of(s.maxc);
@@ -1366,15 +1384,23 @@ hipError_t launch_nested_encode(const spk_layout *L, int mode, uint64_t n, const
   }
   uint8_t *ws = (uint8_t *)d_ws;
   uint64_t *a, *part, nb;
-  hipError_t er = nest_size_scan(e, d_recs, ws, s, &a, &part, &nb);
-  if (er != hipSuccess) return er;
   if (mode == SPK_MODE_VECTOR && !e.N.n_ranks && !fixed_w && !nest_direct_write()) {
+    // the plan that precedes this call on the workspace (spk_encode's
+    // contract, as for the flat layouts) left every record's offset in column
+    // 0, the totals in the partials and the longest container in the control
+    // block: the write pass alone
+    const NWs f = nws_layout(e.n, e.N.n_heaps, e.N.n_ranks);
+    a = reinterpret_cast<uint64_t *>(ws + f.a);
+    part = reinterpret_cast<uint64_t *>(ws + f.part);
+    nb = (e.n + kNScanBlk - 1) / kNScanBlk;
     NEST_D(n_dclass(e.N),
            SPK_LAUNCH(nest_write_win<D>, dim3(nblocks(n, 256)), dim3(256), 0, s, e,
                       (const uint8_t *)d_recs, (const uint64_t *)a, (const uint64_t *)part, nb, ws,
                       (uint8_t *)d_out, out_cap));
     return hipGetLastError();
   }
+  hipError_t er = nest_size_scan(e, d_recs, ws, s, &a, &part, &nb);
+  if (er != hipSuccess) return er;
   NEST_D(n_dclass(e.N),
          SPK_LAUNCH(nest_write<D>, dim3(nblocks(n, 256)), dim3(256), 0, s, e,
                     (const uint8_t *)d_recs, (const uint64_t *)a, (const uint64_t *)part, nb, ws,

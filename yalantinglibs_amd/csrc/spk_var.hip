@@ -48,6 +48,18 @@
 #ifndef SPK_ESPLIT
 #define SPK_ESPLIT 2
 #endif
+#ifndef SPK_K4_LANE   // (A/B) flat K4: one lane per chunk emits its records in order
+#define SPK_K4_LANE 0
+#endif
+#ifndef SPK_NT_REACH  // bytes K1's resolution walks of nested records may cover
+#define SPK_NT_REACH 4096
+#endif
+#ifndef SPK_NT_PAST   // records a nested speculative walk checks past its chunk
+#define SPK_NT_PAST 2
+#endif
+#ifndef SPK_NT_SCR2   // nested candidate starts screened on a second count
+#define SPK_NT_SCR2 1
+#endif
 
 namespace spk {
 
@@ -1162,6 +1174,9 @@ struct WalkProg {
   uint64_t cmax[kVS];    // largest count whose byte size fits 64 bits
   uint32_t optm;                   // bit k: span k is an OPTION ([has_value:1][U?])
   uint32_t pf_all;                 // no first-count screening of candidate starts
+  // nested layouts whose first SPAN (esz0) is followed, after s2skip fixed
+  // bytes, by another count: that count must be <= c1max too (scr2)
+  uint32_t scr2, esz0, s2skip, c1max;
   uint32_t pf_var;                 // screening past segment 0's varints (NS = -1 walks)
   uint32_t rounds;                 // parallel re-verification rounds before the fixup
   uint32_t nv;                     // varint members
@@ -1246,7 +1261,15 @@ __device__ __forceinline__ bool vi_seg_rd(const WalkProg &P, uint32_t k, const R
 // the nested walker (NS = -2, defined with the tile decoder below)
 template <bool SIMPLE, typename Rd>
 __device__ uint64_t nt_len(const Rd &rd, uint64_t len, uint64_t pos, uint64_t *cnt,
-                           uint64_t reach);
+                           uint64_t reach, uint32_t maxel);
+// a bounded nested walk gave up (its reach or element limit): length unknown
+constexpr uint64_t kLenLimit = ~0ull - 8;
+// K1's walks of nested records stop this far past their start: a walk from
+// a wrong entry could otherwise iterate far into the wire one element at a
+// time; a tile whose true path needs more is resolved again by the repair
+// passes, whose walks are unbounded
+template <int NS>
+constexpr uint64_t kK1Reach = NS <= -2 ? (uint64_t)SPK_NT_REACH : 0;
 
 // Wire length of the record at `pos` (0 = incomplete: the reference fails it
 // with no_buffer_space). NS > 0: compile-time span count; 0: runtime count;
@@ -1285,8 +1308,9 @@ __device__ __forceinline__ uint64_t wlen(const WalkProg &P, const uint8_t *wire,
 // wlen() with the count fields read through `rd`
 template <int NS, typename Rd>
 __device__ __forceinline__ uint64_t wlen_rd(const WalkProg &P, const Rd &rd, uint64_t len,
-                                            uint64_t pos, uint32_t w, uint64_t *cnt = nullptr) {
-  if constexpr (NS <= -2) return nt_len<NS == -3>(rd, len, pos, cnt, 0);
+                                            uint64_t pos, uint32_t w, uint64_t *cnt = nullptr,
+                                            uint64_t reach = 0) {
+  if constexpr (NS <= -2) return nt_len<NS == -3>(rd, len, pos, cnt, reach, ~0u);
   uint64_t p = pos + P.skip[0];
   const uint32_t ns = NS > 0 ? (uint32_t)NS : P.ns;
   if (NS < 0 && !vi_seg_rd(P, 0, rd, len, p)) return 0;
@@ -1584,14 +1608,15 @@ struct NTLayout {
   uint32_t n_ops, n_heaps, fv_cnt, fv_has64, fv_bits;
   uint32_t groups;            // a VARIANT / OPTGROUP op: errors inside may be dropped
   uint32_t wp_n;              // walk program length (0: walks run nt_read)
-  uint32_t pad_;
+  uint32_t wp_tail;           // fixed bytes after the last instruction
   uint8_t *heaps[kVS];
-  // walk program of a layout of COPY / SPAN / OPTION / ARRAY ops only: one
-  // u32 per instruction, op | heap << 3 | arg << 8 (WP_*), consecutive COPYs
-  // merged; record lengths and heap use without the interpreter's bookkeeping
-  uint32_t wp[SPK_MAX_OPS];
+  // walk program of a layout of COPY / SPAN / OPTION / ARRAY ops only: per
+  // instruction x = op | heap << 3 | arg << 8 (WP_*; arg: element size, or
+  // an ARRAY's exit), y = the fixed bytes (COPYs) before it; record lengths
+  // and heap use without the interpreter's bookkeeping
+  uint2 wp[SPK_MAX_OPS];
 };
-constexpr uint32_t WP_SKIP = 1, WP_SPAN = 2, WP_OPT = 3, WP_ARR = 4, WP_END = 5;
+constexpr uint32_t WP_SPAN = 1, WP_OPT = 2, WP_ARR = 3, WP_END = 4;
 static_assert(sizeof(NTLayout) % 16 == 0, "NTLayout staged as 16-B words");
 static_assert(SPK_MAX_DEPTH == 4, "the walker's element stack has 4 register frames");
 
@@ -1707,7 +1732,8 @@ __device__ __forceinline__ int32_t nt_fv_read(const NTLayout &N, const Rd &rd, u
 // a failing record is taken with quick = false).
 template <bool EMIT, typename Rd>
 __device__ int32_t nt_read(const NTLayout &N, const Rd &rd, uint64_t &pos, uint64_t lim,
-                           bool bounded, uint8_t *rec, const BigQ *bq, bool quick) {
+                           bool bounded, uint8_t *rec, const BigQ *bq, bool quick,
+                           uint32_t maxel = ~0u) {
   uint32_t *const U = nt_used();  // U[64 * k]: heap k
   const uint32_t w = rd.w;
   // top frame: aop | pend << 8 | first << 16 | ret << 24, element index and
@@ -1879,7 +1905,7 @@ __device__ int32_t nt_read(const NTLayout &N, const Rd &rd, uint64_t &pos, uint6
     }
     if (kind == SPK_OP_ARRAY) {
       // an element takes at least one wire byte
-      if (bounded && cnt > kNTSpecElems) return kNTLimit;
+      if (bounded && cnt > maxel) return kNTLimit;
       if (cnt > lim - pos) {
         if (bounded) return kNTLimit;
         if (quick && !N.groups) {
@@ -1963,20 +1989,21 @@ __device__ int32_t nt_read(const NTLayout &N, const Rd &rd, uint64_t &pos, uint6
 // could drop an error.
 template <typename Rd>
 __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint64_t lim,
-                            bool bounded) {
+                            bool bounded, uint32_t maxel) {
+  // a check that fails on a bounded walk's limit: unknown (the full wire may
+  // have held the record)
+  const uint64_t bad = bounded ? kLenLimit : 0;
   uint32_t *const U = nt_used();
   uint32_t *const F = nt_frames();
   const uint32_t w = rd.w;
   uint64_t p = pos;
   uint32_t pc = 0, d = 0, body = 0, rem = 0;  // top loop frame: body start, elements left
   while (pc < N.wp_n) {
-    const uint32_t ins = N.wp[pc];
-    const uint32_t op = ins & 7u, h = (ins >> 3) & 31u, arg = ins >> 8;
-    if (op == WP_SKIP) {
-      if (lim - p < arg) return 0;
-      p += arg;
-      ++pc;
-    } else if (op == WP_END) {
+    const uint2 ins = N.wp[pc];
+    const uint32_t op = ins.x & 7u, h = (ins.x >> 3) & 31u, arg = ins.x >> 8;
+    if (lim - p < ins.y) return bad;
+    p += ins.y;
+    if (op == WP_END) {
       if (--rem) {
         pc = body;
       } else {
@@ -1986,41 +2013,36 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
           rem = F[64 * (3 * (d - 1) + 1)];
         }
       }
-    } else if (op == WP_OPT) {  // [has_value:1][U if present]; an unreadable value leaves the reader
-      if (p >= lim) return 0;
-      const uint32_t b = rd.byte(p++);
-      if (b) {
-        if (lim - p >= arg) p += arg;
-        atomicAdd(U + 64 * h, 1u);
-      }
-      ++pc;
-    } else {  // WP_SPAN / WP_ARR: [count:w]
-      if (lim - p < w) return 0;
-      const uint64_t c = rd(p);
-      p += w;
-      if (op == WP_SPAN) {
-        if (c && c > (lim - p) / arg) return 0;
-        p += c * arg;
-        atomicAdd(U + 64 * h, (uint32_t)c);
-        ++pc;
-      } else {
-        if (c > lim - p || (bounded && c > kNTSpecElems)) return 0;  // elements take >= 1 byte
-        atomicAdd(U + 64 * h, (uint32_t)c);
-        if (!c) {
-          pc = arg;
-        } else {
-          if (d) {
-            F[64 * (3 * (d - 1))] = body;
-            F[64 * (3 * (d - 1) + 1)] = rem;
-          }
-          ++d;
-          body = ++pc;
-          rem = (uint32_t)c;
-        }
-      }
+      continue;
     }
+    const bool opt = op == WP_OPT;
+    const uint32_t cw = opt ? 1u : w;
+    if (lim - p < cw) return bad;
+    uint64_t c = opt ? (uint64_t)(rd.byte(p) != 0) : rd(p);
+    p += cw;
+    atomicAdd(U + 64 * h, (uint32_t)c);
+    if (op == WP_ARR) {
+      if (c > lim - p || c > maxel) return bad;  // elements take >= 1 byte
+      if (!c) {
+        pc = arg;
+      } else {
+        if (d) {
+          F[64 * (3 * (d - 1))] = body;
+          F[64 * (3 * (d - 1) + 1)] = rem;
+        }
+        ++d;
+        body = ++pc;
+        rem = (uint32_t)c;
+      }
+      continue;
+    }
+    // SPAN: the payload must be there; OPTION: an unreadable value leaves the reader
+    if (!opt && c && c > (lim - p) / arg) return bad;
+    if (!opt || (c && lim - p >= arg)) p += c * arg;
+    ++pc;
   }
-  return p - pos;
+  if (lim - p < N.wp_tail) return bad;
+  return p + N.wp_tail - pos;
 }
 
 // wlen_rd for NS = -2: the record's wire length (0: the path fails here) and
@@ -2028,7 +2050,7 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
 // than a plausible record, kPlaus + 1)
 template <bool SIMPLE, typename Rd>
 __device__ uint64_t nt_len(const Rd &rd, uint64_t len, uint64_t pos, uint64_t *cnt,
-                           uint64_t reach) {
+                           uint64_t reach, uint32_t maxel) {
   const NTLayout &N = nt_lds();
   uint32_t *const U = nt_used();
   const uint32_t nh = N.n_heaps;
@@ -2038,10 +2060,12 @@ __device__ uint64_t nt_len(const Rd &rd, uint64_t len, uint64_t pos, uint64_t *c
   const uint64_t lim = reach && reach < len - pos ? pos + reach : len;
   uint64_t p = pos;
   if constexpr (SIMPLE) {
-    p += nt_walk(N, rd, pos, lim, lim < len);
+    const uint64_t l = nt_walk(N, rd, pos, lim, lim < len, maxel);
+    if (l == kLenLimit) return kLenLimit;
+    p += l;
   } else {
-    const int32_t ec = nt_read<false>(N, rd, p, lim, lim < len, nullptr, nullptr, true);
-    if (ec == kNTLimit) return (uint64_t)kPlaus + 1;
+    const int32_t ec = nt_read<false>(N, rd, p, lim, lim < len, nullptr, nullptr, true, maxel);
+    if (ec == kNTLimit) return kLenLimit;
     if (ec) return 0;
   }
   if (p == pos) return 0;  // (a record takes at least one byte: spk_layout_check)
@@ -2056,10 +2080,132 @@ __device__ uint64_t nt_len(const Rd &rd, uint64_t len, uint64_t pos, uint64_t *c
 template <int NS, typename Rd>
 __device__ __forceinline__ uint64_t wlen_spec(const WalkProg &P, const Rd &rd, uint64_t len,
                                               uint64_t pos, uint32_t w, uint64_t *cnt) {
-  if constexpr (NS <= -2) return nt_len<NS == -3>(rd, len, pos, cnt, (uint64_t)kPlaus + 1);
+  if constexpr (NS <= -2) {
+    const uint64_t l = nt_len<NS == -3>(rd, len, pos, cnt, (uint64_t)kPlaus + 1, kNTSpecElems);
+    return l == kLenLimit ? (uint64_t)kPlaus + 1 : l;  // too long for a plausible start
+  }
   return wlen_rd<NS>(P, rd, len, pos, w, cnt);
 }
+// payload of a SPAN into its heap slots (long ones queued for vec_big_copy)
+__device__ __forceinline__ void nt_put_payload(const WinReader &rd, uint8_t *hp, uint64_t pos,
+                                               uint64_t nb, const BigQ &bq) {
+  if (nb >= kBigCopy) {
+    const uint64_t np = (nb + kBigPiece - 1) / kBigPiece;
+    const uint64_t j0 = atomicAdd(bq.n, (unsigned long long)np);
+    for (uint64_t q = 0; q < np; ++q) {
+      const uint64_t o = q * kBigPiece, m = nb - o < kBigPiece ? nb - o : kBigPiece;
+      if (j0 + q < bq.cap)
+        bq.jobs[j0 + q] = BigJob{pos + o, m, hp + o};
+      else
+        copy_bytes(hp + o, rd.wire + pos + o, m);  // (the cap is never reached)
+    }
+  } else {
+    rd.copy_to(hp, pos, nb);
+  }
+}
+// Emission of a record the walk program accepted (COPY / SPAN / OPTION /
+// ARRAY layouts): the interpreter without error paths (the walk checked
+// every read), frames below the top one in LDS
+__device__ uint64_t nt_emit_simple(const NTLayout &N, const WinReader &rd, uint64_t pos,
+                                   uint64_t len, uint8_t *rec, const BigQ &bq) {
+  uint32_t *const U = nt_used();
+  uint32_t *const F = nt_frames();
+  uint8_t **const FP = nt_fptrs();
+  const uint32_t w = rd.w;
+  uint32_t d = 0, i = 0, iend = N.n_ops, aop = 0, j = 0, cnt = 0;
+  uint8_t *r = rec, *el = nullptr, *pr = nullptr;
+  for (;;) {
+    if (i >= iend) {
+      if (!d) break;
+      if (++j < cnt) {
+        r = el + (uint64_t)j * N.ops[aop].size;
+        i = aop + 1;
+        continue;
+      }
+      i = N.end[aop] + 1u;
+      r = pr;
+      if (--d) {
+        aop = F[64 * (3 * (d - 1))];
+        j = F[64 * (3 * (d - 1) + 1)];
+        cnt = F[64 * (3 * (d - 1) + 2)];
+        el = FP[64 * (2 * (d - 1))];
+        pr = FP[64 * (2 * (d - 1) + 1)];
+        iend = N.end[aop];
+      } else {
+        iend = N.n_ops;
+      }
+      continue;
+    }
+    const spk_op op = N.ops[i];
+    if (op.kind == SPK_OP_COPY) {
+      rd.copy_to(r + op.rec_off, pos, op.size);
+      pos += op.size;
+      ++i;
+      continue;
+    }
+    const uint32_t hk = N.heap[i];
+    const bool opt = op.kind == SPK_OP_OPTION;
+    const uint64_t c = opt ? (uint64_t)(rd.byte(pos) != 0) : rd(pos);
+    pos += opt ? 1u : w;
+    const uint32_t o = U[64 * hk];
+    U[64 * hk] = o + (uint32_t)c;
+    *reinterpret_cast<uint32_t *>(r + op.rec_off) = (uint32_t)c;
+    *reinterpret_cast<uint64_t *>(r + op.aux) = o;
+    uint8_t *hp = N.heaps[hk] + (uint64_t)o * op.size;
+    if (op.kind == SPK_OP_SPAN) {
+      if (c) nt_put_payload(rd, hp, pos, c * op.size, bq);
+      pos += c * op.size;
+      ++i;
+    } else if (opt) {
+      if (c) {
+        if (len - pos >= op.size) {
+          rd.copy_to(hp, pos, op.size);
+          pos += op.size;
+        } else {
+          for (uint32_t b = 0; b < op.size; ++b) hp[b] = 0;  // unreadable value
+        }
+      }
+      ++i;
+    } else if (!c) {  // ARRAY
+      i = N.end[i] + 1u;
+    } else {
+      if (d) {
+        F[64 * (3 * (d - 1))] = aop;
+        F[64 * (3 * (d - 1) + 1)] = j;
+        F[64 * (3 * (d - 1) + 2)] = cnt;
+        FP[64 * (2 * (d - 1))] = el;
+        FP[64 * (2 * (d - 1) + 1)] = pr;
+      }
+      ++d;
+      aop = i;
+      j = 0;
+      cnt = (uint32_t)c;
+      el = hp;
+      pr = r;
+      r = hp;
+      iend = N.end[i];
+      ++i;
+    }
+  }
+  return pos;
+}
+
+// emission with the lane's heap slots already in its LDS counters; the
+// record's end
+template <bool SIMPLE>
+__device__ __forceinline__ uint64_t nt_emit_here(const WinReader &rd, uint64_t pos, uint64_t len,
+                                                 uint8_t *rec, const BigQ &bq) {
+  const NTLayout &N = nt_lds();
+  if constexpr (SIMPLE) {
+    return nt_emit_simple(N, rd, pos, len, rec, bq);
+  } else {
+    nt_read<true>(N, rd, pos, len, false, rec, &bq, false);
+    return pos;
+  }
+}
+
 // emission of the record at pos with heap bases off[]
+template <bool SIMPLE>
 __device__ __forceinline__ void nt_emit(const WinReader &rd, uint64_t pos, uint64_t len,
                                         uint8_t *rec, const uint64_t *off, const BigQ &bq) {
   const NTLayout &N = nt_lds();
@@ -2067,7 +2213,10 @@ __device__ __forceinline__ void nt_emit(const WinReader &rd, uint64_t pos, uint6
 #pragma unroll
   for (uint32_t q = 0; q < kVS; ++q)
     if (q < N.n_heaps) U[64 * q] = (uint32_t)off[q];
-  nt_read<true>(N, rd, pos, len, false, rec, &bq, false);
+  if constexpr (SIMPLE)
+    nt_emit_simple(N, rd, pos, len, rec, bq);
+  else
+    nt_read<true>(N, rd, pos, len, false, rec, &bq, false);
 }
 
 constexpr uint64_t kTermPos = ~0ull;  // "the true path ended before this chunk"
@@ -2145,7 +2294,7 @@ template <int NS, typename Rd>
 __device__ __forceinline__ void walk_true(const WalkProg &P, const Rd &rd, uint64_t len,
                                           uint32_t w, uint64_t entry, uint64_t ce,
                                           uint64_t &ex, uint32_t &cnt, uint64_t *sums,
-                                          uint64_t &term_at) {
+                                          uint64_t &term_at, uint64_t reach = 0) {
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
   cnt = 0;
   QFOR(q) sums[q] = 0;
@@ -2157,7 +2306,11 @@ __device__ __forceinline__ void walk_true(const WalkProg &P, const Rd &rd, uint6
   uint64_t x = entry;
   while (x < ce) {
     uint64_t rc[NS > 0 ? NS : kVS];
-    const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w, rc) : 0;
+    const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w, rc, reach) : 0;
+    if (L == kLenLimit) {  // (a bounded nested walk: the exit is unknown)
+      ex = kNoPos;
+      return;
+    }
     if (!L) {
       term_at = x;
       ex = kTermPos;
@@ -2190,7 +2343,7 @@ template <int NS, typename Rd>
 __device__ __forceinline__ void walk_merge(const WalkProg &P, const Rd &rd, uint64_t len,
                                            uint32_t w, uint64_t entry, uint64_t cs, uint64_t ce,
                                            const SpecPath<NS> &sp, uint64_t &ex, uint32_t &cnt,
-                                           uint64_t *sums, uint64_t &term_at) {
+                                           uint64_t *sums, uint64_t &term_at, uint64_t reach = 0) {
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
   cnt = 0;
   QFOR(q) sums[q] = 0;
@@ -2218,7 +2371,11 @@ __device__ __forceinline__ void walk_merge(const WalkProg &P, const Rd &rd, uint
       return;
     }
     uint64_t rc[NS > 0 ? NS : kVS];
-    const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w, rc) : 0;
+    const uint64_t L = x < len ? wlen_rd<NS>(P, rd, len, x, w, rc, reach) : 0;
+    if (L == kLenLimit) {
+      ex = kNoPos;
+      return;
+    }
     if (!L) {
       term_at = x;
       ex = kTermPos;
@@ -2241,7 +2398,8 @@ __device__ __forceinline__ void resolve_tile(const WalkProg &P, const Rd &rd, ui
   for (int round = 0; round < 66; ++round) {
     const uint64_t prev = __shfl_up(ex, 1);
     const uint64_t entry = lane == 0 ? entry0 : prev;
-    const bool need = entry != used;
+    // (an unknown exit from a known entry: K1's bounded nested walk gave up)
+    const bool need = entry != used || (ex == kNoPos && entry != kNoPos);
     const uint64_t m = __ballot(need);
     if (!m) return;
     // a lane with a start of its own waits while its predecessor re-walks
@@ -2262,7 +2420,8 @@ __device__ __forceinline__ void resolve_tile_sp(const WalkProg &P, const Rd &rd,
                                                 uint32_t lane, uint64_t entry0,
                                                 const SpecPath<NS> &sp, uint64_t &used,
                                                 uint64_t &ex, uint32_t &cnt, uint64_t *sums,
-                                                uint64_t &term_at, uint32_t *stat = nullptr) {
+                                                uint64_t &term_at, uint32_t *stat = nullptr,
+                                                uint64_t reach = 0) {
   for (int round = 0; round < 66; ++round) {
     const uint64_t prev = __shfl_up(ex, 1);
     const uint64_t entry = lane == 0 ? entry0 : prev;
@@ -2272,7 +2431,7 @@ __device__ __forceinline__ void resolve_tile_sp(const WalkProg &P, const Rd &rd,
     if (stat) ++stat[0];
     if (need && (used == kNoPos || !(lane > 0 && ((m >> (lane - 1)) & 1)))) {  // as resolve_tile
       if (stat) ++stat[1];
-      walk_merge<NS>(P, rd, len, w, entry, cs, ce, sp, ex, cnt, sums, term_at);
+      walk_merge<NS>(P, rd, len, w, entry, cs, ce, sp, ex, cnt, sums, term_at, reach);
       used = entry;
     }
   }
@@ -2444,6 +2603,17 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
           }
         }
         if (P.pf_all) m = 0xFFu;  // first span an OPTION / no span: any byte may start a record
+        if (NS <= -2 && P.scr2 && m) {
+          // the second count, past the first span's payload
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk) {
+            if (!((m >> kk) & 1u)) continue;
+            const uint64_t b = b0 + kk;
+            const uint64_t c0 = rd(b);
+            const uint64_t q2 = b + w + c0 * P.esz0 + P.s2skip;
+            if (q2 + w > len || rd(q2) > P.c1max) m &= ~(1u << kk);
+          }
+        }
         const uint64_t rem = ce - (cs + tt);  // candidates must start in the chunk
         if (rem < 8) m &= (1u << rem) - 1u;
         if (!m) {
@@ -2491,7 +2661,7 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
       } else {
         if (!past) ex = x;
         ++past;
-        if (!L || past >= kSpecPast) break;
+        if (!L || past >= (NS <= -2 ? (uint32_t)SPK_NT_PAST : kSpecPast)) break;
       }
       x += L;
     }
@@ -2538,7 +2708,7 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
         uint32_t qc = 0;
         uint64_t qs[NS > 0 ? NS : kVS];
         if (ok) {
-          walk_true<NS>(P, rd, len, w, q, ce0, qe, qc, qs, qt);
+          walk_true<NS>(P, rd, len, w, q, ce0, qe, qc, qs, qt, kK1Reach<NS>);
           ok = qe == x1;
         }
         const uint64_t m = __ballot(ok);
@@ -2564,7 +2734,8 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
     }
   }
   if (X != kNoPos && !(dbg & 32))
-    resolve_tile_sp<NS>(P, rd, len, w, cs, ce, lane, X, sp, used, ex, cnt, sums, term_at, stat);
+    resolve_tile_sp<NS>(P, rd, len, w, cs, ce, lane, X, sp, used, ex, cnt, sums, term_at, stat,
+                        kK1Reach<NS>);
   if (stat && used != used0) ++stat[4];
   return X;
 }
@@ -2580,6 +2751,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t t = (uint64_t)blockIdx.x * kDecWaves + wv;
   if (t >= TB.ntiles || !vec_live(c)) return;  // wave-uniform
+  const uint64_t tclk0 = (dbg & 4096) ? __builtin_readcyclecounter() : 0;
   nt_prologue<NS>(a, lane);
   const uint32_t w = c->w;
   const uint64_t len = a.wire_len, p0 = c->p0;
@@ -2600,6 +2772,11 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
     for (uint32_t k = 0; k < 6; ++k) {
       const uint64_t v = wave_sum_u64(stat[k]);
       if (lane == 0) atomicAdd(&fcd->diag[k], (unsigned long long)v);
+    }
+    const uint64_t dt = __builtin_readcyclecounter() - tclk0;  // this tile's cycles
+    if (lane == 0) {
+      atomicMax(&fcd->diag[6], (unsigned long long)dt);
+      atomicAdd(&fcd->diag[7], (unsigned long long)dt);
     }
   }
   uint64_t &used = st.used, &ex = st.ex;
@@ -2733,7 +2910,9 @@ __global__ __launch_bounds__(256) void vec_tile_pick(uint8_t *__restrict__ ws, T
   if (t >= TB.ntiles || !vec_live(c)) return;
   if (pass > 0 && !fc->broken[pass - 1]) return;  // the previous pass fixed nothing
   const uint64_t T = tile_entry(TB, fc, t);
-  const int32_t sel = T == kNoPos ? kSelBroken : tile_select_for(TB, t, T);
+  int32_t sel = T == kNoPos ? kSelBroken : tile_select_for(TB, t, T);
+  // (a nested tile whose K1 walk gave up has an unknown exit: walked again)
+  if (sel >= 0 && TB.fn[t * kFnWords] == kNoPos) sel = kSelBroken;
   if (sel != kSelBroken || T == kNoPos) {
     TB.sel[t] = sel;
     if (sel >= 0) tile_jump(TB, c->p0, t, TB.fn[t * kFnWords], nsp, 0, &fc->broken[pass], 1);
@@ -2841,6 +3020,7 @@ __global__ __launch_bounds__(64) void vec_tile_seqfix(DecArgs a, WalkProg P,
     if (u < TB.ntiles) {
       const uint64_t T = tile_entry(TB, fc, u);
       sel = tile_select_for(TB, u, T);
+      if (sel >= 0 && TB.fn[u * kFnWords] == kNoPos) sel = kSelBroken;  // exit unknown
       bad = sel == kSelBroken && T != kNoPos;
     }
     const uint64_t m = __ballot(bad);
@@ -3051,9 +3231,11 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
   const uint64_t g = t * 64 + ch;
   uint64_t used = own ? TB.cused[g] : kNoPos, ex = own ? TB.cex[g] : kNoPos;
   uint32_t cnt = own ? TB.ccnt[g] : 0;
-  if (sel > 0 && part == 0 && lane == 0) {  // another entry of chunk 0 (same exit)
+  uint64_t qs[NS > 0 ? NS : kVS];  // (nested: chunk 0's heap sums from that entry)
+  const bool alt0 = sel > 0 && part == 0 && lane == 0;
+  if (alt0) {  // another entry of chunk 0 (same exit)
     const uint64_t T = alt[0];
-    uint64_t qe, qt, qs[NS > 0 ? NS : kVS];
+    uint64_t qe, qt;
     walk_true<NS>(P, rd, len, w, T, ce, qe, cnt, qs, qt);
     used = T;
   }
@@ -3082,6 +3264,75 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
     atomicMin(&fc->term_pos, (unsigned long long)x);
   }
   if (base >= n) return;
+  if constexpr (NS <= -2) {
+    // nested records: each lane emits its own chunk's records in order, from
+    // the chunk state K1 published (first record index and heap bases by a
+    // wave scan of the chunks' counts and heap sums): one walk per record
+    // (the interpreter's walks dominate here, not the stores)
+    uint64_t tot;
+    const uint64_t rofs = wave_excl_scan_u64(cnt, lane, &tot);
+    uint64_t hb[kVS], hs[kVS];
+    bool fits_all = true;
+    QFOR(q) {
+      hs[q] = !own ? 0ull : alt0 ? qs[q] : TB.csum[(uint64_t)q * TB.nchunks + g];
+      hb[q] = psum[q] + wave_excl_scan_u64(hs[q], lane, &tot);
+      if (hb[q] + hs[q] > a.heap_cap[q]) fits_all = false;
+    }
+    uint64_t idx = base + rofs;
+    if (!own || !cnt || idx >= n || used == kNoPos || used == kTermPos) return;
+    uint32_t *const U = nt_used();
+    QFOR(q) U[64 * q] = (uint32_t)hb[q];
+    uint64_t x = used;
+    for (uint32_t r = 0; r < cnt && idx < n; ++r, ++idx) {
+      const uint64_t x0 = x;
+      if (idx < a.rec_cap && fits_all) {
+        x = nt_emit_here<NS == -3>(rd, x, len, recs + idx * a.L.stride, bq);
+      } else {
+        // near a capacity: this record's heap use first, written only if it fits
+        uint64_t b[kVS], rc[kVS];
+        QFOR(q) b[q] = U[64 * q];
+        x += wlen_rd<NS>(P, rd, len, x, w, rc);
+        bool fit = idx < a.rec_cap;
+        QFOR(q) fit = fit && b[q] + rc[q] <= a.heap_cap[q];
+        QFOR(q) U[64 * q] = (uint32_t)b[q];
+        if (fit)
+          nt_emit_here<NS == -3>(rd, x0, len, recs + idx * a.L.stride, bq);
+        else
+          QFOR(q) U[64 * q] = (uint32_t)(b[q] + rc[q]);
+      }
+      if (idx == n - 1) {
+        fc->end_pos = x;
+        QFOR(q) fc->htot[q] = U[64 * q];
+      }
+    }
+    return;
+  } else if constexpr (SPK_K4_LANE != 0) {
+    // (A/B) flat records, one lane per chunk as above
+    uint64_t tot;
+    const uint64_t rofs = wave_excl_scan_u64(cnt, lane, &tot);
+    uint64_t hb[kVS];
+    QFOR(q) {
+      const uint64_t hsq = !own ? 0ull : alt0 ? qs[q] : TB.csum[(uint64_t)q * TB.nchunks + g];
+      hb[q] = psum[q] + wave_excl_scan_u64(hsq, lane, &tot);
+    }
+    uint64_t idx = base + rofs;
+    if (!own || !cnt || idx >= n || used == kNoPos || used == kTermPos) return;
+    uint64_t x = used;
+    for (uint32_t r = 0; r < cnt && idx < n; ++r, ++idx) {
+      uint64_t rc[kVS] = {};
+      const uint64_t L = wlen_rd<NS>(P, rd, len, x, w, rc);
+      bool fits = idx < a.rec_cap;
+      QFOR(q) fits = fits && hb[q] + rc[q] <= a.heap_cap[q];
+      if (fits) emit_record_rd(a.L, rd, x, w, recs + idx * a.L.stride, a.heaps, hb, len, bq, dbg);
+      if (idx == n - 1) {
+        fc->end_pos = x + L;
+        QFOR(q) fc->htot[q] = hb[q] + rc[q];
+      }
+      QFOR(q) hb[q] += rc[q];
+      x += L;
+    }
+    return;
+  }
   uint64_t rofs;  // this chunk's first record, part-relative
   {
     uint64_t tot;
@@ -3126,7 +3377,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
       const uint64_t gr = base + pass0 + i;
       if (act && gr < a.rec_cap && fits && !(dbg & 64)) {
         if constexpr (NS <= -2)
-          nt_emit(rd, pos, len, recs + gr * a.L.stride, off, bq);
+          nt_emit<NS == -3>(rd, pos, len, recs + gr * a.L.stride, off, bq);
         else
           emit_record_rd(a.L, rd, pos, w, recs + gr * a.L.stride, a.heaps, off, len, bq, dbg);
       }
@@ -3701,6 +3952,7 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
   SPK_LAUNCH(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, 0u, (uint64_t)0);
   SPK_LAUNCH(vec_tile_spec<NS>, dim3(grid_for(f.ntiles, kDecWaves)), dim3(64 * kDecWaves), 0, s,
              a, P, wire, (const uint8_t *)ws, TB, tile_dbg());
+  if (tile_dbg() & 8192) return hipGetLastError();  // (A/B timing of K1 alone)
   if (phase == kTilesIndex) SPK_LAUNCH(vec_range_entry, dim3(1), dim3(64), 0, s, ws, TB);
   for (uint32_t pass = 0; pass < 3; ++pass) {
     SPK_LAUNCH(vec_tile_pick, dim3(grid_for(f.ntiles, 256)), dim3(256), 0, s, ws, TB, nsp, pass);
@@ -3733,19 +3985,30 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
   return hipGetLastError();
 }
 
+static bool nested_args(const spk_layout *L, uint64_t wire_len, uint64_t rec_cap,
+                        void *const *d_heaps, const uint64_t *heap_caps, uint8_t *ws,
+                        hipStream_t s, DecArgs &a, WalkProg &P);
 hipError_t launch_var_shard(const spk_layout *L, int phase, const void *d_wire, uint64_t wire_len,
                             uint64_t tile_lo, uint64_t tile_hi, uint64_t entry,
                             spk_shard_t *d_summary, uint64_t first, uint32_t last, void *d_recs,
                             uint64_t rec_cap, void *const *d_heaps, const uint64_t *heap_caps,
                             spk_dresult_t *d_res, void *d_ws, hipStream_t s) {
   DecArgs a = {};
-  a.L = make_klayout(L);
-  a.fmt = L->fmt_vector;
-  a.wire_len = wire_len;
-  a.rec_cap = rec_cap;
-  for (uint32_t k = 0; k < a.L.n_spans; ++k) {
-    a.heaps[k] = d_heaps ? (uint8_t *)d_heaps[k] : nullptr;
-    a.heap_cap[k] = heap_caps ? heap_caps[k] : 0;
+  WalkProg P;
+  bool nested = false, simple = false;
+  if (layout_nested(L)) {  // nested layouts: the interpreter walker (var_nested_tile_ok)
+    nested = true;
+    simple = nested_args(L, wire_len, rec_cap, d_heaps, heap_caps, (uint8_t *)d_ws, s, a, P);
+  } else {
+    a.L = make_klayout(L);
+    a.fmt = L->fmt_vector;
+    a.wire_len = wire_len;
+    a.rec_cap = rec_cap;
+    for (uint32_t k = 0; k < a.L.n_spans; ++k) {
+      a.heaps[k] = d_heaps ? (uint8_t *)d_heaps[k] : nullptr;
+      a.heap_cap[k] = heap_caps ? heap_caps[k] : 0;
+    }
+    P = make_walkprog(L);
   }
   a.range = 1;
   a.range_t0 = tile_lo;
@@ -3756,9 +4019,10 @@ hipError_t launch_var_shard(const spk_layout *L, int phase, const void *d_wire, 
   sc.first = first;
   sc.last = last;
   const int ph = phase == 0 ? kTilesIndex : kTilesEmit;
-  const WalkProg P = make_walkprog(L);
   const uint8_t *wire = (const uint8_t *)d_wire;
   uint8_t *ws = (uint8_t *)d_ws, *r = (uint8_t *)d_recs;
+  if (nested && simple) return launch_vec_tiles_ns<-3>(a, P, L, wire, ws, d_res, r, s, ph, sc);
+  if (nested) return launch_vec_tiles_ns<-2>(a, P, L, wire, ws, d_res, r, s, ph, sc);
   if (P.nv) return launch_vec_tiles_ns<-1>(a, P, L, wire, ws, d_res, r, s, ph, sc);
   if (P.ns == 1) return launch_vec_tiles_ns<1>(a, P, L, wire, ws, d_res, r, s, ph, sc);
   if (P.ns == 2) return launch_vec_tiles_ns<2>(a, P, L, wire, ws, d_res, r, s, ph, sc);
@@ -3780,31 +4044,40 @@ static NTLayout make_ntlayout(const NLayout &N, void *const *heaps) {
   t.fv_cnt = N.fv_cnt;
   t.fv_has64 = N.fv_has64;
   t.fv_bits = N.fv_bits;
-  for (uint32_t k = 0; k < N.n_heaps && k < kVS; ++k) t.heaps[k] = (uint8_t *)heaps[k];
-  // the walk program, when every op is COPY / SPAN / OPTION / ARRAY (+ END)
+  for (uint32_t k = 0; k < N.n_heaps && k < kVS; ++k) t.heaps[k] = heaps ? (uint8_t *)heaps[k] : nullptr;
+  // the walk program, when every op is COPY / SPAN / OPTION / ARRAY (+ END):
+  // COPYs fold into the next instruction's fixed bytes (or the tail)
   uint32_t n = 0, open[SPK_MAX_DEPTH + 1], d = 0;
+  uint64_t fix = 0;
   bool ok = !N.fv_cnt;
   for (uint32_t i = 0; i < N.n_ops && ok; ++i) {
     const spk_op &op = N.ops[i];
     if (op.kind == SPK_OP_COPY) {
-      if (n && (t.wp[n - 1] & 7u) == WP_SKIP && (t.wp[n - 1] >> 8) + op.size < (1u << 24))
-        t.wp[n - 1] += op.size << 8;
-      else
-        t.wp[n++] = WP_SKIP | (op.size << 8);
-    } else if (op.kind == SPK_OP_SPAN || op.kind == SPK_OP_OPTION) {
-      t.wp[n++] = (op.kind == SPK_OP_SPAN ? WP_SPAN : WP_OPT) | ((uint32_t)N.heap[i] << 3) |
-                  ((op.size ? op.size : 1u) << 8);
+      fix += op.size;
+      continue;
+    }
+    uint32_t x;
+    if ((op.kind == SPK_OP_SPAN || op.kind == SPK_OP_OPTION) && op.size < (1u << 24)) {
+      x = (op.kind == SPK_OP_SPAN ? WP_SPAN : WP_OPT) | ((uint32_t)N.heap[i] << 3) |
+          ((op.size ? op.size : 1u) << 8);
     } else if (op.kind == SPK_OP_ARRAY && d < SPK_MAX_DEPTH) {
       open[d++] = n;
-      t.wp[n++] = WP_ARR | ((uint32_t)N.heap[i] << 3);
+      x = WP_ARR | ((uint32_t)N.heap[i] << 3);
     } else if (op.kind == SPK_OP_END && d) {
-      t.wp[n++] = WP_END;
-      t.wp[open[--d]] |= n << 8;  // the loop's exit
+      x = WP_END;
+      --d;
     } else {
       ok = false;
+      break;
     }
+    if (fix >= (1ull << 32)) ok = false;
+    t.wp[n] = make_uint2(x, (uint32_t)fix);
+    fix = 0;
+    ++n;
+    if (x == WP_END) t.wp[open[d]].x |= n << 8;  // the loop's exit
   }
-  t.wp_n = ok && !d ? n : 0;
+  t.wp_n = ok && !d && fix < (1ull << 32) ? n : 0;
+  t.wp_tail = (uint32_t)fix;
   return t;
 }
 // the tile pipeline's walk program for a nested layout: heap use as the span
@@ -3815,6 +4088,20 @@ static WalkProg make_walkprog_nested(const NLayout &N) {
   if (N.scr_off != ~0u) {
     p.skip[0] = N.scr_off;
     p.c0max = kPlaus > N.scr_off ? (kPlaus - N.scr_off) / (N.scr_esz ? N.scr_esz : 1) : 0;
+    // the op after the first count: a SPAN whose payload is followed (after
+    // COPYs) by another SPAN / ARRAY count
+    uint32_t i = 0, fix = 0;
+    while (i < N.n_ops && N.ops[i].kind == SPK_OP_COPY) ++i;
+    if (SPK_NT_SCR2 && i < N.n_ops && N.ops[i].kind == SPK_OP_SPAN) {
+      uint32_t j = i + 1;
+      while (j < N.n_ops && N.ops[j].kind == SPK_OP_COPY) fix += N.ops[j++].size;
+      if (j < N.n_ops && (N.ops[j].kind == SPK_OP_SPAN || N.ops[j].kind == SPK_OP_ARRAY)) {
+        p.scr2 = 1;
+        p.esz0 = N.ops[i].size;
+        p.s2skip = fix;
+        p.c1max = kPlaus / (N.ops[j].kind == SPK_OP_SPAN && N.ops[j].size ? N.ops[j].size : 1);
+      }
+    }
   } else {
     p.pf_all = 1;
   }
@@ -3835,35 +4122,46 @@ size_t var_nested_tile_ws_bytes(const spk_layout *L, uint64_t wire_len) {
   return tile_ws_layout(make_nlayout(L).n_heaps, wire_len).end + 256;
 }
 
-hipError_t launch_var_nested_decode(const spk_layout *L, const void *d_wire, uint64_t wire_len,
-                                    void *d_recs, uint64_t rec_cap, void *const *d_heaps,
-                                    const uint64_t *heap_caps, spk_dresult_t *d_res, void *d_ws,
-                                    hipStream_t s, uint32_t body_w, uint64_t body_n) {
+// decode arguments of a nested layout on the tile decoder; its walker layout
+// goes into the workspace. Returns whether the walk program applies (NS = -3).
+static bool nested_args(const spk_layout *L, uint64_t wire_len, uint64_t rec_cap,
+                        void *const *d_heaps, const uint64_t *heap_caps, uint8_t *ws,
+                        hipStream_t s, DecArgs &a, WalkProg &P) {
   const NLayout N = make_nlayout(L);
-  DecArgs a = {};
+  a = DecArgs{};
   a.L.stride = N.stride;
   a.L.n_spans = N.n_heaps;
   a.L.n_var = 1;  // (no minimum-record-size screen in the header kernel)
   a.fmt = L->fmt_vector;
   a.wire_len = wire_len;
   a.rec_cap = rec_cap;
-  a.body_w = body_w;
-  a.body_n = body_n;
   for (uint32_t k = 0; k < N.n_heaps && k < kVS; ++k) {
-    a.heaps[k] = (uint8_t *)d_heaps[k];
-    a.heap_cap[k] = heap_caps[k];
+    a.heaps[k] = d_heaps ? (uint8_t *)d_heaps[k] : nullptr;
+    a.heap_cap[k] = heap_caps ? heap_caps[k] : 0;
   }
   a.nested = 1;
-  const WalkProg P = make_walkprog_nested(N);
-  uint8_t *ws = (uint8_t *)d_ws;
+  P = make_walkprog_nested(N);
   const TileWs f = tile_ws_layout(P.ns, wire_len);
   a.nl = ws + f.nl;
-  SPK_LAUNCH(nt_put, dim3(1), dim3(256), 0, s, make_ntlayout(N, d_heaps), ws + f.nl);
-  // NS = -3: every walk runs the walk program; -2: the interpreter
   const NTLayout t = make_ntlayout(N, d_heaps);
-  if (t.wp_n)
-    return launch_vec_tiles_ns<-3>(a, P, L, (const uint8_t *)d_wire, ws, d_res, (uint8_t *)d_recs, s);
-  return launch_vec_tiles_ns<-2>(a, P, L, (const uint8_t *)d_wire, ws, d_res, (uint8_t *)d_recs, s);
+  SPK_LAUNCH(nt_put, dim3(1), dim3(256), 0, s, t, ws + f.nl);
+  return t.wp_n != 0;
+}
+
+hipError_t launch_var_nested_decode(const spk_layout *L, const void *d_wire, uint64_t wire_len,
+                                    void *d_recs, uint64_t rec_cap, void *const *d_heaps,
+                                    const uint64_t *heap_caps, spk_dresult_t *d_res, void *d_ws,
+                                    hipStream_t s, uint32_t body_w, uint64_t body_n) {
+  DecArgs a;
+  WalkProg P;
+  uint8_t *ws = (uint8_t *)d_ws;
+  const bool simple = nested_args(L, wire_len, rec_cap, d_heaps, heap_caps, ws, s, a, P);
+  a.body_w = body_w;
+  a.body_n = body_n;
+  // NS = -3: every walk runs the walk program; -2: the interpreter
+  const uint8_t *wire = (const uint8_t *)d_wire;
+  if (simple) return launch_vec_tiles_ns<-3>(a, P, L, wire, ws, d_res, (uint8_t *)d_recs, s);
+  return launch_vec_tiles_ns<-2>(a, P, L, wire, ws, d_res, (uint8_t *)d_recs, s);
 }
 
 size_t var_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len) {
