@@ -912,11 +912,16 @@ def main():
             concat = concat_bench(torch, dist, world, rank, dev, args.concat_records)
         except Exception as e:  # never lose the headline line
             concat = {"error": f"{type(e).__name__}: {e}"}
+    if rank == 0:  # progress on stderr (the JSON line stays the only stdout line)
+        print(f"[bench] {args.config}: {head['ms_per_step']} ms/step", file=sys.stderr, flush=True)
     extra = {}
     if world == 1 and not args.no_extra and args.config == "c2":
         for cfg in EXTRA:
             extra[cfg] = run_config(cfg, args, torch, dist, world, rank, dev, args.extra_steps,
                                     2, 0.5, cpu=True)
+            if rank == 0:
+                print(f"[bench] {cfg}: {extra[cfg].get('ms_per_step')} ms/step", file=sys.stderr,
+                      flush=True)
 
     if rank == 0:
         line = {

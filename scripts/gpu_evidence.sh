@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round evidence in one GPU call: HBM PMC passes (FETCH_SIZE and WRITE_SIZE in
+# Round evidence (one or more GPU calls: SKIP_PMC / SKIP_BENCH / PMC_CONFIGS /
+# PROF_CONFIGS / PMC_DIR select the steps): HBM PMC passes (FETCH_SIZE and WRITE_SIZE in
 # separate runs, each config on its own, --no-extra) summarised per kernel into
 # $OUT/pmc_<cfg>.json; then the default bench line (C2 headline + every other
 # BASELINE config in extra.configs, reading those PMC summaries, host paths);
@@ -15,7 +16,7 @@ step() { local name=$1; shift; local t=$1; shift
   echo "[$name] rc=$rc"; tail -1 "$OUT/$name.log" | cut -c1-300
   if [ $rc -ne 0 ]; then tail -20 "$OUT/$name.log"; exit $rc; fi; }
 if [ -z "$SKIP_PMC" ]; then
-  for c in ${PMC_CONFIGS:-c2 c2b c3 c4 cv c5}; do
+  for c in ${PMC_CONFIGS:-c2 c2b c3 c4 cv c5 cm}; do
     for ctr in FETCH_SIZE WRITE_SIZE; do
       step pmc_${c}_$ctr 300 rocprofv3 --pmc $ctr -d $OUT/pmc_${c}_$ctr -o run --output-format csv -- python bench.py --config $c --steps 3 --warmup 1 --settle 0 --no-cpu-baseline --no-extra
     done
@@ -23,8 +24,8 @@ if [ -z "$SKIP_PMC" ]; then
     rm -rf $OUT/pmc_${c}_FETCH_SIZE $OUT/pmc_${c}_WRITE_SIZE
   done
 fi
-step bench 900 python bench.py --host-path --pmc-dir $OUT
-for c in ${PROF_CONFIGS:-c2 c2b c3 c4 cv c5}; do
+[ -n "$SKIP_BENCH" ] || step bench 900 python bench.py --host-path --pmc-dir ${PMC_DIR:-$OUT}
+for c in ${PROF_CONFIGS:-c2 c2b c3 c4 cv c5 cm}; do
   step prof_$c 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o run --output-format csv -- python bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline --no-extra
   cp $OUT/prof_$c/run_kernel_stats.csv $OUT/${c}_kernel_stats.csv 2>/dev/null || find $OUT/prof_$c -name "*kernel_stats.csv" -exec cp {} $OUT/${c}_kernel_stats.csv \;
   rm -rf $OUT/prof_$c

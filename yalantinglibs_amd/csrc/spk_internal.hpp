@@ -145,6 +145,13 @@ struct Ctl {
   uint32_t pad;
 };
 
+// c elements of `size` bytes: their byte count without a 64-bit division
+// (a runtime divisor is a long software sequence on the GPU); false when the
+// product overflows
+__host__ __device__ __forceinline__ bool span_nb(uint64_t c, uint64_t size, uint64_t *nb) {
+  return !__builtin_mul_overflow(c, size, nb);
+}
+
 __host__ __device__ __forceinline__ uint64_t ld_le(const uint8_t *p, uint32_t w) {
   uint64_t v = 0;
   for (uint32_t i = 0; i < w; ++i) v |= (uint64_t)p[i] << (8 * i);

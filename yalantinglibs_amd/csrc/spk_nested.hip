@@ -713,11 +713,11 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
     // slots an ARRAY can fill: an element takes at least one byte, so at most
     // (bytes left + 1) get decoded (the last one may fail and stay)
     // (a SPAN whose payload is not there fails below without using its heap)
+    uint64_t snb = 0;
+    const bool sfit = op.kind == SPK_OP_SPAN && span_nb(cnt, op.size, &snb) && snb <= end - pos;
     const uint64_t need = op.kind == SPK_OP_ARRAY ? (cnt > end - pos ? end - pos + 1 : cnt)
-                          : op.kind == SPK_OP_SPAN && ((op.size > 1 && cnt > ~0ull / op.size) ||
-                                                       end - pos < cnt * op.size)
-                              ? 0
-                              : cnt;
+                          : op.kind == SPK_OP_SPAN && !sfit ? 0
+                                                            : cnt;
     if (put && (need > 0xFFFFFFFFull || need > heap_cap[hk] - (off < heap_cap[hk] ? off : heap_cap[hk]))) {
       *ovf = 1;
       put = false;
@@ -764,7 +764,7 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
     }
     // SPAN (unpacker.hpp:1127-1156): the whole payload must be present
     if (cnt) {
-      if ((op.size > 1 && cnt > ~0ull / op.size) || end - pos < cnt * op.size) {
+      if (!sfit) {
         if (bounded) return kNLimit;
         ec = SPK_ERRC_NO_BUFFER_SPACE;
         continue;
@@ -1109,12 +1109,15 @@ __global__ __launch_bounds__(256) void nest_size(NEnc e, const uint8_t *__restri
       a[e.n + i] = s.cnts - s.ccnts;
     }
   }
-  // block max -> one atomic per wave
+  // wave max -> an atomic only when it raises the running maximum (one
+  // atomic per wave on one address serialises 10M-record batches)
   for (int o = 32; o > 0; o >>= 1) {
     const uint64_t x = __shfl_xor(m, o);
     m = x > m ? x : m;
   }
-  if ((threadIdx.x & 63) == 0 && m) atomicMax(&ctl->maxc, (unsigned long long)m);
+  if ((threadIdx.x & 63) == 0 && m &&
+      m > __hip_atomic_load(&ctl->maxc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicMax(&ctl->maxc, (unsigned long long)m);
 }
 
 __global__ void nest_ctl_init(uint8_t *ws) {

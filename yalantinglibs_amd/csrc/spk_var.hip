@@ -829,8 +829,8 @@ __device__ __forceinline__ uint64_t rec_wire_len(const KLayout &L, const uint8_t
       const uint64_t c = op.kind == SPK_OP_OPTION ? (uint64_t)(wire[pos] != 0) : ld_le(wire + pos, w);
       pos += pw;
       if (c) {
-        if (op.size > 1 && c > ~0ull / op.size) return 0;
-        const uint64_t nb = c * op.size;
+        uint64_t nb;
+        if (!span_nb(c, op.size, &nb)) return 0;
         if (nb > len - pos) {
           if (op.kind != SPK_OP_OPTION) return 0;
         } else {
@@ -1949,12 +1949,12 @@ __device__ int32_t nt_read(const NTLayout &N, const Rd &rd, uint64_t &pos, uint6
     }
     // SPAN (unpacker.hpp:1127-1156): the whole payload must be present
     if (cnt) {
-      if ((op.size > 1 && cnt > ~0ull / op.size) || lim - pos < cnt * op.size) {
+      uint64_t nb;
+      if (!span_nb(cnt, op.size, &nb) || lim - pos < nb) {
         if (bounded) return kNTLimit;
         ec = SPK_ERRC_NO_BUFFER_SPACE;
         continue;
       }
-      const uint64_t nb = cnt * op.size;
       if constexpr (EMIT) {
         uint8_t *hp = N.heaps[hk] + off * op.size;
         if (nb >= kBigCopy) {
@@ -2037,7 +2037,8 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
       continue;
     }
     // SPAN: the payload must be there; OPTION: an unreadable value leaves the reader
-    if (!opt && c && c > (lim - p) / arg) return bad;
+    // (c < 2^32 and arg < 2^24: the product cannot overflow)
+    if (!opt && (c > lim - p || c * arg > lim - p)) return bad;
     if (!opt || (c && lim - p >= arg)) p += c * arg;
     ++pc;
   }
