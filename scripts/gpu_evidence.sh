@@ -25,7 +25,9 @@ if [ -z "$SKIP_PMC" ]; then
   done
 fi
 [ -n "$SKIP_BENCH" ] || step bench 900 python bench.py --host-path --pmc-dir ${PMC_DIR:-$OUT}
-for c in ${PROF_CONFIGS:-c2 c2b c3 c4 cv c5 cm}; do
+PROF_CONFIGS=${PROF_CONFIGS:-c2 c2b c3 c4 cv c5 cm}
+[ "$PROF_CONFIGS" = none ] && PROF_CONFIGS=""
+for c in $PROF_CONFIGS; do
   step prof_$c 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o run --output-format csv -- python bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline --no-extra
   cp $OUT/prof_$c/run_kernel_stats.csv $OUT/${c}_kernel_stats.csv 2>/dev/null || find $OUT/prof_$c -name "*kernel_stats.csv" -exec cp {} $OUT/${c}_kernel_stats.csv \;
   rm -rf $OUT/prof_$c

@@ -1493,6 +1493,19 @@ struct WinReader {
     auto bf = [this](uint64_t q) { return byte(q); };
     return vi_read(bf, x, len, v);
   }
+  // the count field at x: its w low bytes (wmask) or, for an OPTION's
+  // has_value byte, whether it is non-zero; inside the window one path (8
+  // bytes from three dwords), past it the wire
+  __device__ __forceinline__ uint64_t count_at(uint64_t x, uint64_t wmask, bool opt) const {
+    if (x + 12 <= wend) {
+      const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = o >> 2;
+      const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2];
+      const uint64_t b = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
+                         ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
+      return opt ? (uint64_t)((b & 0xFFu) != 0) : (b & wmask);
+    }
+    return opt ? (uint64_t)(byte(x) != 0) : (*this)(x);
+  }
   // 4 / 16 bytes at x (x + n <= wend: inside the staged window)
   __device__ __forceinline__ uint32_t ld4(uint64_t x) const {
     const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = o >> 2;
@@ -1996,6 +2009,7 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
   uint32_t *const U = nt_used();
   uint32_t *const F = nt_frames();
   const uint32_t w = rd.w;
+  const uint64_t wmask = w >= 8 ? ~0ull : (1ull << (8 * w)) - 1;
   uint64_t p = pos;
   uint32_t pc = 0, d = 0, body = 0, rem = 0;  // top loop frame: body start, elements left
   while (pc < N.wp_n) {
@@ -2018,7 +2032,7 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
     const bool opt = op == WP_OPT;
     const uint32_t cw = opt ? 1u : w;
     if (lim - p < cw) return bad;
-    uint64_t c = opt ? (uint64_t)(rd.byte(p) != 0) : rd(p);
+    const uint64_t c = rd.count_at(p, wmask, opt);
     p += cw;
     atomicAdd(U + 64 * h, (uint32_t)c);
     if (op == WP_ARR) {
@@ -2268,7 +2282,10 @@ constexpr uint32_t kTileVec = (kTileBytes + kWinExtra) / 16;  // staged 16-B slo
 constexpr uint32_t kDecWaves = SPK_TWAVES;                   // tiles (waves) per block
 constexpr uint32_t kTab = 2048;                              // record starts per emission pass
 constexpr uint64_t kNoPos = ~0ull - 1;  // "no plausible start / unknown entry"
-constexpr uint32_t kSpecPast = 2;       // records a speculative walk checks past its chunk
+#ifndef SPK_SPEC_PAST
+#define SPK_SPEC_PAST 2
+#endif
+constexpr uint32_t kSpecPast = SPK_SPEC_PAST;  // records a speculative walk checks past its chunk
 constexpr uint32_t kAlt = 4;            // entries a tile function carries
 constexpr uint32_t kAltWords = 2 + kVS;   // entry, cnt, sums
 constexpr uint32_t kFnWords = 48;       // y, nalt, kAlt x kAltWords (+ pad)
@@ -2520,6 +2537,11 @@ __device__ __forceinline__ bool vec_live(const VCtl *c) { return !c->errc && c->
 
 // One lane's chunk state after the speculative walk and the in-wave
 // resolution (K1 sections 1-2; also the fused decoder's first phase).
+// records a speculative walk checks past its chunk (0: none, the walk stops at
+// the first record start past it)
+template <int NS>
+constexpr uint32_t kNPast = NS <= -2 ? (uint32_t)SPK_NT_PAST : kSpecPast;
+
 template <int NS>
 struct TileLane {
   uint64_t used, ex, term_at;
@@ -2631,6 +2653,10 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
         QFOR(q) ksum[q] = 0;
         searching = false;
       }
+      if (kNPast<NS> == 0 && x >= ce) {  // no walks past the chunk: the exit is known
+        ex = x;
+        break;
+      }
       uint64_t rc[NS > 0 ? NS : kVS];
       // (the exact start of tile 0 walks unbounded: its records may be long)
       const uint64_t L = x >= len ? 0
@@ -2662,7 +2688,7 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
       } else {
         if (!past) ex = x;
         ++past;
-        if (!L || past >= (NS <= -2 ? (uint32_t)SPK_NT_PAST : kSpecPast)) break;
+        if (!L || past >= kNPast<NS>) break;
       }
       x += L;
     }
