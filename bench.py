@@ -249,10 +249,14 @@ class VecWorkload:
             if self.cd.L.dev.trivial:  # one shift_copy per phase: records <-> body
                 return {"shift_copy_kernel": 4 * rb}
             if any(op[0] & 0xFF in (5, 7, 8, 9, 10, 11) for op in self.cd.L.dev.ops):
-                # op-list interpreter (nested layouts): the encode writes each
-                # record's bytes; the chunked decode reads the wire to guess and
-                # walk the chunks, then again to write records + heaps
-                return {"nest_write": rb + wb, "nest_cemit": wb + rb, "nest_cspec": wb}
+                # nested layouts: the encode's window pass writes each record's
+                # bytes; the decode is the tile pipeline with the nested walker
+                # (K1 reads the wire, K4 reads it again and writes records +
+                # element records + heaps); the chunked interpreter's kernels
+                # for layouts the tile decoder does not take
+                return {"nest_write_win": rb + wb, "nest_write": rb + wb,
+                        "vec_tile_emit": wb + rb, "vec_tile_spec": wb,
+                        "nest_cemit": wb + rb, "nest_cspec": wb}
             # wait-free tile decoder: K1 reads the wire once, K4 reads it again
             # and writes the records + heaps
             return {"var_encode_write": rb + wb, "vec_tile_emit": wb + rb,

@@ -55,7 +55,11 @@
 #define SPK_NT_REACH 4096
 #endif
 #ifndef SPK_NT_PAST   // records a nested speculative walk checks past its chunk
-#define SPK_NT_PAST 2
+// (0: none. Nested starts are screened well enough that the in-wave
+// resolution catches the few wrong ones: cm K1 11.1 -> 9.8 ms; flat layouts
+// keep 2 -- without the past walks C3 / C4 / cv tiles go wrong by the
+// thousand and the sequential fixer takes 0.1-0.5 s)
+#define SPK_NT_PAST 0
 #endif
 #ifndef SPK_NT_SCR2   // nested candidate starts screened on a second count
 #define SPK_NT_SCR2 1
@@ -2768,23 +2772,24 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
 }
 
 // ---- K1 ----------------------------------------------------------------------
-template <int NS>
-__global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkProg P,
-                                                                const uint8_t *__restrict__ wire,
-                                                                const uint8_t *__restrict__ ws,
-                                                                TileBufs TB, uint32_t dbg) {
-  __shared__ v4u_t win_s[kDecWaves][kTileVec + 1];
+// W: the count width as a compile-time constant (0: read from the header at
+// run time). The walkers' count reads, screens and bounds checks then carry
+// no width switch: nested walks are divergent loops, so every branch of the
+// switch cost each step its scalar branch code
+template <int NS, uint32_t W>
+__device__ __forceinline__ void vec_tile_spec_body(const DecArgs &a, const WalkProg &P,
+                                                   const uint8_t *__restrict__ wire,
+                                                   const uint8_t *__restrict__ ws,
+                                                   const TileBufs &TB, uint32_t dbg,
+                                                   v4u_t *win, uint64_t t, uint32_t lane) {
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t t = (uint64_t)blockIdx.x * kDecWaves + wv;
-  if (t >= TB.ntiles || !vec_live(c)) return;  // wave-uniform
   const uint64_t tclk0 = (dbg & 4096) ? __builtin_readcyclecounter() : 0;
   nt_prologue<NS>(a, lane);
-  const uint32_t w = c->w;
+  const uint32_t w = W ? W : c->w;
   const uint64_t len = a.wire_len, p0 = c->p0;
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
   const uint64_t ts = p0 + t * kTileBytes;
-  const TileView tv = stage_tile(win_s[wv], wire, len, ts, w, lane);
+  const TileView tv = stage_tile(win, wire, len, ts, w, lane);
   const WinReader &rd = tv.rd;
   const uint64_t wend = tv.wend;
   const uint64_t cs = ts + (uint64_t)lane * kTChunk;
@@ -2873,6 +2878,31 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
     al[0] = lane < nalt ? alt_e : kNoPos;
     al[1] = alt_c;
     QFOR(q) al[2 + q] = alt_s[q];
+  }
+}
+
+#ifndef SPK_WSPEC  // 1: K1 of the nested walk program per count width; 2: every layout
+#define SPK_WSPEC 1
+#endif
+template <int NS>
+__global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkProg P,
+                                                                const uint8_t *__restrict__ wire,
+                                                                const uint8_t *__restrict__ ws,
+                                                                TileBufs TB, uint32_t dbg) {
+  __shared__ v4u_t win_s[kDecWaves][kTileVec + 1];
+  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t t = (uint64_t)blockIdx.x * kDecWaves + wv;
+  if (t >= TB.ntiles || !vec_live(c)) return;  // wave-uniform
+  if constexpr (SPK_WSPEC >= 2 || (SPK_WSPEC == 1 && NS == -3)) {
+    switch (c->w) {  // (uniform: the header's width)
+      case 1: vec_tile_spec_body<NS, 1>(a, P, wire, ws, TB, dbg, win_s[wv], t, lane); return;
+      case 2: vec_tile_spec_body<NS, 2>(a, P, wire, ws, TB, dbg, win_s[wv], t, lane); return;
+      case 4: vec_tile_spec_body<NS, 4>(a, P, wire, ws, TB, dbg, win_s[wv], t, lane); return;
+      default: vec_tile_spec_body<NS, 8>(a, P, wire, ws, TB, dbg, win_s[wv], t, lane); return;
+    }
+  } else {
+    vec_tile_spec_body<NS, 0>(a, P, wire, ws, TB, dbg, win_s[wv], t, lane);
   }
 }
 
