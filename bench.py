@@ -161,6 +161,19 @@ def cpu_baseline(case, n, param, algo_bytes, per="record"):
            "encode_s": full["median_encode_s"], "decode_s": full["median_decode_s"],
            "host": {"cpu_model": cpu_model(), "nproc": os.cpu_count(), "affinity": aff,
                     "cgroup_cpu_quota": cpu_quota(), "threads_used": threads}}
+    # the same run at the whole affinity mask (BASELINE.md section 3 says "all
+    # host cores"; the cgroup quota above still bounds what those threads get)
+    wide = run(n, aff, 5) if aff > threads else None
+    if wide:
+        wmed = wide["median_encode_s"] + wide["median_decode_s"]
+        out["full_affinity"] = {
+            "threads": aff,
+            "value": round(per_unit * n / wmed / 2**30, 3),
+            "best_gib_s": round(per_unit * n / (wide["encode_s"] + wide["decode_s"]) / 2**30, 3),
+            "mean_gib_s": round(per_unit * n / (wide["mean_encode_s"] + wide["mean_decode_s"])
+                                / 2**30, 3),
+            "note": f"{aff} threads (the affinity mask), median of 5 after a warmup; "
+                    f"cgroup quota {cpu_quota()} CPUs"}
     if one:
         out["single_thread_gib_s"] = round(
             per_unit * one["n"] / (one["median_encode_s"] + one["median_decode_s"]) / 2**30, 3)

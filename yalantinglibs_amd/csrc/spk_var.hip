@@ -61,6 +61,12 @@
 // thousand and the sequential fixer takes 0.1-0.5 s)
 #define SPK_NT_PAST 0
 #endif
+#ifndef SPK_SCAP      // K1's speculation caps from the message's first records (vec_hdr_sample)
+#define SPK_SCAP 3        // bit 0: on the speculative walks' records, bit 1: on the candidate screen
+#endif
+#ifndef SPK_SCAP_MUL      // a span's cap: this multiple of its largest sampled count
+#define SPK_SCAP_MUL 2
+#endif
 #ifndef SPK_NT_SCR2   // nested candidate starts screened on a second count
 #define SPK_NT_SCR2 1
 #endif
@@ -1143,6 +1149,11 @@ struct VCtl {
   uint32_t wl_n[kRoundsMax + 1];  // re-verification worklist length per round
   uint32_t pad_;
   uint64_t cap;                // chunk capacity: stride of the per-span chunk arrays
+  // K1's speculation caps (vec_hdr_sample): the largest count per span a
+  // speculative walk accepts, from the counts of the message's first records;
+  // spec_c0 is the first-count screen under them
+  uint64_t scap[kVS];
+  uint64_t spec_c0;
 };
 
 // control words of the tile vector decoder (vec_tile_*)
@@ -1310,10 +1321,13 @@ __device__ __forceinline__ uint64_t wlen(const WalkProg &P, const uint8_t *wire,
 }
 
 // wlen() with the count fields read through `rd`
-template <int NS, typename Rd>
+// CAPS: while `tight`, the per-span count limits are K1's speculation caps
+// scap[] (VCtl, wave-uniform scalar loads) instead of P.cmax
+template <int NS, typename Rd, bool CAPS = false>
 __device__ __forceinline__ uint64_t wlen_rd(const WalkProg &P, const Rd &rd, uint64_t len,
                                             uint64_t pos, uint32_t w, uint64_t *cnt = nullptr,
-                                            uint64_t reach = 0) {
+                                            uint64_t reach = 0, const uint64_t *scap = nullptr,
+                                            bool tight = false) {
   if constexpr (NS <= -2) return nt_len<NS == -3>(rd, len, pos, cnt, reach, ~0u);
   uint64_t p = pos + P.skip[0];
   const uint32_t ns = NS > 0 ? (uint32_t)NS : P.ns;
@@ -1327,7 +1341,7 @@ __device__ __forceinline__ uint64_t wlen_rd(const WalkProg &P, const Rd &rd, uin
     const uint64_t c = opt ? (uint64_t)(rd.byte(p) != 0) : rd(p);
     p += pw;
     if (c) {
-      if (c > P.cmax[k]) return 0;
+      if (c > (CAPS && tight ? scap[k] : P.cmax[k])) return 0;
       const uint64_t nb = c * P.esz[k];
       if (nb > len - p) {
         if (!opt) return 0;  // OPTION: value unreadable, reader stays (opt_nb)
@@ -1354,10 +1368,9 @@ struct GReader {
   }
 };
 
-__global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
-                               uint8_t *__restrict__ ws, spk_dresult_t *res, uint32_t lp,
-                               uint64_t cap) {
-  if (threadIdx.x != 0) return;
+__device__ void vec_hdr_body(const DecArgs &a, const uint8_t *__restrict__ wire,
+                             uint8_t *__restrict__ ws, spk_dresult_t *res, uint32_t lp,
+                             uint64_t cap) {
   VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
   uint64_t pos = 0, dl = 0;
   uint32_t w = a.body_w;
@@ -1423,6 +1436,11 @@ __global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
   r.width = w;
   r.count = c->n;
   *res = r;
+}
+__global__ void vec_hdr_kernel(DecArgs a, const uint8_t *__restrict__ wire,
+                               uint8_t *__restrict__ ws, spk_dresult_t *res, uint32_t lp,
+                               uint64_t cap) {
+  if (threadIdx.x == 0) vec_hdr_body(a, wire, ws, res, lp, cap);
 }
 
 struct VecBufs {
@@ -2098,12 +2116,13 @@ __device__ uint64_t nt_len(const Rd &rd, uint64_t len, uint64_t pos, uint64_t *c
 // the speculative walk's record length (a nested walk is bounded)
 template <int NS, typename Rd>
 __device__ __forceinline__ uint64_t wlen_spec(const WalkProg &P, const Rd &rd, uint64_t len,
-                                              uint64_t pos, uint32_t w, uint64_t *cnt) {
+                                              uint64_t pos, uint32_t w, uint64_t *cnt,
+                                              const uint64_t *scap, bool tight) {
   if constexpr (NS <= -2) {
     const uint64_t l = nt_len<NS == -3>(rd, len, pos, cnt, (uint64_t)kPlaus + 1, kNTSpecElems);
     return l == kLenLimit ? (uint64_t)kPlaus + 1 : l;  // too long for a plausible start
   }
-  return wlen_rd<NS>(P, rd, len, pos, w, cnt);
+  return wlen_rd<NS, Rd, (SPK_SCAP & 1) != 0>(P, rd, len, pos, w, cnt, 0, scap, tight);
 }
 // payload of a SPAN into its heap slots (long ones queued for vec_big_copy)
 __device__ __forceinline__ void nt_put_payload(const WinReader &rd, uint8_t *hp, uint64_t pos,
@@ -2564,7 +2583,8 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
                                                       uint64_t wend, uint64_t cs, uint64_t ce,
                                                       uint32_t lane, bool exact0, uint64_t p0,
                                                       uint32_t dbg, TileLane<NS> &st,
-                                                      uint32_t *stat = nullptr) {
+                                                      uint32_t *stat = nullptr,
+                                                      const VCtl *sc = nullptr) {
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
   uint64_t &used = st.used, &ex = st.ex, &term_at = st.term_at;
   uint32_t &cnt = st.cnt;
@@ -2577,6 +2597,21 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
   QFOR(q) sums[q] = 0;
   const bool exact = exact0 && lane == 0;  // the payload start: no search
   sp.np = 0;
+  // speculation caps (flat layouts, sc: vec_hdr_sample's): a candidate start
+  // and every record of its walk must keep each count within the caps, so
+  // walks from false starts (a 1-byte count accepts any byte under P.cmax)
+  // die within a record or two; a chunk with no start under them is searched
+  // again with the layout's own limits
+  const uint64_t *scap = nullptr;
+  uint64_t c0t = P.c0max;
+  bool tight = false;
+  if constexpr (NS > -2) {
+    if (sc && !(dbg & 65536)) {
+      tight = true;
+      if (SPK_SCAP & 2) c0t = sc->spec_c0;
+      if (SPK_SCAP & 1) scap = sc->scap;
+    }
+  }
   // ---- 1. speculative walk of this lane's chunk ----
   if (cs < len && !(dbg & 8)) {
     uint64_t tt = 0, x = cs, past = 0, sx = exact ? cs : kNoPos;
@@ -2585,6 +2620,7 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
     uint64_t ksum[NS > 0 ? NS : kVS];
     QFOR(q) ksum[q] = 0;
     const uint32_t s0 = P.skip[0];
+    for (;;) {
     while (!done) {
       if (searching) {
         const uint64_t b0 = cs + tt + s0;  // first count field of candidate cs+tt
@@ -2602,7 +2638,7 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
               }
               q += l + P.vafter[j];
             }
-            if (ok) ok = (q + w <= len ? rd(q) : ~0ull) <= P.c0max;
+            if (ok) ok = (q + w <= len ? rd(q) : ~0ull) <= c0t;
             m |= (ok ? 1u : 0u) << kk;
           }
         } else if (b0 + 20 <= wend) {
@@ -2620,13 +2656,13 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
             if (w == 8)
               cv |= (uint64_t)__builtin_amdgcn_alignbyte(wd[(kk >> 2) + 2], wd[(kk >> 2) + 1], kk & 3)
                     << 32;
-            m |= (cv <= P.c0max ? 1u : 0u) << kk;
+            m |= (cv <= c0t ? 1u : 0u) << kk;
           }
         } else {
           for (int kk = 0; kk < 8; ++kk) {
             const uint64_t q = b0 + kk;
             const uint64_t cv = q + w <= len ? rd(q) : ~0ull;
-            m |= (cv <= P.c0max ? 1u : 0u) << kk;
+            m |= (cv <= c0t ? 1u : 0u) << kk;
           }
         }
         if (P.pf_all) m = 0xFFu;  // first span an OPTION / no span: any byte may start a record
@@ -2665,7 +2701,7 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
       // (the exact start of tile 0 walks unbounded: its records may be long)
       const uint64_t L = x >= len ? 0
                          : exact  ? wlen_rd<NS>(P, rd, len, x, w, rc)
-                                  : wlen_spec<NS>(P, rd, len, x, w, rc);
+                                  : wlen_spec<NS>(P, rd, len, x, w, rc, scap, tight);
       if (stat) ++stat[2];
       if (!exact && ((L == 0 && x < len) || L > kPlaus)) {  // off the record grid
         if (stat) ++stat[3];
@@ -2695,6 +2731,15 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
         if (!L || past >= kNPast<NS>) break;
       }
       x += L;
+    }
+    if (sx != kNoPos || !tight) break;
+    // no start under the caps in this chunk: search it again without them
+    tight = false;
+    c0t = P.c0max;
+    tt = 0;
+    x = cs;
+    searching = true;
+    done = false;
     }
     if (sx != kNoPos) {
       used = sx;
@@ -2798,7 +2843,8 @@ __device__ __forceinline__ void vec_tile_spec_body(const DecArgs &a, const WalkP
   TileLane<NS> st;
   uint32_t stat[6] = {0, 0, 0, 0, 0, 0};
   const uint64_t X = tile_spec_resolve<NS>(P, rd, len, w, ts, wend, cs, ce, lane, t == 0 && !rng,
-                                           p0, dbg, st, (dbg & 4096) ? stat : nullptr);
+                                           p0, dbg, st, (dbg & 4096) ? stat : nullptr,
+                                           (NS > -2 && SPK_SCAP) ? c : nullptr);
   if (dbg & 4096) {  // K1 statistics (scripts/diag_tiles.py)
     FCtl *fcd = reinterpret_cast<FCtl *>(const_cast<uint8_t *>(ws) + kWsFCtl);
     for (uint32_t k = 0; k < 6; ++k) {
@@ -2909,6 +2955,65 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
 // tile t's entry: tile t-1's published exit (tile 0: the payload start)
 __device__ __forceinline__ uint64_t tile_entry(const TileBufs &TB, const FCtl *fc, uint64_t t) {
   return t == 0 ? fc->entry0 : TB.fn[(t - 1) * kFnWords];
+}
+
+// K1's speculation caps (VCtl::scap), after the header: one wave stages the first 4 KiB of the
+// records from tile 0's entry in LDS and lane 0 walks up to kSampRecs of them;
+// a span's cap is twice its largest count there (at least 15), never above
+// the layout's own limit. The caps only steer the speculation (a chunk with
+// no start under them is searched without them; the true walks of the
+// resolution, repair and emit passes never see them), so a message whose
+// later records have longer containers decodes the same, a little slower.
+constexpr uint32_t kSampVec = 4096 / 16;
+#ifndef SPK_SAMP_RECS
+#define SPK_SAMP_RECS 16
+#endif
+constexpr uint32_t kSampRecs = SPK_SAMP_RECS;
+template <int NS>
+__global__ __launch_bounds__(64) void vec_hdr_sample(DecArgs a, WalkProg P,
+                                                     const uint8_t *__restrict__ wire,
+                                                     uint8_t *__restrict__ ws,
+                                                     spk_dresult_t *res) {
+  __shared__ v4u_t win[kSampVec + 1];
+  if (threadIdx.x == 0) vec_hdr_body(a, wire, ws, res, 0u, (uint64_t)0);
+  __syncthreads();
+  VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
+  const FCtl *fc = reinterpret_cast<const FCtl *>(ws + kWsFCtl);
+  const uint32_t lane = threadIdx.x, nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  const uint64_t len = a.wire_len, x0 = fc->entry0;
+  const uint32_t w = c->w;
+  uint64_t mx[NS > 0 ? NS : kVS];
+  QFOR(q) mx[q] = 0;
+  uint32_t got = 0;
+  if (vec_live(c) && x0 < len && !P.pf_all) {  // (wave-uniform)
+    const TileView tv = stage_win<kSampVec>(win, wire, len, x0, w, lane);
+    if (lane == 0) {
+      const uint64_t n = c->n < kSampRecs ? c->n : kSampRecs;
+      uint64_t x = x0;
+      for (uint64_t i = 0; i < n && x + 64 <= tv.wend; ++i) {
+        uint64_t rc[NS > 0 ? NS : kVS];
+        const uint64_t L = wlen_rd<NS>(P, tv.rd, len, x, w, rc);
+        if (!L) break;
+        QFOR(q) mx[q] = rc[q] > mx[q] ? rc[q] : mx[q];
+        ++got;
+        x += L;
+      }
+    }
+  }
+  if (lane == 0) {
+    uint64_t c0 = P.c0max;
+    QFOR(q) {
+      uint64_t cp = P.cmax[q];
+      if (got && !((P.optm >> q) & 1u)) {
+        const uint64_t t = mx[q] < (1ull << 60) ? SPK_SCAP_MUL * mx[q] : ~0ull;
+        cp = t < 15 ? 15 : t;
+        if (cp > P.cmax[q]) cp = P.cmax[q];
+        if (q == 0 && cp < c0) c0 = cp;
+      }
+      c->scap[q] = cp;
+    }
+    c->spec_c0 = c0;
+  }
 }
 
 // range mode, entry unknown: tile 0 assumes its own speculated entry
@@ -4006,7 +4111,10 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
     return hipGetLastError();
   }
   if (phase != kTilesEmit) {
-  SPK_LAUNCH(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, 0u, (uint64_t)0);
+  if (NS > -2 && SPK_SCAP)  // (the header, then K1's speculation caps)
+    SPK_LAUNCH(vec_hdr_sample<NS <= -2 ? 0 : NS>, dim3(1), dim3(64), 0, s, a, P, wire, ws, d_res);
+  else
+    SPK_LAUNCH(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, 0u, (uint64_t)0);
   SPK_LAUNCH(vec_tile_spec<NS>, dim3(grid_for(f.ntiles, kDecWaves)), dim3(64 * kDecWaves), 0, s,
              a, P, wire, (const uint8_t *)ws, TB, tile_dbg());
   if (tile_dbg() & 8192) return hipGetLastError();  // (A/B timing of K1 alone)
