@@ -347,6 +347,42 @@ def test_long_records_bounded_time(kind):
         assert r.tiles_sequential + r.tiles_repaired > 0
 
 
+@pytest.mark.parametrize("tail", ["long", "mixed"])
+def test_speculation_caps_mispredicted(tail):
+    """K1's speculation caps come from the first records (vec_hdr_sample):
+    here those are 0-2 byte strings (caps 15) and every later record is far
+    longer ("long": 100-3000 B, so no true record fits the caps; "mixed":
+    every 7th). The speculative walks reject the true records, chunks with no
+    start under the caps are searched again without them, the resolution
+    walks never see the caps: bit-exact with the oracle, in bounded time."""
+    cd = codec_for("recs")
+    rng = np.random.default_rng(23)
+    n = 40000
+    lens = rng.integers(0, 3, n)
+    if tail == "long":
+        lens[64:] = rng.integers(100, 3000, n - 64)
+    else:
+        lens[64::7] = rng.integers(100, 3000, len(lens[64::7]))
+    recs, heaps = _recs_with_lens(lens, 24)
+    exp, _, _ = H.oracle_encode(cd.L, C.SPK_MODE_VECTOR, recs, heaps)
+    w = wire_dev(exp)
+    res, back, _ = cd.deserialize(w, C.SPK_MODE_VECTOR)
+    assert res.errc == 0 and res.count == n and res.consumed == len(exp)
+    assert back.recs.cpu().numpy().tobytes() == np.ascontiguousarray(recs).view(np.uint8).tobytes()
+    assert back.heaps[0][:len(heaps[0])].cpu().numpy().tobytes() == heaps[0].tobytes()
+    ts = []
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        cd.deserialize_to(back, w, C.SPK_MODE_VECTOR)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    assert cd.result().errc == 0
+    print(f"{tail}: {len(exp) / 1e6:.1f} MB decoded in {min(ts):.3f} ms")
+    assert min(ts) < 5.0 + len(exp) / 4e6, ts
+
+
 def test_screen_defeating_payload_bounded_time():
     """Strings whose bytes are themselves a valid record stream (slices of an
     encoded vector<RecS> body at arbitrary offsets): every tile inside such a
