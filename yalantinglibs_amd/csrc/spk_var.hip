@@ -64,6 +64,9 @@
 #ifndef SPK_SCAP      // K1's speculation caps from the message's first records (vec_hdr_sample)
 #define SPK_SCAP 3        // bit 0: on the speculative walks' records, bit 1: on the candidate screen
 #endif
+#ifndef SPK_SCAP_MINR     // ... applied only when the layout's first-count limit is this many times the cap
+#define SPK_SCAP_MINR 32
+#endif
 #ifndef SPK_SCAP_MUL      // a span's cap: this multiple of its largest sampled count
 #define SPK_SCAP_MUL 2
 #endif
@@ -3001,6 +3004,14 @@ __global__ __launch_bounds__(64) void vec_hdr_sample(DecArgs a, WalkProg P,
     }
   }
   if (lane == 0) {
+    // caps only where they tighten the first-count screen by SPK_SCAP_MINR x
+    // or more: a screen already that selective gains nothing from them (C4:
+    // 511 vs 32 measured slower with them; C3 4092 vs ~96, cv 4096 vs 32 faster)
+    {
+      uint64_t t0 = mx[0] < (1ull << 60) ? SPK_SCAP_MUL * mx[0] : ~0ull;
+      t0 = t0 < 15 ? 15 : t0;
+      if ((P.optm & 1u) || (uint64_t)P.c0max < (uint64_t)SPK_SCAP_MINR * t0) got = 0;
+    }
     uint64_t c0 = P.c0max;
     QFOR(q) {
       uint64_t cp = P.cmax[q];
