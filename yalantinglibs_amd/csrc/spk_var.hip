@@ -1182,6 +1182,7 @@ struct FCtl {
   unsigned long long diag[8];    // SPK_TILE_DBG & 4096: K1 statistics (scripts/diag_tiles.py)
 };
 constexpr size_t kWsFCtl = kWsCtl + 1280;
+static_assert(sizeof(VCtl) <= kWsFCtl - kWsCtl, "VCtl overlaps FCtl");
 static_assert(kWsFCtl + sizeof(FCtl) <= kWsScratch, "FCtl overlaps the scratch area");
 
 // Compact walk program of a record: fixed bytes, then per span
