@@ -355,9 +355,9 @@ def test_speculation_caps_mispredicted(tail):
     every 7th). The speculative walks reject the true records, chunks with no
     start under the caps are searched again without them, the resolution
     walks never see the caps: bit-exact with the oracle. The caps are a
-    build option (SPK_SCAP, off by default); with them this message takes
-    ~35 ms (the mispredicted speculation leaves broken tiles to the repair
-    passes), without them a few ms: the bound only rules out per-record
+    build option (SPK_SCAP, off by default); this message takes ~35 ms with
+    and without them (its random-byte strings defeat the speculation, the
+    repair passes resolve those tiles): the bound only rules out per-record
     sequential work."""
     cd = codec_for("recs")
     rng = np.random.default_rng(23)

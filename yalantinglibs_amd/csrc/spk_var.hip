@@ -63,8 +63,7 @@
 #endif
 #ifndef SPK_SCAP      // K1's speculation caps from the message's first records (vec_hdr_sample)
 // (default off: see DESIGN section 6.1 -- C3 / cv K1 faster with them, but
-// their per-lane fallback costs C4's K1 15 % even where no cap applies, and
-// a message whose first records mispredict the rest decodes ~15x slower)
+// their per-lane fallback costs C4's K1 15 % even where no cap applies)
 #define SPK_SCAP 0        // bit 0: on the speculative walks' records, bit 1: on the candidate screen
 #endif
 #ifndef SPK_SCAP_MINR     // ... applied only when the layout's first-count limit is this many times the cap
