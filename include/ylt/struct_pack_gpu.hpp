@@ -533,9 +533,10 @@ err_code decode_one(T &t, const char *data, std::size_t size, std::size_t &consu
   device::copy(wire.data(), data, size, SPK_COPY_H2D, c.stream());
   std::size_t cap = tr::vector ? size / c.min_record_wire() + 1 : 1;
   for (;;) {
-    // the capacities are upper bounds by construction (every record takes at
-    // least min_record_wire bytes, no heap exceeds the wire); the loop only
-    // guards that invariant and never surfaces a non-reference errc
+    // the capacities bound every decodable message (min_record_wire is a
+    // lower bound on a record's wire bytes, fast-varint groups counted as
+    // their bitset; no heap exceeds the wire); the loop only guards that
+    // invariant and never surfaces a non-reference errc
     auto b = c.alloc_for_wire(size, cap);
     spk_dresult_t r;
     if constexpr (tr::vector) {

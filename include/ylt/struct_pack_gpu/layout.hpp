@@ -344,10 +344,14 @@ inline std::vector<uint64_t> heap_caps_for_wire(const spk_layout &L, uint64_t wi
   }
   return caps;
 }
+// Fewest wire bytes of one top-level record: a container count or an
+// optional / variant tag >= 1 byte, compatible members none, and the
+// record's fast-varint group only its bitset of ceil((n + 2) / 8) bytes (zero
+// members take no bytes, packer.hpp:193-212). A true lower bound, so the
+// record capacity wire_len / min + 1 holds every decodable message.
 inline uint64_t min_record_wire_bytes(const spk_layout &L) {
-  uint64_t total = 0;
-  uint32_t open = 0;  // groups (and ARRAY elements) the walk is inside
-  uint32_t stack[SPK_MAX_OPS], sp = 0;
+  uint64_t total = 0, n_fvar = 0;
+  uint32_t stack[SPK_MAX_OPS], sp = 0;  // groups (and ARRAY elements) open
   for (uint32_t i = 0; i < L.n_ops; ++i) {
     const spk_op &o = L.ops[i];
     const uint32_t k = SPK_OP_KIND(o.kind);
@@ -355,11 +359,12 @@ inline uint64_t min_record_wire_bytes(const spk_layout &L) {
       if (--stack[sp - 1] == 0) --sp;
       continue;
     }
-    open = sp;
-    if (!open && k != SPK_OP_COMPAT && k != SPK_OP_CGROUP)
+    if (!sp && k == SPK_OP_FVAR) ++n_fvar;
+    else if (!sp && k != SPK_OP_COMPAT && k != SPK_OP_CGROUP)
       total += k == SPK_OP_COPY ? o.size : 1;
     if (op_groups(o)) stack[sp++] = op_groups(o);
   }
+  if (n_fvar) total += (n_fvar + 2 + 7) / 8;
   return total ? total : 1;
 }
 

@@ -11,7 +11,7 @@ for r in $(seq ${REPS:-2}); do
   for v in old new; do
     cp ab/$v.so $LIB
     for c in ${CONFIGS:-c3 c4}; do
-      timeout -k 10 300 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/ab_$v_$c.log 2>&1 || { echo "bench failed"; tail -5 gpurun_out/ab_$v_$c.log; cp ab/current.so $LIB; exit 1; }
+      timeout -k 10 300 python bench.py --full-line --no-host-path --config $c --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/ab_$v_$c.log 2>&1 || { echo "bench failed"; tail -5 gpurun_out/ab_$v_$c.log; cp ab/current.so $LIB; exit 1; }
       tail -1 gpurun_out/ab_$v_$c.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v', '$c', d['ms_per_step'], d.get('phase_ms'))"
     done
   done

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 C=${CFG:-cm}
 for v in ${DBGS:-0 32 48 56}; do
-  SPK_TILE_DBG=$v timeout -k 10 300 python bench.py --config $C --steps 5 --warmup 1 --no-extra --no-cpu-baseline > gpurun_out/abd_$C.log 2>&1 || { echo "fail $v"; tail -5 gpurun_out/abd_$C.log; exit 1; }
+  SPK_TILE_DBG=$v timeout -k 10 300 python bench.py --full-line --no-host-path --config $C --steps 5 --warmup 1 --no-extra --no-cpu-baseline > gpurun_out/abd_$C.log 2>&1 || { echo "fail $v"; tail -5 gpurun_out/abd_$C.log; exit 1; }
   python - $C "$v" <<'PY'
 import json,sys
 d=json.loads(open(f'gpurun_out/abd_{sys.argv[1]}.log').read().strip().splitlines()[-1])

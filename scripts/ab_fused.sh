@@ -4,7 +4,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 for v in "SPK_FUSED=0" "SPK_FUSED=1" "SPK_FUSED=1 SPK_TILE_DBG=1024" "SPK_FUSED=1 SPK_TILE_DBG=2048" "SPK_FUSED=1 SPK_TILE_DBG=3072"; do
   for c in c3 c4; do
-    env $v timeout -k 10 300 python bench.py --config $c --steps 10 --warmup 2 --no-extra --no-cpu-baseline > gpurun_out/ab_$c.log 2>&1 || { echo "fail $v $c"; tail -5 gpurun_out/ab_$c.log; exit 1; }
+    env $v timeout -k 10 300 python bench.py --full-line --no-host-path --config $c --steps 10 --warmup 2 --no-extra --no-cpu-baseline > gpurun_out/ab_$c.log 2>&1 || { echo "fail $v $c"; tail -5 gpurun_out/ab_$c.log; exit 1; }
     python - $c "$v" <<'PY'
 import json,sys
 d=json.loads(open(f'gpurun_out/ab_{sys.argv[1]}.log').read().strip().splitlines()[-1])

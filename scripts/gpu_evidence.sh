@@ -18,17 +18,17 @@ step() { local name=$1; shift; local t=$1; shift
 if [ -z "$SKIP_PMC" ]; then
   for c in ${PMC_CONFIGS:-c2 c2b c3 c4 cv c5 cm}; do
     for ctr in FETCH_SIZE WRITE_SIZE; do
-      step pmc_${c}_$ctr 300 rocprofv3 --pmc $ctr -d $OUT/pmc_${c}_$ctr -o run --output-format csv -- python bench.py --config $c --steps 3 --warmup 1 --settle 0 --no-cpu-baseline --no-extra
+      step pmc_${c}_$ctr 300 rocprofv3 --pmc $ctr -d $OUT/pmc_${c}_$ctr -o run --output-format csv -- python bench.py --full-line --no-host-path --config $c --steps 3 --warmup 1 --settle 0 --no-cpu-baseline --no-extra
     done
     python scripts/pmc_summary.py $c $OUT > $OUT/pmc_$c.json || exit 1
     rm -rf $OUT/pmc_${c}_FETCH_SIZE $OUT/pmc_${c}_WRITE_SIZE
   done
 fi
-[ -n "$SKIP_BENCH" ] || step bench 900 python bench.py --host-path --pmc-dir ${PMC_DIR:-$OUT}
+[ -n "$SKIP_BENCH" ] || step bench 900 python bench.py --pmc-dir ${PMC_DIR:-$OUT}
 PROF_CONFIGS=${PROF_CONFIGS:-c2 c2b c3 c4 cv c5 cm}
 [ "$PROF_CONFIGS" = none ] && PROF_CONFIGS=""
 for c in $PROF_CONFIGS; do
-  step prof_$c 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o run --output-format csv -- python bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline --no-extra
+  step prof_$c 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o run --output-format csv -- python bench.py --full-line --no-host-path --config $c --steps 5 --warmup 1 --no-cpu-baseline --no-extra
   cp $OUT/prof_$c/run_kernel_stats.csv $OUT/${c}_kernel_stats.csv 2>/dev/null || find $OUT/prof_$c -name "*kernel_stats.csv" -exec cp {} $OUT/${c}_kernel_stats.csv \;
   rm -rf $OUT/prof_$c
 done

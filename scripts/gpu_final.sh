@@ -16,7 +16,7 @@ step() { local name=$1; shift; local t=$1; shift
 [ -n "$SKIP_TESTS" ] || step pytest_gpu 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/
 for c in $CH; do
   for ctr in FETCH_SIZE WRITE_SIZE; do
-    step pmc_${c}_$ctr 300 rocprofv3 --pmc $ctr -d $OUT/pmc_${c}_$ctr -o run --output-format csv -- python bench.py --config $c --steps 3 --warmup 1 --settle 0 --no-cpu-baseline --no-extra
+    step pmc_${c}_$ctr 300 rocprofv3 --pmc $ctr -d $OUT/pmc_${c}_$ctr -o run --output-format csv -- python bench.py --full-line --no-host-path --config $c --steps 3 --warmup 1 --settle 0 --no-cpu-baseline --no-extra
   done
   python scripts/pmc_summary.py $c $OUT > $OUT/pmc_$c.json || exit 1
   rm -rf $OUT/pmc_${c}_FETCH_SIZE $OUT/pmc_${c}_WRITE_SIZE
@@ -24,9 +24,9 @@ done
 for f in profiles/$ROUND/pmc_*.json; do
   b=$(basename $f); [ -e $OUT/$b ] || cp $f $OUT/$b
 done
-step bench 1000 python bench.py --host-path --pmc-dir $OUT
+step bench 1000 python bench.py --pmc-dir $OUT
 for c in $CH; do
-  step prof_$c 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o run --output-format csv -- python bench.py --config $c --steps 5 --warmup 1 --no-cpu-baseline --no-extra
+  step prof_$c 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$c -o run --output-format csv -- python bench.py --full-line --no-host-path --config $c --steps 5 --warmup 1 --no-cpu-baseline --no-extra
   find $OUT/prof_$c -name "*kernel_stats.csv" -exec cp {} $OUT/${c}_kernel_stats.csv \;
   rm -rf $OUT/prof_$c
 done

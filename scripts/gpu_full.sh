@@ -11,7 +11,7 @@ step() { local name=$1; shift; local t=$1; shift
 [ -n "$SKIP_SLOW" ] || step pytest_slow 1200 python -m pytest tests -x -q -m "gpu and slow"
 step probe_bw 300 python scripts/probe_bw.py
 for c in ${CONFIGS:-c2 c2b c3 c4}; do
-  step bench_$c 600 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline
+  step bench_$c 600 python bench.py --full-line --no-host-path --config $c --steps 10 --warmup 2 --no-cpu-baseline
 done
 rm -rf gpurun_out/prof_c2
-step rocprof_c2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2 -o run --output-format csv -- python bench.py --config c2 --steps 10 --warmup 2 --no-cpu-baseline
+step rocprof_c2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2 -o run --output-format csv -- python bench.py --full-line --no-host-path --config c2 --steps 10 --warmup 2 --no-cpu-baseline

@@ -8,6 +8,6 @@ mkdir -p gpurun_out
 CFG=${CFG:-c2}
 for ctr in FETCH_SIZE WRITE_SIZE; do
   rm -rf gpurun_out/pmc_${CFG}_$ctr
-  timeout -k 10 600 rocprofv3 --pmc $ctr -d gpurun_out/pmc_${CFG}_$ctr -o run --output-format csv -- python bench.py --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --no-extra --settle 0 > gpurun_out/pmc_${CFG}_$ctr.log 2>&1 || { echo "pmc $ctr failed"; tail -20 gpurun_out/pmc_${CFG}_$ctr.log; exit 1; }
+  timeout -k 10 600 rocprofv3 --pmc $ctr -d gpurun_out/pmc_${CFG}_$ctr -o run --output-format csv -- python bench.py --full-line --no-host-path --config $CFG --steps 3 --warmup 1 --no-cpu-baseline --no-extra --settle 0 > gpurun_out/pmc_${CFG}_$ctr.log 2>&1 || { echo "pmc $ctr failed"; tail -20 gpurun_out/pmc_${CFG}_$ctr.log; exit 1; }
 done
 python scripts/pmc_summary.py $CFG > gpurun_out/pmc_${CFG}.json && cat gpurun_out/pmc_${CFG}.json

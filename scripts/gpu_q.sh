@@ -9,7 +9,7 @@ if [ -n "$TESTS" ]; then
   tail -1 gpurun_out/pt.log
 fi
 for c in ${CONFIGS:-c3 c4}; do
-  timeout -k 10 300 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-extra $BENCH_ARGS > gpurun_out/q_$c.log 2>&1 || { echo "bench $c failed"; tail -5 gpurun_out/q_$c.log; exit 1; }
+  timeout -k 10 300 python bench.py --full-line --no-host-path --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-extra $BENCH_ARGS > gpurun_out/q_$c.log 2>&1 || { echo "bench $c failed"; tail -5 gpurun_out/q_$c.log; exit 1; }
 done
 for c in ${CONFIGS:-c3 c4}; do
 python - $c <<'PY'

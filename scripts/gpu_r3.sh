@@ -11,7 +11,7 @@ if [ -z "$SKIP_TESTS" ]; then
   tail -2 gpurun_out/pt.log
 fi
 for c in ${CONFIGS:-cm c5}; do
-  timeout -k 10 600 python bench.py --config $c --steps ${STEPS:-10} --warmup 2 --no-extra $BENCH_ARGS > gpurun_out/b_$c.log 2>&1 || { echo "bench $c failed"; tail -20 gpurun_out/b_$c.log; exit 1; }
+  timeout -k 10 600 python bench.py --full-line --no-host-path --config $c --steps ${STEPS:-10} --warmup 2 --no-extra $BENCH_ARGS > gpurun_out/b_$c.log 2>&1 || { echo "bench $c failed"; tail -20 gpurun_out/b_$c.log; exit 1; }
   python - $c <<'PY'
 import json,sys
 c=sys.argv[1]

@@ -754,15 +754,23 @@ def _walk_levels(dev: DeviceLayout):
 def min_record_wire_bytes(dev: DeviceLayout) -> int:
     """Fewest wire bytes one top-level record can take (each container count
     >= 1 byte; an absent optional / a variant's index 1 byte; compatible
-    members none: an older writer has none): bounds a decode's record
-    capacity by the wire length."""
+    members none: an older writer has none; the record's fast-varint group
+    only its bitset of ceil((n + 2) / 8) bytes, since zero members take no
+    bytes, packer.hpp:193-212): bounds a decode's record capacity by the
+    wire length."""
     from . import _capi as C
     total = 0
+    n_fvar = 0
     for (k, _, sz, _), arr, grp in _walk_levels(dev):
         k &= 0xFF
         if arr or grp or k in (C.SPK_OP_COMPAT, C.SPK_OP_CGROUP):
             continue
+        if k == C.SPK_OP_FVAR:
+            n_fvar += 1
+            continue
         total += sz if k == C.SPK_OP_COPY else 1
+    if n_fvar:
+        total += (n_fvar + 2 + 7) // 8
     return max(total, 1)
 
 

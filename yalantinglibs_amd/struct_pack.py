@@ -343,6 +343,11 @@ def _synth_multi(codec: Codec, k: int, n: int, seed: int, param: int, first: int
     (counts pass, exclusive scans per heap, fill pass)."""
     lib, dev, st = codec.lib, codec.device, _stream(stream)
     nh = len(codec.L.dev.spans)
+    # the device generator writes the Monster's 96-B records and its 6 heaps
+    # (csrc/spk_synth.hip kMonHeaps): any other layout would be written past
+    if k == C.SPK_SYNTH_MONSTER and (nh != 6 or codec.L.stride != 96):
+        raise ValueError(f"monster synth needs the Monster layout (6 heaps, 96-B records), "
+                         f"got {nh} heaps and stride {codec.L.stride}")
     cnt = torch.empty((nh, max(n, 1)), dtype=torch.int64, device=dev)
     Codec._check(lib.spk_synth_counts_ex(k, seed, first, n, param, _p(cnt), st),
                  "spk_synth_counts_ex")
