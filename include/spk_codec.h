@@ -584,6 +584,18 @@ int spk_decode_shard_emit(const spk_layout *L, const void *d_wire, uint64_t wire
 int32_t spk_parse_vector_header(const spk_layout *L, const void *h_wire, uint64_t len,
                                 uint64_t *n, uint32_t *width, uint32_t *header_len);
 
+/* Host-side: the header of ONE message of the layout's message type
+ * (fmt_one) at container width `width` into h_out (HOST memory): the whole
+ * message when the type has no payload bytes, e.g. std::monostate, the reply
+ * of a void coro_rpc handler (struct_pack_protocol.hpp:34-36; packer.hpp:
+ * 90-139,250-252). Returns its length, or a negative SPK_E_*. */
+int spk_message_header(const spk_layout *L, uint32_t width, uint8_t *h_out, uint32_t cap);
+/* Host-side: deserialize_metainfo of one message (fmt_one) in host memory
+ * (unpacker.hpp:548-619): reference errc (0 ok) or a negative SPK_E_*; on
+ * success *width and *header_len = bytes before the payload. */
+int32_t spk_parse_message_header(const spk_layout *L, const void *h_wire, uint64_t len,
+                                 uint32_t *width, uint32_t *header_len);
+
 /* Host-side: header + count prefix of a VECTOR message of total_n records at
  * `width` into h_out (HOST memory, capacity cap). Returns its length, or a
  * negative SPK_E_*. (packer.hpp:100-139) */

@@ -105,22 +105,41 @@ constexpr bool record_supported() {
     return false;
 }
 
-// the argument of serialize / deserialize_to: std::vector<R> / std::span<R>
-// (a VECTOR message) or a record R (one message)
-template <typename T>
-struct msg_traits {
-  static constexpr bool vector = false, record = record_supported<T>();
+// the argument of serialize / deserialize_to:
+//  * std::vector<R> / std::span<R> of records R: a VECTOR message;
+//  * a record R (aggregate, YLT_REFL type, std::pair, std::tuple -- the
+//    message of a multi-argument call --, fundamental, std::array): one
+//    MESSAGES message of R;
+//  * any other supported type M (std::string, a container of non-records, an
+//    optional, a variant, a map ...): one message of the record boxed<M>,
+//    whose payload bytes are M's, under M's type code (boxed = true);
+//  * std::monostate (the reply of a void handler, struct_pack_protocol.hpp:
+//    34-36): a message without payload, its header alone (empty = true).
+template <typename T, bool = record_supported<T>()>
+struct msg_traits_of {
+  static constexpr bool vector = false, record = true, boxed = false, empty = false;
   using rec = T;
 };
+template <typename T>
+struct msg_traits_of<T, false> {
+  static constexpr bool empty = is_monostate_v<T>;
+  static constexpr bool vector = false, record = empty || (supported<T>() && !is_compat_v<T>),
+                        boxed = !empty;
+  using rec = detail::boxed<T>;
+};
+template <typename T>
+struct msg_traits : msg_traits_of<T> {};
 template <typename R, typename A>
-struct msg_traits<std::vector<R, A>> {
-  static constexpr bool vector = record_supported<R>(), record = false;
-  using rec = R;
+struct msg_traits<std::vector<R, A>> : msg_traits_of<std::vector<R, A>> {
+  static constexpr bool vector = record_supported<R>(),
+                        record = !vector && msg_traits_of<std::vector<R, A>>::record,
+                        boxed = !vector;
+  using rec = std::conditional_t<vector, R, detail::boxed<std::vector<R, A>>>;
 };
 template <typename R, std::size_t E>
 struct msg_traits<std::span<R, E>> {
   static constexpr bool vector = E == std::dynamic_extent && record_supported<remove_cvref_t<R>>(),
-                        record = false;
+                        record = false, boxed = false, empty = false;
   using rec = remove_cvref_t<R>;
 };
 
@@ -477,6 +496,18 @@ concept byte_writer = requires(T &w, const char *p, std::size_t n) { w.write(p, 
 
 // One planned message of `t` staged on the device (plan + encode); the bytes
 // stay in `out` until copied to the caller.
+// the descriptor of a payload-free message type (std::monostate): only its
+// header shape (fmt_one) is used, by spk_message_header / _parse_
+template <typename M, uint64_t conf>
+const spk_layout &empty_message_layout() {
+  static const spk_layout L = [] {
+    spk_layout l = make_spk_layout<boxed<M>, conf>();
+    device::check(spk_layout_check(&l), "spk_layout_check");
+    return l;
+  }();
+  return L;
+}
+
 template <uint64_t conf, typename T>
 struct staged_message {
   using tr = msg_traits<remove_cvref_t<T>>;
@@ -484,17 +515,31 @@ struct staged_message {
   device::buffer out, offs;
   spk_plan_t plan{};
   std::size_t len = 0;
+  uint8_t hdr[4 + 1 + SPK_MAX_LITERAL + 1] = {};  // tr::empty: the whole message
 
   explicit staged_message(const T &t) {
-    auto &c = device::thread_codec<R, conf>();
-    if constexpr (tr::vector) {
+    if constexpr (tr::empty) {
+      const int n = spk_message_header(&empty_message_layout<remove_cvref_t<T>, conf>(), 1, hdr,
+                                       sizeof hdr);
+      if (n < 0) device::check(n, "spk_message_header");
+      len = static_cast<std::size_t>(n);
+    } else if constexpr (tr::vector) {
+      auto &c = device::thread_codec<R, conf>();
       auto b = c.upload(t.data(), t.size());
       plan = c.plan(b, SPK_MODE_VECTOR);
       len = plan.total_bytes;
       out.resize(len);
       c.encode(b, SPK_MODE_VECTOR, out.data(), out.size());
     } else {
-      auto b = c.upload(&t, 1);
+      auto &c = device::thread_codec<R, conf>();
+      auto b = [&] {
+        if constexpr (tr::boxed) {
+          const R box{t};  // the message as the one member of boxed<M>
+          return c.upload(&box, 1);
+        } else {
+          return c.upload(&t, 1);
+        }
+      }();
       plan = c.plan(b, SPK_MODE_MESSAGES);
       len = plan.total_bytes;
       out.resize(len);
@@ -503,9 +548,13 @@ struct staged_message {
     }
   }
   void copy_to(void *dst) {
-    auto &c = device::thread_codec<R, conf>();
-    device::copy(dst, out.data(), len, SPK_COPY_D2H, c.stream());
-    device::sync(c.stream());
+    if constexpr (tr::empty) {
+      std::memcpy(dst, hdr, len);
+    } else {
+      auto &c = device::thread_codec<R, conf>();
+      device::copy(dst, out.data(), len, SPK_COPY_D2H, c.stream());
+      device::sync(c.stream());
+    }
   }
 };
 
@@ -518,6 +567,9 @@ constexpr void check_message_type() {
                 "and nested records; use the reference's CPU struct_pack for anything else");
 }
 
+template <uint64_t conf, typename T>
+err_code decode_one_dev(T &t, const char *data, std::size_t size, std::size_t &consume_len);
+
 // decode of one message into t: VECTOR for std::vector<R>, one MESSAGES
 // message for a record. errc / consume_len as the reference
 // (struct_pack.hpp:326-357); `t` is left unchanged on an error.
@@ -527,8 +579,25 @@ err_code decode_one(T &t, const char *data, std::size_t size, std::size_t &consu
   using tr = msg_traits<T>;
   using R = typename tr::rec;
   static_assert(!std::is_same_v<T, std::span<R>>, "deserialize into std::vector<R>");
-  auto &c = device::thread_codec<R, conf>();
   consume_len = 0;
+  if constexpr (tr::empty) {  // the header is the whole message
+    uint32_t w = 0, hl = 0;
+    const int32_t e = spk_parse_message_header(&empty_message_layout<T, conf>(), data, size, &w,
+                                               &hl);
+    if (e < 0) device::check(e, "spk_parse_message_header");
+    if (e) return static_cast<errc>(e);
+    consume_len = hl;
+    return {};
+  } else {
+    return decode_one_dev<conf>(t, data, size, consume_len);
+  }
+}
+
+template <uint64_t conf, typename T>
+err_code decode_one_dev(T &t, const char *data, std::size_t size, std::size_t &consume_len) {
+  using tr = msg_traits<T>;
+  using R = typename tr::rec;
+  auto &c = device::thread_codec<R, conf>();
   device::buffer wire(size + 16);
   device::copy(wire.data(), data, size, SPK_COPY_H2D, c.stream());
   std::size_t cap = tr::vector ? size / c.min_record_wire() + 1 : 1;
@@ -562,6 +631,10 @@ err_code decode_one(T &t, const char *data, std::size_t size, std::size_t &consu
       T out(r.count);
       c.download(b, r.count, out.data());
       t = std::move(out);
+    } else if constexpr (tr::boxed) {
+      R box{};
+      c.download(b, 1, &box);
+      t = std::move(box.v);
     } else {
       c.download(b, 1, &t);
     }
@@ -576,22 +649,46 @@ err_code decode_one(T &t, const char *data, std::size_t size, std::size_t &consu
 // Reference-named entry points (host data in, host bytes out)
 // ===========================================================================
 
+namespace detail {
+template <uint64_t conf, typename T>
+serialize_buffer_size needed_size_dev(const T &t);
+}  // namespace detail
+
 // get_needed_size (struct_pack.hpp:131-135)
 template <uint64_t conf = sp_config::DEFAULT, typename T>
 serialize_buffer_size get_needed_size(const T &t) {
   detail::check_message_type<T>();
   using tr = detail::msg_traits<detail::remove_cvref_t<T>>;
+  serialize_buffer_size r;
+  if constexpr (tr::empty) {  // header only, no metainfo byte (no container)
+    detail::staged_message<conf, T> m(t);
+    r.len_ = m.len;
+    r.metainfo_ = m.len > 4 ? m.hdr[4] : 0;
+    return r;
+  } else {
+    return detail::needed_size_dev<conf>(t);
+  }
+}
+
+namespace detail {
+template <uint64_t conf, typename T>
+serialize_buffer_size needed_size_dev(const T &t) {
+  using tr = detail::msg_traits<detail::remove_cvref_t<T>>;
   using R = typename tr::rec;
+  serialize_buffer_size r;
   auto &c = device::thread_codec<R, conf>();
   spk_plan_t p;
   if constexpr (tr::vector) {
     auto b = c.upload(t.data(), t.size());
     p = c.plan(b, SPK_MODE_VECTOR);
+  } else if constexpr (tr::boxed) {
+    const R box{t};
+    auto b = c.upload(&box, 1);
+    p = c.plan(b, SPK_MODE_MESSAGES);
   } else {
     auto b = c.upload(&t, 1);
     p = c.plan(b, SPK_MODE_MESSAGES);
   }
-  serialize_buffer_size r;
   r.len_ = p.total_bytes;
   if constexpr (tr::vector) {
     r.metainfo_ = static_cast<unsigned char>(p.has_meta ? p.metainfo : 0);
@@ -606,6 +703,7 @@ serialize_buffer_size get_needed_size(const T &t) {
   }
   return r;
 }
+}  // namespace detail
 
 // serialize_to(Buffer& | Writer&, t): appends to a byte buffer or writes to
 // a writer (struct_pack.hpp:137-159)

@@ -263,6 +263,21 @@ constexpr uint32_t msg_flags() {
 
 }  // namespace detail
 
+namespace detail {
+// the message type whose code and header a record type's one-record
+// messages carry: boxed<M> -> M, else the record itself
+template <typename T>
+struct message_type {
+  using type = T;
+};
+template <typename M>
+struct message_type<boxed<M>> {
+  using type = M;
+};
+template <typename T>
+using message_type_t = typename message_type<T>::type;
+}  // namespace detail
+
 // Descriptor of record type T for the batch codec (cacheable, immutable).
 template <typename T, uint64_t conf = sp_config::DEFAULT>
 spk_layout make_spk_layout() {
@@ -280,9 +295,10 @@ spk_layout make_spk_layout() {
     const uint32_t al = b.align < 8 ? 8 : b.align;
     b.L.rec_stride = (b.off + al - 1) / al * al;
   }
-  fill_fmt(b.L.fmt_vector, get_type_code<std::vector<T>>(),
-           msg_flags<std::vector<T>, conf>(), get_type_literal<std::vector<T>>());
-  fill_fmt(b.L.fmt_one, get_type_code<T>(), msg_flags<T, conf>(), get_type_literal<T>());
+  using M = message_type_t<T>;
+  fill_fmt(b.L.fmt_vector, get_type_code<std::vector<M>>(),
+           msg_flags<std::vector<M>, conf>(), get_type_literal<std::vector<M>>());
+  fill_fmt(b.L.fmt_one, get_type_code<M>(), msg_flags<M, conf>(), get_type_literal<M>());
   return b.L;
 }
 

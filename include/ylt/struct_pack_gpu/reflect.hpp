@@ -55,6 +55,22 @@ template <typename T> struct is_std_variant : std::false_type {};
 template <typename... A> struct is_std_variant<std::variant<A...>> : std::true_type {};
 template <typename T> struct is_std_pair : std::false_type {};
 template <typename A, typename B> struct is_std_pair<std::pair<A, B>> : std::true_type {};
+// std::tuple: a struct of its elements, never trivially serializable
+// (reflection.hpp:893-895); the message type of a multi-argument call
+// (get_args_type, reflection.hpp:64-67)
+template <typename T> struct is_std_tuple : std::false_type {};
+template <typename... A> struct is_std_tuple<std::tuple<A...>> : std::true_type {};
+
+// A message whose type is not a record (std::string, a container of
+// non-record elements, an optional, a variant, ...) is encoded as the one
+// member of boxed<M>: the same payload bytes, under M's own type code
+// (layout.hpp message_type_t); the front end boxes and unboxes it.
+template <typename M>
+struct boxed {
+  M v;
+};
+template <typename T> struct is_boxed : std::false_type {};
+template <typename M> struct is_boxed<boxed<M>> : std::true_type {};
 
 // set_container_t (type_id.hpp: set, multiset, unordered_set, unordered_multiset)
 template <typename T> struct set_traits : std::false_type {};
@@ -114,11 +130,11 @@ constexpr bool is_aggregate_record_v = std::is_aggregate_v<T> && std::is_class_v
                                        !is_container_v<T> && !is_std_optional<T>::value &&
                                        !is_varint_v<T> && !is_compat_v<T> && !is_ylt_refl_v<T> &&
                                        !is_monostate_v<T>;
-// records: aggregates, YLT_REFL types, and std::pair (a struct of first,
-// second: type_id.hpp, the element of a map container)
+// records: aggregates, YLT_REFL types, std::pair (a struct of first,
+// second: type_id.hpp, the element of a map container) and std::tuple
 template <typename T>
 constexpr bool is_record_v = is_aggregate_record_v<T> || (std::is_class_v<T> && is_ylt_refl_v<T>) ||
-                             is_std_pair<T>::value;
+                             is_std_pair<T>::value || is_std_tuple<T>::value;
 
 // element type of a container as its device record holds it (a map's
 // pair<const K, V> as pair<K, V>)
@@ -208,10 +224,19 @@ constexpr auto tie_aggregate(T &obj) {
 }
 #undef SPK_TIE_CASE
 
+template <typename T, std::size_t... I>
+constexpr auto tie_tuple(T &obj, std::index_sequence<I...>) {
+  return std::forward_as_tuple(std::get<I>(obj)...);
+}
+
 template <typename T>
 constexpr auto tie_members(T &obj) {
   if constexpr (is_std_pair<remove_cvref_t<T>>::value)
     return std::forward_as_tuple(obj.first, obj.second);
+  else if constexpr (is_std_tuple<remove_cvref_t<T>>::value)
+    return tie_tuple(obj, std::make_index_sequence<std::tuple_size_v<remove_cvref_t<T>>>{});
+  else if constexpr (is_boxed<remove_cvref_t<T>>::value)
+    return std::forward_as_tuple(obj.v);
   else if constexpr (is_ylt_refl_v<remove_cvref_t<T>>)
     return refl_tuple(obj);
   else

@@ -124,6 +124,8 @@ constexpr bool is_trivially_serializable() {
     return false;  // reflection.hpp:872-876,899-905
   } else if constexpr (is_ylt_refl_v<T>) {
     return false;  // user_defined_refl: member by member (reflection.hpp:896-898)
+  } else if constexpr (is_std_tuple<T>::value) {
+    return false;  // std::tuple: member by member (reflection.hpp:893-895)
   } else {
     static_assert(is_record_v<T>, "unsupported member type");
     using M = members_tuple_t<T>;

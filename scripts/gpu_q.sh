@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 if [ -n "$TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m "$TESTS" tests/ > gpurun_out/pt.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pt.log; exit 1; }
+  timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m "$TESTS" ${KSEL:+-k "$KSEL"} tests/ > gpurun_out/pt.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pt.log; exit 1; }
   tail -1 gpurun_out/pt.log
 fi
 for c in ${CONFIGS:-c3 c4}; do

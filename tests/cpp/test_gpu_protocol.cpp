@@ -13,6 +13,9 @@
 #include <cstring>
 #include <fstream>
 #include <iterator>
+#include <map>
+#include <optional>
+#include <variant>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -87,11 +90,41 @@ std::vector<Outer> reverse_outer(std::vector<Outer> v) {
   return v;
 }
 int count_people(std::vector<rpcb::person> v) { return (int)v.size(); }  // batch in, int out
-std::string greet(rpcb::person p, int times) {                           // not a batch: CPU path
+std::string greet(rpcb::person p, int times) {  // two arguments: a std::tuple message
   std::string s;
   for (int i = 0; i < times; ++i) s += p.name;
   return s;
 }
+// the ordinary single-call shapes of a coro_rpc service
+rpcb::person echo_person(rpcb::person p) { return p; }
+rpcb::rect echo_rect(rpcb::rect r) { return r; }
+std::string echo_str(std::string s) { return s; }
+int add(int a, int b) { return a + b; }
+static int g_pinged = 0;
+void ping() { ++g_pinged; }                        // no arguments, void reply
+void note(std::string s) { g_pinged += (int)s.size(); }  // void reply
+std::vector<int> iota_n(int n) {
+  std::vector<int> v(n);
+  for (int i = 0; i < n; ++i) v[i] = i * 7 - 3;
+  return v;
+}
+std::vector<std::string> split_name(rpcb::person p, std::string sep) {
+  return {p.name, sep, std::to_string(p.age)};
+}
+std::optional<rpcb::person> maybe(int id, std::optional<std::string> name) {
+  if (!name) return std::nullopt;
+  return rpcb::person{id, *name, 3, 4.5};
+}
+std::map<int, std::string> to_map(std::vector<std::string> v) {
+  std::map<int, std::string> m;
+  for (std::size_t i = 0; i < v.size(); ++i) m[(int)i] = v[i];
+  return m;
+}
+std::variant<int, std::string> pick(bool s, int x) {
+  if (s) return std::to_string(x);
+  return x;
+}
+std::pair<int, double> pair_of(int a, double b) { return {a, b}; }
 
 // the reference benchmark's services (src/struct_pack/benchmark/data_def.hpp,
 // src/coro_rpc/benchmark/api/ValidateRequest.h)
@@ -128,11 +161,26 @@ void same_as_reference(const Arg &arg, const char *what) {
   if (ref.second != gpu.second) std::fprintf(stderr, "  mismatch in %s\n", what);
 }
 
+// a call with any number of arguments, packed as the reference client packs
+// them (serialize_to_with_offset(buffer, offset, args...), coro_rpc_client.hpp:
+// 1398-1410: several arguments are one std::tuple message)
+template <auto func, typename... Args>
+void call_same_as_reference(const char *what, const Args &...args) {
+  std::string req;  // no arguments: no payload (the executor decodes nothing)
+  if constexpr (sizeof...(Args) > 0) struct_pack::serialize_to(req, args...);
+  auto ref = run<func, struct_pack_protocol>(req);
+  auto gpu = run<func, struct_pack_gpu_protocol>(req);
+  CHECK(!ref.first && !gpu.first);
+  CHECK(ref.second == gpu.second);
+  if (ref.first.val() != gpu.first.val() || ref.second != gpu.second)
+    std::fprintf(stderr, "  mismatch in %s (%zu vs %zu bytes)\n", what, ref.second.size(),
+                 gpu.second.size());
+}
+
 int main() {
   using namespace spk_gold;
-  // force the GPU path for every batch size in this test
-  struct_pack_gpu_protocol::min_gpu_bytes = 0;
-  struct_pack_gpu_protocol::min_gpu_records = 0;
+  // (no size thresholds: every payload of every handler below goes through
+  // struct_pack::gpu, compared with the reference's struct_pack_protocol)
   const uint64_t S3 = 0x5EED0003, S4 = 0x5EED0004, S8 = 0x5EED0008;
 
   // 1. the protocol statics against the reference protocol and fixtures
@@ -180,12 +228,18 @@ int main() {
     // an empty batch and a one-record batch
     same_as_reference<echo_recs>(std::vector<RecS>{}, "echo_recs(empty)");
     same_as_reference<echo_recs>(std::vector<RecS>{make_recs(S3, 7, 48)}, "echo_recs(1)");
-    // two arguments: not a batch message, served by the reference codec
+    // two arguments: one std::tuple<person, int> message, through the GPU
+    call_same_as_reference<greet>("greet", make_person(S8, 1, 10), 3);
     const std::string req =
         struct_pack::serialize<std::string>(std::make_tuple(make_person(S8, 1, 10), 3));
-    auto ref = run<greet, struct_pack_protocol>(req);
-    auto gpu = run<greet, struct_pack_gpu_protocol>(req);
-    CHECK(!ref.first && !gpu.first && ref.second == gpu.second);
+    std::string packed;
+    struct_pack::serialize_to(packed, make_person(S8, 1, 10), 3);
+    CHECK(req == packed);  // serialize(a, b) == serialize(std::tuple{a, b})
+    std::tuple<rpcb::person, int> targs;
+    CHECK(struct_pack_gpu_protocol::deserialize_to(targs, req));
+    CHECK(std::get<0>(targs) == make_person(S8, 1, 10) && std::get<1>(targs) == 3);
+    CHECK((struct_pack::gpu::get_type_code<std::tuple<rpcb::person, int>>() ==
+           struct_pack::get_type_code<rpcb::person, int>()));
     // a malformed request: coro_rpc's invalid_rpc_arguments on both paths
     std::string bad = struct_pack::serialize<std::string>(v);
     bad.resize(bad.size() / 2);
@@ -213,6 +267,42 @@ int main() {
                                  "echo_tags");
     same_as_reference<echo_vnt>(make(std::type_identity<Vnt>{}, 1000, 0x5EED0011, 6), "echo_vnt");
     same_as_reference<echo_monsters>(std::vector<Monster>{}, "echo_monsters(empty)");
+  }
+  // 2c. every call shape at default settings: single records, strings, ints,
+  // several arguments (std::tuple messages), no arguments, void replies,
+  // containers of non-records, optionals, maps, variants, pairs as replies
+  {
+    call_same_as_reference<echo_person>("echo_person", make_person(S8, 5, 40));
+    call_same_as_reference<echo_rect>("echo_rect", rpcb::rect{{1, 2}, {3, 4}});
+    call_same_as_reference<echo_str>("echo_str", std::string("hello, coro_rpc"));
+    call_same_as_reference<echo_str>("echo_str(empty)", std::string());
+    call_same_as_reference<echo_str>("echo_str(300)", std::string(300, 'x'));
+    call_same_as_reference<add>("add", 40, 2);
+    call_same_as_reference<ping>("ping");
+    call_same_as_reference<note>("note", std::string("abc"));
+    call_same_as_reference<iota_n>("iota_n", 1000);
+    call_same_as_reference<iota_n>("iota_n(0)", 0);
+    call_same_as_reference<split_name>("split_name", make_person(S8, 9, 20), std::string("/"));
+    call_same_as_reference<maybe>("maybe", 7, std::optional<std::string>("bob"));
+    call_same_as_reference<maybe>("maybe(null)", 7, std::optional<std::string>());
+    call_same_as_reference<to_map>("to_map", std::vector<std::string>{"a", "bb", "ccc"});
+    call_same_as_reference<pick>("pick(s)", true, 77);
+    call_same_as_reference<pick>("pick(i)", false, 77);
+    call_same_as_reference<pair_of>("pair_of", 3, 2.5);
+    call_same_as_reference<count_people>("count_people(1)",
+                                         std::vector<rpcb::person>{make_person(S8, 2, 30)});
+    // a malformed two-argument request: invalid_rpc_arguments on both paths
+    std::string req;
+    struct_pack::serialize_to(req, make_person(S8, 1, 10), 3);
+    req.resize(req.size() - 2);
+    auto rb = run<greet, struct_pack_protocol>(req);
+    auto gb = run<greet, struct_pack_gpu_protocol>(req);
+    CHECK(rb.first && gb.first && rb.first.val() == gb.first.val());
+    // a request of another type: hash_conflict -> invalid arguments on both
+    const std::string other = struct_pack::serialize<std::string>(std::string("x"));
+    auto ro = run<add, struct_pack_protocol>(other);
+    auto go = run<add, struct_pack_gpu_protocol>(other);
+    CHECK(ro.first && go.first && ro.first.val() == go.first.val());
   }
   // 3. the front end's single-record and reference-order entry points next to
   // the reference: identical bytes for one record message, deserialize<conf, T>

@@ -834,3 +834,62 @@ def test_gpu_decodes_reference_binary_goldens(ref, conf):
         assert out.heaps[k][:nb].cpu().numpy().tobytes() == heaps[k].tobytes()
     back, _ = cd.serialize(out, C.SPK_MODE_MESSAGES)
     assert back.cpu().numpy().tobytes() == wire
+
+
+@pytest.mark.parametrize("case,param", [("monster", 20), ("tags", 6), ("lists", 6)])
+def test_nested_encode_stale_plan(case, param):
+    """The nested VECTOR encode reuses its plan's offsets from the workspace
+    only while the plan token holds (csrc/spk_nested.hip NTok): a decode on
+    the same workspace between plan and encode, or a planned encode of
+    another batch, re-runs the size pass and still writes the reference's
+    bytes, within the buffer."""
+    cd = codec_for(case)
+    n = 20000
+    _, ra, ha = synth.make_batch(case, n, 0x57A1, param)
+    _, rb, hb = synth.make_batch(case, n, 0x57A2, param)
+    exp_a, _, _ = H.oracle_encode(cd.L, C.SPK_MODE_VECTOR, ra, ha)
+    exp_b, _, _ = H.oracle_encode(cd.L, C.SPK_MODE_VECTOR, rb, hb)
+    a, b = to_dev(cd, ra, ha), to_dev(cd, rb, hb)
+    guard = 4096
+
+    def encode_planned(batch, exp):
+        buf = torch.full((len(exp) + guard,), 0xA5, dtype=torch.uint8, device="cuda")
+        cd.serialize_to(buf[:len(exp)], batch, C.SPK_MODE_VECTOR, planned=True)
+        torch.cuda.synchronize()
+        assert bool((buf[len(exp):] == 0xA5).all())
+        return buf[:len(exp)].cpu().numpy().tobytes()
+
+    # plan -> encode (the token holds)
+    cd.plan(a, C.SPK_MODE_VECTOR)
+    assert encode_planned(a, exp_a) == exp_a
+    # plan -> decode on the same workspace -> encode
+    cd.plan(a, C.SPK_MODE_VECTOR)
+    res, back, _ = cd.deserialize(wire_dev(exp_b), C.SPK_MODE_VECTOR)
+    assert res.errc == 0 and res.count == n
+    assert encode_planned(a, exp_a) == exp_a
+    # plan of one batch -> encode of another of the same size
+    cd.plan(a, C.SPK_MODE_VECTOR)
+    assert encode_planned(b, exp_b) == exp_b
+    # plan -> plan of a smaller batch -> encode of the first
+    cd.plan(a, C.SPK_MODE_VECTOR)
+    cd.plan(SP.RecordBatch(cd.L, a.recs[:n // 3], a.heaps), C.SPK_MODE_VECTOR)
+    assert encode_planned(a, exp_a) == exp_a
+
+
+@pytest.mark.parametrize("case", ["rect2", "fv"])
+def test_vector_of_zero_fast_varint_records(case):
+    """A VECTOR message of all-zero fast-varint records (one bitset byte per
+    rect2<int32_t> record; zero members take no wire bytes, packer.hpp:
+    193-212) decodes: the allocating decode's record capacity counts a
+    fast-varint group as its bitset, not one byte per member."""
+    cd = codec_for(case)
+    n = 5000
+    _, recs, heaps = synth.make_batch(case, n, 0x2E80, 8)
+    recs = np.zeros_like(recs)
+    heaps = [np.zeros_like(h) for h in heaps]
+    exp, _, _ = H.oracle_encode(cd.L, C.SPK_MODE_VECTOR, recs, heaps)
+    out, _ = cd.serialize(to_dev(cd, recs, heaps), C.SPK_MODE_VECTOR)
+    assert out.cpu().numpy().tobytes() == exp
+    res, back, _ = cd.deserialize(wire_dev(exp), C.SPK_MODE_VECTOR)
+    assert res.errc == 0 and res.count == n and res.consumed == len(exp)
+    assert back.recs.cpu().numpy().tobytes() == np.ascontiguousarray(recs).view(np.uint8).tobytes()

@@ -230,3 +230,27 @@ def test_oracle_decodes_reference_binary_goldens(ref, conf):
     assert H.records_equal(L, out[:1], recs, oh, heaps, res.heap_used)
     back, _, _ = H.oracle_encode(L, C.SPK_MODE_MESSAGES, out[:1], oh)
     assert back == wire
+
+
+@pytest.mark.parametrize("case", sorted(synth.CASE_TYPES))
+def test_min_record_wire_bytes_is_a_lower_bound(case):
+    """schema.min_record_wire_bytes bounds a decode's record capacity: no
+    record of the type takes fewer wire bytes, checked on all-zero records
+    (empty containers, zero varints: the smallest encodings) through the
+    pinned oracle. For rect2<int32_t> (four fast varints) it is the 1-byte
+    bitset (packer.hpp:193-212)."""
+    from yalantinglibs_amd import layout as LY
+    L = LY.case_layout(case)
+    n = 64
+    _, recs, heaps = synth.make_batch(case, n, 0x2E80, 4)
+    recs = np.zeros_like(recs)
+    heaps = [np.zeros_like(h) for h in heaps]
+    try:
+        wire_n, _, _ = H.oracle_encode(L, C.SPK_MODE_VECTOR, recs, heaps)
+    except AssertionError:
+        pytest.skip("all-zero records are not encodable for this case (e.g. a variant index)")
+    wire_1, _, _ = H.oracle_encode(L, C.SPK_MODE_VECTOR, recs[:1], [h[:0] for h in heaps])
+    per_rec = (len(wire_n) - len(wire_1)) / (n - 1)
+    assert per_rec >= S.min_record_wire_bytes(L.dev), (per_rec, S.min_record_wire_bytes(L.dev))
+    if case == "rect2":
+        assert S.min_record_wire_bytes(L.dev) == 1

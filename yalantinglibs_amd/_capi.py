@@ -135,6 +135,7 @@ CODEC_SYMBOLS = ["spk_abi_version", "spk_errc_message", "spk_layout_check",
                  "spk_encode_body",
                  "spk_vector_header", "spk_encode_framed", "spk_decode_framed",
                  "spk_decode_body", "spk_parse_vector_header",
+                 "spk_message_header", "spk_parse_message_header",
                  "spk_decode_shard_index", "spk_decode_shard_emit",
                  # mixed-type frame batches in arrival order
                  "spk_route_workspace_bytes", "spk_route_frames", "spk_route_frames_checked", "spk_decode_frames",
@@ -179,6 +180,10 @@ def _bind_codec(lib):
     lib.spk_parse_vector_header.argtypes = [PL, P, U64, ct.POINTER(U64),
                                             ct.POINTER(ct.c_uint32), ct.POINTER(ct.c_uint32)]
     lib.spk_parse_vector_header.restype = ct.c_int32
+    lib.spk_message_header.argtypes = [PL, ct.c_uint32, ct.POINTER(ct.c_uint8), ct.c_uint32]
+    lib.spk_parse_message_header.argtypes = [PL, P, U64, ct.POINTER(ct.c_uint32),
+                                             ct.POINTER(ct.c_uint32)]
+    lib.spk_parse_message_header.restype = ct.c_int32
     lib.spk_decode_shard_index.argtypes = [PL, P, U64, U64, U64, U64, P, P, ct.c_size_t, P]
     lib.spk_decode_shard_emit.argtypes = [PL, P, U64, U64, U64, U64, ct.c_int, P, U64,
                                           ct.POINTER(P), ct.POINTER(U64), P, P, ct.c_size_t, P]

@@ -574,6 +574,31 @@ int spk_vector_header(const spk_layout *L, uint64_t total_n, uint32_t width, uin
   return (int)len;
 }
 
+int spk_message_header(const spk_layout *L, uint32_t width, uint8_t *h_out, uint32_t cap) {
+  int rc = spk_layout_check(L);
+  if (rc) return rc;
+  if (has_compat(L)) return SPK_E_LAYOUT;
+  if ((width != 1 && width != 2 && width != 4 && width != 8) || !h_out) return SPK_E_ARG;
+  uint8_t hb[4 + 1 + SPK_MAX_LITERAL + 1];
+  const uint32_t len = write_hdr(hb, L->fmt_one, width);
+  if (len > cap) return SPK_E_CAPACITY;
+  for (uint32_t i = 0; i < len; ++i) h_out[i] = hb[i];
+  return (int)len;
+}
+
+int32_t spk_parse_message_header(const spk_layout *L, const void *h_wire, uint64_t len,
+                                 uint32_t *width, uint32_t *header_len) {
+  if (spk_layout_check(L) != SPK_OK) return SPK_E_LAYOUT;
+  if ((len && !h_wire) || !width || !header_len) return SPK_E_ARG;
+  uint64_t pos, dl;
+  uint32_t w;
+  const int32_t e = parse_hdr(L->fmt_one, (const uint8_t *)h_wire, len, &pos, &w, &dl);
+  if (e) return e;
+  *width = w;
+  *header_len = (uint32_t)pos;
+  return SPK_ERRC_OK;
+}
+
 // ---- kernel tracing ---------------------------------------------------------
 int spk_trace_enable(int on) {
   std::lock_guard<std::mutex> lk(g_trace_mu);

@@ -848,10 +848,26 @@ __device__ __forceinline__ uint64_t n_block_excl(uint64_t v, uint64_t *sh, uint6
   return incl - v;
 }
 
+// plan token of the VECTOR encode (see nest_tok_hash below)
+constexpr size_t kWsPlanTok = 1536;  // [1536, 2048) is free (spk_internal.hpp)
+constexpr unsigned long long kTokMagic = 0x4e53504b544f4b31ull;
+struct NTok {
+  unsigned long long magic, n, recs, heaps, layout, tot0, maxc, hash;
+  unsigned long long chk;  // the encode's hash of the same column
+  uint32_t stale, pad_;
+};
+static_assert(kWsPlanTok + sizeof(NTok) <= kWsCtl, "NTok overlaps the control block");
+
+__device__ __forceinline__ bool tok_skip(const uint8_t *ws, const uint32_t *cond) {
+  return cond && !reinterpret_cast<const NTok *>(ws + kWsPlanTok)->stale;
+}
+
 __global__ __launch_bounds__(kNScanT) void nscan_reduce(const uint64_t *__restrict__ col,
                                                         uint64_t n, uint64_t *__restrict__ part,
-                                                        uint64_t nb) {
+                                                        uint64_t nb, const uint8_t *ws,
+                                                        const uint32_t *cond) {
   __shared__ uint64_t sh[kNScanT];
+  if (tok_skip(ws, cond)) return;
   const uint64_t c = blockIdx.y;
   const uint64_t base = (uint64_t)blockIdx.x * kNScanBlk;
   uint64_t s = 0;
@@ -865,9 +881,11 @@ __global__ __launch_bounds__(kNScanT) void nscan_reduce(const uint64_t *__restri
 }
 
 // one block per column: exclusive scan of the block partials, total at [nb]
-__global__ __launch_bounds__(1024) void nscan_top(uint64_t *__restrict__ part, uint64_t nb) {
+__global__ __launch_bounds__(1024) void nscan_top(uint64_t *__restrict__ part, uint64_t nb,
+                                                      const uint8_t *ws, const uint32_t *cond) {
   __shared__ uint64_t sh[1024];
   __shared__ uint64_t carry;
+  if (tok_skip(ws, cond)) return;
   const uint64_t c = blockIdx.x;
   uint64_t *p = part + c * (nb + 1);
   if (threadIdx.x == 0) carry = 0;
@@ -895,8 +913,10 @@ __global__ __launch_bounds__(1024) void nscan_top(uint64_t *__restrict__ part, u
 
 __global__ __launch_bounds__(kNScanT) void nscan_apply(uint64_t *__restrict__ col, uint64_t n,
                                                        const uint64_t *__restrict__ part,
-                                                       uint64_t nb) {
+                                                       uint64_t nb, const uint8_t *ws,
+                                                       const uint32_t *cond) {
   __shared__ uint64_t sh[kNScanT];
+  if (tok_skip(ws, cond)) return;
   const uint64_t c = blockIdx.y;
   const uint64_t base = (uint64_t)blockIdx.x * kNScanBlk + (uint64_t)threadIdx.x * kNScanIPT;
   uint64_t v[kNScanIPT], s = 0;
@@ -917,15 +937,18 @@ __global__ __launch_bounds__(kNScanT) void nscan_apply(uint64_t *__restrict__ co
 // note: nscan_reduce writes partials with row stride nb; nscan_top/apply read
 // them with stride nb + 1 — the host lays the partial table out with nb + 1
 // slots per column and passes nb + 1 to the reduce as its stride.
+// ws + cond: the encode's conditional size pass (skipped while the plan
+// token holds, see NTok); null cond: always run
 static hipError_t nscan(uint64_t *col, uint64_t n, uint32_t ncols, uint64_t *part,
-                        hipStream_t s) {
+                        hipStream_t s, const uint8_t *ws = nullptr,
+                        const uint32_t *cond = nullptr) {
   if (!n || !ncols) return hipSuccess;
   const uint64_t nb = (n + kNScanBlk - 1) / kNScanBlk;
   SPK_LAUNCH(nscan_reduce, dim3((unsigned)nb, ncols), dim3(kNScanT), 0, s, (const uint64_t *)col,
-             n, part, nb + 1);
-  SPK_LAUNCH(nscan_top, dim3(ncols), dim3(1024), 0, s, part, nb);
+             n, part, nb + 1, ws, cond);
+  SPK_LAUNCH(nscan_top, dim3(ncols), dim3(1024), 0, s, part, nb, ws, cond);
   SPK_LAUNCH(nscan_apply, dim3((unsigned)nb, ncols), dim3(kNScanT), 0, s, col, n,
-             (const uint64_t *)part, nb);
+             (const uint64_t *)part, nb, ws, cond);
   return hipGetLastError();
 }
 static size_t nscan_part_bytes(uint64_t n, uint32_t ncols) {
@@ -1064,6 +1087,64 @@ struct NEnc {
   const uint8_t *heaps[SPK_MAX_SPANS];
 };
 
+// ---- plan token -----------------------------------------------------------------------
+// A VECTOR encode of a layout without compatible members reuses the offsets
+// its plan left in the workspace (column 0, the scan totals, maxc). The plan
+// leaves a token beside them: the batch (n, records, heaps, layout) and an
+// order-free hash of the offsets column, the total and maxc. The encode
+// checks it on the device and re-runs the size pass only when it does not
+// match (another call used the workspace in between, or no plan preceded),
+// so a stale workspace never steers the window writes.
+__device__ __forceinline__ uint64_t tok_mix(uint64_t i, uint64_t v) {
+  uint64_t z = v + (i + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static uint64_t tok_heaps(const NEnc &e) {
+  uint64_t h = 0;
+  for (uint32_t k = 0; k < e.N.n_heaps && k < SPK_MAX_SPANS; ++k)
+    h = h * 0x100000001B3ull ^ (uint64_t)(uintptr_t)e.heaps[k];
+  return h;
+}
+static uint64_t tok_layout(const spk_layout *L) {
+  return ((uint64_t)L->fmt_vector.code << 32) ^ ((uint64_t)L->n_ops << 16) ^ L->rec_stride ^
+         ((uint64_t)L->fmt_vector.flags << 48);
+}
+
+// XOR over the records of tok_mix(i, a[i]) into *dst (order-free, one
+// atomic per wave)
+__global__ __launch_bounds__(256) void nest_tok_hash(const uint64_t *__restrict__ a, uint64_t n,
+                                                     unsigned long long *dst) {
+  uint64_t h = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    h ^= tok_mix(i, a[i]);
+  for (int o = 32; o > 0; o >>= 1) h ^= __shfl_xor(h, o);
+  if ((threadIdx.x & 63) == 0 && h) atomicXor(dst, (unsigned long long)h);
+}
+
+// encode: start the check (static fields) and clear the recomputed hash
+__global__ void nest_tok_begin(uint8_t *ws, uint64_t n, uint64_t recs, uint64_t heaps,
+                               uint64_t layout) {
+  NTok *t = reinterpret_cast<NTok *>(ws + kWsPlanTok);
+  t->chk = 0;
+  t->stale = t->magic != kTokMagic || t->n != n || t->recs != recs || t->heaps != heaps ||
+             t->layout != layout;
+}
+
+// encode: the verdict (hash, total, maxc); a stale token is dropped
+__global__ void nest_tok_verdict(uint8_t *ws, const uint64_t *__restrict__ part, uint64_t nb,
+                                 uint64_t n) {
+  NTok *t = reinterpret_cast<NTok *>(ws + kWsPlanTok);
+  const NCtl *ctl = reinterpret_cast<const NCtl *>(ws + kWsCtl);
+  const uint64_t tot0 = n ? part[nb] : 0;
+  const uint32_t stale = t->stale || t->chk != t->hash || t->tot0 != tot0 || t->maxc != ctl->maxc;
+  t->stale = stale;
+  if (stale) t->magic = 0;
+}
+
+
 // a[0][i] = payload bytes, a[1][i] = count fields (VECTOR) or the whole
 // message size (MESSAGES); the longest container into ctl->maxc
 // the block's records staged in LDS with coalesced 16-B loads when they fit:
@@ -1072,9 +1153,11 @@ struct NEnc {
 constexpr uint32_t kNSizeStage = 28 * 1024;
 template <int D>
 __global__ __launch_bounds__(256) void nest_size(NEnc e, const uint8_t *__restrict__ recs,
-                                                 uint64_t *__restrict__ a, uint8_t *ws) {
+                                                 uint64_t *__restrict__ a, uint8_t *ws,
+                                                 const uint32_t *cond) {
   __shared__ NLayout N;
   __shared__ __align__(16) uint8_t rs[kNSizeStage];
+  if (tok_skip(ws, cond)) return;
   n_stage(N, e.N);
   NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1120,7 +1203,13 @@ __global__ __launch_bounds__(256) void nest_size(NEnc e, const uint8_t *__restri
     atomicMax(&ctl->maxc, (unsigned long long)m);
 }
 
-__global__ void nest_ctl_init(uint8_t *ws) {
+__global__ void nest_ctl_init(uint8_t *ws, const uint32_t *cond) {
+  if (tok_skip(ws, cond)) return;
+  if (!cond) {  // an unconditional size pass (a plan) drops any earlier token
+    NTok *t = reinterpret_cast<NTok *>(ws + kWsPlanTok);
+    t->magic = 0;
+    t->hash = 0;
+  }
   NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
   ctl->maxc = 0;
   ctl->nrec = 0;
@@ -1135,8 +1224,10 @@ __global__ void nest_ctl_init(uint8_t *ws) {
 // column 2 + rk: the bytes of record i in the version pass of rank rk
 template <int D>
 __global__ void nest_vec_sizes(NEnc e, const uint8_t *__restrict__ recs,
-                               uint64_t *__restrict__ a, uint8_t *ws) {
+                               uint64_t *__restrict__ a, uint8_t *ws,
+                               const uint32_t *cond) {
   __shared__ NLayout N;
+  if (tok_skip(ws, cond)) return;
   n_stage(N, e.N);
   const NCtl *ctl = reinterpret_cast<const NCtl *>(ws + kWsCtl);
   const uint64_t mx = ctl->maxc > e.n ? ctl->maxc : e.n;
@@ -1150,10 +1241,23 @@ __global__ void nest_vec_sizes(NEnc e, const uint8_t *__restrict__ recs,
 }
 
 // plan result from the column sums (part tables after the scan)
+// (VECTOR without compatible members: also the plan token, tok_* set, whose
+// hash nest_tok_hash accumulated)
 __global__ void nest_plan_fin(NEnc e, const uint64_t *__restrict__ a,
                               const uint64_t *__restrict__ part, uint64_t nb, uint8_t *ws,
-                              spk_plan_t *plan) {
+                              spk_plan_t *plan, uint32_t tok, uint64_t recs, uint64_t heaps,
+                              uint64_t layout) {
   const NCtl *ctl = reinterpret_cast<const NCtl *>(ws + kWsCtl);
+  if (tok) {
+    NTok *t = reinterpret_cast<NTok *>(ws + kWsPlanTok);
+    t->n = e.n;
+    t->recs = recs;
+    t->heaps = heaps;
+    t->layout = layout;
+    t->tot0 = e.n ? part[nb] : 0;
+    t->maxc = ctl->maxc;
+    t->magic = kTokMagic;
+  }
   spk_plan_t p = {};
   const uint64_t tot0 = e.n ? part[nb] : 0;                 // column 0 total
   const uint64_t tot1 = e.n ? part[(nb + 1) + nb] : 0;      // column 1 total
@@ -1299,10 +1403,13 @@ __global__ __launch_bounds__(256) void nest_write_win(NEnc e, const uint8_t *__r
     const NWin W{lds, wlo, wlo + kNEncWin < g1 ? wlo + kNEncWin : g1};
     if (i < e.n && q0 < W.hi && q1 > W.lo) n_write<D>(N, rec, e.heaps, w, W, q0, 0, N.n_ops, true);
     __syncthreads();
-    // flush [max(W.lo, g0), W.hi): aligned 16-B chunks, bytes at the edges
-    for (uint64_t c = W.lo + (uint64_t)threadIdx.x * 16; c < W.hi; c += 256 * 16) {
+    // flush [max(W.lo, g0), min(W.hi, out_cap)): aligned 16-B chunks, bytes
+    // at the edges (the clamp: no offset, however it was planned, writes
+    // past the caller's buffer)
+    const uint64_t whi = W.hi < out_cap ? W.hi : out_cap;
+    for (uint64_t c = W.lo + (uint64_t)threadIdx.x * 16; c < whi; c += 256 * 16) {
       const uint64_t lo = c > g0 ? c : g0;
-      const uint64_t hi = c + 16 < W.hi ? c + 16 : W.hi;
+      const uint64_t hi = c + 16 < whi ? c + 16 : whi;
       if (lo == c && hi == c + 16)
         *reinterpret_cast<v4u_t *>(out + c) = *reinterpret_cast<const v4u_t *>(lds + (c - W.lo));
       else
@@ -1330,20 +1437,23 @@ static NEnc make_nenc(const spk_layout *L, int mode, uint64_t n, const void *con
 }
 
 // size pass + scan; leaves per-record offsets in column a[0]
+// cond (device, non-null): every kernel returns at once while the plan token
+// holds (the encode's check, NTok)
 static hipError_t nest_size_scan(const NEnc &e, const void *d_recs, uint8_t *ws, hipStream_t s,
-                                 uint64_t **a_out, uint64_t **part_out, uint64_t *nb_out) {
+                                 uint64_t **a_out, uint64_t **part_out, uint64_t *nb_out,
+                                 const uint32_t *cond = nullptr) {
   const NWs f = nws_layout(e.n, e.N.n_heaps, e.N.n_ranks);
   uint64_t *a = reinterpret_cast<uint64_t *>(ws + f.a);
   uint64_t *part = reinterpret_cast<uint64_t *>(ws + f.part);
-  SPK_LAUNCH(nest_ctl_init, dim3(1), dim3(1), 0, s, ws);
+  SPK_LAUNCH(nest_ctl_init, dim3(1), dim3(1), 0, s, ws, cond);
   if (e.n) {
     NEST_D(n_dclass(e.N),
            SPK_LAUNCH(nest_size<D>, dim3(nblocks(e.n, 256)), dim3(256), 0, s, e,
-                      (const uint8_t *)d_recs, a, ws));
+                      (const uint8_t *)d_recs, a, ws, cond));
     if (e.mode == SPK_MODE_VECTOR)
       NEST_D(n_dclass(e.N),
              SPK_LAUNCH(nest_vec_sizes<D>, dim3(nblocks(e.n, 256) < 4096 ? nblocks(e.n, 256) : 4096),
-                        dim3(256), 0, s, e, (const uint8_t *)d_recs, a, ws));
+                        dim3(256), 0, s, e, (const uint8_t *)d_recs, a, ws, cond));
   }
   hipError_t er = hipGetLastError();
   if (er != hipSuccess) return er;
@@ -1351,7 +1461,7 @@ static hipError_t nest_size_scan(const NEnc &e, const void *d_recs, uint8_t *ws,
   // passes; MESSAGES: column 0 = message sizes, column 1 = payload bytes. All
   // scanned (totals in part).
   const uint32_t cols = e.mode == SPK_MODE_VECTOR ? 2 + e.N.n_ranks : 2;
-  if ((er = nscan(a, e.n, cols, part, s)) != hipSuccess) return er;
+  if ((er = nscan(a, e.n, cols, part, s, ws, cond)) != hipSuccess) return er;
   *a_out = a;
   *part_out = part;
   *nb_out = (e.n + kNScanBlk - 1) / kNScanBlk;
@@ -1366,8 +1476,14 @@ hipError_t launch_nested_plan(const spk_layout *L, int mode, uint64_t n, const v
   uint64_t *a, *part, nb;
   hipError_t er = nest_size_scan(e, d_recs, ws, s, &a, &part, &nb);
   if (er != hipSuccess) return er;
+  const uint32_t tok = mode == SPK_MODE_VECTOR && !e.N.n_ranks;
+  if (tok && n)
+    SPK_LAUNCH(nest_tok_hash, dim3(nblocks(n, 256) < 2048 ? nblocks(n, 256) : 2048), dim3(256), 0,
+               s, (const uint64_t *)a, n,
+               &reinterpret_cast<NTok *>(ws + kWsPlanTok)->hash);
   SPK_LAUNCH(nest_plan_fin, dim3(1), dim3(1), 0, s, e, (const uint64_t *)a,
-             (const uint64_t *)part, nb, ws, d_plan);
+             (const uint64_t *)part, nb, ws, d_plan, tok, (uint64_t)(uintptr_t)d_recs,
+             tok_heaps(e), tok_layout(L));
   return hipGetLastError();
 }
 
@@ -1391,11 +1507,22 @@ hipError_t launch_nested_encode(const spk_layout *L, int mode, uint64_t n, const
     // the plan that precedes this call on the workspace (spk_encode's
     // contract, as for the flat layouts) left every record's offset in column
     // 0, the totals in the partials and the longest container in the control
-    // block: the write pass alone
+    // block, with its token: the token is checked on the device and the size
+    // pass re-runs (each kernel returns at once otherwise) when it fails
+    NTok *t = reinterpret_cast<NTok *>(ws + kWsPlanTok);
     const NWs f = nws_layout(e.n, e.N.n_heaps, e.N.n_ranks);
     a = reinterpret_cast<uint64_t *>(ws + f.a);
     part = reinterpret_cast<uint64_t *>(ws + f.part);
     nb = (e.n + kNScanBlk - 1) / kNScanBlk;
+    SPK_LAUNCH(nest_tok_begin, dim3(1), dim3(1), 0, s, ws, n, (uint64_t)(uintptr_t)d_recs,
+               tok_heaps(e), tok_layout(L));
+    if (n)
+      SPK_LAUNCH(nest_tok_hash, dim3(nblocks(n, 256) < 2048 ? nblocks(n, 256) : 2048), dim3(256),
+                 0, s, (const uint64_t *)a, n, &t->chk);
+    SPK_LAUNCH(nest_tok_verdict, dim3(1), dim3(1), 0, s, ws, (const uint64_t *)part, nb, n);
+    uint64_t *a2, *part2, nb2;
+    hipError_t er = nest_size_scan(e, d_recs, ws, s, &a2, &part2, &nb2, &t->stale);
+    if (er != hipSuccess) return er;
     NEST_D(n_dclass(e.N),
            SPK_LAUNCH(nest_write_win<D>, dim3(nblocks(n, 256)), dim3(256), 0, s, e,
                       (const uint8_t *)d_recs, (const uint64_t *)a, (const uint64_t *)part, nb, ws,
@@ -2008,7 +2135,7 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
                (const int32_t *)ec, ws, mode, d_res, (int32_t *)nullptr);
     return hipGetLastError();
   }
-  SPK_LAUNCH(nest_ctl_init, dim3(1), dim3(1), 0, s, ws);
+  SPK_LAUNCH(nest_ctl_init, dim3(1), dim3(1), 0, s, ws, (const uint32_t *)nullptr);
   if (!n_msgs) return hipGetLastError();
   SPK_LAUNCH(nest_msg_count, dim3(nblocks(n_msgs, 256)), dim3(256), 0, s, a,
              (const uint8_t *)d_wire, d_msg_offsets, U, ec, cons);
