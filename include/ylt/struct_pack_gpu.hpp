@@ -32,6 +32,7 @@
 // Build: <c++20 compiler> -I include ... -L yalantinglibs_amd -lspk_codec
 #pragma once
 #include <cstring>
+#include <ios>
 #include <memory>
 #include <span>
 #include <stdexcept>
@@ -892,6 +893,131 @@ template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT>
 template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT, detail::byte_view View>
 [[nodiscard]] expected<field_t<T, I>> get_field(const View &v) {
   return get_field<T, I, conf>(reinterpret_cast<const char *>(v.data()), v.size());
+}
+// get_field_to<T, I>(dst, ...) (struct_pack.hpp:565-611)
+template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT, typename Field>
+[[nodiscard]] err_code get_field_to(Field &dst, const char *data, std::size_t size) {
+  auto r = get_field<T, I, conf>(data, size);
+  if (!r.has_value()) return r.error();
+  dst = std::move(r.value());
+  return {};
+}
+template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT, typename Field,
+          detail::byte_view View>
+[[nodiscard]] err_code get_field_to(Field &dst, const View &v) {
+  return get_field_to<T, I, conf>(dst, reinterpret_cast<const char *>(v.data()), v.size());
+}
+
+// ---- stream readers: deserialize_to(t, reader) (struct_pack.hpp:289-323) ----
+// The reference reads a message from a Reader field by field
+// (unpacker.hpp:46-76, 1166-1195). The device decoder needs the message's
+// bytes in one buffer, so the front end reads a growing block from the
+// reader (64 KiB, then x4), decodes it on the GPU, and puts the reader right
+// after the message (seekg to start + consume_len). A prefix decoded with
+// no_buffer_space only means "read more". Layouts whose decode can succeed on
+// a cut message (the reference drops the errc of an optional's value, a
+// variant's alternative and reads absent compatible members as empty:
+// unpacker.hpp:476-490,1271-1273) read the reader's whole remainder at once,
+// so a truncated block never stands in for the message. Readers: the
+// std::istream family, or any type with read / gcount / tellg / seekg / clear
+// (a socket is not one: coro_rpc frames carry their length in req_header).
+namespace detail {
+template <typename R>
+concept seekable_reader = requires(R &r, char *p, std::size_t n) {
+  r.read(p, n);
+  r.gcount();
+  r.tellg();
+  r.seekg(r.tellg());
+  r.seekg(0, std::ios_base::end);
+  r.clear();
+};
+
+inline bool prefix_decode_exact(const spk_layout &L) {
+  for (uint32_t i = 0; i < L.n_ops; ++i) {
+    const uint32_t k = SPK_OP_KIND(L.ops[i].kind);
+    if (k == SPK_OP_OPTION || k == SPK_OP_OPTGROUP || k == SPK_OP_VARIANT || k == SPK_OP_COMPAT ||
+        k == SPK_OP_CGROUP)
+      return false;
+  }
+  return true;
+}
+
+template <uint64_t conf, typename T, typename Reader>
+err_code decode_stream(T &t, Reader &rd, std::size_t &consume_len) {
+  using tr = msg_traits<T>;
+  consume_len = 0;
+  const auto start = rd.tellg();
+  bool exact = true;
+  if constexpr (!tr::empty) exact = prefix_decode_exact(device::codec<typename tr::rec, conf>::layout());
+  std::size_t want = std::size_t(1) << 16;
+  if (!exact) {  // the whole remainder
+    rd.seekg(0, std::ios_base::end);
+    const auto end = rd.tellg();
+    rd.seekg(start);
+    want = end > start ? static_cast<std::size_t>(end - start) : 0;
+  }
+  std::vector<char> buf;
+  for (;;) {
+    const std::size_t have = buf.size();
+    buf.resize(want);
+    if (want > have) rd.read(buf.data() + have, static_cast<std::streamsize>(want - have));
+    const std::size_t got = have + (want > have ? static_cast<std::size_t>(rd.gcount()) : 0);
+    const bool at_end = got < want || !exact;
+    buf.resize(got);
+    rd.clear();
+    std::size_t used = 0;
+    err_code e = decode_one<conf>(t, buf.data(), got, used);
+    if (!e) {
+      rd.seekg(start + static_cast<std::streamoff>(used));
+      consume_len = used;
+      return e;
+    }
+    if (e != errc::no_buffer_space || at_end) {
+      rd.seekg(start + static_cast<std::streamoff>(got));  // the bytes read were consumed
+      return e;
+    }
+    want *= 4;
+  }
+}
+}  // namespace detail
+
+template <uint64_t conf = sp_config::DEFAULT, typename T, typename Reader>
+  requires detail::seekable_reader<Reader>
+[[nodiscard]] err_code deserialize_to(T &t, Reader &reader) {
+  detail::check_message_type<T>();
+  std::size_t consumed;
+  return detail::decode_stream<conf>(t, reader, consumed);
+}
+template <typename T, typename Reader>
+  requires detail::seekable_reader<Reader>
+[[nodiscard]] expected<T> deserialize(Reader &reader) {
+  T t{};
+  if (auto e = deserialize_to(t, reader)) return make_unexpected<T>(e);
+  return t;
+}
+template <uint64_t conf, typename T, typename Reader>
+  requires detail::seekable_reader<Reader>
+[[nodiscard]] expected<T> deserialize(Reader &reader) {
+  T t{};
+  if (auto e = deserialize_to<conf>(t, reader)) return make_unexpected<T>(e);
+  return t;
+}
+template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT, typename Reader>
+  requires detail::seekable_reader<Reader>
+[[nodiscard]] expected<field_t<T, I>> get_field(Reader &reader) {
+  static_assert(detail::is_record_v<T>, "get_field reads a member of a record message");
+  T t{};
+  if (auto e = deserialize_to<conf>(t, reader)) return make_unexpected<field_t<T, I>>(e);
+  return expected<field_t<T, I>>(std::get<I>(detail::tie_members(t)));
+}
+template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT, typename Field,
+          typename Reader>
+  requires detail::seekable_reader<Reader>
+[[nodiscard]] err_code get_field_to(Field &dst, Reader &reader) {
+  auto r = get_field<T, I, conf>(reader);
+  if (!r.has_value()) return r.error();
+  dst = std::move(r.value());
+  return {};
 }
 
 // ---- coro_rpc payload batches: n independent serialize(R) messages --------

@@ -294,6 +294,23 @@ spk_layout make_spk_layout() {
     // offsets as u64): a record of 4-byte members and varints rounds up too
     const uint32_t al = b.align < 8 ? 8 : b.align;
     b.L.rec_stride = (b.off + al - 1) / al * al;
+    // a record that is not trivially serializable but has fixed-size members
+    // only (std::tuple<int, bool>, a YLT_REFL type of plain members): its
+    // wire is the members' bytes back to back (packer.hpp:432-447), so its
+    // device record is that packed form, one COPY -- the marshalling writes
+    // a COPY op's bytes in sequence -- and it takes the trivial kernels
+    bool fixed = true;
+    uint32_t bytes = 0;
+    for (uint32_t i = 0; i < b.L.n_ops; ++i) {
+      fixed = fixed && b.L.ops[i].kind == SPK_OP_COPY;
+      bytes += b.L.ops[i].size;
+    }
+    if (fixed && bytes) {
+      b.L.n_ops = 1;
+      b.L.ops[0] = spk_op{SPK_OP_COPY, 0, bytes, 0};
+      b.L.flags = SPK_LAYOUT_TRIVIAL;
+      b.L.rec_stride = bytes;
+    }
   }
   using M = message_type_t<T>;
   fill_fmt(b.L.fmt_vector, get_type_code<std::vector<M>>(),

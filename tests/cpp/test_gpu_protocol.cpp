@@ -330,6 +330,101 @@ int main() {
     struct_pack::serialize_to_with_offset(roff, 20, p);
     CHECK(off.size() == roff.size() && off.substr(20) == roff.substr(20));
   }
+  // 4. stream readers / writers (the reference's test_stream.cpp shapes): a
+  // file of alternating messages written by the reference is read back by
+  // struct_pack::gpu::deserialize(ifstream) and the other way round; the two
+  // files are byte for byte equal; a cut file is no_buffer_space on both
+  {
+    const std::string f_ref = "/tmp/spk_stream_ref.bin", f_gpu = "/tmp/spk_stream_gpu.bin";
+    std::vector<rpcb::person> ps;
+    std::vector<ValidateRequest> vs;  // optionals: the whole-remainder read
+    std::vector<std::vector<RecS>> bs;
+    for (int i = 0; i < 20; ++i) {
+      ps.push_back(make_person(S8, i, 16 + i));
+      ValidateRequest v{};
+      fill(v, 0x5EED001B, i, 8);
+      vs.push_back(v);
+      std::vector<RecS> b(50 + 100 * i);
+      for (uint64_t j = 0; j < b.size(); ++j) b[j] = make_recs(S3, j + i, 48);
+      bs.push_back(b);
+    }
+    {
+      std::ofstream r(f_ref, std::ios::binary), g(f_gpu, std::ios::binary);
+      for (int i = 0; i < 20; ++i) {
+        struct_pack::serialize_to(r, ps[i]);
+        struct_pack::serialize_to(r, vs[i]);
+        struct_pack::serialize_to(r, bs[i]);
+        struct_pack::gpu::serialize_to(g, ps[i]);
+        struct_pack::gpu::serialize_to(g, vs[i]);
+        struct_pack::gpu::serialize_to(g, bs[i]);
+      }
+    }
+    std::ifstream a(f_ref, std::ios::binary), b(f_gpu, std::ios::binary);
+    const std::string ra((std::istreambuf_iterator<char>(a)), std::istreambuf_iterator<char>());
+    const std::string gb((std::istreambuf_iterator<char>(b)), std::istreambuf_iterator<char>());
+    CHECK(!ra.empty() && ra == gb);
+    std::ifstream gi(f_ref, std::ios::binary), ri(f_gpu, std::ios::binary);
+    bool all = true;
+    for (int i = 0; i < 20; ++i) {
+      auto p = struct_pack::gpu::deserialize<rpcb::person>(gi);
+      auto v = struct_pack::gpu::deserialize<ValidateRequest>(gi);
+      std::vector<RecS> rb;
+      auto e = struct_pack::gpu::deserialize_to(rb, gi);
+      all = all && p.has_value() && p.value() == ps[i] && v.has_value() &&
+            struct_pack::serialize<std::string>(v.value()) ==
+                struct_pack::serialize<std::string>(vs[i]) &&
+            !e && rb == bs[i];
+      auto rp = struct_pack::deserialize<rpcb::person>(ri);
+      auto rv = struct_pack::deserialize<ValidateRequest>(ri);
+      auto rr = struct_pack::deserialize<std::vector<RecS>>(ri);
+      all = all && rp.has_value() && rp.value() == ps[i] && rv.has_value() && rr.has_value() &&
+            rr.value() == bs[i];
+    }
+    CHECK(all);
+    CHECK(static_cast<std::size_t>(gi.tellg()) == ra.size());
+    // get_field from a stream (test_stream.cpp:91-138)
+    std::ifstream gf(f_ref, std::ios::binary);
+    auto name = struct_pack::gpu::get_field<rpcb::person, 1>(gf);
+    CHECK(name.has_value() && name.value() == ps[0].name);
+    std::string name2;
+    std::ifstream gf2(f_ref, std::ios::binary);
+    auto fe = struct_pack::gpu::get_field_to<rpcb::person, 1>(name2, gf2);
+    CHECK(!fe && name2 == ps[0].name);
+    // a file cut short (test_stream.cpp:206-224): no_buffer_space on both
+    {
+      std::vector<std::string> data = {"Hello", "Hi", "Hey", "Hoo"};
+      auto buf = struct_pack::serialize<std::string>(data);
+      buf.resize(buf.size() - 5);
+      std::ofstream(f_ref, std::ios::binary).write(buf.data(), buf.size());
+      std::ifstream x(f_ref, std::ios::binary), y(f_ref, std::ios::binary);
+      std::vector<std::string> d1, d2;
+      auto e1 = struct_pack::deserialize_to(d1, x);
+      auto e2 = struct_pack::gpu::deserialize_to(d2, y);
+      CHECK(e1 == struct_pack::errc::no_buffer_space && e2 == struct_pack::errc::no_buffer_space);
+    }
+    // a 2 MiB string cut to 16 bytes and to 2 MiB - 10000 (test_stream.cpp:226-261)
+    for (std::size_t cut : {std::size_t(16), std::size_t(2 * 1024 * 1024 - 10000)}) {
+      auto buf = struct_pack::serialize<std::string>(std::string(2 * 1024 * 1024, 'A'));
+      buf.resize(cut);
+      std::ofstream(f_ref, std::ios::binary).write(buf.data(), buf.size());
+      std::ifstream y(f_ref, std::ios::binary);
+      std::string d;
+      CHECK(struct_pack::gpu::deserialize_to(d, y) == struct_pack::errc::no_buffer_space);
+    }
+    // the whole 2 MiB string message and one record after it
+    {
+      std::ofstream o(f_gpu, std::ios::binary);
+      struct_pack::serialize_to(o, std::string(2 * 1024 * 1024 + 5, 'B'));
+      struct_pack::serialize_to(o, ps[3]);
+    }
+    std::ifstream y(f_gpu, std::ios::binary);
+    std::string big;
+    CHECK(!struct_pack::gpu::deserialize_to(big, y) && big == std::string(2 * 1024 * 1024 + 5, 'B'));
+    auto p3 = struct_pack::gpu::deserialize<rpcb::person>(y);
+    CHECK(p3.has_value() && p3.value() == ps[3]);
+    std::remove(f_ref.c_str());
+    std::remove(f_gpu.c_str());
+  }
   std::printf("{\"checks\": %d, \"failures\": %d}\n", g_checks, g_fail);
   return g_fail ? 1 : 0;
 }

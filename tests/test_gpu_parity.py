@@ -885,7 +885,7 @@ def test_vector_of_zero_fast_varint_records(case):
     cd = codec_for(case)
     n = 5000
     _, recs, heaps = synth.make_batch(case, n, 0x2E80, 8)
-    recs = np.zeros_like(recs)
+    recs = np.zeros(recs.shape, recs.dtype)  # (zeros_like leaves padding bytes unset)
     heaps = [np.zeros_like(h) for h in heaps]
     exp, _, _ = H.oracle_encode(cd.L, C.SPK_MODE_VECTOR, recs, heaps)
     out, _ = cd.serialize(to_dev(cd, recs, heaps), C.SPK_MODE_VECTOR)

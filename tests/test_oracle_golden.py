@@ -243,7 +243,7 @@ def test_min_record_wire_bytes_is_a_lower_bound(case):
     L = LY.case_layout(case)
     n = 64
     _, recs, heaps = synth.make_batch(case, n, 0x2E80, 4)
-    recs = np.zeros_like(recs)
+    recs = np.zeros(recs.shape, recs.dtype)  # (zeros_like leaves padding bytes unset)
     heaps = [np.zeros_like(h) for h in heaps]
     try:
         wire_n, _, _ = H.oracle_encode(L, C.SPK_MODE_VECTOR, recs, heaps)
