@@ -1,5 +1,5 @@
 """K1 statistics of the tile decoder on a synthetic VECTOR message
-(SPK_TILE_DBG=4096): speculative candidate walks, their failures, lanes whose
+(SPK_TILE_DBG=4096, in a codec built with -DSPK_K1_STATS=1): speculative candidate walks, their failures, lanes whose
 speculative start was wrong, resolution rounds and re-walks, chunk-0
 cross-checks; tiles re-walked by the select passes.
 

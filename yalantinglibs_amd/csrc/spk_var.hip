@@ -2592,10 +2592,13 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
                                                       uint32_t *stat = nullptr,
                                                       const VCtl *sc = nullptr) {
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
-  uint64_t &used = st.used, &ex = st.ex, &term_at = st.term_at;
-  uint32_t &cnt = st.cnt;
-  uint64_t *sums = st.sums;
-  SpecPath<NS> &sp = st.sp;
+  // the lane state in locals, copied to st at the end: worked on through
+  // references into st, the compiler kept it in scratch memory (round 3's C4
+  // K1 0.43 -> 0.59 ms; locals: 0.36 ms, same-box A/B in DESIGN §6.1)
+  uint64_t used, ex, term_at;
+  uint32_t cnt;
+  uint64_t sums[NS > 0 ? NS : kVS];
+  SpecPath<NS> sp;
   used = kNoPos;
   ex = kNoPos;
   term_at = kTermPos;
@@ -2819,10 +2822,22 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
     resolve_tile_sp<NS>(P, rd, len, w, cs, ce, lane, X, sp, used, ex, cnt, sums, term_at, stat,
                         kK1Reach<NS>);
   if (stat && used != used0) ++stat[4];
+  st.used = used;
+  st.ex = ex;
+  st.term_at = term_at;
+  st.cnt = cnt;
+  QFOR(q) st.sums[q] = sums[q];
+  st.sp = sp;
   return X;
 }
 
 // ---- K1 ----------------------------------------------------------------------
+// SPK_K1_STATS=1: the K1 statistics of SPK_TILE_DBG=4096 (scripts/diag_tiles.py)
+// compiled in (off by default: the run-time null checks in the walk loop
+// cost C4's K1 2 %)
+#ifndef SPK_K1_STATS
+#define SPK_K1_STATS 0
+#endif
 // W: the count width as a compile-time constant (0: read from the header at
 // run time). The walkers' count reads, screens and bounds checks then carry
 // no width switch: nested walks are divergent loops, so every branch of the
@@ -2849,9 +2864,9 @@ __device__ __forceinline__ void vec_tile_spec_body(const DecArgs &a, const WalkP
   TileLane<NS> st;
   uint32_t stat[6] = {0, 0, 0, 0, 0, 0};
   const uint64_t X = tile_spec_resolve<NS>(P, rd, len, w, ts, wend, cs, ce, lane, t == 0 && !rng,
-                                           p0, dbg, st, (dbg & 4096) ? stat : nullptr,
+                                           p0, dbg, st, (SPK_K1_STATS && (dbg & 4096)) ? stat : nullptr,
                                            (NS > -2 && SPK_SCAP) ? c : nullptr);
-  if (dbg & 4096) {  // K1 statistics (scripts/diag_tiles.py)
+  if (SPK_K1_STATS && (dbg & 4096)) {  // K1 statistics (scripts/diag_tiles.py)
     FCtl *fcd = reinterpret_cast<FCtl *>(const_cast<uint8_t *>(ws) + kWsFCtl);
     for (uint32_t k = 0; k < 6; ++k) {
       const uint64_t v = wave_sum_u64(stat[k]);
@@ -2863,9 +2878,9 @@ __device__ __forceinline__ void vec_tile_spec_body(const DecArgs &a, const WalkP
       atomicAdd(&fcd->diag[7], (unsigned long long)dt);
     }
   }
-  uint64_t &used = st.used, &ex = st.ex;
-  uint32_t &cnt = st.cnt;
-  uint64_t *sums = st.sums;
+  const uint64_t used = st.used, ex = st.ex;
+  const uint32_t cnt = st.cnt;
+  const uint64_t *sums = st.sums;
   uint64_t tcnt = wave_sum_u64(cnt), tsum[NS > 0 ? NS : kVS];
   QFOR(q) tsum[q] = wave_sum_u64(sums[q]);
   // ---- 3. entry alternatives (tile 0's entry is exact) ----
@@ -2934,7 +2949,7 @@ __device__ __forceinline__ void vec_tile_spec_body(const DecArgs &a, const WalkP
 }
 
 #ifndef SPK_WSPEC  // 1: K1 of the nested walk program per count width; 2: every layout
-#define SPK_WSPEC 1
+#define SPK_WSPEC 2   // (2: C4 K1 -15 %, C3 -13 %, cv -5 % against 1, same-box A/B)
 #endif
 template <int NS>
 __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkProg P,
