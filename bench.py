@@ -40,6 +40,12 @@ CONFIGS = {
             "C2 mode B: 100M independent 68-byte Rec64 messages per GPU (coro_rpc payload shape)"),
     "c3": ("recs", 10_000_000, 48, "A",
            "C3: 10M RecS{int32, std::string len U[0,48], double} per GPU, one vector message"),
+    "c3r": ("recs", 10_000_000, 48 | 1 << 31, "A",
+            "C3 with binary strings: 10M RecS{int32, std::string of random bytes len U[0,48], "
+            "double} per GPU, one vector message"),
+    "c3l": ("recs", 2_000_000, 3000 | 100 << 16 | 1 << 31, "A",
+            "C3 with long binary strings: 2M RecS{int32, std::string of random bytes len "
+            "U[100,3000], double} per GPU, one vector message"),
     "c4": ("outer", 10_000_000, 16, "A",
            "C4: 10M Outer{int64, vector<Inner{int32,float}> n U[0,16]} per GPU, one vector message"),
     "cv": ("var", 10_000_000, 16, "A",
@@ -50,7 +56,7 @@ CONFIGS = {
            "2 x int16, 2 strings, enum, vector<Weapon{string,int16}>, Weapon, vector<Vec3>): "
            "10M per GPU, one vector message"),
 }
-EXTRA = ["c2b", "c3", "c4", "c5", "cv", "cm"]  # timed beside the C2 headline at N=1
+EXTRA = ["c2b", "c3", "c3r", "c3l", "c4", "c5", "cv", "cm"]  # timed beside the C2 headline at N=1
 SEEDS = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004, "var": 0x5EED000C,
          "monster": 0x5EED001E}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)

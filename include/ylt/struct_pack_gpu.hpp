@@ -31,6 +31,7 @@
 //
 // Build: <c++20 compiler> -I include ... -L yalantinglibs_amd -lspk_codec
 #pragma once
+#include <cstdlib>
 #include <cstring>
 #include <ios>
 #include <memory>
@@ -82,10 +83,12 @@ template <typename T>
 constexpr bool supported() {
   if constexpr (is_fundamental_v<T> || is_string_v<T> || is_varint_v<T>) {
     return true;
+  } else if constexpr (is_trivial_view_v<T>) {
+    return is_trivially_serializable<typename trivial_view_traits<T>::value_type>();
   } else if constexpr (is_container_v<T>) {
     return supported<elem_t<T>>();
   } else if constexpr (is_std_optional<T>::value || is_compat_v<T>) {
-    return supported<remove_cvref_t<typename T::value_type>>();
+    return supported<opt_value_t<T>>();
   } else if constexpr (is_std_variant<T>::value) {
     return variant_supported<T>::value;
   } else if constexpr (is_std_array<T>::value) {
@@ -224,12 +227,15 @@ class codec {
   static constexpr bool trivial = detail::is_trivially_serializable<R>();
 
   // ---- staging (host <-> device) -----------------------------------------
-  batch<R> upload(const R *v, std::size_t n) {
+  // X = R, or M for R = boxed<M> (the message marshalled as boxed<M>'s one
+  // member, without a copy: a std::unique_ptr message cannot be copied)
+  template <typename X = R>
+  batch<R> upload(const X *v, std::size_t n) {
     const spk_layout &L = layout();
     batch<R> b;
     b.n = n;
     b.recs.resize(n * L.rec_stride);
-    if constexpr (trivial) {
+    if constexpr (trivial && std::is_same_v<X, R>) {
       copy(b.recs.data(), v, n * sizeof(R), SPK_COPY_H2D, s_);
       sync(s_);
     } else {
@@ -250,18 +256,21 @@ class codec {
     return b;
   }
 
-  // ok(i) selects the records to materialise (failed messages stay default)
-  template <typename Pred = std::nullptr_t>
-  void download(const batch<R> &b, std::size_t n, R *out, Pred ok = nullptr) {
+  // ok(i) selects the records to materialise (failed messages stay default);
+  // X = R, or M for R = boxed<M>
+  template <typename X = R, typename Pred = std::nullptr_t>
+  void download(const batch<R> &b, std::size_t n, X *out, Pred ok = nullptr) {
     const spk_layout &L = layout();
-    if constexpr (trivial) {
+    if constexpr (trivial && std::is_same_v<X, R>) {
       copy(out, b.recs.data(), n * sizeof(R), SPK_COPY_D2H, s_);
       sync(s_);
     } else {
-      std::vector<uint8_t> recs(n * L.rec_stride);
-      // kept in the codec: string_view / span members of the decoded objects
-      // alias these host heaps, valid until this thread's next decode of R
-      // (the reference's views alias its input buffer, unpacker.hpp:1135-1145)
+      // kept in the codec: string_view / span / trivial_view members of the
+      // decoded objects alias these host records and heaps, valid until this
+      // thread's next decode of R (the reference's views alias its input
+      // buffer, unpacker.hpp:787-800,1135-1145)
+      std::vector<uint8_t> &recs = view_recs_;
+      recs.assign(n * L.rec_stride, 0);
       std::vector<std::vector<uint8_t>> &heaps = view_heaps_;
       heaps.assign(n_spans(), {});
       copy(recs.data(), b.recs.data(), recs.size(), SPK_COPY_D2H, s_);
@@ -376,6 +385,35 @@ class codec {
     return r;
   }
 
+  // after plan(SPK_MODE_VECTOR): the records' bytes only, every container
+  // count at `width` bytes (spk_encode_body; struct_pack::write,
+  // user_helper.hpp:16-30). Stream-ordered, no sync.
+  void encode_body(const batch<R> &b, uint32_t width, void *d_out, std::size_t cap) {
+    std::vector<const void *> hp = heap_ptrs(b);
+    check(spk_encode_body(&layout(), b.n, b.recs.data(), hp.data(), width, d_out, cap,
+                          ws_.data(), ws_.size(), s_), "spk_encode_body");
+  }
+  // exactly n records from a body at `width` (spk_decode_body; struct_pack::
+  // read, user_helper.hpp:31-64); result->consumed = body bytes used
+  spk_dresult_t decode_body(batch<R> &out, const void *d_body, std::size_t len, uint32_t width,
+                            std::size_t n) {
+    ws_.resize(spk_workspace_bytes(&layout(), SPK_MODE_VECTOR, out.n, len));
+    res_.resize(sizeof(spk_dresult_t));
+    std::vector<void *> hp(n_spans() ? n_spans() : 1, nullptr);
+    std::vector<uint64_t> caps(n_spans() ? n_spans() : 1, 0);
+    for (uint32_t k = 0; k < n_spans(); ++k) {
+      hp[k] = out.heaps[k].data();
+      caps[k] = out.heap_elems[k];
+    }
+    check(spk_decode_body(&layout(), d_body, len, width, n, out.recs.data(), out.n, hp.data(),
+                          caps.data(), (spk_dresult_t *)res_.data(), ws_.data(), ws_.size(), s_),
+          "spk_decode_body");
+    spk_dresult_t r{};
+    copy(&r, res_.data(), sizeof(r), SPK_COPY_D2H, s_);
+    sync(s_);
+    return r;
+  }
+
   // a batch able to hold the decode of a `len`-byte wire buffer into at most
   // max_records records: every heap can hold the whole wire
   batch<R> alloc_for_wire(std::size_t len, std::size_t max_records) {
@@ -386,6 +424,15 @@ class codec {
     for (uint32_t k = 0; k < n_spans(); ++k) {
       b.heap_elems.push_back(caps[k]);
       b.heaps.emplace_back(caps[k] * span_elem(k));
+    }
+    if (const char *z = std::getenv("SPK_GPU_ZERO_ALLOC"); z && z[0] == '1') {  // (diagnostic)
+      auto zero = [&](buffer &x, std::size_t nb) {
+        std::vector<uint8_t> h(nb, z[1] == 'g' ? 0xAB : 0);
+        copy(x.data(), h.data(), nb, SPK_COPY_H2D, s_);
+        sync(s_);
+      };
+      zero(b.recs, max_records * layout().rec_stride);
+      for (uint32_t k = 0; k < n_spans(); ++k) zero(b.heaps[k], caps[k] * span_elem(k));
     }
     return b;
   }
@@ -417,6 +464,7 @@ class codec {
   void *s_;
   buffer ws_, plan_, res_;
   std::vector<std::vector<uint8_t>> view_heaps_;
+  std::vector<uint8_t> view_recs_;
 };
 
 // A connection's request frames in arrival order, function ids interleaved:
@@ -533,14 +581,7 @@ struct staged_message {
       c.encode(b, SPK_MODE_VECTOR, out.data(), out.size());
     } else {
       auto &c = device::thread_codec<R, conf>();
-      auto b = [&] {
-        if constexpr (tr::boxed) {
-          const R box{t};  // the message as the one member of boxed<M>
-          return c.upload(&box, 1);
-        } else {
-          return c.upload(&t, 1);
-        }
-      }();
+      auto b = c.upload(&t, 1);  // (boxed<M>: t is its one member)
       plan = c.plan(b, SPK_MODE_MESSAGES);
       len = plan.total_bytes;
       out.resize(len);
@@ -632,12 +673,8 @@ err_code decode_one_dev(T &t, const char *data, std::size_t size, std::size_t &c
       T out(r.count);
       c.download(b, r.count, out.data());
       t = std::move(out);
-    } else if constexpr (tr::boxed) {
-      R box{};
-      c.download(b, 1, &box);
-      t = std::move(box.v);
     } else {
-      c.download(b, 1, &t);
+      c.download(b, 1, &t);  // (boxed<M>: t is its one member)
     }
     consume_len = r.consumed;
     return {};
@@ -682,10 +719,6 @@ serialize_buffer_size needed_size_dev(const T &t) {
   if constexpr (tr::vector) {
     auto b = c.upload(t.data(), t.size());
     p = c.plan(b, SPK_MODE_VECTOR);
-  } else if constexpr (tr::boxed) {
-    const R box{t};
-    auto b = c.upload(&box, 1);
-    p = c.plan(b, SPK_MODE_MESSAGES);
   } else {
     auto b = c.upload(&t, 1);
     p = c.plan(b, SPK_MODE_MESSAGES);
@@ -942,13 +975,15 @@ inline bool prefix_decode_exact(const spk_layout &L) {
   return true;
 }
 
-template <uint64_t conf, typename T, typename Reader>
-err_code decode_stream(T &t, Reader &rd, std::size_t &consume_len) {
-  using tr = msg_traits<T>;
+// read a growing block from `rd` and decode it with fn(data, size, used) until
+// the decode succeeds or fails for a reason other than a short buffer; the
+// reader is left after the bytes the decode used (after the bytes read on an
+// error). exact = false: read the whole remainder at once (a prefix may
+// decode "successfully" where the full message would not)
+template <typename Reader, typename Fn>
+err_code stream_decode(Reader &rd, bool exact, std::size_t &consume_len, Fn &&fn) {
   consume_len = 0;
   const auto start = rd.tellg();
-  bool exact = true;
-  if constexpr (!tr::empty) exact = prefix_decode_exact(device::codec<typename tr::rec, conf>::layout());
   std::size_t want = std::size_t(1) << 16;
   if (!exact) {  // the whole remainder
     rd.seekg(0, std::ios_base::end);
@@ -966,7 +1001,7 @@ err_code decode_stream(T &t, Reader &rd, std::size_t &consume_len) {
     buf.resize(got);
     rd.clear();
     std::size_t used = 0;
-    err_code e = decode_one<conf>(t, buf.data(), got, used);
+    err_code e = fn(buf.data(), got, used);
     if (!e) {
       rd.seekg(start + static_cast<std::streamoff>(used));
       consume_len = used;
@@ -978,6 +1013,16 @@ err_code decode_stream(T &t, Reader &rd, std::size_t &consume_len) {
     }
     want *= 4;
   }
+}
+
+template <uint64_t conf, typename T, typename Reader>
+err_code decode_stream(T &t, Reader &rd, std::size_t &consume_len) {
+  using tr = msg_traits<T>;
+  bool exact = true;
+  if constexpr (!tr::empty) exact = prefix_decode_exact(device::codec<typename tr::rec, conf>::layout());
+  return stream_decode(rd, exact, consume_len, [&](const char *d, std::size_t n, std::size_t &u) {
+    return decode_one<conf>(t, d, n, u);
+  });
 }
 }  // namespace detail
 
@@ -1018,6 +1063,122 @@ template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT, typenam
   if (!r.has_value()) return r.error();
   dst = std::move(r.value());
   return {};
+}
+
+// ---- user helpers: struct_pack::write / read / get_write_size --------------
+// (user_helper.hpp:16-85) The payload bytes of t (or of t[0..len)) without
+// header, container counts at size_width bytes: the body of a VECTOR message
+// at that width, so the device codec writes and reads it
+// (spk_encode_body / spk_decode_body). Used by sp_serialize_to /
+// sp_deserialize_to of user-defined types (test_user_defined_type.cpp:55-120).
+namespace detail {
+template <typename T>
+using helper_rec_t = std::conditional_t<record_supported<T>(), T, boxed<T>>;
+
+template <std::size_t W, uint64_t conf, typename T>
+struct staged_body {
+  using R = helper_rec_t<T>;
+  device::buffer out;
+  std::size_t len = 0;
+  staged_body(const T *t, std::size_t n) {
+    static_assert(W == 1 || W == 2 || W == 4 || W == 8, "size_width must be 1, 2, 4 or 8");
+    auto &c = device::thread_codec<R, conf>();
+    auto b = c.upload(t, n);  // (boxed<T>: each t[i] is its one member)
+    const spk_plan_t p = c.plan(b, SPK_MODE_VECTOR);
+    if (c.layout().flags & SPK_LAYOUT_TRIVIAL) {
+      len = n * c.layout().rec_stride;
+    } else {
+      const uint64_t fields = p.width ? (p.total_bytes - p.header_bytes - p.var_bytes) / p.width : 0;
+      len = p.var_bytes + fields * W;
+    }
+    out.resize(len);
+    c.encode_body(b, W, out.data(), len);
+  }
+  void copy_to(void *dst) {
+    auto &c = device::thread_codec<R, conf>();
+    device::copy(dst, out.data(), len, SPK_COPY_D2H, c.stream());
+    device::sync(c.stream());
+  }
+};
+
+// read n records of T from a body in host memory; consumed = body bytes used
+template <std::size_t W, uint64_t conf, typename T>
+err_code decode_body_host(T *t, std::size_t n, const char *data, std::size_t size,
+                          std::size_t &consumed) {
+  using R = helper_rec_t<T>;
+  auto &c = device::thread_codec<R, conf>();
+  consumed = 0;
+  device::buffer wire(size + 16);
+  device::copy(wire.data(), data, size, SPK_COPY_H2D, c.stream());
+  auto b = c.alloc_for_wire(size, n);
+  spk_dresult_t r = c.decode_body(b, wire.data(), size, W, n);
+  if (r.errc == SPK_ERRC_CAPACITY)  // heaps hold the whole wire: unreachable
+    throw std::logic_error("struct_pack::gpu: decode capacity invariant broken");
+  if (r.errc) return static_cast<errc>(r.errc);
+  for (uint32_t k = 0; k < c.n_spans(); ++k) b.heap_elems[k] = r.heap_used[k];
+  c.download(b, n, t);  // (boxed<T>: each t[i] is its one member)
+  consumed = r.consumed;
+  return {};
+}
+}  // namespace detail
+
+template <std::size_t size_width = sizeof(uint64_t), typename Writer, typename T>
+void write(Writer &writer, const T *t, std::size_t len) {
+  static_assert(is_gpu_message_v<T>, "struct_pack::gpu::write: type outside the record model");
+  detail::staged_body<size_width, sp_config::DEFAULT, T> m(t, len);
+  std::vector<char> tmp(m.len);
+  if (m.len) m.copy_to(tmp.data());
+  writer.write(tmp.data(), tmp.size());
+}
+template <std::size_t size_width = sizeof(uint64_t), typename Writer, typename T>
+void write(Writer &writer, const T &t) {
+  write<size_width>(writer, &t, 1);
+}
+template <std::size_t size_width = sizeof(uint64_t), typename T>
+std::size_t get_write_size(const T *t, std::size_t len) {
+  return detail::staged_body<size_width, sp_config::DEFAULT, T>(t, len).len;
+}
+template <std::size_t size_width = sizeof(uint64_t), typename T>
+std::size_t get_write_size(const T &t) {
+  return get_write_size<size_width>(&t, 1);
+}
+// read from a byte view (advancing `pos`) or a seekable reader (left after
+// the bytes read); ifSkip: consume without keeping the values
+template <std::size_t size_width = sizeof(uint64_t), bool ifSkip = false, typename T>
+err_code read_from(const char *data, std::size_t size, std::size_t &pos, T *t, std::size_t len) {
+  std::size_t used = 0;
+  err_code e;
+  if constexpr (ifSkip) {
+    std::vector<T> sink(len);
+    e = detail::decode_body_host<size_width, sp_config::DEFAULT>(sink.data(), len, data + pos,
+                                                                  size - pos, used);
+  } else {
+    e = detail::decode_body_host<size_width, sp_config::DEFAULT>(t, len, data + pos, size - pos,
+                                                                  used);
+  }
+  pos += used;
+  return e;
+}
+template <std::size_t size_width = sizeof(uint64_t), bool ifSkip = false, typename Reader,
+          typename T>
+  requires detail::seekable_reader<Reader>
+err_code read(Reader &reader, T *t, std::size_t len) {
+  using R = detail::helper_rec_t<T>;
+  const bool exact = detail::prefix_decode_exact(device::codec<R, sp_config::DEFAULT>::layout());
+  std::size_t consumed;
+  return detail::stream_decode(reader, exact, consumed,
+                               [&](const char *d, std::size_t n, std::size_t &u) {
+                                 std::size_t pos = 0;
+                                 auto e = read_from<size_width, ifSkip>(d, n, pos, t, len);
+                                 u = pos;
+                                 return e;
+                               });
+}
+template <std::size_t size_width = sizeof(uint64_t), bool ifSkip = false, typename Reader,
+          typename T>
+  requires detail::seekable_reader<Reader>
+err_code read(Reader &reader, T &t) {
+  return read<size_width, ifSkip>(reader, &t, 1);
 }
 
 // ---- coro_rpc payload batches: n independent serialize(R) messages --------

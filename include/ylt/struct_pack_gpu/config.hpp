@@ -136,6 +136,25 @@ inline bool operator==(const compatible<T, v1> &a, const compatible<T, v2> &b) {
   return static_cast<bool>(a) == static_cast<bool>(b) && (!a || *a == *b);
 }
 
+// trivial_view.hpp:79-102: a view of a trivially serializable T, equal to T
+// in the type system and on the wire
+template <typename T, typename = void>
+struct trivial_view {
+ private:
+  const T *ref;
+
+ public:
+  trivial_view(const T *t) : ref(t) {}
+  trivial_view(const T &t) : ref(&t) {}
+  trivial_view(const trivial_view &) = default;
+  trivial_view() : ref(nullptr) {}
+  trivial_view &operator=(const trivial_view &) = default;
+  using value_type = T;
+  void set(const T &obj) { ref = &obj; }
+  const T &get() const { return *ref; }
+  const T *operator->() const { return ref; }
+};
+
 }  // namespace struct_pack
 
 // ---- YLT_REFL(Type, member...) ---------------------------------------------
@@ -246,6 +265,14 @@ template <typename T>
 struct varint_traits<struct_pack::detail::sint<T>> : std::true_type {
   using value_type = T;
   static constexpr bool zigzag = true;
+};
+
+// ---- trivial_view<T> members (trivial_view.hpp:79-102) ----------------------
+template <typename T>
+struct trivial_view_traits : std::false_type {};
+template <typename T, typename E>
+struct trivial_view_traits<struct_pack::trivial_view<T, E>> : std::true_type {
+  using value_type = T;
 };
 
 // ---- compatible<T, version> members (compatible.hpp:21-154) ------------------

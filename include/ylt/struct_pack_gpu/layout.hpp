@@ -149,6 +149,9 @@ template <typename T>
 void flatten_into(layout_builder &b) {
   if constexpr (is_trivially_serializable<T>()) {
     b.copy(sizeof(T), alignof(T));
+  } else if constexpr (is_trivial_view_v<T>) {  // T's bytes (packer.hpp:243-245)
+    using E = typename trivial_view_traits<T>::value_type;
+    b.copy(sizeof(E), alignof(E));
   } else if constexpr (is_varint_v<T>) {
     b.varint(sizeof(typename varint_traits<T>::value_type),
              varint_traits<T>::zigzag ? SPK_VARINT_ZIGZAG : 0u);
@@ -161,7 +164,7 @@ void flatten_into(layout_builder &b) {
     else
       flatten_array<E>(b);
   } else if constexpr (is_std_optional<T>::value) {
-    using E = remove_cvref_t<typename T::value_type>;
+    using E = opt_value_t<T>;
     if constexpr (is_trivially_serializable<E>()) {
       b.span(sizeof(E), SPK_OP_OPTION);
     } else {  // SPK_OP_OPTGROUP: u32 has_value, E's fields inline (packer.hpp:382-388)
@@ -477,6 +480,8 @@ template <typename T>
 void to_device(const T &v, marshal_state &s) {
   if constexpr (is_trivially_serializable<T>()) {
     put_copy(s, &v, sizeof(T));
+  } else if constexpr (is_trivial_view_v<T>) {
+    put_copy(s, &v.get(), sizeof(typename trivial_view_traits<T>::value_type));
   } else if constexpr (is_varint_v<T>) {
     const spk_op &op = s.L->ops[s.op++];
     const typename varint_traits<T>::value_type x = v;
@@ -519,9 +524,9 @@ void to_device(const T &v, marshal_state &s) {
       s.span = h + 1 + nh;
     }
   } else if constexpr (is_std_optional<T>::value || is_compat_v<T>) {
-    using E = remove_cvref_t<typename T::value_type>;
+    using E = opt_value_t<T>;
     const spk_op &op = s.L->ops[s.op];
-    const uint32_t cnt = v.has_value() ? 1u : 0u;
+    const uint32_t cnt = opt_has(v) ? 1u : 0u;
     if constexpr (is_trivially_serializable<E>()) {  // OPTION / COMPAT: heap value
       auto &heap = (*s.heaps)[s.span++];
       ++s.op;
@@ -627,6 +632,18 @@ template <typename T>
 void from_device(T &v, unmarshal_state &s) {
   if constexpr (is_trivially_serializable<T>()) {
     get_copy(s, &v, sizeof(T));
+  } else if constexpr (is_trivial_view_v<T>) {
+    // the view points into the decoded host record (kept by the codec until
+    // this thread's next decode of the type; the reference's view points
+    // into its input buffer, unpacker.hpp:787-800)
+    using E = typename trivial_view_traits<T>::value_type;
+    const spk_op &op = s.L->ops[s.op];
+    v.set(*reinterpret_cast<const E *>(s.rec + op.rec_off + s.within));
+    s.within += sizeof(E);
+    if (s.within == op.size) {
+      ++s.op;
+      s.within = 0;
+    }
   } else if constexpr (is_varint_v<T>) {
     const spk_op &op = s.L->ops[s.op++];
     typename varint_traits<T>::value_type x;
@@ -678,14 +695,14 @@ void from_device(T &v, unmarshal_state &s) {
       s.span = h + 1 + nh;
     }
   } else if constexpr (is_std_optional<T>::value || is_compat_v<T>) {
-    using E = remove_cvref_t<typename T::value_type>;
+    using E = opt_value_t<T>;
     const spk_op &op = s.L->ops[s.op];
     const uint32_t cnt = get_u32(s.rec, op.rec_off);
     if constexpr (is_trivially_serializable<E>()) {
       const uint8_t *heap = s.heaps[s.span++];
       ++s.op;
       if (cnt) {
-        v.emplace();
+        opt_emplace(v);
         std::memcpy(static_cast<void *>(&*v), heap + get_u64(s.rec, op.aux) * op.size, op.size);
       } else {
         v.reset();
@@ -695,7 +712,7 @@ void from_device(T &v, unmarshal_state &s) {
       uint32_t nh = 0;
       const uint32_t next = skip_group(s.L, first, nh);
       if (cnt) {
-        v.emplace();
+        opt_emplace(v);
         unmarshal_state g{s.L, s.rec, first, 0, s.heaps, h0};
         from_device(*v, g);
       } else {

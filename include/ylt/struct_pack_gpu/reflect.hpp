@@ -23,6 +23,7 @@
 #include <unordered_set>
 #include <variant>
 #include <cstdint>
+#include <memory>
 #include <optional>
 #include <span>
 #include <string>
@@ -43,8 +44,39 @@ template <typename T> struct is_std_vector : std::false_type {};
 template <typename T, typename A> struct is_std_vector<std::vector<T, A>> : std::true_type {};
 template <typename T> struct is_std_span : std::false_type {};
 template <typename T, std::size_t E> struct is_std_span<std::span<T, E>> : std::bool_constant<E == std::dynamic_extent> {};
+// optional-like members: std::optional<T> and a non-polymorphic
+// std::unique_ptr<T> share the type literal (optional_t, type_id.hpp:337-346)
+// and the wire [has_value][T] (packer.hpp:271-283,382-388)
 template <typename T> struct is_std_optional : std::false_type {};
 template <typename T> struct is_std_optional<std::optional<T>> : std::true_type {};
+template <typename T, typename D> struct is_std_optional<std::unique_ptr<T, D>> : std::true_type {
+  static_assert(!std::is_polymorphic_v<T>,
+                "struct_pack::gpu: polymorphic std::unique_ptr<Base> members are not supported");
+};
+template <typename T> struct is_std_unique_ptr : std::false_type {};
+template <typename T, typename D> struct is_std_unique_ptr<std::unique_ptr<T, D>> : std::true_type {};
+// the value type of an optional-like / array / compatible / container type
+template <typename T, bool = is_std_unique_ptr<T>::value>
+struct opt_value {
+  using type = std::remove_cv_t<std::remove_reference_t<typename T::value_type>>;
+};
+template <typename T>
+struct opt_value<T, true> {
+  using type = std::remove_cv_t<typename T::element_type>;
+};
+template <typename T>
+using opt_value_t = typename opt_value<T>::type;
+template <typename T>
+bool opt_has(const T &v) {
+  return static_cast<bool>(v);
+}
+template <typename T>
+void opt_emplace(T &v) {
+  if constexpr (is_std_unique_ptr<T>::value)
+    v = std::make_unique<typename T::element_type>();
+  else
+    v.emplace();
+}
 template <typename T> struct is_std_array : std::false_type {};
 template <typename T, std::size_t N> struct is_std_array<std::array<T, N>> : std::true_type {};
 
@@ -124,6 +156,8 @@ template <typename T>
 constexpr bool is_varint_v = varint_traits<T>::value;
 template <typename T>
 constexpr bool is_compat_v = compat_traits<T>::value;
+template <typename T>
+constexpr bool is_trivial_view_v = trivial_view_traits<T>::value;
 template <typename T>
 constexpr bool is_aggregate_record_v = std::is_aggregate_v<T> && std::is_class_v<T> &&
                                        !is_std_array<T>::value && !is_string_v<T> &&

@@ -124,6 +124,8 @@ constexpr bool is_trivially_serializable() {
     return false;  // reflection.hpp:872-876,899-905
   } else if constexpr (is_ylt_refl_v<T>) {
     return false;  // user_defined_refl: member by member (reflection.hpp:896-898)
+  } else if constexpr (is_trivial_view_v<T>) {
+    return false;  // its record goes member by member (reflection.hpp:875-877)
   } else if constexpr (is_std_tuple<T>::value) {
     return false;  // std::tuple: member by member (reflection.hpp:893-895)
   } else {
@@ -150,7 +152,7 @@ constexpr bool has_container() {
   else if constexpr (is_std_variant<T>::value)  // type_calculate.hpp:785-815
     return variant_any_container<T>::value;
   else if constexpr (is_std_array<T>::value || is_std_optional<T>::value || is_compat_v<T>)
-    return has_container<typename T::value_type>();  // type_calculate.hpp:846-849
+    return has_container<opt_value_t<T>>();  // type_calculate.hpp:846-849
   else if constexpr (is_record_v<T>) {
     using M = members_tuple_t<T>;
     return any_container<M>(std::make_index_sequence<std::tuple_size_v<M>>{});
@@ -244,7 +246,9 @@ constexpr void append_alternatives(lit_t &l, std::variant<A...> *) {
 template <typename T>
 constexpr lit_t type_literal() {
   lit_t l;
-  if constexpr (is_fundamental_v<T>) {
+  if constexpr (is_trivial_view_v<T>) {  // T's literal (type_calculate.hpp:196-198)
+    l.append(type_literal<typename trivial_view_traits<T>::value_type>());
+  } else if constexpr (is_fundamental_v<T>) {
     l.push(fundamental_id<T>());
   } else if constexpr (is_string_v<T>) {
     l.push(TID_STRING);
@@ -270,9 +274,9 @@ constexpr lit_t type_literal() {
     constexpr bool zz = varint_traits<T>::zigzag;
     l.push(sizeof(V) == 4 ? (zz ? TID_VINT32 : TID_VUINT32) : (zz ? TID_VINT64 : TID_VUINT64));
   } else if constexpr (is_compat_v<T>) {  // not in the literal (type_calculate.hpp:298-303)
-  } else if constexpr (is_std_optional<T>::value) {  // type_calculate.hpp:273-278
+  } else if constexpr (is_std_optional<T>::value) {  // type_calculate.hpp:269-278
     l.push(TID_OPTIONAL);
-    l.append(type_literal<remove_cvref_t<typename T::value_type>>());
+    l.append(type_literal<opt_value_t<T>>());
   } else if constexpr (is_std_array<T>::value) {
     l.push(TID_ARRAY);
     l.append(type_literal<typename T::value_type>());

@@ -452,12 +452,22 @@ inline Rec64 make_rec64(uint64_t seed, uint64_t i) {
 }
 
 // string of record i: length rnd(i,1) % (maxlen+1); char j from word 2+j/8
-inline std::string make_chars(uint64_t seed, uint64_t i, uint32_t maxlen) {
-  uint32_t len = (uint32_t)(rnd(seed, i, 1) % (uint64_t)(maxlen + 1));
+// param: maxlen in bits 0-15, minlen in bits 16-30 (length U[minlen,
+// maxlen]), bit 31: any byte value instead of 'a'..'z' (bench c3r / c3l:
+// binary std::string payloads); a plain maxlen < 65536 is the original U[0, maxlen]
+inline uint32_t chars_len(uint64_t seed, uint64_t i, uint32_t param) {
+  const uint32_t mx = param & 0xFFFFu, mn = (param >> 16) & 0x7FFFu;
+  return mn + (uint32_t)(rnd(seed, i, 1) % (uint64_t)(mx - mn + 1));
+}
+inline std::string make_chars(uint64_t seed, uint64_t i, uint32_t param) {
+  const uint32_t len = param < 0x10000u ? (uint32_t)(rnd(seed, i, 1) % (uint64_t)(param + 1))
+                                        : chars_len(seed, i, param);
+  const bool raw = (param >> 31) != 0;
   std::string s(len, '\0');
   for (uint32_t j = 0; j < len; ++j) {
     uint64_t w = rnd(seed, i, 2 + (j >> 3) % 56);  // words 2..57, recycled
-    s[j] = (char)('a' + ((w >> ((j & 7) * 8)) & 0xFF) % 26);
+    const uint32_t b = (uint32_t)((w >> ((j & 7) * 8)) & 0xFF);
+    s[j] = (char)(raw ? b : 'a' + b % 26);
   }
   return s;
 }

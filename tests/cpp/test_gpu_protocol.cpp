@@ -9,9 +9,15 @@
 // codes equal the reference's at compile time. The binary is built by
 // __graft_entry__.build() into oracle/_ref/ (it contains reference code) and
 // run by tests/test_gpu_cpp.py on the GPU box.
+#include <csignal>
 #include <cstdio>
+#include <execinfo.h>
+#include <unistd.h>
 #include <cstring>
 #include <fstream>
+#include <sstream>
+#include <array>
+#include <memory>
 #include <iterator>
 #include <map>
 #include <optional>
@@ -32,7 +38,7 @@ using coro_rpc::protocol::struct_pack_gpu_protocol;
 using coro_rpc::protocol::struct_pack_protocol;
 using rpc_protocol = coro_rpc::protocol::coro_rpc_protocol;
 
-static int g_fail = 0, g_checks = 0;
+static int g_fail = 0, g_checks = 0, g_section = 0;
 #define CHECK(c)                                                                 \
   do {                                                                           \
     ++g_checks;                                                                  \
@@ -142,6 +148,42 @@ std::vector<Maps> echo_maps(std::vector<Maps> v) { return v; }
 std::vector<Tags> echo_tags(std::vector<Tags> v) { return v; }
 std::vector<Vnt> echo_vnt(std::vector<Vnt> v) { return v; }
 
+// unique_ptr members (optional-like: packer.hpp:271-283), trivial_view
+// members (trivial_view.hpp:79-102) and the same record without the view
+struct UPtrRec {
+  int32_t id;
+  std::unique_ptr<std::string> s;
+  std::unique_ptr<Inner> p;
+  std::unique_ptr<std::vector<int32_t>> v;
+  std::unique_ptr<RecS> r;
+};
+struct ViewData {
+  std::array<int32_t, 6> a;
+  double d;
+};
+struct ViewRec {
+  std::string name;
+  struct_pack::trivial_view<ViewData> data;
+  int32_t k;
+};
+struct PlainRec {
+  std::string name;
+  ViewData data;
+  int32_t k;
+};
+static_assert(struct_pack::gpu::hash_matches_reference<UPtrRec>() &&
+              struct_pack::gpu::hash_matches_reference<std::vector<UPtrRec>>() &&
+              struct_pack::gpu::hash_matches_reference<ViewRec>() &&
+              struct_pack::gpu::hash_matches_reference<std::tuple<rpcb::person, int>>() &&
+              struct_pack::gpu::hash_matches_reference<std::unique_ptr<Inner>>());
+static_assert(struct_pack::get_type_code<ViewRec>() == struct_pack::get_type_code<PlainRec>());
+
+// a writer for the user helpers (struct_pack::write needs write(const char*, size_t))
+struct str_writer {
+  std::string buf;
+  void write(const char *p, std::size_t n) { buf.append(p, n); }
+};
+
 // the executor as coro_rpc's router calls it (router.hpp:155-163)
 template <auto func, typename Proto>
 std::pair<coro_rpc::err_code, std::string> run(std::string_view args) {
@@ -177,12 +219,24 @@ void call_same_as_reference(const char *what, const Args &...args) {
                  gpu.second.size());
 }
 
+static void on_fault(int sig) {  // a host fault: where (stderr), then die
+  void *bt[64];
+  const int n = backtrace(bt, 64);
+  std::fprintf(stderr, "signal %d, section %d\n", sig, g_section);
+  backtrace_symbols_fd(bt, n, 2);
+  _exit(128 + sig);
+}
+
 int main() {
+  std::signal(SIGSEGV, on_fault);
+  std::signal(SIGABRT, on_fault);
   using namespace spk_gold;
   // (no size thresholds: every payload of every handler below goes through
   // struct_pack::gpu, compared with the reference's struct_pack_protocol)
   const uint64_t S3 = 0x5EED0003, S4 = 0x5EED0004, S8 = 0x5EED0008;
 
+  g_section = 1;
+  std::fprintf(stderr, "section 1\n");
   // 1. the protocol statics against the reference protocol and fixtures
   {
     std::vector<RecS> v(300);
@@ -214,6 +268,8 @@ int main() {
     CHECK(struct_pack_gpu_protocol::deserialize_to(args, want));
     CHECK(std::get<0>(args) == v);
   }
+  g_section = 2;
+  std::fprintf(stderr, "section 2\n");
   // 2. the reference's handler executor with the GPU protocol
   {
     std::vector<RecS> v(5000);
@@ -247,6 +303,8 @@ int main() {
     auto gb = run<echo_recs, struct_pack_gpu_protocol>(bad);
     CHECK(rb.first && gb.first && rb.first.val() == gb.first.val());
   }
+  g_section = 21;
+  std::fprintf(stderr, "section 2b\n");
   // 2b. handlers over nested record types (C++ front end: ARRAY / VARIANT /
   // OPTGROUP / FVAR layouts and map / set containers)
   {
@@ -268,6 +326,8 @@ int main() {
     same_as_reference<echo_vnt>(make(std::type_identity<Vnt>{}, 1000, 0x5EED0011, 6), "echo_vnt");
     same_as_reference<echo_monsters>(std::vector<Monster>{}, "echo_monsters(empty)");
   }
+  g_section = 22;
+  std::fprintf(stderr, "section 2c\n");
   // 2c. every call shape at default settings: single records, strings, ints,
   // several arguments (std::tuple messages), no arguments, void replies,
   // containers of non-records, optionals, maps, variants, pairs as replies
@@ -304,6 +364,8 @@ int main() {
     auto go = run<add, struct_pack_gpu_protocol>(other);
     CHECK(ro.first && go.first && ro.first.val() == go.first.val());
   }
+  g_section = 3;
+  std::fprintf(stderr, "section 3\n");
   // 3. the front end's single-record and reference-order entry points next to
   // the reference: identical bytes for one record message, deserialize<conf, T>
   {
@@ -330,6 +392,8 @@ int main() {
     struct_pack::serialize_to_with_offset(roff, 20, p);
     CHECK(off.size() == roff.size() && off.substr(20) == roff.substr(20));
   }
+  g_section = 4;
+  std::fprintf(stderr, "section 4\n");
   // 4. stream readers / writers (the reference's test_stream.cpp shapes): a
   // file of alternating messages written by the reference is read back by
   // struct_pack::gpu::deserialize(ifstream) and the other way round; the two
@@ -424,6 +488,107 @@ int main() {
     CHECK(p3.has_value() && p3.value() == ps[3]);
     std::remove(f_ref.c_str());
     std::remove(f_gpu.c_str());
+  }
+  g_section = 5;
+  std::fprintf(stderr, "section 5\n");
+  // 5. unique_ptr and trivial_view members, next to the reference
+  {
+    auto mk = [&](int i) {
+      UPtrRec u;
+      u.id = i * 3 - 7;
+      if (i % 3) u.s = std::make_unique<std::string>(std::string(i % 17, (char)('a' + i % 26)));
+      if (i % 2) u.p = std::make_unique<Inner>(Inner{i, 0.5f * i});
+      if (i % 5 != 1) u.v = std::make_unique<std::vector<int32_t>>(std::vector<int32_t>(i % 9, i));
+      if (i % 4 == 0) u.r = std::make_unique<RecS>(make_recs(S3, i, 20));
+      return u;
+    };
+    auto same = [](const UPtrRec &a, const UPtrRec &b) {
+      auto eq = [](const auto &x, const auto &y) { return (!x && !y) || (x && y && *x == *y); };
+      return a.id == b.id && eq(a.s, b.s) && eq(a.p, b.p) && eq(a.v, b.v) && eq(a.r, b.r);
+    };
+    bool ok = true;
+    for (int i = 0; i < 12; ++i) {
+      const UPtrRec u = mk(i);
+      const auto want = struct_pack::serialize<std::string>(u);
+      ok = ok && struct_pack::gpu::serialize<std::string>(u) == want;
+      auto back = struct_pack::gpu::deserialize<UPtrRec>(want);
+      ok = ok && back.has_value() && same(back.value(), u);
+    }
+    CHECK(ok);
+    std::vector<UPtrRec> batch;
+    for (int i = 0; i < 3000; ++i) batch.push_back(mk(i));
+    const auto want = struct_pack::serialize<std::string>(batch);
+    CHECK(struct_pack::gpu::serialize<std::string>(batch) == want);
+    std::vector<UPtrRec> back;
+    CHECK(!struct_pack::gpu::deserialize_to(back, want) && back.size() == batch.size());
+    bool all = back.size() == batch.size();
+    for (std::size_t i = 0; all && i < back.size(); ++i) all = same(back[i], batch[i]);
+    CHECK(all);
+    // a truncated message: the reference's errc
+    std::vector<UPtrRec> b2;
+    auto cut = std::string_view(want).substr(0, want.size() - 5);
+    auto e1 = struct_pack::gpu::deserialize_to(b2, cut);
+    std::vector<UPtrRec> b3;
+    auto e2 = struct_pack::deserialize_to(b3, cut);
+    CHECK(e1.val() == e2.val());
+    // a unique_ptr as the whole message
+    auto up = std::make_unique<Inner>(Inner{4, 2.5f});
+    CHECK(struct_pack::gpu::serialize<std::string>(up) == struct_pack::serialize<std::string>(up));
+  }
+  {
+    ViewData d{{1, 2, 3, 4, 5, 6}, 7.5};
+    ViewRec v{"viewed", d, 42};
+    PlainRec pl{"viewed", d, 42};
+    const auto want = struct_pack::serialize<std::string>(v);
+    CHECK(want == struct_pack::serialize<std::string>(pl));
+    CHECK(struct_pack::gpu::serialize<std::string>(v) == want);
+    auto back = struct_pack::gpu::deserialize<ViewRec>(want);
+    CHECK(back.has_value() && back->name == "viewed" && back->k == 42 &&
+          back->data.get().a == d.a && back->data.get().d == d.d);
+    auto plain = struct_pack::gpu::deserialize<PlainRec>(want);  // the same bytes as T
+    CHECK(plain.has_value() && plain->data.a == d.a);
+  }
+  g_section = 6;
+  std::fprintf(stderr, "section 6\n");
+  // 6. user helpers (user_helper.hpp:16-85) next to the reference's
+  {
+    str_writer rw, gw;
+    const std::string name = "a user-defined type";
+    const std::vector<int32_t> vals = {1, -2, 3, 40000};
+    const std::vector<std::string> strs = {"x", "", "yy"};
+    std::vector<RecS> rs;
+    for (int i = 0; i < 500; ++i) rs.push_back(make_recs(S3, i, 30));
+    const std::array<Inner, 3> in = {Inner{1, 1.f}, Inner{2, 2.f}, Inner{3, 3.f}};
+    struct_pack::write(rw, name);
+    struct_pack::write(rw, vals);
+    struct_pack::write<4>(rw, strs);
+    struct_pack::write(rw, in.data(), in.size());
+    struct_pack::write(rw, rs.data(), rs.size());
+    struct_pack::gpu::write(gw, name);
+    struct_pack::gpu::write(gw, vals);
+    struct_pack::gpu::write<4>(gw, strs);
+    struct_pack::gpu::write(gw, in.data(), in.size());
+    struct_pack::gpu::write(gw, rs.data(), rs.size());
+    CHECK(!rw.buf.empty() && gw.buf == rw.buf);
+    CHECK(struct_pack::gpu::get_write_size(name) == struct_pack::get_write_size(name));
+    CHECK(struct_pack::gpu::get_write_size<4>(strs) == struct_pack::get_write_size<4>(strs));
+    CHECK(struct_pack::gpu::get_write_size(rs.data(), rs.size()) ==
+          struct_pack::get_write_size(rs.data(), rs.size()));
+    std::istringstream is(rw.buf);
+    std::string n2;
+    std::vector<int32_t> v2;
+    std::vector<std::string> s2;
+    std::array<Inner, 3> i2{};
+    std::vector<RecS> r2(rs.size());
+    CHECK(!struct_pack::gpu::read(is, n2) && n2 == name);
+    CHECK(!struct_pack::gpu::read(is, v2) && v2 == vals);
+    CHECK(!struct_pack::gpu::read<4>(is, s2) && s2 == strs);
+    CHECK(!struct_pack::gpu::read(is, i2.data(), i2.size()) && i2 == in);
+    CHECK(!struct_pack::gpu::read(is, r2.data(), r2.size()) && r2 == rs);
+    CHECK(static_cast<std::size_t>(is.tellg()) == rw.buf.size());
+    std::istringstream cut(rw.buf.substr(0, 5));
+    std::string n3;
+    CHECK(struct_pack::gpu::read(cut, n3) == struct_pack::errc::no_buffer_space);
   }
   std::printf("{\"checks\": %d, \"failures\": %d}\n", g_checks, g_fail);
   return g_fail ? 1 : 0;

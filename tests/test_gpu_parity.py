@@ -123,6 +123,24 @@ def test_encode_digest_medium(ent):
 ERRS = H.errs()
 
 
+def _deserialize_filled(cd, wire, mode, offsets, n_msgs, fill):
+    """Codec.deserialize with the output buffers pre-filled with `fill`."""
+    if not fill:
+        return cd.deserialize(wire, mode, offsets, n_msgs)
+    wl = wire.numel()
+    cap = (wl // S.min_record_wire_bytes(cd.L.dev) + 1) if mode == C.SPK_MODE_VECTOR else n_msgs
+    out = cd.alloc_batch(cap, S.heap_caps_for_wire(cd.L.dev, wl, cap))
+    out.recs.fill_(fill)
+    for h in out.heaps:
+        h.fill_(fill)
+    ec = (torch.zeros(max(n_msgs, 1), dtype=torch.int32, device="cuda")
+          if mode == C.SPK_MODE_MESSAGES else None)
+    cd.deserialize_to(out, wire, mode, offsets, n_msgs, ec)
+    res = cd.result()
+    n = res.count if mode == C.SPK_MODE_VECTOR else n_msgs
+    return res, SP.RecordBatch(cd.L, out.recs[:n], out.heaps), ec
+
+
 @pytest.mark.parametrize("base", ERRS, ids=[f"{b['case']}_{b['mode']}_{b['n']}_{b['conf']}"
                                             for b in ERRS])
 def test_error_parity(base):
@@ -131,6 +149,8 @@ def test_error_parity(base):
     cd = codec_for(ent["case"], ent["conf"])
     wire0 = bytes.fromhex(base["base"])
     mode = H.mode_of(ent)
+    groups = any(op[0] & 0xFF in (C.SPK_OP_VARIANT, C.SPK_OP_OPTGROUP, C.SPK_OP_OPTION,
+                                  C.SPK_OP_CGROUP, C.SPK_OP_COMPAT) for op in cd.L.dev.ops)
     bad = []
     for t in base["tests"]:
         buf = bytearray(wire0)
@@ -146,12 +166,16 @@ def test_error_parity(base):
                     buf[p] = v
                 i += 3
         buf = bytes(buf)
+        # layouts whose groups can drop an error decode into outputs filled
+        # with 0xAB: the members past a dropped error must be written as the
+        # reference's value-initialised ones, whatever the buffer held
+        fill = 0xAB if groups else 0
         if mode == C.SPK_MODE_VECTOR:
-            res, out, _ = cd.deserialize(wire_dev(buf), mode)
+            res, out, _ = _deserialize_filled(cd, wire_dev(buf), mode, None, 0, fill)
             e, consumed = res.errc, res.consumed
         else:
             offs = torch.tensor([0, len(buf)], dtype=torch.int64, device="cuda")
-            res, out, ec = cd.deserialize(wire_dev(buf), mode, offs, 1)
+            res, out, ec = _deserialize_filled(cd, wire_dev(buf), mode, offs, 1, fill)
             e, consumed = int(ec[0].item()), res.consumed
         if e != t["errc"] or (e == 0 and consumed != t["consume"]):
             bad.append((t["mut"], e, t["errc"], consumed, t["consume"]))
@@ -436,7 +460,9 @@ def test_screen_defeating_payload_bounded_time():
                                               ("outer", "outer", 16), ("rpcrect", "rpcrect", 0),
                                               ("person", "person", 48),
                                               ("ints", "ints", 1000),
-                                              ("monster", "monster", 20)])
+                                              ("monster", "monster", 20),
+                                              ("recs", "recs", 48 | 1 << 31),
+                                              ("recs", "recs", 3000 | 100 << 16 | 1 << 31)])
 def test_device_synth_matches_host_generator(kind, case, param):
     cd = codec_for(case)
     n = 3001

@@ -506,7 +506,7 @@ static int shard_check(const spk_layout *L, const void *d_wire, uint64_t wire_le
   if (is_trivial(L)) return SPK_E_LAYOUT;
   // nested layouts: on the tile decoder (no compatible members, at most
   // SPK_FLAT_SPANS heaps, wires below 4 GiB)
-  if (layout_nested(L) && (!var_nested_tile_ok(L) || wire_len >= (1ull << 32)))
+  if (layout_nested(L) && (!var_nested_tile_ok(L) || wire_len >= (1ull << 32) - 4096))
     return SPK_E_LAYOUT;
   if (!d_ws || (wire_len && !d_wire)) return SPK_E_ARG;
   if (ws_bytes < spk_workspace_bytes(L, SPK_MODE_VECTOR, rec_cap, wire_len)) return SPK_E_WORKSPACE;

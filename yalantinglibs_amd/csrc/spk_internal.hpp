@@ -152,6 +152,40 @@ __host__ __device__ __forceinline__ bool span_nb(uint64_t c, uint64_t size, uint
   return !__builtin_mul_overflow(c, size, nb);
 }
 
+// A decode error inside a variant / optional group is dropped by the
+// reference (unpacker.hpp:476-490,1251-1277) with the value value-initialised
+// before its decode: the members from the failing one to the end of each
+// level being unwound read as zero / empty / absent. Writes those fields of
+// ops [i, iend) of record r (any output content before the decode): COPY /
+// varint bytes zero, a container / option count 0 at the heap's next slot
+// used(k), an optional / compatible group absent, a variant alternative 0 with
+// its fields zeroed (the walk goes through every alternative, no stack).
+template <typename Lay, typename UsedFn>
+__device__ __forceinline__ void zero_rest(const Lay &N, uint8_t *r, uint32_t i, uint32_t iend,
+                                          UsedFn used) {
+  while (i < iend) {
+    const spk_op op = N.ops[i];
+    const uint32_t k = op.kind & 0xFFu;
+    if (k == SPK_OP_COPY || k == SPK_OP_VARINT || k == SPK_OP_FVAR) {
+      for (uint32_t b = 0; b < op.size; ++b) r[op.rec_off + b] = 0;
+      ++i;
+    } else if (k == SPK_OP_SPAN || k == SPK_OP_OPTION || k == SPK_OP_COMPAT ||
+               k == SPK_OP_ARRAY) {
+      *reinterpret_cast<uint32_t *>(r + op.rec_off) = 0;
+      *reinterpret_cast<uint64_t *>(r + op.aux) = used(N.heap[i]);
+      i = k == SPK_OP_ARRAY ? N.end[i] + 1u : i + 1;
+    } else if (k == SPK_OP_OPTGROUP || k == SPK_OP_CGROUP) {
+      *reinterpret_cast<uint32_t *>(r + op.rec_off) = 0;
+      i = N.end[i] + 1u;
+    } else if (k == SPK_OP_VARIANT) {
+      *reinterpret_cast<uint32_t *>(r + op.rec_off) = 0;
+      ++i;  // into the alternatives (all of them zeroed; 0 is the one read)
+    } else {
+      ++i;  // END
+    }
+  }
+}
+
 __host__ __device__ __forceinline__ uint64_t ld_le(const uint8_t *p, uint32_t w) {
   uint64_t v = 0;
   for (uint32_t i = 0; i < w; ++i) v |= (uint64_t)p[i] << (8 * i);

@@ -571,8 +571,13 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
       // decode's errc is dropped (variant_construct_helper::run,
       // unpacker.hpp:476-490; optional / expected, :1251-1277); an ARRAY
       // keeps its failing element (emplace_back, unpacker.hpp:1208-1226)
+      // The members from the failing one on, at every level unwound, are
+      // value-initialised (zero_rest): the reference default-constructs the
+      // value before its decode, and the output may hold anything.
       bool dropped = false;
-      while (d) {
+      for (;;) {
+        if (r) zero_rest(N, r, i, iend, [&](uint32_t k) { return used[k]; });
+        if (!d) break;
         NFrame &f = st[d - 1];
         const spk_op &fo = N.ops[f.aop];
         if (fo.kind == SPK_OP_VARIANT || fo.kind == SPK_OP_OPTGROUP) {
@@ -586,6 +591,9 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
         used[N.heap[f.aop]] -= f.cnt - (f.j + 1);
         if (f.el) *reinterpret_cast<uint32_t *>(const_cast<uint8_t *>(f.prec) + fo.rec_off) =
             (uint32_t)(f.j + 1);
+        i = f.ret;  // the rest of the enclosing level
+        iend = f.pend;
+        r = const_cast<uint8_t *>(f.prec);
         --d;
       }
       if (!dropped) return ec;
@@ -2055,7 +2063,7 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
                                 hipStream_t s, uint32_t body_w, uint64_t body_n,
                                 const uint64_t *d_msg_ends) {
   // (the tile decoder counts heap slots in 32 bits: wires below 4 GiB)
-  if (mode == SPK_MODE_VECTOR && var_nested_tile_ok(L) && wire_len < (1ull << 32) &&
+  if (mode == SPK_MODE_VECTOR && var_nested_tile_ok(L) && wire_len < (1ull << 32) - 4096 &&
       !nest_chunked())
     return launch_var_nested_decode(L, d_wire, wire_len, d_recs, rec_cap, d_heaps, heap_caps,
                                     d_res, d_ws, s, body_w, body_n);

@@ -52,11 +52,20 @@ __global__ void synth_rec64(uint64_t seed, uint64_t first, uint64_t n, Rec64 *ou
   }
 }
 
+// RECS lengths (types.hpp chars_len): a plain param < 65536 is U[0, param];
+// otherwise maxlen in bits 0-15, minlen in bits 16-30, bit 31 = raw bytes
+__device__ __forceinline__ uint32_t recs_len(uint64_t seed, uint64_t i, uint32_t param) {
+  if (param < 0x10000u) return (uint32_t)(rnd(seed, i, 1) % (uint64_t)(param + 1));
+  const uint32_t mx = param & 0xFFFFu, mn = (param >> 16) & 0x7FFFu;
+  return mn + (uint32_t)(rnd(seed, i, 1) % (uint64_t)(mx - mn + 1));
+}
+
 __global__ void synth_counts(int kind, uint64_t seed, uint64_t first, uint64_t n,
                              uint32_t param, uint64_t *cnt) {
   const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gs)
-    cnt[t] = rnd(seed, first + t, 1) % (uint64_t)(param + 1);
+    cnt[t] = kind == SPK_SYNTH_RECS ? recs_len(seed, first + t, param)
+                                    : rnd(seed, first + t, 1) % (uint64_t)(param + 1);
 }
 
 __global__ void synth_recs(uint64_t seed, uint64_t first, uint64_t n, uint32_t param,
@@ -66,14 +75,16 @@ __global__ void synth_recs(uint64_t seed, uint64_t first, uint64_t n, uint32_t p
     const uint64_t i = first + t;
     RecSDev r;
     r.id = (int32_t)(uint32_t)rnd(seed, i, 0);
-    r.n = (uint32_t)(rnd(seed, i, 1) % (uint64_t)(param + 1));
+    r.n = recs_len(seed, i, param);
     r.off = hoff[t];
     r.v = rd(rnd(seed, i, 60));
     out[t] = r;
     uint8_t *dst = heap + r.off;
+    const bool raw = (param >> 31) != 0;
     for (uint32_t j = 0; j < r.n; ++j) {
       const uint64_t w = rnd(seed, i, 2 + (j >> 3) % 56);
-      dst[j] = (uint8_t)('a' + ((w >> ((j & 7) * 8)) & 0xFF) % 26);
+      const uint32_t b = (uint32_t)((w >> ((j & 7) * 8)) & 0xFF);
+      dst[j] = (uint8_t)(raw ? b : 'a' + b % 26);
     }
   }
 }

@@ -1521,6 +1521,18 @@ struct WinReader {
     auto bf = [this](uint64_t q) { return byte(q); };
     return vi_read(bf, x, len, v);
   }
+  // count_at with a 32-bit wire offset (nested tile walks: wires below
+  // kNT32Wire bytes, so x + 12 cannot wrap)
+  __device__ __forceinline__ uint64_t count_at32(uint32_t x, uint64_t wmask, bool opt) const {
+    if (x + 12u <= (uint32_t)wend) {
+      const uint32_t o = x - (uint32_t)cs, sh = o & 3, i = o >> 2;
+      const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2];
+      const uint64_t b = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
+                         ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
+      return opt ? (uint64_t)((b & 0xFFu) != 0) : (b & wmask);
+    }
+    return opt ? (uint64_t)(byte(x) != 0) : (*this)(x);
+  }
   // the count field at x: its w low bytes (wmask) or, for an OPTION's
   // has_value byte, whether it is non-zero; inside the window one path (8
   // bytes from three dwords), past it the wire
@@ -1724,7 +1736,10 @@ __device__ __forceinline__ uint32_t nt_alt_end(const NTLayout &N, uint32_t j) {
   }
 }
 
-constexpr int32_t kNTLimit = 0x7FFF0001;  // a bounded walk needed bytes past its limit
+constexpr int32_t kNTLimit = 0x7FFF0001;
+// the nested tile decoder's wire limit: positions fit 32 bits with room for
+// a 12-byte count read past any of them
+constexpr uint64_t kNT32Wire = (1ull << 32) - 4096;  // a bounded walk needed bytes past its limit
 // a bounded (speculative) walk also gives up on a container of more elements:
 // from a false start, element counts read from payload bytes would have the
 // walk iterate up to its byte limit one element at a time
@@ -1823,8 +1838,12 @@ __device__ int32_t nt_read(const NTLayout &N, const Rd &rd, uint64_t &pos, uint6
       // unwind to the innermost variant / optional / expected group, whose
       // errc is dropped (unpacker.hpp:476-490, 1251-1277); an ARRAY keeps its
       // failing element and gives back the slots past it (:1208-1226)
+      // (the members from the failing one on, at every level unwound, are
+      // value-initialised: zero_rest, spk_internal.hpp)
       bool dropped = false;
-      while (d) {
+      for (;;) {
+        if constexpr (EMIT) zero_rest(N, r, i, iend, [&](uint32_t k) { return (uint64_t)U[64 * k]; });
+        if (!d) break;
         const uint32_t fo = c_op;
         const spk_op &ao = N.ops[fo & 0xFFu];
         if (ao.kind == SPK_OP_VARIANT || ao.kind == SPK_OP_OPTGROUP) {
@@ -1838,6 +1857,9 @@ __device__ int32_t nt_read(const NTLayout &N, const Rd &rd, uint64_t &pos, uint6
         const uint32_t hk = N.heap[fo & 0xFFu];
         atomicSub(U + 64 * hk, c_cnt - (c_j + 1));
         if constexpr (EMIT) *reinterpret_cast<uint32_t *>(c_pr + ao.rec_off) = c_j + 1;
+        i = fo >> 24;  // the rest of the enclosing level
+        iend = (fo >> 8) & 0xFFu;
+        if constexpr (EMIT) r = c_pr;
         pop(--d);
       }
       if (!dropped) return ec;
@@ -2029,7 +2051,7 @@ __device__ int32_t nt_read(const NTLayout &N, const Rd &rd, uint64_t &pos, uint6
 // counters. Exact for the walk's outcome: these layouts have no group that
 // could drop an error.
 template <typename Rd>
-__device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint64_t lim,
+__device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint64_t lim64,
                             bool bounded, uint32_t maxel) {
   // a check that fails on a bounded walk's limit: unknown (the full wire may
   // have held the record)
@@ -2038,7 +2060,10 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
   uint32_t *const F = nt_frames();
   const uint32_t w = rd.w;
   const uint64_t wmask = w >= 8 ? ~0ull : (1ull << (8 * w)) - 1;
-  uint64_t p = pos;
+  // positions as 32-bit wire offsets (the nested tile path takes wires below
+  // kNT32Wire bytes): half the VALU work of 64-bit position arithmetic
+  const uint32_t lim = (uint32_t)lim64;
+  uint32_t p = (uint32_t)pos;
   uint32_t pc = 0, d = 0, body = 0, rem = 0;  // top loop frame: body start, elements left
   while (pc < N.wp_n) {
     const uint2 ins = N.wp[pc];
@@ -2060,7 +2085,7 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
     const bool opt = op == WP_OPT;
     const uint32_t cw = opt ? 1u : w;
     if (lim - p < cw) return bad;
-    const uint64_t c = rd.count_at(p, wmask, opt);
+    const uint64_t c = rd.count_at32(p, wmask, opt);
     p += cw;
     atomicAdd(U + 64 * h, (uint32_t)c);
     if (op == WP_ARR) {
@@ -2079,13 +2104,13 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
       continue;
     }
     // SPAN: the payload must be there; OPTION: an unreadable value leaves the reader
-    // (c < 2^32 and arg < 2^24: the product cannot overflow)
+    // (c <= lim - p < 2^32 and arg < 2^24: the product cannot overflow)
     if (!opt && (c > lim - p || c * arg > lim - p)) return bad;
-    if (!opt || (c && lim - p >= arg)) p += c * arg;
+    if (!opt || (c && lim - p >= arg)) p += (uint32_t)(c * arg);
     ++pc;
   }
   if (lim - p < N.wp_tail) return bad;
-  return p + N.wp_tail - pos;
+  return (uint64_t)(p + N.wp_tail - (uint32_t)pos);
 }
 
 // wlen_rd for NS = -2: the record's wire length (0: the path fails here) and
@@ -2817,6 +2842,16 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
         }
       }
     }
+  }
+  if (X == kNoPos && !exact0 && !(dbg & 8192)) {
+    // chunk 0 holds no plausible start (it lies inside a long record: a
+    // string of a few hundred bytes spans several chunks): the tile's first
+    // record start is the first start some later chunk speculated. Without
+    // this the tile published no entry at all, pick could not match it and
+    // runs of such tiles fell through the repair passes to the sequential
+    // fixer (binary strings of 100-3000 B: 35.8 ms for 62 MB)
+    const uint64_t mv = __ballot(used != kNoPos);
+    if (mv) X = __shfl(used, (int)__builtin_ctzll(mv));
   }
   if (X != kNoPos && !(dbg & 32))
     resolve_tile_sp<NS>(P, rd, len, w, cs, ce, lane, X, sp, used, ex, cnt, sums, term_at, stat,

@@ -192,15 +192,28 @@ CASE_TYPES = {"rec64": Rec64, "recs": RecS, "outer": Outer, "pad": Pad,
 VECTOR_CONFIG = {"rect": S.DISABLE_ALL_META_INFO, "rect2": S.DISABLE_ALL_META_INFO}
 
 
-def _chars(seed, idx, lens):
-    """make_chars: char j of record i from word 2 + (j>>3)%56."""
+def _chars(seed, idx, lens, raw=False):
+    """make_chars: char j of record i from word 2 + (j>>3)%56 ('a'..'z', or
+    the byte itself when raw)."""
     total = int(lens.sum())
     rec = np.repeat(idx, lens)
     starts = np.concatenate([[0], np.cumsum(lens)[:-1]]) if len(lens) else np.zeros(0, np.int64)
     j = np.arange(total, dtype=np.uint64) - np.repeat(starts, lens).astype(np.uint64)
     w = rnd(seed, rec, np.uint64(2) + (j >> np.uint64(3)) % np.uint64(56))
     b = (w >> ((j & np.uint64(7)) * np.uint64(8))) & np.uint64(0xFF)
+    if raw:
+        return b.astype(np.uint8)
     return (np.uint64(ord("a")) + b % np.uint64(26)).astype(np.uint8)
+
+
+def recs_lens(seed, idx, param):
+    """Lengths of make_chars (types.hpp chars_len): a plain param < 65536 is
+    U[0, param]; otherwise maxlen in bits 0-15, minlen in bits 16-30, bit 31
+    = raw bytes."""
+    if param < 0x10000:
+        return (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+    mx, mn = param & 0xFFFF, (param >> 16) & 0x7FFF
+    return (np.uint64(mn) + rnd(seed, idx, 1) % np.uint64(mx - mn + 1)).astype(np.int64)
 
 
 def _seg(cnt):
@@ -269,12 +282,12 @@ def make_batch(case: str, n: int, seed: int, param: int = 48):
             [rd(rnd(seed, idx, 8 + k)) for k in range(4)], 1)
         recs = raw.view(L.dtype).reshape(n)
     elif case == "recs":
-        lens = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
+        lens = recs_lens(seed, idx, param)
         recs["id"] = i32(rnd(seed, idx, 0))
         recs["name.n"] = lens
         recs["name.off"] = np.concatenate([[0], np.cumsum(lens)[:-1]]) if n else []
         recs["v"] = rd(rnd(seed, idx, 60))
-        heaps.append(_chars(seed, idx, lens))
+        heaps.append(_chars(seed, idx, lens, raw=param >= 0x80000000))
     elif case == "outer":
         cnt = (rnd(seed, idx, 1) % np.uint64(param + 1)).astype(np.int64)
         recs["key"] = rnd(seed, idx, 0).view(np.int64)
