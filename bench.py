@@ -51,14 +51,17 @@ CONFIGS = {
     "cv": ("var", 10_000_000, 16, "A",
            "varint records: 10M Var{var_int32_t, std::string len U[0,16], var_uint64_t, double, "
            "var_int64_t, var_uint32_t} per GPU (LEB128 lengths 1-10 B), one vector message"),
+    "cvm": ("valreq", 1_000_000, 16, "B",
+            "coro_rpc benchmark's ValidateRequest (src/coro_rpc/benchmark/api/ValidateRequest.h): "
+            "1M independent messages per GPU (nested: optional, vector<string>)"),
     "cm": ("monster", 10_000_000, 20, "A",
            "the reference benchmark's Monster (src/struct_pack/benchmark/data_def.hpp: Vec3, "
            "2 x int16, 2 strings, enum, vector<Weapon{string,int16}>, Weapon, vector<Vec3>): "
            "10M per GPU, one vector message"),
 }
-EXTRA = ["c2b", "c3", "c3r", "c3l", "c4", "c5", "cv", "cm"]  # timed beside the C2 headline at N=1
+EXTRA = ["c2b", "c3", "c3r", "c3l", "c4", "c5", "cv", "cm", "cvm"]  # timed beside the C2 headline at N=1
 SEEDS = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004, "var": 0x5EED000C,
-         "monster": 0x5EED001E}
+         "monster": 0x5EED001E, "valreq": 0x5EED001B}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PROFILE_ROUND = "r03"
 
@@ -148,7 +151,8 @@ def cpu_baseline(case, n, param, algo_bytes, per="record"):
     if not os.path.exists(exe):
         return None
     threads, aff = cpu_share()
-    seed = {"c5": 0, "rec64msg": SEEDS["rec64"]}.get(case, SEEDS.get(case, 0))
+    seed = {"c5": 0, "rec64msg": SEEDS["rec64"], "valreqmsg": SEEDS["valreq"]}.get(
+        case, SEEDS.get(case, 0))
 
     def run(nn, t, reps):
         r = subprocess.run([exe, case, str(nn), str(seed), str(param), str(t), str(reps)],
@@ -281,6 +285,9 @@ class VecWorkload:
         ob = 8 * (self.n + 1)
         if self.cd.L.dev.trivial:
             return {"fixed_msg_encode_lds": rb + wb + ob, "fixed_msg_decode_lds": wb + ob + rb}
+        if any(op[0] & 0xFF in (5, 7, 8, 9, 10, 11) for op in self.cd.L.dev.ops):
+            # nested layouts: one lane per message in both directions
+            return {"nest_write": rb + wb + ob, "nest_emit": wb + ob + rb}
         return {"var_encode_write": rb + wb + ob, "var_msg_write": wb + ob + rb}
 
     def config(self):
@@ -292,7 +299,7 @@ class VecWorkload:
 
     def cpu_case(self):
         if self.mode == self.SP.MODE_MESSAGES:
-            return "rec64msg" if self.case == "rec64" else None
+            return {"rec64": "rec64msg", "valreq": "valreqmsg"}.get(self.case)
         return self.case
 
 

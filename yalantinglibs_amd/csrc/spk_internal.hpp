@@ -157,12 +157,12 @@ __host__ __device__ __forceinline__ bool span_nb(uint64_t c, uint64_t size, uint
 // before its decode: the members from the failing one to the end of each
 // level being unwound read as zero / empty / absent. Writes those fields of
 // ops [i, iend) of record r (any output content before the decode): COPY /
-// varint bytes zero, a container / option count 0 at the heap's next slot
-// used(k), an optional / compatible group absent, a variant alternative 0 with
-// its fields zeroed (the walk goes through every alternative, no stack).
-template <typename Lay, typename UsedFn>
-__device__ __forceinline__ void zero_rest(const Lay &N, uint8_t *r, uint32_t i, uint32_t iend,
-                                          UsedFn used) {
+// varint bytes zero, a container / option count 0 at element
+// offset 0 (the oracle's untouched zero), an optional / compatible group
+// absent, a variant alternative 0 with its fields zeroed (the walk goes
+// through every alternative, no stack).
+template <typename Lay>
+__device__ __forceinline__ void zero_rest(const Lay &N, uint8_t *r, uint32_t i, uint32_t iend) {
   while (i < iend) {
     const spk_op op = N.ops[i];
     const uint32_t k = op.kind & 0xFFu;
@@ -172,7 +172,7 @@ __device__ __forceinline__ void zero_rest(const Lay &N, uint8_t *r, uint32_t i, 
     } else if (k == SPK_OP_SPAN || k == SPK_OP_OPTION || k == SPK_OP_COMPAT ||
                k == SPK_OP_ARRAY) {
       *reinterpret_cast<uint32_t *>(r + op.rec_off) = 0;
-      *reinterpret_cast<uint64_t *>(r + op.aux) = used(N.heap[i]);
+      *reinterpret_cast<uint64_t *>(r + op.aux) = 0;
       i = k == SPK_OP_ARRAY ? N.end[i] + 1u : i + 1;
     } else if (k == SPK_OP_OPTGROUP || k == SPK_OP_CGROUP) {
       *reinterpret_cast<uint32_t *>(r + op.rec_off) = 0;

@@ -78,6 +78,32 @@ __device__ __forceinline__ void n_copy(uint8_t *d, const uint8_t *s, uint64_t n)
   for (; i < n; ++i) d[i] = s[i];
 }
 
+// The interpreter's byte reader: the wire in global memory, or a wave's
+// staged LDS copy of [lo, hi) with the bytes outside it from global memory
+// (MESSAGES decode: the wave's 64 consecutive messages, loaded with aligned
+// 16-B loads instead of each lane's scattered byte loads). A raw pointer is
+// the global-only reader.
+typedef __attribute__((address_space(3))) uint8_t nlds_u8;
+struct NRd {
+  const uint8_t *w;
+  const nlds_u8 *lds;
+  uint64_t lo, hi;
+  __device__ __forceinline__ uint8_t operator[](uint64_t p) const {
+    return p - lo < hi - lo ? lds[(uint32_t)(p - lo)] : w[p];
+  }
+};
+__device__ __forceinline__ void n_copy_rd(uint8_t *d, const uint8_t *w, uint64_t p, uint64_t n) {
+  n_copy(d, w + p, n);
+}
+__device__ __forceinline__ void n_copy_rd(uint8_t *d, const NRd &rd, uint64_t p, uint64_t n) {
+  if (p - rd.lo < rd.hi - rd.lo && rd.hi - p >= n) {
+    const uint32_t o = (uint32_t)(p - rd.lo);
+    for (uint64_t i = 0; i < n; ++i) d[i] = rd.lds[o + i];
+  } else {
+    n_copy(d, rd.w + p, n);
+  }
+}
+
 // the layout in LDS: the interpreter reads an op per step, and a kernel
 // argument indexed per lane would be fetched from memory every time
 __device__ __forceinline__ void n_stage(NLayout &dst, const NLayout &src) {
@@ -186,7 +212,8 @@ __device__ __forceinline__ uint64_t n_fv_len(const NLayout &N, const uint8_t *bs
   return b;
 }
 // deserialize_fast_varint: errc; values into rec (zero when the bit is clear)
-__device__ int32_t n_fv_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, uint64_t end,
+template <typename Rd>
+__device__ int32_t n_fv_read(const NLayout &N, const Rd &wire, uint64_t &pos, uint64_t end,
                              uint8_t *rec) {
   if (end - pos < N.fv_bits) return SPK_ERRC_NO_BUFFER_SPACE;
   uint8_t bs[(SPK_MAX_VARINTS + 2 + 7) / 8];
@@ -555,7 +582,8 @@ constexpr int32_t kNLimit = 0x7FFF0001;
 // a value that does not fit leaves the reader in place (a trivially
 // serializable one zero-filled) (unpacker.hpp:1251-1277). `top`: the whole
 // top-level record, its fast-varint group first.
-__device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, uint64_t end,
+template <typename Rd>
+__device__ int32_t n_read(const NLayout &N, const Rd &wire, uint64_t &pos, uint64_t end,
                           uint32_t w, uint8_t *rec, uint8_t *const *heaps, uint64_t *used,
                           const uint64_t *heap_cap, uint32_t *ovf, uint32_t i0, uint32_t i1,
                           bool top, bool bounded = false) {
@@ -576,7 +604,7 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
       // value before its decode, and the output may hold anything.
       bool dropped = false;
       for (;;) {
-        if (r) zero_rest(N, r, i, iend, [&](uint32_t k) { return used[k]; });
+        if (r) zero_rest(N, r, i, iend);
         if (!d) break;
         NFrame &f = st[d - 1];
         const spk_op &fo = N.ops[f.aop];
@@ -625,7 +653,7 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
         ec = SPK_ERRC_NO_BUFFER_SPACE;
         continue;
       }
-      if (r) n_copy(r + op.rec_off, wire + pos, op.size);
+      if (r) n_copy_rd(r + op.rec_off, wire, pos, op.size);
       pos += op.size;
       ++i;
       continue;
@@ -760,7 +788,7 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
         if (!fits && bounded) return kNLimit;
         if (put) {
           if (fits)
-            n_copy(heaps[hk] + off * op.size, wire + pos, op.size);
+            n_copy_rd(heaps[hk] + off * op.size, wire, pos, op.size);
           else
             for (uint32_t b = 0; b < op.size; ++b) heaps[hk][off * op.size + b] = 0;
         }
@@ -778,7 +806,7 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
         continue;
       }
       const uint64_t nb = cnt * op.size;
-      if (put) n_copy(heaps[hk] + off * op.size, wire + pos, nb);
+      if (put) n_copy_rd(heaps[hk] + off * op.size, wire, pos, nb);
       pos += nb;
     }
     if (put) {
@@ -797,7 +825,8 @@ __device__ int32_t n_read(const NLayout &N, const uint8_t *wire, uint64_t &pos, 
 // no_buffer_space (*ec, returns 1); the value's errc is dropped (a trivially
 // serializable one that does not fit reads as present and zero; a group stops
 // where its decode stopped). The main pass left every member absent.
-__device__ int n_read_compat(const NLayout &N, const uint8_t *wire, uint64_t &pos, uint64_t end,
+template <typename Rd>
+__device__ int n_read_compat(const NLayout &N, const Rd &wire, uint64_t &pos, uint64_t end,
                              uint64_t data_end, uint32_t rk, uint32_t w, uint8_t *rec,
                              uint8_t *const *heaps, uint64_t *used, const uint64_t *heap_cap,
                              uint32_t *ovf, int32_t *ec) {
@@ -825,7 +854,7 @@ __device__ int n_read_compat(const NLayout &N, const uint8_t *wire, uint64_t &po
         *reinterpret_cast<uint32_t *>(rec + op.rec_off) = 1;
         *reinterpret_cast<uint64_t *>(rec + op.aux) = off;
         if (fits)
-          n_copy(heaps[hk] + off * op.size, wire + pos, op.size);
+          n_copy_rd(heaps[hk] + off * op.size, wire, pos, op.size);
         else
           for (uint32_t b = 0; b < op.size; ++b) heaps[hk][off * op.size + b] = 0;
       }
@@ -1079,6 +1108,7 @@ struct NCtl {
   unsigned long long htot[SPK_MAX_SPANS];     // heap elements of records 0..n-1
   int32_t werr;                               // the errc of the record the path fails at
   uint32_t pad_;
+  unsigned long long m_ok, m_cap;             // MESSAGES decode: messages ok / over capacity
 };
 static_assert(kWsCtl + sizeof(NCtl) <= kWsScratch, "NCtl overlaps the scratch area");
 
@@ -1226,6 +1256,8 @@ __global__ void nest_ctl_init(uint8_t *ws, const uint32_t *cond) {
   ctl->ovf = 0;
   ctl->w = 1;
   ctl->errc = 0;
+  ctl->m_ok = 0;
+  ctl->m_cap = 0;
 }
 
 // VECTOR: sizes[i] = bytes + cnts * w (in place over a[0]), w from maxc;
@@ -1913,12 +1945,51 @@ __global__ void nest_vec_serial(NDec a, const uint8_t *__restrict__ wire, uint8_
 }
 
 // MESSAGES count pass: errc and heap use of every message (no writes)
-__global__ __launch_bounds__(256) void nest_msg_count(NDec a, const uint8_t *__restrict__ wire,
+// MESSAGES decode: each wave stages its 64 consecutive messages (the first
+// kMsgWin bytes from a 16-B aligned base) in LDS with 16-B loads; the lanes'
+// interpreter walks read them there (NRd). Frames routed out of order
+// (a.ends) and irregular offsets read the wire in place.
+constexpr uint32_t kMsgWin = 4096;
+__device__ __forceinline__ NRd n_stage_msgs(v4u_t *win, const NDec &a, const uint8_t *wire,
+                                            const uint64_t *offs, uint64_t i0, uint32_t lane) {
+  NRd rd{wire, (const nlds_u8 *)win, 0, 0};
+  const uint64_t n = a.n_msgs;
+  if (a.ends || i0 >= n) return rd;
+  const uint64_t b = offs[i0], e = offs[i0 + 64 < n ? i0 + 64 : n];
+  if (e <= b || e > a.wire_len) return rd;
+  const uint64_t base = b & ~15ull;
+  const uint64_t span = e - base < kMsgWin ? e - base : kMsgWin;
+  const uint64_t whole = (a.wire_len - base) / 16;  // 16-B words inside the wire
+  const uint64_t nv = (span + 15) / 16 < whole ? (span + 15) / 16 : whole;
+  constexpr uint32_t kPer = kMsgWin / 16 / 64;
+  v4u_t val[kPer];
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t v = lane + 64 * k;
+    if (v < nv) val[k] = *reinterpret_cast<const v4u_una *>(wire + base + 16ull * v);
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t v = lane + 64 * k;
+    if (v < nv) win[v] = val[k];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  rd.lo = base;
+  rd.hi = base + 16 * nv;
+  return rd;
+}
+
+__global__ __launch_bounds__(256) void nest_msg_count(NDec a, const uint8_t *__restrict__ wire_g,
                                                       const uint64_t *__restrict__ offs,
                                                       uint64_t *__restrict__ U,
                                                       int32_t *__restrict__ ec,
                                                       uint64_t *__restrict__ cons) {
+  __shared__ v4u_t win_s[4][kMsgWin / 16];
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const NRd wire = n_stage_msgs(win_s[threadIdx.x >> 6], a, wire_g, offs, i & ~63ull,
+                                threadIdx.x & 63);
   if (i >= a.n_msgs) return;
   const NLayout &N = a.N;
   uint64_t used[SPK_MAX_SPANS] = {};
@@ -1931,7 +2002,7 @@ __global__ __launch_bounds__(256) void nest_msg_count(NDec a, const uint8_t *__r
     const uint64_t m0 = b + a.prefix;
     uint64_t p0, dl;
     uint32_t w;
-    errc = parse_hdr(a.fmt, wire + m0, e - m0, &p0, &w, &dl);
+    errc = parse_hdr(a.fmt, wire_g + m0, e - m0, &p0, &w, &dl);
     if (!errc) {
       uint64_t pos = m0 + p0;
       uint32_t ovf = 0;
@@ -1958,10 +2029,31 @@ __global__ __launch_bounds__(256) void nest_emit(NDec a, const uint8_t *__restri
                                                  const uint64_t *__restrict__ B, uint64_t nrows,
                                                  const int32_t *__restrict__ ec, uint8_t *ws,
                                                  const uint64_t *__restrict__ cpos,
-                                                 uint8_t *__restrict__ recs, int mode) {
+                                                 uint8_t *__restrict__ recs, int mode,
+                                                 int32_t *__restrict__ errc_out) {
+  __shared__ v4u_t win_s[4][kMsgWin / 16];
   NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const NLayout &N = a.N;
+  const NRd rdm = mode == SPK_MODE_MESSAGES
+                      ? n_stage_msgs(win_s[threadIdx.x >> 6], a, wire, offs, i & ~63ull,
+                                     threadIdx.x & 63)
+                      : NRd{wire, nullptr, 0, 0};
+  if (mode == SPK_MODE_MESSAGES) {
+    // the per-message verdicts: copied out and tallied here, one wave reduce
+    // and one atomic per wave (a one-block loop over 1M messages in
+    // nest_finish took 1.6 ms)
+    const bool in = i < a.n_msgs;
+    const int32_t e = in ? ec[i] : 0;
+    if (in && errc_out) errc_out[i] = e;
+    uint64_t okc = in && e == 0;
+    for (int o = 32; o > 0; o >>= 1) okc += __shfl_xor(okc, o);
+    const uint64_t capm = __ballot(in && e == SPK_ERRC_CAPACITY);
+    if ((threadIdx.x & 63) == 0) {
+      if (okc) atomicAdd(&ctl->m_ok, (unsigned long long)okc);
+      if (capm) atomicOr(&ctl->m_cap, 1ull);
+    }
+  }
   uint64_t pos, end, data_end;
   uint32_t w;
   if (mode == SPK_MODE_VECTOR) {
@@ -1983,14 +2075,14 @@ __global__ __launch_bounds__(256) void nest_emit(NDec a, const uint8_t *__restri
   for (uint32_t k = 0; k < N.n_heaps; ++k) used[k] = B[(uint64_t)k * nrows + i];
   uint32_t ovf = 0;
   uint8_t *rec = recs + i * N.stride;
-  n_read(N, wire, pos, end, w, rec, a.heaps, used, a.heap_cap, &ovf, 0, N.n_ops, true);
+  n_read(N, rdm, pos, end, w, rec, a.heaps, used, a.heap_cap, &ovf, 0, N.n_ops, true);
   int32_t cec = 0;
   for (uint32_t rk = 0; rk < N.n_ranks; ++rk) {
     if (mode == SPK_MODE_VECTOR) {  // this record's group of version rk (walker)
       pos = cpos[(uint64_t)rk * a.rec_cap + i];
       if (pos == ~0ull) break;
     }
-    if (n_read_compat(N, wire, pos, end, data_end, rk, w, rec, a.heaps, used, a.heap_cap, &ovf,
+    if (n_read_compat(N, rdm, pos, end, data_end, rk, w, rec, a.heaps, used, a.heap_cap, &ovf,
                       &cec))
       break;
   }
@@ -2002,24 +2094,11 @@ __global__ void nest_finish(NDec a, const uint64_t *__restrict__ part, uint64_t 
                             const int32_t *__restrict__ ec, uint8_t *ws, int mode,
                             spk_dresult_t *res, int32_t *__restrict__ errc_out) {
   const NCtl *ctl = reinterpret_cast<const NCtl *>(ws + kWsCtl);
-  __shared__ unsigned long long s_ok, s_cap;
-  if (threadIdx.x == 0) {
-    s_ok = 0;
-    s_cap = 0;
-  }
-  __syncthreads();
-  if (mode == SPK_MODE_MESSAGES) {
-    unsigned long long ok = 0, cap = 0;
-    for (uint64_t i = threadIdx.x; i < a.n_msgs; i += blockDim.x) {
-      if (errc_out) errc_out[i] = ec[i];
-      cap |= ec[i] == SPK_ERRC_CAPACITY;
-      ok += ec[i] == 0;
-    }
-    atomicAdd(&s_ok, ok);
-    if (cap) atomicOr(&s_cap, 1ull);
-  }
-  __syncthreads();
+  // (MESSAGES: nest_emit copied the per-message errc out and tallied them)
+  (void)ec;
+  (void)errc_out;
   if (threadIdx.x) return;
+  const unsigned long long s_ok = ctl->m_ok, s_cap = ctl->m_cap;
   spk_dresult_t r = *res;
   const uint32_t nh = a.N.n_heaps;
   if (mode == SPK_MODE_VECTOR) {
@@ -2138,8 +2217,9 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
     if (rows)
       SPK_LAUNCH(nest_emit, dim3(nblocks(rows, 256)), dim3(256), 0, s, a, (const uint8_t *)d_wire,
                  d_msg_offsets, (const uint64_t *)starts, (const uint64_t *)U, rows,
-                 (const int32_t *)ec, ws, (const uint64_t *)cpos, (uint8_t *)d_recs, mode);
-    SPK_LAUNCH(nest_finish, dim3(1), dim3(256), 0, s, a, (const uint64_t *)part, nb,
+                 (const int32_t *)ec, ws, (const uint64_t *)cpos, (uint8_t *)d_recs, mode,
+                 (int32_t *)nullptr);
+    SPK_LAUNCH(nest_finish, dim3(1), dim3(64), 0, s, a, (const uint64_t *)part, nb,
                (const int32_t *)ec, ws, mode, d_res, (int32_t *)nullptr);
     return hipGetLastError();
   }
@@ -2150,8 +2230,8 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
   if ((er = nscan(U, rows, a.N.n_heaps, part, s)) != hipSuccess) return er;
   SPK_LAUNCH(nest_emit, dim3(nblocks(rows, 256)), dim3(256), 0, s, a, (const uint8_t *)d_wire,
              d_msg_offsets, (const uint64_t *)starts, (const uint64_t *)U, rows,
-             (const int32_t *)ec, ws, (const uint64_t *)cpos, (uint8_t *)d_recs, mode);
-  SPK_LAUNCH(nest_finish, dim3(1), dim3(256), 0, s, a, (const uint64_t *)part, nb,
+             (const int32_t *)ec, ws, (const uint64_t *)cpos, (uint8_t *)d_recs, mode, d_errc);
+  SPK_LAUNCH(nest_finish, dim3(1), dim3(64), 0, s, a, (const uint64_t *)part, nb,
              (const int32_t *)ec, ws, mode, d_res, d_errc);
   uint64_t *cpart = reinterpret_cast<uint64_t *>(ws + f.part) + (nb + 1) * a.N.n_heaps;
   if ((er = nscan(cons, rows, 1, cpart, s)) != hipSuccess) return er;

@@ -1842,7 +1842,7 @@ __device__ int32_t nt_read(const NTLayout &N, const Rd &rd, uint64_t &pos, uint6
       // value-initialised: zero_rest, spk_internal.hpp)
       bool dropped = false;
       for (;;) {
-        if constexpr (EMIT) zero_rest(N, r, i, iend, [&](uint32_t k) { return (uint64_t)U[64 * k]; });
+        if constexpr (EMIT) zero_rest(N, r, i, iend);
         if (!d) break;
         const uint32_t fo = c_op;
         const spk_op &ao = N.ops[fo & 0xFFu];
