@@ -379,10 +379,12 @@ def test_speculation_caps_mispredicted(tail):
     every 7th). The speculative walks reject the true records, chunks with no
     start under the caps are searched again without them, the resolution
     walks never see the caps: bit-exact with the oracle. The caps are a
-    build option (SPK_SCAP, off by default); this message takes ~35 ms with
-    and without them (its random-byte strings defeat the speculation, the
-    repair passes resolve those tiles): the bound only rules out per-record
-    sequential work."""
+    build option (SPK_SCAP, off by default). The message's 2-byte counts
+    screen random string bytes weakly (one in 16 passes); K1's speculative
+    walks check SPK_SPEC_PAST_W2 = 5 records past their chunk at that width
+    and a tile whose chunk 0 holds no start takes its first speculated one,
+    so no tile of the binary strings takes a false entry (round 3: 35.8 ms
+    through the sequential fixer; now ~0.6 ms for 62 MB): bounded at 3 ms."""
     cd = codec_for("recs")
     rng = np.random.default_rng(23)
     n = 40000
@@ -407,8 +409,10 @@ def test_speculation_caps_mispredicted(tail):
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
     assert cd.result().errc == 0
-    print(f"{tail}: {len(exp) / 1e6:.1f} MB decoded in {min(ts):.3f} ms")
-    assert min(ts) < 100.0, ts
+    r = cd.result()
+    print(f"{tail}: {len(exp) / 1e6:.1f} MB decoded in {min(ts):.3f} ms, tiles repaired "
+          f"{r.tiles_repaired}, sequential {r.tiles_sequential}")
+    assert min(ts) < 3.0, ts
 
 
 def test_screen_defeating_payload_bounded_time():

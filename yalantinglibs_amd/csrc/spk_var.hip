@@ -2340,6 +2340,14 @@ constexpr uint64_t kNoPos = ~0ull - 1;  // "no plausible start / unknown entry"
 #define SPK_SPEC_PAST 2
 #endif
 constexpr uint32_t kSpecPast = SPK_SPEC_PAST;  // records a speculative walk checks past its chunk
+// ... for a 2-byte count width: a random 16-bit count passes the first-count
+// screen (c0max ~ 4K) one time in 16, so a false start inside binary string
+// bytes survives kSpecPast more records one time in ~250 and half the tiles
+// of a 100-3000 B binary-string message took a false entry; with 5 it is one
+// in ~10^6 (a 4-byte count passes one time in ~10^6 already)
+#ifndef SPK_SPEC_PAST_W2
+#define SPK_SPEC_PAST_W2 5
+#endif
 constexpr uint32_t kAlt = 4;            // entries a tile function carries
 constexpr uint32_t kAltWords = 2 + kVS;   // entry, cnt, sums
 constexpr uint32_t kFnWords = 48;       // y, nalt, kAlt x kAltWords (+ pad)
@@ -2630,6 +2638,7 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
   cnt = 0;
   QFOR(q) sums[q] = 0;
   const bool exact = exact0 && lane == 0;  // the payload start: no search
+  const uint32_t npast = kNPast<NS> && w <= 2 ? (uint32_t)SPK_SPEC_PAST_W2 : kNPast<NS>;
   sp.np = 0;
   // speculation caps (flat layouts, sc: vec_hdr_sample's): a candidate start
   // and every record of its walk must keep each count within the caps, so
@@ -2762,7 +2771,7 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
       } else {
         if (!past) ex = x;
         ++past;
-        if (!L || past >= kNPast<NS>) break;
+        if (!L || past >= npast) break;
       }
       x += L;
     }
