@@ -81,7 +81,7 @@ struct variant_supported<std::variant<A...>> {
 };
 template <typename T>
 constexpr bool supported() {
-  if constexpr (is_fundamental_v<T> || is_string_v<T> || is_varint_v<T>) {
+  if constexpr (is_fundamental_v<T> || is_string_v<T> || is_varint_v<T> || is_bitset_v<T>) {
     return true;
   } else if constexpr (is_trivial_view_v<T>) {
     return is_trivially_serializable<typename trivial_view_traits<T>::value_type>();

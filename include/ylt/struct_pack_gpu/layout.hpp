@@ -156,7 +156,7 @@ void flatten_into(layout_builder &b) {
     b.varint(sizeof(typename varint_traits<T>::value_type),
              varint_traits<T>::zigzag ? SPK_VARINT_ZIGZAG : 0u);
   } else if constexpr (is_string_v<T>) {
-    b.span(1);
+    b.span(sizeof(string_char_t<T>));
   } else if constexpr (is_container_v<T>) {
     using E = elem_t<T>;
     if constexpr (is_trivially_serializable<E>())
@@ -487,7 +487,7 @@ void to_device(const T &v, marshal_state &s) {
     const typename varint_traits<T>::value_type x = v;
     std::memcpy(s.rec + op.rec_off, &x, op.size);
   } else if constexpr (is_string_v<T> || is_container_v<T>) {
-    using E = std::conditional_t<is_string_v<T>, char, elem_t<T>>;
+    using E = std::conditional_t<is_string_v<T>, string_char_t<T>, elem_t<T>>;
     const spk_op &op = s.L->ops[s.op];
     const uint32_t h = s.span;
     const uint32_t cnt = static_cast<uint32_t>(v.size());
@@ -650,14 +650,14 @@ void from_device(T &v, unmarshal_state &s) {
     std::memcpy(&x, s.rec + op.rec_off, op.size);
     v = x;
   } else if constexpr (is_string_v<T> || is_container_v<T>) {
-    using E = std::conditional_t<is_string_v<T>, char, elem_t<T>>;
+    using E = std::conditional_t<is_string_v<T>, string_char_t<T>, elem_t<T>>;
     const spk_op &op = s.L->ops[s.op];
     const uint32_t h = s.span;
     const uint32_t cnt = get_u32(s.rec, op.rec_off);
     const uint64_t eoff = get_u64(s.rec, op.aux);
     const uint8_t *src = s.heaps[h] + eoff * op.size;
     if constexpr (is_trivially_serializable<E>()) {
-      if constexpr (std::is_same_v<T, std::string_view> || is_std_span<T>::value) {
+      if constexpr (is_string_view_v<T> || is_std_span<T>::value) {
         // views alias the decoded heap (the reference's views alias the input)
         v = T(reinterpret_cast<typename T::const_pointer>(src), cnt);
       } else if constexpr (is_string_v<T> || is_contiguous_v<T>) {

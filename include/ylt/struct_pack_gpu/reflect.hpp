@@ -14,6 +14,7 @@
 // aggregates defeat brace-init counting -- use std::array.)
 #pragma once
 #include <array>
+#include <bitset>
 #include <cstddef>
 #include <deque>
 #include <list>
@@ -135,8 +136,50 @@ struct map_traits<std::unordered_multimap<K, V, H, E, A>> : std::true_type {
   static constexpr bool multi = true;
 };
 
+// string_t (type_id.hpp:160-187, reflection.hpp:350-360): std::basic_string /
+// basic_string_view of char, char8_t, char16_t, char32_t and wchar_t (the last
+// only under STRUCT_PACK_ENABLE_UNPORTABLE_TYPE, checked by its type id)
+template <typename C>
+constexpr bool is_char_v = std::is_same_v<C, char> || std::is_same_v<C, char8_t> ||
+                           std::is_same_v<C, char16_t> || std::is_same_v<C, char32_t> ||
+                           std::is_same_v<C, wchar_t>;
+template <typename T> struct string_traits : std::false_type {
+  static constexpr bool view = false;
+};
+template <typename C, typename Tr, typename A>
+struct string_traits<std::basic_string<C, Tr, A>> : std::bool_constant<is_char_v<C>> {
+  using char_type = C;
+  static constexpr bool view = false;
+};
+template <typename C, typename Tr>
+struct string_traits<std::basic_string_view<C, Tr>> : std::bool_constant<is_char_v<C>> {
+  using char_type = C;
+  static constexpr bool view = true;
+};
 template <typename T>
-constexpr bool is_string_v = std::is_same_v<T, std::string> || std::is_same_v<T, std::string_view>;
+constexpr bool is_string_v = string_traits<T>::value;
+template <typename T>
+constexpr bool is_string_view_v = string_traits<T>::value && string_traits<T>::view;
+// the element of a string_t (char for anything else: never used there)
+template <typename T, bool = is_string_v<T>>
+struct string_char { using type = char; };
+template <typename T>
+struct string_char<T, true> { using type = typename string_traits<T>::char_type; };
+template <typename T>
+using string_char_t = typename string_char<T>::type;
+// 128-bit integers (type_id.hpp:190-197: int128_t / uint128_t under
+// STRUCT_PACK_ENABLE_INT128, gcc / clang): fundamentals of 16 bytes
+template <typename T>
+constexpr bool is_int128_v = std::is_same_v<T, __int128> || std::is_same_v<T, unsigned __int128>;
+// bitset_t (reflection.hpp:558-591, under STRUCT_PACK_ENABLE_UNPORTABLE_TYPE):
+// std::bitset<N> whose object is exactly its (N + 7) / 8 bytes, written raw
+template <typename T> struct bitset_traits : std::false_type {};
+template <std::size_t N>
+struct bitset_traits<std::bitset<N>> : std::bool_constant<(N + 7) / 8 == sizeof(std::bitset<N>)> {
+  static constexpr std::size_t bits = N;
+};
+template <typename T>
+constexpr bool is_bitset_v = bitset_traits<T>::value;
 template <typename T>
 constexpr bool is_set_v = set_traits<T>::value;
 template <typename T>
@@ -151,7 +194,7 @@ constexpr bool is_container_v =
 template <typename T>
 constexpr bool is_monostate_v = std::is_same_v<T, std::monostate>;
 template <typename T>
-constexpr bool is_fundamental_v = std::is_arithmetic_v<T> || std::is_enum_v<T>;
+constexpr bool is_fundamental_v = std::is_arithmetic_v<T> || std::is_enum_v<T> || is_int128_v<T>;
 template <typename T>
 constexpr bool is_varint_v = varint_traits<T>::value;
 template <typename T>

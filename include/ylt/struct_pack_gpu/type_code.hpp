@@ -31,11 +31,12 @@ struct lit_t {
 
 enum : uint8_t {
   TID_INT32 = 1, TID_UINT32 = 2, TID_INT64 = 3, TID_UINT64 = 4, TID_INT8 = 5,
-  TID_UINT8 = 6, TID_INT16 = 7, TID_UINT16 = 8, TID_BOOL = 11, TID_CHAR8 = 12,
-  TID_CHAR16 = 13, TID_CHAR32 = 14, TID_FLOAT32 = 17, TID_FLOAT64 = 18,
+  TID_UINT8 = 6, TID_INT16 = 7, TID_UINT16 = 8, TID_INT128 = 9, TID_UINT128 = 10,
+  TID_BOOL = 11, TID_CHAR8 = 12, TID_CHAR16 = 13, TID_CHAR32 = 14, TID_WCHAR = 15,
+  TID_FLOAT32 = 17, TID_FLOAT64 = 18,
   TID_VINT32 = 20, TID_VINT64 = 21, TID_VUINT32 = 22, TID_VUINT64 = 23,
   TID_STRING = 128, TID_ARRAY = 129, TID_MAP = 130, TID_SET = 131, TID_CONTAINER = 132,
-  TID_OPTIONAL = 133, TID_VARIANT = 134, TID_MONOSTATE = 250, TID_STRUCT = 253, TID_END = 255
+  TID_OPTIONAL = 133, TID_VARIANT = 134, TID_BITSET = 136, TID_MONOSTATE = 250, TID_STRUCT = 253, TID_END = 255
 };
 
 // sp_config bits of a record that turn members into varints (reflection.hpp:
@@ -67,9 +68,32 @@ constexpr uint8_t varint_tid() {
   return t;
 }
 
+// the reference's opt-in types (type_id.hpp:168-172,190-197, 317-320): the
+// same macros switch them on here
+#ifdef STRUCT_PACK_ENABLE_UNPORTABLE_TYPE
+inline constexpr bool kUnportableTypes = true;
+#else
+inline constexpr bool kUnportableTypes = false;
+#endif
+#if defined(STRUCT_PACK_ENABLE_INT128) && (defined(__GNUC__) || defined(__clang__))
+inline constexpr bool kInt128Types = true;
+#else
+inline constexpr bool kInt128Types = false;
+#endif
+template <typename T>
+inline constexpr bool dependent_false_v = false;
+
 template <typename T>
 constexpr uint8_t fundamental_id() {
-  if constexpr (std::is_enum_v<T>) {
+  if constexpr (is_int128_v<T>) {
+    static_assert(kInt128Types || dependent_false_v<T>,
+                  "128-bit integers need STRUCT_PACK_ENABLE_INT128 (as in the reference)");
+    return std::is_same_v<T, __int128> ? TID_INT128 : TID_UINT128;
+  } else if constexpr (std::is_same_v<T, wchar_t>) {
+    static_assert(kUnportableTypes || dependent_false_v<T>,
+                  "wchar_t needs STRUCT_PACK_ENABLE_UNPORTABLE_TYPE (as in the reference)");
+    return TID_WCHAR;
+  } else if constexpr (std::is_enum_v<T>) {
     return fundamental_id<std::underlying_type_t<T>>();
   } else if constexpr (std::is_same_v<T, bool>) {
     return TID_BOOL;
@@ -116,6 +140,8 @@ constexpr bool all_trivial(std::index_sequence<I...>) {
 template <typename T>
 constexpr bool is_trivially_serializable() {
   if constexpr (is_fundamental_v<T> || is_monostate_v<T>) {
+    return true;
+  } else if constexpr (is_bitset_v<T>) {  // reflection.hpp:878
     return true;
   } else if constexpr (is_std_array<T>::value) {
     return is_trivially_serializable<typename T::value_type>();
@@ -250,9 +276,14 @@ constexpr lit_t type_literal() {
     l.append(type_literal<typename trivial_view_traits<T>::value_type>());
   } else if constexpr (is_fundamental_v<T>) {
     l.push(fundamental_id<T>());
-  } else if constexpr (is_string_v<T>) {
+  } else if constexpr (is_string_v<T>) {  // string_t + the char type's id
     l.push(TID_STRING);
-    l.push(TID_CHAR8);
+    l.push(fundamental_id<string_char_t<T>>());
+  } else if constexpr (is_bitset_v<T>) {  // bitset_t + its bit count (type_calculate.hpp:264-268)
+    static_assert(kUnportableTypes || dependent_false_v<T>,
+                  "std::bitset needs STRUCT_PACK_ENABLE_UNPORTABLE_TYPE (as in the reference)");
+    l.push(TID_BITSET);
+    l.append(size_literal(bitset_traits<T>::bits));
   } else if constexpr (is_map_v<T>) {  // type_calculate.hpp:284-290
     l.push(TID_MAP);
     l.append(type_literal<remove_cvref_t<typename T::key_type>>());

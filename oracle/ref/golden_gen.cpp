@@ -144,6 +144,17 @@ static int cmd_kat() {
   kat_one<cpx::complicated_object>(os, "complicated_object", first);
   kat_one<uint8_t, uint16_t, uint32_t, uint64_t, int8_t, int16_t, int64_t,
           bool, char, float, double>(os, "fundamentals", first);
+  kat_one<__int128, unsigned __int128, wchar_t, char16_t, char32_t>(os, "wide fundamentals",
+                                                                   first);
+  kat_one<std::bitset<64>>(os, "bitset<64>", first);
+  kat_one<std::bitset<128>>(os, "bitset<128>", first);
+  kat_one<std::u16string>(os, "u16string", first);
+  kat_one<std::u32string>(os, "u32string", first);
+  kat_one<std::wstring>(os, "wstring", first);
+  kat_one<WideT>(os, "WideT", first);
+  kat_one<std::vector<WideT>>(os, "vector<WideT>", first);
+  kat_one<Wide>(os, "Wide", first);
+  kat_one<std::vector<Wide>>(os, "vector<Wide>", first);
   os << "\n}\n";
   std::cout << os.str();
   return 0;
@@ -280,6 +291,10 @@ static bool with_case(const Args &a, F &&f) {
     return f.template operator()<CmpG>([=](CmpG &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "monster")
     return f.template operator()<Monster>([=](Monster &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "widet")
+    return f.template operator()<WideT>([=](WideT &o, uint64_t i) { fill(o, s, i, p); });
+  if (k == "wide")
+    return f.template operator()<Wide>([=](Wide &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "rect2")
     return f.template operator()<rect2<int32_t>>([=](rect2<int32_t> &o, uint64_t i) { fill(o, s, i, p); });
   if (k == "rect")  // C1: benchmark rect<int> default values

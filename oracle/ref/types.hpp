@@ -12,6 +12,7 @@
 // so that the GPU box can regenerate the exact same inputs from a seed.
 #pragma once
 #include <array>
+#include <bitset>
 #include <cstdint>
 #include <cstring>
 #include <deque>
@@ -422,6 +423,30 @@ struct complicated_object {
   std::vector<std::array<trivial_one, 2>> p;
 };
 }  // namespace cpx
+
+// ---- the reference's opt-in types (built with STRUCT_PACK_ENABLE_INT128 and
+// STRUCT_PACK_ENABLE_UNPORTABLE_TYPE, as its own tests are): 128-bit
+// integers, std::bitset, wchar_t, and the char16_t / char32_t strings
+struct WideT {  // trivially serializable: raw bytes with padding
+  __int128 a;
+  std::bitset<64> bits;
+  char32_t c32;
+  wchar_t wc;
+  char16_t c16;
+  unsigned __int128 b;
+};
+struct Wide {
+  int32_t id;
+  std::u16string a;
+  __int128 big;
+  std::u32string b;
+  std::bitset<128> bits;
+  std::wstring c;
+  unsigned __int128 ubig;
+  wchar_t wc;
+  char16_t c16;
+  WideT t;
+};
 
 template <typename T>
 constexpr bool kHasCompat = false;
@@ -903,6 +928,38 @@ inline void fill(rect2<int32_t> &o, uint64_t seed, uint64_t i, uint32_t) {
   o.y = (int32_t)(uint32_t)g.sg(1);
   o.width = (int32_t)(uint32_t)g.sg(2);
   o.height = (int32_t)(uint32_t)g.sg(3);
+}
+
+inline unsigned __int128 u128(uint64_t hi, uint64_t lo) {
+  return ((unsigned __int128)hi << 64) | lo;
+}
+inline void fill(WideT &o, uint64_t seed, uint64_t i, uint32_t) {
+  std::memset((void *)&o, 0, sizeof(o));
+  o.a = (__int128)u128(rnd(seed, i, 20), rnd(seed, i, 21));
+  o.bits = std::bitset<64>(rnd(seed, i, 22));
+  const uint64_t r = rnd(seed, i, 23);
+  o.c32 = (char32_t)(uint32_t)r;
+  o.wc = (wchar_t)(int32_t)(uint32_t)(r >> 32);
+  o.c16 = (char16_t)rnd(seed, i, 24);
+  o.b = u128(rnd(seed, i, 25), rnd(seed, i, 26));
+}
+// element j of a wide string: the low bytes of mix64(word k + j)
+inline void fill(Wide &o, uint64_t seed, uint64_t i, uint32_t maxlen) {
+  o.id = (int32_t)(uint32_t)rnd(seed, i, 0);
+  o.a.resize((size_t)(rnd(seed, i, 1) % (maxlen + 1ull)));
+  for (size_t j = 0; j < o.a.size(); ++j) o.a[j] = (char16_t)mix64(rnd(seed, i, 2) + j);
+  o.big = (__int128)u128(rnd(seed, i, 3), rnd(seed, i, 4));
+  o.b.resize((size_t)(rnd(seed, i, 5) % (maxlen + 1ull)));
+  for (size_t j = 0; j < o.b.size(); ++j) o.b[j] = (char32_t)(uint32_t)mix64(rnd(seed, i, 6) + j);
+  o.bits = (std::bitset<128>(rnd(seed, i, 7)) << 64) | std::bitset<128>(rnd(seed, i, 27));
+  o.c.resize((size_t)(rnd(seed, i, 8) % (maxlen + 1ull)));
+  for (size_t j = 0; j < o.c.size(); ++j)
+    o.c[j] = (wchar_t)(int32_t)(uint32_t)mix64(rnd(seed, i, 9) + j);
+  o.ubig = u128(rnd(seed, i, 10), rnd(seed, i, 11));
+  const uint64_t r = rnd(seed, i, 12);
+  o.wc = (wchar_t)(int32_t)(uint32_t)r;
+  o.c16 = (char16_t)(r >> 32);
+  fill(o.t, seed, i, 0);
 }
 
 }  // namespace spk_gold

@@ -590,6 +590,40 @@ int main() {
     std::string n3;
     CHECK(struct_pack::gpu::read(cut, n3) == struct_pack::errc::no_buffer_space);
   }
+  g_section = 7;
+  std::fprintf(stderr, "section 7\n");
+  // 7. the opt-in types (__int128, std::bitset, wchar_t, u16string / u32string /
+  // wstring; this binary is built with the reference's macros for them)
+  {
+    std::vector<Wide> ws(2500);
+    for (std::size_t i = 0; i < ws.size(); ++i) spk_gold::fill(ws[i], 0x5EED0023, i, 24);
+    const auto want = struct_pack::serialize<std::string>(ws);
+    CHECK(struct_pack::gpu::serialize<std::string>(ws) == want);
+    std::vector<Wide> back;
+    CHECK(!struct_pack::gpu::deserialize_to(back, want) && back.size() == ws.size());
+    CHECK(struct_pack::serialize<std::string>(back) == want);  // every member came back
+    bool ok = back.size() == ws.size();
+    for (std::size_t i = 0; ok && i < ws.size(); ++i)
+      ok = back[i].a == ws[i].a && back[i].c == ws[i].c && back[i].big == ws[i].big &&
+           back[i].bits == ws[i].bits && back[i].t.b == ws[i].t.b;
+    CHECK(ok);
+    Wide one;
+    spk_gold::fill(one, 7, 3, 40);
+    const auto w1 = struct_pack::serialize<std::string>(one);
+    CHECK(struct_pack::gpu::serialize<std::string>(one) == w1);
+    auto b1 = struct_pack::gpu::deserialize<Wide>(w1);
+    CHECK(b1.has_value() && struct_pack::serialize<std::string>(b1.value()) == w1);
+    std::vector<WideT> ts(4000);
+    for (std::size_t i = 0; i < ts.size(); ++i) spk_gold::fill(ts[i], 0x5EED0022, i, 0);
+    const auto wt = struct_pack::serialize<std::string>(ts);
+    CHECK(struct_pack::gpu::serialize<std::string>(ts) == wt);
+    std::vector<WideT> tb;
+    CHECK(!struct_pack::gpu::deserialize_to(tb, wt) && struct_pack::serialize<std::string>(tb) == wt);
+    const std::u32string u = U"wide \U0001F600 chars";
+    CHECK(struct_pack::gpu::serialize<std::string>(u) == struct_pack::serialize<std::string>(u));
+    auto ub = struct_pack::gpu::deserialize<std::u32string>(struct_pack::serialize<std::string>(u));
+    CHECK(ub.has_value() && ub.value() == u);
+  }
   std::printf("{\"checks\": %d, \"failures\": %d}\n", g_checks, g_fail);
   return g_fail ? 1 : 0;
 }

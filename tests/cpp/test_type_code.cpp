@@ -47,6 +47,12 @@ static_assert(is_gpu_batch_v<std::vector<Lists>>);
 static_assert(is_gpu_message_v<CmpG>);
 static_assert(!gpu::detail::is_trivially_serializable<rect2<int32_t>>());
 static_assert(!gpu::detail::is_trivially_serializable<std::variant<int, double>>());
+// the opt-in types (built with STRUCT_PACK_ENABLE_INT128 and
+// STRUCT_PACK_ENABLE_UNPORTABLE_TYPE): kat.json "WideT" / "Wide"
+static_assert(gpu::detail::is_trivially_serializable<WideT>());
+static_assert(get_type_code<WideT>() == 606094358u);
+static_assert(get_type_code<Wide>() == 4056439014u);
+static_assert(gpu::detail::is_bitset_v<std::bitset<128>> && !gpu::detail::is_bitset_v<std::bitset<32>>);
 
 template <typename T>
 static void lit_json(const char *name, bool &first) {
@@ -144,6 +150,15 @@ int main() {
   lit_json<std::map<int32_t, std::string>>("map<int32_t,string>", first);
   lit_json<std::unordered_multimap<int32_t, int32_t>>("unordered_multimap<int32_t,int32_t>",
                                                       first);
+  lit_json<std::bitset<64>>("bitset<64>", first);
+  lit_json<std::bitset<128>>("bitset<128>", first);
+  lit_json<std::u16string>("u16string", first);
+  lit_json<std::u32string>("u32string", first);
+  lit_json<std::wstring>("wstring", first);
+  lit_json<WideT>("WideT", first);
+  lit_json<std::vector<WideT>>("vector<WideT>", first);
+  lit_json<Wide>("Wide", first);
+  lit_json<std::vector<Wide>>("vector<Wide>", first);
   printf("},\n\"layout\": {\n");
   first = true;
   layout_json<Rec64>("rec64", first);
@@ -176,6 +191,8 @@ int main() {
   layout_json<Lists>("lists", first);
   layout_json<Maps>("maps", first);
   layout_json<AlRec>("alrec", first);
+  layout_json<WideT>("widet", first);
+  layout_json<Wide>("wide", first);
   layout_json<RecS, sp_config::ENABLE_TYPE_INFO>("recs_typeinfo", first);
   layout_json<Rec64, sp_config::DISABLE_ALL_META_INFO>("rec64_nometa", first);
   printf("}}\n");

@@ -37,7 +37,8 @@ SEED = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004,
         "cmp": 0x5EED0016, "cmpold": 0x5EED0016, "cmpnew": 0x5EED0016,
         "fv": 0x5EED0017, "fve": 0x5EED0018, "fv32": 0x5EED0019, "ev": 0x5EED001A,
         "valreq": 0x5EED001B, "exp": 0x5EED001C, "cmpg": 0x5EED001D, "monster": 0x5EED001E,
-        "rect2": 0x5EED001F, "lists": 0x5EED0020, "maps": 0x5EED0021, "cplx": 0}
+        "rect2": 0x5EED001F, "lists": 0x5EED0020, "maps": 0x5EED0021, "cplx": 0,
+        "widet": 0x5EED0022, "wide": 0x5EED0023}
 
 # (case_mode, n, param, conf, keep_bin)
 SMALL = [
@@ -137,6 +138,12 @@ SMALL = [
     ("maps_A", 200, 0, "default"), ("maps_B", 200, 0, "default"), ("maps_A", 50, 0, "typeinfo"),
     ("cplx_B", 1, 0, "default"), ("cplx_B", 1, 0, "typeinfo"), ("cplx_A", 3, 0, "default"),
     ("cplx_A", 2, 0, "typeinfo"), ("cplx_B", 5, 0, "nometa"),
+    # opt-in types (STRUCT_PACK_ENABLE_INT128 / _UNPORTABLE_TYPE): __int128,
+    # std::bitset, wchar_t, u16string / u32string / wstring
+    ("widet_A", 0, 0, "default"), ("widet_A", 300, 0, "default"), ("widet_B", 50, 0, "default"),
+    ("widet_A", 40, 0, "typeinfo"), ("wide_A", 0, 6, "default"), ("wide_A", 1, 6, "default"),
+    ("wide_A", 200, 6, "default"), ("wide_B", 100, 6, "default"), ("wide_A", 40, 300, "default"),
+    ("wide_A", 50, 6, "typeinfo"), ("wide_B", 30, 6, "nometa"),
 ]
 MEDIUM = [  # digest only (wire > ~1 MB)
     ("rec64_A", 65535, 0, "default"), ("rec64_A", 65536, 0, "default"),
@@ -161,6 +168,7 @@ MEDIUM = [  # digest only (wire > ~1 MB)
     ("monster_B", 20000, 20, "default"), ("rect2_A", 70000, 0, "default"),
     ("lists_A", 30000, 6, "default"), ("maps_A", 20000, 0, "default"),
     ("maps_B", 10000, 0, "default"), ("cplx_A", 3000, 0, "default"),
+    ("wide_A", 20000, 16, "default"), ("widet_A", 30000, 0, "default"),
 ]
 BIG = [  # BASELINE.json full-size configs (digest only)
     ("rec64_A", 100_000_000, 0, "default"),
@@ -294,6 +302,7 @@ ERR_BASES = [
     ("rect2_A", 6, 0, "default"), ("rect2_B", 1, 0, "default"),
     ("lists_A", 5, 4, "default"), ("lists_B", 1, 6, "default"),
     ("maps_A", 4, 0, "default"), ("maps_B", 1, 0, "default"),
+    ("wide_A", 4, 6, "default"), ("wide_B", 1, 6, "default"), ("widet_A", 3, 0, "default"),
 ]
 # compatible members across writer versions: (writer, reader, n, param) — the
 # writer's message mutated and decoded as the reader's type (one type code)

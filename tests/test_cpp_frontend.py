@@ -24,7 +24,8 @@ def cpp_json(tmp_path_factory):
     if not os.path.exists(CLANG):
         pytest.skip("clang++ not available")
     exe = str(tmp_path_factory.mktemp("cpp") / "ttc")
-    subprocess.run([CLANG, "-std=c++20", "-O1", "-DNDEBUG", "-I", os.path.join(ROOT, "include"),
+    subprocess.run([CLANG, "-std=c++20", "-O1", "-DNDEBUG", "-DSTRUCT_PACK_ENABLE_INT128",
+                    "-DSTRUCT_PACK_ENABLE_UNPORTABLE_TYPE", "-I", os.path.join(ROOT, "include"),
                     "-o", exe, os.path.join(ROOT, "tests", "cpp", "test_type_code.cpp")],
                    check=True)
     return json.loads(subprocess.run([exe], check=True, capture_output=True, text=True).stdout)
@@ -45,6 +46,7 @@ def test_cpp_type_codes_match_reference_kats(cpp_json):
                                        ("fve", 0), ("fv32", 0), ("ev", 0), ("valreq", 0),
                                        ("monster", 0), ("rect2", 0), ("lists", 0), ("maps", 0),
                                        ("alrec", 0), ("cmp", 0), ("cmpnew", 0),
+                                       ("widet", 0), ("wide", 0),
                                        ("recs", S.ENABLE_TYPE_INFO),
                                        ("rec64", S.DISABLE_ALL_META_INFO)])
 def test_cpp_and_python_descriptors_agree(cpp_json, case, conf):
@@ -125,4 +127,50 @@ void use_protocol() {
 """
     r = _compile(cxx, src, ["-I", REF_INC, "-I", REF_INC + "/ylt/thirdparty",
                             "-I", REF_INC + "/ylt/standalone"])
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
+OPT_IN = """
+#include <ylt/struct_pack_gpu.hpp>
+#include <bitset>
+struct wide_rec { int32_t id; %s v; };
+constexpr auto code = struct_pack::gpu::get_type_code<std::vector<wide_rec>>();
+"""
+
+
+@pytest.mark.parametrize("member,macro", [("wchar_t", "STRUCT_PACK_ENABLE_UNPORTABLE_TYPE"),
+                                          ("std::wstring", "STRUCT_PACK_ENABLE_UNPORTABLE_TYPE"),
+                                          ("std::bitset<64>", "STRUCT_PACK_ENABLE_UNPORTABLE_TYPE"),
+                                          ("__int128", "STRUCT_PACK_ENABLE_INT128"),
+                                          ("unsigned __int128", "STRUCT_PACK_ENABLE_INT128")])
+def test_opt_in_types_need_the_reference_macros(member, macro):
+    """wchar_t / std::bitset need STRUCT_PACK_ENABLE_UNPORTABLE_TYPE and the
+    128-bit integers STRUCT_PACK_ENABLE_INT128, as in the reference
+    (type_id.hpp:168-172,190-197,240-244,317-320): a compile error without the
+    macro, a type code with it."""
+    src = OPT_IN % member
+    r = _compile("g++", src, ["-DSPK_GPU_STANDALONE"])
+    assert r.returncode != 0 and "STRUCT_PACK_ENABLE" in r.stderr, r.stderr[-2000:]
+    r = _compile("g++", src, ["-DSPK_GPU_STANDALONE", "-D" + macro])
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_INC), reason="reference headers absent")
+def test_opt_in_type_codes_match_reference():
+    """hash_matches_reference over the opt-in types, both front ends in one
+    translation unit built with the reference's macros."""
+    src = """
+#include <ylt/coro_rpc/impl/protocol/coro_rpc_protocol.hpp>
+#include <ylt/coro_rpc/impl/protocol/struct_pack_gpu_protocol.hpp>
+#include <bitset>
+struct wide_rec { int32_t id; std::u16string a; __int128 b; std::bitset<128> c; std::wstring d;
+                  wchar_t e; char32_t f; unsigned __int128 g; };
+static_assert(struct_pack::gpu::hash_matches_reference<std::vector<wide_rec>>());
+static_assert(struct_pack::gpu::hash_matches_reference<wide_rec>());
+static_assert(struct_pack::gpu::hash_matches_reference<std::u32string>());
+static_assert(struct_pack::gpu::hash_matches_reference<std::bitset<64>>());
+"""
+    r = _compile("g++", src, ["-I", REF_INC, "-I", REF_INC + "/ylt/thirdparty",
+                              "-I", REF_INC + "/ylt/standalone", "-DSTRUCT_PACK_ENABLE_INT128",
+                              "-DSTRUCT_PACK_ENABLE_UNPORTABLE_TYPE"])
     assert r.returncode == 0, r.stderr[-3000:]

@@ -40,6 +40,10 @@ KAT_TYPES = {
     "unordered_multimap<int32_t,int32_t>": S.Map(S.int32, S.int32, multi=True, ordered=False),
     "pair<string,person>": S.Pair(S.String(), synth.CPerson),
     "complicated_object": synth.Cplx,
+    "bitset<64>": S.Bitset(64), "bitset<128>": S.Bitset(128),
+    "u16string": S.String(elem=S.char16), "u32string": S.String(elem=S.char32),
+    "wstring": S.String(elem=S.wchar), "WideT": synth.WideT, "vector<WideT>": S.Vector(synth.WideT),
+    "Wide": synth.Wide, "vector<Wide>": S.Vector(synth.Wide),
 }
 
 
@@ -57,6 +61,9 @@ def test_tuple_and_fundamentals_codes():
     fs = [S.uint8, S.uint16, S.uint32, S.uint64, S.int8, S.int16, S.int64,
           S.boolean, S.char, S.float32, S.float64]
     assert S.get_type_literal(*fs).hex() == k["fundamentals"]["literal"]
+    fs = [S.int128, S.uint128, S.wchar, S.char16, S.char32]
+    assert S.get_type_literal(*fs).hex() == k["wide fundamentals"]["literal"]
+    assert S.get_type_code(*fs) == k["wide fundamentals"]["code"]
 
 
 def test_size_literal():

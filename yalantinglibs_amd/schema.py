@@ -33,11 +33,12 @@ DISABLE_ALL_META_INFO = 0b11
 # ---- type_id (ref type_id.hpp:25-81) --------------------------------------
 TID_INT32, TID_UINT32, TID_INT64, TID_UINT64 = 1, 2, 3, 4
 TID_INT8, TID_UINT8, TID_INT16, TID_UINT16 = 5, 6, 7, 8
-TID_BOOL, TID_CHAR8 = 11, 12
+TID_INT128, TID_UINT128 = 9, 10
+TID_BOOL, TID_CHAR8, TID_CHAR16, TID_CHAR32, TID_WCHAR = 11, 12, 13, 14, 15
 TID_FLOAT32, TID_FLOAT64 = 17, 18
 TID_VINT32, TID_VINT64, TID_VUINT32, TID_VUINT64 = 20, 21, 22, 23
 TID_STRING, TID_ARRAY, TID_MAP, TID_SET, TID_CONTAINER = 128, 129, 130, 131, 132
-TID_OPTIONAL, TID_VARIANT, TID_EXPECTED = 133, 134, 135
+TID_OPTIONAL, TID_VARIANT, TID_EXPECTED, TID_BITSET = 133, 134, 135, 136
 TID_MONOSTATE = 250
 TID_STRUCT = 253
 TID_END = 255
@@ -117,6 +118,34 @@ boolean = Fund("bool", TID_BOOL, 1, "<u1")
 char = Fund("char", TID_CHAR8, 1, "<u1")
 float32 = Fund("float", TID_FLOAT32, 4, "<f4")
 float64 = Fund("double", TID_FLOAT64, 8, "<f8")
+char16 = Fund("char16_t", TID_CHAR16, 2, "<u2")
+char32 = Fund("char32_t", TID_CHAR32, 4, "<u4")
+# the reference's opt-in types (type_id.hpp:37-44,168-172,190-197): wchar_t
+# under STRUCT_PACK_ENABLE_UNPORTABLE_TYPE (4 bytes, Linux), __int128 /
+# unsigned __int128 under STRUCT_PACK_ENABLE_INT128 (16 bytes, alignment 16;
+# raw bytes in the device record)
+wchar = Fund("wchar_t", TID_WCHAR, 4, "<i4")
+int128 = Fund("__int128", TID_INT128, 16, "V16")
+uint128 = Fund("unsigned __int128", TID_UINT128, 16, "V16")
+
+
+class Bitset(Fund):
+    """std::bitset<N> (bitset_t, STRUCT_PACK_ENABLE_UNPORTABLE_TYPE;
+    reflection.hpp:558-591): only bitsets whose object is exactly (N + 7) / 8
+    bytes (libstdc++: whole 64-bit words), written raw (packer.hpp:268-270);
+    literal bitset_t + size literal of N (type_calculate.hpp:264-268)."""
+
+    def __init__(self, nbits: int):
+        size = (nbits + 7) // 8
+        if size % 8:
+            raise ValueError("std::bitset<N> is a struct_pack bitset only when "
+                             "(N + 7) / 8 == sizeof: N in (64k - 8, 64k]")
+        super().__init__(f"std::bitset<{nbits}>", TID_BITSET, size, f"V{size}")
+        self.nbits = nbits
+        self.align = 8
+
+    def literal(self):
+        return bytes([TID_BITSET]) + size_literal(self.nbits)
 
 
 class VarInt(SpType):
@@ -250,16 +279,18 @@ def Pair(first: SpType, second: SpType) -> "Struct":
 
 
 class String(SpType):
-    """std::string / std::string_view (string_t of char)."""
+    """std::string / std::string_view (string_t of char); elem = char16 /
+    char32 / wchar for std::u16string / u32string / wstring (string_t + the
+    char type's id, type_calculate.hpp:274-278; elements raw on the wire)."""
 
-    name = "std::string"
-
-    def __init__(self, config: int = DEFAULT):
+    def __init__(self, config: int = DEFAULT, elem: SpType = None):
         self.config = config
-        self.elem = char
+        self.elem = elem or char
+        self.name = {TID_CHAR16: "std::u16string", TID_CHAR32: "std::u32string",
+                     TID_WCHAR: "std::wstring"}.get(self.elem.tid, "std::string")
 
     def literal(self):
-        return bytes([TID_STRING, TID_CHAR8])
+        return bytes([TID_STRING, self.elem.tid])
 
     @property
     def has_container(self):

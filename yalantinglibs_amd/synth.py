@@ -178,6 +178,14 @@ Cplx = S.Struct("complicated_object", [
     ("k", S.Map(S.int32, S.int32, multi=True, ordered=False)),
     ("m", S.Array(CPerson, 2)), ("n", S.Array(CPerson, 2)), ("o", S.Pair(S.String(), CPerson)),
     ("p", S.Vector(S.Array(TrivialOne, 2)))])
+# the reference's opt-in types (types.hpp WideT / Wide: 128-bit integers,
+# std::bitset, wchar_t, char16_t / char32_t strings)
+WideT = S.Struct("WideT", [("a", S.int128), ("bits", S.Bitset(64)), ("c32", S.char32),
+                           ("wc", S.wchar), ("c16", S.char16), ("b", S.uint128)])
+Wide = S.Struct("Wide", [("id", S.int32), ("a", S.String(elem=S.char16)), ("big", S.int128),
+                         ("b", S.String(elem=S.char32)), ("bits", S.Bitset(128)),
+                         ("c", S.String(elem=S.wchar)), ("ubig", S.uint128), ("wc", S.wchar),
+                         ("c16", S.char16), ("t", WideT)])
 
 CASE_TYPES = {"rec64": Rec64, "recs": RecS, "outer": Outer, "pad": Pad,
               "mixed": Mixed, "rect": RectInt, "rpcrect": RpcRect,
@@ -186,7 +194,8 @@ CASE_TYPES = {"rec64": Rec64, "recs": RecS, "outer": Outer, "pad": Pad,
               "vnt": Vnt, "cmp": Cmp, "cmpold": CmpOld, "cmpnew": CmpNew, "fv": FV, "fve": FVE,
               "fv32": FV32, "ev": EV, "al8": Al8, "alout": AlOuter, "packed": Packed, "alrec": AlRec,
               "valreq": ValidateRequest, "exp": Exp, "cmpg": CmpG, "monster": Monster,
-              "rect2": Rect2, "lists": Lists, "maps": Maps, "cplx": Cplx}
+              "rect2": Rect2, "lists": Lists, "maps": Maps, "cplx": Cplx,
+              "widet": WideT, "wide": Wide}
 # vector<rect<int>> / vector<rect2<int32_t>> have their own ADL set_sp_config
 # (benchmark data_def.hpp:69-72,90-94)
 VECTOR_CONFIG = {"rect": S.DISABLE_ALL_META_INFO, "rect2": S.DISABLE_ALL_META_INFO}
@@ -616,9 +625,46 @@ def make_batch(case: str, n: int, seed: int, param: int = 48):
         recs, heaps = _make_maps(L, recs, idx, seed)
     elif case == "cplx":
         recs, heaps = _make_cplx(L, recs, n)
+    elif case == "widet":
+        recs = _widet_raw(seed, idx).view(L.dtype).reshape(n)
+    elif case == "wide":  # fill(Wide&)
+        recs["id"] = i32(rnd(seed, idx, 0))
+        for f, kl, kw, dt in (("a", 1, 2, np.uint16), ("b", 5, 6, np.uint32), ("c", 8, 9, np.uint32)):
+            lens = (rnd(seed, idx, kl) % np.uint64(param + 1)).astype(np.int64)
+            recs[f + ".n"] = lens
+            recs[f + ".off"] = _excl(lens)
+            owner, j = _seg(lens)
+            with np.errstate(over="ignore"):
+                w = mix64(rnd(seed, idx[owner], kw) + j)
+            heaps.append(w.astype(dt).view(np.uint8).reshape(-1))
+        recs["big"] = _u128_raw(rnd(seed, idx, 3), rnd(seed, idx, 4)).view("V16").reshape(n)
+        recs["bits"] = _u128_raw(rnd(seed, idx, 7), rnd(seed, idx, 27)).view("V16").reshape(n)
+        recs["ubig"] = _u128_raw(rnd(seed, idx, 10), rnd(seed, idx, 11)).view("V16").reshape(n)
+        r = rnd(seed, idx, 12)
+        recs["wc"] = i32(r)
+        recs["c16"] = (r >> np.uint64(32)).astype(np.uint16)
+        recs["t"] = _widet_raw(seed, idx).view("V64").reshape(n)
     else:
         raise KeyError(case)
     return L, recs, heaps
+
+
+def _u128_raw(hi, lo):
+    """(hi << 64) | lo as 16 little-endian bytes per row."""
+    return np.ascontiguousarray(np.stack([np.asarray(lo, np.uint64), np.asarray(hi, np.uint64)],
+                                         1)).view(np.uint8).reshape(-1, 16)
+
+
+def _widet_raw(seed, idx):
+    """fill(WideT&): a (16 B), bits (8), c32, wc, c16, zero padding, b (16) at 48."""
+    raw = np.zeros((len(idx), 64), np.uint8)
+    raw[:, 0:16] = _u128_raw(rnd(seed, idx, 20), rnd(seed, idx, 21))
+    raw[:, 16:24] = rnd(seed, idx, 22)[:, None].view(np.uint8).reshape(-1, 8)
+    r = rnd(seed, idx, 23)
+    raw[:, 24:32] = r[:, None].view(np.uint8).reshape(-1, 8)  # c32 = low word, wc = high
+    raw[:, 32:34] = rnd(seed, idx, 24).astype(np.uint16)[:, None].view(np.uint8).reshape(-1, 2)
+    raw[:, 48:64] = _u128_raw(rnd(seed, idx, 25), rnd(seed, idx, 26))
+    return raw
 
 
 def _opt_span(recs, path, has, lens):
