@@ -75,6 +75,11 @@
 #ifndef SPK_NT_SCR2   // nested candidate starts screened on a second count
 #define SPK_NT_SCR2 1
 #endif
+#ifndef SPK_NT_UNIFORM  // (A/B) walk programs run wave-uniform (nt_walk_u) instead of per lane
+// (off: cm K1 5.6 -> 9.1 ms with it -- every loop runs to its longest trip
+// count and the uniform state adds to K1's SGPR spills)
+#define SPK_NT_UNIFORM 0
+#endif
 
 namespace spk {
 
@@ -2113,6 +2118,109 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
   return (uint64_t)(p + N.wp_tail - (uint32_t)pos);
 }
 
+// nt_walk with the walk program's instruction wave-uniform: every lane of the
+// wave is at the same instruction, so the fetch and the dispatch are scalar
+// (nt_walk's lanes each fetch and branch on their own instruction, and the
+// wave executes the union of the branches under exec masks). A loop runs until
+// its longest trip count ends; a lane whose count ended, or whose walk
+// failed, sits it out masked (act). The enclosing loops' counts and act flags
+// are per-lane LDS frames at the (uniform) depth. Same results and heap use as
+// nt_walk; the END instruction's arg is its loop's body start.
+template <typename Rd>
+__device__ uint64_t nt_walk_u(const NTLayout &N, const Rd &rd, uint64_t pos, uint64_t lim64,
+                              bool bounded, uint32_t maxel) {
+  const uint64_t bad = bounded ? kLenLimit : 0;
+  uint32_t *const U = nt_used();
+  uint32_t *const F = nt_frames();
+  const uint32_t w = rd.w;
+  const uint64_t wmask = w >= 8 ? ~0ull : (1ull << (8 * w)) - 1;
+  const uint32_t lim = (uint32_t)lim64;
+  const uint32_t nw = (uint32_t)__builtin_amdgcn_readfirstlane((int)N.wp_n);
+  uint32_t p = (uint32_t)pos;
+  bool act = true, failed = false;
+  uint32_t rem = 0;      // elements left in the innermost loop (this lane)
+  uint32_t pc = 0, d = 0;  // wave-uniform
+  while (pc < nw) {
+    const uint32_t ix = (uint32_t)__builtin_amdgcn_readfirstlane((int)N.wp[pc].x);
+    const uint32_t iy = (uint32_t)__builtin_amdgcn_readfirstlane((int)N.wp[pc].y);
+    const uint32_t op = ix & 7u, h = (ix >> 3) & 31u, arg = ix >> 8;
+    if (act) {
+      if (lim - p < iy) {
+        act = false;
+        failed = true;
+      } else {
+        p += iy;
+      }
+    }
+    bool pop = false;
+    if (op == WP_END) {
+      if (act) act = --rem != 0;
+      if (__ballot(act)) {
+        pc = arg;
+        continue;
+      }
+      ++pc;
+      pop = true;
+    } else {
+      const bool opt = op == WP_OPT;
+      const uint32_t cw = opt ? 1u : w;
+      uint64_t c = 0;
+      if (act) {
+        if (lim - p < cw) {
+          act = false;
+          failed = true;
+        } else {
+          c = rd.count_at32(p, wmask, opt);
+          p += cw;
+          atomicAdd(U + 64 * h, (uint32_t)c);
+        }
+      }
+      if (op == WP_ARR) {
+        if (act && (c > lim - p || c > maxel)) {  // elements take >= 1 byte
+          act = false;
+          failed = true;
+        }
+        if (d) {
+          F[64 * (2 * (d - 1))] = rem;
+          F[64 * (2 * (d - 1) + 1)] = act ? 1u : 0u;
+        }
+        ++d;
+        rem = (uint32_t)c;
+        act = act && c != 0;
+        if (__ballot(act)) {
+          ++pc;
+        } else {
+          pc = arg;  // no lane enters the loop
+          pop = true;
+        }
+      } else {
+        // SPAN: the payload must be there; OPTION: an unreadable value leaves the reader
+        if (act) {
+          if (!opt && (c > lim - p || c * arg > lim - p)) {
+            act = false;
+            failed = true;
+          } else if (!opt || (c && lim - p >= arg)) {
+            p += (uint32_t)(c * arg);
+          }
+        }
+        ++pc;
+      }
+    }
+    if (pop) {  // the enclosing loop's frame back
+      --d;
+      if (d) {
+        rem = F[64 * (2 * (d - 1))];
+        act = F[64 * (2 * (d - 1) + 1)] != 0 && !failed;
+      } else {
+        act = !failed;
+      }
+    }
+    if (!__ballot(!failed)) break;
+  }
+  if (failed || lim - p < N.wp_tail) return bad;
+  return (uint64_t)(p + N.wp_tail - (uint32_t)pos);
+}
+
 // wlen_rd for NS = -2: the record's wire length (0: the path fails here) and
 // its heap use per heap; reach > 0 bounds a speculative walk (past it: longer
 // than a plausible record, kPlaus + 1)
@@ -2128,7 +2236,8 @@ __device__ uint64_t nt_len(const Rd &rd, uint64_t len, uint64_t pos, uint64_t *c
   const uint64_t lim = reach && reach < len - pos ? pos + reach : len;
   uint64_t p = pos;
   if constexpr (SIMPLE) {
-    const uint64_t l = nt_walk(N, rd, pos, lim, lim < len, maxel);
+    const uint64_t l = SPK_NT_UNIFORM ? nt_walk_u(N, rd, pos, lim, lim < len, maxel)
+                                      : nt_walk(N, rd, pos, lim, lim < len, maxel);
     if (l == kLenLimit) return kLenLimit;
     p += l;
   } else {
@@ -4309,10 +4418,11 @@ static NTLayout make_ntlayout(const NLayout &N, void *const *heaps) {
       break;
     }
     if (fix >= (1ull << 32)) ok = false;
+    if (x == WP_END) x |= (open[d] + 1) << 8;  // (nt_walk_u) the loop's body start
     t.wp[n] = make_uint2(x, (uint32_t)fix);
     fix = 0;
     ++n;
-    if (x == WP_END) t.wp[open[d]].x |= n << 8;  // the loop's exit
+    if ((x & 7u) == WP_END) t.wp[open[d]].x |= n << 8;  // the loop's exit
   }
   t.wp_n = ok && !d && fix < (1ull << 32) ? n : 0;
   t.wp_tail = (uint32_t)fix;
