@@ -75,6 +75,11 @@
 #ifndef SPK_NT_SCR2   // nested candidate starts screened on a second count
 #define SPK_NT_SCR2 1
 #endif
+#ifndef SPK_WPAD  // (A/B) LDS windows padded per 256-B row (bank-conflict-free chunk reads)
+// (off: C3 / C4 / cv / cm K1 0.244 / 0.364 / 1.93 / 5.61 -> 0.269 / 0.390 /
+// 2.07 / 6.63 ms with it: the conflicts cost less than the address arithmetic)
+#define SPK_WPAD 0
+#endif
 #ifndef SPK_NT_UNIFORM  // (A/B) walk programs run wave-uniform (nt_walk_u) instead of per lane
 // (off: cm K1 5.6 -> 9.1 ms with it -- every loop runs to its longest trip
 // count and the uniform state adds to K1's SGPR spills)
@@ -1478,6 +1483,27 @@ struct VecBufs {
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
+// LDS window layout. Lane l's chunk is the window's 256-B row l, and the
+// walkers' lanes read at similar offsets of their own rows (the candidate
+// screen at the same offset in every row): with rows 64 dwords apart every
+// such read of a 32-lane half lands on one bank (a 32-way conflict). With
+// SPK_WPAD a row takes kRowDw = 69 dwords (69 is odd: the 32 rows of a half
+// fall on 32 banks) and its last 5 dwords repeat the next row's first 5, so
+// any read of up to 5 consecutive dwords starting inside a row stays in that
+// row's slot. Positions are window-relative bytes o: dword (o >> 8) * kRowDw +
+// ((o >> 2) & 63), byte (o >> 8) * 4 * kRowDw + (o & 255).
+constexpr uint32_t kRowDw = SPK_WPAD ? 69u : 64u;
+__device__ __forceinline__ uint32_t win_dw(uint32_t o) {
+  return SPK_WPAD ? (o >> 8) * kRowDw + ((o >> 2) & 63u) : o >> 2;
+}
+__device__ __forceinline__ uint32_t win_b(uint32_t o) {
+  return SPK_WPAD ? (o >> 8) * (4u * kRowDw) + (o & 255u) : o;
+}
+// 16-B slots of LDS a window of nv staged 16-B slots takes (+ the read-past slack)
+__host__ __device__ constexpr uint32_t win_slots(uint32_t nv) {
+  return SPK_WPAD ? (((nv + 15) / 16) * kRowDw + 3) / 4 + 2 : nv + 1;
+}
+
 // Count-field reader over a chunk's LDS window: bytes [cs, wend) of the wire
 // are staged in LDS; reads past the window go to global memory.
 struct WinReader {
@@ -1487,8 +1513,8 @@ struct WinReader {
   uint32_t w;
   __device__ __forceinline__ uint64_t operator()(uint64_t x) const {
     if (x + w <= wend) {
-      if (w == 1) return reinterpret_cast<const lds_u8 *>(d)[(uint32_t)(x - cs)];  // ds_read_u8
-      const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = o >> 2;
+      if (w == 1) return reinterpret_cast<const lds_u8 *>(d)[win_b((uint32_t)(x - cs))];  // ds_read_u8
+      const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = win_dw(o);
       const uint32_t d0 = d[i], d1 = d[i + 1];
       const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
       if (w == 1) return lo & 0xFFu;
@@ -1499,7 +1525,7 @@ struct WinReader {
     return wire_le(wire, x, w);
   }
   __device__ __forceinline__ uint32_t byte(uint64_t x) const {
-    if (x < wend) return reinterpret_cast<const lds_u8 *>(d)[(uint32_t)(x - cs)];
+    if (x < wend) return reinterpret_cast<const lds_u8 *>(d)[win_b((uint32_t)(x - cs))];
     return wire[x];
   }
   // LEB128 at x (message end len), as vi_read: eight bytes from the window at
@@ -1507,7 +1533,7 @@ struct WinReader {
   // gathers the 7-bit groups -- and the byte loop for longer / edge varints
   __device__ __forceinline__ uint32_t vread(uint64_t x, uint64_t len, uint64_t *v) const {
     if (x + 12 <= wend) {
-      const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = o >> 2;
+      const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = win_dw(o);
       const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2];
       const uint64_t b = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
                          ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
@@ -1530,7 +1556,7 @@ struct WinReader {
   // kNT32Wire bytes, so x + 12 cannot wrap)
   __device__ __forceinline__ uint64_t count_at32(uint32_t x, uint64_t wmask, bool opt) const {
     if (x + 12u <= (uint32_t)wend) {
-      const uint32_t o = x - (uint32_t)cs, sh = o & 3, i = o >> 2;
+      const uint32_t o = x - (uint32_t)cs, sh = o & 3, i = win_dw(o);
       const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2];
       const uint64_t b = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
                          ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
@@ -1543,7 +1569,7 @@ struct WinReader {
   // bytes from three dwords), past it the wire
   __device__ __forceinline__ uint64_t count_at(uint64_t x, uint64_t wmask, bool opt) const {
     if (x + 12 <= wend) {
-      const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = o >> 2;
+      const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = win_dw(o);
       const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2];
       const uint64_t b = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
                          ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
@@ -1553,11 +1579,11 @@ struct WinReader {
   }
   // 4 / 16 bytes at x (x + n <= wend: inside the staged window)
   __device__ __forceinline__ uint32_t ld4(uint64_t x) const {
-    const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = o >> 2;
+    const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = win_dw(o);
     return __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
   }
   __device__ __forceinline__ v4u_t ld16(uint64_t x) const {
-    const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = o >> 2;
+    const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = win_dw(o);
     const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2], d3 = d[i + 3], d4 = d[i + 4];
     return v4u_t{__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
                  __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh)};
@@ -2648,6 +2674,30 @@ __device__ __forceinline__ bool screen_one(const WalkProg &P, const Rd &rd, uint
 }
 
 
+// staged 16-B slot v of a window (win_dw layout): its 4 dwords, and slots 0 / 1
+// of a row also into the previous row's 5 repeated dwords
+__device__ __forceinline__ void win_put(v4u_t *win, uint32_t v, const v4u_t &x) {
+  if constexpr (!SPK_WPAD) {
+    win[v] = x;
+  } else {
+    lds_u32 *d = (lds_u32 *)win;
+    const uint32_t r = v >> 4, k = v & 15u, b = r * kRowDw + 4u * k;
+    d[b] = x.x;
+    d[b + 1] = x.y;
+    d[b + 2] = x.z;
+    d[b + 3] = x.w;
+    if (r && k < 2) {
+      const uint32_t e = b - kRowDw + 64u;  // the previous row's repeat of dwords 4k..
+      d[e] = x.x;
+      if (k == 0) {
+        d[e + 1] = x.y;
+        d[e + 2] = x.z;
+        d[e + 3] = x.w;
+      }
+    }
+  }
+}
+
 // Stage tile t's bytes (+ extension) in this wave's LDS window; reader over it.
 struct TileView {
   WinReader rd;
@@ -2671,7 +2721,7 @@ __device__ __forceinline__ TileView stage_win(v4u_t *win, const uint8_t *wire, u
 #pragma unroll
     for (uint32_t k = 0; k < kPer; ++k) {
       const uint32_t v = lane + 64 * k;
-      if (NV % 64 == 0 || v < NV) win[v] = val[k];
+      if (NV % 64 == 0 || v < NV) win_put(win, v, val[k]);
     }
   } else
   for (uint32_t v = lane; v < NV; v += 64) {
@@ -2684,7 +2734,7 @@ __device__ __forceinline__ TileView stage_win(v4u_t *win, const uint8_t *wire, u
       for (uint64_t q = g; q < len; ++q) tt[(q - g) >> 2] |= (uint32_t)wire[q] << (8 * ((q - g) & 3));
       val = v4u_t{tt[0], tt[1], tt[2], tt[3]};
     }
-    win[v] = val;
+    win_put(win, v, val);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -2794,7 +2844,7 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
             m |= (ok ? 1u : 0u) << kk;
           }
         } else if (b0 + 20 <= wend) {
-          const uint32_t o0 = (uint32_t)(b0 - ts), i = o0 >> 2, sh = o0 & 3;
+          const uint32_t o0 = (uint32_t)(b0 - ts), i = win_dw(o0), sh = o0 & 3;
           const lds_u32 *d = rd.d;
           const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2], d3 = d[i + 3], d4 = d[i + 4];
           const uint32_t wd[4] = {__builtin_amdgcn_alignbyte(d1, d0, sh),
@@ -3109,7 +3159,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
                                                                 const uint8_t *__restrict__ wire,
                                                                 const uint8_t *__restrict__ ws,
                                                                 TileBufs TB, uint32_t dbg) {
-  __shared__ v4u_t win_s[kDecWaves][kTileVec + 1];
+  __shared__ v4u_t win_s[kDecWaves][win_slots(kTileVec)];
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t t = (uint64_t)blockIdx.x * kDecWaves + wv;
@@ -3148,7 +3198,7 @@ __global__ __launch_bounds__(64) void vec_hdr_sample(DecArgs a, WalkProg P,
                                                      const uint8_t *__restrict__ wire,
                                                      uint8_t *__restrict__ ws,
                                                      spk_dresult_t *res) {
-  __shared__ v4u_t win[kSampVec + 1];
+  __shared__ v4u_t win[win_slots(kSampVec)];
   if (threadIdx.x == 0) vec_hdr_body(a, wire, ws, res, 0u, (uint64_t)0);
   __syncthreads();
   VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
@@ -3278,7 +3328,7 @@ __global__ __launch_bounds__(64) void vec_tile_repair(DecArgs a, WalkProg P,
                                                       const uint8_t *__restrict__ wire,
                                                       uint8_t *__restrict__ ws, TileBufs TB,
                                                       uint32_t pass) {
-  __shared__ v4u_t win_s[1][kTileVec + 1];
+  __shared__ v4u_t win_s[1][win_slots(kTileVec)];
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
   const uint32_t lane = threadIdx.x;
@@ -3346,7 +3396,7 @@ __global__ __launch_bounds__(64) void vec_tile_seqfix(DecArgs a, WalkProg P,
                                                       const uint8_t *__restrict__ wire,
                                                       uint8_t *__restrict__ ws, TileBufs TB,
                                                       uint32_t last_pass) {
-  __shared__ v4u_t win_s[1][kTileVec + 1];
+  __shared__ v4u_t win_s[1][win_slots(kTileVec)];
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
   const uint32_t lane = threadIdx.x;
@@ -3539,7 +3589,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
                                                                 TileBufs TB,
                                                                 uint8_t *__restrict__ recs,
                                                                 BigQ bq, uint32_t dbg) {
-  __shared__ v4u_t win_s[kDecWaves][kEmitVec + 1];
+  __shared__ v4u_t win_s[kDecWaves][win_slots(kEmitVec)];
   __shared__ uint16_t tab_s[kDecWaves][kEmitTab];
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
@@ -3961,7 +4011,7 @@ __global__ __launch_bounds__(64 * kFW) void vec_tile_fused(DecArgs a, WalkProg P
                                                           uint8_t *__restrict__ ws, FusedBufs FB,
                                                           uint8_t *__restrict__ recs, BigQ bq,
                                                           uint32_t dbg) {
-  __shared__ v4u_t win_s[kFW][kTileVec + 1];
+  __shared__ v4u_t win_s[kFW][win_slots(kTileVec)];
   __shared__ uint16_t tab_s[kFW][kFTab];
   __shared__ uint64_t sh_y[kFW], sh_c[kFW], sh_s[kFW][kVS];
   __shared__ uint64_t sh_x0, sh_e, sh_pc, sh_ps[kVS];
