@@ -581,13 +581,19 @@ def measure(wl, args, torch, dist, world, dev, steps, warmup, settle):
     return dt, phase_ms, kernels
 
 
+def _kbase(name):
+    """A traced kernel's base name: "vec_tile_emit<NS>" and "(nest_emit<D, LU>)"
+    (a template launched through SPK_LAUNCH in parentheses) -> the plain name."""
+    return name.strip("() ").split("<")[0]
+
+
 def roofline(wl, kernels, pmc, pmc_src):
     """Roofline of the dominant byte-moving kernel: algorithmic bytes per
     launch / average launch duration (HIP events), against the 8 TB/s HBM
     peak; `traffic` = PMC HBM bytes per launch of the same kernel."""
     kb = wl.kernel_bytes()
     for name, k in kernels.items():
-        base = name.split("<")[0]
+        base = _kbase(name)
         if base in kb:
             k["bytes_per_step"] = kb[base]
             k["achieved_gbs"] = round(kb[base] / (k["ms_per_step"] * 1e-3) / 1e9, 1)
@@ -602,7 +608,7 @@ def roofline(wl, kernels, pmc, pmc_src):
     traffic = None
     for kname, v in pmc.items():
         if kname.split("(")[0].split("<")[0].replace("void ", "").replace("spk::", "") == \
-                dom.split("<")[0]:
+                _kbase(dom):
             traffic = v.get("hbm_bytes_per_launch")
     return {"bound": "hbm", "kernel": dom, "launches_per_step": launches,
             "bytes_per_launch": int(bpl), "ms_per_launch": k["ms_per_launch"],
@@ -981,7 +987,7 @@ def compact_line(line, detail_path):
             cb = e.get("cpu_baseline") or {}
             d = {"ms": e.get("ms_per_step"), "gib_s": e.get("value"),
                  "mrec_s": e.get("mrec_per_s", e.get("mmsg_per_s")),
-                 "kernel": (rf.get("kernel") or "").split("(")[0][:28],
+                 "kernel": (rf.get("kernel") or "").strip("() ").split("(")[0][:28],
                  "frac": rf.get("frac"), "traffic_ratio": rf.get("traffic_ratio"),
                  "cpu_gib_s": cb.get("value")}
             h = compact_host(e)

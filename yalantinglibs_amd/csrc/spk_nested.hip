@@ -582,12 +582,15 @@ constexpr int32_t kNLimit = 0x7FFF0001;
 // a value that does not fit leaves the reader in place (a trivially
 // serializable one zero-filled) (unpacker.hpp:1251-1277). `top`: the whole
 // top-level record, its fast-varint group first.
-template <typename Rd>
+// D: the layout's depth class (n_dclass); the stack's top frame in registers
+// and, for D <= 2, the one below it too (a runtime-indexed frame array lives in
+// scratch memory)
+template <int D = (int)SPK_MAX_DEPTH, typename Rd>
 __device__ int32_t n_read(const NLayout &N, const Rd &wire, uint64_t &pos, uint64_t end,
                           uint32_t w, uint8_t *rec, uint8_t *const *heaps, uint64_t *used,
                           const uint64_t *heap_cap, uint32_t *ovf, uint32_t i0, uint32_t i1,
                           bool top, bool bounded = false) {
-  NFrame st[SPK_MAX_DEPTH];
+  NStk<D> st;
   uint32_t d = 0, i = i0, iend = i1;
   uint8_t *r = rec;
   int32_t ec = SPK_ERRC_OK;
@@ -606,13 +609,13 @@ __device__ int32_t n_read(const NLayout &N, const Rd &wire, uint64_t &pos, uint6
       for (;;) {
         if (r) zero_rest(N, r, i, iend);
         if (!d) break;
-        NFrame &f = st[d - 1];
+        const NFrame &f = st.top;
         const spk_op &fo = N.ops[f.aop];
         if (fo.kind == SPK_OP_VARIANT || fo.kind == SPK_OP_OPTGROUP) {
           i = f.ret;
           iend = f.pend;
           r = const_cast<uint8_t *>(f.prec);
-          --d;
+          st.pop(--d);
           dropped = true;
           break;
         }
@@ -622,7 +625,7 @@ __device__ int32_t n_read(const NLayout &N, const Rd &wire, uint64_t &pos, uint6
         i = f.ret;  // the rest of the enclosing level
         iend = f.pend;
         r = const_cast<uint8_t *>(f.prec);
-        --d;
+        st.pop(--d);
       }
       if (!dropped) return ec;
       ec = SPK_ERRC_OK;
@@ -630,7 +633,7 @@ __device__ int32_t n_read(const NLayout &N, const Rd &wire, uint64_t &pos, uint6
     }
     if (i >= iend) {
       if (!d) break;
-      NFrame &f = st[d - 1];
+      NFrame &f = st.top;
       if (++f.j < f.cnt) {
         r = f.el ? const_cast<uint8_t *>(f.el) + f.j * N.ops[f.aop].size : nullptr;
         i = f.first;
@@ -639,7 +642,7 @@ __device__ int32_t n_read(const NLayout &N, const Rd &wire, uint64_t &pos, uint6
       i = f.ret;
       iend = f.pend;
       r = const_cast<uint8_t *>(f.prec);
-      --d;
+      st.pop(--d);
       continue;
     }
     const spk_op op = N.ops[i];
@@ -710,8 +713,8 @@ __device__ int32_t n_read(const NLayout &N, const Rd &wire, uint64_t &pos, uint6
         continue;
       }
       const uint32_t a0 = n_alt_start(N, i, (uint32_t)a);
-      st[d] = NFrame{i, iend, 0, 1, r, r, a0, (uint32_t)N.end[i] + 1};
-      ++d;
+      if (d == (uint32_t)D) { ec = SPK_ERRC_INVALID_BUFFER; continue; }  // (n_dclass bounds it)
+      st.push(d++, NFrame{i, iend, 0, 1, r, r, a0, (uint32_t)N.end[i] + 1});
       iend = n_alt_end(N, a0);
       i = a0;
       continue;
@@ -773,11 +776,10 @@ __device__ int32_t n_read(const NLayout &N, const Rd &wire, uint64_t &pos, uint6
         i = N.end[i] + 1;
         continue;
       }
-      if (d == SPK_MAX_DEPTH) { ec = SPK_ERRC_INVALID_BUFFER; continue; }  // (layout_check bounds it)
-      st[d] = NFrame{i, iend, 0, cnt, put ? heaps[hk] + off * op.size : nullptr, r, i + 1,
-                     (uint32_t)N.end[i] + 1};
+      if (d == (uint32_t)D) { ec = SPK_ERRC_INVALID_BUFFER; continue; }  // (layout_check bounds it)
+      st.push(d++, NFrame{i, iend, 0, cnt, put ? heaps[hk] + off * op.size : nullptr, r, i + 1,
+                          (uint32_t)N.end[i] + 1});
       r = put ? heaps[hk] + off * op.size : nullptr;
-      ++d;
       iend = N.end[i];
       ++i;
       continue;
@@ -825,7 +827,7 @@ __device__ int32_t n_read(const NLayout &N, const Rd &wire, uint64_t &pos, uint6
 // no_buffer_space (*ec, returns 1); the value's errc is dropped (a trivially
 // serializable one that does not fit reads as present and zero; a group stops
 // where its decode stopped). The main pass left every member absent.
-template <typename Rd>
+template <int D = (int)SPK_MAX_DEPTH, typename Rd>
 __device__ int n_read_compat(const NLayout &N, const Rd &wire, uint64_t &pos, uint64_t end,
                              uint64_t data_end, uint32_t rk, uint32_t w, uint8_t *rec,
                              uint8_t *const *heaps, uint64_t *used, const uint64_t *heap_cap,
@@ -841,7 +843,7 @@ __device__ int n_read_compat(const NLayout &N, const Rd &wire, uint64_t &pos, ui
     if (!wire[pos++]) continue;
     if (op.kind == SPK_OP_CGROUP) {
       if (rec) *reinterpret_cast<uint32_t *>(rec + op.rec_off) = 1;
-      (void)n_read(N, wire, pos, end, w, rec, heaps, used, heap_cap, ovf, i + 1, N.end[i], false);
+      (void)n_read<D>(N, wire, pos, end, w, rec, heaps, used, heap_cap, ovf, i + 1, N.end[i], false);
       continue;
     }
     const bool fits = end - pos >= op.size;
@@ -1981,6 +1983,27 @@ __device__ __forceinline__ NRd n_stage_msgs(v4u_t *win, const NDec &a, const uin
   return rd;
 }
 
+// the lane's heap-use counters: LDS ([lane][heap], dynamic shared memory of
+// 256 x nh words) when the layout has at most kNUseLds heaps, else a local
+// array (runtime-indexed: scratch memory)
+constexpr uint32_t kNUseLds = 16;
+template <bool LU>
+struct NUse {
+  uint64_t loc[LU ? 1 : SPK_MAX_SPANS];
+  __device__ __forceinline__ uint64_t *ptr(uint32_t nh) {
+    if constexpr (LU) {
+      extern __shared__ uint64_t nuse_s[];
+      return nuse_s + threadIdx.x * (nh ? nh : 1u);
+    } else {
+      return loc;
+    }
+  }
+};
+static inline size_t n_use_lds(const NLayout &N) {
+  return N.n_heaps <= kNUseLds ? (size_t)256 * 8 * (N.n_heaps ? N.n_heaps : 1) : 0;
+}
+
+template <int D, bool LU>
 __global__ __launch_bounds__(256) void nest_msg_count(NDec a, const uint8_t *__restrict__ wire_g,
                                                       const uint64_t *__restrict__ offs,
                                                       uint64_t *__restrict__ U,
@@ -1992,7 +2015,9 @@ __global__ __launch_bounds__(256) void nest_msg_count(NDec a, const uint8_t *__r
                                 threadIdx.x & 63);
   if (i >= a.n_msgs) return;
   const NLayout &N = a.N;
-  uint64_t used[SPK_MAX_SPANS] = {};
+  NUse<LU> us;
+  uint64_t *const used = us.ptr(N.n_heaps);
+  for (uint32_t k = 0; k < N.n_heaps; ++k) used[k] = 0;
   const uint64_t b = offs[i], e = a.ends ? a.ends[i] : offs[i + 1];
   int32_t errc = SPK_ERRC_OK;
   uint64_t consumed = 0;
@@ -2006,10 +2031,10 @@ __global__ __launch_bounds__(256) void nest_msg_count(NDec a, const uint8_t *__r
     if (!errc) {
       uint64_t pos = m0 + p0;
       uint32_t ovf = 0;
-      errc = n_read(N, wire, pos, e, w, nullptr, nullptr, used, a.heap_cap, &ovf, 0, N.n_ops,
-                    true);
+      errc = n_read<D>(N, wire, pos, e, w, nullptr, nullptr, used, a.heap_cap, &ovf, 0, N.n_ops,
+                       true);
       for (uint32_t rk = 0; !errc && rk < N.n_ranks; ++rk)
-        if (n_read_compat(N, wire, pos, e, m0 + dl, rk, w, nullptr, nullptr, used, a.heap_cap,
+        if (n_read_compat<D>(N, wire, pos, e, m0 + dl, rk, w, nullptr, nullptr, used, a.heap_cap,
                           &ovf, &errc))
           break;
       consumed = pos - m0 > dl ? pos - m0 : dl;  // consume_len (struct_pack.hpp:343-357)
@@ -2023,6 +2048,7 @@ __global__ __launch_bounds__(256) void nest_msg_count(NDec a, const uint8_t *__r
 
 // write pass (MESSAGES, and VECTOR with compatible members): record i from
 // its start with heap bases B[k][i]
+template <int D, bool LU>
 __global__ __launch_bounds__(256) void nest_emit(NDec a, const uint8_t *__restrict__ wire,
                                                  const uint64_t *__restrict__ offs,
                                                  const uint64_t *__restrict__ starts,
@@ -2071,18 +2097,19 @@ __global__ __launch_bounds__(256) void nest_emit(NDec a, const uint8_t *__restri
     pos = m0 + p0;
     data_end = m0 + dl;
   }
-  uint64_t used[SPK_MAX_SPANS];
+  NUse<LU> us;
+  uint64_t *const used = us.ptr(N.n_heaps);
   for (uint32_t k = 0; k < N.n_heaps; ++k) used[k] = B[(uint64_t)k * nrows + i];
   uint32_t ovf = 0;
   uint8_t *rec = recs + i * N.stride;
-  n_read(N, rdm, pos, end, w, rec, a.heaps, used, a.heap_cap, &ovf, 0, N.n_ops, true);
+  n_read<D>(N, rdm, pos, end, w, rec, a.heaps, used, a.heap_cap, &ovf, 0, N.n_ops, true);
   int32_t cec = 0;
   for (uint32_t rk = 0; rk < N.n_ranks; ++rk) {
     if (mode == SPK_MODE_VECTOR) {  // this record's group of version rk (walker)
       pos = cpos[(uint64_t)rk * a.rec_cap + i];
       if (pos == ~0ull) break;
     }
-    if (n_read_compat(N, rdm, pos, end, data_end, rk, w, rec, a.heaps, used, a.heap_cap, &ovf,
+    if (n_read_compat<D>(N, rdm, pos, end, data_end, rk, w, rec, a.heaps, used, a.heap_cap, &ovf,
                       &cec))
       break;
   }
@@ -2215,22 +2242,40 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
                starts, cpos);
     if ((er = nscan(U, rows, a.N.n_heaps, part, s)) != hipSuccess) return er;
     if (rows)
-      SPK_LAUNCH(nest_emit, dim3(nblocks(rows, 256)), dim3(256), 0, s, a, (const uint8_t *)d_wire,
-                 d_msg_offsets, (const uint64_t *)starts, (const uint64_t *)U, rows,
-                 (const int32_t *)ec, ws, (const uint64_t *)cpos, (uint8_t *)d_recs, mode,
-                 (int32_t *)nullptr);
+      SPK_LAUNCH((nest_emit<SPK_MAX_DEPTH, false>), dim3(nblocks(rows, 256)), dim3(256), 0, s, a,
+                 (const uint8_t *)d_wire, d_msg_offsets, (const uint64_t *)starts,
+                 (const uint64_t *)U, rows, (const int32_t *)ec, ws, (const uint64_t *)cpos,
+                 (uint8_t *)d_recs, mode, (int32_t *)nullptr);
     SPK_LAUNCH(nest_finish, dim3(1), dim3(64), 0, s, a, (const uint64_t *)part, nb,
                (const int32_t *)ec, ws, mode, d_res, (int32_t *)nullptr);
     return hipGetLastError();
   }
   SPK_LAUNCH(nest_ctl_init, dim3(1), dim3(1), 0, s, ws, (const uint32_t *)nullptr);
   if (!n_msgs) return hipGetLastError();
-  SPK_LAUNCH(nest_msg_count, dim3(nblocks(n_msgs, 256)), dim3(256), 0, s, a,
-             (const uint8_t *)d_wire, d_msg_offsets, U, ec, cons);
+  // (the layout's depth class and heap-use placement select the kernels)
+  const size_t ul = n_use_lds(a.N);
+  const unsigned gm = nblocks(n_msgs, 256), ge = nblocks(rows, 256);
+#define SPK_NMSG_LAUNCH(LU)                                                                    \
+  NEST_D(n_dclass(a.N),                                                                        \
+         SPK_LAUNCH((nest_msg_count<D, LU>), dim3(gm), dim3(256), ul, s, a,                     \
+                    (const uint8_t *)d_wire, d_msg_offsets, U, ec, cons))
+#define SPK_NEMIT_LAUNCH(LU)                                                                   \
+  NEST_D(n_dclass(a.N),                                                                        \
+         SPK_LAUNCH((nest_emit<D, LU>), dim3(ge), dim3(256), ul, s, a, (const uint8_t *)d_wire, \
+                    d_msg_offsets, (const uint64_t *)starts, (const uint64_t *)U, rows,         \
+                    (const int32_t *)ec, ws, (const uint64_t *)cpos, (uint8_t *)d_recs, mode,   \
+                    d_errc))
+  if (ul)
+    SPK_NMSG_LAUNCH(true);
+  else
+    SPK_NMSG_LAUNCH(false);
   if ((er = nscan(U, rows, a.N.n_heaps, part, s)) != hipSuccess) return er;
-  SPK_LAUNCH(nest_emit, dim3(nblocks(rows, 256)), dim3(256), 0, s, a, (const uint8_t *)d_wire,
-             d_msg_offsets, (const uint64_t *)starts, (const uint64_t *)U, rows,
-             (const int32_t *)ec, ws, (const uint64_t *)cpos, (uint8_t *)d_recs, mode, d_errc);
+  if (ul)
+    SPK_NEMIT_LAUNCH(true);
+  else
+    SPK_NEMIT_LAUNCH(false);
+#undef SPK_NMSG_LAUNCH
+#undef SPK_NEMIT_LAUNCH
   SPK_LAUNCH(nest_finish, dim3(1), dim3(64), 0, s, a, (const uint64_t *)part, nb,
              (const int32_t *)ec, ws, mode, d_res, d_errc);
   uint64_t *cpart = reinterpret_cast<uint64_t *>(ws + f.part) + (nb + 1) * a.N.n_heaps;
