@@ -76,25 +76,31 @@ __host__ __device__ inline HdrShape hdr_shape(uint32_t flags, uint32_t lit_len,
 // and is followed by the message's total length in 2/4/8 bytes
 // (calculate_size.hpp:457-470; packer.hpp:111-130). `body` = the bytes after
 // the header. Returns the header length; writes it into dst when set.
-__host__ __device__ inline uint32_t compat_hdr(uint8_t *dst, const spk_msgfmt &f, uint32_t w,
-                                               uint64_t body) {
+// (put(p, byte): header byte p; compat_hdr / write_hdr below write to memory)
+template <typename Put>
+__host__ __device__ inline uint32_t compat_hdr_with(Put &&put, const spk_msgfmt &f, uint32_t w,
+                                                    uint64_t body, bool emit) {
   const HdrShape h = hdr_shape(f.flags, f.literal_len, w);
   const uint32_t base = h.len + (h.has_meta ? 0u : 1u);
   const uint64_t l = base + body;
   const uint32_t lw = l + 2 < (1ull << 16) ? 2u : l + 4 < (1ull << 32) ? 4u : 8u;
-  if (dst) {
+  if (emit) {
     uint32_t p = 0;
     const uint32_t head = f.code | 1u;
-    for (uint32_t b = 0; b < 4; ++b) dst[p++] = (uint8_t)(head >> (8 * b));
-    dst[p++] = (uint8_t)(h.meta | (lw == 2 ? 1u : lw == 4 ? 2u : 3u));
+    for (uint32_t b = 0; b < 4; ++b) put(p++, (uint8_t)(head >> (8 * b)));
+    put(p++, (uint8_t)(h.meta | (lw == 2 ? 1u : lw == 4 ? 2u : 3u)));
     const uint64_t total = l + lw;
-    for (uint32_t b = 0; b < lw; ++b) dst[p++] = (uint8_t)(total >> (8 * b));
+    for (uint32_t b = 0; b < lw; ++b) put(p++, (uint8_t)(total >> (8 * b)));
     if (h.lit) {
-      for (uint32_t i = 0; i < f.literal_len; ++i) dst[p++] = f.literal[i];
-      dst[p++] = 0;
+      for (uint32_t i = 0; i < f.literal_len; ++i) put(p++, f.literal[i]);
+      put(p++, (uint8_t)0);
     }
   }
   return base + lw;
+}
+__host__ __device__ inline uint32_t compat_hdr(uint8_t *dst, const spk_msgfmt &f, uint32_t w,
+                                               uint64_t body) {
+  return compat_hdr_with([dst](uint32_t p, uint8_t b) { dst[p] = b; }, f, w, body, dst != nullptr);
 }
 
 __host__ __device__ inline bool op_has_heap(uint32_t kind) {
@@ -103,24 +109,28 @@ __host__ __device__ inline bool op_has_heap(uint32_t kind) {
          kind == SPK_OP_COMPAT;
 }
 
-// Writes the header bytes (at most 4+1+SPK_MAX_LITERAL+1) into dst.
-__host__ __device__ inline uint32_t write_hdr(uint8_t *dst, const spk_msgfmt &f,
-                                              uint32_t w) {
+// The header bytes (at most 4+1+SPK_MAX_LITERAL+1) through put(p, byte).
+template <typename Put>
+__host__ __device__ inline uint32_t write_hdr_with(Put &&put, const spk_msgfmt &f, uint32_t w) {
   HdrShape h = hdr_shape(f.flags, f.literal_len, w);
   uint32_t p = 0;
   if (h.head) {
     uint32_t head = (f.code & ~1u) | (h.has_meta ? 1u : 0u);
-    dst[p++] = (uint8_t)head;
-    dst[p++] = (uint8_t)(head >> 8);
-    dst[p++] = (uint8_t)(head >> 16);
-    dst[p++] = (uint8_t)(head >> 24);
+    put(p++, (uint8_t)head);
+    put(p++, (uint8_t)(head >> 8));
+    put(p++, (uint8_t)(head >> 16));
+    put(p++, (uint8_t)(head >> 24));
   }
-  if (h.has_meta) dst[p++] = (uint8_t)h.meta;
+  if (h.has_meta) put(p++, (uint8_t)h.meta);
   if (h.lit) {
-    for (uint32_t i = 0; i < f.literal_len; ++i) dst[p++] = f.literal[i];
-    dst[p++] = 0;
+    for (uint32_t i = 0; i < f.literal_len; ++i) put(p++, f.literal[i]);
+    put(p++, (uint8_t)0);
   }
   return p;
+}
+// Writes the header bytes into dst.
+__host__ __device__ inline uint32_t write_hdr(uint8_t *dst, const spk_msgfmt &f, uint32_t w) {
+  return write_hdr_with([dst](uint32_t p, uint8_t b) { dst[p] = b; }, f, w);
 }
 
 // Workspace layout (device): fixed region first, then per-launch scratch.

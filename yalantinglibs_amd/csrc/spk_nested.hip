@@ -1353,15 +1353,20 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
     const uint64_t tot0 = e.n ? part[nb] : 0;
     uint64_t totc = 0;
     for (uint32_t rk = 0; rk < N.n_ranks; ++rk) totc += e.n ? part[(2 + rk) * (nb + 1) + nb] : 0;
-    uint8_t hb[4 + 1 + 8 + SPK_MAX_LITERAL + 1];
+    // (the header straight into the output by thread 0: a local byte array
+    // indexed at run time would live in scratch memory for every lane)
     if (with_header)
-      hl = N.n_ranks ? compat_hdr(hb, e.fmt, w, w + tot0 + totc) : write_hdr(hb, e.fmt, w);
+      hl = N.n_ranks ? compat_hdr(nullptr, e.fmt, w, w + tot0 + totc)
+                     : hdr_shape(e.fmt.flags, e.fmt.literal_len, w).len;
     // the whole message must fit, or nothing is written (spk_encode's
     // contract; the caller reads the plan's total_bytes)
     if ((with_header ? hl + w : 0) + tot0 + totc > out_cap) return;
     if (with_header) {
       if (i == 0) {
-        for (uint32_t b = 0; b < hl; ++b) out[b] = hb[b];
+        if (N.n_ranks)
+          compat_hdr(out, e.fmt, w, w + tot0 + totc);
+        else
+          write_hdr(out, e.fmt, w);
         for (uint32_t b = 0; b < w; ++b) out[hl + b] = (uint8_t)(e.n >> (8 * b));
       }
       hl += w;
@@ -1388,10 +1393,8 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
   uint8_t *p = out + off[i];
   if (msg_offsets) msg_offsets[i] = off[i];
   uint8_t *m = p + e.fpre;
-  uint8_t hb[4 + 1 + 8 + SPK_MAX_LITERAL + 1];
-  const uint32_t hl = N.n_ranks ? compat_hdr(hb, e.fmt, w, s.bytes + s.cnts * w)
-                                  : write_hdr(hb, e.fmt, w);
-  for (uint32_t b = 0; b < hl; ++b) m[b] = hb[b];
+  const uint32_t hl = N.n_ranks ? compat_hdr(m, e.fmt, w, s.bytes + s.cnts * w)
+                                  : write_hdr(m, e.fmt, w);
   const NDirect sk{m};
   uint64_t qo = n_write<D>(N, rec, e.heaps, w, sk, hl, 0, N.n_ops, true);
   for (uint32_t rk = 0; rk < N.n_ranks; ++rk) qo = n_write_compat<D>(N, rec, e.heaps, rk, w, sk, qo);
@@ -1448,6 +1451,75 @@ __global__ __launch_bounds__(256) void nest_write_win(NEnc e, const uint8_t *__r
     // flush [max(W.lo, g0), min(W.hi, out_cap)): aligned 16-B chunks, bytes
     // at the edges (the clamp: no offset, however it was planned, writes
     // past the caller's buffer)
+    const uint64_t whi = W.hi < out_cap ? W.hi : out_cap;
+    for (uint64_t c = W.lo + (uint64_t)threadIdx.x * 16; c < whi; c += 256 * 16) {
+      const uint64_t lo = c > g0 ? c : g0;
+      const uint64_t hi = c + 16 < whi ? c + 16 : whi;
+      if (lo == c && hi == c + 16)
+        *reinterpret_cast<v4u_t *>(out + c) = *reinterpret_cast<const v4u_t *>(lds + (c - W.lo));
+      else
+        for (uint64_t x = lo; x < hi; ++x) out[x] = lds[x - W.lo];
+    }
+    __syncthreads();
+  }
+}
+
+// MESSAGES encode (every message with its header and frame, at the scanned
+// offsets): as nest_write_win, the block's 256 consecutive messages are one
+// contiguous output range assembled in the LDS window and flushed with
+// aligned 16-B stores (nest_write stored each lane's bytes straight to HBM).
+// A message's width comes from its own size walk (calculate_one_size), its
+// frame length from the offsets.
+template <int D>
+__global__ __launch_bounds__(256) void nest_write_mwin(NEnc e, const uint8_t *__restrict__ recs,
+                                                       const uint64_t *__restrict__ off,
+                                                       const uint64_t *__restrict__ part,
+                                                       uint64_t nb, uint8_t *__restrict__ out,
+                                                       uint64_t *__restrict__ msg_offsets,
+                                                       uint64_t out_cap) {
+  __shared__ NLayout N;
+  __shared__ __align__(16) uint8_t lds[kNEncWin];
+  n_stage(N, e.N);
+  const uint64_t tot = e.n ? part[nb] : 0;
+  if (tot > out_cap) return;  // every message with its frame, or nothing
+  if (blockIdx.x == 0 && threadIdx.x == 0 && msg_offsets) msg_offsets[e.n] = tot;
+  const uint64_t r0 = (uint64_t)blockIdx.x * 256, i = r0 + threadIdx.x;
+  if (r0 >= e.n) return;
+  const uint64_t rend = r0 + 256 < e.n ? r0 + 256 : e.n;
+  const uint64_t g0 = off[r0], g1 = rend < e.n ? off[rend] : tot;
+  const bool live = i < e.n;
+  const uint8_t *rec = recs + i * N.stride;
+  uint64_t q0 = 0, q1 = 0, body = 0;
+  uint32_t w = 1;
+  if (live) {
+    q0 = off[i];
+    q1 = i + 1 < e.n ? off[i + 1] : tot;
+    if (msg_offsets) msg_offsets[i] = q0;
+    const NSize sz = n_size<D>(N, rec, e.heaps, 0, N.n_ops, true);
+    w = width_of(sz.maxc);
+    body = sz.bytes + sz.cnts * w;
+  }
+  const uint32_t mlen = (uint32_t)(q1 - q0 - e.fpre);
+  const uint32_t sq = live && e.fseq_off != SPK_FRAME_NONE ? seq_value(e.echo, e.fseq_base, i) : 0u;
+  for (uint64_t wlo = g0 & ~15ull; wlo < g1; wlo += kNEncWin) {
+    const NWin W{lds, wlo, wlo + kNEncWin < g1 ? wlo + kNEncWin : g1};
+    if (live && q0 < W.hi && q1 > W.lo) {
+      for (uint32_t b = 0; b < e.fpre; ++b) {  // the frame: template, seq_num, length
+        uint32_t v = e.ftmpl[b];
+        if (e.fseq_off != SPK_FRAME_NONE && b >= e.fseq_off && b < e.fseq_off + 4)
+          v = (sq >> (8 * (b - e.fseq_off))) & 0xFFu;
+        if (e.flen_off != SPK_FRAME_NONE && b >= e.flen_off && b < e.flen_off + 4)
+          v = (mlen >> (8 * (b - e.flen_off))) & 0xFFu;
+        W.byte(q0 + b, v);
+      }
+      const uint64_t m = q0 + e.fpre;
+      auto put = [&W, m](uint32_t p, uint8_t b) { W.byte(m + p, b); };
+      const uint32_t hl = N.n_ranks ? compat_hdr_with(put, e.fmt, w, body, true)
+                                    : write_hdr_with(put, e.fmt, w);
+      uint64_t qo = n_write<D>(N, rec, e.heaps, w, W, m + hl, 0, N.n_ops, true);
+      for (uint32_t rk = 0; rk < N.n_ranks; ++rk) qo = n_write_compat<D>(N, rec, e.heaps, rk, w, W, qo);
+    }
+    __syncthreads();
     const uint64_t whi = W.hi < out_cap ? W.hi : out_cap;
     for (uint64_t c = W.lo + (uint64_t)threadIdx.x * 16; c < whi; c += 256 * 16) {
       const uint64_t lo = c > g0 ? c : g0;
@@ -1573,6 +1645,13 @@ hipError_t launch_nested_encode(const spk_layout *L, int mode, uint64_t n, const
   }
   hipError_t er = nest_size_scan(e, d_recs, ws, s, &a, &part, &nb);
   if (er != hipSuccess) return er;
+  if (mode == SPK_MODE_MESSAGES && !nest_direct_write()) {
+    NEST_D(n_dclass(e.N),
+           SPK_LAUNCH(nest_write_mwin<D>, dim3(nblocks(n, 256)), dim3(256), 0, s, e,
+                      (const uint8_t *)d_recs, (const uint64_t *)a, (const uint64_t *)part, nb,
+                      (uint8_t *)d_out, d_msg_offsets, out_cap));
+    return hipGetLastError();
+  }
   NEST_D(n_dclass(e.N),
          SPK_LAUNCH(nest_write<D>, dim3(nblocks(n, 256)), dim3(256), 0, s, e,
                     (const uint8_t *)d_recs, (const uint64_t *)a, (const uint64_t *)part, nb, ws,
