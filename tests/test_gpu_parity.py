@@ -906,6 +906,54 @@ def test_nested_encode_stale_plan(case, param):
     assert encode_planned(a, exp_a) == exp_a
 
 
+@pytest.mark.parametrize("case,param", [("valreq", 10), ("monster", 20), ("vnt", 6)])
+def test_nested_messages_encode_stale_plan(case, param):
+    """The nested MESSAGES encode (LDS windows, nest_write_mwin) reuses its
+    plan's message sizes while the plan token holds: a decode or a plan of
+    another batch in between, and a framed encode after an unframed plan
+    (other sizes: the frame prefix is in the token), re-run the size pass."""
+    from yalantinglibs_amd import coro_rpc as R
+    cd = codec_for(case)
+    n = 5000
+    _, ra, ha = synth.make_batch(case, n, 0x57B1, param)
+    _, rb, hb = synth.make_batch(case, n, 0x57B2, param)
+    exp_a, offs_a, _ = H.oracle_encode(cd.L, C.SPK_MODE_MESSAGES, ra, ha)
+    exp_b, offs_b, _ = H.oracle_encode(cd.L, C.SPK_MODE_MESSAGES, rb, hb)
+    a, b = to_dev(cd, ra, ha), to_dev(cd, rb, hb)
+    guard = 4096
+
+    def encode_planned(batch, exp, frame=None, total=None):
+        total = total or len(exp)
+        buf = torch.full((total + guard,), 0xA5, dtype=torch.uint8, device="cuda")
+        offs = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+        cd.serialize_to(buf[:total], batch, C.SPK_MODE_MESSAGES, offsets=offs, planned=True,
+                        frame=frame)
+        torch.cuda.synchronize()
+        assert bool((buf[total:] == 0xA5).all())
+        return buf[:total].cpu().numpy().tobytes(), offs.cpu().numpy()
+
+    cd.plan(a, C.SPK_MODE_MESSAGES)
+    got, offs = encode_planned(a, exp_a)
+    assert got == exp_a and np.array_equal(offs, np.asarray(offs_a, np.int64))
+    cd.plan(a, C.SPK_MODE_MESSAGES)
+    res, _, _ = cd.deserialize(wire_dev(exp_b), C.SPK_MODE_MESSAGES,
+                               offsets=torch.from_numpy(np.asarray(offs_b, np.int64)).cuda(),
+                               n_msgs=n)
+    assert res.errc == 0
+    assert encode_planned(a, exp_a)[0] == exp_a
+    cd.plan(a, C.SPK_MODE_MESSAGES)
+    assert encode_planned(b, exp_b)[0] == exp_b
+    # an unframed plan, then a framed encode: each message gets its 16-B
+    # response header (prefix), the message bytes follow unchanged
+    cd.plan(a, C.SPK_MODE_MESSAGES)
+    fr = R.resp_frame(7)
+    got, offs = encode_planned(a, exp_a, frame=fr, total=len(exp_a) + n * fr.prefix_len)
+    lens = np.diff(np.asarray(offs_a, np.int64))
+    for i in (0, 1, n // 2, n - 1):
+        o = int(offs[i]) + fr.prefix_len
+        assert got[o:o + int(lens[i])] == exp_a[int(offs_a[i]):int(offs_a[i + 1])]
+
+
 @pytest.mark.parametrize("case", ["rect2", "fv"])
 def test_vector_of_zero_fast_varint_records(case):
     """A VECTOR message of all-zero fast-varint records (one bitset byte per

@@ -1147,9 +1147,11 @@ static uint64_t tok_heaps(const NEnc &e) {
     h = h * 0x100000001B3ull ^ (uint64_t)(uintptr_t)e.heaps[k];
   return h;
 }
-static uint64_t tok_layout(const spk_layout *L) {
+static uint64_t tok_layout(const spk_layout *L, int mode = SPK_MODE_VECTOR, uint32_t fpre = 0) {
+  // (MESSAGES sizes hold each message's header and frame prefix)
   return ((uint64_t)L->fmt_vector.code << 32) ^ ((uint64_t)L->n_ops << 16) ^ L->rec_stride ^
-         ((uint64_t)L->fmt_vector.flags << 48);
+         ((uint64_t)L->fmt_vector.flags << 48) ^
+         (mode == SPK_MODE_VECTOR ? 0ull : 0x9E3779B97F4A7C15ull * (1ull + fpre));
 }
 
 // XOR over the records of tok_mix(i, a[i]) into *dst (order-free, one
@@ -1161,7 +1163,14 @@ __global__ __launch_bounds__(256) void nest_tok_hash(const uint64_t *__restrict_
        i += (uint64_t)gridDim.x * blockDim.x)
     h ^= tok_mix(i, a[i]);
   for (int o = 32; o > 0; o >>= 1) h ^= __shfl_xor(h, o);
-  if ((threadIdx.x & 63) == 0 && h) atomicXor(dst, (unsigned long long)h);
+  // one atomic per block (thousands on one address serialise at its L2 channel)
+  __shared__ uint64_t wh[4];
+  if ((threadIdx.x & 63) == 0) wh[threadIdx.x >> 6] = h;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t b = wh[0] ^ wh[1] ^ wh[2] ^ wh[3];
+    if (b) atomicXor(dst, (unsigned long long)b);
+  }
 }
 
 // encode: start the check (static fields) and clear the recomputed hash
@@ -1590,14 +1599,14 @@ hipError_t launch_nested_plan(const spk_layout *L, int mode, uint64_t n, const v
   uint64_t *a, *part, nb;
   hipError_t er = nest_size_scan(e, d_recs, ws, s, &a, &part, &nb);
   if (er != hipSuccess) return er;
-  const uint32_t tok = mode == SPK_MODE_VECTOR && !e.N.n_ranks;
+  const uint32_t tok = !e.N.n_ranks;
   if (tok && n)
-    SPK_LAUNCH(nest_tok_hash, dim3(nblocks(n, 256) < 2048 ? nblocks(n, 256) : 2048), dim3(256), 0,
+    SPK_LAUNCH(nest_tok_hash, dim3(nblocks(n, 256) < 512 ? nblocks(n, 256) : 512), dim3(256), 0,
                s, (const uint64_t *)a, n,
                &reinterpret_cast<NTok *>(ws + kWsPlanTok)->hash);
   SPK_LAUNCH(nest_plan_fin, dim3(1), dim3(1), 0, s, e, (const uint64_t *)a,
              (const uint64_t *)part, nb, ws, d_plan, tok, (uint64_t)(uintptr_t)d_recs,
-             tok_heaps(e), tok_layout(L));
+             tok_heaps(e), tok_layout(L, mode));
   return hipGetLastError();
 }
 
@@ -1617,41 +1626,48 @@ hipError_t launch_nested_encode(const spk_layout *L, int mode, uint64_t n, const
   }
   uint8_t *ws = (uint8_t *)d_ws;
   uint64_t *a, *part, nb;
-  if (mode == SPK_MODE_VECTOR && !e.N.n_ranks && !fixed_w && !nest_direct_write()) {
-    // the plan that precedes this call on the workspace (spk_encode's
-    // contract, as for the flat layouts) left every record's offset in column
-    // 0, the totals in the partials and the longest container in the control
-    // block, with its token: the token is checked on the device and the size
-    // pass re-runs (each kernel returns at once otherwise) when it fails
-    NTok *t = reinterpret_cast<NTok *>(ws + kWsPlanTok);
-    const NWs f = nws_layout(e.n, e.N.n_heaps, e.N.n_ranks);
-    a = reinterpret_cast<uint64_t *>(ws + f.a);
-    part = reinterpret_cast<uint64_t *>(ws + f.part);
-    nb = (e.n + kNScanBlk - 1) / kNScanBlk;
-    SPK_LAUNCH(nest_tok_begin, dim3(1), dim3(1), 0, s, ws, n, (uint64_t)(uintptr_t)d_recs,
-               tok_heaps(e), tok_layout(L));
-    if (n)
-      SPK_LAUNCH(nest_tok_hash, dim3(nblocks(n, 256) < 2048 ? nblocks(n, 256) : 2048), dim3(256),
-                 0, s, (const uint64_t *)a, n, &t->chk);
-    SPK_LAUNCH(nest_tok_verdict, dim3(1), dim3(1), 0, s, ws, (const uint64_t *)part, nb, n);
-    uint64_t *a2, *part2, nb2;
-    hipError_t er = nest_size_scan(e, d_recs, ws, s, &a2, &part2, &nb2, &t->stale);
+  const bool vec_win = mode == SPK_MODE_VECTOR && !e.N.n_ranks && !fixed_w && !nest_direct_write();
+  const bool msg_win = mode == SPK_MODE_MESSAGES && !nest_direct_write();
+  if (vec_win || msg_win) {
+    hipError_t er;
+    if (!e.N.n_ranks) {
+      // the plan that precedes this call on the workspace (spk_encode's
+      // contract, as for the flat layouts) left every record's offset (or
+      // message size) in column 0, the totals in the partials and the longest
+      // container in the control block, with its token: the token is checked
+      // on the device and the size pass re-runs (each kernel returns at once
+      // otherwise) when it fails
+      NTok *t = reinterpret_cast<NTok *>(ws + kWsPlanTok);
+      const NWs f = nws_layout(e.n, e.N.n_heaps, e.N.n_ranks);
+      a = reinterpret_cast<uint64_t *>(ws + f.a);
+      part = reinterpret_cast<uint64_t *>(ws + f.part);
+      nb = (e.n + kNScanBlk - 1) / kNScanBlk;
+      SPK_LAUNCH(nest_tok_begin, dim3(1), dim3(1), 0, s, ws, n, (uint64_t)(uintptr_t)d_recs,
+                 tok_heaps(e), tok_layout(L, mode, e.fpre));
+      if (n)
+        SPK_LAUNCH(nest_tok_hash, dim3(nblocks(n, 256) < 512 ? nblocks(n, 256) : 512),
+                   dim3(256), 0, s, (const uint64_t *)a, n, &t->chk);
+      SPK_LAUNCH(nest_tok_verdict, dim3(1), dim3(1), 0, s, ws, (const uint64_t *)part, nb, n);
+      uint64_t *a2, *part2, nb2;
+      er = nest_size_scan(e, d_recs, ws, s, &a2, &part2, &nb2, &t->stale);
+    } else {
+      er = nest_size_scan(e, d_recs, ws, s, &a, &part, &nb);
+    }
     if (er != hipSuccess) return er;
-    NEST_D(n_dclass(e.N),
-           SPK_LAUNCH(nest_write_win<D>, dim3(nblocks(n, 256)), dim3(256), 0, s, e,
-                      (const uint8_t *)d_recs, (const uint64_t *)a, (const uint64_t *)part, nb, ws,
-                      (uint8_t *)d_out, out_cap));
+    if (vec_win)
+      NEST_D(n_dclass(e.N),
+             SPK_LAUNCH(nest_write_win<D>, dim3(nblocks(n, 256)), dim3(256), 0, s, e,
+                        (const uint8_t *)d_recs, (const uint64_t *)a, (const uint64_t *)part, nb,
+                        ws, (uint8_t *)d_out, out_cap));
+    else
+      NEST_D(n_dclass(e.N),
+             SPK_LAUNCH(nest_write_mwin<D>, dim3(nblocks(n, 256)), dim3(256), 0, s, e,
+                        (const uint8_t *)d_recs, (const uint64_t *)a, (const uint64_t *)part, nb,
+                        (uint8_t *)d_out, d_msg_offsets, out_cap));
     return hipGetLastError();
   }
   hipError_t er = nest_size_scan(e, d_recs, ws, s, &a, &part, &nb);
   if (er != hipSuccess) return er;
-  if (mode == SPK_MODE_MESSAGES && !nest_direct_write()) {
-    NEST_D(n_dclass(e.N),
-           SPK_LAUNCH(nest_write_mwin<D>, dim3(nblocks(n, 256)), dim3(256), 0, s, e,
-                      (const uint8_t *)d_recs, (const uint64_t *)a, (const uint64_t *)part, nb,
-                      (uint8_t *)d_out, d_msg_offsets, out_cap));
-    return hipGetLastError();
-  }
   NEST_D(n_dclass(e.N),
          SPK_LAUNCH(nest_write<D>, dim3(nblocks(n, 256)), dim3(256), 0, s, e,
                     (const uint8_t *)d_recs, (const uint64_t *)a, (const uint64_t *)part, nb, ws,
