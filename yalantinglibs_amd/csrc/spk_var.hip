@@ -3576,11 +3576,22 @@ __global__ __launch_bounds__(256) void tscan_apply(const uint8_t *__restrict__ w
 // LDS per wave of a whole tile, so twice the waves per CU hide the walks'
 // LDS latencies. A later part's first record and heap offsets are the
 // tile's selected totals minus what its own and later parts hold.
-constexpr uint32_t kEmitSplit = SPK_ESPLIT;
-constexpr uint32_t kEmitChunks = 64 / kEmitSplit;
-constexpr uint32_t kEmitBytes = kEmitChunks * kTChunk;
-constexpr uint32_t kEmitVec = (kEmitBytes + kWinExtra) / 16;
-constexpr uint32_t kEmitTab = kTab / kEmitSplit;  // record starts per emission pass
+// Nested layouts (NS <= -2) emit one lane per chunk: with two waves per tile
+// half of each wave's lanes had no chunk, so they take one wave per tile
+// (SPK_ESPLIT_NT; cm K4 4.68 ms with 2)
+#ifndef SPK_ESPLIT_NT
+#define SPK_ESPLIT_NT 1
+#endif
+template <int NS>
+constexpr uint32_t kEmitSplit = NS <= -2 ? SPK_ESPLIT_NT : SPK_ESPLIT;
+template <int NS>
+constexpr uint32_t kEmitChunks = 64 / kEmitSplit<NS>;
+template <int NS>
+constexpr uint32_t kEmitBytes = kEmitChunks<NS> * kTChunk;
+template <int NS>
+constexpr uint32_t kEmitVec = (kEmitBytes<NS> + kWinExtra) / 16;
+template <int NS>  // record starts per emission pass (the nested path keeps none)
+constexpr uint32_t kEmitTab = NS <= -2 ? 1u : kTab / kEmitSplit<NS>;
 
 template <int NS>
 __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkProg P,
@@ -3589,6 +3600,9 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
                                                                 TileBufs TB,
                                                                 uint8_t *__restrict__ recs,
                                                                 BigQ bq, uint32_t dbg) {
+  constexpr uint32_t kEmitSplit = spk::kEmitSplit<NS>, kEmitChunks = spk::kEmitChunks<NS>;
+  constexpr uint32_t kEmitBytes = spk::kEmitBytes<NS>, kEmitVec = spk::kEmitVec<NS>;
+  constexpr uint32_t kEmitTab = spk::kEmitTab<NS>;
   __shared__ v4u_t win_s[kDecWaves][win_slots(kEmitVec)];
   __shared__ uint16_t tab_s[kDecWaves][kEmitTab];
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
@@ -4372,7 +4386,7 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
   bq.jobs = reinterpret_cast<BigJob *>(ws + f.jobs);
   bq.n = &reinterpret_cast<FCtl *>(ws + kWsFCtl)->njobs;
   bq.cap = big_jobs_cap(a.wire_len);
-  SPK_LAUNCH(vec_tile_emit<NS>, dim3(grid_for(f.ntiles * kEmitSplit, kDecWaves)),
+  SPK_LAUNCH(vec_tile_emit<NS>, dim3(grid_for(f.ntiles * kEmitSplit<NS>, kDecWaves)),
              dim3(64 * kDecWaves), 0, s, a, P, wire, ws, TB, d_recs, bq, tile_dbg());
   if (P.ns) {
     const uint64_t gb = bq.cap < 2048 ? bq.cap : 2048;
