@@ -1427,6 +1427,10 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
 // window), and flushed with aligned 16-B stores; unaligned byte stores
 // straight to HBM cost several times their bytes in write traffic.
 constexpr uint32_t kNEncWin = 24 * 1024;
+#ifndef SPK_NWIN_STAGE  // (A/B) nest_write_win stages the block's records in LDS (bytes; 0: off)
+// (off: cm nest_write_win 2.86 -> 4.04 ms with 24 KiB staged, the LDS halves the occupancy)
+#define SPK_NWIN_STAGE 0
+#endif
 template <int D>
 __global__ __launch_bounds__(256) void nest_write_win(NEnc e, const uint8_t *__restrict__ recs,
                                                       const uint64_t *__restrict__ off,
@@ -1435,6 +1439,11 @@ __global__ __launch_bounds__(256) void nest_write_win(NEnc e, const uint8_t *__r
                                                       uint8_t *__restrict__ out, uint64_t out_cap) {
   __shared__ NLayout N;
   __shared__ __align__(16) uint8_t lds[kNEncWin];
+#if SPK_NWIN_STAGE
+  // the block's records with coalesced 8-B loads when they fit (as nest_size):
+  // the interpreter reads a record field by field, one dependent load per op
+  __shared__ __align__(16) uint8_t rs[SPK_NWIN_STAGE];
+#endif
   n_stage(N, e.N);
   const NCtl *ctl = reinterpret_cast<const NCtl *>(ws + kWsCtl);
   const uint64_t mx = ctl->maxc > e.n ? ctl->maxc : e.n;
@@ -1453,6 +1462,16 @@ __global__ __launch_bounds__(256) void nest_write_win(NEnc e, const uint8_t *__r
   const uint64_t q0 = i < e.n ? hl + off[i] : 0;
   const uint64_t q1 = i < e.n ? (i + 1 < e.n ? hl + off[i + 1] : hl + tot0) : 0;
   const uint8_t *rec = recs + i * N.stride;
+#if SPK_NWIN_STAGE
+  if (256ull * N.stride <= SPK_NWIN_STAGE && !(N.stride & 7) && !((uintptr_t)recs & 7)) {
+    const uint64_t *src = reinterpret_cast<const uint64_t *>(recs + r0 * N.stride);
+    uint64_t *dst = reinterpret_cast<uint64_t *>(rs);
+    const uint64_t words = (rend - r0) * N.stride / 8;
+    for (uint64_t k = threadIdx.x; k < words; k += 256) dst[k] = src[k];
+    __syncthreads();
+    rec = rs + (i - r0) * N.stride;
+  }
+#endif
   for (uint64_t wlo = g0 & ~15ull; wlo < g1; wlo += kNEncWin) {
     const NWin W{lds, wlo, wlo + kNEncWin < g1 ? wlo + kNEncWin : g1};
     if (i < e.n && q0 < W.hi && q1 > W.lo) n_write<D>(N, rec, e.heaps, w, W, q0, 0, N.n_ops, true);
