@@ -4,9 +4,11 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
+if [ -z "$SQ_ONLY" ]; then
 bash scripts/gpu_cpp_proto.sh || exit 1
 grep -q '"failures": 0' gpurun_out/proto_0.out || { echo "proto failures"; exit 1; }
 NO_BENCH=1 bash scripts/gpu_round.sh || exit 1
+fi
 OUT=gpurun_out/sq; mkdir -p $OUT
 for c in ${CONFIGS:-c3 c4}; do
   for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD" "SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM"; do
