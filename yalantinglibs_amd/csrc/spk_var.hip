@@ -580,10 +580,57 @@ constexpr unsigned kYSplit = 8;  // blocks sharing one write block's output
 // flight per lane, head/tail bytes by single lanes. (A block-wide flattened
 // chunk index over all payloads, searched per chunk, measured 13 % slower on
 // C5's vector<int> messages.)
+#ifndef SPK_COPY_PAIR  // (A/B) wave_copy_all takes two payloads per step (loads of both in flight)
+// (off: C5 var_encode_write 0.37 -> 9.6 ms per launch, var_msg_write 0.34 -> 0.54)
+#define SPK_COPY_PAIR 0
+#endif
+// one payload's head / tail bytes (single lanes) and its 16-B chunk count
+__device__ __forceinline__ uint64_t seg_edges(const BigSeg &e, uint32_t lane, uint64_t *head) {
+  uint64_t h = (16 - ((uintptr_t)e.dptr & 15)) & 15;
+  if (h > e.n) h = e.n;
+  const uint64_t nc = (e.n - h) >> 4, tail = h + 16 * nc;
+  if (lane < h) e.dptr[lane] = e.src[lane];
+  if (lane < e.n - tail) e.dptr[tail + lane] = e.src[tail + lane];
+  *head = h;
+  return nc;
+}
 __device__ __forceinline__ void wave_copy_all(const BigSeg *B, uint32_t m, uint32_t part,
                                               uint32_t nparts) {
   const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const uint32_t gw = part * nw + (threadIdx.x >> 6), W = nparts * nw;
+  if constexpr (SPK_COPY_PAIR) {
+    // payloads k and k + W together: their descriptors and the first
+    // kCoopU / 2 chunks per lane of each in flight at once (a C5 vector<int>
+    // payload is ~4 KiB = 4 chunks per lane: one payload at a time left half
+    // the loads of a step unused and paid a descriptor load latency each)
+    constexpr int H = kCoopU / 2;
+    for (uint32_t k = gw; k < m; k += 2 * W) {
+      const bool two = k + W < m;
+      const BigSeg e0 = B[k];
+      BigSeg e1 = {0, nullptr, nullptr, 0};
+      if (two) e1 = B[k + W];
+      uint64_t h0, h1 = 0;
+      const uint64_t n0 = seg_edges(e0, lane, &h0);
+      const uint64_t n1 = two ? seg_edges(e1, lane, &h1) : 0;
+      const uint8_t *s0 = e0.src + h0, *s1 = e1.src + h1;
+      uint8_t *d0 = e0.dptr + h0, *d1 = e1.dptr + h1;
+      const uint64_t nmax = n0 > n1 ? n0 : n1;
+      for (uint64_t c0 = lane; c0 < nmax; c0 += 64 * H) {
+        v4u_t v[2 * H];
+#pragma unroll
+        for (int u = 0; u < H; ++u) {
+          if (c0 + 64 * u < n0) v[u] = *reinterpret_cast<const v4u_una *>(s0 + 16 * (c0 + 64 * u));
+          if (c0 + 64 * u < n1) v[H + u] = *reinterpret_cast<const v4u_una *>(s1 + 16 * (c0 + 64 * u));
+        }
+#pragma unroll
+        for (int u = 0; u < H; ++u) {
+          if (c0 + 64 * u < n0) *reinterpret_cast<v4u_t *>(d0 + 16 * (c0 + 64 * u)) = v[u];
+          if (c0 + 64 * u < n1) *reinterpret_cast<v4u_t *>(d1 + 16 * (c0 + 64 * u)) = v[H + u];
+        }
+      }
+    }
+    return;
+  }
   for (uint32_t k = gw; k < m; k += W) {
     const BigSeg e = B[k];
     uint64_t head = (16 - ((uintptr_t)e.dptr & 15)) & 15;
