@@ -673,6 +673,32 @@ __global__ __launch_bounds__(1024) void msg_sum_partials(const uint64_t *__restr
   }
 }
 
+// A grid-stride kernel's grid: the blocks the device holds at once (occupancy
+// x CUs), at most `want` and `fixed_cap`. A fixed cap (4096) left a second, partial round of
+// blocks once the first had run: each block strides over the same number of
+// groups, so a grid of 1.8 resident rounds took two full ones.
+#ifndef SPK_RESIDENT_GRID
+#define SPK_RESIDENT_GRID 1
+#endif
+template <typename K>
+static uint64_t resident_grid(K kernel, int threads, size_t shm, uint64_t want, uint64_t fixed_cap) {
+  if (!SPK_RESIDENT_GRID) return want < fixed_cap ? want : fixed_cap;
+  static int ncu = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      v = 0;
+    return v;
+  }();
+  int nb = 0;
+  if (!ncu || hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, threads, shm) != hipSuccess ||
+      nb <= 0)
+    return want < fixed_cap ? want : fixed_cap;
+  uint64_t cap = (uint64_t)nb * (uint64_t)ncu;
+  if (cap > fixed_cap) cap = fixed_cap;  // (the workspace holds fixed_cap blocks' partials)
+  return want < cap ? want : cap;
+}
+
 // messages per block for the LDS-staged kernels: a multiple of 16 whose
 // staging (R messages of M bytes, + alignment slack) fits kMsgStageMax; 0 if
 // a single group of 16 does not fit (very large records: global path)
@@ -891,8 +917,9 @@ hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
     b.R = msg_block_R(a.fixed_M);
     if (b.R && (uintptr_t)d_recs % 16 == 0 && n > 0 && b.stride % 4 == 0) {
       b.cap = b.R * a.fixed_M + 32;
-      uint64_t blocks = (n + b.R - 1) / b.R;
-      if (blocks > 4096) blocks = 4096;  // groups are strided over the grid
+      // groups are strided over the grid: one resident round of blocks
+      const uint64_t blocks = resident_grid(fixed_msg_decode_lds, kMsgThreads, (size_t)b.cap + 16,
+                                            (n + b.R - 1) / b.R, 4096);
       uint64_t *part = payload;  // workspace scratch: 2 words per block
       SPK_LAUNCH(fixed_msg_decode_lds, dim3((unsigned)blocks), dim3(kMsgThreads),
                          (size_t)b.cap + 16, s, b, (const uint8_t *)d_wire, d_offsets, d_errc,
