@@ -96,12 +96,29 @@ __global__ __launch_bounds__(kCopyThreads) void shift_copy_kernel(
   shift_body(reinterpret_cast<v4u *>(d + head), s + head, body >> 4);
 }
 
+#ifndef SPK_COPY_ROUNDS  // (A/B) shift_copy grid in resident rounds of blocks (0: 32 Ki cap)
+// (off: C2 step 4.36 ms with the 32 Ki cap, 4.74 with one resident round, 4.60 with four)
+#define SPK_COPY_ROUNDS 0
+#endif
+__global__ __launch_bounds__(kCopyThreads) void shift_copy_kernel(
+    uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+    const CopyJob *__restrict__ job, const uint8_t *__restrict__ hdr);
 static unsigned copy_grid(uint64_t max_bytes) {
   uint64_t tiles = (max_bytes / 16 + kTile - 1) / kTile;
   uint64_t blocks = (tiles + (kCopyThreads / 64) - 1) / (kCopyThreads / 64);
   // 32 Ki blocks (128 Ki waves) then grid-stride: the probe's best point
   // (scripts/probes/copy_probe.hip: 16 chunks in flight per lane, 6.1-6.2 TB/s)
   if (blocks > 32768) blocks = 32768;
+  if (SPK_COPY_ROUNDS) {  // a whole number of resident rounds
+    int dev = 0, ncu = 0, nb = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, shift_copy_kernel, kCopyThreads, 0) ==
+            hipSuccess && nb > 0 && ncu > 0) {
+      const uint64_t round = (uint64_t)nb * ncu * SPK_COPY_ROUNDS;
+      if (blocks > round) blocks = round;
+    }
+  }
   if (blocks < 1) blocks = 1;
   return (unsigned)blocks;
 }
