@@ -62,9 +62,10 @@
 #define SPK_NT_PAST 0
 #endif
 #ifndef SPK_SCAP      // K1's speculation caps from the message's first records (vec_hdr_sample)
-// (default off: see DESIGN section 6.1 -- C3 / cv K1 faster with them, but
-// their per-lane fallback costs C4's K1 15 % even where no cap applies)
-#define SPK_SCAP 0        // bit 0: on the speculative walks' records, bit 1: on the candidate screen
+// (round 4, after K1's lane state moved back into locals: bit 0 on by default
+// -- C3 / c3r / cv K1 0.243 / 0.253 / 1.93 -> 0.194 / 0.209 / 1.72 ms, C4
+// +1 %; bit 1 as well: cv 1.36 ms but C4 K1 0.363 -> 0.423)
+#define SPK_SCAP 1        // bit 0: on the speculative walks' records, bit 1: on the candidate screen
 #endif
 #ifndef SPK_SCAP_MINR     // ... applied only when the layout's first-count limit is this many times the cap
 #define SPK_SCAP_MINR 32
@@ -1216,6 +1217,7 @@ struct VCtl {
   // spec_c0 is the first-count screen under them
   uint64_t scap[kVS];
   uint64_t spec_c0;
+  uint64_t scap_on;  // the caps tighten something (else K1 walks as without them)
 };
 
 // control words of the tile vector decoder (vec_tile_*)
@@ -2855,7 +2857,9 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
   uint64_t c0t = P.c0max;
   bool tight = false;
   if constexpr (NS > -2) {
-    if (sc && !(dbg & 65536)) {
+    if (sc && sc->scap_on && !(dbg & 65536)) {
+      // (caps that tighten nothing would only add the search without them
+      // for chunks holding no record start: long-string messages)
       tight = true;
       if (SPK_SCAP & 2) c0t = sc->spec_c0;
       if (SPK_SCAP & 1) scap = sc->scap;
@@ -3292,6 +3296,7 @@ __global__ __launch_bounds__(64) void vec_hdr_sample(DecArgs a, WalkProg P,
       c->scap[q] = cp;
     }
     c->spec_c0 = c0;
+    c->scap_on = got ? 1u : 0u;
   }
 }
 
