@@ -64,8 +64,10 @@
 #ifndef SPK_SCAP      // K1's speculation caps from the message's first records (vec_hdr_sample)
 // (round 4, after K1's lane state moved back into locals: bit 0 on by default
 // -- C3 / c3r / cv K1 0.243 / 0.253 / 1.93 -> 0.194 / 0.209 / 1.72 ms, C4
-// +1 %; bit 1 as well: cv 1.36 ms but C4 K1 0.363 -> 0.423)
-#define SPK_SCAP 1        // bit 0: on the speculative walks' records, bit 1: on the candidate screen
+// +1 %; the screen cap too: cv K1 1.71 -> 1.36 ms but C3 0.192 -> 0.216, so
+// it is on for varint layouts only)
+#define SPK_SCAP 5        // bit 0: on the speculative walks' records, bit 1: on the candidate screen,
+                          // bit 2: on the candidate screen of varint layouts (NS = -1)
 #endif
 #ifndef SPK_SCAP_MINR     // ... applied only when the layout's first-count limit is this many times the cap
 #define SPK_SCAP_MINR 32
@@ -2861,7 +2863,7 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
       // (caps that tighten nothing would only add the search without them
       // for chunks holding no record start: long-string messages)
       tight = true;
-      if (SPK_SCAP & 2) c0t = sc->spec_c0;
+      if ((SPK_SCAP & 2) || (NS == -1 && (SPK_SCAP & 4))) c0t = sc->spec_c0;
       if (SPK_SCAP & 1) scap = sc->scap;
     }
   }
