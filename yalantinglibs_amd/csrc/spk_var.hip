@@ -3204,6 +3204,9 @@ __device__ __forceinline__ void vec_tile_spec_body(const DecArgs &a, const WalkP
   }
 }
 
+#ifndef SPK_K1_LDS_PROG  // varint K1 reads its walk program from LDS
+#define SPK_K1_LDS_PROG 1
+#endif
 #ifndef SPK_WSPEC  // 1: K1 of the nested walk program per count width; 2: every layout
 #define SPK_WSPEC 2   // (2: C4 K1 -15 %, C3 -13 %, cv -5 % against 1, same-box A/B)
 #endif
@@ -3217,15 +3220,28 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t t = (uint64_t)blockIdx.x * kDecWaves + wv;
   if (t >= TB.ntiles || !vec_live(c)) return;  // wave-uniform
+#if SPK_K1_LDS_PROG
+  // varint layouts with the speculation caps: the walk program from LDS (the
+  // compiler otherwise copied the by-value argument into scratch memory and
+  // read it from there: 264 B per lane)
+  __shared__ WalkProg Ps;
+  if constexpr (NS == -1 && SPK_SCAP != 0) {
+    if (threadIdx.x == 0) Ps = P;
+    __syncthreads();
+  }
+  const WalkProg &Pk = (NS == -1 && SPK_SCAP != 0) ? Ps : P;
+#else
+  const WalkProg &Pk = P;
+#endif
   if constexpr (SPK_WSPEC >= 2 || (SPK_WSPEC == 1 && NS == -3)) {
     switch (c->w) {  // (uniform: the header's width)
-      case 1: vec_tile_spec_body<NS, 1>(a, P, wire, ws, TB, dbg, win_s[wv], t, lane); return;
-      case 2: vec_tile_spec_body<NS, 2>(a, P, wire, ws, TB, dbg, win_s[wv], t, lane); return;
-      case 4: vec_tile_spec_body<NS, 4>(a, P, wire, ws, TB, dbg, win_s[wv], t, lane); return;
-      default: vec_tile_spec_body<NS, 8>(a, P, wire, ws, TB, dbg, win_s[wv], t, lane); return;
+      case 1: vec_tile_spec_body<NS, 1>(a, Pk, wire, ws, TB, dbg, win_s[wv], t, lane); return;
+      case 2: vec_tile_spec_body<NS, 2>(a, Pk, wire, ws, TB, dbg, win_s[wv], t, lane); return;
+      case 4: vec_tile_spec_body<NS, 4>(a, Pk, wire, ws, TB, dbg, win_s[wv], t, lane); return;
+      default: vec_tile_spec_body<NS, 8>(a, Pk, wire, ws, TB, dbg, win_s[wv], t, lane); return;
     }
   } else {
-    vec_tile_spec_body<NS, 0>(a, P, wire, ws, TB, dbg, win_s[wv], t, lane);
+    vec_tile_spec_body<NS, 0>(a, Pk, wire, ws, TB, dbg, win_s[wv], t, lane);
   }
 }
 
