@@ -3224,12 +3224,14 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
   // varint layouts with the speculation caps: the walk program from LDS (the
   // compiler otherwise copied the by-value argument into scratch memory and
   // read it from there: 264 B per lane)
+  // (SPK_K1_LDS_PROG=2: every flat layout, A/B -- C3 K1 0.193 -> 0.233 ms, off)
+  constexpr bool kLdsProg = (NS == -1 && SPK_SCAP != 0) || (SPK_K1_LDS_PROG == 2 && NS > -2);
   __shared__ WalkProg Ps;
-  if constexpr (NS == -1 && SPK_SCAP != 0) {
+  if constexpr (kLdsProg) {
     if (threadIdx.x == 0) Ps = P;
     __syncthreads();
   }
-  const WalkProg &Pk = (NS == -1 && SPK_SCAP != 0) ? Ps : P;
+  const WalkProg &Pk = kLdsProg ? Ps : P;
 #else
   const WalkProg &Pk = P;
 #endif
