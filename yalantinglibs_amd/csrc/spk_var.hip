@@ -70,7 +70,8 @@
                           // bit 2: on the candidate screen of varint layouts (NS = -1)
 #endif
 #ifndef SPK_SCAP_MINR     // ... applied only when the layout's first-count limit is this many times the cap
-#define SPK_SCAP_MINR 32
+// (round 4: 32 -> 8, so C4's 1-byte counts (limit 511, cap ~32) take them: K1 0.362 -> 0.350 ms)
+#define SPK_SCAP_MINR 8
 #endif
 #ifndef SPK_SCAP_MUL      // a span's cap: this multiple of its largest sampled count
 #define SPK_SCAP_MUL 2
@@ -3298,7 +3299,8 @@ __global__ __launch_bounds__(64) void vec_hdr_sample(DecArgs a, WalkProg P,
   if (lane == 0) {
     // caps only where they tighten the first-count screen by SPK_SCAP_MINR x
     // or more: a screen already that selective gains nothing from them (C4:
-    // 511 vs 32 measured slower with them; C3 4092 vs ~96, cv 4096 vs 32 faster)
+    // 511 vs 32 slower with them in round 3, faster since K1 keeps its state in
+    // locals; C3 4092 vs ~96, cv 4096 vs 32 faster)
     {
       uint64_t t0 = mx[0] < (1ull << 60) ? SPK_SCAP_MUL * mx[0] : ~0ull;
       t0 = t0 < 15 ? 15 : t0;
