@@ -44,6 +44,7 @@
 
 #include "../spk_codec.h"
 #include "struct_pack_gpu/layout.hpp"
+#include "struct_pack_gpu/walk.hpp"
 
 namespace struct_pack::gpu {
 
@@ -267,8 +268,10 @@ class codec {
     } else {
       // kept in the codec: string_view / span / trivial_view members of the
       // decoded objects alias these host records and heaps, valid until this
-      // thread's next decode of R (the reference's views alias its input
-      // buffer, unpacker.hpp:787-800,1135-1145)
+      // thread's next decode of R; the decode entry points that take the
+      // wire from the caller then point them into the caller's buffer
+      // (rebase_views), as the reference's views alias its input
+      // (unpacker.hpp:787-800,1135-1145)
       std::vector<uint8_t> &recs = view_recs_;
       recs.assign(n * L.rec_stride, 0);
       std::vector<std::vector<uint8_t>> &heaps = view_heaps_;
@@ -676,6 +679,12 @@ err_code decode_one_dev(T &t, const char *data, std::size_t size, std::size_t &c
     } else {
       c.download(b, 1, &t);  // (boxed<M>: t is its one member)
     }
+    if constexpr (has_views<T>()) {  // views alias `data`, as the reference's do
+      mem_cursor mc{data, size};
+      header_info h;
+      (void)walk_header(mc, tr::vector ? c.layout().fmt_vector : c.layout().fmt_one, h);
+      rebase_views(t, mc, h.w);
+    }
     consume_len = r.consumed;
     return {};
   }
@@ -909,162 +918,6 @@ template <uint64_t conf, typename T, detail::byte_view View>
   return t;
 }
 
-// get_field<T, I>: member I of a T message (struct_pack.hpp:565-658). The
-// whole record is decoded on the device, member I returned.
-template <typename T, std::size_t I>
-using field_t = std::tuple_element_t<I, detail::members_tuple_t<T>>;
-
-template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT>
-[[nodiscard]] expected<field_t<T, I>> get_field(const char *data, std::size_t size) {
-  static_assert(detail::is_record_v<T>, "get_field reads a member of a record message");
-  T t{};
-  std::size_t consumed;
-  if (auto e = detail::decode_one<conf>(t, data, size, consumed))
-    return make_unexpected<field_t<T, I>>(e);
-  return expected<field_t<T, I>>(std::get<I>(detail::tie_members(t)));
-}
-template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT, detail::byte_view View>
-[[nodiscard]] expected<field_t<T, I>> get_field(const View &v) {
-  return get_field<T, I, conf>(reinterpret_cast<const char *>(v.data()), v.size());
-}
-// get_field_to<T, I>(dst, ...) (struct_pack.hpp:565-611)
-template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT, typename Field>
-[[nodiscard]] err_code get_field_to(Field &dst, const char *data, std::size_t size) {
-  auto r = get_field<T, I, conf>(data, size);
-  if (!r.has_value()) return r.error();
-  dst = std::move(r.value());
-  return {};
-}
-template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT, typename Field,
-          detail::byte_view View>
-[[nodiscard]] err_code get_field_to(Field &dst, const View &v) {
-  return get_field_to<T, I, conf>(dst, reinterpret_cast<const char *>(v.data()), v.size());
-}
-
-// ---- stream readers: deserialize_to(t, reader) (struct_pack.hpp:289-323) ----
-// The reference reads a message from a Reader field by field
-// (unpacker.hpp:46-76, 1166-1195). The device decoder needs the message's
-// bytes in one buffer, so the front end reads a growing block from the
-// reader (64 KiB, then x4), decodes it on the GPU, and puts the reader right
-// after the message (seekg to start + consume_len). A prefix decoded with
-// no_buffer_space only means "read more". Layouts whose decode can succeed on
-// a cut message (the reference drops the errc of an optional's value, a
-// variant's alternative and reads absent compatible members as empty:
-// unpacker.hpp:476-490,1271-1273) read the reader's whole remainder at once,
-// so a truncated block never stands in for the message. Readers: the
-// std::istream family, or any type with read / gcount / tellg / seekg / clear
-// (a socket is not one: coro_rpc frames carry their length in req_header).
-namespace detail {
-template <typename R>
-concept seekable_reader = requires(R &r, char *p, std::size_t n) {
-  r.read(p, n);
-  r.gcount();
-  r.tellg();
-  r.seekg(r.tellg());
-  r.seekg(0, std::ios_base::end);
-  r.clear();
-};
-
-inline bool prefix_decode_exact(const spk_layout &L) {
-  for (uint32_t i = 0; i < L.n_ops; ++i) {
-    const uint32_t k = SPK_OP_KIND(L.ops[i].kind);
-    if (k == SPK_OP_OPTION || k == SPK_OP_OPTGROUP || k == SPK_OP_VARIANT || k == SPK_OP_COMPAT ||
-        k == SPK_OP_CGROUP)
-      return false;
-  }
-  return true;
-}
-
-// read a growing block from `rd` and decode it with fn(data, size, used) until
-// the decode succeeds or fails for a reason other than a short buffer; the
-// reader is left after the bytes the decode used (after the bytes read on an
-// error). exact = false: read the whole remainder at once (a prefix may
-// decode "successfully" where the full message would not)
-template <typename Reader, typename Fn>
-err_code stream_decode(Reader &rd, bool exact, std::size_t &consume_len, Fn &&fn) {
-  consume_len = 0;
-  const auto start = rd.tellg();
-  std::size_t want = std::size_t(1) << 16;
-  if (!exact) {  // the whole remainder
-    rd.seekg(0, std::ios_base::end);
-    const auto end = rd.tellg();
-    rd.seekg(start);
-    want = end > start ? static_cast<std::size_t>(end - start) : 0;
-  }
-  std::vector<char> buf;
-  for (;;) {
-    const std::size_t have = buf.size();
-    buf.resize(want);
-    if (want > have) rd.read(buf.data() + have, static_cast<std::streamsize>(want - have));
-    const std::size_t got = have + (want > have ? static_cast<std::size_t>(rd.gcount()) : 0);
-    const bool at_end = got < want || !exact;
-    buf.resize(got);
-    rd.clear();
-    std::size_t used = 0;
-    err_code e = fn(buf.data(), got, used);
-    if (!e) {
-      rd.seekg(start + static_cast<std::streamoff>(used));
-      consume_len = used;
-      return e;
-    }
-    if (e != errc::no_buffer_space || at_end) {
-      rd.seekg(start + static_cast<std::streamoff>(got));  // the bytes read were consumed
-      return e;
-    }
-    want *= 4;
-  }
-}
-
-template <uint64_t conf, typename T, typename Reader>
-err_code decode_stream(T &t, Reader &rd, std::size_t &consume_len) {
-  using tr = msg_traits<T>;
-  bool exact = true;
-  if constexpr (!tr::empty) exact = prefix_decode_exact(device::codec<typename tr::rec, conf>::layout());
-  return stream_decode(rd, exact, consume_len, [&](const char *d, std::size_t n, std::size_t &u) {
-    return decode_one<conf>(t, d, n, u);
-  });
-}
-}  // namespace detail
-
-template <uint64_t conf = sp_config::DEFAULT, typename T, typename Reader>
-  requires detail::seekable_reader<Reader>
-[[nodiscard]] err_code deserialize_to(T &t, Reader &reader) {
-  detail::check_message_type<T>();
-  std::size_t consumed;
-  return detail::decode_stream<conf>(t, reader, consumed);
-}
-template <typename T, typename Reader>
-  requires detail::seekable_reader<Reader>
-[[nodiscard]] expected<T> deserialize(Reader &reader) {
-  T t{};
-  if (auto e = deserialize_to(t, reader)) return make_unexpected<T>(e);
-  return t;
-}
-template <uint64_t conf, typename T, typename Reader>
-  requires detail::seekable_reader<Reader>
-[[nodiscard]] expected<T> deserialize(Reader &reader) {
-  T t{};
-  if (auto e = deserialize_to<conf>(t, reader)) return make_unexpected<T>(e);
-  return t;
-}
-template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT, typename Reader>
-  requires detail::seekable_reader<Reader>
-[[nodiscard]] expected<field_t<T, I>> get_field(Reader &reader) {
-  static_assert(detail::is_record_v<T>, "get_field reads a member of a record message");
-  T t{};
-  if (auto e = deserialize_to<conf>(t, reader)) return make_unexpected<field_t<T, I>>(e);
-  return expected<field_t<T, I>>(std::get<I>(detail::tie_members(t)));
-}
-template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT, typename Field,
-          typename Reader>
-  requires detail::seekable_reader<Reader>
-[[nodiscard]] err_code get_field_to(Field &dst, Reader &reader) {
-  auto r = get_field<T, I, conf>(reader);
-  if (!r.has_value()) return r.error();
-  dst = std::move(r.value());
-  return {};
-}
-
 // ---- user helpers: struct_pack::write / read / get_write_size --------------
 // (user_helper.hpp:16-85) The payload bytes of t (or of t[0..len)) without
 // header, container counts at size_width bytes: the body of a VECTOR message
@@ -1117,6 +970,10 @@ err_code decode_body_host(T *t, std::size_t n, const char *data, std::size_t siz
   if (r.errc) return static_cast<errc>(r.errc);
   for (uint32_t k = 0; k < c.n_spans(); ++k) b.heap_elems[k] = r.heap_used[k];
   c.download(b, n, t);  // (boxed<T>: each t[i] is its one member)
+  if constexpr (has_views<T>()) {  // views alias `data`
+    mem_cursor mc{data, size};
+    for (std::size_t i = 0; i < n; ++i) rebase_views(t[i], mc, static_cast<uint32_t>(W));
+  }
   consumed = r.consumed;
   return {};
 }
@@ -1142,8 +999,8 @@ template <std::size_t size_width = sizeof(uint64_t), typename T>
 std::size_t get_write_size(const T &t) {
   return get_write_size<size_width>(&t, 1);
 }
-// read from a byte view (advancing `pos`) or a seekable reader (left after
-// the bytes read); ifSkip: consume without keeping the values
+// read from a byte view (advancing `pos`) or a reader (below); ifSkip:
+// consume without keeping the values
 template <std::size_t size_width = sizeof(uint64_t), bool ifSkip = false, typename T>
 err_code read_from(const char *data, std::size_t size, std::size_t &pos, T *t, std::size_t len) {
   std::size_t used = 0;
@@ -1159,24 +1016,298 @@ err_code read_from(const char *data, std::size_t size, std::size_t &pos, T *t, s
   pos += used;
   return e;
 }
+// ---- get_field<T, I> (struct_pack.hpp:565-658) -------------------------------
+// The reference reads members 0..I of a T message and stops: the members
+// before I in skip mode, each result overwriting the previous one (the
+// &&-fold of for_each only stops at member I, unpacker.hpp:1554-1592), then
+// member I into `dst`; a T with compatible members also runs the version
+// passes over members 0..I (deserialize_compatible_fields, unpacker.hpp:
+// 367-444). So on a buffer cut after member I the field still comes back.
+// Here the header is parsed on the host (spk_parse_message_header), members
+// 0..I-1 are skipped by the host walker (walk.hpp) and member I is decoded on
+// the device as a one-record body at the message's width (spk_decode_body).
+// The members of a trivially serializable T are walked one by one too, with
+// no padding, like the reference's get_field_impl.
+template <typename T, std::size_t I>
+using field_t = std::tuple_element_t<I, detail::members_tuple_t<T>>;
+
+namespace detail {
+template <uint64_t conf, typename F>
+err_code decode_field(F &dst, const char *data, std::size_t size, uint32_t w, std::size_t &used) {
+  switch (w) {
+    case 1: return decode_body_host<1, conf>(&dst, 1, data, size, used);
+    case 2: return decode_body_host<2, conf>(&dst, 1, data, size, used);
+    case 4: return decode_body_host<4, conf>(&dst, 1, data, size, used);
+    default: return decode_body_host<8, conf>(&dst, 1, data, size, used);
+  }
+}
+
+// get_field's reads over cursor `c`, after the header: main pass over members
+// 0..I (member I by main(c)), then, for a T with compatible members, the
+// version passes over members 0..I (member I by in_pass(c, past) when it is a
+// compatible member of that version). Returns the reference's errc.
+template <typename T, std::size_t I, typename Cur, typename Main, typename InPass>
+errc get_field_walk(Cur &c, uint32_t w, uint64_t data_len, Main &&main, InPass &&in_pass) {
+  using M = members_tuple_t<T>;
+  static_assert(I < std::tuple_size_v<M>, "get_field: member index out of range");
+  using F = std::tuple_element_t<I, M>;
+  errc code{};
+  [&]<std::size_t... J>(std::index_sequence<J...>) {
+    ((code = walk_one<std::tuple_element_t<J, M>>(c, w)), ...);
+  }(std::make_index_sequence<I>{});
+  if constexpr (is_compat_v<F>)
+    code = {};  // a compatible member is read in its version pass
+  else
+    code = main(c);
+  if constexpr (record_has_compat<T>()) {
+    if (code != errc{}) return code;
+    bool past = false;
+    for (uint64_t v : compat_versions<T>()) {
+      errc pc{};
+      [&]<std::size_t... J>(std::index_sequence<J...>) {
+        auto one = [&](auto jc, auto tagv) {
+          using G = typename decltype(tagv)::type;
+          constexpr std::size_t j = decltype(jc)::value;
+          pc = {};
+          if constexpr (is_compat_v<G>) {
+            if (compat_traits<G>::version == v) {
+              if constexpr (j < I)
+                pc = walk_compat_member<G>(c, w, data_len, past);
+              else
+                pc = in_pass(c, past);
+            }
+          }
+        };
+        (one(std::integral_constant<std::size_t, J>{},
+             std::type_identity<std::tuple_element_t<J, M>>{}),
+         ...);
+      }(std::make_index_sequence<I + 1>{});
+      code = pc;
+      if (code != errc{}) break;
+    }
+    if (past) code = {};  // the buffer ended before a version: not an error
+  }
+  return code;
+}
+
+template <typename T, std::size_t I, uint64_t conf>
+err_code get_field_mem(field_t<T, I> &dst, const char *data, std::size_t size) {
+  static_assert(is_record_v<T>, "get_field reads a member of a record message");
+  using F = field_t<T, I>;
+  const spk_layout &L = device::codec<typename msg_traits<T>::rec, conf>::layout();
+  uint32_t w = 0, hl = 0;
+  const int32_t he = spk_parse_message_header(&L, data, size, &w, &hl);
+  if (he < 0) device::check(he, "spk_parse_message_header");
+  if (he) return static_cast<errc>(he);
+  mem_cursor c{data, size};
+  header_info h;
+  (void)walk_header(c, L.fmt_one, h);  // the header parsed above: positions c, data length
+  auto main = [&](mem_cursor &cc) -> errc {
+    if constexpr (!is_compat_v<F>) {
+      std::size_t used = 0;
+      const err_code e =
+          decode_field<sp_config::DEFAULT>(dst, cc.d + cc.pos, cc.n - cc.pos, w, used);
+      cc.pos += used;
+      return e;
+    } else {
+      return (void)cc, errc{};
+    }
+  };
+  auto in_pass = [&](mem_cursor &cc, bool &past) -> errc {
+    if constexpr (is_compat_v<F>) {
+      if (cc.tell() >= h.data_len) {
+        past = true;
+        return errc::no_buffer_space;
+      }
+      // [has][U] decoded as an optional<U>: the value's errc is dropped like
+      // the reference's (unpacker.hpp:1354-1376)
+      std::optional<typename compat_traits<F>::value_type> o;
+      std::size_t used = 0;
+      const err_code e = decode_field<sp_config::DEFAULT>(o, cc.d + cc.pos, cc.n - cc.pos, w, used);
+      if (e) return e;
+      cc.pos += used;
+      if (o) dst = F{std::move(*o)};
+      return {};
+    } else {
+      (void)cc, (void)past;
+      return {};
+    }
+  };
+  return get_field_walk<T, I>(c, w, h.data_len, main, in_pass);
+}
+}  // namespace detail
+
+template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT, typename Field>
+[[nodiscard]] err_code get_field_to(Field &dst, const char *data, std::size_t size) {
+  static_assert(std::is_same_v<Field, field_t<T, I>>,
+                "The dst's type is not correct. It should be as same as the T's Ith field's type");
+  return detail::get_field_mem<T, I, conf>(dst, data, size);
+}
+template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT, typename Field,
+          detail::byte_view View>
+[[nodiscard]] err_code get_field_to(Field &dst, const View &v) {
+  return gpu::get_field_to<T, I, conf>(dst, reinterpret_cast<const char *>(v.data()), v.size());
+}
+template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT>
+[[nodiscard]] expected<field_t<T, I>> get_field(const char *data, std::size_t size) {
+  field_t<T, I> f{};
+  if (auto e = gpu::get_field_to<T, I, conf>(f, data, size)) return make_unexpected<field_t<T, I>>(e);
+  return expected<field_t<T, I>>(std::move(f));
+}
+template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT, detail::byte_view View>
+[[nodiscard]] expected<field_t<T, I>> get_field(const View &v) {
+  return gpu::get_field<T, I, conf>(reinterpret_cast<const char *>(v.data()), v.size());
+}
+
+// ---- readers (struct_pack.hpp:289-323, 415-533, 595-612, 660-676) -----------
+// Any reader_t of the reference (read / ignore / tellg, reflection.hpp:
+// 110-114): std::istream, the reference's detail::memory_reader, a socket-like
+// reader that cannot seek. The host walker (walk.hpp) reads exactly the
+// message's bytes through read() -- the reads the reference's decoder would
+// make, in the same order -- and the device decodes them. On success the
+// reader is left right after the message (after the compatible-data length,
+// struct_pack.hpp:302-312), as the reference leaves it. After a short read the
+// walker takes whatever the reader still delivers, so the decode sees what
+// the reference's reads could have seen and returns its errc; the reader is
+// then left at its end (the reference leaves it where its last read stopped).
+namespace detail {
+template <typename R>
+concept reader_t = requires(R &r, char *p, std::size_t n) {
+  r.read(p, n);
+  r.ignore(n);
+  r.tellg();
+};
+
+// one message of type T (one std::vector<R>, one record, a boxed message or
+// a header-only one) out of a reader
+template <uint64_t conf, typename T, typename Reader>
+std::vector<char> pull_message(Reader &rd) {
+  using tr = msg_traits<T>;
+  std::vector<char> buf;
+  pull_cursor<Reader> c{rd, buf};
+  header_info h;
+  errc e{};
+  if constexpr (tr::empty) {
+    e = walk_header(c, empty_message_layout<T, conf>().fmt_one, h);
+  } else {
+    const spk_layout &L = device::codec<typename tr::rec, conf>::layout();
+    e = walk_header(c, tr::vector ? L.fmt_vector : L.fmt_one, h);
+    if constexpr (tr::vector && record_has_compat<typename tr::rec>()) {
+      // a vector of records with compatible members: the main pass over its
+      // n records, then the version passes over them
+      using R = typename tr::rec;
+      uint64_t n = 0;
+      if (e == errc{}) e = walk_count(c, h.w, n) ? errc{} : errc::no_buffer_space;
+      for (uint64_t i = 0; i < n && e == errc{}; ++i) e = walk_one<R>(c, h.w);
+      if (e == errc{}) {
+        bool past = false;
+        (void)walk_versions_vec<R>(c, h.w, n, h.data_len, past);
+      }
+    } else {
+      if (e == errc{}) e = walk_one<T>(c, h.w);
+      if constexpr (record_has_compat<T>()) {
+        if (e == errc{}) {
+          bool past = false;
+          (void)walk_versions<T>(c, h.w, h.data_len, past);
+        }
+      }
+    }
+    // a message with compatible members ends at its data length at the
+    // earliest: the reader skips what a newer writer added
+    // (struct_pack.hpp:302-312)
+    if (e == errc{} && !c.dry && c.tell() < h.data_len) (void)c.ignore(h.data_len - c.tell());
+  }
+  if (c.dry) drain(rd, buf);
+  return buf;
+}
+}  // namespace detail
+
+template <uint64_t conf = sp_config::DEFAULT, typename T, typename Reader>
+  requires detail::reader_t<Reader>
+[[nodiscard]] err_code deserialize_to(T &t, Reader &reader) {
+  detail::check_message_type<T>();
+  static_assert(!detail::has_views<T>(),
+                "string_view / span / trivial_view members alias the buffer they are decoded "
+                "from: decode them from a buffer, not a reader");
+  const std::vector<char> buf = detail::pull_message<conf, T>(reader);
+  std::size_t consumed;
+  return detail::decode_one<conf>(t, buf.data(), buf.size(), consumed);
+}
+template <typename T, typename Reader>
+  requires detail::reader_t<Reader>
+[[nodiscard]] expected<T> deserialize(Reader &reader) {
+  T t{};
+  if (auto e = deserialize_to(t, reader)) return make_unexpected<T>(e);
+  return t;
+}
+template <uint64_t conf, typename T, typename Reader>
+  requires detail::reader_t<Reader>
+[[nodiscard]] expected<T> deserialize(Reader &reader) {
+  T t{};
+  if (auto e = deserialize_to<conf>(t, reader)) return make_unexpected<T>(e);
+  return t;
+}
+
+// get_field from a reader: header and members 0..I (and their version
+// passes) pulled through the walker, then get_field over those bytes
+template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT, typename Field,
+          typename Reader>
+  requires detail::reader_t<Reader>
+[[nodiscard]] err_code get_field_to(Field &dst, Reader &reader) {
+  static_assert(std::is_same_v<Field, field_t<T, I>>,
+                "The dst's type is not correct. It should be as same as the T's Ith field's type");
+  static_assert(!detail::has_views<Field>(),
+                "a view member aliases the buffer it is decoded from: get it from a buffer");
+  using namespace detail;
+  const spk_layout &L = device::codec<typename msg_traits<T>::rec, conf>::layout();
+  std::vector<char> buf;
+  pull_cursor<Reader> c{reader, buf};
+  header_info h;
+  if (walk_header(c, L.fmt_one, h) == errc{}) {
+    using F = field_t<T, I>;
+    (void)get_field_walk<T, I>(
+        c, h.w, h.data_len, [&](pull_cursor<Reader> &cc) { return walk_one<F>(cc, h.w); },
+        [&](pull_cursor<Reader> &cc, bool &past) -> errc {
+          if constexpr (is_compat_v<F>)
+            return walk_compat_member<F>(cc, h.w, h.data_len, past);
+          else
+            return (void)cc, (void)past, errc{};
+        });
+  }
+  if (c.dry) drain(reader, buf);
+  return get_field_mem<T, I, conf>(dst, buf.data(), buf.size());
+}
+template <typename T, std::size_t I, uint64_t conf = sp_config::DEFAULT, typename Reader>
+  requires detail::reader_t<Reader>
+[[nodiscard]] expected<field_t<T, I>> get_field(Reader &reader) {
+  field_t<T, I> f{};
+  if (auto e = gpu::get_field_to<T, I, conf>(f, reader)) return make_unexpected<field_t<T, I>>(e);
+  return expected<field_t<T, I>>(std::move(f));
+}
+
+// struct_pack::read over a reader (user_helper.hpp:31-64): len records of T
+// at size_width, pulled by the walker, decoded as a body on the device
 template <std::size_t size_width = sizeof(uint64_t), bool ifSkip = false, typename Reader,
           typename T>
-  requires detail::seekable_reader<Reader>
+  requires detail::reader_t<Reader>
 err_code read(Reader &reader, T *t, std::size_t len) {
-  using R = detail::helper_rec_t<T>;
-  const bool exact = detail::prefix_decode_exact(device::codec<R, sp_config::DEFAULT>::layout());
-  std::size_t consumed;
-  return detail::stream_decode(reader, exact, consumed,
-                               [&](const char *d, std::size_t n, std::size_t &u) {
-                                 std::size_t pos = 0;
-                                 auto e = read_from<size_width, ifSkip>(d, n, pos, t, len);
-                                 u = pos;
-                                 return e;
-                               });
+  using namespace detail;
+  static_assert(!has_views<T>(), "views alias their buffer: read them from a buffer");
+  std::vector<char> buf;
+  pull_cursor<Reader> c{reader, buf};
+  if constexpr (is_trivially_serializable<T>()) {
+    (void)c.ignore(sizeof(T) * len);
+  } else {
+    for (std::size_t i = 0; i < len; ++i)
+      if (walk_one<T>(c, size_width) != errc{}) break;
+  }
+  if (c.dry) drain(reader, buf);
+  std::size_t pos = 0;
+  return read_from<size_width, ifSkip>(buf.data(), buf.size(), pos, t, len);
 }
 template <std::size_t size_width = sizeof(uint64_t), bool ifSkip = false, typename Reader,
           typename T>
-  requires detail::seekable_reader<Reader>
+  requires detail::reader_t<Reader>
 err_code read(Reader &reader, T &t) {
   return read<size_width, ifSkip>(reader, &t, 1);
 }

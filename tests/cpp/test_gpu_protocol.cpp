@@ -17,6 +17,7 @@
 #include <fstream>
 #include <sstream>
 #include <array>
+#include <chrono>
 #include <memory>
 #include <iterator>
 #include <map>
@@ -623,6 +624,74 @@ int main() {
     CHECK(struct_pack::gpu::serialize<std::string>(u) == struct_pack::serialize<std::string>(u));
     auto ub = struct_pack::gpu::deserialize<std::u32string>(struct_pack::serialize<std::string>(u));
     CHECK(ub.has_value() && ub.value() == u);
+  }
+  g_section = 8;
+  std::fprintf(stderr, "section 8\n");
+  // 8. view arguments alias the request buffer (the reference's views point
+  // into the buffer coro_rpc keeps alive for the call, unpacker.hpp:1135-1145):
+  // a handler holding a std::string_view across a second decode of the same
+  // type on this thread (a suspended coroutine handler) still sees its bytes
+  {
+    struct VArg {
+      int32_t id;
+      std::string_view name;
+      std::vector<std::string_view> tags;
+    };
+    const std::string r1 = struct_pack::serialize<std::string>(
+        VArg{1, "first request", {"a", "bb"}});
+    const std::string r2 = struct_pack::serialize<std::string>(
+        VArg{2, "second, longer request", {"ccc", "dddd", "e"}});
+    std::tuple<VArg> a1, a2;
+    CHECK(struct_pack_gpu_protocol::deserialize_to(a1, r1));
+    CHECK(struct_pack_gpu_protocol::deserialize_to(a2, r2));  // same type, same thread
+    const VArg &v1 = std::get<0>(a1), &v2 = std::get<0>(a2);
+    CHECK(v1.id == 1 && v1.name == "first request" && v1.tags.size() == 2 &&
+          v1.tags[0] == "a" && v1.tags[1] == "bb");
+    CHECK(v2.id == 2 && v2.name == "second, longer request" && v2.tags.size() == 3 &&
+          v2.tags[2] == "e");
+    CHECK(v1.name.data() >= r1.data() && v1.name.data() + v1.name.size() <= r1.data() + r1.size());
+    CHECK(v2.tags[1].data() >= r2.data() && v2.tags[1].data() < r2.data() + r2.size());
+    // the same from the front end: a view of a vector message aliases the input
+    std::vector<VArg> many;
+    for (int i = 0; i < 300; ++i) many.push_back(VArg{i, i % 2 ? "odd" : "even", {"x"}});
+    const std::string rm = struct_pack::serialize<std::string>(many);
+    std::vector<VArg> back;
+    CHECK(!struct_pack::gpu::deserialize_to(back, rm) && back.size() == many.size());
+    bool ok = back.size() == many.size();
+    for (std::size_t i = 0; ok && i < back.size(); ++i)
+      ok = back[i].id == (int)i && back[i].name == many[i].name && back[i].tags[0] == "x" &&
+           back[i].name.data() >= rm.data() && back[i].name.data() < rm.data() + rm.size();
+    CHECK(ok);
+    auto f = struct_pack::gpu::get_field<VArg, 1>(r2);
+    CHECK(f.has_value() && f.value() == "second, longer request" && f.value().data() > r2.data() &&
+          f.value().data() < r2.data() + r2.size());
+  }
+  // 9. small-call latency of the protocol (no size threshold: every payload
+  // takes the GPU): add(int, int) and echo_person through the reference's
+  // executor, per call, next to the reference's CPU protocol
+  {
+    auto time_calls = [](auto fn, int n) {
+      const auto t0 = std::chrono::steady_clock::now();
+      for (int i = 0; i < n; ++i) fn();
+      return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0)
+                 .count() / n;
+    };
+    std::string req;
+    struct_pack::serialize_to(req, 40, 2);
+    const std::string preq = struct_pack::serialize<std::string>(make_person(S8, 5, 40));
+    const int n = 300;
+    (void)run<add, struct_pack_gpu_protocol>(req);  // warm the codec and the device
+    (void)run<echo_person, struct_pack_gpu_protocol>(preq);
+    const double g_add = time_calls([&] { (void)run<add, struct_pack_gpu_protocol>(req); }, n);
+    const double r_add = time_calls([&] { (void)run<add, struct_pack_protocol>(req); }, n);
+    const double g_p = time_calls([&] { (void)run<echo_person, struct_pack_gpu_protocol>(preq); }, n);
+    const double r_p = time_calls([&] { (void)run<echo_person, struct_pack_protocol>(preq); }, n);
+    std::fprintf(stderr,
+                 "small-call latency (us per call): add gpu %.1f ref %.2f; echo_person gpu %.1f "
+                 "ref %.2f\n", g_add, r_add, g_p, r_p);
+    std::printf("{\"small_call_us\": {\"add_gpu\": %.2f, \"add_ref\": %.3f, "
+                "\"echo_person_gpu\": %.2f, \"echo_person_ref\": %.3f}}\n",
+                g_add, r_add, g_p, r_p);
   }
   std::printf("{\"checks\": %d, \"failures\": %d}\n", g_checks, g_fail);
   return g_fail ? 1 : 0;

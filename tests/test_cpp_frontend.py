@@ -174,3 +174,19 @@ static_assert(struct_pack::gpu::hash_matches_reference<std::bitset<64>>());
                               "-I", REF_INC + "/ylt/standalone", "-DSTRUCT_PACK_ENABLE_INT128",
                               "-DSTRUCT_PACK_ENABLE_UNPORTABLE_TYPE"])
     assert r.returncode == 0, r.stderr[-3000:]
+
+
+def test_host_walker_matches_reference_readers():
+    """The front end's host walker (include/ylt/struct_pack_gpu/walk.hpp) on
+    the CPU: for 27 record types, one-record and vector messages and every cut
+    of them, the bytes it pulls out of the reference's memory_reader and out
+    of a forward-only reader, and the bytes get_field<T, I> pulls per member,
+    equal the reference's own reader positions (oracle/_ref/test_reader_field
+    built next to the reference headers; no GPU call)."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "test_reader_field")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref/test_reader_field not built (needs /root/reference)")
+    r = subprocess.run([exe, "cpu"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["failures"] == 0 and res["checks"] > 20000

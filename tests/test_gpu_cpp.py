@@ -4,6 +4,10 @@ through libspk_codec.so, against the reference's golden bytes:
     __graft_entry__.build_cpp_tests) and compiled next to the reference
     header (oracle/_ref/test_device_codec_ref: struct_pack::errc, sp_config,
     var_int*_t are then the reference's own types);
+  * tests/cpp/test_reader_field.cpp (oracle/_ref/test_reader_field):
+    get_field<T, I> on every fixture cut at every byte, and
+    deserialize_to / get_field over the reference's memory_reader and a
+    forward-only reader, against the reference in the same process;
   * tests/cpp/test_gpu_protocol.cpp (oracle/_ref/test_gpu_protocol): the
     reference's coro_rpc handler executor running batch handlers with
     struct_pack_gpu_protocol, byte-compared with the reference's
@@ -34,7 +38,8 @@ def test_cpp_frontend_device_roundtrips():
 
 
 @pytest.mark.parametrize("name,min_checks", [("test_device_codec_ref", 40),
-                                             ("test_gpu_protocol", 25)])
+                                             ("test_gpu_protocol", 25),
+                                             ("test_reader_field", 50000)])
 def test_cpp_next_to_reference(name, min_checks):
     exe = os.path.join(REF_BIN, name)
     if not os.path.exists(exe):
