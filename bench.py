@@ -19,7 +19,13 @@ At N=1 the same line carries `extra.configs`: the other BASELINE configs
 per-kernel times (HIP events around every codec launch, spk_trace_*), the
 dominant kernel's roofline and the reference CPU baseline on the same N.
 
+At N>1 the line carries the sharded BASELINE configs as `extra.configs`
+too: C4 (10M Outer per rank) and C5 (1M request frames per rank), each
+rank its own batch (weak scaling, value = all ranks' bytes / max time).
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c2b|c3|c4|c5|cv|cm]
+`--gpus N` alone launches the N ranks (torch.distributed.run, 127.0.0.1);
+under a launcher, WORLD_SIZE must equal --gpus.
 """
 import argparse
 import json
@@ -102,7 +108,45 @@ def parse():
                     help="N>1: skip the one-message concatenation timing (concat_*)")
     ap.add_argument("--concat-records", type=int, default=8_000_000,
                     help="N>1: Rec64 records per rank of the one-message concatenation")
+    ap.add_argument("--no-shard-extra", action="store_true",
+                    help="N>1: skip the per-rank C4 / C5 weak-scaling entries")
+    ap.add_argument("--spawn-probe", action="store_true",
+                    help="(test of the launcher) each rank prints RANK/WORLD_SIZE and exits "
+                         "before touching torch")
     return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------
+# N ranks from one command: `python bench.py --gpus N` without a launcher
+# starts N fresh rank processes through torch.distributed.run and exits with
+# their status. The parent never touches a GPU (no torch import), so nothing
+# that initialised the GPU is ever replaced or forked.
+# ---------------------------------------------------------------------------
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(gpus, argv, port):
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={gpus}", "--master-addr", "127.0.0.1", "--master-port",
+            str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def spawn_ranks(gpus, argv):
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL
+    print(f"[bench] launching {gpus} ranks (torch.distributed.run)", file=sys.stderr, flush=True)
+    return subprocess.call(launcher_cmd(gpus, argv, free_port()), env=env)
+
+
+def check_world(gpus, world):
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={world} "
+                         f"ranks; run `python bench.py --gpus {gpus}` (it launches the ranks) "
+                         f"or pass --gpus equal to --nproc-per-node")
 
 
 # ---------------------------------------------------------------------------
@@ -983,6 +1027,9 @@ def compact_line(line, detail_path):
     if ex:
         cc = {}
         for name, e in ex.items():
+            if "error" in e:
+                cc[name] = {"error": str(e["error"])[:100]}
+                continue
             rf = e.get("roofline") or {}
             cb = e.get("cpu_baseline") or {}
             d = {"ms": e.get("ms_per_step"), "gib_s": e.get("value"),
@@ -1001,12 +1048,18 @@ def compact_line(line, detail_path):
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    check_world(args.gpus, world)
+    if args.spawn_probe:
+        print(json.dumps({"rank": rank, "world": world, "local": local}), flush=True)
+        return
+    import torch
+    import torch.distributed as dist
+
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     # one rank per GPU; the modulo only matters when rehearsing several ranks
@@ -1031,6 +1084,18 @@ def main():
     if rank == 0:  # progress on stderr (the JSON line stays the only stdout line)
         print(f"[bench] {args.config}: {head['ms_per_step']} ms/step", file=sys.stderr, flush=True)
     extra = {}
+    if world > 1 and not args.no_shard_extra and args.config == "c2":
+        # the sharded BASELINE configs, weak scaling: every rank its own 10M
+        # Outer (C4) / 1M request frames (C5), no data-path collective
+        for cfg in ("c4", "c5"):
+            try:
+                extra[cfg] = run_config(cfg, args, torch, dist, world, rank, dev,
+                                        args.extra_steps, 2, 0.5, cpu=False)
+            except Exception as e:  # never lose the headline line
+                extra[cfg] = {"error": f"{type(e).__name__}: {e}"}
+            if rank == 0:
+                print(f"[bench] {cfg} x{world}: {extra[cfg].get('ms_per_step')} ms/step",
+                      file=sys.stderr, flush=True)
     if world == 1 and not args.no_extra and args.config == "c2":
         for cfg in EXTRA:
             extra[cfg] = run_config(cfg, args, torch, dist, world, rank, dev, args.extra_steps,
