@@ -4,7 +4,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-IFS=';' read -ra EV <<< "${ENVS:--;SPK_FUSED=1}"
+IFS=';' read -ra EV <<< "${ENVS:--}"
 for r in $(seq ${REPS:-2}); do
   for e in "${EV[@]}"; do
     for c in ${CONFIGS:-c3 c4}; do

@@ -368,12 +368,14 @@ def mutations(wire_len, rng):
 
 
 def make_errs(tmp):
-    rng = random.Random(1234)
     out = []
     for eb in ERR_BASES + [(r, n, p, "default", 0, w) for w, r, n, p in XERR_BASES]:
         cm, n, param, conf = eb[:4]
         width = eb[4] if len(eb) > 4 else 0
         writer = eb[5] if len(eb) > 5 else cm
+        # each base's mutations from an RNG of its own key: adding a base never
+        # changes the mutation sets of the others
+        rng = random.Random(f"{cm}|{n}|{param}|{conf}|{width}|{writer}")
         case = cm[:-2]
         seed = SEED[case]
         wire = os.path.join(tmp, "ewire.bin")
@@ -420,7 +422,15 @@ def make_errs(tmp):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--big", action="store_true", help="also the full-size configs")
+    ap.add_argument("--errs-only", action="store_true", help="rewrite errs.json only")
     args = ap.parse_args()
+    if args.errs_only:
+        with tempfile.TemporaryDirectory() as tmp:
+            errs = make_errs(tmp)
+        with open(os.path.join(HERE, "errs.json"), "w") as f:
+            json.dump(errs, f, indent=0)
+        print(f"{sum(len(e['tests']) for e in errs)} mutation tests")
+        return
     if not os.path.exists(GEN):
         sys.exit(f"{GEN} missing: run `make -C oracle ref` (needs /root/reference)")
     kat = json.loads(subprocess.run([GEN, "kat"], check=True, capture_output=True,

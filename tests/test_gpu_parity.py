@@ -378,8 +378,9 @@ def test_speculation_caps_mispredicted(tail):
     longer ("long": 100-3000 B, so no true record fits the caps; "mixed":
     every 7th). The speculative walks reject the true records, chunks with no
     start under the caps are searched again without them, the resolution
-    walks never see the caps: bit-exact with the oracle. The caps are a
-    build option (SPK_SCAP, off by default). The message's 2-byte counts
+    walks never see the caps: bit-exact with the oracle. The caps are on by
+    default (SPK_SCAP = 5: on every flat layout's speculative walks, and on
+    the candidate screen of varint layouts, below). The message's 2-byte counts
     screen random string bytes weakly (one in 16 passes); K1's speculative
     walks check SPK_SPEC_PAST_W2 = 5 records past their chunk at that width
     and a tile whose chunk 0 holds no start takes its first speculated one,
@@ -413,6 +414,49 @@ def test_speculation_caps_mispredicted(tail):
     print(f"{tail}: {len(exp) / 1e6:.1f} MB decoded in {min(ts):.3f} ms, tiles repaired "
           f"{r.tiles_repaired}, sequential {r.tiles_sequential}")
     assert min(ts) < 3.0, ts
+
+
+@pytest.mark.parametrize("tail", ["long", "mixed", "uniform"])
+def test_varint_screen_caps_mispredicted(tail):
+    """The same for a varint layout (Var: var_int32_t, string, var_uint64_t,
+    double, var_int64_t, var_uint32_t), where the caps also bound K1's
+    candidate screen (SPK_SCAP bit 2): the first records' strings are 0-2
+    bytes, later ones 100-3000 (every one, or every 7th), so the screen under
+    the caps rejects every true start and the chunk is searched again without
+    them. Bit-exact with the oracle, bounded time."""
+    cd = codec_for("var")
+    rng = np.random.default_rng(29)
+    n = 30000
+    lens = rng.integers(0, 3, n)
+    if tail == "long":
+        lens[64:] = rng.integers(100, 3000, n - 64)
+    elif tail == "mixed":
+        lens[64::7] = rng.integers(100, 3000, len(lens[64::7]))
+    else:  # (no misprediction: the same strings from the first record on)
+        lens[:] = rng.integers(100, 3000, n)
+    _, recs, _ = synth.make_batch("var", n, 0x5EED000C, 16)
+    recs["s.n"] = lens
+    recs["s.off"] = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    heaps = [rng.integers(0, 256, int(lens.sum()), dtype=np.uint8).view(np.int8)]
+    exp, _, _ = H.oracle_encode(cd.L, C.SPK_MODE_VECTOR, recs, heaps)
+    w = wire_dev(exp)
+    res, back, _ = cd.deserialize(w, C.SPK_MODE_VECTOR)
+    assert res.errc == 0 and res.count == n and res.consumed == len(exp)
+    assert back.recs.cpu().numpy().tobytes() == np.ascontiguousarray(recs).view(np.uint8).tobytes()
+    assert back.heaps[0][:len(heaps[0])].cpu().numpy().tobytes() == heaps[0].tobytes()
+    ts = []
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        cd.deserialize_to(back, w, C.SPK_MODE_VECTOR)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    assert cd.result().errc == 0
+    r = cd.result()
+    print(f"var {tail}: {len(exp) / 1e6:.1f} MB decoded in {min(ts):.3f} ms, tiles repaired "
+          f"{r.tiles_repaired}, sequential {r.tiles_sequential}")
+    assert min(ts) < 12.0, ts
 
 
 def test_screen_defeating_payload_bounded_time():

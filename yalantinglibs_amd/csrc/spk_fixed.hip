@@ -96,10 +96,6 @@ __global__ __launch_bounds__(kCopyThreads) void shift_copy_kernel(
   shift_body(reinterpret_cast<v4u *>(d + head), s + head, body >> 4);
 }
 
-#ifndef SPK_COPY_ROUNDS  // (A/B) shift_copy grid in resident rounds of blocks (0: 32 Ki cap)
-// (off: C2 step 4.36 ms with the 32 Ki cap, 4.74 with one resident round, 4.60 with four)
-#define SPK_COPY_ROUNDS 0
-#endif
 __global__ __launch_bounds__(kCopyThreads) void shift_copy_kernel(
     uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
     const CopyJob *__restrict__ job, const uint8_t *__restrict__ hdr);
@@ -108,17 +104,9 @@ static unsigned copy_grid(uint64_t max_bytes) {
   uint64_t blocks = (tiles + (kCopyThreads / 64) - 1) / (kCopyThreads / 64);
   // 32 Ki blocks (128 Ki waves) then grid-stride: the probe's best point
   // (scripts/probes/copy_probe.hip: 16 chunks in flight per lane, 6.1-6.2 TB/s)
+  // (a whole number of resident rounds of blocks instead was measured slower:
+  // C2 step 4.36 -> 4.60-4.74 ms)
   if (blocks > 32768) blocks = 32768;
-  if (SPK_COPY_ROUNDS) {  // a whole number of resident rounds
-    int dev = 0, ncu = 0, nb = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, shift_copy_kernel, kCopyThreads, 0) ==
-            hipSuccess && nb > 0 && ncu > 0) {
-      const uint64_t round = (uint64_t)nb * ncu * SPK_COPY_ROUNDS;
-      if (blocks > round) blocks = round;
-    }
-  }
   if (blocks < 1) blocks = 1;
   return (unsigned)blocks;
 }
@@ -386,10 +374,6 @@ static unsigned elem_grid(uint64_t items, unsigned threads = 256) {
 constexpr int kMsgThreads = 256;
 constexpr uint32_t kMsgStageMax = 32768;  // staging bytes per block
 constexpr uint32_t kStagePer = 5;  // 16-B staging loads in flight per lane (decode)
-#ifndef SPK_MSG_PREFETCH  // (A/B) mode-B fixed decode: the next group's wire loaded during this one
-// (off: C2b decode 2.90 -> 3.94 ms with it)
-#define SPK_MSG_PREFETCH 0
-#endif
 
 struct MsgLdsArgs {
   spk_msgfmt fmt;   // decode only
@@ -500,7 +484,6 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
   extern __shared__ v4u smem_v4[];
   uint8_t *stage = reinterpret_cast<uint8_t *>(smem_v4);
   __shared__ uint64_t s_lo[kMsgThreads / 64], s_hi[kMsgThreads / 64];
-  __shared__ uint64_t s_lo2[kMsgThreads / 64], s_hi2[kMsgThreads / 64];  // the next group's
   __shared__ uint64_t s_pay[kMsgThreads];  // payload position (staged: LDS offset)
   const uint32_t tid = threadIdx.x;
   const uint32_t S = a.stride;
@@ -520,13 +503,6 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
   };
   uint64_t b_nx = 0, e_nx = 0;
   bounds(blockIdx.x, b_nx, e_nx);
-  // the next group's wire span, loaded into registers while this group is
-  // parsed and written (SPK_MSG_PREFETCH): its loads overlap this group's
-  // LDS reads and stores instead of following them
-  v4u pv[kStagePer];
-  bool pf = false;
-  uint64_t pf_lo = 0;
-  uint32_t pf_nc = 0;
   for (uint64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
     const uint64_t first = g * a.R;
     const uint32_t nR = (uint32_t)((N - first) < a.R ? (N - first) : a.R);
@@ -561,13 +537,7 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
       const uint32_t nb = (uint32_t)(hi - lo);
       const uint64_t full = (a.wire_len - lo) / 16;  // 16-B chunks inside the wire
       const uint32_t nc = (nb + 15) / 16;
-      if (pf && pf_lo == lo && pf_nc == nc) {  // prefetched during the previous group
-#pragma unroll
-        for (uint32_t k = 0; k < kStagePer; ++k) {
-          const uint32_t c = tid + k * kMsgThreads;
-          if (c < nc) reinterpret_cast<v4u *>(stage)[c] = pv[k];
-        }
-      } else if (nc <= full) {
+      if (nc <= full) {
         // each lane issues kStagePer 16-B loads before its LDS writes (a
         // load / store loop waits one load latency per 4 KiB); one round
         // covers 256 68-B messages
@@ -596,50 +566,7 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
         }
       }
     }
-    pf = false;
-    const uint64_t g2 = g + gridDim.x;
-    if (SPK_MSG_PREFETCH && g2 < ngroups) {  // the next group's span (block min / max)
-      const uint64_t first2 = g2 * a.R;
-      const uint32_t nR2 = (uint32_t)((N - first2) < a.R ? (N - first2) : a.R);
-      bool inr2 = false;
-      uint64_t b2 = b_nx;
-      if (tid < nR2) {
-        inr2 = e_nx >= b_nx && e_nx <= a.wire_len && e_nx - b_nx >= a.prefix;
-        b2 += a.prefix;
-      }
-      uint64_t mn2 = inr2 ? b2 : ~0ull, mx2 = inr2 ? e_nx : 0;
-      for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t on = __shfl_xor(mn2, o), ox = __shfl_xor(mx2, o);
-        mn2 = on < mn2 ? on : mn2;
-        mx2 = ox > mx2 ? ox : mx2;
-      }
-      if ((tid & 63) == 0) {
-        s_lo2[tid >> 6] = mn2;
-        s_hi2[tid >> 6] = mx2;
-      }
-    }
     __syncthreads();
-    if (SPK_MSG_PREFETCH && g2 < ngroups) {
-      uint64_t blo2 = s_lo2[0], hi2 = s_hi2[0];
-      for (int k = 1; k < kMsgThreads / 64; ++k) {
-        blo2 = s_lo2[k] < blo2 ? s_lo2[k] : blo2;
-        hi2 = s_hi2[k] > hi2 ? s_hi2[k] : hi2;
-      }
-      const uint64_t lo2 = blo2 & ~15ull;
-      if (blo2 != ~0ull && hi2 - lo2 <= a.cap) {
-        const uint32_t nc2 = (uint32_t)((hi2 - lo2 + 15) / 16);
-        if (nc2 <= kStagePer * kMsgThreads && nc2 <= (a.wire_len - lo2) / 16) {
-#pragma unroll
-          for (uint32_t k = 0; k < kStagePer; ++k) {
-            const uint32_t c = tid + k * kMsgThreads;
-            if (c < nc2) pv[k] = *reinterpret_cast<const v4u_unaligned *>(wire + lo2 + 16 * (uint64_t)c);
-          }
-          pf = true;
-          pf_lo = lo2;
-          pf_nc = nc2;
-        }
-      }
-    }
     if (tid < nR) {
       const uint64_t i = first + tid;
       int32_t ec = SPK_ERRC_OK;

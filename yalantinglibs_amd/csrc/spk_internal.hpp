@@ -19,6 +19,11 @@ constexpr int kWave = 64;
 // Heaps the flat-record kernels (spk_var.hip) carry per record; layouts with
 // more run the op-list interpreter (spk_nested.hip).
 #define SPK_FLAT_SPANS 8u
+// diagnostics build (-DSPK_DIAG=1): SPK_TILE_DBG switches the tile kernels'
+// diagnostic bits at run time; a release build never reads the environment
+#ifndef SPK_DIAG
+#define SPK_DIAG 0
+#endif
 
 // Kernel-argument copy of the descriptor, without the literal tables (the
 // type literal lives in the device header buffer produced by the plan).

@@ -1059,25 +1059,6 @@ static CWs cws_layout(uint64_t wire_len, uint32_t n_heaps) {
   return f;
 }
 
-// SPK_NEST_DIRECT=1: nested VECTOR encodes store bytes straight to HBM
-// (nest_write) instead of through LDS windows (nest_write_win) (A/B)
-static bool nest_direct_write() {
-  static const bool v = [] {
-    const char *e = getenv("SPK_NEST_DIRECT");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
-// SPK_NEST_CHUNKED=1: VECTOR decodes of nested layouts take the chunked
-// interpreter below instead of the tile decoder (A/B)
-static bool nest_chunked() {
-  static const bool v = [] {
-    const char *e = getenv("SPK_NEST_CHUNKED");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
 
 size_t nested_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len) {
   const NLayout N = make_nlayout(L);
@@ -1425,12 +1406,10 @@ __global__ __launch_bounds__(256) void nest_write(NEnc e, const uint8_t *__restr
 // (its 256 records at their scanned offsets) is assembled in an LDS window,
 // kNEncWin bytes at a time (a lane writes the part of its record inside the
 // window), and flushed with aligned 16-B stores; unaligned byte stores
-// straight to HBM cost several times their bytes in write traffic.
+// straight to HBM cost several times their bytes in write traffic. (Staging
+// the block's records in LDS as well was measured slower: cm 2.86 -> 4.04 ms,
+// the LDS halves the occupancy.)
 constexpr uint32_t kNEncWin = 24 * 1024;
-#ifndef SPK_NWIN_STAGE  // (A/B) nest_write_win stages the block's records in LDS (bytes; 0: off)
-// (off: cm nest_write_win 2.86 -> 4.04 ms with 24 KiB staged, the LDS halves the occupancy)
-#define SPK_NWIN_STAGE 0
-#endif
 template <int D>
 __global__ __launch_bounds__(256) void nest_write_win(NEnc e, const uint8_t *__restrict__ recs,
                                                       const uint64_t *__restrict__ off,
@@ -1439,11 +1418,6 @@ __global__ __launch_bounds__(256) void nest_write_win(NEnc e, const uint8_t *__r
                                                       uint8_t *__restrict__ out, uint64_t out_cap) {
   __shared__ NLayout N;
   __shared__ __align__(16) uint8_t lds[kNEncWin];
-#if SPK_NWIN_STAGE
-  // the block's records with coalesced 8-B loads when they fit (as nest_size):
-  // the interpreter reads a record field by field, one dependent load per op
-  __shared__ __align__(16) uint8_t rs[SPK_NWIN_STAGE];
-#endif
   n_stage(N, e.N);
   const NCtl *ctl = reinterpret_cast<const NCtl *>(ws + kWsCtl);
   const uint64_t mx = ctl->maxc > e.n ? ctl->maxc : e.n;
@@ -1462,16 +1436,6 @@ __global__ __launch_bounds__(256) void nest_write_win(NEnc e, const uint8_t *__r
   const uint64_t q0 = i < e.n ? hl + off[i] : 0;
   const uint64_t q1 = i < e.n ? (i + 1 < e.n ? hl + off[i + 1] : hl + tot0) : 0;
   const uint8_t *rec = recs + i * N.stride;
-#if SPK_NWIN_STAGE
-  if (256ull * N.stride <= SPK_NWIN_STAGE && !(N.stride & 7) && !((uintptr_t)recs & 7)) {
-    const uint64_t *src = reinterpret_cast<const uint64_t *>(recs + r0 * N.stride);
-    uint64_t *dst = reinterpret_cast<uint64_t *>(rs);
-    const uint64_t words = (rend - r0) * N.stride / 8;
-    for (uint64_t k = threadIdx.x; k < words; k += 256) dst[k] = src[k];
-    __syncthreads();
-    rec = rs + (i - r0) * N.stride;
-  }
-#endif
   for (uint64_t wlo = g0 & ~15ull; wlo < g1; wlo += kNEncWin) {
     const NWin W{lds, wlo, wlo + kNEncWin < g1 ? wlo + kNEncWin : g1};
     if (i < e.n && q0 < W.hi && q1 > W.lo) n_write<D>(N, rec, e.heaps, w, W, q0, 0, N.n_ops, true);
@@ -1645,8 +1609,8 @@ hipError_t launch_nested_encode(const spk_layout *L, int mode, uint64_t n, const
   }
   uint8_t *ws = (uint8_t *)d_ws;
   uint64_t *a, *part, nb;
-  const bool vec_win = mode == SPK_MODE_VECTOR && !e.N.n_ranks && !fixed_w && !nest_direct_write();
-  const bool msg_win = mode == SPK_MODE_MESSAGES && !nest_direct_write();
+  const bool vec_win = mode == SPK_MODE_VECTOR && !e.N.n_ranks && !fixed_w;
+  const bool msg_win = mode == SPK_MODE_MESSAGES;
   if (vec_win || msg_win) {
     hipError_t er;
     if (!e.N.n_ranks) {
@@ -2283,8 +2247,7 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
                                 hipStream_t s, uint32_t body_w, uint64_t body_n,
                                 const uint64_t *d_msg_ends) {
   // (the tile decoder counts heap slots in 32 bits: wires below 4 GiB)
-  if (mode == SPK_MODE_VECTOR && var_nested_tile_ok(L) && wire_len < (1ull << 32) - 4096 &&
-      !nest_chunked())
+  if (mode == SPK_MODE_VECTOR && var_nested_tile_ok(L) && wire_len < (1ull << 32) - 4096)
     return launch_var_nested_decode(L, d_wire, wire_len, d_recs, rec_cap, d_heaps, heap_caps,
                                     d_res, d_ws, s, body_w, body_n);
   NDec a = {};

@@ -48,9 +48,6 @@
 #ifndef SPK_ESPLIT
 #define SPK_ESPLIT 2
 #endif
-#ifndef SPK_K4_LANE   // (A/B) flat K4: one lane per chunk emits its records in order
-#define SPK_K4_LANE 0
-#endif
 #ifndef SPK_NT_REACH  // bytes K1's resolution walks of nested records may cover
 #define SPK_NT_REACH 4096
 #endif
@@ -78,16 +75,6 @@
 #endif
 #ifndef SPK_NT_SCR2   // nested candidate starts screened on a second count
 #define SPK_NT_SCR2 1
-#endif
-#ifndef SPK_WPAD  // (A/B) LDS windows padded per 256-B row (bank-conflict-free chunk reads)
-// (off: C3 / C4 / cv / cm K1 0.244 / 0.364 / 1.93 / 5.61 -> 0.269 / 0.390 /
-// 2.07 / 6.63 ms with it: the conflicts cost less than the address arithmetic)
-#define SPK_WPAD 0
-#endif
-#ifndef SPK_NT_UNIFORM  // (A/B) walk programs run wave-uniform (nt_walk_u) instead of per lane
-// (off: cm K1 5.6 -> 9.1 ms with it -- every loop runs to its longest trip
-// count and the uniform state adds to K1's SGPR spills)
-#define SPK_NT_UNIFORM 0
 #endif
 
 namespace spk {
@@ -251,6 +238,20 @@ __device__ __forceinline__ void vi_store(const spk_op &op, uint8_t *rec, uint64_
     *reinterpret_cast<uint32_t *>(rec + op.rec_off) = (uint32_t)v;
   else
     *reinterpret_cast<uint64_t *>(rec + op.rec_off) = v;
+}
+// LEB128 from the 8 bytes b (little-endian) when it ends inside them: the
+// terminator is the first byte without its high bit, the value gathers the
+// 7-bit groups; 0 when all 8 bytes continue (the caller reads on)
+__device__ __forceinline__ uint32_t vi_decode8(uint64_t b, uint64_t *v) {
+  const uint64_t t = ~b & 0x8080808080808080ull;
+  if (!t) return 0;
+  const uint32_t l = ((uint32_t)__builtin_ctzll(t) >> 3) + 1;
+  uint64_t m = b & 0x7F7F7F7F7F7F7F7Full;
+  if (l < 8) m &= (1ull << (8 * l)) - 1;
+  *v = (m & 0x7Full) | ((m >> 1) & (0x7Full << 7)) | ((m >> 2) & (0x7Full << 14)) |
+       ((m >> 3) & (0x7Full << 21)) | ((m >> 4) & (0x7Full << 28)) |
+       ((m >> 5) & (0x7Full << 35)) | ((m >> 6) & (0x7Full << 42)) | ((m >> 7) & (0x7Full << 49));
+  return l;
 }
 struct WireBytes {
   const uint8_t *wire;
@@ -584,10 +585,6 @@ constexpr unsigned kYSplit = 8;  // blocks sharing one write block's output
 // flight per lane, head/tail bytes by single lanes. (A block-wide flattened
 // chunk index over all payloads, searched per chunk, measured 13 % slower on
 // C5's vector<int> messages.)
-#ifndef SPK_COPY_PAIR  // (A/B) wave_copy_all takes two payloads per step (loads of both in flight)
-// (off: C5 var_encode_write 0.37 -> 9.6 ms per launch, var_msg_write 0.34 -> 0.54)
-#define SPK_COPY_PAIR 0
-#endif
 // one payload's head / tail bytes (single lanes) and its 16-B chunk count
 __device__ __forceinline__ uint64_t seg_edges(const BigSeg &e, uint32_t lane, uint64_t *head) {
   uint64_t h = (16 - ((uintptr_t)e.dptr & 15)) & 15;
@@ -602,39 +599,6 @@ __device__ __forceinline__ void wave_copy_all(const BigSeg *B, uint32_t m, uint3
                                               uint32_t nparts) {
   const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const uint32_t gw = part * nw + (threadIdx.x >> 6), W = nparts * nw;
-  if constexpr (SPK_COPY_PAIR) {
-    // payloads k and k + W together: their descriptors and the first
-    // kCoopU / 2 chunks per lane of each in flight at once (a C5 vector<int>
-    // payload is ~4 KiB = 4 chunks per lane: one payload at a time left half
-    // the loads of a step unused and paid a descriptor load latency each)
-    constexpr int H = kCoopU / 2;
-    for (uint32_t k = gw; k < m; k += 2 * W) {
-      const bool two = k + W < m;
-      const BigSeg e0 = B[k];
-      BigSeg e1 = {0, nullptr, nullptr, 0};
-      if (two) e1 = B[k + W];
-      uint64_t h0, h1 = 0;
-      const uint64_t n0 = seg_edges(e0, lane, &h0);
-      const uint64_t n1 = two ? seg_edges(e1, lane, &h1) : 0;
-      const uint8_t *s0 = e0.src + h0, *s1 = e1.src + h1;
-      uint8_t *d0 = e0.dptr + h0, *d1 = e1.dptr + h1;
-      const uint64_t nmax = n0 > n1 ? n0 : n1;
-      for (uint64_t c0 = lane; c0 < nmax; c0 += 64 * H) {
-        v4u_t v[2 * H];
-#pragma unroll
-        for (int u = 0; u < H; ++u) {
-          if (c0 + 64 * u < n0) v[u] = *reinterpret_cast<const v4u_una *>(s0 + 16 * (c0 + 64 * u));
-          if (c0 + 64 * u < n1) v[H + u] = *reinterpret_cast<const v4u_una *>(s1 + 16 * (c0 + 64 * u));
-        }
-#pragma unroll
-        for (int u = 0; u < H; ++u) {
-          if (c0 + 64 * u < n0) *reinterpret_cast<v4u_t *>(d0 + 16 * (c0 + 64 * u)) = v[u];
-          if (c0 + 64 * u < n1) *reinterpret_cast<v4u_t *>(d1 + 16 * (c0 + 64 * u)) = v[H + u];
-        }
-      }
-    }
-    return;
-  }
   for (uint32_t k = gw; k < m; k += W) {
     const BigSeg e = B[k];
     uint64_t head = (16 - ((uintptr_t)e.dptr & 15)) & 15;
@@ -1535,26 +1499,14 @@ struct VecBufs {
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
-// LDS window layout. Lane l's chunk is the window's 256-B row l, and the
-// walkers' lanes read at similar offsets of their own rows (the candidate
-// screen at the same offset in every row): with rows 64 dwords apart every
-// such read of a 32-lane half lands on one bank (a 32-way conflict). With
-// SPK_WPAD a row takes kRowDw = 69 dwords (69 is odd: the 32 rows of a half
-// fall on 32 banks) and its last 5 dwords repeat the next row's first 5, so
-// any read of up to 5 consecutive dwords starting inside a row stays in that
-// row's slot. Positions are window-relative bytes o: dword (o >> 8) * kRowDw +
-// ((o >> 2) & 63), byte (o >> 8) * 4 * kRowDw + (o & 255).
-constexpr uint32_t kRowDw = SPK_WPAD ? 69u : 64u;
-__device__ __forceinline__ uint32_t win_dw(uint32_t o) {
-  return SPK_WPAD ? (o >> 8) * kRowDw + ((o >> 2) & 63u) : o >> 2;
-}
-__device__ __forceinline__ uint32_t win_b(uint32_t o) {
-  return SPK_WPAD ? (o >> 8) * (4u * kRowDw) + (o & 255u) : o;
-}
+// LDS window layout: window-relative byte o is dword o >> 2, byte o. (Rows
+// padded to 69 dwords, so that the candidate screen's same-offset reads of a
+// 32-lane half fall on 32 banks, were measured slower in round 4: the
+// conflicts cost less than the address arithmetic.)
+__device__ __forceinline__ uint32_t win_dw(uint32_t o) { return o >> 2; }
+__device__ __forceinline__ uint32_t win_b(uint32_t o) { return o; }
 // 16-B slots of LDS a window of nv staged 16-B slots takes (+ the read-past slack)
-__host__ __device__ constexpr uint32_t win_slots(uint32_t nv) {
-  return SPK_WPAD ? (((nv + 15) / 16) * kRowDw + 3) / 4 + 2 : nv + 1;
-}
+__host__ __device__ constexpr uint32_t win_slots(uint32_t nv) { return nv + 1; }
 
 // Count-field reader over a chunk's LDS window: bytes [cs, wend) of the wire
 // are staged in LDS; reads past the window go to global memory.
@@ -1584,23 +1536,18 @@ struct WinReader {
   // once -- the terminator is the first byte without its high bit, the value
   // gathers the 7-bit groups -- and the byte loop for longer / edge varints
   __device__ __forceinline__ uint32_t vread(uint64_t x, uint64_t len, uint64_t *v) const {
+    uint32_t l = 0;
     if (x + 12 <= wend) {
       const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = win_dw(o);
       const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2];
-      const uint64_t b = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
-                         ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
-      const uint64_t t = ~b & 0x8080808080808080ull;
-      if (t) {
-        const uint32_t l = ((uint32_t)__builtin_ctzll(t) >> 3) + 1;
-        uint64_t m = b & 0x7F7F7F7F7F7F7F7Full;
-        if (l < 8) m &= (1ull << (8 * l)) - 1;
-        *v = (m & 0x7Full) | ((m >> 1) & (0x7Full << 7)) | ((m >> 2) & (0x7Full << 14)) |
-             ((m >> 3) & (0x7Full << 21)) | ((m >> 4) & (0x7Full << 28)) |
-             ((m >> 5) & (0x7Full << 35)) | ((m >> 6) & (0x7Full << 42)) |
-             ((m >> 7) & (0x7Full << 49));
-        return l;
-      }
+      l = vi_decode8((uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
+                         ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32), v);
+    } else if (x >= wend && x + 8 <= len) {
+      // past the window: the 8 bytes in one load, not one dependent byte load
+      // each (speculative walks of varint records leave the window)
+      l = vi_decode8(*reinterpret_cast<const u64_unaligned *>(wire + x), v);
     }
+    if (l) return l;
     auto bf = [this](uint64_t q) { return byte(q); };
     return vi_read(bf, x, len, v);
   }
@@ -2196,108 +2143,6 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
   return (uint64_t)(p + N.wp_tail - (uint32_t)pos);
 }
 
-// nt_walk with the walk program's instruction wave-uniform: every lane of the
-// wave is at the same instruction, so the fetch and the dispatch are scalar
-// (nt_walk's lanes each fetch and branch on their own instruction, and the
-// wave executes the union of the branches under exec masks). A loop runs until
-// its longest trip count ends; a lane whose count ended, or whose walk
-// failed, sits it out masked (act). The enclosing loops' counts and act flags
-// are per-lane LDS frames at the (uniform) depth. Same results and heap use as
-// nt_walk; the END instruction's arg is its loop's body start.
-template <typename Rd>
-__device__ uint64_t nt_walk_u(const NTLayout &N, const Rd &rd, uint64_t pos, uint64_t lim64,
-                              bool bounded, uint32_t maxel) {
-  const uint64_t bad = bounded ? kLenLimit : 0;
-  uint32_t *const U = nt_used();
-  uint32_t *const F = nt_frames();
-  const uint32_t w = rd.w;
-  const uint64_t wmask = w >= 8 ? ~0ull : (1ull << (8 * w)) - 1;
-  const uint32_t lim = (uint32_t)lim64;
-  const uint32_t nw = (uint32_t)__builtin_amdgcn_readfirstlane((int)N.wp_n);
-  uint32_t p = (uint32_t)pos;
-  bool act = true, failed = false;
-  uint32_t rem = 0;      // elements left in the innermost loop (this lane)
-  uint32_t pc = 0, d = 0;  // wave-uniform
-  while (pc < nw) {
-    const uint32_t ix = (uint32_t)__builtin_amdgcn_readfirstlane((int)N.wp[pc].x);
-    const uint32_t iy = (uint32_t)__builtin_amdgcn_readfirstlane((int)N.wp[pc].y);
-    const uint32_t op = ix & 7u, h = (ix >> 3) & 31u, arg = ix >> 8;
-    if (act) {
-      if (lim - p < iy) {
-        act = false;
-        failed = true;
-      } else {
-        p += iy;
-      }
-    }
-    bool pop = false;
-    if (op == WP_END) {
-      if (act) act = --rem != 0;
-      if (__ballot(act)) {
-        pc = arg;
-        continue;
-      }
-      ++pc;
-      pop = true;
-    } else {
-      const bool opt = op == WP_OPT;
-      const uint32_t cw = opt ? 1u : w;
-      uint64_t c = 0;
-      if (act) {
-        if (lim - p < cw) {
-          act = false;
-          failed = true;
-        } else {
-          c = rd.count_at32(p, wmask, opt);
-          p += cw;
-          atomicAdd(U + 64 * h, (uint32_t)c);
-        }
-      }
-      if (op == WP_ARR) {
-        if (act && (c > lim - p || c > maxel)) {  // elements take >= 1 byte
-          act = false;
-          failed = true;
-        }
-        if (d) {
-          F[64 * (2 * (d - 1))] = rem;
-          F[64 * (2 * (d - 1) + 1)] = act ? 1u : 0u;
-        }
-        ++d;
-        rem = (uint32_t)c;
-        act = act && c != 0;
-        if (__ballot(act)) {
-          ++pc;
-        } else {
-          pc = arg;  // no lane enters the loop
-          pop = true;
-        }
-      } else {
-        // SPAN: the payload must be there; OPTION: an unreadable value leaves the reader
-        if (act) {
-          if (!opt && (c > lim - p || c * arg > lim - p)) {
-            act = false;
-            failed = true;
-          } else if (!opt || (c && lim - p >= arg)) {
-            p += (uint32_t)(c * arg);
-          }
-        }
-        ++pc;
-      }
-    }
-    if (pop) {  // the enclosing loop's frame back
-      --d;
-      if (d) {
-        rem = F[64 * (2 * (d - 1))];
-        act = F[64 * (2 * (d - 1) + 1)] != 0 && !failed;
-      } else {
-        act = !failed;
-      }
-    }
-    if (!__ballot(!failed)) break;
-  }
-  if (failed || lim - p < N.wp_tail) return bad;
-  return (uint64_t)(p + N.wp_tail - (uint32_t)pos);
-}
 
 // wlen_rd for NS = -2: the record's wire length (0: the path fails here) and
 // its heap use per heap; reach > 0 bounds a speculative walk (past it: longer
@@ -2314,8 +2159,7 @@ __device__ uint64_t nt_len(const Rd &rd, uint64_t len, uint64_t pos, uint64_t *c
   const uint64_t lim = reach && reach < len - pos ? pos + reach : len;
   uint64_t p = pos;
   if constexpr (SIMPLE) {
-    const uint64_t l = SPK_NT_UNIFORM ? nt_walk_u(N, rd, pos, lim, lim < len, maxel)
-                                      : nt_walk(N, rd, pos, lim, lim < len, maxel);
+    const uint64_t l = nt_walk(N, rd, pos, lim, lim < len, maxel);
     if (l == kLenLimit) return kLenLimit;
     p += l;
   } else {
@@ -2726,29 +2570,8 @@ __device__ __forceinline__ bool screen_one(const WalkProg &P, const Rd &rd, uint
 }
 
 
-// staged 16-B slot v of a window (win_dw layout): its 4 dwords, and slots 0 / 1
-// of a row also into the previous row's 5 repeated dwords
-__device__ __forceinline__ void win_put(v4u_t *win, uint32_t v, const v4u_t &x) {
-  if constexpr (!SPK_WPAD) {
-    win[v] = x;
-  } else {
-    lds_u32 *d = (lds_u32 *)win;
-    const uint32_t r = v >> 4, k = v & 15u, b = r * kRowDw + 4u * k;
-    d[b] = x.x;
-    d[b + 1] = x.y;
-    d[b + 2] = x.z;
-    d[b + 3] = x.w;
-    if (r && k < 2) {
-      const uint32_t e = b - kRowDw + 64u;  // the previous row's repeat of dwords 4k..
-      d[e] = x.x;
-      if (k == 0) {
-        d[e + 1] = x.y;
-        d[e + 2] = x.z;
-        d[e + 3] = x.w;
-      }
-    }
-  }
-}
+// staged 16-B slot v of a window
+__device__ __forceinline__ void win_put(v4u_t *win, uint32_t v, const v4u_t &x) { win[v] = x; }
 
 // Stage tile t's bytes (+ extension) in this wave's LDS window; reader over it.
 struct TileView {
@@ -3205,9 +3028,6 @@ __device__ __forceinline__ void vec_tile_spec_body(const DecArgs &a, const WalkP
   }
 }
 
-#ifndef SPK_K1_LDS_PROG  // varint K1 reads its walk program from LDS
-#define SPK_K1_LDS_PROG 1
-#endif
 #ifndef SPK_WSPEC  // 1: K1 of the nested walk program per count width; 2: every layout
 #define SPK_WSPEC 2   // (2: C4 K1 -15 %, C3 -13 %, cv -5 % against 1, same-box A/B)
 #endif
@@ -3220,22 +3040,19 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_spec(DecArgs a, WalkP
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t t = (uint64_t)blockIdx.x * kDecWaves + wv;
-  if (t >= TB.ntiles || !vec_live(c)) return;  // wave-uniform
-#if SPK_K1_LDS_PROG
   // varint layouts with the speculation caps: the walk program from LDS (the
   // compiler otherwise copied the by-value argument into scratch memory and
-  // read it from there: 264 B per lane)
-  // (SPK_K1_LDS_PROG=2: every flat layout, A/B -- C3 K1 0.193 -> 0.233 ms, off)
-  constexpr bool kLdsProg = (NS == -1 && SPK_SCAP != 0) || (SPK_K1_LDS_PROG == 2 && NS > -2);
+  // read it from there: 264 B per lane). (Every flat layout from LDS was
+  // measured slower: C3 K1 0.193 -> 0.233 ms.) Staged before any wave of the
+  // block may leave, so every wave reaches the barrier.
+  constexpr bool kLdsProg = NS == -1 && SPK_SCAP != 0;
   __shared__ WalkProg Ps;
   if constexpr (kLdsProg) {
     if (threadIdx.x == 0) Ps = P;
     __syncthreads();
   }
   const WalkProg &Pk = kLdsProg ? Ps : P;
-#else
-  const WalkProg &Pk = P;
-#endif
+  if (t >= TB.ntiles || !vec_live(c)) return;  // wave-uniform
   if constexpr (SPK_WSPEC >= 2 || (SPK_WSPEC == 1 && NS == -3)) {
     switch (c->w) {  // (uniform: the header's width)
       case 1: vec_tile_spec_body<NS, 1>(a, Pk, wire, ws, TB, dbg, win_s[wv], t, lane); return;
@@ -3788,32 +3605,6 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
       }
     }
     return;
-  } else if constexpr (SPK_K4_LANE != 0) {
-    // (A/B) flat records, one lane per chunk as above
-    uint64_t tot;
-    const uint64_t rofs = wave_excl_scan_u64(cnt, lane, &tot);
-    uint64_t hb[kVS];
-    QFOR(q) {
-      const uint64_t hsq = !own ? 0ull : alt0 ? qs[q] : TB.csum[(uint64_t)q * TB.nchunks + g];
-      hb[q] = psum[q] + wave_excl_scan_u64(hsq, lane, &tot);
-    }
-    uint64_t idx = base + rofs;
-    if (!own || !cnt || idx >= n || used == kNoPos || used == kTermPos) return;
-    uint64_t x = used;
-    for (uint32_t r = 0; r < cnt && idx < n; ++r, ++idx) {
-      uint64_t rc[kVS] = {};
-      const uint64_t L = wlen_rd<NS>(P, rd, len, x, w, rc);
-      bool fits = idx < a.rec_cap;
-      QFOR(q) fits = fits && hb[q] + rc[q] <= a.heap_cap[q];
-      if (fits) emit_record_rd(a.L, rd, x, w, recs + idx * a.L.stride, a.heaps, hb, len, bq, dbg);
-      if (idx == n - 1) {
-        fc->end_pos = x + L;
-        QFOR(q) fc->htot[q] = hb[q] + rc[q];
-      }
-      QFOR(q) hb[q] += rc[q];
-      x += L;
-    }
-    return;
   }
   uint64_t rofs;  // this chunk's first record, part-relative
   {
@@ -3995,315 +3786,6 @@ __global__ void vec_tile_finish(DecArgs a, const uint8_t *__restrict__ wire,
 }
 
 // ===========================================================================
-// DECODE, SPK_MODE_VECTOR — one fused pass with a decoupled look-back
-// ===========================================================================
-// A block of kFW waves owns kFW consecutive tiles (64 KiB of payload), staged
-// once in LDS. Each wave speculates and resolves its tile (K1's phase); the
-// block composes its tiles (tile k's entry = tile k-1's exit, a tile whose
-// entry lies past its end passes it through) and publishes an AGGREGATE
-// under its assumed entry: (entry X, exit Y, records, span sums). Wave 0 then
-// looks back over the 64 preceding blocks (blocks take ordered ids, so every
-// predecessor is running or done): from the nearest block that published its
-// INCLUSIVE state (true exit, records and span sums up to it), the chain of
-// aggregates whose entries equal their predecessors' exits gives this block's
-// true entry and its first record / heap offsets; an aggregate that does not
-// fit is waited for until its block publishes its inclusive state. The block
-// re-resolves if its assumed entry was wrong, publishes its inclusive state
-// and emits its records from the same LDS window: the wire is read once and
-// no per-chunk state leaves the chip (K1 + K2-K4 in one kernel).
-// Published words carry a tag bit and are written / read with agent-scope
-// relaxed atomics (no ordering between words is needed: a reader takes a
-// block's words only once every one of them is tagged).
-constexpr uint32_t kFW = 4;                                  // tiles (waves) per block
-constexpr uint64_t kFBlockBytes = (uint64_t)kFW * kTileBytes;
-constexpr uint32_t kFTab = 1024;                             // record starts per emission pass
-constexpr uint32_t kAggWords = 16;                           // >= 3 + kVS
-constexpr uint64_t kFailPos = ~0ull - 2;                     // "the look-back gave up"
-constexpr uint32_t kLookSpin = 1u << 20;                     // polls before giving up
-struct FusedBufs {
-  uint64_t *aw;             // [nblk][kAggWords] X, Y, records, sums (tagged)
-  uint64_t *pw;             // [nblk][kAggWords] true Y, inclusive records, sums (tagged)
-  unsigned long long *ctr;  // ordered block ids
-  uint64_t nblk;
-};
-__device__ __forceinline__ uint64_t fz_tag(uint64_t v) {
-  // values < 2^62; kFailPos / kNoPos / kTermPos map to 2^63 - 3 / - 2 / - 1
-  const uint64_t e = v >= kFailPos ? 0x7FFFFFFFFFFFFFFFull - (~0ull - v) : v;
-  return (e << 1) | 1ull;
-}
-__device__ __forceinline__ uint64_t fz_untag(uint64_t t) {
-  const uint64_t e = t >> 1;
-  return e >= 0x7FFFFFFFFFFFFFFDull ? ~0ull - (0x7FFFFFFFFFFFFFFFull - e) : e;
-}
-__device__ __forceinline__ uint64_t ld_agent(const uint64_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(uint64_t *p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l);
-  return (uint64_t)lo | ((uint64_t)hi << 32);
-}
-
-// words [0, nw) of a published block state once all are tagged (false: not yet)
-__device__ __forceinline__ bool fz_read(const uint64_t *p, uint32_t nw, uint64_t *v) {
-  for (uint32_t q = 0; q < nw; ++q) {
-    const uint64_t x = ld_agent(p + q);
-    if (!(x & 1)) return false;
-    v[q] = fz_untag(x);
-  }
-  return true;
-}
-
-// The block's tiles in order from entry e0: wave k re-resolves when its
-// entry differs from the one its lane states were computed under (tin); a
-// tile whose entry is past its end (inside a record spanning it), the path's
-// end or unknown passes it through (tpass: no records; the lane states are
-// kept for a later entry). Results per wave in sh_y / sh_c / sh_s.
-template <int NS>
-__device__ __forceinline__ void fz_compose(const WalkProg &P, const WinReader &rd, uint64_t len,
-                                           uint32_t w, uint64_t ts, uint64_t cs, uint64_t ce,
-                                           uint32_t wv, uint32_t lane, uint64_t e0,
-                                           TileLane<NS> &st, uint64_t &tin, bool &tpass,
-                                           uint64_t *sh_y, uint64_t *sh_c, uint64_t (*sh_s)[kVS]) {
-  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
-  for (uint32_t k = 0; k < kFW; ++k) {
-    if (wv == k) {
-      const uint64_t e = k ? sh_y[k - 1] : e0;
-      if (e != tin) {
-        tpass = e == kTermPos || e == kNoPos || e >= ts + kTileBytes;
-        if (!tpass)
-          resolve_tile_sp<NS>(P, rd, len, w, cs, ce, lane, e, st.sp, st.used, st.ex, st.cnt,
-                              st.sums, st.term_at);
-        tin = e;
-      }
-      const uint64_t y = tpass ? e : __shfl(st.ex, 63);
-      const uint64_t tc = wave_sum_u64(tpass ? 0u : st.cnt);
-      uint64_t tsq[NS > 0 ? NS : kVS];
-      QFOR(q) tsq[q] = wave_sum_u64(tpass ? 0ull : st.sums[q]);
-      if (lane == 0) {
-        sh_y[k] = y;
-        sh_c[k] = tc;
-        QFOR(q) sh_s[k][q] = tsq[q];
-      }
-    }
-    __syncthreads();
-  }
-}
-
-template <int NS>
-__global__ __launch_bounds__(64 * kFW) void vec_tile_fused(DecArgs a, WalkProg P,
-                                                          const uint8_t *__restrict__ wire,
-                                                          uint8_t *__restrict__ ws, FusedBufs FB,
-                                                          uint8_t *__restrict__ recs, BigQ bq,
-                                                          uint32_t dbg) {
-  __shared__ v4u_t win_s[kFW][win_slots(kTileVec)];
-  __shared__ uint16_t tab_s[kFW][kFTab];
-  __shared__ uint64_t sh_y[kFW], sh_c[kFW], sh_s[kFW][kVS];
-  __shared__ uint64_t sh_x0, sh_e, sh_pc, sh_ps[kVS];
-  __shared__ unsigned long long sh_bid;
-  __shared__ uint32_t sh_fail;
-  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
-  FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
-  if (!vec_live(c)) return;  // block-uniform
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (threadIdx.x == 0) sh_bid = atomicAdd(FB.ctr, 1ull);
-  __syncthreads();
-  const uint64_t b = sh_bid;
-  const uint32_t w = c->w;
-  const uint64_t len = a.wire_len, p0 = c->p0;
-  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
-  const uint64_t t = b * kFW + wv;
-  const uint64_t ts = p0 + t * kTileBytes;
-  const TileView tv = stage_tile(win_s[wv], wire, len, ts, w, lane);
-  const WinReader &rd = tv.rd;
-  const uint64_t cs = ts + (uint64_t)lane * kTChunk;
-  const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
-  // ---- 1. speculate + resolve this tile under its own assumed entry ----
-  TileLane<NS> st;
-  uint64_t tin = tile_spec_resolve<NS>(P, rd, len, w, ts, tv.wend, cs, ce, lane, t == 0, p0, 0u,
-                                       st);
-  bool tpass = false;
-  if (wv == 0 && lane == 0) sh_x0 = tin;
-  __syncthreads();
-  const uint64_t x0 = sh_x0;
-  // ---- 2. the block under its assumed entry -> aggregate ----
-  fz_compose<NS>(P, rd, len, w, ts, cs, ce, wv, lane, x0, st, tin, tpass, sh_y, sh_c, sh_s);
-  const uint32_t na = 3 + nsp, np = 2 + nsp;
-  if (wv == 0 && x0 != kNoPos && lane < na) {
-    uint64_t v;
-    if (lane == 0) v = x0;
-    else if (lane == 1) v = sh_y[kFW - 1];
-    else if (lane == 2) { v = 0; for (uint32_t k = 0; k < kFW; ++k) v += sh_c[k]; }
-    else { v = 0; for (uint32_t k = 0; k < kFW; ++k) v += sh_s[k][lane - 3]; }
-    st_agent(FB.aw + b * kAggWords + lane, fz_tag(v));
-  }
-  // ---- 3. look-back (wave 0): true entry and first record / heap offsets ----
-  if (wv == 0 && (dbg & 1024)) {  // A/B timing only: no look-back (wrong offsets)
-    if (lane == 0) {
-      sh_e = b == 0 ? p0 : x0;
-      sh_pc = 0;
-      QFOR(q) sh_ps[q] = 0;
-      sh_fail = 0;
-    }
-  } else if (wv == 0) {
-    uint64_t cur = kFailPos, pc = 0, ps[kVS] = {};
-    for (uint32_t spin = 0; spin < kLookSpin; ++spin) {
-      const int64_t j = (int64_t)b - 64 + (int64_t)lane;
-      uint32_t stt = 0;  // 0 nothing, 1 aggregate, 2 inclusive, 3 failed
-      uint64_t v[3 + kVS];
-      if (j == -1) {
-        stt = 2;
-        v[0] = p0;
-        for (uint32_t q = 1; q < np; ++q) v[q] = 0;
-      } else if (j >= 0) {
-        if (fz_read(FB.pw + (uint64_t)j * kAggWords, np, v))
-          stt = v[0] == kFailPos ? 3 : 2;
-        else if (fz_read(FB.aw + (uint64_t)j * kAggWords, na, v))
-          stt = 1;
-      }
-      const uint64_t mP = __ballot(stt >= 2);
-      if (mP) {
-        const uint32_t kp = 63 - (uint32_t)__builtin_clzll(mP);
-        if (__builtin_amdgcn_readlane((int)stt, (int)kp) == 3) break;  // a predecessor gave up
-        // inclusive lane kp: v = (Y, records, sums); aggregate lanes: (X, Y, records, sums)
-        uint64_t y = readlane64(v[0], kp), c0 = readlane64(v[1], kp), s0[kVS];
-        QFOR(q) s0[q] = readlane64(v[2 + q], kp);
-        bool ok = true;
-        for (uint32_t l = kp + 1; l < 64 && ok; ++l) {
-          if (y == kTermPos) continue;  // the path ended: the rest adds nothing
-          const uint64_t bend = p0 + (b - 64 + l + 1) * kFBlockBytes;
-          if (y >= bend) continue;  // a record spans block l: it passes y through
-          const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((int)stt, (int)l);
-          if (sl != 1 || readlane64(v[0], l) != y) {
-            ok = false;
-            break;
-          }
-          c0 += readlane64(v[2], l);
-          QFOR(q) s0[q] += readlane64(v[3 + q], l);
-          y = readlane64(v[1], l);
-        }
-        if (ok) {
-          cur = y;
-          pc = c0;
-          QFOR(q) ps[q] = s0[q];
-          break;
-        }
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    if (lane == 0) {
-      sh_e = cur;
-      sh_pc = pc;
-      QFOR(q) sh_ps[q] = ps[q];
-      sh_fail = cur == kFailPos ? 1u : 0u;
-    }
-  }
-  __syncthreads();
-  if (sh_fail) {  // never expected: the finish kernel reports an internal error
-    if (threadIdx.x < np) st_agent(FB.pw + b * kAggWords + threadIdx.x, fz_tag(kFailPos));
-    if (threadIdx.x == 0) atomicAdd(&fc->unresolved, 1ull);
-    return;
-  }
-  const uint64_t E = sh_e;
-  // ---- 4. the true block: re-resolve from E when it differs from x0 ----
-  if (E != x0) {
-    fz_compose<NS>(P, rd, len, w, ts, cs, ce, wv, lane, E, st, tin, tpass, sh_y, sh_c, sh_s);
-    if (threadIdx.x == 0) atomicAdd(&fc->broken[0], 1ull);
-  }
-  if (wv == 0 && lane < np) {
-    uint64_t v;
-    if (lane == 0) v = sh_y[kFW - 1];
-    else if (lane == 1) { v = sh_pc; for (uint32_t k = 0; k < kFW; ++k) v += sh_c[k]; }
-    else { v = sh_ps[lane - 2]; for (uint32_t k = 0; k < kFW; ++k) v += sh_s[k][lane - 2]; }
-    st_agent(FB.pw + b * kAggWords + lane, fz_tag(v));
-  }
-  if (b == FB.nblk - 1 && threadIdx.x == 0) {  // the path's totals
-    uint64_t v = sh_pc;
-    for (uint32_t k = 0; k < kFW; ++k) v += sh_c[k];
-    fc->total = v;
-    QFOR(q) {
-      uint64_t sv = sh_ps[q];
-      for (uint32_t k = 0; k < kFW; ++k) sv += sh_s[k][q];
-      fc->stot[q] = sv;
-    }
-  }
-  // ---- 5. emission of this wave's tile ----
-  const uint64_t n = c->n;
-  uint64_t base = sh_pc, carry[NS > 0 ? NS : kVS];
-  QFOR(q) carry[q] = sh_ps[q];
-  for (uint32_t k = 0; k < wv; ++k) {
-    base += sh_c[k];
-    QFOR(q) carry[q] += sh_s[k][q];
-  }
-  const uint32_t cnt = st.cnt;
-  const uint64_t used = st.used;
-  if (!tpass && st.ex == kTermPos && used != kNoPos && used != kTermPos) {
-    // where the true path ends: past this chunk's records
-    uint64_t x = used;
-    for (uint32_t r = 0; r < cnt; ++r) {
-      uint64_t rc[NS > 0 ? NS : kVS];
-      x += wlen_rd<NS>(P, rd, len, x, w, rc);
-    }
-    atomicMin(&fc->term_pos, (unsigned long long)x);
-  }
-  const uint64_t tcnt = sh_c[wv];
-  if (!tcnt || base >= n || (dbg & 2048)) return;
-  uint64_t rofs;  // this chunk's first record, tile-relative
-  {
-    uint64_t tot;
-    rofs = wave_excl_scan_u64(cnt, lane, &tot);
-  }
-  uint16_t *tab = tab_s[wv];
-  const uint64_t nemit = (n - base < tcnt) ? n - base : tcnt;
-  for (uint64_t pass0 = 0; pass0 < nemit; pass0 += kFTab) {
-    const uint64_t pend = pass0 + kFTab < nemit ? pass0 + kFTab : nemit;
-    if (cnt && rofs < pend && rofs + cnt > pass0) {
-      uint64_t x = used;
-      for (uint32_t r = 0; r < cnt; ++r) {
-        const uint64_t i = rofs + r;
-        if (i >= pend) break;
-        if (i >= pass0) tab[i - pass0] = (uint16_t)(x - ts);
-        uint64_t rc[NS > 0 ? NS : kVS];
-        x += wlen_rd<NS>(P, rd, len, x, w, rc);
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint64_t nrec = pend - pass0;
-    for (uint64_t i0 = 0; i0 < nrec; i0 += 64) {
-      const uint64_t i = i0 + lane;
-      const bool act = i < nrec;
-      const uint64_t pos = ts + (act ? tab[i] : 0);
-      uint64_t rc[kVS] = {};
-      uint64_t L = 0;
-      if (act) L = wlen_rd<NS>(P, rd, len, pos, w, rc);
-      uint64_t off[kVS];
-      bool fits = true;
-      QFOR(q) {
-        uint64_t tot;
-        off[q] = carry[q] + wave_excl_scan_u64(act ? rc[q] : 0, lane, &tot);
-        carry[q] += tot;
-        if (off[q] + rc[q] > a.heap_cap[q]) fits = false;
-      }
-      const uint64_t gr = base + pass0 + i;
-      if (act && gr < a.rec_cap && fits)
-        emit_record_rd(a.L, rd, pos, w, recs + gr * a.L.stride, a.heaps, off, len, bq);
-      if (act && gr == n - 1) {
-        fc->end_pos = pos + L;
-        QFOR(q) fc->htot[q] = off[q] + rc[q];
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-}
-
-// ===========================================================================
 // host launchers
 // ===========================================================================
 static unsigned grid_for(uint64_t items, uint64_t per_block) {
@@ -4313,8 +3795,8 @@ static unsigned grid_for(uint64_t items, uint64_t per_block) {
 
 // ---- tile decoder: workspace and launch ---------------------------------------
 struct TileWs {
-  size_t fn, cused, cex, ccnt, csum, sel, contrib, scan, blist, jobs, agg, nl, end;
-  uint64_t ntiles, nchunks, nsb, nblk;
+  size_t fn, cused, cex, ccnt, csum, sel, contrib, scan, blist, jobs, nl, end;
+  uint64_t ntiles, nchunks, nsb;
 };
 // ns: span counts per record (flat: SPAN + OPTION members; nested: heaps)
 static TileWs tile_ws_layout(uint32_t ns, uint64_t wire_len) {
@@ -4339,30 +3821,24 @@ static TileWs tile_ws_layout(uint32_t ns, uint64_t wire_len) {
   f.scan = take(f.nsb * 8 * (1 + ns));
   f.blist = take(f.ntiles * 4);
   f.jobs = take(big_jobs_cap(wire_len) * sizeof(BigJob));
-  f.nblk = (f.ntiles + kFW - 1) / kFW;
-  f.agg = take(2 * f.nblk * kAggWords * 8 + 64);  // fused decode: aggregates, inclusive, ids
   f.nl = take(sizeof(NTLayout));                  // nested layouts: the walker's layout
   f.end = off;
   return f;
 }
 
-// SPK_FUSED=1: the fused look-back kernel for the whole-message decode
-// instead of the multi-kernel tile pipeline (K1-K4) (A/B)
-static bool tile_fused() {
-  static const bool v = [] {
-    const char *e = getenv("SPK_FUSED");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
-// SPK_TILE_DBG bits (A/B experiments): 4 = compute entry alternatives in K1
+// Diagnostic bits of the tile kernels (K1 statistics, stages switched off for
+// timing, alternative entries): read from SPK_TILE_DBG only in a build with
+// -DSPK_DIAG=1 (scripts/ab_dbg.sh); a release build always runs 0.
 static uint32_t tile_dbg() {
+#if SPK_DIAG
   static const uint32_t v = [] {
     const char *e = getenv("SPK_TILE_DBG");
     return e ? (uint32_t)strtoul(e, nullptr, 0) : 0u;
   }();
   return v;
+#else
+  return 0u;
+#endif
 }
 
 // phase: kTilesAll (one decode), kTilesIndex (spk_decode_shard_index: K1-K3
@@ -4406,28 +3882,6 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
       SPK_LAUNCH(vec_shard_setn, dim3(1), dim3(64), 0, s, ws, sc.first, sc.last, d_res);
       SPK_LAUNCH(vec_tile_finish, dim3(1), dim3(64), 0, s, a, wire, (const uint8_t *)ws, d_res);
     }
-    return hipGetLastError();
-  }
-  if (NS > -2 && phase == kTilesAll && tile_fused()) {
-    FusedBufs FB;
-    FB.nblk = f.nblk;
-    FB.aw = reinterpret_cast<uint64_t *>(ws + f.agg);
-    FB.pw = FB.aw + f.nblk * kAggWords;
-    FB.ctr = reinterpret_cast<unsigned long long *>(FB.pw + f.nblk * kAggWords);
-    BigQ bq;
-    bq.jobs = reinterpret_cast<BigJob *>(ws + f.jobs);
-    bq.n = &reinterpret_cast<FCtl *>(ws + kWsFCtl)->njobs;
-    bq.cap = big_jobs_cap(a.wire_len);
-    SPK_LAUNCH(vec_hdr_kernel, dim3(1), dim3(64), 0, s, a, wire, ws, d_res, 0u, (uint64_t)0);
-    hipError_t e = hipMemsetAsync(ws + f.agg, 0, 2 * f.nblk * kAggWords * 8 + 64, s);
-    if (e != hipSuccess) return e;
-    SPK_LAUNCH(vec_tile_fused<NS <= -2 ? 0 : NS>, dim3((unsigned)f.nblk), dim3(64 * kFW), 0, s, a,
-               P, wire, ws, FB, d_recs, bq, tile_dbg());
-    if (P.ns) {
-      const uint64_t gb = bq.cap < 2048 ? bq.cap : 2048;
-      SPK_LAUNCH(vec_big_copy, dim3((unsigned)gb), dim3(256), 0, s, wire, (const uint8_t *)ws, bq);
-    }
-    SPK_LAUNCH(vec_tile_finish, dim3(1), dim3(64), 0, s, a, wire, (const uint8_t *)ws, d_res);
     return hipGetLastError();
   }
   if (phase != kTilesEmit) {
@@ -4556,7 +4010,6 @@ static NTLayout make_ntlayout(const NLayout &N, void *const *heaps) {
       break;
     }
     if (fix >= (1ull << 32)) ok = false;
-    if (x == WP_END) x |= (open[d] + 1) << 8;  // (nt_walk_u) the loop's body start
     t.wp[n] = make_uint2(x, (uint32_t)fix);
     fix = 0;
     ++n;
