@@ -1509,14 +1509,20 @@ __device__ __forceinline__ uint32_t win_b(uint32_t o) { return o; }
 __host__ __device__ constexpr uint32_t win_slots(uint32_t nv) { return nv + 1; }
 
 // Count-field reader over a chunk's LDS window: bytes [cs, wend) of the wire
-// are staged in LDS; reads past the window go to global memory.
-struct WinReader {
+// are staged in LDS; reads past the window go to global memory. LO (LDS
+// only): the caller guarantees every read lies inside the window, so the
+// reader never touches global memory -- and the compiler then has no load of
+// it to wait for: a global fallback merged into a read makes every use wait
+// vmcnt(0), i.e. for all of the wave's outstanding STORES too (gfx950 counts
+// stores in vmcnt), which serialised K4's record stores.
+template <bool LO>
+struct WinReaderT {
   const lds_u32 *d;
   const uint8_t *wire;
   uint64_t cs, wend;
   uint32_t w;
   __device__ __forceinline__ uint64_t operator()(uint64_t x) const {
-    if (x + w <= wend) {
+    if (LO || x + w <= wend) {
       if (w == 1) return reinterpret_cast<const lds_u8 *>(d)[win_b((uint32_t)(x - cs))];  // ds_read_u8
       const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = win_dw(o);
       const uint32_t d0 = d[i], d1 = d[i + 1];
@@ -1529,7 +1535,7 @@ struct WinReader {
     return wire_le(wire, x, w);
   }
   __device__ __forceinline__ uint32_t byte(uint64_t x) const {
-    if (x < wend) return reinterpret_cast<const lds_u8 *>(d)[win_b((uint32_t)(x - cs))];
+    if (LO || x < wend) return reinterpret_cast<const lds_u8 *>(d)[win_b((uint32_t)(x - cs))];
     return wire[x];
   }
   // LEB128 at x (message end len), as vi_read: eight bytes from the window at
@@ -1537,12 +1543,12 @@ struct WinReader {
   // gathers the 7-bit groups -- and the byte loop for longer / edge varints
   __device__ __forceinline__ uint32_t vread(uint64_t x, uint64_t len, uint64_t *v) const {
     uint32_t l = 0;
-    if (x + 12 <= wend) {
+    if (LO || x + 12 <= wend) {
       const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = win_dw(o);
       const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2];
       l = vi_decode8((uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
                          ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32), v);
-    } else if (x >= wend && x + 8 <= len) {
+    } else if (!LO && x >= wend && x + 8 <= len) {
       // past the window: the 8 bytes in one load, not one dependent byte load
       // each (speculative walks of varint records leave the window)
       l = vi_decode8(*reinterpret_cast<const u64_unaligned *>(wire + x), v);
@@ -1554,7 +1560,7 @@ struct WinReader {
   // count_at with a 32-bit wire offset (nested tile walks: wires below
   // kNT32Wire bytes, so x + 12 cannot wrap)
   __device__ __forceinline__ uint64_t count_at32(uint32_t x, uint64_t wmask, bool opt) const {
-    if (x + 12u <= (uint32_t)wend) {
+    if (LO || x + 12u <= (uint32_t)wend) {
       const uint32_t o = x - (uint32_t)cs, sh = o & 3, i = win_dw(o);
       const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2];
       const uint64_t b = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
@@ -1567,7 +1573,7 @@ struct WinReader {
   // has_value byte, whether it is non-zero; inside the window one path (8
   // bytes from three dwords), past it the wire
   __device__ __forceinline__ uint64_t count_at(uint64_t x, uint64_t wmask, bool opt) const {
-    if (x + 12 <= wend) {
+    if (LO || x + 12 <= wend) {
       const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = win_dw(o);
       const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2];
       const uint64_t b = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
@@ -1589,7 +1595,7 @@ struct WinReader {
   }
   // dst[0, n) = wire[x, x + n): from LDS when inside the window
   __device__ __forceinline__ void copy_to(uint8_t *dst, uint64_t x, uint64_t n) const {
-    if (x + n + 4 > wend) {
+    if (!LO && x + n + 4 > wend) {
       copy_bytes(dst, wire + x, n);
       return;
     }
@@ -1606,7 +1612,10 @@ struct WinReader {
     }
     for (; i < n; ++i) dst[i] = (uint8_t)byte(x + i);
   }
+  // the same window with reads that never leave it (see LO)
+  __device__ __forceinline__ WinReaderT<true> lds() const { return {d, wire, cs, wend, w}; }
 };
+using WinReader = WinReaderT<false>;
 
 // Long spans are not copied by the lane that emits their record: the lane
 // queues them in <= kBigPiece pieces and vec_big_copy moves every piece with
@@ -1627,7 +1636,8 @@ __host__ __device__ constexpr uint64_t big_jobs_cap(uint64_t wire_len) {
 }
 
 // emit_record reading the wire through an LDS window reader
-__device__ __forceinline__ void emit_record_rd(const KLayout &L, const WinReader &rd,
+template <typename Rd>
+__device__ __forceinline__ void emit_record_rd(const KLayout &L, const Rd &rd,
                                                uint64_t pos, uint32_t w, uint8_t *rec,
                                                uint8_t *const *heaps, const uint64_t *off,
                                                uint64_t end, const BigQ &bq, uint32_t dbg = 0) {
@@ -3483,6 +3493,7 @@ template <int NS>
 constexpr uint32_t kEmitVec = (kEmitBytes<NS> + kWinExtra) / 16;
 template <int NS>  // record starts per emission pass (the nested path keeps none)
 constexpr uint32_t kEmitTab = NS <= -2 ? 1u : kTab / kEmitSplit<NS>;
+constexpr uint16_t kTabFar = 0xFFFFu;  // a table end past the window
 
 template <int NS>
 __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkProg P,
@@ -3495,65 +3506,78 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
   constexpr uint32_t kEmitBytes = spk::kEmitBytes<NS>, kEmitVec = spk::kEmitVec<NS>;
   constexpr uint32_t kEmitTab = spk::kEmitTab<NS>;
   __shared__ v4u_t win_s[kDecWaves][win_slots(kEmitVec)];
-  __shared__ uint16_t tab_s[kDecWaves][kEmitTab];
+  __shared__ uint16_t tab_s[kDecWaves][kEmitTab + 2];  // (+ the pass's end)
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t gw = (uint64_t)blockIdx.x * kDecWaves + wv;
   const uint64_t t = gw / kEmitSplit;
   const uint32_t part = (uint32_t)(gw % kEmitSplit);
-  if (t >= TB.ntiles || !vec_live(c) || t > fc->term_tile) return;
+  if (t >= TB.ntiles || !vec_live(c)) return;
+  const uint64_t term_tile = fc->term_tile;
+  if (t > term_tile) return;
   const uint64_t n = c->n;
-  const uint64_t tbase = TB.contrib[t];
-  const int32_t sel = TB.sel[t];
-  if (tbase >= n || sel < 0) return;
-  const uint64_t *alt = TB.fn + t * kFnWords + 2 + sel * kAltWords;  // entry, cnt, sums
-  // a tile without records (inside a record that spans it) emits nothing,
-  // unless the path ends in it (term_pos below)
-  if (!alt[1] && t != fc->term_tile) return;
   const uint32_t w = c->w;
   const uint64_t len = a.wire_len, p0 = c->p0;
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
   const uint64_t ts = p0 + t * kTileBytes;
   const uint64_t wb = ts + (uint64_t)part * kEmitBytes;  // this part's window
-  nt_prologue<NS>(a, lane);
-  const TileView tv = stage_win<kEmitVec>(win_s[wv], wire, len, wb, w, lane);
-  const WinReader &rd = tv.rd;
-  if (dbg & 128) {
-    if (lane == 0 && rd.byte(wb) == 0x1234) fc->end_pos = 1;  // keep the staging alive
-    return;
-  }
   const bool own = lane < kEmitChunks;
   const uint32_t ch = part * kEmitChunks + lane;  // tile-relative chunk
   const uint64_t cs = ts + (uint64_t)ch * kTChunk;
   const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
   const uint64_t g = t * 64 + ch;
+  // Everything the part reads from the tile's state is loaded in one round
+  // trip, before the window is staged: the selection, the tile's exclusive
+  // contributions, every entry alternative of its function (lane k: word k of
+  // the alternatives, selected below), its chunks' states and, for a later
+  // part, the counts and sums of the chunks after it. (Loaded one after the
+  // other, the selection -> alternative -> chunk states -> sums chain cost
+  // the wave four memory latencies before any work.)
+  const uint64_t tbase = TB.contrib[t];
+  const int32_t sel = TB.sel[t];
+  uint64_t psum[kVS];
+  QFOR(q) psum[q] = TB.contrib[(uint64_t)(1 + q) * TB.ntiles + t];
+  const uint64_t fnw = lane < kAlt * kAltWords ? TB.fn[t * kFnWords + 2 + lane] : 0;
   uint64_t used = own ? TB.cused[g] : kNoPos, ex = own ? TB.cex[g] : kNoPos;
   uint32_t cnt = own ? TB.ccnt[g] : 0;
+  uint64_t rest = 0, rs[kVS];
+  QFOR(q) rs[q] = 0;
+  if (part > 0) {  // everything from this part to the tile's end (chunk 0 is not among it)
+    for (uint32_t cc = ch; cc < 64; cc += kEmitChunks) {
+      rest += TB.ccnt[t * 64 + cc];
+      QFOR(q) rs[q] += TB.csum[(uint64_t)q * TB.nchunks + t * 64 + cc];
+    }
+  }
+  nt_prologue<NS>(a, lane);
+  const TileView tv = stage_win<kEmitVec>(win_s[wv], wire, len, wb, w, lane);
+  const WinReader &rd = tv.rd;
+  if (tbase >= n || sel < 0) return;
+  // the selected alternative: entry, records, sums (words of lane sel * kAltWords + k)
+  const uint32_t sb = (uint32_t)sel * kAltWords;
+  const uint64_t alt_e = __shfl(fnw, (int)sb), alt_c = __shfl(fnw, (int)sb + 1);
+  // a tile without records (inside a record that spans it) emits nothing,
+  // unless the path ends in it (term_pos below)
+  if (!alt_c && t != term_tile) return;
+  if (dbg & 128) {
+    if (lane == 0 && rd.byte(wb) == 0x1234) fc->end_pos = 1;  // keep the staging alive
+    return;
+  }
   uint64_t qs[NS > 0 ? NS : kVS];  // (nested: chunk 0's heap sums from that entry)
   const bool alt0 = sel > 0 && part == 0 && lane == 0;
   if (alt0) {  // another entry of chunk 0 (same exit)
-    const uint64_t T = alt[0];
+    const uint64_t T = alt_e;
     uint64_t qe, qt;
     walk_true<NS>(P, rd, len, w, T, ce, qe, cnt, qs, qt);
     used = T;
   }
   const uint64_t pcnt = wave_sum_u64(cnt);  // records starting in this part
-  uint64_t base = tbase, psum[kVS];
-  QFOR(q) psum[q] = TB.contrib[(uint64_t)(1 + q) * TB.ntiles + t];
+  uint64_t base = tbase;
   if (part > 0) {
-    // everything from this part to the tile's end (chunk 0 is not among it)
-    uint64_t rest = 0;
-    for (uint32_t cc = ch; cc < 64; cc += kEmitChunks) rest += TB.ccnt[t * 64 + cc];
-    base += alt[1] - wave_sum_u64(own ? rest : 0);
-    QFOR(q) {
-      uint64_t rs = 0;
-      for (uint32_t cc = ch; cc < 64; cc += kEmitChunks)
-        rs += TB.csum[(uint64_t)q * TB.nchunks + t * 64 + cc];
-      psum[q] += alt[2 + q] - wave_sum_u64(own ? rs : 0);
-    }
+    base += alt_c - wave_sum_u64(own ? rest : 0);
+    QFOR(q) psum[q] += __shfl(fnw, (int)sb + 2 + (int)q) - wave_sum_u64(own ? rs[q] : 0);
   }
-  if (own && ex == kTermPos && used != kNoPos && used != kTermPos && t == fc->term_tile) {
+  if (own && ex == kTermPos && used != kNoPos && used != kTermPos && t == term_tile) {
     // where the true path ends: past this chunk's records
     uint64_t x = used;
     for (uint32_t r = 0; r < cnt; ++r) {
@@ -3617,7 +3641,8 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
   const uint64_t nemit = (n - base < pcnt) ? n - base : pcnt;
   for (uint64_t pass0 = 0; pass0 < nemit; pass0 += kEmitTab) {
     const uint64_t pend = pass0 + kEmitTab < nemit ? pass0 + kEmitTab : nemit;
-    // record starts of this pass into the table
+    // record starts of this pass into the table, and after the last one its
+    // end (kTabFar when it lies too far past the window for the fast path)
     if (cnt && rofs < pend && rofs + cnt > pass0) {
       uint64_t x = used;
       for (uint32_t r = 0; r < cnt; ++r) {
@@ -3626,19 +3651,25 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
         if (i >= pass0) tab[i - pass0] = (uint16_t)(x - wb);
         uint64_t rc[NS > 0 ? NS : kVS];
         x += wlen_rd<NS>(P, rd, len, x, w, rc);
+        if (i + 1 == pend)
+          tab[pend - pass0] = x + 16 <= tv.wend ? (uint16_t)(x - wb) : kTabFar;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const uint64_t nrec = pend - pass0;
-    for (uint64_t i0 = 0; i0 < nrec; i0 += 64) {
+    // 64 records at a time: positions from the table, heap offsets by wave
+    // scans of their counts, then the record and its payloads written. R: the
+    // window reader; the LDS-only one when all 64 records lie inside the
+    // window (their stores then never wait on a load)
+    auto emit64 = [&](const auto &R, uint64_t i0) {
       const uint64_t i = i0 + lane;
       const bool act = i < nrec;
       const uint64_t pos = wb + (act ? tab[i] : 0);
       uint64_t rc[kVS] = {};
       uint64_t L = 0;
-      if (act) L = wlen_rd<NS>(P, rd, len, pos, w, rc);
+      if (act) L = wlen_rd<NS>(P, R, len, pos, w, rc);
       uint64_t off[kVS];
       bool fits = true;
       QFOR(q) {
@@ -3652,12 +3683,26 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
         if constexpr (NS <= -2)
           nt_emit<NS == -3>(rd, pos, len, recs + gr * a.L.stride, off, bq);
         else
-          emit_record_rd(a.L, rd, pos, w, recs + gr * a.L.stride, a.heaps, off, len, bq, dbg);
+          emit_record_rd(a.L, R, pos, w, recs + gr * a.L.stride, a.heaps, off, len, bq, dbg);
       }
       if (act && gr == n - 1) {
         fc->end_pos = pos + L;
         QFOR(q) fc->htot[q] = off[q] + rc[q];
       }
+    };
+    for (uint64_t i0 = 0; i0 < nrec; i0 += 64) {
+      if constexpr (NS > -2) {
+        // every read of a record lies below its end (+ 12 bytes of the
+        // readers' word fetches): the next record's start in the table
+        const uint64_t i = i0 + lane;
+        const uint32_t e = i < nrec ? tab[i + 1] : 0u;
+        const bool inside = i >= nrec || (e != kTabFar && wb + e + 16 <= tv.wend);
+        if (__all(inside)) {
+          emit64(rd.lds(), i0);
+          continue;
+        }
+      }
+      emit64(rd, i0);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
