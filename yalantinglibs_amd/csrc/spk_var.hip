@@ -2197,7 +2197,8 @@ __device__ __forceinline__ uint64_t wlen_spec(const WalkProg &P, const Rd &rd, u
   return wlen_rd<NS, Rd, (SPK_SCAP & 1) != 0>(P, rd, len, pos, w, cnt, 0, scap, tight);
 }
 // payload of a SPAN into its heap slots (long ones queued for vec_big_copy)
-__device__ __forceinline__ void nt_put_payload(const WinReader &rd, uint8_t *hp, uint64_t pos,
+template <typename Rd>
+__device__ __forceinline__ void nt_put_payload(const Rd &rd, uint8_t *hp, uint64_t pos,
                                                uint64_t nb, const BigQ &bq) {
   if (nb >= kBigCopy) {
     const uint64_t np = (nb + kBigPiece - 1) / kBigPiece;
@@ -2216,7 +2217,8 @@ __device__ __forceinline__ void nt_put_payload(const WinReader &rd, uint8_t *hp,
 // Emission of a record the walk program accepted (COPY / SPAN / OPTION /
 // ARRAY layouts): the interpreter without error paths (the walk checked
 // every read), frames below the top one in LDS
-__device__ uint64_t nt_emit_simple(const NTLayout &N, const WinReader &rd, uint64_t pos,
+template <typename Rd>
+__device__ uint64_t nt_emit_simple(const NTLayout &N, const Rd &rd, uint64_t pos,
                                    uint64_t len, uint8_t *rec, const BigQ &bq) {
   uint32_t *const U = nt_used();
   uint32_t *const F = nt_frames();
@@ -2302,8 +2304,8 @@ __device__ uint64_t nt_emit_simple(const NTLayout &N, const WinReader &rd, uint6
 
 // emission with the lane's heap slots already in its LDS counters; the
 // record's end
-template <bool SIMPLE>
-__device__ __forceinline__ uint64_t nt_emit_here(const WinReader &rd, uint64_t pos, uint64_t len,
+template <bool SIMPLE, typename Rd>
+__device__ __forceinline__ uint64_t nt_emit_here(const Rd &rd, uint64_t pos, uint64_t len,
                                                  uint8_t *rec, const BigQ &bq) {
   const NTLayout &N = nt_lds();
   if constexpr (SIMPLE) {
@@ -3602,32 +3604,43 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
       if (hb[q] + hs[q] > a.heap_cap[q]) fits_all = false;
     }
     uint64_t idx = base + rofs;
-    if (!own || !cnt || idx >= n || used == kNoPos || used == kTermPos) return;
+    // every read of the lane's records lies below its chunk's exit (+ the
+    // readers' 12-byte word fetches): when that holds for every lane the
+    // records are emitted through the LDS-only reader (no store waits on a load)
+    const bool live = own && cnt && idx < n && used != kNoPos && used != kTermPos;
+    const bool inside = !live || (ex != kTermPos && ex != kNoPos && ex + 16 <= tv.wend);
+    if (!live) return;
     uint32_t *const U = nt_used();
     QFOR(q) U[64 * q] = (uint32_t)hb[q];
-    uint64_t x = used;
-    for (uint32_t r = 0; r < cnt && idx < n; ++r, ++idx) {
-      const uint64_t x0 = x;
-      if (idx < a.rec_cap && fits_all) {
-        x = nt_emit_here<NS == -3>(rd, x, len, recs + idx * a.L.stride, bq);
-      } else {
-        // near a capacity: this record's heap use first, written only if it fits
-        uint64_t b[kVS], rc[kVS];
-        QFOR(q) b[q] = U[64 * q];
-        x += wlen_rd<NS>(P, rd, len, x, w, rc);
-        bool fit = idx < a.rec_cap;
-        QFOR(q) fit = fit && b[q] + rc[q] <= a.heap_cap[q];
-        QFOR(q) U[64 * q] = (uint32_t)b[q];
-        if (fit)
-          nt_emit_here<NS == -3>(rd, x0, len, recs + idx * a.L.stride, bq);
-        else
-          QFOR(q) U[64 * q] = (uint32_t)(b[q] + rc[q]);
+    auto emit_lane = [&](const auto &R) {
+      uint64_t x = used;
+      for (uint32_t r = 0; r < cnt && idx < n; ++r, ++idx) {
+        const uint64_t x0 = x;
+        if (idx < a.rec_cap && fits_all) {
+          x = nt_emit_here<NS == -3>(R, x, len, recs + idx * a.L.stride, bq);
+        } else {
+          // near a capacity: this record's heap use first, written only if it fits
+          uint64_t b[kVS], rc[kVS];
+          QFOR(q) b[q] = U[64 * q];
+          x += wlen_rd<NS>(P, R, len, x, w, rc);
+          bool fit = idx < a.rec_cap;
+          QFOR(q) fit = fit && b[q] + rc[q] <= a.heap_cap[q];
+          QFOR(q) U[64 * q] = (uint32_t)b[q];
+          if (fit)
+            nt_emit_here<NS == -3>(R, x0, len, recs + idx * a.L.stride, bq);
+          else
+            QFOR(q) U[64 * q] = (uint32_t)(b[q] + rc[q]);
+        }
+        if (idx == n - 1) {
+          fc->end_pos = x;
+          QFOR(q) fc->htot[q] = U[64 * q];
+        }
       }
-      if (idx == n - 1) {
-        fc->end_pos = x;
-        QFOR(q) fc->htot[q] = U[64 * q];
-      }
-    }
+    };
+    if (__all(inside))
+      emit_lane(rd.lds());
+    else
+      emit_lane(rd);
     return;
   }
   uint64_t rofs;  // this chunk's first record, part-relative
