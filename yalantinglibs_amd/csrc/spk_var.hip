@@ -1498,6 +1498,12 @@ struct VecBufs {
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
+// byte-aligned LDS words: gfx950 reads them with one ds_read_b32 / b64 / b128
+// (unaligned DS access), not with 2-5 aligned dword reads + alignbyte
+typedef __attribute__((address_space(3))) uint16_t lds_u16_una __attribute__((aligned(1)));
+typedef __attribute__((address_space(3))) uint32_t lds_u32_una __attribute__((aligned(1)));
+typedef __attribute__((address_space(3))) uint64_t lds_u64_una __attribute__((aligned(1)));
+typedef __attribute__((address_space(3))) v4u_t lds_v4u_una __attribute__((aligned(1)));
 
 // LDS window layout: window-relative byte o is dword o >> 2, byte o. (Rows
 // padded to 69 dwords, so that the candidate screen's same-offset reads of a
@@ -1521,16 +1527,15 @@ struct WinReaderT {
   const uint8_t *wire;
   uint64_t cs, wend;
   uint32_t w;
+  __device__ __forceinline__ const lds_u8 *at(uint64_t x) const {
+    return reinterpret_cast<const lds_u8 *>(d) + (uint32_t)(x - cs);
+  }
   __device__ __forceinline__ uint64_t operator()(uint64_t x) const {
     if (LO || x + w <= wend) {
-      if (w == 1) return reinterpret_cast<const lds_u8 *>(d)[win_b((uint32_t)(x - cs))];  // ds_read_u8
-      const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = win_dw(o);
-      const uint32_t d0 = d[i], d1 = d[i + 1];
-      const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
-      if (w == 1) return lo & 0xFFu;
-      if (w == 2) return lo & 0xFFFFu;
-      if (w == 4) return lo;
-      return lo | ((uint64_t)__builtin_amdgcn_alignbyte(d[i + 2], d1, sh) << 32);
+      if (w == 1) return *at(x);  // ds_read_u8
+      if (w == 2) return *reinterpret_cast<const lds_u16_una *>(at(x));
+      if (w == 4) return *reinterpret_cast<const lds_u32_una *>(at(x));
+      return *reinterpret_cast<const lds_u64_una *>(at(x));
     }
     return wire_le(wire, x, w);
   }
@@ -1544,10 +1549,7 @@ struct WinReaderT {
   __device__ __forceinline__ uint32_t vread(uint64_t x, uint64_t len, uint64_t *v) const {
     uint32_t l = 0;
     if (LO || x + 12 <= wend) {
-      const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = win_dw(o);
-      const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2];
-      l = vi_decode8((uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
-                         ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32), v);
+      l = vi_decode8(*reinterpret_cast<const lds_u64_una *>(at(x)), v);
     } else if (!LO && x >= wend && x + 8 <= len) {
       // past the window: the 8 bytes in one load, not one dependent byte load
       // each (speculative walks of varint records leave the window)
@@ -1561,10 +1563,8 @@ struct WinReaderT {
   // kNT32Wire bytes, so x + 12 cannot wrap)
   __device__ __forceinline__ uint64_t count_at32(uint32_t x, uint64_t wmask, bool opt) const {
     if (LO || x + 12u <= (uint32_t)wend) {
-      const uint32_t o = x - (uint32_t)cs, sh = o & 3, i = win_dw(o);
-      const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2];
-      const uint64_t b = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
-                         ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
+      const uint64_t b = *reinterpret_cast<const lds_u64_una *>(
+          reinterpret_cast<const lds_u8 *>(d) + (x - (uint32_t)cs));
       return opt ? (uint64_t)((b & 0xFFu) != 0) : (b & wmask);
     }
     return opt ? (uint64_t)(byte(x) != 0) : (*this)(x);
@@ -1574,24 +1574,17 @@ struct WinReaderT {
   // bytes from three dwords), past it the wire
   __device__ __forceinline__ uint64_t count_at(uint64_t x, uint64_t wmask, bool opt) const {
     if (LO || x + 12 <= wend) {
-      const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = win_dw(o);
-      const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2];
-      const uint64_t b = (uint64_t)__builtin_amdgcn_alignbyte(d1, d0, sh) |
-                         ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, sh) << 32);
+      const uint64_t b = *reinterpret_cast<const lds_u64_una *>(at(x));
       return opt ? (uint64_t)((b & 0xFFu) != 0) : (b & wmask);
     }
     return opt ? (uint64_t)(byte(x) != 0) : (*this)(x);
   }
   // 4 / 16 bytes at x (x + n <= wend: inside the staged window)
   __device__ __forceinline__ uint32_t ld4(uint64_t x) const {
-    const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = win_dw(o);
-    return __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+    return *reinterpret_cast<const lds_u32_una *>(at(x));
   }
   __device__ __forceinline__ v4u_t ld16(uint64_t x) const {
-    const uint32_t o = (uint32_t)(x - cs), sh = o & 3, i = win_dw(o);
-    const uint32_t d0 = d[i], d1 = d[i + 1], d2 = d[i + 2], d3 = d[i + 3], d4 = d[i + 4];
-    return v4u_t{__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
-                 __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh)};
+    return *reinterpret_cast<const lds_v4u_una *>(at(x));
   }
   // dst[0, n) = wire[x, x + n): from LDS when inside the window
   __device__ __forceinline__ void copy_to(uint8_t *dst, uint64_t x, uint64_t n) const {
