@@ -1205,6 +1205,8 @@ struct FCtl {
   unsigned long long stot[kVS];  // span-count sums on the path
   unsigned long long nlist[4];   // tiles listed for re-resolution by select pass k
   unsigned long long diag[8];    // SPK_TILE_DBG & 4096: K1 statistics (scripts/diag_tiles.py)
+  unsigned long long chain_f0;   // the tile chain's first tile (atomicMin), ~0
+  unsigned long long chain_ticket;  // tiles the chain's blocks have taken
 };
 constexpr size_t kWsFCtl = kWsCtl + 1280;
 static_assert(sizeof(VCtl) <= kWsFCtl - kWsCtl, "VCtl overlaps FCtl");
@@ -1455,6 +1457,8 @@ __device__ void vec_hdr_body(const DecArgs &a, const uint8_t *__restrict__ wire,
   fc->unresolved = 0;
   for (int k = 0; k < 8; ++k) fc->diag[k] = 0;
   fc->seq = 0;
+  fc->chain_f0 = ~0ull;
+  fc->chain_ticket = 0;
   fc->njobs = 0;
   fc->term_tile = ~0ull;
   fc->term_pos = ~0ull;
@@ -2504,6 +2508,28 @@ __device__ __forceinline__ void walk_merge(const WalkProg &P, const Rd &rd, uint
   ex = x;
 }
 
+// After a resolution round: the lanes following a lane that walked, up to the
+// first whose chunk end lies past that walk's exit, hold no record start (a
+// record spans their chunks): each takes that exit as its entry and its exit
+// at once, as its own walk would, instead of one lane per round (c3l: the
+// long strings of a tile cost ~60 rounds).
+template <int NS>
+__device__ __forceinline__ void pass_through_run(uint64_t walked, uint32_t lane, uint64_t ce,
+                                                 uint32_t nsp, uint64_t &used, uint64_t &ex,
+                                                 uint32_t &cnt, uint64_t *sums,
+                                                 uint64_t &term_at) {
+  const uint64_t below = walked & ((1ull << lane) - 1ull);
+  const uint32_t k = below ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
+  const uint64_t X = __shfl(ex, (int)k);  // the last walker below this lane
+  if (below && !((walked >> lane) & 1ull) && X >= ce) {
+    used = X;
+    ex = X;
+    cnt = 0;
+    QFOR(q) sums[q] = 0;
+    term_at = kTermPos;
+  }
+}
+
 // In-wave resolution: until every lane's state was computed from its true
 // entry (lane 0: entry0; lane c: lane c-1's exit), lanes that disagree re-walk.
 template <int NS, typename Rd>
@@ -2511,6 +2537,7 @@ __device__ __forceinline__ void resolve_tile(const WalkProg &P, const Rd &rd, ui
                                              uint32_t w, uint64_t ce, uint32_t lane,
                                              uint64_t entry0, uint64_t &used, uint64_t &ex,
                                              uint32_t &cnt, uint64_t *sums, uint64_t &term_at) {
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
   for (int round = 0; round < 66; ++round) {
     const uint64_t prev = __shfl_up(ex, 1);
     const uint64_t entry = lane == 0 ? entry0 : prev;
@@ -2523,10 +2550,12 @@ __device__ __forceinline__ void resolve_tile(const WalkProg &P, const Rd &rd, ui
     // would only pass the error on, one lane per round (the first mismatch
     // always proceeds). A lane without any start walks anyway: records
     // resynchronise, so its walk from a wrong entry is often already right.
-    if (need && (used == kNoPos || !(lane > 0 && ((m >> (lane - 1)) & 1)))) {
+    const bool go = need && (used == kNoPos || !(lane > 0 && ((m >> (lane - 1)) & 1)));
+    if (go) {
       walk_true<NS>(P, rd, len, w, entry, ce, ex, cnt, sums, term_at);
       used = entry;
     }
+    pass_through_run<NS>(__ballot(go), lane, ce, nsp, used, ex, cnt, sums, term_at);
   }
 }
 // ... with each lane's speculative path for early merges
@@ -2538,6 +2567,7 @@ __device__ __forceinline__ void resolve_tile_sp(const WalkProg &P, const Rd &rd,
                                                 uint64_t &ex, uint32_t &cnt, uint64_t *sums,
                                                 uint64_t &term_at, uint32_t *stat = nullptr,
                                                 uint64_t reach = 0) {
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
   for (int round = 0; round < 66; ++round) {
     const uint64_t prev = __shfl_up(ex, 1);
     const uint64_t entry = lane == 0 ? entry0 : prev;
@@ -2545,11 +2575,13 @@ __device__ __forceinline__ void resolve_tile_sp(const WalkProg &P, const Rd &rd,
     const uint64_t m = __ballot(need);
     if (!m) return;
     if (stat) ++stat[0];
-    if (need && (used == kNoPos || !(lane > 0 && ((m >> (lane - 1)) & 1)))) {  // as resolve_tile
+    const bool go = need && (used == kNoPos || !(lane > 0 && ((m >> (lane - 1)) & 1)));
+    if (go) {  // as resolve_tile
       if (stat) ++stat[1];
       walk_merge<NS>(P, rd, len, w, entry, cs, ce, sp, ex, cnt, sums, term_at, reach);
       used = entry;
     }
+    pass_through_run<NS>(__ballot(go), lane, ce, nsp, used, ex, cnt, sums, term_at);
   }
 }
 
@@ -2583,6 +2615,22 @@ struct TileView {
   WinReader rd;
   uint64_t ts, wend;
 };
+// the reader over a window staged at ts (by this wave or, behind a barrier,
+// another of the block)
+template <uint32_t NV>
+__device__ __forceinline__ TileView win_view(const v4u_t *win, const uint8_t *wire, uint64_t len,
+                                             uint64_t ts, uint32_t w) {
+  const uint64_t wend = ts + NV * 16 < len ? ts + NV * 16 : len;
+  TileView tv;
+  tv.rd.d = (const lds_u32 *)win;
+  tv.rd.wire = wire;
+  tv.rd.cs = ts;
+  tv.rd.wend = wend;
+  tv.rd.w = w;
+  tv.ts = ts;
+  tv.wend = wend;
+  return tv;
+}
 template <uint32_t NV>
 __device__ __forceinline__ TileView stage_win(v4u_t *win, const uint8_t *wire, uint64_t len,
                                               uint64_t ts, uint32_t w, uint32_t lane) {
@@ -2619,15 +2667,7 @@ __device__ __forceinline__ TileView stage_win(v4u_t *win, const uint8_t *wire, u
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  TileView tv;
-  tv.rd.d = (const lds_u32 *)win;
-  tv.rd.wire = wire;
-  tv.rd.cs = ts;
-  tv.rd.wend = wend;
-  tv.rd.w = w;
-  tv.ts = ts;
-  tv.wend = wend;
-  return tv;
+  return win_view<NV>(win, wire, len, ts, w);
 }
 __device__ __forceinline__ TileView stage_tile(v4u_t *win, const uint8_t *wire, uint64_t len,
                                                uint64_t ts, uint32_t w, uint32_t lane) {
@@ -3218,6 +3258,48 @@ __global__ __launch_bounds__(256) void vec_tile_pick(uint8_t *__restrict__ ws, T
   TB.blist[atomicAdd(&fc->nlist[pass], 1ull)] = (uint32_t)t;
 }
 
+// Tile t re-resolved from its true entry T, its window staged in tv: the
+// chunk states and a one-entry tile function; returns the tile's exit.
+template <int NS>
+__device__ __forceinline__ uint64_t tile_resolve_from(const WalkProg &P, const TileView &tv,
+                                                      const TileBufs &TB, uint64_t len, uint32_t w,
+                                                      uint64_t t, uint64_t ts, uint64_t T,
+                                                      uint32_t lane) {
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  const uint64_t cs = ts + (uint64_t)lane * kTChunk;
+  const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
+  const uint64_t g = t * 64 + lane;
+  uint64_t used = TB.cused[g], ex = TB.cex[g], term_at = kTermPos;
+  uint32_t cnt = TB.ccnt[g];
+  uint64_t sums[NS > 0 ? NS : kVS];
+  QFOR(q) sums[q] = TB.csum[(uint64_t)q * TB.nchunks + g];
+  resolve_tile<NS>(P, tv.rd, len, w, ce, lane, T, used, ex, cnt, sums, term_at);
+  const uint64_t tcnt = wave_sum_u64(cnt);
+  uint64_t tsum[NS > 0 ? NS : kVS];
+  QFOR(q) tsum[q] = wave_sum_u64(sums[q]);
+  TB.cused[g] = used;
+  TB.cex[g] = ex;
+  TB.ccnt[g] = cnt;
+  QFOR(q) TB.csum[(uint64_t)q * TB.nchunks + g] = sums[q];
+  const uint64_t y63 = __shfl(ex, 63);
+  if (lane == 0) {
+    uint64_t *fn = TB.fn + t * kFnWords;
+    fn[0] = y63;
+    fn[1] = 1;
+    fn[2] = T;
+    fn[3] = tcnt;
+    QFOR(q) fn[4 + q] = tsum[q];
+    TB.sel[t] = 0;
+  }
+  return y63;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 constexpr unsigned kRepairGrid = 2048;
 template <int NS>
 __global__ __launch_bounds__(64) void vec_tile_repair(DecArgs a, WalkProg P,
@@ -3237,7 +3319,6 @@ __global__ __launch_bounds__(64) void vec_tile_repair(DecArgs a, WalkProg P,
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
   for (uint64_t j = blockIdx.x; j < nl; j += gridDim.x) {
     const uint64_t t = TB.blist[j];
-    uint64_t *fn = TB.fn + t * kFnWords;
     const uint64_t T = tile_entry(TB, fc, t);  // (re-read: a predecessor may have moved)
     const uint64_t ts = p0 + t * kTileBytes;
     if (T == kNoPos) {
@@ -3250,118 +3331,246 @@ __global__ __launch_bounds__(64) void vec_tile_repair(DecArgs a, WalkProg P,
       continue;
     }
     const TileView tv = stage_tile(win_s[0], wire, len, ts, w, lane);
-    const uint64_t cs = ts + (uint64_t)lane * kTChunk;
-    const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
-    const uint64_t g = t * 64 + lane;
-    uint64_t used = TB.cused[g], ex = TB.cex[g], term_at = kTermPos;
-    uint32_t cnt = TB.ccnt[g];
-    uint64_t sums[NS > 0 ? NS : kVS];
-    QFOR(q) sums[q] = TB.csum[(uint64_t)q * TB.nchunks + g];
-    resolve_tile<NS>(P, tv.rd, len, w, ce, lane, T, used, ex, cnt, sums, term_at);
-    const uint64_t tcnt = wave_sum_u64(cnt);
-    uint64_t tsum[NS > 0 ? NS : kVS];
-    QFOR(q) tsum[q] = wave_sum_u64(sums[q]);
-    TB.cused[g] = used;
-    TB.cex[g] = ex;
-    TB.ccnt[g] = cnt;
-    QFOR(q) TB.csum[(uint64_t)q * TB.nchunks + g] = sums[q];
-    const uint64_t y63 = __shfl(ex, 63);
-    if (lane == 0) {
-      fn[0] = y63;
-      fn[1] = 1;
-      fn[2] = T;
-      fn[3] = tcnt;
-      QFOR(q) fn[4 + q] = tsum[q];
-      TB.sel[t] = 0;
-    }
+    const uint64_t y63 = tile_resolve_from<NS>(P, tv, TB, len, w, t, ts, T, lane);
     tile_jump(TB, p0, t, y63, nsp, lane, &fc->broken[pass]);
-    // the window is restaged for the next listed tile
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    wave_lds_sync();  // the window is restaged for the next listed tile
   }
 }
 
-// Residual entries no pass could select (an exit that moved twice in a row,
-// or a chain of tiles inside records longer than a tile): one wave, in tile
-// order. It checks 64 tiles per step, jumps a run of tiles that a record
-// spans in one step, and re-resolves only the tiles still broken. Normally
-// exits at once.
-template <int NS>
-__global__ __launch_bounds__(64) void vec_tile_seqfix(DecArgs a, WalkProg P,
-                                                      const uint8_t *__restrict__ wire,
-                                                      uint8_t *__restrict__ ws, TileBufs TB,
-                                                      uint32_t last_pass) {
-  __shared__ v4u_t win_s[1][win_slots(kTileVec)];
+// ---- K2, what the passes leave: the tile chain ------------------------------
+// A tile whose entry none of its alternatives takes after the three passes
+// starts a chain: each later tile's true entry is known only once its
+// predecessor's is (strings whose bytes are themselves a record stream: every
+// tile inside one speculates a plausible false grid, and where such a string
+// ends the true entry is none of the speculated ones). vec_chain_first finds
+// the chain's first tile f0; in vec_tile_chain a persistent grid of one-wave
+// blocks takes the tiles from f0 on in order and, before it needs the entry,
+// computes each tile's exit for EVERY entry byte in LDS: the next record start
+// of each byte (one record walk per byte), then pointer jumping to the last
+// record start of each path inside the tile. The chain itself is then one
+// hand-off per entered tile: its block looks the exit up (one more record
+// walk) and stores it, tagged, into the entry word of the tile it lands in
+// (the tiles between pass it through), then re-resolves its own chunk states
+// from the entry off the chain's critical path. Hand-offs are 8-B agent-scope
+// atomic stores polled with agent-scope loads (no payload rides on them: the
+// word is the value); every other output is read by later launches.
+constexpr uint64_t kEntEnter = 1ull << 62, kEntThru = 2ull << 62, kEntTerm = 3ull << 62;
+constexpr uint64_t kEntPos = (1ull << 62) - 1;
+// map entries (u16): below kTileBytes the next record start in the tile (the
+// byte itself: its record ends too far past the tile to code); from kMapExit
+// the path's exit, coded as its distance past the tile's end
+constexpr uint16_t kMapBad = 0xFFFFu;  // the path from this byte fails inside the tile
+constexpr uint16_t kMapUnk = 0xFFFEu;  // a bounded nested walk gave up: walked at the hand-off
+constexpr uint32_t kMapExit = kTileBytes, kMapNear = 0xFFF0u - kMapExit;
+static_assert(kTileBytes <= 0x8000u, "chain map entries are u16 tile offsets");
+constexpr unsigned kChainGrid = 512;
+constexpr uint32_t kChainSpin = 1u << 20;  // poll rounds (~1 us each) before a lost hand-off is an error
+
+// the chain's first tile: the first whose entry none of its alternatives takes
+// (as the passes left them); every tile's selection as of now; entry words
+// cleared (TB.contrib, rewritten by K3)
+__global__ __launch_bounds__(256) void vec_chain_first(uint8_t *__restrict__ ws, TileBufs TB,
+                                                       uint32_t last_pass) {
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
-  const uint32_t lane = threadIdx.x;
-  if (!vec_live(c) || !fc->broken[last_pass]) return;
-  nt_prologue<NS>(a, lane);
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= TB.ntiles || !vec_live(c) || !fc->broken[last_pass]) return;
+  TB.contrib[t] = 0;
+  const uint64_t T = tile_entry(TB, fc, t);
+  int32_t sel = tile_select_for(TB, t, T);
+  if (sel >= 0 && TB.fn[t * kFnWords] == kNoPos) sel = kSelBroken;  // exit unknown
+  TB.sel[t] = sel;
+  if (sel == kSelBroken && T != kNoPos) atomicMin(&fc->chain_f0, (unsigned long long)t);
+}
+
+// waves per chain block: the map of a flat or varint layout is built by four
+// (one-wave blocks were bound by it: 31 MB screen-defeating 3.96 ms at 256
+// blocks, 2.59 at 768); the nested walker keeps its stack per lane in LDS, so
+// one wave per block
+template <int NS>
+constexpr uint32_t kChainWaves = NS <= -2 ? 1u : 4u;
+
+template <int NS>
+__global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
+    DecArgs a, WalkProg P, const uint8_t *__restrict__ wire, uint8_t *__restrict__ ws,
+    TileBufs TB, uint32_t last_pass) {
+  constexpr uint32_t kNT = 64 * kChainWaves<NS>;
+  __shared__ v4u_t win_s[win_slots(kTileVec)];
+  __shared__ uint16_t nxt[kTileBytes];
+  __shared__ uint64_t tile_s;
+  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
+  FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const bool w0 = tid < 64;
+  if (!vec_live(c) || !fc->broken[last_pass]) return;  // (block-uniform)
+  const uint64_t f0 = fc->chain_f0, nt = TB.ntiles;
+  if (f0 >= nt) return;
+  if (w0) nt_prologue<NS>(a, lane);
   const uint32_t w = c->w;
   const uint64_t len = a.wire_len, p0 = c->p0;
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
-  uint64_t t = 0;
-  while (t < TB.ntiles) {
-    // 64 tiles at once: the first whose entry none of its alternatives takes
-    const uint64_t u = t + lane;
-    int32_t sel = kSelTerm;
-    bool bad = false;
-    if (u < TB.ntiles) {
-      const uint64_t T = tile_entry(TB, fc, u);
-      sel = tile_select_for(TB, u, T);
-      if (sel >= 0 && TB.fn[u * kFnWords] == kNoPos) sel = kSelBroken;  // exit unknown
-      bad = sel == kSelBroken && T != kNoPos;
-    }
-    const uint64_t m = __ballot(bad);
-    const uint64_t f = m ? t + (uint64_t)__builtin_ctzll(m) : ~0ull;
-    if (u < TB.ntiles && u < f) TB.sel[u] = sel;
-    if (!m) {
-      t += 64;
-      continue;
-    }
-    const uint64_t T = tile_entry(TB, fc, f);
-    const uint64_t ts = p0 + f * kTileBytes;
-    if (T >= ts + kTileBytes) {
-      // a record spans tiles f .. e-1: all pass the entry through
-      const uint64_t e0 = (T - p0) / kTileBytes;
-      const uint64_t e = e0 < TB.ntiles ? e0 : TB.ntiles;
-      for (uint64_t v = f + lane; v < e; v += 64) tile_pass_through(TB, v, T, nsp);
-      if (lane == 0) fc->seq += e - f;
-      t = e;
-    } else {
-      const TileView tv = stage_tile(win_s[0], wire, len, ts, w, lane);
-      const uint64_t cs = ts + (uint64_t)lane * kTChunk;
-      const uint64_t ce = cs + kTChunk < len ? cs + kTChunk : (cs < len ? len : cs);
-      const uint64_t g = f * 64 + lane;
-      uint64_t used = TB.cused[g], ex = TB.cex[g], term_at = kTermPos;
-      uint32_t cnt = TB.ccnt[g];
-      uint64_t sums[NS > 0 ? NS : kVS];
-      QFOR(q) sums[q] = TB.csum[(uint64_t)q * TB.nchunks + g];
-      resolve_tile<NS>(P, tv.rd, len, w, ce, lane, T, used, ex, cnt, sums, term_at);
-      const uint64_t tcnt = wave_sum_u64(cnt);
-      uint64_t tsum[NS > 0 ? NS : kVS];
-      QFOR(q) tsum[q] = wave_sum_u64(sums[q]);
-      TB.cused[g] = used;
-      TB.cex[g] = ex;
-      TB.ccnt[g] = cnt;
-      QFOR(q) TB.csum[(uint64_t)q * TB.nchunks + g] = sums[q];
-      const uint64_t y63 = __shfl(ex, 63);
-      if (lane == 0) {
-        uint64_t *fn = TB.fn + f * kFnWords;
-        fn[0] = y63;
-        fn[1] = 1;
-        fn[2] = T;
-        fn[3] = tcnt;
-        QFOR(q) fn[4 + q] = tsum[q];
-        TB.sel[f] = 0;
-        fc->seq += 1;
+  uint64_t *ent = TB.contrib;
+  for (;;) {
+    // tiles in order: a block waits only for tiles claimed before its own,
+    // and those belong to blocks already running
+    if (tid == 0) tile_s = f0 + atomicAdd(&fc->chain_ticket, 1ull);
+    __syncthreads();
+    const uint64_t u = tile_s;
+    if (u >= nt) break;
+    const uint64_t ts = p0 + u * kTileBytes;
+    if (w0) stage_tile(win_s, wire, len, ts, w, lane);
+    __syncthreads();
+    const TileView tv = win_view<kTileVec>(win_s, wire, len, ts, w);
+    // ---- the next in-tile record start of every byte (the byte itself: its
+    // record ends too far past the tile to code; bytes at or past the wire
+    // end: the path's end) ----
+    for (uint32_t o = tid; o < kTileBytes; o += kNT) {
+      const uint64_t x = ts + o;
+      uint16_t v = (uint16_t)o;
+      if (x < len) {
+        const uint64_t L = wlen_rd<NS>(P, tv.rd, len, x, w, nullptr, kK1Reach<NS>);
+        v = L == kLenLimit ? kMapUnk
+            : !L           ? kMapBad
+            : L < kTileBytes - o ? (uint16_t)(o + L)
+            : L - (kTileBytes - o) < kMapNear ? (uint16_t)(kMapExit + (o + L - kTileBytes))
+                                              : (uint16_t)o;
       }
-      t = f + 1;
+      nxt[o] = v;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    __syncthreads();
+    // ---- pointer jumping: every byte to its path's exit code (or to the
+    // start of its last record, when that record's end is too far to code) ----
+    for (uint32_t r = 0; r < 32; ++r) {
+      int ch = 0;
+#pragma unroll 4
+      for (uint32_t o = tid; o < kTileBytes; o += kNT) {
+        const uint32_t v = nxt[o];
+        if (v < kTileBytes && v != o) {
+          const uint32_t v2 = nxt[v];
+          if (v2 != v) {
+            nxt[o] = (uint16_t)v2;
+            ch = 1;
+          }
+        }
+      }
+      if (!__syncthreads_or(ch)) break;
+    }
+    if (w0) {
+      // this tile's function words (entry alternatives), loaded before the wait
+      const uint64_t fnw = lane < 2 + kAlt * kAltWords ? TB.fn[u * kFnWords + lane] : 0;
+      // ---- the entry ----
+      uint64_t ev = 0;
+      if (u == f0) {
+        ev = kEntEnter | tile_entry(TB, fc, u);
+      } else {
+        if (lane == 0) {
+          // kPoll polls in flight, a few hundred cycles apart
+          constexpr int kPoll = 8;
+          uint64_t pv[kPoll];
+#pragma unroll
+          for (int k = 0; k < kPoll; ++k) {
+            pv[k] = __hip_atomic_load(&ent[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_s_sleep(3);
+          }
+          for (uint32_t i = 0; !ev; ++i) {
+#pragma unroll
+            for (int k = 0; k < kPoll; ++k) {
+              if (pv[k]) {
+                ev = pv[k];
+                break;
+              }
+              pv[k] = __hip_atomic_load(&ent[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              __builtin_amdgcn_s_sleep(3);
+            }
+            if (!ev && i >= kChainSpin) {  // (never expected: a decode error, not a hang)
+              ev = kEntTerm;
+              atomicAdd(&fc->unresolved, 1ull);
+            }
+          }
+        }
+        ev = __shfl(ev, 0);
+      }
+      const uint64_t kind = ev & ~kEntPos, e = ev & kEntPos;
+      if (kind == kEntThru) {  // inside a record spanning the tile
+        if (lane == 0) {
+          tile_pass_through(TB, u, e, nsp);
+          atomicAdd(&fc->seq, 1ull);
+        }
+      } else if (kind == kEntTerm) {  // past the path's end
+        if (lane == 0) TB.sel[u] = kSelTerm;
+      } else {
+        // ---- entered at e: the exit X ----
+        uint64_t X;
+        bool redo = false;
+        if (e >= ts + kTileBytes) {  // (f0 only: its entry lies past it)
+          if (lane == 0) tile_pass_through(TB, u, e, nsp);
+          X = e;
+        } else {
+          const uint32_t nalt = (uint32_t)__shfl(fnw, 1);
+          const uint32_t ai = (lane - 2) / kAltWords;
+          const bool hit = lane >= 2 && lane < 2 + kAlt * kAltWords &&
+                           (lane - 2) % kAltWords == 0 && ai < nalt && fnw == e;
+          const uint64_t hm = __ballot(hit);
+          const uint64_t fn0 = __shfl(fnw, 0);
+          if (hm && fn0 != kNoPos) {  // one of its own alternatives
+            if (lane == 0) TB.sel[u] = (int32_t)(((uint32_t)__builtin_ctzll(hm) - 2) / kAltWords);
+            X = fn0;
+          } else {
+            // X from the map; kNoPos: from the re-resolution below (a nested
+            // walk the map gave up on, the wire's end inside this tile, or an
+            // entry before it: a tile past the wire's end)
+            redo = true;
+            X = kNoPos;
+            if (e >= ts) {
+              uint32_t r = nxt[e - ts];
+              while (r < kTileBytes && nxt[r] != r) r = nxt[r];  // (jumping converged: no steps)
+              if (r == kMapBad) {
+                X = kTermPos;
+              } else if (r >= kMapExit && r < kMapExit + kMapNear) {
+                X = ts + kTileBytes + (r - kMapExit);
+              } else if (r < kTileBytes && ts + r < len) {
+                uint64_t L = 0;
+                if (lane == 0) L = wlen_rd<NS>(P, tv.rd, len, ts + r, w);
+                L = __shfl(L, 0);
+                X = L ? ts + r + L : kTermPos;
+              }
+            }
+          }
+        }
+        // ---- hand-off: the landing tile's entry first, then the tiles between ----
+        auto publish = [&](uint64_t Y) {
+          if (Y == kTermPos) {
+            for (uint64_t v = u + 1 + lane; v < nt; v += 64)
+              __hip_atomic_store(&ent[v], kEntTerm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+          }
+          if (Y == kNoPos) return;
+          uint64_t l0 = Y >= p0 ? (Y - p0) / kTileBytes : 0;
+          if (l0 <= u) {
+            if (Y < len) return;  // (no exit: never)
+            l0 = u + 1;  // the wire's end: the tile after, if any (past the end), enters there
+          }
+          const uint64_t l = l0 < nt ? l0 : nt;
+          if (lane == 0 && l < nt)
+            __hip_atomic_store(&ent[l], kEntEnter | Y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (uint64_t v = u + 1 + lane; v < l; v += 64)
+            __hip_atomic_store(&ent[v], kEntThru | Y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        };
+        if (X != kNoPos) publish(X);
+        if (redo) {
+          const uint64_t y = tile_resolve_from<NS>(P, tv, TB, len, w, u, ts, e, lane);
+          if (X == kNoPos) publish(y);
+          if (lane == 0) {
+            atomicAdd(&fc->broken[3], 1ull);
+#if SPK_DIAG
+            if (X != kNoPos && X < len && y != X) atomicAdd(&fc->diag[0], 1ull);  // map vs walk
+#endif
+          }
+        }
+        if (lane == 0) atomicAdd(&fc->seq, 1ull);
+      }
+    }
+    __syncthreads();  // the window, the map and tile_s are reused
   }
 }
 
@@ -3948,7 +4157,9 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
     SPK_LAUNCH(vec_tile_pick, dim3(grid_for(f.ntiles, 256)), dim3(256), 0, s, ws, TB, nsp, pass);
     SPK_LAUNCH(vec_tile_repair<NS>, dim3(kRepairGrid), dim3(64), 0, s, a, P, wire, ws, TB, pass);
   }
-  SPK_LAUNCH(vec_tile_seqfix<NS>, dim3(1), dim3(64), 0, s, a, P, wire, ws, TB, 2u);
+  SPK_LAUNCH(vec_chain_first, dim3(grid_for(f.ntiles, 256)), dim3(256), 0, s, ws, TB, 2u);
+  SPK_LAUNCH(vec_tile_chain<NS>, dim3(kChainGrid), dim3(64 * kChainWaves<NS>), 0, s, a, P, wire,
+             ws, TB, 2u);
   SPK_LAUNCH(vec_tile_contrib, dim3(grid_for(f.ntiles, 256)), dim3(256), 0, s, ws, TB, nsp);
   SPK_LAUNCH(tscan_reduce, dim3(nb), dim3(256), 0, s, (const uint8_t *)ws, TB, 1 + nsp);
   SPK_LAUNCH(tscan_top, dim3(1), dim3(1024), 0, s, ws, TB, 1 + nsp, (uint64_t)nb);
