@@ -1205,8 +1205,10 @@ struct FCtl {
   unsigned long long stot[kVS];  // span-count sums on the path
   unsigned long long nlist[4];   // tiles listed for re-resolution by select pass k
   unsigned long long diag[8];    // SPK_TILE_DBG & 4096: K1 statistics (scripts/diag_tiles.py)
-  unsigned long long chain_f0;   // the tile chain's first tile (atomicMin), ~0
   unsigned long long chain_ticket;  // tiles the chain's blocks have taken
+  unsigned long long chain_arrive;  // chain blocks arrived (the first one finds the first tile)
+  unsigned long long chain_ready;   // the chain's first tile + 1 (0: not yet found)
+  unsigned long long copy_done;     // vec_big_copy blocks done (the last one writes the result)
 };
 constexpr size_t kWsFCtl = kWsCtl + 1280;
 static_assert(sizeof(VCtl) <= kWsFCtl - kWsCtl, "VCtl overlaps FCtl");
@@ -1457,8 +1459,10 @@ __device__ void vec_hdr_body(const DecArgs &a, const uint8_t *__restrict__ wire,
   fc->unresolved = 0;
   for (int k = 0; k < 8; ++k) fc->diag[k] = 0;
   fc->seq = 0;
-  fc->chain_f0 = ~0ull;
   fc->chain_ticket = 0;
+  fc->chain_arrive = 0;
+  fc->chain_ready = 0;
+  fc->copy_done = 0;
   fc->njobs = 0;
   fc->term_tile = ~0ull;
   fc->term_pos = ~0ull;
@@ -2404,6 +2408,7 @@ struct TileBufs {
   uint64_t *contrib;  // [1 + nsp][ntiles] selected (records, sums) -> exclusive prefix
   uint64_t *scan;     // block sums of the tile scan
   uint32_t *blist;    // [ntiles] tiles a select pass found broken
+  uint64_t *ent;      // [ntiles] the tile chain's tagged entry words
   uint64_t ntiles, nchunks;
 };
 
@@ -2634,7 +2639,6 @@ __device__ __forceinline__ TileView win_view(const v4u_t *win, const uint8_t *wi
 template <uint32_t NV>
 __device__ __forceinline__ TileView stage_win(v4u_t *win, const uint8_t *wire, uint64_t len,
                                               uint64_t ts, uint32_t w, uint32_t lane) {
-  const uint64_t wend = ts + NV * 16 < len ? ts + NV * 16 : len;
   if (ts + NV * 16 <= len) {
     // the whole window exists: every lane issues all its 16-B loads before
     // the first LDS write, so the wave waits for one load latency, not one
@@ -3337,6 +3341,27 @@ __global__ __launch_bounds__(64) void vec_tile_repair(DecArgs a, WalkProg P,
   }
 }
 
+// ---- K3: the selected contribution of tile t (vec_tile_chain, once the
+// tile's selection is final); the first tile whose path ends inside it (its
+// exit is kTermPos) ----------------------------------------------------------
+__device__ __forceinline__ void tile_contrib(const TileBufs &TB, FCtl *fc, uint64_t t,
+                                             uint32_t nsp) {
+  const uint64_t *fn = TB.fn + t * kFnWords;
+  const int32_t sel = TB.sel[t];
+  uint64_t cnt = 0, s[kVS] = {};
+  if (sel >= 0) {
+    cnt = fn[2 + sel * kAltWords + 1];
+    QFORV(q) s[q] = fn[2 + sel * kAltWords + 2 + q];
+    if (fn[0] == kTermPos) atomicMin(&fc->term_tile, (unsigned long long)t);
+  } else if (sel == kSelTerm) {
+    atomicMin(&fc->term_tile, (unsigned long long)t);
+  } else {
+    atomicAdd(&fc->unresolved, 1ull);  // never expected after the fix passes
+  }
+  TB.contrib[t] = cnt;
+  QFORV(q) TB.contrib[(uint64_t)(1 + q) * TB.ntiles + t] = s[q];
+}
+
 // ---- K2, what the passes leave: the tile chain ------------------------------
 // A tile whose entry none of its alternatives takes after the three passes
 // starts a chain: each later tile's true entry is known only once its
@@ -3366,21 +3391,30 @@ static_assert(kTileBytes <= 0x8000u, "chain map entries are u16 tile offsets");
 constexpr unsigned kChainGrid = 512;
 constexpr uint32_t kChainSpin = 1u << 20;  // poll rounds (~1 us each) before a lost hand-off is an error
 
-// the chain's first tile: the first whose entry none of its alternatives takes
-// (as the passes left them); every tile's selection as of now; entry words
-// cleared (TB.contrib, rewritten by K3)
-__global__ __launch_bounds__(256) void vec_chain_first(uint8_t *__restrict__ ws, TileBufs TB,
-                                                       uint32_t last_pass) {
-  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
-  FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= TB.ntiles || !vec_live(c) || !fc->broken[last_pass]) return;
-  TB.contrib[t] = 0;
+template <uint32_t NW>
+__device__ __forceinline__ uint64_t block_min_u64(uint64_t v, uint64_t *sh) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t x = __shfl_down(v, o);
+    v = x < v ? x : v;
+  }
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint64_t m = sh[0];
+#pragma unroll
+  for (uint32_t k = 1; k < NW; ++k) m = sh[k] < m ? sh[k] : m;
+  __syncthreads();
+  return m;
+}
+
+// tile t's selection under its current entry (kSelBroken also when the
+// selected exit is unknown); *bad: broken although its entry is known
+__device__ __forceinline__ int32_t tile_sel_now(const TileBufs &TB, const FCtl *fc, uint64_t t,
+                                                bool *bad) {
   const uint64_t T = tile_entry(TB, fc, t);
   int32_t sel = tile_select_for(TB, t, T);
   if (sel >= 0 && TB.fn[t * kFnWords] == kNoPos) sel = kSelBroken;  // exit unknown
-  TB.sel[t] = sel;
-  if (sel == kSelBroken && T != kNoPos) atomicMin(&fc->chain_f0, (unsigned long long)t);
+  *bad = sel == kSelBroken && T != kNoPos;
+  return sel;
 }
 
 // waves per chain block: the map of a flat or varint layout is built by four
@@ -3397,19 +3431,67 @@ __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
   constexpr uint32_t kNT = 64 * kChainWaves<NS>;
   __shared__ v4u_t win_s[win_slots(kTileVec)];
   __shared__ uint16_t nxt[kTileBytes];
-  __shared__ uint64_t tile_s;
+  __shared__ uint64_t tile_s, red_s[kChainWaves<NS>];
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const bool w0 = tid < 64;
-  if (!vec_live(c) || !fc->broken[last_pass]) return;  // (block-uniform)
-  const uint64_t f0 = fc->chain_f0, nt = TB.ntiles;
+  if (!vec_live(c)) return;  // (block-uniform)
+  const uint64_t nt = TB.ntiles, gstride = (uint64_t)gridDim.x * kNT;
+  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
+  if (!fc->broken[last_pass]) {  // the passes left nothing: every tile's contribution
+    for (uint64_t t = (uint64_t)blockIdx.x * kNT + tid; t < nt; t += gstride)
+      tile_contrib(TB, fc, t, nsp);
+    return;
+  }
+  uint64_t *ent = TB.ent;
+  // ---- the chain's first tile f0: found by the first block to arrive (it
+  // runs, so the others may wait for it), which also clears the entry words ----
+  if (tid == 0) tile_s = atomicAdd(&fc->chain_arrive, 1ull);
+  __syncthreads();
+  if (tile_s == 0) {
+    uint64_t m = ~0ull;
+    for (uint64_t t = tid; t < nt; t += kNT) {
+      bool bad;
+      tile_sel_now(TB, fc, t, &bad);
+      if (bad && t < m) m = t;
+    }
+    m = block_min_u64<kChainWaves<NS>>(m, red_s);
+    for (uint64_t t = m + tid; t < nt; t += kNT)
+      __hip_atomic_store(&ent[t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      __hip_atomic_store(&fc->chain_ready, (m < nt ? m : nt) + 1, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    tile_s = m < nt ? m : nt;
+  } else if (tid == 0) {
+    uint64_t r;
+    for (uint32_t i = 0;; ++i) {
+      r = __hip_atomic_load(&fc->chain_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (r) break;
+      if (i >= kChainSpin) {  // (never expected: a decode error, not a hang)
+        r = nt + 1;
+        atomicAdd(&fc->unresolved, 1ull);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(4);
+    }
+    tile_s = r - 1;
+  }
+  __syncthreads();
+  const uint64_t f0 = tile_s;
+  // tiles before f0: selected as the passes left them
+  for (uint64_t t = (uint64_t)blockIdx.x * kNT + tid; t < f0; t += gstride) {
+    bool bad;
+    TB.sel[t] = tile_sel_now(TB, fc, t, &bad);
+    tile_contrib(TB, fc, t, nsp);
+  }
   if (f0 >= nt) return;
+  __syncthreads();
   if (w0) nt_prologue<NS>(a, lane);
   const uint32_t w = c->w;
   const uint64_t len = a.wire_len, p0 = c->p0;
-  const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
-  uint64_t *ent = TB.contrib;
   for (;;) {
     // tiles in order: a block waits only for tiles claimed before its own,
     // and those belong to blocks already running
@@ -3494,10 +3576,14 @@ __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
       if (kind == kEntThru) {  // inside a record spanning the tile
         if (lane == 0) {
           tile_pass_through(TB, u, e, nsp);
+          tile_contrib(TB, fc, u, nsp);
           atomicAdd(&fc->seq, 1ull);
         }
       } else if (kind == kEntTerm) {  // past the path's end
-        if (lane == 0) TB.sel[u] = kSelTerm;
+        if (lane == 0) {
+          TB.sel[u] = kSelTerm;
+          tile_contrib(TB, fc, u, nsp);
+        }
       } else {
         // ---- entered at e: the exit X ----
         uint64_t X;
@@ -3567,35 +3653,14 @@ __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
 #endif
           }
         }
-        if (lane == 0) atomicAdd(&fc->seq, 1ull);
+        if (lane == 0) {
+          tile_contrib(TB, fc, u, nsp);  // (its selection and function as this lane wrote them)
+          atomicAdd(&fc->seq, 1ull);
+        }
       }
     }
     __syncthreads();  // the window, the map and tile_s are reused
   }
-}
-
-// ---- K3: the selected contribution of every tile; the first tile whose
-// path ends inside it (its exit is kTermPos) --------------------------------
-__global__ __launch_bounds__(256) void vec_tile_contrib(uint8_t *__restrict__ ws, TileBufs TB,
-                                                        uint32_t nsp) {
-  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
-  FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
-  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= TB.ntiles || !vec_live(c)) return;
-  const uint64_t *fn = TB.fn + t * kFnWords;
-  const int32_t sel = TB.sel[t];
-  uint64_t cnt = 0, s[kVS] = {};
-  if (sel >= 0) {
-    cnt = fn[2 + sel * kAltWords + 1];
-    QFORV(q) s[q] = fn[2 + sel * kAltWords + 2 + q];
-    if (fn[0] == kTermPos) atomicMin(&fc->term_tile, (unsigned long long)t);
-  } else if (sel == kSelTerm) {
-    atomicMin(&fc->term_tile, (unsigned long long)t);
-  } else {
-    atomicAdd(&fc->unresolved, 1ull);  // never expected after the fix passes
-  }
-  TB.contrib[t] = cnt;
-  QFORV(q) TB.contrib[(uint64_t)(1 + q) * TB.ntiles + t] = s[q];
 }
 
 // exclusive prefix sums of the 1 + nsp contribution columns over the tiles,
@@ -3624,37 +3689,43 @@ __global__ __launch_bounds__(256) void tscan_reduce(const uint8_t *__restrict__ 
     __syncthreads();
   }
 }
-__global__ __launch_bounds__(1024) void tscan_top(uint8_t *__restrict__ ws, TileBufs TB,
-                                                  uint32_t ncol, uint64_t nb) {
-  __shared__ uint64_t sh[16];
+// (the carry of each block: the sums of the blocks before it, added up here
+// from tscan_reduce's block sums; block 0 writes the totals)
+__global__ __launch_bounds__(256) void tscan_apply(uint8_t *__restrict__ ws, TileBufs TB,
+                                                   uint32_t ncol) {
+  __shared__ uint64_t sh[4], sh2[4], carry_s[1 + kVS];
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
   if (!vec_live(c)) return;
   for (uint32_t col = 0; col < ncol; ++col) {
-    uint64_t *bs = TB.scan + (uint64_t)col * nb;
-    uint64_t carry = 0;
-    for (uint64_t b0 = 0; b0 < nb; b0 += blockDim.x) {
-      const uint64_t b = b0 + threadIdx.x;
-      const uint64_t v = b < nb ? bs[b] : 0;
-      uint64_t tot;
-      const uint64_t ex = block_excl_scan(v, &tot, sh);
-      if (b < nb) bs[b] = carry + ex;
-      carry += tot;
+    const uint64_t *bs = TB.scan + (uint64_t)col * gridDim.x;
+    uint64_t before = 0, all = 0;
+    for (uint32_t b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
+      const uint64_t v = bs[b];
+      all += v;
+      before += b < blockIdx.x ? v : 0;
     }
+    for (int o = 32; o > 0; o >>= 1) {
+      before += __shfl_down(before, o);
+      all += __shfl_down(all, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      sh[threadIdx.x >> 6] = before;
+      sh2[threadIdx.x >> 6] = all;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
-      if (col == 0)
-        fc->total = carry;
-      else
-        fc->stot[col - 1] = carry;
+      carry_s[col] = sh[0] + sh[1] + sh[2] + sh[3];
+      const uint64_t tot = sh2[0] + sh2[1] + sh2[2] + sh2[3];
+      if (blockIdx.x == 0) {
+        if (col == 0)
+          fc->total = tot;
+        else
+          fc->stot[col - 1] = tot;
+      }
     }
+    __syncthreads();
   }
-}
-__global__ __launch_bounds__(256) void tscan_apply(const uint8_t *__restrict__ ws, TileBufs TB,
-                                                   uint32_t ncol) {
-  __shared__ uint64_t sh[4];
-  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
-  const FCtl *fc = reinterpret_cast<const FCtl *>(ws + kWsFCtl);
-  if (!vec_live(c)) return;
   const uint64_t lim = fc->term_tile < TB.ntiles ? fc->term_tile + 1 : TB.ntiles;
   const uint64_t b0 = (uint64_t)blockIdx.x * kTScanBlock;
   const uint64_t i0 = b0 + (uint64_t)threadIdx.x * kTScanIPT;
@@ -3667,7 +3738,7 @@ __global__ __launch_bounds__(256) void tscan_apply(const uint8_t *__restrict__ w
       s += v[j];
     }
     uint64_t tot;
-    uint64_t run = TB.scan[(uint64_t)col * gridDim.x + blockIdx.x] + block_excl_scan(s, &tot, sh);
+    uint64_t run = carry_s[col] + block_excl_scan(s, &tot, sh);
 #pragma unroll
     for (uint32_t j = 0; j < kTScanIPT; ++j) {
       if (i0 + j < TB.ntiles) io[i0 + j] = run;
@@ -3925,10 +3996,15 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
   }
 }
 
-// The queued long-span pieces: one block per piece, 16-B aligned stores.
-__global__ __launch_bounds__(256) void vec_big_copy(const uint8_t *__restrict__ wire,
-                                                    const uint8_t *__restrict__ ws, BigQ bq) {
-  const FCtl *fc = reinterpret_cast<const FCtl *>(ws + kWsFCtl);
+__device__ void tile_finish(const DecArgs &a, const uint8_t *__restrict__ wire,
+                            const uint8_t *__restrict__ ws, spk_dresult_t *res);
+// The queued long-span pieces: one block per piece, 16-B aligned stores; the
+// last block to finish writes the result (tile_finish: one launch less).
+__global__ __launch_bounds__(256) void vec_big_copy(DecArgs a, const uint8_t *__restrict__ wire,
+                                                    uint8_t *__restrict__ ws, BigQ bq,
+                                                    spk_dresult_t *res) {
+  __shared__ uint32_t last_s;
+  FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
   const uint64_t nj = fc->njobs < bq.cap ? fc->njobs : bq.cap;
   for (uint64_t j = blockIdx.x; j < nj; j += gridDim.x) {
     const BigJob jb = bq.jobs[j];
@@ -3943,6 +4019,9 @@ __global__ __launch_bounds__(256) void vec_big_copy(const uint8_t *__restrict__ 
           *reinterpret_cast<const v4u_una *>(src + h + 16 * v);
     for (uint64_t b = h + 16 * nv + threadIdx.x; b < jb.n; b += blockDim.x) dst[b] = src[b];
   }
+  if (threadIdx.x == 0) last_s = atomicAdd(&fc->copy_done, 1ull) == gridDim.x - 1;
+  __syncthreads();
+  if (last_s && threadIdx.x < 64) tile_finish(a, wire, ws, res);
 }
 
 // spk_decode_shard_index's summary of the range
@@ -3981,14 +4060,16 @@ __global__ void vec_shard_setn(uint8_t *__restrict__ ws, uint64_t first, uint32_
   fc->last = last;
   fc->end_pos = 0;
   fc->njobs = 0;
+  fc->copy_done = 0;
   for (int k = 0; k < kVS; ++k) fc->htot[k] = 0;
 }
 
 // Result: count / consume_len / heap use, or the errc of a short payload
 // (no_buffer_space; invalid_buffer for an overlong varint where the path ends).
-__global__ void vec_tile_finish(DecArgs a, const uint8_t *__restrict__ wire,
-                                const uint8_t *__restrict__ ws, spk_dresult_t *res) {
-  if (a.nested) nt_stage_wave(a.nl, threadIdx.x);  // (launched with one wave)
+// One wave (lane 0 writes).
+__device__ void tile_finish(const DecArgs &a, const uint8_t *__restrict__ wire,
+                            const uint8_t *__restrict__ ws, spk_dresult_t *res) {
+  if (a.nested) nt_stage_wave(a.nl, threadIdx.x & 63);
   if (threadIdx.x != 0) return;
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   const FCtl *fc = reinterpret_cast<const FCtl *>(ws + kWsFCtl);
@@ -4044,6 +4125,10 @@ __global__ void vec_tile_finish(DecArgs a, const uint8_t *__restrict__ wire,
   }
   *res = r;
 }
+__global__ void vec_tile_finish(DecArgs a, const uint8_t *__restrict__ wire,
+                                const uint8_t *__restrict__ ws, spk_dresult_t *res) {
+  tile_finish(a, wire, ws, res);  // (launched with one wave)
+}
 
 // ===========================================================================
 // host launchers
@@ -4055,7 +4140,7 @@ static unsigned grid_for(uint64_t items, uint64_t per_block) {
 
 // ---- tile decoder: workspace and launch ---------------------------------------
 struct TileWs {
-  size_t fn, cused, cex, ccnt, csum, sel, contrib, scan, blist, jobs, nl, end;
+  size_t fn, cused, cex, ccnt, csum, sel, contrib, scan, blist, ent, jobs, nl, end;
   uint64_t ntiles, nchunks, nsb;
 };
 // ns: span counts per record (flat: SPAN + OPTION members; nested: heaps)
@@ -4080,6 +4165,7 @@ static TileWs tile_ws_layout(uint32_t ns, uint64_t wire_len) {
   f.contrib = take(f.ntiles * 8 * (1 + ns));
   f.scan = take(f.nsb * 8 * (1 + ns));
   f.blist = take(f.ntiles * 4);
+  f.ent = take(f.ntiles * 8);
   f.jobs = take(big_jobs_cap(wire_len) * sizeof(BigJob));
   f.nl = take(sizeof(NTLayout));                  // nested layouts: the walker's layout
   f.end = off;
@@ -4129,6 +4215,7 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
   TB.contrib = reinterpret_cast<uint64_t *>(ws + f.contrib);
   TB.scan = reinterpret_cast<uint64_t *>(ws + f.scan);
   TB.blist = reinterpret_cast<uint32_t *>(ws + f.blist);
+  TB.ent = reinterpret_cast<uint64_t *>(ws + f.ent);
   TB.ntiles = f.ntiles;
   TB.nchunks = f.nchunks;
   const uint32_t nsp = P.ns ? P.ns : 1;
@@ -4157,13 +4244,10 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
     SPK_LAUNCH(vec_tile_pick, dim3(grid_for(f.ntiles, 256)), dim3(256), 0, s, ws, TB, nsp, pass);
     SPK_LAUNCH(vec_tile_repair<NS>, dim3(kRepairGrid), dim3(64), 0, s, a, P, wire, ws, TB, pass);
   }
-  SPK_LAUNCH(vec_chain_first, dim3(grid_for(f.ntiles, 256)), dim3(256), 0, s, ws, TB, 2u);
   SPK_LAUNCH(vec_tile_chain<NS>, dim3(kChainGrid), dim3(64 * kChainWaves<NS>), 0, s, a, P, wire,
              ws, TB, 2u);
-  SPK_LAUNCH(vec_tile_contrib, dim3(grid_for(f.ntiles, 256)), dim3(256), 0, s, ws, TB, nsp);
   SPK_LAUNCH(tscan_reduce, dim3(nb), dim3(256), 0, s, (const uint8_t *)ws, TB, 1 + nsp);
-  SPK_LAUNCH(tscan_top, dim3(1), dim3(1024), 0, s, ws, TB, 1 + nsp, (uint64_t)nb);
-  SPK_LAUNCH(tscan_apply, dim3(nb), dim3(256), 0, s, (const uint8_t *)ws, TB, 1 + nsp);
+  SPK_LAUNCH(tscan_apply, dim3(nb), dim3(256), 0, s, ws, TB, 1 + nsp);
   }
   if (phase == kTilesIndex) {
     SPK_LAUNCH(vec_shard_summary, dim3(1), dim3(64), 0, s, (const uint8_t *)ws, TB, nsp,
@@ -4180,9 +4264,10 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
              dim3(64 * kDecWaves), 0, s, a, P, wire, ws, TB, d_recs, bq, tile_dbg());
   if (P.ns) {
     const uint64_t gb = bq.cap < 2048 ? bq.cap : 2048;
-    SPK_LAUNCH(vec_big_copy, dim3((unsigned)gb), dim3(256), 0, s, wire, (const uint8_t *)ws, bq);
+    SPK_LAUNCH(vec_big_copy, dim3((unsigned)gb), dim3(256), 0, s, a, wire, ws, bq, d_res);
+  } else {
+    SPK_LAUNCH(vec_tile_finish, dim3(1), dim3(64), 0, s, a, wire, (const uint8_t *)ws, d_res);
   }
-  SPK_LAUNCH(vec_tile_finish, dim3(1), dim3(64), 0, s, a, wire, (const uint8_t *)ws, d_res);
   return hipGetLastError();
 }
 
