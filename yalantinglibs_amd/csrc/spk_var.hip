@@ -4019,7 +4019,10 @@ __global__ __launch_bounds__(256) void vec_big_copy(DecArgs a, const uint8_t *__
           *reinterpret_cast<const v4u_una *>(src + h + 16 * v);
     for (uint64_t b = h + 16 * nv + threadIdx.x; b < jb.n; b += blockDim.x) dst[b] = src[b];
   }
-  if (threadIdx.x == 0) last_s = atomicAdd(&fc->copy_done, 1ull) == gridDim.x - 1;
+  // (blocks without a piece take no part: one counter add per busy block)
+  const uint64_t busy = nj < gridDim.x ? nj : gridDim.x;
+  if (blockIdx.x >= (busy ? busy : 1)) return;
+  if (threadIdx.x == 0) last_s = !busy || atomicAdd(&fc->copy_done, 1ull) == busy - 1;
   __syncthreads();
   if (last_s && threadIdx.x < 64) tile_finish(a, wire, ws, res);
 }
