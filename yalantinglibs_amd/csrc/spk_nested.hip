@@ -70,11 +70,23 @@ __device__ __forceinline__ uint32_t n_vi_len(uint64_t v) {
   }
   return n;
 }
+// (unaligned 16-, 8- and 4-B accesses: one load and one store each on gfx950;
+// a string copied byte by byte was one partial-line store per byte)
+typedef uint64_t n_u64_una __attribute__((aligned(1)));
+typedef uint32_t n_u32_una __attribute__((aligned(1)));
+typedef v4u_t n_v4u_una __attribute__((aligned(1)));
 __device__ __forceinline__ void n_copy(uint8_t *d, const uint8_t *s, uint64_t n) {
   uint64_t i = 0;
-  if ((((uintptr_t)d | (uintptr_t)s) & 7) == 0)
-    for (; i + 8 <= n; i += 8)
-      *reinterpret_cast<uint64_t *>(d + i) = *reinterpret_cast<const uint64_t *>(s + i);
+  for (; i + 16 <= n; i += 16)
+    *reinterpret_cast<n_v4u_una *>(d + i) = *reinterpret_cast<const n_v4u_una *>(s + i);
+  if (i + 8 <= n) {
+    *reinterpret_cast<n_u64_una *>(d + i) = *reinterpret_cast<const n_u64_una *>(s + i);
+    i += 8;
+  }
+  if (i + 4 <= n) {
+    *reinterpret_cast<n_u32_una *>(d + i) = *reinterpret_cast<const n_u32_una *>(s + i);
+    i += 4;
+  }
   for (; i < n; ++i) d[i] = s[i];
 }
 
@@ -84,6 +96,9 @@ __device__ __forceinline__ void n_copy(uint8_t *d, const uint8_t *s, uint64_t n)
 // 16-B loads instead of each lane's scattered byte loads). A raw pointer is
 // the global-only reader.
 typedef __attribute__((address_space(3))) uint8_t nlds_u8;
+typedef __attribute__((address_space(3))) uint32_t nlds_u32_una __attribute__((aligned(1)));
+typedef __attribute__((address_space(3))) uint64_t nlds_u64_una __attribute__((aligned(1)));
+typedef __attribute__((address_space(3))) v4u_t nlds_v4u_una __attribute__((aligned(1)));
 struct NRd {
   const uint8_t *w;
   const nlds_u8 *lds;
@@ -97,8 +112,19 @@ __device__ __forceinline__ void n_copy_rd(uint8_t *d, const uint8_t *w, uint64_t
 }
 __device__ __forceinline__ void n_copy_rd(uint8_t *d, const NRd &rd, uint64_t p, uint64_t n) {
   if (p - rd.lo < rd.hi - rd.lo && rd.hi - p >= n) {
-    const uint32_t o = (uint32_t)(p - rd.lo);
-    for (uint64_t i = 0; i < n; ++i) d[i] = rd.lds[o + i];
+    const nlds_u8 *l = rd.lds + (uint32_t)(p - rd.lo);
+    uint32_t i = 0;
+    for (; i + 16 <= n; i += 16)
+      *reinterpret_cast<n_v4u_una *>(d + i) = *reinterpret_cast<const nlds_v4u_una *>(l + i);
+    if (i + 8 <= n) {
+      *reinterpret_cast<n_u64_una *>(d + i) = *reinterpret_cast<const nlds_u64_una *>(l + i);
+      i += 8;
+    }
+    if (i + 4 <= n) {
+      *reinterpret_cast<n_u32_una *>(d + i) = *reinterpret_cast<const nlds_u32_una *>(l + i);
+      i += 4;
+    }
+    for (; i < n; ++i) d[i] = l[i];
   } else {
     n_copy(d, rd.w + p, n);
   }
