@@ -896,6 +896,7 @@ __device__ int n_read_compat(const NLayout &N, const Rd &wire, uint64_t &pos, ui
 // ---- device-wide exclusive scan of C u64 columns [C][n] (in place) ---------------
 constexpr uint32_t kNScanT = 256, kNScanIPT = 8;
 constexpr uint64_t kNScanBlk = (uint64_t)kNScanT * kNScanIPT;
+constexpr uint64_t kNScanFold = 2048;
 
 __device__ __forceinline__ uint64_t n_block_excl(uint64_t v, uint64_t *sh, uint64_t *tot) {
   const uint32_t t = threadIdx.x;
@@ -976,26 +977,77 @@ __global__ __launch_bounds__(1024) void nscan_top(uint64_t *__restrict__ part, u
   if (threadIdx.x == 0) p[nb] = carry;
 }
 
+__device__ __forceinline__ uint64_t n_wave_incl(uint64_t v, uint32_t lane) {
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint64_t x = __shfl_up(v, o);
+    if (lane >= o) v += x;
+  }
+  return v;
+}
+// sum over the block (every thread gets it)
+__device__ __forceinline__ uint64_t n_block_sum(uint64_t v, uint64_t *sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint64_t t = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kNScanT / 64; ++w) t += sh[w];
+  __syncthreads();
+  return t;
+}
+// Each wave scans 512 consecutive elements loaded 64 at a time (coalesced;
+// round 4 loaded 8 consecutive per thread: every load instruction touched 64
+// lines). fold: the block adds up the partial sums of the blocks before it
+// (nscan_top not launched; block 0 writes the column total at [nb]).
 __global__ __launch_bounds__(kNScanT) void nscan_apply(uint64_t *__restrict__ col, uint64_t n,
-                                                       const uint64_t *__restrict__ part,
+                                                       uint64_t *__restrict__ part,
                                                        uint64_t nb, const uint8_t *ws,
-                                                       const uint32_t *cond) {
-  __shared__ uint64_t sh[kNScanT];
+                                                       const uint32_t *cond, uint32_t fold) {
+  __shared__ uint64_t sh[kNScanT / 64], wsum[kNScanT / 64];
   if (tok_skip(ws, cond)) return;
   const uint64_t c = blockIdx.y;
-  const uint64_t base = (uint64_t)blockIdx.x * kNScanBlk + (uint64_t)threadIdx.x * kNScanIPT;
-  uint64_t v[kNScanIPT], s = 0;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t base = (uint64_t)blockIdx.x * kNScanBlk + (uint64_t)wv * 64 * kNScanIPT;
+  uint64_t *cc = col + c * n;
+  uint64_t v[kNScanIPT], ex[kNScanIPT], run = 0;
+#pragma unroll
   for (uint32_t k = 0; k < kNScanIPT; ++k) {
-    const uint64_t i = base + k;
-    v[k] = i < n ? col[c * n + i] : 0;
-    s += v[k];
+    const uint64_t i = base + (uint64_t)k * 64 + lane;
+    v[k] = i < n ? cc[i] : 0;
   }
-  uint64_t tot;
-  uint64_t run = part[c * (nb + 1) + blockIdx.x] + n_block_excl(s, sh, &tot);
+#pragma unroll
   for (uint32_t k = 0; k < kNScanIPT; ++k) {
-    const uint64_t i = base + k;
-    if (i < n) col[c * n + i] = run;
-    run += v[k];
+    const uint64_t incl = n_wave_incl(v[k], lane);
+    ex[k] = run + incl - v[k];
+    run += __shfl(incl, 63);
+  }
+  if (lane == 0) wsum[wv] = run;
+  uint64_t *p = part + c * (nb + 1);
+  uint64_t carry;
+  if (fold) {
+    uint64_t before = 0, all = 0;
+    for (uint64_t b = threadIdx.x; b < nb; b += kNScanT) {
+      const uint64_t x = p[b];
+      before += b < blockIdx.x ? x : 0;
+      all += x;
+    }
+    carry = n_block_sum(before, sh);
+    if (blockIdx.x == 0) {
+      all = n_block_sum(all, sh);
+      if (threadIdx.x == 0) p[nb] = all;
+    }
+  } else {
+    carry = p[blockIdx.x];
+    __syncthreads();
+  }
+  uint64_t woff = 0;
+  for (uint32_t w = 0; w < wv; ++w) woff += wsum[w];
+#pragma unroll
+  for (uint32_t k = 0; k < kNScanIPT; ++k) {
+    const uint64_t i = base + (uint64_t)k * 64 + lane;
+    if (i < n) cc[i] = carry + woff + ex[k];
   }
 }
 
@@ -1011,9 +1063,12 @@ static hipError_t nscan(uint64_t *col, uint64_t n, uint32_t ncols, uint64_t *par
   const uint64_t nb = (n + kNScanBlk - 1) / kNScanBlk;
   SPK_LAUNCH(nscan_reduce, dim3((unsigned)nb, ncols), dim3(kNScanT), 0, s, (const uint64_t *)col,
              n, part, nb + 1, ws, cond);
-  SPK_LAUNCH(nscan_top, dim3(ncols), dim3(1024), 0, s, part, nb, ws, cond);
-  SPK_LAUNCH(nscan_apply, dim3((unsigned)nb, ncols), dim3(kNScanT), 0, s, col, n,
-             (const uint64_t *)part, nb, ws, cond);
+  // (up to kNScanFold blocks a column, each apply block adds up the partials
+  // before it: one launch less)
+  const uint32_t fold = nb <= kNScanFold ? 1u : 0u;
+  if (!fold) SPK_LAUNCH(nscan_top, dim3(ncols), dim3(1024), 0, s, part, nb, ws, cond);
+  SPK_LAUNCH(nscan_apply, dim3((unsigned)nb, ncols), dim3(kNScanT), 0, s, col, n, part, nb, ws,
+             cond, fold);
   return hipGetLastError();
 }
 static size_t nscan_part_bytes(uint64_t n, uint32_t ncols) {
