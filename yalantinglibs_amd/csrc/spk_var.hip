@@ -1531,6 +1531,7 @@ __host__ __device__ constexpr uint32_t win_slots(uint32_t nv) { return nv + 1; }
 // stores in vmcnt), which serialised K4's record stores.
 template <bool LO>
 struct WinReaderT {
+  static constexpr bool kLO = LO;
   const lds_u32 *d;
   const uint8_t *wire;
   uint64_t cs, wend;
@@ -1636,12 +1637,55 @@ __host__ __device__ constexpr uint64_t big_jobs_cap(uint64_t wire_len) {
   return wire_len / kBigCopy + wire_len / kBigPiece + 1;
 }
 
-// emit_record reading the wire through an LDS window reader
+// Spans of kWaveCopy bytes and more (below kBigCopy) in a group of records
+// that leaves the window are copied by the whole wave after the group's
+// records are written (copied by their own lanes, 64 strings of 100-3000 B
+// went at the pace of the longest, every instruction touching 64 lines:
+// c3l K4 5.3 ms). A group inside the window (the LDS-only reader) holds no
+// such span, and its path has none of this code (registers: C3 K4).
+constexpr uint64_t kWaveCopy = 256;
+struct Deferred {
+  uint64_t src, n;
+  uint8_t *dst;
+};
 template <typename Rd>
-__device__ __forceinline__ void emit_record_rd(const KLayout &L, const Rd &rd,
+__device__ __forceinline__ void wave_span_copy(const Rd &R, uint64_t x, uint8_t *dst, uint64_t n,
+                                               uint32_t lane) {
+  const uint64_t nc = n >> 4;
+  for (uint64_t c = lane; c < nc; c += 64) {
+    const uint64_t s = x + 16 * c;
+    v4u_t v;
+    if (s + 16 <= R.wend)
+      v = R.ld16(s);
+    else
+      v = *reinterpret_cast<const v4u_una *>(R.wire + s);
+    *reinterpret_cast<v4u_una *>(dst + 16 * c) = v;
+  }
+  const uint64_t t = nc << 4;
+  if (lane < n - t) dst[t + lane] = (uint8_t)R.byte(x + t + lane);
+}
+// the spans the lanes of mask m listed (list[lane], LDS), each by the whole wave
+template <typename Rd>
+__device__ __forceinline__ void wave_copy_deferred(const Rd &R, const Deferred *list, uint64_t m,
+                                                   uint32_t lane) {
+  while (m) {
+    const uint32_t l = (uint32_t)__builtin_ctzll(m);
+    m &= m - 1;
+    const Deferred d = list[l];
+    wave_span_copy(R, d.src, d.dst, d.n, lane);
+  }
+}
+
+// emit_record reading the wire through an LDS window reader; with df set,
+// the first span of kWaveCopy bytes or more goes to *df (returns whether one
+// did)
+template <typename Rd>
+__device__ __forceinline__ bool emit_record_rd(const KLayout &L, const Rd &rd,
                                                uint64_t pos, uint32_t w, uint8_t *rec,
                                                uint8_t *const *heaps, const uint64_t *off,
-                                               uint64_t end, const BigQ &bq, uint32_t dbg = 0) {
+                                               uint64_t end, const BigQ &bq, uint32_t dbg = 0,
+                                               Deferred *df = nullptr) {
+  bool deferred = false;
   uint32_t sk = 0;
   for (uint32_t o = 0; o < L.n_ops; ++o) {
     const spk_op op = L.ops[o];
@@ -1673,6 +1717,9 @@ __device__ __forceinline__ void emit_record_rd(const KLayout &L, const Rd &rd,
           else
             copy_bytes(hp + o, rd.wire + pos + o, m);  // (the cap is never reached)
         }
+      } else if (!Rd::kLO && df && nb >= kWaveCopy && !deferred) {
+        *df = Deferred{pos, nb, hp};
+        deferred = true;
       } else if (!(dbg & 256)) {
         rd.copy_to(hp, pos, nb);
       }
@@ -1680,6 +1727,7 @@ __device__ __forceinline__ void emit_record_rd(const KLayout &L, const Rd &rd,
       ++sk;
     }
   }
+  return deferred;
 }
 
 // ===========================================================================
@@ -3770,7 +3818,12 @@ template <int NS>  // record starts per emission pass (the nested path keeps non
 constexpr uint32_t kEmitTab = NS <= -2 ? 1u : kTab / kEmitSplit<NS>;
 constexpr uint16_t kTabFar = 0xFFFFu;  // a table end past the window
 
-template <int NS>
+// DEFER: spans of kWaveCopy bytes or more in groups that leave the window
+// are copied by the whole wave (wave_copy_deferred). The launch takes it when
+// the caller's records average kWaveCopy wire bytes or more (wire_len /
+// rec_cap): its registers cost K4 a wave per SIMD (C3 K4 0.304 -> 0.326 ms),
+// which messages of short records need not pay (c3l K4 5.3 -> 2.2 ms).
+template <int NS, bool DEFER = false>
 __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkProg P,
                                                                 const uint8_t *__restrict__ wire,
                                                                 uint8_t *__restrict__ ws,
@@ -3782,6 +3835,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
   constexpr uint32_t kEmitTab = spk::kEmitTab<NS>;
   __shared__ v4u_t win_s[kDecWaves][win_slots(kEmitVec)];
   __shared__ uint16_t tab_s[kDecWaves][kEmitTab + 2];  // (+ the pass's end)
+  __shared__ Deferred dfl_s[kDecWaves][DEFER ? 64 : 1];  // spans for the wave
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -3949,7 +4003,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
     // scans of their counts, then the record and its payloads written. R: the
     // window reader; the LDS-only one when all 64 records lie inside the
     // window (their stores then never wait on a load)
-    auto emit64 = [&](const auto &R, uint64_t i0) {
+    auto emit64 = [&](const auto &R, uint64_t i0) -> uint64_t {
       const uint64_t i = i0 + lane;
       const bool act = i < nrec;
       const uint64_t pos = wb + (act ? tab[i] : 0);
@@ -3965,16 +4019,21 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
         if (off[q] + rc[q] > a.heap_cap[q]) fits = false;
       }
       const uint64_t gr = base + pass0 + i;
+      bool dfd = false;
       if (act && gr < a.rec_cap && fits && !(dbg & 64)) {
         if constexpr (NS <= -2)
           nt_emit<NS == -3>(rd, pos, len, recs + gr * a.L.stride, off, bq);
-        else
+        else if constexpr (!DEFER || std::decay_t<decltype(R)>::kLO)
           emit_record_rd(a.L, R, pos, w, recs + gr * a.L.stride, a.heaps, off, len, bq, dbg);
+        else
+          dfd = emit_record_rd(a.L, R, pos, w, recs + gr * a.L.stride, a.heaps, off, len, bq,
+                               dbg, &dfl_s[wv][lane]);
       }
       if (act && gr == n - 1) {
         fc->end_pos = pos + L;
         QFOR(q) fc->htot[q] = off[q] + rc[q];
       }
+      return __ballot(dfd);
     };
     for (uint64_t i0 = 0; i0 < nrec; i0 += 64) {
       if constexpr (NS > -2) {
@@ -3988,7 +4047,8 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
           continue;
         }
       }
-      emit64(rd, i0);
+      const uint64_t dm = emit64(rd, i0);
+      if (DEFER && dm) wave_copy_deferred(rd, dfl_s[wv], dm, lane);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -4263,8 +4323,12 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
   bq.jobs = reinterpret_cast<BigJob *>(ws + f.jobs);
   bq.n = &reinterpret_cast<FCtl *>(ws + kWsFCtl)->njobs;
   bq.cap = big_jobs_cap(a.wire_len);
-  SPK_LAUNCH(vec_tile_emit<NS>, dim3(grid_for(f.ntiles * kEmitSplit<NS>, kDecWaves)),
-             dim3(64 * kDecWaves), 0, s, a, P, wire, ws, TB, d_recs, bq, tile_dbg());
+  if (NS > -2 && a.rec_cap && a.wire_len / a.rec_cap >= kWaveCopy)
+    SPK_LAUNCH((vec_tile_emit<NS, (NS > -2)>), dim3(grid_for(f.ntiles * kEmitSplit<NS>, kDecWaves)),
+               dim3(64 * kDecWaves), 0, s, a, P, wire, ws, TB, d_recs, bq, tile_dbg());
+  else
+    SPK_LAUNCH(vec_tile_emit<NS>, dim3(grid_for(f.ntiles * kEmitSplit<NS>, kDecWaves)),
+               dim3(64 * kDecWaves), 0, s, a, P, wire, ws, TB, d_recs, bq, tile_dbg());
   if (P.ns) {
     const uint64_t gb = bq.cap < 2048 ? bq.cap : 2048;
     SPK_LAUNCH(vec_big_copy, dim3((unsigned)gb), dim3(256), 0, s, a, wire, ws, bq, d_res);
