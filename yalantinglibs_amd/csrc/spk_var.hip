@@ -1208,6 +1208,7 @@ struct FCtl {
   unsigned long long chain_ticket;  // tiles the chain's blocks have taken
   unsigned long long chain_arrive;  // chain blocks arrived (the first one finds the first tile)
   unsigned long long chain_ready;   // the chain's first tile + 1 (0: not yet found)
+  unsigned long long chain_done;    // chain blocks out (the last one sums the tile scan)
   unsigned long long copy_done;     // vec_big_copy blocks done (the last one writes the result)
 };
 constexpr size_t kWsFCtl = kWsCtl + 1280;
@@ -1462,6 +1463,7 @@ __device__ void vec_hdr_body(const DecArgs &a, const uint8_t *__restrict__ wire,
   fc->chain_ticket = 0;
   fc->chain_arrive = 0;
   fc->chain_ready = 0;
+  fc->chain_done = 0;
   fc->copy_done = 0;
   fc->njobs = 0;
   fc->term_tile = ~0ull;
@@ -3393,7 +3395,7 @@ __global__ __launch_bounds__(64) void vec_tile_repair(DecArgs a, WalkProg P,
 // tile's selection is final); the first tile whose path ends inside it (its
 // exit is kTermPos) ----------------------------------------------------------
 __device__ __forceinline__ void tile_contrib(const TileBufs &TB, FCtl *fc, uint64_t t,
-                                             uint32_t nsp) {
+                                             uint32_t nsp, uint64_t *col = nullptr) {
   const uint64_t *fn = TB.fn + t * kFnWords;
   const int32_t sel = TB.sel[t];
   uint64_t cnt = 0, s[kVS] = {};
@@ -3408,6 +3410,47 @@ __device__ __forceinline__ void tile_contrib(const TileBufs &TB, FCtl *fc, uint6
   }
   TB.contrib[t] = cnt;
   QFORV(q) TB.contrib[(uint64_t)(1 + q) * TB.ntiles + t] = s[q];
+  if (col) {
+    col[0] += cnt;
+    QFORV(q) col[1 + q] += s[q];
+  }
+}
+
+// K3's segments: kTScanBlock consecutive tiles; the tile scan's carries are
+// the segment sums (tscan_apply)
+constexpr uint32_t kTScanIPT = 8;
+constexpr uint64_t kTScanBlock = 256ull * kTScanIPT;
+// segment seg's column sums into TB.scan[col * nb + seg] (a block of NT
+// threads); CONTRIB: each tile's contribution is written on the way
+template <uint32_t NT, bool CONTRIB>
+__device__ void tscan_segment(const TileBufs &TB, FCtl *fc, uint64_t seg, uint64_t nb,
+                              uint32_t nsp, uint64_t *sh) {
+  uint64_t v[1 + kVS] = {};
+  const uint64_t b0 = seg * kTScanBlock;
+  for (uint64_t k = threadIdx.x; k < kTScanBlock; k += NT) {
+    const uint64_t i = b0 + k;
+    if (i >= TB.ntiles) break;
+    if (CONTRIB) {
+      tile_contrib(TB, fc, i, nsp, v);
+    } else {
+      v[0] += TB.contrib[i];
+      QFORV(q) v[1 + q] += TB.contrib[(uint64_t)(1 + q) * TB.ntiles + i];
+    }
+  }
+  for (uint32_t c = 0; c < 1 + nsp && c < 1 + kVS; ++c) {
+    uint64_t x = v[0];
+#pragma unroll
+    for (uint32_t k = 1; k < 1 + kVS; ++k) x = c == k ? v[k] : x;
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint64_t t = 0;
+      for (uint32_t w = 0; w < NT / 64; ++w) t += sh[w];
+      TB.scan[(uint64_t)c * nb + seg] = t;
+    }
+    __syncthreads();
+  }
 }
 
 // ---- K2, what the passes leave: the tile chain ------------------------------
@@ -3487,9 +3530,12 @@ __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
   if (!vec_live(c)) return;  // (block-uniform)
   const uint64_t nt = TB.ntiles, gstride = (uint64_t)gridDim.x * kNT;
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
-  if (!fc->broken[last_pass]) {  // the passes left nothing: every tile's contribution
-    for (uint64_t t = (uint64_t)blockIdx.x * kNT + tid; t < nt; t += gstride)
-      tile_contrib(TB, fc, t, nsp);
+  const uint64_t nb = (nt + kTScanBlock - 1) / kTScanBlock;
+  if (!fc->broken[last_pass]) {
+    // the passes left nothing: every tile's contribution and the tile scan's
+    // segment sums (no tscan_reduce launch)
+    for (uint64_t seg = blockIdx.x; seg < nb; seg += gridDim.x)
+      tscan_segment<kNT, true>(TB, fc, seg, nb, nsp, red_s);
     return;
   }
   uint64_t *ent = TB.ent;
@@ -3535,12 +3581,12 @@ __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
     TB.sel[t] = tile_sel_now(TB, fc, t, &bad);
     tile_contrib(TB, fc, t, nsp);
   }
-  if (f0 >= nt) return;
   __syncthreads();
   if (w0) nt_prologue<NS>(a, lane);
   const uint32_t w = c->w;
   const uint64_t len = a.wire_len, p0 = c->p0;
   for (;;) {
+    if (f0 >= nt) break;
     // tiles in order: a block waits only for tiles claimed before its own,
     // and those belong to blocks already running
     if (tid == 0) tile_s = f0 + atomicAdd(&fc->chain_ticket, 1ull);
@@ -3709,72 +3755,48 @@ __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
     }
     __syncthreads();  // the window, the map and tile_s are reused
   }
+  // every tile is final once all blocks are out: the last block out adds up
+  // the tile scan's segment sums (the producer / consumer fences of the
+  // counter hand-off: every wave's stores drained, then an agent release
+  // before the add; the last one acquires before it reads)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tile_s = atomicAdd(&fc->chain_done, 1ull) == gridDim.x - 1 ? 1ull : 0ull;
+    if (tile_s) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (tile_s)
+    for (uint64_t seg = 0; seg < nb; ++seg) tscan_segment<kNT, false>(TB, fc, seg, nb, nsp, red_s);
 }
 
-// exclusive prefix sums of the 1 + nsp contribution columns over the tiles,
-// zero past fc->term_tile; totals -> fc->total / fc->stot
-constexpr uint32_t kTScanIPT = 8;
-constexpr uint64_t kTScanBlock = 256ull * kTScanIPT;
-__global__ __launch_bounds__(256) void tscan_reduce(const uint8_t *__restrict__ ws, TileBufs TB,
-                                                    uint32_t ncol) {
-  __shared__ uint64_t sh[4];
-  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
-  const FCtl *fc = reinterpret_cast<const FCtl *>(ws + kWsFCtl);
-  if (!vec_live(c)) return;
-  const uint64_t lim = fc->term_tile < TB.ntiles ? fc->term_tile + 1 : TB.ntiles;
-  const uint64_t b0 = (uint64_t)blockIdx.x * kTScanBlock;
-  for (uint32_t col = 0; col < ncol; ++col) {
-    const uint64_t *in = TB.contrib + (uint64_t)col * TB.ntiles;
-    uint64_t v = 0;
-    for (uint32_t j = 0; j < kTScanIPT; ++j) {
-      const uint64_t i = b0 + (uint64_t)j * 256 + threadIdx.x;
-      if (i < lim) v += in[i];
-    }
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o);
-    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) TB.scan[(uint64_t)col * gridDim.x + blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
-    __syncthreads();
-  }
-}
-// (the carry of each block: the sums of the blocks before it, added up here
-// from tscan_reduce's block sums; block 0 writes the totals)
+// exclusive prefix sums of the 1 + nsp contribution columns over the tiles up
+// to fc->term_tile; totals -> fc->total / fc->stot (the carry of each block:
+// the segment sums before it, added up here from the sums vec_tile_chain
+// wrote; the block holding the path's last tile writes the totals)
 __global__ __launch_bounds__(256) void tscan_apply(uint8_t *__restrict__ ws, TileBufs TB,
                                                    uint32_t ncol) {
-  __shared__ uint64_t sh[4], sh2[4], carry_s[1 + kVS];
+  __shared__ uint64_t sh[4], carry_s[1 + kVS];
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
   if (!vec_live(c)) return;
+  // segments past the one holding the path's last tile: K4 reads no prefix there
+  const uint64_t lim = fc->term_tile < TB.ntiles ? fc->term_tile + 1 : TB.ntiles;
+  const uint64_t lb = lim ? (lim - 1) / kTScanBlock : 0;
+  if (blockIdx.x > lb) return;
   for (uint32_t col = 0; col < ncol; ++col) {
     const uint64_t *bs = TB.scan + (uint64_t)col * gridDim.x;
-    uint64_t before = 0, all = 0;
-    for (uint32_t b = threadIdx.x; b < gridDim.x; b += blockDim.x) {
-      const uint64_t v = bs[b];
-      all += v;
-      before += b < blockIdx.x ? v : 0;
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      before += __shfl_down(before, o);
-      all += __shfl_down(all, o);
-    }
-    if ((threadIdx.x & 63) == 0) {
-      sh[threadIdx.x >> 6] = before;
-      sh2[threadIdx.x >> 6] = all;
-    }
+    uint64_t before = 0;
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += blockDim.x) before += bs[b];
+    for (int o = 32; o > 0; o >>= 1) before += __shfl_down(before, o);
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = before;
     __syncthreads();
-    if (threadIdx.x == 0) {
-      carry_s[col] = sh[0] + sh[1] + sh[2] + sh[3];
-      const uint64_t tot = sh2[0] + sh2[1] + sh2[2] + sh2[3];
-      if (blockIdx.x == 0) {
-        if (col == 0)
-          fc->total = tot;
-        else
-          fc->stot[col - 1] = tot;
-      }
-    }
+    if (threadIdx.x == 0) carry_s[col] = sh[0] + sh[1] + sh[2] + sh[3];
     __syncthreads();
   }
-  const uint64_t lim = fc->term_tile < TB.ntiles ? fc->term_tile + 1 : TB.ntiles;
   const uint64_t b0 = (uint64_t)blockIdx.x * kTScanBlock;
   const uint64_t i0 = b0 + (uint64_t)threadIdx.x * kTScanIPT;
   for (uint32_t col = 0; col < ncol; ++col) {
@@ -3791,6 +3813,13 @@ __global__ __launch_bounds__(256) void tscan_apply(uint8_t *__restrict__ ws, Til
     for (uint32_t j = 0; j < kTScanIPT; ++j) {
       if (i0 + j < TB.ntiles) io[i0 + j] = run;
       run += v[j];
+    }
+    // the totals: records and heap elements on the path
+    if (blockIdx.x == lb && threadIdx.x == 0) {
+      if (col == 0)
+        fc->total = carry_s[0] + tot;
+      else
+        fc->stot[col - 1] = carry_s[col] + tot;
     }
   }
 }
@@ -4309,7 +4338,6 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
   }
   SPK_LAUNCH(vec_tile_chain<NS>, dim3(kChainGrid), dim3(64 * kChainWaves<NS>), 0, s, a, P, wire,
              ws, TB, 2u);
-  SPK_LAUNCH(tscan_reduce, dim3(nb), dim3(256), 0, s, (const uint8_t *)ws, TB, 1 + nsp);
   SPK_LAUNCH(tscan_apply, dim3(nb), dim3(256), 0, s, ws, TB, 1 + nsp);
   }
   if (phase == kTilesIndex) {
