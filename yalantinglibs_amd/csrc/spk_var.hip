@@ -3416,18 +3416,21 @@ __device__ __forceinline__ void tile_contrib(const TileBufs &TB, FCtl *fc, uint6
   }
 }
 
-// K3's segments: kTScanBlock consecutive tiles; the tile scan's carries are
-// the segment sums (tscan_apply)
+// K3: tscan_apply blocks cover kTScanBlock consecutive tiles; their carries
+// are sums of the segment sums (kTSeg tiles each) that vec_tile_chain writes
+// (segments of a whole apply block kept 12 of its blocks busy for C3, each
+// thread 8 tiles deep: 9.7 us)
 constexpr uint32_t kTScanIPT = 8;
 constexpr uint64_t kTScanBlock = 256ull * kTScanIPT;
+constexpr uint64_t kTSeg = 256;
 // segment seg's column sums into TB.scan[col * nb + seg] (a block of NT
 // threads); CONTRIB: each tile's contribution is written on the way
 template <uint32_t NT, bool CONTRIB>
 __device__ void tscan_segment(const TileBufs &TB, FCtl *fc, uint64_t seg, uint64_t nb,
                               uint32_t nsp, uint64_t *sh) {
   uint64_t v[1 + kVS] = {};
-  const uint64_t b0 = seg * kTScanBlock;
-  for (uint64_t k = threadIdx.x; k < kTScanBlock; k += NT) {
+  const uint64_t b0 = seg * kTSeg;
+  for (uint64_t k = threadIdx.x; k < kTSeg; k += NT) {
     const uint64_t i = b0 + k;
     if (i >= TB.ntiles) break;
     if (CONTRIB) {
@@ -3530,7 +3533,7 @@ __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
   if (!vec_live(c)) return;  // (block-uniform)
   const uint64_t nt = TB.ntiles, gstride = (uint64_t)gridDim.x * kNT;
   const uint32_t nsp = NS > 0 ? (uint32_t)NS : P.ns;
-  const uint64_t nb = (nt + kTScanBlock - 1) / kTScanBlock;
+  const uint64_t nb = (nt + kTSeg - 1) / kTSeg;
   if (!fc->broken[last_pass]) {
     // the passes left nothing: every tile's contribution and the tile scan's
     // segment sums (no tscan_reduce launch)
@@ -3775,8 +3778,9 @@ __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
 
 // exclusive prefix sums of the 1 + nsp contribution columns over the tiles up
 // to fc->term_tile; totals -> fc->total / fc->stot (the carry of each block:
-// the segment sums before it, added up here from the sums vec_tile_chain
-// wrote; the block holding the path's last tile writes the totals)
+// the segment sums before its tiles, added up here from the sums
+// vec_tile_chain wrote; the block holding the path's last tile writes the
+// totals)
 __global__ __launch_bounds__(256) void tscan_apply(uint8_t *__restrict__ ws, TileBufs TB,
                                                    uint32_t ncol) {
   __shared__ uint64_t sh[4], carry_s[1 + kVS];
@@ -3787,10 +3791,12 @@ __global__ __launch_bounds__(256) void tscan_apply(uint8_t *__restrict__ ws, Til
   const uint64_t lim = fc->term_tile < TB.ntiles ? fc->term_tile + 1 : TB.ntiles;
   const uint64_t lb = lim ? (lim - 1) / kTScanBlock : 0;
   if (blockIdx.x > lb) return;
+  const uint64_t nseg = (TB.ntiles + kTSeg - 1) / kTSeg;
+  const uint64_t s0 = (uint64_t)blockIdx.x * (kTScanBlock / kTSeg);  // segments before it
   for (uint32_t col = 0; col < ncol; ++col) {
-    const uint64_t *bs = TB.scan + (uint64_t)col * gridDim.x;
+    const uint64_t *bs = TB.scan + (uint64_t)col * nseg;
     uint64_t before = 0;
-    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += blockDim.x) before += bs[b];
+    for (uint64_t b = threadIdx.x; b < s0; b += blockDim.x) before += bs[b];
     for (int o = 32; o > 0; o >>= 1) before += __shfl_down(before, o);
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = before;
     __syncthreads();
@@ -4241,7 +4247,7 @@ static TileWs tile_ws_layout(uint32_t ns, uint64_t wire_len) {
   if (!ns) ns = 1;
   f.ntiles = wire_len / kTileBytes + 1;  // the payload starts past the header
   f.nchunks = f.ntiles * 64;
-  f.nsb = (f.ntiles + kTScanBlock - 1) / kTScanBlock + 1;
+  f.nsb = (f.ntiles + kTSeg - 1) / kTSeg + 1;  // (tile scan segment sums)
   size_t off = kWsScratch;
   auto take = [&](size_t bytes) {
     size_t o = off;
