@@ -204,6 +204,7 @@ RANDOM = [("recs", 1, 300), ("recs", 257, 5), ("recs", 5000, 48), ("recs", 20000
           ("fv", 5000, 48), ("fv", 200, 400), ("fve", 3000, 8), ("fv32", 4000, 0),
           ("ev", 5000, 16), ("ev", 30000, 4), ("valreq", 3000, 16), ("valreq", 100, 400),
           ("exp", 3000, 16), ("cmpg", 3000, 16), ("cmpg", 100, 400), ("monster", 5000, 20),
+          ("cmp", 60000, 16), ("cmpg", 20000, 16), ("cmpnew", 60000, 4),
           ("monster", 200, 400), ("rect2", 20000, 0), ("lists", 3000, 6), ("lists", 100, 300),
           ("maps", 2000, 0), ("cplx", 500, 0)]
 
@@ -227,6 +228,38 @@ def test_random_vs_oracle(case, n, param, modech):
     for k in range(len(heaps)):
         nb = len(heaps[k])
         assert back.heaps[k][:nb].cpu().numpy().tobytes() == heaps[k].tobytes()
+
+
+@pytest.mark.parametrize("case,n,param", [("recs", 5000, 48), ("outer", 3000, 16),
+                                          ("monster", 300, 20), ("cmp", 3000, 16),
+                                          ("cmpg", 1000, 16), ("opt", 3000, 48)])
+@pytest.mark.parametrize("tail", ["zeros", "random", "copy"])
+def test_vector_trailing_bytes(case, n, param, tail):
+    """A VECTOR message followed by other bytes: the reference decodes its
+    count of records and reports consume_len = the message's length
+    (struct_pack.hpp:343-357); the bytes after it need not parse as records.
+    (Round 5: 100 KB of random bytes after an `outer` or `monster` message
+    left a tile unresolved past the message's end, errc 101.)"""
+    cd = codec_for(case)
+    _, recs, heaps = synth.make_batch(case, n, 0x7A11 + n, param)
+    out, _ = cd.serialize(to_dev(cd, recs, heaps), C.SPK_MODE_VECTOR)
+    m = out.cpu().numpy().tobytes()
+    rng = np.random.default_rng(n)
+    for tl in (7, 5000, 100000):
+        t = (bytes(tl) if tail == "zeros" else
+             rng.integers(0, 256, tl, dtype=np.uint8).tobytes() if tail == "random" else
+             (m * (tl // len(m) + 1))[:tl])
+        wire = m + t
+        eres, erecs, eheaps, _ = H.oracle_decode(cd.L, C.SPK_MODE_VECTOR, wire)
+        assert eres.errc == 0 and eres.count == n and eres.consumed == len(m)
+        res, back, _ = cd.deserialize(wire_dev(wire), C.SPK_MODE_VECTOR)
+        assert (res.errc, res.count, res.consumed) == (0, n, len(m)), (tl, res.errc)
+        assert back.recs[:n].cpu().numpy().tobytes() == \
+            np.ascontiguousarray(recs).view(np.uint8).tobytes()
+        for k in range(len(heaps)):
+            assert res.heap_used[k] == eres.heap_used[k]
+            nb = len(heaps[k])
+            assert back.heaps[k][:nb].cpu().numpy().tobytes() == heaps[k].tobytes()
 
 
 def _irregular_messages(cd, case, n, seed, param):

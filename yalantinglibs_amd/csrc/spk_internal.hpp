@@ -304,6 +304,26 @@ hipError_t launch_var_nested_decode(const spk_layout *L, const void *d_wire, uin
                                     void *d_recs, uint64_t rec_cap, void *const *d_heaps,
                                     const uint64_t *heap_caps, spk_dresult_t *d_res, void *d_ws,
                                     hipStream_t s, uint32_t body_w, uint64_t body_n);
+// spk_var.hip: VECTOR decode of a layout with compatible members on the tile
+// decoder: the main pass (the layout without them), then one pass per version
+// rank (its members as OPTIONs / OPTGROUPs) from where the previous pass
+// ended. Control words at ws + ctl_off (past every pass's workspace); when a
+// pass is not clean (an error, or the data length ending it part-way),
+// CompatCtl::serial is set and spk_nested.hip's one-lane walk, launched
+// behind it on that flag, decodes the message instead.
+struct CompatCtl {
+  unsigned long long chain[4];  // the next pass: start, records, width, data length
+  unsigned long long end;       // where the last pass that ran ended
+  uint32_t serial;              // 1: the one-lane walk decodes the message
+  uint32_t stop;                // first rank whose pass starts at or past the data length
+  spk_dresult_t pres;           // a version pass's result
+};
+bool compat_tiles_ok(const spk_layout *L, uint64_t wire_len);
+size_t compat_tiles_ws_bytes(const spk_layout *L, uint64_t wire_len);
+hipError_t launch_compat_tiles(const spk_layout *L, const void *d_wire, uint64_t wire_len,
+                               void *d_recs, uint64_t rec_cap, void *const *d_heaps,
+                               const uint64_t *heap_caps, spk_dresult_t *d_res, void *d_ws,
+                               size_t ctl_off, hipStream_t s);
 // spk_nested.hip: layouts with SPK_OP_ARRAY
 bool layout_nested(const spk_layout *L);
 size_t nested_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len);

@@ -924,8 +924,11 @@ struct NTok {
 };
 static_assert(kWsPlanTok + sizeof(NTok) <= kWsCtl, "NTok overlaps the control block");
 
+// cond (device, non-null): the kernel runs only while *cond is non-zero (the
+// encode: NTok::stale; a compatible-member VECTOR decode: CompatCtl::serial)
 __device__ __forceinline__ bool tok_skip(const uint8_t *ws, const uint32_t *cond) {
-  return cond && !reinterpret_cast<const NTok *>(ws + kWsPlanTok)->stale;
+  (void)ws;
+  return cond && !*cond;
 }
 
 __global__ __launch_bounds__(kNScanT) void nscan_reduce(const uint64_t *__restrict__ col,
@@ -1141,9 +1144,20 @@ static CWs cws_layout(uint64_t wire_len, uint32_t n_heaps) {
 }
 
 
+// a compatible-member VECTOR decode on the tile passes: its CompatCtl, past
+// the workspace of every pass and of the one-lane walk behind them
+static size_t compat_ctl_off(const spk_layout *L, uint64_t rows, uint64_t wire_len) {
+  const NLayout N = make_nlayout(L);
+  const size_t b = nws_layout(rows, N.n_heaps, N.n_ranks).end;
+  const size_t t = compat_tiles_ws_bytes(L, wire_len);
+  return ((b > t ? b : t) + 255) & ~size_t(255);
+}
+
 size_t nested_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len) {
   const NLayout N = make_nlayout(L);
   size_t b = nws_layout(n, N.n_heaps, N.n_ranks).end;
+  if (mode == SPK_MODE_VECTOR && N.n_ranks && compat_tiles_ok(L, wire_len))
+    b = compat_ctl_off(L, n, wire_len) + sizeof(CompatCtl);
   if (mode == SPK_MODE_VECTOR && !N.n_ranks) {
     const size_t c = cws_layout(wire_len, N.n_heaps).end;
     if (c > b) b = c;
@@ -1749,12 +1763,17 @@ struct NDec {
   uint8_t *heaps[SPK_MAX_SPANS];
   uint64_t heap_cap[SPK_MAX_SPANS];
   const uint64_t *ends;  // MESSAGES: message i ends at ends[i] (null: offs[i + 1])
+  // compatible-member VECTOR decode behind the tile passes: the one-lane walk's
+  // kernels run only while *serial is non-zero (CompatCtl); null: always
+  const uint32_t *serial;
 };
+__device__ __forceinline__ bool n_skip(const NDec &a) { return a.serial && !*a.serial; }
 
 // VECTOR header (deserialize_metainfo, unpacker.hpp:548-619, + the count) or
 // the body of spk_decode_body; initialises the control block and *res
 __global__ void nest_vhdr(NDec a, const uint8_t *__restrict__ wire, uint8_t *ws,
                           spk_dresult_t *res) {
+  if (n_skip(a)) return;
   NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
   const uint64_t len = a.wire_len;
   uint64_t pos = 0, n = 0, dl = 0;
@@ -2067,6 +2086,14 @@ __global__ void nest_cfinish(NDec a, const uint64_t *__restrict__ part, uint64_t
   *res = r;
 }
 
+// p[0, n) = v while *cond (null: always)
+__global__ void nest_fill_u64(uint64_t *p, uint64_t n, uint64_t v, const uint32_t *cond) {
+  if (cond && !*cond) return;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
 // VECTOR layouts with compatible members: the version passes trail every
 // record's main pass, so one lane walks the message (main pass, then the
 // version passes, unpacker.hpp:292-366,1354-1376) and records each record's
@@ -2075,7 +2102,7 @@ __global__ void nest_vec_serial(NDec a, const uint8_t *__restrict__ wire, uint8_
                                 uint64_t *__restrict__ U, uint64_t *__restrict__ starts,
                                 uint64_t *__restrict__ cpos) {
   NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
-  if (threadIdx.x || ctl->errc) return;
+  if (threadIdx.x || n_skip(a) || ctl->errc) return;
   const NLayout &N = a.N;
   const uint64_t n = ctl->nrec, len = a.wire_len, data_end = ctl->data_len;
   const uint32_t w = ctl->w;
@@ -2217,6 +2244,7 @@ __global__ __launch_bounds__(256) void nest_emit(NDec a, const uint8_t *__restri
                                                  uint8_t *__restrict__ recs, int mode,
                                                  int32_t *__restrict__ errc_out) {
   __shared__ v4u_t win_s[4][kMsgWin / 16];
+  if (n_skip(a)) return;  // (uniform)
   NCtl *ctl = reinterpret_cast<NCtl *>(ws + kWsCtl);
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const NLayout &N = a.N;
@@ -2283,7 +2311,7 @@ __global__ void nest_finish(NDec a, const uint64_t *__restrict__ part, uint64_t 
   // (MESSAGES: nest_emit copied the per-message errc out and tallied them)
   (void)ec;
   (void)errc_out;
-  if (threadIdx.x) return;
+  if (threadIdx.x || n_skip(a)) return;
   const unsigned long long s_ok = ctl->m_ok, s_cap = ctl->m_cap;
   spk_dresult_t r = *res;
   const uint32_t nh = a.N.n_heaps;
@@ -2390,15 +2418,28 @@ hipError_t launch_nested_decode(const spk_layout *L, int mode, const void *d_wir
   uint64_t *starts = reinterpret_cast<uint64_t *>(ws + f.starts);
   int32_t *ec = reinterpret_cast<int32_t *>(ws + f.starts);  // MESSAGES: errc per message
   const uint64_t nb = (rows + kNScanBlk - 1) / kNScanBlk;
-  if ((er = hipMemsetAsync(d_res, 0, sizeof(spk_dresult_t), s)) != hipSuccess) return er;
-  if (mode == SPK_MODE_VECTOR) {  // compatible members: one lane walks the message
-    if (rows && (er = hipMemsetAsync(U, 0, rows * 8 * a.N.n_heaps, s)) != hipSuccess) return er;
-    if (rows && (er = hipMemsetAsync(cpos, 0xFF, rows * 8 * a.N.n_ranks, s)) != hipSuccess)
+  if (mode == SPK_MODE_VECTOR && !body_w && compat_tiles_ok(L, wire_len)) {
+    // compatible members on the tile decoder, pass by pass; the one-lane walk
+    // below runs only when a pass was not clean (CompatCtl::serial)
+    const size_t co = compat_ctl_off(L, rows, wire_len);
+    if ((er = launch_compat_tiles(L, d_wire, wire_len, d_recs, rec_cap, d_heaps, heap_caps, d_res,
+                                  d_ws, co, s)) != hipSuccess)
       return er;
+    a.serial = &reinterpret_cast<CompatCtl *>(ws + co)->serial;
+  } else if ((er = hipMemsetAsync(d_res, 0, sizeof(spk_dresult_t), s)) != hipSuccess) {
+    return er;
+  }
+  if (mode == SPK_MODE_VECTOR) {  // compatible members: one lane walks the message
+    if (rows) {
+      const unsigned g = nblocks(rows, 256) < 4096 ? nblocks(rows, 256) : 4096;
+      SPK_LAUNCH(nest_fill_u64, dim3(g), dim3(256), 0, s, U, rows * a.N.n_heaps, 0ull, a.serial);
+      SPK_LAUNCH(nest_fill_u64, dim3(g), dim3(256), 0, s, cpos, rows * a.N.n_ranks, ~0ull,
+                 a.serial);
+    }
     SPK_LAUNCH(nest_vhdr, dim3(1), dim3(1), 0, s, a, (const uint8_t *)d_wire, ws, d_res);
     SPK_LAUNCH(nest_vec_serial, dim3(1), dim3(64), 0, s, a, (const uint8_t *)d_wire, ws, U,
                starts, cpos);
-    if ((er = nscan(U, rows, a.N.n_heaps, part, s)) != hipSuccess) return er;
+    if ((er = nscan(U, rows, a.N.n_heaps, part, s, ws, a.serial)) != hipSuccess) return er;
     if (rows)
       SPK_LAUNCH((nest_emit<SPK_MAX_DEPTH, false>), dim3(nblocks(rows, 256)), dim3(256), 0, s, a,
                  (const uint8_t *)d_wire, d_msg_offsets, (const uint64_t *)starts,

@@ -146,6 +146,14 @@ typedef uint32_t u32_unaligned __attribute__((aligned(1)));
 typedef uint64_t u64_unaligned __attribute__((aligned(1)));
 typedef uint32_t v4u_t __attribute__((ext_vector_type(4)));
 typedef v4u_t v4u_una __attribute__((aligned(1)));
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+// byte-aligned LDS words: gfx950 reads (and writes) them with one ds_read_b32 / b64 / b128
+// (unaligned DS access), not with 2-5 aligned dword reads + alignbyte
+typedef __attribute__((address_space(3))) uint16_t lds_u16_una __attribute__((aligned(1)));
+typedef __attribute__((address_space(3))) uint32_t lds_u32_una __attribute__((aligned(1)));
+typedef __attribute__((address_space(3))) uint64_t lds_u64_una __attribute__((aligned(1)));
+typedef __attribute__((address_space(3))) v4u_t lds_v4u_una __attribute__((aligned(1)));
 
 // unaligned byte copy in 16/8/4/1-byte pieces (gfx950 runs in unaligned mode)
 __device__ __forceinline__ void copy_bytes(uint8_t *d, const uint8_t *s, uint64_t n) {
@@ -544,7 +552,10 @@ __device__ __forceinline__ void lds_put_u32(uint8_t *d, uint32_t v, uint32_t n) 
 }
 
 // bytes [pos, pos+n) of the output come from src[0, n): store the part that
-// falls in the window
+// falls in the window. LDS: W.lds is the LDS window, written with byte-aligned
+// 4 / 8 / 16-B DS stores (round 4: one ds_write_b8 per byte); otherwise it is
+// global memory (the direct mode), written bytewise.
+template <bool LDS = false>
 __device__ __forceinline__ void win_put(const Win &W, uint64_t pos, const uint8_t *src,
                                         uint64_t n) {
   const uint64_t a = pos > W.lo ? pos : W.lo;
@@ -553,6 +564,20 @@ __device__ __forceinline__ void win_put(const Win &W, uint64_t pos, const uint8_
   uint64_t i = a - pos;
   const uint64_t e = b - pos;
   uint8_t *d = W.lds + (pos - W.lo);
+  if constexpr (LDS) {
+    for (; i + 16 <= e; i += 16)
+      *(lds_v4u_una *)(d + i) = *reinterpret_cast<const v4u_una *>(src + i);
+    if (e - i >= 8) {
+      *(lds_u64_una *)(d + i) = *reinterpret_cast<const u64_unaligned *>(src + i);
+      i += 8;
+    }
+    if (e - i >= 4) {
+      *(lds_u32_una *)(d + i) = *reinterpret_cast<const u32_unaligned *>(src + i);
+      i += 4;
+    }
+    for (; i < e; ++i) d[i] = src[i];
+    return;
+  }
   for (; i + 16 <= e; i += 16) {
     const v4u_t v = *reinterpret_cast<const v4u_una *>(src + i);
     lds_put_u32(d + i, v.x, 4);
@@ -583,13 +608,14 @@ __device__ __forceinline__ void win_put_le(const Win &W, uint64_t pos, uint64_t 
 
 // one record at output position pos (width w) into the window; span payloads
 // whose bit is set in `skip` are copied cooperatively by the block instead
+template <bool LDS = false>
 __device__ __forceinline__ void win_record(const VarArgs &a, const uint8_t *rec, uint32_t w,
                                            uint64_t pos, const Win &W, uint32_t skip = 0) {
   uint32_t sk = 0;
   for (uint32_t o = 0; o < a.L.n_ops; ++o) {
     const spk_op op = a.L.ops[o];
     if (op.kind == SPK_OP_COPY) {
-      win_put(W, pos, rec + op.rec_off, op.size);
+      win_put<LDS>(W, pos, rec + op.rec_off, op.size);
       pos += op.size;
     } else if (op.kind == SPK_OP_VARINT) {  // serialize_varint (varint.hpp:245-268)
       uint64_t v = vi_value(op, rec);
@@ -606,7 +632,7 @@ __device__ __forceinline__ void win_record(const VarArgs &a, const uint8_t *rec,
       win_put_le(W, pos, c, pw);
       pos += pw;
       const uint64_t nb = c * op.size;
-      if (nb && !(skip >> sk & 1)) win_put(W, pos, a.heaps[sk] + rec_u64(rec, op.aux) * op.size, nb);
+      if (nb && !(skip >> sk & 1)) win_put<LDS>(W, pos, a.heaps[sk] + rec_u64(rec, op.aux) * op.size, nb);
       pos += nb;
       ++sk;
     }
@@ -888,10 +914,10 @@ __global__ __launch_bounds__(kThreads, 5) void var_encode_write(
         }
         const uint32_t sl = wlog(wj[j]);
         const uint32_t hl = ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + sl];
-        win_put(W, q, ws + kWsHdrMsg + sl * kWsHdrSlot, hl);
+        win_put<true>(W, q, ws + kWsHdrMsg + sl * kWsHdrSlot, hl);
         q += hl;
       }
-      win_record(a, recs + i * a.L.stride, wj[j], q, W, skip[j]);
+      win_record<true>(a, recs + i * a.L.stride, wj[j], q, W, skip[j]);
     }
     // listed payloads are in output order: fill the window slots they cover
     while (k0 < nbig_tot && big[k0].dst + big[k0].n <= W.lo) ++k0;
@@ -1023,6 +1049,9 @@ struct DecArgs {
   const uint64_t *ends;  // MESSAGES: message i ends at ends[i] (null: offs[i + 1])
   const uint64_t *dn;    // MESSAGES: device count (min(*dn, n_msgs)) or null
   const void *nl;        // nested: the NTLayout in device memory (workspace)
+  // VECTOR pass of a compatible-member layout (launch_compat_tiles): device
+  // words {start, n, w, data_len} in place of the header, or null
+  const uint64_t *chain;
 };
 
 
@@ -1281,6 +1310,9 @@ struct FCtl {
   unsigned long long chain_ready;   // the chain's first tile + 1 (0: not yet found)
   unsigned long long chain_done;    // chain blocks out (the last one sums the tile scan)
   unsigned long long copy_done;     // vec_big_copy blocks done (the last one writes the result)
+  // the first tile left unresolved: harmless when it starts at or past the
+  // end of record n-1 (bytes after the message, which need not parse)
+  unsigned long long unres_tile;
 };
 constexpr size_t kWsFCtl = kWsCtl + 1280;
 static_assert(sizeof(VCtl) <= kWsFCtl - kWsCtl, "VCtl overlaps FCtl");
@@ -1482,9 +1514,15 @@ __device__ void vec_hdr_body(const DecArgs &a, const uint8_t *__restrict__ wire,
   VCtl *c = reinterpret_cast<VCtl *>(ws + kWsCtl);
   uint64_t pos = 0, dl = 0;
   uint32_t w = a.body_w;
-  int32_t e = a.body_w ? SPK_ERRC_OK : parse_hdr(a.fmt, wire, a.wire_len, &pos, &w, &dl);
+  int32_t e = a.body_w || a.chain ? SPK_ERRC_OK : parse_hdr(a.fmt, wire, a.wire_len, &pos, &w, &dl);
   uint64_t n = 0;
-  if (a.body_w) {
+  if (a.chain) {  // a version pass: its records start where the previous pass ended
+    pos = a.chain[0];
+    n = a.chain[1];
+    w = (uint32_t)a.chain[2];
+    dl = a.chain[3];
+    if (n && pos >= a.wire_len) e = SPK_ERRC_NO_BUFFER_SPACE;
+  } else if (a.body_w) {
     n = a.body_n;
   } else if (!e) {
     if (a.wire_len < pos + w)
@@ -1529,6 +1567,7 @@ __device__ void vec_hdr_body(const DecArgs &a, const uint8_t *__restrict__ wire,
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);  // tile decoder state
   for (int k = 0; k < 4; ++k) fc->broken[k] = fc->nlist[k] = 0;
   fc->unresolved = 0;
+  fc->unres_tile = ~0ull;
   for (int k = 0; k < 8; ++k) fc->diag[k] = 0;
   fc->seq = 0;
   fc->chain_ticket = 0;
@@ -1577,14 +1616,6 @@ struct VecBufs {
   uint64_t *scan;   // block sums for the device-wide scans
 };
 
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-typedef __attribute__((address_space(3))) uint8_t lds_u8;
-// byte-aligned LDS words: gfx950 reads them with one ds_read_b32 / b64 / b128
-// (unaligned DS access), not with 2-5 aligned dword reads + alignbyte
-typedef __attribute__((address_space(3))) uint16_t lds_u16_una __attribute__((aligned(1)));
-typedef __attribute__((address_space(3))) uint32_t lds_u32_una __attribute__((aligned(1)));
-typedef __attribute__((address_space(3))) uint64_t lds_u64_una __attribute__((aligned(1)));
-typedef __attribute__((address_space(3))) v4u_t lds_v4u_una __attribute__((aligned(1)));
 
 // LDS window layout: window-relative byte o is dword o >> 2, byte o. (Rows
 // padded to 69 dwords, so that the candidate screen's same-offset reads of a
@@ -3477,7 +3508,8 @@ __device__ __forceinline__ void tile_contrib(const TileBufs &TB, FCtl *fc, uint6
   } else if (sel == kSelTerm) {
     atomicMin(&fc->term_tile, (unsigned long long)t);
   } else {
-    atomicAdd(&fc->unresolved, 1ull);  // never expected after the fix passes
+    atomicAdd(&fc->unresolved, 1ull);  // (only past the message's end: bytes after it)
+    atomicMin(&fc->unres_tile, (unsigned long long)t);
   }
   TB.contrib[t] = cnt;
   QFORV(q) TB.contrib[(uint64_t)(1 + q) * TB.ntiles + t] = s[q];
@@ -3641,6 +3673,7 @@ __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
       if (i >= kChainSpin) {  // (never expected: a decode error, not a hang)
         r = nt + 1;
         atomicAdd(&fc->unresolved, 1ull);
+        atomicMin(&fc->unres_tile, 0ull);
         break;
       }
       __builtin_amdgcn_s_sleep(4);
@@ -3735,6 +3768,7 @@ __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
             if (!ev && i >= kChainSpin) {  // (never expected: a decode error, not a hang)
               ev = kEntTerm;
               atomicAdd(&fc->unresolved, 1ull);
+              atomicMin(&fc->unres_tile, (unsigned long long)u);
             }
           }
         }
@@ -3793,12 +3827,14 @@ __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
         }
         // ---- hand-off: the landing tile's entry first, then the tiles between ----
         auto publish = [&](uint64_t Y) {
-          if (Y == kTermPos) {
+          // (kNoPos: no exit from this entry -- only in bytes past the
+          // message, which need not parse: the path ends here, so that no
+          // later tile waits for an entry)
+          if (Y == kTermPos || Y == kNoPos) {
             for (uint64_t v = u + 1 + lane; v < nt; v += 64)
               __hip_atomic_store(&ent[v], kEntTerm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return;
           }
-          if (Y == kNoPos) return;
           uint64_t l0 = Y >= p0 ? (Y - p0) / kTileBytes : 0;
           if (l0 <= u) {
             if (Y < len) return;  // (no exit: never)
@@ -4248,12 +4284,17 @@ __device__ void tile_finish(const DecArgs &a, const uint8_t *__restrict__ wire,
   for (int k = 0; k < 4; ++k) rep += fc->broken[k];
   r.tiles_repaired = (uint32_t)(rep < 0xFFFFFFFFull ? rep : 0xFFFFFFFFull);
   r.tiles_sequential = (uint32_t)(fc->seq < 0xFFFFFFFFull ? fc->seq : 0xFFFFFFFFull);
-  if (fc->unresolved) {
+  const uint64_t total = c->n ? (uint64_t)fc->total : 0;
+  // an unresolved tile is an internal error unless it starts at or past the
+  // end of record n-1: the bytes after a message need not parse as records
+  // (the reference stops at its count, struct_pack.hpp:343-357)
+  if (fc->unresolved &&
+      (fc->range || !c->n || total < c->n ||
+       c->p0 + fc->unres_tile * (uint64_t)kTileBytes < (uint64_t)fc->end_pos)) {
     r.errc = SPK_ERRC_INTERNAL;
     *res = r;
     return;
   }
-  const uint64_t total = c->n ? (uint64_t)fc->total : 0;
   if (fc->range && !fc->last) {  // a middle shard: its records, up to the message's count
     const uint64_t k = total < c->n ? total : c->n;
     r.count = k;
@@ -4620,6 +4661,261 @@ hipError_t launch_var_nested_decode(const spk_layout *L, const void *d_wire, uin
   const uint8_t *wire = (const uint8_t *)d_wire;
   if (simple) return launch_vec_tiles_ns<-3>(a, P, L, wire, ws, d_res, (uint8_t *)d_recs, s);
   return launch_vec_tiles_ns<-2>(a, P, L, wire, ws, d_res, (uint8_t *)d_recs, s);
+}
+
+// ---- compatible members, VECTOR mode, on the tile decoder --------------------------
+// unpacker.hpp:292-366,1354-1376: the main pass reads every record without its
+// compatible members; then, per version rank in ascending order, a pass reads
+// [has:1][U if has] of that rank's members of every record (packer.hpp:66-78,
+// 453-461 writes them so). Each pass is a record stream of its own: a derived
+// layout (the main one without the members; a rank's of its members, COMPAT
+// as OPTION and CGROUP as OPTGROUP, which read alike: a value that does not
+// fit reads as present and zero, a group's errc is dropped with the rest of
+// the group zeroed) runs the whole tile pipeline, its start and record count
+// chained on the device from the previous pass (DecArgs::chain). The
+// reference's data-length rule (a has byte at or past the header's length
+// ends every pass, no error) is taken exactly in the clean cases: a pass that
+// starts at or past the length is skipped and its members read as absent (an
+// older writer), and a pass that ends at or before it never met it. Anything
+// else -- an error, a capacity overflow, a pass running past the length --
+// sets CompatCtl::serial, and the one-lane walk that spk_nested.hip enqueues
+// behind it on that flag decodes the whole message instead.
+struct CompatSplit {
+  spk_layout L;
+  uint32_t nh;
+  uint8_t hmap[SPK_MAX_SPANS];  // the derived layout's heap j -> the layout's heap
+};
+// rank < 0: the main pass's layout; else the version pass of that rank
+static CompatSplit compat_split(const spk_layout *L, const NLayout &N, int rank) {
+  CompatSplit c = {};
+  c.L = *L;
+  c.L.n_ops = 0;
+  auto push = [&](spk_op op, uint32_t i) {
+    c.L.ops[c.L.n_ops++] = op;
+    if (op_has_heap(op.kind)) c.hmap[c.nh++] = N.heap[i];
+  };
+  for (uint32_t i = 0; i < L->n_ops;) {
+    const spk_op op = L->ops[i];
+    const uint32_t k = SPK_OP_KIND(op.kind);
+    if (k != SPK_OP_COMPAT && k != SPK_OP_CGROUP) {
+      if (rank < 0) push(op, i);
+      ++i;
+      continue;
+    }
+    const uint32_t last = k == SPK_OP_CGROUP ? N.end[i] : i;  // a CGROUP: through its END
+    if (rank >= 0 && N.crank[i] == (uint32_t)rank) {
+      spk_op o = op;
+      if (k == SPK_OP_COMPAT) {
+        o.kind = SPK_OP_OPTION;
+      } else {
+        o.kind = SPK_OP_OPTGROUP;
+        o.size = 1;
+        o.aux = 0;
+      }
+      push(o, i);
+      for (uint32_t j = i + 1; j <= last; ++j) push(L->ops[j], j);
+    }
+    i = last + 1;
+  }
+  return c;
+}
+
+// a derived layout the tile pipeline takes
+static bool tiles_layout_ok(const spk_layout *L) {
+  uint32_t h = 0, v = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i) {
+    const uint32_t k = SPK_OP_KIND(L->ops[i].kind);
+    h += op_has_heap(k);
+    v += k == SPK_OP_VARINT || k == SPK_OP_FVAR || k == SPK_OP_VARIANT || k == SPK_OP_OPTGROUP;
+  }
+  if (!h && !v) return false;  // (fixed-size records: never a non-trivial layout's pass)
+  return layout_nested(L) ? var_nested_tile_ok(L) : true;
+}
+static size_t tiles_ws_bytes(const spk_layout *L, uint64_t wire_len) {
+  if (layout_nested(L)) return var_nested_tile_ws_bytes(L, wire_len);
+  uint32_t ns = 0;
+  for (uint32_t i = 0; i < L->n_ops; ++i)
+    ns += L->ops[i].kind == SPK_OP_SPAN || L->ops[i].kind == SPK_OP_OPTION;
+  return tile_ws_layout(ns, wire_len).end + 256;
+}
+// one VECTOR pass of a derived layout on the tile pipeline
+static hipError_t tiles_decode(const spk_layout *L, const void *d_wire, uint64_t wire_len,
+                               void *d_recs, uint64_t rec_cap, void *const *d_heaps,
+                               const uint64_t *heap_caps, spk_dresult_t *d_res, uint8_t *ws,
+                               hipStream_t s, const uint64_t *chain) {
+  DecArgs a = {};
+  WalkProg P;
+  const uint8_t *wire = (const uint8_t *)d_wire;
+  uint8_t *r = (uint8_t *)d_recs;
+  if (layout_nested(L)) {
+    const bool simple = nested_args(L, wire_len, rec_cap, d_heaps, heap_caps, ws, s, a, P);
+    a.chain = chain;
+    if (simple) return launch_vec_tiles_ns<-3>(a, P, L, wire, ws, d_res, r, s);
+    return launch_vec_tiles_ns<-2>(a, P, L, wire, ws, d_res, r, s);
+  }
+  a.L = make_klayout(L);
+  a.fmt = L->fmt_vector;
+  a.wire_len = wire_len;
+  a.rec_cap = rec_cap;
+  for (uint32_t k = 0; k < a.L.n_spans; ++k) {
+    a.heaps[k] = (uint8_t *)d_heaps[k];
+    a.heap_cap[k] = heap_caps[k];
+  }
+  a.chain = chain;
+  P = make_walkprog(L);
+  if (P.nv) return launch_vec_tiles_ns<-1>(a, P, L, wire, ws, d_res, r, s);
+  if (P.ns == 1) return launch_vec_tiles_ns<1>(a, P, L, wire, ws, d_res, r, s);
+  if (P.ns == 2) return launch_vec_tiles_ns<2>(a, P, L, wire, ws, d_res, r, s);
+  return launch_vec_tiles_ns<0>(a, P, L, wire, ws, d_res, r, s);
+}
+
+bool compat_tiles_ok(const spk_layout *L, uint64_t wire_len) {
+  const NLayout N = make_nlayout(L);
+  if (!N.n_ranks || wire_len >= (1ull << 32) - 4096) return false;
+  for (int rk = -1; rk < (int)N.n_ranks; ++rk) {
+    const CompatSplit c = compat_split(L, N, rk);
+    if (!tiles_layout_ok(&c.L)) return false;
+  }
+  return true;
+}
+size_t compat_tiles_ws_bytes(const spk_layout *L, uint64_t wire_len) {
+  const NLayout N = make_nlayout(L);
+  size_t b = 0;
+  for (int rk = -1; rk < (int)N.n_ranks; ++rk) {
+    const CompatSplit c = compat_split(L, N, rk);
+    const size_t t = tiles_ws_bytes(&c.L, wire_len);
+    b = t > b ? t : b;
+  }
+  return b;
+}
+
+struct HeapMap {
+  uint32_t nh;
+  uint8_t h[SPK_MAX_SPANS];
+};
+// after a pass (rank -1: the main one): is it clean, where does the next start
+__global__ void compat_link(const uint8_t *ws, CompatCtl *cc, spk_dresult_t *res, HeapMap hm,
+                            int rank, uint32_t n_ranks) {
+  if (threadIdx.x) return;
+  const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
+  const FCtl *fc = reinterpret_cast<const FCtl *>(ws + kWsFCtl);
+  const uint64_t end = c->n ? (uint64_t)fc->end_pos : c->p0;
+  if (rank < 0) {
+    cc->serial = 0;
+    cc->stop = n_ranks;
+    spk_dresult_t r = *res;
+    if (r.errc || c->errc) {
+      cc->serial = 1;
+      cc->chain[1] = 0;
+      return;
+    }
+    uint64_t hu[SPK_MAX_SPANS] = {};
+    for (uint32_t j = 0; j < hm.nh; ++j) hu[hm.h[j]] = r.heap_used[j];
+    for (uint32_t k = 0; k < SPK_MAX_SPANS; ++k) r.heap_used[k] = hu[k];
+    *res = r;
+    cc->end = end;
+    cc->chain[0] = end;
+    cc->chain[1] = c->n;
+    cc->chain[2] = c->w;
+    cc->chain[3] = c->data_len;
+    if (end >= c->data_len) {  // no version pass was written (or none fits): all absent
+      cc->stop = 0;
+      cc->chain[1] = 0;
+    }
+    return;
+  }
+  if (cc->serial || cc->stop <= (uint32_t)rank) return;  // (the pass read no record)
+  const spk_dresult_t p = cc->pres;
+  if (p.errc || c->errc || end > cc->chain[3]) {
+    cc->serial = 1;
+    cc->chain[1] = 0;
+    return;
+  }
+  for (uint32_t j = 0; j < hm.nh; ++j) res->heap_used[hm.h[j]] = p.heap_used[j];
+  cc->end = end;
+  cc->chain[0] = end;
+  if (end >= cc->chain[3]) {  // the next pass's first has byte is at or past the length
+    cc->stop = (uint32_t)rank + 1;
+    cc->chain[1] = 0;
+  }
+}
+
+// the compatible members of the ranks from CompatCtl::stop on read as absent
+// (no pass wrote them): count 0 at element offset 0 (the heap holds none of
+// them), a CGROUP's has_value 0 -- what the one-lane walk leaves
+struct CompatOps {
+  uint32_t n, n_ranks, stride, pad_;
+  uint32_t rec_off[SPK_MAX_OPS], aux[SPK_MAX_OPS];
+  uint8_t group[SPK_MAX_OPS], rank[SPK_MAX_OPS];
+};
+__global__ void compat_absent(CompatOps co, const CompatCtl *cc, const spk_dresult_t *res,
+                              uint8_t *recs, uint64_t rec_cap) {
+  if (cc->serial || cc->stop >= co.n_ranks) return;
+  const uint32_t stop = cc->stop;
+  const uint64_t n = res->count < rec_cap ? res->count : rec_cap;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    uint8_t *r = recs + i * co.stride;
+    for (uint32_t q = 0; q < co.n; ++q) {
+      if (co.rank[q] < stop) continue;
+      *reinterpret_cast<uint32_t *>(r + co.rec_off[q]) = 0;
+      if (!co.group[q]) *reinterpret_cast<uint64_t *>(r + co.aux[q]) = 0;
+    }
+  }
+}
+
+// the message's result when every pass was clean
+__global__ void compat_done(const CompatCtl *cc, spk_dresult_t *res) {
+  if (threadIdx.x || cc->serial) return;
+  const uint64_t dl = cc->chain[3];
+  res->consumed = cc->end > dl ? cc->end : dl;
+}
+
+hipError_t launch_compat_tiles(const spk_layout *L, const void *d_wire, uint64_t wire_len,
+                               void *d_recs, uint64_t rec_cap, void *const *d_heaps,
+                               const uint64_t *heap_caps, spk_dresult_t *d_res, void *d_ws,
+                               size_t ctl_off, hipStream_t s) {
+  const NLayout N = make_nlayout(L);
+  uint8_t *ws = (uint8_t *)d_ws;
+  CompatCtl *cc = reinterpret_cast<CompatCtl *>(ws + ctl_off);
+  hipError_t er;
+  for (int rk = -1; rk < (int)N.n_ranks; ++rk) {
+    const CompatSplit c = compat_split(L, N, rk);
+    void *hp[SPK_MAX_SPANS];
+    uint64_t hc[SPK_MAX_SPANS];
+    HeapMap hm = {};
+    hm.nh = c.nh;
+    for (uint32_t j = 0; j < c.nh; ++j) {
+      hp[j] = d_heaps[c.hmap[j]];
+      hc[j] = heap_caps[c.hmap[j]];
+      hm.h[j] = c.hmap[j];
+    }
+    // the main pass writes the message's result; a version pass its own
+    if ((er = tiles_decode(&c.L, d_wire, wire_len, d_recs, rec_cap, hp, hc,
+                           rk < 0 ? d_res : &cc->pres, ws, s,
+                           rk < 0 ? nullptr : reinterpret_cast<const uint64_t *>(cc->chain))) !=
+        hipSuccess)
+      return er;
+    SPK_LAUNCH(compat_link, dim3(1), dim3(64), 0, s, (const uint8_t *)ws, cc, d_res, hm, rk,
+               N.n_ranks);
+  }
+  CompatOps co = {};
+  co.n_ranks = N.n_ranks;
+  co.stride = L->rec_stride;
+  for (uint32_t i = 0; i < N.n_ops; ++i) {
+    const uint32_t k = N.ops[i].kind;
+    if (k != SPK_OP_COMPAT && k != SPK_OP_CGROUP) continue;
+    co.rec_off[co.n] = N.ops[i].rec_off;
+    co.aux[co.n] = N.ops[i].aux;
+    co.group[co.n] = k == SPK_OP_CGROUP;
+    co.rank[co.n++] = N.crank[i];
+  }
+  if (rec_cap)
+    SPK_LAUNCH(compat_absent, dim3(grid_for(rec_cap, 256) < 4096 ? grid_for(rec_cap, 256) : 4096),
+               dim3(256), 0, s, co, (const CompatCtl *)cc, (const spk_dresult_t *)d_res,
+               (uint8_t *)d_recs, rec_cap);
+  SPK_LAUNCH(compat_done, dim3(1), dim3(64), 0, s, (const CompatCtl *)cc, d_res);
+  return hipGetLastError();
 }
 
 size_t var_workspace_bytes(const spk_layout *L, int mode, uint64_t n, uint64_t wire_len) {
