@@ -64,10 +64,14 @@ CONFIGS = {
            "the reference benchmark's Monster (src/struct_pack/benchmark/data_def.hpp: Vec3, "
            "2 x int16, 2 strings, enum, vector<Weapon{string,int16}>, Weapon, vector<Vec3>): "
            "10M per GPU, one vector message"),
+    "cmpg": ("cmpg", 2_000_000, 16, "A",
+             "compatible members: 2M CmpG{int32, compatible<string, v1>, string, "
+             "compatible<vector<int32>, v1>, compatible<Inner, v2>, compatible<ResponseCode, v2>} "
+             "per GPU, one vector message (a main pass and two version passes)"),
 }
-EXTRA = ["c2b", "c3", "c3r", "c3l", "c4", "c5", "cv", "cm", "cvm"]  # timed beside the C2 headline at N=1
+EXTRA = ["c2b", "c3", "c3r", "c3l", "c4", "c5", "cv", "cm", "cvm", "cmpg"]  # timed beside the C2 headline at N=1
 SEEDS = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004, "var": 0x5EED000C,
-         "monster": 0x5EED001E, "valreq": 0x5EED001B}
+         "monster": 0x5EED001E, "valreq": 0x5EED001B, "cmpg": 0x5EED0021}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PROFILE_ROUND = "r05"
 

@@ -2126,6 +2126,11 @@ __device__ int32_t nt_read(const NTLayout &N, const Rd &rd, uint64_t &pos, uint6
         a = (int)b;
         if constexpr (EMIT) *reinterpret_cast<uint32_t *>(r + op.rec_off) = b;
       } else {
+        // (a bounded walk -- speculative, or the chain's map -- gives up on a
+        // has_value byte other than the 0 / 1 every writer stores: a false
+        // start inside string bytes dies at once; the exact walk that
+        // replaces a given-up one reads any non-zero byte as present)
+        if (bounded && b > 1) return kNTLimit;
         a = b ? 0 : (op.size == 2 ? 1 : -1);
         if constexpr (EMIT) *reinterpret_cast<uint32_t *>(r + op.rec_off) = b ? 1u : 0u;
       }
@@ -2151,6 +2156,7 @@ __device__ int32_t nt_read(const NTLayout &N, const Rd &rd, uint64_t &pos, uint6
       ec = SPK_ERRC_NO_BUFFER_SPACE;
       continue;
     }
+    if (bounded && kind == SPK_OP_OPTION && rd.byte(pos) > 1) return kNTLimit;  // (as above)
     uint64_t cnt = kind == SPK_OP_OPTION ? (uint64_t)(rd.byte(pos) != 0) : rd(pos);
     pos += pw;
     uint64_t off = 0;
@@ -2278,6 +2284,7 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
     const bool opt = op == WP_OPT;
     const uint32_t cw = opt ? 1u : w;
     if (lim - p < cw) return bad;
+    if (bounded && opt && rd.byte(p) > 1) return bad;  // (nt_read: a has_value byte above 1)
     const uint64_t c = rd.count_at32(p, wmask, opt);
     p += cw;
     atomicAdd(U + 64 * h, (uint32_t)c);
