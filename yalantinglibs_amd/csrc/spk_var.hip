@@ -1310,6 +1310,9 @@ struct FCtl {
   unsigned long long chain_ready;   // the chain's first tile + 1 (0: not yet found)
   unsigned long long chain_done;    // chain blocks out (the last one sums the tile scan)
   unsigned long long copy_done;     // vec_big_copy blocks done (the last one writes the result)
+  // records of the tiles the chain has finalised, plus those before its first
+  // tile (a running lower bound of the records before the chain's next tile)
+  unsigned long long chain_cnt;
   // the first tile left unresolved: harmless when it starts at or past the
   // end of record n-1 (bytes after the message, which need not parse)
   unsigned long long unres_tile;
@@ -1574,6 +1577,7 @@ __device__ void vec_hdr_body(const DecArgs &a, const uint8_t *__restrict__ wire,
   fc->chain_arrive = 0;
   fc->chain_ready = 0;
   fc->chain_done = 0;
+  fc->chain_cnt = 0;
   fc->copy_done = 0;
   fc->njobs = 0;
   fc->term_tile = ~0ull;
@@ -3503,8 +3507,8 @@ __global__ __launch_bounds__(64) void vec_tile_repair(DecArgs a, WalkProg P,
 // ---- K3: the selected contribution of tile t (vec_tile_chain, once the
 // tile's selection is final); the first tile whose path ends inside it (its
 // exit is kTermPos) ----------------------------------------------------------
-__device__ __forceinline__ void tile_contrib(const TileBufs &TB, FCtl *fc, uint64_t t,
-                                             uint32_t nsp, uint64_t *col = nullptr) {
+__device__ __forceinline__ uint64_t tile_contrib(const TileBufs &TB, FCtl *fc, uint64_t t,
+                                                 uint32_t nsp, uint64_t *col = nullptr) {
   const uint64_t *fn = TB.fn + t * kFnWords;
   const int32_t sel = TB.sel[t];
   uint64_t cnt = 0, s[kVS] = {};
@@ -3524,6 +3528,7 @@ __device__ __forceinline__ void tile_contrib(const TileBufs &TB, FCtl *fc, uint6
     col[0] += cnt;
     QFORV(q) col[1 + q] += s[q];
   }
+  return cnt;
 }
 
 // K3: tscan_apply blocks cover kTScanBlock consecutive tiles; their carries
@@ -3666,6 +3671,16 @@ __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
     m = block_min_u64<kChainWaves<NS>>(m, red_s);
     for (uint64_t t = m + tid; t < nt; t += kNT)
       __hip_atomic_store(&ent[t], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the records of the tiles before the chain (as the passes selected
+    // them): the chain's running count starts there
+    uint64_t pre = 0;
+    for (uint64_t t = tid; t < m && t < nt; t += kNT) {
+      bool bad;
+      const int32_t sel = tile_sel_now(TB, fc, t, &bad);
+      if (sel >= 0) pre += TB.fn[t * kFnWords + 2 + sel * kAltWords + 1];
+    }
+    for (int o = 32; o > 0; o >>= 1) pre += __shfl_down(pre, o);
+    if (lane == 0 && pre) atomicAdd(&fc->chain_cnt, (unsigned long long)pre);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0)
@@ -3707,6 +3722,23 @@ __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
     __syncthreads();
     const uint64_t u = tile_s;
     if (u >= nt) break;
+    // the tiles before this one already hold the message's n records: this
+    // and every later tile lie past its end (bytes after a message, e.g. a
+    // compatible-member message's version passes, need not be chained
+    // through; the count only lags, so a tile is never cut early)
+    if (!fc->range && c->n &&
+        __hip_atomic_load(&fc->chain_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= c->n) {
+      if (w0) {
+        if (lane == 0) {
+          TB.sel[u] = kSelTerm;
+          tile_contrib(TB, fc, u, nsp);
+        }
+        for (uint64_t v = u + 1 + lane; v < nt; v += 64)
+          __hip_atomic_store(&ent[v], kEntTerm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      continue;
+    }
     const uint64_t ts = p0 + u * kTileBytes;
     if (w0) stage_tile(win_s, wire, len, ts, w, lane);
     __syncthreads();
@@ -3785,7 +3817,8 @@ __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
       if (kind == kEntThru) {  // inside a record spanning the tile
         if (lane == 0) {
           tile_pass_through(TB, u, e, nsp);
-          tile_contrib(TB, fc, u, nsp);
+          const uint64_t k = tile_contrib(TB, fc, u, nsp);
+          if (k) atomicAdd(&fc->chain_cnt, (unsigned long long)k);
           atomicAdd(&fc->seq, 1ull);
         }
       } else if (kind == kEntTerm) {  // past the path's end
@@ -3865,7 +3898,9 @@ __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
           }
         }
         if (lane == 0) {
-          tile_contrib(TB, fc, u, nsp);  // (its selection and function as this lane wrote them)
+          // (its selection and function as this lane wrote them)
+          const uint64_t k = tile_contrib(TB, fc, u, nsp);
+          if (k) atomicAdd(&fc->chain_cnt, (unsigned long long)k);
           atomicAdd(&fc->seq, 1ull);
         }
       }
