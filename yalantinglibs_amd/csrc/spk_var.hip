@@ -3598,6 +3598,10 @@ constexpr uint16_t kMapUnk = 0xFFFEu;  // a bounded nested walk gave up: walked 
 constexpr uint32_t kMapExit = kTileBytes, kMapNear = 0xFFF0u - kMapExit;
 static_assert(kTileBytes <= 0x8000u, "chain map entries are u16 tile offsets");
 constexpr unsigned kChainGrid = 512;
+#ifndef SPK_PICK_PASSES  // pick / repair passes before the chain takes what they leave (1..3)
+#define SPK_PICK_PASSES 3
+#endif
+constexpr uint32_t kPickPasses = SPK_PICK_PASSES;
 constexpr uint32_t kChainSpin = 1u << 20;  // poll rounds (~1 us each) before a lost hand-off is an error
 
 template <uint32_t NW>
@@ -4492,12 +4496,12 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
              a, P, wire, (const uint8_t *)ws, TB, tile_dbg());
   if (tile_dbg() & 8192) return hipGetLastError();  // (A/B timing of K1 alone)
   if (phase == kTilesIndex) SPK_LAUNCH(vec_range_entry, dim3(1), dim3(64), 0, s, ws, TB);
-  for (uint32_t pass = 0; pass < 3; ++pass) {
+  for (uint32_t pass = 0; pass < kPickPasses; ++pass) {
     SPK_LAUNCH(vec_tile_pick, dim3(grid_for(f.ntiles, 256)), dim3(256), 0, s, ws, TB, nsp, pass);
     SPK_LAUNCH(vec_tile_repair<NS>, dim3(kRepairGrid), dim3(64), 0, s, a, P, wire, ws, TB, pass);
   }
   SPK_LAUNCH(vec_tile_chain<NS>, dim3(kChainGrid), dim3(64 * kChainWaves<NS>), 0, s, a, P, wire,
-             ws, TB, 2u);
+             ws, TB, kPickPasses - 1);
   SPK_LAUNCH(tscan_apply, dim3(nb), dim3(256), 0, s, ws, TB, 1 + nsp);
   }
   if (phase == kTilesIndex) {
