@@ -3404,25 +3404,40 @@ __global__ __launch_bounds__(256) void vec_tile_pick(uint8_t *__restrict__ ws, T
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= TB.ntiles || !vec_live(c)) return;
+  if (!vec_live(c)) return;                               // (uniform)
   if (pass > 0 && !fc->broken[pass - 1]) return;  // the previous pass fixed nothing
-  const uint64_t T = tile_entry(TB, fc, t);
-  int32_t sel = T == kNoPos ? kSelBroken : tile_select_for(TB, t, T);
-  // (a nested tile whose K1 walk gave up has an unknown exit: walked again)
-  if (sel >= 0 && TB.fn[t * kFnWords] == kNoPos) sel = kSelBroken;
-  if (sel != kSelBroken || T == kNoPos) {
-    TB.sel[t] = sel;
-    if (sel >= 0) tile_jump(TB, c->p0, t, TB.fn[t * kFnWords], nsp, 0, &fc->broken[pass], 1);
-    return;
+  // broken tiles are counted and listed with one atomic per wave (a broken
+  // tile per thread adding to the same two words serialised thousands of
+  // atomics: bytes after a message, e.g. a compatible member's version
+  // passes, break most of their tiles)
+  bool brk = false, list = false;
+  if (t < TB.ntiles) {
+    const uint64_t T = tile_entry(TB, fc, t);
+    int32_t sel = T == kNoPos ? kSelBroken : tile_select_for(TB, t, T);
+    // (a nested tile whose K1 walk gave up has an unknown exit: walked again)
+    if (sel >= 0 && TB.fn[t * kFnWords] == kNoPos) sel = kSelBroken;
+    if (sel != kSelBroken || T == kNoPos) {
+      TB.sel[t] = sel;
+      if (sel >= 0) tile_jump(TB, c->p0, t, TB.fn[t * kFnWords], nsp, 0, &fc->broken[pass], 1);
+    } else {
+      brk = true;
+      const uint64_t ts = c->p0 + t * kTileBytes;
+      if (T >= ts + kTileBytes) {  // inside a record that spans the tile
+        tile_pass_through(TB, t, T, nsp);
+        tile_jump(TB, c->p0, t, T, nsp, 0, &fc->broken[pass], 1);
+      } else {
+        list = true;
+      }
+    }
   }
-  atomicAdd(&fc->broken[pass], 1ull);
-  const uint64_t ts = c->p0 + t * kTileBytes;
-  if (T >= ts + kTileBytes) {  // inside a record that spans the tile
-    tile_pass_through(TB, t, T, nsp);
-    tile_jump(TB, c->p0, t, T, nsp, 0, &fc->broken[pass], 1);
-    return;
-  }
-  TB.blist[atomicAdd(&fc->nlist[pass], 1ull)] = (uint32_t)t;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t mb = __ballot(brk), ml = __ballot(list);
+  if (lane == 0 && mb) atomicAdd(&fc->broken[pass], (unsigned long long)__popcll(mb));
+  if (!ml) return;
+  uint64_t base = 0;
+  if (lane == 0) base = atomicAdd(&fc->nlist[pass], (unsigned long long)__popcll(ml));
+  base = __shfl(base, 0);
+  if (list) TB.blist[base + __popcll(ml & ((1ull << lane) - 1))] = (uint32_t)t;
 }
 
 // Tile t re-resolved from its true entry T, its window staged in tv: the
