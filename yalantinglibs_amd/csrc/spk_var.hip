@@ -3614,7 +3614,7 @@ constexpr uint32_t kMapExit = kTileBytes, kMapNear = 0xFFF0u - kMapExit;
 static_assert(kTileBytes <= 0x8000u, "chain map entries are u16 tile offsets");
 constexpr unsigned kChainGrid = 512;
 #ifndef SPK_PICK_PASSES  // pick / repair passes before the chain takes what they leave (1..3)
-#define SPK_PICK_PASSES 3
+#define SPK_PICK_PASSES 2
 #endif
 constexpr uint32_t kPickPasses = SPK_PICK_PASSES;
 constexpr uint32_t kChainSpin = 1u << 20;  // poll rounds (~1 us each) before a lost hand-off is an error
