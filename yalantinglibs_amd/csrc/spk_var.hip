@@ -1338,6 +1338,7 @@ struct WalkProg {
   uint32_t pf_var;                 // screening past segment 0's varints (NS = -1 walks)
   uint32_t rounds;                 // parallel re-verification rounds before the fixup
   uint32_t nv;                     // varint members
+  uint32_t hscr;                   // pf_all, nested: a has_value byte at skip[0] (screened 0 / 1)
   uint8_t vfirst[kVS + 2];  // segment k's varints: [vfirst[k], vfirst[k+1])
   uint32_t vafter[SPK_MAX_VARINTS];   // fixed bytes after varint j (same segment)
 };
@@ -2956,7 +2957,18 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
             m |= (cv <= c0t ? 1u : 0u) << kk;
           }
         }
-        if (P.pf_all) m = 0xFFu;  // first span an OPTION / no span: any byte may start a record
+        if (P.pf_all) {  // first span an OPTION / no span: any byte may start a record
+          m = 0xFFu;
+          if (NS <= -2 && P.hscr) {
+            // ... but a nested record that opens with an optional / expected
+            // group starts with a has_value byte, 0 or 1 from every writer
+            // (a start behind a larger one is found by the exact repair walk)
+            m = 0;
+#pragma unroll
+            for (int kk = 0; kk < 8; ++kk)
+              m |= (b0 + kk < len && rd.byte(b0 + kk) <= 1u ? 1u : 0u) << kk;
+          }
+        }
         if (NS <= -2 && P.scr2 && m) {
           // the second count, past the first span's payload
 #pragma unroll
@@ -4664,6 +4676,15 @@ static WalkProg make_walkprog_nested(const NLayout &N) {
     }
   } else {
     p.pf_all = 1;
+    // a record opening (after fixed bytes) with an optional / expected group
+    // or an OPTION: K1 screens candidate starts on that has_value byte
+    uint32_t i = 0, pre = 0;
+    while (i < N.n_ops && N.ops[i].kind == SPK_OP_COPY) pre += N.ops[i++].size;
+    if (i < N.n_ops && !N.fv_cnt &&
+        (N.ops[i].kind == SPK_OP_OPTGROUP || N.ops[i].kind == SPK_OP_OPTION)) {
+      p.hscr = 1;
+      p.skip[0] = pre;
+    }
   }
   p.rounds = kRounds;
   return p;
