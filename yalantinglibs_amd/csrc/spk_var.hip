@@ -1372,6 +1372,8 @@ static WalkProg make_walkprog(const spk_layout *L) {
   // a varint before the first count (or no count at all): the first count's
   // position is data-dependent, so every byte may start a record
   p.pf_all = (p.optm & 1u) || k == 0;
+  // (no has_value screen of candidate starts here: on Cmp's version passes,
+  // [has][int64][has][int16] records, it left 3x the broken tiles)
   p.pf_var = !p.pf_all && p.vfirst[1] > 0;
   // varint walks leave longer chains of unverified chunks: more parallel
   // rounds keep the one-lane fixup short
