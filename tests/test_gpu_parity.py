@@ -262,6 +262,29 @@ def test_vector_trailing_bytes(case, n, param, tail):
             assert back.heaps[k][:nb].cpu().numpy().tobytes() == heaps[k].tobytes()
 
 
+@pytest.mark.parametrize("case", ["cmp", "cmpg", "cmpnew"])
+@pytest.mark.parametrize("n,cap", [(0, 1), (1, 1), (700, 700), (700, 300)])
+def test_compat_vector_edges(case, n, cap):
+    """Compatible-member VECTOR decode on the tile passes at the edges: an
+    empty message, one record, and a record capacity below the count (the
+    passes are not clean: the one-lane walk behind them reports it) — errc,
+    count, consume_len and the records against the oracle."""
+    cd = codec_for(case)
+    _, recs, heaps = synth.make_batch(case, n, 0xED6E + n, 16)
+    out, _ = cd.serialize(to_dev(cd, recs, heaps), C.SPK_MODE_VECTOR)
+    wire = out.cpu().numpy().tobytes()
+    eres, erecs, eheaps, _ = H.oracle_decode(cd.L, C.SPK_MODE_VECTOR, wire, rec_cap=cap)
+    elems = [max(c, len(wire) // sp.elem.size + 1) for c, sp in
+             zip(S.heap_caps_for_wire(cd.L.dev, len(wire), cap), cd.L.dev.spans)]
+    b = cd.alloc_batch(cap, elems)
+    cd.deserialize_to(b, wire_dev(wire), C.SPK_MODE_VECTOR)
+    res = cd.result()
+    assert (res.errc, res.count, res.consumed) == (eres.errc, eres.count, eres.consumed)
+    if res.errc == 0 and n:
+        exp = np.ascontiguousarray(erecs[:n]).view(np.uint8).reshape(n, cd.L.stride)
+        assert b.recs[:n].cpu().numpy().tobytes() == exp.tobytes()
+
+
 def _irregular_messages(cd, case, n, seed, param):
     """A coro_rpc-style batch whose messages are not all canonical: trailing
     bytes, an explicit (zero) metainfo byte, truncations, broken heads,
