@@ -285,6 +285,43 @@ def test_compat_vector_edges(case, n, cap):
         assert b.recs[:n].cpu().numpy().tobytes() == exp.tobytes()
 
 
+@pytest.mark.parametrize("writer,reader", [("cmpold", "cmp"), ("cmpnew", "cmp"),
+                                           ("cmp", "cmpnew"), ("cmpold", "cmpnew")])
+def test_compat_vector_other_writer(writer, reader):
+    """One type code, three writer versions: a vector written by an older
+    writer (its version passes missing: every member absent) or a newer one
+    (passes the reader skips: consume_len is the compat length) decoded on
+    the tile passes == the oracle."""
+    cw, cr = codec_for(writer), codec_for(reader)
+    n = 3000
+    _, recs, heaps = synth.make_batch(writer, n, 0x01D + n, 16)
+    out, _ = cw.serialize(to_dev(cw, recs, heaps), C.SPK_MODE_VECTOR)
+    wire = out.cpu().numpy().tobytes()
+    eres, erecs, eheaps, _ = H.oracle_decode(cr.L, C.SPK_MODE_VECTOR, wire, rec_cap=n)
+    assert eres.errc == 0 and eres.count == n
+    elems = [max(c, len(wire) // sp.elem.size + 1) for c, sp in
+             zip(S.heap_caps_for_wire(cr.L.dev, len(wire), n), cr.L.dev.spans)]
+    b = cr.alloc_batch(n, elems)
+    b.recs.fill_(0xAB)
+    cr.deserialize_to(b, wire_dev(wire), C.SPK_MODE_VECTOR)
+    res = cr.result()
+    assert (res.errc, res.count, res.consumed) == (0, n, eres.consumed)
+    exp = np.ascontiguousarray(erecs[:n]).view(np.uint8).reshape(n, cr.L.stride)
+    got = b.recs[:n].cpu().numpy()
+    # the bytes the layout's ops describe (padding is not written)
+    mask = np.zeros(cr.L.stride, bool)
+    for op in cr.L.dev.ops:
+        k = op[0] & 0xFF
+        if k in (C.SPK_OP_COPY,):
+            mask[op[1]:op[1] + op[2]] = True
+        elif k in (C.SPK_OP_SPAN, C.SPK_OP_OPTION, C.SPK_OP_COMPAT):
+            mask[op[1]:op[1] + 4] = True
+            mask[op[3]:op[3] + 8] = True
+    assert np.array_equal(got[:, mask], exp[:, mask])
+    for k in range(len(cr.L.dev.spans)):
+        assert res.heap_used[k] == eres.heap_used[k]
+
+
 def _irregular_messages(cd, case, n, seed, param):
     """A coro_rpc-style batch whose messages are not all canonical: trailing
     bytes, an explicit (zero) metainfo byte, truncations, broken heads,
