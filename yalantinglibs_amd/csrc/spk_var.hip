@@ -1870,6 +1870,18 @@ struct NTLayout {
   uint2 wp[SPK_MAX_OPS];
 };
 constexpr uint32_t WP_SPAN = 1, WP_OPT = 2, WP_ARR = 3, WP_END = 4;
+// an optional / compatible group holding one SPAN (optional<string>,
+// compatible<vector<int>>): [has:1] then, if present, [count:w][payload]; an
+// error inside the group is dropped with the reader where it stopped
+// (unpacker.hpp:1251-1277) -- h / arg are the SPAN's heap and element size
+constexpr uint32_t WP_OSPAN = 5;
+// SPK_WP_OSPAN=1: the walk program takes optional / compatible groups of one
+// SPAN (late round 5, same-box A/B: cmpg 8.04 -> 6.0 ms per step, but cm 11.97
+// -> 12.45 ms: the NS = -3 kernels' extra code costs Monster's K1 / K4 ~5 %;
+// off until it gets an instantiation of its own)
+#ifndef SPK_WP_OSPAN
+#define SPK_WP_OSPAN 0
+#endif
 static_assert(sizeof(NTLayout) % 16 == 0, "NTLayout staged as 16-B words");
 static_assert(SPK_MAX_DEPTH == 4, "the walker's element stack has 4 register frames");
 
@@ -2288,6 +2300,32 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
       }
       continue;
     }
+#if SPK_WP_OSPAN
+    if (op == WP_OSPAN) {
+      if (lim - p < 1) return bad;  // (the has byte itself: the record fails)
+      const uint32_t b = rd.byte(p);
+      if (bounded && b > 1) return bad;  // (nt_read: a has_value byte above 1)
+      ++p;
+      if (b) {
+        // a count or payload that is not there: a bounded walk gives up, an
+        // exact one drops the group's error (reader after what it read)
+        if (lim - p < w) {
+          if (bounded) return bad;
+        } else {
+          const uint64_t c = rd.count_at32(p, wmask, false);
+          p += w;
+          if (c > lim - p || c * arg > lim - p) {
+            if (bounded) return bad;
+          } else {
+            atomicAdd(U + 64 * h, (uint32_t)c);
+            p += (uint32_t)(c * arg);
+          }
+        }
+      }
+      ++pc;
+      continue;
+    }
+#endif
     const bool opt = op == WP_OPT;
     const uint32_t cw = opt ? 1u : w;
     if (lim - p < cw) return bad;
@@ -2422,6 +2460,36 @@ __device__ uint64_t nt_emit_simple(const NTLayout &N, const Rd &rd, uint64_t pos
       ++i;
       continue;
     }
+#if SPK_WP_OSPAN
+    if (op.kind == SPK_OP_OPTGROUP) {  // WP_OSPAN: [has] [count][payload]
+      const uint32_t b = rd.byte(pos++);
+      *reinterpret_cast<uint32_t *>(r + op.rec_off) = b ? 1u : 0u;
+      if (b) {
+        const spk_op sp = N.ops[i + 1];
+        const uint32_t h = N.heap[i + 1];
+        uint64_t c = 0, nb = 0;
+        bool ok = len - pos >= w;
+        if (ok) {
+          c = rd(pos);
+          pos += w;
+          ok = span_nb(c, sp.size, &nb) && nb <= len - pos;
+        }
+        if (ok) {
+          const uint32_t o = U[64 * h];
+          U[64 * h] = o + (uint32_t)c;
+          *reinterpret_cast<uint32_t *>(r + sp.rec_off) = (uint32_t)c;
+          *reinterpret_cast<uint64_t *>(r + sp.aux) = o;
+          if (c) nt_put_payload(rd, N.heaps[h] + (uint64_t)o * sp.size, pos, nb, bq);
+          pos += nb;
+        } else {  // the group's error dropped: its members value-initialised (zero_rest)
+          *reinterpret_cast<uint32_t *>(r + sp.rec_off) = 0;
+          *reinterpret_cast<uint64_t *>(r + sp.aux) = 0;
+        }
+      }
+      i = N.end[i] + 1u;
+      continue;
+    }
+#endif
     const uint32_t hk = N.heap[i];
     const bool opt = op.kind == SPK_OP_OPTION;
     const uint64_t c = opt ? (uint64_t)(rd.byte(pos) != 0) : rd(pos);
@@ -4644,6 +4712,12 @@ static NTLayout make_ntlayout(const NLayout &N, void *const *heaps) {
     } else if (op.kind == SPK_OP_ARRAY && d < SPK_MAX_DEPTH) {
       open[d++] = n;
       x = WP_ARR | ((uint32_t)N.heap[i] << 3);
+    } else if (SPK_WP_OSPAN && op.kind == SPK_OP_OPTGROUP && op.size == 1 && i + 2 < N.n_ops &&
+               N.ops[i + 1].kind == SPK_OP_SPAN && N.ops[i + 2].kind == SPK_OP_END &&
+               N.end[i] == i + 2 && N.ops[i + 1].size < (1u << 24)) {
+      x = WP_OSPAN | ((uint32_t)N.heap[i + 1] << 3) |
+          ((N.ops[i + 1].size ? N.ops[i + 1].size : 1u) << 8);
+      i += 2;  // (the group's SPAN and END are this instruction)
     } else if (op.kind == SPK_OP_END && d) {
       x = WP_END;
       --d;
