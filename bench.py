@@ -570,20 +570,46 @@ def pmc_traffic(cfg, pmc_dir):
     return {}, None
 
 
+class ConfigFailed(RuntimeError):
+    """A config failed on at least one rank; raised on EVERY rank (after the
+    ranks agreed on it), so no rank is left waiting in a collective."""
+
+    def __init__(self, msg, code=1):
+        super().__init__(msg)
+        self.code = code
+
+
+def agree_ok(ok, torch, dist, world, dev):
+    """True iff every rank passed `ok` (MIN over ranks; trivially ok at N=1).
+    Every rank must call it at the same point: it is itself a collective."""
+    if world <= 1:
+        return bool(ok)
+    on = dev if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=on)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
 def measure(wl, args, torch, dist, world, dev, steps, warmup, settle):
     """Gate, settle, warmup, K timed steps (barrier + sync on both sides,
     max over ranks), then instrumented steps: phase events + per-kernel
     hipEvents (spk_trace) on the launch stream."""
     from yalantinglibs_amd import _capi as C
     stream = torch.cuda.current_stream(dev)
-    wl.step(stream)
-    torch.cuda.synchronize(dev)
-    diag = os.environ.get("SPK_TILE_DBG", "0") not in ("", "0")  # (diagnostics builds)
-    bad = None if diag else wl.check()  # diagnostics runs (wrong output by design): no gate
+    bad = None
+    try:
+        wl.step(stream)
+        torch.cuda.synchronize(dev)
+        diag = os.environ.get("SPK_TILE_DBG", "0") not in ("", "0")  # (diagnostics builds)
+        bad = None if diag else wl.check()  # diagnostics runs (wrong output by design): no gate
+    except Exception as e:  # a local fault: report it, then fail on every rank together
+        bad = f"{type(e).__name__}: {e}"
     if bad:
         print(json.dumps({"error": "round trip mismatch", "config": wl.cfg, "what": bad}),
               flush=True)
-        sys.exit(3)
+    if not agree_ok(not bad, torch, dist, world, dev):
+        raise ConfigFailed(f"{wl.cfg}: first step failed on "
+                           f"{'this rank' if bad else 'another rank'}", code=3)
     t_settle = time.perf_counter()
     while time.perf_counter() - t_settle < settle:
         wl.step(stream)
@@ -668,7 +694,19 @@ def roofline(wl, kernels, pmc, pmc_src):
 
 def run_config(cfg, args, torch, dist, world, rank, dev, steps, warmup, settle, cpu):
     n = args.records if cfg == args.config else 0
-    wl = C5Workload(torch, n, rank, dev) if cfg == "c5" else VecWorkload(torch, cfg, n, rank, dev)
+    wl, err = None, None
+    try:  # build on every rank, then agree before the first collective
+        wl = C5Workload(torch, n, rank, dev) if cfg == "c5" else VecWorkload(torch, cfg, n, rank,
+                                                                             dev)
+    except Exception as e:
+        err = f"{type(e).__name__}: {e}"
+        print(f"[bench] rank {rank}: {cfg} workload build failed: {err}", file=sys.stderr,
+              flush=True)
+    if not agree_ok(err is None, torch, dist, world, dev):
+        wl = None
+        torch.cuda.empty_cache()
+        raise ConfigFailed(f"{cfg}: workload build failed on "
+                           f"{'this rank: ' + err if err else 'another rank'}")
     dt, phase_ms, kernels = measure(wl, args, torch, dist, world, dev, steps, warmup, settle)
     ms_step = dt * 1e3 / steps
     sync_variant = None
@@ -765,9 +803,15 @@ def concat_bench(torch, dist, world, rank, dev, n, reps=3):
     from yalantinglibs_amd import layout as LY
     from yalantinglibs_amd import parallel as PAR
     from yalantinglibs_amd import struct_pack as SP
-    cd = SP.Codec(LY.case_layout("rec64"), device=dev)
-    batch = SP.synth_batch(cd, "rec64", n, SEEDS["rec64"], 0, first=rank * n)
-    enc = PAR.ShardedVectorEncoder(cd)
+    err = None
+    try:  # local setup on every rank, agreed on before the first collective
+        cd = SP.Codec(LY.case_layout("rec64"), device=dev)
+        batch = SP.synth_batch(cd, "rec64", n, SEEDS["rec64"], 0, first=rank * n)
+        enc = PAR.ShardedVectorEncoder(cd)
+    except Exception as e:
+        err = f"{type(e).__name__}: {e}"
+    if not agree_ok(err is None, torch, dist, world, dev):
+        raise ConfigFailed(f"concat: setup failed on {'this rank: ' + err if err else 'another rank'}")
     red_dev = torch.device("cpu") if dist.get_backend() == "gloo" else dev
 
     def timed(fn):
@@ -814,8 +858,8 @@ def concat_bench(torch, dist, world, rank, dev, n, reps=3):
     dec = None
     try:
         dec = sharded_decode_bench(torch, dist, world, rank, dev, timed)
-    except Exception as e:  # never lose the concat numbers
-        dec = {"error": f"{type(e).__name__}: {e}"}
+    except ConfigFailed as e:  # raised on every rank together (other faults propagate:
+        dec = {"error": str(e)}  # torch.distributed.run then ends every rank)
     return {
         "sharded_decode": dec,
         "workload": f"one serialize(vector<Rec64>) message of {world} x {n} records "
@@ -929,13 +973,20 @@ def sharded_decode_bench(torch, dist, world, rank, dev, timed, per_rank=2_000_00
     from yalantinglibs_amd import layout as LY
     from yalantinglibs_amd import parallel as PAR
     from yalantinglibs_amd import struct_pack as SP
-    cd = SP.Codec(LY.case_layout("outer"), device=dev)
     n = per_rank * world
-    batch = SP.synth_batch(cd, "outer", n, SEEDS["outer"], 16)
-    wire, _ = cd.serialize(batch, SP.MODE_VECTOR)
-    del batch
-    torch.cuda.empty_cache()
-    dec = PAR.ShardedVectorDecoder(cd)
+    err = None
+    try:  # local setup on every rank, agreed on before the first collective
+        cd = SP.Codec(LY.case_layout("outer"), device=dev)
+        batch = SP.synth_batch(cd, "outer", n, SEEDS["outer"], 16)
+        wire, _ = cd.serialize(batch, SP.MODE_VECTOR)
+        del batch
+        torch.cuda.empty_cache()
+        dec = PAR.ShardedVectorDecoder(cd)
+    except Exception as e:
+        err = f"{type(e).__name__}: {e}"
+    if not agree_ok(err is None, torch, dist, world, dev):
+        raise ConfigFailed(f"sharded decode: setup failed on "
+                           f"{'this rank: ' + err if err else 'another rank'}")
     out = [None]
 
     def run():
@@ -1077,14 +1128,21 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    head = run_config(args.config, args, torch, dist, world, rank, dev, args.steps,
-                      args.warmup, args.settle, cpu=True)
+    try:
+        head = run_config(args.config, args, torch, dist, world, rank, dev, args.steps,
+                          args.warmup, args.settle, cpu=True)
+    except ConfigFailed as e:  # every rank got here together: no rank waits in a collective
+        if rank == 0:
+            print(json.dumps({"error": str(e), "config": args.config}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        sys.exit(e.code)
     concat = None
     if world > 1 and not args.no_concat:
         try:
             concat = concat_bench(torch, dist, world, rank, dev, args.concat_records)
-        except Exception as e:  # never lose the headline line
-            concat = {"error": f"{type(e).__name__}: {e}"}
+        except ConfigFailed as e:  # raised on every rank together; any other fault
+            concat = {"error": str(e)}  # propagates and torch.distributed.run ends every rank
     if rank == 0:  # progress on stderr (the JSON line stays the only stdout line)
         print(f"[bench] {args.config}: {head['ms_per_step']} ms/step", file=sys.stderr, flush=True)
     extra = {}
@@ -1095,8 +1153,8 @@ def main():
             try:
                 extra[cfg] = run_config(cfg, args, torch, dist, world, rank, dev,
                                         args.extra_steps, 2, 0.5, cpu=False)
-            except Exception as e:  # never lose the headline line
-                extra[cfg] = {"error": f"{type(e).__name__}: {e}"}
+            except ConfigFailed as e:  # raised on every rank together: skip it everywhere
+                extra[cfg] = {"error": str(e)}
             if rank == 0:
                 print(f"[bench] {cfg} x{world}: {extra[cfg].get('ms_per_step')} ms/step",
                       file=sys.stderr, flush=True)

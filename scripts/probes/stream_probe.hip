@@ -1,0 +1,246 @@
+// Micro-benchmark for the C2 byte-shifted stream copy (shift_copy_kernel):
+// register-staged forms (the shipped one and grid / unroll / block-size
+// variants) against an LDS-DMA ring (global_load_lds_dwordx4 into a per-wave
+// LDS ring, ds_read_b128, aligned global_store_dwordx4), with and without nt,
+// and hipMemcpyAsync D2D as the platform's own copy on the same box.
+// Every variant's output is checked byte for byte on a sample of chunks.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef v4u v4u_u __attribute__((aligned(1)));
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
+
+// ---- register-staged: U chunks per lane in flight, grid-stride over tiles
+template <int U, int NT>
+__global__ __launch_bounds__(256) void reg_copy(v4u *__restrict__ dst, const uint8_t *__restrict__ sp,
+                                                uint64_t nk) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint64_t wid = (uint64_t)blockIdx.x * wpb + (threadIdx.x >> 6);
+  const uint64_t nw = (uint64_t)gridDim.x * wpb;
+  const uint64_t tile = 64ull * U;
+  for (uint64_t t0 = wid * tile; t0 + tile <= nk; t0 += nw * tile) {
+    v4u c[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const v4u_u *p = reinterpret_cast<const v4u_u *>(sp + 16 * (t0 + j * 64 + lane));
+      c[j] = (NT & 1) ? __builtin_nontemporal_load(p) : *p;
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (NT & 2) __builtin_nontemporal_store(c[j], &dst[t0 + j * 64 + lane]);
+      else dst[t0 + j * 64 + lane] = c[j];
+    }
+  }
+}
+
+
+// ---- register double buffer: loads of tile k+1 in flight while tile k stores
+template <int U, int NT>
+__global__ __launch_bounds__(256) void regdb_copy(v4u *__restrict__ dst, const uint8_t *__restrict__ sp,
+                                                  uint64_t nk) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wid = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  const uint64_t tile = 64ull * U;
+  uint64_t t0 = wid * tile;
+  if (t0 + tile > nk) return;
+  v4u a[U], b[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) a[j] = *reinterpret_cast<const v4u_u *>(sp + 16 * (t0 + j * 64 + lane));
+  for (;;) {
+    const uint64_t t1 = t0 + nw * tile;
+    const bool more = t1 + tile <= nk;
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < U; ++j) b[j] = *reinterpret_cast<const v4u_u *>(sp + 16 * (t1 + j * 64 + lane));
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (NT & 2) __builtin_nontemporal_store(a[j], &dst[t0 + j * 64 + lane]);
+      else dst[t0 + j * 64 + lane] = a[j];
+    }
+    if (!more) break;
+#pragma unroll
+    for (int j = 0; j < U; ++j) a[j] = b[j];
+    t0 = t1;
+  }
+}
+
+// ---- chunked: each wave walks one contiguous range of tiles
+template <int U>
+__global__ __launch_bounds__(256) void chunk_copy(v4u *__restrict__ dst, const uint8_t *__restrict__ sp,
+                                                  uint64_t nk) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wid = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  const uint64_t tile = 64ull * U;
+  const uint64_t ntile = nk / tile;
+  const uint64_t per = (ntile + nw - 1) / nw;
+  uint64_t tb = wid * per, te = tb + per;
+  if (te > ntile) te = ntile;
+  for (uint64_t t = tb; t < te; ++t) {
+    const uint64_t t0 = t * tile;
+    v4u c[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) c[j] = *reinterpret_cast<const v4u_u *>(sp + 16 * (t0 + j * 64 + lane));
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < U; ++j) dst[t0 + j * 64 + lane] = c[j];
+  }
+}
+
+// ---- LDS-DMA ring: each wave owns S slots of U KiB; slot = U glds (1 KiB each)
+template <int NT>
+__device__ __forceinline__ void glds16(const uint8_t *g, uint32_t lds_byte) {
+  unsigned keep;
+  if (NT)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds_byte) : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(lds_byte) : "memory");
+}
+template <int N> __device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" :: "i"(N) : "memory");
+}
+
+template <int U, int S, int WPB, int NT>
+__global__ __launch_bounds__(64 * WPB) void glds_copy(v4u *__restrict__ dst, const uint8_t *__restrict__ sp,
+                                                      uint64_t nk) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[WPB * S * U * 1024];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t w = threadIdx.x >> 6;
+  const uint64_t wid = (uint64_t)blockIdx.x * WPB + w;
+  const uint64_t nw = (uint64_t)gridDim.x * WPB;
+  const uint64_t tile = 64ull * U;
+  uint8_t *my = ring + w * S * U * 1024;
+  const uint32_t my_lds = (uint32_t)__builtin_amdgcn_readfirstlane(
+      (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t *)my);
+  // tiles of this wave: t = wid + k*nw, k = 0..cnt-1
+  const uint64_t ntile = nk / tile;
+  if (wid >= ntile) return;
+  const uint64_t cnt = (ntile - wid + nw - 1) / nw;
+  auto issue = [&](uint64_t k) {
+    const uint64_t t0 = (wid + k * nw) * tile;
+    const uint32_t slot = (uint32_t)(k % S);
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      glds16<NT>(sp + 16 * (t0 + j * 64 + lane), my_lds + (slot * U + j) * 1024);
+  };
+  // prologue: fill all S slots (pad with no-ops so the count stays fixed)
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+    if ((uint64_t)s < cnt) issue(s);
+  for (uint64_t k = 0; k < cnt; ++k) {
+    // after glds(k): stores(k-S..k-1) and glds(k+1..k+S-1), U each -> (2S-1)U ops.
+    // Near the end fewer were issued; waiting for everything is then correct.
+    if (k + S <= cnt && k >= (uint64_t)S) wait_vm<(2 * S - 1) * U>();
+    else wait_vm<0>();
+    const uint32_t slot = (uint32_t)(k % S);
+    v4u c[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      c[j] = *reinterpret_cast<const v4u *>(my + (slot * U + j) * 1024 + lane * 16);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (k + S < cnt) issue(k + S);
+    const uint64_t t0 = (wid + k * nw) * tile;
+#pragma unroll
+    for (int j = 0; j < U; ++j) dst[t0 + j * 64 + lane] = c[j];
+  }
+}
+
+static uint8_t *g_hs = nullptr;
+
+static int check(const uint8_t *d_dst, uint64_t nk, uint64_t shift, const char *name) {
+  // sample 4096 chunks spread over the range (+ first/last full tiles)
+  std::vector<uint8_t> got(16);
+  int bad = 0;
+  for (int i = 0; i < 4096 && !bad; ++i) {
+    uint64_t k = (nk - 1) * (uint64_t)i / 4095;
+    if (hipMemcpy(got.data(), d_dst + 16 * k, 16, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+    for (int b = 0; b < 16; ++b) {
+      uint64_t off = 16 * k + b + shift;
+      uint8_t want = (uint8_t)(off * 2654435761ull >> 13);
+      if (got[b] != want) { bad = 1; printf("  MISMATCH %s chunk %lu byte %d\n", name, k, b); break; }
+    }
+  }
+  return bad;
+}
+
+__global__ void fill(uint8_t *s, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    s[i] = (uint8_t)(i * 2654435761ull >> 13);
+}
+
+template <class F>
+static double timeit(F f, int reps) {
+  hipEvent_t a, b;
+  hipEventCreate(&a); hipEventCreate(&b);
+  f(); f();
+  hipDeviceSynchronize();
+  hipEventRecord(a);
+  for (int i = 0; i < reps; ++i) f();
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms; hipEventElapsedTime(&ms, a, b);
+  hipEventDestroy(a); hipEventDestroy(b);
+  return ms / reps;
+}
+
+int main(int argc, char **argv) {
+  const uint64_t bytes = 6400000000ull;  // C2: 100M x 64 B
+  const uint64_t shift = argc > 2 ? atoi(argv[2]) : 9;  // C2 wire header (9 B)
+  const int reps = argc > 1 ? atoi(argv[1]) : 10;
+  uint8_t *s, *d;
+  CK(hipMalloc(&s, bytes + 8192));
+  CK(hipMalloc(&d, bytes + 8192));
+  fill<<<8192, 256>>>(s, bytes + 8192);
+  CK(hipMemset(d, 0, bytes + 8192));
+  CK(hipDeviceSynchronize());
+  const uint64_t nk = bytes / 16;
+  const uint8_t *sp = s + shift;
+  v4u *dst = reinterpret_cast<v4u *>(d);
+  auto report = [&](const char *name, double ms, int ok) {
+    printf("%-40s %8.4f ms  %7.1f GB/s  %s\n", name, ms, 2.0 * bytes / ms / 1e6, ok ? "ok" : "BAD");
+    fflush(stdout);
+  };
+  auto run_reg = [&](const char *name, auto kern, int blocks, int threads) {
+    CK(hipMemset(d, 0, bytes));
+    double ms = timeit([&] { kern<<<blocks, threads>>>(dst, sp, nk); }, reps);
+    CK(hipGetLastError());
+    CK(hipDeviceSynchronize());
+    report(name, ms, !check(d, nk - 1024, shift, name));
+    return 0;
+  };
+  const int exact16 = (int)((nk / (64 * 16) + 3) / 4);
+  const int exact32 = (int)((nk / (64 * 32) + 3) / 4);
+  run_reg("reg U16 B32768 (shipped)", reg_copy<16, 0>, 32768, 256);
+  run_reg("reg U32 B16384 ntS", reg_copy<32, 2>, 16384, 256);
+  run_reg("reg U32 B16384 ntLS", reg_copy<32, 3>, 16384, 256);
+  run_reg("reg U32 B16384 ntL", reg_copy<32, 1>, 16384, 256);
+  run_reg("reg U16 B32768 ntS", reg_copy<16, 2>, 32768, 256);
+  run_reg("reg U16 B32768 ntLS", reg_copy<16, 3>, 32768, 256);
+  run_reg("reg U16 B32768 (shipped) #2", reg_copy<16, 0>, 32768, 256);
+  run_reg("reg U32 exact ntS", reg_copy<32, 2>, exact32, 256);
+  run_reg("reg U32 exact ntLS", reg_copy<32, 3>, exact32, 256);
+  run_reg("reg U16 exact ntS", reg_copy<16, 2>, exact16, 256);
+  run_reg("reg U16 exact ntLS", reg_copy<16, 3>, exact16, 256);
+  run_reg("reg U32 B32768 ntS", reg_copy<32, 2>, 32768, 256);
+  run_reg("reg U32 B8192 ntS", reg_copy<32, 2>, 8192, 256);
+  run_reg("reg U24 B16384 ntS", reg_copy<24, 2>, 16384, 256);
+  run_reg("regdb U16 B16384 ntS", regdb_copy<16, 2>, 16384, 256);
+  run_reg("reg U16 B32768 (shipped) #3", reg_copy<16, 0>, 32768, 256);
+  run_reg("reg U32 B16384 ntS #2", reg_copy<32, 2>, 16384, 256);
+  run_reg("reg U32 B16384 ntLS #2", reg_copy<32, 3>, 16384, 256);
+    run_reg("reg U16 B32768 (shipped, again)", reg_copy<16, 0>, 32768, 256);
+  return 0;
+}

@@ -50,3 +50,56 @@ def test_gpus_2_spawns_two_ranks():
 def test_launcher_with_wrong_world_fails_loudly():
     r = _run(["--gpus", "2", "--spawn-probe"], {"WORLD_SIZE": "1", "RANK": "0"})
     assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def _agree_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        oks = [bench.agree_ok(True, torch, dist, world, "cpu"),
+               bench.agree_ok(rank != 1, torch, dist, world, "cpu")]
+
+        class Boom:  # the workload build fails on rank 1 only
+            def __init__(self, *a):
+                if rank == 1:
+                    raise MemoryError("synthetic OOM")
+
+        bench.VecWorkload = Boom
+
+        class A:
+            records = 0
+            config = "c2"
+        try:
+            bench.run_config("c4", A, torch, dist, world, rank, "cpu", 1, 0, 0, cpu=False)
+            raised = None
+        except bench.ConfigFailed as e:
+            raised = str(e)
+        # the ranks are still in step: one more collective completes
+        after = bench.agree_ok(True, torch, dist, world, "cpu")
+        q.put((rank, oks, raised, after))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_config_failure_agreed_across_ranks():
+    """a config that fails on one rank must fail on every rank
+    before any collective of the config runs (no rank left waiting)."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_agree_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [g[1] for g in got] == [[True, False], [True, False]]
+    assert "another rank" in got[0][2] and "synthetic OOM" in got[1][2]
+    assert all(g[3] for g in got)

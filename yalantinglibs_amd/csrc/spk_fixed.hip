@@ -9,9 +9,15 @@
 // wave-instruction) and reads each one with a single byte-aligned
 // global_load_dwordx4 (gfx950 runs in unaligned-access mode): every HBM byte
 // is read once and written once, no cross-lane shuffles. Measured on MI355X
-// (scripts/probes/copy_probe.hip): this form runs at least as fast as an
-// aligned 16-B copy; 16 chunks in flight per lane (256 B) beat 8 by 5-13 %
-// (6.1-6.2 TB/s on a good box), 32 Ki blocks.
+// (scripts/probes/stream_probe.hip, gpurun_out logs in profiles/r06/): 32
+// chunks in flight per lane (512 B, a 32 KiB wave-tile) with non-temporal
+// loads AND stores and one wave-tile per wave (exact grid) run at 6.15-6.17
+// TB/s where the round-5 form (16 chunks, default policy, 32 Ki blocks) runs
+// at 5.64-5.66 on the same box (+9 %); nt on either side alone, or nt at 16
+// chunks, does not pay. An LDS-DMA ring (global_load_lds_dwordx4 into a
+// per-wave 2-4 slot ring, ds_read_b128, aligned stores; with and without nt)
+// measured 4-10 % SLOWER than the register form, and hipMemcpyAsync D2D
+// slower still (4.4-5.0 TB/s).
 // The shift is data-dependent on decode (width/meta/type-literal of the
 // incoming header): the kernel reads it from a device-side CopyJob written by
 // the header kernel, so no host round trip is needed.
@@ -42,7 +48,7 @@ typedef uint32_t v4u __attribute__((ext_vector_type(4)));
 typedef v4u v4u_unaligned __attribute__((aligned(1)));
 
 constexpr int kCopyThreads = 256;
-constexpr int kCopyUnroll = 16;
+constexpr int kCopyUnroll = 32;
 constexpr uint64_t kTile = 64ull * kCopyUnroll;  // chunks per wave-tile
 
 // dst chunk k (k in [0, nk)) = 16 source bytes at sp + 16k (any alignment)
@@ -56,14 +62,15 @@ __device__ __forceinline__ void shift_body(v4u *__restrict__ dst,
       v4u c[kCopyUnroll];
 #pragma unroll
       for (int j = 0; j < kCopyUnroll; ++j)
-        c[j] = *reinterpret_cast<const v4u_unaligned *>(sp + 16 * (t0 + j * 64 + lane));
+        c[j] = __builtin_nontemporal_load(
+            reinterpret_cast<const v4u_unaligned *>(sp + 16 * (t0 + j * 64 + lane)));
       // Keep all kCopyUnroll loads in flight before the first store: after
       // inlining, the compiler no longer proves dst and sp disjoint and
       // would otherwise interleave load/store pairs (2 loads in flight,
       // ~12 % slower: scripts/probes/c2_probe.cpp vs copy_probe.hip).
       asm volatile("" ::: "memory");
 #pragma unroll
-      for (int j = 0; j < kCopyUnroll; ++j) dst[t0 + j * 64 + lane] = c[j];
+      for (int j = 0; j < kCopyUnroll; ++j) __builtin_nontemporal_store(c[j], &dst[t0 + j * 64 + lane]);
     } else {
       for (uint64_t k = t0 + lane; k < nk; k += 64)
         dst[k] = *reinterpret_cast<const v4u_unaligned *>(sp + 16 * k);
@@ -102,11 +109,9 @@ __global__ __launch_bounds__(kCopyThreads) void shift_copy_kernel(
 static unsigned copy_grid(uint64_t max_bytes) {
   uint64_t tiles = (max_bytes / 16 + kTile - 1) / kTile;
   uint64_t blocks = (tiles + (kCopyThreads / 64) - 1) / (kCopyThreads / 64);
-  // 32 Ki blocks (128 Ki waves) then grid-stride: the probe's best point
-  // (scripts/probes/copy_probe.hip: 16 chunks in flight per lane, 6.1-6.2 TB/s)
-  // (a whole number of resident rounds of blocks instead was measured slower:
-  // C2 step 4.36 -> 4.60-4.74 ms)
-  if (blocks > 32768) blocks = 32768;
+  // one wave-tile per wave (exact grid; 48,828 blocks for C2's 6.4 GB) — the
+  // probe's best point; grid-stride only past 2^20 blocks (> 128 GiB)
+  if (blocks > (1u << 20)) blocks = 1u << 20;
   if (blocks < 1) blocks = 1;
   return (unsigned)blocks;
 }
