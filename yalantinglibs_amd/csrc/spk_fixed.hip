@@ -408,6 +408,24 @@ __device__ __forceinline__ uint32_t g_u32_at(const uint8_t *p) {
   return *reinterpret_cast<const uint32_t __attribute__((aligned(1))) *>(p);
 }
 
+// MESSAGES mode: non-temporal staging loads and record / wire stores (C2b
+// A/B on one box: encode 2.556 -> 2.47 ms, decode 2.89 -> 2.85 ms). (A
+// software-pipelined decode — the next group's staging loads in registers
+// while this group is parsed and stored — measured 25 % SLOWER: 2.81 ->
+// 3.65 ms, same box, profiles/r06/ab_c2b.txt.)
+#ifndef SPK_MSG_NT
+#define SPK_MSG_NT 1
+#endif
+__device__ __forceinline__ v4u msg_ld16(const uint8_t *p) {
+  const v4u_unaligned *q = reinterpret_cast<const v4u_unaligned *>(p);
+  if (SPK_MSG_NT) return __builtin_nontemporal_load(q);
+  return *q;
+}
+__device__ __forceinline__ void msg_st16(uint8_t *p, const v4u &v) {
+  if (SPK_MSG_NT) __builtin_nontemporal_store(v, reinterpret_cast<v4u *>(p));
+  else *reinterpret_cast<v4u *>(p) = v;
+}
+
 template <bool DW>
 __global__ __launch_bounds__(kMsgThreads) void fixed_msg_encode_lds(
     MsgLdsArgs a, const uint8_t *__restrict__ in, uint8_t *__restrict__ out,
@@ -431,7 +449,7 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_encode_lds(
 #pragma unroll
     for (uint32_t k = 0; k < kStagePer; ++k) {
       const uint32_t c = c0 + tid + k * kMsgThreads;
-      if (c < bin / 16) val[k] = *reinterpret_cast<const v4u_unaligned *>(src + 16 * c);
+      if (c < bin / 16) val[k] = msg_ld16(src + 16 * c);
     }
 #pragma unroll
     for (uint32_t k = 0; k < kStagePer; ++k) {
@@ -466,7 +484,7 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_encode_lds(
       }
       if (q0 + 4 <= nq) {
         v4u o = {v[0], v[1], v[2], v[3]};
-        *reinterpret_cast<v4u *>(dst + 16 * t) = o;
+        msg_st16(dst + 16 * t, o);
       } else {
         for (uint32_t k = 0; q0 + k < nq; ++k)
           reinterpret_cast<uint32_t *>(dst)[q0 + k] = v[k];
@@ -551,7 +569,7 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
 #pragma unroll
           for (uint32_t k = 0; k < kStagePer; ++k) {
             const uint32_t c = c0 + tid + k * kMsgThreads;
-            if (c < nc) val[k] = *reinterpret_cast<const v4u_unaligned *>(wire + lo + 16 * (uint64_t)c);
+            if (c < nc) val[k] = msg_ld16(wire + lo + 16 * (uint64_t)c);
           }
 #pragma unroll
           for (uint32_t k = 0; k < kStagePer; ++k) {
@@ -623,7 +641,7 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
         }
         if (valid == 0xF) {
           v4u o = {v[0], v[1], v[2], v[3]};
-          *reinterpret_cast<v4u *>(dst + 16 * t) = o;
+          msg_st16(dst + 16 * t, o);
         } else {
           for (int k = 0; k < 4; ++k)
             if (valid & (1u << k)) reinterpret_cast<uint32_t *>(dst)[d0 + k] = v[k];
