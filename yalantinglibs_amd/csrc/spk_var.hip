@@ -4115,6 +4115,9 @@ constexpr uint16_t kTabFar = 0xFFFFu;  // a table end past the window
 // the caller's records average kWaveCopy wire bytes or more (wire_len /
 // rec_cap): its registers cost K4 a wave per SIMD (C3 K4 0.304 -> 0.326 ms),
 // which messages of short records need not pay (c3l K4 5.3 -> 2.2 ms).
+#ifndef SPK_K4_REV  // K4 takes the tiles last to first
+#define SPK_K4_REV 1  // (reversed: K4 first reads the tiles K1 read last; c3 K4 0.306 -> 0.298 ms, c4 0.483 -> 0.476, cv 1.136 -> 1.113, same-box A/B)
+#endif
 template <int NS, bool DEFER = false>
 __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkProg P,
                                                                 const uint8_t *__restrict__ wire,
@@ -4131,7 +4134,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t gw = (uint64_t)blockIdx.x * kDecWaves + wv;
+  const uint64_t gw = (uint64_t)(SPK_K4_REV ? gridDim.x - 1 - blockIdx.x : blockIdx.x) * kDecWaves + wv;
   const uint64_t t = gw / kEmitSplit;
   const uint32_t part = (uint32_t)(gw % kEmitSplit);
   if (t >= TB.ntiles || !vec_live(c)) return;
