@@ -198,10 +198,35 @@ class buffer {
   std::size_t n_ = 0;
 };
 
+// RAII pinned host allocation (spk_host_alloc_pinned), grows only
+class pinned {
+ public:
+  pinned() = default;
+  pinned(const pinned &) = delete;
+  pinned &operator=(const pinned &) = delete;
+  ~pinned() {
+    if (p_) (void)spk_host_free_pinned(p_);
+  }
+  void resize(std::size_t n) {  // contents not preserved
+    if (n <= n_ && p_) return;
+    if (p_) check(spk_host_free_pinned(p_), "spk_host_free_pinned");
+    p_ = nullptr;
+    n_ = 0;
+    check(spk_host_alloc_pinned(&p_, n ? n : 1), "spk_host_alloc_pinned");
+    n_ = n;
+  }
+  uint8_t *data() const { return static_cast<uint8_t *>(p_); }
+
+ private:
+  void *p_ = nullptr;
+  std::size_t n_ = 0;
+};
+
 inline void copy(void *dst, const void *src, std::size_t n, int kind, void *s) {
   check(spk_copy_async(dst, src, n, kind, s), "spk_copy_async");
 }
 inline void sync(void *s) { check(spk_stream_sync(s), "spk_stream_sync"); }
+
 
 // A batch of R in device memory: device records + one heap per span.
 template <typename R>
@@ -288,6 +313,159 @@ class codec {
         if constexpr (!std::is_same_v<Pred, std::nullptr_t>)
           if (!ok(i)) continue;
         detail::unmarshal_state st{&L, recs.data() + i * L.rec_stride, 0, 0, hp.data(), 0};
+        detail::from_device(out[i], st);
+      }
+    }
+  }
+
+  // ---- one small message per call (the coro_rpc seam) ---------------------
+  // A per-thread device arena and a pinned staging buffer with the same
+  // layout, both reused across calls (grown, never freed per call): the
+  // records and heaps go to the device in ONE copy, plan + encode (or the
+  // decode) run stream-ordered in the arena, the plan / result and the
+  // output come back in ONE copy, and the call syncs once. No allocation
+  // after the first call of a size. Calls larger than kSmallBytes take the
+  // batch path (upload / plan / encode / download).
+  static constexpr std::size_t kSmallBytes = std::size_t(1) << 20;
+  static constexpr std::size_t al(std::size_t x) { return (x + 255) & ~std::size_t(255); }
+
+  // Marshal n values into the encode scratch (records + one vector per heap).
+  template <typename X = R>
+  std::size_t marshal(const X *v, std::size_t n) {
+    const spk_layout &L = layout();
+    mrecs_.assign(n * L.rec_stride, 0);
+    mheaps_.resize(n_spans());
+    for (auto &h : mheaps_) h.clear();
+    if constexpr (trivial && std::is_same_v<X, R>) {
+      if (n) std::memcpy(mrecs_.data(), v, n * sizeof(R));
+    } else {
+      for (std::size_t i = 0; i < n; ++i) {
+        detail::marshal_state st{&L, mrecs_.data() + i * L.rec_stride, 0, 0, &mheaps_, 0};
+        detail::to_device(v[i], st);
+      }
+    }
+    std::size_t b = mrecs_.size();
+    for (auto &h : mheaps_) b += h.size();
+    return b;
+  }
+
+  // serialize n values as one message (VECTOR) or one record message
+  // (MESSAGES, n == 1): returns false (nothing done) when the call is not
+  // small; otherwise sink(bytes, len) gets the message.
+  template <typename X, typename Sink>
+  bool encode_small(const X *v, std::size_t n, int mode, Sink &&sink) {
+    const spk_layout &L = layout();
+    const std::size_t in_bytes = marshal(v, n);
+    if (in_bytes > kSmallBytes) return false;
+    // arena: [plan 256][out cap][offsets 256][records][heap 0]...[heap k]
+    // (the first two come back in one D2H, the rest goes over in one H2D)
+    const std::size_t out_cap = al(2 * in_bytes + 16 * n + 4096);
+    const std::size_t o_out = 256, o_offs = o_out + out_cap, o_recs = o_offs + 256;
+    std::size_t end = al(o_recs + mrecs_.size());
+    std::vector<std::size_t> o_heap(n_spans());
+    for (uint32_t k = 0; k < n_spans(); ++k) {
+      o_heap[k] = end;
+      end = al(end + mheaps_[k].size());
+    }
+    arena_.resize(end);
+    pin_.resize(end);
+    uint8_t *hp = pin_.data(), *dp = static_cast<uint8_t *>(arena_.data());
+    if (!mrecs_.empty()) std::memcpy(hp + o_recs, mrecs_.data(), mrecs_.size());
+    std::vector<const void *> dheaps(n_spans() ? n_spans() : 1, nullptr);
+    for (uint32_t k = 0; k < n_spans(); ++k) {
+      if (!mheaps_[k].empty()) std::memcpy(hp + o_heap[k], mheaps_[k].data(), mheaps_[k].size());
+      dheaps[k] = dp + o_heap[k];
+    }
+    if (end > o_recs) copy(dp + o_recs, hp + o_recs, end - o_recs, SPK_COPY_H2D, s_);
+    ws_.resize(spk_workspace_bytes(&L, mode, n, 0));
+    spk_plan_t *d_plan = reinterpret_cast<spk_plan_t *>(dp);
+    check(spk_plan_ex(&L, mode, n, dp + o_recs, dheaps.data(), d_plan, ws_.data(), ws_.size(), s_),
+          "spk_plan_ex");
+    uint64_t *d_offs = mode == SPK_MODE_MESSAGES ? reinterpret_cast<uint64_t *>(dp + o_offs) : nullptr;
+    check(spk_encode(&L, mode, n, dp + o_recs, dheaps.data(), d_plan, dp + o_out, out_cap, d_offs,
+                     ws_.data(), ws_.size(), s_), "spk_encode");
+    copy(hp, dp, o_out + out_cap, SPK_COPY_D2H, s_);
+    sync(s_);
+    spk_plan_t p;
+    std::memcpy(&p, hp, sizeof p);
+    last_plan_ = p;
+    if (p.total_bytes <= out_cap) {
+      sink(reinterpret_cast<const char *>(hp + o_out), static_cast<std::size_t>(p.total_bytes));
+      return true;
+    }
+    // (a bound that did not hold: encode again into an exact buffer; the
+    // plan and workspace in the arena are still this message's)
+    buffer big(p.total_bytes);
+    check(spk_encode(&L, mode, n, dp + o_recs, dheaps.data(), d_plan, big.data(), p.total_bytes,
+                     d_offs, ws_.data(), ws_.size(), s_), "spk_encode");
+    std::vector<char> tmp(p.total_bytes);
+    copy(tmp.data(), big.data(), tmp.size(), SPK_COPY_D2H, s_);
+    sync(s_);
+    sink(tmp.data(), tmp.size());
+    return true;
+  }
+  const spk_plan_t &last_plan() const { return last_plan_; }
+
+  // decode one message of `size` bytes (VECTOR into at most cap records, or
+  // one MESSAGES record): false when the call is not small; otherwise r is
+  // the result and, when r.errc == 0, the records / heaps are in the host
+  // view buffers (view_recs_ / view_heaps_) for unmarshal().
+  bool decode_small(const char *data, std::size_t size, int mode, std::size_t cap,
+                    spk_dresult_t &r) {
+    const spk_layout &L = layout();
+    const std::vector<uint64_t> caps = detail::heap_caps_for_wire(L, size, cap);
+    // arena: [result 256][errc 256][records][heap 0]...[heap k] | [offsets 256][wire]
+    const std::size_t o_errc = 256, o_recs = 512;
+    std::size_t end = al(o_recs + cap * L.rec_stride);
+    std::vector<std::size_t> o_heap(n_spans());
+    for (uint32_t k = 0; k < n_spans(); ++k) {
+      o_heap[k] = end;
+      end = al(end + caps[k] * span_elem(k));
+    }
+    const std::size_t back = end, o_offs = end, o_wire = end + 256;
+    end = al(o_wire + size + 16);
+    if (back > kSmallBytes || size > kSmallBytes) return false;
+    arena_.resize(end);
+    pin_.resize(end);
+    uint8_t *hp = pin_.data(), *dp = static_cast<uint8_t *>(arena_.data());
+    const uint64_t o[2] = {0, size};
+    std::memcpy(hp + o_offs, o, sizeof o);
+    if (size) std::memcpy(hp + o_wire, data, size);
+    copy(dp + o_offs, hp + o_offs, o_wire + size - o_offs, SPK_COPY_H2D, s_);
+    ws_.resize(spk_workspace_bytes(&L, mode, mode == SPK_MODE_VECTOR ? cap : 1, size));
+    std::vector<void *> dheaps(n_spans() ? n_spans() : 1, nullptr);
+    for (uint32_t k = 0; k < n_spans(); ++k) dheaps[k] = dp + o_heap[k];
+    spk_dresult_t *d_res = reinterpret_cast<spk_dresult_t *>(dp);
+    int32_t *d_errc = mode == SPK_MODE_MESSAGES ? reinterpret_cast<int32_t *>(dp + o_errc) : nullptr;
+    check(spk_decode(&L, mode, dp + o_wire, size,
+                     mode == SPK_MODE_MESSAGES ? reinterpret_cast<const uint64_t *>(dp + o_offs)
+                                               : nullptr,
+                     mode == SPK_MODE_MESSAGES ? 1 : 0, dp + o_recs, cap, dheaps.data(),
+                     caps.data(), d_res, d_errc, ws_.data(), ws_.size(), s_), "spk_decode");
+    copy(hp, dp, back, SPK_COPY_D2H, s_);
+    sync(s_);
+    std::memcpy(&r, hp, sizeof r);
+    if (mode == SPK_MODE_MESSAGES) std::memcpy(&r.errc, hp + o_errc, sizeof r.errc);
+    if (r.errc) return true;
+    const std::size_t nrec = mode == SPK_MODE_VECTOR ? r.count : 1;
+    view_recs_.assign(hp + o_recs, hp + o_recs + nrec * L.rec_stride);
+    view_heaps_.resize(n_spans());
+    for (uint32_t k = 0; k < n_spans(); ++k)
+      view_heaps_[k].assign(hp + o_heap[k], hp + o_heap[k] + r.heap_used[k] * span_elem(k));
+    return true;
+  }
+
+  // the n records held in the host view buffers -> out (decode_small)
+  template <typename X = R>
+  void unmarshal(std::size_t n, X *out) {
+    const spk_layout &L = layout();
+    if constexpr (trivial && std::is_same_v<X, R>) {
+      if (n) std::memcpy(static_cast<void *>(out), view_recs_.data(), n * sizeof(R));
+    } else {
+      std::vector<const uint8_t *> hp(n_spans());
+      for (uint32_t k = 0; k < n_spans(); ++k) hp[k] = view_heaps_[k].data();
+      for (std::size_t i = 0; i < n; ++i) {
+        detail::unmarshal_state st{&L, view_recs_.data() + i * L.rec_stride, 0, 0, hp.data(), 0};
         detail::from_device(out[i], st);
       }
     }
@@ -468,6 +646,12 @@ class codec {
   buffer ws_, plan_, res_;
   std::vector<std::vector<uint8_t>> view_heaps_;
   std::vector<uint8_t> view_recs_;
+  // small-call state (encode_small / decode_small)
+  buffer arena_;
+  pinned pin_;
+  std::vector<uint8_t> mrecs_;
+  std::vector<std::vector<uint8_t>> mheaps_;
+  spk_plan_t last_plan_{};
 };
 
 // A connection's request frames in arrival order, function ids interleaved:
@@ -520,9 +704,35 @@ class frame_router {
   buffer counts_, ws_;
 };
 
+// The calling thread's own non-blocking stream for the front end's per-call
+// codecs (call_codec: serialize / deserialize of one message take host data
+// and sync before they return, so no caller work on other streams is ordered
+// against it). On the legacy null stream each copy and launch paid its
+// implicit device-wide ordering (small calls ~7 % slower).
+struct thread_stream_holder {
+  void *s = nullptr;
+  thread_stream_holder() { check(spk_stream_create(&s), "spk_stream_create"); }
+  ~thread_stream_holder() {
+    if (s) (void)spk_stream_destroy(s);
+  }
+};
+inline void *thread_stream() {
+  thread_local thread_stream_holder h;
+  return h.s;
+}
+
+// the thread's codec of R on the null stream (callers may order their own
+// null-stream work after its stream-ordered calls)
 template <typename R, uint64_t conf>
 codec<R, conf> &thread_codec() {
   thread_local codec<R, conf> c;
+  return c;
+}
+// the thread's codec of R for whole calls of the front end (staged_message,
+// decode_one_dev): its own stream, synced inside every call
+template <typename R, uint64_t conf>
+codec<R, conf> &call_codec() {
+  thread_local codec<R, conf> c(thread_stream());
   return c;
 }
 
@@ -569,21 +779,41 @@ struct staged_message {
   std::size_t len = 0;
   uint8_t hdr[4 + 1 + SPK_MAX_LITERAL + 1] = {};  // tr::empty: the whole message
 
+  std::vector<char> host;  // the message, when the small-call path made it
+  bool on_host = false;
+
   explicit staged_message(const T &t) {
     if constexpr (tr::empty) {
       const int n = spk_message_header(&empty_message_layout<remove_cvref_t<T>, conf>(), 1, hdr,
                                        sizeof hdr);
       if (n < 0) device::check(n, "spk_message_header");
       len = static_cast<std::size_t>(n);
+    } else {
+      // small messages: one H2D, plan + encode in the codec's arena, one D2H
+      auto &c = device::call_codec<R, conf>();
+      auto sink = [&](const char *p, std::size_t k) {
+        host.assign(p, p + k);
+        len = k;
+        plan = c.last_plan();
+      };
+      if constexpr (tr::vector)
+        on_host = c.encode_small(t.data(), t.size(), SPK_MODE_VECTOR, sink);
+      else
+        on_host = c.encode_small(&t, 1, SPK_MODE_MESSAGES, sink);
+      if (!on_host) stage_on_device(t);
+    }
+  }
+  void stage_on_device(const T &t) {
+    if constexpr (tr::empty) {
     } else if constexpr (tr::vector) {
-      auto &c = device::thread_codec<R, conf>();
+      auto &c = device::call_codec<R, conf>();
       auto b = c.upload(t.data(), t.size());
       plan = c.plan(b, SPK_MODE_VECTOR);
       len = plan.total_bytes;
       out.resize(len);
       c.encode(b, SPK_MODE_VECTOR, out.data(), out.size());
     } else {
-      auto &c = device::thread_codec<R, conf>();
+      auto &c = device::call_codec<R, conf>();
       auto b = c.upload(&t, 1);  // (boxed<M>: t is its one member)
       plan = c.plan(b, SPK_MODE_MESSAGES);
       len = plan.total_bytes;
@@ -595,8 +825,10 @@ struct staged_message {
   void copy_to(void *dst) {
     if constexpr (tr::empty) {
       std::memcpy(dst, hdr, len);
+    } else if (on_host) {
+      if (len) std::memcpy(dst, host.data(), len);
     } else {
-      auto &c = device::thread_codec<R, conf>();
+      auto &c = device::call_codec<R, conf>();
       device::copy(dst, out.data(), len, SPK_COPY_D2H, c.stream());
       device::sync(c.stream());
     }
@@ -642,10 +874,35 @@ template <uint64_t conf, typename T>
 err_code decode_one_dev(T &t, const char *data, std::size_t size, std::size_t &consume_len) {
   using tr = msg_traits<T>;
   using R = typename tr::rec;
-  auto &c = device::thread_codec<R, conf>();
+  auto &c = device::call_codec<R, conf>();
+  std::size_t cap = tr::vector ? size / c.min_record_wire() + 1 : 1;
+  // small messages: one H2D, the decode in the codec's arena, one D2H
+  for (spk_dresult_t r;;) {
+    if (!c.decode_small(data, size, tr::vector ? SPK_MODE_VECTOR : SPK_MODE_MESSAGES, cap, r))
+      break;  // not small: the batch path below
+    if (r.errc == SPK_ERRC_CAPACITY) {
+      cap = cap * 2 + 1;
+      continue;
+    }
+    if (r.errc) return static_cast<errc>(r.errc);
+    if constexpr (tr::vector) {
+      T out(r.count);
+      c.unmarshal(r.count, out.data());
+      t = std::move(out);
+    } else {
+      c.unmarshal(1, &t);  // (boxed<M>: t is its one member)
+    }
+    if constexpr (has_views<T>()) {  // views alias `data`, as the reference's do
+      mem_cursor mc{data, size};
+      header_info h;
+      (void)walk_header(mc, tr::vector ? c.layout().fmt_vector : c.layout().fmt_one, h);
+      rebase_views(t, mc, h.w);
+    }
+    consume_len = r.consumed;
+    return {};
+  }
   device::buffer wire(size + 16);
   device::copy(wire.data(), data, size, SPK_COPY_H2D, c.stream());
-  std::size_t cap = tr::vector ? size / c.min_record_wire() + 1 : 1;
   for (;;) {
     // the capacities bound every decodable message (min_record_wire is a
     // lower bound on a record's wire bytes, fast-varint groups counted as

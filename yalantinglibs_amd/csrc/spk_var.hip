@@ -1420,7 +1420,12 @@ __device__ __forceinline__ bool vi_seg_rd(const WalkProg &P, uint32_t k, const R
 }
 
 // the nested walker (NS = -2, defined with the tile decoder below)
-template <bool SIMPLE, typename Rd>
+// walker level of a nested tile instantiation: NS = -2 the interpreter (0),
+// -3 the walk program (1), -4 the walk program with optional / compatible
+// groups of one SPAN (2, WP_OSPAN; an instantiation of its own so that the
+// -3 kernels carry none of its code: Monster's K1 / K4 lost ~5 % to it)
+constexpr int nt_level(int ns) { return ns == -3 ? 1 : ns == -4 ? 2 : 0; }
+template <int SIMPLE, typename Rd>
 __device__ uint64_t nt_len(const Rd &rd, uint64_t len, uint64_t pos, uint64_t *cnt,
                            uint64_t reach, uint32_t maxel);
 // a bounded nested walk gave up (its reach or element limit): length unknown
@@ -1474,7 +1479,7 @@ __device__ __forceinline__ uint64_t wlen_rd(const WalkProg &P, const Rd &rd, uin
                                             uint64_t pos, uint32_t w, uint64_t *cnt = nullptr,
                                             uint64_t reach = 0, const uint64_t *scap = nullptr,
                                             bool tight = false) {
-  if constexpr (NS <= -2) return nt_len<NS == -3>(rd, len, pos, cnt, reach, ~0u);
+  if constexpr (NS <= -2) return nt_len<nt_level(NS)>(rd, len, pos, cnt, reach, ~0u);
   uint64_t p = pos + P.skip[0];
   const uint32_t ns = NS > 0 ? (uint32_t)NS : P.ns;
   if (NS < 0 && !vi_seg_rd(P, 0, rd, len, p)) return 0;
@@ -1875,13 +1880,9 @@ constexpr uint32_t WP_SPAN = 1, WP_OPT = 2, WP_ARR = 3, WP_END = 4;
 // error inside the group is dropped with the reader where it stopped
 // (unpacker.hpp:1251-1277) -- h / arg are the SPAN's heap and element size
 constexpr uint32_t WP_OSPAN = 5;
-// SPK_WP_OSPAN=1: the walk program takes optional / compatible groups of one
-// SPAN (late round 5, same-box A/B: cmpg 8.04 -> 6.0 ms per step, but cm 11.97
-// -> 12.45 ms: the NS = -3 kernels' extra code costs Monster's K1 / K4 ~5 %;
-// off until it gets an instantiation of its own)
-#ifndef SPK_WP_OSPAN
-#define SPK_WP_OSPAN 0
-#endif
+// (late round 5 measured it inside the NS = -3 kernels: cmpg 8.04 -> 6.0 ms
+// per step, but Monster's K1 / K4 ~5 % slower for the extra code; round 6:
+// layouts whose walk program holds a WP_OSPAN run NS = -4 kernels of their own)
 static_assert(sizeof(NTLayout) % 16 == 0, "NTLayout staged as 16-B words");
 static_assert(SPK_MAX_DEPTH == 4, "the walker's element stack has 4 register frames");
 
@@ -2268,7 +2269,7 @@ __device__ int32_t nt_read(const NTLayout &N, const Rd &rd, uint64_t &pos, uint6
 // bounded walk would need bytes past lim); heap use into the lane's LDS
 // counters. Exact for the walk's outcome: these layouts have no group that
 // could drop an error.
-template <typename Rd>
+template <bool OSPAN, typename Rd>
 __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint64_t lim64,
                             bool bounded, uint32_t maxel) {
   // a check that fails on a bounded walk's limit: unknown (the full wire may
@@ -2300,8 +2301,7 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
       }
       continue;
     }
-#if SPK_WP_OSPAN
-    if (op == WP_OSPAN) {
+    if (OSPAN && op == WP_OSPAN) {
       if (lim - p < 1) return bad;  // (the has byte itself: the record fails)
       const uint32_t b = rd.byte(p);
       if (bounded && b > 1) return bad;  // (nt_read: a has_value byte above 1)
@@ -2325,7 +2325,6 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
       ++pc;
       continue;
     }
-#endif
     const bool opt = op == WP_OPT;
     const uint32_t cw = opt ? 1u : w;
     if (lim - p < cw) return bad;
@@ -2362,7 +2361,7 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
 // wlen_rd for NS = -2: the record's wire length (0: the path fails here) and
 // its heap use per heap; reach > 0 bounds a speculative walk (past it: longer
 // than a plausible record, kPlaus + 1)
-template <bool SIMPLE, typename Rd>
+template <int SIMPLE, typename Rd>
 __device__ uint64_t nt_len(const Rd &rd, uint64_t len, uint64_t pos, uint64_t *cnt,
                            uint64_t reach, uint32_t maxel) {
   const NTLayout &N = nt_lds();
@@ -2373,8 +2372,8 @@ __device__ uint64_t nt_len(const Rd &rd, uint64_t len, uint64_t pos, uint64_t *c
     if (q < nh) U[64 * q] = 0;
   const uint64_t lim = reach && reach < len - pos ? pos + reach : len;
   uint64_t p = pos;
-  if constexpr (SIMPLE) {
-    const uint64_t l = nt_walk(N, rd, pos, lim, lim < len, maxel);
+  if constexpr (SIMPLE != 0) {
+    const uint64_t l = nt_walk<SIMPLE == 2>(N, rd, pos, lim, lim < len, maxel);
     if (l == kLenLimit) return kLenLimit;
     p += l;
   } else {
@@ -2396,7 +2395,7 @@ __device__ __forceinline__ uint64_t wlen_spec(const WalkProg &P, const Rd &rd, u
                                               uint64_t pos, uint32_t w, uint64_t *cnt,
                                               const uint64_t *scap, bool tight) {
   if constexpr (NS <= -2) {
-    const uint64_t l = nt_len<NS == -3>(rd, len, pos, cnt, (uint64_t)kPlaus + 1, kNTSpecElems);
+    const uint64_t l = nt_len<nt_level(NS)>(rd, len, pos, cnt, (uint64_t)kPlaus + 1, kNTSpecElems);
     return l == kLenLimit ? (uint64_t)kPlaus + 1 : l;  // too long for a plausible start
   }
   return wlen_rd<NS, Rd, (SPK_SCAP & 1) != 0>(P, rd, len, pos, w, cnt, 0, scap, tight);
@@ -2422,7 +2421,7 @@ __device__ __forceinline__ void nt_put_payload(const Rd &rd, uint8_t *hp, uint64
 // Emission of a record the walk program accepted (COPY / SPAN / OPTION /
 // ARRAY layouts): the interpreter without error paths (the walk checked
 // every read), frames below the top one in LDS
-template <typename Rd>
+template <bool OSPAN, typename Rd>
 __device__ uint64_t nt_emit_simple(const NTLayout &N, const Rd &rd, uint64_t pos,
                                    uint64_t len, uint8_t *rec, const BigQ &bq) {
   uint32_t *const U = nt_used();
@@ -2460,8 +2459,7 @@ __device__ uint64_t nt_emit_simple(const NTLayout &N, const Rd &rd, uint64_t pos
       ++i;
       continue;
     }
-#if SPK_WP_OSPAN
-    if (op.kind == SPK_OP_OPTGROUP) {  // WP_OSPAN: [has] [count][payload]
+    if (OSPAN && op.kind == SPK_OP_OPTGROUP) {  // WP_OSPAN: [has] [count][payload]
       const uint32_t b = rd.byte(pos++);
       *reinterpret_cast<uint32_t *>(r + op.rec_off) = b ? 1u : 0u;
       if (b) {
@@ -2489,7 +2487,6 @@ __device__ uint64_t nt_emit_simple(const NTLayout &N, const Rd &rd, uint64_t pos
       i = N.end[i] + 1u;
       continue;
     }
-#endif
     const uint32_t hk = N.heap[i];
     const bool opt = op.kind == SPK_OP_OPTION;
     const uint64_t c = opt ? (uint64_t)(rd.byte(pos) != 0) : rd(pos);
@@ -2539,12 +2536,12 @@ __device__ uint64_t nt_emit_simple(const NTLayout &N, const Rd &rd, uint64_t pos
 
 // emission with the lane's heap slots already in its LDS counters; the
 // record's end
-template <bool SIMPLE, typename Rd>
+template <int SIMPLE, typename Rd>
 __device__ __forceinline__ uint64_t nt_emit_here(const Rd &rd, uint64_t pos, uint64_t len,
                                                  uint8_t *rec, const BigQ &bq) {
   const NTLayout &N = nt_lds();
-  if constexpr (SIMPLE) {
-    return nt_emit_simple(N, rd, pos, len, rec, bq);
+  if constexpr (SIMPLE != 0) {
+    return nt_emit_simple<SIMPLE == 2>(N, rd, pos, len, rec, bq);
   } else {
     nt_read<true>(N, rd, pos, len, false, rec, &bq, false);
     return pos;
@@ -2552,7 +2549,7 @@ __device__ __forceinline__ uint64_t nt_emit_here(const Rd &rd, uint64_t pos, uin
 }
 
 // emission of the record at pos with heap bases off[]
-template <bool SIMPLE>
+template <int SIMPLE>
 __device__ __forceinline__ void nt_emit(const WinReader &rd, uint64_t pos, uint64_t len,
                                         uint8_t *rec, const uint64_t *off, const BigQ &bq) {
   const NTLayout &N = nt_lds();
@@ -2560,8 +2557,8 @@ __device__ __forceinline__ void nt_emit(const WinReader &rd, uint64_t pos, uint6
 #pragma unroll
   for (uint32_t q = 0; q < kVS; ++q)
     if (q < N.n_heaps) U[64 * q] = (uint32_t)off[q];
-  if constexpr (SIMPLE)
-    nt_emit_simple(N, rd, pos, len, rec, bq);
+  if constexpr (SIMPLE != 0)
+    nt_emit_simple<SIMPLE == 2>(N, rd, pos, len, rec, bq);
   else
     nt_read<true>(N, rd, pos, len, false, rec, &bq, false);
 }
@@ -4239,7 +4236,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
       for (uint32_t r = 0; r < cnt && idx < n; ++r, ++idx) {
         const uint64_t x0 = x;
         if (idx < a.rec_cap && fits_all) {
-          x = nt_emit_here<NS == -3>(R, x, len, recs + idx * a.L.stride, bq);
+          x = nt_emit_here<nt_level(NS)>(R, x, len, recs + idx * a.L.stride, bq);
         } else {
           // near a capacity: this record's heap use first, written only if it fits
           uint64_t b[kVS], rc[kVS];
@@ -4249,7 +4246,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
           QFOR(q) fit = fit && b[q] + rc[q] <= a.heap_cap[q];
           QFOR(q) U[64 * q] = (uint32_t)b[q];
           if (fit)
-            nt_emit_here<NS == -3>(R, x0, len, recs + idx * a.L.stride, bq);
+            nt_emit_here<nt_level(NS)>(R, x0, len, recs + idx * a.L.stride, bq);
           else
             QFOR(q) U[64 * q] = (uint32_t)(b[q] + rc[q]);
         }
@@ -4317,7 +4314,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
       bool dfd = false;
       if (act && gr < a.rec_cap && fits && !(dbg & 64)) {
         if constexpr (NS <= -2)
-          nt_emit<NS == -3>(rd, pos, len, recs + gr * a.L.stride, off, bq);
+          nt_emit<nt_level(NS)>(rd, pos, len, recs + gr * a.L.stride, off, bq);
         else if constexpr (!DEFER || std::decay_t<decltype(R)>::kLO)
           emit_record_rd(a.L, R, pos, w, recs + gr * a.L.stride, a.heaps, off, len, bq, dbg);
         else
@@ -4637,9 +4634,9 @@ static hipError_t launch_vec_tiles_ns(const DecArgs &a, const WalkProg &P, const
   return hipGetLastError();
 }
 
-static bool nested_args(const spk_layout *L, uint64_t wire_len, uint64_t rec_cap,
-                        void *const *d_heaps, const uint64_t *heap_caps, uint8_t *ws,
-                        hipStream_t s, DecArgs &a, WalkProg &P);
+static int nested_args(const spk_layout *L, uint64_t wire_len, uint64_t rec_cap,
+                       void *const *d_heaps, const uint64_t *heap_caps, uint8_t *ws,
+                       hipStream_t s, DecArgs &a, WalkProg &P);
 hipError_t launch_var_shard(const spk_layout *L, int phase, const void *d_wire, uint64_t wire_len,
                             uint64_t tile_lo, uint64_t tile_hi, uint64_t entry,
                             spk_shard_t *d_summary, uint64_t first, uint32_t last, void *d_recs,
@@ -4647,10 +4644,11 @@ hipError_t launch_var_shard(const spk_layout *L, int phase, const void *d_wire, 
                             spk_dresult_t *d_res, void *d_ws, hipStream_t s) {
   DecArgs a = {};
   WalkProg P;
-  bool nested = false, simple = false;
+  bool nested = false;
+  int lvl = 0;
   if (layout_nested(L)) {  // nested layouts: the interpreter walker (var_nested_tile_ok)
     nested = true;
-    simple = nested_args(L, wire_len, rec_cap, d_heaps, heap_caps, (uint8_t *)d_ws, s, a, P);
+    lvl = nested_args(L, wire_len, rec_cap, d_heaps, heap_caps, (uint8_t *)d_ws, s, a, P);
   } else {
     a.L = make_klayout(L);
     a.fmt = L->fmt_vector;
@@ -4673,7 +4671,8 @@ hipError_t launch_var_shard(const spk_layout *L, int phase, const void *d_wire, 
   const int ph = phase == 0 ? kTilesIndex : kTilesEmit;
   const uint8_t *wire = (const uint8_t *)d_wire;
   uint8_t *ws = (uint8_t *)d_ws, *r = (uint8_t *)d_recs;
-  if (nested && simple) return launch_vec_tiles_ns<-3>(a, P, L, wire, ws, d_res, r, s, ph, sc);
+  if (nested && lvl == 2) return launch_vec_tiles_ns<-4>(a, P, L, wire, ws, d_res, r, s, ph, sc);
+  if (nested && lvl == 1) return launch_vec_tiles_ns<-3>(a, P, L, wire, ws, d_res, r, s, ph, sc);
   if (nested) return launch_vec_tiles_ns<-2>(a, P, L, wire, ws, d_res, r, s, ph, sc);
   if (P.nv) return launch_vec_tiles_ns<-1>(a, P, L, wire, ws, d_res, r, s, ph, sc);
   if (P.ns == 1) return launch_vec_tiles_ns<1>(a, P, L, wire, ws, d_res, r, s, ph, sc);
@@ -4715,7 +4714,7 @@ static NTLayout make_ntlayout(const NLayout &N, void *const *heaps) {
     } else if (op.kind == SPK_OP_ARRAY && d < SPK_MAX_DEPTH) {
       open[d++] = n;
       x = WP_ARR | ((uint32_t)N.heap[i] << 3);
-    } else if (SPK_WP_OSPAN && op.kind == SPK_OP_OPTGROUP && op.size == 1 && i + 2 < N.n_ops &&
+    } else if (op.kind == SPK_OP_OPTGROUP && op.size == 1 && i + 2 < N.n_ops &&
                N.ops[i + 1].kind == SPK_OP_SPAN && N.ops[i + 2].kind == SPK_OP_END &&
                N.end[i] == i + 2 && N.ops[i + 1].size < (1u << 24)) {
       x = WP_OSPAN | ((uint32_t)N.heap[i + 1] << 3) |
@@ -4791,9 +4790,9 @@ size_t var_nested_tile_ws_bytes(const spk_layout *L, uint64_t wire_len) {
 
 // decode arguments of a nested layout on the tile decoder; its walker layout
 // goes into the workspace. Returns whether the walk program applies (NS = -3).
-static bool nested_args(const spk_layout *L, uint64_t wire_len, uint64_t rec_cap,
-                        void *const *d_heaps, const uint64_t *heap_caps, uint8_t *ws,
-                        hipStream_t s, DecArgs &a, WalkProg &P) {
+static int nested_args(const spk_layout *L, uint64_t wire_len, uint64_t rec_cap,
+                       void *const *d_heaps, const uint64_t *heap_caps, uint8_t *ws,
+                       hipStream_t s, DecArgs &a, WalkProg &P) {
   const NLayout N = make_nlayout(L);
   a = DecArgs{};
   a.L.stride = N.stride;
@@ -4812,7 +4811,10 @@ static bool nested_args(const spk_layout *L, uint64_t wire_len, uint64_t rec_cap
   a.nl = ws + f.nl;
   const NTLayout t = make_ntlayout(N, d_heaps);
   SPK_LAUNCH(nt_put, dim3(1), dim3(256), 0, s, t, ws + f.nl);
-  return t.wp_n != 0;
+  if (!t.wp_n) return 0;  // the interpreter (NS = -2)
+  for (uint32_t k = 0; k < t.wp_n; ++k)
+    if ((t.wp[k].x & 7u) == WP_OSPAN) return 2;  // NS = -4
+  return 1;                                      // NS = -3
 }
 
 hipError_t launch_var_nested_decode(const spk_layout *L, const void *d_wire, uint64_t wire_len,
@@ -4822,12 +4824,13 @@ hipError_t launch_var_nested_decode(const spk_layout *L, const void *d_wire, uin
   DecArgs a;
   WalkProg P;
   uint8_t *ws = (uint8_t *)d_ws;
-  const bool simple = nested_args(L, wire_len, rec_cap, d_heaps, heap_caps, ws, s, a, P);
+  const int lvl = nested_args(L, wire_len, rec_cap, d_heaps, heap_caps, ws, s, a, P);
   a.body_w = body_w;
   a.body_n = body_n;
-  // NS = -3: every walk runs the walk program; -2: the interpreter
+  // NS = -3 / -4: every walk runs the walk program; -2: the interpreter
   const uint8_t *wire = (const uint8_t *)d_wire;
-  if (simple) return launch_vec_tiles_ns<-3>(a, P, L, wire, ws, d_res, (uint8_t *)d_recs, s);
+  if (lvl == 2) return launch_vec_tiles_ns<-4>(a, P, L, wire, ws, d_res, (uint8_t *)d_recs, s);
+  if (lvl == 1) return launch_vec_tiles_ns<-3>(a, P, L, wire, ws, d_res, (uint8_t *)d_recs, s);
   return launch_vec_tiles_ns<-2>(a, P, L, wire, ws, d_res, (uint8_t *)d_recs, s);
 }
 
@@ -4916,9 +4919,10 @@ static hipError_t tiles_decode(const spk_layout *L, const void *d_wire, uint64_t
   const uint8_t *wire = (const uint8_t *)d_wire;
   uint8_t *r = (uint8_t *)d_recs;
   if (layout_nested(L)) {
-    const bool simple = nested_args(L, wire_len, rec_cap, d_heaps, heap_caps, ws, s, a, P);
+    const int lvl = nested_args(L, wire_len, rec_cap, d_heaps, heap_caps, ws, s, a, P);
     a.chain = chain;
-    if (simple) return launch_vec_tiles_ns<-3>(a, P, L, wire, ws, d_res, r, s);
+    if (lvl == 2) return launch_vec_tiles_ns<-4>(a, P, L, wire, ws, d_res, r, s);
+    if (lvl == 1) return launch_vec_tiles_ns<-3>(a, P, L, wire, ws, d_res, r, s);
     return launch_vec_tiles_ns<-2>(a, P, L, wire, ws, d_res, r, s);
   }
   a.L = make_klayout(L);
