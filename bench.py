@@ -73,7 +73,7 @@ EXTRA = ["c2b", "c3", "c3r", "c3l", "c4", "c5", "cv", "cm", "cvm", "cmpg"]  # ti
 SEEDS = {"rec64": 0x5EED0002, "recs": 0x5EED0003, "outer": 0x5EED0004, "var": 0x5EED000C,
          "monster": 0x5EED001E, "valreq": 0x5EED001B, "cmpg": 0x5EED0021}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PROFILE_ROUND = "r05"
+PROFILE_ROUND = "r06"
 
 C5_TYPES = [  # (case, share of messages, param, rpc function name) — coro_rpc bench shapes
     ("rpcrect", 1, 0, "echo_rect"),          # rect{point p1, p2}   (api/Rect.h)

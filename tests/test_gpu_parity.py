@@ -1161,3 +1161,35 @@ def test_nonzero_has_value_bytes(n):
         assert res.heap_used[k] == eres.heap_used[k]
         nb = int(eres.heap_used[k]) * cd.L.dev.spans[k].elem.size
         assert back.heaps[k][:nb].cpu().numpy().tobytes() == eheaps[k][:nb].tobytes()
+
+
+@pytest.mark.parametrize("case,n,param,world", [("recs", 60000, 48, 4), ("outer", 30000, 16, 3),
+                                                ("monster", 20000, 20, 4)])
+@pytest.mark.parametrize("tail", ["random", "copy"])
+def test_sharded_decode_trailing_bytes(case, n, param, world, tail):
+    """one message followed by 100 KB of other bytes, decoded
+    by `world` simulated ranks: the reference decodes its count of records and
+    reports consume_len = the message's length (struct_pack.hpp:343-357); the
+    bytes after it need not parse. The ranks' records are the message's."""
+    from yalantinglibs_amd import layout as LY
+    from yalantinglibs_amd import parallel as PAR
+    cds = [SP.Codec(LY.case_layout(case)) for _ in range(world)]
+    _, recs, heaps = synth.make_batch(case, n, 0x7A12 + n, param)
+    m, _, _ = H.oracle_encode(cds[0].L, C.SPK_MODE_VECTOR, recs, heaps)
+    rng = np.random.default_rng(n)
+    tl = 100000
+    t = (rng.integers(0, 256, tl, dtype=np.uint8).tobytes() if tail == "random" else
+         (m * (tl // len(m) + 1))[:tl])
+    out, rounds = PAR.shard_decode([PAR.DeviceShardBackend(c) for c in cds], wire_dev(m + t),
+                                   world, lambda mine: mine)
+    total = 0
+    for (b, first, res), cd in zip(out, cds):
+        assert res.errc == 0, (res.errc, first)
+        assert first == total
+        total += b.n
+    assert total == n
+    got = np.concatenate([b.recs[:b.n].cpu().numpy().reshape(-1) for b, _, _ in out if b.n])
+    if case == "recs":  # flat: the records equal the input's (heap offsets rank-local)
+        exp = np.ascontiguousarray(recs).view(np.uint8).reshape(n, -1)
+        g = got.reshape(n, -1)
+        assert np.array_equal(g[:, :8], exp[:, :8]) and np.array_equal(g[:, 16:], exp[:, 16:])

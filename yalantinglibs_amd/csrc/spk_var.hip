@@ -4437,9 +4437,12 @@ __device__ void tile_finish(const DecArgs &a, const uint8_t *__restrict__ wire,
   const uint64_t total = c->n ? (uint64_t)fc->total : 0;
   // an unresolved tile is an internal error unless it starts at or past the
   // end of record n-1: the bytes after a message need not parse as records
-  // (the reference stops at its count, struct_pack.hpp:343-357)
+  // (the reference stops at its count, struct_pack.hpp:343-357). A shard
+  // knows that end only in its emit of the range that holds it (fc->last,
+  // c->n = the records from the range's first on, end_pos from K4); any
+  // other range's unresolved tile is an error.
   if (fc->unresolved &&
-      (fc->range || !c->n || total < c->n ||
+      ((fc->range && !fc->last) || !c->n || total < c->n ||
        c->p0 + fc->unres_tile * (uint64_t)kTileBytes < (uint64_t)fc->end_pos)) {
     r.errc = SPK_ERRC_INTERNAL;
     *res = r;
