@@ -745,7 +745,11 @@ __device__ __forceinline__ void win_frame(const VarArgs &a, const Win &W, uint64
   }
 }
 
-constexpr uint32_t kEncWin = 20 * 1024;  // LDS assembly window per block
+// LDS assembly window per block. (Round 6: the block's records staged in LDS
+// beside a 16 KiB window: C3 0.321 -> 0.311 ms, but C4's 19 KiB blocks then
+// took two window passes, 0.373 -> 0.477 ms; with the 20 KiB window the LDS
+// leaves one block per SIMD less. Not kept.)
+constexpr uint32_t kEncWin = 20 * 1024;
 
 // Write pass: records r0 + j*kThreads + tid (consecutive lanes on consecutive
 // records), byte offsets from a block scan per round on top of the block's
@@ -787,6 +791,8 @@ __global__ __launch_bounds__(kThreads, 5) void var_encode_write(
   }
   if (a.mode == SPK_MODE_VECTOR && blockIdx.x == 0 && ysub == 0)
     for (uint32_t i = threadIdx.x; i < hdr_vec; i += blockDim.x) out[i] = ws[kWsHdrVec + i];
+  const uint8_t *rbase = recs + r0 * a.L.stride;
+#define SPK_REC(i) (rbase + ((i) - r0) * a.L.stride)
   uint64_t pj[kIPT], szj[kIPT];
   uint32_t wj[kIPT];
   uint64_t g = g0;
@@ -796,7 +802,7 @@ __global__ __launch_bounds__(kThreads, 5) void var_encode_write(
     uint32_t w = w_vec;
     if (i < N) {
       uint64_t var, maxc;
-      rec_sizes(a.L, recs + i * a.L.stride, var, maxc);
+      rec_sizes(a.L, SPK_REC(i), var, maxc);
       if (a.mode == SPK_MODE_VECTOR) {
         sz = var + (uint64_t)a.L.n_cont * w_vec;
       } else {
@@ -825,7 +831,7 @@ __global__ __launch_bounds__(kThreads, 5) void var_encode_write(
     const uint64_t i = r0 + (uint64_t)j * kThreads + threadIdx.x;
     uint32_t nbig = 0;
     if (i < N) {
-      const uint8_t *rec = recs + i * a.L.stride;
+      const uint8_t *rec = SPK_REC(i);
       for (uint32_t o = 0; o < a.L.n_ops; ++o)
         if ((a.L.ops[o].kind == SPK_OP_SPAN || a.L.ops[o].kind == SPK_OP_OPTION) &&
             op_rec_count(a.L.ops[o], rec) * a.L.ops[o].size >= kBigBytes)
@@ -835,7 +841,7 @@ __global__ __launch_bounds__(kThreads, 5) void var_encode_write(
     uint64_t slot = nbig_tot + block_excl_scan(nbig, &round_tot, sh);
     nbig_tot += round_tot;
     if (nbig && slot + nbig <= kBigMax) {
-      const uint8_t *rec = recs + i * a.L.stride;
+      const uint8_t *rec = SPK_REC(i);
       uint64_t q = pj[j];
       if (a.mode == SPK_MODE_MESSAGES)
         q += a.fpre + ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + wlog(wj[j])];
@@ -888,7 +894,7 @@ __global__ __launch_bounds__(kThreads, 5) void var_encode_write(
             win_put(D, q, ws + kWsHdrMsg + sl * kWsHdrSlot, hl);
             q += hl;
           }
-          win_record(a, recs + i * a.L.stride, wj[j], q, D, skip[j]);
+          win_record(a, SPK_REC(i), wj[j], q, D, skip[j]);
         }
       }
       __syncthreads();  // the payload list
@@ -917,7 +923,7 @@ __global__ __launch_bounds__(kThreads, 5) void var_encode_write(
         win_put<true>(W, q, ws + kWsHdrMsg + sl * kWsHdrSlot, hl);
         q += hl;
       }
-      win_record<true>(a, recs + i * a.L.stride, wj[j], q, W, skip[j]);
+      win_record<true>(a, SPK_REC(i), wj[j], q, W, skip[j]);
     }
     // listed payloads are in output order: fill the window slots they cover
     while (k0 < nbig_tot && big[k0].dst + big[k0].n <= W.lo) ++k0;
@@ -937,6 +943,7 @@ __global__ __launch_bounds__(kThreads, 5) void var_encode_write(
     __syncthreads();
   }
 }
+#undef SPK_REC
 
 // ===========================================================================
 // DECODE — shared record walker over the wire
@@ -2867,7 +2874,7 @@ __device__ __forceinline__ TileView win_view(const v4u_t *win, const uint8_t *wi
   tv.wend = wend;
   return tv;
 }
-template <uint32_t NV>
+template <uint32_t NV, bool NT = false>
 __device__ __forceinline__ TileView stage_win(v4u_t *win, const uint8_t *wire, uint64_t len,
                                               uint64_t ts, uint32_t w, uint32_t lane) {
   if (ts + NV * 16 <= len) {
@@ -2879,7 +2886,10 @@ __device__ __forceinline__ TileView stage_win(v4u_t *win, const uint8_t *wire, u
 #pragma unroll
     for (uint32_t k = 0; k < kPer; ++k) {
       const uint32_t v = lane + 64 * k;
-      if (NV % 64 == 0 || v < NV) val[k] = *reinterpret_cast<const v4u_una *>(wire + ts + 16ull * v);
+      if (NV % 64 == 0 || v < NV) {
+        const v4u_una *q = reinterpret_cast<const v4u_una *>(wire + ts + 16ull * v);
+        val[k] = NT ? __builtin_nontemporal_load(q) : *q;
+      }
     }
 #pragma unroll
     for (uint32_t k = 0; k < kPer; ++k) {
@@ -4112,6 +4122,10 @@ constexpr uint16_t kTabFar = 0xFFFFu;  // a table end past the window
 // the caller's records average kWaveCopy wire bytes or more (wire_len /
 // rec_cap): its registers cost K4 a wave per SIMD (C3 K4 0.304 -> 0.326 ms),
 // which messages of short records need not pay (c3l K4 5.3 -> 2.2 ms).
+#ifndef SPK_K4_NT  // K4: bit 0 non-temporal window loads (the wire's last read; round-6
+                   // A/B on C3 / C4 / cv: within noise, off)
+#define SPK_K4_NT 0
+#endif
 #ifndef SPK_K4_REV  // K4 takes the tiles last to first
 #define SPK_K4_REV 1  // (reversed: K4 first reads the tiles K1 read last; c3 K4 0.306 -> 0.298 ms, c4 0.483 -> 0.476, cv 1.136 -> 1.113, same-box A/B)
 #endif
@@ -4171,7 +4185,7 @@ __global__ __launch_bounds__(64 * kDecWaves) void vec_tile_emit(DecArgs a, WalkP
     }
   }
   nt_prologue<NS>(a, lane);
-  const TileView tv = stage_win<kEmitVec>(win_s[wv], wire, len, wb, w, lane);
+  const TileView tv = stage_win<kEmitVec, (SPK_K4_NT & 1) != 0>(win_s[wv], wire, len, wb, w, lane);
   const WinReader &rd = tv.rd;
   if (tbase >= n || sel < 0) return;
   // the selected alternative: entry, records, sums (words of lane sel * kAltWords + k)
