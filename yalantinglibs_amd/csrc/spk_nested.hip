@@ -75,6 +75,18 @@ __device__ __forceinline__ uint32_t n_vi_len(uint64_t v) {
 typedef uint64_t n_u64_una __attribute__((aligned(1)));
 typedef uint32_t n_u32_una __attribute__((aligned(1)));
 typedef v4u_t n_v4u_una __attribute__((aligned(1)));
+
+// an encode window's 16-B chunk to the output (write-once streams):
+// SPK_FLUSH_NT = 1 stores it non-temporally
+#ifndef SPK_FLUSH_NT
+#define SPK_FLUSH_NT 1  // (encode windows: C3 0.323 -> 0.318 ms, C4 0.375 -> 0.371, cm 2.865 -> 2.823, cvm 0.481 -> 0.473)
+#endif
+__device__ __forceinline__ void flush16(uint8_t *dst, const v4u_t &v) {
+  if (SPK_FLUSH_NT)
+    __builtin_nontemporal_store(v, reinterpret_cast<v4u_t *>(dst));
+  else
+    *reinterpret_cast<v4u_t *>(dst) = v;
+}
 __device__ __forceinline__ void n_copy(uint8_t *d, const uint8_t *s, uint64_t n) {
   uint64_t i = 0;
   for (; i + 16 <= n; i += 16)
@@ -1543,7 +1555,7 @@ __global__ __launch_bounds__(256) void nest_write_win(NEnc e, const uint8_t *__r
       const uint64_t lo = c > g0 ? c : g0;
       const uint64_t hi = c + 16 < whi ? c + 16 : whi;
       if (lo == c && hi == c + 16)
-        *reinterpret_cast<v4u_t *>(out + c) = *reinterpret_cast<const v4u_t *>(lds + (c - W.lo));
+        flush16(out + c, *reinterpret_cast<const v4u_t *>(lds + (c - W.lo)));
       else
         for (uint64_t x = lo; x < hi; ++x) out[x] = lds[x - W.lo];
     }
@@ -1612,7 +1624,7 @@ __global__ __launch_bounds__(256) void nest_write_mwin(NEnc e, const uint8_t *__
       const uint64_t lo = c > g0 ? c : g0;
       const uint64_t hi = c + 16 < whi ? c + 16 : whi;
       if (lo == c && hi == c + 16)
-        *reinterpret_cast<v4u_t *>(out + c) = *reinterpret_cast<const v4u_t *>(lds + (c - W.lo));
+        flush16(out + c, *reinterpret_cast<const v4u_t *>(lds + (c - W.lo)));
       else
         for (uint64_t x = lo; x < hi; ++x) out[x] = lds[x - W.lo];
     }

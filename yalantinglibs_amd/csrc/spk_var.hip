@@ -146,6 +146,18 @@ typedef uint32_t u32_unaligned __attribute__((aligned(1)));
 typedef uint64_t u64_unaligned __attribute__((aligned(1)));
 typedef uint32_t v4u_t __attribute__((ext_vector_type(4)));
 typedef v4u_t v4u_una __attribute__((aligned(1)));
+
+// an encode window's 16-B chunk to the output (write-once streams):
+// SPK_FLUSH_NT = 1 stores it non-temporally
+#ifndef SPK_FLUSH_NT
+#define SPK_FLUSH_NT 1  // (encode windows: C3 0.323 -> 0.318 ms, C4 0.375 -> 0.371, cm 2.865 -> 2.823, cvm 0.481 -> 0.473)
+#endif
+__device__ __forceinline__ void flush16(uint8_t *dst, const v4u_t &v) {
+  if (SPK_FLUSH_NT)
+    __builtin_nontemporal_store(v, reinterpret_cast<v4u_t *>(dst));
+  else
+    *reinterpret_cast<v4u_t *>(dst) = v;
+}
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 // byte-aligned LDS words: gfx950 reads (and writes) them with one ds_read_b32 / b64 / b128
@@ -674,7 +686,13 @@ __device__ __forceinline__ void win_put_coop(const Win &W, uint64_t pos, const u
         *reinterpret_cast<const v4u_una *>(src + (c - pos));
 }
 
-constexpr int kCoopU = 8;       // loads in flight per lane in wave_copy_all
+#ifndef SPK_COOP_NT  // wave_copy_all: bit 0 non-temporal loads, bit 1 stores
+#define SPK_COOP_NT 3  // (C5 1.667 -> 1.559 ms per step, c3l encode 1.707 -> 1.532 ms; same-box A/B)
+#endif
+#ifndef SPK_COOP_U
+#define SPK_COOP_U 8
+#endif
+constexpr int kCoopU = SPK_COOP_U;  // loads in flight per lane in wave_copy_all
 constexpr unsigned kYSplit = 8;  // blocks sharing one write block's output
 
 // All m listed payloads (B[k].dptr <- B[k].src, B[k].n bytes), one wave per
@@ -710,10 +728,17 @@ __device__ __forceinline__ void wave_copy_all(const BigSeg *B, uint32_t m, uint3
       v4u_t v[kCoopU];
 #pragma unroll
       for (int u = 0; u < kCoopU; ++u)
-        if (c0 + 64 * u < nc) v[u] = *reinterpret_cast<const v4u_una *>(src + 16 * (c0 + 64 * u));
+        if (c0 + 64 * u < nc) {
+          const v4u_una *q = reinterpret_cast<const v4u_una *>(src + 16 * (c0 + 64 * u));
+          v[u] = (SPK_COOP_NT & 1) ? __builtin_nontemporal_load(q) : *q;
+        }
 #pragma unroll
       for (int u = 0; u < kCoopU; ++u)
-        if (c0 + 64 * u < nc) *reinterpret_cast<v4u_t *>(dst + 16 * (c0 + 64 * u)) = v[u];
+        if (c0 + 64 * u < nc) {
+          v4u_t *q = reinterpret_cast<v4u_t *>(dst + 16 * (c0 + 64 * u));
+          if (SPK_COOP_NT & 2) __builtin_nontemporal_store(v[u], q);
+          else *q = v[u];
+        }
     }
   }
 }
@@ -935,7 +960,7 @@ __global__ __launch_bounds__(kThreads, 5) void var_encode_write(
       const uint64_t lo = c > g0 ? c : g0;
       const uint64_t hi = c + 16 < W.hi ? c + 16 : W.hi;
       if (lo == c && hi == c + 16) {
-        *reinterpret_cast<v4u_t *>(out + c) = *reinterpret_cast<const v4u_t *>(lds + (c - W.lo));
+        flush16(out + c, *reinterpret_cast<const v4u_t *>(lds + (c - W.lo)));
       } else {
         for (uint64_t x = lo; x < hi; ++x) out[x] = lds[x - W.lo];
       }
@@ -1766,6 +1791,9 @@ __host__ __device__ constexpr uint64_t big_jobs_cap(uint64_t wire_len) {
 // went at the pace of the longest, every instruction touching 64 lines:
 // c3l K4 5.3 ms). A group inside the window (the LDS-only reader) holds no
 // such span, and its path has none of this code (registers: C3 K4).
+#ifndef SPK_SPAN_NT  // wave_span_copy: non-temporal stores of the span bytes
+#define SPK_SPAN_NT 1  // (c3l K4 2.202 -> 2.142 ms, same-box A/B)
+#endif
 constexpr uint64_t kWaveCopy = 256;
 struct Deferred {
   uint64_t src, n;
@@ -1782,7 +1810,10 @@ __device__ __forceinline__ void wave_span_copy(const Rd &R, uint64_t x, uint8_t 
       v = R.ld16(s);
     else
       v = *reinterpret_cast<const v4u_una *>(R.wire + s);
-    *reinterpret_cast<v4u_una *>(dst + 16 * c) = v;
+    if (SPK_SPAN_NT)
+      __builtin_nontemporal_store(v, reinterpret_cast<v4u_una *>(dst + 16 * c));
+    else
+      *reinterpret_cast<v4u_una *>(dst + 16 * c) = v;
   }
   const uint64_t t = nc << 4;
   if (lane < n - t) dst[t + lane] = (uint8_t)R.byte(x + t + lane);
@@ -4380,9 +4411,21 @@ __global__ __launch_bounds__(256) void vec_big_copy(DecArgs a, const uint8_t *__
     const uint64_t h = head < jb.n ? head : jb.n;
     if (threadIdx.x < h) dst[threadIdx.x] = src[threadIdx.x];
     const uint64_t nv = (jb.n - h) / 16;
-    for (uint64_t v = threadIdx.x; v < nv; v += blockDim.x)
-      *reinterpret_cast<v4u_t *>(dst + h + 16 * v) =
-          *reinterpret_cast<const v4u_una *>(src + h + 16 * v);
+    // 4 loads in flight per thread (a piece is <= 64 KiB: one round), the
+    // wire's last read and a write-once destination: non-temporal both ways
+    for (uint64_t v0 = threadIdx.x; v0 < nv; v0 += 4 * (uint64_t)blockDim.x) {
+      v4u_t x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (v0 + u * blockDim.x < nv)
+          x[u] = __builtin_nontemporal_load(
+              reinterpret_cast<const v4u_una *>(src + h + 16 * (v0 + u * blockDim.x)));
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (v0 + u * blockDim.x < nv)
+          __builtin_nontemporal_store(
+              x[u], reinterpret_cast<v4u_t *>(dst + h + 16 * (v0 + u * blockDim.x)));
+    }
     for (uint64_t b = h + 16 * nv + threadIdx.x; b < jb.n; b += blockDim.x) dst[b] = src[b];
   }
   // (blocks without a piece take no part: one counter add per busy block)
