@@ -17,8 +17,8 @@ typedef v4u v4u_u __attribute__((aligned(1)));
   printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); return 1; } } while (0)
 
 // ---- register-staged: U chunks per lane in flight, grid-stride over tiles
-template <int U, int NT>
-__global__ __launch_bounds__(256) void reg_copy(v4u *__restrict__ dst, const uint8_t *__restrict__ sp,
+template <int U, int NT, int TPB = 256>
+__global__ __launch_bounds__(TPB) void reg_copy(v4u *__restrict__ dst, const uint8_t *__restrict__ sp,
                                                 uint64_t nk) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wpb = blockDim.x >> 6;
@@ -223,24 +223,22 @@ int main(int argc, char **argv) {
   };
   const int exact16 = (int)((nk / (64 * 16) + 3) / 4);
   const int exact32 = (int)((nk / (64 * 32) + 3) / 4);
-  run_reg("reg U16 B32768 (shipped)", reg_copy<16, 0>, 32768, 256);
-  run_reg("reg U32 B16384 ntS", reg_copy<32, 2>, 16384, 256);
-  run_reg("reg U32 B16384 ntLS", reg_copy<32, 3>, 16384, 256);
-  run_reg("reg U32 B16384 ntL", reg_copy<32, 1>, 16384, 256);
-  run_reg("reg U16 B32768 ntS", reg_copy<16, 2>, 32768, 256);
-  run_reg("reg U16 B32768 ntLS", reg_copy<16, 3>, 32768, 256);
-  run_reg("reg U16 B32768 (shipped) #2", reg_copy<16, 0>, 32768, 256);
-  run_reg("reg U32 exact ntS", reg_copy<32, 2>, exact32, 256);
-  run_reg("reg U32 exact ntLS", reg_copy<32, 3>, exact32, 256);
-  run_reg("reg U16 exact ntS", reg_copy<16, 2>, exact16, 256);
-  run_reg("reg U16 exact ntLS", reg_copy<16, 3>, exact16, 256);
-  run_reg("reg U32 B32768 ntS", reg_copy<32, 2>, 32768, 256);
-  run_reg("reg U32 B8192 ntS", reg_copy<32, 2>, 8192, 256);
-  run_reg("reg U24 B16384 ntS", reg_copy<24, 2>, 16384, 256);
-  run_reg("regdb U16 B16384 ntS", regdb_copy<16, 2>, 16384, 256);
-  run_reg("reg U16 B32768 (shipped) #3", reg_copy<16, 0>, 32768, 256);
-  run_reg("reg U32 B16384 ntS #2", reg_copy<32, 2>, 16384, 256);
-  run_reg("reg U32 B16384 ntLS #2", reg_copy<32, 3>, 16384, 256);
-    run_reg("reg U16 B32768 (shipped, again)", reg_copy<16, 0>, 32768, 256);
+  const int exact32_128 = (int)((nk / (64 * 32) + 1) / 2);
+  const int exact32_512 = (int)((nk / (64 * 32) + 7) / 8);
+  const int exact48 = (int)((nk / (64 * 48) + 3) / 4);
+  const int exact64 = (int)((nk / (64 * 64) + 3) / 4);
+  const int exact24 = (int)((nk / (64 * 24) + 3) / 4);
+  run_reg("U32 ntLS exact (shipped r6)", reg_copy<32, 3>, exact32, 256);
+  run_reg("U16 ntLS exact", reg_copy<16, 3>, exact16, 256);
+  run_reg("U24 ntLS exact", reg_copy<24, 3>, exact24, 256);
+  run_reg("U16 ntLS B32768", reg_copy<16, 3>, 32768, 256);
+  run_reg("U16 default B32768 (r5)", reg_copy<16, 0>, 32768, 256);
+  run_reg("U32 ntLS exact 128thr", reg_copy<32, 3, 128>, exact32_128, 128);
+  run_reg("U16 ntLS exact 512thr", reg_copy<16, 3, 512>, (int)((nk / (64 * 16) + 7) / 8), 512);
+  run_reg("U32 ntLS exact (shipped r6) #2", reg_copy<32, 3>, exact32, 256);
+  run_reg("U16 ntLS exact #2", reg_copy<16, 3>, exact16, 256);
+  run_reg("U32 ntLS exact (shipped r6) #3", reg_copy<32, 3>, exact32, 256);
+  run_reg("U16 ntLS exact #3", reg_copy<16, 3>, exact16, 256);
+  (void)exact48; (void)exact64; (void)exact32_512;
   return 0;
 }
