@@ -1193,3 +1193,33 @@ def test_sharded_decode_trailing_bytes(case, n, param, world, tail):
         exp = np.ascontiguousarray(recs).view(np.uint8).reshape(n, -1)
         g = got.reshape(n, -1)
         assert np.array_equal(g[:, :8], exp[:, :8]) and np.array_equal(g[:, 16:], exp[:, 16:])
+
+
+@pytest.mark.parametrize("case,n", [("cmpg", 300), ("valreq", 200), ("cmpg", 5000)])
+def test_group_walk_truncations(case, n):
+    """Round 6: optional / compatible groups of COPY / SPAN / OPTION members
+    (compatible<ResponseCode{int32, optional<string>}>, optional<ResponseCode>)
+    run the walk program (WP_GRP, NS = -4) instead of the interpreter. An
+    error inside such a group is dropped with the reader where it stopped and
+    the group's members from the failing one value-initialised: a VECTOR
+    message cut inside the last records' groups must decode as the oracle
+    does (errc, count, consume_len, records)."""
+    cd = codec_for(case)
+    _, recs, heaps = synth.make_batch(case, n, 0x6A0 + n, 16)
+    exp, _, _ = H.oracle_encode(cd.L, C.SPK_MODE_VECTOR, recs, heaps)
+    rng = np.random.default_rng(n)
+    cuts = sorted(set(list(range(max(0, len(exp) - 160), len(exp) + 1)) +
+                      rng.integers(0, len(exp), 40).tolist()))
+    for cut in cuts:
+        wire = exp[:cut]
+        eres, erecs, eheaps, _ = H.oracle_decode(cd.L, C.SPK_MODE_VECTOR, wire, rec_cap=n)
+        elems = [max(c, len(wire) // sp.elem.size + 1) for c, sp in
+                 zip(S.heap_caps_for_wire(cd.L.dev, len(wire), n), cd.L.dev.spans)]
+        b = cd.alloc_batch(n, elems)
+        b.recs.zero_()
+        cd.deserialize_to(b, wire_dev(wire), C.SPK_MODE_VECTOR)
+        res = cd.result()
+        assert (res.errc, res.count, res.consumed) == (eres.errc, eres.count, eres.consumed), cut
+        if res.errc == 0:
+            got = b.recs[:n].cpu().numpy().tobytes()
+            assert got == np.ascontiguousarray(erecs[:n]).view(np.uint8).tobytes(), cut

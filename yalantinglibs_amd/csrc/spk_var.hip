@@ -1918,6 +1918,13 @@ constexpr uint32_t WP_SPAN = 1, WP_OPT = 2, WP_ARR = 3, WP_END = 4;
 // error inside the group is dropped with the reader where it stopped
 // (unpacker.hpp:1251-1277) -- h / arg are the SPAN's heap and element size
 constexpr uint32_t WP_OSPAN = 5;
+// an optional / compatible group whose members are COPY / SPAN / OPTION ops
+// and one-SPAN groups (compatible<ResponseCode{int32, optional<string>}>):
+// [has] then, if present, the members (arg: the instruction after the group);
+// an error inside it is dropped with the reader where it stopped. Its COPYs
+// are instructions of their own (WP_CPY, fixed bytes = the COPY) so that a
+// short COPY leaves the reader where the reference's does.
+constexpr uint32_t WP_GRP = 6, WP_CPY = 7;
 // (late round 5 measured it inside the NS = -3 kernels: cmpg 8.04 -> 6.0 ms
 // per step, but Monster's K1 / K4 ~5 % slower for the extra code; round 6:
 // layouts whose walk program holds a WP_OSPAN run NS = -4 kernels of their own)
@@ -2322,11 +2329,41 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
   const uint32_t lim = (uint32_t)lim64;
   uint32_t p = (uint32_t)pos;
   uint32_t pc = 0, d = 0, body = 0, rem = 0;  // top loop frame: body start, elements left
+  // (OSPAN kernels) the instruction after the open optional / compatible
+  // group (WP_GRP), 0: none. An exact walk drops an error inside it with the
+  // reader where the failing read left it (unpacker.hpp:1251-1277): it goes
+  // on after the group; a bounded walk gives up.
+  uint32_t gend = 0;
   while (pc < N.wp_n) {
+    if (OSPAN && pc == gend) gend = 0;
     const uint2 ins = N.wp[pc];
     const uint32_t op = ins.x & 7u, h = (ins.x >> 3) & 31u, arg = ins.x >> 8;
-    if (lim - p < ins.y) return bad;
+    if (lim - p < ins.y) {
+      if (OSPAN && gend && !bounded) {  // a COPY inside the group (WP_CPY: not folded)
+        pc = gend;
+        gend = 0;
+        continue;
+      }
+      return bad;
+    }
     p += ins.y;
+    if (OSPAN && op == WP_CPY) {  // (its bytes were the fixed bytes above)
+      ++pc;
+      continue;
+    }
+    if (OSPAN && op == WP_GRP) {  // [has] then the members up to instruction arg
+      if (lim - p < 1) return bad;  // (not inside a group: the record fails)
+      const uint32_t b = rd.byte(p);
+      if (bounded && b > 1) return bad;  // (nt_read: a has_value byte above 1)
+      ++p;
+      if (b) {
+        gend = arg;
+        ++pc;
+      } else {
+        pc = arg;
+      }
+      continue;
+    }
     if (op == WP_END) {
       if (--rem) {
         pc = body;
@@ -2340,7 +2377,14 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
       continue;
     }
     if (OSPAN && op == WP_OSPAN) {
-      if (lim - p < 1) return bad;  // (the has byte itself: the record fails)
+      if (lim - p < 1) {  // (the has byte itself: the record fails, or the outer group)
+        if (gend && !bounded) {
+          pc = gend;
+          gend = 0;
+          continue;
+        }
+        return bad;
+      }
       const uint32_t b = rd.byte(p);
       if (bounded && b > 1) return bad;  // (nt_read: a has_value byte above 1)
       ++p;
@@ -2365,10 +2409,23 @@ __device__ uint64_t nt_walk(const NTLayout &N, const Rd &rd, uint64_t pos, uint6
     }
     const bool opt = op == WP_OPT;
     const uint32_t cw = opt ? 1u : w;
-    if (lim - p < cw) return bad;
+    if (lim - p < cw) {
+      if (OSPAN && gend && !bounded) {
+        pc = gend;
+        gend = 0;
+        continue;
+      }
+      return bad;
+    }
     if (bounded && opt && rd.byte(p) > 1) return bad;  // (nt_read: a has_value byte above 1)
     const uint64_t c = rd.count_at32(p, wmask, opt);
     p += cw;
+    if (OSPAN && gend && op == WP_SPAN && (c > lim - p || c * arg > lim - p)) {
+      if (bounded) return bad;
+      pc = gend;  // (a failed SPAN adds no heap use: nt_read counts it on success)
+      gend = 0;
+      continue;
+    }
     atomicAdd(U + 64 * h, (uint32_t)c);
     if (op == WP_ARR) {
       if (c > lim - p || c > maxel) return bad;  // elements take >= 1 byte
@@ -2497,32 +2554,96 @@ __device__ uint64_t nt_emit_simple(const NTLayout &N, const Rd &rd, uint64_t pos
       ++i;
       continue;
     }
-    if (OSPAN && op.kind == SPK_OP_OPTGROUP) {  // WP_OSPAN: [has] [count][payload]
+    if (OSPAN && op.kind == SPK_OP_OPTGROUP) {
+      // a one-SPAN group (WP_OSPAN: [has] [count][payload], its error dropped
+      // with the SPAN empty) at op k; returns the op after it
+      auto ospan = [&](uint32_t k) -> uint32_t {
+        const spk_op go = N.ops[k];
+        const uint32_t b = rd.byte(pos++);
+        *reinterpret_cast<uint32_t *>(r + go.rec_off) = b ? 1u : 0u;
+        if (b) {
+          const spk_op sp = N.ops[k + 1];
+          const uint32_t h = N.heap[k + 1];
+          uint64_t c = 0, nb = 0;
+          bool ok = len - pos >= w;
+          if (ok) {
+            c = rd(pos);
+            pos += w;
+            ok = span_nb(c, sp.size, &nb) && nb <= len - pos;
+          }
+          if (ok) {
+            const uint32_t o = U[64 * h];
+            U[64 * h] = o + (uint32_t)c;
+            *reinterpret_cast<uint32_t *>(r + sp.rec_off) = (uint32_t)c;
+            *reinterpret_cast<uint64_t *>(r + sp.aux) = o;
+            if (c) nt_put_payload(rd, N.heaps[h] + (uint64_t)o * sp.size, pos, nb, bq);
+            pos += nb;
+          } else {  // the group's error dropped: its members value-initialised (zero_rest)
+            *reinterpret_cast<uint32_t *>(r + sp.rec_off) = 0;
+            *reinterpret_cast<uint64_t *>(r + sp.aux) = 0;
+          }
+        }
+        return N.end[k] + 1u;
+      };
+      const uint32_t ge = N.end[i];
+      if (ge == i + 2 && N.ops[i + 1].kind == SPK_OP_SPAN) {
+        i = ospan(i);
+        continue;
+      }
+      // WP_GRP: [has] then COPY / SPAN / OPTION / one-SPAN group members; an
+      // error inside is dropped (nt_read: the members from the failing one on
+      // value-initialised, the reader where the failing read left it)
       const uint32_t b = rd.byte(pos++);
       *reinterpret_cast<uint32_t *>(r + op.rec_off) = b ? 1u : 0u;
-      if (b) {
-        const spk_op sp = N.ops[i + 1];
-        const uint32_t h = N.heap[i + 1];
-        uint64_t c = 0, nb = 0;
-        bool ok = len - pos >= w;
-        if (ok) {
-          c = rd(pos);
-          pos += w;
-          ok = span_nb(c, sp.size, &nb) && nb <= len - pos;
+      uint32_t k = i + 1;
+      while (b && k < ge) {
+        const spk_op m = N.ops[k];
+        if (m.kind == SPK_OP_COPY) {
+          if (len - pos < m.size) break;
+          rd.copy_to(r + m.rec_off, pos, m.size);
+          pos += m.size;
+          ++k;
+          continue;
         }
-        if (ok) {
-          const uint32_t o = U[64 * h];
-          U[64 * h] = o + (uint32_t)c;
-          *reinterpret_cast<uint32_t *>(r + sp.rec_off) = (uint32_t)c;
-          *reinterpret_cast<uint64_t *>(r + sp.aux) = o;
-          if (c) nt_put_payload(rd, N.heaps[h] + (uint64_t)o * sp.size, pos, nb, bq);
+        if (m.kind == SPK_OP_OPTGROUP) {
+          if (len - pos < 1) break;
+          k = ospan(k);
+          continue;
+        }
+        const bool mopt = m.kind == SPK_OP_OPTION;
+        const uint32_t cw = mopt ? 1u : w;
+        if (len - pos < cw) break;
+        const uint64_t c = mopt ? (uint64_t)(rd.byte(pos) != 0) : rd(pos);
+        pos += cw;
+        const uint32_t hk = N.heap[k];
+        uint8_t *hp = N.heaps[hk] + (uint64_t)U[64 * hk] * m.size;
+        if (!mopt) {  // SPAN: the whole payload must be there
+          uint64_t nb = 0;
+          if (!span_nb(c, m.size, &nb) || nb > len - pos) break;
+          const uint32_t o = U[64 * hk];
+          U[64 * hk] = o + (uint32_t)c;
+          *reinterpret_cast<uint32_t *>(r + m.rec_off) = (uint32_t)c;
+          *reinterpret_cast<uint64_t *>(r + m.aux) = o;
+          if (c) nt_put_payload(rd, hp, pos, nb, bq);
           pos += nb;
-        } else {  // the group's error dropped: its members value-initialised (zero_rest)
-          *reinterpret_cast<uint32_t *>(r + sp.rec_off) = 0;
-          *reinterpret_cast<uint64_t *>(r + sp.aux) = 0;
+        } else {  // OPTION: an unreadable value leaves the reader and reads as zeros
+          const uint32_t o = U[64 * hk];
+          U[64 * hk] = o + (uint32_t)c;
+          *reinterpret_cast<uint32_t *>(r + m.rec_off) = (uint32_t)c;
+          *reinterpret_cast<uint64_t *>(r + m.aux) = o;
+          if (c) {
+            if (len - pos >= m.size) {
+              rd.copy_to(hp, pos, m.size);
+              pos += m.size;
+            } else {
+              for (uint32_t x = 0; x < m.size; ++x) hp[x] = 0;
+            }
+          }
         }
+        ++k;
       }
-      i = N.end[i] + 1u;
+      if (b && k < ge) zero_rest(N, r, k, ge);  // (the dropped error's members)
+      i = ge + 1u;
       continue;
     }
     const uint32_t hk = N.heap[i];
@@ -4761,11 +4882,51 @@ static NTLayout make_ntlayout(const NLayout &N, void *const *heaps) {
   uint32_t n = 0, open[SPK_MAX_DEPTH + 1], d = 0;
   uint64_t fix = 0;
   bool ok = !N.fv_cnt;
+  // an open WP_GRP: its instruction and its END op (~0u: none)
+  uint32_t grp_ins = 0, grp_end = ~0u;
+  auto ospan_at = [&](uint32_t i) {  // a one-SPAN optional / compatible group at op i
+    return N.ops[i].kind == SPK_OP_OPTGROUP && N.ops[i].size == 1 && i + 2 < N.n_ops &&
+           N.ops[i + 1].kind == SPK_OP_SPAN && N.ops[i + 2].kind == SPK_OP_END &&
+           N.end[i] == i + 2 && N.ops[i + 1].size < (1u << 24);
+  };
   for (uint32_t i = 0; i < N.n_ops && ok; ++i) {
     const spk_op &op = N.ops[i];
+    if (grp_end != ~0u && i == grp_end) {  // the group's END: its members end here
+      t.wp[grp_ins].x |= n << 8;
+      grp_end = ~0u;
+      continue;
+    }
     if (op.kind == SPK_OP_COPY) {
+      if (grp_end != ~0u) {  // inside a group: an instruction of its own (exact drop point)
+        t.wp[n] = make_uint2(WP_CPY, op.size);
+        ++n;
+        continue;
+      }
       fix += op.size;
       continue;
+    }
+    if (op.kind == SPK_OP_OPTGROUP && op.size == 1 && !ospan_at(i) && grp_end == ~0u && !d) {
+      // WP_GRP: members COPY / SPAN / OPTION / one-SPAN groups only
+      bool simple_members = true;
+      for (uint32_t k = i + 1; k < N.end[i] && simple_members;) {
+        const uint32_t mk = N.ops[k].kind;
+        if (mk == SPK_OP_COPY || mk == SPK_OP_OPTION ||
+            (mk == SPK_OP_SPAN && N.ops[k].size < (1u << 24))) {
+          ++k;
+        } else if (ospan_at(k)) {
+          k += 3;
+        } else {
+          simple_members = false;
+        }
+      }
+      if (simple_members) {
+        if (fix >= (1ull << 32)) ok = false;
+        t.wp[n] = make_uint2(WP_GRP, (uint32_t)fix);  // (the exit patched at its END)
+        fix = 0;
+        grp_ins = n++;
+        grp_end = N.end[i];
+        continue;
+      }
     }
     uint32_t x;
     if ((op.kind == SPK_OP_SPAN || op.kind == SPK_OP_OPTION) && op.size < (1u << 24)) {
@@ -4774,9 +4935,7 @@ static NTLayout make_ntlayout(const NLayout &N, void *const *heaps) {
     } else if (op.kind == SPK_OP_ARRAY && d < SPK_MAX_DEPTH) {
       open[d++] = n;
       x = WP_ARR | ((uint32_t)N.heap[i] << 3);
-    } else if (op.kind == SPK_OP_OPTGROUP && op.size == 1 && i + 2 < N.n_ops &&
-               N.ops[i + 1].kind == SPK_OP_SPAN && N.ops[i + 2].kind == SPK_OP_END &&
-               N.end[i] == i + 2 && N.ops[i + 1].size < (1u << 24)) {
+    } else if (ospan_at(i)) {
       x = WP_OSPAN | ((uint32_t)N.heap[i + 1] << 3) |
           ((N.ops[i + 1].size ? N.ops[i + 1].size : 1u) << 8);
       i += 2;  // (the group's SPAN and END are this instruction)
@@ -4793,7 +4952,7 @@ static NTLayout make_ntlayout(const NLayout &N, void *const *heaps) {
     ++n;
     if ((x & 7u) == WP_END) t.wp[open[d]].x |= n << 8;  // the loop's exit
   }
-  t.wp_n = ok && !d && fix < (1ull << 32) ? n : 0;
+  t.wp_n = ok && !d && grp_end == ~0u && fix < (1ull << 32) ? n : 0;
   t.wp_tail = (uint32_t)fix;
   return t;
 }
@@ -4872,8 +5031,10 @@ static int nested_args(const spk_layout *L, uint64_t wire_len, uint64_t rec_cap,
   const NTLayout t = make_ntlayout(N, d_heaps);
   SPK_LAUNCH(nt_put, dim3(1), dim3(256), 0, s, t, ws + f.nl);
   if (!t.wp_n) return 0;  // the interpreter (NS = -2)
-  for (uint32_t k = 0; k < t.wp_n; ++k)
-    if ((t.wp[k].x & 7u) == WP_OSPAN) return 2;  // NS = -4
+  for (uint32_t k = 0; k < t.wp_n; ++k) {
+    const uint32_t o = t.wp[k].x & 7u;
+    if (o == WP_OSPAN || o == WP_GRP || o == WP_CPY) return 2;  // NS = -4
+  }
   return 1;                                      // NS = -3
 }
 
