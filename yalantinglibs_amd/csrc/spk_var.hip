@@ -1677,6 +1677,12 @@ __host__ __device__ constexpr uint32_t win_slots(uint32_t nv) { return nv + 1; }
 // it to wait for: a global fallback merged into a read makes every use wait
 // vmcnt(0), i.e. for all of the wave's outstanding STORES too (gfx950 counts
 // stores in vmcnt), which serialised K4's record stores.
+// WinReader::copy_to with non-temporal 16-B stores: K4's payload pieces are
+// small and unaligned, so nt stores leave partial lines (round-6 A/B: C4 K4
+// 0.475 -> 1.475 ms, cm K4 2.65 -> 2.88); off
+#ifndef SPK_COPYTO_NT
+#define SPK_COPYTO_NT 0
+#endif
 template <bool LO>
 struct WinReaderT {
   static constexpr bool kLO = LO;
@@ -1750,7 +1756,12 @@ struct WinReaderT {
       return;
     }
     uint64_t i = 0;
-    for (; i + 16 <= n; i += 16) *reinterpret_cast<v4u_una *>(dst + i) = ld16(x + i);
+    for (; i + 16 <= n; i += 16) {
+      if (SPK_COPYTO_NT)
+        __builtin_nontemporal_store(ld16(x + i), reinterpret_cast<v4u_una *>(dst + i));
+      else
+        *reinterpret_cast<v4u_una *>(dst + i) = ld16(x + i);
+    }
     if (n - i >= 8) {
       const uint64_t lo = ld4(x + i), hi = ld4(x + i + 4);
       *reinterpret_cast<u64_unaligned *>(dst + i) = lo | (hi << 32);
