@@ -29,6 +29,7 @@ struct Person {
 };
 
 int main() {
+  setvbuf(stdout, nullptr, _IONBF, 0);
   void *s = gp::device::thread_stream();
   void *d = nullptr, *h = nullptr;
   gp::device::check(spk_device_alloc(&d, 1 << 20), "alloc");
