@@ -1223,3 +1223,45 @@ def test_group_walk_truncations(case, n):
         if res.errc == 0:
             got = b.recs[:n].cpu().numpy().tobytes()
             assert got == np.ascontiguousarray(erecs[:n]).view(np.uint8).tobytes(), cut
+
+
+@pytest.mark.parametrize("case,n,world", [("cmp", 20000, 3), ("cmpg", 9000, 4), ("cmpnew", 5000, 2)])
+@pytest.mark.parametrize("tail", [0, 50000])
+def test_sharded_decode_compatible(case, n, world, tail):
+    """sharded decode of layouts with compatible members (the
+    replica protocol of parallel.shard_decode: every rank decodes the whole
+    message, keeps its even share of the records, which index the full
+    heaps): the ranks' records, in rank order, are the oracle's decode."""
+    from yalantinglibs_amd import layout as LY
+    from yalantinglibs_amd import parallel as PAR
+    cds = [SP.Codec(LY.case_layout(case)) for _ in range(world)]
+    _, recs, heaps = synth.make_batch(case, n, 0x5C0 + n, 16)
+    m, _, _ = H.oracle_encode(cds[0].L, C.SPK_MODE_VECTOR, recs, heaps)
+    wire = m + np.random.default_rng(n).integers(0, 256, tail, dtype=np.uint8).tobytes()
+    eres, erecs, eheaps, _ = H.oracle_decode(cds[0].L, C.SPK_MODE_VECTOR, wire, rec_cap=n)
+    assert eres.errc == 0 and eres.count == n
+    out, _ = PAR.shard_decode([PAR.DeviceShardBackend(c) for c in cds], wire_dev(wire), world,
+                              lambda mine: mine)
+    L = cds[0].L
+    mask = np.zeros(L.stride, bool)
+    for op in L.dev.ops:
+        k = op[0] & 0xFF
+        if k == C.SPK_OP_COPY:
+            mask[op[1]:op[1] + op[2]] = True
+        elif k in (C.SPK_OP_SPAN, C.SPK_OP_OPTION, C.SPK_OP_COMPAT):
+            mask[op[1]:op[1] + 4] = True
+    total = 0
+    rows = []
+    for b, first, res in out:
+        assert res.errc == 0 and first == total
+        total += b.n
+        rows.append(b.recs[:b.n].cpu().numpy())
+    assert total == n
+    got = np.concatenate(rows).reshape(n, L.stride)
+    exp = np.ascontiguousarray(erecs[:n]).view(np.uint8).reshape(n, L.stride)
+    assert np.array_equal(got[:, mask], exp[:, mask])
+    # the heaps the ranks' records index hold the oracle's elements
+    for k, sp in enumerate(L.dev.spans):
+        nb = int(eres.heap_used[k]) * sp.elem.size
+        for b, _, _ in out:
+            assert b.heaps[k][:nb].cpu().numpy().tobytes() == eheaps[k][:nb].tobytes()

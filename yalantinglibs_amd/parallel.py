@@ -299,6 +299,36 @@ class DeviceShardBackend:
         return RecordBatch(cd.L, out.recs[:count], out.heaps), res
 
 
+def has_compat(ops) -> bool:
+    """A layout with compatible members (SPK_OP_COMPAT / CGROUP ops)."""
+    return any((op[0] & 0xFF) in (C.SPK_OP_COMPAT, C.SPK_OP_CGROUP) for op in ops)
+
+
+def replica_decode(backends, wire, world: int, gather, mine_ranks):
+    """Layouts with compatible members: the message is a main pass followed by
+    one pass per version (ref:include/ylt/struct_pack/unpacker.hpp:1354-1376),
+    record i's members spread over every pass, so a byte range holds no whole
+    records; sharding the passes would need an all-to-all of members. Every
+    rank decodes the whole message on its GPU (the tile passes) and keeps the
+    even share [first, first + k) of the records: its records index the full
+    heaps with their global offsets (a valid RecordBatch, no rebasing). The
+    verdict is the same on every rank (one gather of the results)."""
+    out = []
+    for i, r in enumerate(mine_ranks):
+        res, full, _ = backends[i].cd.deserialize(wire, C.SPK_MODE_VECTOR)
+        n = int(res.count) if res.errc == 0 else 0
+        first, last = n * r // world, n * (r + 1) // world
+        b = RecordBatch(full.layout, full.recs[first:last], full.heaps)
+        res.count = last - first
+        out.append((b, first, res))
+    verdicts = gather([ShardSummary(int(res.errc), int(res.width), 0, 0, 0, int(res.count),
+                                    [0] * C.SPK_MAX_SPANS) for _, _, res in out])
+    errc = next((v.errc for v in verdicts if v.errc), 0)
+    for _, _, res in out:
+        res.errc = errc
+    return out
+
+
 def shard_decode(backends, wire, world: int, gather, rank: Optional[int] = None):
     """The protocol of ShardedVectorDecoder. `backends[r]` runs rank r's
     kernels (one entry when `rank` is given: this process is that rank);
@@ -312,6 +342,9 @@ def shard_decode(backends, wire, world: int, gather, rank: Optional[int] = None)
     SPK_ERRC_CAPACITY) is written into every rank's result."""
     mine_ranks = [rank] if rank is not None else list(range(world))
     be0 = backends[0]
+    cd0 = getattr(be0, "cd", None)  # (device backends; test backends may have none)
+    if cd0 is not None and has_compat(cd0.L.dev.ops):
+        return replica_decode(backends, wire, world, gather, mine_ranks), 0
     e, n, w, hl = be0.header(wire)
     if e:
         raise ValueError(f"header errc {e}")
