@@ -376,7 +376,10 @@ static unsigned elem_grid(uint64_t items, unsigned threads = 256) {
 //           the staged bytes (payloads start at any byte offset).
 // Spans that do not fit the staging buffer (malformed offsets) fall back to
 // global loads inside the same kernel, so results never depend on the path.
-constexpr int kMsgThreads = 256;
+#ifndef SPK_MSG_THREADS
+#define SPK_MSG_THREADS 256
+#endif
+constexpr int kMsgThreads = SPK_MSG_THREADS;
 constexpr uint32_t kMsgStageMax = 32768;  // staging bytes per block
 constexpr uint32_t kStagePer = 5;  // 16-B staging loads in flight per lane (decode)
 
