@@ -1265,3 +1265,72 @@ def test_sharded_decode_compatible(case, n, world, tail):
         nb = int(eres.heap_used[k]) * sp.elem.size
         for b, _, _ in out:
             assert b.heaps[k][:nb].cpu().numpy().tobytes() == eheaps[k][:nb].tobytes()
+
+
+def _cmpg_has_positions(recs, wire_len, w):
+    """Byte positions of CmpG's has_value bytes in a VECTOR wire: the main
+    pass (id, name), then version 20230101 (note, ints), then 20240101 (in,
+    rc{retcode, error_message}); the header is what the passes leave."""
+    n = len(recs)
+    nl = recs["name.n"].astype(np.int64)
+    nh, nv = recs["note.has"].astype(np.int64), recs["note.value.n"].astype(np.int64)
+    ih, iv = recs["ints.has"].astype(np.int64), recs["ints.value.n"].astype(np.int64)
+    inh = recs["in.n"].astype(np.int64)
+    rh = recs["rc.has"].astype(np.int64)
+    eh = recs["rc.value.error_message.has"].astype(np.int64)
+    ev = recs["rc.value.error_message.value.n"].astype(np.int64)
+    main = 4 + w + nl
+    p1 = 1 + nh * (w + nv) + 1 + ih * (w + 4 * iv)
+    p2 = 1 + inh * 8 + 1 + rh * (4 + 1 + eh * (w + ev))
+    hl = wire_len - int(main.sum() + p1.sum() + p2.sum())
+    s1 = hl + int(main.sum())
+    st1 = s1 + np.concatenate([[0], np.cumsum(p1)[:-1]])
+    s2 = s1 + int(p1.sum())
+    st2 = s2 + np.concatenate([[0], np.cumsum(p2)[:-1]])
+    note_has = st1
+    ints_has = st1 + 1 + nh * (w + nv)
+    in_has = st2
+    rc_has = st2 + 1 + inh * 8
+    em_has = rc_has + 1 + 4
+    return hl, {"note": note_has, "ints": ints_has, "in": in_has, "rc": rc_has,
+                "em": np.where(rh == 1, em_has, -1)}
+
+
+@pytest.mark.parametrize("n", [2000, 30000])
+def test_nonzero_has_value_bytes_compatible(n):
+    """has_value bytes of 2..255 in CmpG's version passes (the group walk
+    program's WP_OSPAN / WP_GRP / OPTION has bytes, and the optional inside
+    the compatible<ResponseCode> group): present, as the oracle reads them."""
+    cd = codec_for("cmpg")
+    _, recs, heaps = synth.make_batch("cmpg", n, 0xA5A + n, 16)
+    out, _ = cd.serialize(to_dev(cd, recs, heaps), C.SPK_MODE_VECTOR)
+    wire = bytearray(out.cpu().numpy().tobytes())
+    for w in (1, 2, 4, 8):
+        hl, pos = _cmpg_has_positions(recs, len(wire), w)
+        if 0 < hl < 40 and all(wire[int(p)] in (0, 1) for p in pos["note"][:50]):
+            break
+    else:
+        pytest.fail("no width fits the CmpG passes")
+    rng = np.random.default_rng(n)
+    changed = 0
+    for key, ps in pos.items():
+        for i in rng.choice(n, n // 5, replace=False):
+            p = int(ps[i])
+            if p >= 0 and wire[p] == 1:
+                wire[p] = int(rng.integers(2, 256))
+                changed += 1
+    assert changed > n // 4
+    wire = bytes(wire)
+    eres, erecs, eheaps, _ = H.oracle_decode(cd.L, C.SPK_MODE_VECTOR, wire, rec_cap=n)
+    assert eres.errc == 0 and eres.count == n
+    b = cd.alloc_batch(n, [max(c, len(wire) // sp.elem.size + 1) for c, sp in
+                           zip(S.heap_caps_for_wire(cd.L.dev, len(wire), n), cd.L.dev.spans)])
+    b.recs.zero_()
+    cd.deserialize_to(b, wire_dev(wire), C.SPK_MODE_VECTOR)
+    res = cd.result()
+    assert (res.errc, res.count, res.consumed) == (eres.errc, eres.count, eres.consumed)
+    assert b.recs[:n].cpu().numpy().tobytes() == \
+        np.ascontiguousarray(erecs[:n]).view(np.uint8).tobytes()
+    for k in range(len(heaps)):
+        nb = int(eres.heap_used[k]) * cd.L.dev.spans[k].elem.size
+        assert b.heaps[k][:nb].cpu().numpy().tobytes() == eheaps[k][:nb].tobytes()
