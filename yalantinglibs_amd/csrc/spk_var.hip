@@ -1288,6 +1288,9 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
 // the walks; see the pipeline overview before kTChunk. (Round 1's multi-pass
 // chunk walker with P/E lists and verification rounds was removed in round 2
 // after the tile pipeline replaced it.)
+#ifndef SPK_VSCREEN  // varint layouts: K1's candidate screen from a terminator mask
+#define SPK_VSCREEN 1  // (cv K1 1.255 -> 0.988 ms, cv 3.077 -> 2.807 ms per step, same-box A/B)
+#endif
 constexpr uint32_t kSpec = 256;        // payload bytes per speculation chunk
 constexpr uint32_t kWinExtra = 512;    // extension bytes staged past a wave's chunks
 constexpr uint32_t kPlaus = 4096;      // longest record a speculative walk accepts
@@ -3157,7 +3160,38 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
       if (searching) {
         const uint64_t b0 = cs + tt + s0;  // first count field of candidate cs+tt
         uint32_t m = 0;
-        if (NS < 0 && P.pf_var) {
+        if (NS < 0 && P.pf_var && SPK_VSCREEN && b0 + 48 <= wend) {
+          // the terminator bytes (high bit clear) of the 32 bytes from b0 as
+          // a mask: a varint's length is a ctz, not an 8-byte decode; a
+          // candidate whose varints run past the mask takes vread
+          const uint32_t o0 = (uint32_t)(b0 - ts), i = win_dw(o0), sh = o0 & 3;
+          const lds_u32 *d = rd.d;
+          uint32_t T = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const uint32_t dk = __builtin_amdgcn_alignbyte(d[i + k + 1], d[i + k], sh);
+            T |= ((((~dk) & 0x80808080u) * 0x00204081u) >> 28) << (4 * k);
+          }
+          for (int kk = 0; kk < 8; ++kk) {
+            uint32_t off = (uint32_t)kk;
+            bool ok = true;
+            for (uint32_t j = 0; j < P.vfirst[1] && ok; ++j) {
+              uint32_t l;
+              if (off + 10 <= 32) {
+                const uint32_t mm = T >> off;  // (off < 32)
+                l = mm ? (uint32_t)__builtin_ctz(mm) + 1 : 11;
+              } else {
+                uint64_t v;
+                l = rd.vread(b0 + off, len, &v);
+                if (!l) l = 11;
+              }
+              if (l > 10) ok = false;
+              off += l + P.vafter[j];
+            }
+            if (ok) ok = (b0 + off + w <= len ? rd(b0 + off) : ~0ull) <= c0t;
+            m |= (ok ? 1u : 0u) << kk;
+          }
+        } else if (NS < 0 && P.pf_var) {
           for (int kk = 0; kk < 8; ++kk) {
             uint64_t q = b0 + kk;
             bool ok = true;
