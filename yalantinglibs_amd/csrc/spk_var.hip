@@ -3416,6 +3416,16 @@ __device__ __forceinline__ uint64_t tile_spec_resolve(const WalkProg &P, const W
 #ifndef SPK_K1_STATS
 #define SPK_K1_STATS 0
 #endif
+// SPK_K1_PRINT=1 (with SPK_K1_STATS and SPK_TILE_DBG=4096, scripts/diag_k1.sh):
+// the first pick of every decode prints them, the tile times in 10 ns ticks
+#ifndef SPK_K1_PRINT
+#define SPK_K1_PRINT 0
+#endif
+#if SPK_K1_PRINT
+__device__ __forceinline__ uint64_t k1_clock() { return __builtin_amdgcn_s_memrealtime(); }
+#else
+__device__ __forceinline__ uint64_t k1_clock() { return __builtin_readcyclecounter(); }
+#endif
 // W: the count width as a compile-time constant (0: read from the header at
 // run time). The walkers' count reads, screens and bounds checks then carry
 // no width switch: nested walks are divergent loops, so every branch of the
@@ -3427,7 +3437,7 @@ __device__ __forceinline__ void vec_tile_spec_body(const DecArgs &a, const WalkP
                                                    const TileBufs &TB, uint32_t dbg,
                                                    v4u_t *win, uint64_t t, uint32_t lane) {
   const VCtl *c = reinterpret_cast<const VCtl *>(ws + kWsCtl);
-  const uint64_t tclk0 = (dbg & 4096) ? __builtin_readcyclecounter() : 0;
+  const uint64_t tclk0 = (dbg & 4096) ? k1_clock() : 0;
   nt_prologue<NS>(a, lane);
   const uint32_t w = W ? W : c->w;
   const uint64_t len = a.wire_len, p0 = c->p0;
@@ -3450,7 +3460,7 @@ __device__ __forceinline__ void vec_tile_spec_body(const DecArgs &a, const WalkP
       const uint64_t v = wave_sum_u64(stat[k]);
       if (lane == 0) atomicAdd(&fcd->diag[k], (unsigned long long)v);
     }
-    const uint64_t dt = __builtin_readcyclecounter() - tclk0;  // this tile's cycles
+    const uint64_t dt = k1_clock() - tclk0;  // this tile's cycles (or ticks)
     if (lane == 0) {
       atomicMax(&fcd->diag[6], (unsigned long long)dt);
       atomicAdd(&fcd->diag[7], (unsigned long long)dt);
@@ -3691,6 +3701,14 @@ __global__ __launch_bounds__(256) void vec_tile_pick(uint8_t *__restrict__ ws, T
   FCtl *fc = reinterpret_cast<FCtl *>(ws + kWsFCtl);
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (!vec_live(c)) return;                               // (uniform)
+#if SPK_K1_PRINT
+  if (pass == 0 && t == 0)
+    printf("[k1] ntiles %llu n %llu w %u p0 %llu rounds %llu walks %llu wlen %llu offgrid %llu "
+           "changed %llu xchk %llu maxtile %llu sumtile %llu\n",
+           (unsigned long long)TB.ntiles, (unsigned long long)c->n, c->w,
+           (unsigned long long)c->p0, fc->diag[0], fc->diag[1], fc->diag[2], fc->diag[3],
+           fc->diag[4], fc->diag[5], fc->diag[6], fc->diag[7]);
+#endif
   if (pass > 0 && !fc->broken[pass - 1]) return;  // the previous pass fixed nothing
   // broken tiles are counted and listed with one atomic per wave (a broken
   // tile per thread adding to the same two words serialised thousands of
