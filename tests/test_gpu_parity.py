@@ -263,12 +263,12 @@ def test_vector_trailing_bytes(case, n, param, tail):
 
 
 @pytest.mark.parametrize("case", ["cmp", "cmpg", "cmpnew"])
-@pytest.mark.parametrize("n,cap", [(0, 1), (1, 1), (700, 700), (700, 300)])
+@pytest.mark.parametrize("n,cap", [(0, 1), (1, 1), (700, 700), (700, 300), (700, 0)])
 def test_compat_vector_edges(case, n, cap):
     """Compatible-member VECTOR decode on the tile passes at the edges: an
-    empty message, one record, and a record capacity below the count (the
-    passes are not clean: the one-lane walk behind them reports it) — errc,
-    count, consume_len and the records against the oracle."""
+    empty message, one record, and a record capacity below the count (every
+    pass still walks all records and writes those that fit; errc CAPACITY) —
+    errc, count, consume_len and the records against the oracle."""
     cd = codec_for(case)
     _, recs, heaps = synth.make_batch(case, n, 0xED6E + n, 16)
     out, _ = cd.serialize(to_dev(cd, recs, heaps), C.SPK_MODE_VECTOR)
@@ -283,6 +283,39 @@ def test_compat_vector_edges(case, n, cap):
     if res.errc == 0 and n:
         exp = np.ascontiguousarray(erecs[:n]).view(np.uint8).reshape(n, cd.L.stride)
         assert b.recs[:n].cpu().numpy().tobytes() == exp.tobytes()
+
+
+@pytest.mark.parametrize("case", ["cmp", "cmpg"])
+def test_compat_capacity_probe_fast(case):
+    """A capacity probe (record capacity below the count, e.g. to learn the
+    count) of a 200K-record compatible message stays on the tile passes: the
+    oracle's errc / count / consume_len and the records that fit, in bounded
+    time (round 5 fell back to the one-lane walk: ~1.8 s)."""
+    cd = codec_for(case)
+    n, cap = 200_000, 1000
+    _, recs, heaps = synth.make_batch(case, n, 0xCA9 + n, 16)
+    out, _ = cd.serialize(to_dev(cd, recs, heaps), C.SPK_MODE_VECTOR)
+    wire = out.cpu().numpy().tobytes()
+    eres, erecs, _, _ = H.oracle_decode(cd.L, C.SPK_MODE_VECTOR, wire, rec_cap=cap)
+    assert eres.errc == C.ERRC_CAPACITY
+    elems = [max(c, len(wire) // sp.elem.size + 1) for c, sp in
+             zip(S.heap_caps_for_wire(cd.L.dev, len(wire), n), cd.L.dev.spans)]
+    b = cd.alloc_batch(cap, elems)
+    w = wire_dev(wire)
+    ts = []
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        cd.deserialize_to(b, w, C.SPK_MODE_VECTOR)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    res = cd.result()
+    assert (res.errc, res.count, res.consumed) == (eres.errc, eres.count, eres.consumed)
+    exp = np.ascontiguousarray(erecs[:cap]).view(np.uint8).reshape(cap, cd.L.stride)
+    assert b.recs[:cap].cpu().numpy().tobytes() == exp.tobytes()
+    print(f"{case}: capacity probe of {n} records in {min(ts):.3f} ms")
+    assert min(ts) < 100.0, ts  # complexity guard: the passes take a few ms
 
 
 @pytest.mark.parametrize("writer,reader", [("cmpold", "cmp"), ("cmpnew", "cmp"),

@@ -5260,7 +5260,13 @@ __global__ void compat_link(const uint8_t *ws, CompatCtl *cc, spk_dresult_t *res
     cc->serial = 0;
     cc->stop = n_ranks;
     spk_dresult_t r = *res;
-    if (r.errc || c->errc) {
+    // a record or heap capacity below the message's needs (CAPACITY: the
+    // pass walked every record, K4 wrote the ones that fit) is no reason for
+    // the one-lane walk: the version passes run on, the errc stays, and a
+    // read error of a later pass still takes precedence (the serial walk
+    // reports it). A capacity probe (rec_cap 0) of a compatible message took
+    // the one-lane walk: ~1.8 s for 200K records.
+    if ((r.errc && r.errc != SPK_ERRC_CAPACITY) || c->errc) {
       cc->serial = 1;
       cc->chain[1] = 0;
       return;
@@ -5282,11 +5288,12 @@ __global__ void compat_link(const uint8_t *ws, CompatCtl *cc, spk_dresult_t *res
   }
   if (cc->serial || cc->stop <= (uint32_t)rank) return;  // (the pass read no record)
   const spk_dresult_t p = cc->pres;
-  if (p.errc || c->errc || end > cc->chain[3]) {
+  if ((p.errc && p.errc != SPK_ERRC_CAPACITY) || c->errc || end > cc->chain[3]) {
     cc->serial = 1;
     cc->chain[1] = 0;
     return;
   }
+  if (p.errc && !res->errc) res->errc = p.errc;  // (a version member's heap overflowed)
   for (uint32_t j = 0; j < hm.nh; ++j) res->heap_used[hm.h[j]] = p.heap_used[j];
   cc->end = end;
   cc->chain[0] = end;
