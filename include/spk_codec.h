@@ -359,7 +359,12 @@ int spk_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
  * i with its errc in d_errc[i] (nullable) and d_res->count = #ok.
  * Records go to d_recs (capacity rec_cap records); span elements go to
  * d_heaps[k] (capacity heap_caps[k] elements; HOST arrays of device
- * pointers / sizes) at canonical offsets (record order, packed). */
+ * pointers / sizes) at canonical offsets (record order, packed).
+ * SPK_MODE_VECTOR with rec_cap below the message's count (or a heap too
+ * small): the records that fit are written, d_res->count = the message's
+ * count, consumed = its length, errc SPK_ERRC_CAPACITY -- unless the wire has
+ * a read error, whose errc wins as in the reference -- so rec_cap 0 is a
+ * count probe (compatible-member layouts included). */
 int spk_decode(const spk_layout *L, int mode, const void *d_wire,
                uint64_t wire_len, const uint64_t *d_msg_offsets, uint64_t n_msgs,
                void *d_recs, uint64_t rec_cap, void *const *d_heaps,
