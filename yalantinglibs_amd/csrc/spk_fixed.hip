@@ -514,6 +514,13 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
   const uint32_t tid = threadIdx.x;
   const uint32_t S = a.stride;
   const uint64_t ngroups = (N + a.R - 1) / a.R;
+  // one block (a small call's messages): it resets and writes the result
+  // itself, no memset and no msg_sum_partials launch
+  const bool solo = gridDim.x == 1 && part == nullptr;
+  if (solo) {
+    if (tid == 0) *res = spk_dresult_t{};
+    __syncthreads();
+  }
   // more frames than the caller's n_max: the excess is not decoded
   if (a.dn && blockIdx.x == 0 && tid == 0 && *a.dn > a.n) atomicExch(&res->errc, SPK_ERRC_CAPACITY);
   // ok / consumed accumulate over the block's groups: one atomic per wave at
@@ -670,8 +677,13 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_decode_lds(
       o += s_lo[k];
       c += s_hi[k];
     }
-    part[2 * blockIdx.x] = o;
-    part[2 * blockIdx.x + 1] = c;
+    if (solo) {
+      res->count = o;
+      res->consumed = c;
+    } else {
+      part[2 * blockIdx.x] = o;
+      part[2 * blockIdx.x + 1] = c;
+    }
   }
   if (__any(cap_hit) && (tid & 63) == 0) atomicExch(&res->errc, SPK_ERRC_CAPACITY);
 }
@@ -932,8 +944,7 @@ hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
   uint8_t hb[4 + 1 + SPK_MAX_LITERAL + 1];
   a.fixed_M = prefix + write_hdr(hb, L->fmt_one, 1) + L->rec_stride;
   uint64_t *payload = reinterpret_cast<uint64_t *>((uint8_t *)d_ws + kWsScratch);
-  hipError_t e = hipMemsetAsync(d_res, 0, sizeof(spk_dresult_t), s);
-  if (e != hipSuccess) return e;
+  hipError_t e;
   {
     MsgLdsArgs b = {};
     b.fmt = L->fmt_one;
@@ -952,6 +963,13 @@ hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
       const uint64_t blocks = resident_grid(fixed_msg_decode_lds, kMsgThreads, (size_t)b.cap + 16,
                                             (n + b.R - 1) / b.R, 4096);
       uint64_t *part = payload;  // workspace scratch: 2 words per block
+      if (blocks == 1) {  // (the kernel resets d_res and writes it: one launch)
+        SPK_LAUNCH(fixed_msg_decode_lds, dim3(1), dim3(kMsgThreads), (size_t)b.cap + 16, s, b,
+                   (const uint8_t *)d_wire, d_offsets, d_errc, d_res, (uint8_t *)d_recs,
+                   (uint64_t *)nullptr);
+        return hipGetLastError();
+      }
+      if ((e = hipMemsetAsync(d_res, 0, sizeof(spk_dresult_t), s)) != hipSuccess) return e;
       SPK_LAUNCH(fixed_msg_decode_lds, dim3((unsigned)blocks), dim3(kMsgThreads),
                          (size_t)b.cap + 16, s, b, (const uint8_t *)d_wire, d_offsets, d_errc,
                          d_res, (uint8_t *)d_recs, part);
@@ -960,6 +978,7 @@ hipError_t launch_fixed_decode_messages(const spk_layout *L, const void *d_wire,
       return hipGetLastError();
     }
   }
+  if ((e = hipMemsetAsync(d_res, 0, sizeof(spk_dresult_t), s)) != hipSuccess) return e;
   SPK_LAUNCH(fixed_msg_parse, dim3(elem_grid(n)), dim3(256), 0, s, a,
                      (const uint8_t *)d_wire, d_offsets, payload, d_errc, d_res);
   if ((e = hipGetLastError()) != hipSuccess) return e;

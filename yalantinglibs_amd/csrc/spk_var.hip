@@ -380,6 +380,9 @@ __host__ __device__ inline PlanScratch plan_scratch(uint8_t *ws, uint64_t nb) {
 }
 static size_t plan_scratch_bytes(uint64_t nb) { return kPlanHead + nb * (2 + kPlanSub) * 8; }
 
+#ifndef SPK_PLAN_SMALL  // <= kPlanRPB records: one fused plan launch (var_plan_small)
+#define SPK_PLAN_SMALL 1
+#endif
 struct FinArgs {
   spk_msgfmt fmt;
   uint64_t n;
@@ -395,6 +398,9 @@ struct FinArgs {
 constexpr uint32_t kFinPer = 16, kFinThreads = 1024;
 constexpr uint32_t kFinTW = kFinPer * (kFinThreads / 64);  // wave totals per chunk
 constexpr uint32_t kFinG = kFinTW / 64;                     // ... per lane of the scanning wave
+__device__ __forceinline__ void plan_result(const FinArgs &a, uint64_t carry, uint64_t mx,
+                                            uint8_t *__restrict__ ws,
+                                            spk_plan_t *__restrict__ plan);
 __global__ __launch_bounds__(kFinThreads) void var_plan_finalize(FinArgs a, uint64_t nb,
                                                                  uint8_t *__restrict__ ws,
                                                                  spk_plan_t *__restrict__ plan) {
@@ -451,6 +457,12 @@ __global__ __launch_bounds__(kFinThreads) void var_plan_finalize(FinArgs a, uint
   __syncthreads();
   if (t != 0) return;
   for (uint32_t w = 1; w < NW; ++w) mx = tw[w] > mx ? tw[w] : mx;
+  plan_result(a, carry, mx, ws, plan);
+}
+// the plan from the payload byte sum and the largest count (one thread)
+__device__ __forceinline__ void plan_result(const FinArgs &a, uint64_t carry, uint64_t mx,
+                                            uint8_t *__restrict__ ws,
+                                            spk_plan_t *__restrict__ plan) {
   spk_plan_t r;
   if (a.mode == SPK_MODE_VECTOR) {
     const uint64_t maxc = mx > a.n ? mx : a.n;  // outer vector counts too
@@ -481,12 +493,13 @@ __global__ __launch_bounds__(kFinThreads) void var_plan_finalize(FinArgs a, uint
 // Per plan block (kPlanSub write blocks of kRPB records): the byte sums and
 // the largest count. (A last-block-out finalize inside this kernel measured
 // 6x slower for C3: 9,766 agent-scope release fences and same-address adds.)
-__global__ __launch_bounds__(kThreads) void var_plan_reduce(
-    VarArgs a, const uint8_t *__restrict__ recs, uint8_t *__restrict__ ws,
-    const uint8_t *__restrict__ hdrlen_tbl) {
+__device__ __forceinline__ void plan_reduce_body(const VarArgs &a, const uint8_t *__restrict__ recs,
+                                                 uint8_t *__restrict__ ws,
+                                                 const uint8_t *__restrict__ hdrlen_tbl,
+                                                 uint64_t bx, uint64_t nb,
+                                                 uint64_t (*red)[kThreads / 64]) {
   const uint64_t N = dev_count(a.n, a.dn);
-  __shared__ uint64_t red[kPlanSub + 1][kThreads / 64];
-  const uint64_t r0 = (uint64_t)blockIdx.x * kPlanRPB;
+  const uint64_t r0 = bx * kPlanRPB;
   // every record's sizes first (all loads in flight at once), then one block
   // reduction of the kPlanSub write-block sums and the max (round 4: a block
   // scan per write block, its loads waiting on the previous scan's barriers)
@@ -520,20 +533,25 @@ __global__ __launch_bounds__(kThreads) void var_plan_reduce(
     if ((threadIdx.x & 63) == 0) red[j][threadIdx.x >> 6] = v;
   }
   __syncthreads();
-  const uint64_t nb = gridDim.x;
   const PlanScratch q = plan_scratch(ws, nb);
   if (threadIdx.x == 0) {
     uint64_t sum = 0, m = 0;
     for (int j = 0; j < kPlanSub; ++j) {
       uint64_t t = 0;
       for (uint32_t w = 0; w < kThreads / 64; ++w) t += red[j][w];
-      q.wsub[blockIdx.x * kPlanSub + j] = t;
+      q.wsub[bx * kPlanSub + j] = t;
       sum += t;
     }
     for (uint32_t w = 0; w < kThreads / 64; ++w) m = red[kPlanSub][w] > m ? red[kPlanSub][w] : m;
-    q.psum[blockIdx.x] = sum;
-    q.pmax[blockIdx.x] = m;
+    q.psum[bx] = sum;
+    q.pmax[bx] = m;
   }
+}
+__global__ __launch_bounds__(kThreads) void var_plan_reduce(
+    VarArgs a, const uint8_t *__restrict__ recs, uint8_t *__restrict__ ws,
+    const uint8_t *__restrict__ hdrlen_tbl) {
+  __shared__ uint64_t red[kPlanSub + 1][kThreads / 64];
+  plan_reduce_body(a, recs, ws, hdrlen_tbl, blockIdx.x, gridDim.x, red);
 }
 
 // message headers per width for MESSAGES mode (host computes: no data needed)
@@ -542,11 +560,29 @@ struct MsgHdrTable {
   uint8_t bytes[4][4 + 1 + SPK_MAX_LITERAL + 1];
 };
 
-__global__ void write_msg_hdrs(MsgHdrTable t, uint8_t *ws) {
+__device__ __forceinline__ void msg_hdrs_body(const MsgHdrTable &t, uint8_t *ws) {
   for (int s = 0; s < 4; ++s)
     for (uint32_t i = threadIdx.x; i < t.len[s]; i += blockDim.x)
       ws[kWsHdrMsg + s * kWsHdrSlot + i] = t.bytes[s][i];
   if (threadIdx.x < 4) ws[kWsHdrMsg + 4 * kWsHdrSlot - 8 + threadIdx.x] = t.len[threadIdx.x];
+}
+__global__ void write_msg_hdrs(MsgHdrTable t, uint8_t *ws) { msg_hdrs_body(t, ws); }
+
+// the plan of at most kPlanRPB records (a small call): header table, block
+// sums and the plan in one launch of one block instead of three
+__global__ __launch_bounds__(kThreads) void var_plan_small(VarArgs a, FinArgs f, MsgHdrTable t,
+                                                           const uint8_t *__restrict__ recs,
+                                                           uint8_t *__restrict__ ws,
+                                                           spk_plan_t *__restrict__ plan) {
+  __shared__ uint64_t red[kPlanSub + 1][kThreads / 64];
+  if (a.mode == SPK_MODE_MESSAGES) msg_hdrs_body(t, ws);
+  __syncthreads();
+  plan_reduce_body(a, recs, ws, ws + kWsHdrMsg + 4 * kWsHdrSlot - 8, 0, 1, red);
+  if (threadIdx.x != 0) return;
+  const PlanScratch q = plan_scratch(ws, 1);
+  const uint64_t carry = q.psum[0], mx = q.pmax[0];
+  q.psum[0] = 0;  // (the exclusive scan of one block sum)
+  plan_result(f, carry, mx, ws, plan);
 }
 
 // ---- LDS-staged output ------------------------------------------------------
@@ -1102,14 +1138,18 @@ struct MsgState {
   int32_t errc;
 };
 
-__global__ __launch_bounds__(kThreads) void var_msg_parse(
-    DecArgs a, const uint8_t *__restrict__ wire, const uint64_t *__restrict__ offs,
-    uint8_t *__restrict__ ws, int32_t *__restrict__ errc_out, spk_dresult_t *res) {
-  __shared__ uint64_t sh[kThreads / 64];
+#ifndef SPK_MSG_SMALL  // <= kThreads MESSAGES: one fused decode launch (var_msg_decode_small)
+#define SPK_MSG_SMALL 1
+#endif
+__device__ __forceinline__ void msg_parse_body(const DecArgs &a, const uint8_t *__restrict__ wire,
+                                               const uint64_t *__restrict__ offs,
+                                               uint8_t *__restrict__ ws,
+                                               int32_t *__restrict__ errc_out, spk_dresult_t *res,
+                                               uint64_t bx, uint64_t *sh) {
   MsgState *st = reinterpret_cast<MsgState *>(ws + kWsScratch);
   uint64_t *bsum = reinterpret_cast<uint64_t *>(ws + kWsScratch +
                                                 sizeof(MsgState) * a.n_msgs);
-  const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  const uint64_t i = bx * kThreads + threadIdx.x;
   uint64_t cnt[kVS] = {};
   uint64_t ok = 0, consumed = 0;
   // more frames than the caller's n_max: the excess is not decoded
@@ -1152,25 +1192,28 @@ __global__ __launch_bounds__(kThreads) void var_msg_parse(
   for (uint32_t k = 0; k < a.L.n_spans; ++k) {
     uint64_t tot;
     block_excl_scan(cnt[k], &tot, sh);
-    if (threadIdx.x == 0) bsum[(uint64_t)blockIdx.x * kBs + k] = tot;
+    if (threadIdx.x == 0) bsum[bx * kBs + k] = tot;
   }
   uint64_t tok, tcons;
   block_excl_scan(ok, &tok, sh);
   block_excl_scan(consumed, &tcons, sh);
   if (threadIdx.x == 0) {
-    bsum[(uint64_t)blockIdx.x * kBs + kVS] = tok;
-    bsum[(uint64_t)blockIdx.x * kBs + kVS + 1] = tcons;
+    bsum[bx * kBs + kVS] = tok;
+    bsum[bx * kBs + kVS + 1] = tcons;
   }
+}
+__global__ __launch_bounds__(kThreads) void var_msg_parse(
+    DecArgs a, const uint8_t *__restrict__ wire, const uint64_t *__restrict__ offs,
+    uint8_t *__restrict__ ws, int32_t *__restrict__ errc_out, spk_dresult_t *res) {
+  __shared__ uint64_t sh[kThreads / 64];
+  msg_parse_body(a, wire, offs, ws, errc_out, res, blockIdx.x, sh);
 }
 
 // one block: exclusive scan of per-block span totals (in place), heap_used,
 // capacity check
-__global__ __launch_bounds__(1024) void var_scan_blocks(uint64_t nblocks,
-                                                        uint32_t n_spans,
-                                                        uint64_t *__restrict__ bsum,
-                                                        DecArgs a,
-                                                        spk_dresult_t *res) {
-  __shared__ uint64_t sh[1024 / 64];
+__device__ __forceinline__ void scan_blocks_body(uint64_t nblocks, uint32_t n_spans,
+                                                 uint64_t *__restrict__ bsum, const DecArgs &a,
+                                                 spk_dresult_t *res, uint64_t *sh) {
   for (uint32_t k = 0; k < n_spans; ++k) {
     uint64_t carry = 0;
     for (uint64_t b0 = 0; b0 < nblocks; b0 += blockDim.x) {
@@ -1203,11 +1246,21 @@ __global__ __launch_bounds__(1024) void var_scan_blocks(uint64_t nblocks,
     }
   }
 }
+__global__ __launch_bounds__(1024) void var_scan_blocks(uint64_t nblocks,
+                                                        uint32_t n_spans,
+                                                        uint64_t *__restrict__ bsum,
+                                                        DecArgs a,
+                                                        spk_dresult_t *res) {
+  __shared__ uint64_t sh[1024 / 64];
+  scan_blocks_body(nblocks, n_spans, bsum, a, res, sh);
+}
 
-__global__ __launch_bounds__(kThreads) void var_msg_write(
-    DecArgs a, const uint8_t *__restrict__ wire, const uint64_t *__restrict__ offs,
-    const uint8_t *__restrict__ ws, uint8_t *__restrict__ recs, const spk_dresult_t *res) {
-  __shared__ uint64_t sh[kThreads / 64];
+__device__ __forceinline__ void msg_write_body(const DecArgs &a, const uint8_t *__restrict__ wire,
+                                               const uint64_t *__restrict__ offs,
+                                               const uint8_t *__restrict__ ws,
+                                               uint8_t *__restrict__ recs,
+                                               const spk_dresult_t *res, uint64_t bx, uint32_t by,
+                                               uint32_t gy, uint64_t *sh, BigSeg *big) {
   const MsgState *st = reinterpret_cast<const MsgState *>(ws + kWsScratch);
   const uint64_t *bsum = reinterpret_cast<const uint64_t *>(ws + kWsScratch +
                                                             sizeof(MsgState) * a.n_msgs);
@@ -1215,7 +1268,7 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
   // CAPACITY errc and are skipped below; the others are still written)
   for (uint32_t k = 0; k < a.L.n_spans; ++k)
     if (res->heap_used[k] > a.heap_cap[k]) return;
-  const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  const uint64_t i = bx * kThreads + threadIdx.x;
   MsgState s{~0ull, 1, 1};
   uint64_t cnt[kVS] = {};
   uint64_t end = 0;
@@ -1229,11 +1282,10 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
   uint64_t hoff[kVS] = {};
   for (uint32_t k = 0; k < a.L.n_spans; ++k) {
     uint64_t tot;
-    hoff[k] = bsum[(uint64_t)blockIdx.x * kBs + k] + block_excl_scan(cnt[k], &tot, sh);
+    hoff[k] = bsum[bx * kBs + k] + block_excl_scan(cnt[k], &tot, sh);
   }
   const bool live = s.pos != ~0ull && !s.errc;
   // large payloads go to the block's cooperative list (record order)
-  __shared__ BigSeg big[kBigMax];
   uint32_t nbig = 0, skip = 0;
   if (live) {
     uint32_t sk = 0;
@@ -1271,12 +1323,40 @@ __global__ __launch_bounds__(kThreads) void var_msg_write(
   }
   // copy split: gridDim.y blocks share the block's listed payloads; block 0
   // also writes the records and the short payloads
-  if (live && blockIdx.y == 0)
+  if (live && by == 0)
     decode_record(a.L, wire, s.pos, s.w, recs + i * a.L.stride, a.heaps, hoff, end, skip);
   __syncthreads();
   if (nbig_tot > kBigMax) nbig_tot = kBigMax;
   if (nbig_tot == 0) return;  // block-uniform
-  wave_copy_all(big, (uint32_t)nbig_tot, blockIdx.y, gridDim.y);
+  wave_copy_all(big, (uint32_t)nbig_tot, by, gy);
+}
+__global__ __launch_bounds__(kThreads) void var_msg_write(
+    DecArgs a, const uint8_t *__restrict__ wire, const uint64_t *__restrict__ offs,
+    const uint8_t *__restrict__ ws, uint8_t *__restrict__ recs, const spk_dresult_t *res) {
+  __shared__ uint64_t sh[kThreads / 64];
+  __shared__ BigSeg big[kBigMax];
+  msg_write_body(a, wire, offs, ws, recs, res, blockIdx.x, blockIdx.y, gridDim.y, sh, big);
+}
+
+// MESSAGES decode of at most kThreads messages (a coro_rpc call's one
+// request or response): the result reset, parse, block scan and write in one
+// launch of one block instead of a memset and three kernels (each dependent
+// launch costs a small call ~4-5 us)
+__global__ __launch_bounds__(kThreads) void var_msg_decode_small(
+    DecArgs a, const uint8_t *__restrict__ wire, const uint64_t *__restrict__ offs,
+    uint8_t *__restrict__ ws, int32_t *__restrict__ errc_out, uint8_t *__restrict__ recs,
+    spk_dresult_t *res) {
+  __shared__ uint64_t sh[kThreads / 64];
+  __shared__ BigSeg big[kBigMax];
+  if (threadIdx.x == 0) *res = spk_dresult_t{};
+  __syncthreads();
+  msg_parse_body(a, wire, offs, ws, errc_out, res, 0, sh);
+  __syncthreads();
+  scan_blocks_body(1, a.L.n_spans, reinterpret_cast<uint64_t *>(ws + kWsScratch +
+                                                                 sizeof(MsgState) * a.n_msgs),
+                   a, res, sh);
+  __syncthreads();
+  msg_write_body(a, wire, offs, ws, recs, res, 0, 0, 1, sh, big);
 }
 
 // ===========================================================================
@@ -5420,17 +5500,24 @@ hipError_t launch_var_plan(const spk_layout *L, int mode, uint64_t n, const void
   VarArgs a = make_varargs(L, mode, n, nullptr);
   a.dn = d_n;
   uint8_t *ws = (uint8_t *)d_ws;
-  if (mode == SPK_MODE_MESSAGES) {  // (the per-width header table: messages only)
-    const MsgHdrTable t = msg_hdr_table(L);
-    SPK_LAUNCH(write_msg_hdrs, dim3(1), dim3(256), 0, s, t, ws);
-  }
   const uint64_t nb = n ? grid_for(n, kPlanRPB) : 1;  // (n = 0: one block of no records)
-  const uint8_t *tbl = ws + kWsHdrMsg + 4 * kWsHdrSlot - 8;
   FinArgs f;
   f.fmt = mode == SPK_MODE_VECTOR ? L->fmt_vector : L->fmt_one;
   f.n = n;
   f.n_cont = a.L.n_cont;
   f.mode = mode;
+  if (SPK_PLAN_SMALL && nb == 1) {
+    const MsgHdrTable t = mode == SPK_MODE_MESSAGES ? msg_hdr_table(L) : MsgHdrTable{};
+    SPK_LAUNCH(var_plan_small, dim3(1), dim3(kThreads), 0, s, a, f, t, (const uint8_t *)d_recs,
+               ws, d_plan);
+    (void)ws_bytes;
+    return hipGetLastError();
+  }
+  if (mode == SPK_MODE_MESSAGES) {  // (the per-width header table: messages only)
+    const MsgHdrTable t = msg_hdr_table(L);
+    SPK_LAUNCH(write_msg_hdrs, dim3(1), dim3(256), 0, s, t, ws);
+  }
+  const uint8_t *tbl = ws + kWsHdrMsg + 4 * kWsHdrSlot - 8;
   SPK_LAUNCH(var_plan_reduce, dim3(nb), dim3(kThreads), 0, s, a, (const uint8_t *)d_recs, ws,
              tbl);
   SPK_LAUNCH(var_plan_finalize, dim3(1), dim3(kFinThreads), 0, s, f, nb, ws, d_plan);
@@ -5522,6 +5609,11 @@ hipError_t launch_var_decode(const spk_layout *L, int mode, const void *d_wire,
   const uint8_t *wire = (const uint8_t *)d_wire;
   hipError_t e;
   if (mode == SPK_MODE_MESSAGES) {
+    if (SPK_MSG_SMALL && n_msgs && n_msgs <= kThreads) {
+      SPK_LAUNCH(var_msg_decode_small, dim3(1), dim3(kThreads), 0, s, a, wire, d_offsets, ws,
+                 d_errc, (uint8_t *)d_recs, d_res);
+      return hipGetLastError();
+    }
     if ((e = hipMemsetAsync(d_res, 0, sizeof(spk_dresult_t), s)) != hipSuccess) return e;
     if (n_msgs == 0) return hipSuccess;
     const unsigned nb = grid_for(n_msgs, kThreads);
