@@ -352,6 +352,18 @@ int spk_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
                void *d_out, uint64_t out_cap, uint64_t *d_msg_offsets,
                void *d_ws, size_t ws_bytes, void *stream);
 
+/* Plan + encode in one call: serialize(t) as get_needed_size then
+ * serialize_to (ref struct_pack.hpp:75-190), spk_plan_ex followed by
+ * spk_encode with the same arguments -- d_plan receives the plan, d_out the
+ * bytes when plan->total_bytes <= out_cap (a variable-size layout's write
+ * otherwise writes nothing: read the plan, encode again with spk_encode).
+ * A batch of at most 256 records of a flat variable-size layout (a small
+ * call's message) takes one kernel launch instead of three to five. */
+int spk_plan_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
+                    const void *const *d_heaps, spk_plan_t *d_plan, void *d_out,
+                    uint64_t out_cap, uint64_t *d_msg_offsets, void *d_ws, size_t ws_bytes,
+                    void *stream);
+
 /* Decode: deserialize_to(vector<T>&, const char*, size_t, size_t&)
  * (ref struct_pack.hpp:343-357, unpacker.hpp:101-162,548-619,780-1349) for
  * SPK_MODE_VECTOR; for SPK_MODE_MESSAGES, message i is

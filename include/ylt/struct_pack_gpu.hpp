@@ -379,11 +379,10 @@ class codec {
     if (end > o_recs) copy(dp + o_recs, hp + o_recs, end - o_recs, SPK_COPY_H2D, s_);
     ws_.resize(spk_workspace_bytes(&L, mode, n, 0));
     spk_plan_t *d_plan = reinterpret_cast<spk_plan_t *>(dp);
-    check(spk_plan_ex(&L, mode, n, dp + o_recs, dheaps.data(), d_plan, ws_.data(), ws_.size(), s_),
-          "spk_plan_ex");
     uint64_t *d_offs = mode == SPK_MODE_MESSAGES ? reinterpret_cast<uint64_t *>(dp + o_offs) : nullptr;
-    check(spk_encode(&L, mode, n, dp + o_recs, dheaps.data(), d_plan, dp + o_out, out_cap, d_offs,
-                     ws_.data(), ws_.size(), s_), "spk_encode");
+    // (plan + write: one launch for a small flat variable-size message)
+    check(spk_plan_encode(&L, mode, n, dp + o_recs, dheaps.data(), d_plan, dp + o_out, out_cap,
+                          d_offs, ws_.data(), ws_.size(), s_), "spk_plan_encode");
     copy(hp, dp, o_out + out_cap, SPK_COPY_D2H, s_);
     sync(s_);
     spk_plan_t p;

@@ -130,7 +130,8 @@ ORACLE_PATH = os.path.join(_ROOT, "oracle", "libspk_oracle.so")
 
 # exported symbols of include/spk_codec.h (checked by tests/test_capi.py)
 CODEC_SYMBOLS = ["spk_abi_version", "spk_errc_message", "spk_layout_check",
-                 "spk_workspace_bytes", "spk_plan", "spk_plan_ex", "spk_encode", "spk_decode",
+                 "spk_workspace_bytes", "spk_plan", "spk_plan_ex", "spk_encode", "spk_plan_encode",
+                 "spk_decode",
                  "spk_synth", "spk_synth_counts", "spk_synth_ex", "spk_synth_counts_ex",
                  "spk_encode_body",
                  "spk_vector_header", "spk_encode_framed", "spk_decode_framed",
@@ -167,6 +168,8 @@ def _bind_codec(lib):
     lib.spk_plan_ex.argtypes = [PL, ct.c_int, U64, P, ct.POINTER(P), P, P, ct.c_size_t, P]
     lib.spk_encode.argtypes = [PL, ct.c_int, U64, P, ct.POINTER(P), P, P, U64,
                                P, P, ct.c_size_t, P]
+    lib.spk_plan_encode.argtypes = [PL, ct.c_int, U64, P, ct.POINTER(P), P, P, U64,
+                                    P, P, ct.c_size_t, P]
     lib.spk_decode.argtypes = [PL, ct.c_int, P, U64, P, U64, P, U64,
                                ct.POINTER(P), ct.POINTER(U64), P, P, P,
                                ct.c_size_t, P]

@@ -321,6 +321,29 @@ int spk_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
                      nullptr, d_ws, ws_bytes, stream);
 }
 
+int spk_plan_encode(const spk_layout *L, int mode, uint64_t n, const void *d_recs,
+                    const void *const *d_heaps, spk_plan_t *d_plan, void *d_out,
+                    uint64_t out_cap, uint64_t *d_msg_offsets, void *d_ws, size_t ws_bytes,
+                    void *stream) {
+  int rc = spk_layout_check(L);
+  if (rc) return rc;
+  if ((mode != SPK_MODE_VECTOR && mode != SPK_MODE_MESSAGES) || !d_plan || !d_ws || !d_out)
+    return SPK_E_ARG;
+  if (n && !d_recs) return SPK_E_ARG;
+  if (ws_bytes < spk_workspace_bytes(L, mode, n, 0)) return SPK_E_WORKSPACE;
+  if (!is_trivial(L) && var_plan_encode_small_ok(L, n)) {
+    // a small batch of a flat variable-size layout: plan and write in one launch
+    if ((uintptr_t)d_recs % 8) return SPK_E_ARG;
+    if ((rc = heaps_check(L, n, d_heaps))) return rc;
+    return hip_rc(launch_var_plan_encode_small(L, mode, n, d_recs, d_heaps, d_plan, d_out,
+                                               out_cap, d_msg_offsets, d_ws,
+                                               (hipStream_t)stream));
+  }
+  if ((rc = spk_plan_ex(L, mode, n, d_recs, d_heaps, d_plan, d_ws, ws_bytes, stream))) return rc;
+  return spk_encode(L, mode, n, d_recs, d_heaps, d_plan, d_out, out_cap, d_msg_offsets, d_ws,
+                    ws_bytes, stream);
+}
+
 int spk_encode_framed(const spk_layout *L, uint64_t n, const void *d_recs,
                       const void *const *d_heaps, const spk_plan_t *d_plan,
                       const spk_frame *F, void *d_out, uint64_t out_cap,

@@ -381,6 +381,11 @@ size_t var_workspace_bytes(const spk_layout *L, int mode, uint64_t n,
 hipError_t launch_var_plan(const spk_layout *L, int mode, uint64_t n,
                            const void *d_recs, spk_plan_t *d_plan, void *d_ws,
                            size_t ws_bytes, hipStream_t s, const uint64_t *d_n = nullptr);
+bool var_plan_encode_small_ok(const spk_layout *L, uint64_t n);
+hipError_t launch_var_plan_encode_small(const spk_layout *L, int mode, uint64_t n,
+                                        const void *d_recs, const void *const *d_heaps,
+                                        spk_plan_t *d_plan, void *d_out, uint64_t out_cap,
+                                        uint64_t *d_offsets, void *d_ws, hipStream_t s);
 hipError_t launch_var_encode(const spk_layout *L, int mode, uint64_t n,
                              const void *d_recs, const void *const *d_heaps,
                              const spk_plan_t *d_plan, void *d_out,

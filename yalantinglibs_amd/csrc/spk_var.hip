@@ -815,42 +815,40 @@ constexpr uint32_t kEncWin = 20 * 1024;
 // Write pass: records r0 + j*kThreads + tid (consecutive lanes on consecutive
 // records), byte offsets from a block scan per round on top of the block's
 // planned base; the block's output range is assembled window by window.
-__global__ __launch_bounds__(kThreads, 5) void var_encode_write(
-    VarArgs a, const uint8_t *__restrict__ recs, uint8_t *__restrict__ out,
-    uint64_t out_cap, const uint8_t *__restrict__ ws,
-    const spk_plan_t *__restrict__ plan, uint64_t *__restrict__ offs) {
+__device__ __forceinline__ void encode_write_body(
+    const VarArgs &a, const uint8_t *__restrict__ recs, uint8_t *__restrict__ out,
+    uint64_t out_cap, const uint8_t *__restrict__ ws, const spk_plan_t *__restrict__ plan,
+    uint64_t *__restrict__ offs, uint64_t bx, uint64_t gx, uint32_t by, uint32_t gy,
+    uint8_t *lds, uint64_t *sh, BigSeg *big) {
   const uint64_t N = dev_count(a.n, a.dn);
-  __shared__ __align__(16) uint8_t lds[kEncWin];
-  __shared__ uint64_t sh[kThreads / 64];
-  __shared__ BigSeg big[kBigMax];
   const uint64_t total =
       plan->total_bytes + (a.mode == SPK_MODE_MESSAGES ? N * (uint64_t)a.fpre : 0);
   if (total > out_cap) return;  // caller reads plan->total_bytes
   const uint32_t w_vec = plan->width;
   const uint32_t hdr_vec = plan->header_bytes;
-  const PlanScratch ps = plan_scratch(const_cast<uint8_t *>(ws), (gridDim.x + kPlanSub - 1) / kPlanSub);
-  const uint64_t r0 = (uint64_t)blockIdx.x * kRPB;
+  const PlanScratch ps = plan_scratch(const_cast<uint8_t *>(ws), (gx + kPlanSub - 1) / kPlanSub);
+  const uint64_t r0 = bx * kRPB;
   // output base of write block b (b == gridDim.x: the end of the output)
   auto base_of = [&](uint64_t b) -> uint64_t {
-    if (b >= gridDim.x) return total;
+    if (b >= gx) return total;
     uint64_t gb = ps.psum[b / kPlanSub];
     for (uint32_t j = 0; j < b % kPlanSub; ++j) gb += ps.wsub[b / kPlanSub * kPlanSub + j];
     const uint64_t rb = b * kRPB;
     return a.mode == SPK_MODE_VECTOR ? hdr_vec + gb + rb * (uint64_t)a.L.n_cont * w_vec
                                      : gb + rb * (uint64_t)a.fpre;
   };
-  const uint64_t g0 = base_of(blockIdx.x);
+  const uint64_t g0 = base_of(bx);
   // Window split: gridDim.y blocks share one write block's output range, block
   // y assembling windows y, y + gridDim.y, ... (a few blocks of multi-KiB
   // messages would otherwise leave most CUs idle). The range end comes from
   // the next block's base, so a block without windows leaves before reading
   // any record.
-  const uint32_t ysub = blockIdx.y, ny = gridDim.y;
+  const uint32_t ysub = by, ny = gy;
   if (ysub > 0) {
-    const uint64_t ge = base_of((uint64_t)blockIdx.x + 1);
+    const uint64_t ge = base_of(bx + 1);
     if ((g0 & ~15ull) + (uint64_t)ysub * kEncWin >= ge) return;
   }
-  if (a.mode == SPK_MODE_VECTOR && blockIdx.x == 0 && ysub == 0)
+  if (a.mode == SPK_MODE_VECTOR && bx == 0 && ysub == 0)
     for (uint32_t i = threadIdx.x; i < hdr_vec; i += blockDim.x) out[i] = ws[kWsHdrVec + i];
   const uint8_t *rbase = recs + r0 * a.L.stride;
 #define SPK_REC(i) (rbase + ((i) - r0) * a.L.stride)
@@ -879,7 +877,7 @@ __global__ __launch_bounds__(kThreads, 5) void var_encode_write(
     g += btot;
     if (a.mode == SPK_MODE_MESSAGES && offs && i < N && ysub == 0) offs[i] = pj[j];
   }
-  if (a.mode == SPK_MODE_MESSAGES && offs && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 &&
+  if (a.mode == SPK_MODE_MESSAGES && offs && bx == gx - 1 && threadIdx.x == 0 &&
       ysub == 0)
     offs[N] = total;
   const uint64_t g1 = g;
@@ -1003,6 +1001,39 @@ __global__ __launch_bounds__(kThreads, 5) void var_encode_write(
     }
     __syncthreads();
   }
+}
+__global__ __launch_bounds__(kThreads, 5) void var_encode_write(
+    VarArgs a, const uint8_t *__restrict__ recs, uint8_t *__restrict__ out,
+    uint64_t out_cap, const uint8_t *__restrict__ ws,
+    const spk_plan_t *__restrict__ plan, uint64_t *__restrict__ offs) {
+  __shared__ __align__(16) uint8_t lds[kEncWin];
+  __shared__ uint64_t sh[kThreads / 64];
+  __shared__ BigSeg big[kBigMax];
+  encode_write_body(a, recs, out, out_cap, ws, plan, offs, blockIdx.x, gridDim.x, blockIdx.y,
+                    gridDim.y, lds, sh, big);
+}
+
+// plan + write of at most kRPB records (a small call's message) in one launch
+// of one block: var_plan_small's phases, then the one write block's
+__global__ __launch_bounds__(kThreads) void var_plan_encode_small(
+    VarArgs a, FinArgs f, MsgHdrTable t, const uint8_t *__restrict__ recs,
+    uint8_t *__restrict__ out, uint64_t out_cap, uint8_t *__restrict__ ws,
+    spk_plan_t *__restrict__ plan, uint64_t *__restrict__ offs) {
+  __shared__ __align__(16) uint8_t lds[kEncWin];
+  __shared__ uint64_t sh[kThreads / 64];
+  __shared__ BigSeg big[kBigMax];
+  __shared__ uint64_t red[kPlanSub + 1][kThreads / 64];
+  if (a.mode == SPK_MODE_MESSAGES) msg_hdrs_body(t, ws);
+  __syncthreads();
+  plan_reduce_body(a, recs, ws, ws + kWsHdrMsg + 4 * kWsHdrSlot - 8, 0, 1, red);
+  if (threadIdx.x == 0) {
+    const PlanScratch q = plan_scratch(ws, 1);
+    const uint64_t carry = q.psum[0], mx = q.pmax[0];
+    q.psum[0] = 0;  // (the exclusive scan of one block sum)
+    plan_result(f, carry, mx, ws, plan);
+  }
+  __syncthreads();
+  encode_write_body(a, recs, out, out_cap, ws, plan, offs, 0, 1, 0, 1, lds, sh, big);
 }
 #undef SPK_REC
 
@@ -5553,6 +5584,26 @@ hipError_t launch_var_encode(const spk_layout *L, int mode, uint64_t n,
                      s, a, (const uint8_t *)d_recs, (uint8_t *)d_out, out_cap,
                      (const uint8_t *)ws, d_plan, d_offsets);
   (void)ws_bytes;
+  return hipGetLastError();
+}
+
+bool var_plan_encode_small_ok(const spk_layout *L, uint64_t n) {
+  return SPK_PLAN_SMALL && n >= 1 && n <= kRPB && !layout_nested(L);
+}
+hipError_t launch_var_plan_encode_small(const spk_layout *L, int mode, uint64_t n,
+                                        const void *d_recs, const void *const *d_heaps,
+                                        spk_plan_t *d_plan, void *d_out, uint64_t out_cap,
+                                        uint64_t *d_offsets, void *d_ws, hipStream_t s) {
+  VarArgs a = make_varargs(L, mode, n, d_heaps);
+  FinArgs f;
+  f.fmt = mode == SPK_MODE_VECTOR ? L->fmt_vector : L->fmt_one;
+  f.n = n;
+  f.n_cont = a.L.n_cont;
+  f.mode = mode;
+  const MsgHdrTable t = mode == SPK_MODE_MESSAGES ? msg_hdr_table(L) : MsgHdrTable{};
+  SPK_LAUNCH(var_plan_encode_small, dim3(1), dim3(kThreads), 0, s, a, f, t,
+             (const uint8_t *)d_recs, (uint8_t *)d_out, out_cap, (uint8_t *)d_ws, d_plan,
+             d_offsets);
   return hipGetLastError();
 }
 

@@ -126,9 +126,15 @@ class Codec:
         """Plan + write into a caller-owned device buffer (no host sync).
         `frame` (MODE_MESSAGES only) reserves and fills a per-message prefix
         such as coro_rpc's req_header (see yalantinglibs_amd.coro_rpc)."""
+        ws = self.workspace(mode, batch.n)
+        if not planned and frame is None:  # (one launch for a small batch)
+            self._check(self.lib.spk_plan_encode(
+                self.L.ptr, mode, batch.n, _p(batch.recs), self._heap_ptrs(batch.heaps),
+                _p(self.plan_buf), _p(out), out.numel(), _p(offsets), _p(ws), ws.numel(),
+                _stream(stream)), "spk_plan_encode")
+            return
         if not planned:
             self.plan(batch, mode, stream)
-        ws = self.workspace(mode, batch.n)
         if frame is not None:
             if mode != MODE_MESSAGES:
                 raise ValueError("frames apply to MODE_MESSAGES batches")
