@@ -318,6 +318,36 @@ def test_compat_capacity_probe_fast(case):
     assert min(ts) < 100.0, ts  # complexity guard: the passes take a few ms
 
 
+@pytest.mark.parametrize("case,param", [("recs", 48), ("person", 24), ("opt", 16), ("var", 16),
+                                        ("ints", 8), ("fv", 0), ("rec64", 0), ("outer", 8)])
+@pytest.mark.parametrize("n", [1, 7, 256, 257])
+@pytest.mark.parametrize("modech", ["A", "B"])
+def test_plan_encode_one_call(case, param, n, modech):
+    """spk_plan_encode (serialize_to without a prior plan): a small batch of a
+    flat variable-size layout is planned and written by one launch
+    (var_plan_encode_small, n <= 256), larger ones and other layouts by
+    spk_plan_ex + spk_encode -- the plan and the bytes equal the oracle's; an
+    output buffer below the size leaves the plan for a second call."""
+    cd = codec_for(case)
+    _, recs, heaps = synth.make_batch(case, n, 0x9E0 + n, param)
+    mode = C.SPK_MODE_VECTOR if modech == "A" else C.SPK_MODE_MESSAGES
+    exp, eoffs, _ = H.oracle_encode(cd.L, mode, recs, heaps)
+    batch = to_dev(cd, recs, heaps)
+    out = torch.zeros(len(exp) + 64, dtype=torch.uint8, device="cuda")
+    offs = torch.empty(n + 1, dtype=torch.int64, device="cuda") if modech == "B" else None
+    cd.serialize_to(out, batch, mode, offs)
+    plan = C.spk_plan_t.from_buffer_copy(bytes(cd.plan_buf.cpu().numpy()))
+    assert plan.total_bytes == len(exp)
+    assert out[:len(exp)].cpu().numpy().tobytes() == exp
+    if offs is not None:
+        assert np.array_equal(offs.cpu().numpy().astype(np.uint64), eoffs)
+    if cd.L.dev.spans and case != "outer":  # (a variable-size layout: the short buffer case)
+        small = torch.zeros(len(exp) - 1, dtype=torch.uint8, device="cuda")
+        cd.serialize_to(small, batch, mode, offs)
+        plan = C.spk_plan_t.from_buffer_copy(bytes(cd.plan_buf.cpu().numpy()))
+        assert plan.total_bytes == len(exp)
+
+
 @pytest.mark.parametrize("writer,reader", [("cmpold", "cmp"), ("cmpnew", "cmp"),
                                            ("cmp", "cmpnew"), ("cmpold", "cmpnew")])
 def test_compat_vector_other_writer(writer, reader):
