@@ -331,6 +331,18 @@ int spk_plan_encode(const spk_layout *L, int mode, uint64_t n, const void *d_rec
     return SPK_E_ARG;
   if (n && !d_recs) return SPK_E_ARG;
   if (ws_bytes < spk_workspace_bytes(L, mode, n, 0)) return SPK_E_WORKSPACE;
+  if (is_trivial(L) && mode == SPK_MODE_MESSAGES) {
+    // the plan is the host's: the encode kernel stores it (one launch)
+    uint8_t hb[4 + 1 + SPK_MAX_LITERAL + 1];
+    const uint64_t total = n * (uint64_t)(write_hdr(hb, L->fmt_one, 1) + L->rec_stride);
+    if (total > out_cap) {
+      if ((rc = spk_plan_ex(L, mode, n, d_recs, d_heaps, d_plan, d_ws, ws_bytes, stream)))
+        return rc;
+      return SPK_E_CAPACITY;
+    }
+    return hip_rc(launch_fixed_plan_encode_messages(L, n, d_recs, d_out, d_msg_offsets, d_plan,
+                                                    d_ws, (hipStream_t)stream));
+  }
   if (!is_trivial(L) && var_plan_encode_small_ok(L, n)) {
     // a small batch of a flat variable-size layout: plan and write in one launch
     if ((uintptr_t)d_recs % 8) return SPK_E_ARG;

@@ -399,6 +399,8 @@ struct MsgLdsArgs {
   uint32_t seq_base;
   SeqEcho echo;     // encode: seq_num echoed from request frames
   const uint64_t *ends;  // decode: message i ends at ends[i] (null: offs[i + 1])
+  spk_plan_t *plan_out;  // encode: block 0 stores plan_val there (spk_plan_encode)
+  spk_plan_t plan_val;
   uint8_t hdr[kMsgHdrMax];
 };
 
@@ -441,6 +443,7 @@ __global__ __launch_bounds__(kMsgThreads) void fixed_msg_encode_lds(
   const uint32_t S = a.stride, H = a.hlen, M = H + S;
   const uint64_t first = (uint64_t)blockIdx.x * a.R;
   if (offs && blockIdx.x == gridDim.x - 1 && tid == 0) offs[N] = N * M;
+  if (a.plan_out && blockIdx.x == 0 && tid == 0) *a.plan_out = a.plan_val;
   if (first >= N) return;
   const uint32_t nR = (uint32_t)((N - first) < a.R ? (N - first) : a.R);
   for (uint32_t k = tid; k < H; k += kMsgThreads) hdr[k] = a.hdr[k];
@@ -775,13 +778,43 @@ static uint32_t msg_header(const spk_layout *L, const spk_frame *F, uint8_t *hdr
   return P + H;
 }
 
+// spk_plan_encode, trivially copyable records, MESSAGES: the plan is known on
+// the host (fixed_plan_kernel's), so the encode kernel's block 0 stores it --
+// one launch instead of two for a small call's message
+hipError_t launch_fixed_plan_encode_messages(const spk_layout *L, uint64_t n,
+                                             const void *d_recs, void *d_out,
+                                             uint64_t *d_offsets, spk_plan_t *d_plan,
+                                             void *d_ws, hipStream_t s) {
+  const HdrShape h = hdr_shape(L->fmt_one.flags, L->fmt_one.literal_len, 1);
+  spk_plan_t p = {};
+  p.total_bytes = n * (h.len + (uint64_t)L->rec_stride);
+  p.max_count = 0;
+  p.var_bytes = n * (uint64_t)L->rec_stride;
+  p.width = 1;
+  p.header_bytes = h.len;
+  p.metainfo = h.meta;
+  p.has_meta = h.has_meta;
+  hipError_t e = launch_fixed_encode_messages(L, n, d_recs, d_out, d_offsets, nullptr, s,
+                                              nullptr, nullptr, d_plan, &p);
+  if (e == hipErrorNotSupported)  // (not the LDS kernel: plan, then encode)
+    if ((e = launch_fixed_plan(L, SPK_MODE_MESSAGES, n, d_plan, d_ws, s)) == hipSuccess)
+      e = launch_fixed_encode_messages(L, n, d_recs, d_out, d_offsets, nullptr, s, nullptr,
+                                       nullptr);
+  return e;
+}
+
 hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
                                         const void *d_recs, void *d_out,
                                         uint64_t *d_offsets, const spk_frame *F,
                                         hipStream_t s, const SeqEcho *echo,
-                                        const uint64_t *d_n) {
+                                        const uint64_t *d_n, spk_plan_t *d_plan_out,
+                                        const spk_plan_t *plan_val) {
   {
     MsgLdsArgs b = {};
+    if (d_plan_out) {
+      b.plan_out = d_plan_out;
+      b.plan_val = *plan_val;
+    }
     if (echo) b.echo = *echo;
     b.n = n;
     b.dn = d_n;
@@ -807,6 +840,7 @@ hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
       return hipGetLastError();
     }
   }
+  if (d_plan_out) return hipErrorNotSupported;  // (the caller plans separately)
   MsgEncArgs a = {};
   if (echo) a.echo = *echo;
   a.n = n;

@@ -359,7 +359,13 @@ hipError_t launch_fixed_encode_messages(const spk_layout *L, uint64_t n,
                                         const void *d_recs, void *d_out,
                                         uint64_t *d_offsets, const spk_frame *F,
                                         hipStream_t s, const SeqEcho *echo = nullptr,
-                                        const uint64_t *d_n = nullptr);
+                                        const uint64_t *d_n = nullptr,
+                                        spk_plan_t *d_plan_out = nullptr,
+                                        const spk_plan_t *plan_val = nullptr);
+hipError_t launch_fixed_plan_encode_messages(const spk_layout *L, uint64_t n,
+                                             const void *d_recs, void *d_out,
+                                             uint64_t *d_offsets, spk_plan_t *d_plan,
+                                             void *d_ws, hipStream_t s);
 // body_w != 0: d_wire is a message BODY of body_n records at width body_w
 // (no header / count: spk_decode_body)
 hipError_t launch_fixed_decode_vector(const spk_layout *L, const void *d_wire,
