@@ -3803,6 +3803,9 @@ __device__ __forceinline__ int32_t tile_select_for(const TileBufs &TB, uint64_t 
   return kSelBroken;
 }
 
+#ifndef SPK_PICK_WAVEJUMP
+#define SPK_PICK_WAVEJUMP 1  // (cmpg 5.144 -> 4.772 ms per step, same-box A/B)
+#endif
 // ---- K2: select each tile's entry (one thread per tile); tiles whose entry
 // is none of theirs are listed and re-walked by vec_tile_repair (one wave per
 // listed tile, a fixed grid striding over the list) -------------------------
@@ -3826,6 +3829,7 @@ __global__ __launch_bounds__(256) void vec_tile_pick(uint8_t *__restrict__ ws, T
   // atomics: bytes after a message, e.g. a compatible member's version
   // passes, break most of their tiles)
   bool brk = false, list = false;
+  uint64_t jE = kNoPos;  // SPK_PICK_WAVEJUMP: this tile's pass-through run, for the wave
   if (t < TB.ntiles) {
     const uint64_t T = tile_entry(TB, fc, t);
     int32_t sel = T == kNoPos ? kSelBroken : tile_select_for(TB, t, T);
@@ -3840,19 +3844,41 @@ __global__ __launch_bounds__(256) void vec_tile_pick(uint8_t *__restrict__ ws, T
                        tile_entry(TB, fc, t - 1) == T;
     if (sel != kSelBroken || T == kNoPos) {
       TB.sel[t] = sel;
-      if (sel >= 0 && !inner)
-        tile_jump(TB, c->p0, t, TB.fn[t * kFnWords], nsp, 0, &fc->broken[pass], 1);
+      if (sel >= 0 && !inner) {
+        if (SPK_PICK_WAVEJUMP)
+          jE = TB.fn[t * kFnWords];
+        else
+          tile_jump(TB, c->p0, t, TB.fn[t * kFnWords], nsp, 0, &fc->broken[pass], 1);
+      }
     } else {
       brk = true;
       if (T >= ts + kTileBytes) {  // inside a record that spans the tile
         tile_pass_through(TB, t, T, nsp);
-        if (!inner) tile_jump(TB, c->p0, t, T, nsp, 0, &fc->broken[pass], 1);
+        if (!inner) {
+          if (SPK_PICK_WAVEJUMP)
+            jE = T;
+          else
+            tile_jump(TB, c->p0, t, T, nsp, 0, &fc->broken[pass], 1);
+        }
       } else {
         list = true;
       }
     }
   }
   const uint32_t lane = threadIdx.x & 63;
+  if (SPK_PICK_WAVEJUMP) {
+    // a run of pass-through tiles written by the whole wave, one run at a
+    // time, not by its tile's one thread (a false exit far ahead in the bytes
+    // after a message wrote thousands of tiles serially)
+    const uint64_t E0 = c->p0;
+    uint64_t mj = __ballot(jE != kNoPos && jE != kTermPos && jE >= E0 &&
+                           (jE - E0) / kTileBytes > t + 1);
+    while (mj) {
+      const int l = (int)__builtin_ctzll(mj);
+      mj &= mj - 1;
+      tile_jump(TB, E0, __shfl(t, l), __shfl(jE, l), nsp, lane, &fc->broken[pass], 64);
+    }
+  }
   const uint64_t mb = __ballot(brk), ml = __ballot(list);
   if (lane == 0 && mb) atomicAdd(&fc->broken[pass], (unsigned long long)__popcll(mb));
   if (!ml) return;
