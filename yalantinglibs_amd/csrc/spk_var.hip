@@ -1455,6 +1455,7 @@ struct FCtl {
   unsigned long long chain_arrive;  // chain blocks arrived (the first one finds the first tile)
   unsigned long long chain_ready;   // the chain's first tile + 1 (0: not yet found)
   unsigned long long chain_done;    // chain blocks out (the last one sums the tile scan)
+  unsigned long long term_from;     // SPK_CHAIN_TERM1: entry words [term_from, nt) hold kEntTerm
   unsigned long long copy_done;     // vec_big_copy blocks done (the last one writes the result)
   // records of the tiles the chain has finalised, plus those before its first
   // tile (a running lower bound of the records before the chain's next tile)
@@ -1731,6 +1732,7 @@ __device__ void vec_hdr_body(const DecArgs &a, const uint8_t *__restrict__ wire,
   fc->chain_arrive = 0;
   fc->chain_ready = 0;
   fc->chain_done = 0;
+  fc->term_from = ~0ull;
   fc->chain_cnt = 0;
   fc->copy_done = 0;
   fc->njobs = 0;
@@ -3803,6 +3805,9 @@ __device__ __forceinline__ int32_t tile_select_for(const TileBufs &TB, uint64_t 
   return kSelBroken;
 }
 
+#ifndef SPK_CHAIN_TERM1
+#define SPK_CHAIN_TERM1 1  // (cmpg chain 0.506 -> 0.430 ms, 4.714 -> 4.649 ms per step, same box)
+#endif
 #ifndef SPK_PICK_WAVEJUMP
 #define SPK_PICK_WAVEJUMP 1  // (cmpg 5.144 -> 4.772 ms per step, same-box A/B)
 #endif
@@ -4100,6 +4105,24 @@ __device__ __forceinline__ int32_t tile_sel_now(const TileBufs &TB, const FCtl *
 template <int NS>
 constexpr uint32_t kChainWaves = NS <= -2 ? 1u : 4u;
 
+// the path ends before tile u + 1: every later tile's entry word is kEntTerm
+// (one wave). SPK_CHAIN_TERM1: each word is written once -- the range past
+// what an earlier end already covered (term_from) -- not once per tile past
+// the end (the bytes after a message: thousands of tiles, each rewriting all
+// the words after it)
+__device__ __forceinline__ void chain_term_after(uint64_t *ent, FCtl *fc, uint64_t u, uint64_t nt,
+                                                 uint32_t lane) {
+  uint64_t hi = nt;
+  if (SPK_CHAIN_TERM1) {
+    uint64_t old = 0;
+    if (lane == 0) old = atomicMin(&fc->term_from, (unsigned long long)(u + 1));
+    old = __shfl(old, 0);
+    hi = old < nt ? old : nt;
+  }
+  for (uint64_t v = u + 1 + lane; v < hi; v += 64)
+    __hip_atomic_store(&ent[v], kEntTerm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int NS>
 __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
     DecArgs a, WalkProg P, const uint8_t *__restrict__ wire, uint8_t *__restrict__ ws,
@@ -4200,8 +4223,7 @@ __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
           TB.sel[u] = kSelTerm;
           tile_contrib(TB, fc, u, nsp);
         }
-        for (uint64_t v = u + 1 + lane; v < nt; v += 64)
-          __hip_atomic_store(&ent[v], kEntTerm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        chain_term_after(ent, fc, u, nt, lane);
       }
       __syncthreads();
       continue;
@@ -4338,8 +4360,7 @@ __global__ __launch_bounds__(64 * kChainWaves<NS>) void vec_tile_chain(
           // message, which need not parse: the path ends here, so that no
           // later tile waits for an entry)
           if (Y == kTermPos || Y == kNoPos) {
-            for (uint64_t v = u + 1 + lane; v < nt; v += 64)
-              __hip_atomic_store(&ent[v], kEntTerm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            chain_term_after(ent, fc, u, nt, lane);
             return;
           }
           uint64_t l0 = Y >= p0 ? (Y - p0) / kTileBytes : 0;
